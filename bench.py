@@ -1,0 +1,184 @@
+#!/usr/bin/env python3
+"""bench.py — point-residuals/s of H-SLAM's windowed photometric BA on MI355X.
+
+Workload (BASELINE.json configs[3], "C4"): full windowed photometric BA including the
+Schur complement, 8 keyframes x 2000 active points per GPU, 640x480 synthetic scene
+(hslam_amd.scene, seed 20261015), ~13.6k point-residuals per GPU.  One *step* = one
+Gauss-Newton iteration of System::optimize (solveSystemF + doStepFromBackup +
+linearizeAll + applyRes), i.e. hs_ba_iterate(1).  Multi-GPU: one rank per GPU, every
+rank holds its own 2000-point shard of a (2000 x N)-point window over the same 8 KFs
+("weak" scaling); per step one RCCL all-reduce of the stitched 68x68 system and one
+all-gather of the newest-frame energies.
+
+JSON line fields follow the driver contract; `roofline` is for the dominant kernel
+(hs_k_linearize, timed with HIP events on the context's own stream), `cpu_baseline` is
+the oracle's C++ restatement of the reference SSE/IndexThreadReduce path timed on
+this host (rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "h-slam_amd"))
+
+METRIC = "point-residuals/sec in windowed photometric BA (8 KF × 2k pts), 1→8 GPU"
+BYTES_PER_PRES = 448      # algorithmic bytes per point-residual (fused K1-K5)
+HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def cpu_baseline(points: int, seconds: float):
+    """Oracle (C++ restatement of the reference CPU path, -O2 -march=x86-64-v3) on this host."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle_ffi import OracleBA  # test infrastructure: the CPU baseline leg only
+    from hslam_amd.scene import make_ba_scene
+
+    threads = os.cpu_count() or 1
+    env_t = os.environ.get("OMP_NUM_THREADS")
+    if env_t and env_t.isdigit():
+        threads = min(threads, int(env_t))
+    scene = make_ba_scene(n_points=points)
+    o = OracleBA(scene, nthreads=threads, fast=True)
+    o.linearize_all(reset=True)
+    o.apply_res()
+    o.iterate(0, 3)  # warm-up
+    it, t = 0, 0.0
+    per = []
+    while t < seconds:
+        t0 = time.perf_counter()
+        o.iterate(3 + it, 1)
+        dt = time.perf_counter() - t0
+        per.append(dt)
+        t += dt
+        it += 1
+    per.sort()
+    med = per[len(per) // 2]
+    return {
+        "value": scene.n_res * it / t,
+        "unit": "point-residuals/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{it} GN iterations of the C4 window (8 KF x {points} pts, {scene.n_res} residuals) after 3 warm-up "
+                  f"iterations, IndexThreadReduce-style pool with {threads} threads (chunk 50 / ceil(n/T)); "
+                  f"median iteration {med * 1e3:.2f} ms",
+        "median_ms_per_step": med * 1e3,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--points", type=int, default=2000, help="active points per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from hslam_amd.ba import BAWindow
+    from hslam_amd.scene import make_ba_scene
+
+    scene = make_ba_scene(n_points=args.points * world)
+    shard = scene.shard(rank, world) if world > 1 else scene
+    comm = None
+    if world > 1:
+        uid = [BAWindow.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = (uid[0], rank, world)
+    ba = BAWindow(shard, device=local if world > 1 else 0, comm=comm)
+    ba.linearizeAll(reset=True)
+    if args.warmup > 0:
+        ba.iterate(0, args.warmup)
+
+    def barrier():
+        if dist is not None:
+            import torch
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    ba.iterate(args.warmup, args.steps)  # each GN iteration ends with a host sync on the context stream
+    t1 = time.perf_counter()
+    barrier()
+    dt = t1 - t0
+    n_res_total = shard.n_res
+    if dist is not None:
+        import torch
+        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+        nr = torch.tensor([shard.n_res], dtype=torch.int64, device="cuda")
+        dist.all_reduce(nr)
+        n_res_total = int(nr.item())
+    tim = ba.timings()
+    lin_ms = tim["linearize_ms"] / max(1, tim["iters"])
+    achieved = BYTES_PER_PRES * shard.n_res / (lin_ms * 1e-3) / 1e9
+    result = {
+        "metric": METRIC,
+        "value": n_res_total * args.steps / dt,
+        "unit": "point-residuals/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {
+            "workload": "C4 (BASELINE.json configs[3]): full windowed photometric BA incl. Schur complement, "
+                        f"8 KF x {args.points} pts per GPU, 640x480, 4 pyramid levels, GN step = solve+step+"
+                        "linearize (fp32 residuals, fp64 stitch/solve)",
+            "frames": shard.n_frames,
+            "points_per_gpu": args.points,
+            "point_residuals": n_res_total,
+            "parallelism": f"point-shard x{world}",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "hs_k_linearize",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": None,
+            "bytes_per_unit": BYTES_PER_PRES,
+            "units_per_launch": shard.n_res,
+            "avg_launch_ms": lin_ms,
+        },
+        "phase_ms_per_step": {
+            "linearize_kernel": lin_ms,
+            "reduce_stitch": tim["reduce_stitch_ms"] / max(1, tim["iters"]),
+            "resubstitute": tim["resub_ms"] / max(1, tim["iters"]),
+            "energy_threshold": tim["energy_th_ms"] / max(1, tim["iters"]),
+        },
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        result["cpu_baseline"] = cpu_baseline(args.points, args.cpu_seconds)
+        result["speedup_vs_cpu"] = result["value"] / result["cpu_baseline"]["value"]
+    ba.close()
+    if rank == 0:
+        print(json.dumps(result))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,107 @@
+"""Loader of the product library ``h-slam_amd/lib/libhslam_amd.so`` (HIP, gfx950).
+
+There is no CPU fallback: if the library is missing, or no HIP device is present
+when a context is created, the call raises.  Build with ``make -C h-slam_amd/csrc``
+(or ``__graft_entry__.build()``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libhslam_amd.so")
+
+# data-contract structs (include/hs_types.h)
+
+
+class hs_camera(C.Structure):
+    _fields_ = [("width", C.c_int), ("height", C.c_int), ("n_levels", C.c_int), ("pad", C.c_int),
+                ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float)]
+
+
+class hs_frame(C.Structure):
+    _fields_ = [("worldToCam_evalPT", C.c_double * 7), ("state", C.c_double * 10), ("state_zero", C.c_double * 10),
+                ("ab_exposure", C.c_float), ("frameEnergyTH", C.c_float), ("id", C.c_int), ("pad", C.c_int)]
+
+
+class hs_points(C.Structure):
+    _fields_ = [("n", C.c_int), ("host", C.c_void_p), ("u", C.c_void_p), ("v", C.c_void_p), ("idepth", C.c_void_p),
+                ("idepth_zero", C.c_void_p), ("color", C.c_void_p), ("weights", C.c_void_p),
+                ("has_depth_prior", C.c_void_p)]
+
+
+class hs_residuals(C.Structure):
+    _fields_ = [("n", C.c_int), ("point", C.c_void_p), ("target", C.c_void_p), ("state", C.c_void_p)]
+
+
+class hs_params(C.Structure):
+    _fields_ = [(n, C.c_float) for n in (
+        "huberTH", "outlierTHSumComponent", "frameEnergyTHN", "frameEnergyTHFacMedian", "frameEnergyTHConstWeight",
+        "overallEnergyTHWeight", "idepthFixPrior", "initialCalibHessian", "affineOptModeA", "affineOptModeB",
+        "initialRotPrior", "initialTransPrior", "initialAffAPrior", "initialAffBPrior")] + [
+        ("solverModeDelta", C.c_double), ("thOptIterations", C.c_float), ("coarseCutoffTH", C.c_float),
+        ("minOptIterations", C.c_int), ("pad", C.c_int)]
+
+
+# exported symbols of include/hs_ba.h (argument types)
+VP, I, D = C.c_void_p, C.c_int, C.c_double
+SIGNATURES = {
+    "hs_params_default": ([VP], I),
+    "hs_last_error": ([], C.c_char_p),
+    "hs_create": ([VP, VP, I], I),
+    "hs_destroy": ([VP], None),
+    "hs_ba_set_window": ([VP, VP, I, VP, VP, VP, VP], I),
+    "hs_ba_linearize": ([VP, I, VP], I),
+    "hs_ba_solve_system": ([VP, I, VP], I),
+    "hs_ba_do_step": ([VP, VP], I),
+    "hs_ba_optimize": ([VP, I, I, VP, VP], I),
+    "hs_ba_iterate": ([VP, I, I, VP], I),
+    "hs_ba_get_system": ([VP, I, VP, VP], I),
+    "hs_ba_get_residuals": ([VP] * 7, I),
+    "hs_ba_get_points": ([VP] * 5, I),
+    "hs_ba_get_frames": ([VP] * 5, I),
+    "hs_ba_set_marginal_prior": ([VP, VP, VP], I),
+    "hs_ba_get_timings": ([VP, VP], I),
+    "hs_comm_get_unique_id": ([VP], I),
+    "hs_comm_init": ([VP, VP, I, I], I),
+}
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: build it with `make -C h-slam_amd/csrc` "
+                           "(there is no CPU fallback for the hot path)")
+    lib = C.CDLL(LIB_PATH)
+    for name, (args, res) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = lib
+    return lib
+
+
+class HsError(RuntimeError):
+    pass
+
+
+def check(rc):
+    if rc != 0:
+        raise HsError(f"hs call failed ({rc}): {load().hs_last_error().decode(errors='replace')}")
+
+
+def ptr(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def default_params():
+    p = hs_params()
+    check(load().hs_params_default(C.byref(p)))
+    return p

@@ -1,0 +1,417 @@
+"""Deterministic synthetic scenes for the photometric-BA hot path.
+
+The reference reads real datasets through OpenCV (Include/DatasetLoader.h); that
+layer is out of scope, so benches and parity tests run on scenes rendered here:
+
+* camera 640x480, TumMono useK intrinsics fx=256.0 fy=254.4 cx=319.5 cy=239.5
+  (Src/GeometricUndistorter.cpp:111-122), pyramid levels by Include/CalibData.h:107-115;
+* three textured planes at Z = 2, 3, 5 m, texture = 24 random-phase sinusoids
+  (6-48 px wavelength on the image plane) + blurred uniform noise, intensity 20..235;
+* images rendered by exact ray/plane intersection (photo-consistent up to occlusion);
+* direct pyramids + central-difference gradients exactly as Frame::CreateDirPyrs
+  (Src/Frame.cpp:104-166) in float32 (rows 0 and h-1, which the reference leaves
+  uninitialised, get gradient 0);
+* points: best |grad|^2 pixel per cell, colour / weight sampled as the ImmaturePoint
+  constructor (Src/ImmaturePoint.cpp:7-32), idepth = 1/Z (1 + N(0, 0.01));
+* one residual per (host, other KF) whose centre projects inside the image.
+
+Everything is seeded (default 20261015) and float32 where the reference is float.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+
+PATTERN = np.array([[0, -2], [-1, -1], [1, -1], [-2, 0], [0, 0], [2, 0], [-1, 1], [0, 2]], dtype=np.int32)
+SEED = 20261015
+
+
+def pyramid_levels(w: int, h: int, max_levels: int = 6) -> int:
+    """CalibData constructor rule (Include/CalibData.h:107-115)."""
+    lv = 1
+    while w % 2 == 0 and h % 2 == 0 and w * h > 5000 and lv < max_levels:
+        w //= 2
+        h //= 2
+        lv += 1
+    return lv
+
+
+# ----------------------------------------------------------------- rotations / SE3 (fp64)
+def rodrigues(w):
+    w = np.asarray(w, dtype=np.float64)
+    th = np.linalg.norm(w)
+    if th < 1e-15:
+        return np.eye(3)
+    k = w / th
+    K = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.eye(3) + math.sin(th) * K + (1 - math.cos(th)) * (K @ K)
+
+
+def rot_to_quat(R):
+    """Unit quaternion (x, y, z, w) of a rotation matrix (w >= 0)."""
+    tr = R[0, 0] + R[1, 1] + R[2, 2]
+    if tr > 0:
+        s = math.sqrt(tr + 1.0) * 2
+        w = 0.25 * s
+        x = (R[2, 1] - R[1, 2]) / s
+        y = (R[0, 2] - R[2, 0]) / s
+        z = (R[1, 0] - R[0, 1]) / s
+    elif R[0, 0] > R[1, 1] and R[0, 0] > R[2, 2]:
+        s = math.sqrt(1.0 + R[0, 0] - R[1, 1] - R[2, 2]) * 2
+        w = (R[2, 1] - R[1, 2]) / s
+        x = 0.25 * s
+        y = (R[0, 1] + R[1, 0]) / s
+        z = (R[0, 2] + R[2, 0]) / s
+    elif R[1, 1] > R[2, 2]:
+        s = math.sqrt(1.0 + R[1, 1] - R[0, 0] - R[2, 2]) * 2
+        w = (R[0, 2] - R[2, 0]) / s
+        x = (R[0, 1] + R[1, 0]) / s
+        y = 0.25 * s
+        z = (R[1, 2] + R[2, 1]) / s
+    else:
+        s = math.sqrt(1.0 + R[2, 2] - R[0, 0] - R[1, 1]) * 2
+        w = (R[1, 0] - R[0, 1]) / s
+        x = (R[0, 2] + R[2, 0]) / s
+        y = (R[1, 2] + R[2, 1]) / s
+        z = 0.25 * s
+    q = np.array([x, y, z, w])
+    q /= np.linalg.norm(q)
+    if q[3] < 0:
+        q = -q
+    return q
+
+
+def quat_to_rot(q):
+    x, y, z, w = q
+    return np.array([
+        [1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+        [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+        [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)],
+    ])
+
+
+def se3_data(R, t):
+    """Sophus SE3d::data() layout: qx qy qz qw tx ty tz."""
+    q = rot_to_quat(R)
+    return np.concatenate([q, np.asarray(t, dtype=np.float64)])
+
+
+def se3_from_data(d):
+    return quat_to_rot(np.asarray(d[:4]) / np.linalg.norm(d[:4])), np.asarray(d[4:7], dtype=np.float64)
+
+
+# ----------------------------------------------------------------- texture / rendering
+@dataclass
+class Plane:
+    z: float
+    xmin: float = -1e9
+    xmax: float = 1e9
+    ymin: float = -1e9
+    ymax: float = 1e9
+    dirs: np.ndarray = field(default=None)
+    freqs: np.ndarray = field(default=None)
+    phases: np.ndarray = field(default=None)
+    amps: np.ndarray = field(default=None)
+    noise: np.ndarray = field(default=None)
+    noise_step: float = 0.0
+    lo: float = 0.0
+    hi: float = 1.0
+
+
+def _blur1(a):
+    """Separable Gaussian blur, sigma = 1 sample."""
+    k = np.exp(-0.5 * np.arange(-3, 4) ** 2)
+    k /= k.sum()
+    a = np.apply_along_axis(lambda r: np.convolve(r, k, mode="same"), 0, a)
+    a = np.apply_along_axis(lambda r: np.convolve(r, k, mode="same"), 1, a)
+    return a
+
+
+def make_plane(rng, z, f, **kw):
+    p = Plane(z=z, **kw)
+    n = 24
+    ang = rng.uniform(0, 2 * np.pi, n)
+    lam_px = rng.uniform(6.0, 48.0, n)
+    lam_world = lam_px * z / f
+    p.dirs = np.stack([np.cos(ang), np.sin(ang)], 1)
+    p.freqs = 2 * np.pi / lam_world
+    p.phases = rng.uniform(0, 2 * np.pi, n)
+    p.amps = rng.uniform(0.5, 1.0, n)
+    # blurred uniform noise on a grid of 1 px (at this depth) spacing, 2048 x 2048 samples
+    p.noise_step = z / f
+    p.noise = _blur1(rng.uniform(-1, 1, (512, 512)))
+    p.noise *= 1.0 / (np.abs(p.noise).max() + 1e-12)
+    # normalise the sinusoid sum to [lo, hi] via the amplitude bound
+    p.lo, p.hi = -p.amps.sum(), p.amps.sum()
+    return p
+
+
+def plane_texture(p: Plane, X, Y):
+    s = np.zeros_like(X)
+    for k in range(len(p.freqs)):
+        s += p.amps[k] * np.sin(p.freqs[k] * (p.dirs[k, 0] * X + p.dirs[k, 1] * Y) + p.phases[k])
+    s = (s - p.lo) / (p.hi - p.lo)  # 0..1, concentrated around 0.5
+    s = 0.5 + 2.2 * (s - 0.5)
+    gx = X / p.noise_step
+    gy = Y / p.noise_step
+    n = p.noise.shape[0]
+    ix = np.floor(gx).astype(np.int64)
+    iy = np.floor(gy).astype(np.int64)
+    fx = gx - ix
+    fy = gy - iy
+    ix0, iy0 = ix % n, iy % n
+    ix1, iy1 = (ix + 1) % n, (iy + 1) % n
+    nz = (p.noise[iy0, ix0] * (1 - fx) * (1 - fy) + p.noise[iy0, ix1] * fx * (1 - fy)
+          + p.noise[iy1, ix0] * (1 - fx) * fy + p.noise[iy1, ix1] * fx * fy)
+    val = s + 0.08 * nz
+    return np.clip(20.0 + 215.0 * val, 20.0, 235.0)
+
+
+def render(planes, K, R_c2w, C, w, h, a=0.0, b=0.0):
+    """Exact ray/plane intersection at pixel centres; returns float32 image and depth."""
+    xs, ys = np.meshgrid(np.arange(w, dtype=np.float64), np.arange(h, dtype=np.float64))
+    Ki = np.linalg.inv(K)
+    d = np.stack([xs, ys, np.ones_like(xs)], -1) @ Ki.T
+    dw = d @ R_c2w.T
+    best = np.full((h, w), np.inf)
+    img = np.zeros((h, w))
+    for p in planes:
+        s = (p.z - C[2]) / dw[..., 2]
+        X = C[0] + s * dw[..., 0]
+        Y = C[1] + s * dw[..., 1]
+        ok = (s > 0) & (X >= p.xmin) & (X <= p.xmax) & (Y >= p.ymin) & (Y <= p.ymax) & (s < best)
+        if not ok.any():
+            continue
+        tex = plane_texture(p, X[ok], Y[ok])
+        img[ok] = tex
+        best[ok] = s[ok]
+    # camera-frame depth Z = s * d_z (d_z = 1 for the normalised ray)
+    depth = best * d[..., 2]
+    img = math.exp(a) * img + b
+    return img.astype(np.float32), depth
+
+
+def make_dir_pyramid(img0: np.ndarray, levels: int):
+    """Frame::CreateDirPyrs (Src/Frame.cpp:104-166): list of (h_l, w_l, 3) float32 [I, dx, dy]."""
+    pyr = []
+    I = img0.astype(np.float32)
+    for lvl in range(levels):
+        if lvl > 0:
+            prev = pyr[-1][..., 0]
+            h, w = prev.shape[0] // 2, prev.shape[1] // 2
+            a = prev[0:2 * h:2, 0:2 * w:2]
+            bb = prev[0:2 * h:2, 1:2 * w:2]
+            c = prev[1:2 * h:2, 0:2 * w:2]
+            d = prev[1:2 * h:2, 1:2 * w:2]
+            I = np.float32(0.25) * (((a + bb) + c) + d)
+        h, w = I.shape
+        out = np.zeros((h, w, 3), dtype=np.float32)
+        out[..., 0] = I
+        flat = I.reshape(-1)
+        idx = np.arange(w, w * (h - 1))
+        dx = np.float32(0.5) * (flat[idx + 1] - flat[idx - 1])
+        dy = np.float32(0.5) * (flat[idx + w] - flat[idx - w])
+        dx[~np.isfinite(dx)] = 0
+        dy[~np.isfinite(dy)] = 0
+        o = out.reshape(-1, 3)
+        o[idx, 1] = dx
+        o[idx, 2] = dy
+        pyr.append(out)
+    return pyr
+
+
+# ----------------------------------------------------------------- BA window
+@dataclass
+class BAScene:
+    width: int
+    height: int
+    K: np.ndarray                 # level-0 intrinsics (fp64)
+    n_levels: int
+    frames_pose: np.ndarray       # [nF, 7] true worldToCam (SE3 data)
+    frames_eval: np.ndarray       # [nF, 7] evalPT given to the BA (perturbed)
+    frames_state: np.ndarray      # [nF, 10]
+    frames_state_zero: np.ndarray
+    frames_exposure: np.ndarray   # [nF] float32
+    frames_energyTH: np.ndarray   # [nF] float32
+    frames_id: np.ndarray         # [nF] int32
+    pyramids: list                # per frame: list of (h_l, w_l, 3) float32
+    pt_host: np.ndarray           # [n] int32 (sorted)
+    pt_u: np.ndarray              # [n] float32
+    pt_v: np.ndarray
+    pt_idepth: np.ndarray
+    pt_idepth_zero: np.ndarray
+    pt_color: np.ndarray          # [n, 8] float32
+    pt_weights: np.ndarray        # [n, 8] float32
+    pt_idepth_true: np.ndarray
+    res_point: np.ndarray         # [m] int32 (grouped by point)
+    res_target: np.ndarray        # [m] int32
+    planes: list = field(default=None, repr=False)
+
+    @property
+    def n_frames(self):
+        return len(self.frames_id)
+
+    @property
+    def n_points(self):
+        return len(self.pt_u)
+
+    @property
+    def n_res(self):
+        return len(self.res_point)
+
+    def shard(self, rank: int, nranks: int) -> "BAScene":
+        """Point shard for multi-GPU: points p with p % nranks == rank (stays sorted by host),
+        with their residuals (all residuals of a point live on one rank)."""
+        import copy
+        sel = np.nonzero(np.arange(self.n_points) % nranks == rank)[0]
+        remap = -np.ones(self.n_points, np.int64)
+        remap[sel] = np.arange(len(sel))
+        rsel = remap[self.res_point] >= 0
+        out = copy.copy(self)
+        for name in ("pt_host", "pt_u", "pt_v", "pt_idepth", "pt_idepth_zero", "pt_color", "pt_weights",
+                     "pt_idepth_true"):
+            setattr(out, name, np.ascontiguousarray(getattr(self, name)[sel]))
+        out.res_point = remap[self.res_point[rsel]].astype(np.int32)
+        out.res_target = np.ascontiguousarray(self.res_target[rsel])
+        return out
+
+    def images_level0(self):
+        return [np.ascontiguousarray(p[0]) for p in self.pyramids]
+
+
+def _select_points(img_pyr0, n_pts, border, rng):
+    h, w = img_pyr0.shape[:2]
+    g2 = img_pyr0[..., 1].astype(np.float64) ** 2 + img_pyr0[..., 2].astype(np.float64) ** 2
+    area = (w - 2 * border) * (h - 2 * border)
+    cell = max(1, int(math.floor(math.sqrt(area / float(n_pts)))))
+    cands = []
+    for y0 in range(border, h - border - cell + 1, cell):
+        for x0 in range(border, w - border - cell + 1, cell):
+            blk = g2[y0:y0 + cell, x0:x0 + cell]
+            k = int(np.argmax(blk))
+            cands.append((y0 + k // cell, x0 + k % cell))
+    while len(cands) < n_pts:  # degenerate: fall back to random pixels
+        cands.append((int(rng.integers(border, h - border)), int(rng.integers(border, w - border))))
+    cands = np.array(cands)
+    sel = np.round(np.arange(n_pts) * (len(cands) / float(n_pts))).astype(np.int64)
+    sel = np.minimum(sel, len(cands) - 1)
+    return cands[sel]
+
+
+def make_ba_scene(n_points: int = 2000, n_frames: int = 8, width: int = 640, height: int = 480,
+                  K=None, seed: int = SEED, pose_noise=(0.004, 0.002), idepth_noise: float = 0.01,
+                  baseline: float = 0.06, max_rot_deg: float = 1.0, kitti: bool = False) -> BAScene:
+    """C3/C4 window: n_frames KFs x n_points (n_points / n_frames per host)."""
+    rng = np.random.default_rng(seed)
+    if K is None:
+        if kitti:
+            K = np.array([[718.856, 0, 615.5], [0, 718.856, 183.5], [0, 0, 1.0]])
+        else:
+            K = np.array([[256.0, 0, 319.5], [0, 254.4, 239.5], [0, 0, 1.0]])
+    K = np.asarray(K, dtype=np.float64)
+    f = K[0, 0]
+    planes = [make_plane(rng, 5.0, f), make_plane(rng, 3.0, f, xmax=-0.25), make_plane(rng, 2.0, f, xmin=0.55, ymax=0.15)]
+    levels = pyramid_levels(width, height)
+    poses, evals, pyrs = [], [], []
+    for i in range(n_frames):
+        ax = rng.normal(size=3)
+        ax /= np.linalg.norm(ax)
+        ang = math.radians(rng.uniform(0, max_rot_deg))
+        R_c2w = rodrigues(ax * ang)
+        C = np.array([baseline * i, 0.0, 0.0])
+        img, _ = render(planes, K, R_c2w, C, width, height)
+        pyrs.append(make_dir_pyramid(img, levels))
+        R_w2c = R_c2w.T
+        t_w2c = -R_w2c @ C
+        poses.append(se3_data(R_w2c, t_w2c))
+        if i == 0:
+            evals.append(se3_data(R_w2c, t_w2c))
+        else:
+            dR = rodrigues(rng.normal(size=3) * pose_noise[1])
+            dt = rng.normal(size=3) * pose_noise[0]
+            evals.append(se3_data(dR @ R_w2c, dR @ t_w2c + dt))
+    poses = np.array(poses)
+    evals = np.array(evals)
+
+    per = [n_points // n_frames + (1 if i < n_points % n_frames else 0) for i in range(n_frames)]
+    hosts, us, vs, ids, idt, cols, wts = [], [], [], [], [], [], []
+    for hst in range(n_frames):
+        if per[hst] == 0:
+            continue
+        pix = _select_points(pyrs[hst][0], per[hst], 4, rng)
+        R_w2c, t_w2c = se3_from_data(poses[hst])
+        R_c2w = R_w2c.T
+        C = -R_c2w @ t_w2c
+        _, depth = render_depth_at(planes, K, R_c2w, C, pix)
+        lvl0 = pyrs[hst][0]
+        py = pix[:, 0:1] + PATTERN[None, :, 1]
+        px = pix[:, 1:2] + PATTERN[None, :, 0]
+        smp = lvl0[py, px]                       # [n, 8, 3], exact pixels (BiLin at integer coords)
+        gx, gy = smp[..., 1], smp[..., 2]
+        c2500 = np.float32(2500.0)
+        wgt = np.sqrt(c2500 / (c2500 + (gx * gx + gy * gy))).astype(np.float32)
+        it = 1.0 / depth
+        hosts.append(np.full(len(pix), hst, np.int32))
+        us.append(pix[:, 1].astype(np.float32))
+        vs.append(pix[:, 0].astype(np.float32))
+        idt.append(it)
+        ids.append((it * (1.0 + idepth_noise * rng.normal(size=len(pix)))).astype(np.float32))
+        cols.append(smp[..., 0].astype(np.float32))
+        wts.append(wgt)
+    pt_host = np.concatenate(hosts)
+    pt_u = np.concatenate(us)
+    pt_v = np.concatenate(vs)
+    pt_id = np.concatenate(ids)
+
+    # residuals: centre projection of the noisy point into every other KF with the evalPT poses
+    Ki = np.linalg.inv(K)
+    hom = np.stack([pt_u, pt_v, np.ones_like(pt_u)], 1).astype(np.float64) @ Ki.T
+    ok_all = np.zeros((len(pt_host), n_frames), bool)
+    for hst in range(n_frames):
+        sel = np.nonzero(pt_host == hst)[0]
+        Rh, th = se3_from_data(evals[hst])
+        for t in range(n_frames):
+            if t == hst or len(sel) == 0:
+                continue
+            Rt, tt = se3_from_data(evals[t])
+            R = Rt @ Rh.T
+            tr = tt - R @ th
+            q = hom[sel] @ R.T + tr[None, :] * pt_id[sel, None].astype(np.float64)
+            with np.errstate(divide="ignore", invalid="ignore"):
+                ku = K[0, 0] * q[:, 0] / q[:, 2] + K[0, 2]
+                kv = K[1, 1] * q[:, 1] / q[:, 2] + K[1, 2]
+            ok_all[sel, t] = (q[:, 2] > 0) & (ku > 5.0) & (ku < width - 6) & (kv > 5.0) & (kv < height - 6)
+    rp, rt = np.nonzero(ok_all)   # row-major: grouped by point, targets ascending
+    rp = rp.astype(np.int32)
+    rt = rt.astype(np.int32)
+    return BAScene(
+        width=width, height=height, K=K, n_levels=levels,
+        frames_pose=poses, frames_eval=evals,
+        frames_state=np.zeros((n_frames, 10)), frames_state_zero=np.zeros((n_frames, 10)),
+        frames_exposure=np.ones(n_frames, np.float32),
+        frames_energyTH=np.full(n_frames, 8 * 8 * 8, np.float32),
+        frames_id=np.arange(n_frames, dtype=np.int32),
+        pyramids=pyrs,
+        pt_host=pt_host, pt_u=pt_u, pt_v=pt_v, pt_idepth=pt_id, pt_idepth_zero=pt_id.copy(),
+        pt_color=np.ascontiguousarray(np.concatenate(cols)), pt_weights=np.ascontiguousarray(np.concatenate(wts)),
+        pt_idepth_true=np.concatenate(idt),
+        res_point=rp, res_target=rt, planes=planes)
+
+
+def render_depth_at(planes, K, R_c2w, C, pix):
+    """Depth (camera Z) of the visible surface at integer pixels (y, x)."""
+    ys = pix[:, 0].astype(np.float64)
+    xs = pix[:, 1].astype(np.float64)
+    Ki = np.linalg.inv(K)
+    d = np.stack([xs, ys, np.ones_like(xs)], -1) @ Ki.T
+    dw = d @ R_c2w.T
+    best = np.full(len(xs), np.inf)
+    for p in planes:
+        s = (p.z - C[2]) / dw[:, 2]
+        X = C[0] + s * dw[:, 0]
+        Y = C[1] + s * dw[:, 1]
+        ok = (s > 0) & (X >= p.xmin) & (X <= p.xmax) & (Y >= p.ymin) & (Y <= p.ymax) & (s < best)
+        best[ok] = s[ok]
+    return None, best * d[:, 2]

@@ -1,0 +1,99 @@
+/*
+ * hs_ba.h — C-ABI drop-in boundary of H-SLAM's windowed photometric BA hot path
+ * on MI355X (gfx950).  Plain C: pointers + sizes, caller-owned host buffers
+ * copied in/out, the context owns all device memory and its HIP stream.
+ * Every entry point returns an hs status code (hs_types.h); no exception
+ * crosses the ABI.  A context is single-caller (not thread-safe); use one
+ * context per thread (tracking vs mapping, Src/System.cpp:182-212).
+ *
+ * Reference interface each entry point replaces (AUBVRL/H-SLAM):
+ *   hs_create / hs_destroy      new/delete EnergyFunctional + its IndexThreadReduce pool
+ *                               (Src/System.cpp:51; Include/EnergyFunctional.h:37-38)
+ *   hs_ba_set_window            EnergyFunctional::insertFrame/insertPoint/insertResidual + makeIDX +
+ *                               setAdjointsF + System::setPrecalcValues
+ *                               (Src/EnergyFunctional.cpp:371-425,819-840,22-82; Src/System.cpp:321-331)
+ *   hs_ba_linearize             System::linearizeAll(false) + applyRes_Reductor + setNewFrameEnergyTH
+ *                               (Src/FullSystemOptimize.cpp:102-124,55-59,60-101); on the GPU the
+ *                               accumulateAF/SCF_MT point loops (Src/EnergyFunctional.cpp:155-220)
+ *                               are fused into the same pass.
+ *   hs_ba_solve_system          System::solveSystem -> EnergyFunctional::solveSystemF
+ *                               (Src/FullSystemOptimize.cpp:552-561; Src/EnergyFunctional.cpp:705-817):
+ *                               stitch, prior, Schur, scaled LDLT, orthogonalize, resubstituteF_MT.
+ *   hs_ba_do_step               System::backupState + doStepFromBackup(1,1,1,1,1) + setPrecalcValues
+ *                               (Src/FullSystemOptimize.cpp:269-314,171-264)
+ *   hs_ba_optimize              System::optimize GN loop (Src/FullSystemOptimize.cpp:362-494),
+ *                               setting_forceAceptStep = true.
+ *   hs_ba_iterate               the loop body of System::optimize (Src/FullSystemOptimize.cpp:420-494)
+ *   hs_ba_get_system            HA/bA (accumulateAF_MT), HL/bL (accumulateLF_MT), H_sc/b_sc (accumulateSCF_MT)
+ *   hs_ba_get_* / hs_ba_set_marginal_prior   read-back of PointFrameResidual / MapPoint / FrameOptimizationData
+ *                               state; EnergyFunctional::HM/bM.
+ *   hs_comm_*                   (new) RCCL communicator for point-sharded windows; one rank per GPU.
+ */
+#ifndef HS_BA_H
+#define HS_BA_H
+
+#include "hs_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct hs_ctx hs_ctx;
+
+int hs_params_default(hs_params* out);
+const char* hs_last_error(void);
+
+int hs_create(hs_ctx** out, const hs_params* params, int device_id);
+void hs_destroy(hs_ctx* ctx);
+
+/* images: nF host pointers to level-0 (I, dI/dx, dI/dy) float triplets, W*H*3 floats each
+   (Frame::DirPyr[0] layout).  points MUST be sorted by host, residuals grouped by point. */
+int hs_ba_set_window(hs_ctx* ctx, const hs_camera* cam, int nF, const hs_frame* frames,
+                     const float* const* images, const hs_points* points, const hs_residuals* residuals);
+
+/* one linearizeAll(false) + applyRes over all residuals; reset=1 applies resetOOB first (optimize() entry).
+   energy_out: sum of the linearize() energies (nullable; forces a sync). */
+int hs_ba_linearize(hs_ctx* ctx, int reset, double* energy_out);
+
+/* solveSystemF on the systems accumulated by the last hs_ba_linearize. x_out: dim = 4 + 8*nF (nullable). */
+int hs_ba_solve_system(hs_ctx* ctx, int iteration, double* x_out);
+
+/* doStepFromBackup with all step factors 1; canbreak_out nullable. */
+int hs_ba_do_step(hs_ctx* ctx, int* canbreak_out);
+
+/* System::optimize loop: energies_out[max_iters+1] nullable, iters_done nullable. */
+int hs_ba_optimize(hs_ctx* ctx, int max_iters, int allow_break, double* energies_out, int* iters_done);
+
+/* n_iters GN iterations (solve + step + linearize) continuing from the current linearization,
+   iteration numbers first_iteration.. (orthogonalize from iteration 2); no early break.
+   energies_out[n_iters] nullable.  This is the benchmark's "step". */
+int hs_ba_iterate(hs_ctx* ctx, int first_iteration, int n_iters, double* energies_out);
+
+/* which: 0 = HA/bA, 1 = HL/bL (priors), 2 = H_sc/b_sc. H: dim*dim row-major, b: dim. */
+int hs_ba_get_system(hs_ctx* ctx, int which, double* H, double* b);
+
+/* per-residual read-back (all nullable): ResState, isActive, energy, energy-with-outlier (-1 = none),
+   JpJdF [n][8], centerProjectedTo [n][3] */
+int hs_ba_get_residuals(hs_ctx* ctx, uint8_t* state, uint8_t* active, float* energy, float* energy_wo,
+                        float* JpJdF, float* center);
+/* per-point read-back (all nullable) */
+int hs_ba_get_points(hs_ctx* ctx, float* idepth, float* step, float* HdiF, float* bdSumF);
+/* per-frame: state[nF][10], frameEnergyTH[nF], PRE_worldToCam[nF][7]; calib value[4] (all nullable) */
+int hs_ba_get_frames(hs_ctx* ctx, double* state, float* energyTH, double* pose7, double* calib4);
+/* EnergyFunctional::HM / bM (marginalization prior); dim*dim and dim */
+int hs_ba_set_marginal_prior(hs_ctx* ctx, const double* HM, const double* bM);
+
+/* device-event timing of the last hs_ba_optimize (ms): [0] linearize kernel sum, [1] reduce+stitch,
+   [2] resub, [3] energy-threshold, [4] total GN loop wall (host clock), [5] iterations */
+int hs_ba_get_timings(hs_ctx* ctx, double* out6);
+
+/* multi-GPU (point sharding): 128-byte RCCL unique id from rank 0, broadcast by the caller.
+   hs_comm_init must be called before hs_ba_set_window.  Each rank loads its own point shard (same frames);
+   per GN iteration the stitched H/b/energy are all-reduced and the newest-frame energies all-gathered. */
+int hs_comm_get_unique_id(char* id128);
+int hs_comm_init(hs_ctx* ctx, const char* id128, int rank, int nranks);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HS_BA_H */

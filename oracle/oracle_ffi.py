@@ -1,0 +1,259 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+ctypes bindings of the CPU restatement (oracle/_build/liboracle*.so).  Only
+tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this.
+Parity status: unpinned against the reference (see oracle/oracle_common.h).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+BUILD = os.path.join(HERE, "_build")
+
+
+class hs_camera(C.Structure):
+    _fields_ = [("width", C.c_int), ("height", C.c_int), ("n_levels", C.c_int), ("pad", C.c_int),
+                ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float)]
+
+
+class hs_frame(C.Structure):
+    _fields_ = [("worldToCam_evalPT", C.c_double * 7), ("state", C.c_double * 10), ("state_zero", C.c_double * 10),
+                ("ab_exposure", C.c_float), ("frameEnergyTH", C.c_float), ("id", C.c_int), ("pad", C.c_int)]
+
+
+class hs_points(C.Structure):
+    _fields_ = [("n", C.c_int), ("host", C.c_void_p), ("u", C.c_void_p), ("v", C.c_void_p), ("idepth", C.c_void_p),
+                ("idepth_zero", C.c_void_p), ("color", C.c_void_p), ("weights", C.c_void_p),
+                ("has_depth_prior", C.c_void_p)]
+
+
+class hs_residuals(C.Structure):
+    _fields_ = [("n", C.c_int), ("point", C.c_void_p), ("target", C.c_void_p), ("state", C.c_void_p)]
+
+
+class hs_params(C.Structure):
+    _fields_ = [(n, C.c_float) for n in (
+        "huberTH", "outlierTHSumComponent", "frameEnergyTHN", "frameEnergyTHFacMedian", "frameEnergyTHConstWeight",
+        "overallEnergyTHWeight", "idepthFixPrior", "initialCalibHessian", "affineOptModeA", "affineOptModeB",
+        "initialRotPrior", "initialTransPrior", "initialAffAPrior", "initialAffBPrior")] + [
+        ("solverModeDelta", C.c_double), ("thOptIterations", C.c_float), ("coarseCutoffTH", C.c_float),
+        ("minOptIterations", C.c_int), ("pad", C.c_int)]
+
+
+def build(quiet=True):
+    r = subprocess.run(["make", "-C", HERE, "-j4"], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("oracle build failed:\n" + r.stdout + r.stderr)
+
+
+_LIBS = {}
+
+
+def load(fast=False):
+    name = "liboracle_fast.so" if fast else "liboracle.so"
+    if name in _LIBS:
+        return _LIBS[name]
+    path = os.path.join(BUILD, name)
+    if not os.path.exists(path):
+        build()
+    lib = C.CDLL(path)
+    vp = C.c_void_p
+    lib.hso_ba_create.restype = vp
+    lib.hso_ba_create.argtypes = [vp, vp, C.c_int, vp, vp, vp, vp, C.c_int]
+    lib.hso_ba_destroy.argtypes = [vp]
+    lib.hso_ba_optimize.argtypes = [vp, C.c_int, C.c_int, vp]
+    lib.hso_ba_optimize.restype = C.c_int
+    lib.hso_ba_iterate.argtypes = [vp, C.c_int, C.c_int, vp]
+    lib.hso_ba_linearize_all.argtypes = [vp, C.c_int]
+    lib.hso_ba_linearize_all.restype = C.c_double
+    lib.hso_ba_apply_res.argtypes = [vp]
+    lib.hso_ba_accumulate.argtypes = [vp, C.c_int, vp, vp]
+    lib.hso_ba_solve_system.argtypes = [vp, C.c_int, vp]
+    lib.hso_ba_backup_state.argtypes = [vp]
+    lib.hso_ba_do_step.argtypes = [vp]
+    lib.hso_ba_do_step.restype = C.c_int
+    lib.hso_ba_get_residuals.argtypes = [vp] * 10
+    lib.hso_ba_get_points.argtypes = [vp] * 6
+    lib.hso_ba_get_frames.argtypes = [vp] * 5
+    lib.hso_ba_get_precalc.argtypes = [vp, vp]
+    lib.hso_ba_get_nullspaces.argtypes = [vp, vp]
+    lib.hso_ba_res_in_A.argtypes = [vp]
+    lib.hso_ba_res_in_A.restype = C.c_int
+    for n in ("hso_se3_exp", "hso_se3_log", "hso_se3_inverse", "hso_se3_adj", "hso_se3_matrix"):
+        getattr(lib, n).argtypes = [vp, vp]
+    lib.hso_se3_mul.argtypes = [vp, vp, vp]
+    for n, a in (("hso_track_create", None),):
+        pass
+    _LIBS[name] = lib
+    return lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+def default_params():
+    p = hs_params()
+    load().hso_params_default(C.byref(p))
+    return p
+
+
+class OracleBA:
+    """The reference's EnergyFunctional/System BA on one window, as a CPU restatement."""
+
+    def __init__(self, scene, nthreads=1, fast=False, params=None):
+        self.lib = load(fast)
+        self.scene = scene
+        nF = scene.n_frames
+        self._keep = []
+        cam = hs_camera(scene.width, scene.height, scene.n_levels, 0, float(scene.K[0, 0]), float(scene.K[1, 1]),
+                        float(scene.K[0, 2]), float(scene.K[1, 2]))
+        fr = (hs_frame * nF)()
+        for i in range(nF):
+            fr[i].worldToCam_evalPT[:] = list(scene.frames_eval[i])
+            fr[i].state[:] = list(scene.frames_state[i])
+            fr[i].state_zero[:] = list(scene.frames_state_zero[i])
+            fr[i].ab_exposure = float(scene.frames_exposure[i])
+            fr[i].frameEnergyTH = float(scene.frames_energyTH[i])
+            fr[i].id = int(scene.frames_id[i])
+        imgs = [np.ascontiguousarray(scene.pyramids[i][0], dtype=np.float32) for i in range(nF)]
+        self._keep += imgs
+        img_ptrs = (C.c_void_p * nF)(*[im.ctypes.data for im in imgs])
+        arrs = dict(host=np.ascontiguousarray(scene.pt_host, np.int32), u=np.ascontiguousarray(scene.pt_u, np.float32),
+                    v=np.ascontiguousarray(scene.pt_v, np.float32),
+                    idepth=np.ascontiguousarray(scene.pt_idepth, np.float32),
+                    idepth_zero=np.ascontiguousarray(scene.pt_idepth_zero, np.float32),
+                    color=np.ascontiguousarray(scene.pt_color, np.float32),
+                    weights=np.ascontiguousarray(scene.pt_weights, np.float32))
+        self._keep += list(arrs.values())
+        pts = hs_points(scene.n_points, *[_p(arrs[k]) for k in ("host", "u", "v", "idepth", "idepth_zero", "color",
+                                                                 "weights")], None)
+        rp = np.ascontiguousarray(scene.res_point, np.int32)
+        rt = np.ascontiguousarray(scene.res_target, np.int32)
+        self._keep += [rp, rt]
+        rs = hs_residuals(scene.n_res, _p(rp), _p(rt), None)
+        self.params = params if params is not None else default_params()
+        self.h = self.lib.hso_ba_create(C.byref(self.params), C.byref(cam), nF, C.cast(fr, C.c_void_p),
+                                        C.cast(img_ptrs, C.c_void_p), C.byref(pts),
+                                        C.byref(rs), nthreads)
+        if not self.h:
+            raise RuntimeError("hso_ba_create failed")
+        self.nF = nF
+        self.dim = 4 + 8 * nF
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.lib.hso_ba_destroy(self.h)
+            self.h = None
+
+    def optimize(self, iters=6, allow_break=False):
+        e = np.zeros(max(iters, 20) + 2)
+        n = self.lib.hso_ba_optimize(self.h, iters, int(allow_break), _p(e))
+        return n, e[: n + 1]
+
+    def iterate(self, it0, K):
+        e = np.zeros(K)
+        self.lib.hso_ba_iterate(self.h, it0, K, _p(e))
+        return e
+
+    def linearize_all(self, reset=False):
+        return self.lib.hso_ba_linearize_all(self.h, int(reset))
+
+    def apply_res(self):
+        self.lib.hso_ba_apply_res(self.h)
+
+    def accumulate(self, which):
+        H = np.zeros((self.dim, self.dim))
+        b = np.zeros(self.dim)
+        self.lib.hso_ba_accumulate(self.h, which, _p(H), _p(b))
+        return H, b
+
+    def solve_system(self, iteration):
+        x = np.zeros(self.dim)
+        self.lib.hso_ba_solve_system(self.h, iteration, _p(x))
+        return x
+
+    def backup_state(self):
+        self.lib.hso_ba_backup_state(self.h)
+
+    def do_step(self):
+        return bool(self.lib.hso_ba_do_step(self.h))
+
+    def residuals(self):
+        n = self.scene.n_res
+        out = dict(state=np.zeros(n, np.uint8), new_state=np.zeros(n, np.uint8), energy=np.zeros(n),
+                   new_energy=np.zeros(n), energy_wo=np.zeros(n), resF=np.zeros((n, 8), np.float32),
+                   J=np.zeros((n, 28), np.float32), JpJdF=np.zeros((n, 8), np.float32),
+                   center=np.zeros((n, 3), np.float32))
+        self.lib.hso_ba_get_residuals(self.h, *[_p(out[k]) for k in ("state", "new_state", "energy", "new_energy",
+                                                                      "energy_wo", "resF", "J", "JpJdF", "center")])
+        return out
+
+    def points(self):
+        n = self.scene.n_points
+        out = {k: np.zeros(n, np.float32) for k in ("idepth", "step", "HdiF", "bdSumF", "Hdd_accAF")}
+        self.lib.hso_ba_get_points(self.h, *[_p(out[k]) for k in ("idepth", "step", "HdiF", "bdSumF", "Hdd_accAF")])
+        return out
+
+    def frames(self):
+        st = np.zeros((self.nF, 10))
+        th = np.zeros(self.nF, np.float32)
+        pose = np.zeros((self.nF, 7))
+        cal = np.zeros(4)
+        self.lib.hso_ba_get_frames(self.h, _p(st), _p(th), _p(pose), _p(cal))
+        return dict(state=st, energyTH=th, pose=pose, calib=cal)
+
+    def precalc(self):
+        out = np.zeros((self.nF * self.nF, 39), np.float32)
+        self.lib.hso_ba_get_precalc(self.h, _p(out))
+        return out
+
+    def nullspaces(self):
+        N = np.zeros((7, self.dim))
+        self.lib.hso_ba_get_nullspaces(self.h, _p(N))
+        return N
+
+    def res_in_A(self):
+        return self.lib.hso_ba_res_in_A(self.h)
+
+
+# ------------------------------------------------------------------ SE3 helpers (Sophus restatement)
+def se3_exp(a):
+    out = np.zeros(7)
+    load().hso_se3_exp(_p(np.ascontiguousarray(a, np.float64)), _p(out))
+    return out
+
+
+def se3_log(d):
+    out = np.zeros(6)
+    load().hso_se3_log(_p(np.ascontiguousarray(d, np.float64)), _p(out))
+    return out
+
+
+def se3_mul(a, b):
+    out = np.zeros(7)
+    load().hso_se3_mul(_p(np.ascontiguousarray(a, np.float64)), _p(np.ascontiguousarray(b, np.float64)), _p(out))
+    return out
+
+
+def se3_inverse(a):
+    out = np.zeros(7)
+    load().hso_se3_inverse(_p(np.ascontiguousarray(a, np.float64)), _p(out))
+    return out
+
+
+def se3_adj(a):
+    out = np.zeros(36)
+    load().hso_se3_adj(_p(np.ascontiguousarray(a, np.float64)), _p(out))
+    return out.reshape(6, 6)
+
+
+def se3_matrix(a):
+    out = np.zeros(9)
+    load().hso_se3_matrix(_p(np.ascontiguousarray(a, np.float64)), _p(out))
+    return out.reshape(3, 3)

@@ -1,0 +1,25 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (os.path.join(ROOT, "h-slam_amd"), os.path.join(ROOT, "oracle"), ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device); run with -m gpu")
+
+
+@pytest.fixture(scope="session")
+def scene2k():
+    from hslam_amd.scene import make_ba_scene
+    return make_ba_scene(n_points=2000)
+
+
+@pytest.fixture(scope="session")
+def scene_small():
+    from hslam_amd.scene import make_ba_scene
+    return make_ba_scene(n_points=240, seed=7)
