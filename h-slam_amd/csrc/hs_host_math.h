@@ -17,6 +17,10 @@
 #include "hs_layout.h"
 #include "hs_se3.h"
 
+#ifndef HS_HD
+#define HS_HD __host__ __device__
+#endif
+
 namespace hs {
 
 constexpr float SCALE_XI_ROT = 1.0f, SCALE_XI_TRANS = 0.5f, SCALE_F = 50.0f, SCALE_C = 50.0f;
@@ -24,16 +28,16 @@ constexpr float SCALE_A = 10.0f, SCALE_B = 1000.0f;
 constexpr float SCALE_XI_ROT_INVERSE = 1.0f / SCALE_XI_ROT, SCALE_XI_TRANS_INVERSE = 1.0f / SCALE_XI_TRANS;
 constexpr float SCALE_F_INVERSE = 1.0f / SCALE_F, SCALE_C_INVERSE = 1.0f / SCALE_C;
 
-inline void mm3f(const float A[9], const float B[9], float C[9]) {
+HS_HD inline void mm3f(const float A[9], const float B[9], float C[9]) {
   for (int r = 0; r < 3; r++)
     for (int c = 0; c < 3; c++)
       C[r * 3 + c] = A[r * 3 + 0] * B[0 * 3 + c] + A[r * 3 + 1] * B[1 * 3 + c] + A[r * 3 + 2] * B[2 * 3 + c];
 }
-inline void mv3f(const float A[9], const float v[3], float o[3]) {
+HS_HD inline void mv3f(const float A[9], const float v[3], float o[3]) {
   for (int r = 0; r < 3; r++) o[r] = A[r * 3 + 0] * v[0] + A[r * 3 + 1] * v[1] + A[r * 3 + 2] * v[2];
 }
 // Eigen compute_inverse_size3 in float
-inline void inv3f(const float m[9], float r[9]) {
+HS_HD inline void inv3f(const float m[9], float r[9]) {
   auto M = [&](int i, int j) { return m[i * 3 + j]; };
   auto cof = [&](int i, int j) {
     int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
@@ -46,10 +50,10 @@ inline void inv3f(const float m[9], float r[9]) {
   r[3] = cof(0, 1) * invdet; r[4] = cof(1, 1) * invdet; r[5] = cof(2, 1) * invdet;
   r[6] = cof(0, 2) * invdet; r[7] = cof(1, 2) * invdet; r[8] = cof(2, 2) * invdet;
 }
-inline void fromToVecExposure(float eF, float eT, double g2Fa, double g2Fb, double g2Ta, double g2Tb,
+HS_HD inline void fromToVecExposure(float eF, float eT, double g2Fa, double g2Fb, double g2Ta, double g2Tb,
                               double out[2]) {
   if (eF == 0 || eT == 0) eT = eF = 1;
-  double a = std::exp(g2Ta - g2Fa) * eT / eF;
+  double a = exp(g2Ta - g2Fa) * eT / eF;
   out[0] = a;
   out[1] = g2Tb - a * g2Fb;
 }
@@ -58,7 +62,7 @@ struct CalibH {
   int W = 0, H = 0;
   double value[4], value_zero[4], value_minus_value_zero[4], value_scaled[4], value_backup[4], step[4];
   float value_scaledf[4], value_scaledi[4];
-  void setValueScaled(const double vs[4]) {
+  HS_HD void setValueScaled(const double vs[4]) {
     for (int i = 0; i < 4; i++) value_scaled[i] = vs[i];
     for (int i = 0; i < 4; i++) value_scaledf[i] = (float)value_scaled[i];
     value[0] = SCALE_F_INVERSE * vs[0];
@@ -68,7 +72,7 @@ struct CalibH {
     for (int i = 0; i < 4; i++) value_minus_value_zero[i] = value[i] - value_zero[i];
     scaledi();
   }
-  void setValue(const double v[4]) {
+  HS_HD void setValue(const double v[4]) {
     for (int i = 0; i < 4; i++) value[i] = v[i];
     value_scaled[0] = SCALE_F * v[0];
     value_scaled[1] = SCALE_F * v[1];
@@ -78,13 +82,13 @@ struct CalibH {
     scaledi();
     for (int i = 0; i < 4; i++) value_minus_value_zero[i] = value[i] - value_zero[i];
   }
-  void scaledi() {
+  HS_HD void scaledi() {
     value_scaledi[0] = 1.0f / value_scaledf[0];
     value_scaledi[1] = 1.0f / value_scaledf[1];
     value_scaledi[2] = -value_scaledf[2] / value_scaledf[0];
     value_scaledi[3] = -value_scaledf[3] / value_scaledf[1];
   }
-  HsCalib device() const {
+  HS_HD HsCalib device() const {
     HsCalib c;
     c.fxl = value_scaledf[0]; c.fyl = value_scaledf[1]; c.cxl = value_scaledf[2]; c.cyl = value_scaledf[3];
     c.fxli = value_scaledi[0]; c.fyli = value_scaledi[1];
@@ -101,12 +105,12 @@ struct FrameH {
   double nullspaces_pose[6][6], nullspaces_scale[6];
   double prior[8] = {0}, delta_prior[8] = {0}, delta[8] = {0};
 
-  double aff_a() const { return state_scaled[6]; }
-  double aff_b() const { return state_scaled[7]; }
-  double aff0_a() const { return state_zero[6] * SCALE_A; }
-  double aff0_b() const { return state_zero[7] * SCALE_B; }
+  HS_HD double aff_a() const { return state_scaled[6]; }
+  HS_HD double aff_b() const { return state_scaled[7]; }
+  HS_HD double aff0_a() const { return state_zero[6] * SCALE_A; }
+  HS_HD double aff0_b() const { return state_zero[7] * SCALE_B; }
 
-  void setState(const double s[10]) {
+  HS_HD void setState(const double s[10]) {
     for (int i = 0; i < 10; i++) state[i] = s[i];
     for (int i = 0; i < 3; i++) state_scaled[i] = SCALE_XI_TRANS * s[i];
     for (int i = 3; i < 6; i++) state_scaled[i] = SCALE_XI_ROT * s[i];
@@ -117,7 +121,7 @@ struct FrameH {
     PRE_worldToCam = SE3::exp(state_scaled) * evalPT;
     PRE_camToWorld = PRE_worldToCam.inverse();
   }
-  void setStateZero(const double sz[10]) {
+  HS_HD void setStateZero(const double sz[10]) {
     for (int i = 0; i < 10; i++) state_zero[i] = sz[i];
     for (int i = 0; i < 6; i++) {
       double ep[6] = {0, 0, 0, 0, 0, 0}, em[6] = {0, 0, 0, 0, 0, 0};
@@ -161,7 +165,7 @@ struct FrameH {
 };
 
 // FrameFramePrecalc::set -> device record
-inline HsPrecalc make_precalc(const FrameH& H, const FrameH& T, const CalibH& cal) {
+HS_HD inline HsPrecalc make_precalc(const FrameH& H, const FrameH& T, const CalibH& cal) {
   HsPrecalc pc;
   SE3 l2l0 = T.evalPT * H.evalPT.inverse();
   double R0[9];
@@ -190,7 +194,7 @@ inline HsPrecalc make_precalc(const FrameH& H, const FrameH& T, const CalibH& ca
 }
 
 // setAdjointsF for one (h, t): AH, AT (row-major 8x8, fp64) + float copies
-inline void make_adjoints(const FrameH& H, const FrameH& T, double AH[64], double AT[64]) {
+HS_HD inline void make_adjoints(const FrameH& H, const FrameH& T, double AH[64], double AT[64]) {
   SE3 h2t = T.evalPT * H.evalPT.inverse();
   for (int i = 0; i < 64; i++) AH[i] = AT[i] = (i % 9 == 0) ? 1.0 : 0.0;
   double Ad[36];

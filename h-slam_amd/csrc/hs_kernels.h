@@ -1,101 +1,149 @@
-// hs_kernels.h — kernel argument blocks and launch declarations (host <-> device).
+// hs_kernels.h — kernel argument blocks, the device-resident window state and launch declarations.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "../../include/hs_types.h"
+#include "hs_host_math.h"
 #include "hs_layout.h"
+
+// Window state owned by the device between GN iterations (updated by hs_k_solve).
+struct HsDevState {
+  hs::FrameH frames[HS_MAXF];
+  hs::CalibH calib;
+  HsCalib dcal;             // scaled calib read by the linearize kernel
+  float cstep[4];           // xF.head<CPARS>() of the last solve (resubstituteF_MT)
+  double lastX[HS_MAXDIM];
+  int nF;
+  int iteration;            // next GN iteration index (orthogonalize from 2)
+  int status;               // != 0: non-finite system / step
+  int log_count;            // number of energies written to the log
+  int canbreak;
+  int pad[3];
+};
 
 struct HsLinArgs {
   const float4* img[HS_MAXF];  // level-0 texels per window frame
-  HsCalib calib;
+  const HsDevState* st;
   HsLinParams lp;
   int nF;
   int write_center;
+  int fuse_step;               // apply resubstitute + point step of the previous solve first
   const HsPrecalc* pre;        // [nF*nF] host*nF + target
   const float* frameTH;        // [nF]
+  const float* xAd;            // [nF*nF][8] index h*nF + t (fuse_step)
   // points
+  const int* pt_host;
   const float* u;
   const float* v;
-  const float* idepth;
-  const float* idepth_zero;
+  float* idepth;
+  float* idepth_zero;
   const float* priorF;
   const float* color;          // [n][8]
   const float* weight;         // [n][8]
   const int* res_of_slot;      // [n][8]
   const int8_t* res_order;     // [n][8]
-  const int* chunk_begin;      // [n_chunks+1]
-  const int* chunk_host;       // [n_chunks]
   // residual state (in/out)
   uint8_t* r_state;
   uint8_t* r_active;
   float* r_energy;
   float* r_newEnergy;
   float* r_ewo;
-  float* r_JpJdF;              // [m][8]
   float* r_center;             // [m][3]
-  // point outputs
+  // per point outputs (slot layout)
+  uint8_t* p_actmask;
   float* p_HdiF;
   float* p_bdSumF;
   float* p_Hcd;                // [n][4]
-  uint8_t* p_ngood;
-  // accumulators
-  HsWavePartial* partials;
+  float* p_JpJdF;              // [n][8][8]
+  float* p_Jrec;               // [n][8][HS_JREC]
+  double* p_energy;            // [n]
+  float* p_step;               // [n]
   float* newest_cand;          // energies of residuals into the newest frame (setNewFrameEnergyTH)
   int* newest_cnt;
 };
 
-struct HsReduceArgs {
-  const HsWavePartial* partials;
-  const int* host_chunk_begin;  // [nF+1]
-  int n_chunks;
-  HsHostSlab* slabs;            // [nF]
-  double* energy;
-};
-
-struct HsStitchArgs {
-  int nF;
-  const HsHostSlab* slabs;
-  const double* adHost;         // [nF*nF][64]  index h + nF*t
-  const double* adTarget;
-  double* HA;                   // [n*n] zeroed
-  double* bA;
-  double* HSC;
-  double* bSC;
-};
-
-struct HsResubArgs {
-  int n, nF, apply;
-  float cstep[4];
-  const int* host;
-  const float* xAd;             // [nF*nF][8] index h*nF + t
-  const float* bdSumF;
+struct HsAccArgs {
+  int nF, S, nP;
+  const int* host_pt_begin;    // [nF+1]
+  const uint8_t* actmask;
   const float* HdiF;
+  const float* bdSumF;
   const float* Hcd;
-  const uint8_t* ngood;
-  const int* res_of_slot;
-  const int8_t* res_order;
-  const uint8_t* r_active;
   const float* JpJdF;
-  float* idepth;
-  float* idepth_zero;
-  float* step;
-  double* stat_partial;         // [blocks][2]
-};
-
-struct HsEnergyThArgs {
-  const float* cand;            // [nranks][stride]
-  const int* cnt;               // [nranks]
-  int nranks;
-  int stride;
+  const float* Jrec;
+  float* part;                 // [nF*nF][S][HS_PART_N]
+  int* part_cnt;               // [nF*nF][S][16]: top count, D counts (per k), E count
+  const double* p_energy;
+  const float* idepth;         // |idepth| sum for doStepFromBackup's sumNID
+  double* energy_out;          // [3]: energy, sum |idepth|, number of points
+  double* hccbc;               // [20] finished Hcc (16) + bc (4), fp64
+  // setNewFrameEnergyTH
+  const float* cand;
+  const int* cnt;
+  int nranks, stride;
   float* frameTH;
   int newest;
   float frameEnergyTHN, facMedian, constWeight, overallWeight;
 };
 
+struct HsStitchArgs {
+  int nF, S;
+  const float* part;
+  const int* part_cnt;
+  const double* hccbc;
+  const double* adHost;        // [nF*nF][64]  index h + nF*t
+  const double* adTarget;
+  double* HA;                  // [n*n] zeroed
+  double* bA;
+  double* HSC;
+  double* bSC;
+};
+
+enum { HS_SOLVE = 1, HS_APPLY = 2 };
+
+struct HsSolveArgs {
+  int flags;
+  int iteration;               // < 0: use st->iteration
+  HsDevState* st;
+  double* HA;                  // HA | bA | HSC | bSC, consumed then zeroed (SOLVE)
+  double* bA;
+  double* HSC;
+  double* bSC;
+  const double* HM;
+  const double* bM;
+  const double* Porth;         // [n*n] nullspace projector
+  const float* adHostF;        // [nF*nF][64]
+  const float* adTargetF;
+  float* xAd;                  // out [nF*nF][8]
+  HsPrecalc* pre;              // out [nF*nF]
+  double* x_out;               // [n]
+  const double* sysE;          // [3] energy, sum |idepth|, #points of the consumed linearization
+  double* energy_log;          // SOLVE appends sysE[0] at st->log_count
+  int* cnt_reset;              // newest-frame candidate counter zeroed for the next linearization
+  double initialCalibHessian;
+  float thOptIterations;
+};
+
+struct HsResubArgs {
+  int n, nF, apply;
+  const HsDevState* st;
+  const int* host;
+  const float* xAd;            // [nF*nF][8] index h*nF + t
+  const uint8_t* actmask;
+  const float* bdSumF;
+  const float* HdiF;
+  const float* Hcd;
+  const float* JpJdF;          // [n][8][8]
+  const int8_t* res_order;
+  float* idepth;
+  float* idepth_zero;
+  float* step;
+};
+
 __global__ void hs_k_linearize(HsLinArgs a);
-__global__ void hs_k_reduce(HsReduceArgs a);
+__global__ void hs_k_accumulate(HsAccArgs a);
 __global__ void hs_k_stitch(HsStitchArgs a);
+__global__ void hs_k_solve(HsSolveArgs a);
 __global__ void hs_k_resub(HsResubArgs a);
-__global__ void hs_k_energy_th(HsEnergyThArgs a);
 __global__ void hs_k_apply_step(int n, const float* step, float* idepth, float* idepth_zero);

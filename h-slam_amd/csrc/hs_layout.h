@@ -3,25 +3,40 @@
 // HBM; the reference's shared_ptr graph never exists on the
 // device.
 //
-//   images   : per frame, per level, float4 (I, dI/dx, dI/dy, 0) row-major
-//              (Frame::DirPyr, Include/Frame.h:39; 16-B texels so a bilinear
-//              tap is one dwordx4 load)
-//   points   : u, v, idepth, idepth_zero, priorF, host   [n]
-//              color, weight                           [n][8]
-//              res_of_slot                             [n][8]  residual index per
-//                                                      target frame (-1 = none)
-//              res_order                               [n][8]  target frames in the
-//                                                      point's residual-list order
-//   residuals: state / energy / new energy / energy-with-outlier / active,
-//              JpJdF [m][8], centre projection [m][3]
-//   precalc  : HsPrecalc [nF*nF] indexed host*nF + target (Frame::targetPrecalc)
-//   partials : one HsWavePartial per BA wave (per-host chunk of points)
+//   images    : per frame float4 (I, dI/dx, dI/dy, 0) row-major (Frame::DirPyr[0], Include/Frame.h:39;
+//               16-B texels: a bilinear tap is one dwordx4 load)
+//   points    : u, v, idepth, idepth_zero, priorF, host                       [n]
+//               color, weight                                                [n][8]
+//               res_of_slot  residual index per target frame slot (-1 none)  [n][8]
+//               res_order    target slots in the point's residual-list order [n][8]
+//   per point outputs of a linearization (slot layout, read by accumulate / resubstitute):
+//               actmask (bit t = residual into frame t is active), HdiF, bdSumF, Hcd[4],
+//               JpJdF [n][8 slots][8], Jrec [n][8 slots][36] (the residual's Jacobian digest),
+//               energy (double, the point's share of linearizeAll's sum), step
+//   residuals : state / energy / new energy / energy-with-outlier / active, centre projection [m][3]
+//   precalc   : HsPrecalc [nF*nF] indexed host*nF + target (Frame::targetPrecalc)
 #pragma once
 #include <stdint.h>
 
 #define HS_PN 8
 #define HS_MAXF 8
-#define HS_TOP_N 91   // 55 (10x10 upper) + 30 (10 x {a,b,r}) + 6 (3x3 upper)
+#define HS_MAXDIM (4 + 8 * HS_MAXF)
+#define HS_TOP_N 91    // 55 (10x10 upper) + 30 (10 x {a,b,r}) + 6 (3x3 upper)
+#define HS_JREC 36     // floats per residual Jacobian digest
+#define HS_PART_N 648  // per (host,target,split) partial: top 96 + D 512 + E 32 + EB 8
+
+// Jrec layout (per residual):
+//   [0..9]  x = [Jpdc0(4) Jpdxi0(6)]   [10..19] y = [Jpdc1 Jpdxi1]
+//   [20..22] JIdx2 00,01,11   [23..25] Jab2 00,01,11   [26..29] JabJIdx 00,01,10,11
+//   [30,31] JI_r   [32,33] Jab_r   [34] rr
+#define HS_JR_X 0
+#define HS_JR_Y 10
+#define HS_JR_JIDX2 20
+#define HS_JR_JAB2 23
+#define HS_JR_JABJIDX 26
+#define HS_JR_JIR 30
+#define HS_JR_JABR 32
+#define HS_JR_RR 34
 
 // FrameFramePrecalc restricted to what the linearize kernel reads
 // (Include/OptimizationClasses.h:55-86)
@@ -47,34 +62,4 @@ struct HsLinParams {
   float outlierTHSumComponent;
   float affineOptModeA;
   float affineOptModeB;
-};
-
-// one BA wave's accumulators (fp32), host frame = chunk host.
-// layout of top[t][e]: e < 55 : Data (upper-tri of [calib4|xi6]),
-//                      e < 85 : TopRight[3*r + {a,b,r}], e < 91 : BotRight
-struct HsWavePartial {
-  float top[HS_MAXF][96];              // [target][entry] (91 used)
-  float D[HS_MAXF][HS_MAXF][64];       // [t1][t2][8x8]   (accD host fixed)
-  float E[HS_MAXF][32];                // [t1][8x4]
-  float EB[HS_MAXF][8];                // [t1][8]
-  float Hcc[16];
-  float bc[4];
-  int cnt[HS_MAXF];                    // residuals accumulated per target (AccumulatorApprox::num)
-  int host;
-  int pad[3];
-  double energy;                       // sum of linearize() energies of the chunk's residuals
-  double pad2;
-};
-
-#define HS_WP_FLOATS (HS_MAXF * 96 + HS_MAXF * HS_MAXF * 64 + HS_MAXF * 32 + HS_MAXF * 8 + 16 + 4)
-
-// reduced per-host slab (fp64)
-struct HsHostSlab {
-  double top[HS_MAXF][96];
-  double D[HS_MAXF][HS_MAXF][64];
-  double E[HS_MAXF][32];
-  double EB[HS_MAXF][8];
-  double Hcc[16];
-  double bc[4];
-  int cnt[HS_MAXF];
 };

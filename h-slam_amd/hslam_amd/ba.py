@@ -135,7 +135,7 @@ class BAWindow:
     def timings(self):
         t = np.zeros(6)
         check(self.lib.hs_ba_get_timings(self.h, ptr(t)))
-        return dict(linearize_ms=t[0], reduce_stitch_ms=t[1], resub_ms=t[2], energy_th_ms=t[3], wall_ms=t[4],
+        return dict(linearize_ms=t[0], acc_stitch_ms=t[1], solve_ms=t[2], timed_iters=int(t[3]), wall_ms=t[4],
                     iters=int(t[5]))
 
     # --------------------------------------------------------------- multi-GPU

@@ -83,8 +83,9 @@ int hs_ba_get_frames(hs_ctx* ctx, double* state, float* energyTH, double* pose7,
 /* EnergyFunctional::HM / bM (marginalization prior); dim*dim and dim */
 int hs_ba_set_marginal_prior(hs_ctx* ctx, const double* HM, const double* bM);
 
-/* device-event timing of the last hs_ba_optimize (ms): [0] linearize kernel sum, [1] reduce+stitch,
-   [2] resub, [3] energy-threshold, [4] total GN loop wall (host clock), [5] iterations */
+/* device-event timing of the last hs_ba_optimize / hs_ba_iterate (ms, summed over the timed iterations):
+   [0] linearize kernel, [1] accumulate + stitch (+ RCCL exchange), [2] solve + step kernel,
+   [3] number of event-timed iterations, [4] total GN loop wall (host clock), [5] iterations */
 int hs_ba_get_timings(hs_ctx* ctx, double* out6);
 
 /* multi-GPU (point sharding): 128-byte RCCL unique id from rank 0, broadcast by the caller.
