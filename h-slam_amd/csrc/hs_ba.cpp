@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstddef>
 #include <cstdio>
@@ -33,7 +34,7 @@ int fail(int code, const std::string& msg) {
 
 constexpr int kLogCap = 4096;     // energies logged on the device per optimize / iterate call
 constexpr int kEventIters = 128;  // iterations timed with HIP events per call
-constexpr int kPointsPerSplit = 512;
+constexpr int kPointsPerSplit = 64;  // points per accumulate workgroup (env HS_ACC_SPLIT_POINTS)
 }  // namespace
 
 #define HS_HIP(x)                                                                                  \
@@ -70,7 +71,7 @@ struct hs_ctx {
   bool events = true;
 
   // window (host side)
-  int nF = 0, nP = 0, nR = 0, S = 1;
+  int nF = 0, nP = 0, nR = 0, S = 1, maxPtsPerBlock = 0;
   std::vector<int> pt_host, res_point, res_target, host_pt_begin;
   std::vector<int> res_of_slot;   // [nP*8]
   std::vector<int8_t> res_order;  // [nP*8]
@@ -106,9 +107,12 @@ struct hs_ctx {
   float* d_xAd = nullptr;
   double* d_x = nullptr;
   double* d_elog = nullptr;
-  float* d_cand = nullptr;  // [nranks][cand_stride]; this rank writes slot `rank`
-  int* d_cnt = nullptr;     // [nranks]
+  float* d_cand = nullptr;  // [nranks][cand_stride] newest-frame energy per point (-1 / NaN = none)
   int cand_stride = 0;
+  bool hm_zero = true;      // marginalization prior not set: the solve skips HM
+  // kernel tracing (env HS_KTRACE=1): per-block wall-clock checkpoints of the last iteration
+  bool tracing = false;
+  long long *d_tr_lin = nullptr, *d_tr_acc = nullptr, *d_tr_solve = nullptr, *d_tr_stitch = nullptr;
 
   // RCCL
   ncclComm_t comm = nullptr;
@@ -138,7 +142,7 @@ static void free_window(hs_ctx* c) {
                   c->d_r_center, c->d_p_actmask, c->d_p_HdiF, c->d_p_bdSumF, c->d_p_Hcd, c->d_p_JpJdF,
                   c->d_p_Jrec, c->d_p_step, c->d_p_energy, c->d_part, c->d_part_cnt, c->d_hccbc, c->d_adHost,
                   c->d_adTarget, c->d_adHostF, c->d_adTargetF, c->d_sys, c->d_HM, c->d_bM, c->d_Porth, c->d_xAd,
-                  c->d_x, c->d_elog, c->d_cand, c->d_cnt};
+                  c->d_x, c->d_elog, c->d_cand, c->d_tr_lin, c->d_tr_acc, c->d_tr_solve, c->d_tr_stitch};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   c->d_state = nullptr; c->d_pre = nullptr; c->d_frameTH = nullptr;
@@ -154,7 +158,8 @@ static void free_window(hs_ctx* c) {
   c->d_part = nullptr; c->d_part_cnt = nullptr; c->d_hccbc = nullptr;
   c->d_adHost = c->d_adTarget = nullptr; c->d_adHostF = c->d_adTargetF = nullptr;
   c->d_sys = nullptr; c->d_HM = c->d_bM = c->d_Porth = nullptr;
-  c->d_xAd = nullptr; c->d_x = nullptr; c->d_elog = nullptr; c->d_cand = nullptr; c->d_cnt = nullptr;
+  c->d_xAd = nullptr; c->d_x = nullptr; c->d_elog = nullptr; c->d_cand = nullptr;
+  c->d_tr_lin = c->d_tr_acc = c->d_tr_solve = c->d_tr_stitch = nullptr;
   c->nF = c->nP = c->nR = 0;
   c->haveSystem = false;
 }
@@ -215,7 +220,7 @@ static int launch_linearize(hs_ctx* c, int fuse) {
   a.p_actmask = c->d_p_actmask; a.p_HdiF = c->d_p_HdiF; a.p_bdSumF = c->d_p_bdSumF; a.p_Hcd = c->d_p_Hcd;
   a.p_JpJdF = c->d_p_JpJdF; a.p_Jrec = c->d_p_Jrec; a.p_energy = c->d_p_energy; a.p_step = c->d_p_step;
   a.newest_cand = c->d_cand + (size_t)c->rank * c->cand_stride;
-  a.newest_cnt = c->d_cnt + c->rank;
+  a.trace = c->d_tr_lin;
   if (c->nP > 0) hipLaunchKernelGGL(hs_k_linearize, dim3(c->nP), dim3(64), 0, c->stream, a);
   HS_HIP(hipGetLastError());
   return HS_OK;
@@ -223,21 +228,21 @@ static int launch_linearize(hs_ctx* c, int fuse) {
 
 // all-gather of newest-frame candidates, accumulate, stitch, all-reduce of the systems
 static int launch_reduce(hs_ctx* c) {
-  if (c->comm && c->nranks > 1) {
-    HS_NCCL(ncclAllGather(c->d_cnt + c->rank, c->d_cnt, 1, ncclInt, c->comm, c->stream));
+  if (c->comm && c->nranks > 1)
     HS_NCCL(ncclAllGather(c->d_cand + (size_t)c->rank * c->cand_stride, c->d_cand, c->cand_stride, ncclFloat,
                           c->comm, c->stream));
-  }
   HsAccArgs a;
   std::memset(&a, 0, sizeof(a));
   a.nF = c->nF; a.S = c->S; a.nP = c->nP;
+  a.blocked = c->maxPtsPerBlock > 1000 ? 1 : 0;
   a.host_pt_begin = c->d_host_pt_begin;
   a.actmask = c->d_p_actmask; a.HdiF = c->d_p_HdiF; a.bdSumF = c->d_p_bdSumF; a.Hcd = c->d_p_Hcd;
   a.JpJdF = c->d_p_JpJdF; a.Jrec = c->d_p_Jrec;
   a.part = c->d_part; a.part_cnt = c->d_part_cnt;
   a.p_energy = c->d_p_energy; a.idepth = c->d_idepth; a.energy_out = c->sysE();
   a.hccbc = c->d_hccbc;
-  a.cand = c->d_cand; a.cnt = c->d_cnt; a.nranks = c->nranks; a.stride = c->cand_stride;
+  a.cand = c->d_cand; a.nranks = c->nranks; a.stride = c->cand_stride;
+  a.trace = c->d_tr_acc;
   a.frameTH = c->d_frameTH; a.newest = c->nF - 1;
   a.frameEnergyTHN = c->P.frameEnergyTHN; a.facMedian = c->P.frameEnergyTHFacMedian;
   a.constWeight = c->P.frameEnergyTHConstWeight; a.overallWeight = c->P.overallEnergyTHWeight;
@@ -248,6 +253,7 @@ static int launch_reduce(hs_ctx* c) {
   s.part = c->d_part; s.part_cnt = c->d_part_cnt; s.hccbc = c->d_hccbc;
   s.adHost = c->d_adHost; s.adTarget = c->d_adTarget;
   s.HA = c->HA(); s.bA = c->bA(); s.HSC = c->HSC(); s.bSC = c->bSC();
+  s.trace = c->d_tr_stitch;
   hipLaunchKernelGGL(hs_k_stitch, dim3(c->nF * c->nF), dim3(64), 0, c->stream, s);
   HS_HIP(hipGetLastError());
   if (c->comm && c->nranks > 1)
@@ -262,15 +268,16 @@ static int launch_solve(hs_ctx* c, int flags, int iteration, bool log) {
   a.iteration = iteration;
   a.st = c->d_state;
   a.HA = c->HA(); a.bA = c->bA(); a.HSC = c->HSC(); a.bSC = c->bSC();
-  a.HM = c->d_HM; a.bM = c->d_bM; a.Porth = c->d_Porth;
+  a.HM = c->hm_zero ? nullptr : c->d_HM;
+  a.bM = c->d_bM; a.Porth = c->d_Porth;
   a.adHostF = c->d_adHostF; a.adTargetF = c->d_adTargetF;
   a.xAd = c->d_xAd; a.pre = c->d_pre; a.x_out = c->d_x;
   a.sysE = c->sysE();
   a.energy_log = log ? c->d_elog : nullptr;
-  a.cnt_reset = c->d_cnt + c->rank;
+  a.trace = c->d_tr_solve;
   a.initialCalibHessian = c->P.initialCalibHessian;
   a.thOptIterations = c->P.thOptIterations;
-  hipLaunchKernelGGL(hs_k_solve, dim3(1), dim3(256), 0, c->stream, a);
+  hipLaunchKernelGGL(hs_k_solve, dim3(1), dim3(512), 0, c->stream, a);
   HS_HIP(hipGetLastError());
   return HS_OK;
 }
@@ -287,7 +294,6 @@ static int reset_states(hs_ctx* c) {  // PointFrameResidual::resetOOB on every a
 static int linearize_pass(hs_ctx* c, bool reset) {
   if (reset) HS_TRY(reset_states(c));
   HS_HIP(hipMemsetAsync(c->d_sys, 0, sizeof(double) * c->acc_len(), c->stream));
-  HS_HIP(hipMemsetAsync(c->d_cnt + c->rank, 0, sizeof(int), c->stream));
   HS_TRY(launch_linearize(c, 0));
   HS_TRY(launch_reduce(c));
   c->haveSystem = true;
@@ -300,6 +306,42 @@ static int set_loop_counters(hs_ctx* c, int iteration) {
   c->h_ctl[2] = 0;          // log_count
   HS_HIP(hipMemcpyAsync((char*)c->d_state + offsetof(HsDevState, iteration), c->h_ctl, 3 * sizeof(int),
                         hipMemcpyHostToDevice, c->stream));
+  return HS_OK;
+}
+
+// per-kernel checkpoint summary of the last traced launch (stderr): for every checkpoint the
+// min / median / max over blocks of (checkpoint - the block's start) and the launch span, in us
+static int dump_one(const char* name, const long long* d, int nblocks, double tick_us, hipStream_t s) {
+  std::vector<long long> h((size_t)nblocks * 16);
+  HS_HIP(hipMemcpyAsync(h.data(), d, sizeof(long long) * h.size(), hipMemcpyDeviceToHost, s));
+  HS_HIP(hipStreamSynchronize(s));
+  long long t0 = -1, t1 = 0;
+  for (int b = 0; b < nblocks; b++) {
+    if (h[b * 16] == 0) continue;
+    t0 = t0 < 0 ? h[b * 16] : std::min(t0, h[b * 16]);
+    for (int k = 1; k < 16; k++) t1 = std::max(t1, h[b * 16 + k]);
+  }
+  std::fprintf(stderr, "[hs trace] %-12s blocks %5d span %8.2f us\n", name, nblocks, t0 < 0 ? 0.0 : (t1 - t0) * tick_us);
+  for (int k = 1; k < 16; k++) {
+    std::vector<double> v;
+    for (int b = 0; b < nblocks; b++)
+      if (h[b * 16] && h[b * 16 + k]) v.push_back((h[b * 16 + k] - h[b * 16]) * tick_us);
+    if (v.empty()) continue;
+    std::sort(v.begin(), v.end());
+    std::fprintf(stderr, "[hs trace] %-12s cp%-2d n %5zu  min %8.2f  med %8.2f  max %8.2f us (start spread %.2f)\n",
+                 name, k, v.size(), v.front(), v[v.size() / 2], v.back(), 0.0);
+  }
+  return HS_OK;
+}
+
+static int dump_traces(hs_ctx* c) {
+  int khz = 0;
+  HS_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device));
+  const double tick_us = khz > 0 ? 1e3 / khz : 0.01;
+  HS_TRY(dump_one("solve", c->d_tr_solve, 1, tick_us, c->stream));
+  HS_TRY(dump_one("linearize", c->d_tr_lin, c->nP, tick_us, c->stream));
+  HS_TRY(dump_one("accumulate", c->d_tr_acc, c->nF * c->nF * c->S + 3, tick_us, c->stream));
+  HS_TRY(dump_one("stitch", c->d_tr_stitch, c->nF * c->nF, tick_us, c->stream));
   return HS_OK;
 }
 
@@ -351,6 +393,7 @@ static int gn_iterations(hs_ctx* c, int it0, int K, bool allow_break, double* en
     ta += ms;
   }
   c->t_lin = tl; c->t_acc = ta; c->t_solve = ts; c->t_timed = std::min(k, nev); c->t_iters = k;
+  if (c->tracing) HS_TRY(dump_traces(c));
   if (done) *done = k;
   if (energies_out)
     for (int q = 0; q < k; q++) energies_out[q] = elog[q + 1];
@@ -496,7 +539,10 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
   }
   int maxHost = 0;
   for (int h = 0; h < nF; h++) maxHost = std::max(maxHost, c->host_pt_begin[h + 1] - c->host_pt_begin[h]);
-  c->S = std::max(1, std::min(64, (maxHost + kPointsPerSplit - 1) / kPointsPerSplit));
+  int splitPts = kPointsPerSplit;
+  if (const char* e = std::getenv("HS_ACC_SPLIT_POINTS")) splitPts = std::max(1, std::atoi(e));
+  c->S = std::max(1, std::min(256, (maxHost + splitPts - 1) / splitPts));
+  c->maxPtsPerBlock = (maxHost + c->S - 1) / c->S;
 
   // ---- window state: calib (CalibData ctor: setValueScaled, value_zero = value) and frames
   HsDevState& S = *c->h_state;
@@ -543,13 +589,14 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
   const int n = c->dim();
   c->HM.assign((size_t)n * n, 0.0);
   c->bM.assign(n, 0.0);
+  c->hm_zero = true;
   compute_projector(c);
   std::vector<HsPrecalc> pre(nF * nF);
   for (int h = 0; h < nF; h++)
     for (int t = 0; t < nF; t++) pre[h * nF + t] = make_precalc(S.frames[h], S.frames[t], cal);
 
-  // ---- candidate buffer stride: the same on every rank (max residual count)
-  c->cand_stride = nR > 0 ? nR : 1;
+  // ---- candidate buffer stride: the same on every rank (max point count)
+  c->cand_stride = nP > 0 ? nP : 1;
   if (c->comm && c->nranks > 1) {
     int* d_tmp = nullptr;
     HS_TRY(dalloc(&d_tmp, 1));
@@ -592,7 +639,16 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
   HS_TRY(dalloc(&c->d_sys, c->sys_len()));
   HS_TRY(dalloc(&c->d_HM, (size_t)n * n)); HS_TRY(dalloc(&c->d_bM, n)); HS_TRY(dalloc(&c->d_Porth, (size_t)n * n));
   HS_TRY(dalloc(&c->d_xAd, nF * nF * 8)); HS_TRY(dalloc(&c->d_x, n)); HS_TRY(dalloc(&c->d_elog, kLogCap));
-  HS_TRY(dalloc(&c->d_cand, (size_t)c->cand_stride * c->nranks)); HS_TRY(dalloc(&c->d_cnt, c->nranks));
+  HS_TRY(dalloc(&c->d_cand, (size_t)c->cand_stride * c->nranks));
+  HS_HIP(hipMemset(c->d_cand, 0xff, sizeof(float) * c->cand_stride * c->nranks));  // NaN, sign set: no candidate
+  const char* tr = std::getenv("HS_KTRACE");
+  c->tracing = tr && tr[0] == '1';
+  if (c->tracing) {
+    HS_TRY(dalloc(&c->d_tr_lin, (size_t)std::max(nP, 1) * 16));
+    HS_TRY(dalloc(&c->d_tr_acc, (size_t)(nF * nF * c->S + 3) * 16));
+    HS_TRY(dalloc(&c->d_tr_solve, 16));
+    HS_TRY(dalloc(&c->d_tr_stitch, (size_t)nF * nF * 16));
+  }
 
   std::vector<float> prior(nP, 0.f);
   for (int i = 0; i < nP; i++)
@@ -683,8 +739,9 @@ int hs_ba_do_step(hs_ctx* c, int* canbreak_out) {
 int hs_ba_optimize(hs_ctx* c, int max_iters, int allow_break, double* energies_out, int* iters_done) {
   if (!c || c->nF == 0) return fail(HS_ERR_STATE, "no window");
   HS_HIP(hipSetDevice(c->device));
+  // System::optimize: two sequential overrides, so a 2- or 3-frame window runs 15 iterations
   if (c->nF < 3) max_iters = 20;
-  else if (c->nF < 4) max_iters = 15;
+  if (c->nF < 4) max_iters = 15;
   auto t0 = std::chrono::steady_clock::now();
   HS_TRY(linearize_pass(c, true));
   int done = 0;
@@ -809,6 +866,7 @@ int hs_ba_set_marginal_prior(hs_ctx* c, const double* HM, const double* bM) {
   const int n = c->dim();
   c->HM.assign(HM, HM + n * n);
   c->bM.assign(bM, bM + n);
+  c->hm_zero = std::all_of(c->HM.begin(), c->HM.end(), [](double v) { return v == 0.0; });
   HS_HIP(hipMemcpyAsync(c->d_HM, c->HM.data(), sizeof(double) * n * n, hipMemcpyHostToDevice, c->stream));
   HS_HIP(hipMemcpyAsync(c->d_bM, c->bM.data(), sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
   HS_HIP(hipStreamSynchronize(c->stream));

@@ -74,8 +74,15 @@ struct BlkCnt {
   __device__ __forceinline__ int total() const { return n1 + n1k + n1m; }
 };
 
+// wall-clock checkpoint of a block (thread 0) when tracing is enabled
+#define HS_TRACE(A, slot)                                                                          \
+  do {                                                                                             \
+    if ((A).trace && threadIdx.x == 0) (A).trace[(size_t)blockIdx.x * 16 + (slot)] = wall_clock64(); \
+  } while (0)
+
 struct LinLds {
   float q[HS_MAXF][Q_N][8];
+  float dot[HS_MAXF][8];
   float s[HS_MAXF][Q_N + 3];
   float econ[HS_MAXF];
   float act[HS_MAXF];
@@ -119,25 +126,62 @@ __global__ __launch_bounds__(64) void hs_k_linearize(HsLinArgs a) {
   const int h = a.pt_host[p];
   const HsCalib cal = a.st->dcal;
 
+  HS_TRACE(a, 0);
+  // everything the linearization reads is loaded up front (independent of the fused point step)
   float idep = a.idepth[p], idep0 = a.idepth_zero[p];
+  const float pu = a.u[p], pv = a.v[p];
+  const int r = a.res_of_slot[p * 8 + t];
+  const bool has = r >= 0;
+  const int st = has ? (int)a.r_state[r] : HS_RES_OOB;
+  const float oldE = has ? a.r_energy[r] : 0.f;
+  const float oldNewE = has ? a.r_newEnergy[r] : 0.f;
+  const float thr = fmaxf(a.frameTH[h], a.frameTH[t < nF ? t : 0]);  // std::max<float>(host TH, target TH)
+  const float colorK = a.color[p * 8 + k], weightK = a.weight[p * 8 + k];
+  HsPrecalc pc;
+  if (has) pc = a.pre[h * nF + t];
+  const uint2 ro2 = reinterpret_cast<const uint2*>(a.res_order)[p];  // the point's 8 residual-list slots
+  auto res_slot = [&](int q) -> int { return (int)(int8_t)(((q < 4 ? ro2.x : ro2.y) >> (8 * (q & 3))) & 0xffu); };
   if (a.fuse_step) {
-    // resubstituteFPt of the previous linearization + doStepFromBackup point part (stepfacD = 1)
-    const float step = point_step(p, h, nF, a.p_actmask[p], a.st->cstep, a.p_Hcd, a.p_bdSumF[p], a.p_HdiF[p],
-                                  a.res_order, a.xAd, a.p_JpJdF);
+    // resubstituteFPt of the previous linearization (Src/EnergyFunctional.cpp:249-274) + the point part of
+    // doStepFromBackup (stepfacD = 1).  Lane (t, k) forms xAd[h][t][k] * JpJdF[t][k]; the sums then run
+    // in the reference order (k ascending per residual, residuals in list order).
+    const unsigned m = a.p_actmask[p];
+    L.dot[t][k] = ((m >> t) & 1u) ? a.xAd[(h * nF + t) * 8 + k] * a.p_JpJdF[(p * 8 + t) * 8 + k] : 0.f;
+    float step = 0.f;
+    const float bds = a.p_bdSumF[p], hdi = a.p_HdiF[p];
+    const float4 hcd = reinterpret_cast<const float4*>(a.p_Hcd)[p];
+    __syncthreads();  // every lane has read the previous per-point data before it is overwritten
+    if (lane == 0 && m != 0u) {
+      float b = bds;
+      const float* cs = a.st->cstep;
+      float dot = 0.f;
+      dot += cs[0] * hcd.x;
+      dot += cs[1] * hcd.y;
+      dot += cs[2] * hcd.z;
+      dot += cs[3] * hcd.w;
+      b -= dot;
+      for (int q = 0; q < 8; q++) {
+        const int tt = res_slot(q);
+        if (tt < 0) break;
+        if (!((m >> tt) & 1u)) continue;
+        float d = 0.f;
+        for (int i = 0; i < 8; i++) d += L.dot[tt][i];
+        b -= d;
+      }
+      step = -b * hdi;
+    }
+    if (lane == 0) L.dot[0][0] = step;
+    __syncthreads();
+    step = L.dot[0][0];
     idep = idep + 1.0f * step;
     idep0 = idep;
-    __syncthreads();  // every lane has read the previous per-point data before it is overwritten
     if (lane == 0) {
       a.idepth[p] = idep;
       a.idepth_zero[p] = idep;
       a.p_step[p] = step;
     }
   }
-
-  const float pu = a.u[p], pv = a.v[p];
-  const int r = a.res_of_slot[p * 8 + t];
-  const bool has = r >= 0;
-  const int st = has ? (int)a.r_state[r] : HS_RES_OOB;
+  HS_TRACE(a, 1);
 
   bool oob = false;
   float Jx[10] = {0}, Jy[10] = {0}, Jd0 = 0.f, Jd1 = 0.f;
@@ -147,7 +191,6 @@ __global__ __launch_bounds__(64) void hs_k_linearize(HsLinArgs a) {
   float centre[3] = {0.f, 0.f, 0.f};
   bool centreOk = false;
   if (has && st != HS_RES_OOB) {
-    const HsPrecalc& pc = a.pre[h * nF + t];
     // centre: projectPoint(u, v, idepth_zero, 0, 0, R_0, t_0)  Include/DirectProjection.h:20-38
     const float Kl0 = (pu + 0 - cal.cxl) * cal.fxli;
     const float Kl1 = (pv + 0 - cal.cyl) * cal.fyli;
@@ -219,7 +262,7 @@ __global__ __launch_bounds__(64) void hs_k_linearize(HsLinArgs a) {
           oob = true;
         } else {
           const float3 hit = interp33(a.img[t], PKu, PKv, cal.W);
-          const float color = a.color[p * 8 + k];
+          const float color = colorK;
           const float residual = hit.x - (float)(pc.aff[0] * color + pc.aff[1]);
           const float drdA = (color - pc.b0);
           if (!isfinite(hit.x)) {
@@ -227,7 +270,7 @@ __global__ __launch_bounds__(64) void hs_k_linearize(HsLinArgs a) {
           } else {
             float w = sqrtf(a.lp.outlierTHSumComponent /
                             (a.lp.outlierTHSumComponent + (hit.y * hit.y + hit.z * hit.z)));
-            w = 0.5f * (w + a.weight[p * 8 + k]);
+            w = 0.5f * (w + weightK);
             float hw = fabsf(residual) < a.lp.huberTH ? 1 : a.lp.huberTH / fabsf(residual);
             qv[0] = w * w * hw * residual * residual * (2 - hw);
             if (hw < 1) hw = sqrtf(hw);
@@ -262,6 +305,7 @@ __global__ __launch_bounds__(64) void hs_k_linearize(HsLinArgs a) {
   }
   const unsigned long long oobMask = __ballot(oob);
   const bool slotOob = ((oobMask >> (t * 8)) & 0xffull) != 0ull;
+  HS_TRACE(a, 2);
 
 #pragma unroll
   for (int qi = 0; qi < Q_N; qi++) L.q[t][qi][k] = qv[qi];
@@ -279,7 +323,6 @@ __global__ __launch_bounds__(64) void hs_k_linearize(HsLinArgs a) {
   bool active = false;
   float econ = 0.f;
   if (has) {
-    const float oldE = a.r_energy[r];
     if (st == HS_RES_OOB) {
       econ = oldE;  // linearize returns state_energy; applyRes returns early (OOB is sticky)
       if (k == 0) a.r_ewo[r] = -1.f;
@@ -289,18 +332,14 @@ __global__ __launch_bounds__(64) void hs_k_linearize(HsLinArgs a) {
         a.r_ewo[r] = -1.f;
         a.r_state[r] = HS_RES_OOB;
         a.r_active[r] = 0;
-        a.r_energy[r] = a.r_newEnergy[r];
+        a.r_energy[r] = oldNewE;
       }
     } else {
-      const float thr = fmaxf(a.frameTH[h], a.frameTH[t]);  // std::max<float>(host TH, target TH)
       float energyLeft = L.s[t][0];
       const float wJI2 = L.s[t][11];
       int ns;
       if (k == 0) a.r_ewo[r] = energyLeft;
-      if (a.newest_cand != nullptr && t == nF - 1 && k == 0) {
-        const int slot = atomicAdd(a.newest_cnt, 1);
-        a.newest_cand[slot] = energyLeft;
-      }
+      if (t == nF - 1 && k == 0) a.newest_cand[p] = energyLeft;
       if (energyLeft > thr || wJI2 < 2) {
         energyLeft = thr;
         ns = HS_RES_OUT;
@@ -343,6 +382,7 @@ __global__ __launch_bounds__(64) void hs_k_linearize(HsLinArgs a) {
     }
     if (a.write_center && centreOk && k < 3) a.r_center[r * 3 + k] = centre[k];
   }
+  if (t == nF - 1 && k == 0 && !(has && st != HS_RES_OOB && !slotOob)) a.newest_cand[p] = -1.f;
   if (k == 0) {
     L.econ[t] = econ;
     L.act[t] = active ? 1.f : 0.f;
@@ -361,7 +401,7 @@ __global__ __launch_bounds__(64) void hs_k_linearize(HsLinArgs a) {
     float Hdd = 0.f, bd = 0.f, Hcd[4] = {0.f, 0.f, 0.f, 0.f};
     unsigned mask = 0u;
     for (int qn = 0; qn < 8; qn++) {
-      const int tt = a.res_order[p * 8 + qn];
+      const int tt = res_slot(qn);
       if (tt < 0) break;
       eSum += (double)L.econ[tt];
       if (L.act[tt] == 0.f) continue;
@@ -389,21 +429,23 @@ __global__ __launch_bounds__(64) void hs_k_linearize(HsLinArgs a) {
       bdSumF += priorF * (idep - idep0);
       a.p_bdSumF[p] = bdSumF;
     }
-#pragma unroll
-    for (int c = 0; c < 4; c++) a.p_Hcd[p * 4 + c] = Hcd[c] + 0.f;
+    reinterpret_cast<float4*>(a.p_Hcd)[p] = make_float4(Hcd[0] + 0.f, Hcd[1] + 0.f, Hcd[2] + 0.f, Hcd[3] + 0.f);
   }
+  HS_TRACE(a, 3);
 }
 
 // =====================================================================================================
 // accumulate: (host i, target slot j, split s) blocks + energy / Hcc,bc / energy threshold blocks
 // =====================================================================================================
 namespace {
-constexpr int ACC_TILE = 64;
+constexpr int ACC_TILE = 64;  // points per LDS tile (one wave does the order-preserving compaction)
+// per-point LDS record: Jacobian digest of residual (p, j) | 1 | 0 | HdiF | bdSumF | Hcd | JpJdF of all slots
+constexpr int R_ONE = 36, R_ZERO = 37, R_HDI = 38, R_BDS = 39, R_HCD = 40, R_JP = 44, R_N = 108;
 struct AccLds {
-  float jp[ACC_TILE][64];
-  float jr[ACC_TILE][HS_JREC];
-  float hdi[ACC_TILE], bds[ACC_TILE], hcd[ACC_TILE][4];
+  float rec[ACC_TILE][R_N];
   unsigned char m[ACC_TILE];
+  unsigned char list[ACC_TILE];
+  int cnt;
 };
 
 // linearizeAll's energy (+ the sumNID / numID statistics of doStepFromBackup); fixed-order tree in fp64
@@ -437,6 +479,7 @@ __device__ void acc_energy_block(const HsAccArgs& a) {
 // per-thread fp32 accumulators in fp64)
 __device__ void acc_hcc_block(const HsAccArgs& a) {
   __shared__ float red[20][257];
+  __shared__ double part[20][12];
   const int tid = threadIdx.x;
   float acc[20];
   for (int e = 0; e < 20; e++) acc[e] = 0.f;
@@ -451,10 +494,8 @@ __device__ void acc_hcc_block(const HsAccArgs& a) {
       acc[16 + rr] += bds * hdi * hc[rr];
     }
   }
-  __shared__ double part[20][12];
   for (int e = 0; e < 20; e++) red[e][tid] = acc[e];
   __syncthreads();
-  // 20 entries x 12 lanes partial sums, then a lane-ordered combine
   const int e = tid / 12, l = tid % 12;
   if (tid < 240) {
     double s = 0.0;
@@ -469,37 +510,26 @@ __device__ void acc_hcc_block(const HsAccArgs& a) {
   }
 }
 
-// setNewFrameEnergyTH: k-th smallest candidate by 4-pass radix select with a parallel bin scan.
-// Candidates of all ranks (all-gathered) are selected together, so every rank computes the same TH.
+// setNewFrameEnergyTH: k-th smallest candidate by a 4-pass radix select with a parallel bin scan.
+// Candidates: one float per point and rank (-1 / negative = none); the ranks' arrays are all-gathered so
+// every rank selects over the same union and computes the same threshold.
 __device__ void acc_energy_th_block(const HsAccArgs& a) {
   __shared__ unsigned int hist[256], scan[256];
   __shared__ unsigned int s_prefix, s_mask, s_k, s_n;
   const int tid = threadIdx.x;
   if (tid == 0) {
-    int n = 0;
-    for (int r = 0; r < a.nranks; r++) n += a.cnt[r];
-    s_n = (unsigned)n;
     s_prefix = 0;
     s_mask = 0;
-    s_k = (unsigned int)(int)(a.frameEnergyTHN * (float)n);
-  }
-  __syncthreads();
-  if (s_n == 0) {
-    if (tid == 0) a.frameTH[a.newest] = 12 * 12 * 8;
-    return;
   }
   for (int pass = 0; pass < 4; pass++) {
     const int shift = 24 - 8 * pass;
     hist[tid] = 0;
     __syncthreads();
     const unsigned int prefix = s_prefix, mask = s_mask;
-    for (int r = 0; r < a.nranks; r++) {
-      const float* cr = a.cand + (size_t)r * a.stride;
-      const int nr = a.cnt[r];
-      for (int i = tid; i < nr; i += 256) {
-        const unsigned int v = __float_as_uint(cr[i]);
-        if ((v & mask) == prefix) atomicAdd(&hist[(v >> shift) & 255u], 1u);
-      }
+    const int total = a.nranks * a.stride;
+    for (int i = tid; i < total; i += 256) {
+      const unsigned int v = __float_as_uint(a.cand[i]);
+      if (v < 0x80000000u && (v & mask) == prefix) atomicAdd(&hist[(v >> shift) & 255u], 1u);
     }
     __syncthreads();
     scan[tid] = hist[tid];
@@ -510,6 +540,12 @@ __device__ void acc_energy_th_block(const HsAccArgs& a) {
       scan[tid] += v;
       __syncthreads();
     }
+    if (pass == 0 && tid == 0) {
+      s_n = scan[255];
+      s_k = (unsigned int)(int)(a.frameEnergyTHN * (float)scan[255]);
+    }
+    __syncthreads();
+    if (s_n == 0) break;
     const unsigned int incl = scan[tid], excl = incl - hist[tid], kk = s_k;
     __syncthreads();
     if (excl <= kk && kk < incl) {
@@ -520,145 +556,205 @@ __device__ void acc_energy_th_block(const HsAccArgs& a) {
     __syncthreads();
   }
   if (tid == 0) {
-    const float nth = sqrtf(__uint_as_float(s_prefix));
-    float th = nth * a.facMedian;
-    th = 26.0f * a.constWeight + th * (1 - a.constWeight);
-    th = th * th;
-    th *= a.overallWeight * a.overallWeight;
-    a.frameTH[a.newest] = th;
+    if (s_n == 0) {
+      a.frameTH[a.newest] = 12 * 12 * 8;
+    } else {
+      const float nth = sqrtf(__uint_as_float(s_prefix));
+      float th = nth * a.facMedian;
+      th = 26.0f * a.constWeight + th * (1 - a.constWeight);
+      th = th * th;
+      th *= a.overallWeight * a.overallWeight;
+      a.frameTH[a.newest] = th;
+    }
   }
 }
+
+struct AccOps {
+  float a, b, c, xr, xc, yr, yc;  // top entry operands
+  float hdi, wj, x0, x1;          // accD: HdiF, JpJdF[j][dr], JpJdF[kD0][dc], JpJdF[kD1][dc]
+  float ex, ey;                   // accE / accEB operands
+  unsigned m;
+};
 }  // namespace
 
-__global__ __launch_bounds__(256) void hs_k_accumulate(HsAccArgs a) {
-  const int nF = a.nF, S = a.S;
-  const int nb = nF * nF * S;
-  const int b = blockIdx.x;
-  if (b == nb) { acc_energy_block(a); return; }
-  if (b == nb + 1) { acc_hcc_block(a); return; }
-  if (b == nb + 2) { acc_energy_th_block(a); return; }
-
-  __shared__ AccLds T;
+// Stages one tile of per-point records into LDS: all global loads are issued before any LDS store
+// (clamped, always-valid addresses), then the order-preserving list of points active into j is built.
+__device__ __forceinline__ void acc_load_tile(const HsAccArgs& a, AccLds& T, int t0, int tn, int j) {
   const int tid = threadIdx.x;
+  const int qa0 = min((tid + 0) >> 4, tn - 1), qa1 = min((tid + 256) >> 4, tn - 1);
+  const int qa2 = min((tid + 512) >> 4, tn - 1), qa3 = min((tid + 768) >> 4, tn - 1);
+  const int w = tid & 15;
+  const float4* jp = reinterpret_cast<const float4*>(a.JpJdF);
+  const float4 j0 = jp[(size_t)(t0 + qa0) * 16 + w], j1 = jp[(size_t)(t0 + qa1) * 16 + w];
+  const float4 j2 = jp[(size_t)(t0 + qa2) * 16 + w], j3 = jp[(size_t)(t0 + qa3) * 16 + w];
+  constexpr int NW = HS_JREC / 4;
+  const int r0 = tid, r1 = tid + 256, r2 = tid + 512;
+  const float4* jr = reinterpret_cast<const float4*>(a.Jrec);
+  const float4 k0 = jr[((size_t)(t0 + min(r0 / NW, tn - 1)) * 8 + j) * NW + r0 % NW];
+  const float4 k1 = jr[((size_t)(t0 + min(r1 / NW, tn - 1)) * 8 + j) * NW + r1 % NW];
+  const float4 k2 = jr[((size_t)(t0 + min(r2 / NW, tn - 1)) * 8 + j) * NW + r2 % NW];
+  const int qs = min(tid, tn - 1);
+  const unsigned char mk = a.actmask[t0 + qs];
+  const float4 hcd = reinterpret_cast<const float4*>(a.Hcd)[t0 + qs];
+  const float hdi = a.HdiF[t0 + qs], bds = a.bdSumF[t0 + qs];
+  __syncthreads();  // the previous tile's records are no longer read
+  // rows >= tn receive copies of the last point; they are never listed
+  *reinterpret_cast<float4*>(&T.rec[(tid + 0) >> 4][R_JP + 4 * w]) = j0;
+  *reinterpret_cast<float4*>(&T.rec[(tid + 256) >> 4][R_JP + 4 * w]) = j1;
+  *reinterpret_cast<float4*>(&T.rec[(tid + 512) >> 4][R_JP + 4 * w]) = j2;
+  *reinterpret_cast<float4*>(&T.rec[(tid + 768) >> 4][R_JP + 4 * w]) = j3;
+  *reinterpret_cast<float4*>(&T.rec[r0 / NW][4 * (r0 % NW)]) = k0;
+  *reinterpret_cast<float4*>(&T.rec[r1 / NW][4 * (r1 % NW)]) = k1;
+  if (r2 < ACC_TILE * NW) *reinterpret_cast<float4*>(&T.rec[r2 / NW][4 * (r2 % NW)]) = k2;
+  if (tid < ACC_TILE) {
+    T.m[tid] = mk;
+    *reinterpret_cast<float4*>(&T.rec[tid][R_HCD]) = hcd;
+    T.rec[tid][R_HDI] = hdi;
+    T.rec[tid][R_BDS] = bds;
+    T.rec[tid][R_ONE] = 1.0f;
+    T.rec[tid][R_ZERO] = 0.0f;
+    const bool act = tid < tn && ((mk >> j) & 1u);
+    const unsigned long long bal = __ballot(act);
+    if (act) T.list[__popcll(bal & ((1ull << tid) - 1ull))] = (unsigned char)tid;
+    if (tid == 0) T.cnt = __popcll(bal);
+  }
+  __syncthreads();
+}
+
+// One (host i, target j, split s) accumulator block.  kBlocked: the reference's 1k/1m flush blocking is
+// emulated (needed when a block sums more than 1000 updates; below that shiftUp never fires and
+// finish() returns the plain running sum, so the counters are dropped).
+template <bool kBlocked>
+__device__ __forceinline__ void acc_pair_block(const HsAccArgs& a, AccLds& T) {
+  const int nF = a.nF, S = a.S;
+  const int tid = threadIdx.x;
+  const int b = blockIdx.x;
   const int ij = b / S, s = b % S;
   const int i = ij % nF, j = ij / nF;  // host i, target j (accumulator index i + nF*j)
   const int hb = a.host_pt_begin[i], he = a.host_pt_begin[i + 1];
   const int span = he - hb;
   const int pb = hb + (int)((long long)span * s / S), pe = hb + (int)((long long)span * (s + 1) / S);
 
-  // ---- thread roles
-  // top entry (tid < 91): Data (r, c >= r) for e < 55, TopRight (r, col) for e < 85, BotRight for e < 91
-  int er = 0, ec = 0, ttype = -1;
-  if (tid < HS_TOP_N) {
-    const int e = tid;
-    if (e < 55) {
-      int idx = 0;
-      for (int rr = 0; rr < 10; rr++)
-        for (int cc = rr; cc < 10; cc++) {
-          if (idx == e) { er = rr; ec = cc; }
-          idx++;
-        }
-      ttype = 0;
-    } else if (e < 85) {
-      er = (e - 55) / 3;
-      ec = (e - 55) % 3;
-      ttype = 1;
-    } else {
-      ec = e - 85;
-      ttype = 2;
-    }
+  // ---- thread roles as LDS record offsets.  Every top entry is evaluated with the AccumulatorApprox::update
+  // expression  ((a*xc)*xr + (c*yc)*yr) + b*((xc*yr) + (yc*xr));  TopRight (xr*T0 + yr*T1) and BotRight (v)
+  // are that expression with 1 / 0 operands, which leaves their rounding unchanged.
+  int oa = R_ZERO, ob = R_ZERO, oc = R_ZERO, oxr = R_ZERO, oxc = R_ZERO, oyr = R_ZERO, oyc = R_ZERO;
+  bool isData = false;
+  if (tid < 55) {
+    int er = 0, ec = 0, idx = 0;
+    for (int rr = 0; rr < 10; rr++)
+      for (int cc = rr; cc < 10; cc++) {
+        if (idx == tid) { er = rr; ec = cc; }
+        idx++;
+      }
+    isData = true;
+    oa = HS_JR_JIDX2 + 0; ob = HS_JR_JIDX2 + 1; oc = HS_JR_JIDX2 + 2;
+    oxr = HS_JR_X + er; oxc = HS_JR_X + ec; oyr = HS_JR_Y + er; oyc = HS_JR_Y + ec;
+  } else if (tid < 85) {
+    const int er = (tid - 55) / 3, ec = (tid - 55) % 3;
+    oa = ec == 0 ? HS_JR_JABJIDX + 0 : (ec == 1 ? HS_JR_JABJIDX + 2 : HS_JR_JIR + 0);
+    oc = ec == 0 ? HS_JR_JABJIDX + 1 : (ec == 1 ? HS_JR_JABJIDX + 3 : HS_JR_JIR + 1);
+    oxr = HS_JR_X + er; oyr = HS_JR_Y + er; oxc = R_ONE; oyc = R_ONE;
+  } else if (tid < HS_TOP_N) {
+    const int ec = tid - 85;
+    oa = ec == 0 ? HS_JR_JAB2 + 0
+       : ec == 1 ? HS_JR_JAB2 + 1
+       : ec == 2 ? HS_JR_JABR + 0
+       : ec == 3 ? HS_JR_JAB2 + 2
+       : ec == 4 ? HS_JR_JABR + 1 : HS_JR_RR;
+    oxr = oxc = oyr = oyc = R_ONE;
   }
-  // D entries (target j, target kD) [dr][dc] for kD = kD0 and kD0 + 4
+  // D entries (target j, target kD) [dr][dc] for kD = kD0 and kD0 + 4 (wave-uniform kD)
   const int kD0 = tid >> 6, kD1 = kD0 + 4, dr = (tid & 63) >> 3, dc = tid & 7;
-  // E entries: tid 91..122 (r = e >> 2, c = e & 3), EB: tid 123..130
+  const int owj = R_JP + j * 8 + dr, ox0 = R_JP + kD0 * 8 + dc, ox1 = R_JP + kD1 * 8 + dc;
+  // E entries: tid 91..122 ((HdiF*JpJdF[j][r])*Hcd[c]); EB: tid 123..130 ((HdiF*bdSumF)*JpJdF[j][r])
   const int eE = tid - 91, eB = tid - 123;
+  int oex = R_ZERO, oey = R_ZERO;
+  if (eE >= 0 && eE < 32) { oex = R_JP + j * 8 + (eE >> 2); oey = R_HCD + (eE & 3); }
+  else if (eB >= 0 && eB < 8) { oex = R_BDS; oey = R_JP + j * 8 + eB; }
 
   Blk top, d0, d1, ex;
   BlkCnt ctop, cd0, cd1, cex;
+  int nTop = 0, nD0 = 0, nD1 = 0;
+
+  auto load = [&](int q, AccOps& o) {
+    const float* R = T.rec[q];
+    o.a = R[oa]; o.b = R[ob]; o.c = R[oc]; o.xr = R[oxr]; o.xc = R[oxc]; o.yr = R[oyr]; o.yc = R[oyc];
+    o.hdi = R[R_HDI]; o.wj = R[owj]; o.x0 = R[ox0]; o.x1 = R[ox1];
+    o.ex = R[oex]; o.ey = R[oey];
+    o.m = T.m[q];
+  };
 
   for (int t0 = pb; t0 < pe; t0 += ACC_TILE) {
     const int tn = min(ACC_TILE, pe - t0);
-    __syncthreads();
-    for (int idx = tid; idx < tn * 16; idx += 256) {  // JpJdF of all slots, float4
-      const int q = idx >> 4, w = idx & 15;
-      reinterpret_cast<float4*>(T.jp[q])[w] = reinterpret_cast<const float4*>(a.JpJdF + (size_t)(t0 + q) * 64)[w];
-    }
-    for (int idx = tid; idx < tn * (HS_JREC / 4); idx += 256) {  // Jacobian digest of slot j, float4
-      const int q = idx / (HS_JREC / 4), w = idx % (HS_JREC / 4);
-      reinterpret_cast<float4*>(T.jr[q])[w] =
-          reinterpret_cast<const float4*>(a.Jrec + ((size_t)(t0 + q) * 8 + j) * HS_JREC)[w];
-    }
-    for (int q = tid; q < tn; q += 256) {
-      T.m[q] = a.actmask[t0 + q];
-      T.hdi[q] = a.HdiF[t0 + q];
-      T.bds[q] = a.bdSumF[t0 + q];
-      reinterpret_cast<float4*>(T.hcd[q])[0] = reinterpret_cast<const float4*>(a.Hcd)[t0 + q];
-    }
-    __syncthreads();
-    for (int q = 0; q < tn; q++) {
-      const unsigned m = T.m[q];
-      if (!((m >> j) & 1u)) continue;  // uniform
-      const float* jr = T.jr[q];
-      // ---- AccumulatedTopHessianSSE::addPoint<0>: update() (Data, then shiftUp), updateBotRight, updateTopRight
-      if (ttype == 0) {
-        const float xr = jr[HS_JR_X + er], xc = jr[HS_JR_X + ec], yr = jr[HS_JR_Y + er], yc = jr[HS_JR_Y + ec];
-        top.A += jr[HS_JR_JIDX2 + 0] * xc * xr + jr[HS_JR_JIDX2 + 2] * yc * yr +
-                 jr[HS_JR_JIDX2 + 1] * (xc * yr + yc * xr);
-        top.flush(ctop.bump());
-      } else if (ttype == 1) {
-        top.flush(ctop.bump());
-        const float xr = jr[HS_JR_X + er], yr = jr[HS_JR_Y + er];
-        const float T0 = ec == 0 ? jr[HS_JR_JABJIDX + 0] : (ec == 1 ? jr[HS_JR_JABJIDX + 2] : jr[HS_JR_JIR + 0]);
-        const float T1 = ec == 0 ? jr[HS_JR_JABJIDX + 1] : (ec == 1 ? jr[HS_JR_JABJIDX + 3] : jr[HS_JR_JIR + 1]);
-        top.A += xr * T0 + yr * T1;
-      } else if (ttype == 2) {
-        top.flush(ctop.bump());
-        const float v = ec == 0 ? jr[HS_JR_JAB2 + 0]
-                      : ec == 1 ? jr[HS_JR_JAB2 + 1]
-                      : ec == 2 ? jr[HS_JR_JABR + 0]
-                      : ec == 3 ? jr[HS_JR_JAB2 + 2]
-                      : ec == 4 ? jr[HS_JR_JABR + 1] : jr[HS_JR_RR];
-        top.A += v;
-      } else {
-        ctop.bump();
-      }
-      // ---- AccumulatedSCHessianSSE::addPoint: accD[j][k] (both active), accE / accEB[j]
-      const float hdi = T.hdi[q];
-      const float wl = hdi * T.jp[q][j * 8 + dr];
-      if ((m >> kD0) & 1u) {
-        d0.A += wl * T.jp[q][kD0 * 8 + dc];
-        d0.flush(cd0.bump());
-      }
-      if ((m >> kD1) & 1u) {
-        d1.A += wl * T.jp[q][kD1 * 8 + dc];
-        d1.flush(cd1.bump());
-      }
-      if (eE >= 0 && eE < 32) {
-        ex.A += hdi * T.jp[q][j * 8 + (eE >> 2)] * T.hcd[q][eE & 3];
-        ex.flush(cex.bump());
-      } else if (eB >= 0 && eB < 8) {
-        ex.A += hdi * T.bds[q] * T.jp[q][j * 8 + eB];
+    acc_load_tile(a, T, t0, tn, j);
+    HS_TRACE(a, 2);
+    const int n = T.cnt;
+    AccOps nx;
+    if (n > 0) load(T.list[0], nx);
+    for (int c = 0; c < n; c++) {
+      const AccOps o = nx;
+      if (c + 1 < n) load(T.list[c + 1], nx);
+      // ---- AccumulatedTopHessianSSE::addPoint<0>: update() adds Data then shiftUp; BotRight / TopRight after
+      const float upd = ((o.a * o.xc) * o.xr + (o.c * o.yc) * o.yr) + o.b * ((o.xc * o.yr) + (o.yc * o.xr));
+      const float wl = o.hdi * o.wj;
+      const bool b0 = (o.m >> kD0) & 1u, b1 = (o.m >> kD1) & 1u;
+      if (kBlocked) {
+        const int f = ctop.bump();
+        if (isData) top.A += upd;
+        if (f) top.flush(f);
+        if (!isData) top.A += upd;
+        if (b0) {
+          d0.A += wl * o.x0;
+          d0.flush(cd0.bump());
+        }
+        if (b1) {
+          d1.A += wl * o.x1;
+          d1.flush(cd1.bump());
+        }
+        ex.A += (o.hdi * o.ex) * o.ey;
         ex.flush(cex.bump());
       } else {
-        cex.bump();
+        top.A += upd;
+        if (b0) d0.A += wl * o.x0;
+        if (b1) d1.A += wl * o.x1;
+        ex.A += (o.hdi * o.ex) * o.ey;
+        nTop++;
+        nD0 += b0 ? 1 : 0;
+        nD1 += b1 ? 1 : 0;
       }
     }
   }
+  HS_TRACE(a, 1);
   float* P = a.part + ((size_t)ij * S + s) * HS_PART_N;
   int* PC = a.part_cnt + ((size_t)ij * S + s) * 16;
+  // finish(): A1m = (A1k + A) + A1m  (== A when nothing was flushed)
   if (tid < HS_TOP_N) P[tid] = top.finish();
   P[96 + kD0 * 64 + dr * 8 + dc] = d0.finish();
   P[96 + kD1 * 64 + dr * 8 + dc] = d1.finish();
   if (eE >= 0 && eE < 32) P[96 + 512 + eE] = ex.finish();
   else if (eB >= 0 && eB < 8) P[96 + 512 + 32 + eB] = ex.finish();
   if (tid == 0) {
-    PC[0] = ctop.total();
-    PC[9] = cex.total();
+    PC[0] = kBlocked ? ctop.total() : nTop;
+    PC[9] = kBlocked ? cex.total() : nTop;
   }
   if ((tid & 63) == 0) {
-    PC[1 + kD0] = cd0.total();
-    PC[1 + kD1] = cd1.total();
+    PC[1 + kD0] = kBlocked ? cd0.total() : nD0;
+    PC[1 + kD1] = kBlocked ? cd1.total() : nD1;
   }
+}
+
+__global__ __launch_bounds__(256) void hs_k_accumulate(HsAccArgs a) {
+  const int nb = a.nF * a.nF * a.S;
+  const int b = blockIdx.x;
+  HS_TRACE(a, 0);
+  if (b == nb) { acc_energy_block(a); HS_TRACE(a, 15); return; }
+  if (b == nb + 1) { acc_hcc_block(a); HS_TRACE(a, 15); return; }
+  if (b == nb + 2) { acc_energy_th_block(a); HS_TRACE(a, 15); return; }
+  __shared__ AccLds T;
+  if (a.blocked) acc_pair_block<true>(a, T);
+  else acc_pair_block<false>(a, T);
+  HS_TRACE(a, 15);
 }
 
 // =====================================================================================================
@@ -691,36 +787,59 @@ __global__ __launch_bounds__(64) void hs_k_stitch(HsStitchArgs a) {
   const int tid = threadIdx.x;
   const int n = 4 + 8 * nF;
   const int iIdx = 4 + 8 * i, jIdx = 4 + 8 * j;
-  __shared__ double e[96], A88[64], A84[32], a8r[8], tmp[64], aH[64], aT[64], D[64], aH2[64], aT2[64], v8[8], Hpc[32];
-  __shared__ int topCnt;
-  aH[tid] = a.adHost[ij * 64 + tid];
-  aT[tid] = a.adTarget[ij * 64 + tid];
-  // sum of the split partials (stitchDoubleInternal: accH += acc[tid2].H.cast<double>() for num > 0)
+  __shared__ double e[96], A88[64], A84[32], a8r[8], tmp[64], aH[64], aT[64], v8[8], Hpc[32];
+  __shared__ double D[HS_MAXF][64], aH2[HS_MAXF][64], aT2[HS_MAXF][64];
+  __shared__ int cnt[16];
+  HS_TRACE(a, 0);
+  // ---- everything this pair needs, loads in flight together
   const float* P0 = a.part + (size_t)ij * S * HS_PART_N;
   const int* C0 = a.part_cnt + (size_t)ij * S * 16;
-  if (tid == 0) {
+  aH[tid] = a.adHost[ij * 64 + tid];
+  aT[tid] = a.adTarget[ij * 64 + tid];
+#pragma unroll
+  for (int kk = 0; kk < HS_MAXF; kk++)
+    if (kk < nF) {
+      aH2[kk][tid] = a.adHost[(i + nF * kk) * 64 + tid];
+      aT2[kk][tid] = a.adTarget[(i + nF * kk) * 64 + tid];
+    }
+  if (tid < 16) {
     int c = 0;
-    for (int s = 0; s < S; s++) c += C0[s * 16];
-    topCnt = c;
+    for (int s = 0; s < S; s++) c += C0[s * 16 + tid];
+    cnt[tid] = c;
   }
-  for (int q = tid; q < 96; q += 64) {
-    double sum = 0.0;
-    for (int s = 0; s < S; s++)
-      if (C0[s * 16] > 0) sum += (double)P0[s * HS_PART_N + q];
-    e[q] = sum;
+  // split partials summed in fp64 (stitchDoubleInternal: accH += acc[tid2].H.cast<double>() for num > 0)
+  double se0 = 0.0, se1 = 0.0, sE = 0.0, sD[HS_MAXF];
+#pragma unroll
+  for (int kk = 0; kk < HS_MAXF; kk++) sD[kk] = 0.0;
+  for (int s = 0; s < S; s++) {
+    const float* Ps = P0 + (size_t)s * HS_PART_N;
+    const int* Cs = C0 + s * 16;
+    const bool top = Cs[0] > 0;
+    // clamped, unconditional loads (kept in flight together)
+    const float p0 = Ps[tid], p1 = Ps[64 + (tid & 31)];
+    const float pe = Ps[96 + 512 + min(tid, 39)];
+    float pd[HS_MAXF];
+#pragma unroll
+    for (int kk = 0; kk < HS_MAXF; kk++) pd[kk] = Ps[96 + min(kk, nF - 1) * 64 + tid];
+    if (top) {
+      se0 += (double)p0;
+      se1 += (double)p1;
+    }
+    sE += (double)pe;
+#pragma unroll
+    for (int kk = 0; kk < HS_MAXF; kk++)
+      if (kk < nF && Cs[1 + kk] > 0) sD[kk] += (double)pd[kk];
   }
-  if (tid < 32) {
-    double sum = 0.0;
-    for (int s = 0; s < S; s++) sum += (double)P0[s * HS_PART_N + 96 + 512 + tid];
-    Hpc[tid] = sum;
-  }
-  if (tid < 8) {
-    double sum = 0.0;
-    for (int s = 0; s < S; s++) sum += (double)P0[s * HS_PART_N + 96 + 512 + 32 + tid];
-    v8[tid] = sum;
-  }
+  e[tid] = se0;
+  if (tid < 32) e[64 + tid] = se1;
+  if (tid < 32) Hpc[tid] = sE;
+  else if (tid < 40) v8[tid - 32] = sE;
+#pragma unroll
+  for (int kk = 0; kk < HS_MAXF; kk++)
+    if (kk < nF) D[kk][tid] = sD[kk];
   __syncthreads();
-  const bool haveTop = topCnt > 0;
+  HS_TRACE(a, 1);
+  const bool haveTop = cnt[0] > 0;
   if (haveTop) {  // AccumulatorApprox::finish -> 13x13 [calib4|xi6|a|b|r]
     const int r = tid >> 3, c = tid & 7;  // A88 = H[4+r][4+c]
     const int R = 4 + r, Cc = 4 + c;
@@ -798,186 +917,288 @@ __global__ __launch_bounds__(64) void hs_k_stitch(HsStitchArgs a) {
     atomicAdd(&a.bSC[jIdx + tid], s2);
   }
   for (int kk = 0; kk < nF; kk++) {
+    if (cnt[1 + kk] == 0) continue;  // accD num == 0 (uniform)
     const int kIdx = 4 + 8 * kk;
-    const int ik = i + nF * kk;
-    int dcnt = 0;
-    for (int s = 0; s < S; s++) dcnt += C0[s * 16 + 1 + kk];
-    if (dcnt == 0) continue;  // accD num == 0 (uniform)
-    __syncthreads();
-    double sum = 0.0;
-    for (int s = 0; s < S; s++)
-      if (C0[s * 16 + 1 + kk] > 0) sum += (double)P0[s * HS_PART_N + 96 + kk * 64 + tid];
-    D[tid] = sum;
-    aH2[tid] = a.adHost[ik * 64 + tid];
-    aT2[tid] = a.adTarget[ik * 64 + tid];
-    __syncthreads();
     double o;
-    o = sandwich(aH, D, aH2, tmp, tid);
+    o = sandwich(aH, D[kk], aH2[kk], tmp, tid);
     atomicAdd(&a.HSC[(iIdx + r) * n + iIdx + c], o);
-    o = sandwich(aT, D, aT2, tmp, tid);
+    o = sandwich(aT, D[kk], aT2[kk], tmp, tid);
     atomicAdd(&a.HSC[(jIdx + r) * n + kIdx + c], o);
-    o = sandwich(aT, D, aH2, tmp, tid);
+    o = sandwich(aT, D[kk], aH2[kk], tmp, tid);
     atomicAdd(&a.HSC[(jIdx + r) * n + iIdx + c], o);
-    o = sandwich(aH, D, aT2, tmp, tid);
+    o = sandwich(aH, D[kk], aT2[kk], tmp, tid);
     atomicAdd(&a.HSC[(iIdx + r) * n + kIdx + c], o);
   }
   if (blockIdx.x == 0 && tid < 16) atomicAdd(&a.HSC[(tid >> 2) * n + (tid & 3)], a.hccbc[tid]);
   if (blockIdx.x == 0 && tid < 4) atomicAdd(&a.bSC[tid], a.hccbc[16 + tid]);
+  HS_TRACE(a, 15);
 }
 
 // =====================================================================================================
 // solve + step (fp64), one workgroup of 256 threads
 // =====================================================================================================
-__global__ __launch_bounds__(256) void hs_k_solve(HsSolveArgs a) {
-  __shared__ double Hs[HS_MAXDIM * HS_MAXDIM];
-  __shared__ double Hp[HS_MAXDIM * HS_MAXDIM];
+namespace {
+constexpr int SOLVE_NT = 512;
+constexpr int SOLVE_NU = (HS_MAXDIM * HS_MAXDIM + SOLVE_NT - 1) / SOLVE_NT;  // matrix entries per thread
+
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), lane);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+}  // namespace
+
+__global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
+  __shared__ double A[HS_MAXDIM * HS_MAXDIM];  // raw HA, then the scaled system, then Porth
+  __shared__ double B[HS_MAXDIM * HS_MAXDIM];  // raw HSC, then the published LDLT rows
   __shared__ double bf[HS_MAXDIM], Sv[HS_MAXDIM], xs[HS_MAXDIM], yv[HS_MAXDIM], px[HS_MAXDIM], dl[HS_MAXDIM];
   __shared__ float xF[HS_MAXDIM];
-  __shared__ int pos[HS_MAXDIM];
-  __shared__ int s_it;
+  __shared__ int pos[HS_MAXDIM], sorted_[HS_MAXDIM], elem_at[HS_MAXDIM], pos_of[HS_MAXDIM];
+  __shared__ int s_it, s_tie;
   HsDevState* st = a.st;
-  const int tid = threadIdx.x, nt = blockDim.x;
-  const int nF = st->nF, n = 4 + 8 * nF;
+  const int tid = threadIdx.x, nt = SOLVE_NT;
+  const int nF = st->nF, n = 4 + 8 * nF, nn = n * n;
   const double lambda = 1e-5;  // SOLVER_FIX_LAMBDA
-  if (tid == 0) s_it = a.iteration >= 0 ? a.iteration : st->iteration;
+  HS_TRACE(a, 0);
+  if (tid == 0) {
+    s_it = a.iteration >= 0 ? a.iteration : st->iteration;
+    s_tie = 0;
+  }
+  // owned entries idx = tid + u*nt  ->  (R, C)
+  int Ru[SOLVE_NU], Cu[SOLVE_NU];
+#pragma unroll
+  for (int u = 0; u < SOLVE_NU; u++) {
+    const int idx = tid + u * nt;
+    Ru[u] = idx < nn ? idx / n : n;
+    Cu[u] = idx < nn ? idx - Ru[u] * n : n;
+  }
 
   if (a.flags & HS_SOLVE) {
     if (tid == 0 && a.energy_log) {
       a.energy_log[st->log_count] = a.sysE[0];
       st->log_count = st->log_count + 1;
     }
-    // getStitchedDeltaF for bM + HM * delta
-    for (int q = tid; q < n; q += nt)
-      dl[q] = q < 4 ? (double)(float)st->calib.value_minus_value_zero[q] : st->frames[(q - 4) / 8].delta[(q - 4) % 8];
-    __syncthreads();
-    // HFinal = (HL + HM) + HA ; diag *= (1+lambda) ; HFinal -= HSC / (1+lambda)
-    const double sc = (double)(1.0f / (1 + lambda));
-    for (int idx = tid; idx < n * n; idx += nt) {
-      const int r = idx / n, c = idx % n;
-      const int fr = r < 4 ? -1 : (r - 4) / 8, fc = c < 4 ? -1 : (c - 4) / 8;
-      double ha = a.HA[idx];
-      if (fr >= 0 && fc >= 0 && fr != fc) ha = a.HA[idx] + a.HA[c * n + r];  // stitchDoubleMT symmetrization
-      else if (r < 4 && c >= 4) ha = a.HA[c * n + r];                          // calib row <- column
-      double hsc = a.HSC[idx];
-      if (r < 4 && c >= 4) hsc = a.HSC[c * n + r];
-      double hl = 0.0;
-      if (r == c) hl = r < 4 ? a.initialCalibHessian : st->frames[fr].prior[(r - 4) % 8];
-      double hf = (hl + a.HM[idx]) + ha;
-      if (r == c) hf *= (1 + lambda);
-      hf = hf - hsc * sc;
-      Hs[idx] = hf;
+    // stage the raw stitched systems: clamped (always valid) addresses, every load in flight before any use
+    {
+      double ha[SOLVE_NU], hs[SOLVE_NU];
+#pragma unroll
+      for (int u = 0; u < SOLVE_NU; u++) {
+        const int idx = min(tid + u * nt, nn - 1);
+        ha[u] = a.HA[idx];
+        hs[u] = a.HSC[idx];
+      }
+#pragma unroll
+      for (int u = 0; u < SOLVE_NU; u++)
+        if (tid + u * nt < nn) {
+          A[tid + u * nt] = ha[u];
+          B[tid + u * nt] = hs[u];
+        }
     }
-    for (int q = tid; q < n; q += nt) {
-      double bl;
+    if (tid < n) {
+      const int q = tid;
+      dl[q] = q < 4 ? (double)(float)st->calib.value_minus_value_zero[q] : st->frames[(q - 4) / 8].delta[(q - 4) % 8];
+      double bl, pr;
       if (q < 4) {
+        pr = a.initialCalibHessian;
         bl = a.initialCalibHessian * dl[q];
       } else {
         const hs::FrameH& f = st->frames[(q - 4) / 8];
+        pr = f.prior[(q - 4) % 8];
         bl = f.prior[(q - 4) % 8] * f.delta_prior[(q - 4) % 8];
       }
+      px[q] = pr;  // HL diagonal (priors); staging only: these four arrays are reused below
+      xs[q] = bl;
+      yv[q] = a.bA[q];
+      Sv[q] = a.bSC[q];
+    }
+    __syncthreads();
+    HS_TRACE(a, 7);
+    // HFinal = (HL + HM) + HA' ; diag *= (1+lambda) ; HFinal -= HSC' / (1+lambda)   (' = stitchDoubleMT
+    // post-processing: frame off-diagonal blocks symmetrized, calib rows copied from the calib columns)
+    const double sc = (double)(1.0f / (1 + lambda));
+    double v[SOLVE_NU];
+#pragma unroll
+    for (int u = 0; u < SOLVE_NU; u++) {
+      const int r = min(Ru[u], n - 1), c = min(Cu[u], n - 1);
+      const int idx = r * n + c, tdx = c * n + r;
+      const int fr = r < 4 ? -1 : (r - 4) >> 3, fc = c < 4 ? -1 : (c - 4) >> 3;
+      const double a0 = A[idx], a1 = A[tdx], b0 = B[idx], b1 = B[tdx], hl0 = px[r];
+      const double hm = a.HM ? a.HM[idx] : 0.0;
+      const bool sym = fr >= 0 && fc >= 0 && fr != fc, calrow = r < 4 && c >= 4;
+      const double ha = sym ? a0 + a1 : (calrow ? a1 : a0);
+      const double hsc = calrow ? b1 : b0;
+      const double hl = r == c ? hl0 : 0.0;
+      double hv = (hl + hm) + ha;
+      hv = r == c ? hv * (1 + lambda) : hv;
+      v[u] = hv - hsc * sc;
+    }
+    if (tid < n) {
+      const int q = tid;
       double hmd = 0.0;
-      for (int c = 0; c < n; c++) hmd += a.HM[q * n + c] * dl[c];
-      bf[q] = ((bl + (a.bM[q] + hmd)) + a.bA[q]) - a.bSC[q];
+      if (a.HM)
+        for (int c = 0; c < n; c++) hmd += a.HM[q * n + c] * dl[c];
+      // ((bL + (bM + HM delta)) + bA) - bSC
+      bf[q] = ((xs[q] + (a.bM[q] + hmd)) + yv[q]) - Sv[q];
     }
     __syncthreads();
-    // the consumed accumulation targets are zeroed for the next linearization
-    for (int idx = tid; idx < n * n; idx += nt) {
-      a.HA[idx] = 0.0;
-      a.HSC[idx] = 0.0;
+    HS_TRACE(a, 8);
+#pragma unroll
+    for (int u = 0; u < SOLVE_NU; u++)
+      if (tid + u * nt < nn) {
+        A[tid + u * nt] = v[u];
+      }
+    __syncthreads();
+    HS_TRACE(a, 9);
+    if (tid < n) Sv[tid] = 1.0 / sqrt(A[tid * n + tid] + 10);
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < SOLVE_NU; u++) {
+      const int r = min(Ru[u], n - 1), c = min(Cu[u], n - 1);
+      const double sv = Sv[r] * A[r * n + c] * Sv[c];
+      if (Ru[u] < n) A[r * n + c] = sv;
     }
-    for (int q = tid; q < n; q += nt) {
-      a.bA[q] = 0.0;
-      a.bSC[q] = 0.0;
-      Sv[q] = 1.0 / sqrt(Hs[q * n + q] + 10);
+    if (tid < n) bf[tid] = Sv[tid] * bf[tid];
+    __syncthreads();
+    HS_TRACE(a, 1);
+    // Eigen LDLT pivot order (left-looking: the pivot is the largest |original diagonal| among the remaining
+    // ones, first current position on ties).  Stable descending order by |diag|; where values tie, the
+    // swap sequence is replayed by one thread to get the exact positions.
+    if (tid < n) {
+      const double w0 = fabs(A[tid * n + tid]);
+      int rank = 0, tie = 0;
+      for (int p = 0; p < n; p++) {
+        const double w = fabs(A[p * n + p]);
+        rank += (w > w0 || (w == w0 && p < tid)) ? 1 : 0;
+        tie |= (p != tid && w == w0) ? 1 : 0;
+      }
+      sorted_[rank] = tid;
+      pos[rank] = tid;
+      elem_at[tid] = tid;
+      pos_of[tid] = tid;
+      if (tie) s_tie = 1;
     }
     __syncthreads();
-    for (int idx = tid; idx < n * n; idx += nt) {
-      const int r = idx / n, c = idx % n;
-      Hs[idx] = Sv[r] * Hs[idx] * Sv[c];
-    }
-    for (int q = tid; q < n; q += nt) bf[q] = Sv[q] * bf[q];
-    __syncthreads();
-    // Eigen LDLT pivot order: largest |diagonal| among the remaining (left-looking: the original diagonal),
-    // first position on ties; equivalent to an unpivoted LDLT of P H P^T.
-    if (tid < 64) {
-      for (int q = tid; q < n; q += 64) pos[q] = q;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      __builtin_amdgcn_wave_barrier();
-      for (int kq = 0; kq < n; kq++) {
-        double best = -1.0;
-        int bi = n;
-        for (int q = kq + tid; q < n; q += 64) {
-          const double v = fabs(Hs[pos[q] * n + pos[q]]);
-          if (v > best) { best = v; bi = q; }
+    if (s_tie && tid == 0) {
+      int gs = 0;
+      while (gs < n) {
+        const double gv = fabs(A[sorted_[gs] * n + sorted_[gs]]);
+        int ge = gs + 1;
+        while (ge < n && fabs(A[sorted_[ge] * n + sorted_[ge]]) == gv) ge++;
+        for (int kq = gs; kq < ge; kq++) {
+          // remaining group members are sorted_[kq..ge) (selected ones are swapped to the front)
+          int bq = kq, bp = pos_of[sorted_[kq]];
+          for (int q = kq + 1; q < ge; q++) {
+            const int pq = pos_of[sorted_[q]];
+            if (pq < bp) { bp = pq; bq = q; }
+          }
+          const int sel = sorted_[bq];
+          sorted_[bq] = sorted_[kq];
+          sorted_[kq] = sel;
+          const int ek = elem_at[kq];
+          elem_at[kq] = sel;
+          elem_at[bp] = ek;
+          pos_of[ek] = bp;
+          pos_of[sel] = kq;
+          pos[kq] = sel;
         }
-        for (int o = 32; o > 0; o >>= 1) {
-          const double ob = __shfl_xor(best, o);
-          const int oi = __shfl_xor(bi, o);
-          if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
-        }
-        if (tid == 0 && bi != kq) {
-          const int tq = pos[kq];
-          pos[kq] = pos[bi];
-          pos[bi] = tq;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        __builtin_amdgcn_wave_barrier();
+        gs = ge;
       }
     }
     __syncthreads();
-    for (int idx = tid; idx < n * n; idx += nt) {
-      const int r = idx / n, c = idx % n;
-      Hp[idx] = Hs[pos[r] * n + pos[c]];
+    // owned entries of the permuted system P S H S P^T; row 0 is published for the first step
+#pragma unroll
+    for (int u = 0; u < SOLVE_NU; u++) {
+      const int r = min(Ru[u], n - 1), c = min(Cu[u], n - 1);
+      v[u] = A[pos[r] * n + pos[c]];
     }
-    for (int q = tid; q < n; q += nt) yv[q] = bf[pos[q]];
+#pragma unroll
+    for (int u = 0; u < SOLVE_NU; u++)
+      if (Ru[u] == 0) B[Cu[u]] = v[u];
+    if (tid < n) yv[tid] = bf[pos[tid]];
     __syncthreads();
-    // right-looking LDLT of the lower triangle; forward substitution L z = P b fused into the sweep
+    HS_TRACE(a, 2);
+    // right-looking LDLT with register-resident entries (both triangles): step k reads the published
+    // row k (B[k][*] = D_k, L(r,k) D_k) and the owners of row k+1 publish it after their update.
+    // The forward substitution L z = P S b rides along.  Loads are unconditional, updates are selects.
+    int Rc[SOLVE_NU], Cc[SOLVE_NU];
+#pragma unroll
+    for (int u = 0; u < SOLVE_NU; u++) {
+      Rc[u] = min(Ru[u], n - 1);
+      Cc[u] = min(Cu[u], n - 1);
+    }
     for (int kq = 0; kq < n; kq++) {
-      const double d = Hp[kq * n + kq];
-      const bool valid = fabs(d) > DBL_MIN;
-      if (valid)
-        for (int q = kq + 1 + tid; q < n; q += nt) Hp[q * n + kq] /= d;
-      __syncthreads();
-      const double yk = yv[kq];
-      for (int q = kq + 1 + tid; q < n; q += nt) yv[q] -= Hp[q * n + kq] * yk;
+      const double* rowk = B + kq * n;
+      const double d = rowk[kq];
+      const double dinv = fabs(d) > DBL_MIN ? 1.0 / d : 0.0;
       const int m = n - kq - 1;
-      const int ntri = m * (m + 1) / 2;
-      for (int t = tid; t < ntri; t += nt) {
-        // t -> (rr >= cc) in the trailing lower triangle
-        int rr = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-        while (rr * (rr + 1) / 2 > t) rr--;
-        while ((rr + 1) * (rr + 2) / 2 <= t) rr++;
-        const int cc = t - rr * (rr + 1) / 2;
-        const int R = kq + 1 + rr, Cc = kq + 1 + cc;
-        Hp[R * n + Cc] -= Hp[R * n + kq] * (d * Hp[Cc * n + kq]);
+      const double yk = yv[kq];
+      const double ry = rowk[min(kq + 1 + tid, n - 1)];
+      double rr[SOLVE_NU], rc[SOLVE_NU];
+#pragma unroll
+      for (int u = 0; u < SOLVE_NU; u++) {
+        rr[u] = rowk[Rc[u]];
+        rc[u] = rowk[Cc[u]];
       }
+      if (tid < m) yv[kq + 1 + tid] -= (ry * dinv) * yk;
+      // every owned entry is updated: entries outside the trailing block are either in an already
+      // published row or strictly below the diagonal, and neither is ever published again
+#pragma unroll
+      for (int u = 0; u < SOLVE_NU; u++) v[u] -= rr[u] * (rc[u] * dinv);
+      // publish row k+1
+#pragma unroll
+      for (int u = 0; u < SOLVE_NU; u++)
+        if (Ru[u] == kq + 1 && Cu[u] > kq) B[Ru[u] * n + Cu[u]] = v[u];
       __syncthreads();
+      if (kq == 0) HS_TRACE(a, 10);
+      if (kq == 3) HS_TRACE(a, 11);
+      if (kq == 15) HS_TRACE(a, 12);
+      if (kq == 31) HS_TRACE(a, 13);
+      if (kq == 63) HS_TRACE(a, 14);
     }
-    for (int q = tid; q < n; q += nt) {
-      const double d = Hp[q * n + q];
-      yv[q] = fabs(d) > DBL_MIN ? yv[q] / d : 0.0;
-    }
-    __syncthreads();
-    // backward substitution L^T x = z: one wave, a dot product per row
+    HS_TRACE(a, 3);
+    // D^-1, then the backward substitution L^T x = z by one wave: lane l owns rows l and l + 64
     if (tid < 64) {
-      for (int kq = n - 1; kq >= 0; kq--) {
-        double s = 0.0;
-        for (int q = kq + 1 + tid; q < n; q += 64) s += Hp[q * n + kq] * yv[q];
-        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-        if (tid == 0) yv[kq] = yv[kq] - s;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        __builtin_amdgcn_wave_barrier();
+      const int i0 = tid, i1 = min(tid + 64, n - 1);
+      const bool own1 = tid + 64 < n;
+      const double d0 = B[min(i0, n - 1) * n + min(i0, n - 1)], d1 = B[i1 * n + i1];
+      const double di0 = fabs(d0) > DBL_MIN ? 1.0 / d0 : 0.0, di1 = fabs(d1) > DBL_MIN ? 1.0 / d1 : 0.0;
+      double y0 = i0 < n ? (fabs(d0) > DBL_MIN ? yv[i0] / d0 : 0.0) : 0.0;
+      double y1 = own1 ? (fabs(d1) > DBL_MIN ? yv[i1] / d1 : 0.0) : 0.0;
+      const double* rb0 = B + min(i0, n - 1) * n;
+      const double* rb1 = B + i1 * n;
+      double nb0 = rb0[n - 1], nb1 = rb1[n - 1];
+      for (int kq = n - 1; kq > 0; kq--) {
+        // x_k is final: broadcast it, then x_i -= L(k,i) x_k for i < k  (L(k,i) D_i = B[i][k])
+        const double b0 = nb0, b1 = nb1;
+        nb0 = rb0[kq - 1];  // prefetch the next step's L entries
+        nb1 = rb1[kq - 1];
+        const double xk = kq >= 64 ? readlane_f64(y1, kq - 64) : readlane_f64(y0, kq);
+        const double n0 = y0 - (b0 * di0) * xk, n1 = y1 - (b1 * di1) * xk;
+        y0 = i0 < kq ? n0 : y0;
+        y1 = (own1 && tid + 64 < kq) ? n1 : y1;
       }
+      if (i0 < n) yv[i0] = y0;
+      if (own1) yv[tid + 64] = y1;
     }
     __syncthreads();
+    HS_TRACE(a, 4);
     for (int q = tid; q < n; q += nt) xs[pos[q]] = yv[q];
+    {
+      double po[SOLVE_NU];
+#pragma unroll
+      for (int u = 0; u < SOLVE_NU; u++) po[u] = a.Porth[min(tid + u * nt, nn - 1)];
+#pragma unroll
+      for (int u = 0; u < SOLVE_NU; u++)
+        if (tid + u * nt < nn) A[tid + u * nt] = po[u];
+    }
     __syncthreads();
     for (int q = tid; q < n; q += nt) xs[q] = Sv[q] * xs[q];
     __syncthreads();
-    if (s_it >= 2) {  // SOLVER_ORTHOGONALIZE_X_LATER
+    if (s_it >= 2) {  // SOLVER_ORTHOGONALIZE_X_LATER: x -= Porth x
       for (int q = tid; q < n; q += nt) {
         double s = 0.0;
-        for (int c = 0; c < n; c++) s += a.Porth[q * n + c] * xs[c];
+        for (int c = 0; c < n; c++) s += A[q * n + c] * xs[c];
         px[q] = s;
       }
       __syncthreads();
@@ -1010,6 +1231,16 @@ __global__ __launch_bounds__(256) void hs_k_solve(HsSolveArgs a) {
       for (int rr = 0; rr < 8; rr++) s2 += xF[4 + 8 * tt + rr] * aTf[rr * 8 + c];
       a.xAd[o] = s1 + s2;
     }
+    // the consumed accumulation targets are zeroed for the next linearization (no barrier waits on these)
+    for (int idx = tid; idx < nn; idx += nt) {
+      a.HA[idx] = 0.0;
+      a.HSC[idx] = 0.0;
+    }
+    if (tid < n) {
+      a.bA[tid] = 0.0;
+      a.bSC[tid] = 0.0;
+    }
+    HS_TRACE(a, 5);
   }
   __syncthreads();
   if (a.flags & HS_APPLY) {
@@ -1024,8 +1255,8 @@ __global__ __launch_bounds__(256) void hs_k_solve(HsSolveArgs a) {
       cal.setValue(nv);
       st->dcal = cal.device();
     }
-    if (tid < nF) {
-      hs::FrameH& f = st->frames[tid];
+    if (tid >= 64 && tid < 64 + nF) {
+      hs::FrameH& f = st->frames[tid - 64];
       double s[10];
       for (int q = 0; q < 10; q++) {
         f.state_backup[q] = f.state[q];
@@ -1038,11 +1269,12 @@ __global__ __launch_bounds__(256) void hs_k_solve(HsSolveArgs a) {
       }
     }
     __syncthreads();
+    HS_TRACE(a, 6);
     for (int pr = tid; pr < nF * nF; pr += nt) {
       const int hh = pr / nF, tt = pr % nF;
       a.pre[pr] = hs::make_precalc(st->frames[hh], st->frames[tt], st->calib);
     }
-    if (tid == 0) {
+    if (tid == 128) {
       float sumA = 0, sumB = 0, sumT = 0, sumR = 0;
       for (int f = 0; f < nF; f++) {
         const double* sp = st->frames[f].step;
@@ -1060,7 +1292,7 @@ __global__ __launch_bounds__(256) void hs_k_solve(HsSolveArgs a) {
       st->iteration = s_it + 1;
     }
   }
-  if (tid == 0 && a.cnt_reset) *a.cnt_reset = 0;
+  HS_TRACE(a, 15);
 }
 
 // =====================================================================================================

@@ -59,12 +59,13 @@ struct HsLinArgs {
   float* p_Jrec;               // [n][8][HS_JREC]
   double* p_energy;            // [n]
   float* p_step;               // [n]
-  float* newest_cand;          // energies of residuals into the newest frame (setNewFrameEnergyTH)
-  int* newest_cnt;
+  float* newest_cand;          // [n] energy of the point's residual into the newest frame, -1 = none
+  long long* trace;            // nullable: per-block wall-clock checkpoints [grid][16]
 };
 
 struct HsAccArgs {
   int nF, S, nP;
+  int blocked;                 // a (host, target, split) block can exceed 1000 updates: emulate shiftUp
   const int* host_pt_begin;    // [nF+1]
   const uint8_t* actmask;
   const float* HdiF;
@@ -78,13 +79,13 @@ struct HsAccArgs {
   const float* idepth;         // |idepth| sum for doStepFromBackup's sumNID
   double* energy_out;          // [3]: energy, sum |idepth|, number of points
   double* hccbc;               // [20] finished Hcc (16) + bc (4), fp64
-  // setNewFrameEnergyTH
+  // setNewFrameEnergyTH over the candidates of all ranks (rank r at cand + r*stride, -1 = none)
   const float* cand;
-  const int* cnt;
   int nranks, stride;
   float* frameTH;
   int newest;
   float frameEnergyTHN, facMedian, constWeight, overallWeight;
+  long long* trace;
 };
 
 struct HsStitchArgs {
@@ -98,6 +99,7 @@ struct HsStitchArgs {
   double* bA;
   double* HSC;
   double* bSC;
+  long long* trace;
 };
 
 enum { HS_SOLVE = 1, HS_APPLY = 2 };
@@ -110,7 +112,7 @@ struct HsSolveArgs {
   double* bA;
   double* HSC;
   double* bSC;
-  const double* HM;
+  const double* HM;            // nullable: marginalization prior is zero
   const double* bM;
   const double* Porth;         // [n*n] nullspace projector
   const float* adHostF;        // [nF*nF][64]
@@ -120,7 +122,7 @@ struct HsSolveArgs {
   double* x_out;               // [n]
   const double* sysE;          // [3] energy, sum |idepth|, #points of the consumed linearization
   double* energy_log;          // SOLVE appends sysE[0] at st->log_count
-  int* cnt_reset;              // newest-frame candidate counter zeroed for the next linearization
+  long long* trace;
   double initialCalibHessian;
   float thOptIterations;
 };
