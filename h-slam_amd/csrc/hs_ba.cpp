@@ -71,7 +71,7 @@ struct hs_ctx {
   bool events = true;
 
   // window (host side)
-  int nF = 0, nP = 0, nR = 0, S = 1, maxPtsPerBlock = 0;
+  int nF = 0, nP = 0, nR = 0, S = 1, W = 4, maxPtsPerBlock = 0;
   std::vector<int> pt_host, res_point, res_target, host_pt_begin;
   std::vector<int> res_of_slot;   // [nP*8]
   std::vector<int8_t> res_order;  // [nP*8]
@@ -97,7 +97,7 @@ struct hs_ctx {
   float *d_p_HdiF = nullptr, *d_p_bdSumF = nullptr, *d_p_Hcd = nullptr, *d_p_JpJdF = nullptr, *d_p_Jrec = nullptr;
   float* d_p_step = nullptr;
   double* d_p_energy = nullptr;
-  float* d_part = nullptr;
+  double* d_part = nullptr;
   int* d_part_cnt = nullptr;
   double* d_hccbc = nullptr;
   double *d_adHost = nullptr, *d_adTarget = nullptr;
@@ -233,8 +233,8 @@ static int launch_reduce(hs_ctx* c) {
                           c->comm, c->stream));
   HsAccArgs a;
   std::memset(&a, 0, sizeof(a));
-  a.nF = c->nF; a.S = c->S; a.nP = c->nP;
-  a.blocked = c->maxPtsPerBlock > 1000 ? 1 : 0;
+  a.nF = c->nF; a.S = c->S; a.nP = c->nP; a.W = c->W;
+  a.blocked = (c->maxPtsPerBlock + c->W - 1) / c->W > 1000 ? 1 : 0;
   a.host_pt_begin = c->d_host_pt_begin;
   a.actmask = c->d_p_actmask; a.HdiF = c->d_p_HdiF; a.bdSumF = c->d_p_bdSumF; a.Hcd = c->d_p_Hcd;
   a.JpJdF = c->d_p_JpJdF; a.Jrec = c->d_p_Jrec;
@@ -277,7 +277,7 @@ static int launch_solve(hs_ctx* c, int flags, int iteration, bool log) {
   a.trace = c->d_tr_solve;
   a.initialCalibHessian = c->P.initialCalibHessian;
   a.thOptIterations = c->P.thOptIterations;
-  hipLaunchKernelGGL(hs_k_solve, dim3(1), dim3(512), 0, c->stream, a);
+  hipLaunchKernelGGL(hs_k_solve, dim3(1), dim3(384), 0, c->stream, a);
   HS_HIP(hipGetLastError());
   return HS_OK;
 }
@@ -539,9 +539,14 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
   }
   int maxHost = 0;
   for (int h = 0; h < nF; h++) maxHost = std::max(maxHost, c->host_pt_begin[h + 1] - c->host_pt_begin[h]);
+  // accumulate partitioning: S splits per (host, target) x W accumulating waves per split.
+  // HS_ACC_EXACT=1: one partial per (host, target) in point order = the single-thread reference's sums.
   int splitPts = kPointsPerSplit;
   if (const char* e = std::getenv("HS_ACC_SPLIT_POINTS")) splitPts = std::max(1, std::atoi(e));
-  c->S = std::max(1, std::min(256, (maxHost + splitPts - 1) / splitPts));
+  const char* ex = std::getenv("HS_ACC_EXACT");
+  const bool exact = ex && ex[0] == '1';
+  c->S = exact ? 1 : std::max(1, std::min(256, (maxHost + splitPts - 1) / splitPts));
+  c->W = exact ? 1 : 4;
   c->maxPtsPerBlock = (maxHost + c->S - 1) / c->S;
 
   // ---- window state: calib (CalibData ctor: setValueScaled, value_zero = value) and frames

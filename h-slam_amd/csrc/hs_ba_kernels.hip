@@ -442,11 +442,13 @@ constexpr int ACC_TILE = 64;  // points per LDS tile (one wave does the order-pr
 // per-point LDS record: Jacobian digest of residual (p, j) | 1 | 0 | HdiF | bdSumF | Hcd | JpJdF of all slots
 constexpr int R_ONE = 36, R_ZERO = 37, R_HDI = 38, R_BDS = 39, R_HCD = 40, R_JP = 44, R_N = 108;
 struct AccLds {
-  float rec[ACC_TILE][R_N];
+  float rec[ACC_TILE][R_N];  // also the staging of the waves' partials (4 x HS_PART_N floats)
   unsigned char m[ACC_TILE];
   unsigned char list[ACC_TILE];
   int cnt;
+  int wcnt[4][16];
 };
+static_assert(ACC_TILE * R_N >= 4 * HS_PART_N, "partial staging fits in the tile records");
 
 // linearizeAll's energy (+ the sumNID / numID statistics of doStepFromBackup); fixed-order tree in fp64
 __device__ void acc_energy_block(const HsAccArgs& a) {
@@ -569,10 +571,44 @@ __device__ void acc_energy_th_block(const HsAccArgs& a) {
   }
 }
 
+// operand offsets of one AccumulatorApprox entry evaluated as ((a*xc)*xr + (c*yc)*yr) + b*((xc*yr) + (yc*xr));
+// TopRight (xr*T0 + yr*T1) and BotRight (v) are that expression with 1 / 0 operands (same rounding)
+struct TopRole {
+  int oa = R_ZERO, ob = R_ZERO, oc = R_ZERO, oxr = R_ZERO, oxc = R_ZERO, oyr = R_ZERO, oyc = R_ZERO;
+  bool isData = false;
+};
+__device__ __forceinline__ TopRole top_role(int e) {
+  TopRole t;
+  if (e < 55) {
+    int er = 0, ec = 0, idx = 0;
+    for (int rr = 0; rr < 10; rr++)
+      for (int cc = rr; cc < 10; cc++) {
+        if (idx == e) { er = rr; ec = cc; }
+        idx++;
+      }
+    t.isData = true;
+    t.oa = HS_JR_JIDX2 + 0; t.ob = HS_JR_JIDX2 + 1; t.oc = HS_JR_JIDX2 + 2;
+    t.oxr = HS_JR_X + er; t.oxc = HS_JR_X + ec; t.oyr = HS_JR_Y + er; t.oyc = HS_JR_Y + ec;
+  } else if (e < 85) {
+    const int er = (e - 55) / 3, ec = (e - 55) % 3;
+    t.oa = ec == 0 ? HS_JR_JABJIDX + 0 : (ec == 1 ? HS_JR_JABJIDX + 2 : HS_JR_JIR + 0);
+    t.oc = ec == 0 ? HS_JR_JABJIDX + 1 : (ec == 1 ? HS_JR_JABJIDX + 3 : HS_JR_JIR + 1);
+    t.oxr = HS_JR_X + er; t.oyr = HS_JR_Y + er; t.oxc = R_ONE; t.oyc = R_ONE;
+  } else if (e < HS_TOP_N) {
+    const int ec = e - 85;
+    t.oa = ec == 0 ? HS_JR_JAB2 + 0
+         : ec == 1 ? HS_JR_JAB2 + 1
+         : ec == 2 ? HS_JR_JABR + 0
+         : ec == 3 ? HS_JR_JAB2 + 2
+         : ec == 4 ? HS_JR_JABR + 1 : HS_JR_RR;
+    t.oxr = t.oxc = t.oyr = t.oyc = R_ONE;
+  }
+  return t;
+}
 struct AccOps {
-  float a, b, c, xr, xc, yr, yc;  // top entry operands
-  float hdi, wj, x0, x1;          // accD: HdiF, JpJdF[j][dr], JpJdF[kD0][dc], JpJdF[kD1][dc]
-  float ex, ey;                   // accE / accEB operands
+  float t0[7], t1[7];  // top entry operands (lane, 64 + lane)
+  float hdi, wj, x[HS_MAXF];  // accD: HdiF, JpJdF[j][dr], JpJdF[k][dc]
+  float ex, ey;        // accE / accEB operands
   unsigned m;
 };
 }  // namespace
@@ -624,10 +660,15 @@ __device__ __forceinline__ void acc_load_tile(const HsAccArgs& a, AccLds& T, int
 // One (host i, target j, split s) accumulator block.  kBlocked: the reference's 1k/1m flush blocking is
 // emulated (needed when a block sums more than 1000 updates; below that shiftUp never fires and
 // finish() returns the plain running sum, so the counters are dropped).
+// One (host i, target j, split s) block: its 4 waves each accumulate a contiguous share of the split's
+// points (a.W = 1: wave 0 takes all of them, i.e. the single-thread reference order) and write one partial
+// each.  Lane roles: top entries lane / 64+lane, accD (j, k=0..7)[lane>>3][lane&7], accE / accEB lane < 40.
+// kBlocked: the reference's 1k/1m flush blocking is emulated (needed above 1000 updates per partial;
+// below that shiftUp never fires and finish() is the plain running sum, so the counters are dropped).
 template <bool kBlocked>
 __device__ __forceinline__ void acc_pair_block(const HsAccArgs& a, AccLds& T) {
-  const int nF = a.nF, S = a.S;
-  const int tid = threadIdx.x;
+  const int nF = a.nF, S = a.S, W = a.W;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int b = blockIdx.x;
   const int ij = b / S, s = b % S;
   const int i = ij % nF, j = ij / nF;  // host i, target j (accumulator index i + nF*j)
@@ -635,112 +676,114 @@ __device__ __forceinline__ void acc_pair_block(const HsAccArgs& a, AccLds& T) {
   const int span = he - hb;
   const int pb = hb + (int)((long long)span * s / S), pe = hb + (int)((long long)span * (s + 1) / S);
 
-  // ---- thread roles as LDS record offsets.  Every top entry is evaluated with the AccumulatorApprox::update
-  // expression  ((a*xc)*xr + (c*yc)*yr) + b*((xc*yr) + (yc*xr));  TopRight (xr*T0 + yr*T1) and BotRight (v)
-  // are that expression with 1 / 0 operands, which leaves their rounding unchanged.
-  int oa = R_ZERO, ob = R_ZERO, oc = R_ZERO, oxr = R_ZERO, oxc = R_ZERO, oyr = R_ZERO, oyc = R_ZERO;
-  bool isData = false;
-  if (tid < 55) {
-    int er = 0, ec = 0, idx = 0;
-    for (int rr = 0; rr < 10; rr++)
-      for (int cc = rr; cc < 10; cc++) {
-        if (idx == tid) { er = rr; ec = cc; }
-        idx++;
-      }
-    isData = true;
-    oa = HS_JR_JIDX2 + 0; ob = HS_JR_JIDX2 + 1; oc = HS_JR_JIDX2 + 2;
-    oxr = HS_JR_X + er; oxc = HS_JR_X + ec; oyr = HS_JR_Y + er; oyc = HS_JR_Y + ec;
-  } else if (tid < 85) {
-    const int er = (tid - 55) / 3, ec = (tid - 55) % 3;
-    oa = ec == 0 ? HS_JR_JABJIDX + 0 : (ec == 1 ? HS_JR_JABJIDX + 2 : HS_JR_JIR + 0);
-    oc = ec == 0 ? HS_JR_JABJIDX + 1 : (ec == 1 ? HS_JR_JABJIDX + 3 : HS_JR_JIR + 1);
-    oxr = HS_JR_X + er; oyr = HS_JR_Y + er; oxc = R_ONE; oyc = R_ONE;
-  } else if (tid < HS_TOP_N) {
-    const int ec = tid - 85;
-    oa = ec == 0 ? HS_JR_JAB2 + 0
-       : ec == 1 ? HS_JR_JAB2 + 1
-       : ec == 2 ? HS_JR_JABR + 0
-       : ec == 3 ? HS_JR_JAB2 + 2
-       : ec == 4 ? HS_JR_JABR + 1 : HS_JR_RR;
-    oxr = oxc = oyr = oyc = R_ONE;
-  }
-  // D entries (target j, target kD) [dr][dc] for kD = kD0 and kD0 + 4 (wave-uniform kD)
-  const int kD0 = tid >> 6, kD1 = kD0 + 4, dr = (tid & 63) >> 3, dc = tid & 7;
-  const int owj = R_JP + j * 8 + dr, ox0 = R_JP + kD0 * 8 + dc, ox1 = R_JP + kD1 * 8 + dc;
-  // E entries: tid 91..122 ((HdiF*JpJdF[j][r])*Hcd[c]); EB: tid 123..130 ((HdiF*bdSumF)*JpJdF[j][r])
-  const int eE = tid - 91, eB = tid - 123;
+  const TopRole r0 = top_role(lane), r1 = top_role(64 + lane);
+  const int dr = lane >> 3, dc = lane & 7;
+  const int owj = R_JP + j * 8 + dr;
   int oex = R_ZERO, oey = R_ZERO;
-  if (eE >= 0 && eE < 32) { oex = R_JP + j * 8 + (eE >> 2); oey = R_HCD + (eE & 3); }
-  else if (eB >= 0 && eB < 8) { oex = R_BDS; oey = R_JP + j * 8 + eB; }
+  if (lane < 32) { oex = R_JP + j * 8 + (lane >> 2); oey = R_HCD + (lane & 3); }
+  else if (lane < 40) { oex = R_BDS; oey = R_JP + j * 8 + (lane - 32); }
 
-  Blk top, d0, d1, ex;
-  BlkCnt ctop, cd0, cd1, cex;
-  int nTop = 0, nD0 = 0, nD1 = 0;
+  Blk top0, top1, d[HS_MAXF], ex;
+  BlkCnt ctop, cd[HS_MAXF], cex;
+  int nTop = 0, nD[HS_MAXF];
+#pragma unroll
+  for (int k = 0; k < HS_MAXF; k++) nD[k] = 0;
 
   auto load = [&](int q, AccOps& o) {
     const float* R = T.rec[q];
-    o.a = R[oa]; o.b = R[ob]; o.c = R[oc]; o.xr = R[oxr]; o.xc = R[oxc]; o.yr = R[oyr]; o.yc = R[oyc];
-    o.hdi = R[R_HDI]; o.wj = R[owj]; o.x0 = R[ox0]; o.x1 = R[ox1];
+    o.t0[0] = R[r0.oa]; o.t0[1] = R[r0.ob]; o.t0[2] = R[r0.oc]; o.t0[3] = R[r0.oxr]; o.t0[4] = R[r0.oxc];
+    o.t0[5] = R[r0.oyr]; o.t0[6] = R[r0.oyc];
+    o.t1[0] = R[r1.oa]; o.t1[1] = R[r1.ob]; o.t1[2] = R[r1.oc]; o.t1[3] = R[r1.oxr]; o.t1[4] = R[r1.oxc];
+    o.t1[5] = R[r1.oyr]; o.t1[6] = R[r1.oyc];
+    o.hdi = R[R_HDI]; o.wj = R[owj];
+#pragma unroll
+    for (int k = 0; k < HS_MAXF; k++) o.x[k] = R[R_JP + k * 8 + dc];
     o.ex = R[oex]; o.ey = R[oey];
     o.m = T.m[q];
+  };
+  auto topv = [](const float* t) {  // a b c xr xc yr yc
+    return ((t[0] * t[4]) * t[3] + (t[2] * t[6]) * t[5]) + t[1] * ((t[4] * t[5]) + (t[6] * t[3]));
   };
 
   for (int t0 = pb; t0 < pe; t0 += ACC_TILE) {
     const int tn = min(ACC_TILE, pe - t0);
     acc_load_tile(a, T, t0, tn, j);
     HS_TRACE(a, 2);
-    const int n = T.cnt;
+    const int cnt = T.cnt;
+    const int c0 = wv < W ? (cnt * wv) / W : cnt, c1 = wv < W ? (cnt * (wv + 1)) / W : cnt;
     AccOps nx;
-    if (n > 0) load(T.list[0], nx);
-    for (int c = 0; c < n; c++) {
+    if (c0 < c1) load(T.list[c0], nx);
+    for (int c = c0; c < c1; c++) {
       const AccOps o = nx;
-      if (c + 1 < n) load(T.list[c + 1], nx);
+      if (c + 1 < c1) load(T.list[c + 1], nx);
       // ---- AccumulatedTopHessianSSE::addPoint<0>: update() adds Data then shiftUp; BotRight / TopRight after
-      const float upd = ((o.a * o.xc) * o.xr + (o.c * o.yc) * o.yr) + o.b * ((o.xc * o.yr) + (o.yc * o.xr));
+      const float u0 = topv(o.t0), u1 = topv(o.t1);
       const float wl = o.hdi * o.wj;
-      const bool b0 = (o.m >> kD0) & 1u, b1 = (o.m >> kD1) & 1u;
       if (kBlocked) {
         const int f = ctop.bump();
-        if (isData) top.A += upd;
-        if (f) top.flush(f);
-        if (!isData) top.A += upd;
-        if (b0) {
-          d0.A += wl * o.x0;
-          d0.flush(cd0.bump());
-        }
-        if (b1) {
-          d1.A += wl * o.x1;
-          d1.flush(cd1.bump());
-        }
+        if (r0.isData) top0.A += u0;
+        if (r1.isData) top1.A += u1;
+        if (f) { top0.flush(f); top1.flush(f); }
+        if (!r0.isData) top0.A += u0;
+        if (!r1.isData) top1.A += u1;
+#pragma unroll
+        for (int k = 0; k < HS_MAXF; k++)
+          if ((o.m >> k) & 1u) {  // wave-uniform
+            d[k].A += wl * o.x[k];
+            d[k].flush(cd[k].bump());
+          }
         ex.A += (o.hdi * o.ex) * o.ey;
         ex.flush(cex.bump());
       } else {
-        top.A += upd;
-        if (b0) d0.A += wl * o.x0;
-        if (b1) d1.A += wl * o.x1;
+        top0.A += u0;
+        top1.A += u1;
+#pragma unroll
+        for (int k = 0; k < HS_MAXF; k++) {
+          const bool bk = (o.m >> k) & 1u;
+          d[k].A = bk ? d[k].A + wl * o.x[k] : d[k].A;
+          nD[k] += bk ? 1 : 0;
+        }
         ex.A += (o.hdi * o.ex) * o.ey;
         nTop++;
-        nD0 += b0 ? 1 : 0;
-        nD1 += b1 ? 1 : 0;
       }
     }
   }
   HS_TRACE(a, 1);
-  float* P = a.part + ((size_t)ij * S + s) * HS_PART_N;
-  int* PC = a.part_cnt + ((size_t)ij * S + s) * 16;
-  // finish(): A1m = (A1k + A) + A1m  (== A when nothing was flushed)
-  if (tid < HS_TOP_N) P[tid] = top.finish();
-  P[96 + kD0 * 64 + dr * 8 + dc] = d0.finish();
-  P[96 + kD1 * 64 + dr * 8 + dc] = d1.finish();
-  if (eE >= 0 && eE < 32) P[96 + 512 + eE] = ex.finish();
-  else if (eB >= 0 && eB < 8) P[96 + 512 + 32 + eB] = ex.finish();
-  if (tid == 0) {
-    PC[0] = kBlocked ? ctop.total() : nTop;
-    PC[9] = kBlocked ? cex.total() : nTop;
+  // the waves' partials are combined in wave order in fp64 (the reference sums its per-thread fp32
+  // accumulators in fp64) into one partial of this split
+  __syncthreads();  // tile records are no longer read
+  float* stage = &T.rec[0][0];
+  if (wv < W) {
+    float* Ps = stage + wv * HS_PART_N;
+    // finish(): A1m = (A1k + A) + A1m  (== A when nothing was flushed)
+    Ps[lane] = top0.finish();
+    if (64 + lane < 96) Ps[64 + lane] = 64 + lane < HS_TOP_N ? top1.finish() : 0.f;
+#pragma unroll
+    for (int k = 0; k < HS_MAXF; k++) Ps[96 + k * 64 + lane] = d[k].finish();
+    if (lane < 40) Ps[96 + 512 + lane] = ex.finish();
+    if (lane == 0) {
+      T.wcnt[wv][0] = kBlocked ? ctop.total() : nTop;
+      T.wcnt[wv][9] = kBlocked ? cex.total() : nTop;
+    }
+    if (lane < HS_MAXF) {
+      int v = 0;
+#pragma unroll
+      for (int k = 0; k < HS_MAXF; k++) v = k == lane ? (kBlocked ? cd[k].total() : nD[k]) : v;
+      T.wcnt[wv][1 + lane] = v;
+    }
   }
-  if ((tid & 63) == 0) {
-    PC[1 + kD0] = kBlocked ? cd0.total() : nD0;
-    PC[1 + kD1] = kBlocked ? cd1.total() : nD1;
+  __syncthreads();
+  double* P = a.part + ((size_t)ij * S + s) * HS_PART_N;
+  int* PC = a.part_cnt + ((size_t)ij * S + s) * 16;
+  for (int e = tid; e < HS_PART_N; e += 256) {
+    double sum = 0.0;
+    for (int w = 0; w < W; w++) sum += (double)stage[w * HS_PART_N + e];
+    P[e] = sum;
+  }
+  if (tid < 10) {
+    int c = 0;
+    for (int w = 0; w < W; w++) c += T.wcnt[w][tid];
+    PC[tid] = c;
   }
 }
 
@@ -792,7 +835,7 @@ __global__ __launch_bounds__(64) void hs_k_stitch(HsStitchArgs a) {
   __shared__ int cnt[16];
   HS_TRACE(a, 0);
   // ---- everything this pair needs, loads in flight together
-  const float* P0 = a.part + (size_t)ij * S * HS_PART_N;
+  const double* P0 = a.part + (size_t)ij * S * HS_PART_N;
   const int* C0 = a.part_cnt + (size_t)ij * S * 16;
   aH[tid] = a.adHost[ij * 64 + tid];
   aT[tid] = a.adTarget[ij * 64 + tid];
@@ -812,23 +855,23 @@ __global__ __launch_bounds__(64) void hs_k_stitch(HsStitchArgs a) {
 #pragma unroll
   for (int kk = 0; kk < HS_MAXF; kk++) sD[kk] = 0.0;
   for (int s = 0; s < S; s++) {
-    const float* Ps = P0 + (size_t)s * HS_PART_N;
+    const double* Ps = P0 + (size_t)s * HS_PART_N;
     const int* Cs = C0 + s * 16;
     const bool top = Cs[0] > 0;
     // clamped, unconditional loads (kept in flight together)
-    const float p0 = Ps[tid], p1 = Ps[64 + (tid & 31)];
-    const float pe = Ps[96 + 512 + min(tid, 39)];
-    float pd[HS_MAXF];
+    const double p0 = Ps[tid], p1 = Ps[64 + (tid & 31)];
+    const double pe = Ps[96 + 512 + min(tid, 39)];
+    double pd[HS_MAXF];
 #pragma unroll
     for (int kk = 0; kk < HS_MAXF; kk++) pd[kk] = Ps[96 + min(kk, nF - 1) * 64 + tid];
     if (top) {
-      se0 += (double)p0;
-      se1 += (double)p1;
+      se0 += p0;
+      se1 += p1;
     }
-    sE += (double)pe;
+    sE += pe;
 #pragma unroll
     for (int kk = 0; kk < HS_MAXF; kk++)
-      if (kk < nF && Cs[1 + kk] > 0) sD[kk] += (double)pd[kk];
+      if (kk < nF && Cs[1 + kk] > 0) sD[kk] += pd[kk];
   }
   e[tid] = se0;
   if (tid < 32) e[64 + tid] = se1;
@@ -938,7 +981,7 @@ __global__ __launch_bounds__(64) void hs_k_stitch(HsStitchArgs a) {
 // solve + step (fp64), one workgroup of 256 threads
 // =====================================================================================================
 namespace {
-constexpr int SOLVE_NT = 512;
+constexpr int SOLVE_NT = 384;  // 6 waves: the lower-triangle 8x8 tile groups of the blocked LDLT
 constexpr int SOLVE_NU = (HS_MAXDIM * HS_MAXDIM + SOLVE_NT - 1) / SOLVE_NT;  // matrix entries per thread
 
 __device__ __forceinline__ double readlane_f64(double v, int lane) {
@@ -949,9 +992,134 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
 }
 }  // namespace
 
+
+// Solves (L D L^T) y = z in place for the permuted, scaled system of one GN step: right-looking LDLT in
+// 4-column blocks (n = 4 + 8 nF is a multiple of 4).  Per block: wave 0 factors the 4-column panel with
+// readlane broadcasts (and carries the forward substitution), then every lower-triangle 4x4 tile
+// (register-resident; wave w owns an 8x8 group of tiles so its LDS reads hit 8 distinct rows of the
+// column-major panel arrays: no bank conflicts) takes the rank-4 update  A -= (L D) L^T  in column order,
+// and the owners of the next panel publish it.  Two workgroup barriers per block.  The result is Eigen's
+// LDLT solve up to fp64 rounding order (the pivot order is applied by the caller).  Then D^-1 and the
+// backward substitution by wave 0.
+//   M : the permuted system (row-major, stride n) in; L (strictly lower, stride LSTR) out
+//   W : scratch of 13 * HS_MAXDIM doubles
+constexpr int LSTR = HS_MAXDIM + 1;  // padded row stride of L (column writes / row reads: 2-way banks)
+__device__ __forceinline__ void ldlt_solve_blocked(double* M, double* W, double* yv, int n, int tid, long long* trace) {
+  constexpr int MD = HS_MAXDIM;
+  const int nb = n >> 2;
+  double* PB = W;           // [4][MD] current panel, column-major
+  double* LW = W + 4 * MD;  // [4][MD] L D of the panel columns
+  double* LS = W + 8 * MD;  // [4][MD] L of the panel columns
+  double* Dv = W + 12 * MD; // [MD]
+  // lower-triangle 8x8 tile groups: wave -> (group row, group col)
+  const int wv = tid >> 6, lane = tid & 63;
+  const int gr = wv == 0 ? 0 : (wv <= 2 ? 1 : 2), gc = wv == 0 ? 0 : (wv <= 2 ? wv - 1 : wv - 3);
+  const int tr = 8 * gr + (lane >> 3), tc = 8 * gc + (lane & 7);
+  const bool lower = wv < 6 && tr < nb && tc < nb && tr >= tc;
+  double v[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+#pragma unroll
+    for (int c = 0; c < 4; c++) v[i][c] = lower ? M[(4 * tr + i) * n + 4 * tc + c] : 0.0;
+  if (lower && tc == 0)
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int c = 0; c < 4; c++) PB[c * MD + 4 * tr + i] = v[i][c];
+  __syncthreads();
+  for (int kb = 0; kb < nb; kb++) {
+    const int k0 = 4 * kb;
+    if (tid < 64) {  // panel: rows k0 + lane and k0 + 64 + lane
+      const int r0 = k0 + lane, r1 = k0 + 64 + lane;
+      const bool v0 = r0 < n, v1 = r1 < n;
+      const int c0 = min(r0, n - 1), c1 = min(r1, n - 1);
+      double p0[4], p1[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        p0[j] = PB[j * MD + c0];
+        p1[j] = PB[j * MD + c1];
+      }
+      double y0 = yv[c0], y1 = yv[c1];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const double d = readlane_f64(p0[j], j);
+        const double dinv = fabs(d) > DBL_MIN ? 1.0 / d : 0.0;
+        const double l0 = lane > j ? p0[j] * dinv : 0.0, l1 = v1 ? p1[j] * dinv : 0.0;
+#pragma unroll
+        for (int jp = j + 1; jp < 4; jp++) {
+          const double aj = readlane_f64(p0[j], jp);  // A[k0+jp][k0+j]
+          p0[jp] = p0[jp] - l0 * aj;
+          p1[jp] = p1[jp] - l1 * aj;
+        }
+        const double yj = readlane_f64(y0, j);
+        y0 = y0 - l0 * yj;
+        y1 = y1 - l1 * yj;
+        if (lane == j) Dv[k0 + j] = d;
+        if (v0) {
+          LW[j * MD + r0] = p0[j];
+          LS[j * MD + r0] = l0;
+          if (lane > j) M[r0 * LSTR + k0 + j] = l0;
+        }
+        if (v1) {
+          LW[j * MD + r1] = p1[j];
+          LS[j * MD + r1] = l1;
+          M[r1 * LSTR + k0 + j] = l1;
+        }
+      }
+      if (v0) yv[r0] = y0;
+      if (v1) yv[r1] = y1;
+    }
+    __syncthreads();
+    if (lower && tc > kb) {  // rank-4 update of a trailing lower tile
+      double lw[4][4], ls[4][4];
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          lw[i][j] = LW[j * MD + 4 * tr + i];
+          ls[i][j] = LS[j * MD + 4 * tc + i];
+        }
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+          for (int c = 0; c < 4; c++) v[i][c] = __builtin_fma(-lw[i][j], ls[c][j], v[i][c]);
+      if (tc == kb + 1)
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+          for (int c = 0; c < 4; c++) PB[c * MD + 4 * tr + i] = v[i][c];
+    }
+    __syncthreads();
+    if (trace && tid == 0 && kb == 8) trace[14] = wall_clock64();  // mid-factorization checkpoint
+  }
+  // D^-1 z, then L^T x = D^-1 z by wave 0 (lane l owns rows l and l + 64)
+  if (tid < 64) {
+    const int i0 = tid, i1 = tid + 64;
+    const bool o0 = i0 < n, o1 = i1 < n;
+    const int c0 = min(i0, n - 1), c1 = min(i1, n - 1);
+    const double d0 = Dv[c0], d1 = Dv[c1];
+    double y0 = o0 && fabs(d0) > DBL_MIN ? yv[c0] / d0 : 0.0;
+    double y1 = o1 && fabs(d1) > DBL_MIN ? yv[c1] / d1 : 0.0;
+    double nb0 = M[(n - 1) * LSTR + c0], nb1 = M[(n - 1) * LSTR + c1];
+    for (int k = n - 1; k > 0; k--) {
+      const double b0 = nb0, b1 = nb1;  // L(k, i)
+      nb0 = M[(k - 1) * LSTR + c0];
+      nb1 = M[(k - 1) * LSTR + c1];
+      const double xk = k >= 64 ? readlane_f64(y1, k - 64) : readlane_f64(y0, k);
+      const double n0 = y0 - b0 * xk, n1 = y1 - b1 * xk;
+      y0 = i0 < k ? n0 : y0;
+      y1 = i1 < k ? n1 : y1;
+    }
+    if (o0) yv[i0] = y0;
+    if (o1) yv[i1] = y1;
+  }
+}
+
 __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
   __shared__ double A[HS_MAXDIM * HS_MAXDIM];  // raw HA, then the scaled system, then Porth
-  __shared__ double B[HS_MAXDIM * HS_MAXDIM];  // raw HSC, then the published LDLT rows
+  __shared__ double B[HS_MAXDIM * (HS_MAXDIM + 1)];  // raw HSC, then the permuted system, then L
   __shared__ double bf[HS_MAXDIM], Sv[HS_MAXDIM], xs[HS_MAXDIM], yv[HS_MAXDIM], px[HS_MAXDIM], dl[HS_MAXDIM];
   __shared__ float xF[HS_MAXDIM];
   __shared__ int pos[HS_MAXDIM], sorted_[HS_MAXDIM], elem_at[HS_MAXDIM], pos_of[HS_MAXDIM];
@@ -964,14 +1132,6 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
   if (tid == 0) {
     s_it = a.iteration >= 0 ? a.iteration : st->iteration;
     s_tie = 0;
-  }
-  // owned entries idx = tid + u*nt  ->  (R, C)
-  int Ru[SOLVE_NU], Cu[SOLVE_NU];
-#pragma unroll
-  for (int u = 0; u < SOLVE_NU; u++) {
-    const int idx = tid + u * nt;
-    Ru[u] = idx < nn ? idx / n : n;
-    Cu[u] = idx < nn ? idx - Ru[u] * n : n;
   }
 
   if (a.flags & HS_SOLVE) {
@@ -1020,7 +1180,7 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     double v[SOLVE_NU];
 #pragma unroll
     for (int u = 0; u < SOLVE_NU; u++) {
-      const int r = min(Ru[u], n - 1), c = min(Cu[u], n - 1);
+      const int ix = min(tid + u * nt, nn - 1), r = ix / n, c = ix - r * n;
       const int idx = r * n + c, tdx = c * n + r;
       const int fr = r < 4 ? -1 : (r - 4) >> 3, fc = c < 4 ? -1 : (c - 4) >> 3;
       const double a0 = A[idx], a1 = A[tdx], b0 = B[idx], b1 = B[tdx], hl0 = px[r];
@@ -1054,9 +1214,9 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < SOLVE_NU; u++) {
-      const int r = min(Ru[u], n - 1), c = min(Cu[u], n - 1);
+      const int ix = min(tid + u * nt, nn - 1), r = ix / n, c = ix - r * n;
       const double sv = Sv[r] * A[r * n + c] * Sv[c];
-      if (Ru[u] < n) A[r * n + c] = sv;
+      if (tid + u * nt < nn) A[r * n + c] = sv;
     }
     if (tid < n) bf[tid] = Sv[tid] * bf[tid];
     __syncthreads();
@@ -1106,82 +1266,17 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
       }
     }
     __syncthreads();
-    // owned entries of the permuted system P S H S P^T; row 0 is published for the first step
-#pragma unroll
-    for (int u = 0; u < SOLVE_NU; u++) {
-      const int r = min(Ru[u], n - 1), c = min(Cu[u], n - 1);
-      v[u] = A[pos[r] * n + pos[c]];
+    // the permuted system P S H S P^T and right-hand side for the single-wave factorization
+    for (int idx = tid; idx < nn; idx += nt) {
+      const int r = idx / n, c = idx - r * n;
+      B[idx] = A[pos[r] * n + pos[c]];
     }
-#pragma unroll
-    for (int u = 0; u < SOLVE_NU; u++)
-      if (Ru[u] == 0) B[Cu[u]] = v[u];
     if (tid < n) yv[tid] = bf[pos[tid]];
     __syncthreads();
     HS_TRACE(a, 2);
-    // right-looking LDLT with register-resident entries (both triangles): step k reads the published
-    // row k (B[k][*] = D_k, L(r,k) D_k) and the owners of row k+1 publish it after their update.
-    // The forward substitution L z = P S b rides along.  Loads are unconditional, updates are selects.
-    int Rc[SOLVE_NU], Cc[SOLVE_NU];
-#pragma unroll
-    for (int u = 0; u < SOLVE_NU; u++) {
-      Rc[u] = min(Ru[u], n - 1);
-      Cc[u] = min(Cu[u], n - 1);
-    }
-    for (int kq = 0; kq < n; kq++) {
-      const double* rowk = B + kq * n;
-      const double d = rowk[kq];
-      const double dinv = fabs(d) > DBL_MIN ? 1.0 / d : 0.0;
-      const int m = n - kq - 1;
-      const double yk = yv[kq];
-      const double ry = rowk[min(kq + 1 + tid, n - 1)];
-      double rr[SOLVE_NU], rc[SOLVE_NU];
-#pragma unroll
-      for (int u = 0; u < SOLVE_NU; u++) {
-        rr[u] = rowk[Rc[u]];
-        rc[u] = rowk[Cc[u]];
-      }
-      if (tid < m) yv[kq + 1 + tid] -= (ry * dinv) * yk;
-      // every owned entry is updated: entries outside the trailing block are either in an already
-      // published row or strictly below the diagonal, and neither is ever published again
-#pragma unroll
-      for (int u = 0; u < SOLVE_NU; u++) v[u] -= rr[u] * (rc[u] * dinv);
-      // publish row k+1
-#pragma unroll
-      for (int u = 0; u < SOLVE_NU; u++)
-        if (Ru[u] == kq + 1 && Cu[u] > kq) B[Ru[u] * n + Cu[u]] = v[u];
-      __syncthreads();
-      if (kq == 0) HS_TRACE(a, 10);
-      if (kq == 3) HS_TRACE(a, 11);
-      if (kq == 15) HS_TRACE(a, 12);
-      if (kq == 31) HS_TRACE(a, 13);
-      if (kq == 63) HS_TRACE(a, 14);
-    }
-    HS_TRACE(a, 3);
-    // D^-1, then the backward substitution L^T x = z by one wave: lane l owns rows l and l + 64
-    if (tid < 64) {
-      const int i0 = tid, i1 = min(tid + 64, n - 1);
-      const bool own1 = tid + 64 < n;
-      const double d0 = B[min(i0, n - 1) * n + min(i0, n - 1)], d1 = B[i1 * n + i1];
-      const double di0 = fabs(d0) > DBL_MIN ? 1.0 / d0 : 0.0, di1 = fabs(d1) > DBL_MIN ? 1.0 / d1 : 0.0;
-      double y0 = i0 < n ? (fabs(d0) > DBL_MIN ? yv[i0] / d0 : 0.0) : 0.0;
-      double y1 = own1 ? (fabs(d1) > DBL_MIN ? yv[i1] / d1 : 0.0) : 0.0;
-      const double* rb0 = B + min(i0, n - 1) * n;
-      const double* rb1 = B + i1 * n;
-      double nb0 = rb0[n - 1], nb1 = rb1[n - 1];
-      for (int kq = n - 1; kq > 0; kq--) {
-        // x_k is final: broadcast it, then x_i -= L(k,i) x_k for i < k  (L(k,i) D_i = B[i][k])
-        const double b0 = nb0, b1 = nb1;
-        nb0 = rb0[kq - 1];  // prefetch the next step's L entries
-        nb1 = rb1[kq - 1];
-        const double xk = kq >= 64 ? readlane_f64(y1, kq - 64) : readlane_f64(y0, kq);
-        const double n0 = y0 - (b0 * di0) * xk, n1 = y1 - (b1 * di1) * xk;
-        y0 = i0 < kq ? n0 : y0;
-        y1 = (own1 && tid + 64 < kq) ? n1 : y1;
-      }
-      if (i0 < n) yv[i0] = y0;
-      if (own1) yv[tid + 64] = y1;
-    }
+    ldlt_solve_blocked(B, A, yv, n, tid, a.trace);
     __syncthreads();
+    HS_TRACE(a, 3);
     HS_TRACE(a, 4);
     for (int q = tid; q < n; q += nt) xs[pos[q]] = yv[q];
     {

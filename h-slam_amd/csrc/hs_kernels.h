@@ -65,6 +65,7 @@ struct HsLinArgs {
 
 struct HsAccArgs {
   int nF, S, nP;
+  int W;                       // waves of a block that accumulate (1: one wave, the reference's point order)
   int blocked;                 // a (host, target, split) block can exceed 1000 updates: emulate shiftUp
   const int* host_pt_begin;    // [nF+1]
   const uint8_t* actmask;
@@ -73,7 +74,7 @@ struct HsAccArgs {
   const float* Hcd;
   const float* JpJdF;
   const float* Jrec;
-  float* part;                 // [nF*nF][S][HS_PART_N]
+  double* part;                // [nF*nF][S][HS_PART_N] (fp64 sums of the waves' fp32 partials)
   int* part_cnt;               // [nF*nF][S][16]: top count, D counts (per k), E count
   const double* p_energy;
   const float* idepth;         // |idepth| sum for doStepFromBackup's sumNID
@@ -90,7 +91,7 @@ struct HsAccArgs {
 
 struct HsStitchArgs {
   int nF, S;
-  const float* part;
+  const double* part;
   const int* part_cnt;
   const double* hccbc;
   const double* adHost;        // [nF*nF][64]  index h + nF*t

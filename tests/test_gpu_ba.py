@@ -16,17 +16,18 @@ pytestmark = pytest.mark.gpu
 H_TOL = 1e-4
 
 
-def _pair(scene, nthreads=1, split_points=1 << 30):
-    """GPU window + oracle.  By default every (host, target) accumulator is one workgroup in point order
-    (HS_ACC_SPLIT_POINTS huge), i.e. the single-thread reference's summation order."""
+def _pair(scene, nthreads=1, exact=True):
+    """GPU window + oracle.  exact: every (host, target) accumulator is one sequential partial in point order
+    (HS_ACC_EXACT=1), i.e. the single-thread reference's fp32 summation order."""
     import os
     from hslam_amd.ba import BAWindow
     from oracle_ffi import OracleBA
-    os.environ["HS_ACC_SPLIT_POINTS"] = str(split_points)
+    if exact:
+        os.environ["HS_ACC_EXACT"] = "1"
     try:
         g = BAWindow(scene)
     finally:
-        os.environ.pop("HS_ACC_SPLIT_POINTS", None)
+        os.environ.pop("HS_ACC_EXACT", None)
     return g, OracleBA(scene, nthreads=nthreads)
 
 
@@ -142,10 +143,10 @@ def test_window_edge_cases():
 
 
 def test_split_accumulation_matches_threaded_reference(scene2k):
-    """The production split (64 points per accumulate workgroup) changes only the fp32 summation order,
+    """The production partitioning (64-point splits x 4 waves) changes only the fp32 summation order,
     like the reference's IndexThreadReduce pool does: the GN trajectory must stay as close to the
     single-thread oracle as the oracle's own 8-thread pool does."""
-    g, o1 = _pair(scene2k, split_points=64)
+    g, o1 = _pair(scene2k, exact=False)
     from oracle_ffi import OracleBA
     o8 = OracleBA(scene2k, nthreads=8)
     _, eg = g.optimize(6)
