@@ -163,7 +163,7 @@ def main():
             "units_per_launch": shard.n_res,
             "avg_launch_ms": lin_ms,
         },
-        "phase_ms_per_step": {
+        "phase_ms_per_step": {  # per-phase split: HS_EVENT_TIMING=2 (default times the linearize kernel only)
             "solve_step_kernel": tim["solve_ms"] / nt,
             "linearize_kernel": lin_ms,
             "accumulate_stitch": tim["acc_stitch_ms"] / nt,

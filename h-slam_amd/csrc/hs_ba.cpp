@@ -68,7 +68,7 @@ struct hs_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   std::vector<hipEvent_t> ev;  // 4 per timed iteration
-  bool events = true;
+  int events = 1;              // HS_EVENT_TIMING: 0 none, 1 linearize kernel only (default), 2 every phase
 
   // window (host side)
   int nF = 0, nP = 0, nR = 0, S = 1, W = 4, maxPtsPerBlock = 0;
@@ -254,7 +254,7 @@ static int launch_reduce(hs_ctx* c) {
   s.adHost = c->d_adHost; s.adTarget = c->d_adTarget;
   s.HA = c->HA(); s.bA = c->bA(); s.HSC = c->HSC(); s.bSC = c->bSC();
   s.trace = c->d_tr_stitch;
-  hipLaunchKernelGGL(hs_k_stitch, dim3(c->nF * c->nF), dim3(64), 0, c->stream, s);
+  hipLaunchKernelGGL(hs_k_stitch, dim3(c->nF * c->nF), dim3(256), 0, c->stream, s);
   HS_HIP(hipGetLastError());
   if (c->comm && c->nranks > 1)
     HS_NCCL(ncclAllReduce(c->d_sys, c->d_sys, c->sys_len(), ncclDouble, ncclSum, c->comm, c->stream));
@@ -352,15 +352,16 @@ static int gn_iterations(hs_ctx* c, int it0, int K, bool allow_break, double* en
   HS_TRY(set_loop_counters(c, it0));
   int k = 0;
   const int nev = c->events ? std::min(K, kEventIters) : 0;
+  const bool all = c->events >= 2;
   for (; k < K; k++) {
     const bool timed = k < nev;
-    if (timed) HS_HIP(hipEventRecord(c->ev[4 * k + 0], c->stream));
+    if (timed && all) HS_HIP(hipEventRecord(c->ev[4 * k + 0], c->stream));
     HS_TRY(launch_solve(c, HS_SOLVE | HS_APPLY, -1, true));
     if (timed) HS_HIP(hipEventRecord(c->ev[4 * k + 1], c->stream));
     HS_TRY(launch_linearize(c, 1));
     if (timed) HS_HIP(hipEventRecord(c->ev[4 * k + 2], c->stream));
     HS_TRY(launch_reduce(c));
-    if (timed) HS_HIP(hipEventRecord(c->ev[4 * k + 3], c->stream));
+    if (timed && all) HS_HIP(hipEventRecord(c->ev[4 * k + 3], c->stream));
     if (allow_break) {
       int cb = 0;
       HS_HIP(hipMemcpyAsync(&c->h_ctl[3], (char*)c->d_state + offsetof(HsDevState, canbreak), sizeof(int),
@@ -385,10 +386,11 @@ static int gn_iterations(hs_ctx* c, int it0, int K, bool allow_break, double* en
   double tl = 0, ta = 0, ts = 0;
   for (int q = 0; q < std::min(k, nev); q++) {
     float ms;
-    HS_HIP(hipEventElapsedTime(&ms, c->ev[4 * q + 0], c->ev[4 * q + 1]));
-    ts += ms;
     HS_HIP(hipEventElapsedTime(&ms, c->ev[4 * q + 1], c->ev[4 * q + 2]));
     tl += ms;
+    if (!all) continue;
+    HS_HIP(hipEventElapsedTime(&ms, c->ev[4 * q + 0], c->ev[4 * q + 1]));
+    ts += ms;
     HS_HIP(hipEventElapsedTime(&ms, c->ev[4 * q + 2], c->ev[4 * q + 3]));
     ta += ms;
   }
@@ -460,7 +462,7 @@ int hs_create(hs_ctx** out, const hs_params* params, int device_id) {
   else hs_params_default(&c->P);
   c->device = device_id;
   const char* ev = std::getenv("HS_EVENT_TIMING");
-  c->events = !(ev && ev[0] == '0');
+  c->events = ev ? std::atoi(ev) : 1;
   if (hipSetDevice(device_id) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc((void**)&c->h_state, sizeof(HsDevState)) != hipSuccess ||
       hipHostMalloc((void**)&c->h_ctl, 8 * sizeof(int)) != hipSuccess) {

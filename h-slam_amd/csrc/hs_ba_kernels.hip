@@ -823,68 +823,78 @@ __device__ __forceinline__ int tri_idx(int r, int c) {
 }
 }  // namespace
 
-__global__ __launch_bounds__(64) void hs_k_stitch(HsStitchArgs a) {
+// out(8x8) = A(8x8) * M(8x8) * B(8x8)^T by one wave (lane = r*8 + c), tmp = the wave's own LDS scratch;
+// a wave executes its LDS operations in order, so no workgroup barrier is needed
+__device__ __forceinline__ double sandwich_w(const double* A, const double* M, const double* B, double* tmp, int lane) {
+  const int r = lane >> 3, c = lane & 7;
+  double s = 0.0;
+  for (int l = 0; l < 8; l++) s += A[r * 8 + l] * M[l * 8 + c];
+  __builtin_amdgcn_wave_barrier();
+  tmp[lane] = s;
+  __builtin_amdgcn_wave_barrier();
+  double o = 0.0;
+  for (int l = 0; l < 8; l++) o += tmp[r * 8 + l] * B[c * 8 + l];
+  __builtin_amdgcn_wave_barrier();
+  return o;
+}
+
+// one workgroup (4 waves) per (host i, target j): fp64 sum of the split partials, then the top block
+// (wave 0), the Schur rows (i, j, k) for k = wave, wave+4 (all waves) and the calib / b parts
+__global__ __launch_bounds__(256) void hs_k_stitch(HsStitchArgs a) {
   const int nF = a.nF, S = a.S;
   const int i = blockIdx.x % nF, j = blockIdx.x / nF;
   const int ij = i + nF * j;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int n = 4 + 8 * nF;
   const int iIdx = 4 + 8 * i, jIdx = 4 + 8 * j;
-  __shared__ double e[96], A88[64], A84[32], a8r[8], tmp[64], aH[64], aT[64], v8[8], Hpc[32];
-  __shared__ double D[HS_MAXF][64], aH2[HS_MAXF][64], aT2[HS_MAXF][64];
+  __shared__ double E[HS_PART_N];  // summed partial: top 96 | D 8x64 | E 32 | EB 8
+  __shared__ double A88[64], A84[32], a8r[8], aH[64], aT[64];
+  __shared__ double aH2[HS_MAXF][64], aT2[HS_MAXF][64], tmpw[4][64];
   __shared__ int cnt[16];
   HS_TRACE(a, 0);
-  // ---- everything this pair needs, loads in flight together
+  // ---- everything this pair needs, all loads in flight together
   const double* P0 = a.part + (size_t)ij * S * HS_PART_N;
   const int* C0 = a.part_cnt + (size_t)ij * S * 16;
-  aH[tid] = a.adHost[ij * 64 + tid];
-  aT[tid] = a.adTarget[ij * 64 + tid];
+  if (tid < 64) {
+    aH[tid] = a.adHost[ij * 64 + tid];
+    aT[tid] = a.adTarget[ij * 64 + tid];
+  }
 #pragma unroll
-  for (int kk = 0; kk < HS_MAXF; kk++)
-    if (kk < nF) {
-      aH2[kk][tid] = a.adHost[(i + nF * kk) * 64 + tid];
-      aT2[kk][tid] = a.adTarget[(i + nF * kk) * 64 + tid];
+  for (int u = 0; u < 4; u++) {  // adjoints of (i, k) for all k: 2 * 8 * 64 values
+    const int q = tid + 256 * u, kk = q >> 7, w = q & 127;
+    const int kc = min(kk, nF - 1);
+    const double v = (w < 64 ? a.adHost : a.adTarget)[(i + nF * kc) * 64 + (w & 63)];
+    if (kk < nF) (w < 64 ? aH2[kk] : aT2[kk])[w & 63] = v;
+  }
+  // split partials summed in fp64 (stitchDoubleInternal: accH += acc[tid2].H.cast<double>() for num > 0)
+  double sum[3] = {0.0, 0.0, 0.0};
+  for (int s = 0; s < S; s++) {
+    const double* Ps = P0 + (size_t)s * HS_PART_N;
+    const int* Cs = C0 + s * 16;
+#pragma unroll
+    for (int u = 0; u < 3; u++) {
+      const int e = tid + 256 * u;
+      const double pv = Ps[min(e, HS_PART_N - 1)];
+      const int grp = e < 96 ? 0 : (e < 96 + 512 ? 1 + ((e - 96) >> 6) : 9);  // count slot of the entry
+      if (e < HS_PART_N && (grp == 9 || Cs[grp] > 0)) sum[u] += pv;
     }
+  }
+#pragma unroll
+  for (int u = 0; u < 3; u++)
+    if (tid + 256 * u < HS_PART_N) E[tid + 256 * u] = sum[u];
   if (tid < 16) {
     int c = 0;
     for (int s = 0; s < S; s++) c += C0[s * 16 + tid];
     cnt[tid] = c;
   }
-  // split partials summed in fp64 (stitchDoubleInternal: accH += acc[tid2].H.cast<double>() for num > 0)
-  double se0 = 0.0, se1 = 0.0, sE = 0.0, sD[HS_MAXF];
-#pragma unroll
-  for (int kk = 0; kk < HS_MAXF; kk++) sD[kk] = 0.0;
-  for (int s = 0; s < S; s++) {
-    const double* Ps = P0 + (size_t)s * HS_PART_N;
-    const int* Cs = C0 + s * 16;
-    const bool top = Cs[0] > 0;
-    // clamped, unconditional loads (kept in flight together)
-    const double p0 = Ps[tid], p1 = Ps[64 + (tid & 31)];
-    const double pe = Ps[96 + 512 + min(tid, 39)];
-    double pd[HS_MAXF];
-#pragma unroll
-    for (int kk = 0; kk < HS_MAXF; kk++) pd[kk] = Ps[96 + min(kk, nF - 1) * 64 + tid];
-    if (top) {
-      se0 += p0;
-      se1 += p1;
-    }
-    sE += pe;
-#pragma unroll
-    for (int kk = 0; kk < HS_MAXF; kk++)
-      if (kk < nF && Cs[1 + kk] > 0) sD[kk] += pd[kk];
-  }
-  e[tid] = se0;
-  if (tid < 32) e[64 + tid] = se1;
-  if (tid < 32) Hpc[tid] = sE;
-  else if (tid < 40) v8[tid - 32] = sE;
-#pragma unroll
-  for (int kk = 0; kk < HS_MAXF; kk++)
-    if (kk < nF) D[kk][tid] = sD[kk];
   __syncthreads();
   HS_TRACE(a, 1);
-  const bool haveTop = cnt[0] > 0;
-  if (haveTop) {  // AccumulatorApprox::finish -> 13x13 [calib4|xi6|a|b|r]
-    const int r = tid >> 3, c = tid & 7;  // A88 = H[4+r][4+c]
+  const double* e = E;
+  const double* Hpc = E + 96 + 512;
+  const double* v8 = E + 96 + 512 + 32;
+  const int r = lane >> 3, c = lane & 7;
+  double* tmp = tmpw[wv];
+  if (wv == 0 && cnt[0] > 0) {  // top block: AccumulatorApprox::finish -> 13x13 [calib4|xi6|a|b|r]
     const int R = 4 + r, Cc = 4 + c;
     double v;
     if (R < 10 && Cc < 10) {
@@ -896,29 +906,26 @@ __global__ __launch_bounds__(64) void hs_k_stitch(HsStitchArgs a) {
       const int bi = (R - 10) + (Cc - 10);  // (a,a) 0, (a,b) 1, (b,b) 3
       v = e[85 + (bi == 2 ? 3 : bi)];
     }
-    A88[tid] = v;
-    if (tid < 32) {  // A84 = H[4+r][c]
-      const int rr = tid >> 2, cc = tid & 3;
+    A88[lane] = v;
+    if (lane < 32) {  // A84 = H[4+r][c]
+      const int rr = lane >> 2, cc = lane & 3;
       const int RR = 4 + rr;
-      A84[tid] = RR < 10 ? e[tri_idx(cc, RR)] : e[55 + 3 * cc + (RR - 10)];
+      A84[lane] = RR < 10 ? e[tri_idx(cc, RR)] : e[55 + 3 * cc + (RR - 10)];
     }
-    if (tid < 8) {  // a8r = H[4+r][12]
-      const int RR = 4 + tid;
-      a8r[tid] = RR < 10 ? e[55 + 3 * RR + 2] : (RR == 10 ? e[85 + 2] : e[85 + 4]);
+    if (lane < 8) {  // a8r = H[4+r][12]
+      const int RR = 4 + lane;
+      a8r[lane] = RR < 10 ? e[55 + 3 * RR + 2] : (RR == 10 ? e[85 + 2] : e[85 + 4]);
     }
-  }
-  __syncthreads();
-  const int r = tid >> 3, c = tid & 7;
-  if (haveTop) {
+    __builtin_amdgcn_wave_barrier();
     double o;
-    o = sandwich(aH, A88, aH, tmp, tid);
+    o = sandwich_w(aH, A88, aH, tmp, lane);
     atomicAdd(&a.HA[(iIdx + r) * n + iIdx + c], o);
-    o = sandwich(aT, A88, aT, tmp, tid);
+    o = sandwich_w(aT, A88, aT, tmp, lane);
     atomicAdd(&a.HA[(jIdx + r) * n + jIdx + c], o);
-    o = sandwich(aH, A88, aT, tmp, tid);
+    o = sandwich_w(aH, A88, aT, tmp, lane);
     atomicAdd(&a.HA[(iIdx + r) * n + jIdx + c], o);
-    if (tid < 32) {
-      const int rr = tid >> 2, cc = tid & 3;
+    if (lane < 32) {
+      const int rr = lane >> 2, cc = lane & 3;
       double s1 = 0.0, s2 = 0.0;
       for (int l = 0; l < 8; l++) {
         s1 += aH[rr * 8 + l] * A84[l * 4 + cc];
@@ -927,53 +934,55 @@ __global__ __launch_bounds__(64) void hs_k_stitch(HsStitchArgs a) {
       atomicAdd(&a.HA[(iIdx + rr) * n + cc], s1);
       atomicAdd(&a.HA[(jIdx + rr) * n + cc], s2);
     }
-    if (tid < 16) atomicAdd(&a.HA[(tid >> 2) * n + (tid & 3)], e[tri_idx(tid >> 2, tid & 3)]);
-    if (tid < 8) {
+    if (lane < 16) atomicAdd(&a.HA[(lane >> 2) * n + (lane & 3)], e[tri_idx(lane >> 2, lane & 3)]);
+    if (lane < 8) {
       double s1 = 0.0, s2 = 0.0;
       for (int l = 0; l < 8; l++) {
-        s1 += aH[tid * 8 + l] * a8r[l];
-        s2 += aT[tid * 8 + l] * a8r[l];
+        s1 += aH[lane * 8 + l] * a8r[l];
+        s2 += aT[lane * 8 + l] * a8r[l];
       }
-      atomicAdd(&a.bA[iIdx + tid], s1);
-      atomicAdd(&a.bA[jIdx + tid], s2);
+      atomicAdd(&a.bA[iIdx + lane], s1);
+      atomicAdd(&a.bA[jIdx + lane], s2);
     }
-    if (tid < 4) atomicAdd(&a.bA[tid], e[55 + 3 * tid + 2]);
+    if (lane < 4) atomicAdd(&a.bA[lane], e[55 + 3 * lane + 2]);
   }
-  // ---- Schur complement rows (i, j, k)
-  if (tid < 32) {
-    const int rr = tid >> 2, cc = tid & 3;
-    double s1 = 0.0, s2 = 0.0;
-    for (int l = 0; l < 8; l++) {
-      s1 += aH[rr * 8 + l] * Hpc[l * 4 + cc];
-      s2 += aT[rr * 8 + l] * Hpc[l * 4 + cc];
+  if (wv == 1) {  // Schur calib columns and b: adH/adT * accE, * accEB
+    if (lane < 32) {
+      const int rr = lane >> 2, cc = lane & 3;
+      double s1 = 0.0, s2 = 0.0;
+      for (int l = 0; l < 8; l++) {
+        s1 += aH[rr * 8 + l] * Hpc[l * 4 + cc];
+        s2 += aT[rr * 8 + l] * Hpc[l * 4 + cc];
+      }
+      atomicAdd(&a.HSC[(iIdx + rr) * n + cc], s1);
+      atomicAdd(&a.HSC[(jIdx + rr) * n + cc], s2);
     }
-    atomicAdd(&a.HSC[(iIdx + rr) * n + cc], s1);
-    atomicAdd(&a.HSC[(jIdx + rr) * n + cc], s2);
-  }
-  if (tid < 8) {
-    double s1 = 0.0, s2 = 0.0;
-    for (int l = 0; l < 8; l++) {
-      s1 += aH[tid * 8 + l] * v8[l];
-      s2 += aT[tid * 8 + l] * v8[l];
+    if (lane < 8) {
+      double s1 = 0.0, s2 = 0.0;
+      for (int l = 0; l < 8; l++) {
+        s1 += aH[lane * 8 + l] * v8[l];
+        s2 += aT[lane * 8 + l] * v8[l];
+      }
+      atomicAdd(&a.bSC[iIdx + lane], s1);
+      atomicAdd(&a.bSC[jIdx + lane], s2);
     }
-    atomicAdd(&a.bSC[iIdx + tid], s1);
-    atomicAdd(&a.bSC[jIdx + tid], s2);
   }
-  for (int kk = 0; kk < nF; kk++) {
-    if (cnt[1 + kk] == 0) continue;  // accD num == 0 (uniform)
+  for (int kk = wv; kk < nF; kk += 4) {  // Schur rows (i, j, k)
+    if (cnt[1 + kk] == 0) continue;  // accD num == 0
     const int kIdx = 4 + 8 * kk;
+    const double* D = E + 96 + kk * 64;
     double o;
-    o = sandwich(aH, D[kk], aH2[kk], tmp, tid);
+    o = sandwich_w(aH, D, aH2[kk], tmp, lane);
     atomicAdd(&a.HSC[(iIdx + r) * n + iIdx + c], o);
-    o = sandwich(aT, D[kk], aT2[kk], tmp, tid);
+    o = sandwich_w(aT, D, aT2[kk], tmp, lane);
     atomicAdd(&a.HSC[(jIdx + r) * n + kIdx + c], o);
-    o = sandwich(aT, D[kk], aH2[kk], tmp, tid);
+    o = sandwich_w(aT, D, aH2[kk], tmp, lane);
     atomicAdd(&a.HSC[(jIdx + r) * n + iIdx + c], o);
-    o = sandwich(aH, D[kk], aT2[kk], tmp, tid);
+    o = sandwich_w(aH, D, aT2[kk], tmp, lane);
     atomicAdd(&a.HSC[(iIdx + r) * n + kIdx + c], o);
   }
-  if (blockIdx.x == 0 && tid < 16) atomicAdd(&a.HSC[(tid >> 2) * n + (tid & 3)], a.hccbc[tid]);
-  if (blockIdx.x == 0 && tid < 4) atomicAdd(&a.bSC[tid], a.hccbc[16 + tid]);
+  if (blockIdx.x == 0 && wv == 2 && lane < 16) atomicAdd(&a.HSC[(lane >> 2) * n + (lane & 3)], a.hccbc[lane]);
+  if (blockIdx.x == 0 && wv == 2 && lane < 4) atomicAdd(&a.bSC[lane], a.hccbc[16 + lane]);
   HS_TRACE(a, 15);
 }
 

@@ -85,7 +85,8 @@ int hs_ba_set_marginal_prior(hs_ctx* ctx, const double* HM, const double* bM);
 
 /* device-event timing of the last hs_ba_optimize / hs_ba_iterate (ms, summed over the timed iterations):
    [0] linearize kernel, [1] accumulate + stitch (+ RCCL exchange), [2] solve + step kernel,
-   [3] number of event-timed iterations, [4] total GN loop wall (host clock), [5] iterations */
+   [3] number of event-timed iterations, [4] total GN loop wall (host clock), [5] iterations.
+   Env HS_EVENT_TIMING: 1 (default) times the linearize kernel only, 2 every phase, 0 none. */
 int hs_ba_get_timings(hs_ctx* ctx, double* out6);
 
 /* multi-GPU (point sharding): 128-byte RCCL unique id from rank 0, broadcast by the caller.
