@@ -24,9 +24,11 @@
 
 using namespace hs;
 
-namespace {
-thread_local std::string g_err;
+namespace hs {
+thread_local std::string g_err;  // hs_last_error(), shared by every entry point of the library
+}
 
+namespace {
 int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;

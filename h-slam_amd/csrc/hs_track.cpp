@@ -1,0 +1,453 @@
+// hs_track.cpp — C-ABI implementation of the CoarseTracker boundary (include/hs_track.h): tracker context,
+// device pyramids / reference points, makeCoarseDepthL0 launches, the hypothesis kernel and the exact
+// host replay of trackNewestCoarse's early abort and System::trackNewCoarse's try loop.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/hs_ba.h"
+#include "../../include/hs_track.h"
+#include "hs_track_kernels.h"
+
+namespace hs {
+extern thread_local std::string g_err;
+}
+
+namespace {
+int tfail(int code, const std::string& msg) {
+  hs::g_err = msg;
+  return code;
+}
+}  // namespace
+
+#define TS_HIP(x)                                                                                   \
+  do {                                                                                              \
+    hipError_t e_ = (x);                                                                            \
+    if (e_ != hipSuccess) return tfail(HS_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+#define TS_TRY(x)        \
+  do {                   \
+    int rc_ = (x);       \
+    if (rc_) return rc_; \
+  } while (0)
+
+struct hs_tracker {
+  hs_params P;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int W = 0, H = 0, nlev = 0;
+  int w[HS_TRK_MAXLEV], h[HS_TRK_MAXLEV];
+  float fx[HS_TRK_MAXLEV], fy[HS_TRK_MAXLEV], cx[HS_TRK_MAXLEV], cy[HS_TRK_MAXLEV], Ki[HS_TRK_MAXLEV][9];
+  float4* d_ref[HS_TRK_MAXLEV] = {nullptr};
+  float4* d_new[HS_TRK_MAXLEV] = {nullptr};
+  float *d_id[HS_TRK_MAXLEV] = {nullptr}, *d_ws[HS_TRK_MAXLEV] = {nullptr}, *d_bak[HS_TRK_MAXLEV] = {nullptr};
+  float *d_pu[HS_TRK_MAXLEV] = {nullptr}, *d_pv[HS_TRK_MAXLEV] = {nullptr}, *d_pid[HS_TRK_MAXLEV] = {nullptr},
+        *d_pcol[HS_TRK_MAXLEV] = {nullptr};
+  int* d_pcn = nullptr;
+  int *d_bcnt = nullptr, *d_boff = nullptr;
+  float *d_pts = nullptr;  // cu | cv | cid | hdi
+  int pts_cap = 0;
+  double* d_Tin = nullptr;
+  HsTryOut* d_out = nullptr;
+  HsTryOut* h_out = nullptr;
+  double* d_lmlog = nullptr;
+  int* d_lmlvl = nullptr;
+  int try_cap = 0, last_n_tries = 0;
+  float refExposure = 1, newExposure = 1;
+  double refAff[2] = {0, 0};
+  bool haveRef = false, haveFrame = false;
+  double last_ms = 0;
+};
+
+static int upload_pyr(hs_tracker* t, float4** dst, const float* const* pyr) {
+  for (int l = 0; l < t->nlev; l++) {
+    const size_t n = (size_t)t->w[l] * t->h[l];
+    std::vector<float4> tex(n);
+    const float* s = pyr[l];
+    if (!s) return tfail(HS_ERR_INVALID, "null pyramid level");
+    for (size_t i = 0; i < n; i++) tex[i] = make_float4(s[3 * i], s[3 * i + 1], s[3 * i + 2], 0.f);
+    TS_HIP(hipMemcpyAsync(dst[l], tex.data(), n * sizeof(float4), hipMemcpyHostToDevice, t->stream));
+    TS_HIP(hipStreamSynchronize(t->stream));  // tex is a temporary
+  }
+  return HS_OK;
+}
+
+static int ensure_tries(hs_tracker* t, int n) {
+  if (n <= t->try_cap) return HS_OK;
+  if (t->d_Tin) (void)hipFree(t->d_Tin);
+  if (t->d_out) (void)hipFree(t->d_out);
+  if (t->h_out) (void)hipHostFree(t->h_out);
+  if (t->d_lmlog) (void)hipFree(t->d_lmlog);
+  if (t->d_lmlvl) (void)hipFree(t->d_lmlvl);
+  t->d_Tin = nullptr; t->d_out = nullptr; t->h_out = nullptr; t->d_lmlog = nullptr; t->d_lmlvl = nullptr;
+  TS_HIP(hipMalloc((void**)&t->d_Tin, sizeof(double) * 9 * n));  // T (7) | aff (2)
+  TS_HIP(hipMalloc((void**)&t->d_out, sizeof(HsTryOut) * n));
+  TS_HIP(hipMalloc((void**)&t->d_lmlog, sizeof(double) * 3 * HS_TRK_MAXLOG * n));
+  TS_HIP(hipMalloc((void**)&t->d_lmlvl, sizeof(int) * HS_TRK_MAXLOG * n));
+  TS_HIP(hipHostMalloc((void**)&t->h_out, sizeof(HsTryOut) * n));
+  t->try_cap = n;
+  return HS_OK;
+}
+
+static HsTrackArgs make_args(hs_tracker* t) {
+  HsTrackArgs a;
+  std::memset(&a, 0, sizeof(a));
+  for (int l = 0; l < t->nlev; l++) {
+    HsTrkLevel& L = a.lv[l];
+    L.w = t->w[l]; L.h = t->h[l];
+    L.fx = t->fx[l]; L.fy = t->fy[l]; L.cx = t->cx[l]; L.cy = t->cy[l];
+    for (int q = 0; q < 9; q++) L.Ki[q] = t->Ki[l][q];
+    L.img = t->d_new[l];
+    L.pc_u = t->d_pu[l]; L.pc_v = t->d_pv[l]; L.pc_id = t->d_pid[l]; L.pc_col = t->d_pcol[l];
+    L.pc_n = t->d_pcn + l;
+  }
+  a.huberTH = t->P.huberTH;
+  a.coarseCutoffTH = t->P.coarseCutoffTH;
+  a.affineOptModeA = t->P.affineOptModeA;
+  a.affineOptModeB = t->P.affineOptModeB;
+  a.refExposure = t->refExposure;
+  a.newExposure = t->newExposure;
+  a.refAff[0] = t->refAff[0];
+  a.refAff[1] = t->refAff[1];
+  return a;
+}
+
+// n hypotheses (T | aff per row in h_in), run to completion without abort
+static int run_tries(hs_tracker* t, int n, const double* h_in, int coarsest, int single_pass, int lvl, float cutoff) {
+  TS_TRY(ensure_tries(t, n));
+  TS_HIP(hipMemcpyAsync(t->d_Tin, h_in, sizeof(double) * 9 * n, hipMemcpyHostToDevice, t->stream));
+  HsTrackArgs a = make_args(t);
+  a.coarsest = coarsest;
+  a.T_in = t->d_Tin;
+  a.aff_in = t->d_Tin + 7 * n;
+  a.out = t->d_out;
+  a.lm_log = t->d_lmlog;
+  a.lm_lvl = t->d_lmlvl;
+  a.single_pass = single_pass;
+  a.pass_lvl = lvl;
+  a.pass_cutoff = cutoff;
+  TS_HIP(hipEventRecord(t->e0, t->stream));
+  hipLaunchKernelGGL(hs_k_track, dim3(n), dim3(512), 0, t->stream, a);
+  TS_HIP(hipGetLastError());
+  TS_HIP(hipEventRecord(t->e1, t->stream));
+  TS_HIP(hipMemcpyAsync(t->h_out, t->d_out, sizeof(HsTryOut) * n, hipMemcpyDeviceToHost, t->stream));
+  TS_HIP(hipStreamSynchronize(t->stream));
+  float ms = 0;
+  TS_HIP(hipEventElapsedTime(&ms, t->e0, t->e1));
+  t->last_ms = ms;
+  t->last_n_tries = single_pass ? 0 : n;
+  return HS_OK;
+}
+
+// trackNewestCoarse's per-level abort (Src/CoarseTracker.cpp:647-651) replayed on a hypothesis' log:
+// returns the reference's return value and its lastResiduals / lastFlowIndicators at return
+static bool replay_abort(const HsTryOut& o, const double minRes[5], double lastRes[5], double flow[3]) {
+  for (int i = 0; i < 5; i++) lastRes[i] = NAN;
+  for (int i = 0; i < 3; i++) flow[i] = 1000;
+  for (int c = 0; c < o.n_checks; c++) {
+    const int l = o.check_lvl[c];
+    if (l < 5) lastRes[l] = o.check_res[c];
+    for (int i = 0; i < 3; i++) flow[i] = o.check_flow[c][i];
+    if (l < 5 && o.check_res[c] > 1.5 * minRes[l]) return false;
+  }
+  return o.ok != 0;
+}
+
+extern "C" {
+
+int hs_tracker_create(hs_tracker** out, const hs_params* params, int device_id, int width, int height,
+                      int n_levels, const float K4[4]) {
+  if (!out || !K4) return tfail(HS_ERR_INVALID, "null argument");
+  *out = nullptr;
+  if (n_levels < 1 || n_levels > HS_TRK_MAXLEV) return tfail(HS_ERR_INVALID, "n_levels out of range");
+  if (width < 16 || height < 16 || (width >> (n_levels - 1)) < 8 || (height >> (n_levels - 1)) < 8)
+    return tfail(HS_ERR_INVALID, "image too small for the pyramid");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return tfail(HS_ERR_HIP, "no HIP device");
+  if (device_id < 0 || device_id >= ndev) return tfail(HS_ERR_INVALID, "bad device id");
+  hs_tracker* t = new hs_tracker();
+  if (params) t->P = *params;
+  else hs_params_default(&t->P);
+  t->device = device_id;
+  t->W = width; t->H = height; t->nlev = n_levels;
+  // CoarseTracker::makeK (Src/CoarseTracker.cpp:73-101)
+  t->w[0] = width; t->h[0] = height;
+  t->fx[0] = K4[0]; t->fy[0] = K4[1]; t->cx[0] = K4[2]; t->cy[0] = K4[3];
+  for (int l = 1; l < n_levels; l++) {
+    t->w[l] = t->w[0] >> l;
+    t->h[l] = t->h[0] >> l;
+    t->fx[l] = t->fx[l - 1] * 0.5;
+    t->fy[l] = t->fy[l - 1] * 0.5;
+    t->cx[l] = (t->cx[0] + 0.5) / ((int)1 << l) - 0.5;
+    t->cy[l] = (t->cy[0] + 0.5) / ((int)1 << l) - 0.5;
+  }
+  for (int l = 0; l < n_levels; l++) {
+    const float K[9] = {t->fx[l], 0, t->cx[l], 0, t->fy[l], t->cy[l], 0, 0, 1};
+    hs::inv3f(K, t->Ki[l]);
+  }
+  if (hipSetDevice(device_id) != hipSuccess || hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&t->e0) != hipSuccess || hipEventCreate(&t->e1) != hipSuccess) {
+    delete t;
+    return tfail(HS_ERR_HIP, "stream / event creation failed");
+  }
+  int maxBlocks = 1;
+  for (int l = 0; l < n_levels; l++) {
+    const size_t n = (size_t)t->w[l] * t->h[l];
+    TS_HIP(hipMalloc((void**)&t->d_ref[l], n * sizeof(float4)));
+    TS_HIP(hipMalloc((void**)&t->d_new[l], n * sizeof(float4)));
+    TS_HIP(hipMalloc((void**)&t->d_id[l], n * sizeof(float)));
+    TS_HIP(hipMalloc((void**)&t->d_ws[l], n * sizeof(float)));
+    TS_HIP(hipMalloc((void**)&t->d_bak[l], n * sizeof(float)));
+    TS_HIP(hipMalloc((void**)&t->d_pu[l], n * sizeof(float)));
+    TS_HIP(hipMalloc((void**)&t->d_pv[l], n * sizeof(float)));
+    TS_HIP(hipMalloc((void**)&t->d_pid[l], n * sizeof(float)));
+    TS_HIP(hipMalloc((void**)&t->d_pcol[l], n * sizeof(float)));
+    maxBlocks = std::max(maxBlocks, (int)((n + 255) / 256));
+  }
+  TS_HIP(hipMalloc((void**)&t->d_pcn, sizeof(int) * HS_TRK_MAXLEV));
+  TS_HIP(hipMemset(t->d_pcn, 0, sizeof(int) * HS_TRK_MAXLEV));
+  TS_HIP(hipMalloc((void**)&t->d_bcnt, sizeof(int) * maxBlocks));
+  TS_HIP(hipMalloc((void**)&t->d_boff, sizeof(int) * maxBlocks));
+  *out = t;
+  return HS_OK;
+}
+
+void hs_tracker_destroy(hs_tracker* t) {
+  if (!t) return;
+  (void)hipSetDevice(t->device);
+  if (t->stream) (void)hipStreamSynchronize(t->stream);
+  for (int l = 0; l < HS_TRK_MAXLEV; l++) {
+    void* ps[] = {t->d_ref[l], t->d_new[l], t->d_id[l], t->d_ws[l], t->d_bak[l], t->d_pu[l], t->d_pv[l], t->d_pid[l],
+                  t->d_pcol[l]};
+    for (void* p : ps)
+      if (p) (void)hipFree(p);
+  }
+  void* ps[] = {t->d_pcn, t->d_bcnt, t->d_boff, t->d_pts, t->d_Tin, t->d_out, t->d_lmlog, t->d_lmlvl};
+  for (void* p : ps)
+    if (p) (void)hipFree(p);
+  if (t->h_out) (void)hipHostFree(t->h_out);
+  if (t->e0) (void)hipEventDestroy(t->e0);
+  if (t->e1) (void)hipEventDestroy(t->e1);
+  if (t->stream) (void)hipStreamDestroy(t->stream);
+  delete t;
+}
+
+int hs_tracker_set_ref(hs_tracker* t, const float* const* ref_pyr, float ab_exposure, const double aff_g2l[2], int n,
+                       const float* cu, const float* cv, const float* cid, const float* hdi) {
+  if (!t || !ref_pyr || !aff_g2l || n < 0 || (n > 0 && (!cu || !cv || !cid || !hdi)))
+    return tfail(HS_ERR_INVALID, "null argument");
+  TS_HIP(hipSetDevice(t->device));
+  TS_TRY(upload_pyr(t, t->d_ref, ref_pyr));
+  t->refExposure = ab_exposure;
+  t->refAff[0] = aff_g2l[0];
+  t->refAff[1] = aff_g2l[1];
+  if (n > t->pts_cap) {
+    if (t->d_pts) (void)hipFree(t->d_pts);
+    t->d_pts = nullptr;
+    TS_HIP(hipMalloc((void**)&t->d_pts, sizeof(float) * 4 * n));
+    t->pts_cap = n;
+  }
+  if (n > 0) {
+    std::vector<float> h((size_t)4 * n);
+    std::memcpy(h.data(), cu, 4 * n);
+    std::memcpy(h.data() + n, cv, 4 * n);
+    std::memcpy(h.data() + 2 * n, cid, 4 * n);
+    std::memcpy(h.data() + 3 * n, hdi, 4 * n);
+    TS_HIP(hipMemcpy(t->d_pts, h.data(), sizeof(float) * 4 * n, hipMemcpyHostToDevice));
+  }
+  // makeCoarseDepthL0
+  const size_t n0 = (size_t)t->w[0] * t->h[0];
+  TS_HIP(hipMemsetAsync(t->d_id[0], 0, n0 * sizeof(float), t->stream));
+  TS_HIP(hipMemsetAsync(t->d_ws[0], 0, n0 * sizeof(float), t->stream));
+  if (n > 0)
+    hipLaunchKernelGGL(hs_k_trk_scatter, dim3(1), dim3(64), 0, t->stream, n, t->d_pts, t->d_pts + n, t->d_pts + 2 * n,
+                       t->d_pts + 3 * n, t->w[0], t->h[0], t->d_id[0], t->d_ws[0]);
+  TS_HIP(hipGetLastError());
+  for (int l = 1; l < t->nlev; l++) {
+    const int np = t->w[l] * t->h[l];
+    hipLaunchKernelGGL(hs_k_trk_down, dim3((np + 255) / 256), dim3(256), 0, t->stream, t->w[l], t->h[l], t->w[l - 1],
+                       t->d_id[l - 1], t->d_ws[l - 1], t->d_id[l], t->d_ws[l]);
+    TS_HIP(hipGetLastError());
+  }
+  for (int l = 0; l < t->nlev; l++) {
+    const int np = t->w[l] * t->h[l];
+    TS_HIP(hipMemcpyAsync(t->d_bak[l], t->d_ws[l], np * sizeof(float), hipMemcpyDeviceToDevice, t->stream));
+    const int inner = np - 2 * t->w[l];
+    hipLaunchKernelGGL(hs_k_trk_dilate, dim3((inner + 255) / 256), dim3(256), 0, t->stream, t->w[l], t->h[l],
+                       l < 2 ? 1 : 0, t->d_bak[l], t->d_id[l], t->d_ws[l]);
+    TS_HIP(hipGetLastError());
+  }
+  for (int l = 0; l < t->nlev; l++) {
+    const int np = t->w[l] * t->h[l], nb = (np + 255) / 256;
+    hipLaunchKernelGGL(hs_k_trk_count, dim3(nb), dim3(256), 0, t->stream, t->w[l], t->h[l], t->d_id[l], t->d_ws[l],
+                       t->d_ref[l], t->d_bcnt);
+    hipLaunchKernelGGL(hs_k_trk_scan, dim3(1), dim3(1024), 0, t->stream, nb, t->d_bcnt, t->d_boff, t->d_pcn + l);
+    hipLaunchKernelGGL(hs_k_trk_compact, dim3(nb), dim3(256), 0, t->stream, t->w[l], t->h[l], t->d_id[l], t->d_ws[l],
+                       t->d_ref[l], t->d_boff, t->d_pu[l], t->d_pv[l], t->d_pid[l], t->d_pcol[l]);
+    TS_HIP(hipGetLastError());
+  }
+  TS_HIP(hipStreamSynchronize(t->stream));
+  t->haveRef = true;
+  return HS_OK;
+}
+
+int hs_tracker_get_ref(hs_tracker* t, int lvl, int* n, float* u, float* v, float* idepth, float* color) {
+  if (!t || !n) return tfail(HS_ERR_INVALID, "null argument");
+  if (lvl < 0 || lvl >= t->nlev) return tfail(HS_ERR_INVALID, "bad level");
+  if (!t->haveRef) return tfail(HS_ERR_STATE, "no reference set");
+  TS_HIP(hipSetDevice(t->device));
+  TS_HIP(hipStreamSynchronize(t->stream));
+  TS_HIP(hipMemcpy(n, t->d_pcn + lvl, sizeof(int), hipMemcpyDeviceToHost));
+  const size_t b = sizeof(float) * (size_t)*n;
+  if (*n > 0) {
+    if (u) TS_HIP(hipMemcpy(u, t->d_pu[lvl], b, hipMemcpyDeviceToHost));
+    if (v) TS_HIP(hipMemcpy(v, t->d_pv[lvl], b, hipMemcpyDeviceToHost));
+    if (idepth) TS_HIP(hipMemcpy(idepth, t->d_pid[lvl], b, hipMemcpyDeviceToHost));
+    if (color) TS_HIP(hipMemcpy(color, t->d_pcol[lvl], b, hipMemcpyDeviceToHost));
+  }
+  return HS_OK;
+}
+
+int hs_tracker_set_frame(hs_tracker* t, const float* const* new_pyr, float ab_exposure) {
+  if (!t || !new_pyr) return tfail(HS_ERR_INVALID, "null argument");
+  TS_HIP(hipSetDevice(t->device));
+  TS_TRY(upload_pyr(t, t->d_new, new_pyr));
+  t->newExposure = ab_exposure;
+  t->haveFrame = true;
+  return HS_OK;
+}
+
+int hs_tracker_calc_res(hs_tracker* t, int lvl, const double T7[7], const double aff[2], float cutoffTH, double res6[6],
+                        double H64[64], double b8[8], int* n_warped) {
+  if (!t || !T7 || !aff || !res6) return tfail(HS_ERR_INVALID, "null argument");
+  if (lvl < 0 || lvl >= t->nlev) return tfail(HS_ERR_INVALID, "bad level");
+  if (!t->haveRef || !t->haveFrame) return tfail(HS_ERR_STATE, "reference and frame must be set");
+  TS_HIP(hipSetDevice(t->device));
+  double in[9];
+  std::memcpy(in, T7, sizeof(double) * 7);
+  in[7] = aff[0];
+  in[8] = aff[1];
+  TS_TRY(run_tries(t, 1, in, lvl, 1, lvl, cutoffTH));
+  const HsTryOut& o = t->h_out[0];
+  std::memcpy(res6, o.res6, sizeof(double) * 6);
+  if (H64) std::memcpy(H64, o.H, sizeof(double) * 64);
+  if (b8) std::memcpy(b8, o.b, sizeof(double) * 8);
+  if (n_warped) *n_warped = o.n_warped;
+  return HS_OK;
+}
+
+int hs_tracker_track(hs_tracker* t, double T_inout[7], double aff_inout[2], int coarsest_lvl,
+                     const double minResForAbort[5], double lastResiduals[5], double flow[3], int* ok) {
+  if (!t || !T_inout || !aff_inout || !minResForAbort || !lastResiduals || !flow || !ok)
+    return tfail(HS_ERR_INVALID, "null argument");
+  if (coarsest_lvl < 0 || coarsest_lvl >= t->nlev || coarsest_lvl >= 5)
+    return tfail(HS_ERR_INVALID, "coarsest level must be < min(5, n_levels)");
+  if (!t->haveRef || !t->haveFrame) return tfail(HS_ERR_STATE, "reference and frame must be set");
+  TS_HIP(hipSetDevice(t->device));
+  double in[9];
+  std::memcpy(in, T_inout, sizeof(double) * 7);
+  in[7] = aff_inout[0];
+  in[8] = aff_inout[1];
+  TS_TRY(run_tries(t, 1, in, coarsest_lvl, 0, 0, 0.f));
+  const HsTryOut& o = t->h_out[0];
+  const bool good = replay_abort(o, minResForAbort, lastResiduals, flow);
+  *ok = good ? 1 : 0;
+  bool completed = true;  // the abort returns before "set!": the outputs keep their inputs
+  for (int c = 0; c < o.n_checks; c++)
+    if (o.check_lvl[c] < 5 && o.check_res[c] > 1.5 * minResForAbort[o.check_lvl[c]]) completed = false;
+  if (completed) {
+    std::memcpy(T_inout, o.T, sizeof(double) * 7);
+    aff_inout[0] = o.aff[0];
+    aff_inout[1] = o.aff[1];
+  }
+  return HS_OK;
+}
+
+int hs_tracker_track_tries(hs_tracker* t, int n_tries, const double* tries7, const double aff_last[2],
+                           const double lastCoarseRMSE[5], float reTrackThreshold, double T_out[7], double aff_out[2],
+                           double achievedRes[5], double flowVecs[3], int* have_one_good, int* n_tried) {
+  if (!t || n_tries < 1 || !tries7 || !aff_last || !lastCoarseRMSE || !T_out || !aff_out || !achievedRes || !flowVecs ||
+      !have_one_good || !n_tried)
+    return tfail(HS_ERR_INVALID, "null argument");
+  if (!t->haveRef || !t->haveFrame) return tfail(HS_ERR_STATE, "reference and frame must be set");
+  TS_HIP(hipSetDevice(t->device));
+  const int coarsest = std::min(t->nlev - 1, 4);
+  std::vector<double> in((size_t)9 * n_tries);
+  std::memcpy(in.data(), tries7, sizeof(double) * 7 * n_tries);
+  for (int i = 0; i < n_tries; i++) {
+    in[7 * n_tries + 2 * i] = aff_last[0];
+    in[7 * n_tries + 2 * i + 1] = aff_last[1];
+  }
+  TS_TRY(run_tries(t, n_tries, in.data(), coarsest, 0, 0, 0.f));
+  // System::trackNewCoarse try loop (Src/System.cpp:413-481), replayed in the reference's order
+  double ach[5];
+  for (int k = 0; k < 5; k++) ach[k] = NAN;
+  bool haveOneGood = false;
+  double flow[3] = {100, 100, 100};
+  int best = -1, tried = 0;
+  for (int i = 0; i < n_tries; i++) {
+    const HsTryOut& o = t->h_out[i];
+    double lastRes[5], lf[3];
+    const bool good = replay_abort(o, ach, lastRes, lf);
+    tried++;
+    if (good && std::isfinite((float)lastRes[0]) && !(lastRes[0] >= ach[0])) {
+      for (int k = 0; k < 3; k++) flow[k] = lf[k];
+      best = i;
+      haveOneGood = true;
+    }
+    if (haveOneGood)
+      for (int k = 0; k < 5; k++)
+        if (!std::isfinite((float)ach[k]) || ach[k] > lastRes[k]) ach[k] = lastRes[k];
+    if (haveOneGood && ach[0] < lastCoarseRMSE[0] * reTrackThreshold) break;
+  }
+  if (haveOneGood) {
+    std::memcpy(T_out, t->h_out[best].T, sizeof(double) * 7);
+    aff_out[0] = t->h_out[best].aff[0];
+    aff_out[1] = t->h_out[best].aff[1];
+  } else {
+    flow[0] = flow[1] = flow[2] = 0;
+    std::memcpy(T_out, tries7, sizeof(double) * 7);
+    aff_out[0] = aff_last[0];
+    aff_out[1] = aff_last[1];
+  }
+  for (int k = 0; k < 5; k++) achievedRes[k] = ach[k];
+  for (int k = 0; k < 3; k++) flowVecs[k] = flow[k];
+  *have_one_good = haveOneGood ? 1 : 0;
+  *n_tried = tried;
+  return HS_OK;
+}
+
+int hs_tracker_get_lm_log(hs_tracker* t, int try_idx, int cap, int* n, int* lvl, double* new_ratio,
+                          double* old_ratio, double* inc_norm) {
+  if (!t || !n) return tfail(HS_ERR_INVALID, "null argument");
+  if (try_idx < 0 || try_idx >= t->last_n_tries) return tfail(HS_ERR_INVALID, "no such hypothesis in the last call");
+  TS_HIP(hipSetDevice(t->device));
+  const int iters = t->h_out[try_idx].iters;
+  *n = iters;
+  const int m = std::min(std::min(iters, cap), HS_TRK_MAXLOG);
+  if (m > 0) {
+    std::vector<double> lg((size_t)3 * m);
+    TS_HIP(hipMemcpy(lg.data(), t->d_lmlog + (size_t)try_idx * HS_TRK_MAXLOG * 3, sizeof(double) * 3 * m,
+                     hipMemcpyDeviceToHost));
+    if (lvl)
+      TS_HIP(hipMemcpy(lvl, t->d_lmlvl + (size_t)try_idx * HS_TRK_MAXLOG, sizeof(int) * m, hipMemcpyDeviceToHost));
+    for (int i = 0; i < m; i++) {
+      if (new_ratio) new_ratio[i] = lg[3 * i];
+      if (old_ratio) old_ratio[i] = lg[3 * i + 1];
+      if (inc_norm) inc_norm[i] = lg[3 * i + 2];
+    }
+  }
+  return HS_OK;
+}
+
+int hs_tracker_last_ms(hs_tracker* t, double* ms) {
+  if (!t || !ms) return tfail(HS_ERR_INVALID, "null argument");
+  *ms = t->last_ms;
+  return HS_OK;
+}
+
+}  // extern "C"

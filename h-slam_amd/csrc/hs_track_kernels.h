@@ -1,0 +1,64 @@
+// hs_track_kernels.h — argument blocks of the CoarseTracker kernels (hs_track_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/hs_track.h"
+#include "hs_host_math.h"
+
+#define HS_TRK_MAXCHECK 12
+#define HS_TRK_MAXLOG 256  // LM iterations logged per hypothesis (10+20+3*50 + one repeated level <= 230)
+
+constexpr double hs_trk_scale_rot = 1.0, hs_trk_scale_trans = 0.5, hs_trk_scale_a = 10.0, hs_trk_scale_b = 1000.0;
+
+// one pyramid level: CoarseTracker's K / Ki (makeK) and the device images / reference points
+struct HsTrkLevel {
+  int w, h;
+  float fx, fy, cx, cy;
+  float Ki[9];
+  const float4* img;    // new frame (I, dx, dy, 0)
+  const float* pc_u;
+  const float* pc_v;
+  const float* pc_id;
+  const float* pc_col;
+  const int* pc_n;
+};
+
+// per hypothesis: the outcome without abort + the per-level residual log for the caller's replay
+struct HsTryOut {
+  double T[7];
+  double aff[2];
+  int ok, n_checks, iters, n_warped;
+  int check_lvl[HS_TRK_MAXCHECK];
+  double check_res[HS_TRK_MAXCHECK];
+  double check_flow[HS_TRK_MAXCHECK][3];
+  double res6[6];
+  double H[64];
+  double b[8];
+};
+
+struct HsTrackArgs {
+  HsTrkLevel lv[HS_TRK_MAXLEV];
+  int coarsest;
+  float huberTH, coarseCutoffTH, affineOptModeA, affineOptModeB;
+  float refExposure, newExposure;
+  double refAff[2];
+  const double* T_in;   // [n][7]
+  const double* aff_in; // [n][2]
+  HsTryOut* out;        // [n]
+  int single_pass, pass_lvl;
+  float pass_cutoff;
+  double* lm_log;       // [n][HS_TRK_MAXLOG][3]: resNew/N, resOld/N (accept test), |inc| (break test) per LM iteration
+  int* lm_lvl;          // [n][HS_TRK_MAXLOG]
+  long long* trace;
+};
+
+__global__ void hs_k_track(HsTrackArgs a);
+__global__ void hs_k_trk_scatter(int n, const float* cu, const float* cv, const float* cid, const float* hdi, int w,
+                                 int h, float* idepth0, float* wsum0);
+__global__ void hs_k_trk_down(int wl, int hl, int wlm1, const float* idm, const float* wsm, float* idl, float* wsl);
+__global__ void hs_k_trk_dilate(int wl, int hl, int diag, const float* bak, float* id, float* ws);
+__global__ void hs_k_trk_count(int wl, int hl, const float* id, const float* ws, const float4* ref, int* blockCount);
+__global__ void hs_k_trk_scan(int nb, const int* blockCount, int* blockOff, int* pc_n);
+__global__ void hs_k_trk_compact(int wl, int hl, const float* id, const float* ws, const float4* ref,
+                                 const int* blockOff, float* pu, float* pv, float* pid, float* pcol);

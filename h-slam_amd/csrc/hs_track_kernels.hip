@@ -1,0 +1,586 @@
+// hs_track_kernels.hip — gfx950 kernels of H-SLAM's CoarseTracker.
+//
+//   makeCoarseDepthL0 (Src/CoarseTracker.cpp:105-263), once per keyframe:
+//     hs_k_trk_scatter      point -> level-0 idepth / weight sums, in the reference's point order (1 thread:
+//                           colliding points add in order, so the sums are the reference's)
+//     hs_k_trk_down         2x2 sums up the pyramid
+//     hs_k_trk_dilate       one dilation pass (diagonal neighbours on levels 0-1, 4-neighbours above)
+//     hs_k_trk_count / hs_k_trk_scan / hs_k_trk_compact
+//                           normalisation + order-preserving (raster order) compaction into pc_* arrays
+//   trackNewestCoarse (Src/CoarseTracker.cpp:506-683), per frame:
+//     hs_k_track            one workgroup (1024 threads) runs the whole coarse-to-fine LM loop of one
+//                           pose hypothesis: calcRes (Src/CoarseTracker.cpp:329-485) and the calcGSSSE
+//                           normal equations (:267-324) fused in one pass over the reference points,
+//                           block reductions, the 8x8 fp64 LDLT step (Eigen pivot order) and SE3 update.
+//                           A grid of N workgroups runs N hypotheses of System::trackNewCoarse at once.
+// Per-point arithmetic follows the reference's fp32 operation order (fp contraction off), so the
+// in-bounds / saturation / warped-set decisions of a pass are bit-identical; the energy and Hessian
+// sums are fixed-order parallel reductions (the reference sums in 4 SSE lanes).
+#pragma clang fp contract(off)
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+
+#include "hs_track_kernels.h"
+
+namespace {
+
+constexpr int TRK_NT = 512;
+constexpr int TRK_NACC = 45;          // upper triangle of the 9x9 [J | r] normal equations
+constexpr int TRK_NRED = TRK_NACC + 4 + 3;  // + E, flowT, flowRT, flowNum | numE, numSat, numWarped
+
+__device__ __forceinline__ float3 interp33(const float4* __restrict__ img, float x, float y, int w) {
+  int ix = (int)x, iy = (int)y;
+  float dx = x - ix, dy = y - iy, dxdy = dx * dy;
+  const float4* bp = img + ix + iy * w;
+  const float4 p00 = bp[0], p10 = bp[1], p01 = bp[w], p11 = bp[w + 1];
+  const float w11 = dxdy, w01 = dy - dxdy, w10 = dx - dxdy, w00 = 1 - dx - dy + dxdy;
+  float3 r;
+  r.x = w11 * p11.x + w01 * p01.x + w10 * p10.x + w00 * p00.x;
+  r.y = w11 * p11.y + w01 * p01.y + w10 * p10.y + w00 * p00.y;
+  r.z = w11 * p11.z + w01 * p01.z + w10 * p10.z + w00 * p00.z;
+  return r;
+}
+
+#define HS_TRACE(A, slot)                                                                          \
+  do {                                                                                             \
+    if ((A).trace && threadIdx.x == 0) (A).trace[(size_t)blockIdx.x * 16 + (slot)] = wall_clock64(); \
+  } while (0)
+
+// Eigen LDLT (diagonal pivoting) solve of an 8x8 system by one thread, fully unrolled so every array is
+// register-resident: the pivot order is the swap sequence on the original diagonal (left-looking LDLT).
+__device__ __forceinline__ void ldlt8_solve(const double* __restrict__ A, const double* __restrict__ rhs, double* __restrict__ x) {
+  double dg[8];
+  int pm[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    dg[i] = fabs(A[i * 8 + i]);
+    pm[i] = i;
+  }
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    double best = dg[k];
+    int bi = k;
+#pragma unroll
+    for (int j = k + 1; j < 8; j++)
+      if (dg[j] > best) { best = dg[j]; bi = j; }
+#pragma unroll
+    for (int j = k + 1; j < 8; j++)
+      if (j == bi) {
+        const double td = dg[k]; dg[k] = dg[j]; dg[j] = td;
+        const int tp = pm[k]; pm[k] = pm[j]; pm[j] = tp;
+      }
+  }
+  double M[8][8], y[8], D[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) M[i][j] = A[pm[i] * 8 + pm[j]];
+    y[i] = rhs[pm[i]];
+  }
+  // left-looking as Eigen's ldlt_inplace::unblocked: column k is updated with the finished columns j < k
+  // (temp_j = D_j L_kj), then scaled by the pivot
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    double temp[8];
+#pragma unroll
+    for (int j = 0; j < k; j++) temp[j] = D[j] * M[k][j];
+    double s = 0;
+#pragma unroll
+    for (int j = 0; j < k; j++) s += M[k][j] * temp[j];
+    M[k][k] -= s;
+#pragma unroll
+    for (int i = k + 1; i < 8; i++) {
+      double t = 0;
+#pragma unroll
+      for (int j = 0; j < k; j++) t += M[i][j] * temp[j];
+      M[i][k] -= t;
+    }
+    const double d = M[k][k];
+    D[k] = d;
+    if (fabs(d) > DBL_MIN) {
+#pragma unroll
+      for (int i = k + 1; i < 8; i++) M[i][k] /= d;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+#pragma unroll
+    for (int k = 0; k < i; k++) y[i] = y[i] - M[i][k] * y[k];
+#pragma unroll
+  for (int i = 0; i < 8; i++) y[i] = fabs(D[i]) > DBL_MIN ? y[i] / D[i] : 0.0;
+#pragma unroll
+  for (int i = 7; i >= 0; i--)
+#pragma unroll
+    for (int j = i + 1; j < 8; j++) y[i] = y[i] - M[j][i] * y[j];
+#pragma unroll
+  for (int i = 0; i < 8; i++) x[pm[i]] = y[i];
+}
+
+struct TrkShared {
+  // pass inputs (thread 0 writes)
+  float RKi[9], t[3], affLL[2], a_gs, b0, cutoff, maxEnergy;
+  int lvl;
+  // pass outputs
+  double red[TRK_NT / 64][TRK_NRED];
+  double res[6];
+  double H[64], b[8];
+  int nWarped;
+  // LM state
+  double T[7], Tn[7];
+  double aff[2], affn[2];
+  double Hs[64], bs[8], resOld[6], Hl[64];
+  double incNorm;
+  float lambda, cutoffRep;
+  int brk, accept;
+};
+
+// calcRes + calcGSSSE at S.RKi / S.t / S.affLL for level S.lvl; results in S.res / S.H / S.b / S.nWarped
+__device__ void trk_pass(const HsTrackArgs& a, TrkShared& S) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int lvl = S.lvl;
+  const HsTrkLevel& L = a.lv[lvl];
+  const int n = *L.pc_n, wl = L.w, hl = L.h;
+  const float fxl = L.fx, fyl = L.fy, cxl = L.cx, cyl = L.cy;
+  float RKi[9], Ki[9];
+#pragma unroll
+  for (int q = 0; q < 9; q++) { RKi[q] = S.RKi[q]; Ki[q] = L.Ki[q]; }
+  const float t0 = S.t[0], t1 = S.t[1], t2 = S.t[2];
+  const float aff0 = S.affLL[0], aff1 = S.affLL[1], ags = S.a_gs, b0 = S.b0;
+  const float cutoff = S.cutoff, maxEnergy = S.maxEnergy, huberTH = a.huberTH;
+  float E = 0.f, sT = 0.f, sRT = 0.f, sN = 0.f;
+  int nE = 0, nSat = 0, nW = 0;
+  float acc[TRK_NACC];
+#pragma unroll
+  for (int q = 0; q < TRK_NACC; q++) acc[q] = 0.f;
+  for (int i = tid; i < n; i += TRK_NT) {
+    const float id = L.pc_id[i], x = L.pc_u[i], y = L.pc_v[i];
+    float pt0 = RKi[0] * x + RKi[1] * y + RKi[2] * 1.f;
+    float pt1 = RKi[3] * x + RKi[4] * y + RKi[5] * 1.f;
+    float pt2 = RKi[6] * x + RKi[7] * y + RKi[8] * 1.f;
+    const float ra0 = pt0, ra1 = pt1, ra2 = pt2;
+    pt0 = pt0 + t0 * id;
+    pt1 = pt1 + t1 * id;
+    pt2 = pt2 + t2 * id;
+    const float u = pt0 / pt2, v = pt1 / pt2;
+    const float Ku = fxl * u + cxl, Kv = fyl * v + cyl;
+    const float new_idepth = id / pt2;
+    if (lvl == 0 && i % 32 == 0) {
+      const float k0 = Ki[0] * x + Ki[1] * y + Ki[2] * 1.f;
+      const float k1 = Ki[3] * x + Ki[4] * y + Ki[5] * 1.f;
+      const float k2 = Ki[6] * x + Ki[7] * y + Ki[8] * 1.f;
+      const float pT0 = k0 + t0 * id, pT1 = k1 + t1 * id, pT2 = k2 + t2 * id;
+      const float pS0 = k0 - t0 * id, pS1 = k1 - t1 * id, pS2 = k2 - t2 * id;
+      const float p30 = ra0 - t0 * id, p31 = ra1 - t1 * id, p32 = ra2 - t2 * id;
+      const float uT = pT0 / pT2, vT = pT1 / pT2;
+      const float KuT = fxl * uT + cxl, KvT = fyl * vT + cyl;
+      const float uT2 = pS0 / pS2, vT2 = pS1 / pS2;
+      const float KuT2 = fxl * uT2 + cxl, KvT2 = fyl * vT2 + cyl;
+      const float u3 = p30 / p32, v3 = p31 / p32;
+      const float Ku3 = fxl * u3 + cxl, Kv3 = fyl * v3 + cyl;
+      float s = (KuT - x) * (KuT - x) + (KvT - y) * (KvT - y);
+      sT += s;
+      s = (KuT2 - x) * (KuT2 - x) + (KvT2 - y) * (KvT2 - y);
+      sT += s;
+      s = (Ku - x) * (Ku - x) + (Kv - y) * (Kv - y);
+      sRT += s;
+      s = (Ku3 - x) * (Ku3 - x) + (Kv3 - y) * (Kv3 - y);
+      sRT += s;
+      sN += 2;
+    }
+    if (!(Ku > 2 && Kv > 2 && Ku < wl - 3 && Kv < hl - 3 && new_idepth > 0)) continue;
+    const float refColor = L.pc_col[i];
+    const float3 hit = interp33(L.img, Ku, Kv, wl);
+    if (!isfinite(hit.x)) continue;
+    const float residual = hit.x - (float)(aff0 * refColor + aff1);
+    const float hw = fabsf(residual) < huberTH ? 1 : huberTH / fabsf(residual);
+    if (fabsf(residual) > cutoff) {
+      E += maxEnergy;
+      nE++;
+      nSat++;
+    } else {
+      E += hw * residual * residual * (2 - hw);
+      nE++;
+      nW++;
+      // calcGSSSE Jacobian of this warped point (Src/CoarseTracker.cpp:282-306)
+      const float dx = hit.y * fxl, dy = hit.z * fyl;
+      float J[9];
+      J[0] = new_idepth * dx;
+      J[1] = new_idepth * dy;
+      J[2] = 0.f - new_idepth * (u * dx + v * dy);
+      J[3] = 0.f - ((u * v) * dx + dy * (1.f + v * v));
+      J[4] = (u * v) * dy + dx * (1.f + u * u);
+      J[5] = u * dy - v * dx;
+      J[6] = ags * (b0 - refColor);
+      J[7] = -1.f;
+      J[8] = residual;
+      int q = 0;
+#pragma unroll
+      for (int r = 0; r < 9; r++) {
+        const float Jw = J[r] * hw;
+#pragma unroll
+        for (int c = r; c < 9; c++) acc[q++] += Jw * J[c];
+      }
+    }
+  }
+  // wave reductions (fixed xor tree), then the waves in order in fp64
+  float vals[TRK_NRED];
+#pragma unroll
+  for (int q = 0; q < TRK_NACC; q++) vals[q] = acc[q];
+  vals[TRK_NACC + 0] = E;
+  vals[TRK_NACC + 1] = sT;
+  vals[TRK_NACC + 2] = sRT;
+  vals[TRK_NACC + 3] = sN;
+  vals[TRK_NACC + 4] = __int_as_float(nE);
+  vals[TRK_NACC + 5] = __int_as_float(nSat);
+  vals[TRK_NACC + 6] = __int_as_float(nW);
+#pragma unroll
+  for (int q = 0; q < TRK_NRED; q++) {
+    if (q < TRK_NACC + 4) {
+      float v = vals[q];
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+      vals[q] = v;
+    } else {
+      int v = __float_as_int(vals[q]);
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+      vals[q] = __int_as_float(v);
+    }
+  }
+  if (lane == 0)
+#pragma unroll
+    for (int q = 0; q < TRK_NRED; q++)
+      S.red[wv][q] = q < TRK_NACC + 4 ? (double)vals[q] : (double)__float_as_int(vals[q]);
+  __syncthreads();
+  if (tid < TRK_NRED) {
+    double s = 0.0;
+    for (int w = 0; w < TRK_NT / 64; w++) s += S.red[w][tid];
+    S.red[0][tid] = s;  // wave 0's slot is only read by this thread before the sum
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const double* R = S.red[0];
+    const float Ef = (float)R[TRK_NACC + 0];
+    const int numE = (int)R[TRK_NACC + 4], numSat = (int)R[TRK_NACC + 5], numW = (int)R[TRK_NACC + 6];
+    const float fT = (float)R[TRK_NACC + 1], fRT = (float)R[TRK_NACC + 2], fN = (float)R[TRK_NACC + 3];
+    S.res[0] = Ef;
+    S.res[1] = numE;
+    S.res[2] = fT / (fN + 0.1);
+    S.res[3] = 0;
+    S.res[4] = fRT / (fN + 0.1);
+    S.res[5] = numSat / (float)numE;
+    const int npad = (numW + 3) & ~3;  // buf_warped_n includes the zero padding (quirk kept)
+    S.nWarped = npad;
+    const double inv = (double)(1.0f / npad);
+    const double sc[8] = {hs_trk_scale_rot, hs_trk_scale_rot, hs_trk_scale_rot, hs_trk_scale_trans,
+                          hs_trk_scale_trans, hs_trk_scale_trans, hs_trk_scale_a, hs_trk_scale_b};
+    int q = 0;
+#pragma unroll
+    for (int r = 0; r < 9; r++)
+#pragma unroll
+      for (int c = r; c < 9; c++) {
+        const double v = (double)(float)R[q++];
+        if (r < 8 && c < 8) {
+          S.H[r * 8 + c] = ((v * inv) * sc[c]) * sc[r];
+          S.H[c * 8 + r] = ((v * inv) * sc[r]) * sc[c];
+        }
+        if (c == 8) S.b[r] = (v * inv) * sc[r];
+      }
+  }
+  __syncthreads();
+}
+
+// thread 0: the pass inputs for state (T, aff) at level lvl
+__device__ void trk_setup(const HsTrackArgs& a, TrkShared& S, const double T7[7], const double aff[2], int lvl,
+                          float cutoff) {
+  const hs::SE3 T = hs::SE3::fromData(T7);
+  double Rd[9];
+  T.rotationMatrix(Rd);
+  float R[9];
+  for (int q = 0; q < 9; q++) R[q] = (float)Rd[q];
+  const float* Ki = a.lv[lvl].Ki;
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++) S.RKi[r * 3 + c] = R[r * 3 + 0] * Ki[0 * 3 + c] + R[r * 3 + 1] * Ki[1 * 3 + c] + R[r * 3 + 2] * Ki[2 * 3 + c];
+  for (int q = 0; q < 3; q++) S.t[q] = (float)T.t[q];
+  double rel[2];
+  hs::fromToVecExposure(a.refExposure, a.newExposure, a.refAff[0], a.refAff[1], aff[0], aff[1], rel);
+  S.affLL[0] = (float)rel[0];
+  S.affLL[1] = (float)rel[1];
+  S.a_gs = (float)rel[0];
+  S.b0 = (float)a.refAff[1];
+  S.cutoff = cutoff;
+  S.maxEnergy = 2 * a.huberTH * cutoff - a.huberTH * a.huberTH;
+  S.lvl = lvl;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
+  __shared__ TrkShared S;
+  const int tid = threadIdx.x;
+  const int h = blockIdx.x;  // hypothesis
+  HsTryOut& out = a.out[h];
+  HS_TRACE(a, 0);
+  if (a.single_pass) {  // hs_tracker_calc_res
+    if (tid == 0) trk_setup(a, S, a.T_in + 7 * h, a.aff_in + 2 * h, a.pass_lvl, a.pass_cutoff);
+    __syncthreads();
+    trk_pass(a, S);
+    if (tid == 0) {
+      for (int q = 0; q < 6; q++) out.res6[q] = S.res[q];
+      for (int q = 0; q < 64; q++) out.H[q] = S.H[q];
+      for (int q = 0; q < 8; q++) out.b[q] = S.b[q];
+      out.n_warped = S.nWarped;
+    }
+    return;
+  }
+  const int maxIterations[5] = {10, 20, 50, 50, 50};
+  const float lambdaExtrapolationLimit = 0.001f;
+  if (tid == 0) {
+    for (int q = 0; q < 7; q++) S.T[q] = a.T_in[7 * h + q];
+    S.aff[0] = a.aff_in[2 * h + 0];
+    S.aff[1] = a.aff_in[2 * h + 1];
+    out.n_checks = 0;
+    out.iters = 0;
+  }
+  __syncthreads();
+  bool haveRepeated = false;
+  for (int lvl = a.coarsest; lvl >= 0; lvl--) {
+    if (tid == 0) {
+      S.cutoffRep = 1;
+      trk_setup(a, S, S.T, S.aff, lvl, a.coarseCutoffTH * S.cutoffRep);
+    }
+    __syncthreads();
+    trk_pass(a, S);
+    while (S.res[5] > 0.6 && S.cutoffRep < 50) {  // uniform: S.res / S.cutoffRep are shared
+      __syncthreads();
+      if (tid == 0) {
+        S.cutoffRep *= 2;
+        trk_setup(a, S, S.T, S.aff, lvl, a.coarseCutoffTH * S.cutoffRep);
+      }
+      __syncthreads();
+      trk_pass(a, S);
+    }
+    if (tid == 0) {  // calcGSSSE of the last calcRes; lambda = 0.01
+      for (int q = 0; q < 64; q++) S.Hs[q] = S.H[q];
+      for (int q = 0; q < 8; q++) S.bs[q] = S.b[q];
+      for (int q = 0; q < 6; q++) S.resOld[q] = S.res[q];
+      S.lambda = 0.01f;
+    }
+    __syncthreads();
+    for (int iteration = 0; iteration < maxIterations[lvl]; iteration++) {
+      __syncthreads();  // every thread has read S.brk of the previous iteration
+      if (tid == 0) {
+        out.iters++;
+        // Hl = H with the diagonal scaled by (1 + lambda), in LDS (the solver reads it with pivoted indices)
+        double* Hl = S.Hl;
+        double mb[8], inc[8];
+        for (int q = 0; q < 64; q++) Hl[q] = S.Hs[q];
+#pragma unroll
+        for (int i = 0; i < 8; i++) Hl[i * 8 + i] *= (1 + S.lambda);
+#pragma unroll
+        for (int i = 0; i < 8; i++) mb[i] = -S.bs[i];
+        ldlt8_solve(Hl, mb, inc);
+        float extrapFac = 1;
+        if (S.lambda < lambdaExtrapolationLimit) extrapFac = sqrtf(sqrtf(lambdaExtrapolationLimit / S.lambda));
+        for (int i = 0; i < 8; i++) inc[i] *= extrapFac;
+        double incScaled[8];
+        for (int i = 0; i < 8; i++) incScaled[i] = inc[i];
+        for (int i = 0; i < 3; i++) incScaled[i] *= hs_trk_scale_rot;
+        for (int i = 3; i < 6; i++) incScaled[i] *= hs_trk_scale_trans;
+        incScaled[6] *= hs_trk_scale_a;
+        incScaled[7] *= hs_trk_scale_b;
+        double ssum = 0;
+        for (int i = 0; i < 8; i++) ssum += incScaled[i];
+        if (!isfinite(ssum))
+          for (int i = 0; i < 8; i++) incScaled[i] = 0;
+        const hs::SE3 nw = hs::SE3::exp(incScaled) * hs::SE3::fromData(S.T);
+        nw.toData(S.Tn);
+        S.affn[0] = S.aff[0] + incScaled[6];
+        S.affn[1] = S.aff[1] + incScaled[7];
+        double nn = 0;
+        for (int i = 0; i < 8; i++) nn += inc[i] * inc[i];
+        S.incNorm = sqrt(nn);
+        S.brk = !(S.incNorm > 1e-3);
+        trk_setup(a, S, S.Tn, S.affn, lvl, a.coarseCutoffTH * S.cutoffRep);
+      }
+      __syncthreads();
+      trk_pass(a, S);
+      if (tid == 0) {
+        const bool accept = (S.res[0] / S.res[1]) < (S.resOld[0] / S.resOld[1]);
+        const int it = out.iters - 1;
+        if (it < HS_TRK_MAXLOG) {
+          a.lm_log[((size_t)h * HS_TRK_MAXLOG + it) * 3 + 0] = S.res[0] / S.res[1];
+          a.lm_log[((size_t)h * HS_TRK_MAXLOG + it) * 3 + 1] = S.resOld[0] / S.resOld[1];
+          a.lm_log[((size_t)h * HS_TRK_MAXLOG + it) * 3 + 2] = S.incNorm;
+          a.lm_lvl[(size_t)h * HS_TRK_MAXLOG + it] = lvl;
+        }
+        if (accept) {
+          for (int q = 0; q < 64; q++) S.Hs[q] = S.H[q];
+          for (int q = 0; q < 8; q++) S.bs[q] = S.b[q];
+          for (int q = 0; q < 6; q++) S.resOld[q] = S.res[q];
+          S.aff[0] = S.affn[0];
+          S.aff[1] = S.affn[1];
+          for (int q = 0; q < 7; q++) S.T[q] = S.Tn[q];
+          S.lambda *= 0.5;
+        } else {
+          S.lambda *= 4;
+          if (S.lambda < lambdaExtrapolationLimit) S.lambda = lambdaExtrapolationLimit;
+        }
+      }
+      __syncthreads();
+      if (S.brk) break;
+    }
+    if (tid == 0) {  // lastResiduals[lvl] / lastFlowIndicators: logged for the caller's abort replay
+      const int c = out.n_checks;
+      if (c < HS_TRK_MAXCHECK) {
+        out.check_lvl[c] = lvl;
+        out.check_res[c] = sqrtf((float)(S.resOld[0] / S.resOld[1]));
+        out.check_flow[c][0] = S.resOld[2];
+        out.check_flow[c][1] = S.resOld[3];
+        out.check_flow[c][2] = S.resOld[4];
+        out.n_checks = c + 1;
+      }
+    }
+    const bool rep = S.cutoffRep > 1 && !haveRepeated;
+    __syncthreads();
+    if (rep) {  // REPEAT LEVEL
+      lvl++;
+      haveRepeated = true;
+    }
+  }
+  if (tid == 0) {
+    for (int q = 0; q < 7; q++) out.T[q] = S.T[q];
+    out.aff[0] = S.aff[0];
+    out.aff[1] = S.aff[1];
+    bool ok = true;
+    if ((a.affineOptModeA != 0 && (fabsf((float)S.aff[0]) > 1.2f)) ||
+        (a.affineOptModeB != 0 && (fabsf((float)S.aff[1]) > 200)))
+      ok = false;
+    double rel[2];
+    hs::fromToVecExposure(a.refExposure, a.newExposure, a.refAff[0], a.refAff[1], S.aff[0], S.aff[1], rel);
+    if ((a.affineOptModeA == 0 && (fabsf(logf((float)rel[0])) > 1.5f)) ||
+        (a.affineOptModeB == 0 && (fabsf((float)rel[1]) > 200)))
+      ok = false;
+    if (a.affineOptModeA < 0) out.aff[0] = 0;
+    if (a.affineOptModeB < 0) out.aff[1] = 0;
+    out.ok = ok ? 1 : 0;
+  }
+  HS_TRACE(a, 15);
+}
+
+// ---------------------------------------------------------------- makeCoarseDepthL0
+__global__ void hs_k_trk_scatter(int n, const float* cu, const float* cv, const float* cid, const float* hdi, int w,
+                                 int h, float* idepth0, float* wsum0) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  for (int i = 0; i < n; i++) {  // the reference's order: colliding points add in sequence
+    const int u = (int)(cu[i] + 0.5f);
+    const int v = (int)(cv[i] + 0.5f);
+    if (u < 0 || v < 0 || u >= w || v >= h) continue;  // the reference assumes in-image centres
+    const float new_idepth = cid[i];
+    const float weight = sqrtf(1e-3 / (hdi[i] + 1e-12));
+    idepth0[u + w * v] += new_idepth * weight;
+    wsum0[u + w * v] += weight;
+  }
+}
+
+__global__ void hs_k_trk_down(int wl, int hl, int wlm1, const float* idm, const float* wsm, float* idl, float* wsl) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= wl * hl) return;
+  const int y = i / wl, x = i - y * wl;
+  const int b = 2 * x + 2 * y * wlm1;
+  idl[i] = idm[b] + idm[b + 1] + idm[b + wlm1] + idm[b + wlm1 + 1];
+  wsl[i] = wsm[b] + wsm[b + 1] + wsm[b + wlm1] + wsm[b + wlm1 + 1];
+}
+
+// reads only pixels with bak > 0 and writes only pixels with bak <= 0: race free in parallel
+__global__ void hs_k_trk_dilate(int wl, int hl, int diag, const float* bak, float* id, float* ws) {
+  const int i = wl + blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= wl * hl - wl) return;
+  if (bak[i] > 0) return;
+  int o[4];
+  if (diag) { o[0] = 1 + wl; o[1] = -1 - wl; o[2] = wl - 1; o[3] = -wl + 1; }
+  else { o[0] = 1; o[1] = -1; o[2] = wl; o[3] = -wl; }
+  float sum = 0, num = 0, numn = 0;
+  const int n = wl * hl;
+#pragma unroll
+  for (int q = 0; q < 4; q++)
+    // the reference reads one element past either end at pixels (0,1) / (w-1,h-2) (CoarseTracker.cpp:175-178);
+    // those two pixels never reach pc_* (border 2), so out-of-range neighbours count as empty
+    if (i + o[q] >= 0 && i + o[q] < n && bak[i + o[q]] > 0) {
+      sum += id[i + o[q]];
+      num += bak[i + o[q]];
+      numn++;
+    }
+  if (numn > 0) {
+    id[i] = sum / numn;
+    ws[i] = num / numn;
+  }
+}
+
+namespace {
+__device__ __forceinline__ bool trk_keep(int i, int wl, int hl, const float* id, const float* ws, const float4* ref,
+                                         float* idn) {
+  const int y = i / wl, x = i - y * wl;
+  if (y < 2 || y >= hl - 2 || x < 2 || x >= wl - 2) return false;
+  if (!(ws[i] > 0)) return false;
+  const float v = id[i] / ws[i];
+  *idn = v;
+  return isfinite(ref[i].x) && v > 0;
+}
+}  // namespace
+
+__global__ __launch_bounds__(256) void hs_k_trk_count(int wl, int hl, const float* id, const float* ws,
+                                                       const float4* ref, int* blockCount) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  float idn;
+  const bool k = i < wl * hl && trk_keep(i, wl, hl, id, ws, ref, &idn);
+  const int c = __syncthreads_count(k);
+  if (threadIdx.x == 0) blockCount[blockIdx.x] = c;
+}
+
+// exclusive scan of the block counts (one workgroup); total -> *pc_n
+__global__ __launch_bounds__(1024) void hs_k_trk_scan(int nb, const int* blockCount, int* blockOff, int* pc_n) {
+  __shared__ int s[1024];
+  __shared__ int carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int base = 0; base < nb; base += 1024) {
+    const int i = base + threadIdx.x;
+    const int v = i < nb ? blockCount[i] : 0;
+    s[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+      const int t = threadIdx.x >= o ? s[threadIdx.x - o] : 0;
+      __syncthreads();
+      s[threadIdx.x] += t;
+      __syncthreads();
+    }
+    if (i < nb) blockOff[i] = carry + s[threadIdx.x] - v;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry += s[1023];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *pc_n = carry;
+}
+
+__global__ __launch_bounds__(256) void hs_k_trk_compact(int wl, int hl, const float* id, const float* ws,
+                                                         const float4* ref, const int* blockOff, float* pu, float* pv,
+                                                         float* pid, float* pcol) {
+  __shared__ int waveCnt[4];
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float idn = 0.f;
+  const bool k = i < wl * hl && trk_keep(i, wl, hl, id, ws, ref, &idn);
+  const unsigned long long bal = __ballot(k);
+  if (lane == 0) waveCnt[wv] = __popcll(bal);
+  __syncthreads();
+  int off = blockOff[blockIdx.x];
+  for (int w = 0; w < wv; w++) off += waveCnt[w];
+  off += __popcll(bal & ((1ull << lane) - 1ull));
+  if (k) {
+    const int y = i / wl, x = i - y * wl;
+    pu[off] = (float)x;
+    pv[off] = (float)y;
+    pid[off] = idn;
+    pcol[off] = ref[i].x;
+  }
+}

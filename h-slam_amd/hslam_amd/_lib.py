@@ -67,6 +67,17 @@ SIGNATURES = {
     "hs_ba_get_timings": ([VP, VP], I),
     "hs_comm_get_unique_id": ([VP], I),
     "hs_comm_init": ([VP, VP, I, I], I),
+    # include/hs_track.h
+    "hs_tracker_create": ([VP, VP, I, I, I, I, VP], I),
+    "hs_tracker_destroy": ([VP], None),
+    "hs_tracker_set_ref": ([VP, VP, C.c_float, VP, I, VP, VP, VP, VP], I),
+    "hs_tracker_get_ref": ([VP, I, VP, VP, VP, VP, VP], I),
+    "hs_tracker_set_frame": ([VP, VP, C.c_float], I),
+    "hs_tracker_calc_res": ([VP, I, VP, VP, C.c_float, VP, VP, VP, VP], I),
+    "hs_tracker_track": ([VP, VP, VP, I, VP, VP, VP, VP], I),
+    "hs_tracker_track_tries": ([VP, I, VP, VP, VP, C.c_float, VP, VP, VP, VP, VP, VP], I),
+    "hs_tracker_get_lm_log": ([VP, I, I, VP, VP, VP, VP, VP], I),
+    "hs_tracker_last_ms": ([VP, VP], I),
 }
 
 _lib = None

@@ -415,3 +415,84 @@ def render_depth_at(planes, K, R_c2w, C, pix):
         ok = (s > 0) & (X >= p.xmin) & (X <= p.xmax) & (Y >= p.ymin) & (Y <= p.ymax) & (s < best)
         best[ok] = s[ok]
     return None, best * d[:, 2]
+
+
+# ----------------------------------------------------------------- tracking pair (C2 / C5)
+@dataclass
+class TrackScene:
+    width: int
+    height: int
+    K: np.ndarray                 # level-0 intrinsics (fp64)
+    n_levels: int
+    ref_pyr: list                 # lastRef DirPyr: per level (h_l, w_l, 3) float32
+    new_pyr: list                 # the frame being tracked
+    ref_exposure: float
+    new_exposure: float
+    ref_aff: np.ndarray           # lastRef aff_g2l (a, b)
+    pt_u: np.ndarray              # [n] float32 centerProjectedTo u in lastRef
+    pt_v: np.ndarray
+    pt_idepth: np.ndarray         # [n] float32 centerProjectedTo idepth
+    pt_hdi: np.ndarray            # [n] float32 point HdiF
+    T_true: np.ndarray            # [7] true refToNew (SE3 data)
+    aff_true: np.ndarray          # [2] true aff_g2l of the new frame
+    planes: list = field(default=None, repr=False)
+
+    @property
+    def K4(self):
+        return np.array([self.K[0, 0], self.K[1, 1], self.K[0, 2], self.K[1, 2]], np.float32)
+
+
+def make_track_scene(n_points: int = 2000, width: int = 640, height: int = 480, K=None, seed: int = SEED,
+                     trans: float = 0.02, rot_deg: float = 0.5, a: float = 0.05, b: float = 3.0,
+                     idepth_noise: float = 0.01, dup_frac: float = 0.05, kitti: bool = False,
+                     n_levels: int | None = None) -> TrackScene:
+    """lastRef + a new frame moved by (rot_deg about a random axis, trans m in a random direction) and
+    re-lit by I_new = e^a I + b.  The reference points are the centre projections of window points into
+    lastRef (sub-pixel positions, idepth with 1% noise, HdiF in [5e-4, 2e-3]); dup_frac of them are
+    near-duplicates that round to the same pixel, exercising the scatter-add order of makeCoarseDepthL0."""
+    rng = np.random.default_rng(seed + 7)
+    if K is None:
+        K = (np.array([[718.856, 0, 615.5], [0, 718.856, 183.5], [0, 0, 1.0]]) if kitti
+             else np.array([[256.0, 0, 319.5], [0, 254.4, 239.5], [0, 0, 1.0]]))
+    K = np.asarray(K, dtype=np.float64)
+    f = K[0, 0]
+    planes = [make_plane(rng, 5.0, f), make_plane(rng, 3.0, f, xmax=-0.25), make_plane(rng, 2.0, f, xmin=0.55, ymax=0.15)]
+    levels = n_levels or min(pyramid_levels(width, height), 5)
+    R_ref_c2w = rodrigues(np.array([0.0, 0.01, 0.0]))
+    C_ref = np.array([0.3, 0.0, 0.0])
+    img_ref, _ = render(planes, K, R_ref_c2w, C_ref, width, height)
+    ax = rng.normal(size=3)
+    ax /= np.linalg.norm(ax)
+    dR = rodrigues(ax * math.radians(rot_deg))
+    dt = rng.normal(size=3)
+    dt *= trans / np.linalg.norm(dt)
+    # refToNew = (dR, dt): X_new = dR X_ref + dt
+    R_new_w2c = dR @ R_ref_c2w.T
+    t_new_w2c = dR @ (-R_ref_c2w.T @ C_ref) + dt
+    R_new_c2w = R_new_w2c.T
+    C_new = -R_new_c2w @ t_new_w2c
+    img_new, _ = render(planes, K, R_new_c2w, C_new, width, height, a=a, b=b)
+    ref_pyr = make_dir_pyramid(img_ref, levels)
+    new_pyr = make_dir_pyramid(img_new, levels)
+    n_dup = int(round(n_points * dup_frac))
+    n_base = n_points - n_dup
+    pix = _select_points(ref_pyr[0], n_base, 6, rng)
+    u = pix[:, 1] + rng.uniform(-0.45, 0.45, n_base)
+    v = pix[:, 0] + rng.uniform(-0.45, 0.45, n_base)
+    _, depth = render_depth_at(planes, K, R_ref_c2w, C_ref, pix)
+    idp = (1.0 / depth) * (1.0 + idepth_noise * rng.normal(size=n_base))
+    if n_dup:
+        src = rng.integers(0, n_base, n_dup)
+        du = np.round(u[src]) + rng.uniform(-0.45, 0.45, n_dup)
+        dv = np.round(v[src]) + rng.uniform(-0.45, 0.45, n_dup)
+        u = np.concatenate([u, du])
+        v = np.concatenate([v, dv])
+        idp = np.concatenate([idp, idp[src] * (1.0 + idepth_noise * rng.normal(size=n_dup))])
+        perm = rng.permutation(n_points)
+        u, v, idp = u[perm], v[perm], idp[perm]
+    hdi = rng.uniform(5e-4, 2e-3, n_points)
+    return TrackScene(width=width, height=height, K=K, n_levels=levels, ref_pyr=ref_pyr, new_pyr=new_pyr,
+                      ref_exposure=1.0, new_exposure=1.0, ref_aff=np.zeros(2),
+                      pt_u=u.astype(np.float32), pt_v=v.astype(np.float32), pt_idepth=idp.astype(np.float32),
+                      pt_hdi=hdi.astype(np.float32), T_true=se3_data(dR, dt), aff_true=np.array([a, b]),
+                      planes=planes)

@@ -87,8 +87,19 @@ def load(fast=False):
     for n in ("hso_se3_exp", "hso_se3_log", "hso_se3_inverse", "hso_se3_adj", "hso_se3_matrix"):
         getattr(lib, n).argtypes = [vp, vp]
     lib.hso_se3_mul.argtypes = [vp, vp, vp]
-    for n, a in (("hso_track_create", None),):
-        pass
+    lib.hso_trk_create.restype = vp
+    lib.hso_trk_create.argtypes = [vp, C.c_int, C.c_int, C.c_int, vp]
+    lib.hso_trk_destroy.argtypes = [vp]
+    lib.hso_trk_set_ref.argtypes = [vp, vp, C.c_float, vp, C.c_int, vp, vp, vp, vp]
+    lib.hso_trk_set_frame.argtypes = [vp, vp, C.c_float]
+    lib.hso_trk_get_ref.argtypes = [vp, C.c_int, vp, vp, vp, vp]
+    lib.hso_trk_get_ref.restype = C.c_int
+    lib.hso_trk_calc_res.argtypes = [vp, C.c_int, vp, vp, C.c_float, vp, vp, vp, vp]
+    lib.hso_trk_track.argtypes = [vp, vp, vp, C.c_int, vp, vp, vp, vp]
+    lib.hso_trk_track.restype = C.c_int
+    lib.hso_trk_get_log.argtypes = [vp, C.c_int, vp, vp, vp, vp]
+    lib.hso_trk_get_log.restype = C.c_int
+    lib.hso_trk_track_tries.argtypes = [vp, C.c_int, vp, vp, vp, C.c_float, C.c_int] + [vp] * 6
     _LIBS[name] = lib
     return lib
 
@@ -257,3 +268,82 @@ def se3_matrix(a):
     out = np.zeros(9)
     load().hso_se3_matrix(_p(np.ascontiguousarray(a, np.float64)), _p(out))
     return out.reshape(3, 3)
+
+
+# ------------------------------------------------------------------ CoarseTracker restatement
+class OracleTracker:
+    """CoarseTracker + System::trackNewCoarse's try loop as a CPU restatement (oracle/track_oracle.cpp)."""
+
+    def __init__(self, width, height, K4, n_levels, params=None, fast=False):
+        self.lib = load(fast)
+        self.params = params if params is not None else default_params()
+        k4 = np.ascontiguousarray(K4, np.float32)
+        self.w = [width >> l for l in range(n_levels)]
+        self.h_ = [height >> l for l in range(n_levels)]
+        self.n_levels = n_levels
+        self.h = self.lib.hso_trk_create(C.byref(self.params), width, height, n_levels, _p(k4))
+        self._keep = []
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.lib.hso_trk_destroy(self.h)
+            self.h = None
+
+    @staticmethod
+    def _pyr(pyr):
+        arrs = [np.ascontiguousarray(p, np.float32) for p in pyr]
+        return arrs, (C.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+
+    def set_ref(self, ref_pyr, ab_exposure, aff, u, v, idepth, hdi):
+        arrs, pp = self._pyr(ref_pyr)
+        cols = [np.ascontiguousarray(a, np.float32) for a in (u, v, idepth, hdi)]
+        self.lib.hso_trk_set_ref(self.h, C.cast(pp, C.c_void_p), float(ab_exposure),
+                                 _p(np.ascontiguousarray(aff, np.float64)), len(cols[0]), *[_p(c) for c in cols])
+
+    def set_frame(self, new_pyr, ab_exposure):
+        arrs, pp = self._pyr(new_pyr)
+        self.lib.hso_trk_set_frame(self.h, C.cast(pp, C.c_void_p), float(ab_exposure))
+
+    def set_scene(self, s):
+        self.set_ref(s.ref_pyr, s.ref_exposure, s.ref_aff, s.pt_u, s.pt_v, s.pt_idepth, s.pt_hdi)
+        self.set_frame(s.new_pyr, s.new_exposure)
+
+    def pc(self, lvl):
+        cap = self.w[lvl] * self.h_[lvl]
+        out = {k: np.zeros(cap, np.float32) for k in ("u", "v", "idepth", "color")}
+        n = self.lib.hso_trk_get_ref(self.h, lvl, *[_p(out[k]) for k in ("u", "v", "idepth", "color")])
+        return {k: a[:n] for k, a in out.items()}
+
+    def calc_res(self, lvl, T7, aff, cutoff):
+        res6, H, b = np.zeros(6), np.zeros(64), np.zeros(8)
+        nw = C.c_int()
+        self.lib.hso_trk_calc_res(self.h, lvl, _p(np.ascontiguousarray(T7, np.float64)),
+                                  _p(np.ascontiguousarray(aff, np.float64)), float(cutoff), _p(res6), _p(H), _p(b),
+                                  C.byref(nw))
+        return res6, H.reshape(8, 8), b, nw.value
+
+    def track(self, T7, aff, coarsest, minRes):
+        T = np.array(T7, np.float64)
+        a = np.array(aff, np.float64)
+        lr, fl = np.zeros(5), np.zeros(3)
+        its = C.c_int()
+        ok = self.lib.hso_trk_track(self.h, _p(T), _p(a), coarsest, _p(np.ascontiguousarray(minRes, np.float64)),
+                                    _p(lr), _p(fl), C.byref(its))
+        return dict(ok=bool(ok), T=T, aff=a, lastResiduals=lr, flow=fl, iters=its.value)
+
+    def lm_log(self, cap=512):
+        lvl, nr, orr, inc = np.zeros(cap, np.int32), np.zeros(cap), np.zeros(cap), np.zeros(cap)
+        n = self.lib.hso_trk_get_log(self.h, cap, _p(lvl), _p(nr), _p(orr), _p(inc))
+        n = min(n, cap)
+        return lvl[:n], nr[:n], orr[:n], inc[:n]
+
+    def track_tries(self, tries, aff_last, lastCoarseRMSE, reTrackThreshold=1.5, coarsest=None):
+        tr = np.ascontiguousarray(np.asarray(tries, np.float64).reshape(-1, 7))
+        if coarsest is None:
+            coarsest = min(self.n_levels - 1, 4)
+        T, a, ach, fl = np.zeros(7), np.zeros(2), np.zeros(5), np.zeros(3)
+        good, n = C.c_int(), C.c_int()
+        self.lib.hso_trk_track_tries(self.h, len(tr), _p(tr), _p(np.ascontiguousarray(aff_last, np.float64)),
+                                     _p(np.ascontiguousarray(lastCoarseRMSE, np.float64)), float(reTrackThreshold),
+                                     coarsest, _p(T), _p(a), _p(ach), _p(fl), C.byref(good), C.byref(n))
+        return dict(T=T, aff=a, achievedRes=ach, flowVecs=fl, haveOneGood=bool(good.value), tryIterations=n.value)

@@ -1,0 +1,190 @@
+"""GPU parity of the CoarseTracker path (HIP kernels through include/hs_track.h) against the CPU oracle.
+
+Bars:
+* makeCoarseDepthL0 pc_u / pc_v / pc_idepth / pc_color and pc_n per level: bit-exact;
+* calcRes categorical counts (numTermsInE, saturated, buf_warped_n): exact;
+  energy E (fp32 sum in a different order): rel <= 2e-5; flow indicators rel <= 1e-4;
+  calcGSSSE H / b: |d| <= 1e-4 (|ref| + 1e-3 max|diag H|);
+* trackNewestCoarse / the try loop: the per-iteration LM logs (accept-test ratios, step norms) agree to
+  1e-4 rel up to the first decision that is a near-tie in the oracle itself (fp32 sums in another order
+  can flip a tie); if no such tie occurs the final pose agrees to 1e-5 and lastResiduals to 1e-4 rel,
+  otherwise to the LM's own stopping tolerance (pose 2e-3, lastResiduals 1e-2 rel).  ok / haveOneGood /
+  tryIterations: equal.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def vga():
+    from hslam_amd.scene import make_track_scene
+    return make_track_scene(n_points=2000, n_levels=5)
+
+
+@pytest.fixture(scope="module")
+def pair(vga):
+    from hslam_amd.track import CoarseTracker
+    from oracle_ffi import OracleTracker
+    g = CoarseTracker(vga.width, vga.height, vga.K4, vga.n_levels)
+    g.set_scene(vga)
+    o = OracleTracker(vga.width, vga.height, vga.K4, vga.n_levels)
+    o.set_scene(vga)
+    return g, o
+
+
+def _pose_err(a, b):
+    from hslam_amd.se3 import SE3
+    return float(np.linalg.norm((SE3.from_data(a) * SE3.from_data(b).inverse()).log()))
+
+
+def test_coarse_depth_bit_exact(vga, pair):
+    g, o = pair
+    for l in range(vga.n_levels):
+        pg, po = g.pc(l), o.pc(l)
+        assert len(pg["u"]) == len(po["u"]) > 0
+        for k in ("u", "v", "idepth", "color"):
+            assert np.array_equal(pg[k], po[k]), (l, k)
+
+
+@pytest.mark.parametrize("kitti", [False, True])
+def test_coarse_depth_dups_and_kitti(kitti):
+    from hslam_amd.scene import make_track_scene
+    from hslam_amd.track import CoarseTracker
+    from oracle_ffi import OracleTracker
+    s = (make_track_scene(n_points=3000, width=1232, height=368, kitti=True, n_levels=5, dup_frac=0.2) if kitti
+         else make_track_scene(n_points=1500, dup_frac=0.4, seed=11))
+    g = CoarseTracker(s.width, s.height, s.K4, s.n_levels)
+    g.set_scene(s)
+    o = OracleTracker(s.width, s.height, s.K4, s.n_levels)
+    o.set_scene(s)
+    for l in range(s.n_levels):
+        pg, po = g.pc(l), o.pc(l)
+        for k in ("u", "v", "idepth", "color"):
+            assert np.array_equal(pg[k], po[k]), (l, k)
+
+
+def _close_H(Hg, Ho, tol=1e-4):
+    scale = np.abs(np.diag(Ho)).max()
+    return bool(np.all(np.abs(Hg - Ho) <= tol * (np.abs(Ho) + 1e-3 * scale)))
+
+
+@pytest.mark.parametrize("which", ["identity", "truth", "perturbed"])
+def test_calc_res_parity(vga, pair, which):
+    from hslam_amd.se3 import SE3
+    g, o = pair
+    T = {"identity": SE3().data(), "truth": vga.T_true,
+         "perturbed": (SE3.exp([0.004, -0.003, 0.002, 0.002, 0.001, -0.002]) * SE3.from_data(vga.T_true)).data()}[which]
+    aff = [0.0, 0.0] if which == "identity" else list(vga.aff_true)
+    for lvl in range(vga.n_levels):
+        for cut in (g.params.coarseCutoffTH, 2 * g.params.coarseCutoffTH):
+            rg, Hg, bg, ng = g.calcRes(lvl, T, aff, cut)
+            ro, Ho, bo, no = o.calc_res(lvl, T, aff, cut)
+            assert ng == no and rg[1] == ro[1], (lvl, cut)
+            assert round(rg[5] * rg[1]) == round(ro[5] * ro[1])
+            assert abs(rg[0] - ro[0]) <= 2e-5 * abs(ro[0]) + 1e-3
+            for k in (2, 4):
+                assert abs(rg[k] - ro[k]) <= 1e-4 * abs(ro[k]) + 1e-6
+            assert _close_H(Hg, Ho), (lvl, np.abs(Hg - Ho).max())
+            sb = np.abs(bo).max() + 1e-30
+            assert np.all(np.abs(bg - bo) <= 1e-4 * (np.abs(bo) + 1e-3 * sb))
+
+
+def _lm_divergence(lg, lo):
+    """Walk the two LM logs (level, resNew/N, resOld/N, |inc|) in lockstep.  Until the trajectories part, every
+    operand agrees to fp32-summation-order precision; they may only part at a decision that is a near-tie in
+    the oracle itself (accept: resNew/N vs resOld/N, break: |inc| vs 1e-3) or at a step from a near-singular
+    system (|inc| > 1).  Returns the index of that decision, or None when the logs are identical in length and
+    decisions."""
+    lvg, ng, og, ig = lg
+    lvo, no, oo, io = lo
+    for k in range(min(len(lvg), len(lvo))):
+        assert lvg[k] == lvo[k], k
+        assert abs(ng[k] - no[k]) <= 1e-4 * abs(no[k]), (k, ng[k], no[k])
+        assert abs(og[k] - oo[k]) <= 1e-4 * abs(oo[k]), (k, og[k], oo[k])
+        if io[k] > 1.0:   # a step of > 1 (scaled units) comes from a near-singular H: fp order decides the rest
+            return k
+        assert abs(ig[k] - io[k]) <= 1e-3 * io[k] + 1e-7, (k, ig[k], io[k])
+        if (ng[k] < og[k]) != (no[k] < oo[k]):
+            assert abs(no[k] - oo[k]) <= 1e-4 * oo[k], ("accept flip without a tie", k)
+            return k
+        if (ig[k] > 1e-3) != (io[k] > 1e-3):
+            assert abs(io[k] - 1e-3) <= 1e-6, ("break flip without a tie", k)
+            return k
+    assert len(lvg) == len(lvo)
+    return None
+
+
+@pytest.mark.parametrize("start", ["identity", "near"])
+def test_track_parity(vga, pair, start):
+    from hslam_amd.se3 import SE3
+    g, o = pair
+    T0 = SE3().data() if start == "identity" else (SE3.exp([0.002, 0, -0.001, 0, 0.001, 0]) *
+                                                   SE3.from_data(vga.T_true)).data()
+    minRes = np.full(5, np.nan)
+    okg, Tg, ag = g.trackNewestCoarse(T0, [0.0, 0.0], vga.n_levels - 1, minRes)
+    ro = o.track(T0, [0.0, 0.0], vga.n_levels - 1, minRes)
+    assert okg == ro["ok"] and okg
+    k = _lm_divergence(g.lm_log(0), o.lm_log())
+    tol_T, tol_a, tol_b = (1e-5, 1e-5, 1e-3) if k is None else (2e-3, 1e-2, 0.5)
+    assert _pose_err(Tg, ro["T"]) < tol_T, k
+    assert abs(ag[0] - ro["aff"][0]) < tol_a and abs(ag[1] - ro["aff"][1]) < tol_b, k
+    lr = g.lastResiduals
+    fin = np.isfinite(ro["lastResiduals"])
+    assert np.array_equal(np.isfinite(lr), fin)
+    assert np.allclose(lr[fin], ro["lastResiduals"][fin], rtol=1e-4 if k is None else 1e-2)
+    assert _pose_err(Tg, vga.T_true) < 3e-3
+    assert g.last_ms() > 0
+
+
+def test_track_abort_parity(vga, pair):
+    from hslam_amd.se3 import SE3
+    g, o = pair
+    T0 = SE3().data()
+    minRes = np.full(5, 1e-3)
+    okg, Tg, ag = g.trackNewestCoarse(T0, [0.0, 0.0], vga.n_levels - 1, minRes)
+    ro = o.track(T0, [0.0, 0.0], vga.n_levels - 1, minRes)
+    assert not okg and not ro["ok"]
+    assert np.array_equal(Tg, T0) and np.array_equal(Tg, ro["T"])
+    assert np.array_equal(np.isfinite(g.lastResiduals), np.isfinite(ro["lastResiduals"]))
+
+
+def test_track_tries_parity(vga, pair):
+    from hslam_amd.se3 import SE3
+    from hslam_amd.track import motion_hypotheses, trackNewCoarse
+    g, o = pair
+    # hypotheses around a last-frame motion that is half the true one
+    half = SE3.exp(SE3.from_data(vga.T_true).log() * 0.5)
+    lastF = SE3()
+    slast = half.inverse()
+    sprelast = (half * half).inverse()
+    tries = motion_hypotheses(lastF, slast, sprelast)
+    tries = np.concatenate([SE3.exp([0, 0, 0, 0.3, -0.25, 0.2]).data()[None], tries])  # a hopeless first try
+    for rmse in (np.full(5, 100.0), np.full(5, 1e-6)):
+        og = trackNewCoarse(g, tries, [0.0, 0.0], rmse)
+        oo = o.track_tries(tries, [0.0, 0.0], rmse)
+        assert og["haveOneGood"] == oo["haveOneGood"]
+        assert og["tryIterations"] == oo["tryIterations"]
+        assert _pose_err(og["T"], oo["T"]) < 2e-3
+        fin = np.isfinite(oo["achievedRes"])
+        assert np.array_equal(np.isfinite(og["achievedRes"]), fin)
+        assert np.allclose(og["achievedRes"][fin], oo["achievedRes"][fin], rtol=1e-2)
+    # every hypothesis' own LM run agrees with the oracle's run of that hypothesis up to a near-tie
+    for i in (0, 1, 5, 17, len(tries) - 1):
+        o.track(tries[i], [0.0, 0.0], vga.n_levels - 1, np.full(5, np.nan))
+        _lm_divergence(g.lm_log(i), o.lm_log())
+
+
+def test_errors_are_loud(vga):
+    from hslam_amd._lib import HsError
+    from hslam_amd.se3 import SE3
+    from hslam_amd.track import CoarseTracker
+    g = CoarseTracker(vga.width, vga.height, vga.K4, vga.n_levels)
+    with pytest.raises(HsError):
+        g.calcRes(0, SE3().data(), [0, 0], 20.0)        # no reference / frame yet
+    g.set_scene(vga)
+    with pytest.raises(HsError):
+        g.trackNewestCoarse(SE3().data(), [0, 0], 5, np.full(5, np.nan))   # coarsest must be < 5
+    with pytest.raises(HsError):
+        CoarseTracker(vga.width, vga.height, vga.K4, 7)
