@@ -7,7 +7,7 @@ mkdir -p $OUT
 cd $GRAFT_REPO_ROOT
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.txt 2>&1 || { echo "smoke failed rc=$?"; tail -30 $OUT/smoke.txt; exit 1; }
 tail -3 $OUT/smoke.txt
-timeout -k 10 600 python -m pytest tests -m gpu -q -x > $OUT/pytest_gpu.txt 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.txt 2>&1
 rc=$?
 echo "pytest rc=$rc"; tail -30 $OUT/pytest_gpu.txt
 if [ $rc -gt 1 ]; then exit $rc; fi
