@@ -79,7 +79,7 @@ struct hs_ctx {
   std::vector<int8_t> res_order;  // [nP*8]
   std::vector<double> adHost, adTarget;
   std::vector<float> adHostF, adTargetF;
-  std::vector<double> HM, bM, Porth;
+  std::vector<double> HM, bM, Porth, Nproj;
   HsDevState* h_state = nullptr;  // pinned staging of the device state
   int* h_ctl = nullptr;           // pinned: iteration, status, log_count
   bool haveSystem = false;        // a stitched, not yet solved system is in d_sys
@@ -105,7 +105,7 @@ struct hs_ctx {
   double *d_adHost = nullptr, *d_adTarget = nullptr;
   float *d_adHostF = nullptr, *d_adTargetF = nullptr;
   double* d_sys = nullptr;  // HA | bA | HSC | bSC | energy, sum|idepth|, #points
-  double *d_HM = nullptr, *d_bM = nullptr, *d_Porth = nullptr;
+  double *d_HM = nullptr, *d_bM = nullptr, *d_Nproj = nullptr;
   float* d_xAd = nullptr;
   double* d_x = nullptr;
   double* d_elog = nullptr;
@@ -143,7 +143,7 @@ static void free_window(hs_ctx* c) {
                   c->d_res_order, c->d_r_state, c->d_r_active, c->d_r_energy, c->d_r_newEnergy, c->d_r_ewo,
                   c->d_r_center, c->d_p_actmask, c->d_p_HdiF, c->d_p_bdSumF, c->d_p_Hcd, c->d_p_JpJdF,
                   c->d_p_Jrec, c->d_p_step, c->d_p_energy, c->d_part, c->d_part_cnt, c->d_hccbc, c->d_adHost,
-                  c->d_adTarget, c->d_adHostF, c->d_adTargetF, c->d_sys, c->d_HM, c->d_bM, c->d_Porth, c->d_xAd,
+                  c->d_adTarget, c->d_adHostF, c->d_adTargetF, c->d_sys, c->d_HM, c->d_bM, c->d_Nproj, c->d_xAd,
                   c->d_x, c->d_elog, c->d_cand, c->d_tr_lin, c->d_tr_acc, c->d_tr_solve, c->d_tr_stitch};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -159,7 +159,7 @@ static void free_window(hs_ctx* c) {
   c->d_p_energy = nullptr;
   c->d_part = nullptr; c->d_part_cnt = nullptr; c->d_hccbc = nullptr;
   c->d_adHost = c->d_adTarget = nullptr; c->d_adHostF = c->d_adTargetF = nullptr;
-  c->d_sys = nullptr; c->d_HM = c->d_bM = c->d_Porth = nullptr;
+  c->d_sys = nullptr; c->d_HM = c->d_bM = c->d_Nproj = nullptr;
   c->d_xAd = nullptr; c->d_x = nullptr; c->d_elog = nullptr; c->d_cand = nullptr;
   c->d_tr_lin = c->d_tr_acc = c->d_tr_solve = c->d_tr_stitch = nullptr;
   c->nF = c->nP = c->nR = 0;
@@ -188,7 +188,7 @@ static void compute_projector(hs_ctx* c) {
     for (int k = 3; k < 6; k++) v[4 + f.idx * 8 + k] *= SCALE_XI_ROT_INVERSE;
   }
   ns.push_back(v);
-  nullspace_projector(ns, n, c->P.solverModeDelta, c->Porth);
+  nullspace_projector(ns, n, c->P.solverModeDelta, c->Porth, &c->Nproj);
 }
 
 static int fetch_state(hs_ctx* c) {
@@ -268,10 +268,11 @@ static int launch_solve(hs_ctx* c, int flags, int iteration, bool log) {
   std::memset(&a, 0, sizeof(a));
   a.flags = flags;
   a.iteration = iteration;
+  a.nF = c->nF;
   a.st = c->d_state;
   a.HA = c->HA(); a.bA = c->bA(); a.HSC = c->HSC(); a.bSC = c->bSC();
   a.HM = c->hm_zero ? nullptr : c->d_HM;
-  a.bM = c->d_bM; a.Porth = c->d_Porth;
+  a.bM = c->d_bM; a.Nproj = c->d_Nproj;
   a.adHostF = c->d_adHostF; a.adTargetF = c->d_adTargetF;
   a.xAd = c->d_xAd; a.pre = c->d_pre; a.x_out = c->d_x;
   a.sysE = c->sysE();
@@ -279,7 +280,7 @@ static int launch_solve(hs_ctx* c, int flags, int iteration, bool log) {
   a.trace = c->d_tr_solve;
   a.initialCalibHessian = c->P.initialCalibHessian;
   a.thOptIterations = c->P.thOptIterations;
-  hipLaunchKernelGGL(hs_k_solve, dim3(1), dim3(384), 0, c->stream, a);
+  hipLaunchKernelGGL(hs_k_solve, dim3(1), dim3(HS_SOLVE_NT), 0, c->stream, a);
   HS_HIP(hipGetLastError());
   return HS_OK;
 }
@@ -324,7 +325,11 @@ static int dump_one(const char* name, const long long* d, int nblocks, double ti
     for (int k = 1; k < 16; k++) t1 = std::max(t1, h[b * 16 + k]);
   }
   std::fprintf(stderr, "[hs trace] %-12s blocks %5d span %8.2f us\n", name, nblocks, t0 < 0 ? 0.0 : (t1 - t0) * tick_us);
+  if (std::string(name) == "solve" && h[0] && h[10] && h[11] && h[15] > h[0])  // slots 10/11: shader clock
+    std::fprintf(stderr, "[hs trace] %-12s shader clock %.0f MHz\n", name,
+                 (double)(h[11] - h[10]) / ((h[15] - h[0]) * tick_us));
   for (int k = 1; k < 16; k++) {
+    if (std::string(name) == "solve" && (k == 10 || k == 11)) continue;
     std::vector<double> v;
     for (int b = 0; b < nblocks; b++)
       if (h[b * 16] && h[b * 16 + k]) v.push_back((h[b * 16 + k] - h[b * 16]) * tick_us);
@@ -341,6 +346,13 @@ static int dump_traces(hs_ctx* c) {
   HS_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device));
   const double tick_us = khz > 0 ? 1e3 / khz : 0.01;
   HS_TRY(dump_one("solve", c->d_tr_solve, 1, tick_us, c->stream));
+  {  // in-loop shader-clock stamps of the solve (slots 16..23, cycles after slot 16)
+    long long h[32];
+    HS_HIP(hipMemcpy(h, c->d_tr_solve, sizeof(h), hipMemcpyDeviceToHost));
+    std::fprintf(stderr, "[hs trace] solve kb4 cycles:");
+    for (int k = 17; k < 24; k++) std::fprintf(stderr, " s%d=%lld", k, h[k] ? h[k] - h[16] : -1);
+    std::fprintf(stderr, "\n");
+  }
   HS_TRY(dump_one("linearize", c->d_tr_lin, c->nP, tick_us, c->stream));
   HS_TRY(dump_one("accumulate", c->d_tr_acc, c->nF * c->nF * c->S + 3, tick_us, c->stream));
   HS_TRY(dump_one("stitch", c->d_tr_stitch, c->nF * c->nF, tick_us, c->stream));
@@ -646,7 +658,7 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
   HS_TRY(dalloc(&c->d_adHost, nF * nF * 64)); HS_TRY(dalloc(&c->d_adTarget, nF * nF * 64));
   HS_TRY(dalloc(&c->d_adHostF, nF * nF * 64)); HS_TRY(dalloc(&c->d_adTargetF, nF * nF * 64));
   HS_TRY(dalloc(&c->d_sys, c->sys_len()));
-  HS_TRY(dalloc(&c->d_HM, (size_t)n * n)); HS_TRY(dalloc(&c->d_bM, n)); HS_TRY(dalloc(&c->d_Porth, (size_t)n * n));
+  HS_TRY(dalloc(&c->d_HM, (size_t)n * n)); HS_TRY(dalloc(&c->d_bM, n)); HS_TRY(dalloc(&c->d_Nproj, (size_t)2 * n * HS_NNS));
   HS_TRY(dalloc(&c->d_xAd, nF * nF * 8)); HS_TRY(dalloc(&c->d_x, n)); HS_TRY(dalloc(&c->d_elog, kLogCap));
   HS_TRY(dalloc(&c->d_cand, (size_t)c->cand_stride * c->nranks));
   HS_HIP(hipMemset(c->d_cand, 0xff, sizeof(float) * c->cand_stride * c->nranks));  // NaN, sign set: no candidate
@@ -655,7 +667,7 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
   if (c->tracing) {
     HS_TRY(dalloc(&c->d_tr_lin, (size_t)std::max(nP, 1) * 16));
     HS_TRY(dalloc(&c->d_tr_acc, (size_t)(nF * nF * c->S + 3) * 16));
-    HS_TRY(dalloc(&c->d_tr_solve, 16));
+    HS_TRY(dalloc(&c->d_tr_solve, 32));
     HS_TRY(dalloc(&c->d_tr_stitch, (size_t)nF * nF * 16));
   }
 
@@ -684,7 +696,7 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
   HS_HIP(hipMemcpy(c->d_adTarget, c->adTarget.data(), sizeof(double) * nF * nF * 64, hipMemcpyHostToDevice));
   HS_HIP(hipMemcpy(c->d_adHostF, c->adHostF.data(), sizeof(float) * nF * nF * 64, hipMemcpyHostToDevice));
   HS_HIP(hipMemcpy(c->d_adTargetF, c->adTargetF.data(), sizeof(float) * nF * nF * 64, hipMemcpyHostToDevice));
-  HS_HIP(hipMemcpy(c->d_Porth, c->Porth.data(), sizeof(double) * n * n, hipMemcpyHostToDevice));
+  HS_HIP(hipMemcpy(c->d_Nproj, c->Nproj.data(), sizeof(double) * 2 * n * HS_NNS, hipMemcpyHostToDevice));
   if (nR > 0) {
     if (rs->state) HS_HIP(hipMemcpy(c->d_r_state, rs->state, nR, hipMemcpyHostToDevice));
     else HS_TRY(reset_states(c));

@@ -990,7 +990,7 @@ __global__ __launch_bounds__(256) void hs_k_stitch(HsStitchArgs a) {
 // solve + step (fp64), one workgroup of 256 threads
 // =====================================================================================================
 namespace {
-constexpr int SOLVE_NT = 384;  // 6 waves: the lower-triangle 8x8 tile groups of the blocked LDLT
+constexpr int SOLVE_NT = HS_SOLVE_NT;  // 4 waves, one per SIMD: one lower-triangle 4x4 tile per lane in the LDLT
 constexpr int SOLVE_NU = (HS_MAXDIM * HS_MAXDIM + SOLVE_NT - 1) / SOLVE_NT;  // matrix entries per thread
 
 __device__ __forceinline__ double readlane_f64(double v, int lane) {
@@ -1002,91 +1002,177 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
 }  // namespace
 
 
-// Solves (L D L^T) y = z in place for the permuted, scaled system of one GN step: right-looking LDLT in
-// 4-column blocks (n = 4 + 8 nF is a multiple of 4).  Per block: wave 0 factors the 4-column panel with
-// readlane broadcasts (and carries the forward substitution), then every lower-triangle 4x4 tile
-// (register-resident; wave w owns an 8x8 group of tiles so its LDS reads hit 8 distinct rows of the
-// column-major panel arrays: no bank conflicts) takes the rank-4 update  A -= (L D) L^T  in column order,
-// and the owners of the next panel publish it.  Two workgroup barriers per block.  The result is Eigen's
-// LDLT solve up to fp64 rounding order (the pivot order is applied by the caller).  Then D^-1 and the
-// backward substitution by wave 0.
-//   M : the permuted system (row-major, stride n) in; L (strictly lower, stride LSTR) out
-//   W : scratch of 13 * HS_MAXDIM doubles
-constexpr int LSTR = HS_MAXDIM + 1;  // padded row stride of L (column writes / row reads: 2-way banks)
-__device__ __forceinline__ void ldlt_solve_blocked(double* M, double* W, double* yv, int n, int tid, long long* trace) {
+// Solves (L D L^T) y = z in place for the permuted, scaled system of one GN step (n = 4 + 8 nF, a multiple
+// of 4): right-looking LDLT in 4-column blocks with one-block look-ahead, ONE workgroup barrier per block.
+//  wave 0 (the panel wave): in phase k it applies block k's rank-4 update to the rows of column block
+//    k + 1 (one row per lane), takes the updated 4x4 diagonal block from lanes 0-3 (readlane), factors it
+//    uniformly, reduces its row to the (L D) / L entries of panel k + 1 and carries the forward substitution;
+//  waves 1-3: every lower 4x4 tile right of the next panel (register-resident, one per lane) takes block
+//    k's rank-4 update; the owners of column block k + 2 publish it for the panel wave's next phase.
+// The panel chain (the critical path) thus overlaps the trailing update.  fp64 throughout, FMA-contracted,
+// reciprocals by v_rcp_f64 + 2 Newton steps: the solve is checked against the oracle's Eigen-order LDLT by
+// tolerance (the LDLT is parity-unpinned), not bitwise.  The pivot order is applied by the
+// caller.  Then D^-1 and the backward substitution (one wave, 4x4 diagonal blocks solved uniformly).
+//   M  : the permuted system (row-major, stride n), read only
+//   LT : L transposed, LT[i * LSTR + k] = L(k, i); MUST be zero on entry (its upper part stays zero)
+//   W  : scratch of 26 * HS_MAXDIM doubles;  yv : right-hand side in, solution out
+constexpr int LSTR = HS_MAXDIM + 1;  // padded row stride of LT
+
+__device__ __forceinline__ double rcp_f64(double d) {  // 1/d to ~1 ulp; 0 for a (near-)zero pivot
+  double r = __builtin_amdgcn_rcp(d);
+  double e = __builtin_fma(-d, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-d, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  return fabs(d) > DBL_MIN ? r : 0.0;
+}
+
+// The panel's uniform factors: pivots d, their reciprocals, the partially reduced diagonal-block entries
+// q(jp, j) (after the columns < j) and the substituted right-hand side yd of the 4 diagonal rows.
+struct Panel4 {
+  double d[4], dinv[4], q[4][4], yd[4];
+};
+struct PanelOut {
+  double lw[4], ls[4], yr;
+};
+// wave-cooperative panel factorization: lane l holds row K0 + l (lanes 0-3: the diagonal block's rows), a =
+// its entries of the panel columns, yr its rhs; every lane of the wave executes this.  Column by column: the
+// pivot and the reduced entries come from lanes 0-3 by readlane, so the critical path per column is one
+// readlane, one reciprocal and one multiply-add.  A diagonal row l takes L entries only for j < l.
+__device__ __forceinline__ void panel_coop(const double a[4], double yr, int l, Panel4& P, PanelOut& o) {
+  double pr[4] = {a[0], a[1], a[2], a[3]};
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const double d = readlane_f64(pr[j], j);
+    const double dinv = rcp_f64(d);
+    const double ydj = readlane_f64(yr, j);
+    P.d[j] = d;
+    P.dinv[j] = dinv;
+    P.yd[j] = ydj;
+#pragma unroll
+    for (int jp = j + 1; jp < 4; jp++) P.q[jp][j] = readlane_f64(pr[j], jp);
+    const double lj = pr[j] * dinv;
+    o.lw[j] = l > j ? pr[j] : 0.0;
+    o.ls[j] = l > j ? lj : 0.0;
+#pragma unroll
+    for (int jp = j + 1; jp < 4; jp++) pr[jp] = __builtin_fma(-o.ls[j], P.q[jp][j], pr[jp]);
+    yr = __builtin_fma(-o.ls[j], ydj, yr);
+  }
+  o.yr = yr;
+}
+// a further (non-diagonal) row with the panel's factors: the same operations as panel_coop's lanes l >= 4
+__device__ __forceinline__ void panel_row_uniform(const double a[4], double yr, const Panel4& P, PanelOut& o) {
+  double pr[4] = {a[0], a[1], a[2], a[3]};
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    o.lw[j] = pr[j];
+    o.ls[j] = pr[j] * P.dinv[j];
+#pragma unroll
+    for (int jp = j + 1; jp < 4; jp++) pr[jp] = __builtin_fma(-o.ls[j], P.q[jp][j], pr[jp]);
+    yr = __builtin_fma(-o.ls[j], P.yd[j], yr);
+  }
+  o.yr = yr;
+}
+
+// publishes one panel row r (l = r - K0): LW / LS (zero for the diagonal rows, which take no part in the
+// trailing update), its L entries, and the substituted rhs; lane j < 4 also stores pivot j
+__device__ __forceinline__ void panel_row_store(const PanelOut& o, const Panel4& P, int r, int l, int K0, double* LWn,
+                                                double* LSn, double* LT, double* Dv, double* yf, double* yv) {
   constexpr int MD = HS_MAXDIM;
+  const bool diag = l < 4;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    LWn[j * MD + r] = diag ? 0.0 : o.lw[j];
+    LSn[j * MD + r] = diag ? 0.0 : o.ls[j];
+    LT[(K0 + j) * LSTR + r] = o.ls[j];  // zero on and above the diagonal
+  }
+  if (diag) {
+    Dv[r] = l == 0 ? P.d[0] : l == 1 ? P.d[1] : l == 2 ? P.d[2] : P.d[3];
+    yf[r] = o.yr;
+  } else {
+    yv[r] = o.yr;
+  }
+}
+
+__device__ __forceinline__ void ldlt_solve_blocked(const double* M, double* LT, double* W, double* yv, int n, int tid,
+                                                   long long* trace) {
+  constexpr int MD = HS_MAXDIM;
+  static_assert((HS_MAXDIM / 4 - 2) * (HS_MAXDIM / 4 - 1) / 2 <= SOLVE_NT - 64, "one trailing tile per lane");
   const int nb = n >> 2;
-  double* PB = W;           // [4][MD] current panel, column-major
-  double* LW = W + 4 * MD;  // [4][MD] L D of the panel columns
-  double* LS = W + 8 * MD;  // [4][MD] L of the panel columns
-  double* Dv = W + 12 * MD; // [MD]
-  // lower-triangle 8x8 tile groups: wave -> (group row, group col)
-  const int wv = tid >> 6, lane = tid & 63;
-  const int gr = wv == 0 ? 0 : (wv <= 2 ? 1 : 2), gc = wv == 0 ? 0 : (wv <= 2 ? wv - 1 : wv - 3);
-  const int tr = 8 * gr + (lane >> 3), tc = 8 * gc + (lane & 7);
-  const bool lower = wv < 6 && tr < nb && tc < nb && tr >= tc;
+  double* PBq = W;            // [2][4][MD] column block k+1 before block k's update, column-major
+  double* LWb = W + 8 * MD;   // [2][4][MD] (L D) of panel k
+  double* LSb = W + 16 * MD;  // [2][4][MD] L of panel k
+  double* Dv = W + 24 * MD;   // [MD] pivots
+  double* yf = W + 25 * MD;   // [MD] forward-substituted rhs of the diagonal rows
+  const bool pw = tid < 64;   // the panel wave
+  // waves 1-3: trailing tile (tr, tc), tc >= 2, row-major over the lower triangle
+  const int u = tid - 64;
+  int trp = 0;
+  while ((trp + 1) * (trp + 2) / 2 <= u) trp++;
+  const int tr = 2 + trp, tc = 2 + (u - trp * (trp + 1) / 2);
+  const bool tile = !pw && tr < nb;
   double v[4][4];
 #pragma unroll
   for (int i = 0; i < 4; i++)
 #pragma unroll
-    for (int c = 0; c < 4; c++) v[i][c] = lower ? M[(4 * tr + i) * n + 4 * tc + c] : 0.0;
-  if (lower && tc == 0)
+    for (int c = 0; c < 4; c++) v[i][c] = tile ? M[(4 * tr + i) * n + 4 * tc + c] : 0.0;
+  if (tid < n)
 #pragma unroll
-    for (int i = 0; i < 4; i++)
+    for (int c = 0; c < 4; c++) PBq[4 * MD + c * MD + tid] = M[tid * n + 4 + c];  // column block 1
+  // prologue: panel 0 over rows 0 .. n-1 by the panel wave (lanes 0-3 also take rows 64 .. n-1)
+  if (pw) {
+    const int r = min(tid, n - 1);
+    double a4[4];
 #pragma unroll
-      for (int c = 0; c < 4; c++) PB[c * MD + 4 * tr + i] = v[i][c];
-  __syncthreads();
-  for (int kb = 0; kb < nb; kb++) {
-    const int k0 = 4 * kb;
-    if (tid < 64) {  // panel: rows k0 + lane and k0 + 64 + lane
-      const int r0 = k0 + lane, r1 = k0 + 64 + lane;
-      const bool v0 = r0 < n, v1 = r1 < n;
-      const int c0 = min(r0, n - 1), c1 = min(r1, n - 1);
-      double p0[4], p1[4];
+    for (int c = 0; c < 4; c++) a4[c] = M[r * n + c];
+    Panel4 P;
+    PanelOut o;
+    panel_coop(a4, yv[r], tid, P, o);
+    if (tid < n) panel_row_store(o, P, tid, tid, 0, LWb, LSb, LT, Dv, yf, yv);
+    if (tid + 64 < n) {
+      const int r2 = tid + 64;
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
-        p0[j] = PB[j * MD + c0];
-        p1[j] = PB[j * MD + c1];
-      }
-      double y0 = yv[c0], y1 = yv[c1];
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const double d = readlane_f64(p0[j], j);
-        const double dinv = fabs(d) > DBL_MIN ? 1.0 / d : 0.0;
-        const double l0 = lane > j ? p0[j] * dinv : 0.0, l1 = v1 ? p1[j] * dinv : 0.0;
-#pragma unroll
-        for (int jp = j + 1; jp < 4; jp++) {
-          const double aj = readlane_f64(p0[j], jp);  // A[k0+jp][k0+j]
-          p0[jp] = p0[jp] - l0 * aj;
-          p1[jp] = p1[jp] - l1 * aj;
-        }
-        const double yj = readlane_f64(y0, j);
-        y0 = y0 - l0 * yj;
-        y1 = y1 - l1 * yj;
-        if (lane == j) Dv[k0 + j] = d;
-        if (v0) {
-          LW[j * MD + r0] = p0[j];
-          LS[j * MD + r0] = l0;
-          if (lane > j) M[r0 * LSTR + k0 + j] = l0;
-        }
-        if (v1) {
-          LW[j * MD + r1] = p1[j];
-          LS[j * MD + r1] = l1;
-          M[r1 * LSTR + k0 + j] = l1;
-        }
-      }
-      if (v0) yv[r0] = y0;
-      if (v1) yv[r1] = y1;
+      for (int c = 0; c < 4; c++) a4[c] = M[r2 * n + c];
+      panel_row_uniform(a4, yv[r2], P, o);
+      panel_row_store(o, P, r2, r2, 0, LWb, LSb, LT, Dv, yf, yv);
     }
-    __syncthreads();
-    if (lower && tc > kb) {  // rank-4 update of a trailing lower tile
+  }
+  __syncthreads();
+  for (int k = 0; k + 1 < nb; k++) {
+    const int K0 = 4 * (k + 1);
+    const double* LWk = LWb + (k & 1) * 4 * MD;
+    const double* LSk = LSb + (k & 1) * 4 * MD;
+    if (trace && tid == 0 && k == 4) trace[16] = clock64();
+    if (pw) {  // panel k+1: row r = K0 + lane
+      const int l = tid, r = min(K0 + l, n - 1);
+      const double* PBc = PBq + ((k + 1) & 1) * 4 * MD;
+      double a4[4], lwk[4], lsd[4][4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        a4[j] = PBc[j * MD + r];
+        lwk[j] = LWk[j * MD + r];
+#pragma unroll
+        for (int c = 0; c < 4; c++) lsd[c][j] = LSk[j * MD + K0 + c];
+      }
+      const double yr = yv[r];
+#pragma unroll
+      for (int j = 0; j < 4; j++)  // block k's update of this row of column block k+1
+#pragma unroll
+        for (int c = 0; c < 4; c++) a4[c] = __builtin_fma(-lwk[j], lsd[c][j], a4[c]);
+      Panel4 P;
+      PanelOut o;
+      panel_coop(a4, yr, l, P, o);
+      if (K0 + l < n)
+        panel_row_store(o, P, r, l, K0, LWb + ((k + 1) & 1) * 4 * MD, LSb + ((k + 1) & 1) * 4 * MD, LT, Dv, yf, yv);
+      if (trace && tid == 0 && k == 4) trace[17] = clock64();
+    } else if (tile && tc >= k + 2) {  // block k's rank-4 update of a trailing tile
       double lw[4][4], ls[4][4];
 #pragma unroll
       for (int j = 0; j < 4; j++)
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-          lw[i][j] = LW[j * MD + 4 * tr + i];
-          ls[i][j] = LS[j * MD + 4 * tc + i];
+          lw[i][j] = LWk[j * MD + 4 * tr + i];
+          ls[i][j] = LSk[j * MD + 4 * tc + i];
         }
 #pragma unroll
       for (int j = 0; j < 4; j++)
@@ -1094,76 +1180,138 @@ __device__ __forceinline__ void ldlt_solve_blocked(double* M, double* W, double*
         for (int i = 0; i < 4; i++)
 #pragma unroll
           for (int c = 0; c < 4; c++) v[i][c] = __builtin_fma(-lw[i][j], ls[c][j], v[i][c]);
-      if (tc == kb + 1)
+      if (tc == k + 2) {
+        double* PBn = PBq + (k & 1) * 4 * MD;
 #pragma unroll
         for (int i = 0; i < 4; i++)
 #pragma unroll
-          for (int c = 0; c < 4; c++) PB[c * MD + 4 * tr + i] = v[i][c];
+          for (int c = 0; c < 4; c++) PBn[c * MD + 4 * tr + i] = v[i][c];
+      }
     }
+    if (trace && tid == 64 && k == 4) trace[18] = clock64();
     __syncthreads();
-    if (trace && tid == 0 && kb == 8) trace[14] = wall_clock64();  // mid-factorization checkpoint
+    if (trace && tid == 0 && k == 4) trace[19] = clock64();
+    if (trace && tid == 0 && k == 4) trace[12] = wall_clock64();
+    if (trace && tid == 0 && k == 8) trace[14] = wall_clock64();  // mid-factorization checkpoint
   }
-  // D^-1 z, then L^T x = D^-1 z by wave 0 (lane l owns rows l and l + 64)
-  if (tid < 64) {
-    const int i0 = tid, i1 = tid + 64;
-    const bool o0 = i0 < n, o1 = i1 < n;
-    const int c0 = min(i0, n - 1), c1 = min(i1, n - 1);
-    const double d0 = Dv[c0], d1 = Dv[c1];
-    double y0 = o0 && fabs(d0) > DBL_MIN ? yv[c0] / d0 : 0.0;
-    double y1 = o1 && fabs(d1) > DBL_MIN ? yv[c1] / d1 : 0.0;
-    double nb0 = M[(n - 1) * LSTR + c0], nb1 = M[(n - 1) * LSTR + c1];
-    for (int k = n - 1; k > 0; k--) {
-      const double b0 = nb0, b1 = nb1;  // L(k, i)
-      nb0 = M[(k - 1) * LSTR + c0];
-      nb1 = M[(k - 1) * LSTR + c1];
-      const double xk = k >= 64 ? readlane_f64(y1, k - 64) : readlane_f64(y0, k);
-      const double n0 = y0 - b0 * xk, n1 = y1 - b1 * xk;
-      y0 = i0 < k ? n0 : y0;
-      y1 = i1 < k ? n1 : y1;
+  // D^-1 z, then L^T x = D^-1 z by wave 0: lane i owns row i (< 64); rows 64 .. n-1 (at most the last block)
+  // are solved uniformly first.  Per 4-row block the unknowns are solved uniformly from the block's diagonal
+  // L entries, then every lane updates its row in decreasing k; LT is zero on and above the diagonal, so the
+  // updates need no masks and a row of the block ends equal to its unknown.
+  if (pw) {
+    const int i = tid;
+    const int ci = min(i, n - 1);
+    double y = i < n ? yf[ci] * rcp_f64(Dv[ci]) : 0.0;
+    int kb = nb - 1;
+    if (n > 64) {  // the last block (rows 64 .. 67)
+      const int k0 = 64;
+      double x[4];
+#pragma unroll
+      for (int j = 3; j >= 0; j--) {
+        double zz = yf[k0 + j] * rcp_f64(Dv[k0 + j]);
+#pragma unroll
+        for (int jj = 3; jj > j; jj--) zz = __builtin_fma(-LT[(k0 + j) * LSTR + k0 + jj], x[jj], zz);
+        x[j] = zz;
+      }
+#pragma unroll
+      for (int j = 3; j >= 0; j--) y = __builtin_fma(-LT[i * LSTR + k0 + j], x[j], y);
+      if (i < 4) yv[k0 + i] = i == 0 ? x[0] : i == 1 ? x[1] : i == 2 ? x[2] : x[3];
+      kb = 15;
     }
-    if (o0) yv[i0] = y0;
-    if (o1) yv[i1] = y1;
+    for (; kb >= 0; kb--) {
+      const int k0 = 4 * kb;
+      double z[4], Li[4], Ld[4][4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        z[j] = readlane_f64(y, k0 + j);
+        Li[j] = LT[i * LSTR + k0 + j];
+#pragma unroll
+        for (int jj = j + 1; jj < 4; jj++) Ld[jj][j] = LT[(k0 + j) * LSTR + k0 + jj];
+      }
+      double x[4];
+#pragma unroll
+      for (int j = 3; j >= 0; j--) {
+        double zz = z[j];
+#pragma unroll
+        for (int jj = 3; jj > j; jj--) zz = __builtin_fma(-Ld[jj][j], x[jj], zz);
+        x[j] = zz;
+      }
+#pragma unroll
+      for (int j = 3; j >= 0; j--) y = __builtin_fma(-Li[j], x[j], y);
+    }
+    if (i < n && i < 64) yv[i] = y;
+    if (trace && tid == 0) trace[13] = wall_clock64();
   }
 }
 
 __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
-  __shared__ double A[HS_MAXDIM * HS_MAXDIM];  // raw HA, then the scaled system, then Porth
+  __shared__ double A[HS_MAXDIM * HS_MAXDIM];  // raw HA, then the scaled system, then LDLT scratch
   __shared__ double B[HS_MAXDIM * (HS_MAXDIM + 1)];  // raw HSC, then the permuted system, then L
+  __shared__ double LT[HS_MAXDIM * (HS_MAXDIM + 1)];  // L^T of the factorization (zeroed at entry)
+  __shared__ double Nf[2 * HS_MAXDIM * HS_NNS];  // nullspace factors N | Npi (prefetched at entry)
+  __shared__ double tk[2 * HS_NNS];
   __shared__ double bf[HS_MAXDIM], Sv[HS_MAXDIM], xs[HS_MAXDIM], yv[HS_MAXDIM], px[HS_MAXDIM], dl[HS_MAXDIM];
+  __shared__ double dgs[HS_MAXDIM];  // |diagonal| of the scaled system (pivot keys)
   __shared__ float xF[HS_MAXDIM];
   __shared__ int pos[HS_MAXDIM], sorted_[HS_MAXDIM], elem_at[HS_MAXDIM], pos_of[HS_MAXDIM];
   __shared__ int s_it, s_tie;
-  HsDevState* st = a.st;
+  // the window state lives in LDS for the whole kernel: every field is touched by dependent scalar code
+  // (steps, SE3 updates, precalc), which would otherwise pay a global-memory round trip per access
+  __shared__ __align__(16) unsigned char st_raw[sizeof(HsDevState)];
+  static_assert(sizeof(HsDevState) % 8 == 0, "HsDevState is copied as 8-byte words");
+  HsDevState* st = reinterpret_cast<HsDevState*>(st_raw);
   const int tid = threadIdx.x, nt = SOLVE_NT;
-  const int nF = st->nF, n = 4 + 8 * nF, nn = n * n;
-  const double lambda = 1e-5;  // SOLVER_FIX_LAMBDA
   HS_TRACE(a, 0);
-  if (tid == 0) {
-    s_it = a.iteration >= 0 ? a.iteration : st->iteration;
-    s_tie = 0;
+  if (a.trace && threadIdx.x == 0) a.trace[10] = clock64();  // shader clock (effective-clock probe)
+  {
+    const uint2* gs = reinterpret_cast<const uint2*>(a.st);
+    uint2* ls = reinterpret_cast<uint2*>(st_raw);
+    for (int i = tid; i < (int)(sizeof(HsDevState) / 8); i += nt) ls[i] = gs[i];
   }
+  const bool solve = (a.flags & HS_SOLVE) != 0;
+  // entry prefetch (SOLVE): every global input of the solve is requested before the first barrier
+  const int nF = a.nF, n = 4 + 8 * nF, nn = n * n;
+  const unsigned inv_n = (unsigned)((0x100000000ull + n - 1) / n);  // idx / n == umulhi(idx, inv_n) for idx < n*n
+  double ha[SOLVE_NU], hs[SOLVE_NU];
+  float adh[2][8], adt[2][8];
+  if (solve) {
+#pragma unroll
+    for (int u = 0; u < SOLVE_NU; u++) {
+      const int idx = min(tid + u * nt, nn - 1);
+      ha[u] = a.HA[idx];
+      hs[u] = a.HSC[idx];
+    }
+    for (int idx = tid; idx < 2 * n * HS_NNS; idx += nt) Nf[idx] = a.Nproj[idx];
+    for (int idx = tid; idx < HS_MAXDIM * (HS_MAXDIM + 1); idx += nt) LT[idx] = 0.0;
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const int o = min(tid + k * nt, nF * nF * 8 - 1);
+      const int pair = o >> 3, c = o & 7, hh = pair / nF, tt = pair - hh * nF;
+      const float* aHf = a.adHostF + (hh + nF * tt) * 64;
+      const float* aTf = a.adTargetF + (hh + nF * tt) * 64;
+#pragma unroll
+      for (int rr = 0; rr < 8; rr++) {
+        adh[k][rr] = aHf[rr * 8 + c];
+        adt[k][rr] = aTf[rr * 8 + c];
+      }
+    }
+  }
+  if (tid == 0) s_tie = 0;
+  __syncthreads();
+  if (tid == 0) s_it = a.iteration >= 0 ? a.iteration : st->iteration;
+  const double lambda = 1e-5;  // SOLVER_FIX_LAMBDA
 
-  if (a.flags & HS_SOLVE) {
+  if (solve) {
     if (tid == 0 && a.energy_log) {
       a.energy_log[st->log_count] = a.sysE[0];
       st->log_count = st->log_count + 1;
     }
-    // stage the raw stitched systems: clamped (always valid) addresses, every load in flight before any use
-    {
-      double ha[SOLVE_NU], hs[SOLVE_NU];
 #pragma unroll
-      for (int u = 0; u < SOLVE_NU; u++) {
-        const int idx = min(tid + u * nt, nn - 1);
-        ha[u] = a.HA[idx];
-        hs[u] = a.HSC[idx];
+    for (int u = 0; u < SOLVE_NU; u++)
+      if (tid + u * nt < nn) {
+        A[tid + u * nt] = ha[u];
+        B[tid + u * nt] = hs[u];
       }
-#pragma unroll
-      for (int u = 0; u < SOLVE_NU; u++)
-        if (tid + u * nt < nn) {
-          A[tid + u * nt] = ha[u];
-          B[tid + u * nt] = hs[u];
-        }
-    }
     if (tid < n) {
       const int q = tid;
       dl[q] = q < 4 ? (double)(float)st->calib.value_minus_value_zero[q] : st->frames[(q - 4) / 8].delta[(q - 4) % 8];
@@ -1189,16 +1337,16 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     double v[SOLVE_NU];
 #pragma unroll
     for (int u = 0; u < SOLVE_NU; u++) {
-      const int ix = min(tid + u * nt, nn - 1), r = ix / n, c = ix - r * n;
+      const int ix = min(tid + u * nt, nn - 1), r = (int)__umulhi((unsigned)ix, inv_n), c = ix - r * n;
       const int idx = r * n + c, tdx = c * n + r;
       const int fr = r < 4 ? -1 : (r - 4) >> 3, fc = c < 4 ? -1 : (c - 4) >> 3;
       const double a0 = A[idx], a1 = A[tdx], b0 = B[idx], b1 = B[tdx], hl0 = px[r];
       const double hm = a.HM ? a.HM[idx] : 0.0;
       const bool sym = fr >= 0 && fc >= 0 && fr != fc, calrow = r < 4 && c >= 4;
-      const double ha = sym ? a0 + a1 : (calrow ? a1 : a0);
+      const double ha_ = sym ? a0 + a1 : (calrow ? a1 : a0);
       const double hsc = calrow ? b1 : b0;
       const double hl = r == c ? hl0 : 0.0;
-      double hv = (hl + hm) + ha;
+      double hv = (hl + hm) + ha_;
       hv = r == c ? hv * (1 + lambda) : hv;
       v[u] = hv - hsc * sc;
     }
@@ -1214,30 +1362,32 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     HS_TRACE(a, 8);
 #pragma unroll
     for (int u = 0; u < SOLVE_NU; u++)
-      if (tid + u * nt < nn) {
-        A[tid + u * nt] = v[u];
-      }
+      if (tid + u * nt < nn) A[tid + u * nt] = v[u];
     __syncthreads();
     HS_TRACE(a, 9);
-    if (tid < n) Sv[tid] = 1.0 / sqrt(A[tid * n + tid] + 10);
+    // scaling S = 1/sqrt(diag + 10); the pivot keys |S H S|_qq in the scaling's own operation order
+    if (tid < n) {
+      const double hqq = A[tid * n + tid];
+      const double sq = 1.0 / sqrt(hqq + 10);
+      Sv[tid] = sq;
+      dgs[tid] = fabs(sq * hqq * sq);
+      bf[tid] = sq * bf[tid];
+    }
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < SOLVE_NU; u++) {
-      const int ix = min(tid + u * nt, nn - 1), r = ix / n, c = ix - r * n;
-      const double sv = Sv[r] * A[r * n + c] * Sv[c];
-      if (tid + u * nt < nn) A[r * n + c] = sv;
+      const int ix = min(tid + u * nt, nn - 1), r = (int)__umulhi((unsigned)ix, inv_n), c = ix - r * n;
+      const double sv = Sv[r] * A[ix] * Sv[c];
+      if (tid + u * nt < nn) A[ix] = sv;
     }
-    if (tid < n) bf[tid] = Sv[tid] * bf[tid];
-    __syncthreads();
-    HS_TRACE(a, 1);
     // Eigen LDLT pivot order (left-looking: the pivot is the largest |original diagonal| among the remaining
     // ones, first current position on ties).  Stable descending order by |diag|; where values tie, the
     // swap sequence is replayed by one thread to get the exact positions.
     if (tid < n) {
-      const double w0 = fabs(A[tid * n + tid]);
+      const double w0 = dgs[tid];
       int rank = 0, tie = 0;
       for (int p = 0; p < n; p++) {
-        const double w = fabs(A[p * n + p]);
+        const double w = dgs[p];
         rank += (w > w0 || (w == w0 && p < tid)) ? 1 : 0;
         tie |= (p != tid && w == w0) ? 1 : 0;
       }
@@ -1248,12 +1398,13 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
       if (tie) s_tie = 1;
     }
     __syncthreads();
+    HS_TRACE(a, 1);
     if (s_tie && tid == 0) {
       int gs = 0;
       while (gs < n) {
-        const double gv = fabs(A[sorted_[gs] * n + sorted_[gs]]);
+        const double gv = dgs[sorted_[gs]];
         int ge = gs + 1;
-        while (ge < n && fabs(A[sorted_[ge] * n + sorted_[ge]]) == gv) ge++;
+        while (ge < n && dgs[sorted_[ge]] == gv) ge++;
         for (int kq = gs; kq < ge; kq++) {
           // remaining group members are sorted_[kq..ge) (selected ones are swapped to the front)
           int bq = kq, bp = pos_of[sorted_[kq]];
@@ -1275,42 +1426,51 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
       }
     }
     __syncthreads();
-    // the permuted system P S H S P^T and right-hand side for the single-wave factorization
-    for (int idx = tid; idx < nn; idx += nt) {
-      const int r = idx / n, c = idx - r * n;
-      B[idx] = A[pos[r] * n + pos[c]];
+    // the permuted system P S H S P^T and right-hand side for the factorization
+#pragma unroll
+    for (int u = 0; u < SOLVE_NU; u++) {
+      const int ix = tid + u * nt;
+      if (ix < nn) {
+        const int r = (int)__umulhi((unsigned)ix, inv_n), c = ix - r * n;
+        B[ix] = A[pos[r] * n + pos[c]];
+      }
     }
     if (tid < n) yv[tid] = bf[pos[tid]];
     __syncthreads();
     HS_TRACE(a, 2);
-    ldlt_solve_blocked(B, A, yv, n, tid, a.trace);
+    ldlt_solve_blocked(B, LT, A, yv, n, tid, a.trace);
     __syncthreads();
     HS_TRACE(a, 3);
+    if (tid < n) xs[pos[tid]] = Sv[pos[tid]] * yv[tid];
+    __syncthreads();
     HS_TRACE(a, 4);
-    for (int q = tid; q < n; q += nt) xs[pos[q]] = yv[q];
-    {
-      double po[SOLVE_NU];
-#pragma unroll
-      for (int u = 0; u < SOLVE_NU; u++) po[u] = a.Porth[min(tid + u * nt, nn - 1)];
-#pragma unroll
-      for (int u = 0; u < SOLVE_NU; u++)
-        if (tid + u * nt < nn) A[tid + u * nt] = po[u];
-    }
-    __syncthreads();
-    for (int q = tid; q < n; q += nt) xs[q] = Sv[q] * xs[q];
-    __syncthreads();
-    if (s_it >= 2) {  // SOLVER_ORTHOGONALIZE_X_LATER: x -= Porth x
-      for (int q = tid; q < n; q += nt) {
-        double s = 0.0;
-        for (int c = 0; c < n; c++) s += A[q * n + c] * xs[c];
-        px[q] = s;
+    if (s_it >= 2) {  // SOLVER_ORTHOGONALIZE_X_LATER: x -= P x, P = (N Npi^T + Npi N^T) / 2 (orthogonalize)
+      // t1 = Npi^T x, t2 = N^T x: 14 dot products over n, 4 lanes each
+      const int d = tid >> 2, part = tid & 3, len = n >> 2;
+      if (d < 2 * HS_NNS) {
+        const double* col = Nf + (d < HS_NNS ? n * HS_NNS : 0);  // Npi for t1, N for t2
+        const int kk = d % HS_NNS;
+        double sacc = 0.0;
+        for (int c = part * len; c < (part + 1) * len; c++) sacc = __builtin_fma(col[c * HS_NNS + kk], xs[c], sacc);
+        sacc += __shfl_xor(sacc, 1);
+        sacc += __shfl_xor(sacc, 2);
+        if (part == 0) tk[d] = sacc;
       }
       __syncthreads();
-      for (int q = tid; q < n; q += nt) xs[q] -= px[q];
+      if (tid < n) {
+        double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+        for (int kk = 0; kk < HS_NNS; kk++) {
+          s1 = __builtin_fma(Nf[tid * HS_NNS + kk], tk[kk], s1);
+          s2 = __builtin_fma(Nf[n * HS_NNS + tid * HS_NNS + kk], tk[HS_NNS + kk], s2);
+        }
+        xs[tid] -= 0.5 * (s1 + s2);
+      }
       __syncthreads();
     }
     // resubstituteF_MT: frame / calib steps, xAd, cstep
-    for (int q = tid; q < n; q += nt) {
+    if (tid < n) {
+      const int q = tid;
       const double xv = xs[q];
       if (!isfinite(xv)) st->status = 1;
       xF[q] = (float)xv;
@@ -1325,15 +1485,18 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     }
     __syncthreads();
     if (tid < 4) st->cstep[tid] = xF[tid];
-    for (int o = tid; o < nF * nF * 8; o += nt) {
-      const int pair = o >> 3, c = o & 7;
-      const int hh = pair / nF, tt = pair % nF;  // xAd[nF*h + t]
-      const float* aHf = a.adHostF + (hh + nF * tt) * 64;
-      const float* aTf = a.adTargetF + (hh + nF * tt) * 64;
-      float s1 = 0.f, s2 = 0.f;
-      for (int rr = 0; rr < 8; rr++) s1 += xF[4 + 8 * hh + rr] * aHf[rr * 8 + c];
-      for (int rr = 0; rr < 8; rr++) s2 += xF[4 + 8 * tt + rr] * aTf[rr * 8 + c];
-      a.xAd[o] = s1 + s2;
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const int o = tid + k * nt;
+      if (o < nF * nF * 8) {
+        const int pair = o >> 3, hh = pair / nF, tt = pair - hh * nF;  // xAd[nF*h + t]
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int rr = 0; rr < 8; rr++) s1 += xF[4 + 8 * hh + rr] * adh[k][rr];
+#pragma unroll
+        for (int rr = 0; rr < 8; rr++) s2 += xF[4 + 8 * tt + rr] * adt[k][rr];
+        a.xAd[o] = s1 + s2;
+      }
     }
     // the consumed accumulation targets are zeroed for the next linearization (no barrier waits on these)
     for (int idx = tid; idx < nn; idx += nt) {
@@ -1396,6 +1559,13 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
       st->iteration = s_it + 1;
     }
   }
+  __syncthreads();
+  {  // write the window state back
+    const uint2* ls = reinterpret_cast<const uint2*>(st_raw);
+    uint2* gs = reinterpret_cast<uint2*>(a.st);
+    for (int i = tid; i < (int)(sizeof(HsDevState) / 8); i += nt) gs[i] = ls[i];
+  }
+  if (a.trace && threadIdx.x == 0) a.trace[11] = clock64();
   HS_TRACE(a, 15);
 }
 

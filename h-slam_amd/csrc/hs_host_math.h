@@ -262,7 +262,9 @@ inline void ldlt_solve(std::vector<double> A, int n, const std::vector<double>& 
 }
 
 // symmetric projector N (N^T N)^+ N^T with the reference's singular-value cut (one-sided Jacobi SVD)
-inline void nullspace_projector(const std::vector<std::vector<double>>& ns, int n, double cut, std::vector<double>& P) {
+// P = (N Npi^T + Npi N^T) / 2 (EnergyFunctional::orthogonalize); factors (nullable) = [N | Npi], each [n][m]
+inline void nullspace_projector(const std::vector<std::vector<double>>& ns, int n, double cut, std::vector<double>& P,
+                               std::vector<double>* factors = nullptr) {
   const int m = (int)ns.size();
   std::vector<double> U(n * m), V(m * m, 0.0);
   for (int j = 0; j < m; j++) {
@@ -328,6 +330,10 @@ inline void nullspace_projector(const std::vector<std::vector<double>>& ns, int 
   P.assign(n * n, 0.0);
   for (int i = 0; i < n; i++)
     for (int j = 0; j < n; j++) P[i * n + j] = 0.5 * (NNpiT[i * n + j] + NNpiT[j * n + i]);
+  if (factors) {
+    factors->assign(N.begin(), N.end());
+    factors->insert(factors->end(), Npi.begin(), Npi.end());
+  }
 }
 
 }  // namespace hs

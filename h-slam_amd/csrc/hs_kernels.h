@@ -7,6 +7,9 @@
 #include "hs_host_math.h"
 #include "hs_layout.h"
 
+constexpr int HS_SOLVE_NT = 256;  // hs_k_solve workgroup size
+constexpr int HS_NNS = 7;         // gauge nullspaces: 6 pose + 1 scale (System::getNullspaces)
+
 // Window state owned by the device between GN iterations (updated by hs_k_solve).
 struct HsDevState {
   hs::FrameH frames[HS_MAXF];
@@ -108,6 +111,7 @@ enum { HS_SOLVE = 1, HS_APPLY = 2 };
 struct HsSolveArgs {
   int flags;
   int iteration;               // < 0: use st->iteration
+  int nF;                      // window size (== st->nF)
   HsDevState* st;
   double* HA;                  // HA | bA | HSC | bSC, consumed then zeroed (SOLVE)
   double* bA;
@@ -115,7 +119,7 @@ struct HsSolveArgs {
   double* bSC;
   const double* HM;            // nullable: marginalization prior is zero
   const double* bM;
-  const double* Porth;         // [n*n] nullspace projector
+  const double* Nproj;         // [2][n][HS_NNS] nullspace factors N | Npi (P = (N Npi^T + Npi N^T) / 2)
   const float* adHostF;        // [nF*nF][64]
   const float* adTargetF;
   float* xAd;                  // out [nF*nF][8]
