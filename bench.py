@@ -31,6 +31,22 @@ BYTES_PER_PRES = 448      # algorithmic bytes per point-residu
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
+def pmc_traffic(points: int, kernel: str = "hs_k_linearize"):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/*_pmc_traffic.json,
+    made by tools/pmc.sh + tools/pmc_summary.py: separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this
+    bench at the same --points).  None when no pass at this size has been committed."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+            k = d["points_per_gpu"][str(points)][kernel]
+            return k["hbm_bytes_per_launch"], os.path.relpath(f, ROOT)
+        except (KeyError, ValueError, OSError):
+            continue
+    return None, None
+
+
 def cpu_baseline(points: int, seconds: float):
     """Oracle (C++ restatement of the reference CPU path, -O2 -march=x86-64-v3) on this host."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -129,6 +145,7 @@ def main():
     nt = max(1, tim["timed_iters"])
     lin_ms = tim["linearize_ms"] / nt
     achieved = BYTES_PER_PRES * shard.n_res / (lin_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(args.points) if world == 1 else (None, None)
     result = {
         "metric": METRIC,
         "value": n_res_total * args.steps / dt,
@@ -158,7 +175,8 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_source": traffic_src,
             "bytes_per_unit": BYTES_PER_PRES,
             "units_per_launch": shard.n_res,
             "avg_launch_ms": lin_ms,
