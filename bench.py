@@ -23,6 +23,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "h-slam_amd"))
 
@@ -85,8 +87,124 @@ def cpu_baseline(points: int, seconds: float):
     }
 
 
+TRACE_BYTES_PER_STEP = 8 * 4 * 12   # SURVEY.md §8(d) traceOn unit: 8 pattern taps x 4 texels x 12 B per search step
+
+
+def bench_trace(args):
+    """C5 (BASELINE.json configs[4]): ImmaturePoint::traceOn of 20k immature points (8 hosts x 2.5k, KITTI
+    1232x368, first trace: idepth_max = NaN, full maxPixSearch).  One step = the ImmaturePoint ctor of every
+    point on the device (a fresh first-trace state) + traceNewCoarse over all of them.  Single GPU
+    (traceOn shards by point with no collective)."""
+    from hslam_amd.scene import make_trace_scene
+    from hslam_amd.trace import ImmatureTracer
+
+    s = make_trace_scene(n_points=args.points if args.points != 2000 else 20000)
+    t = ImmatureTracer(s.width, s.height, s.n_points)
+    t.set_scene(s)
+    for _ in range(max(1, args.warmup)):
+        t.reinit()
+        t.traceNewCoarse(s.KRKi, s.Kt, s.aff, counts=False)
+    t.last_stats()
+    kern, steps = 0.0, 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        t.reinit()
+        t.traceNewCoarse(s.KRKi, s.Kt, s.aff, counts=False)
+        ms, st = t.last_stats()  # waits for the step: per-step device time of the traceOn kernel
+        kern += ms
+        steps += st
+    dt = time.perf_counter() - t0
+    counts = t.traceNewCoarse(s.KRKi, s.Kt, s.aff)  # one more (second-trace state) only for the tallies
+    kern_ms = kern / args.steps
+    algo_bytes = steps / args.steps * TRACE_BYTES_PER_STEP
+    achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
+    res = {
+        "metric": "immature points traced/sec (ImmaturePoint::traceOn, C5 KITTI 1232x368, 20k points)",
+        "value": s.n_points * args.steps / dt, "unit": "points/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": dt * 1e3 / args.steps, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": "C5 (BASELINE.json configs[4]) traceOn part: ctor + first traceOn of 20k immature "
+                               "points, 8 host KFs, 1232x368", "points": s.n_points, "hosts": s.n_hosts,
+                   "search_steps_per_trace": steps // args.steps, "parallelism": "single GPU"},
+        "roofline": {"bound": "hbm", "kernel": "hs_k_trace_on", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "bytes_per_unit": TRACE_BYTES_PER_STEP, "unit_of_bytes": "discrete-search step (GN taps excluded)",
+                     "avg_launch_ms": kern_ms},
+        "second_trace_counts": dict(zip(("good", "oob", "outlier", "skipped", "badcondition", "uninitialized"),
+                                        map(int, counts))),
+        "cpu_baseline": None,
+    }
+    if not args.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        from oracle_ffi import OracleTracer  # test infrastructure: the CPU baseline leg only
+        o = OracleTracer(s.width, s.height, fast=True)
+        o.set_scene(s)
+        n, tt = 0, 0.0
+        while tt < args.cpu_seconds / 2 and n < 200:
+            o2 = OracleTracer(s.width, s.height, fast=True)
+            o2.set_scene(s)
+            t1 = time.perf_counter()
+            o2.trace(s.new_img, s.KRKi, s.Kt, s.aff)
+            tt += time.perf_counter() - t1
+            n += 1
+        res["cpu_baseline"] = {"value": s.n_points * n / tt, "unit": "points/s", "cores": 1, "kind": "port",
+                               "sample": f"{n} first traces of the same 20k points (System::traceNewCoarse is serial "
+                                         "in the reference, Src/Mapping.cpp:494-538), ctor excluded"}
+        res["speedup_vs_cpu"] = res["value"] / res["cpu_baseline"]["value"]
+    t.close()
+    return res
+
+
+def bench_track(args):
+    """C2 (BASELINE.json configs[1]): CoarseTracker::trackNewestCoarse, 5-level pyramid, 640x480, one
+    hypothesis from identity.  One step = one trackNewestCoarse on the device."""
+    from hslam_amd.scene import make_track_scene
+    from hslam_amd.track import CoarseTracker
+
+    s = make_track_scene(n_points=2000, n_levels=5)
+    ct = CoarseTracker(s.width, s.height, s.K4, s.n_levels)
+    ct.set_scene(s)
+    T0 = np.array([0, 0, 0, 1.0, 0, 0, 0])
+    minRes = np.full(5, np.nan)
+    for _ in range(max(1, args.warmup)):
+        ct.trackNewestCoarse(T0, [0.0, 0.0], s.n_levels - 1, minRes)
+    dev = 0.0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ok, T, a = ct.trackNewestCoarse(T0, [0.0, 0.0], s.n_levels - 1, minRes)
+        dev += ct.last_ms()
+    dt = time.perf_counter() - t0
+    res = {
+        "metric": "frames tracked/sec (CoarseTracker::trackNewestCoarse, C2 640x480, 5 levels)",
+        "value": args.steps / dt, "unit": "frames/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": dt * 1e3 / args.steps, "higher_is_better": True, "scaling": "replicas only",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": "C2 (BASELINE.json configs[1]): trackNewestCoarse from identity, 2000 reference "
+                               "points, 640x480, 5 levels", "ok": bool(ok), "device_ms_per_track": dev / args.steps},
+        "cpu_baseline": None,
+    }
+    if not args.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        from oracle_ffi import OracleTracker  # test infrastructure: the CPU baseline leg only
+        o = OracleTracker(s.width, s.height, s.K4, s.n_levels, fast=True)
+        o.set_scene(s)
+        n, tt = 0, 0.0
+        while tt < args.cpu_seconds / 2 and n < 500:
+            t1 = time.perf_counter()
+            o.track(T0, [0.0, 0.0], s.n_levels - 1, minRes)
+            tt += time.perf_counter() - t1
+            n += 1
+        res["cpu_baseline"] = {"value": n / tt, "unit": "frames/s", "cores": 1, "kind": "port",
+                               "sample": f"{n} trackNewestCoarse calls (the reference's SSE path is single-threaded)"}
+        res["speedup_vs_cpu"] = res["value"] / res["cpu_baseline"]["value"]
+    ct.close()
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", choices=("ba", "trace", "track"), default="ba",
+                    help="ba = the headline metric (C4); trace = C5 traceOn; track = C2 CoarseTracker")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
@@ -94,6 +212,10 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
+    if args.workload != "ba":
+        res = bench_trace(args) if args.workload == "trace" else bench_track(args)
+        print(json.dumps(res))
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -43,7 +43,10 @@ class hs_params(C.Structure):
         "overallEnergyTHWeight", "idepthFixPrior", "initialCalibHessian", "affineOptModeA", "affineOptModeB",
         "initialRotPrior", "initialTransPrior", "initialAffAPrior", "initialAffBPrior")] + [
         ("solverModeDelta", C.c_double), ("thOptIterations", C.c_float), ("coarseCutoffTH", C.c_float),
-        ("minOptIterations", C.c_int), ("pad", C.c_int)]
+        ("minOptIterations", C.c_int), ("pad", C.c_int)] + [(n, C.c_float) for n in (
+        "outlierTH", "maxPixSearch", "trace_slackInterval", "trace_stepsize", "trace_minImprovementFactor",
+        "trace_GNThreshold", "trace_extraSlackOnTH")] + [
+        ("minTraceTestRadius", C.c_int), ("trace_GNIterations", C.c_int), ("pad2", C.c_int)]
 
 
 # exported symbols of include/hs_ba.h (argument types)
@@ -78,6 +81,18 @@ SIGNATURES = {
     "hs_tracker_track_tries": ([VP, I, VP, VP, VP, C.c_float, VP, VP, VP, VP, VP, VP], I),
     "hs_tracker_get_lm_log": ([VP, I, I, VP, VP, VP, VP, VP], I),
     "hs_tracker_last_ms": ([VP, VP], I),
+    # include/hs_trace.h
+    "hs_tracer_create": ([VP, VP, I, I, I, I], I),
+    "hs_tracer_destroy": ([VP], None),
+    "hs_tracer_set_host_image": ([VP, I, VP], I),
+    "hs_tracer_add_points": ([VP, I, VP, VP, VP], I),
+    "hs_tracer_clear": ([VP], I),
+    "hs_tracer_set_state": ([VP] * 5, I),
+    "hs_tracer_set_frame": ([VP, VP], I),
+    "hs_tracer_trace": ([VP, I, VP, VP], I),
+    "hs_tracer_get_points": ([VP] * 12, I),
+    "hs_tracer_reinit": ([VP], I),
+    "hs_tracer_last_stats": ([VP, VP, VP], I),
 }
 
 _lib = None

@@ -496,3 +496,98 @@ def make_track_scene(n_points: int = 2000, width: int = 640, height: int = 480, 
                       pt_u=u.astype(np.float32), pt_v=v.astype(np.float32), pt_idepth=idp.astype(np.float32),
                       pt_hdi=hdi.astype(np.float32), T_true=se3_data(dR, dt), aff_true=np.array([a, b]),
                       planes=planes)
+
+
+# ----------------------------------------------------------------- immature-point tracing (C5)
+@dataclass
+class TraceScene:
+    width: int
+    height: int
+    K: np.ndarray                 # level-0 intrinsics (fp64)
+    host_imgs: list               # per host KF: DirPyr[0] (h, w, 3) float32
+    new_img: np.ndarray           # the new frame's DirPyr[0]
+    KRKi: np.ndarray              # [nH, 9] float32 (traceNewCoarse, Src/Mapping.cpp:505-507)
+    Kt: np.ndarray                # [nH, 3] float32
+    aff: np.ndarray               # [nH, 2] float32 (AffLight::fromToVecExposure host -> new)
+    pt_host: np.ndarray           # [n] int32
+    pt_u: np.ndarray              # [n] float32
+    pt_v: np.ndarray
+    pt_idepth_true: np.ndarray    # [n] float64 (ground truth, for interval variants)
+    planes: list = field(default=None, repr=False)
+
+    @property
+    def n_points(self):
+        return len(self.pt_u)
+
+    @property
+    def n_hosts(self):
+        return len(self.host_imgs)
+
+    def finite_intervals(self, seed: int = 3):
+        """A second-trace state: [idepth_min, idepth_max] around the true idepth with widths from 0.2% to 60%
+        (mixes SKIPPED, BADCONDITION and GOOD), some intervals offset so the truth lies outside."""
+        rng = np.random.default_rng(seed)
+        n = self.n_points
+        w = np.exp(rng.uniform(np.log(0.002), np.log(0.6), n))
+        c = self.pt_idepth_true * (1.0 + rng.normal(0, 0.05, n))
+        lo = np.maximum(c * (1.0 - w), 0.0)
+        hi = c * (1.0 + w)
+        return lo.astype(np.float32), hi.astype(np.float32)
+
+
+def make_trace_scene(n_points: int = 20000, n_hosts: int = 8, width: int = 1232, height: int = 368, K=None,
+                     seed: int = SEED, spacing: float = 0.02, new_offset=(0.02, 0.03, 0.01), a: float = 0.05,
+                     b: float = 3.0, max_rot_deg: float = 0.5, subpixel_frac: float = 0.3) -> TraceScene:
+    """n_hosts keyframes spaced `spacing` m along x and one new frame `new_offset` past the last one, relit by
+    I_new = e^a I + b.  n_points immature points (n_points / n_hosts per host) at the top-gradient pixel per
+    cell (a fraction at sub-pixel positions).  Default = C5 (KITTI 1232x368, 20k points, 8 hosts)."""
+    rng = np.random.default_rng(seed + 13)
+    if K is None:
+        K = (np.array([[718.856, 0, 615.5], [0, 718.856, 183.5], [0, 0, 1.0]]) if width >= 1000
+             else np.array([[256.0, 0, 319.5], [0, 254.4, 239.5], [0, 0, 1.0]]))
+    K = np.asarray(K, dtype=np.float64)
+    f = K[0, 0]
+    planes = [make_plane(rng, 5.0, f), make_plane(rng, 3.0, f, xmax=-0.25), make_plane(rng, 2.0, f, xmin=0.55, ymax=0.15)]
+    poses = []
+    imgs = []
+    for i in range(n_hosts + 1):
+        ax = rng.normal(size=3)
+        ax /= np.linalg.norm(ax)
+        R_c2w = rodrigues(ax * math.radians(rng.uniform(0, max_rot_deg)))
+        C = (np.array([spacing * i, 0.0, 0.0]) if i < n_hosts
+             else np.array([spacing * (n_hosts - 1), 0.0, 0.0]) + np.asarray(new_offset, np.float64))
+        img, _ = render(planes, K, R_c2w, C, width, height, *((a, b) if i == n_hosts else (0.0, 0.0)))
+        imgs.append(make_dir_pyramid(img, 1)[0])
+        poses.append((R_c2w, C))
+    Rn_c2w, Cn = poses[-1]
+    Rn_w2c = Rn_c2w.T
+    KRKi, Kt, aff = [], [], []
+    Ki = np.linalg.inv(K)
+    for i in range(n_hosts):
+        Rh_c2w, Ch = poses[i]
+        R = Rn_w2c @ Rh_c2w                  # hostToNew = worldToNew * hostToWorld
+        t = Rn_w2c @ (Ch - Cn)
+        KRKi.append((K @ R @ Ki).astype(np.float32).reshape(9))
+        Kt.append((K @ t).astype(np.float32))
+        aff.append(np.array([math.exp(a), b], np.float32))
+    per = [n_points // n_hosts + (1 if i < n_points % n_hosts else 0) for i in range(n_hosts)]
+    hosts, us, vs, idt = [], [], [], []
+    for h in range(n_hosts):
+        if per[h] == 0:
+            continue
+        pix = _select_points(imgs[h], per[h], 8, rng)
+        Rh_c2w, Ch = poses[h]
+        _, depth = render_depth_at(planes, K, Rh_c2w, Ch, pix)
+        u = pix[:, 1].astype(np.float64)
+        v = pix[:, 0].astype(np.float64)
+        sub = rng.uniform(size=len(u)) < subpixel_frac
+        u[sub] += rng.uniform(-0.45, 0.45, sub.sum())
+        v[sub] += rng.uniform(-0.45, 0.45, sub.sum())
+        hosts.append(np.full(len(u), h, np.int32))
+        us.append(u.astype(np.float32))
+        vs.append(v.astype(np.float32))
+        idt.append(1.0 / depth)
+    return TraceScene(width=width, height=height, K=K, host_imgs=imgs[:n_hosts], new_img=imgs[-1],
+                      KRKi=np.array(KRKi), Kt=np.array(Kt), aff=np.array(aff), pt_host=np.concatenate(hosts),
+                      pt_u=np.concatenate(us), pt_v=np.concatenate(vs), pt_idepth_true=np.concatenate(idt),
+                      planes=planes)

@@ -99,6 +99,17 @@ typedef struct hs_params {
   float coarseCutoffTH;          /* 20     :77 */
   int minOptIterations;          /* 1      :61 */
   int pad;
+  /* ImmaturePoint (ctor + traceOn, Src/ImmaturePoint.cpp:7-350) */
+  float outlierTH;               /* 12*12  :65 */
+  float maxPixSearch;            /* 0.027  :85 */
+  float trace_slackInterval;     /* 1.5    :87 */
+  float trace_stepsize;          /* 1      :88 */
+  float trace_minImprovementFactor; /* 2   :89 */
+  float trace_GNThreshold;       /* 0.1    :92 */
+  float trace_extraSlackOnTH;    /* 1.2    :93 */
+  int minTraceTestRadius;        /* 2      :90 */
+  int trace_GNIterations;        /* 3      :91 */
+  int pad2;
 } hs_params;
 
 #ifdef __cplusplus

@@ -140,6 +140,16 @@ inline void params_default(hs_params* p) {
   p->coarseCutoffTH = 20;
   p->minOptIterations = 1;
   p->pad = 0;
+  p->outlierTH = 12 * 12;
+  p->maxPixSearch = 0.027f;
+  p->trace_slackInterval = 1.5f;
+  p->trace_stepsize = 1.0f;
+  p->trace_minImprovementFactor = 2;
+  p->trace_GNThreshold = 0.1f;
+  p->trace_extraSlackOnTH = 1.2f;
+  p->minTraceTestRadius = 2;
+  p->trace_GNIterations = 3;
+  p->pad2 = 0;
 }
 
 }  // namespace hso

@@ -42,7 +42,10 @@ class hs_params(C.Structure):
         "overallEnergyTHWeight", "idepthFixPrior", "initialCalibHessian", "affineOptModeA", "affineOptModeB",
         "initialRotPrior", "initialTransPrior", "initialAffAPrior", "initialAffBPrior")] + [
         ("solverModeDelta", C.c_double), ("thOptIterations", C.c_float), ("coarseCutoffTH", C.c_float),
-        ("minOptIterations", C.c_int), ("pad", C.c_int)]
+        ("minOptIterations", C.c_int), ("pad", C.c_int)] + [(n, C.c_float) for n in (
+        "outlierTH", "maxPixSearch", "trace_slackInterval", "trace_stepsize", "trace_minImprovementFactor",
+        "trace_GNThreshold", "trace_extraSlackOnTH")] + [
+        ("minTraceTestRadius", C.c_int), ("trace_GNIterations", C.c_int), ("pad2", C.c_int)]
 
 
 def build(quiet=True):
@@ -100,6 +103,14 @@ def load(fast=False):
     lib.hso_trk_get_log.argtypes = [vp, C.c_int, vp, vp, vp, vp]
     lib.hso_trk_get_log.restype = C.c_int
     lib.hso_trk_track_tries.argtypes = [vp, C.c_int, vp, vp, vp, C.c_float, C.c_int] + [vp] * 6
+    lib.hso_trc_create.restype = vp
+    lib.hso_trc_create.argtypes = [vp, C.c_int, C.c_int]
+    lib.hso_trc_destroy.argtypes = [vp]
+    lib.hso_trc_add_points.argtypes = [vp, C.c_int, vp, C.c_int, vp, vp, vp]
+    lib.hso_trc_add_points.restype = C.c_int
+    lib.hso_trc_set_state.argtypes = [vp] * 5
+    lib.hso_trc_trace.argtypes = [vp] * 4
+    lib.hso_trc_get.argtypes = [vp] * 11
     _LIBS[name] = lib
     return lib
 
@@ -347,3 +358,66 @@ class OracleTracker:
                                      _p(np.ascontiguousarray(lastCoarseRMSE, np.float64)), float(reTrackThreshold),
                                      coarsest, _p(T), _p(a), _p(ach), _p(fl), C.byref(good), C.byref(n))
         return dict(T=T, aff=a, achievedRes=ach, flowVecs=fl, haveOneGood=bool(good.value), tryIterations=n.value)
+
+
+# ------------------------------------------------------------------ ImmaturePoint::traceOn restatement
+TRACE_FIELDS = ("status", "idepth_min", "idepth_max", "quality", "uv", "interval", "energyTH", "color", "weights",
+                "gradH")
+
+
+def trace_hosts_array(KRKi, Kt, aff):
+    """[nH] hs_trace_host records (KRKi[9], Kt[3], aff[2] float32) as a contiguous float32 [nH, 14] array."""
+    return np.ascontiguousarray(np.concatenate([np.asarray(KRKi, np.float32).reshape(-1, 9),
+                                                np.asarray(Kt, np.float32).reshape(-1, 3),
+                                                np.asarray(aff, np.float32).reshape(-1, 2)], 1))
+
+
+class OracleTracer:
+    """ImmaturePoint ctor + System::traceNewCoarse / traceOn as a CPU restatement (oracle/trace_oracle.cpp)."""
+
+    def __init__(self, width, height, params=None, fast=False):
+        self.lib = load(fast)
+        self.params = params if params is not None else default_params()
+        self.W, self.H = width, height
+        self.h = self.lib.hso_trc_create(C.byref(self.params), width, height)
+        self.n = 0
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.lib.hso_trc_destroy(self.h)
+            self.h = None
+
+    def add_points(self, host_imgs, host, u, v):
+        imgs = [np.ascontiguousarray(a, np.float32) for a in host_imgs]
+        pp = (C.c_void_p * len(imgs))(*[a.ctypes.data for a in imgs])
+        h, uu, vv = (np.ascontiguousarray(host, np.int32), np.ascontiguousarray(u, np.float32),
+                     np.ascontiguousarray(v, np.float32))
+        rc = self.lib.hso_trc_add_points(self.h, len(imgs), C.cast(pp, C.c_void_p), len(h), _p(h), _p(uu), _p(vv))
+        assert rc == 0
+        self.n += len(h)
+
+    def set_state(self, idepth_min=None, idepth_max=None, quality=None, status=None):
+        arr = [None if a is None else np.ascontiguousarray(a, dt)
+               for a, dt in ((idepth_min, np.float32), (idepth_max, np.float32), (quality, np.float32),
+                             (status, np.uint8))]
+        self.lib.hso_trc_set_state(self.h, *[_p(a) for a in arr])
+
+    def trace(self, new_img, KRKi, Kt, aff):
+        img = np.ascontiguousarray(new_img, np.float32)
+        hosts = trace_hosts_array(KRKi, Kt, aff)
+        counts = np.zeros(6, np.int32)
+        self.lib.hso_trc_trace(self.h, _p(img), _p(hosts), _p(counts))
+        return counts
+
+    def set_scene(self, s):
+        self.add_points(s.host_imgs, s.pt_host, s.pt_u, s.pt_v)
+
+    def points(self):
+        n = self.n
+        out = dict(status=np.zeros(n, np.uint8), idepth_min=np.zeros(n, np.float32),
+                   idepth_max=np.zeros(n, np.float32), quality=np.zeros(n, np.float32), uv=np.zeros((n, 2), np.float32),
+                   interval=np.zeros(n, np.float32), energyTH=np.zeros(n, np.float32),
+                   color=np.zeros((n, 8), np.float32), weights=np.zeros((n, 8), np.float32),
+                   gradH=np.zeros((n, 4), np.float32))
+        self.lib.hso_trc_get(self.h, *[_p(out[k]) for k in TRACE_FIELDS])
+        return out

@@ -53,3 +53,23 @@ def test_params_default_and_no_device_error():
         rc = _lib.load().hs_create(ctypes.byref(h), ctypes.byref(p), 0)
         assert rc != 0  # fails loudly: no CPU fallback
         assert b"device" in _lib.load().hs_last_error()
+
+
+def test_ctypes_structs_match_c_layout(tmp_path):
+    """The ctypes mirrors (hslam_amd._lib, oracle_ffi) have the C structs' sizes (compiled here with gcc)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "h-slam_amd"))
+    from hslam_amd import _lib
+    src = tmp_path / "sz.c"
+    src.write_text('#include <stdio.h>\n#include "hs_types.h"\n#include "hs_trace.h"\n'
+                   'int main(void){printf("%zu %zu %zu %zu %zu %zu\\n", sizeof(hs_params), sizeof(hs_camera),'
+                   ' sizeof(hs_frame), sizeof(hs_points), sizeof(hs_residuals), sizeof(hs_trace_host));return 0;}\n')
+    exe = tmp_path / "sz"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    sizes = list(map(int, subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()))
+    py = [ctypes.sizeof(c) for c in (_lib.hs_params, _lib.hs_camera, _lib.hs_frame, _lib.hs_points,
+                                     _lib.hs_residuals)] + [14 * 4]
+    assert sizes == py, (sizes, py)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_ffi
+    assert ctypes.sizeof(oracle_ffi.hs_params) == sizes[0]
