@@ -210,6 +210,7 @@ static int launch_linearize(hs_ctx* c, int fuse) {
   a.nF = c->nF;
   a.write_center = 1;
   a.fuse_step = fuse;
+  for (int i = 0; i <= c->nF; i++) a.host_begin[i] = c->host_pt_begin[i];
   a.pre = c->d_pre;
   a.frameTH = c->d_frameTH;
   a.xAd = c->d_xAd;
@@ -286,10 +287,11 @@ static int launch_solve(hs_ctx* c, int flags, int iteration, bool log) {
 }
 
 static int reset_states(hs_ctx* c) {  // PointFrameResidual::resetOOB on every active residual
-  HS_HIP(hipMemsetAsync(c->d_r_state, HS_RES_IN, c->nR, c->stream));
-  HS_HIP(hipMemsetAsync(c->d_r_active, 0, c->nR, c->stream));
-  HS_HIP(hipMemsetAsync(c->d_r_energy, 0, sizeof(float) * c->nR, c->stream));
-  HS_HIP(hipMemsetAsync(c->d_r_newEnergy, 0, sizeof(float) * c->nR, c->stream));
+  const size_t P8 = (size_t)c->nP * 8;  // slot layout
+  HS_HIP(hipMemsetAsync(c->d_r_state, HS_RES_IN, P8, c->stream));
+  HS_HIP(hipMemsetAsync(c->d_r_active, 0, P8, c->stream));
+  HS_HIP(hipMemsetAsync(c->d_r_energy, 0, sizeof(float) * P8, c->stream));
+  HS_HIP(hipMemsetAsync(c->d_r_newEnergy, 0, sizeof(float) * P8, c->stream));
   return HS_OK;
 }
 
@@ -656,9 +658,10 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
   HS_TRY(dalloc(&c->d_color, P8)); HS_TRY(dalloc(&c->d_weight, P8));
   HS_TRY(dalloc(&c->d_res_of_slot, P8)); HS_TRY(dalloc(&c->d_res_order, P8));
   HS_TRY(dalloc(&c->d_pt_host, nP)); HS_TRY(dalloc(&c->d_host_pt_begin, nF + 1));
-  HS_TRY(dalloc(&c->d_r_state, nR)); HS_TRY(dalloc(&c->d_r_active, nR));
-  HS_TRY(dalloc(&c->d_r_energy, nR)); HS_TRY(dalloc(&c->d_r_newEnergy, nR)); HS_TRY(dalloc(&c->d_r_ewo, nR));
-  HS_TRY(dalloc(&c->d_r_center, (size_t)nR * 3));
+  // residual state in the slot layout [point][target slot] (P8 entries; slots without a residual unused)
+  HS_TRY(dalloc(&c->d_r_state, P8)); HS_TRY(dalloc(&c->d_r_active, P8));
+  HS_TRY(dalloc(&c->d_r_energy, P8)); HS_TRY(dalloc(&c->d_r_newEnergy, P8)); HS_TRY(dalloc(&c->d_r_ewo, P8));
+  HS_TRY(dalloc(&c->d_r_center, (size_t)P8 * 3));
   HS_TRY(dalloc(&c->d_p_actmask, nP)); HS_TRY(dalloc(&c->d_p_HdiF, nP)); HS_TRY(dalloc(&c->d_p_bdSumF, nP));
   HS_TRY(dalloc(&c->d_p_Hcd, (size_t)nP * 4)); HS_TRY(dalloc(&c->d_p_JpJdF, P8 * 8));
   HS_TRY(dalloc(&c->d_p_Jrec, P8 * HS_JREC)); HS_TRY(dalloc(&c->d_p_step, nP)); HS_TRY(dalloc(&c->d_p_energy, nP));
@@ -708,8 +711,13 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
   HS_HIP(hipMemcpy(c->d_adTargetF, c->adTargetF.data(), sizeof(float) * nF * nF * 64, hipMemcpyHostToDevice));
   HS_HIP(hipMemcpy(c->d_Nproj, c->Nproj.data(), sizeof(double) * 2 * n * HS_NNS, hipMemcpyHostToDevice));
   if (nR > 0) {
-    if (rs->state) HS_HIP(hipMemcpy(c->d_r_state, rs->state, nR, hipMemcpyHostToDevice));
-    else HS_TRY(reset_states(c));
+    if (rs->state) {
+      std::vector<uint8_t> slot_state(P8, HS_RES_OOB);
+      for (int r = 0; r < nR; r++) slot_state[(size_t)c->res_point[r] * 8 + c->res_target[r]] = rs->state[r];
+      HS_HIP(hipMemcpy(c->d_r_state, slot_state.data(), P8, hipMemcpyHostToDevice));
+    } else {
+      HS_TRY(reset_states(c));
+    }
   }
   HS_HIP(hipStreamSynchronize(c->stream));
   return HS_OK;
@@ -843,20 +851,36 @@ int hs_ba_get_residuals(hs_ctx* c, uint8_t* state, uint8_t* active, float* energ
   HS_HIP(hipStreamSynchronize(c->stream));
   const size_t m = c->nR;
   if (m == 0) return HS_OK;
-  if (state) HS_HIP(hipMemcpy(state, c->d_r_state, m, hipMemcpyDeviceToHost));
-  if (active) HS_HIP(hipMemcpy(active, c->d_r_active, m, hipMemcpyDeviceToHost));
-  if (energy) HS_HIP(hipMemcpy(energy, c->d_r_energy, m * 4, hipMemcpyDeviceToHost));
-  if (energy_wo) HS_HIP(hipMemcpy(energy_wo, c->d_r_ewo, m * 4, hipMemcpyDeviceToHost));
-  if (center) HS_HIP(hipMemcpy(center, c->d_r_center, m * 12, hipMemcpyDeviceToHost));
+  // slot layout [point][target] -> residual order
+  const size_t P8 = (size_t)c->nP * 8;
+  auto slot_of = [&](size_t r) { return (size_t)c->res_point[r] * 8 + c->res_target[r]; };
+  std::vector<uint8_t> act(P8);
+  HS_HIP(hipMemcpy(act.data(), c->d_r_active, P8, hipMemcpyDeviceToHost));
+  if (state) {
+    std::vector<uint8_t> v(P8);
+    HS_HIP(hipMemcpy(v.data(), c->d_r_state, P8, hipMemcpyDeviceToHost));
+    for (size_t r = 0; r < m; r++) state[r] = v[slot_of(r)];
+  }
+  if (active)
+    for (size_t r = 0; r < m; r++) active[r] = act[slot_of(r)];
+  for (auto pr : {std::make_pair(energy, c->d_r_energy), std::make_pair(energy_wo, c->d_r_ewo)}) {
+    if (!pr.first) continue;
+    std::vector<float> v(P8);
+    HS_HIP(hipMemcpy(v.data(), pr.second, P8 * 4, hipMemcpyDeviceToHost));
+    for (size_t r = 0; r < m; r++) pr.first[r] = v[slot_of(r)];
+  }
+  if (center) {
+    std::vector<float> v(P8 * 3);
+    HS_HIP(hipMemcpy(v.data(), c->d_r_center, P8 * 12, hipMemcpyDeviceToHost));
+    for (size_t r = 0; r < m; r++)
+      for (int i = 0; i < 3; i++) center[r * 3 + i] = v[slot_of(r) * 3 + i];
+  }
   if (JpJdF) {
     // slot layout [point][target][8] -> residual order; zero for inactive residuals
-    std::vector<float> slot((size_t)c->nP * 64);
-    std::vector<uint8_t> act(m);
+    std::vector<float> slot(P8 * 8);
     if (c->nP > 0) HS_HIP(hipMemcpy(slot.data(), c->d_p_JpJdF, slot.size() * 4, hipMemcpyDeviceToHost));
-    HS_HIP(hipMemcpy(act.data(), c->d_r_active, m, hipMemcpyDeviceToHost));
     for (size_t r = 0; r < m; r++)
-      for (int i = 0; i < 8; i++)
-        JpJdF[r * 8 + i] = act[r] ? slot[((size_t)c->res_point[r] * 8 + c->res_target[r]) * 8 + i] : 0.f;
+      for (int i = 0; i < 8; i++) JpJdF[r * 8 + i] = act[slot_of(r)] ? slot[slot_of(r) * 8 + i] : 0.f;
   }
   return HS_OK;
 }

@@ -28,8 +28,6 @@
 
 namespace {
 
-__constant__ int c_pattern[8][2] = {{0, -2}, {-1, -1}, {1, -1}, {-2, 0}, {0, 0}, {2, 0}, {-1, 1}, {0, 2}};
-
 constexpr float SCALE_F = 50.0f, SCALE_C = 50.0f, SCALE_IDEPTH = 1.0f;
 constexpr int Q_N = 17;  // per-pixel quantities summed over the pattern
 
@@ -81,13 +79,25 @@ struct BlkCnt {
   } while (0)
 
 struct LinLds {
-  float q[HS_MAXF][Q_N][8];
-  float dot[HS_MAXF][8];
   float s[HS_MAXF][Q_N + 3];
-  float econ[HS_MAXF];
-  float act[HS_MAXF];
-  float jx[HS_MAXF][4], jy[HS_MAXF][4], jd[HS_MAXF][2];
 };
+
+// lane l <- lane l-1 within each row of 16 (DPP row_shr:1; a row's lane 0 gets 0)
+__device__ __forceinline__ float dpp_shr1(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xf, 0xf, false));
+}
+// Left fold over the 8 lanes of each octet (= a target slot's pattern pixels): lane 8g+7 returns
+// ((((0 + x[8g]) + x[8g+1]) + ...) + x[8g+7]), the reference's running sum in pattern order, bit for bit
+// (step j: s[l] = s[l-1] + x[l], so after 7 steps lane 8g+7 holds the in-order fold of its octet).
+__device__ __forceinline__ float octet_fold(float x) {
+  float s = 0.f + x;
+#pragma unroll
+  for (int j = 0; j < 7; j++) s = dpp_shr1(s) + x;
+  return s;
+}
+__device__ __forceinline__ float readlane_f(float v, int lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
 
 // resubstituteFPt: the point's idepth step from the previous linearization's per-point data
 __device__ __forceinline__ float point_step(int p, int h, int nF, unsigned m, const float* cstep, const float* Hcd,
@@ -123,56 +133,70 @@ __global__ __launch_bounds__(64) void hs_k_linearize(HsLinArgs a) {
   const int k = lane & 7;   // pattern pixel
   const int p = blockIdx.x;
   const int nF = a.nF;
-  const int h = a.pt_host[p];
+  int h = 0;  // points are sorted by host: the host is found from the kernel-argument boundaries, no load
+#pragma unroll
+  for (int i = 1; i < HS_MAXF; i++) h += (i < nF && p >= a.host_begin[i]) ? 1 : 0;
   const HsCalib cal = a.st->dcal;
 
   HS_TRACE(a, 0);
-  // everything the linearization reads is loaded up front (independent of the fused point step)
+  // everything the linearization reads is loaded up front, unconditionally (clamped indices), so the
+  // prologue is ONE memory round trip: residual state is in the slot layout [point][target slot] and the
+  // host comes from the kernel arguments, so no load depends on another
+  const int sl = p * 8 + t;                 // this lane's residual slot
+  const int tc_ = t < nF ? t : 0;
   float idep = a.idepth[p], idep0 = a.idepth_zero[p];
   const float pu = a.u[p], pv = a.v[p];
-  const int r = a.res_of_slot[p * 8 + t];
-  const bool has = r >= 0;
-  const int st = has ? (int)a.r_state[r] : HS_RES_OOB;
-  const float oldE = has ? a.r_energy[r] : 0.f;
-  const float oldNewE = has ? a.r_newEnergy[r] : 0.f;
-  const float thr = fmaxf(a.frameTH[h], a.frameTH[t < nF ? t : 0]);  // std::max<float>(host TH, target TH)
+  const bool has = a.res_of_slot[sl] >= 0;
+  const int st_raw = (int)a.r_state[sl];
+  const float oldE_raw = a.r_energy[sl];
+  const float oldNewE_raw = a.r_newEnergy[sl];
+  const float thr = fmaxf(a.frameTH[h], a.frameTH[tc_]);  // std::max<float>(host TH, target TH)
   const float colorK = a.color[p * 8 + k], weightK = a.weight[p * 8 + k];
-  HsPrecalc pc;
-  if (has) pc = a.pre[h * nF + t];
+  const HsPrecalc pc = a.pre[h * nF + tc_];
+  // the target's image: selected from the kernel-argument pointers (uniform SGPRs), not loaded per lane
+  const float4* timg = a.img[0];
+#pragma unroll
+  for (int i = 1; i < HS_MAXF; i++) timg = (t == i) ? a.img[i] : timg;
   const uint2 ro2 = reinterpret_cast<const uint2*>(a.res_order)[p];  // the point's 8 residual-list slots
   auto res_slot = [&](int q) -> int { return (int)(int8_t)(((q < 4 ? ro2.x : ro2.y) >> (8 * (q & 3))) & 0xffu); };
+  // the previous linearization's per-point data for the fused step (read unconditionally: one batch)
+  const unsigned fm = a.p_actmask[p];
+  const float xad = a.xAd[(h * nF + tc_) * 8 + k];
+  const float jpj = a.p_JpJdF[sl * 8 + k];
+  const float bds = a.p_bdSumF[p], hdi = a.p_HdiF[p];
+  const float4 hcd = reinterpret_cast<const float4*>(a.p_Hcd)[p];
+  const float4 cs4 = *reinterpret_cast<const float4*>(a.st->cstep);
+  const float cs0 = cs4.x, cs1 = cs4.y, cs2 = cs4.z, cs3 = cs4.w;
+  // pin the batch: without this the compiler sinks the fused-step loads into the fuse_step branch, behind
+  // the wait for res_order (a second memory round trip)
+  asm volatile("" ::"v"(fm), "v"(xad), "v"(jpj), "v"(bds), "v"(hdi), "v"(hcd.x), "v"(hcd.y), "v"(hcd.z), "v"(hcd.w),
+               "v"(cs0), "v"(cs1), "v"(cs2), "v"(cs3), "v"(ro2.x), "v"(ro2.y));
   if (a.fuse_step) {
     // resubstituteFPt of the previous linearization (Src/EnergyFunctional.cpp:249-274) + the point part of
-    // doStepFromBackup (stepfacD = 1).  Lane (t, k) forms xAd[h][t][k] * JpJdF[t][k]; the sums then run
-    // in the reference order (k ascending per residual, residuals in list order).
-    const unsigned m = a.p_actmask[p];
-    L.dot[t][k] = ((m >> t) & 1u) ? a.xAd[(h * nF + t) * 8 + k] * a.p_JpJdF[(p * 8 + t) * 8 + k] : 0.f;
-    float step = 0.f;
-    const float bds = a.p_bdSumF[p], hdi = a.p_HdiF[p];
-    const float4 hcd = reinterpret_cast<const float4*>(a.p_Hcd)[p];
-    __syncthreads();  // every lane has read the previous per-point data before it is overwritten
-    if (lane == 0 && m != 0u) {
-      float b = bds;
-      const float* cs = a.st->cstep;
-      float dot = 0.f;
-      dot += cs[0] * hcd.x;
-      dot += cs[1] * hcd.y;
-      dot += cs[2] * hcd.z;
-      dot += cs[3] * hcd.w;
-      b -= dot;
-      for (int q = 0; q < 8; q++) {
-        const int tt = res_slot(q);
-        if (tt < 0) break;
-        if (!((m >> tt) & 1u)) continue;
-        float d = 0.f;
-        for (int i = 0; i < 8; i++) d += L.dot[tt][i];
-        b -= d;
-      }
-      step = -b * hdi;
+    // doStepFromBackup (stepfacD = 1).  Lane (t, k) forms xAd[h][t][k] * JpJdF[t][k]; the 8-term dot of a
+    // residual is an in-order octet fold, the residual terms are then subtracted in list order (uniform).
+    const unsigned m = fm;
+    const float prod = ((m >> t) & 1u) ? xad * jpj : 0.f;
+    const float dsum = octet_fold(prod);
+    // branch-free (no load-dependent scalar control flow here, so every prologue load is one batch):
+    // the list-order subtraction walks the point's residual slots with ds_bpermute reads of the folds
+    float b = bds;
+    float dot = 0.f;
+    dot += cs0 * hcd.x;
+    dot += cs1 * hcd.y;
+    dot += cs2 * hcd.z;
+    dot += cs3 * hcd.w;
+    b -= dot;
+    bool live = true;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int tt = res_slot(q);
+      live = live && tt >= 0;
+      const int ts = tt < 0 ? 0 : tt;
+      const float d = __shfl(dsum, ts * 8 + 7);
+      if (live && ((m >> ts) & 1u)) b -= d;
     }
-    if (lane == 0) L.dot[0][0] = step;
-    __syncthreads();
-    step = L.dot[0][0];
+    const float step = m != 0u ? -b * hdi : 0.f;
     idep = idep + 1.0f * step;
     idep0 = idep;
     if (lane == 0) {
@@ -181,6 +205,9 @@ __global__ __launch_bounds__(64) void hs_k_linearize(HsLinArgs a) {
       a.p_step[p] = step;
     }
   }
+  const int st = has ? st_raw : HS_RES_OOB;
+  const float oldE = has ? oldE_raw : 0.f;
+  const float oldNewE = has ? oldNewE_raw : 0.f;
   HS_TRACE(a, 1);
 
   bool oob = false;
@@ -249,8 +276,11 @@ __global__ __launch_bounds__(64) void hs_k_linearize(HsLinArgs a) {
         Jy[8] = u * v * fy;
         Jy[9] = u * fy;
 
-        // pattern pixel k
-        const float px = pu + c_pattern[k][0], py = pv + c_pattern[k][1];
+        // pattern pixel k (staticPattern[8], Include/GlobalTypes.h:181-184) as selects: a lane-indexed
+        // constant-memory table would cost a dependent memory round trip here
+        const int pdx = (k == 1 || k == 6) ? -1 : (k == 2) ? 1 : (k == 3) ? -2 : (k == 5) ? 2 : 0;
+        const int pdy = (k == 0) ? -2 : (k <= 2) ? -1 : (k <= 5) ? 0 : (k == 6) ? 1 : 2;
+        const float px = pu + pdx, py = pv + pdy;
         float q0 = pc.KRKi[0] * px + pc.KRKi[1] * py + pc.KRKi[2] * 1.f;
         float q1 = pc.KRKi[3] * px + pc.KRKi[4] * py + pc.KRKi[5] * 1.f;
         float q2 = pc.KRKi[6] * px + pc.KRKi[7] * py + pc.KRKi[8] * 1.f;
@@ -261,7 +291,10 @@ __global__ __launch_bounds__(64) void hs_k_linearize(HsLinArgs a) {
         if (!(PKu > 1.1f && PKv > 1.1f && PKu < (cal.W - 3) && PKv < (cal.H - 3))) {
           oob = true;
         } else {
-          const float3 hit = interp33(a.img[t], PKu, PKv, cal.W);
+          float3 hit = interp33(timg, PKu, PKv, cal.W);
+          // all three channels are materialised here: otherwise the compiler sinks the dI/dx, dI/dy loads
+          // under the isfinite(I) branch below, a second dependent memory round trip
+          asm volatile("" : "+v"(hit.x), "+v"(hit.y), "+v"(hit.z));
           const float color = colorK;
           const float residual = hit.x - (float)(pc.aff[0] * color + pc.aff[1]);
           const float drdA = (color - pc.b0);
@@ -307,129 +340,136 @@ __global__ __launch_bounds__(64) void hs_k_linearize(HsLinArgs a) {
   const bool slotOob = ((oobMask >> (t * 8)) & 0xffull) != 0ull;
   HS_TRACE(a, 2);
 
+  // sequential (pattern-order) sums = the reference's running sums: octet folds, published by lane k == 7
+  {
+    float sq[Q_N];
 #pragma unroll
-  for (int qi = 0; qi < Q_N; qi++) L.q[t][qi][k] = qv[qi];
-  __syncthreads();
-  // sequential (pattern-order) sums = the reference's running sums
-  for (int qi = k; qi < Q_N; qi += 8) {
-    float s = 0.f;
+    for (int qi = 0; qi < Q_N; qi++) sq[qi] = octet_fold(qv[qi]);
+    if (k == 7) {
 #pragma unroll
-    for (int kk = 0; kk < 8; kk++) s += L.q[t][qi][kk];
-    L.s[t][qi] = s;
-  }
-  __syncthreads();
-
-  // ---------------- state decision + applyRes (the 8 lanes of a slot agree; lane k == 0 writes)
-  bool active = false;
-  float econ = 0.f;
-  if (has) {
-    if (st == HS_RES_OOB) {
-      econ = oldE;  // linearize returns state_energy; applyRes returns early (OOB is sticky)
-      if (k == 0) a.r_ewo[r] = -1.f;
-    } else if (slotOob) {
-      econ = oldE;  // returns state_energy; applyRes: isActive = false, state = OOB, energy = NewEnergy
-      if (k == 0) {
-        a.r_ewo[r] = -1.f;
-        a.r_state[r] = HS_RES_OOB;
-        a.r_active[r] = 0;
-        a.r_energy[r] = oldNewE;
-      }
-    } else {
-      float energyLeft = L.s[t][0];
-      const float wJI2 = L.s[t][11];
-      int ns;
-      if (k == 0) a.r_ewo[r] = energyLeft;
-      if (t == nF - 1 && k == 0) a.newest_cand[p] = energyLeft;
-      if (energyLeft > thr || wJI2 < 2) {
-        energyLeft = thr;
-        ns = HS_RES_OUT;
-      } else {
-        ns = HS_RES_IN;
-      }
-      econ = energyLeft;
-      active = ns == HS_RES_IN;
-      if (active) {
-        // takeData (Include/OptimizationClasses.h:195-201)
-        const float J00 = L.s[t][1], J11 = L.s[t][2], J10 = L.s[t][3];
-        const float aa = J00 * Jd0 + J10 * Jd1;
-        const float bb = J10 * Jd0 + J11 * Jd1;
-        float jj;
-        if (k < 6) jj = Jx[4 + k] * aa + Jy[4 + k] * bb;
-        else if (k == 6) jj = L.s[t][4] * Jd0 + L.s[t][5] * Jd1;
-        else jj = L.s[t][6] * Jd0 + L.s[t][7] * Jd1;
-        a.p_JpJdF[(p * 8 + t) * 8 + k] = jj;
-        // Jacobian digest for the accumulate kernel (layout: hs_layout.h)
-        float* jr = a.p_Jrec + (size_t)(p * 8 + t) * HS_JREC;
-        for (int e = k; e < HS_JREC - 1; e += 8) {
-          float v;
-          if (e < 10) v = Jx[e];
-          else if (e < 20) v = Jy[e - 10];
-          else if (e == 20) v = J00;
-          else if (e == 21) v = J10;
-          else if (e == 22) v = J11;
-          else if (e < 26) v = L.s[t][8 + (e - 23)];
-          else if (e < 30) v = L.s[t][4 + (e - 26)];
-          else v = L.s[t][12 + (e - 30)];
-          jr[e] = v;
-        }
-      }
-      if (k == 0) {
-        a.r_state[r] = (uint8_t)ns;
-        a.r_active[r] = active ? 1 : 0;
-        a.r_energy[r] = energyLeft;
-        a.r_newEnergy[r] = energyLeft;
-      }
+      for (int qi = 0; qi < Q_N; qi++) L.s[t][qi] = sq[qi];
     }
-    if (a.write_center && centreOk && k < 3) a.r_center[r * 3 + k] = centre[k];
-  }
-  if (t == nF - 1 && k == 0 && !(has && st != HS_RES_OOB && !slotOob)) a.newest_cand[p] = -1.f;
-  if (k == 0) {
-    L.econ[t] = econ;
-    L.act[t] = active ? 1.f : 0.f;
-    L.jd[t][0] = Jd0;
-    L.jd[t][1] = Jd1;
-  }
-  if (k < 4) {
-    L.jx[t][k] = Jx[k];
-    L.jy[t][k] = Jy[k];
   }
   __syncthreads();
+  HS_TRACE(a, 4);
 
-  // ---------------- per-point sums in the point's residual-list order (lane 0): addPoint<0> + SC prelude
-  if (lane == 0) {
+  // ---------------- state decision + applyRes (the 8 lanes of a slot agree; lane k == 0 writes).
+  // Predicated rather than branched: the slot's sums are read from LDS in one batch and every store is
+  // issued under a mask, so the divergent slot cases cost no serialised LDS round trips.
+  float S[Q_N];
+#pragma unroll
+  for (int qi = 0; qi < Q_N; qi++) S[qi] = L.s[t][qi];
+  const bool live = has && st != HS_RES_OOB;      // OOB is sticky: linearize returns state_energy
+  const bool eval = live && !slotOob;             // a full linearization of this residual
+  const bool isOut = S[0] > thr || S[11] < 2;
+  const float energyLeft = isOut ? thr : S[0];
+  const bool active = eval && !isOut;
+  const float econ = eval ? energyLeft : oldE;
+  if (has && k == 0) {
+    a.r_ewo[sl] = eval ? S[0] : -1.f;
+    if (live) {  // applyRes: OOB now -> inactive, state OOB, energy = NewEnergy; else the new state
+      a.r_state[sl] = (uint8_t)(slotOob ? HS_RES_OOB : (isOut ? HS_RES_OUT : HS_RES_IN));
+      a.r_active[sl] = active ? 1 : 0;
+      a.r_energy[sl] = slotOob ? oldNewE : energyLeft;
+      if (!slotOob) a.r_newEnergy[sl] = energyLeft;
+    }
+  }
+  if (t == nF - 1 && k == 0) a.newest_cand[p] = eval ? S[0] : -1.f;
+  if (has && a.write_center && centreOk && k < 3) a.r_center[sl * 3 + k] = centre[k];
+  float tHdd = 0.f, tbd = 0.f, tc[4] = {0.f, 0.f, 0.f, 0.f};  // the slot's terms of the per-point sums
+  {
+    // takeData (Include/OptimizationClasses.h:195-201), computed unconditionally, stored when active
+    const float J00 = S[1], J11 = S[2], J10 = S[3];
+    const float aa = J00 * Jd0 + J10 * Jd1;
+    const float bb = J10 * Jd0 + J11 * Jd1;
+    // this residual's terms of the point sums (AccumulatedTopHessianSSE::addPoint<0> / SC prelude)
+    tbd = S[12] * Jd0 + S[13] * Jd1;
+    tHdd = aa * Jd0 + bb * Jd1;
+#pragma unroll
+    for (int c = 0; c < 4; c++) tc[c] = Jx[c] * aa + Jy[c] * bb;
+    float jx4 = Jx[4], jy4 = Jy[4];
+#pragma unroll
+    for (int c = 5; c < 10; c++) {
+      jx4 = k == c - 4 ? Jx[c] : jx4;
+      jy4 = k == c - 4 ? Jy[c] : jy4;
+    }
+    const float jj = k < 6 ? jx4 * aa + jy4 * bb : (k == 6 ? S[4] * Jd0 + S[5] * Jd1 : S[6] * Jd0 + S[7] * Jd1);
+    // Jacobian digest entries e = k + 8i (layout: hs_layout.h), selected with constant indices
+    float v0 = Jx[0];
+#pragma unroll
+    for (int c = 1; c < 8; c++) v0 = k == c ? Jx[c] : v0;           // e = k
+    float v1;
+    {
+      float y = Jy[0];
+#pragma unroll
+      for (int c = 1; c < 6; c++) y = k - 2 == c ? Jy[c] : y;      // e = k + 8 >= 10 -> Jy[k - 2]
+      v1 = k == 0 ? Jx[8] : (k == 1 ? Jx[9] : y);
+    }
+    float v2 = Jy[6];                                               // e = k + 16
+    v2 = k == 1 ? Jy[7] : v2;
+    v2 = k == 2 ? Jy[8] : v2;
+    v2 = k == 3 ? Jy[9] : v2;
+    v2 = k == 4 ? J00 : v2;
+    v2 = k == 5 ? J10 : v2;
+    v2 = k == 6 ? J11 : v2;
+    v2 = k == 7 ? S[8] : v2;
+    float v3 = S[9];                                                // e = k + 24
+    v3 = k == 1 ? S[10] : v3;
+    v3 = k == 2 ? S[4] : v3;
+    v3 = k == 3 ? S[5] : v3;
+    v3 = k == 4 ? S[6] : v3;
+    v3 = k == 5 ? S[7] : v3;
+    v3 = k == 6 ? S[12] : v3;
+    v3 = k == 7 ? S[13] : v3;
+    float v4 = S[14];                                               // e = k + 32 (k < 3)
+    v4 = k == 1 ? S[15] : v4;
+    v4 = k == 2 ? S[16] : v4;
+    if (active) {
+      a.p_JpJdF[(p * 8 + t) * 8 + k] = jj;
+      float* jr = a.p_Jrec + (size_t)(p * 8 + t) * HS_JREC;
+      jr[k] = v0;
+      jr[k + 8] = v1;
+      jr[k + 16] = v2;
+      jr[k + 24] = v3;
+      if (k < 3) jr[k + 32] = v4;
+    }
+  }
+  HS_TRACE(a, 5);
+  // ---------------- per-point sums in the point's residual-list order (uniform; readlane from lane 8 * slot)
+  {
+    const unsigned long long actBits = __ballot(active);
     double eSum = 0.0;
     float Hdd = 0.f, bd = 0.f, Hcd[4] = {0.f, 0.f, 0.f, 0.f};
     unsigned mask = 0u;
     for (int qn = 0; qn < 8; qn++) {
       const int tt = res_slot(qn);
       if (tt < 0) break;
-      eSum += (double)L.econ[tt];
-      if (L.act[tt] == 0.f) continue;
+      const int src = tt * 8;
+      eSum += (double)readlane_f(econ, src);
+      if (!((actBits >> src) & 1ull)) continue;
       mask |= 1u << tt;
-      const float J00 = L.s[tt][1], J11 = L.s[tt][2], J10 = L.s[tt][3];
-      const float d0 = L.jd[tt][0], d1 = L.jd[tt][1];
-      const float aa = J00 * d0 + J10 * d1;
-      const float bb = J10 * d0 + J11 * d1;
-      bd += L.s[tt][12] * d0 + L.s[tt][13] * d1;
-      Hdd += aa * d0 + bb * d1;
+      bd += readlane_f(tbd, src);
+      Hdd += readlane_f(tHdd, src);
 #pragma unroll
-      for (int c = 0; c < 4; c++) Hcd[c] += L.jx[tt][c] * aa + L.jy[tt][c] * bb;
+      for (int c = 0; c < 4; c++) Hcd[c] += readlane_f(tc[c], src);
     }
-    a.p_energy[p] = eSum;
-    a.p_actmask[p] = (uint8_t)mask;
-    if (mask == 0u) {
-      a.p_HdiF[p] = 0.f;
-      a.p_bdSumF[p] = 0.f;
-    } else {
-      const float priorF = a.priorF[p];
-      float Hh = Hdd + 0.f + priorF;  // Hdd_accAF + Hdd_accLF (no linearized residuals) + priorF
-      if ((double)Hh < 1e-10) Hh = (float)1e-10;
-      a.p_HdiF[p] = (float)(1.0 / (double)Hh);
-      float bdSumF = bd + 0.f;
-      bdSumF += priorF * (idep - idep0);
-      a.p_bdSumF[p] = bdSumF;
+    if (lane == 0) {
+      a.p_energy[p] = eSum;
+      a.p_actmask[p] = (uint8_t)mask;
+      if (mask == 0u) {
+        a.p_HdiF[p] = 0.f;
+        a.p_bdSumF[p] = 0.f;
+      } else {
+        const float priorF = a.priorF[p];
+        float Hh = Hdd + 0.f + priorF;  // Hdd_accAF + Hdd_accLF (no linearized residuals) + priorF
+        if ((double)Hh < 1e-10) Hh = (float)1e-10;
+        a.p_HdiF[p] = (float)(1.0 / (double)Hh);
+        float bdSumF = bd + 0.f;
+        bdSumF += priorF * (idep - idep0);
+        a.p_bdSumF[p] = bdSumF;
+      }
+      reinterpret_cast<float4*>(a.p_Hcd)[p] = make_float4(Hcd[0] + 0.f, Hcd[1] + 0.f, Hcd[2] + 0.f, Hcd[3] + 0.f);
     }
-    reinterpret_cast<float4*>(a.p_Hcd)[p] = make_float4(Hcd[0] + 0.f, Hcd[1] + 0.f, Hcd[2] + 0.f, Hcd[3] + 0.f);
   }
   HS_TRACE(a, 3);
 }
@@ -1263,16 +1303,23 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
   const int tid = threadIdx.x, nt = SOLVE_NT;
   HS_TRACE(a, 0);
   if (a.trace && threadIdx.x == 0) a.trace[10] = clock64();  // shader clock (effective-clock probe)
-  {
-    const uint2* gs = reinterpret_cast<const uint2*>(a.st);
-    uint2* ls = reinterpret_cast<uint2*>(st_raw);
-    for (int i = tid; i < (int)(sizeof(HsDevState) / 8); i += nt) ls[i] = gs[i];
-  }
+  // entry prefetch: every global input (window state, systems, nullspace factors, b vectors, adjoints) is
+  // requested into registers before the first LDS store, so the kernel pays ONE memory round trip here
+  // instead of one per dependent load-store loop iteration
+  constexpr int ST_WORDS = (int)(sizeof(HsDevState) / 8);
+  constexpr int ST_NU = (ST_WORDS + SOLVE_NT - 1) / SOLVE_NT;
+  constexpr int NF_NU = (2 * HS_MAXDIM * HS_NNS + SOLVE_NT - 1) / SOLVE_NT;
   const bool solve = (a.flags & HS_SOLVE) != 0;
-  // entry prefetch (SOLVE): every global input of the solve is requested before the first barrier
   const int nF = a.nF, n = 4 + 8 * nF, nn = n * n;
   const unsigned inv_n = (unsigned)((0x100000000ull + n - 1) / n);  // idx / n == umulhi(idx, inv_n) for idx < n*n
-  double ha[SOLVE_NU], hs[SOLVE_NU];
+  uint2 stw[ST_NU];
+  {
+    const uint2* gs = reinterpret_cast<const uint2*>(a.st);
+#pragma unroll
+    for (int u = 0; u < ST_NU; u++) stw[u] = gs[min(tid + u * SOLVE_NT, ST_WORDS - 1)];
+  }
+  double ha[SOLVE_NU], hs[SOLVE_NU], nfv[NF_NU];
+  double bA_q = 0.0, bSC_q = 0.0;
   float adh[2][8], adt[2][8];
   if (solve) {
 #pragma unroll
@@ -1281,8 +1328,12 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
       ha[u] = a.HA[idx];
       hs[u] = a.HSC[idx];
     }
-    for (int idx = tid; idx < 2 * n * HS_NNS; idx += nt) Nf[idx] = a.Nproj[idx];
-    for (int idx = tid; idx < HS_MAXDIM * (HS_MAXDIM + 1); idx += nt) LT[idx] = 0.0;
+#pragma unroll
+    for (int u = 0; u < NF_NU; u++) nfv[u] = a.Nproj[min(tid + u * SOLVE_NT, 2 * n * HS_NNS - 1)];
+    if (tid < n) {
+      bA_q = a.bA[tid];
+      bSC_q = a.bSC[tid];
+    }
 #pragma unroll
     for (int k = 0; k < 2; k++) {
       const int o = min(tid + k * nt, nF * nF * 8 - 1);
@@ -1295,6 +1346,18 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
         adt[k][rr] = aTf[rr * 8 + c];
       }
     }
+  }
+  {
+    uint2* ls = reinterpret_cast<uint2*>(st_raw);
+#pragma unroll
+    for (int u = 0; u < ST_NU; u++)
+      if (tid + u * SOLVE_NT < ST_WORDS) ls[tid + u * SOLVE_NT] = stw[u];
+  }
+  if (solve) {
+#pragma unroll
+    for (int u = 0; u < NF_NU; u++)
+      if (tid + u * SOLVE_NT < 2 * n * HS_NNS) Nf[tid + u * SOLVE_NT] = nfv[u];
+    for (int idx = tid; idx < HS_MAXDIM * (HS_MAXDIM + 1); idx += nt) LT[idx] = 0.0;
   }
   if (tid == 0) s_tie = 0;
   __syncthreads();
@@ -1326,8 +1389,8 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
       }
       px[q] = pr;  // HL diagonal (priors); staging only: these four arrays are reused below
       xs[q] = bl;
-      yv[q] = a.bA[q];
-      Sv[q] = a.bSC[q];
+      yv[q] = bA_q;
+      Sv[q] = bSC_q;
     }
     __syncthreads();
     HS_TRACE(a, 7);
@@ -1386,6 +1449,7 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     if (tid < n) {
       const double w0 = dgs[tid];
       int rank = 0, tie = 0;
+#pragma unroll 4
       for (int p = 0; p < n; p++) {
         const double w = dgs[p];
         rank += (w > w0 || (w == w0 && p < tid)) ? 1 : 0;

@@ -32,6 +32,7 @@ struct HsLinArgs {
   int nF;
   int write_center;
   int fuse_step;               // apply resubstitute + point step of the previous solve first
+  int host_begin[HS_MAXF + 1]; // first point of each host (points are sorted by host)
   const HsPrecalc* pre;        // [nF*nF] host*nF + target
   const float* frameTH;        // [nF]
   const float* xAd;            // [nF*nF][8] index h*nF + t (fuse_step)
