@@ -2,7 +2,7 @@
 // device-resident GN loop of System::optimize.  The window state (frames, calib, precalc,
 // systems, steps) lives in HBM between iterations; one GN iteration is the launch sequence
 //   hs_k_solve(SOLVE|APPLY) -> hs_k_linearize(fused point step) -> [all-gather]
-//   -> hs_k_accumulate -> hs_k_stitch -> [all-reduce]
+//   -> hs_k_accumulate (+ fused per-pair stitch) -> [all-reduce]
 // with no host synchronisation.  The host only prepares the window (adjoints, nullspace
 // projector, initial precalc — the reference's once-per-window Eigen/Sophus work) and reads
 // results back.  Compiled by hipcc as HIP together with hs_ba_kernels.hip; no torch, no Eigen.
@@ -114,7 +114,8 @@ struct hs_ctx {
   bool hm_zero = true;      // marginalization prior not set: the solve skips HM
   // kernel tracing (env HS_KTRACE=1): per-block wall-clock checkpoints of the last iteration
   bool tracing = false;
-  long long *d_tr_lin = nullptr, *d_tr_acc = nullptr, *d_tr_solve = nullptr, *d_tr_stitch = nullptr;
+  long long *d_tr_lin = nullptr, *d_tr_acc = nullptr, *d_tr_solve = nullptr;
+  int* d_ticket = nullptr;  // [nF*nF] stitch hand-off counters of hs_k_accumulate
 
   // RCCL
   ncclComm_t comm = nullptr;
@@ -144,7 +145,7 @@ static void free_window(hs_ctx* c) {
                   c->d_r_center, c->d_p_actmask, c->d_p_HdiF, c->d_p_bdSumF, c->d_p_Hcd, c->d_p_JpJdF,
                   c->d_p_Jrec, c->d_p_step, c->d_p_energy, c->d_part, c->d_part_cnt, c->d_hccbc, c->d_adHost,
                   c->d_adTarget, c->d_adHostF, c->d_adTargetF, c->d_sys, c->d_HM, c->d_bM, c->d_Nproj, c->d_xAd,
-                  c->d_x, c->d_elog, c->d_cand, c->d_tr_lin, c->d_tr_acc, c->d_tr_solve, c->d_tr_stitch};
+                  c->d_x, c->d_elog, c->d_cand, c->d_tr_lin, c->d_tr_acc, c->d_tr_solve, c->d_ticket};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   c->d_state = nullptr; c->d_pre = nullptr; c->d_frameTH = nullptr;
@@ -161,7 +162,8 @@ static void free_window(hs_ctx* c) {
   c->d_adHost = c->d_adTarget = nullptr; c->d_adHostF = c->d_adTargetF = nullptr;
   c->d_sys = nullptr; c->d_HM = c->d_bM = c->d_Nproj = nullptr;
   c->d_xAd = nullptr; c->d_x = nullptr; c->d_elog = nullptr; c->d_cand = nullptr;
-  c->d_tr_lin = c->d_tr_acc = c->d_tr_solve = c->d_tr_stitch = nullptr;
+  c->d_tr_lin = c->d_tr_acc = c->d_tr_solve = nullptr;
+  c->d_ticket = nullptr;
   c->nF = c->nP = c->nR = 0;
   c->haveSystem = false;
 }
@@ -249,15 +251,16 @@ static int launch_reduce(hs_ctx* c) {
   a.frameTH = c->d_frameTH; a.newest = c->nF - 1;
   a.frameEnergyTHN = c->P.frameEnergyTHN; a.facMedian = c->P.frameEnergyTHFacMedian;
   a.constWeight = c->P.frameEnergyTHConstWeight; a.overallWeight = c->P.overallEnergyTHWeight;
+  HsStitchArgs& st = a.stitch;
+  st.nF = c->nF; st.S = c->S;
+  st.part = c->d_part; st.part_cnt = c->d_part_cnt; st.hccbc = c->d_hccbc;
+  st.adHost = c->d_adHost; st.adTarget = c->d_adTarget;
+  st.HA = c->HA(); st.bA = c->bA(); st.HSC = c->HSC(); st.bSC = c->bSC();
+  st.trace = nullptr;
+  a.ticket = c->d_ticket;
+  if (a.trace)  // which blocks stitch varies per launch: clear the rows so stale checkpoints are not read
+    HS_HIP(hipMemsetAsync(a.trace, 0, sizeof(long long) * 16 * (c->nF * c->nF * c->S + 3), c->stream));
   hipLaunchKernelGGL(hs_k_accumulate, dim3(c->nF * c->nF * c->S + 3), dim3(256), 0, c->stream, a);
-  HS_HIP(hipGetLastError());
-  HsStitchArgs s;
-  s.nF = c->nF; s.S = c->S;
-  s.part = c->d_part; s.part_cnt = c->d_part_cnt; s.hccbc = c->d_hccbc;
-  s.adHost = c->d_adHost; s.adTarget = c->d_adTarget;
-  s.HA = c->HA(); s.bA = c->bA(); s.HSC = c->HSC(); s.bSC = c->bSC();
-  s.trace = c->d_tr_stitch;
-  hipLaunchKernelGGL(hs_k_stitch, dim3(c->nF * c->nF), dim3(256), 0, c->stream, s);
   HS_HIP(hipGetLastError());
   if (c->comm && c->nranks > 1)
     HS_NCCL(ncclAllReduce(c->d_sys, c->d_sys, c->sys_len(), ncclDouble, ncclSum, c->comm, c->stream));
@@ -357,7 +360,6 @@ static int dump_traces(hs_ctx* c) {
   }
   HS_TRY(dump_one("linearize", c->d_tr_lin, c->nP, tick_us, c->stream));
   HS_TRY(dump_one("accumulate", c->d_tr_acc, c->nF * c->nF * c->S + 3, tick_us, c->stream));
-  HS_TRY(dump_one("stitch", c->d_tr_stitch, c->nF * c->nF, tick_us, c->stream));
   return HS_OK;
 }
 
@@ -668,6 +670,7 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
   HS_TRY(dalloc(&c->d_part, (size_t)nF * nF * c->S * HS_PART_N));
   HS_TRY(dalloc(&c->d_part_cnt, (size_t)nF * nF * c->S * 16));
   HS_TRY(dalloc(&c->d_hccbc, 20));
+  HS_TRY(dalloc(&c->d_ticket, (size_t)nF * nF));  // zeroed; each stitching block resets its own counter
   HS_TRY(dalloc(&c->d_adHost, nF * nF * 64)); HS_TRY(dalloc(&c->d_adTarget, nF * nF * 64));
   HS_TRY(dalloc(&c->d_adHostF, nF * nF * 64)); HS_TRY(dalloc(&c->d_adTargetF, nF * nF * 64));
   HS_TRY(dalloc(&c->d_sys, c->sys_len()));
@@ -681,7 +684,6 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
     HS_TRY(dalloc(&c->d_tr_lin, (size_t)std::max(nP, 1) * 16));
     HS_TRY(dalloc(&c->d_tr_acc, (size_t)(nF * nF * c->S + 3) * 16));
     HS_TRY(dalloc(&c->d_tr_solve, 32));
-    HS_TRY(dalloc(&c->d_tr_stitch, (size_t)nF * nF * 16));
   }
 
   std::vector<float> prior(nP, 0.f);

@@ -16,8 +16,9 @@
 //                   updates (Include/MatrixAccumulators.h) in the reference's point order with the 1k/1m
 //                   blocking, so an unsplit block equals the single-thread reference bit for bit; plus the
 //                   energy sum, setNewFrameEnergyTH (Src/FullSystemOptimize.cpp:60-101) and accHcc/accbc.
-//   hs_k_stitch     stitchDoubleInternal (top: Src/AccumulatedTopHessian.cpp:218-280, Schur:
-//                   Src/AccumulatedSCHessian.cpp:54-133) in fp64, one workgroup per (host, target).
+//   stitch_pair     stitchDoubleInternal (top: Src/AccumulatedTopHessian.cpp:218-280, Schur:
+//                   Src/AccumulatedSCHessian.cpp:54-133) in fp64, fused into hs_k_accumulate: the last
+//                   split block of each (host, target) pair to finish stitches it.
 // Per-residual arithmetic follows the reference operation order with fp contraction off.
 #pragma clang fp contract(off)
 #include <hip/hip_runtime.h>
@@ -549,6 +550,10 @@ __device__ void acc_hcc_block(const HsAccArgs& a) {
     double t = 0.0;
     for (int q = 0; q < 12; q++) t += part[tid][q];
     a.hccbc[tid] = t;
+    // accHcc into the calib block of H_sc, accbc into b_sc (stitchDoubleMT, Include/AccumulatedSCHessian.h:92-99)
+    const int n = 4 + 8 * a.nF;
+    if (tid < 16) atomicAdd(&a.stitch.HSC[(tid >> 2) * n + (tid & 3)], t);
+    else atomicAdd(&a.stitch.bSC[tid - 16], t);
   }
 }
 
@@ -815,16 +820,26 @@ __device__ __forceinline__ void acc_pair_block(const HsAccArgs& a, AccLds& T) {
   __syncthreads();
   double* P = a.part + ((size_t)ij * S + s) * HS_PART_N;
   int* PC = a.part_cnt + ((size_t)ij * S + s) * 16;
+  // the partial is handed to the pair's stitching block (hs_k_accumulate): sc1 (write-through) stores
   for (int e = tid; e < HS_PART_N; e += 256) {
     double sum = 0.0;
     for (int w = 0; w < W; w++) sum += (double)stage[w * HS_PART_N + e];
-    P[e] = sum;
+    __hip_atomic_store(&P[e], sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (tid < 10) {
     int c = 0;
     for (int w = 0; w < W; w++) c += T.wcnt[w][tid];
-    PC[tid] = c;
+    __hip_atomic_store(&PC[tid], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+}
+
+__device__ void stitch_pair(const HsStitchArgs& a, int ij, long long* trace);
+
+// agent-scope relaxed load = global_load ... sc1 (bypasses this CU's L1; the L2 line of a write-through
+// sc1 store is dropped, so the load is served from memory side)
+template <typename T>
+__device__ __forceinline__ T ld_sc1(const T* p) {
+  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ __launch_bounds__(256) void hs_k_accumulate(HsAccArgs a) {
@@ -835,8 +850,26 @@ __global__ __launch_bounds__(256) void hs_k_accumulate(HsAccArgs a) {
   if (b == nb + 1) { acc_hcc_block(a); HS_TRACE(a, 15); return; }
   if (b == nb + 2) { acc_energy_th_block(a); HS_TRACE(a, 15); return; }
   __shared__ AccLds T;
+  __shared__ int s_last;
   if (a.blocked) acc_pair_block<true>(a, T);
   else acc_pair_block<false>(a, T);
+  HS_TRACE(a, 11);
+  // hand-off to the pair's stitch (MI355X_MICROARCH.md "Valid forms", counter row; cdna_hip_programming.md
+  // §6 Guideline 16): the partial was stored sc1 (write-through, no L2 write-back fence needed); every
+  // storing wave drains its stores, then after a barrier ONE lane adds to the pair's ticket; the block
+  // whose add returns S - 1 (the last) stitches the pair with sc1 loads of the partials.  No block waits
+  // on another (no spin), so any dispatch order and XCD placement is safe.
+  const int ij = b / a.S;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(&a.ticket[ij], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.S - 1;
+  __syncthreads();
+  if (s_last) {
+    stitch_pair(a.stitch, ij, a.trace ? a.trace + (size_t)blockIdx.x * 16 : nullptr);
+    if (threadIdx.x == 0)  // ready for the next launch (the kernel boundary orders it)
+      __hip_atomic_store(&a.ticket[ij], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   HS_TRACE(a, 15);
 }
 
@@ -844,18 +877,6 @@ __global__ __launch_bounds__(256) void hs_k_accumulate(HsAccArgs a) {
 // stitch (fp64): one block (64 threads) per (host i, target j)
 // =====================================================================================================
 namespace {
-// out(8x8) = A(8x8) * M(8x8) * B(8x8)^T, 64 threads (r = tid>>3, c = tid&7), tmp in LDS
-__device__ __forceinline__ double sandwich(const double* A, const double* M, const double* B, double* tmp, int tid) {
-  const int r = tid >> 3, c = tid & 7;
-  double s = 0.0;
-  for (int l = 0; l < 8; l++) s += A[r * 8 + l] * M[l * 8 + c];
-  __syncthreads();
-  tmp[tid] = s;
-  __syncthreads();
-  double o = 0.0;
-  for (int l = 0; l < 8; l++) o += tmp[r * 8 + l] * B[c * 8 + l];
-  return o;
-}
 // index of (r, c) in the 10x10 upper-triangle Data block
 __device__ __forceinline__ int tri_idx(int r, int c) {
   const int lo = r < c ? r : c, hi = r < c ? c : r;
@@ -863,35 +884,43 @@ __device__ __forceinline__ int tri_idx(int r, int c) {
 }
 }  // namespace
 
-// out(8x8) = A(8x8) * M(8x8) * B(8x8)^T by one wave (lane = r*8 + c), tmp = the wave's own LDS scratch;
-// a wave executes its LDS operations in order, so no workgroup barrier is needed
-__device__ __forceinline__ double sandwich_w(const double* A, const double* M, const double* B, double* tmp, int lane) {
+// lane (r, c) of one wave: X(r, c) = sum_l PH(r, l) M(l, c) and Y(r, c) = sum_l PT(r, l) M(l, c) (rows r of PH / PT
+// in registers), in l order as the reference's 8x8 products; staged to the wave's LDS scratch tx / ty
+__device__ __forceinline__ void left2(const double ph[8], const double pt[8], const double* M, double* tx, double* ty,
+                                      int lane) {
+  const int c = lane & 7;
+  double x = 0.0, y = 0.0;
+#pragma unroll
+  for (int l = 0; l < 8; l++) {
+    const double m = M[l * 8 + c];
+    x += ph[l] * m;
+    y += pt[l] * m;
+  }
+  tx[lane] = x;
+  ty[lane] = y;
+}
+// out(r, c) = sum_l T(r, l) B(c, l): the right product of a sandwich (T staged by left2)
+__device__ __forceinline__ double right_t(const double* T, const double* B, int lane) {
   const int r = lane >> 3, c = lane & 7;
-  double s = 0.0;
-  for (int l = 0; l < 8; l++) s += A[r * 8 + l] * M[l * 8 + c];
-  __builtin_amdgcn_wave_barrier();
-  tmp[lane] = s;
-  __builtin_amdgcn_wave_barrier();
   double o = 0.0;
-  for (int l = 0; l < 8; l++) o += tmp[r * 8 + l] * B[c * 8 + l];
-  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int l = 0; l < 8; l++) o += T[r * 8 + l] * B[c * 8 + l];
   return o;
 }
 
-// one workgroup (4 waves) per (host i, target j): fp64 sum of the split partials, then the top block
-// (wave 0), the Schur rows (i, j, k) for k = wave, wave+4 (all waves) and the calib / b parts
-__global__ __launch_bounds__(256) void hs_k_stitch(HsStitchArgs a) {
+// stitch of one (host i, target j) pair by a 256-thread block (4 waves): fp64 sum of the split partials,
+// then the top block (wave 0), the Schur rows (i, j, k) for k = wave, wave+4 (all waves) and the calib / b
+// parts, atomically added into HA / bA / HSC / bSC.  trace: the block's checkpoint row (slots 12 / 14).
+__device__ void stitch_pair(const HsStitchArgs& a, int ij, long long* trace) {
   const int nF = a.nF, S = a.S;
-  const int i = blockIdx.x % nF, j = blockIdx.x / nF;
-  const int ij = i + nF * j;
+  const int i = ij % nF, j = ij / nF;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int n = 4 + 8 * nF;
   const int iIdx = 4 + 8 * i, jIdx = 4 + 8 * j;
   __shared__ double E[HS_PART_N];  // summed partial: top 96 | D 8x64 | E 32 | EB 8
   __shared__ double A88[64], A84[32], a8r[8], aH[64], aT[64];
-  __shared__ double aH2[HS_MAXF][64], aT2[HS_MAXF][64], tmpw[4][64];
+  __shared__ double aH2[HS_MAXF][64], aT2[HS_MAXF][64], tmpw[4][128];
   __shared__ int cnt[16];
-  HS_TRACE(a, 0);
   // ---- everything this pair needs, all loads in flight together
   const double* P0 = a.part + (size_t)ij * S * HS_PART_N;
   const int* C0 = a.part_cnt + (size_t)ij * S * 16;
@@ -906,34 +935,48 @@ __global__ __launch_bounds__(256) void hs_k_stitch(HsStitchArgs a) {
     const double v = (w < 64 ? a.adHost : a.adTarget)[(i + nF * kc) * 64 + (w & 63)];
     if (kk < nF) (w < 64 ? aH2[kk] : aT2[kk])[w & 63] = v;
   }
-  // split partials summed in fp64 (stitchDoubleInternal: accH += acc[tid2].H.cast<double>() for num > 0)
+  // split partials summed in fp64 in split order (stitchDoubleInternal: accH += acc[tid2].H.cast<double>()
+  // for num > 0; a split with num == 0 made no update, so its partial is exactly +0 and adding it is the
+  // same as skipping it).  sc1 loads (the partials were handed off without an acquire fence), four splits
+  // per batch so the loads of a batch are in flight together.
   double sum[3] = {0.0, 0.0, 0.0};
-  for (int s = 0; s < S; s++) {
-    const double* Ps = P0 + (size_t)s * HS_PART_N;
-    const int* Cs = C0 + s * 16;
+  int csum = 0;
+  for (int s0 = 0; s0 < S; s0 += 4) {
+    double v[4][3];
+    int cv[4];
 #pragma unroll
-    for (int u = 0; u < 3; u++) {
-      const int e = tid + 256 * u;
-      const double pv = Ps[min(e, HS_PART_N - 1)];
-      const int grp = e < 96 ? 0 : (e < 96 + 512 ? 1 + ((e - 96) >> 6) : 9);  // count slot of the entry
-      if (e < HS_PART_N && (grp == 9 || Cs[grp] > 0)) sum[u] += pv;
+    for (int q = 0; q < 4; q++) {
+      const int sq = min(s0 + q, S - 1);
+      const double* Ps = P0 + (size_t)sq * HS_PART_N;
+#pragma unroll
+      for (int u = 0; u < 3; u++) v[q][u] = ld_sc1(&Ps[min(tid + 256 * u, HS_PART_N - 1)]);
+      cv[q] = ld_sc1(&C0[sq * 16 + (tid & 15)]);
     }
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      if (s0 + q < S) {
+#pragma unroll
+        for (int u = 0; u < 3; u++) sum[u] += v[q][u];
+        csum += cv[q];
+      }
   }
 #pragma unroll
   for (int u = 0; u < 3; u++)
     if (tid + 256 * u < HS_PART_N) E[tid + 256 * u] = sum[u];
-  if (tid < 16) {
-    int c = 0;
-    for (int s = 0; s < S; s++) c += C0[s * 16 + tid];
-    cnt[tid] = c;
-  }
+  if (tid < 16) cnt[tid] = csum;
   __syncthreads();
-  HS_TRACE(a, 1);
+  if (trace && tid == 0) trace[12] = wall_clock64();
   const double* e = E;
   const double* Hpc = E + 96 + 512;
   const double* v8 = E + 96 + 512 + 32;
   const int r = lane >> 3, c = lane & 7;
   double* tmp = tmpw[wv];
+  double ahr[8], atr[8];  // this lane's rows r of the adjoints, in registers for every left product
+#pragma unroll
+  for (int l = 0; l < 8; l++) {
+    ahr[l] = aH[r * 8 + l];
+    atr[l] = aT[r * 8 + l];
+  }
   if (wv == 0 && cnt[0] > 0) {  // top block: AccumulatorApprox::finish -> 13x13 [calib4|xi6|a|b|r]
     const int R = 4 + r, Cc = 4 + c;
     double v;
@@ -957,13 +1000,14 @@ __global__ __launch_bounds__(256) void hs_k_stitch(HsStitchArgs a) {
       a8r[lane] = RR < 10 ? e[55 + 3 * RR + 2] : (RR == 10 ? e[85 + 2] : e[85 + 4]);
     }
     __builtin_amdgcn_wave_barrier();
-    double o;
-    o = sandwich_w(aH, A88, aH, tmp, lane);
-    atomicAdd(&a.HA[(iIdx + r) * n + iIdx + c], o);
-    o = sandwich_w(aT, A88, aT, tmp, lane);
-    atomicAdd(&a.HA[(jIdx + r) * n + jIdx + c], o);
-    o = sandwich_w(aH, A88, aT, tmp, lane);
-    atomicAdd(&a.HA[(iIdx + r) * n + jIdx + c], o);
+    // aH A aH^T, aT A aT^T, aH A aT^T: the two left products once, then three right products
+    left2(ahr, atr, A88, tmp, tmp + 64, lane);
+    __builtin_amdgcn_wave_barrier();
+    const double o1 = right_t(tmp, aH, lane), o2 = right_t(tmp + 64, aT, lane), o3 = right_t(tmp, aT, lane);
+    __builtin_amdgcn_wave_barrier();
+    atomicAdd(&a.HA[(iIdx + r) * n + iIdx + c], o1);
+    atomicAdd(&a.HA[(jIdx + r) * n + jIdx + c], o2);
+    atomicAdd(&a.HA[(iIdx + r) * n + jIdx + c], o3);
     if (lane < 32) {
       const int rr = lane >> 2, cc = lane & 3;
       double s1 = 0.0, s2 = 0.0;
@@ -1011,19 +1055,18 @@ __global__ __launch_bounds__(256) void hs_k_stitch(HsStitchArgs a) {
     if (cnt[1 + kk] == 0) continue;  // accD num == 0
     const int kIdx = 4 + 8 * kk;
     const double* D = E + 96 + kk * 64;
-    double o;
-    o = sandwich_w(aH, D, aH2[kk], tmp, lane);
-    atomicAdd(&a.HSC[(iIdx + r) * n + iIdx + c], o);
-    o = sandwich_w(aT, D, aT2[kk], tmp, lane);
-    atomicAdd(&a.HSC[(jIdx + r) * n + kIdx + c], o);
-    o = sandwich_w(aT, D, aH2[kk], tmp, lane);
-    atomicAdd(&a.HSC[(jIdx + r) * n + iIdx + c], o);
-    o = sandwich_w(aH, D, aT2[kk], tmp, lane);
-    atomicAdd(&a.HSC[(iIdx + r) * n + kIdx + c], o);
+    // X = aH D, Y = aT D once; X aH2^T, Y aT2^T, Y aH2^T, X aT2^T (the reference's four sandwiches)
+    left2(ahr, atr, D, tmp, tmp + 64, lane);
+    __builtin_amdgcn_wave_barrier();
+    const double o1 = right_t(tmp, aH2[kk], lane), o2 = right_t(tmp + 64, aT2[kk], lane);
+    const double o3 = right_t(tmp + 64, aH2[kk], lane), o4 = right_t(tmp, aT2[kk], lane);
+    __builtin_amdgcn_wave_barrier();
+    atomicAdd(&a.HSC[(iIdx + r) * n + iIdx + c], o1);
+    atomicAdd(&a.HSC[(jIdx + r) * n + kIdx + c], o2);
+    atomicAdd(&a.HSC[(jIdx + r) * n + iIdx + c], o3);
+    atomicAdd(&a.HSC[(iIdx + r) * n + kIdx + c], o4);
   }
-  if (blockIdx.x == 0 && wv == 2 && lane < 16) atomicAdd(&a.HSC[(lane >> 2) * n + (lane & 3)], a.hccbc[lane]);
-  if (blockIdx.x == 0 && wv == 2 && lane < 4) atomicAdd(&a.bSC[lane], a.hccbc[16 + lane]);
-  HS_TRACE(a, 15);
+  if (trace && tid == 0) trace[14] = wall_clock64();
 }
 
 // =====================================================================================================

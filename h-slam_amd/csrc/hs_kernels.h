@@ -67,6 +67,20 @@ struct HsLinArgs {
   long long* trace;            // nullable: per-block wall-clock checkpoints [grid][16]
 };
 
+struct HsStitchArgs {
+  int nF, S;
+  const double* part;
+  const int* part_cnt;
+  const double* hccbc;
+  const double* adHost;        // [nF*nF][64]  index h + nF*t
+  const double* adTarget;
+  double* HA;                  // [n*n] zeroed
+  double* bA;
+  double* HSC;
+  double* bSC;
+  long long* trace;
+};
+
 struct HsAccArgs {
   int nF, S, nP;
   int W;                       // waves of a block that accumulate (1: one wave, the reference's point order)
@@ -91,21 +105,12 @@ struct HsAccArgs {
   int newest;
   float frameEnergyTHN, facMedian, constWeight, overallWeight;
   long long* trace;
+  // stitch fused into the accumulate launch: the last split block of a (host, target) pair to finish
+  // (ticket counter) stitches that pair; the Hcc block adds accHcc / accbc itself
+  HsStitchArgs stitch;
+  int* ticket;                 // [nF*nF] zero between launches (the stitching block resets its counter)
 };
 
-struct HsStitchArgs {
-  int nF, S;
-  const double* part;
-  const int* part_cnt;
-  const double* hccbc;
-  const double* adHost;        // [nF*nF][64]  index h + nF*t
-  const double* adTarget;
-  double* HA;                  // [n*n] zeroed
-  double* bA;
-  double* HSC;
-  double* bSC;
-  long long* trace;
-};
 
 enum { HS_SOLVE = 1, HS_APPLY = 2 };
 
@@ -151,7 +156,6 @@ struct HsResubArgs {
 
 __global__ void hs_k_linearize(HsLinArgs a);
 __global__ void hs_k_accumulate(HsAccArgs a);
-__global__ void hs_k_stitch(HsStitchArgs a);
 __global__ void hs_k_solve(HsSolveArgs a);
 __global__ void hs_k_resub(HsResubArgs a);
 __global__ void hs_k_apply_step(int n, const float* step, float* idepth, float* idepth_zero);
