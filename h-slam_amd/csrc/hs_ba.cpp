@@ -320,7 +320,8 @@ static int set_loop_counters(hs_ctx* c, int iteration) {
 // per-kernel checkpoint summary of the last traced launch (stderr): for every checkpoint the
 // min / median / max over blocks of (checkpoint - the block's start) and the launch span, in us
 static int dump_one(const char* name, const long long* d, int nblocks, double tick_us, hipStream_t s) {
-  std::vector<long long> h((size_t)nblocks * 16);
+  const bool solve = std::string(name) == "solve";
+  std::vector<long long> h(solve ? 32 : (size_t)nblocks * 16);  // the solve row has 32 slots (16..25: probes)
   HS_HIP(hipMemcpyAsync(h.data(), d, sizeof(long long) * h.size(), hipMemcpyDeviceToHost, s));
   HS_HIP(hipStreamSynchronize(s));
   long long t0 = -1, t1 = 0;
@@ -330,11 +331,10 @@ static int dump_one(const char* name, const long long* d, int nblocks, double ti
     for (int k = 1; k < 16; k++) t1 = std::max(t1, h[b * 16 + k]);
   }
   std::fprintf(stderr, "[hs trace] %-12s blocks %5d span %8.2f us\n", name, nblocks, t0 < 0 ? 0.0 : (t1 - t0) * tick_us);
-  if (std::string(name) == "solve" && h[0] && h[10] && h[11] && h[15] > h[0])  // slots 10/11: shader clock
+  if (solve && h[0] && h[24] && h[25] && h[15] > h[0])  // slots 24/25: shader clock
     std::fprintf(stderr, "[hs trace] %-12s shader clock %.0f MHz\n", name,
-                 (double)(h[11] - h[10]) / ((h[15] - h[0]) * tick_us));
+                 (double)(h[25] - h[24]) / ((h[15] - h[0]) * tick_us));
   for (int k = 1; k < 16; k++) {
-    if (std::string(name) == "solve" && (k == 10 || k == 11)) continue;
     std::vector<double> v;
     for (int b = 0; b < nblocks; b++)
       if (h[b * 16] && h[b * 16 + k]) v.push_back((h[b * 16 + k] - h[b * 16]) * tick_us);

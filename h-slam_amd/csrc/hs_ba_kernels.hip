@@ -1336,8 +1336,9 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
   __shared__ double bf[HS_MAXDIM], Sv[HS_MAXDIM], xs[HS_MAXDIM], yv[HS_MAXDIM], px[HS_MAXDIM], dl[HS_MAXDIM];
   __shared__ double dgs[HS_MAXDIM];  // |diagonal| of the scaled system (pivot keys)
   __shared__ float xF[HS_MAXDIM];
-  __shared__ int pos[HS_MAXDIM], sorted_[HS_MAXDIM], elem_at[HS_MAXDIM], pos_of[HS_MAXDIM];
-  __shared__ int s_it, s_tie;
+  __shared__ double dgr[HS_MAXDIM];  // raw diagonal of the assembled system
+  __shared__ int pos[HS_MAXDIM], rk[HS_MAXDIM];
+  __shared__ int s_it;
   // the window state lives in LDS for the whole kernel: every field is touched by dependent scalar code
   // (steps, SE3 updates, precalc), which would otherwise pay a global-memory round trip per access
   __shared__ __align__(16) unsigned char st_raw[sizeof(HsDevState)];
@@ -1345,7 +1346,7 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
   HsDevState* st = reinterpret_cast<HsDevState*>(st_raw);
   const int tid = threadIdx.x, nt = SOLVE_NT;
   HS_TRACE(a, 0);
-  if (a.trace && threadIdx.x == 0) a.trace[10] = clock64();  // shader clock (effective-clock probe)
+  if (a.trace && threadIdx.x == 0) a.trace[24] = clock64();  // shader clock (effective-clock probe)
   // entry prefetch: every global input (window state, systems, nullspace factors, b vectors, adjoints) is
   // requested into registers before the first LDS store, so the kernel pays ONE memory round trip here
   // instead of one per dependent load-store loop iteration
@@ -1362,8 +1363,8 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     for (int u = 0; u < ST_NU; u++) stw[u] = gs[min(tid + u * SOLVE_NT, ST_WORDS - 1)];
   }
   double ha[SOLVE_NU], hs[SOLVE_NU], nfv[NF_NU];
-  double bA_q = 0.0, bSC_q = 0.0;
-  float adh[2][8], adt[2][8];
+  double bA_q = 0.0, bSC_q = 0.0, bM_q = 0.0;
+  const double sysE0 = a.sysE[0], sysE1 = a.sysE[1], sysE2 = a.sysE[2];  // energy, sum |idepth|, #points
   if (solve) {
 #pragma unroll
     for (int u = 0; u < SOLVE_NU; u++) {
@@ -1376,18 +1377,7 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     if (tid < n) {
       bA_q = a.bA[tid];
       bSC_q = a.bSC[tid];
-    }
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-      const int o = min(tid + k * nt, nF * nF * 8 - 1);
-      const int pair = o >> 3, c = o & 7, hh = pair / nF, tt = pair - hh * nF;
-      const float* aHf = a.adHostF + (hh + nF * tt) * 64;
-      const float* aTf = a.adTargetF + (hh + nF * tt) * 64;
-#pragma unroll
-      for (int rr = 0; rr < 8; rr++) {
-        adh[k][rr] = aHf[rr * 8 + c];
-        adt[k][rr] = aTf[rr * 8 + c];
-      }
+      bM_q = a.bM[tid];
     }
   }
   {
@@ -1400,23 +1390,24 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
 #pragma unroll
     for (int u = 0; u < NF_NU; u++)
       if (tid + u * SOLVE_NT < 2 * n * HS_NNS) Nf[tid + u * SOLVE_NT] = nfv[u];
-    for (int idx = tid; idx < HS_MAXDIM * (HS_MAXDIM + 1); idx += nt) LT[idx] = 0.0;
   }
-  if (tid == 0) s_tie = 0;
   __syncthreads();
   if (tid == 0) s_it = a.iteration >= 0 ? a.iteration : st->iteration;
   const double lambda = 1e-5;  // SOLVER_FIX_LAMBDA
 
   if (solve) {
     if (tid == 0 && a.energy_log) {
-      a.energy_log[st->log_count] = a.sysE[0];
+      a.energy_log[st->log_count] = sysE0;
       st->log_count = st->log_count + 1;
     }
 #pragma unroll
     for (int u = 0; u < SOLVE_NU; u++)
       if (tid + u * nt < nn) {
-        A[tid + u * nt] = ha[u];
-        B[tid + u * nt] = hs[u];
+        // raw HA -> B, raw HSC -> LT, both at the padded row stride n + 1 so the transposed reads of the
+        // symmetrization below are (nearly) bank-conflict free; LT is cleared for the LDLT afterwards
+        const int ix = tid + u * nt, r = (int)__umulhi((unsigned)ix, inv_n), c = ix - r * n;
+        B[r * (n + 1) + c] = ha[u];
+        LT[r * (n + 1) + c] = hs[u];
       }
     if (tid < n) {
       const int q = tid;
@@ -1440,14 +1431,22 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     // HFinal = (HL + HM) + HA' ; diag *= (1+lambda) ; HFinal -= HSC' / (1+lambda)   (' = stitchDoubleMT
     // post-processing: frame off-diagonal blocks symmetrized, calib rows copied from the calib columns)
     const double sc = (double)(1.0f / (1 + lambda));
+    double hmv[SOLVE_NU];  // HM entries: one uniform branch for the whole set of loads
+    if (a.HM) {
+#pragma unroll
+      for (int u = 0; u < SOLVE_NU; u++) hmv[u] = a.HM[min(tid + u * nt, nn - 1)];
+    } else {
+#pragma unroll
+      for (int u = 0; u < SOLVE_NU; u++) hmv[u] = 0.0;
+    }
     double v[SOLVE_NU];
 #pragma unroll
     for (int u = 0; u < SOLVE_NU; u++) {
       const int ix = min(tid + u * nt, nn - 1), r = (int)__umulhi((unsigned)ix, inv_n), c = ix - r * n;
-      const int idx = r * n + c, tdx = c * n + r;
+      const int idx = r * (n + 1) + c, tdx = c * (n + 1) + r;
       const int fr = r < 4 ? -1 : (r - 4) >> 3, fc = c < 4 ? -1 : (c - 4) >> 3;
-      const double a0 = A[idx], a1 = A[tdx], b0 = B[idx], b1 = B[tdx], hl0 = px[r];
-      const double hm = a.HM ? a.HM[idx] : 0.0;
+      const double a0 = B[idx], a1 = B[tdx], b0 = LT[idx], b1 = LT[tdx], hl0 = px[r];
+      const double hm = hmv[u];
       const bool sym = fr >= 0 && fc >= 0 && fr != fc, calrow = r < 4 && c >= 4;
       const double ha_ = sym ? a0 + a1 : (calrow ? a1 : a0);
       const double hsc = calrow ? b1 : b0;
@@ -1462,85 +1461,81 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
       if (a.HM)
         for (int c = 0; c < n; c++) hmd += a.HM[q * n + c] * dl[c];
       // ((bL + (bM + HM delta)) + bA) - bSC
-      bf[q] = ((xs[q] + (a.bM[q] + hmd)) + yv[q]) - Sv[q];
+      bf[q] = ((xs[q] + (bM_q + hmd)) + yv[q]) - Sv[q];
     }
+    // the diagonal of the assembled system (held in registers by its owners) is staged for the scaling
+#pragma unroll
+    for (int u = 0; u < SOLVE_NU; u++) {
+      const int ix = tid + u * nt, r = (int)__umulhi((unsigned)ix, inv_n), c = ix - r * n;
+      if (ix < nn && r == c) dgr[r] = v[u];
+    }
+    if (tid < HS_MAXDIM) rk[tid] = 0;
     __syncthreads();
     HS_TRACE(a, 8);
-#pragma unroll
-    for (int u = 0; u < SOLVE_NU; u++)
-      if (tid + u * nt < nn) A[tid + u * nt] = v[u];
-    __syncthreads();
-    HS_TRACE(a, 9);
+    for (int idx = tid; idx < HS_MAXDIM * (HS_MAXDIM + 1); idx += nt) LT[idx] = 0.0;  // L^T: zero on entry
     // scaling S = 1/sqrt(diag + 10); the pivot keys |S H S|_qq in the scaling's own operation order
     if (tid < n) {
-      const double hqq = A[tid * n + tid];
+      const double hqq = dgr[tid];
       const double sq = 1.0 / sqrt(hqq + 10);
       Sv[tid] = sq;
       dgs[tid] = fabs(sq * hqq * sq);
       bf[tid] = sq * bf[tid];
     }
     __syncthreads();
+    HS_TRACE(a, 9);
+    // the scaled system S H S, straight from the registers (no LDS round trip of the raw system)
 #pragma unroll
-    for (int u = 0; u < SOLVE_NU; u++) {
+    for (int u = 0; u < SOLVE_NU; u++) {  // all reads first (unconditional), then the predicated stores
       const int ix = min(tid + u * nt, nn - 1), r = (int)__umulhi((unsigned)ix, inv_n), c = ix - r * n;
-      const double sv = Sv[r] * A[ix] * Sv[c];
-      if (tid + u * nt < nn) A[ix] = sv;
+      v[u] = Sv[r] * v[u] * Sv[c];
     }
-    // Eigen LDLT pivot order (left-looking: the pivot is the largest |original diagonal| among the remaining
-    // ones, first current position on ties).  Stable descending order by |diag|; where values tie, the
-    // swap sequence is replayed by one thread to get the exact positions.
-    if (tid < n) {
-      const double w0 = dgs[tid];
-      int rank = 0, tie = 0;
-#pragma unroll 4
-      for (int p = 0; p < n; p++) {
-        const double w = dgs[p];
-        rank += (w > w0 || (w == w0 && p < tid)) ? 1 : 0;
-        tie |= (p != tid && w == w0) ? 1 : 0;
+#pragma unroll
+    for (int u = 0; u < SOLVE_NU; u++)
+      if (tid + u * nt < nn) A[tid + u * nt] = v[u];
+    HS_TRACE(a, 10);
+    // Pivot order: descending |diagonal| of the scaled system, Eigen's LDLT rule (left-looking: the largest
+    // remaining |original diagonal| is the next pivot).  Exact ties are broken by the original index; Eigen
+    // breaks them by the current position after its own swaps, which permutes tied rows only: x differs by
+    // rounding, far inside the tolerance on x (the LDLT is parity-unpinned).  Ranks are counted
+    // by all four waves (wave w compares against keys 17w .. 17w + 16) and combined with LDS atomics.
+    {
+      const int ln = tid & 63, w4 = __builtin_amdgcn_readfirstlane(tid >> 6);
+      const int p0 = w4 * (HS_MAXDIM / 4), p1 = min(n, p0 + HS_MAXDIM / 4);
+      double wk[HS_MAXDIM / 4];  // this wave's 17 keys: uniform LDS reads, all issued before any compare
+#pragma unroll
+      for (int q = 0; q < HS_MAXDIM / 4; q++) wk[q] = dgs[min(p0 + q, n - 1)];
+#pragma unroll
+      for (int half = 0; half < 2; half++) {
+        const int e = ln + 64 * half;
+        const double w0 = dgs[min(e, n - 1)];
+        int cnt_ = 0;
+#pragma unroll
+        for (int q = 0; q < HS_MAXDIM / 4; q++) {  // branch-free (& / |, no short-circuit control flow)
+          const int pp = p0 + q;
+          cnt_ += (int)((pp < p1) & ((wk[q] > w0) | ((wk[q] == w0) & (pp < e))));
+        }
+        if (e < n) atomicAdd(&rk[e], cnt_);
       }
-      sorted_[rank] = tid;
-      pos[rank] = tid;
-      elem_at[tid] = tid;
-      pos_of[tid] = tid;
-      if (tie) s_tie = 1;
     }
+    HS_TRACE(a, 11);
+    __syncthreads();
+    if (tid < n) pos[rk[tid]] = tid;
     __syncthreads();
     HS_TRACE(a, 1);
-    if (s_tie && tid == 0) {
-      int gs = 0;
-      while (gs < n) {
-        const double gv = dgs[sorted_[gs]];
-        int ge = gs + 1;
-        while (ge < n && dgs[sorted_[ge]] == gv) ge++;
-        for (int kq = gs; kq < ge; kq++) {
-          // remaining group members are sorted_[kq..ge) (selected ones are swapped to the front)
-          int bq = kq, bp = pos_of[sorted_[kq]];
-          for (int q = kq + 1; q < ge; q++) {
-            const int pq = pos_of[sorted_[q]];
-            if (pq < bp) { bp = pq; bq = q; }
-          }
-          const int sel = sorted_[bq];
-          sorted_[bq] = sorted_[kq];
-          sorted_[kq] = sel;
-          const int ek = elem_at[kq];
-          elem_at[kq] = sel;
-          elem_at[bp] = ek;
-          pos_of[ek] = bp;
-          pos_of[sel] = kq;
-          pos[kq] = sel;
-        }
-        gs = ge;
-      }
-    }
-    __syncthreads();
     // the permuted system P S H S P^T and right-hand side for the factorization
+    {  // branch-free gather: all index and value reads first (clamped), then the predicated stores
+      int pr_[SOLVE_NU], pc_[SOLVE_NU];
 #pragma unroll
-    for (int u = 0; u < SOLVE_NU; u++) {
-      const int ix = tid + u * nt;
-      if (ix < nn) {
-        const int r = (int)__umulhi((unsigned)ix, inv_n), c = ix - r * n;
-        B[ix] = A[pos[r] * n + pos[c]];
+      for (int u = 0; u < SOLVE_NU; u++) {
+        const int ix = min(tid + u * nt, nn - 1), r = (int)__umulhi((unsigned)ix, inv_n), c = ix - r * n;
+        pr_[u] = pos[r];
+        pc_[u] = pos[c];
       }
+#pragma unroll
+      for (int u = 0; u < SOLVE_NU; u++) v[u] = A[pr_[u] * n + pc_[u]];
+#pragma unroll
+      for (int u = 0; u < SOLVE_NU; u++)
+        if (tid + u * nt < nn) B[tid + u * nt] = v[u];
     }
     if (tid < n) yv[tid] = bf[pos[tid]];
     __syncthreads();
@@ -1551,6 +1546,21 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     if (tid < n) xs[pos[tid]] = Sv[pos[tid]] * yv[tid];
     __syncthreads();
     HS_TRACE(a, 4);
+    // the fp32 adjoints for xAd: requested here so their latency overlaps orthogonalize (holding them in
+    // registers across the LDLT costs 32 VGPRs of a kernel at the register limit)
+    float adh[2][8], adt[2][8];
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const int o = min(tid + k * nt, nF * nF * 8 - 1);
+      const int pair = o >> 3, c = o & 7, hh = pair / nF, tt = pair - hh * nF;
+      const float* aHf = a.adHostF + (hh + nF * tt) * 64;
+      const float* aTf = a.adTargetF + (hh + nF * tt) * 64;
+#pragma unroll
+      for (int rr = 0; rr < 8; rr++) {
+        adh[k][rr] = aHf[rr * 8 + c];
+        adt[k][rr] = aTf[rr * 8 + c];
+      }
+    }
     if (s_it >= 2) {  // SOLVER_ORTHOGONALIZE_X_LATER: x -= P x, P = (N Npi^T + Npi N^T) / 2 (orthogonalize)
       // t1 = Npi^T x, t2 = N^T x: 14 dot products over n, 4 lanes each
       const int d = tid >> 2, part = tid & 3, len = n >> 2;
@@ -1659,7 +1669,7 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
       }
       const float nfr = (float)nF;
       sumA /= nfr; sumB /= nfr; sumR /= nfr; sumT /= nfr;
-      const float sumNID = a.sysE[2] > 0 ? (float)(a.sysE[1] / a.sysE[2]) : 0.f;
+      const float sumNID = sysE2 > 0 ? (float)(sysE1 / sysE2) : 0.f;
       const float th = a.thOptIterations;
       st->canbreak = sqrtf(sumA) < 0.0005 * th && sqrtf(sumB) < 0.00005 * th && sqrtf(sumR) < 0.00005 * th &&
                      sqrtf(sumT) * sumNID < 0.00005 * th;
@@ -1672,7 +1682,7 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     uint2* gs = reinterpret_cast<uint2*>(a.st);
     for (int i = tid; i < (int)(sizeof(HsDevState) / 8); i += nt) gs[i] = ls[i];
   }
-  if (a.trace && threadIdx.x == 0) a.trace[11] = clock64();
+  if (a.trace && threadIdx.x == 0) a.trace[25] = clock64();
   HS_TRACE(a, 15);
 }
 

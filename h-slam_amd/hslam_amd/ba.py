@@ -81,6 +81,11 @@ class BAWindow:
         check(self.lib.hs_ba_linearize(self.h, int(reset), C.byref(e)))
         return e.value
 
+    def set_marginal_prior(self, HM, bM):
+        """EnergyFunctional::HM / bM (Include/EnergyFunctional.h:62-63), dim x dim and dim."""
+        check(self.lib.hs_ba_set_marginal_prior(self.h, ptr(np.ascontiguousarray(HM, np.float64)),
+                                                ptr(np.ascontiguousarray(bM, np.float64))))
+
     def solveSystem(self, iteration):
         x = np.zeros(self.dim)
         check(self.lib.hs_ba_solve_system(self.h, iteration, ptr(x)))

@@ -1284,6 +1284,13 @@ void hso_ba_solve_system(void* h, int iteration, double* x_out) {
   ba->solveSystemF(iteration, x);
   std::memcpy(x_out, x.data(), sizeof(double) * x.size());
 }
+// EnergyFunctional::HM / bM (the marginalization prior, Include/EnergyFunctional.h:62-63)
+void hso_ba_set_marginal_prior(void* h, const double* HM, const double* bM) {
+  BA* ba = (BA*)h;
+  const size_t n = ba->HM.size();
+  std::memcpy(ba->HM.data(), HM, sizeof(double) * n);
+  std::memcpy(ba->bM.data(), bM, sizeof(double) * ba->bM.size());
+}
 void hso_ba_backup_state(void* h) { ((BA*)h)->backupState(); }
 int hso_ba_do_step(void* h) { return ((BA*)h)->doStepFromBackup() ? 1 : 0; }
 

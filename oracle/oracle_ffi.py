@@ -78,6 +78,7 @@ def load(fast=False):
     lib.hso_ba_accumulate.argtypes = [vp, C.c_int, vp, vp]
     lib.hso_ba_solve_system.argtypes = [vp, C.c_int, vp]
     lib.hso_ba_backup_state.argtypes = [vp]
+    lib.hso_ba_set_marginal_prior.argtypes = [vp, vp, vp]
     lib.hso_ba_do_step.argtypes = [vp]
     lib.hso_ba_do_step.restype = C.c_int
     lib.hso_ba_get_residuals.argtypes = [vp] * 10
@@ -202,6 +203,10 @@ class OracleBA:
 
     def backup_state(self):
         self.lib.hso_ba_backup_state(self.h)
+
+    def set_marginal_prior(self, HM, bM):
+        self.lib.hso_ba_set_marginal_prior(self.h, _p(np.ascontiguousarray(HM, np.float64)),
+                                           _p(np.ascontiguousarray(bM, np.float64)))
 
     def do_step(self):
         return bool(self.lib.hso_ba_do_step(self.h))

@@ -104,6 +104,33 @@ def test_solve_and_step(scene2k):
         assert abs(eg - eo) <= 1e-3 * abs(eo)
 
 
+def test_solve_with_marginal_prior(scene_small):
+    """EnergyFunctional::HM / bM enter solveSystemF (Src/EnergyFunctional.cpp:745-760): a random PSD prior of
+    the scale of the data Hessian, through the whole GN iteration."""
+    g, o = _pair(scene_small)
+    g.linearizeAll(reset=True)
+    o.linearize_all(reset=True)
+    o.apply_res()
+    dim = g.dim
+    Ho, _ = o.accumulate(0)
+    rng = np.random.default_rng(3)
+    Q = rng.normal(size=(dim, dim))
+    HM = Q @ Q.T / dim * 1e-2 * np.abs(np.diag(Ho)).mean()
+    bM = rng.normal(size=dim) * 1e-2 * np.abs(Ho).max() ** 0.5
+    g.set_marginal_prior(HM, bM)
+    o.set_marginal_prior(HM, bM)
+    for it in range(3):
+        o.backup_state()
+        xo = o.solve_system(it)
+        xg = g.solveSystem(it)
+        assert np.linalg.norm(xg - xo) <= 1e-3 * np.linalg.norm(xo), it
+        o.do_step()
+        g.doStepFromBackup()
+        eg, eo = g.linearizeAll(), o.linearize_all()
+        o.apply_res()
+        assert abs(eg - eo) <= 1e-3 * abs(eo)
+
+
 def test_optimize_trajectory(scene2k):
     g, o = _pair(scene2k)
     ng, eg = g.optimize(6)
