@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
+#include <type_traits>
 
 #include "hs_kernels.h"
 
@@ -1101,11 +1102,12 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
 //   W  : scratch of 26 * HS_MAXDIM doubles;  yv : right-hand side in, solution out
 constexpr int LSTR = HS_MAXDIM + 1;  // padded row stride of LT
 
-__device__ __forceinline__ double rcp_f64(double d) {  // 1/d to ~1 ulp; 0 for a (near-)zero pivot
+// 1/d: v_rcp_f64 (~2^-26 relative) refined by ONE Newton step (~2^-50, 4e-15 relative) -- the pivots' error
+// then sits ~1e11 below the 1e-3 tolerance on x, and the LDLT's critical path is 68 reciprocals long;
+// 0 for a (near-)zero pivot
+__device__ __forceinline__ double rcp_f64(double d) {
   double r = __builtin_amdgcn_rcp(d);
-  double e = __builtin_fma(-d, r, 1.0);
-  r = __builtin_fma(r, e, r);
-  e = __builtin_fma(-d, r, 1.0);
+  const double e = __builtin_fma(-d, r, 1.0);
   r = __builtin_fma(r, e, r);
   return fabs(d) > DBL_MIN ? r : 0.0;
 }
@@ -1431,30 +1433,28 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     // HFinal = (HL + HM) + HA' ; diag *= (1+lambda) ; HFinal -= HSC' / (1+lambda)   (' = stitchDoubleMT
     // post-processing: frame off-diagonal blocks symmetrized, calib rows copied from the calib columns)
     const double sc = (double)(1.0f / (1 + lambda));
-    double hmv[SOLVE_NU];  // HM entries: one uniform branch for the whole set of loads
-    if (a.HM) {
-#pragma unroll
-      for (int u = 0; u < SOLVE_NU; u++) hmv[u] = a.HM[min(tid + u * nt, nn - 1)];
-    } else {
-#pragma unroll
-      for (int u = 0; u < SOLVE_NU; u++) hmv[u] = 0.0;
-    }
     double v[SOLVE_NU];
+    // HM (the marginalization prior) is usually absent: two instances of the loop, chosen by one uniform
+    // branch, so the common one carries no HM registers or loads
+    auto assemble = [&](auto withHM) {
 #pragma unroll
-    for (int u = 0; u < SOLVE_NU; u++) {
-      const int ix = min(tid + u * nt, nn - 1), r = (int)__umulhi((unsigned)ix, inv_n), c = ix - r * n;
-      const int idx = r * (n + 1) + c, tdx = c * (n + 1) + r;
-      const int fr = r < 4 ? -1 : (r - 4) >> 3, fc = c < 4 ? -1 : (c - 4) >> 3;
-      const double a0 = B[idx], a1 = B[tdx], b0 = LT[idx], b1 = LT[tdx], hl0 = px[r];
-      const double hm = hmv[u];
-      const bool sym = fr >= 0 && fc >= 0 && fr != fc, calrow = r < 4 && c >= 4;
-      const double ha_ = sym ? a0 + a1 : (calrow ? a1 : a0);
-      const double hsc = calrow ? b1 : b0;
-      const double hl = r == c ? hl0 : 0.0;
-      double hv = (hl + hm) + ha_;
-      hv = r == c ? hv * (1 + lambda) : hv;
-      v[u] = hv - hsc * sc;
-    }
+      for (int u = 0; u < SOLVE_NU; u++) {
+        const int ix = min(tid + u * nt, nn - 1), r = (int)__umulhi((unsigned)ix, inv_n), c = ix - r * n;
+        const int idx = r * (n + 1) + c, tdx = c * (n + 1) + r;
+        const int fr = r < 4 ? -1 : (r - 4) >> 3, fc = c < 4 ? -1 : (c - 4) >> 3;
+        const double a0 = B[idx], a1 = B[tdx], b0 = LT[idx], b1 = LT[tdx], hl0 = px[r];
+        const double hm = decltype(withHM)::value ? a.HM[r * n + c] : 0.0;
+        const bool sym = (fr >= 0) & (fc >= 0) & (fr != fc), calrow = (r < 4) & (c >= 4);
+        const double ha_ = sym ? a0 + a1 : (calrow ? a1 : a0);
+        const double hsc = calrow ? b1 : b0;
+        const double hl = r == c ? hl0 : 0.0;
+        double hv = (hl + hm) + ha_;
+        hv = r == c ? hv * (1 + lambda) : hv;
+        v[u] = hv - hsc * sc;
+      }
+    };
+    if (a.HM) assemble(std::integral_constant<bool, true>{});
+    else assemble(std::integral_constant<bool, false>{});
     if (tid < n) {
       const int q = tid;
       double hmd = 0.0;
