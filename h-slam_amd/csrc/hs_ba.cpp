@@ -112,6 +112,9 @@ struct hs_ctx {
   float* d_cand = nullptr;  // [nranks][cand_stride] newest-frame energy per point (-1 / NaN = none)
   int cand_stride = 0;
   bool hm_zero = true;      // marginalization prior not set: the solve skips HM
+  uint8_t* d_marg = nullptr;     // [nP] marginalization flags (hs_ba_marginalize_points)
+  float* d_adHTdelta = nullptr;  // [nF*nF][8] EnergyFunctional::adHTdeltaF for fixLinearizationF
+  float cDelta[4] = {0, 0, 0, 0};
   // kernel tracing (env HS_KTRACE=1): per-block wall-clock checkpoints of the last iteration
   bool tracing = false;
   long long *d_tr_lin = nullptr, *d_tr_acc = nullptr, *d_tr_solve = nullptr;
@@ -145,7 +148,8 @@ static void free_window(hs_ctx* c) {
                   c->d_r_center, c->d_p_actmask, c->d_p_HdiF, c->d_p_bdSumF, c->d_p_Hcd, c->d_p_JpJdF,
                   c->d_p_Jrec, c->d_p_step, c->d_p_energy, c->d_part, c->d_part_cnt, c->d_hccbc, c->d_adHost,
                   c->d_adTarget, c->d_adHostF, c->d_adTargetF, c->d_sys, c->d_HM, c->d_bM, c->d_Nproj, c->d_xAd,
-                  c->d_x, c->d_elog, c->d_cand, c->d_tr_lin, c->d_tr_acc, c->d_tr_solve, c->d_ticket};
+                  c->d_x, c->d_elog, c->d_cand, c->d_tr_lin, c->d_tr_acc, c->d_tr_solve, c->d_ticket,
+                  c->d_marg, c->d_adHTdelta};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   c->d_state = nullptr; c->d_pre = nullptr; c->d_frameTH = nullptr;
@@ -164,6 +168,8 @@ static void free_window(hs_ctx* c) {
   c->d_xAd = nullptr; c->d_x = nullptr; c->d_elog = nullptr; c->d_cand = nullptr;
   c->d_tr_lin = c->d_tr_acc = c->d_tr_solve = nullptr;
   c->d_ticket = nullptr;
+  c->d_marg = nullptr;
+  c->d_adHTdelta = nullptr;
   c->nF = c->nP = c->nR = 0;
   c->haveSystem = false;
 }
@@ -200,9 +206,15 @@ static int fetch_state(hs_ctx* c) {
 }
 
 // ---------------------------------------------------------------- launches (asynchronous)
-static int launch_linearize(hs_ctx* c, int fuse) {
+static int launch_linearize(hs_ctx* c, int fuse, bool marg = false) {
   HsLinArgs a;
   std::memset(&a, 0, sizeof(a));
+  if (marg) {  // hs_ba_marginalize_points: flags, adHTdeltaF and cDeltaF uploaded by the caller
+    a.marg = c->d_marg;
+    a.adHTdelta = c->d_adHTdelta;
+    for (int i = 0; i < 4; i++) a.cDelta[i] = c->cDelta[i];
+    a.margPriorFac = c->P.idepthFixPriorMargFac;
+  }
   for (int i = 0; i < c->nF; i++) a.img[i] = c->d_img[i];
   a.st = c->d_state;
   a.lp.huberTH = c->P.huberTH;
@@ -232,7 +244,7 @@ static int launch_linearize(hs_ctx* c, int fuse) {
 }
 
 // all-gather of newest-frame candidates, accumulate, stitch, all-reduce of the systems
-static int launch_reduce(hs_ctx* c) {
+static int launch_reduce(hs_ctx* c, bool skip_threshold = false) {
   if (c->comm && c->nranks > 1)
     HS_NCCL(ncclAllGather(c->d_cand + (size_t)c->rank * c->cand_stride, c->d_cand, c->cand_stride, ncclFloat,
                           c->comm, c->stream));
@@ -251,6 +263,7 @@ static int launch_reduce(hs_ctx* c) {
   a.frameTH = c->d_frameTH; a.newest = c->nF - 1;
   a.frameEnergyTHN = c->P.frameEnergyTHN; a.facMedian = c->P.frameEnergyTHFacMedian;
   a.constWeight = c->P.frameEnergyTHConstWeight; a.overallWeight = c->P.overallEnergyTHWeight;
+  a.skip_threshold = skip_threshold ? 1 : 0;
   HsStitchArgs& st = a.stitch;
   st.nF = c->nF; st.S = c->S;
   st.part = c->d_part; st.part_cnt = c->d_part_cnt; st.hccbc = c->d_hccbc;
@@ -473,7 +486,8 @@ int hs_params_default(hs_params* p) {
   p->trace_extraSlackOnTH = 1.2f;
   p->minTraceTestRadius = 2;
   p->trace_GNIterations = 3;
-  p->pad2 = 0;
+  p->idepthFixPriorMargFac = 600 * 600;
+  p->margWeightFac = 0.5f * 0.5f;
   return HS_OK;
 }
 
@@ -927,6 +941,67 @@ int hs_ba_set_marginal_prior(hs_ctx* c, const double* HM, const double* bM) {
   HS_HIP(hipMemcpyAsync(c->d_HM, c->HM.data(), sizeof(double) * n * n, hipMemcpyHostToDevice, c->stream));
   HS_HIP(hipMemcpyAsync(c->d_bM, c->bM.data(), sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
   HS_HIP(hipStreamSynchronize(c->stream));
+  return HS_OK;
+}
+
+// System::flagPointsForRemoval's per-point part (Src/Mapping.cpp:280-293) + EnergyFunctional::marginalizePointsF
+// (Src/EnergyFunctional.cpp:545-609) for n window points: one marginalization pass of the linearize / accumulate
+// kernels over the flagged points (resetOOB, linearize, applyRes, fixLinearizationF, addPoint<2>, SC addPoint(p,
+// false)), stitched into M and Msc; HM += margWeightFac (M - Msc), bM likewise.
+int hs_ba_marginalize_points(hs_ctx* c, int n, const int* points, double* HM_out, double* bM_out) {
+  if (!c || c->nF == 0) return fail(HS_ERR_STATE, "no window");
+  if (n < 0 || (n > 0 && !points)) return fail(HS_ERR_INVALID, "bad point list");
+  HS_HIP(hipSetDevice(c->device));
+  const int nF = c->nF, dim = c->dim();
+  std::vector<uint8_t> flag((size_t)std::max(c->nP, 1), 0);
+  for (int i = 0; i < n; i++) {
+    if (points[i] < 0 || points[i] >= c->nP) return fail(HS_ERR_INVALID, "point index out of range");
+    if (flag[points[i]]) return fail(HS_ERR_INVALID, "duplicate point in the marginalization list");
+    flag[points[i]] = 1;
+  }
+  if (!c->d_marg) HS_TRY(dalloc(&c->d_marg, (size_t)std::max(c->nP, 1)));
+  if (!c->d_adHTdelta) HS_TRY(dalloc(&c->d_adHTdelta, (size_t)nF * nF * 8));
+  // EnergyFunctional::setDeltaF (Src/EnergyFunctional.cpp:128-152) from the current device state, in fp32
+  HS_TRY(fetch_state(c));
+  const HsDevState& S = *c->h_state;
+  std::vector<float> adHTd((size_t)nF * nF * 8);
+  for (int h = 0; h < nF; h++)
+    for (int t = 0; t < nF; t++) {
+      const int idx = h + t * nF;
+      float dh[8], dt[8];
+      for (int i = 0; i < 8; i++) {
+        dh[i] = (float)(S.frames[h].state[i] - S.frames[h].state_zero[i]);
+        dt[i] = (float)(S.frames[t].state[i] - S.frames[t].state_zero[i]);
+      }
+      for (int q = 0; q < 8; q++) {
+        float s1 = 0, s2 = 0;
+        for (int r = 0; r < 8; r++) s1 += dh[r] * c->adHostF[(size_t)idx * 64 + r * 8 + q];
+        for (int r = 0; r < 8; r++) s2 += dt[r] * c->adTargetF[(size_t)idx * 64 + r * 8 + q];
+        adHTd[(size_t)idx * 8 + q] = s1 + s2;
+      }
+    }
+  for (int i = 0; i < 4; i++) c->cDelta[i] = (float)S.calib.value_minus_value_zero[i];
+  if (c->nP > 0) HS_HIP(hipMemcpy(c->d_marg, flag.data(), c->nP, hipMemcpyHostToDevice));
+  HS_HIP(hipMemcpy(c->d_adHTdelta, adHTd.data(), sizeof(float) * adHTd.size(), hipMemcpyHostToDevice));
+  // the pass: its own clean accumulation target; setNewFrameEnergyTH is not part of it
+  HS_HIP(hipMemsetAsync(c->d_sys, 0, sizeof(double) * c->acc_len(), c->stream));
+  HS_TRY(launch_linearize(c, 0, true));
+  HS_TRY(launch_reduce(c, true));
+  HS_HIP(hipStreamSynchronize(c->stream));
+  c->haveSystem = true;
+  std::vector<double> M((size_t)dim * dim), Mb(dim), Msc((size_t)dim * dim), Mbsc(dim);
+  HS_TRY(hs_ba_get_system(c, 0, M.data(), Mb.data()));    // stitchDouble(M, Mb, usePrior = false)
+  HS_TRY(hs_ba_get_system(c, 2, Msc.data(), Mbsc.data()));  // accSSE_bot->stitchDouble(Msc, Mbsc)
+  // the window's linearization is consumed: the caller drops the points (hs_ba_set_window) and relinearizes
+  c->haveSystem = false;
+  if (c->HM.size() != (size_t)dim * dim) c->HM.assign((size_t)dim * dim, 0.0);
+  if (c->bM.size() != (size_t)dim) c->bM.assign(dim, 0.0);
+  const double w = c->P.margWeightFac;
+  for (size_t i = 0; i < (size_t)dim * dim; i++) c->HM[i] += w * (M[i] - Msc[i]);
+  for (int i = 0; i < dim; i++) c->bM[i] += w * (Mb[i] - Mbsc[i]);
+  HS_TRY(hs_ba_set_marginal_prior(c, c->HM.data(), c->bM.data()));
+  if (HM_out) std::memcpy(HM_out, c->HM.data(), sizeof(double) * dim * dim);
+  if (bM_out) std::memcpy(bM_out, c->bM.data(), sizeof(double) * dim);
   return HS_OK;
 }
 

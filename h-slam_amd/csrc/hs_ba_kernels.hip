@@ -144,6 +144,17 @@ __global__ __launch_bounds__(64) void hs_k_linearize(HsLinArgs a) {
   // everything the linearization reads is loaded up front, unconditionally (clamped indices), so the
   // prologue is ONE memory round trip: residual state is in the slot layout [point][target slot] and the
   // host comes from the kernel arguments, so no load depends on another
+  if (a.marg && a.marg[p] == 0) {  // marginalization pass, point not marginalized: no active residual
+    if (lane == 0) {
+      a.p_energy[p] = 0.0;
+      a.p_actmask[p] = 0;
+      a.p_HdiF[p] = 0.f;
+      a.p_bdSumF[p] = 0.f;
+      reinterpret_cast<float4*>(a.p_Hcd)[p] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (t == nF - 1 && k == 0) a.newest_cand[p] = -1.f;
+    return;
+  }
   const int sl = p * 8 + t;                 // this lane's residual slot
   const int tc_ = t < nF ? t : 0;
   float idep = a.idepth[p], idep0 = a.idepth_zero[p];
@@ -207,9 +218,10 @@ __global__ __launch_bounds__(64) void hs_k_linearize(HsLinArgs a) {
       a.p_step[p] = step;
     }
   }
-  const int st = has ? st_raw : HS_RES_OOB;
-  const float oldE = has ? oldE_raw : 0.f;
-  const float oldNewE = has ? oldNewE_raw : 0.f;
+  // the marginalization pass starts from resetOOB (state IN, energies 0; Src/Mapping.cpp:285)
+  const int st = has ? (a.marg ? HS_RES_IN : st_raw) : HS_RES_OOB;
+  const float oldE = (has && !a.marg) ? oldE_raw : 0.f;
+  const float oldNewE = (has && !a.marg) ? oldNewE_raw : 0.f;
   HS_TRACE(a, 1);
 
   bool oob = false;
@@ -327,12 +339,36 @@ __global__ __launch_bounds__(64) void hs_k_linearize(HsLinArgs a) {
             qv[11] = hw * hw * (hy * hy + hz * hz);
             if (a.lp.affineOptModeA < 0) jab0 = 0;
             if (a.lp.affineOptModeB < 0) jab1 = 0;
-            // AccumulatedTopHessianSSE::addPoint<0>: JI_r, Jab_r, rr over resApprox = resF
-            qv[12] = resF * hy;
-            qv[13] = resF * hz;
-            qv[14] = resF * jab0;
-            qv[15] = resF * jab1;
-            qv[16] = resF * resF;
+            // AccumulatedTopHessianSSE::addPoint<0>: JI_r, Jab_r, rr over resApprox = resF; in the
+            // marginalization pass addPoint<2> over res_toZeroF = resF - [JI Jp, Jab] delta
+            // (fixLinearizationF, Src/OptimizationClasses.cpp:258-284)
+            float rz = resF;
+            if (a.marg) {
+              const float* dp = a.adHTdelta + (h + nF * t) * 8;
+              float jx = 0.f, jy = 0.f, cx = 0.f, cy = 0.f;
+#pragma unroll
+              for (int i = 0; i < 6; i++) {
+                jx += Jx[4 + i] * dp[i];
+                jy += Jy[4 + i] * dp[i];
+              }
+#pragma unroll
+              for (int i = 0; i < 4; i++) {
+                cx += Jx[i] * a.cDelta[i];
+                cy += Jy[i] * a.cDelta[i];
+              }
+              const float dF = idep - idep0;
+              const float Jpdx = jx + cx + Jd0 * dF;
+              const float Jpdy = jy + cy + Jd1 * dF;
+              rz = rz - hy * Jpdx;
+              rz = rz - hz * Jpdy;
+              rz = rz - jab0 * dp[6];
+              rz = rz - jab1 * dp[7];
+            }
+            qv[12] = rz * hy;
+            qv[13] = rz * hz;
+            qv[14] = rz * jab0;
+            qv[15] = rz * jab1;
+            qv[16] = rz * rz;
           }
         }
       }
@@ -462,15 +498,20 @@ __global__ __launch_bounds__(64) void hs_k_linearize(HsLinArgs a) {
         a.p_HdiF[p] = 0.f;
         a.p_bdSumF[p] = 0.f;
       } else {
-        const float priorF = a.priorF[p];
-        float Hh = Hdd + 0.f + priorF;  // Hdd_accAF + Hdd_accLF (no linearized residuals) + priorF
+        // marginalization pass: priorF *= idepthFixPriorMargFac, the sums are the LF ones (AF = 0), and
+        // AccumulatedSCHessianSSE::addPoint(p, shiftPriorToZero = false) (Src/EnergyFunctional.cpp:563,577)
+        const float priorF = a.marg ? a.priorF[p] * a.margPriorFac : a.priorF[p];
+        float Hh = a.marg ? (0.f + Hdd) + priorF : Hdd + 0.f + priorF;  // Hdd_accAF + Hdd_accLF + priorF
         if ((double)Hh < 1e-10) Hh = (float)1e-10;
         a.p_HdiF[p] = (float)(1.0 / (double)Hh);
-        float bdSumF = bd + 0.f;
-        bdSumF += priorF * (idep - idep0);
+        float bdSumF = a.marg ? 0.f + bd : bd + 0.f;
+        if (!a.marg) bdSumF += priorF * (idep - idep0);
         a.p_bdSumF[p] = bdSumF;
       }
-      reinterpret_cast<float4*>(a.p_Hcd)[p] = make_float4(Hcd[0] + 0.f, Hcd[1] + 0.f, Hcd[2] + 0.f, Hcd[3] + 0.f);
+      if (a.marg)
+        reinterpret_cast<float4*>(a.p_Hcd)[p] = make_float4(0.f + Hcd[0], 0.f + Hcd[1], 0.f + Hcd[2], 0.f + Hcd[3]);
+      else
+        reinterpret_cast<float4*>(a.p_Hcd)[p] = make_float4(Hcd[0] + 0.f, Hcd[1] + 0.f, Hcd[2] + 0.f, Hcd[3] + 0.f);
     }
   }
   HS_TRACE(a, 3);
@@ -849,7 +890,11 @@ __global__ __launch_bounds__(256) void hs_k_accumulate(HsAccArgs a) {
   HS_TRACE(a, 0);
   if (b == nb) { acc_energy_block(a); HS_TRACE(a, 15); return; }
   if (b == nb + 1) { acc_hcc_block(a); HS_TRACE(a, 15); return; }
-  if (b == nb + 2) { acc_energy_th_block(a); HS_TRACE(a, 15); return; }
+  if (b == nb + 2) {
+    if (!a.skip_threshold) acc_energy_th_block(a);
+    HS_TRACE(a, 15);
+    return;
+  }
   __shared__ AccLds T;
   __shared__ int s_last;
   if (a.blocked) acc_pair_block<true>(a, T);

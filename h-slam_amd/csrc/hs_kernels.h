@@ -33,6 +33,13 @@ struct HsLinArgs {
   int write_center;
   int fuse_step;               // apply resubstitute + point step of the previous solve first
   int host_begin[HS_MAXF + 1]; // first point of each host (points are sorted by host)
+  // marginalization pass (hs_ba_marginalize_points): only points with marg[p] != 0 are linearized (after
+  // resetOOB), their active residuals take fixLinearizationF, the SC prelude uses priorF * margPriorFac and no
+  // prior shift; every other point reports no active residual.  nullptr = the normal pass.
+  const uint8_t* marg;
+  const float* adHTdelta;      // [nF*nF][8] index host + nF*target (EnergyFunctional::adHTdeltaF)
+  float cDelta[4];             // EnergyFunctional::cDeltaF
+  float margPriorFac;          // setting_idepthFixPriorMargFac
   const HsPrecalc* pre;        // [nF*nF] host*nF + target
   const float* frameTH;        // [nF]
   const float* xAd;            // [nF*nF][8] index h*nF + t (fuse_step)
@@ -104,6 +111,7 @@ struct HsAccArgs {
   float* frameTH;
   int newest;
   float frameEnergyTHN, facMedian, constWeight, overallWeight;
+  int skip_threshold;          // marginalization pass: setNewFrameEnergyTH is not part of it
   long long* trace;
   // stitch fused into the accumulate launch: the last split block of a (host, target) pair to finish
   // (ticket counter) stitches that pair; the Hcc block adds accHcc / accbc itself

@@ -46,7 +46,8 @@ class hs_params(C.Structure):
         ("minOptIterations", C.c_int), ("pad", C.c_int)] + [(n, C.c_float) for n in (
         "outlierTH", "maxPixSearch", "trace_slackInterval", "trace_stepsize", "trace_minImprovementFactor",
         "trace_GNThreshold", "trace_extraSlackOnTH")] + [
-        ("minTraceTestRadius", C.c_int), ("trace_GNIterations", C.c_int), ("pad2", C.c_int)]
+        ("minTraceTestRadius", C.c_int), ("trace_GNIterations", C.c_int),
+        ("idepthFixPriorMargFac", C.c_float), ("margWeightFac", C.c_float)]
 
 
 # exported symbols of include/hs_ba.h (argument types)
@@ -67,6 +68,7 @@ SIGNATURES = {
     "hs_ba_get_points": ([VP] * 5, I),
     "hs_ba_get_frames": ([VP] * 5, I),
     "hs_ba_set_marginal_prior": ([VP, VP, VP], I),
+    "hs_ba_marginalize_points": ([VP, I, VP, VP, VP], I),
     "hs_ba_get_timings": ([VP, VP], I),
     "hs_comm_get_unique_id": ([VP], I),
     "hs_comm_init": ([VP, VP, I, I], I),

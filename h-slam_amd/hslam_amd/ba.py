@@ -86,6 +86,15 @@ class BAWindow:
         check(self.lib.hs_ba_set_marginal_prior(self.h, ptr(np.ascontiguousarray(HM, np.float64)),
                                                 ptr(np.ascontiguousarray(bM, np.float64))))
 
+    def marginalizePointsF(self, points):
+        """flagPointsForRemoval (per-point part) + EnergyFunctional::marginalizePointsF for window points
+        `points` (Src/Mapping.cpp:280-293, Src/EnergyFunctional.cpp:545-609).  Returns the updated (HM, bM);
+        the window's linearization is consumed (drop the points and relinearize)."""
+        p = np.ascontiguousarray(points, np.int32)
+        HM, bM = np.zeros((self.dim, self.dim)), np.zeros(self.dim)
+        check(self.lib.hs_ba_marginalize_points(self.h, len(p), ptr(p), ptr(HM), ptr(bM)))
+        return HM, bM
+
     def solveSystem(self, iteration):
         x = np.zeros(self.dim)
         check(self.lib.hs_ba_solve_system(self.h, iteration, ptr(x)))

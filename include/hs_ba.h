@@ -27,6 +27,8 @@
  *   hs_ba_get_system            HA/bA (accumulateAF_MT), HL/bL (accumulateLF_MT), H_sc/b_sc (accumulateSCF_MT)
  *   hs_ba_get_* / hs_ba_set_marginal_prior   read-back of PointFrameResidual / MapPoint / FrameOptimizationData
  *                               state; EnergyFunctional::HM/bM.
+ *   hs_ba_marginalize_points    System::flagPointsForRemoval (per-point part) + EnergyFunctional::marginalizePointsF
+ *                               (Src/Mapping.cpp:280-293; Src/EnergyFunctional.cpp:545-609).
  *   hs_comm_*                   (new) RCCL communicator for point-sharded windows; one rank per GPU.
  */
 #ifndef HS_BA_H
@@ -82,6 +84,16 @@ int hs_ba_get_points(hs_ctx* ctx, float* idepth, float* step, float* HdiF, float
 int hs_ba_get_frames(hs_ctx* ctx, double* state, float* energyTH, double* pose7, double* calib4);
 /* EnergyFunctional::HM / bM (marginalization prior); dim*dim and dim */
 int hs_ba_set_marginal_prior(hs_ctx* ctx, const double* HM, const double* bM);
+
+/* Marginalization of n window points (indices into the hs_points of hs_ba_set_window), replacing
+   System::flagPointsForRemoval's per-point part (Src/Mapping.cpp:280-293: resetOOB, linearize, applyRes,
+   fixLinearizationF of the active residuals) and EnergyFunctional::marginalizePointsF
+   (Src/EnergyFunctional.cpp:545-609: priorF *= idepthFixPriorMargFac, AccumulatedTopHessianSSE::addPoint<2>,
+   AccumulatedSCHessianSSE::addPoint(p, false), HM += margWeightFac (M - Msc), bM likewise).
+   HM_out / bM_out (nullable, dim*dim / dim): the updated prior, also kept by the context.  The call consumes the
+   window's current linearization: the caller drops the points (removePoint: hs_ba_set_window without them),
+   passes HM / bM to hs_ba_set_marginal_prior and linearizes again. */
+int hs_ba_marginalize_points(hs_ctx* ctx, int n, const int* points, double* HM_out, double* bM_out);
 
 /* device-event timing of the last hs_ba_optimize / hs_ba_iterate (ms, summed over the timed iterations):
    [0] linearize kernel, [1] accumulate + stitch (+ RCCL exchange), [2] solve + step kernel,

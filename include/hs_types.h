@@ -109,7 +109,9 @@ typedef struct hs_params {
   float trace_extraSlackOnTH;    /* 1.2    :93 */
   int minTraceTestRadius;        /* 2      :90 */
   int trace_GNIterations;        /* 3      :91 */
-  int pad2;
+  /* marginalization (EnergyFunctional::marginalizePointsF, Src/EnergyFunctional.cpp:563,601) */
+  float idepthFixPriorMargFac;   /* 600*600 :101 */
+  float margWeightFac;           /* 0.25   :80 */
 } hs_params;
 
 #ifdef __cplusplus

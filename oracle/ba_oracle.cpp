@@ -821,20 +821,25 @@ struct BA {
     }
   }
 
-  void accumulateTop(int mode, std::vector<double>& H, std::vector<double>& b) {
-    auto& acc = mode == 0 ? accTopA : accTopL;
-    auto& nres = mode == 0 ? nresA : nresL;
+  // mode 0: accumulateAF_MT, 1: accumulateLF_MT (Src/EnergyFunctional.cpp:155-220); 2: the marginalization pass of
+  // marginalizePointsF over `subset` (Src/EnergyFunctional.cpp:572-583, accSSE_top_A->addPoint<2>)
+  void accumulateTop(int mode, std::vector<double>& H, std::vector<double>& b, const std::vector<int>* subset = nullptr) {
+    auto& acc = mode == 1 ? accTopL : accTopA;
+    auto& nres = mode == 1 ? nresL : nresA;
     acc.assign(T, std::vector<AccApprox>(nF * nF));
     nres.assign(T, 0);
     for (auto& v : acc) for (auto& a : v) a.initialize();
+    const int N = subset ? (int)subset->size() : (int)points.size();
     auto body = [&](int mn, int mx, int tid) {
-      for (int i = mn; i < mx; i++) {
-        if (mode == 0) topAddPoint<0>(points[i], acc[tid], nres[tid]);
-        else topAddPoint<1>(points[i], acc[tid], nres[tid]);
+      for (int q = mn; q < mx; q++) {
+        PointO& pt = points[subset ? (*subset)[q] : q];
+        if (mode == 0) topAddPoint<0>(pt, acc[tid], nres[tid]);
+        else if (mode == 1) topAddPoint<1>(pt, acc[tid], nres[tid]);
+        else topAddPoint<2>(pt, acc[tid], nres[tid]);
       }
     };
-    if (mt) pool->reduce([&](int mn, int mx, double*, int tid) { body(mn, mx, tid); }, 0, (int)points.size(), 50);
-    else body(0, (int)points.size(), 0);
+    if (mt) pool->reduce([&](int mn, int mx, double*, int tid) { body(mn, mx, tid); }, 0, N, 50);
+    else body(0, N, 0);
     topStitch(acc, mode == 1, H, b);
     if (mode == 0) { lastResInA = 0; for (int v : nres) lastResInA += v; }
   }
@@ -872,7 +877,8 @@ struct BA {
     }
   }
 
-  void accumulateSC(std::vector<double>& H, std::vector<double>& b) {
+  void accumulateSC(std::vector<double>& H, std::vector<double>& b, const std::vector<int>* subset = nullptr,
+                    bool shiftPriorToZero = true) {
     const int n = dim();
     accE.assign(T, std::vector<AccXX<8, 4>>(nF * nF));
     accEB.assign(T, std::vector<AccX<8>>(nF * nF));
@@ -886,9 +892,12 @@ struct BA {
       accHcc[t].initialize();
       accbc[t].initialize();
     }
-    auto body = [&](int mn, int mx, int tid) { for (int i = mn; i < mx; i++) scAddPoint(points[i], true, tid); };
-    if (mt) pool->reduce([&](int mn, int mx, double*, int tid) { body(mn, mx, tid); }, 0, (int)points.size(), 50);
-    else body(0, (int)points.size(), 0);
+    const int N = subset ? (int)subset->size() : (int)points.size();
+    auto body = [&](int mn, int mx, int tid) {
+      for (int q = mn; q < mx; q++) scAddPoint(points[subset ? (*subset)[q] : q], shiftPriorToZero, tid);
+    };
+    if (mt) pool->reduce([&](int mn, int mx, double*, int tid) { body(mn, mx, tid); }, 0, N, 50);
+    else body(0, N, 0);
 
     std::vector<std::vector<double>> Hs(T, std::vector<double>(n * n, 0.0)), bs(T, std::vector<double>(n, 0.0));
     const int nf = nF, nframes2 = nF * nF;
@@ -963,6 +972,33 @@ struct BA {
       int hIdx = CP + h * 8;
       for (int r = 0; r < 8; r++) for (int c = 0; c < 4; c++) H[c * n + hIdx + r] = H[(hIdx + r) * n + c];
     }
+  }
+
+  // ------------------------------------------------------------ marginalization of points
+  // System::flagPointsForRemoval's per-point part for the points to marginalize (Src/Mapping.cpp:280-293:
+  // resetOOB, linearize, isLinearized = false, applyRes, fixLinearizationF of the active residuals), then
+  // EnergyFunctional::marginalizePointsF (Src/EnergyFunctional.cpp:545-609): priorF *= idepthFixPriorMargFac,
+  // top addPoint<2> + SC addPoint(p, false), M - Msc, HM += margWeightFac (M - Msc), bM likewise
+  // (SOLVER_ORTHOGONALIZE_POINTMARG is off in setting_solverMode, Src/Settings.cpp:114).
+  void marginalizePoints(const std::vector<int>& pts, float priorMargFac, float margWeightFac) {
+    setDeltaF();
+    for (int pi : pts) {
+      for (int ri : points[pi].residuals) {
+        ResO& r = res[ri];
+        r.resetOOB();
+        linearize(r);
+        r.isLinearized = false;
+        applyRes(r);
+        if (r.isActive()) fixLinearizationF(r);
+      }
+    }
+    for (int pi : pts) points[pi].priorF *= priorMargFac;
+    std::vector<double> M, Mb, Msc, Mbsc;
+    accumulateTop(2, M, Mb, &pts);
+    accumulateSC(Msc, Mbsc, &pts, false);
+    const int n = dim();
+    for (int i = 0; i < n * n; i++) HM[i] += margWeightFac * (M[i] - Msc[i]);
+    for (int i = 0; i < n; i++) bM[i] += margWeightFac * (Mb[i] - Mbsc[i]);
   }
 
   // ------------------------------------------------------------ nullspaces (System::getNullspaces)
@@ -1370,6 +1406,15 @@ void hso_ba_get_nullspaces(void* h, double* N /* 7 x dim */) {
 }
 
 int hso_ba_res_in_A(void* h) { return ((BA*)h)->lastResInA; }
+
+// marginalize n points (window indices): HM / bM updated in place and returned (dim*dim, dim)
+void hso_ba_marginalize_points(void* h, int n, const int* pts, float priorMargFac, float margWeightFac, double* HM_out,
+                               double* bM_out) {
+  BA* ba = (BA*)h;
+  ba->marginalizePoints(std::vector<int>(pts, pts + n), priorMargFac, margWeightFac);
+  std::memcpy(HM_out, ba->HM.data(), sizeof(double) * ba->HM.size());
+  std::memcpy(bM_out, ba->bM.data(), sizeof(double) * ba->bM.size());
+}
 
 /* SE3 helpers for the Sophus-vector tests */
 void hso_se3_exp(const double a[6], double out7[7]) { SE3::exp(a).toData(out7); }

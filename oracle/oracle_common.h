@@ -149,7 +149,8 @@ inline void params_default(hs_params* p) {
   p->trace_extraSlackOnTH = 1.2f;
   p->minTraceTestRadius = 2;
   p->trace_GNIterations = 3;
-  p->pad2 = 0;
+  p->idepthFixPriorMargFac = 600 * 600;
+  p->margWeightFac = 0.5f * 0.5f;
 }
 
 }  // namespace hso

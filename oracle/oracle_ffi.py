@@ -45,7 +45,8 @@ class hs_params(C.Structure):
         ("minOptIterations", C.c_int), ("pad", C.c_int)] + [(n, C.c_float) for n in (
         "outlierTH", "maxPixSearch", "trace_slackInterval", "trace_stepsize", "trace_minImprovementFactor",
         "trace_GNThreshold", "trace_extraSlackOnTH")] + [
-        ("minTraceTestRadius", C.c_int), ("trace_GNIterations", C.c_int), ("pad2", C.c_int)]
+        ("minTraceTestRadius", C.c_int), ("trace_GNIterations", C.c_int),
+        ("idepthFixPriorMargFac", C.c_float), ("margWeightFac", C.c_float)]
 
 
 def build(quiet=True):
@@ -79,6 +80,7 @@ def load(fast=False):
     lib.hso_ba_solve_system.argtypes = [vp, C.c_int, vp]
     lib.hso_ba_backup_state.argtypes = [vp]
     lib.hso_ba_set_marginal_prior.argtypes = [vp, vp, vp]
+    lib.hso_ba_marginalize_points.argtypes = [vp, C.c_int, vp, C.c_float, C.c_float, vp, vp]
     lib.hso_ba_do_step.argtypes = [vp]
     lib.hso_ba_do_step.restype = C.c_int
     lib.hso_ba_get_residuals.argtypes = [vp] * 10
@@ -203,6 +205,14 @@ class OracleBA:
 
     def backup_state(self):
         self.lib.hso_ba_backup_state(self.h)
+
+    def marginalize_points(self, pts):
+        """flagPointsForRemoval (per-point part) + marginalizePointsF for window points `pts`; returns (HM, bM)."""
+        p = np.ascontiguousarray(pts, np.int32)
+        HM, bM = np.zeros((self.dim, self.dim)), np.zeros(self.dim)
+        self.lib.hso_ba_marginalize_points(self.h, len(p), _p(p), self.params.idepthFixPriorMargFac,
+                                           self.params.margWeightFac, _p(HM), _p(bM))
+        return HM, bM
 
     def set_marginal_prior(self, HM, bM):
         self.lib.hso_ba_set_marginal_prior(self.h, _p(np.ascontiguousarray(HM, np.float64)),

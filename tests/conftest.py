@@ -23,3 +23,10 @@ def scene2k():
 def scene_small():
     from hslam_amd.scene import make_ba_scene
     return make_ba_scene(n_points=240, seed=7)
+
+
+@pytest.fixture(scope="session")
+def scene_marg():
+    """A nearly converged small window (most residuals IN at the first linearization): marginalization tests."""
+    from hslam_amd.scene import make_ba_scene
+    return make_ba_scene(n_points=240, seed=7, pose_noise=(0.001, 0.0005), idepth_noise=0.002)

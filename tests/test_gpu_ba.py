@@ -131,6 +131,37 @@ def test_solve_with_marginal_prior(scene_small):
         assert abs(eg - eo) <= 1e-3 * abs(eo)
 
 
+def test_marginalize_points(scene_marg):
+    """flagPointsForRemoval + marginalizePointsF on the device vs the oracle: the frames carry a state offset
+    from their linearization point (state != state_zero), so fixLinearizationF's adHTdeltaF term is live."""
+    import copy
+    s = copy.copy(scene_marg)
+    rng = np.random.default_rng(11)
+    st = np.zeros((s.n_frames, 10))
+    st[1:, :6] = rng.normal(size=(s.n_frames - 1, 6)) * 2e-3
+    st[1:, 6:8] = rng.normal(size=(s.n_frames - 1, 2)) * 1e-3
+    s.frames_state = st
+    g, o = _pair(s)
+    g.linearizeAll(reset=True)
+    o.linearize_all(reset=True)
+    o.apply_res()
+    pts = np.nonzero(s.pt_host == 0)[0][::2]
+    HMg, bMg = g.marginalizePointsF(pts)
+    HMo, bMo = o.marginalize_points(pts)
+    assert np.abs(HMo).max() > 0 and np.abs(bMo).max() > 0
+    okH, rH = _close_H(HMg, HMo)
+    okb, rb = _close_b(bMg, bMo, HMo)
+    assert okH, f"HM worst ratio {rH}"
+    assert okb, f"bM worst ratio {rb}"
+    rg, ro = g.residuals(), o.residuals()
+    assert np.array_equal(rg["state"], ro["state"])  # the marginalized points' residuals were relinearized
+    assert np.array_equal(rg["energy"], ro["energy"].astype(np.float32))
+    # the window is consumed: iterate refuses until relinearized
+    from hslam_amd._lib import HsError
+    with pytest.raises(HsError):
+        g.iterate(0, 1)
+
+
 def test_optimize_trajectory(scene2k):
     g, o = _pair(scene2k)
     ng, eg = g.optimize(6)

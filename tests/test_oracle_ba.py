@@ -80,3 +80,24 @@ def test_ground_truth_has_lower_energy():
     e_gt = OracleBA(s_gt).linearize_all(reset=True)
     e_n = OracleBA(s_noisy).linearize_all(reset=True)
     assert e_gt < 0.5 * e_n
+
+
+def test_marginalize_points_properties(scene_marg):
+    """marginalizePointsF restatement: HM = margWeightFac (M - Msc) is the Schur complement of the marginalized
+    points' Hessian block, so it is symmetric positive semi-definite (up to fp32 accumulation rounding) and
+    carries the same gauge freedoms as the window's Hessian."""
+    from oracle_ffi import OracleBA
+    o = OracleBA(scene_marg)
+    o.linearize_all(reset=True)
+    o.apply_res()
+    pts = np.nonzero(scene_marg.pt_host == 0)[0]
+    HM, bM = o.marginalize_points(pts)
+    scale = np.abs(np.diag(HM)).max()
+    assert scale > 0
+    assert np.abs(HM - HM.T).max() <= 1e-6 * scale
+    w = np.linalg.eigvalsh(0.5 * (HM + HM.T))
+    assert w.min() >= -1e-6 * scale
+    # marginalizing the same points again adds a second, identical contribution (the pass is a pure function of
+    # the window state once the points are relinearized)
+    HM2, bM2 = o.marginalize_points(pts)
+    np.testing.assert_allclose(HM2, 2 * HM, rtol=1e-6, atol=1e-9 * scale)
