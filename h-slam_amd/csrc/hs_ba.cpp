@@ -1005,6 +1005,104 @@ int hs_ba_marginalize_points(hs_ctx* c, int n, const int* points, double* HM_out
   return HS_OK;
 }
 
+// 8x8 inverse: LU with partial pivoting (row swaps recorded), then solve for the identity columns
+static bool inverse8(const double* A, double* Ainv) {
+  double lu[64];
+  int piv[8];
+  std::memcpy(lu, A, sizeof(lu));
+  for (int k = 0; k < 8; k++) {
+    int p = k;
+    for (int r = k + 1; r < 8; r++)
+      if (std::fabs(lu[r * 8 + k]) > std::fabs(lu[p * 8 + k])) p = r;
+    piv[k] = p;
+    if (p != k)
+      for (int j = 0; j < 8; j++) std::swap(lu[k * 8 + j], lu[p * 8 + j]);
+    if (lu[k * 8 + k] == 0.0) return false;
+    for (int r = k + 1; r < 8; r++) {
+      lu[r * 8 + k] /= lu[k * 8 + k];
+      for (int j = k + 1; j < 8; j++) lu[r * 8 + j] -= lu[r * 8 + k] * lu[k * 8 + j];
+    }
+  }
+  for (int col = 0; col < 8; col++) {
+    double x[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    x[col] = 1.0;
+    for (int k = 0; k < 8; k++) std::swap(x[k], x[piv[k]]);
+    for (int r = 1; r < 8; r++)
+      for (int j = 0; j < r; j++) x[r] -= lu[r * 8 + j] * x[j];
+    for (int r = 7; r >= 0; r--) {
+      for (int j = r + 1; j < 8; j++) x[r] -= lu[r * 8 + j] * x[j];
+      x[r] /= lu[r * 8 + r];
+    }
+    for (int r = 0; r < 8; r++) Ainv[r * 8 + col] = x[r];
+  }
+  return true;
+}
+
+// EnergyFunctional::marginalizeFrame (Src/EnergyFunctional.cpp:456-543) on the context's HM / bM: a dense 68x68
+// host operation once per marginalized keyframe (not on the GN path).
+int hs_ba_marginalize_frame(hs_ctx* c, int frame, double* HM_out, double* bM_out) {
+  if (!c || c->nF == 0) return fail(HS_ERR_STATE, "no window");
+  if (frame < 0 || frame >= c->nF) return fail(HS_ERR_INVALID, "frame index out of range");
+  if (c->nF < 2) return fail(HS_ERR_INVALID, "cannot marginalize the only frame");
+  HS_HIP(hipSetDevice(c->device));
+  HS_TRY(fetch_state(c));
+  const int od = c->dim(), nd = od - 8, f0 = 4 + 8 * frame;
+  std::vector<double> HMc = c->HM, bMc = c->bM;
+  if (HMc.size() != (size_t)od * od) HMc.assign((size_t)od * od, 0.0);
+  if (bMc.size() != (size_t)od) bMc.assign(od, 0.0);
+  // order: every row except the frame's, then the frame's 8 (the reference's move-to-end)
+  std::vector<int> ord;
+  for (int i = 0; i < od; i++)
+    if (i < f0 || i >= f0 + 8) ord.push_back(i);
+  for (int i = 0; i < 8; i++) ord.push_back(f0 + i);
+  std::vector<double> H((size_t)od * od), b(od);
+  for (int r = 0; r < od; r++) {
+    b[r] = bMc[ord[r]];
+    for (int q = 0; q < od; q++) H[(size_t)r * od + q] = HMc[(size_t)ord[r] * od + ord[q]];
+  }
+  const hs::FrameH& F = c->h_state->frames[frame];
+  for (int i = 0; i < 8; i++) {  // the frame's prior, added here instead of to the active system
+    H[(size_t)(nd + i) * od + nd + i] += F.prior[i];
+    b[nd + i] += F.prior[i] * F.delta_prior[i];
+  }
+  std::vector<double> sv(od);
+  for (int i = 0; i < od; i++) sv[i] = std::sqrt(std::fabs(H[(size_t)i * od + i]) + 10.0);
+  for (int r = 0; r < od; r++) {
+    for (int q = 0; q < od; q++) H[(size_t)r * od + q] = (1.0 / sv[r]) * H[(size_t)r * od + q] * (1.0 / sv[q]);
+    b[r] = (1.0 / sv[r]) * b[r];
+  }
+  double hpi[64], hinv[64];
+  for (int r = 0; r < 8; r++)
+    for (int q = 0; q < 8; q++) hpi[r * 8 + q] = 0.5f * (H[(size_t)(nd + r) * od + nd + q] * 2.0);
+  if (!inverse8(hpi, hinv)) return fail(HS_ERR_NONFINITE, "singular frame block in marginalizeFrame");
+  for (int i = 0; i < 64; i++) hinv[i] = 0.5f * (hinv[i] * 2.0);
+  for (int r = 0; r < nd; r++) {
+    double bl[8];  // row r of (bottom-left)^T * hpi
+    for (int q = 0; q < 8; q++) {
+      double t = 0;
+      for (int k = 0; k < 8; k++) t += H[(size_t)(nd + k) * od + r] * hinv[k * 8 + q];
+      bl[q] = t;
+    }
+    for (int q = 0; q < nd; q++) {
+      double t = 0;
+      for (int k = 0; k < 8; k++) t += bl[k] * H[(size_t)(nd + k) * od + q];
+      H[(size_t)r * od + q] -= t;
+    }
+    double t = 0;
+    for (int k = 0; k < 8; k++) t += bl[k] * b[nd + k];
+    b[r] -= t;
+  }
+  std::vector<double> HMn((size_t)nd * nd), bMn(nd);
+  for (int r = 0; r < nd; r++) {
+    bMn[r] = sv[r] * b[r];
+    for (int q = 0; q < nd; q++)
+      HMn[(size_t)r * nd + q] = 0.5 * (sv[r] * H[(size_t)r * od + q] * sv[q] + sv[q] * H[(size_t)q * od + r] * sv[r]);
+  }
+  if (HM_out) std::memcpy(HM_out, HMn.data(), sizeof(double) * nd * nd);
+  if (bM_out) std::memcpy(bM_out, bMn.data(), sizeof(double) * nd);
+  return HS_OK;
+}
+
 int hs_ba_get_timings(hs_ctx* c, double* out6) {
   if (!c || !out6) return fail(HS_ERR_INVALID, "null");
   out6[0] = c->t_lin; out6[1] = c->t_acc; out6[2] = c->t_solve; out6[3] = c->t_timed; out6[4] = c->t_wall;

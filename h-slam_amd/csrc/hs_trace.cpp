@@ -11,6 +11,7 @@
 #include "../../include/hs_ba.h"
 #include "../../include/hs_trace.h"
 #include "hs_trace_kernels.h"
+#include "hs_pyr_kernels.h"
 
 namespace hs {
 extern thread_local std::string g_err;
@@ -43,6 +44,7 @@ struct hs_tracer {
   float4* d_host_img[HS_TRC_MAXHOST] = {nullptr};
   const float4** d_host_tab = nullptr;
   float4* d_new = nullptr;
+  float* d_raw = nullptr;  // staging of a raw level-0 frame (hs_tracer_set_frame_raw)
   bool have_frame = false;
   hs_trace_host* d_hosts = nullptr;
   int* d_host = nullptr;
@@ -160,7 +162,7 @@ void hs_tracer_destroy(hs_tracer* t) {
   for (auto* p : t->d_host_img) (void)hipFree(p);
   void* bufs[] = {t->d_host_tab, t->d_new, t->d_hosts, t->d_host, t->d_u, t->d_v, t->d_color, t->d_weights,
                   t->d_gradH, t->d_energyTH, t->d_quality, t->d_idmin, t->d_idmax, t->d_uv, t->d_interval,
-                  t->d_status, t->d_steps, t->d_counts};
+                  t->d_status, t->d_steps, t->d_counts, t->d_raw};
   for (void* b : bufs) (void)hipFree(b);
   (void)hipHostFree(t->h_counts);
   if (t->e0) (void)hipEventDestroy(t->e0);
@@ -231,6 +233,18 @@ int hs_tracer_set_frame(hs_tracer* t, const float* img) {
   TR_HIP(hipSetDevice(t->device));
   int rc = upload_img(t, t->d_new, img);
   if (rc) return rc;
+  t->have_frame = true;
+  return HS_OK;
+}
+
+int hs_tracer_set_frame_raw(hs_tracer* t, const float* img) {
+  if (!t || !img) return cfail(HS_ERR_INVALID, "null argument");
+  TR_HIP(hipSetDevice(t->device));
+  if (!t->d_raw) TR_HIP(hipMalloc((void**)&t->d_raw, sizeof(float) * t->W * t->H));
+  TR_HIP(hipMemcpyAsync(t->d_raw, img, sizeof(float) * t->W * t->H, hipMemcpyHostToDevice, t->stream));
+  float4* lv[1] = {t->d_new};
+  TR_HIP(hs_build_dir_pyramid(t->stream, t->d_raw, t->W, t->H, 1, lv, nullptr));
+  TR_HIP(hipStreamSynchronize(t->stream));
   t->have_frame = true;
   return HS_OK;
 }

@@ -11,6 +11,7 @@
 #include "../../include/hs_ba.h"
 #include "../../include/hs_track.h"
 #include "hs_track_kernels.h"
+#include "hs_pyr_kernels.h"
 
 namespace hs {
 extern thread_local std::string g_err;
@@ -50,6 +51,7 @@ struct hs_tracker {
   int* d_pcn = nullptr;
   int *d_bcnt = nullptr, *d_boff = nullptr;
   float *d_pts = nullptr;  // cu | cv | cid | hdi
+  float* d_raw = nullptr;  // staging of a raw level-0 frame (hs_tracker_set_frame_raw)
   int pts_cap = 0;
   double* d_Tin = nullptr;
   HsTryOut* d_out = nullptr;
@@ -226,7 +228,7 @@ void hs_tracker_destroy(hs_tracker* t) {
     for (void* p : ps)
       if (p) (void)hipFree(p);
   }
-  void* ps[] = {t->d_pcn, t->d_bcnt, t->d_boff, t->d_pts, t->d_Tin, t->d_out, t->d_lmlog, t->d_lmlvl};
+  void* ps[] = {t->d_pcn, t->d_bcnt, t->d_boff, t->d_pts, t->d_Tin, t->d_out, t->d_lmlog, t->d_lmlvl, t->d_raw};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   if (t->h_out) (void)hipHostFree(t->h_out);
@@ -316,6 +318,18 @@ int hs_tracker_set_frame(hs_tracker* t, const float* const* new_pyr, float ab_ex
   if (!t || !new_pyr) return tfail(HS_ERR_INVALID, "null argument");
   TS_HIP(hipSetDevice(t->device));
   TS_TRY(upload_pyr(t, t->d_new, new_pyr));
+  t->newExposure = ab_exposure;
+  t->haveFrame = true;
+  return HS_OK;
+}
+
+int hs_tracker_set_frame_raw(hs_tracker* t, const float* img, float ab_exposure) {
+  if (!t || !img) return tfail(HS_ERR_INVALID, "null argument");
+  TS_HIP(hipSetDevice(t->device));
+  if (!t->d_raw) TS_HIP(hipMalloc((void**)&t->d_raw, sizeof(float) * t->W * t->H));
+  TS_HIP(hipMemcpyAsync(t->d_raw, img, sizeof(float) * t->W * t->H, hipMemcpyHostToDevice, t->stream));
+  TS_HIP(hs_build_dir_pyramid(t->stream, t->d_raw, t->W, t->H, t->nlev, t->d_new, nullptr));
+  TS_HIP(hipStreamSynchronize(t->stream));  // the caller's buffer may go away after return
   t->newExposure = ab_exposure;
   t->haveFrame = true;
   return HS_OK;

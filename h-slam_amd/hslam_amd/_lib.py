@@ -69,6 +69,7 @@ SIGNATURES = {
     "hs_ba_get_frames": ([VP] * 5, I),
     "hs_ba_set_marginal_prior": ([VP, VP, VP], I),
     "hs_ba_marginalize_points": ([VP, I, VP, VP, VP], I),
+    "hs_ba_marginalize_frame": ([VP, I, VP, VP], I),
     "hs_ba_get_timings": ([VP, VP], I),
     "hs_comm_get_unique_id": ([VP], I),
     "hs_comm_init": ([VP, VP, I, I], I),
@@ -83,6 +84,9 @@ SIGNATURES = {
     "hs_tracker_track_tries": ([VP, I, VP, VP, VP, C.c_float, VP, VP, VP, VP, VP, VP], I),
     "hs_tracker_get_lm_log": ([VP, I, I, VP, VP, VP, VP, VP], I),
     "hs_tracker_last_ms": ([VP, VP], I),
+    "hs_tracker_set_frame_raw": ([VP, VP, C.c_float], I),
+    # include/hs_pyr.h
+    "hs_dir_pyramid": ([I, I, I, I, VP, VP, VP], I),
     # include/hs_trace.h
     "hs_tracer_create": ([VP, VP, I, I, I, I], I),
     "hs_tracer_destroy": ([VP], None),
@@ -91,6 +95,7 @@ SIGNATURES = {
     "hs_tracer_clear": ([VP], I),
     "hs_tracer_set_state": ([VP] * 5, I),
     "hs_tracer_set_frame": ([VP, VP], I),
+    "hs_tracer_set_frame_raw": ([VP, VP], I),
     "hs_tracer_trace": ([VP, I, VP, VP], I),
     "hs_tracer_get_points": ([VP] * 12, I),
     "hs_tracer_reinit": ([VP], I),

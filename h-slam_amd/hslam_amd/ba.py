@@ -95,6 +95,14 @@ class BAWindow:
         check(self.lib.hs_ba_marginalize_points(self.h, len(p), ptr(p), ptr(HM), ptr(bM)))
         return HM, bM
 
+    def marginalizeFrame(self, frame):
+        """EnergyFunctional::marginalizeFrame (Src/EnergyFunctional.cpp:456-543) on this window's HM / bM:
+        returns the (dim-8) prior of the window without `frame`."""
+        n = self.dim - 8
+        HM, bM = np.zeros((n, n)), np.zeros(n)
+        check(self.lib.hs_ba_marginalize_frame(self.h, int(frame), ptr(HM), ptr(bM)))
+        return HM, bM
+
     def solveSystem(self, iteration):
         x = np.zeros(self.dim)
         check(self.lib.hs_ba_solve_system(self.h, iteration, ptr(x)))

@@ -69,6 +69,12 @@ class ImmatureTracer:
         assert a.shape == (self.H, self.W, 3)
         check(self.lib.hs_tracer_set_frame(self.h, ptr(a)))
 
+    def set_frame_raw(self, img):
+        """The frame to trace on as its raw level-0 image: DirPyr[0] is built on the device."""
+        a = np.ascontiguousarray(img, np.float32)
+        assert a.shape == (self.H, self.W)
+        check(self.lib.hs_tracer_set_frame_raw(self.h, ptr(a)))
+
     def traceNewCoarse(self, KRKi, Kt, aff, counts=True):
         hosts = hosts_array(KRKi, Kt, aff)
         c = np.zeros(6, np.int32)

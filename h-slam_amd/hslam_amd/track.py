@@ -60,6 +60,12 @@ class CoarseTracker:
         arrs, pp = _pyr_ptrs(new_pyr)
         check(self.lib.hs_tracker_set_frame(self.h, C.cast(pp, C.c_void_p), float(ab_exposure)))
 
+    def setNewFrameRaw(self, img, ab_exposure):
+        """The frame to track as its raw level-0 image: Frame::CreateDirPyrs runs on the device."""
+        a = np.ascontiguousarray(img, dtype=np.float32)
+        assert a.shape == (self.height, self.width)
+        check(self.lib.hs_tracker_set_frame_raw(self.h, ptr(a), float(ab_exposure)))
+
     def set_scene(self, s):
         """Reference + new frame of a hslam_amd.scene.TrackScene."""
         self.setCoarseTrackingRef(s.ref_pyr, s.ref_exposure, s.ref_aff, s.pt_u, s.pt_v, s.pt_idepth, s.pt_hdi)

@@ -29,6 +29,7 @@
  *                               state; EnergyFunctional::HM/bM.
  *   hs_ba_marginalize_points    System::flagPointsForRemoval (per-point part) + EnergyFunctional::marginalizePointsF
  *                               (Src/Mapping.cpp:280-293; Src/EnergyFunctional.cpp:545-609).
+ *   hs_ba_marginalize_frame     EnergyFunctional::marginalizeFrame (Src/EnergyFunctional.cpp:456-543).
  *   hs_comm_*                   (new) RCCL communicator for point-sharded windows; one rank per GPU.
  */
 #ifndef HS_BA_H
@@ -94,6 +95,12 @@ int hs_ba_set_marginal_prior(hs_ctx* ctx, const double* HM, const double* bM);
    window's current linearization: the caller drops the points (removePoint: hs_ba_set_window without them),
    passes HM / bM to hs_ba_set_marginal_prior and linearizes again. */
 int hs_ba_marginalize_points(hs_ctx* ctx, int n, const int* points, double* HM_out, double* bM_out);
+
+/* EnergyFunctional::marginalizeFrame (Src/EnergyFunctional.cpp:456-543) of window frame `frame` on the
+   context's HM / bM: the frame's prior is added, its 8 rows are Schur-complemented out of the scaled prior.
+   HM_out / bM_out: (dim-8)^2 / dim-8, the prior of the window without that frame (pass it to
+   hs_ba_set_marginal_prior after the next hs_ba_set_window).  The context's own window is unchanged. */
+int hs_ba_marginalize_frame(hs_ctx* ctx, int frame, double* HM_out, double* bM_out);
 
 /* device-event timing of the last hs_ba_optimize / hs_ba_iterate (ms, summed over the timed iterations):
    [0] linearize kernel, [1] accumulate + stitch (+ RCCL exchange), [2] solve + step kernel,

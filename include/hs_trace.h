@@ -55,6 +55,8 @@ int hs_tracer_set_state(hs_tracer* t, const float* idepth_min, const float* idep
 
 /* the frame to trace on (level 0 image); stays resident until the next call */
 int hs_tracer_set_frame(hs_tracer* t, const float* img_lvl0);
+/* the same from the raw level-0 image (W*H floats): DirPyr[0] built on the device (include/hs_pyr.h) */
+int hs_tracer_set_frame_raw(hs_tracer* t, const float* img);
 /* traceOn of every point; hosts[n_hosts] indexed by the points' host slot.  counts6 (nullable): number of
    points per ImmaturePointStatus after the call (the trace_good/oob/... tallies of Mapping.cpp:513-520);
    with counts6 == NULL the call returns without waiting for the device. */

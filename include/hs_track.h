@@ -45,6 +45,9 @@ int hs_tracker_set_ref(hs_tracker* t, const float* const* ref_pyr, float ab_expo
 int hs_tracker_get_ref(hs_tracker* t, int lvl, int* n, float* u, float* v, float* idepth, float* color);
 /* the frame to track: its pyramid and ab_exposure */
 int hs_tracker_set_frame(hs_tracker* t, const float* const* new_pyr, float ab_exposure);
+/* the frame to track as its raw level-0 image (W*H floats, ImageData::fImgL): Frame::CreateDirPyrs runs on the
+   device (include/hs_pyr.h, Src/Frame.cpp:104-181) into the tracker's pyramid */
+int hs_tracker_set_frame_raw(hs_tracker* t, const float* img, float ab_exposure);
 /* one calcRes at (refToNew, aff) with cutoffTH; res6 = {E, numTermsInE, flowT, 0, flowRT, saturated ratio};
    H64 / b8 (nullable) = calcGSSSE on the warped buffer; n_warped = buf_warped_n (padded to 4) */
 int hs_tracker_calc_res(hs_tracker* t, int lvl, const double T7[7], const double aff[2], float cutoffTH,

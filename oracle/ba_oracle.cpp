@@ -1001,6 +1001,93 @@ struct BA {
     for (int i = 0; i < n; i++) bM[i] += margWeightFac * (Mb[i] - Mbsc[i]);
   }
 
+  // ------------------------------------------------------------ EnergyFunctional::marginalizeFrame
+  // (Src/EnergyFunctional.cpp:456-543): move frame f's 8 rows / cols of HM / bM to the end, add its prior,
+  // scale by 1/sqrt(|diag| + 10), Schur-complement the 8x8 block out (hpi = 0.5f*(hpi+hpi) kept as in the
+  // reference: a no-op), unscale, symmetrize.  Outputs the (dim-8) prior; the window itself is not changed.
+  void marginalizeFrame(int f, std::vector<double>& HMo, std::vector<double>& bMo) {
+    setDeltaF();  // EFDeltaValid
+    const int odim = dim(), ndim = odim - 8;
+    std::vector<int> perm(odim);  // new position -> old index
+    int q = 0;
+    for (int i = 0; i < odim; i++)
+      if (i < CP + 8 * f || i >= CP + 8 * f + 8) perm[q++] = i;
+    for (int i = 0; i < 8; i++) perm[q++] = CP + 8 * f + i;
+    std::vector<double> H(odim * odim), b(odim);
+    for (int r = 0; r < odim; r++) {
+      b[r] = bM[perm[r]];
+      for (int c = 0; c < odim; c++) H[r * odim + c] = HM[perm[r] * odim + perm[c]];
+    }
+    const FrameO& fr = frames[f];
+    for (int i = 0; i < 8; i++) {
+      H[(ndim + i) * odim + ndim + i] += fr.prior[i];
+      b[ndim + i] += fr.prior[i] * fr.delta_prior[i];
+    }
+    std::vector<double> S(odim), SI(odim);
+    for (int i = 0; i < odim; i++) {
+      S[i] = std::sqrt(std::fabs(H[i * odim + i]) + 10.0);
+      SI[i] = 1.0 / S[i];
+    }
+    for (int r = 0; r < odim; r++) {
+      for (int c = 0; c < odim; c++) H[r * odim + c] = SI[r] * H[r * odim + c] * SI[c];
+      b[r] = SI[r] * b[r];
+    }
+    double hpi[64], inv[64];
+    for (int r = 0; r < 8; r++)
+      for (int c = 0; c < 8; c++) hpi[r * 8 + c] = H[(ndim + r) * odim + ndim + c];
+    for (int i = 0; i < 64; i++) hpi[i] = 0.5f * (hpi[i] + hpi[i]);
+    invert_pp(hpi, inv, 8);
+    for (int i = 0; i < 64; i++) inv[i] = 0.5f * (inv[i] + inv[i]);
+    // bli = H(bottom, left)^T * hpi  (ndim x 8)
+    std::vector<double> bli(ndim * 8, 0.0);
+    for (int r = 0; r < ndim; r++)
+      for (int c = 0; c < 8; c++) {
+        double acc = 0;
+        for (int k = 0; k < 8; k++) acc += H[(ndim + k) * odim + r] * inv[k * 8 + c];
+        bli[r * 8 + c] = acc;
+      }
+    for (int r = 0; r < ndim; r++) {
+      for (int c = 0; c < ndim; c++) {
+        double acc = 0;
+        for (int k = 0; k < 8; k++) acc += bli[r * 8 + k] * H[(ndim + k) * odim + c];
+        H[r * odim + c] -= acc;
+      }
+      double acc = 0;
+      for (int k = 0; k < 8; k++) acc += bli[r * 8 + k] * b[ndim + k];
+      b[r] -= acc;
+    }
+    HMo.assign(ndim * ndim, 0.0);
+    bMo.assign(ndim, 0.0);
+    for (int r = 0; r < ndim; r++) {
+      bMo[r] = S[r] * b[r];
+      for (int c = 0; c < ndim; c++) {
+        const double u = S[r] * H[r * odim + c] * S[c], ut = S[c] * H[c * odim + r] * S[r];
+        HMo[r * ndim + c] = 0.5 * (u + ut);
+      }
+    }
+  }
+  // inverse by Gauss-Jordan elimination with partial pivoting (Eigen's PartialPivLU-based inverse for 8x8)
+  static void invert_pp(const double* A, double* X, int n) {
+    std::vector<double> M(A, A + n * n);
+    for (int i = 0; i < n * n; i++) X[i] = 0;
+    for (int i = 0; i < n; i++) X[i * n + i] = 1;
+    for (int c = 0; c < n; c++) {
+      int pr = c;
+      for (int r = c + 1; r < n; r++)
+        if (std::fabs(M[r * n + c]) > std::fabs(M[pr * n + c])) pr = r;
+      if (pr != c)
+        for (int k = 0; k < n; k++) { std::swap(M[c * n + k], M[pr * n + k]); std::swap(X[c * n + k], X[pr * n + k]); }
+      const double d = M[c * n + c];
+      for (int k = 0; k < n; k++) { M[c * n + k] /= d; X[c * n + k] /= d; }
+      for (int r = 0; r < n; r++) {
+        if (r == c) continue;
+        const double f = M[r * n + c];
+        if (f == 0.0) continue;
+        for (int k = 0; k < n; k++) { M[r * n + k] -= f * M[c * n + k]; X[r * n + k] -= f * X[c * n + k]; }
+      }
+    }
+  }
+
   // ------------------------------------------------------------ nullspaces (System::getNullspaces)
   void getNullspaces() {
     const int n = dim();
@@ -1406,6 +1493,15 @@ void hso_ba_get_nullspaces(void* h, double* N /* 7 x dim */) {
 }
 
 int hso_ba_res_in_A(void* h) { return ((BA*)h)->lastResInA; }
+
+// marginalizeFrame(f): the (dim-8) prior after removing frame f (the window is not changed)
+void hso_ba_marginalize_frame(void* h, int f, double* HM_out, double* bM_out) {
+  BA* ba = (BA*)h;
+  std::vector<double> H, b;
+  ba->marginalizeFrame(f, H, b);
+  std::memcpy(HM_out, H.data(), sizeof(double) * H.size());
+  std::memcpy(bM_out, b.data(), sizeof(double) * b.size());
+}
 
 // marginalize n points (window indices): HM / bM updated in place and returned (dim*dim, dim)
 void hso_ba_marginalize_points(void* h, int n, const int* pts, float priorMargFac, float margWeightFac, double* HM_out,

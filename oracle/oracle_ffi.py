@@ -81,6 +81,7 @@ def load(fast=False):
     lib.hso_ba_backup_state.argtypes = [vp]
     lib.hso_ba_set_marginal_prior.argtypes = [vp, vp, vp]
     lib.hso_ba_marginalize_points.argtypes = [vp, C.c_int, vp, C.c_float, C.c_float, vp, vp]
+    lib.hso_ba_marginalize_frame.argtypes = [vp, C.c_int, vp, vp]
     lib.hso_ba_do_step.argtypes = [vp]
     lib.hso_ba_do_step.restype = C.c_int
     lib.hso_ba_get_residuals.argtypes = [vp] * 10
@@ -106,6 +107,7 @@ def load(fast=False):
     lib.hso_trk_get_log.argtypes = [vp, C.c_int, vp, vp, vp, vp]
     lib.hso_trk_get_log.restype = C.c_int
     lib.hso_trk_track_tries.argtypes = [vp, C.c_int, vp, vp, vp, C.c_float, C.c_int] + [vp] * 6
+    lib.hso_dir_pyramid.argtypes = [C.c_int, C.c_int, C.c_int, vp, vp, vp]
     lib.hso_trc_create.restype = vp
     lib.hso_trc_create.argtypes = [vp, C.c_int, C.c_int]
     lib.hso_trc_destroy.argtypes = [vp]
@@ -212,6 +214,13 @@ class OracleBA:
         HM, bM = np.zeros((self.dim, self.dim)), np.zeros(self.dim)
         self.lib.hso_ba_marginalize_points(self.h, len(p), _p(p), self.params.idepthFixPriorMargFac,
                                            self.params.margWeightFac, _p(HM), _p(bM))
+        return HM, bM
+
+    def marginalize_frame(self, f):
+        """EnergyFunctional::marginalizeFrame(f): the (dim-8) HM / bM after removing frame f."""
+        n = self.dim - 8
+        HM, bM = np.zeros((n, n)), np.zeros(n)
+        self.lib.hso_ba_marginalize_frame(self.h, int(f), _p(HM), _p(bM))
         return HM, bM
 
     def set_marginal_prior(self, HM, bM):
@@ -436,3 +445,21 @@ class OracleTracer:
                    gradH=np.zeros((n, 4), np.float32))
         self.lib.hso_trc_get(self.h, *[_p(out[k]) for k in TRACE_FIELDS])
         return out
+
+
+# ------------------------------------------------------------------ Frame::CreateDirPyrs restatement
+def dir_pyramid(img, n_levels):
+    """([(h_l, w_l, 3) float32 DirPyr levels], [(h_l, w_l) absSquaredGrad]) of a W x H fp32 image."""
+    img = np.ascontiguousarray(img, np.float32)
+    H, W = img.shape
+    sizes = [(H >> l, W >> l) for l in range(n_levels)]
+    out = np.zeros(sum(h * w * 3 for h, w in sizes), np.float32)
+    ag = np.zeros(sum(h * w for h, w in sizes), np.float32)
+    load().hso_dir_pyramid(W, H, n_levels, _p(img), _p(out), _p(ag))
+    pyr, grads, o3, o1 = [], [], 0, 0
+    for h, w in sizes:
+        pyr.append(out[o3:o3 + h * w * 3].reshape(h, w, 3))
+        grads.append(ag[o1:o1 + h * w].reshape(h, w))
+        o3 += h * w * 3
+        o1 += h * w
+    return pyr, grads

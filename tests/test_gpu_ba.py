@@ -162,6 +162,24 @@ def test_marginalize_points(scene_marg):
         g.iterate(0, 1)
 
 
+@pytest.mark.parametrize("frame", [0, 3, 7])
+def test_marginalize_frame(scene_marg, frame):
+    """EnergyFunctional::marginalizeFrame on the same HM / bM (a marginalized-points prior) in the product library
+    and in the oracle: move-to-end, frame prior, scaled 8x8 Schur complement, unscale, symmetrize."""
+    g, o = _pair(scene_marg)
+    o.linearize_all(reset=True)
+    o.apply_res()
+    HM, bM = o.marginalize_points(np.nonzero(scene_marg.pt_host == 1)[0])
+    g.set_marginal_prior(HM, bM)
+    Hg, bg = g.marginalizeFrame(frame)
+    Ho, bo = o.marginalize_frame(frame)
+    assert Hg.shape == (g.dim - 8, g.dim - 8)
+    scale = np.abs(Ho).max()
+    assert scale > 0 and np.allclose(Hg, Hg.T)
+    np.testing.assert_allclose(Hg, Ho, rtol=1e-8, atol=1e-10 * scale)
+    np.testing.assert_allclose(bg, bo, rtol=1e-8, atol=1e-10 * np.abs(bo).max())
+
+
 def test_optimize_trajectory(scene2k):
     g, o = _pair(scene2k)
     ng, eg = g.optimize(6)

@@ -101,3 +101,32 @@ def test_marginalize_points_properties(scene_marg):
     # the window state once the points are relinearized)
     HM2, bM2 = o.marginalize_points(pts)
     np.testing.assert_allclose(HM2, 2 * HM, rtol=1e-6, atol=1e-9 * scale)
+
+
+def test_marginalize_frame_schur_identity(scene_marg):
+    """marginalizeFrame restatement against a direct float64 Schur complement of the prior-augmented HM: the
+    reference's 1/sqrt(|diag| + 10) scaling is a similarity transform, so both agree to rounding.  For a
+    frame with id != 0 the prior is the affine one only (FrameOptimizationData::getPrior, Include/Frame.h:230-258:
+    a -> affineOptModeA, b -> affineOptModeB), and delta_prior = state = 0 here."""
+    from oracle_ffi import OracleBA, default_params
+    P = default_params()
+    o = OracleBA(scene_marg)
+    o.linearize_all(reset=True)
+    o.apply_res()
+    HM, bM = o.marginalize_points(np.nonzero(scene_marg.pt_host == 1)[0])
+    dim = HM.shape[0]
+    for f in (2, 7):
+        Hn, bn = o.marginalize_frame(f)
+        idx = 4 + 8 * f + np.arange(8)
+        keep = np.setdiff1d(np.arange(dim), idx)
+        H = HM.copy()
+        H[idx[6], idx[6]] += P.affineOptModeA
+        H[idx[7], idx[7]] += P.affineOptModeB
+        Hbb = H[np.ix_(idx, idx)]
+        Hkb = H[np.ix_(keep, idx)]
+        ref = H[np.ix_(keep, keep)] - Hkb @ np.linalg.solve(Hbb, H[np.ix_(idx, keep)])
+        ref = 0.5 * (ref + ref.T)
+        rb = bM[keep] - Hkb @ np.linalg.solve(Hbb, bM[idx])
+        scale = np.abs(ref).max()
+        np.testing.assert_allclose(Hn, ref, rtol=1e-6, atol=1e-7 * scale)  # cancellation-limited entries
+        np.testing.assert_allclose(bn, rb, rtol=1e-6, atol=1e-9 * np.abs(rb).max())
