@@ -1,0 +1,333 @@
+// hs_act_kernels.hip — point activation (System::activatePointsMT, Src/Mapping.cpp:330-480) on CDNA4.
+//
+// hs_k_act_seed      makeDistanceMap (Src/CoarseTracker.cpp:726-756): one thread per active point, level-1
+//                    projection into the newest keyframe, seed byte set to 0 with a word CAS (duplicates dropped).
+// hs_k_act_cand      the per-point part of the selection loop (Mapping.cpp:378-426): delete / skip / the
+//                    projected cell, the sub-pixel fraction and the threshold of every entry of the loop order.
+// hs_k_act_select    one workgroup: growDistBFS of the seeds, then the greedy loop — the first entry (in loop
+//                    order) whose distance passes is taken, addIntoDistFinal grows the map from it, the rest of
+//                    the chunk is re-tested.  BFS steps are frontier-parallel; a cell joins the next frontier
+//                    only through the CAS that lowered it, so the map after each step is the reference's
+//                    (its per-step result does not depend on the order the frontier is walked in).
+//                    The map lives in LDS as bytes (0..39, 255 = the reference's 1000) when it fits.
+// hs_k_act_optimize  optimizeImmaturePoint (Src/FullSystemOptPoint.cpp:24-175) with
+//                    ImmaturePoint::linearizeResidual (Src/ImmaturePoint.cpp:389-451): one wave per point,
+//                    lane = residual (target frame) x pattern pixel; energy, Hdd and bd are summed in the
+//                    reference's sequential order from readlane, including the partial sums a mid-pattern OOB
+//                    leaves behind.
+#include <hip/hip_runtime.h>
+
+#include "hs_trace_kernels.h"
+
+#pragma clang fp contract(off)
+#include "hs_interp.h"
+
+namespace {
+
+constexpr int kPat[8][2] = {{0, -2}, {-1, -1}, {1, -1}, {-2, 0}, {0, 0}, {2, 0}, {-1, 1}, {0, 2}};
+constexpr uint8_t kIpsGood = 0, kIpsOob = 1, kIpsOutlier = 2, kIpsSkipped = 3, kIpsBadCondition = 4;
+constexpr int kResIn = 0, kResOob = 1, kResOut = 2;
+
+// Eigen `KRKi * Vec3f(x, y, 1) + Kt * s`
+__device__ __forceinline__ void proj3(const float* K, const float* t, float x, float y, float s, float p[3]) {
+#pragma unroll
+  for (int i = 0; i < 3; i++) p[i] = (K[3 * i] * x + K[3 * i + 1] * y + K[3 * i + 2] * 1.0f) + t[i] * s;
+}
+
+// lower the distance byte of cell q to k when it is larger; true when this call lowered it
+__device__ __forceinline__ bool lower_cell(uint8_t* map, int q, uint32_t k) {
+  uint32_t* w = reinterpret_cast<uint32_t*>(map + (q & ~3));
+  const int sh = (q & 3) * 8;
+  uint32_t old = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  while (((old >> sh) & 0xffu) > k) {
+    const uint32_t nw = (old & ~(0xffu << sh)) | (k << sh);
+    const uint32_t prev = atomicCAS(w, old, nw);
+    if (prev == old) return true;
+    old = prev;
+  }
+  return false;
+}
+
+__device__ __forceinline__ float decode(uint8_t b) { return b == 255 ? 1000.f : (float)b; }
+
+}  // namespace
+
+__global__ void __launch_bounds__(256) hs_k_act_seed(HsActSeedArgs a) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n) return;
+  const int f = a.frame[i];
+  if (f == a.newest) return;
+  const hs_act_frame& fr = a.frames[f];
+  float ptp[3];
+  proj3(fr.KRKi, fr.Kt, a.u[i], a.v[i], a.idepth[i], ptp);
+  const int u = ptp[0] / ptp[2] + 0.5f;
+  const int v = ptp[1] / ptp[2] + 0.5f;
+  if (!(u > 0 && v > 0 && u < a.w1 && v < a.h1)) return;
+  const int q = u + a.w1 * v;
+  if (lower_cell(a.dist, q, 0)) a.list[atomicAdd(a.count, 1)] = q;
+}
+
+__global__ void __launch_bounds__(256) hs_k_act_cand(HsActCandArgs a) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= a.m) return;
+  const int i = a.order ? a.order[j] : j;
+  const int f = a.frame_of_slot[a.host[i]];
+  uint8_t c = HS_CAND_SKIP;
+  if (f >= 0 && f != a.newest) {
+    const float idmax = a.idepth_max[i], idmin = a.idepth_min[i];
+    const uint8_t st = a.status[i];
+    if (!isfinite(idmax) || st == kIpsOutlier) {
+      c = HS_CAND_DELETE;
+    } else {
+      const bool canActivate =
+          (st == kIpsGood || st == kIpsSkipped || st == kIpsBadCondition || st == kIpsOob) && a.interval[i] < 8 &&
+          a.quality[i] > a.minTraceQuality && (idmax + idmin) > 0;
+      if (!canActivate) {
+        c = (a.frames[f].flagged_for_marg || st == kIpsOob) ? HS_CAND_DELETE : HS_CAND_SKIP;
+      } else {
+        float ptp[3];
+        proj3(a.frames[f].KRKi, a.frames[f].Kt, a.u[i], a.v[i], 0.5f * (idmax + idmin), ptp);
+        const int u = ptp[0] / ptp[2] + 0.5f;
+        const int v = ptp[1] / ptp[2] + 0.5f;
+        if (u > 0 && v > 0 && u < a.w1 && v < a.h1) {
+          c = HS_CAND_PENDING;
+          a.cell[j] = u + a.w1 * v;
+          a.frac[j] = ptp[0] - floorf((float)(ptp[0]));
+          a.thr[j] = a.currentMinActDist * a.my_type[i];
+        } else {
+          c = HS_CAND_DELETE;
+        }
+      }
+    }
+  }
+  a.cand[j] = c;
+  a.action[i] = (c == HS_CAND_DELETE) ? HS_ACT_DELETED : HS_ACT_KEEP;
+}
+
+// growDistBFS from the n cells in *in (Src/CoarseTracker.cpp:759-857), frontier-parallel over the workgroup.
+// s_n[0] holds the frontier size on entry; lists swap every step.
+__device__ static void bfs_grow(uint8_t* map, int w1, int h1, int*& in, int*& out, int* s_n) {
+  for (int k = 1; k < HS_ACT_BFS_STEPS; k++) {
+    const int n = s_n[0];
+    if (n == 0) break;  // the reference keeps looping over empty lists: nothing changes
+    if (threadIdx.x == 0) s_n[1] = 0;
+    __syncthreads();
+    const bool diag = (k & 1) != 0;
+    for (int e = threadIdx.x; e < n; e += blockDim.x) {
+      const int idx = in[e];
+      const int x = idx % w1, y = idx / w1;
+      if (x == 0 || y == 0 || x == w1 - 1 || y == h1 - 1) continue;
+      const int nb[8] = {idx + 1, idx - 1, idx + w1, idx - w1, idx + 1 + w1, idx - 1 + w1, idx - 1 - w1, idx + 1 - w1};
+      const int cnt = diag ? 8 : 4;
+      for (int d = 0; d < cnt; d++)
+        if (lower_cell(map, nb[d], (uint32_t)k)) out[atomicAdd(&s_n[1], 1)] = nb[d];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) s_n[0] = s_n[1];
+    int* t = in;
+    in = out;
+    out = t;
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(1024) hs_k_act_select(HsActSelectArgs a) {
+  extern __shared__ uint32_t s_map32[];
+  __shared__ int s_n[2];
+  __shared__ int s_first;
+  __shared__ int s_nt;
+  const int wh1 = a.w1 * a.h1;
+  const int words = (wh1 + 3) / 4;
+  uint8_t* map = reinterpret_cast<uint8_t*>(a.dist);
+  if (a.lds_map) {
+    const uint32_t* g = reinterpret_cast<const uint32_t*>(a.dist);
+    for (int w = threadIdx.x; w < words; w += blockDim.x) s_map32[w] = g[w];
+    map = reinterpret_cast<uint8_t*>(s_map32);
+  }
+  if (threadIdx.x == 0) {
+    s_n[0] = *a.seed_count;
+    s_nt = 0;
+  }
+  __syncthreads();
+  int* in = a.list_a;
+  int* out = a.list_b;
+  bfs_grow(map, a.w1, a.h1, in, out, s_n);  // makeDistanceMap's growDistBFS(numItems)
+
+  for (int base = 0; base < a.m; base += blockDim.x) {
+    const int j = base + threadIdx.x;
+    bool pend = j < a.m && a.cand[j] == HS_CAND_PENDING;
+    const int cell = pend ? a.cell[j] : 0;
+    const float frac = pend ? a.frac[j] : 0.f;
+    const float thr = pend ? a.thr[j] : 0.f;
+    for (;;) {
+      if (threadIdx.x == 0) s_first = 0x7fffffff;
+      __syncthreads();
+      // dist = fwdWarpedIDDistFinal[u + w1 * v] + (ptp[0] - floorf(ptp[0])) >= currentMinActDist * my_type
+      const bool acc = pend && (decode(map[cell]) + frac >= thr);
+      if (acc) atomicMin(&s_first, (int)threadIdx.x);
+      __syncthreads();
+      const int first = s_first;
+      if (first == 0x7fffffff) break;  // every remaining entry of the chunk fails: they stay immature
+      if ((int)threadIdx.x <= first) pend = false;
+      if ((int)threadIdx.x == first) {
+        a.toopt[s_nt] = a.order ? a.order[j] : j;
+        s_nt = s_nt + 1;
+        lower_cell(map, cell, 0);  // addIntoDistFinal: the cell becomes 0 even when it already was
+        in[0] = cell;
+        s_n[0] = 1;
+      }
+      __syncthreads();
+      bfs_grow(map, a.w1, a.h1, in, out, s_n);
+    }
+    __syncthreads();
+  }
+  if (a.lds_map) {
+    uint32_t* g = reinterpret_cast<uint32_t*>(a.dist);
+    for (int w = threadIdx.x; w < words; w += blockDim.x) g[w] = s_map32[w];
+  }
+  if (threadIdx.x == 0) *a.n_toopt = s_nt;
+}
+
+__global__ void __launch_bounds__(256) hs_k_act_optimize(HsActOptArgs a) {
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (wave >= a.n) return;  // wave-uniform
+  const int p = a.toopt[wave];
+  const int hostF = a.frame_of_slot[a.host[p]];
+  const int nres = a.nF - 1;
+  const int r = lane >> 3, idx = lane & 7;
+  const bool live = r < nres;
+  const int tf = r < hostF ? r : r + 1;  // the r-th window frame other than the host
+  const int tfc = live ? tf : 0;
+  const hs_act_pair& pc = a.pairs[hostF * a.nF + tfc];
+  const float4* img = a.img[a.frames[tfc].slot];
+  const float pu = a.u[p], pv = a.v[p];
+  const float color = a.color[8 * p + idx], wgt = a.weights[8 * p + idx];
+  const float energyTH = a.energyTH[p];
+  float R[9], t[3], aff0, aff1;
+#pragma unroll
+  for (int k = 0; k < 9; k++) R[k] = pc.RTll[k];
+#pragma unroll
+  for (int k = 0; k < 3; k++) t[k] = pc.tTll[k];
+  aff0 = pc.aff[0];
+  aff1 = pc.aff[1];
+  const float KliP0 = (pu + kPat[idx][0] - a.cxl) * a.fxli;
+  const float KliP1 = (pv + kPat[idx][1] - a.cyl) * a.fyli;
+
+  // ImmaturePointTemporaryResidual of this lane's residual (replicated over its 8 lanes)
+  int st_state = kResIn, st_new = kResOut;
+  float st_energy = 0.f, st_newE = 0.f;
+
+  // one pass of linearizeResidual over all residuals at idepth; returns the summed energy (float +=)
+  auto evaluate = [&](float idepth, float slack, float& Hdd, float& bd) -> float {
+    float ptp[3];
+#pragma unroll
+    for (int i = 0; i < 3; i++) ptp[i] = (R[3 * i] * KliP0 + R[3 * i + 1] * KliP1 + R[3 * i + 2] * 1.0f) + t[i] * idepth;
+    const float drescale = 1.0f / ptp[2];
+    const float u = ptp[0] * drescale, v = ptp[1] * drescale;
+    const float Ku = u * a.fxl + a.cxl, Kv = v * a.fyl + a.cyl;
+    bool ok = (drescale > 0) & (Ku > 1.1f) & (Kv > 1.1f) & (Ku < (float)(a.W - 3)) & (Kv < (float)(a.H - 3));
+    const float Kuc = ok ? Ku : 2.f, Kvc = ok ? Kv : 2.f;
+    const float3 hit = hs_img::interp33(img, Kuc, Kvc, a.W, a.H);
+    ok = ok & isfinite(hit.x);
+    const float residual = hit.x - (aff0 * color + aff1);
+    float hw = fabsf(residual) < a.huberTH ? 1 : a.huberTH / fabsf(residual);
+    const float eterm = wgt * wgt * hw * residual * residual * (2 - hw);
+    const float dxInterp = hit.y * a.fxl;
+    const float dyInterp = hit.z * a.fyl;
+    const float d_idepth = (dxInterp * drescale * (t[0] - t[2] * u) + dyInterp * drescale * (t[1] - t[2] * v)) * 1.0f;
+    hw *= wgt * wgt;
+    const float hterm = (hw * d_idepth) * d_idepth;
+    const float bterm = (hw * residual) * d_idepth;
+    const unsigned long long bad = __ballot(live && !ok);
+    float E = 0.f;
+    for (int rr = 0; rr < nres; rr++) {
+      const int l0 = rr * 8;
+      const int sst = __builtin_amdgcn_readlane(st_state, l0);
+      const float sE = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(st_energy), l0));
+      float contrib;
+      int ns;
+      float nE = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(st_newE), l0));
+      if (sst == kResOob) {
+        ns = kResOob;
+        contrib = sE;
+      } else {
+        const unsigned badr = (unsigned)(bad >> l0) & 0xffu;
+        const int nvalid = badr ? __builtin_ctz(badr) : 8;
+        for (int q = 0; q < nvalid; q++) {
+          Hdd += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hterm), l0 + q));
+          bd += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bterm), l0 + q));
+        }
+        if (badr) {
+          ns = kResOob;
+          contrib = sE;
+        } else {
+          float el = 0.f;
+          for (int q = 0; q < 8; q++) el += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(eterm), l0 + q));
+          const float cap = energyTH * slack;
+          if (el > cap) {
+            el = cap;
+            ns = kResOut;
+          } else {
+            ns = kResIn;
+          }
+          nE = el;
+          contrib = el;
+        }
+      }
+      if (r == rr) {
+        st_new = ns;
+        st_newE = nE;
+      }
+      E = (float)((double)E + (double)contrib);
+    }
+    return E;
+  };
+  auto take = [&]() {
+    st_state = st_new;
+    st_energy = st_newE;
+  };
+
+  float lastHdd = 0.f, lastbd = 0.f;
+  float currentIdepth = (a.idepth_max[p] + a.idepth_min[p]) * 0.5f;
+  float lastEnergy = evaluate(currentIdepth, 1000.f, lastHdd, lastbd);
+  take();
+  bool good = isfinite(lastEnergy) && !(lastHdd < a.minIdepthH_act);
+  if (good) {
+    float lambda = 0.1f;
+    for (int it = 0; it < a.GNIts; it++) {
+      float H = lastHdd;
+      H *= 1 + lambda;
+      const float step = (float)((1.0 / (double)H) * (double)lastbd);
+      const float newIdepth = currentIdepth - step;
+      float newHdd = 0.f, newbd = 0.f;
+      const float newEnergy = evaluate(newIdepth, 1.f, newHdd, newbd);
+      if (!isfinite(lastEnergy) || newHdd < a.minIdepthH_act) {
+        good = false;
+        break;
+      }
+      if (newEnergy < lastEnergy) {
+        currentIdepth = newIdepth;
+        lastHdd = newHdd;
+        lastbd = newbd;
+        lastEnergy = newEnergy;
+        take();
+        lambda = (float)((double)lambda * 0.5);
+      } else {
+        lambda = (float)((double)lambda * 5.0);
+      }
+      if ((double)fabsf(step) < 0.0001 * (double)currentIdepth) break;
+    }
+  }
+  good = good && isfinite(currentIdepth);
+  const unsigned long long inb = __ballot(live && idx == 0 && st_state == kResIn);
+  unsigned mask = 0;
+  for (int rr = 0; rr < nres; rr++)
+    if ((inb >> (rr * 8)) & 1ull) mask |= 1u << (rr < hostF ? rr : rr + 1);
+  good = good && mask != 0 && isfinite(energyTH);
+  if (lane == 0) {
+    a.action[p] = good ? HS_ACT_ACTIVATED : HS_ACT_DELETED;
+    a.idepth_out[p] = currentIdepth;
+    a.res_in[p] = good ? (uint8_t)mask : 0;
+  }
+}

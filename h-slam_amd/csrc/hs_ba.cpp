@@ -488,6 +488,10 @@ int hs_params_default(hs_params* p) {
   p->trace_GNIterations = 3;
   p->idepthFixPriorMargFac = 600 * 600;
   p->margWeightFac = 0.5f * 0.5f;
+  p->desiredPointDensity = 2000;
+  p->minTraceQuality = 3;
+  p->minIdepthH_act = 100;
+  p->GNItsOnPointActivation = 3;
   return HS_OK;
 }
 

@@ -13,6 +13,9 @@
 #include "hs_trace_kernels.h"
 #include "hs_pyr_kernels.h"
 
+#define HS_MAXF_ACT 8                        // activation window (nF <= 8 keyframes)
+#define HS_ACT_LDS_MAP_MAX (156 * 1024)     // level-1 distance map in LDS up to this size
+
 namespace hs {
 extern thread_local std::string g_err;
 }
@@ -59,6 +62,20 @@ struct hs_tracer {
   long long last_steps = 0;
   bool stats_pending = false;
   int max_host = -1;  // largest host slot of the stored points
+  float* d_type = nullptr;  // ImmaturePoint::my_type
+  // point activation scratch (allocated by the first hs_tracer_activate)
+  bool act_ready = false;
+  int w1 = 0, h1 = 0, act_cap = 0;
+  uint8_t* d_dist = nullptr;
+  int *d_list_a = nullptr, *d_list_b = nullptr, *d_act_cnt = nullptr;
+  hs_act_frame* d_act_frames = nullptr;
+  hs_act_pair* d_act_pairs = nullptr;
+  int* d_frame_of_slot = nullptr;
+  int *d_order = nullptr, *d_cell = nullptr, *d_toopt = nullptr;
+  uint8_t *d_cand = nullptr, *d_action = nullptr, *d_res_in = nullptr;
+  float *d_frac = nullptr, *d_thr = nullptr, *d_act_idepth = nullptr;
+  int* d_ap_frame = nullptr;
+  float *d_ap_u = nullptr, *d_ap_v = nullptr, *d_ap_id = nullptr;
 };
 
 static int upload_img(hs_tracer* t, float4* dst, const float* src) {
@@ -149,6 +166,7 @@ int hs_tracer_create(hs_tracer** out, const hs_params* params, int device_id, in
   TR_HIP(hipMalloc((void**)&t->d_interval, sizeof(float) * c));
   TR_HIP(hipMalloc((void**)&t->d_status, c));
   TR_HIP(hipMalloc((void**)&t->d_steps, sizeof(int) * c));
+  TR_HIP(hipMalloc((void**)&t->d_type, sizeof(float) * c));
   TR_HIP(hipMalloc((void**)&t->d_counts, sizeof(int) * 8));
   TR_HIP(hipHostMalloc((void**)&t->h_counts, sizeof(int) * 8));
   *out = t;
@@ -162,7 +180,10 @@ void hs_tracer_destroy(hs_tracer* t) {
   for (auto* p : t->d_host_img) (void)hipFree(p);
   void* bufs[] = {t->d_host_tab, t->d_new, t->d_hosts, t->d_host, t->d_u, t->d_v, t->d_color, t->d_weights,
                   t->d_gradH, t->d_energyTH, t->d_quality, t->d_idmin, t->d_idmax, t->d_uv, t->d_interval,
-                  t->d_status, t->d_steps, t->d_counts, t->d_raw};
+                  t->d_status, t->d_steps, t->d_counts, t->d_raw, t->d_type, t->d_dist, t->d_list_a,
+                  t->d_list_b, t->d_act_cnt, t->d_act_frames, t->d_act_pairs, t->d_frame_of_slot, t->d_order,
+                  t->d_cell, t->d_toopt, t->d_cand, t->d_action, t->d_res_in, t->d_frac, t->d_thr,
+                  t->d_act_idepth, t->d_ap_frame, t->d_ap_u, t->d_ap_v, t->d_ap_id};
   for (void* b : bufs) (void)hipFree(b);
   (void)hipHostFree(t->h_counts);
   if (t->e0) (void)hipEventDestroy(t->e0);
@@ -205,6 +226,8 @@ int hs_tracer_add_points(hs_tracer* t, int n, const int* host, const float* u, c
   TR_HIP(hipMemcpyAsync(t->d_host + f, host, sizeof(int) * n, hipMemcpyHostToDevice, t->stream));
   TR_HIP(hipMemcpyAsync(t->d_u + f, u, sizeof(float) * n, hipMemcpyHostToDevice, t->stream));
   TR_HIP(hipMemcpyAsync(t->d_v + f, v, sizeof(float) * n, hipMemcpyHostToDevice, t->stream));
+  const std::vector<float> ones(n, 1.f);
+  TR_HIP(hipMemcpyAsync(t->d_type + f, ones.data(), sizeof(float) * n, hipMemcpyHostToDevice, t->stream));
   for (int i = 0; i < n; i++) t->max_host = std::max(t->max_host, host[i]);
   TR_TRY(launch_ctor(t, f, n));
   TR_HIP(hipStreamSynchronize(t->stream));  // host arrays may go away after return
@@ -213,7 +236,7 @@ int hs_tracer_add_points(hs_tracer* t, int n, const int* host, const float* u, c
 }
 
 int hs_tracer_set_state(hs_tracer* t, const float* idepth_min, const float* idepth_max, const float* quality,
-                        const uint8_t* status) {
+                        const uint8_t* status, const float* interval) {
   if (!t) return cfail(HS_ERR_INVALID, "null tracer");
   if (status)
     for (int i = 0; i < t->n; i++)
@@ -224,6 +247,7 @@ int hs_tracer_set_state(hs_tracer* t, const float* idepth_min, const float* idep
   if (idepth_max) TR_HIP(hipMemcpyAsync(t->d_idmax, idepth_max, 4 * n, hipMemcpyHostToDevice, t->stream));
   if (quality) TR_HIP(hipMemcpyAsync(t->d_quality, quality, 4 * n, hipMemcpyHostToDevice, t->stream));
   if (status) TR_HIP(hipMemcpyAsync(t->d_status, status, n, hipMemcpyHostToDevice, t->stream));
+  if (interval) TR_HIP(hipMemcpyAsync(t->d_interval, interval, 4 * n, hipMemcpyHostToDevice, t->stream));
   TR_HIP(hipStreamSynchronize(t->stream));
   return HS_OK;
 }
@@ -339,6 +363,300 @@ int hs_tracer_reinit(hs_tracer* t) {
   if (t->n == 0) return HS_OK;
   TR_HIP(hipSetDevice(t->device));
   return launch_ctor(t, 0, t->n);
+}
+
+int hs_tracer_set_types(hs_tracer* t, const float* my_type) {
+  if (!t || (t->n > 0 && !my_type)) return cfail(HS_ERR_INVALID, "null argument");
+  TR_HIP(hipSetDevice(t->device));
+  TR_HIP(hipMemcpyAsync(t->d_type, my_type, sizeof(float) * t->n, hipMemcpyHostToDevice, t->stream));
+  TR_HIP(hipStreamSynchronize(t->stream));
+  return HS_OK;
+}
+
+static int act_alloc(hs_tracer* t) {
+  if (t->act_ready) return HS_OK;
+  t->w1 = t->W >> 1;
+  t->h1 = t->H >> 1;
+  const size_t wh1 = (size_t)t->w1 * t->h1, c = t->cap;
+  TR_HIP(hipMalloc((void**)&t->d_dist, (wh1 + 3) & ~(size_t)3));
+  TR_HIP(hipMalloc((void**)&t->d_list_a, sizeof(int) * wh1));
+  TR_HIP(hipMalloc((void**)&t->d_list_b, sizeof(int) * wh1));
+  TR_HIP(hipMalloc((void**)&t->d_act_cnt, sizeof(int) * 2));
+  TR_HIP(hipMalloc((void**)&t->d_act_frames, sizeof(hs_act_frame) * HS_MAXF_ACT));
+  TR_HIP(hipMalloc((void**)&t->d_act_pairs, sizeof(hs_act_pair) * HS_MAXF_ACT * HS_MAXF_ACT));
+  TR_HIP(hipMalloc((void**)&t->d_frame_of_slot, sizeof(int) * HS_TRC_MAXHOST));
+  TR_HIP(hipMalloc((void**)&t->d_order, sizeof(int) * c));
+  TR_HIP(hipMalloc((void**)&t->d_cell, sizeof(int) * c));
+  TR_HIP(hipMalloc((void**)&t->d_toopt, sizeof(int) * c));
+  TR_HIP(hipMalloc((void**)&t->d_cand, c));
+  TR_HIP(hipMalloc((void**)&t->d_action, c));
+  TR_HIP(hipMalloc((void**)&t->d_res_in, c));
+  TR_HIP(hipMalloc((void**)&t->d_frac, sizeof(float) * c));
+  TR_HIP(hipMalloc((void**)&t->d_thr, sizeof(float) * c));
+  TR_HIP(hipMalloc((void**)&t->d_act_idepth, sizeof(float) * c));
+  t->act_ready = true;
+  return HS_OK;
+}
+
+static int act_points_alloc(hs_tracer* t, int n) {
+  if (n <= t->act_cap) return HS_OK;
+  void* old[] = {t->d_ap_frame, t->d_ap_u, t->d_ap_v, t->d_ap_id};
+  for (void* b : old) TR_HIP(hipFree(b));
+  t->d_ap_frame = nullptr;
+  t->d_ap_u = t->d_ap_v = t->d_ap_id = nullptr;
+  t->act_cap = 0;
+  TR_HIP(hipMalloc((void**)&t->d_ap_frame, sizeof(int) * n));
+  TR_HIP(hipMalloc((void**)&t->d_ap_u, sizeof(float) * n));
+  TR_HIP(hipMalloc((void**)&t->d_ap_v, sizeof(float) * n));
+  TR_HIP(hipMalloc((void**)&t->d_ap_id, sizeof(float) * n));
+  t->act_cap = n;
+  return HS_OK;
+}
+
+// System::activatePointsMT :332-352 (float currentMinActDist, double constants as in the reference)
+static void update_min_act_dist(const hs_params& P, int nPoints, float& d) {
+  if (nPoints < P.desiredPointDensity * 0.66) d -= 0.8;
+  if (nPoints < P.desiredPointDensity * 0.8) d -= 0.5;
+  else if (nPoints < P.desiredPointDensity * 0.9) d -= 0.2;
+  else if (nPoints < P.desiredPointDensity) d -= 0.1;
+  if (nPoints > P.desiredPointDensity * 1.5) d += 0.8;
+  if (nPoints > P.desiredPointDensity * 1.3) d += 0.5;
+  if (nPoints > P.desiredPointDensity * 1.15) d += 0.2;
+  if (nPoints > P.desiredPointDensity) d += 0.1;
+  if (d < 0) d = 0;
+  if (d > 4) d = 4;
+}
+
+int hs_tracer_activate(hs_tracer* t, const float K4[4], int nF, const hs_act_frame* frames, const hs_act_pair* pairs,
+                       int n_active, const int* act_frame, const float* act_u, const float* act_v,
+                       const float* act_idepth, int ef_nPoints, float* currentMinActDist, int n_order,
+                       const int* order, uint8_t* action, float* idepth, uint8_t* res_in, int* activated,
+                       int* n_activated) {
+  if (!t || !K4 || !frames || !pairs || !currentMinActDist) return cfail(HS_ERR_INVALID, "null argument");
+  if (nF < 2 || nF > HS_MAXF_ACT) return cfail(HS_ERR_INVALID, "window size out of range (2..8 keyframes)");
+  if (n_active < 0 || (n_active > 0 && (!act_frame || !act_u || !act_v || !act_idepth)))
+    return cfail(HS_ERR_INVALID, "bad active point arrays");
+  if (!(K4[0] > 0) || !(K4[1] > 0)) return cfail(HS_ERR_INVALID, "bad intrinsics");
+  std::vector<int> fos(HS_TRC_MAXHOST, -1);
+  for (int f = 0; f < nF; f++) {
+    const int sl = frames[f].slot;
+    if (sl < 0 || sl >= HS_TRC_MAXHOST || !t->d_host_img[sl]) return cfail(HS_ERR_INVALID, "window frame without an image slot");
+    if (fos[sl] >= 0) return cfail(HS_ERR_INVALID, "two window frames on one slot");
+    fos[sl] = f;
+  }
+  for (int i = 0; i < n_active; i++)
+    if (act_frame[i] < 0 || act_frame[i] >= nF) return cfail(HS_ERR_INVALID, "active point on no window frame");
+  const int m = order ? n_order : t->n;
+  if (order) {
+    if (n_order < 0 || n_order > t->n) return cfail(HS_ERR_INVALID, "bad n_order");
+    std::vector<char> seen(t->n, 0);
+    for (int j = 0; j < n_order; j++) {
+      if (order[j] < 0 || order[j] >= t->n || seen[order[j]]) return cfail(HS_ERR_INVALID, "order is not a subset permutation");
+      seen[order[j]] = 1;
+    }
+  }
+  TR_HIP(hipSetDevice(t->device));
+  TR_TRY(sync_stats(t));
+  TR_TRY(act_alloc(t));
+  TR_TRY(act_points_alloc(t, std::max(1, n_active)));
+  update_min_act_dist(t->P, ef_nPoints, *currentMinActDist);
+  hipStream_t s = t->stream;
+  const int wh1 = t->w1 * t->h1;
+  TR_HIP(hipMemcpyAsync(t->d_act_frames, frames, sizeof(hs_act_frame) * nF, hipMemcpyHostToDevice, s));
+  TR_HIP(hipMemcpyAsync(t->d_act_pairs, pairs, sizeof(hs_act_pair) * nF * nF, hipMemcpyHostToDevice, s));
+  TR_HIP(hipMemcpyAsync(t->d_frame_of_slot, fos.data(), sizeof(int) * HS_TRC_MAXHOST, hipMemcpyHostToDevice, s));
+  if (order && m > 0) TR_HIP(hipMemcpyAsync(t->d_order, order, sizeof(int) * m, hipMemcpyHostToDevice, s));
+  if (n_active > 0) {
+    TR_HIP(hipMemcpyAsync(t->d_ap_frame, act_frame, sizeof(int) * n_active, hipMemcpyHostToDevice, s));
+    TR_HIP(hipMemcpyAsync(t->d_ap_u, act_u, sizeof(float) * n_active, hipMemcpyHostToDevice, s));
+    TR_HIP(hipMemcpyAsync(t->d_ap_v, act_v, sizeof(float) * n_active, hipMemcpyHostToDevice, s));
+    TR_HIP(hipMemcpyAsync(t->d_ap_id, act_idepth, sizeof(float) * n_active, hipMemcpyHostToDevice, s));
+  }
+  TR_HIP(hipMemsetAsync(t->d_dist, 0xff, (wh1 + 3) & ~3, s));
+  TR_HIP(hipMemsetAsync(t->d_act_cnt, 0, sizeof(int) * 2, s));
+  TR_HIP(hipMemsetAsync(t->d_action, HS_ACT_KEEP, std::max(1, t->n), s));
+  TR_HIP(hipMemsetAsync(t->d_res_in, 0, std::max(1, t->n), s));
+
+  HsActSeedArgs sa;
+  sa.n = n_active;
+  sa.newest = nF - 1;
+  sa.w1 = t->w1;
+  sa.h1 = t->h1;
+  sa.frames = t->d_act_frames;
+  sa.frame = t->d_ap_frame;
+  sa.u = t->d_ap_u;
+  sa.v = t->d_ap_v;
+  sa.idepth = t->d_ap_id;
+  sa.dist = t->d_dist;
+  sa.list = t->d_list_a;
+  sa.count = t->d_act_cnt;
+  if (n_active > 0) {
+    hipLaunchKernelGGL(hs_k_act_seed, dim3((n_active + 255) / 256), dim3(256), 0, s, sa);
+    TR_HIP(hipGetLastError());
+  }
+  HsActCandArgs ca;
+  ca.m = m;
+  ca.newest = nF - 1;
+  ca.w1 = t->w1;
+  ca.h1 = t->h1;
+  ca.minTraceQuality = t->P.minTraceQuality;
+  ca.currentMinActDist = *currentMinActDist;
+  ca.order = order ? t->d_order : nullptr;
+  ca.frame_of_slot = t->d_frame_of_slot;
+  ca.frames = t->d_act_frames;
+  ca.host = t->d_host;
+  ca.u = t->d_u;
+  ca.v = t->d_v;
+  ca.idepth_min = t->d_idmin;
+  ca.idepth_max = t->d_idmax;
+  ca.quality = t->d_quality;
+  ca.interval = t->d_interval;
+  ca.my_type = t->d_type;
+  ca.status = t->d_status;
+  ca.cand = t->d_cand;
+  ca.cell = t->d_cell;
+  ca.frac = t->d_frac;
+  ca.thr = t->d_thr;
+  ca.action = t->d_action;
+  if (m > 0) {
+    hipLaunchKernelGGL(hs_k_act_cand, dim3((m + 255) / 256), dim3(256), 0, s, ca);
+    TR_HIP(hipGetLastError());
+  }
+  HsActSelectArgs se;
+  se.m = m;
+  se.w1 = t->w1;
+  se.h1 = t->h1;
+  const size_t map_bytes = (size_t)((wh1 + 3) & ~3);
+  se.lds_map = map_bytes <= HS_ACT_LDS_MAP_MAX ? 1 : 0;
+  se.order = order ? t->d_order : nullptr;
+  se.cand = t->d_cand;
+  se.cell = t->d_cell;
+  se.frac = t->d_frac;
+  se.thr = t->d_thr;
+  se.dist = t->d_dist;
+  se.list_a = t->d_list_a;
+  se.list_b = t->d_list_b;
+  se.seed_count = t->d_act_cnt;
+  se.toopt = t->d_toopt;
+  se.n_toopt = t->d_act_cnt + 1;
+  const size_t lds = se.lds_map ? map_bytes : 0;
+  if (lds > 65536)
+    TR_HIP(hipFuncSetAttribute((const void*)hs_k_act_select, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(hs_k_act_select, dim3(1), dim3(1024), lds, s, se);
+  TR_HIP(hipGetLastError());
+  int cnt[2] = {0, 0};
+  TR_HIP(hipMemcpyAsync(cnt, t->d_act_cnt, sizeof(cnt), hipMemcpyDeviceToHost, s));
+  TR_HIP(hipStreamSynchronize(s));
+  const int n_toopt = cnt[1];
+  if (n_toopt > 0) {
+    HsActOptArgs oa;
+    oa.n = n_toopt;
+    oa.nF = nF;
+    oa.W = t->W;
+    oa.H = t->H;
+    oa.fxl = K4[0];
+    oa.fyl = K4[1];
+    oa.cxl = K4[2];
+    oa.cyl = K4[3];
+    oa.fxli = 1.0f / K4[0];
+    oa.fyli = 1.0f / K4[1];
+    oa.huberTH = t->P.huberTH;
+    oa.minIdepthH_act = t->P.minIdepthH_act;
+    oa.GNIts = t->P.GNItsOnPointActivation;
+    oa.toopt = t->d_toopt;
+    oa.frame_of_slot = t->d_frame_of_slot;
+    oa.frames = t->d_act_frames;
+    oa.pairs = t->d_act_pairs;
+    oa.img = t->d_host_tab;
+    oa.host = t->d_host;
+    oa.u = t->d_u;
+    oa.v = t->d_v;
+    oa.idepth_min = t->d_idmin;
+    oa.idepth_max = t->d_idmax;
+    oa.color = t->d_color;
+    oa.weights = t->d_weights;
+    oa.energyTH = t->d_energyTH;
+    oa.action = t->d_action;
+    oa.idepth_out = t->d_act_idepth;
+    oa.res_in = t->d_res_in;
+    hipLaunchKernelGGL(hs_k_act_optimize, dim3((n_toopt + 3) / 4), dim3(256), 0, s, oa);
+    TR_HIP(hipGetLastError());
+  }
+  const size_t n = t->n;
+  std::vector<uint8_t> act(std::max<size_t>(1, n));
+  std::vector<int> toopt(std::max(1, n_toopt));
+  TR_HIP(hipMemcpyAsync(act.data(), t->d_action, n, hipMemcpyDeviceToHost, s));
+  if (n_toopt > 0) TR_HIP(hipMemcpyAsync(toopt.data(), t->d_toopt, sizeof(int) * n_toopt, hipMemcpyDeviceToHost, s));
+  if (idepth && n) TR_HIP(hipMemcpyAsync(idepth, t->d_act_idepth, sizeof(float) * n, hipMemcpyDeviceToHost, s));
+  if (res_in && n) TR_HIP(hipMemcpyAsync(res_in, t->d_res_in, n, hipMemcpyDeviceToHost, s));
+  TR_HIP(hipStreamSynchronize(s));
+  if (action && n) memcpy(action, act.data(), n);
+  int na = 0;
+  for (int k = 0; k < n_toopt; k++)
+    if (act[toopt[k]] == HS_ACT_ACTIVATED) {
+      if (activated) activated[na] = toopt[k];
+      na++;
+    }
+  if (idepth)  // the idepth output is defined for activated points only
+    for (size_t i = 0; i < n; i++)
+      if (act[i] != HS_ACT_ACTIVATED) idepth[i] = 0.f;
+  if (n_activated) *n_activated = na;
+  return HS_OK;
+}
+
+int hs_tracer_get_distance_map(hs_tracer* t, float* dist) {
+  if (!t || !dist) return cfail(HS_ERR_INVALID, "null argument");
+  if (!t->act_ready) return cfail(HS_ERR_STATE, "no activation has run");
+  TR_HIP(hipSetDevice(t->device));
+  const size_t wh1 = (size_t)t->w1 * t->h1;
+  std::vector<uint8_t> b(wh1);
+  TR_HIP(hipStreamSynchronize(t->stream));
+  TR_HIP(hipMemcpy(b.data(), t->d_dist, wh1, hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < wh1; i++) dist[i] = b[i] == 255 ? 1000.f : (float)b[i];
+  return HS_OK;
+}
+
+// stable compaction of every per-point array (a host round trip: once per keyframe)
+extern "C++" template <typename T>
+static int compact_array(hs_tracer* t, T* d, int per, const std::vector<int>& keep_idx) {
+  const size_t n = t->n;
+  std::vector<T> h(n * per), o(keep_idx.size() * per);
+  if (n) TR_HIP(hipMemcpy(h.data(), d, sizeof(T) * n * per, hipMemcpyDeviceToHost));
+  for (size_t k = 0; k < keep_idx.size(); k++)
+    for (int c = 0; c < per; c++) o[k * per + c] = h[(size_t)keep_idx[k] * per + c];
+  if (!o.empty()) TR_HIP(hipMemcpy(d, o.data(), sizeof(T) * o.size(), hipMemcpyHostToDevice));
+  return HS_OK;
+}
+
+int hs_tracer_compact(hs_tracer* t, const uint8_t* keep) {
+  if (!t || (t->n > 0 && !keep)) return cfail(HS_ERR_INVALID, "null argument");
+  TR_HIP(hipSetDevice(t->device));
+  TR_TRY(sync_stats(t));
+  TR_HIP(hipStreamSynchronize(t->stream));
+  std::vector<int> idx;
+  for (int i = 0; i < t->n; i++)
+    if (keep[i]) idx.push_back(i);
+  TR_TRY(compact_array(t, t->d_host, 1, idx));
+  TR_TRY(compact_array(t, t->d_u, 1, idx));
+  TR_TRY(compact_array(t, t->d_v, 1, idx));
+  TR_TRY(compact_array(t, t->d_color, 8, idx));
+  TR_TRY(compact_array(t, t->d_weights, 8, idx));
+  TR_TRY(compact_array(t, t->d_gradH, 4, idx));
+  TR_TRY(compact_array(t, t->d_energyTH, 1, idx));
+  TR_TRY(compact_array(t, t->d_quality, 1, idx));
+  TR_TRY(compact_array(t, t->d_idmin, 1, idx));
+  TR_TRY(compact_array(t, t->d_idmax, 1, idx));
+  TR_TRY(compact_array(t, t->d_uv, 2, idx));
+  TR_TRY(compact_array(t, t->d_interval, 1, idx));
+  TR_TRY(compact_array(t, t->d_status, 1, idx));
+  TR_TRY(compact_array(t, t->d_steps, 1, idx));
+  TR_TRY(compact_array(t, t->d_type, 1, idx));
+  std::vector<int> hosts(idx.size());
+  if (!idx.empty()) TR_HIP(hipMemcpy(hosts.data(), t->d_host, sizeof(int) * idx.size(), hipMemcpyDeviceToHost));
+  t->max_host = -1;
+  for (int h : hosts) t->max_host = std::max(t->max_host, h);
+  t->n = (int)idx.size();
+  return HS_OK;
 }
 
 }  // extern "C"

@@ -52,3 +52,90 @@ struct HsTraceArgs {
 __global__ void hs_k_imm_ctor(HsImmCtorArgs a);
 __global__ void hs_k_trace_on(HsTraceArgs a);
 __global__ void hs_k_trace_count(int n, const uint8_t* status, const int* steps, int* out);
+
+// ---- point activation (System::activatePointsMT), hs_act_kernels.hip ----------------------------------------
+#define HS_ACT_BFS_STEPS 40  // growDistBFS: k = 1 .. 39
+
+// candidate states of the selection loop (per entry of the loop order)
+enum { HS_CAND_SKIP = 0, HS_CAND_DELETE = 1, HS_CAND_PENDING = 2 };
+
+// makeDistanceMap seeds: every active point's level-1 projection into the newest keyframe
+struct HsActSeedArgs {
+  int n, newest, w1, h1;
+  const hs_act_frame* frames;
+  const int* frame;
+  const float* u;
+  const float* v;
+  const float* idepth;
+  uint8_t* dist;   // [w1*h1] distance bytes (255 = 1000, untouched)
+  int* list;       // [w1*h1] seed cells (deduplicated)
+  int* count;
+};
+
+// per loop-order entry: the state-only part of the selection loop (Mapping.cpp:378-426 up to the distance test)
+struct HsActCandArgs {
+  int m, newest, w1, h1;
+  float minTraceQuality, currentMinActDist;
+  const int* order;          // nullable: identity
+  const int* frame_of_slot;  // [HS_TRC_MAXHOST] window frame index of a tracer slot, -1 = none
+  const hs_act_frame* frames;
+  const int* host;
+  const float* u;
+  const float* v;
+  const float* idepth_min;
+  const float* idepth_max;
+  const float* quality;
+  const float* interval;
+  const float* my_type;
+  const uint8_t* status;
+  uint8_t* cand;     // [m] HS_CAND_*
+  int* cell;         // [m] u + w1 * v of a pending entry
+  float* frac;       // [m] ptp[0] - floorf(ptp[0])
+  float* thr;        // [m] currentMinActDist * my_type
+  uint8_t* action;   // [n points] HS_ACT_*
+};
+
+// the sequential part: multi-source BFS, then the greedy distance test + addIntoDistFinal in loop order
+struct HsActSelectArgs {
+  int m, w1, h1, lds_map;
+  const int* order;
+  const uint8_t* cand;
+  const int* cell;
+  const float* frac;
+  const float* thr;
+  uint8_t* dist;             // global map (in: seeded, out: final)
+  int* list_a;               // [w1*h1] frontier lists
+  int* list_b;
+  const int* seed_count;
+  int* toopt;                // [m] points to optimize, in order
+  int* n_toopt;
+};
+
+// optimizeImmaturePoint, one wave per point to optimize
+struct HsActOptArgs {
+  int n, nF, W, H;
+  float fxl, fyl, cxl, cyl, fxli, fyli;
+  float huberTH, minIdepthH_act;
+  int GNIts;
+  const int* toopt;
+  const int* frame_of_slot;
+  const hs_act_frame* frames;
+  const hs_act_pair* pairs;
+  const float4* const* img;  // per tracer slot
+  const int* host;
+  const float* u;
+  const float* v;
+  const float* idepth_min;
+  const float* idepth_max;
+  const float* color;
+  const float* weights;
+  const float* energyTH;
+  uint8_t* action;
+  float* idepth_out;
+  uint8_t* res_in;
+};
+
+__global__ void hs_k_act_seed(HsActSeedArgs a);
+__global__ void hs_k_act_cand(HsActCandArgs a);
+__global__ void hs_k_act_select(HsActSelectArgs a);
+__global__ void hs_k_act_optimize(HsActOptArgs a);

@@ -47,7 +47,9 @@ class hs_params(C.Structure):
         "outlierTH", "maxPixSearch", "trace_slackInterval", "trace_stepsize", "trace_minImprovementFactor",
         "trace_GNThreshold", "trace_extraSlackOnTH")] + [
         ("minTraceTestRadius", C.c_int), ("trace_GNIterations", C.c_int),
-        ("idepthFixPriorMargFac", C.c_float), ("margWeightFac", C.c_float)]
+        ("idepthFixPriorMargFac", C.c_float), ("margWeightFac", C.c_float),
+        ("desiredPointDensity", C.c_float), ("minTraceQuality", C.c_float), ("minIdepthH_act", C.c_float),
+        ("GNItsOnPointActivation", C.c_int)]
 
 
 # exported symbols of include/hs_ba.h (argument types)
@@ -93,7 +95,11 @@ SIGNATURES = {
     "hs_tracer_set_host_image": ([VP, I, VP], I),
     "hs_tracer_add_points": ([VP, I, VP, VP, VP], I),
     "hs_tracer_clear": ([VP], I),
-    "hs_tracer_set_state": ([VP] * 5, I),
+    "hs_tracer_set_state": ([VP] * 6, I),
+    "hs_tracer_set_types": ([VP, VP], I),
+    "hs_tracer_activate": ([VP, VP, I, VP, VP, I, VP, VP, VP, VP, I, VP, I, VP, VP, VP, VP, VP, VP], I),
+    "hs_tracer_get_distance_map": ([VP, VP], I),
+    "hs_tracer_compact": ([VP, VP], I),
     "hs_tracer_set_frame": ([VP, VP], I),
     "hs_tracer_set_frame_raw": ([VP, VP], I),
     "hs_tracer_trace": ([VP, I, VP, VP], I),

@@ -591,3 +591,118 @@ def make_trace_scene(n_points: int = 20000, n_hosts: int = 8, width: int = 1232,
                       KRKi=np.array(KRKi), Kt=np.array(Kt), aff=np.array(aff), pt_host=np.concatenate(hosts),
                       pt_u=np.concatenate(us), pt_v=np.concatenate(vs), pt_idepth_true=np.concatenate(idt),
                       planes=planes)
+
+
+# ----------------------------------------------------------------- point activation
+@dataclass
+class ActivationScene:
+    width: int
+    height: int
+    K: np.ndarray                 # level-0 intrinsics (fp64)
+    imgs: list                    # per window KF: DirPyr[0] (h, w, 3) float32
+    slots: np.ndarray             # [nF] tracer image slot of each KF
+    flagged: np.ndarray           # [nF] FlaggedForMarginalization
+    KRKi1: np.ndarray             # [nF, 9] float32 CoarseDistanceMap K[1] R(f -> newest) Ki[0]
+    Kt1: np.ndarray               # [nF, 3] float32
+    RTll: np.ndarray              # [nF*nF, 9] float32 targetPrecalc PRE_RTll (host-major)
+    tTll: np.ndarray              # [nF*nF, 3]
+    aff: np.ndarray               # [nF*nF, 2] PRE_aff_mode
+    act_frame: np.ndarray         # active MapPoints: window frame, u, v, idepth
+    act_u: np.ndarray
+    act_v: np.ndarray
+    act_idepth: np.ndarray
+    imm_frame: np.ndarray         # immature points: host window frame, u, v and their trace state
+    imm_u: np.ndarray
+    imm_v: np.ndarray
+    imm_idepth_min: np.ndarray
+    imm_idepth_max: np.ndarray
+    imm_quality: np.ndarray
+    imm_status: np.ndarray
+    imm_interval: np.ndarray
+    imm_type: np.ndarray
+    order: np.ndarray             # the reference's loop order over the stored points
+    ef_nPoints: int
+    currentMinActDist: float
+
+    @property
+    def n_frames(self):
+        return len(self.imgs)
+
+    @property
+    def K4(self):
+        return np.array([self.K[0, 0], self.K[1, 1], self.K[0, 2], self.K[1, 2]], np.float32)
+
+
+def make_activation_scene(n_active: int = 1500, n_immature: int = 3000, n_frames: int = 8, width: int = 640,
+                          height: int = 480, seed: int = SEED, kitti: bool = False,
+                          currentMinActDist: float = 2.0) -> ActivationScene:
+    """A window (make_ba_scene's keyframes, evalPT as PRE_worldToCam) with n_active MapPoints and n_immature traced
+    immature points on all keyframes: intervals around the true idepth (1% .. 50% wide, some NaN / negative),
+    every lastTraceStatus, quality 0..20, lastTracePixelInterval 0..12, my_type 1/2/4.  Points are stored
+    interleaved across hosts; `order` is the reference's per-host loop order.  Slots are 2f+1 and keyframe 0 is
+    flagged for marginalization."""
+    bs = make_ba_scene(n_points=n_active, n_frames=n_frames, width=width, height=height, seed=seed, kitti=kitti,
+                       pose_noise=(0.001, 0.0005))
+    rng = np.random.default_rng(seed + 29)
+    K = bs.K
+    nF = n_frames
+    Rs, ts = zip(*[se3_from_data(e) for e in bs.frames_eval])
+    aff_g2l = np.where(rng.random((nF, 1)) < 0.5, 0.0, rng.uniform([-0.02, -2.0], [0.02, 2.0], (nF, 2)))
+    # CoarseDistanceMap::makeK (Src/CoarseTracker.cpp:870-899): level-1 K in float, Ki[0] = K[0].inverse()
+    fx0, fy0, cx0, cy0 = (np.float32(x) for x in (K[0, 0], K[1, 1], K[0, 2], K[1, 2]))
+    K1 = np.array([[np.float32(fx0 * 0.5), 0, np.float32((float(cx0) + 0.5) / 2 - 0.5)],
+                   [0, np.float32(fy0 * 0.5), np.float32((float(cy0) + 0.5) / 2 - 0.5)], [0, 0, 1]], np.float32)
+    K0 = np.array([[fx0, 0, cx0], [0, fy0, cy0], [0, 0, 1]], np.float64)
+    Ki0 = np.linalg.inv(K0).astype(np.float32)
+    new = nF - 1
+    KRKi1, Kt1 = [], []
+    for f in range(nF):
+        R = Rs[new] @ Rs[f].T
+        t = ts[new] - R @ ts[f]
+        KRKi1.append((K1 @ R.astype(np.float32) @ Ki0).reshape(9))
+        Kt1.append(K1 @ t.astype(np.float32))
+    RT, tT, af = [], [], []
+    for h in range(nF):
+        for t_ in range(nF):
+            R = Rs[t_] @ Rs[h].T
+            RT.append(R.astype(np.float32).reshape(9))
+            tT.append((ts[t_] - R @ ts[h]).astype(np.float32))
+            a = math.exp(aff_g2l[t_, 0] - aff_g2l[h, 0])
+            af.append(np.array([a, aff_g2l[t_, 1] - a * aff_g2l[h, 1]], np.float32))
+    # immature points: top-gradient pixels of every host (not the MapPoints' cells), sub-pixel offsets
+    per = [n_immature // nF + (1 if i < n_immature % nF else 0) for i in range(nF)]
+    fr, us, vs, tru = [], [], [], []
+    for f in range(nF):
+        if per[f] == 0:
+            continue
+        pix = _select_points(bs.pyramids[f][0], per[f], 8, rng)
+        R_w2c, t_w2c = se3_from_data(bs.frames_pose[f])
+        R_c2w = R_w2c.T
+        _, depth = render_depth_at(bs.planes, K, R_c2w, -R_c2w @ t_w2c, pix)
+        fr.append(np.full(len(pix), f, np.int32))
+        us.append(pix[:, 1] + rng.uniform(-0.4, 0.4, len(pix)))
+        vs.append(pix[:, 0] + rng.uniform(-0.4, 0.4, len(pix)))
+        tru.append(1.0 / depth)
+    fr, us, vs, tru = (np.concatenate(x) for x in (fr, us, vs, tru))
+    n = len(fr)
+    c = tru * (1.0 + rng.normal(0, 0.02, n))
+    w = np.exp(rng.uniform(np.log(0.01), np.log(0.5), n))
+    lo, hi = c * (1.0 - w), c * (1.0 + w)
+    hi[rng.random(n) < 0.05] = np.nan
+    neg = rng.random(n) < 0.02
+    lo[neg] = -hi[neg] - 0.01
+    status = rng.choice(6, n, p=[0.45, 0.1, 0.1, 0.1, 0.1, 0.15]).astype(np.uint8)  # IPS_* order: G,OOB,OUT,SK,BC,UN
+    perm = rng.permutation(n)
+    fr, us, vs, lo, hi, status = fr[perm], us[perm], vs[perm], lo[perm], hi[perm], status[perm]
+    order = np.argsort(fr, kind="stable").astype(np.int32)
+    return ActivationScene(
+        width=width, height=height, K=K, imgs=bs.images_level0(), slots=(2 * np.arange(nF) + 1).astype(np.int32),
+        flagged=(np.arange(nF) == 0).astype(np.int32), KRKi1=np.array(KRKi1, np.float32),
+        Kt1=np.array(Kt1, np.float32), RTll=np.array(RT, np.float32), tTll=np.array(tT, np.float32),
+        aff=np.array(af, np.float32), act_frame=bs.pt_host.astype(np.int32), act_u=bs.pt_u, act_v=bs.pt_v,
+        act_idepth=bs.pt_idepth, imm_frame=fr, imm_u=us.astype(np.float32), imm_v=vs.astype(np.float32),
+        imm_idepth_min=lo.astype(np.float32), imm_idepth_max=hi.astype(np.float32),
+        imm_quality=rng.uniform(0, 20, n).astype(np.float32), imm_status=status,
+        imm_interval=rng.uniform(0, 12, n).astype(np.float32),
+        imm_type=rng.choice([1.0, 2.0, 4.0], n, p=[0.6, 0.25, 0.15]).astype(np.float32), order=order,
+        ef_nPoints=n_active, currentMinActDist=currentMinActDist)

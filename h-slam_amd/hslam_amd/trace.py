@@ -21,6 +21,32 @@ FIELDS = ("status", "idepth_min", "idepth_max", "quality", "uv", "interval", "en
 IPS = ("GOOD", "OOB", "OUTLIER", "SKIPPED", "BADCONDITION", "UNINITIALIZED")
 
 
+ACT = ("KEEP", "DELETED", "ACTIVATED")
+# hs_act_frame / hs_act_pair (include/hs_trace.h) as numpy records
+ACT_FRAME_DT = np.dtype([("slot", np.int32), ("flagged_for_marg", np.int32), ("KRKi", np.float32, 9),
+                         ("Kt", np.float32, 3)])
+ACT_PAIR_DT = np.dtype([("RTll", np.float32, 9), ("tTll", np.float32, 3), ("aff", np.float32, 2)])
+
+
+def act_frames_array(slot, flagged, KRKi, Kt):
+    """[nF] hs_act_frame records: tracer slot, FlaggedForMarginalization, level-1 KRKi / Kt to the newest KF."""
+    out = np.zeros(len(slot), ACT_FRAME_DT)
+    out["slot"] = slot
+    out["flagged_for_marg"] = flagged
+    out["KRKi"] = np.asarray(KRKi, np.float32).reshape(-1, 9)
+    out["Kt"] = np.asarray(Kt, np.float32).reshape(-1, 3)
+    return out
+
+
+def act_pairs_array(RTll, tTll, aff):
+    """[nF*nF] hs_act_pair records (FrameFramePrecalc PRE_RTll / PRE_tTll / PRE_aff_mode, host-major)."""
+    out = np.zeros(len(RTll), ACT_PAIR_DT)
+    out["RTll"] = np.asarray(RTll, np.float32).reshape(-1, 9)
+    out["tTll"] = np.asarray(tTll, np.float32).reshape(-1, 3)
+    out["aff"] = np.asarray(aff, np.float32).reshape(-1, 2)
+    return out
+
+
 def hosts_array(KRKi, Kt, aff):
     """[nH] hs_trace_host records (KRKi[9], Kt[3], aff[2], float32) as a contiguous [nH, 14] float32 array."""
     return np.ascontiguousarray(np.concatenate([np.asarray(KRKi, np.float32).reshape(-1, 9),
@@ -58,10 +84,10 @@ class ImmatureTracer:
         check(self.lib.hs_tracer_add_points(self.h, len(h), ptr(h), ptr(uu), ptr(vv)))
         self.n += len(h)
 
-    def set_state(self, idepth_min=None, idepth_max=None, quality=None, status=None):
+    def set_state(self, idepth_min=None, idepth_max=None, quality=None, status=None, interval=None):
         arr = [None if a is None else np.ascontiguousarray(a, dt)
                for a, dt in ((idepth_min, np.float32), (idepth_max, np.float32), (quality, np.float32),
-                             (status, np.uint8))]
+                             (status, np.uint8), (interval, np.float32))]
         check(self.lib.hs_tracer_set_state(self.h, *[ptr(a) for a in arr]))
 
     def set_frame(self, img):
@@ -97,6 +123,48 @@ class ImmatureTracer:
         m = C.c_int()
         check(self.lib.hs_tracer_get_points(self.h, C.byref(m), *[ptr(out[k]) for k in FIELDS]))
         return out
+
+    def set_types(self, my_type):
+        """ImmaturePoint::my_type of every stored point (PixelSelector's 1 / 2 / 4)."""
+        a = np.ascontiguousarray(my_type, np.float32)
+        assert len(a) == self.n
+        check(self.lib.hs_tracer_set_types(self.h, ptr(a)))
+
+    # Src/Mapping.cpp:330-480 (System::activatePointsMT)
+    def activatePointsMT(self, K4, frames, pairs, act_frame, act_u, act_v, act_idepth, ef_nPoints,
+                         currentMinActDist, order=None):
+        """One activation over the stored points.  frames / pairs: act_frames_array / act_pairs_array records.
+        Returns dict(action, idepth, res_in, activated, currentMinActDist)."""
+        k4 = np.ascontiguousarray(K4, np.float32)
+        fr = np.ascontiguousarray(frames, ACT_FRAME_DT)
+        pr = np.ascontiguousarray(pairs, ACT_PAIR_DT)
+        af = np.ascontiguousarray(act_frame, np.int32)
+        au, av, ai = (np.ascontiguousarray(x, np.float32) for x in (act_u, act_v, act_idepth))
+        od = None if order is None else np.ascontiguousarray(order, np.int32)
+        n = self.n
+        action, idepth, res_in = np.zeros(n, np.uint8), np.zeros(n, np.float32), np.zeros(n, np.uint8)
+        activated = np.zeros(max(n, 1), np.int32)
+        cmad = C.c_float(currentMinActDist)
+        na = C.c_int()
+        check(self.lib.hs_tracer_activate(self.h, ptr(k4), len(fr), ptr(fr), ptr(pr), len(af), ptr(af), ptr(au),
+                                          ptr(av), ptr(ai), int(ef_nPoints), C.byref(cmad),
+                                          0 if od is None else len(od), ptr(od), ptr(action), ptr(idepth),
+                                          ptr(res_in), ptr(activated), C.byref(na)))
+        return dict(action=action, idepth=idepth, res_in=res_in, activated=activated[: na.value],
+                    currentMinActDist=cmad.value)
+
+    def distance_map(self):
+        """CoarseDistanceMap::fwdWarpedIDDistFinal after the last activation, (H/2, W/2) float32."""
+        out = np.zeros((self.H >> 1) * (self.W >> 1), np.float32)
+        check(self.lib.hs_tracer_get_distance_map(self.h, ptr(out)))
+        return out.reshape(self.H >> 1, self.W >> 1)
+
+    def compact(self, keep):
+        """Drop the points with keep == 0 (survivors keep their order)."""
+        k = np.ascontiguousarray(keep, np.uint8)
+        assert len(k) == self.n
+        check(self.lib.hs_tracer_compact(self.h, ptr(k)))
+        self.n = int(k.astype(bool).sum())
 
     def reinit(self):
         """ImmaturePoint ctor again on every stored point (a fresh first-trace state), on the device."""

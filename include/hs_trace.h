@@ -12,6 +12,13 @@
  *                          traceNewCoarse passes (Mapping.cpp:505-511).
  *   hs_tracer_get_points   read-back of ImmaturePoint's public members (lastTraceStatus, idepth_min/max,
  *                          quality, lastTraceUV, lastTracePixelInterval, energyTH, color, weights, gradH).
+ *   hs_tracer_activate     System::activatePointsMT (Src/Mapping.cpp:330-480): the currentMinActDist update,
+ *                          CoarseDistanceMap::makeDistanceMap / growDistBFS / addIntoDistFinal
+ *                          (Src/CoarseTracker.cpp:726-868), the immature-point selection loop and
+ *                          System::optimizeImmaturePoint (Src/FullSystemOptPoint.cpp:24-175) with
+ *                          ImmaturePoint::linearizeResidual (Src/ImmaturePoint.cpp:389-451) for every selected
+ *                          point.  The MapPoint / PointFrameResidual objects themselves are built by the caller
+ *                          from the outputs (activated flag, idepth, IN-residual mask).
  *
  * Conventions as include/hs_ba.h: status codes (hs_types.h), caller-owned host buffers copied in/out,
  * the context owns device memory and its own HIP stream, single caller.  Images are Frame::DirPyr[0]:
@@ -49,9 +56,10 @@ int hs_tracer_set_host_image(hs_tracer* t, int slot, const float* img_lvl0);
 int hs_tracer_add_points(hs_tracer* t, int n, const int* host, const float* u, const float* v);
 /* drop all points (a new window) */
 int hs_tracer_clear(hs_tracer* t);
-/* overwrite the search state of all points (nullable arrays of length n_points): a point traced before */
+/* overwrite the search state of all points (nullable arrays of length n_points): a point traced before;
+   interval = lastTracePixelInterval */
 int hs_tracer_set_state(hs_tracer* t, const float* idepth_min, const float* idepth_max, const float* quality,
-                        const uint8_t* status);
+                        const uint8_t* status, const float* interval);
 
 /* the frame to trace on (level 0 image); stays resident until the next call */
 int hs_tracer_set_frame(hs_tracer* t, const float* img_lvl0);
@@ -67,6 +75,54 @@ int hs_tracer_trace(hs_tracer* t, int n_hosts, const hs_trace_host* hosts, int c
 int hs_tracer_get_points(hs_tracer* t, int* n, uint8_t* status, float* idepth_min, float* idepth_max,
                          float* quality, float* uv, float* interval, float* energyTH, float* color, float* weights,
                          float* gradH);
+/* ImmaturePoint::my_type of every stored point (n_points floats; PixelSelector's 1 / 2 / 4).  Points are
+   added with my_type 1. */
+int hs_tracer_set_types(hs_tracer* t, const float* my_type);
+
+/* ---- point activation (activatePointsMT) ----------------------------------------------------------------- */
+
+/* one window keyframe, in frameHessians order (the newest keyframe last) */
+typedef struct hs_act_frame {
+  int slot;              /* tracer image slot holding this keyframe's DirPyr[0] (hs_tracer_set_host_image) */
+  int flagged_for_marg;  /* Frame::FlaggedForMarginalization (Mapping.cpp:397) */
+  float KRKi[9];         /* CoarseDistanceMap::K[1] * R(frame -> newest) * Ki[0], row-major (Mapping.cpp:368,
+                            CoarseTracker.cpp:745); unused for the newest keyframe */
+  float Kt[3];           /* K[1] * t(frame -> newest) */
+} hs_act_frame;
+
+/* Frame::targetPrecalc[target] of a host keyframe (FrameFramePrecalc::set, Src/OptimizationClasses.cpp:13-39) */
+typedef struct hs_act_pair {
+  float RTll[9];         /* PRE_RTll, row-major */
+  float tTll[3];         /* PRE_tTll */
+  float aff[2];          /* PRE_aff_mode */
+} hs_act_pair;
+
+/* what activatePointsMT did to an immature point */
+enum { HS_ACT_KEEP = 0, HS_ACT_DELETED = 1, HS_ACT_ACTIVATED = 2 };
+
+/* One activatePointsMT call.
+     K4            level-0 fx, fy, cx, cy (CalibData fxl .. cyl); fxli = 1/fx and fyli = 1/fy in float
+     frames[nF]    the window (nF <= 8), pairs[nF*nF] at [host*nF + target]
+     active points (for makeDistanceMap): window frame index act_frame[i], u, v, idepth of every MapPoint
+     ef_nPoints, *currentMinActDist: EnergyFunctional::nPoints and System::currentMinActDist (updated in place)
+     order[n_order]: the tracer points in the reference's loop order (for host in frameHessians, for i in
+                   host->ImmaturePoints); NULL = storage order.  Points whose slot is no window frame's, and
+                   points of the newest keyframe, are left untouched (HS_ACT_KEEP).
+   Outputs (nullable, indexed by tracer point): action[n] (HS_ACT_*), idepth[n] (the new MapPoint's idepth
+   and idepth_zero, activated points only), res_in[n] (bit f set: a PointFrameResidual into window frame f in
+   state IN); activated[n] = the activated points in the reference's toOptimize order, *n_activated their
+   number.  The tracer's points are not removed: hs_tracer_compact does that. */
+int hs_tracer_activate(hs_tracer* t, const float K4[4], int nF, const hs_act_frame* frames, const hs_act_pair* pairs,
+                       int n_active, const int* act_frame, const float* act_u, const float* act_v,
+                       const float* act_idepth, int ef_nPoints, float* currentMinActDist, int n_order,
+                       const int* order, uint8_t* action, float* idepth, uint8_t* res_in, int* activated,
+                       int* n_activated);
+/* the distance map of the last hs_tracer_activate after its selection loop (fwdWarpedIDDistFinal,
+   (W/2)*(H/2) floats) */
+int hs_tracer_get_distance_map(hs_tracer* t, float* dist);
+/* drop the points with keep[i] == 0; the survivors keep their relative order */
+int hs_tracer_compact(hs_tracer* t, const uint8_t* keep);
+
 /* re-run the ImmaturePoint ctor on every point already added (same host / u / v, no upload): a fresh
    first-trace state (idepth_min 0, idepth_max NaN, quality 10000, IPS_UNINITIALIZED) */
 int hs_tracer_reinit(hs_tracer* t);

@@ -112,6 +112,12 @@ typedef struct hs_params {
   /* marginalization (EnergyFunctional::marginalizePointsF, Src/EnergyFunctional.cpp:563,601) */
   float idepthFixPriorMargFac;   /* 600*600 :101 */
   float margWeightFac;           /* 0.25   :80 */
+  /* point activation (System::activatePointsMT + optimizeImmaturePoint, Src/Mapping.cpp:330-492,
+     Src/FullSystemOptPoint.cpp:24-175) */
+  float desiredPointDensity;     /* 2000   :121 */
+  float minTraceQuality;         /* 3      :86 */
+  float minIdepthH_act;          /* 100    :118 */
+  int GNItsOnPointActivation;    /* 3      :54 */
 } hs_params;
 
 #ifdef __cplusplus

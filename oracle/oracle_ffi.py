@@ -46,7 +46,9 @@ class hs_params(C.Structure):
         "outlierTH", "maxPixSearch", "trace_slackInterval", "trace_stepsize", "trace_minImprovementFactor",
         "trace_GNThreshold", "trace_extraSlackOnTH")] + [
         ("minTraceTestRadius", C.c_int), ("trace_GNIterations", C.c_int),
-        ("idepthFixPriorMargFac", C.c_float), ("margWeightFac", C.c_float)]
+        ("idepthFixPriorMargFac", C.c_float), ("margWeightFac", C.c_float),
+        ("desiredPointDensity", C.c_float), ("minTraceQuality", C.c_float), ("minIdepthH_act", C.c_float),
+        ("GNItsOnPointActivation", C.c_int)]
 
 
 def build(quiet=True):
@@ -113,7 +115,13 @@ def load(fast=False):
     lib.hso_trc_destroy.argtypes = [vp]
     lib.hso_trc_add_points.argtypes = [vp, C.c_int, vp, C.c_int, vp, vp, vp]
     lib.hso_trc_add_points.restype = C.c_int
-    lib.hso_trc_set_state.argtypes = [vp] * 5
+    lib.hso_trc_set_state.argtypes = [vp] * 6
+    lib.hso_trc_set_types.argtypes = [vp, vp]
+    lib.hso_trc_activate.argtypes = [vp, vp, C.c_int, vp, vp, vp, C.c_int, vp, vp, vp, vp, C.c_int, vp, C.c_int,
+                                     vp, vp, vp, vp, vp, vp]
+    lib.hso_trc_activate.restype = C.c_int
+    lib.hso_trc_distance_map.argtypes = [vp, vp]
+    lib.hso_trc_compact.argtypes = [vp, vp]
     lib.hso_trc_trace.argtypes = [vp] * 4
     lib.hso_trc_get.argtypes = [vp] * 11
     _LIBS[name] = lib
@@ -420,10 +428,10 @@ class OracleTracer:
         assert rc == 0
         self.n += len(h)
 
-    def set_state(self, idepth_min=None, idepth_max=None, quality=None, status=None):
+    def set_state(self, idepth_min=None, idepth_max=None, quality=None, status=None, interval=None):
         arr = [None if a is None else np.ascontiguousarray(a, dt)
                for a, dt in ((idepth_min, np.float32), (idepth_max, np.float32), (quality, np.float32),
-                             (status, np.uint8))]
+                             (status, np.uint8), (interval, np.float32))]
         self.lib.hso_trc_set_state(self.h, *[_p(a) for a in arr])
 
     def trace(self, new_img, KRKi, Kt, aff):
@@ -445,6 +453,44 @@ class OracleTracer:
                    gradH=np.zeros((n, 4), np.float32))
         self.lib.hso_trc_get(self.h, *[_p(out[k]) for k in TRACE_FIELDS])
         return out
+
+
+    def set_types(self, my_type):
+        self.lib.hso_trc_set_types(self.h, _p(np.ascontiguousarray(my_type, np.float32)))
+
+    def activatePointsMT(self, frame_imgs, K4, frames, pairs, act_frame, act_u, act_v, act_idepth, ef_nPoints,
+                         currentMinActDist, order=None):
+        """System::activatePointsMT restated (oracle/trace_oracle.cpp).  frames / pairs: numpy records laid out as
+        hs_act_frame / hs_act_pair; frame_imgs[nF]: DirPyr[0] of the window keyframes."""
+        imgs = [np.ascontiguousarray(a, np.float32) for a in frame_imgs]
+        pp = (C.c_void_p * len(imgs))(*[a.ctypes.data for a in imgs])
+        k4 = np.ascontiguousarray(K4, np.float32)
+        fr, pr = np.ascontiguousarray(frames), np.ascontiguousarray(pairs)
+        af = np.ascontiguousarray(act_frame, np.int32)
+        au, av, ai = (np.ascontiguousarray(x, np.float32) for x in (act_u, act_v, act_idepth))
+        od = None if order is None else np.ascontiguousarray(order, np.int32)
+        n = self.n
+        action, idepth, res_in = np.zeros(n, np.uint8), np.zeros(n, np.float32), np.zeros(n, np.uint8)
+        activated = np.zeros(max(n, 1), np.int32)
+        cmad = C.c_float(currentMinActDist)
+        na = C.c_int()
+        rc = self.lib.hso_trc_activate(self.h, _p(k4), len(fr), C.cast(pp, C.c_void_p), _p(fr), _p(pr), len(af),
+                                       _p(af), _p(au), _p(av), _p(ai), int(ef_nPoints), C.byref(cmad),
+                                       0 if od is None else len(od), _p(od), _p(action), _p(idepth), _p(res_in),
+                                       _p(activated), C.byref(na))
+        assert rc == 0
+        return dict(action=action, idepth=idepth, res_in=res_in, activated=activated[: na.value],
+                    currentMinActDist=cmad.value)
+
+    def distance_map(self):
+        out = np.zeros((self.H >> 1) * (self.W >> 1), np.float32)
+        self.lib.hso_trc_distance_map(self.h, _p(out))
+        return out.reshape(self.H >> 1, self.W >> 1)
+
+    def compact(self, keep):
+        k = np.ascontiguousarray(keep, np.uint8)
+        self.lib.hso_trc_compact(self.h, _p(k))
+        self.n = int(k.astype(bool).sum())
 
 
 # ------------------------------------------------------------------ Frame::CreateDirPyrs restatement

@@ -16,6 +16,8 @@
 #include "../include/hs_trace.h"
 #include "oracle_common.h"
 
+#define HS_TRC_MAXSLOT_ORACLE 64
+
 namespace hso {
 
 // The texel base index ix + iy*W is clamped to [0, W*H - W - 2] (the last base whose 2x2 taps lie in the
@@ -77,6 +79,7 @@ struct ImmPt {
   int lastTraceStatus;
   float lastTraceUV[2];
   float lastTracePixelInterval;
+  float my_type;
 };
 
 // ImmaturePoint ctor, Src/ImmaturePoint.cpp:7-32
@@ -297,10 +300,181 @@ static int trace_on(ImmPt& p, const float* img, int W, int H, const float KRKi[9
   return p.lastTraceStatus = IPS_GOOD;
 }
 
+
+// ============================================================================ point activation
+// CoarseDistanceMap (Src/CoarseTracker.cpp:698-868): fwdWarpedIDDistFinal at pyramid level 1 and its BFS.
+struct DistMap {
+  int w1 = 0, h1 = 0;
+  std::vector<float> d;
+  std::vector<int> l1, l2;  // bfsList1 / bfsList2 as packed (x, y) pairs
+  void grow(int bfsNum) {  // growDistBFS, :759-857 (k even: 4-neighbourhood, k odd: 8-neighbourhood)
+    for (int k = 1; k < 40; k++) {
+      int bfsNum2 = bfsNum;
+      std::swap(l1, l2);
+      bfsNum = 0;
+      for (int i = 0; i < bfsNum2; i++) {
+        const int x = l2[2 * i], y = l2[2 * i + 1];
+        if (x == 0 || y == 0 || x == w1 - 1 || y == h1 - 1) continue;
+        const int idx = x + y * w1;
+        const int nb = (k % 2 == 0) ? 4 : 8;
+        static const int off[8][2] = {{1, 0}, {-1, 0}, {0, 1}, {0, -1}, {1, 1}, {-1, 1}, {-1, -1}, {1, -1}};
+        for (int j = 0; j < nb; j++) {
+          const int q = idx + off[j][0] + off[j][1] * w1;
+          if (d[q] > k) {
+            d[q] = k;
+            l1[2 * bfsNum] = x + off[j][0];
+            l1[2 * bfsNum + 1] = y + off[j][1];
+            bfsNum++;
+          }
+        }
+      }
+    }
+  }
+  void add(int u, int v) {  // addIntoDistFinal, :860-866
+    l1[0] = u;
+    l1[1] = v;
+    d[u + w1 * v] = 0;
+    grow(1);
+  }
+};
+
+// ImmaturePointTemporaryResidual (Include/ImmaturePoint.h:13-22)
+struct TmpRes {
+  int target;
+  int state_state, state_NewState;
+  float state_energy, state_NewEnergy;
+};
+
+struct ActCalib {
+  int W, H;
+  float fxl, fyl, cxl, cyl, fxli, fyli;
+};
+
+// ImmaturePoint::linearizeResidual, Src/ImmaturePoint.cpp:389-451
+static double imm_linearize_residual(const ImmPt& p, float outlierTHSlack, TmpRes& r, float& Hdd, float& bd,
+                                     float idepth, const float* dIl, const hs_act_pair& pc, const ActCalib& c,
+                                     const hs_params& P) {
+  if (r.state_state == HS_RES_OOB) {
+    r.state_NewState = HS_RES_OOB;
+    return r.state_energy;
+  }
+  float energyLeft = 0;
+  const float affLL0 = pc.aff[0], affLL1 = pc.aff[1];
+  for (int idx = 0; idx < PN; idx++) {
+    const int dx = kPattern[idx][0], dy = kPattern[idx][1];
+    // projectPoint(u, v, idepth, dx, dy, Calib, PRE_RTll, PRE_tTll, ...)  Include/DirectProjection.h:20-38
+    float KliP[3] = {(p.u + dx - c.cxl) * c.fxli, (p.v + dy - c.cyl) * c.fyli, 1};
+    float ptp[3], Rk[3];
+    mv3f(pc.RTll, KliP, Rk);
+    for (int i = 0; i < 3; i++) ptp[i] = Rk[i] + pc.tTll[i] * idepth;
+    const float drescale = 1.0f / ptp[2];
+    if (!(drescale > 0)) {
+      r.state_NewState = HS_RES_OOB;
+      return r.state_energy;
+    }
+    const float u = ptp[0] * drescale, v = ptp[1] * drescale;
+    const float Ku = u * c.fxl + c.cxl, Kv = v * c.fyl + c.cyl;
+    if (!(Ku > 1.1f && Kv > 1.1f && Ku < (c.W - 3) && Kv < (c.H - 3))) {
+      r.state_NewState = HS_RES_OOB;
+      return r.state_energy;
+    }
+    const V3f hit = interp33(dIl, Ku, Kv, c.W);
+    if (!std::isfinite(hit.x)) {
+      r.state_NewState = HS_RES_OOB;
+      return r.state_energy;
+    }
+    const float residual = hit.x - (affLL0 * p.color[idx] + affLL1);
+    float hw = fabsf(residual) < P.huberTH ? 1 : P.huberTH / fabsf(residual);
+    energyLeft += p.weights[idx] * p.weights[idx] * hw * residual * residual * (2 - hw);
+    const float dxInterp = hit.y * c.fxl;
+    const float dyInterp = hit.z * c.fyl;
+    // derive_idepth, Include/DirectProjection.h:7-10
+    const float d_idepth =
+        (dxInterp * drescale * (pc.tTll[0] - pc.tTll[2] * u) + dyInterp * drescale * (pc.tTll[1] - pc.tTll[2] * v)) *
+        SCALE_IDEPTH;
+    hw *= p.weights[idx] * p.weights[idx];
+    Hdd += (hw * d_idepth) * d_idepth;
+    bd += (hw * residual) * d_idepth;
+  }
+  if (energyLeft > p.energyTH * outlierTHSlack) {
+    energyLeft = p.energyTH * outlierTHSlack;
+    r.state_NewState = HS_RES_OUT;
+  } else {
+    r.state_NewState = HS_RES_IN;
+  }
+  r.state_NewEnergy = energyLeft;
+  return energyLeft;
+}
+
+// System::optimizeImmaturePoint, Src/FullSystemOptPoint.cpp:24-175 (minObs = 1).  Returns true when a MapPoint is
+// made; idepth / res_in (bit = target window frame, state IN) describe it.
+static bool optimize_immature_point(const ImmPt& p, int hostF, int nF, const float* const* imgs,
+                                    const hs_act_pair* pairs, const ActCalib& c, const hs_params& P, float& idepth_out,
+                                    uint8_t& res_in) {
+  TmpRes res[8];
+  int nres = 0;
+  for (int f = 0; f < nF; f++) {
+    if (f == hostF) continue;
+    TmpRes& r = res[nres++];
+    r.state_NewEnergy = r.state_energy = 0;
+    r.state_NewState = HS_RES_OUT;
+    r.state_state = HS_RES_IN;
+    r.target = f;
+  }
+  float lastEnergy = 0, lastHdd = 0, lastbd = 0;
+  float currentIdepth = (p.idepth_max + p.idepth_min) * 0.5f;
+  for (int i = 0; i < nres; i++) {
+    lastEnergy += imm_linearize_residual(p, 1000, res[i], lastHdd, lastbd, currentIdepth, imgs[res[i].target],
+                                         pairs[hostF * nF + res[i].target], c, P);
+    res[i].state_state = res[i].state_NewState;
+    res[i].state_energy = res[i].state_NewEnergy;
+  }
+  if (!std::isfinite(lastEnergy) || lastHdd < P.minIdepthH_act) return false;
+  float lambda = 0.1;
+  for (int iteration = 0; iteration < P.GNItsOnPointActivation; iteration++) {
+    float H = lastHdd;
+    H *= 1 + lambda;
+    const float step = (1.0 / H) * lastbd;
+    const float newIdepth = currentIdepth - step;
+    float newHdd = 0, newbd = 0, newEnergy = 0;
+    for (int i = 0; i < nres; i++)
+      newEnergy += imm_linearize_residual(p, 1, res[i], newHdd, newbd, newIdepth, imgs[res[i].target],
+                                          pairs[hostF * nF + res[i].target], c, P);
+    if (!std::isfinite(lastEnergy) || newHdd < P.minIdepthH_act) return false;
+    if (newEnergy < lastEnergy) {
+      currentIdepth = newIdepth;
+      lastHdd = newHdd;
+      lastbd = newbd;
+      lastEnergy = newEnergy;
+      for (int i = 0; i < nres; i++) {
+        res[i].state_state = res[i].state_NewState;
+        res[i].state_energy = res[i].state_NewEnergy;
+      }
+      lambda *= 0.5;
+    } else {
+      lambda *= 5;
+    }
+    if (fabsf(step) < 0.0001 * currentIdepth) break;
+  }
+  if (!std::isfinite(currentIdepth)) return false;
+  int numGoodRes = 0;
+  res_in = 0;
+  for (int i = 0; i < nres; i++)
+    if (res[i].state_state == HS_RES_IN) {
+      numGoodRes++;
+      res_in |= (uint8_t)(1u << res[i].target);
+    }
+  if (numGoodRes < 1) return false;
+  if (!std::isfinite(p.energyTH)) return false;  // MapPoint ctor copies energyTH (Include/MapPoint.h:92-115)
+  idepth_out = currentIdepth;
+  return true;
+}
+
 struct Tracer {
   hs_params P;
   int W, H;
   std::vector<ImmPt> pts;
+  DistMap dm;
 };
 
 }  // namespace hso
@@ -331,6 +505,7 @@ int hso_trc_add_points(void* h, int nH, const float* const* host_imgs, int n, co
     p.host = host[i];
     p.u = u[i];
     p.v = v[i];
+    p.my_type = 1;
     immature_ctor(p, host_imgs[host[i]], t->W, t->H, t->P);
     t->pts.push_back(p);
   }
@@ -339,13 +514,14 @@ int hso_trc_add_points(void* h, int nH, const float* const* host_imgs, int n, co
 
 // overwrite the search state (a point traced before): idepth_min/max, quality, lastTraceStatus (all nullable)
 void hso_trc_set_state(void* h, const float* idepth_min, const float* idepth_max, const float* quality,
-                       const uint8_t* status) {
+                       const uint8_t* status, const float* interval) {
   Tracer* t = (Tracer*)h;
   for (size_t i = 0; i < t->pts.size(); i++) {
     if (idepth_min) t->pts[i].idepth_min = idepth_min[i];
     if (idepth_max) t->pts[i].idepth_max = idepth_max[i];
     if (quality) t->pts[i].quality = quality[i];
     if (status) t->pts[i].lastTraceStatus = status[i];
+    if (interval) t->pts[i].lastTracePixelInterval = interval[i];
   }
 }
 
@@ -379,6 +555,137 @@ void hso_trc_get(void* h, uint8_t* status, float* idepth_min, float* idepth_max,
     }
     if (gradH) for (int k = 0; k < 4; k++) gradH[4 * i + k] = p.gradH[k];
   }
+}
+
+void hso_trc_set_types(void* h, const float* my_type) {
+  Tracer* t = (Tracer*)h;
+  for (size_t i = 0; i < t->pts.size(); i++) t->pts[i].my_type = my_type[i];
+}
+
+// System::activatePointsMT, Src/Mapping.cpp:330-480.  frame_imgs[nF]: DirPyr[0] of the window keyframes (AoS).
+int hso_trc_activate(void* h, const float K4[4], int nF, const float* const* frame_imgs, const hs_act_frame* frames,
+                     const hs_act_pair* pairs, int n_active, const int* act_frame, const float* act_u,
+                     const float* act_v, const float* act_idepth, int ef_nPoints, float* currentMinActDist,
+                     int n_order, const int* order, uint8_t* action, float* idepth, uint8_t* res_in, int* activated,
+                     int* n_activated) {
+  Tracer* t = (Tracer*)h;
+  const hs_params& P = t->P;
+  const int n = (int)t->pts.size();
+  float& cmad = *currentMinActDist;
+  // :332-352
+  if (ef_nPoints < P.desiredPointDensity * 0.66) cmad -= 0.8;
+  if (ef_nPoints < P.desiredPointDensity * 0.8) cmad -= 0.5;
+  else if (ef_nPoints < P.desiredPointDensity * 0.9) cmad -= 0.2;
+  else if (ef_nPoints < P.desiredPointDensity) cmad -= 0.1;
+  if (ef_nPoints > P.desiredPointDensity * 1.5) cmad += 0.8;
+  if (ef_nPoints > P.desiredPointDensity * 1.3) cmad += 0.5;
+  if (ef_nPoints > P.desiredPointDensity * 1.15) cmad += 0.2;
+  if (ef_nPoints > P.desiredPointDensity) cmad += 0.1;
+  if (cmad < 0) cmad = 0;
+  if (cmad > 4) cmad = 4;
+
+  const int newest = nF - 1;
+  DistMap& dm = t->dm;
+  dm.w1 = t->W >> 1;
+  dm.h1 = t->H >> 1;
+  const int wh1 = dm.w1 * dm.h1;
+  dm.d.assign(wh1, 1000.f);
+  dm.l1.assign(2 * wh1, 0);
+  dm.l2.assign(2 * wh1, 0);
+  // makeDistanceMap, Src/CoarseTracker.cpp:726-756
+  int numItems = 0;
+  for (int i = 0; i < n_active; i++) {
+    const int f = act_frame[i];
+    if (f == newest) continue;
+    const float* KRKi = frames[f].KRKi;
+    const float* Kt = frames[f].Kt;
+    float pt[3] = {act_u[i], act_v[i], 1}, ptp[3];
+    mv3f(KRKi, pt, ptp);
+    for (int k = 0; k < 3; k++) ptp[k] = ptp[k] + Kt[k] * act_idepth[i];
+    const int u = ptp[0] / ptp[2] + 0.5f;
+    const int v = ptp[1] / ptp[2] + 0.5f;
+    if (!(u > 0 && v > 0 && u < dm.w1 && v < dm.h1)) continue;
+    dm.d[u + dm.w1 * v] = 0;
+    dm.l1[2 * numItems] = u;
+    dm.l1[2 * numItems + 1] = v;
+    numItems++;
+  }
+  dm.grow(numItems);
+
+  ActCalib c{t->W, t->H, K4[0], K4[1], K4[2], K4[3], 1.0f / K4[0], 1.0f / K4[1]};
+  std::vector<int> frame_of_slot(HS_TRC_MAXSLOT_ORACLE, -1);
+  for (int f = 0; f < nF; f++) frame_of_slot[frames[f].slot] = f;
+  for (int i = 0; i < n; i++) {
+    if (action) action[i] = HS_ACT_KEEP;
+    if (res_in) res_in[i] = 0;
+  }
+  std::vector<int> toOptimize;
+  const int m = order ? n_order : n;
+  for (int j = 0; j < m; j++) {  // :364-429
+    const int i = order ? order[j] : j;
+    ImmPt& ph = t->pts[i];
+    const int f = frame_of_slot[ph.host];
+    if (f < 0 || f == newest) continue;
+    if (!std::isfinite(ph.idepth_max) || ph.lastTraceStatus == IPS_OUTLIER) {
+      if (action) action[i] = HS_ACT_DELETED;
+      continue;
+    }
+    const bool canActivate = (ph.lastTraceStatus == IPS_GOOD || ph.lastTraceStatus == IPS_SKIPPED ||
+                              ph.lastTraceStatus == IPS_BADCONDITION || ph.lastTraceStatus == IPS_OOB) &&
+                             ph.lastTracePixelInterval < 8 && ph.quality > P.minTraceQuality &&
+                             (ph.idepth_max + ph.idepth_min) > 0;
+    if (!canActivate) {
+      if (frames[f].flagged_for_marg || ph.lastTraceStatus == IPS_OOB)
+        if (action) action[i] = HS_ACT_DELETED;
+      continue;
+    }
+    float pt[3] = {ph.u, ph.v, 1}, ptp[3];
+    mv3f(frames[f].KRKi, pt, ptp);
+    const float mid = 0.5f * (ph.idepth_max + ph.idepth_min);
+    for (int k = 0; k < 3; k++) ptp[k] = ptp[k] + frames[f].Kt[k] * mid;
+    const int u = ptp[0] / ptp[2] + 0.5f;
+    const int v = ptp[1] / ptp[2] + 0.5f;
+    if (u > 0 && v > 0 && u < dm.w1 && v < dm.h1) {
+      const float dist = dm.d[u + dm.w1 * v] + (ptp[0] - floorf((float)(ptp[0])));
+      if (dist >= cmad * ph.my_type) {
+        dm.add(u, v);
+        toOptimize.push_back(i);
+      }
+    } else {
+      if (action) action[i] = HS_ACT_DELETED;
+    }
+  }
+  // activatePointsMT_Reductor + the result loop, :434-480: every optimized point is either activated or deleted
+  int na = 0;
+  for (int i : toOptimize) {
+    const ImmPt& ph = t->pts[i];
+    const int f = frame_of_slot[ph.host];
+    float id = 0;
+    uint8_t mask = 0;
+    const bool ok = optimize_immature_point(ph, f, nF, frame_imgs, pairs, c, P, id, mask);
+    if (action) action[i] = ok ? HS_ACT_ACTIVATED : HS_ACT_DELETED;
+    if (ok) {
+      if (idepth) idepth[i] = id;
+      if (res_in) res_in[i] = mask;
+      if (activated) activated[na] = i;
+      na++;
+    }
+  }
+  if (n_activated) *n_activated = na;
+  return 0;
+}
+
+void hso_trc_distance_map(void* h, float* out) {
+  Tracer* t = (Tracer*)h;
+  for (size_t i = 0; i < t->dm.d.size(); i++) out[i] = t->dm.d[i];
+}
+
+void hso_trc_compact(void* h, const uint8_t* keep) {
+  Tracer* t = (Tracer*)h;
+  std::vector<ImmPt> kept;
+  for (size_t i = 0; i < t->pts.size(); i++)
+    if (keep[i]) kept.push_back(t->pts[i]);
+  t->pts.swap(kept);
 }
 
 }  // extern "C"
