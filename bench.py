@@ -201,10 +201,65 @@ def bench_track(args):
     return res
 
 
+def bench_act(args):
+    """SURVEY §8f rank 1: System::activatePointsMT on a KITTI window (1232x368, 8 KFs, 2000 MapPoints, 14k traced
+    immature points over the 8 hosts).  One step = one activation: makeDistanceMap + growDistBFS, the greedy
+    selection with addIntoDistFinal, optimizeImmaturePoint of every selected point, read-back of the outputs.
+    The call leaves the immature points unchanged, so steps repeat the same activation."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from hslam_amd.scene import make_activation_scene
+    from hslam_amd.trace import ImmatureTracer, act_frames_array, act_pairs_array
+
+    s = make_activation_scene(2000, 14000, width=1232, height=368, kitti=True, seed=3)
+    g = ImmatureTracer(s.width, s.height, len(s.imm_u))
+    for f in range(s.n_frames):
+        g.set_host_image(int(s.slots[f]), s.imgs[f])
+    g.add_points(s.slots[s.imm_frame], s.imm_u, s.imm_v)
+    g.set_state(s.imm_idepth_min, s.imm_idepth_max, s.imm_quality, s.imm_status, s.imm_interval)
+    g.set_types(s.imm_type)
+    fr = act_frames_array(s.slots, s.flagged, s.KRKi1, s.Kt1)
+    pr = act_pairs_array(s.RTll, s.tTll, s.aff)
+    call = (s.K4, fr, pr, s.act_frame, s.act_u, s.act_v, s.act_idepth, s.ef_nPoints, s.currentMinActDist, s.order)
+    for _ in range(max(1, args.warmup)):
+        r = g.activatePointsMT(*call)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        r = g.activatePointsMT(*call)
+    dt = time.perf_counter() - t0
+    n_opt = int((r["action"] == 2).sum() + 0)
+    res = {
+        "metric": "point activations/sec (System::activatePointsMT, KITTI 1232x368 window, 14k immature points)",
+        "value": args.steps / dt, "unit": "activations/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": dt * 1e3 / args.steps, "higher_is_better": True, "scaling": "replicas only",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": "activatePointsMT: 8 KFs 1232x368, 2000 MapPoints, 14000 immature points",
+                   "activated": len(r["activated"]), "deleted": int((r["action"] == 1).sum()),
+                   "immature_points": len(s.imm_u)},
+        "cpu_baseline": None,
+    }
+    if not args.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        from test_act import oracle_tracer  # test infrastructure: the CPU baseline leg only
+        o = oracle_tracer(s)
+        n, tt = 0, 0.0
+        while tt < args.cpu_seconds / 2 and n < 500:
+            t1 = time.perf_counter()
+            o.activatePointsMT(s.imgs, *call)
+            tt += time.perf_counter() - t1
+            n += 1
+        res["cpu_baseline"] = {"value": n / tt, "unit": "activations/s", "cores": 1, "kind": "port",
+                               "sample": f"{n} activations of the same window (the reference's selection loop and "
+                                         "BFS are serial; optimizeImmaturePoint runs on its thread pool)"}
+        res["speedup_vs_cpu"] = res["value"] / res["cpu_baseline"]["value"]
+    g.close()
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=("ba", "trace", "track"), default="ba",
-                    help="ba = the headline metric (C4); trace = C5 traceOn; track = C2 CoarseTracker")
+    ap.add_argument("--workload", choices=("ba", "trace", "track", "act"), default="ba",
+                    help="ba = the headline metric (C4); trace = C5 traceOn; track = C2 CoarseTracker; "
+                         "act = point activation")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
@@ -213,7 +268,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
     if args.workload != "ba":
-        res = bench_trace(args) if args.workload == "trace" else bench_track(args)
+        res = {"trace": bench_trace, "track": bench_track, "act": bench_act}[args.workload](args)
         print(json.dumps(res))
         return
 

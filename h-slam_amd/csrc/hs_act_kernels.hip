@@ -4,11 +4,12 @@
 //                    projection into the newest keyframe, seed byte set to 0 with a word CAS (duplicates dropped).
 // hs_k_act_cand      the per-point part of the selection loop (Mapping.cpp:378-426): delete / skip / the
 //                    projected cell, the sub-pixel fraction and the threshold of every entry of the loop order.
-// hs_k_act_select    one workgroup: growDistBFS of the seeds, then the greedy loop — the first entry (in loop
-//                    order) whose distance passes is taken, addIntoDistFinal grows the map from it, the rest of
-//                    the chunk is re-tested.  BFS steps are frontier-parallel; a cell joins the next frontier
-//                    only through the CAS that lowered it, so the map after each step is the reference's
-//                    (its per-step result does not depend on the order the frontier is walked in).
+// hs_k_act_select    one workgroup: growDistBFS of the seeds over the whole workgroup, then the greedy loop on
+//                    wave 0 alone — per batch of 64 entries the first one (in loop order) whose distance passes
+//                    is taken, addIntoDistFinal grows the map from it, the rest of the batch is re-tested.
+//                    BFS steps are frontier-parallel; a cell joins the next frontier only through the CAS that
+//                    lowered it, so the map after each step is the reference's (its per-step result does not
+//                    depend on the order the frontier is walked in).
 //                    The map lives in LDS as bytes (0..39, 255 = the reference's 1000) when it fits.
 // hs_k_act_optimize  optimizeImmaturePoint (Src/FullSystemOptPoint.cpp:24-175) with
 //                    ImmaturePoint::linearizeResidual (Src/ImmaturePoint.cpp:389-451): one wave per point,
@@ -63,8 +64,7 @@ __global__ void __launch_bounds__(256) hs_k_act_seed(HsActSeedArgs a) {
   const int u = ptp[0] / ptp[2] + 0.5f;
   const int v = ptp[1] / ptp[2] + 0.5f;
   if (!(u > 0 && v > 0 && u < a.w1 && v < a.h1)) return;
-  const int q = u + a.w1 * v;
-  if (lower_cell(a.dist, q, 0)) a.list[atomicAdd(a.count, 1)] = q;
+  if (lower_cell(a.dist, u + a.w1 * v, 0)) a.list[atomicAdd(a.count, 1)] = u | (v << 16);
 }
 
 __global__ void __launch_bounds__(256) hs_k_act_cand(HsActCandArgs a) {
@@ -91,7 +91,7 @@ __global__ void __launch_bounds__(256) hs_k_act_cand(HsActCandArgs a) {
         const int v = ptp[1] / ptp[2] + 0.5f;
         if (u > 0 && v > 0 && u < a.w1 && v < a.h1) {
           c = HS_CAND_PENDING;
-          a.cell[j] = u + a.w1 * v;
+          a.cell[j] = u | (v << 16);
           a.frac[j] = ptp[0] - floorf((float)(ptp[0]));
           a.thr[j] = a.currentMinActDist * a.my_type[i];
         } else {
@@ -104,23 +104,81 @@ __global__ void __launch_bounds__(256) hs_k_act_cand(HsActCandArgs a) {
   a.action[i] = (c == HS_CAND_DELETE) ? HS_ACT_DELETED : HS_ACT_KEEP;
 }
 
-// growDistBFS from the n cells in *in (Src/CoarseTracker.cpp:759-857), frontier-parallel over the workgroup.
-// s_n[0] holds the frontier size on entry; lists swap every step.
-__device__ static void bfs_grow(uint8_t* map, int w1, int h1, int*& in, int*& out, int* s_n) {
+// Frontier entries are packed cells x | y << 16 (no division to find a cell's neighbours).
+__device__ __forceinline__ int xy_index(int xy, int w1) { return (xy & 0xffff) + w1 * (xy >> 16); }
+
+// One growDistBFS step's work for one frontier entry: probe the 4 / 8 neighbour words, CAS the bytes that are
+// larger than k (the probe's word is the CAS's expected value), report which neighbours this lane lowered.
+__device__ __forceinline__ unsigned expand_cell(uint8_t* map, int w1, int h1, int xy, bool valid, uint32_t k,
+                                                bool diag, int nbxy[8]) {
+  const int x = xy & 0xffff, y = xy >> 16;
+  const bool live = valid & (x != 0) & (y != 0) & (x != w1 - 1) & (y != h1 - 1);
+  const int idx = live ? x + w1 * y : w1 + 1;
+  const int nbi[8] = {idx + 1, idx - 1, idx + w1, idx - w1, idx + 1 + w1, idx - 1 + w1, idx - 1 - w1, idx + 1 - w1};
+  const int dxy[8] = {1, -1, 1 << 16, -(1 << 16), 1 + (1 << 16), -1 + (1 << 16), -1 - (1 << 16), 1 - (1 << 16)};
+  const int cnt = diag ? 8 : 4;
+  uint32_t word[8];
+#pragma unroll
+  for (int d = 0; d < 8; d++) {
+    nbxy[d] = xy + dxy[d];
+    word[d] = d < cnt ? *reinterpret_cast<const uint32_t*>(map + (nbi[d] & ~3)) : 0u;
+  }
+  // every wanted CAS is issued before any result is waited for; a CAS that lost to another lane's update of
+  // the same word is retried
+  unsigned want = 0;
+  uint32_t prev[8];
+#pragma unroll
+  for (int d = 0; d < 8; d++) {
+    const int sh = (nbi[d] & 3) * 8;
+    const bool w = live & (d < cnt) & (((word[d] >> sh) & 0xffu) > k);
+    want |= (unsigned)w << d;
+    if (w)
+      prev[d] = atomicCAS(reinterpret_cast<uint32_t*>(map + (nbi[d] & ~3)), word[d],
+                          (word[d] & ~(0xffu << sh)) | (k << sh));
+  }
+  unsigned got = 0;
+#pragma unroll
+  for (int d = 0; d < 8; d++) {
+    if (!((want >> d) & 1u)) continue;
+    const int sh = (nbi[d] & 3) * 8;
+    uint32_t old = word[d];
+    uint32_t pv = prev[d];
+    while (pv != old) {  // lost a race on this word: retry while the byte still needs lowering
+      old = pv;
+      if (((old >> sh) & 0xffu) <= k) break;
+      pv = atomicCAS(reinterpret_cast<uint32_t*>(map + (nbi[d] & ~3)), old, (old & ~(0xffu << sh)) | (k << sh));
+    }
+    got |= (unsigned)(pv == old && ((old >> sh) & 0xffu) > k) << d;
+  }
+  return got;
+}
+
+// growDistBFS from the n cells in *in (Src/CoarseTracker.cpp:759-857), frontier-parallel over the workgroup
+// (makeDistanceMap's multi-seed BFS; its frontiers can span the map).  s_n[0] holds the frontier size on entry.
+__device__ __forceinline__ void bfs_grow_wg(uint8_t* map, int w1, int h1, int*& in, int*& out, int* s_n) {
+  const int lane = threadIdx.x & 63;
   for (int k = 1; k < HS_ACT_BFS_STEPS; k++) {
     const int n = s_n[0];
     if (n == 0) break;  // the reference keeps looping over empty lists: nothing changes
     if (threadIdx.x == 0) s_n[1] = 0;
     __syncthreads();
     const bool diag = (k & 1) != 0;
-    for (int e = threadIdx.x; e < n; e += blockDim.x) {
-      const int idx = in[e];
-      const int x = idx % w1, y = idx / w1;
-      if (x == 0 || y == 0 || x == w1 - 1 || y == h1 - 1) continue;
-      const int nb[8] = {idx + 1, idx - 1, idx + w1, idx - w1, idx + 1 + w1, idx - 1 + w1, idx - 1 - w1, idx + 1 - w1};
-      const int cnt = diag ? 8 : 4;
-      for (int d = 0; d < cnt; d++)
-        if (lower_cell(map, nb[d], (uint32_t)k)) out[atomicAdd(&s_n[1], 1)] = nb[d];
+    for (int e0 = threadIdx.x & ~63; e0 < n; e0 += blockDim.x) {  // wave-uniform trip count
+      const int e = e0 + lane;
+      const int xy = e < n ? in[e] : 0;
+      int nbxy[8];
+      const unsigned got = expand_cell(map, w1, h1, xy, e < n, (uint32_t)k, diag, nbxy);
+#pragma unroll
+      for (int d = 0; d < 8; d++) {
+        const unsigned long long bm = __ballot((got >> d) & 1u);
+        if (bm == 0) continue;
+        int base = 0;
+        if (lane == (int)__builtin_ctzll(bm)) base = atomicAdd(&s_n[1], (int)__popcll(bm));
+        base = __shfl(base, (int)__builtin_ctzll(bm));
+        if ((got >> d) & 1u)
+          out[base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u))] =
+              nbxy[d];
+      }
     }
     __syncthreads();
     if (threadIdx.x == 0) s_n[0] = s_n[1];
@@ -131,61 +189,148 @@ __device__ static void bfs_grow(uint8_t* map, int w1, int h1, int*& in, int*& ou
   }
 }
 
+// addIntoDistFinal's growDistBFS from one cell, run by a single wave: the frontier of a one-seed BFS is at most
+// the ring of its step (<= 8k cells), so one wave walks it with no workgroup barrier.  Lane = frontier entry
+// (8 or 16 per pass) x neighbour direction, so a pass is one straight-line sequence: read entry, probe word, CAS,
+// append (ballot + mbcnt, no atomics).  The lists are LDS.
+__device__ __forceinline__ void bfs_grow_wave(uint8_t* map, int w1, int h1, int* in, int* out, int n,
+                                              long long* cnt) {
+  const int lane = threadIdx.x & 63;
+  // growDistBFS's neighbour order: +x, -x, +y, -y, then the diagonals (+1+w1, -1+w1, -1-w1, +1-w1)
+  const int sub8 = lane & 7, sub4 = lane & 3;
+  const int dx8 = (sub8 == 0 || sub8 == 4 || sub8 == 7) ? 1 : ((sub8 == 1 || sub8 == 5 || sub8 == 6) ? -1 : 0);
+  const int dy8 = (sub8 == 2 || sub8 == 4 || sub8 == 5) ? 1 : ((sub8 == 3 || sub8 == 6 || sub8 == 7) ? -1 : 0);
+  const int dx4 = sub4 == 0 ? 1 : (sub4 == 1 ? -1 : 0);
+  const int dy4 = sub4 == 2 ? 1 : (sub4 == 3 ? -1 : 0);
+  for (int k = 1; k < HS_ACT_BFS_STEPS && n > 0; k++) {
+    // odd steps: 8 entries x 8 directions per pass; even steps: 16 entries x 4 directions
+    const bool diag = (k & 1) != 0;
+    const int slot = diag ? lane >> 3 : lane >> 2;
+    const int per = diag ? 8 : 16;
+    const int dx = diag ? dx8 : dx4, dy = diag ? dy8 : dy4;
+    const int dxy = dx + dy * 65536;
+    int m = 0;
+    cnt[0]++;
+    for (int e0 = 0; e0 < n; e0 += per) {
+      cnt[1]++;
+      const int e = e0 + slot;
+      const bool valid = e < n;
+      const int xy = in[valid ? e : 0];
+      const int x = xy & 0xffff, y = xy >> 16;
+      const bool live = valid & (x != 0) & (y != 0) & (x != w1 - 1) & (y != h1 - 1);
+      const int q = live ? (x + dx) + (y + dy) * w1 : 0;
+      const int sh = (q & 3) * 8;
+      uint32_t* wp = reinterpret_cast<uint32_t*>(map + (q & ~3));
+      uint32_t old = *wp;
+      bool want = live & (((old >> sh) & 0xffu) > (uint32_t)k);
+      bool got = false;
+      while (want) {
+        const uint32_t pv = atomicCAS(wp, old, (old & ~(0xffu << sh)) | ((uint32_t)k << sh));
+        got = pv == old;
+        old = pv;
+        want = !got & (((old >> sh) & 0xffu) > (uint32_t)k);
+      }
+      const unsigned long long bm = __ballot(got);
+      if (got)
+        out[m + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u))] =
+            xy + dxy;
+      m += (int)__popcll(bm);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    n = m < HS_ACT_WAVE_LIST ? m : HS_ACT_WAVE_LIST;
+    int* t = in;
+    in = out;
+    out = t;
+  }
+}
+
+// makeDistanceMap's BFS (whole workgroup), then the selection loop (wave 0).  Inlined once per map location so
+// the LDS instance compiles to ds_* instructions.
+__device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* map, int* s_n, int* wl0, int* wl1) {
+  int* in = a.list_a;
+  int* out = a.list_b;
+  bfs_grow_wg(map, a.w1, a.h1, in, out, s_n);
+  if (threadIdx.x >= 64) return 0;  // the greedy loop is sequential: wave 0 alone
+  if (a.prof && threadIdx.x == 0) {
+    a.prof[1] = wall_clock64();
+    a.prof[6] = clock64();
+  }
+  const int lane = threadIdx.x;
+  int nt = 0;
+  long long cnt[3] = {0, 0, 0};
+  // candidate batches of 64, the next batch's loads in flight while the current one is processed
+  int j = lane;
+  bool npend = j < a.m && a.cand[j] == HS_CAND_PENDING;
+  int ncell = npend ? a.cell[j] : 0;
+  int npt = npend ? (a.order ? a.order[j] : j) : 0;
+  float nfrac = npend ? a.frac[j] : 0.f, nthr = npend ? a.thr[j] : 0.f;
+  for (int base = 0; base < a.m; base += 64) {
+    bool pend = npend;
+    const int cell = ncell;
+    const int cidx = xy_index(cell, a.w1);
+    const float frac = nfrac, thr = nthr;
+    const int pt = npt;
+    j = base + 64 + lane;
+    npend = j < a.m && a.cand[j] == HS_CAND_PENDING;
+    ncell = npend ? a.cell[j] : 0;
+    npt = npend ? (a.order ? a.order[j] : j) : 0;
+    nfrac = npend ? a.frac[j] : 0.f;
+    nthr = npend ? a.thr[j] : 0.f;
+    for (;;) {
+      // dist = fwdWarpedIDDistFinal[u + w1 * v] + (ptp[0] - floorf(ptp[0])) >= currentMinActDist * my_type
+      const bool acc = pend && (decode(map[cidx]) + frac >= thr);
+      const unsigned long long bm = __ballot(acc);
+      if (bm == 0) break;  // every remaining entry of the batch fails: they stay immature
+      const int first = (int)__builtin_ctzll(bm);
+      if (lane <= first) pend = false;
+      if (lane == first) {
+        a.toopt[nt] = pt;
+        lower_cell(map, cidx, 0);  // addIntoDistFinal: the cell becomes 0 even when it already was
+        wl0[0] = cell;
+      }
+      nt++;
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      const long long c0 = a.prof ? wall_clock64() : 0;
+      bfs_grow_wave(map, a.w1, a.h1, wl0, wl1, 1, cnt);
+      if (a.prof) cnt[2] += wall_clock64() - c0;
+    }
+  }
+  if (a.prof && lane == 0) {
+    a.prof[3] = cnt[0];
+    a.prof[4] = cnt[1];
+    a.prof[5] = cnt[2];
+  }
+  return nt;
+}
+
 __global__ void __launch_bounds__(1024) hs_k_act_select(HsActSelectArgs a) {
   extern __shared__ uint32_t s_map32[];
   __shared__ int s_n[2];
-  __shared__ int s_first;
-  __shared__ int s_nt;
-  const int wh1 = a.w1 * a.h1;
-  const int words = (wh1 + 3) / 4;
-  uint8_t* map = reinterpret_cast<uint8_t*>(a.dist);
+  __shared__ int s_wl[2][HS_ACT_WAVE_LIST];
+  const int words = (a.w1 * a.h1 + 3) / 4;
+  if (a.prof && threadIdx.x == 0) a.prof[0] = wall_clock64();
+  if (threadIdx.x == 0) s_n[0] = *a.seed_count;
+  int nt;
   if (a.lds_map) {
     const uint32_t* g = reinterpret_cast<const uint32_t*>(a.dist);
     for (int w = threadIdx.x; w < words; w += blockDim.x) s_map32[w] = g[w];
-    map = reinterpret_cast<uint8_t*>(s_map32);
-  }
-  if (threadIdx.x == 0) {
-    s_n[0] = *a.seed_count;
-    s_nt = 0;
-  }
-  __syncthreads();
-  int* in = a.list_a;
-  int* out = a.list_b;
-  bfs_grow(map, a.w1, a.h1, in, out, s_n);  // makeDistanceMap's growDistBFS(numItems)
-
-  for (int base = 0; base < a.m; base += blockDim.x) {
-    const int j = base + threadIdx.x;
-    bool pend = j < a.m && a.cand[j] == HS_CAND_PENDING;
-    const int cell = pend ? a.cell[j] : 0;
-    const float frac = pend ? a.frac[j] : 0.f;
-    const float thr = pend ? a.thr[j] : 0.f;
-    for (;;) {
-      if (threadIdx.x == 0) s_first = 0x7fffffff;
-      __syncthreads();
-      // dist = fwdWarpedIDDistFinal[u + w1 * v] + (ptp[0] - floorf(ptp[0])) >= currentMinActDist * my_type
-      const bool acc = pend && (decode(map[cell]) + frac >= thr);
-      if (acc) atomicMin(&s_first, (int)threadIdx.x);
-      __syncthreads();
-      const int first = s_first;
-      if (first == 0x7fffffff) break;  // every remaining entry of the chunk fails: they stay immature
-      if ((int)threadIdx.x <= first) pend = false;
-      if ((int)threadIdx.x == first) {
-        a.toopt[s_nt] = a.order ? a.order[j] : j;
-        s_nt = s_nt + 1;
-        lower_cell(map, cell, 0);  // addIntoDistFinal: the cell becomes 0 even when it already was
-        in[0] = cell;
-        s_n[0] = 1;
-      }
-      __syncthreads();
-      bfs_grow(map, a.w1, a.h1, in, out, s_n);
-    }
     __syncthreads();
+    nt = select_body(a, reinterpret_cast<uint8_t*>(s_map32), s_n, s_wl[0], s_wl[1]);
+    if (threadIdx.x >= 64) return;
+    uint32_t* go = reinterpret_cast<uint32_t*>(a.dist);
+    for (int w = threadIdx.x; w < words; w += 64) go[w] = s_map32[w];
+  } else {
+    __syncthreads();
+    nt = select_body(a, a.dist, s_n, s_wl[0], s_wl[1]);
+    if (threadIdx.x >= 64) return;
   }
-  if (a.lds_map) {
-    uint32_t* g = reinterpret_cast<uint32_t*>(a.dist);
-    for (int w = threadIdx.x; w < words; w += blockDim.x) g[w] = s_map32[w];
+  if (threadIdx.x == 0) *a.n_toopt = nt;
+  if (a.prof && threadIdx.x == 0) {
+    a.prof[2] = wall_clock64();
+    a.prof[7] = clock64();
   }
-  if (threadIdx.x == 0) *a.n_toopt = s_nt;
 }
 
 __global__ void __launch_bounds__(256) hs_k_act_optimize(HsActOptArgs a) {

@@ -4,6 +4,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -14,7 +16,7 @@
 #include "hs_pyr_kernels.h"
 
 #define HS_MAXF_ACT 8                        // activation window (nF <= 8 keyframes)
-#define HS_ACT_LDS_MAP_MAX (156 * 1024)     // level-1 distance map in LDS up to this size
+#define HS_ACT_LDS_MAP_MAX (140 * 1024)     // level-1 distance map in LDS up to this size (+16 KB of lists)
 
 namespace hs {
 extern thread_local std::string g_err;
@@ -539,6 +541,10 @@ int hs_tracer_activate(hs_tracer* t, const float K4[4], int nF, const hs_act_fra
   se.seed_count = t->d_act_cnt;
   se.toopt = t->d_toopt;
   se.n_toopt = t->d_act_cnt + 1;
+  static const bool prof_on = getenv("HS_ACT_PROF") != nullptr;
+  long long* d_prof = nullptr;
+  if (prof_on) TR_HIP(hipMalloc((void**)&d_prof, sizeof(long long) * 8));
+  se.prof = d_prof;
   const size_t lds = se.lds_map ? map_bytes : 0;
   if (lds > 65536)
     TR_HIP(hipFuncSetAttribute((const void*)hs_k_act_select, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -548,6 +554,15 @@ int hs_tracer_activate(hs_tracer* t, const float K4[4], int nF, const hs_act_fra
   TR_HIP(hipMemcpyAsync(cnt, t->d_act_cnt, sizeof(cnt), hipMemcpyDeviceToHost, s));
   TR_HIP(hipStreamSynchronize(s));
   const int n_toopt = cnt[1];
+  if (d_prof) {
+    long long pr[8];
+    TR_HIP(hipMemcpy(pr, d_prof, sizeof(pr), hipMemcpyDeviceToHost));
+    TR_HIP(hipFree(d_prof));
+    fprintf(stderr, "hs act prof: seed BFS %.1f us, greedy %.1f us (wall_clock64 @100 MHz), %d selected; "
+            "wave BFS: %lld steps, %lld passes, %.1f us; core clock %.0f MHz\n",
+            (pr[1] - pr[0]) * 1e-2, (pr[2] - pr[1]) * 1e-2, n_toopt, pr[3], pr[4], pr[5] * 1e-2,
+            (double)(pr[7] - pr[6]) / ((pr[2] - pr[1]) * 1e-2));
+  }
   if (n_toopt > 0) {
     HsActOptArgs oa;
     oa.n = n_toopt;

@@ -54,7 +54,8 @@ __global__ void hs_k_trace_on(HsTraceArgs a);
 __global__ void hs_k_trace_count(int n, const uint8_t* status, const int* steps, int* out);
 
 // ---- point activation (System::activatePointsMT), hs_act_kernels.hip ----------------------------------------
-#define HS_ACT_BFS_STEPS 40  // growDistBFS: k = 1 .. 39
+#define HS_ACT_BFS_STEPS 40    // growDistBFS: k = 1 .. 39
+#define HS_ACT_WAVE_LIST 2048  // one-seed BFS frontier capacity (a step-k ring holds <= 8k cells)
 
 // candidate states of the selection loop (per entry of the loop order)
 enum { HS_CAND_SKIP = 0, HS_CAND_DELETE = 1, HS_CAND_PENDING = 2 };
@@ -68,7 +69,7 @@ struct HsActSeedArgs {
   const float* v;
   const float* idepth;
   uint8_t* dist;   // [w1*h1] distance bytes (255 = 1000, untouched)
-  int* list;       // [w1*h1] seed cells (deduplicated)
+  int* list;       // [w1*h1] seed cells x | y << 16 (deduplicated)
   int* count;
 };
 
@@ -89,7 +90,7 @@ struct HsActCandArgs {
   const float* my_type;
   const uint8_t* status;
   uint8_t* cand;     // [m] HS_CAND_*
-  int* cell;         // [m] u + w1 * v of a pending entry
+  int* cell;         // [m] projected cell u | v << 16 of a pending entry
   float* frac;       // [m] ptp[0] - floorf(ptp[0])
   float* thr;        // [m] currentMinActDist * my_type
   uint8_t* action;   // [n points] HS_ACT_*
@@ -109,6 +110,7 @@ struct HsActSelectArgs {
   const int* seed_count;
   int* toopt;                // [m] points to optimize, in order
   int* n_toopt;
+  long long* prof;           // nullable: wall_clock64 at entry, after the seed BFS, at exit (HS_ACT_PROF=1)
 };
 
 // optimizeImmaturePoint, one wave per point to optimize

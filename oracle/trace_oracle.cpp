@@ -307,9 +307,13 @@ struct DistMap {
   int w1 = 0, h1 = 0;
   std::vector<float> d;
   std::vector<int> l1, l2;  // bfsList1 / bfsList2 as packed (x, y) pairs
-  void grow(int bfsNum) {  // growDistBFS, :759-857 (k even: 4-neighbourhood, k odd: 8-neighbourhood)
+  long long st_grows = 0, st_steps = 0, st_cells = 0;  // statistics: BFS calls, non-empty steps, frontier cells
+  void grow(int bfsNum) {
+    st_grows++;  // growDistBFS, :759-857 (k even: 4-neighbourhood, k odd: 8-neighbourhood)
     for (int k = 1; k < 40; k++) {
       int bfsNum2 = bfsNum;
+      if (bfsNum2) st_steps++;
+      st_cells += bfsNum2;
       std::swap(l1, l2);
       bfsNum = 0;
       for (int i = 0; i < bfsNum2; i++) {
@@ -678,6 +682,13 @@ int hso_trc_activate(void* h, const float K4[4], int nF, const float* const* fra
 void hso_trc_distance_map(void* h, float* out) {
   Tracer* t = (Tracer*)h;
   for (size_t i = 0; i < t->dm.d.size(); i++) out[i] = t->dm.d[i];
+}
+
+void hso_trc_bfs_stats(void* h, long long* out3) {
+  Tracer* t = (Tracer*)h;
+  out3[0] = t->dm.st_grows;
+  out3[1] = t->dm.st_steps;
+  out3[2] = t->dm.st_cells;
 }
 
 void hso_trc_compact(void* h, const uint8_t* keep) {

@@ -73,3 +73,23 @@ def test_ctypes_structs_match_c_layout(tmp_path):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_ffi
     assert ctypes.sizeof(oracle_ffi.hs_params) == sizes[0]
+
+
+def test_built_libraries_are_current():
+    """The in-tree .so files (they travel to the GPU box prebuilt) are newer than every source they are built from:
+    a stale library would make GPU parity compare two stale builds."""
+    def newest(paths):
+        return max(os.path.getmtime(p) for p in paths)
+
+    def files(d, exts):
+        return [os.path.join(d, f) for f in os.listdir(d) if f.endswith(exts)]
+
+    csrc = os.path.join(ROOT, "h-slam_amd", "csrc")
+    inc = os.path.join(ROOT, "include")
+    ora = os.path.join(ROOT, "oracle")
+    lib_src = files(csrc, (".hip", ".cpp", ".h")) + files(inc, (".h",)) + [os.path.join(csrc, "Makefile")]
+    ora_src = files(ora, (".cpp", ".h")) + files(inc, (".h",)) + [os.path.join(ora, "Makefile")]
+    assert os.path.getmtime(LIB) >= newest(lib_src), "libhslam_amd.so is stale: make -C h-slam_amd/csrc"
+    for so in ("liboracle.so", "liboracle_fast.so"):
+        p = os.path.join(ora, "_build", so)
+        assert os.path.getmtime(p) >= newest(ora_src), f"{so} is stale: make -C oracle"
