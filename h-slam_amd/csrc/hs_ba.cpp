@@ -492,6 +492,10 @@ int hs_params_default(hs_params* p) {
   p->minTraceQuality = 3;
   p->minIdepthH_act = 100;
   p->GNItsOnPointActivation = 3;
+  p->minGradHistCut = 0.5f;
+  p->minGradHistAdd = 7;
+  p->gradDownweightPerLevel = 0.75f;
+  p->selectDirectionDistribution = 1;
   return HS_OK;
 }
 

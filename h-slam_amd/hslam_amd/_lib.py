@@ -49,7 +49,8 @@ class hs_params(C.Structure):
         ("minTraceTestRadius", C.c_int), ("trace_GNIterations", C.c_int),
         ("idepthFixPriorMargFac", C.c_float), ("margWeightFac", C.c_float),
         ("desiredPointDensity", C.c_float), ("minTraceQuality", C.c_float), ("minIdepthH_act", C.c_float),
-        ("GNItsOnPointActivation", C.c_int)]
+        ("GNItsOnPointActivation", C.c_int), ("minGradHistCut", C.c_float), ("minGradHistAdd", C.c_float),
+        ("gradDownweightPerLevel", C.c_float), ("selectDirectionDistribution", C.c_int)]
 
 
 # exported symbols of include/hs_ba.h (argument types)
@@ -106,6 +107,14 @@ SIGNATURES = {
     "hs_tracer_get_points": ([VP] * 12, I),
     "hs_tracer_reinit": ([VP], I),
     "hs_tracer_last_stats": ([VP, VP, VP], I),
+    # include/hs_select.h
+    "hs_selector_create": ([VP, VP, I, I, I], I),
+    "hs_selector_destroy": ([VP], None),
+    "hs_selector_make_maps": ([VP, I, VP, VP, VP, VP, C.c_float, I, C.c_float, VP, VP], I),
+    "hs_selector_make_maps_raw": ([VP, I, VP, C.c_float, I, C.c_float, VP, VP], I),
+    "hs_selector_get_potential": ([VP, VP], I),
+    "hs_selector_set_potential": ([VP, I], I),
+    "hs_selector_last_stats": ([VP, VP, VP], I),
 }
 
 _lib = None

@@ -706,3 +706,32 @@ def make_activation_scene(n_active: int = 1500, n_immature: int = 3000, n_frames
         imm_interval=rng.uniform(0, 12, n).astype(np.float32),
         imm_type=rng.choice([1.0, 2.0, 4.0], n, p=[0.6, 0.25, 0.15]).astype(np.float32), order=order,
         ef_nPoints=n_active, currentMinActDist=currentMinActDist)
+
+
+def make_select_frames(n_frames: int = 3, width: int = 640, height: int = 480, seed: int = SEED,
+                       quantize: bool = False, flat_frac: float = 0.0, contrast_ramp: bool = False):
+    """Raw level-0 frames for PixelSelector::makeMaps (Src/PixelSelector.cpp:118-262): the textured planes seen from
+    a camera drifting along x.  quantize=True rounds to 8-bit values, as a camera image, so gradients are multiples
+    of 0.5 and axis-aligned / diagonal ones score exactly 0 against some directions (the ambiguous-slot path of the
+    device select).  flat_frac blanks that fraction of the image rows (textureless regions); contrast_ramp scales the
+    texture contrast from 3% at the left edge to 100% at the right, so cells span the regimes where select takes a
+    level-0, a level-1 (2pot) or a level-2 (4pot) pixel."""
+    rng = np.random.default_rng(seed + 29)
+    K = (np.array([[718.856, 0, 615.5], [0, 718.856, 183.5], [0, 0, 1.0]]) if width >= 1000
+         else np.array([[0.4 * width, 0, width / 2 - 0.5], [0, 0.53 * height, height / 2 - 0.5], [0, 0, 1.0]]))
+    f = K[0, 0]
+    planes = [make_plane(rng, 5.0, f), make_plane(rng, 3.0, f, xmax=-0.25), make_plane(rng, 2.0, f, xmin=0.55, ymax=0.15)]
+    out = []
+    for i in range(n_frames):
+        ax = rng.normal(size=3)
+        ax /= np.linalg.norm(ax)
+        R_c2w = rodrigues(ax * math.radians(rng.uniform(0, 1.0)))
+        img, _ = render(planes, K, R_c2w, np.array([0.05 * i, 0.0, 0.0]), width, height)
+        if contrast_ramp:
+            img = (128.0 + (img - 128.0) * np.linspace(0.03, 1.0, width)[None, :] ** 2).astype(np.float32)
+        if flat_frac > 0:
+            img[: int(flat_frac * height)] = 128.0
+        if quantize:
+            img = np.round(img).astype(np.float32)
+        out.append(img)
+    return out

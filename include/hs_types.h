@@ -118,6 +118,11 @@ typedef struct hs_params {
   float minTraceQuality;         /* 3      :86 */
   float minIdepthH_act;          /* 100    :118 */
   int GNItsOnPointActivation;    /* 3      :54 */
+  /* PixelSelector (Src/PixelSelector.cpp:54-418) */
+  float minGradHistCut;          /* 0.5    :29 */
+  float minGradHistAdd;          /* 7      :30 */
+  float gradDownweightPerLevel;  /* 0.75   :31 */
+  int selectDirectionDistribution; /* 1    :32 */
 } hs_params;
 
 #ifdef __cplusplus

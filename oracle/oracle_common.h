@@ -155,6 +155,10 @@ inline void params_default(hs_params* p) {
   p->minTraceQuality = 3;
   p->minIdepthH_act = 100;
   p->GNItsOnPointActivation = 3;
+  p->minGradHistCut = 0.5f;
+  p->minGradHistAdd = 7;
+  p->gradDownweightPerLevel = 0.75f;
+  p->selectDirectionDistribution = 1;
 }
 
 }  // namespace hso

@@ -48,7 +48,8 @@ class hs_params(C.Structure):
         ("minTraceTestRadius", C.c_int), ("trace_GNIterations", C.c_int),
         ("idepthFixPriorMargFac", C.c_float), ("margWeightFac", C.c_float),
         ("desiredPointDensity", C.c_float), ("minTraceQuality", C.c_float), ("minIdepthH_act", C.c_float),
-        ("GNItsOnPointActivation", C.c_int)]
+        ("GNItsOnPointActivation", C.c_int), ("minGradHistCut", C.c_float), ("minGradHistAdd", C.c_float),
+        ("gradDownweightPerLevel", C.c_float), ("selectDirectionDistribution", C.c_int)]
 
 
 def build(quiet=True):
@@ -124,6 +125,16 @@ def load(fast=False):
     lib.hso_trc_compact.argtypes = [vp, vp]
     lib.hso_trc_trace.argtypes = [vp] * 4
     lib.hso_trc_get.argtypes = [vp] * 11
+    lib.hso_sel_create.restype = vp
+    lib.hso_sel_create.argtypes = [vp, C.c_int, C.c_int]
+    lib.hso_sel_destroy.argtypes = [vp]
+    lib.hso_sel_make_maps.argtypes = [vp, C.c_int, vp, vp, vp, vp, C.c_float, C.c_int, C.c_float, vp]
+    lib.hso_sel_make_maps.restype = C.c_int
+    lib.hso_sel_potential.argtypes = [vp]
+    lib.hso_sel_potential.restype = C.c_int
+    lib.hso_sel_set_potential.argtypes = [vp, C.c_int]
+    lib.hso_sel_random_pattern.argtypes = [vp, vp]
+    lib.hso_sel_ths.argtypes = [vp, vp, vp]
     _LIBS[name] = lib
     return lib
 
@@ -509,3 +520,45 @@ def dir_pyramid(img, n_levels):
         o3 += h * w * 3
         o1 += h * w
     return pyr, grads
+
+
+class PixelSelector:
+    """PixelSelector (Src/PixelSelector.cpp:14-418) restated (oracle/sel_oracle.cpp)."""
+
+    def __init__(self, width, height, params=None, fast=False):
+        self.lib = load(fast)
+        self.W, self.H = width, height
+        self.h = self.lib.hso_sel_create(C.byref(params) if params is not None else None, width, height)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.lib.hso_sel_destroy(self.h)
+            self.h = None
+
+    def makeMaps(self, frame_id, dirpyr0, absg, density, recursionsLeft=1, thFactor=1.0):
+        """-> (selection map (H, W) float32, numHaveSub).  dirpyr0: (H, W, 3); absg: levels 0..2."""
+        d = np.ascontiguousarray(dirpyr0, np.float32)
+        g = [np.ascontiguousarray(x, np.float32) for x in absg[:3]]
+        out = np.zeros((self.H, self.W), np.float32)
+        n = self.lib.hso_sel_make_maps(self.h, frame_id, _p(d), _p(g[0]), _p(g[1]), _p(g[2]), density,
+                                       recursionsLeft, thFactor, _p(out))
+        return out, n
+
+    @property
+    def currentPotential(self):
+        return self.lib.hso_sel_potential(self.h)
+
+    @currentPotential.setter
+    def currentPotential(self, p):
+        self.lib.hso_sel_set_potential(self.h, int(p))
+
+    def randomPattern(self):
+        out = np.zeros(self.W * self.H, np.uint8)
+        self.lib.hso_sel_random_pattern(self.h, _p(out))
+        return out
+
+    def ths(self):
+        n = (self.W // 32) * (self.H // 32)
+        a, b = np.zeros(n, np.float32), np.zeros(n, np.float32)
+        self.lib.hso_sel_ths(self.h, _p(a), _p(b))
+        return a.reshape(self.H // 32, self.W // 32), b.reshape(self.H // 32, self.W // 32)
