@@ -1118,6 +1118,20 @@ int hs_ba_get_timings(hs_ctx* c, double* out6) {
   return HS_OK;
 }
 
+int hs_ba_time_linearize(hs_ctx* c, int reps, double* avg_ms) {
+  if (!c || !avg_ms || reps < 1) return fail(HS_ERR_INVALID, "bad args");
+  if (c->nF == 0) return fail(HS_ERR_STATE, "no window");
+  HS_HIP(hipSetDevice(c->device));
+  HS_HIP(hipEventRecord(c->ev[0], c->stream));
+  for (int k = 0; k < reps; k++) HS_TRY(launch_linearize(c, 0));
+  HS_HIP(hipEventRecord(c->ev[1], c->stream));
+  HS_HIP(hipEventSynchronize(c->ev[1]));
+  float ms = 0;
+  HS_HIP(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+  *avg_ms = ms / reps;
+  return HS_OK;
+}
+
 int hs_comm_get_unique_id(char* id128) {
   if (!id128) return fail(HS_ERR_INVALID, "null");
   ncclUniqueId id;

@@ -160,6 +160,12 @@ class BAWindow:
         return dict(linearize_ms=t[0], acc_stitch_ms=t[1], solve_ms=t[2], timed_iters=int(t[3]), wall_ms=t[4],
                     iters=int(t[5]))
 
+    def time_linearize(self, reps: int) -> float:
+        """Average ms of `reps` back-to-back linearize launches (one HIP event pair)."""
+        t = np.zeros(1)
+        check(self.lib.hs_ba_time_linearize(self.h, int(reps), ptr(t)))
+        return float(t[0])
+
     # --------------------------------------------------------------- multi-GPU
     @staticmethod
     def comm_unique_id() -> bytes:

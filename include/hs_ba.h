@@ -108,6 +108,11 @@ int hs_ba_marginalize_frame(hs_ctx* ctx, int frame, double* HM_out, double* bM_o
    Env HS_EVENT_TIMING: 1 (default) times the linearize kernel only, 2 every phase, 0 none. */
 int hs_ba_get_timings(hs_ctx* ctx, double* out6);
 
+/* Roofline timing: reps back-to-back launches of the linearize kernel (no fused point step) on the
+   context's stream between one HIP event pair; avg_ms = elapsed / reps.  Leaves the residual states of a
+   re-linearization at the current point depths.  Measurement only (no reference counterpart). */
+int hs_ba_time_linearize(hs_ctx* ctx, int reps, double* avg_ms);
+
 /* multi-GPU (point sharding): 128-byte RCCL unique id from rank 0, broadcast by the caller.
    hs_comm_init must be called before hs_ba_set_window.  Each rank loads its own point shard (same frames);
    per GN iteration the stitched H/b/energy are all-reduced and the newest-frame energies all-gathered. */
