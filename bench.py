@@ -255,11 +255,60 @@ def bench_act(args):
     return res
 
 
+def bench_refine(args):
+    """SURVEY §8f rank 4: the initializer's DirectRefinement::Refine (level-0 LM over calcResAndGS, doStep,
+    applyStep, calcEC, optReg) on a 640x480 two-frame pair with 2000 ORB-like keypoints (85% triangulated).
+    One step = one Refine from the initializer's pose: the point set-up upload (the ctor) is outside the timed
+    call, the kernel, its read-back of the pose and the _videpth write-back are inside."""
+    from hslam_amd.refine import DirectRefinement
+    from hslam_amd.scene import make_refine_scene
+
+    s = make_refine_scene(2000)
+    g = DirectRefinement(s)
+    for _ in range(max(1, args.warmup)):
+        g.set_points(s.u, s.v, s.tri, s.z)
+        T, vid, good, it, sn = g.Refine(s.T_init)
+    dt, dev = 0.0, 0.0
+    for _ in range(args.steps):
+        g.set_points(s.u, s.v, s.tri, s.z)
+        t0 = time.perf_counter()
+        T, vid, good, it, sn = g.Refine(s.T_init)
+        dt += time.perf_counter() - t0
+        dev += g.last_ms()
+    passes = it + 1  # calcResAndGS evaluations per Refine
+    res = {
+        "metric": "refinements/sec (DirectRefinement::Refine, 640x480 pair, 2000 keypoints)",
+        "value": args.steps / dt, "unit": "refinements/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": dt * 1e3 / args.steps, "higher_is_better": True, "scaling": "replicas only",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": "DirectRefinement::Refine: 640x480, 2000 keypoints, 85% triangulated",
+                   "lm_iterations": it, "snapped": sn, "good_points": int(good.sum()),
+                   "device_ms_per_refine": dev / args.steps, "calcResAndGS_passes": passes,
+                   "device_us_per_pass": dev / args.steps * 1e3 / passes},
+        "cpu_baseline": None,
+    }
+    if not args.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        from oracle_ffi import OracleRefiner  # test infrastructure: the CPU baseline leg only
+        n, tt = 0, 0.0
+        while tt < args.cpu_seconds / 2 and n < 2000:
+            o = OracleRefiner(s, fast=True)
+            t1 = time.perf_counter()
+            o.refine(s.T_init)
+            tt += time.perf_counter() - t1
+            n += 1
+        res["cpu_baseline"] = {"value": n / tt, "unit": "refinements/s", "cores": 1, "kind": "port",
+                               "sample": f"{n} Refine calls on the same pair (the reference's Refine is serial)"}
+        res["speedup_vs_cpu"] = res["value"] / res["cpu_baseline"]["value"]
+    g.close()
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=("ba", "trace", "track", "act"), default="ba",
+    ap.add_argument("--workload", choices=("ba", "trace", "track", "act", "refine"), default="ba",
                     help="ba = the headline metric (C4); trace = C5 traceOn; track = C2 CoarseTracker; "
-                         "act = point activation")
+                         "act = point activation; refine = initializer DirectRefinement")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
@@ -268,7 +317,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
     if args.workload != "ba":
-        res = {"trace": bench_trace, "track": bench_track, "act": bench_act}[args.workload](args)
+        res = {"trace": bench_trace, "track": bench_track, "act": bench_act, "refine": bench_refine}[args.workload](args)
         print(json.dumps(res))
         return
 

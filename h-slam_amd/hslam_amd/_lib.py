@@ -116,6 +116,16 @@ SIGNATURES = {
     "hs_selector_get_potential": ([VP, VP], I),
     "hs_selector_set_potential": ([VP, I], I),
     "hs_selector_last_stats": ([VP, VP, VP], I),
+    # include/hs_refine.h
+    "hs_refiner_create": ([VP, I, I, I, VP], I),
+    "hs_refiner_destroy": ([VP], None),
+    "hs_refiner_set_frames": ([VP, VP, VP, C.c_float, C.c_float], I),
+    "hs_refiner_set_points": ([VP, I, VP, VP, VP, VP], I),
+    "hs_refiner_refine": ([VP, VP, VP, VP, VP, VP], I),
+    "hs_refiner_calc_res": ([VP, VP, VP, VP, VP, VP, VP, VP], I),
+    "hs_refiner_get_points": ([VP, VP, VP, VP], I),
+    "hs_refiner_get_log": ([VP, I, VP], I),
+    "hs_refiner_last_ms": ([VP, VP], I),
 }
 
 _lib = None

@@ -735,3 +735,54 @@ def make_select_frames(n_frames: int = 3, width: int = 640, height: int = 480, s
             img = np.round(img).astype(np.float32)
         out.append(img)
     return out
+
+
+# ----------------------------------------------------------------- initializer refinement (DirectRefinement)
+@dataclass
+class RefineScene:
+    width: int
+    height: int
+    K: np.ndarray
+    img1: np.ndarray      # FirstFrame DirPyr[0], H*W*3
+    img2: np.ndarray      # SecondFrame DirPyr[0]
+    expo1: float
+    expo2: float
+    u: np.ndarray         # mvKeys[i].pt (sub-pixel)
+    v: np.ndarray
+    tri: np.ndarray       # Triangulated[i]
+    z: np.ndarray         # Pts3D[i].z (noisy where triangulated, 1 elsewhere)
+    T_true: np.ndarray    # refToNew (first -> second), SE3 data
+    T_init: np.ndarray    # the initializer's pose handed to DirectRefinement
+
+    @property
+    def n_points(self):
+        return len(self.u)
+
+    @property
+    def K4(self):
+        return np.array([self.K[0, 0], self.K[1, 1], self.K[0, 2], self.K[1, 2]], np.float64)
+
+
+def make_refine_scene(n_points: int = 2000, width: int = 640, height: int = 480, K=None, seed: int = SEED,
+                      trans: float = 0.15, rot_deg: float = 2.0, tri_frac: float = 0.85, z_noise: float = 0.03,
+                      pose_rot_deg: float = 0.3, pose_trans_frac: float = 0.1, exposures=(1.0, 1.0)) -> RefineScene:
+    """Two frames of the textured-plane world with a wide baseline (the monocular initializer's pair), ORB-like
+    sub-pixel keypoints in the first frame, Triangulated for tri_frac of them with Pts3D.z carrying z_noise
+    relative noise, and an initial refToNew perturbed from the truth (pose_rot_deg, pose_trans_frac of |t|)."""
+    ts = make_track_scene(n_points=n_points, width=width, height=height, K=K, seed=seed, trans=trans,
+                          rot_deg=rot_deg, a=0.0, b=0.0, idepth_noise=0.0, dup_frac=0.0, n_levels=1)
+    rng = np.random.default_rng(seed + 11)
+    n = len(ts.pt_u)
+    tri = (rng.random(n) < tri_frac).astype(np.uint8)
+    z = (1.0 / ts.pt_idepth.astype(np.float64)) * (1.0 + z_noise * rng.normal(size=n))
+    z = np.where(tri == 1, z, 1.0).astype(np.float32)
+    R_true, t_true = quat_to_rot(ts.T_true[:4]), ts.T_true[4:]
+    ax = rng.normal(size=3)
+    ax /= np.linalg.norm(ax)
+    dR = rodrigues(ax * math.radians(pose_rot_deg))
+    dt = rng.normal(size=3)
+    dt *= pose_trans_frac * np.linalg.norm(t_true) / np.linalg.norm(dt)
+    T_init = se3_data(dR @ R_true, t_true + dt)
+    return RefineScene(width=width, height=height, K=ts.K, img1=ts.ref_pyr[0], img2=ts.new_pyr[0],
+                       expo1=float(exposures[0]), expo2=float(exposures[1]), u=ts.pt_u, v=ts.pt_v, tri=tri, z=z,
+                       T_true=ts.T_true, T_init=T_init)

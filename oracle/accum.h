@@ -5,7 +5,8 @@
  *   AccumulatorX<i>      :177-237   A += w*L
  *   Accumulator11        :91-172    4-lane SSE partial sums
  *   AccumulatorApprox    :595-972   13x13 [calib4|xi6|a|b|r], update/TopRight/BotRight
- *   Accumulator9         :982-1345  4-lane SSE 9x9 (45 entries) for CoarseTracker
+ *   Accumulator9         :982-1345  4-lane SSE 9x9 (45 entries) for CoarseTracker (updateSSE_eighted) and
+ *                                   DirectRefinement (updateSSE :1025-1087, updateSingleWeighted :1242-1331)
  * shiftUp: flush to the next level when the level holds > 1000 updates.
  * The 4-lane SSE adds are restated lane by lane (same rounding as _mm_add_ps).
  */
@@ -56,6 +57,12 @@ struct AccX {
   void finish() { shiftUp(true); num = (size_t)(numIn1 + numIn1k + numIn1m); }
   void update(const float* L, float w) {
     for (int r = 0; r < I; r++) A[r] += w * L[r];
+    numIn1++;
+    shiftUp(false);
+  }
+  // updateNoWeight (Include/MatrixAccumulators.h:210-215)
+  void updateNoWeight(const float* L) {
+    for (int r = 0; r < I; r++) A[r] += L[r];
     numIn1++;
     shiftUp(false);
   }
@@ -188,6 +195,37 @@ struct Acc9 {
     numIn1++;
     shiftUp(false);
   }
+  // updateSSE (Include/MatrixAccumulators.h:1025-1087): J[k][lane], unweighted
+  void updateSSE(const float J[9][4]) {
+    float* pt = S;
+    for (int r = 0; r < 9; r++)
+      for (int c = r; c < 9; c++) {
+        for (int l = 0; l < 4; l++) pt[l] = pt[l] + J[r][l] * J[c][l];
+        pt += 4;
+      }
+    num += 4;
+    numIn1++;
+    shiftUp(false);
+  }
+  // updateSingleWeighted (Include/MatrixAccumulators.h:1242-1331), off = 0: lane 0 only;
+  // the diagonal term is (J_r*J_r)*w, then J_r *= w for the rest of its row
+  void updateSingleWeighted(const float Jin[9], float w) {
+    float J[9];
+    for (int k = 0; k < 9; k++) J[k] = Jin[k];
+    float* pt = S;
+    for (int r = 0; r < 9; r++) {
+      *pt += J[r] * J[r] * w;
+      pt += 4;
+      J[r] *= w;
+      for (int c = r + 1; c < 9; c++) {
+        *pt += J[c] * J[r];
+        pt += 4;
+      }
+    }
+    num++;
+    numIn1++;
+    shiftUp(false);
+  }
   void shiftUp(bool force) {
     if (numIn1 > 1000 || force) {
       for (int i = 0; i < 180; i++) S1k[i] = S[i] + S1k[i];
@@ -198,6 +236,39 @@ struct Acc9 {
       for (int i = 0; i < 180; i++) S1m[i] = S1k[i] + S1m[i];
       numIn1m += numIn1k; numIn1k = 0;
       std::memset(S1k, 0, sizeof(S1k));
+    }
+  }
+};
+
+// Accumulator11 (Include/MatrixAccumulators.h:91-172): updateSingle adds to lane 0; finish() sets A
+// from the 1m level.  Updates after finish() change num but not A (DirectRefinement relies on that).
+struct Acc11 {
+  float A;
+  size_t num;
+  float S[4], S1k[4], S1m[4];
+  float numIn1, numIn1k, numIn1m;
+  void initialize() {
+    A = 0;
+    std::memset(S, 0, sizeof(S)); std::memset(S1k, 0, sizeof(S1k)); std::memset(S1m, 0, sizeof(S1m));
+    num = 0; numIn1 = numIn1k = numIn1m = 0;
+  }
+  void finish() {
+    shiftUp(true);
+    A = S1m[0] + S1m[1] + S1m[2] + S1m[3];
+  }
+  void updateSingle(float val) {
+    S[0] += val;
+    num++; numIn1++;
+    shiftUp(false);
+  }
+  void shiftUp(bool force) {
+    if (numIn1 > 1000 || force) {
+      for (int l = 0; l < 4; l++) { S1k[l] = S[l] + S1k[l]; S[l] = 0; }
+      numIn1k += numIn1; numIn1 = 0;
+    }
+    if (numIn1k > 1000 || force) {
+      for (int l = 0; l < 4; l++) { S1m[l] = S1k[l] + S1m[l]; S1k[l] = 0; }
+      numIn1m += numIn1k; numIn1k = 0;
     }
   }
 };

@@ -97,6 +97,16 @@ def load(fast=False):
     for n in ("hso_se3_exp", "hso_se3_log", "hso_se3_inverse", "hso_se3_adj", "hso_se3_matrix"):
         getattr(lib, n).argtypes = [vp, vp]
     lib.hso_se3_mul.argtypes = [vp, vp, vp]
+    lib.hso_ref_create.restype = vp
+    lib.hso_ref_create.argtypes = [C.c_int, C.c_int, vp, vp, vp, C.c_float, C.c_float]
+    lib.hso_ref_destroy.argtypes = [vp]
+    lib.hso_ref_set_points.argtypes = [vp, C.c_int, vp, vp, vp, vp]
+    lib.hso_ref_calc.argtypes = [vp] * 8
+    lib.hso_ref_refine.argtypes = [vp, vp, vp, vp]
+    lib.hso_ref_refine.restype = C.c_int
+    lib.hso_ref_get_log.argtypes = [vp, C.c_int, vp]
+    lib.hso_ref_get_log.restype = C.c_int
+    lib.hso_ref_get_points.argtypes = [vp, vp, vp, vp]
     lib.hso_trk_create.restype = vp
     lib.hso_trk_create.argtypes = [vp, C.c_int, C.c_int, C.c_int, vp]
     lib.hso_trk_destroy.argtypes = [vp]
@@ -562,3 +572,55 @@ class PixelSelector:
         a, b = np.zeros(n, np.float32), np.zeros(n, np.float32)
         self.lib.hso_sel_ths(self.h, _p(a), _p(b))
         return a.reshape(self.H // 32, self.W // 32), b.reshape(self.H // 32, self.W // 32)
+
+
+class OracleRefiner:
+    """DirectRefinement (Src/Initializer.cpp:1330-2270) as a CPU restatement (oracle/refine_oracle.cpp)."""
+
+    def __init__(self, scene, fast=False):
+        self.lib = load(fast)
+        s = scene
+        k4 = np.ascontiguousarray(s.K4, np.float64)
+        self._img = [np.ascontiguousarray(s.img1, np.float32), np.ascontiguousarray(s.img2, np.float32)]
+        self.h = self.lib.hso_ref_create(s.width, s.height, _p(k4), _p(self._img[0]), _p(self._img[1]),
+                                         float(s.expo1), float(s.expo2))
+        self.n = s.n_points
+        cols = [np.ascontiguousarray(s.u, np.float32), np.ascontiguousarray(s.v, np.float32),
+                np.ascontiguousarray(s.tri, np.uint8), np.ascontiguousarray(s.z, np.float32)]
+        self.lib.hso_ref_set_points(self.h, self.n, *[_p(c) for c in cols])
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.lib.hso_ref_destroy(self.h)
+            self.h = None
+
+    def calc_res(self, T7, aff=(0.0, 0.0)):
+        H, Hs = np.zeros(64, np.float32), np.zeros(64, np.float32)
+        b, bs, res = np.zeros(8, np.float32), np.zeros(8, np.float32), np.zeros(3, np.float32)
+        self.lib.hso_ref_calc(self.h, _p(np.ascontiguousarray(T7, np.float64)), _p(np.ascontiguousarray(aff, np.float64)),
+                              _p(H), _p(b), _p(Hs), _p(bs), _p(res))
+        return H.reshape(8, 8), b, Hs.reshape(8, 8), bs, res
+
+    def refine(self, T7):
+        T = np.array(T7, np.float64)
+        aff = np.zeros(2)
+        sn = C.c_int()
+        it = self.lib.hso_ref_refine(self.h, _p(T), _p(aff), C.byref(sn))
+        return T, it, bool(sn.value)
+
+    def log(self):
+        out = np.zeros((1001, 8), np.float32)
+        n = self.lib.hso_ref_get_log(self.h, 1001, _p(out))
+        return out[:n]
+
+    def points(self):
+        f7 = np.zeros((self.n, 7), np.float32)
+        g2 = np.zeros((self.n, 2), np.uint8)
+        jb = np.zeros((self.n, 10), np.float32)
+        self.lib.hso_ref_get_points(self.h, _p(f7), _p(g2), _p(jb))
+        return _ref_points(f7, g2, jb)
+
+
+def _ref_points(f7, g2, jb):
+    return dict(idepth=f7[:, 0], idepth_new=f7[:, 1], iR=f7[:, 2], energy_new0=f7[:, 3], energy_new1=f7[:, 4],
+                maxstep=f7[:, 5], lastHessian_new=f7[:, 6], isGood=g2[:, 0], isGood_new=g2[:, 1], jb_new=jb)
