@@ -1,5 +1,6 @@
 // hs_refine.cpp — C-ABI implementation of the DirectRefinement boundary (include/hs_refine.h): refiner
-// context, device frames and point state (structure of arrays), and the single-workgroup LM kernel launch.
+// context, device frames and point state (structure of arrays), and the LM step launches (one kernel per
+// iteration, enqueued in batches; the device-side control block decides and stops).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -66,8 +67,11 @@ struct hs_refiner {
   float* d_pf = nullptr;     // PF_COUNT planes of cap floats
   uint8_t* d_pb = nullptr;   // tri | good | good_new, cap bytes each
   int jb_sel = 0;
-  HsRefOut* d_out = nullptr;
-  HsRefOut* h_out = nullptr;
+  HsRefCtl* d_ctl = nullptr;
+  HsRefCtl* h_ctl = nullptr;
+  int* h_flags = nullptr;
+  double* d_part = nullptr;  // [nblocks][HS_REF_NRED]
+  int* d_ticket = nullptr;
   float* d_log = nullptr;
   int last_iters = 0;
   double last_ms = 0;
@@ -87,38 +91,91 @@ static HsRefPoints points_of(hs_refiner* r) {
   return p;
 }
 
-static int launch(hs_refiner* r, const double T7[7], const double aff[2], int single) {
-  if (!r->haveFrames) return rfail(HS_ERR_STATE, "hs_refiner_set_frames first");
-  if (r->n <= 0) return rfail(HS_ERR_STATE, "hs_refiner_set_points first");
-  RF_HIP(hipSetDevice(r->device));
+static HsRefArgs make_args(hs_refiner* r, int mode) {
   HsRefArgs a;
   std::memset(&a, 0, sizeof(a));
   a.p = points_of(r);
   a.n = r->n;
   a.W = r->W; a.H = r->H;
+  a.mode = mode;
+  a.nblocks = (r->n + HS_REF_PPB - 1) / HS_REF_PPB;
   a.fx = (float)r->K4[0]; a.fy = (float)r->K4[1]; a.cx = (float)r->K4[2]; a.cy = (float)r->K4[3];
   for (int q = 0; q < 9; q++) a.Ki[q] = r->Ki[q];
   a.img1 = r->d_img1;
   a.img2 = r->d_img2;
-  for (int q = 0; q < 7; q++) a.T_in[q] = T7[q];
-  a.aff_in[0] = aff[0];
-  a.aff_in[1] = aff[1];
   a.huberTH = 9.f;                  // setting_huberTH (Src/Settings.cpp:68)
   a.outlierTH = 12 * 12;            // setting_outlierTH (Src/Settings.cpp:65)
-  a.single_pass = single;
-  a.jb_sel = r->jb_sel;
-  a.out = r->d_out;
+  a.jb_sel0 = r->jb_sel;
+  a.ctl = r->d_ctl;
+  a.part = r->d_part;
+  a.ticket = r->d_ticket;
   a.log = r->d_log;
-  RF_HIP(hipEventRecord(r->e0, r->stream));
-  hipLaunchKernelGGL(hs_k_refine, dim3(1), dim3(512), 0, r->stream, a);
+  return a;
+}
+
+static int enqueue(hs_refiner* r, const HsRefArgs& a) {
+  hipLaunchKernelGGL(hs_k_refine_step, dim3(a.nblocks), dim3(256), 0, r->stream, a);
   RF_HIP(hipGetLastError());
-  RF_HIP(hipEventRecord(r->e1, r->stream));
-  RF_HIP(hipMemcpyAsync(r->h_out, r->d_out, sizeof(HsRefOut), hipMemcpyDeviceToHost, r->stream));
+  return HS_OK;
+}
+
+static int read_ctl(hs_refiner* r) {
+  RF_HIP(hipMemcpyAsync(r->h_ctl, r->d_ctl, sizeof(HsRefCtl), hipMemcpyDeviceToHost, r->stream));
   RF_HIP(hipStreamSynchronize(r->stream));
+  return HS_OK;
+}
+
+static int check_ready(hs_refiner* r) {
+  if (!r->haveFrames) return rfail(HS_ERR_STATE, "hs_refiner_set_frames first");
+  if (r->n <= 0) return rfail(HS_ERR_STATE, "hs_refiner_set_points first");
+  RF_HIP(hipSetDevice(r->device));
+  return HS_OK;
+}
+
+// resetPoints + one calcResAndGS at (T, aff)
+static int run_calc(hs_refiner* r, const double T7[7], const double aff[2]) {
+  RF_TRY(check_ready(r));
+  HsRefArgs a = make_args(r, HS_REF_CALC);
+  hs_ref_pass_consts(T7, aff, r->Ki, r->n, &a.pc0);
+  RF_HIP(hipEventRecord(r->e0, r->stream));
+  RF_TRY(enqueue(r, a));
+  RF_HIP(hipEventRecord(r->e1, r->stream));
+  RF_TRY(read_ctl(r));
   float ms = 0;
   RF_HIP(hipEventElapsedTime(&ms, r->e0, r->e1));
   r->last_ms = ms;
-  r->jb_sel = r->h_out->jb_sel;
+  return HS_OK;
+}
+
+// Refine: the first pass, then LM steps enqueued in batches until the device sets done, then the final applyStep
+static int run_refine(hs_refiner* r, const double T7[7], const double aff[2]) {
+  RF_TRY(check_ready(r));
+  HsRefArgs a = make_args(r, HS_REF_INIT);
+  hs_ref_pass_consts(T7, aff, r->Ki, r->n, &a.pc0);
+  for (int q = 0; q < 7; q++) a.T0[q] = T7[q];
+  a.aff0[0] = aff[0];
+  a.aff0[1] = aff[1];
+  RF_HIP(hipEventRecord(r->e0, r->stream));
+  RF_TRY(enqueue(r, a));
+  HsRefArgs it = make_args(r, HS_REF_ITER);
+  int launched = 0, batch = 4;
+  for (;;) {
+    for (int k = 0; k < batch; k++) RF_TRY(enqueue(r, it));
+    launched += batch;
+    RF_HIP(hipMemcpyAsync(&r->h_flags[0], &r->d_ctl->done, sizeof(int), hipMemcpyDeviceToHost, r->stream));
+    RF_HIP(hipStreamSynchronize(r->stream));
+    if (r->h_flags[0]) break;
+    if (launched > HS_REF_MAXLOG + 8) return rfail(HS_ERR_STATE, "refine did not stop within the iteration cap");
+    batch = std::min(2 * batch, 32);
+  }
+  RF_TRY(enqueue(r, make_args(r, HS_REF_FINAL)));  // the pending applyStep + optReg of the last accepted pass
+  RF_HIP(hipEventRecord(r->e1, r->stream));
+  RF_TRY(read_ctl(r));
+  float ms = 0;
+  RF_HIP(hipEventElapsedTime(&ms, r->e0, r->e1));
+  r->last_ms = ms;
+  r->jb_sel = r->h_ctl->jb_sel ^ r->h_ctl->apply_prev;
+  r->last_iters = r->h_ctl->iteration + 1;
   return HS_OK;
 }
 
@@ -137,7 +194,9 @@ int hs_refiner_create(hs_refiner** out, int device_id, int width, int height, co
   if (hipSetDevice(device_id) != hipSuccess || hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&r->e0) != hipSuccess || hipEventCreate(&r->e1) != hipSuccess ||
       hipMalloc(&r->d_img1, np * sizeof(float4)) != hipSuccess || hipMalloc(&r->d_img2, np * sizeof(float4)) != hipSuccess ||
-      hipMalloc(&r->d_out, sizeof(HsRefOut)) != hipSuccess || hipHostMalloc(&r->h_out, sizeof(HsRefOut)) != hipSuccess ||
+      hipMalloc(&r->d_ctl, sizeof(HsRefCtl)) != hipSuccess || hipHostMalloc(&r->h_ctl, sizeof(HsRefCtl)) != hipSuccess ||
+      hipHostMalloc(&r->h_flags, 4 * sizeof(int)) != hipSuccess || hipMalloc(&r->d_ticket, sizeof(int)) != hipSuccess ||
+      hipMemset(r->d_ticket, 0, sizeof(int)) != hipSuccess || hipMemset(r->d_ctl, 0, sizeof(HsRefCtl)) != hipSuccess ||
       hipMalloc(&r->d_log, sizeof(float) * HS_REF_MAXLOG * HS_REF_LOGW) != hipSuccess) {
     hs_refiner_destroy(r);
     return rfail(HS_ERR_HIP, "refiner allocation failed");
@@ -154,9 +213,12 @@ void hs_refiner_destroy(hs_refiner* r) {
   (void)hipFree(r->d_img2);
   (void)hipFree(r->d_pf);
   (void)hipFree(r->d_pb);
-  (void)hipFree(r->d_out);
+  (void)hipFree(r->d_ctl);
+  (void)hipFree(r->d_part);
+  (void)hipFree(r->d_ticket);
   (void)hipFree(r->d_log);
-  if (r->h_out) (void)hipHostFree(r->h_out);
+  if (r->h_ctl) (void)hipHostFree(r->h_ctl);
+  if (r->h_flags) (void)hipHostFree(r->h_flags);
   if (r->e0) (void)hipEventDestroy(r->e0);
   if (r->e1) (void)hipEventDestroy(r->e1);
   if (r->stream) (void)hipStreamDestroy(r->stream);
@@ -189,11 +251,15 @@ int hs_refiner_set_points(hs_refiner* r, int n, const float* u, const float* v, 
   RF_HIP(hipSetDevice(r->device));
   (void)hipFree(r->d_pf);
   (void)hipFree(r->d_pb);
+  (void)hipFree(r->d_part);
   r->d_pf = nullptr;
   r->d_pb = nullptr;
+  r->d_part = nullptr;
+  r->n = 0;
   r->cap = n;  // planes of exactly n: the [2][n] energy blocks are two adjacent planes
   RF_HIP(hipMalloc(&r->d_pf, sizeof(float) * PF_COUNT * (size_t)n));
   RF_HIP(hipMalloc(&r->d_pb, 3 * (size_t)n));
+  RF_HIP(hipMalloc(&r->d_part, sizeof(double) * HS_REF_NRED * (size_t)((n + HS_REF_PPB - 1) / HS_REF_PPB)));
   // the ctor's Pnt set-up (Src/Initializer.cpp:1362-1382)
   std::vector<float> pf((size_t)PF_COUNT * n, 0.f);
   std::vector<uint8_t> pb(3 * (size_t)n, 0);
@@ -222,11 +288,10 @@ int hs_refiner_refine(hs_refiner* r, double pose[7], float* idepth_out, uint8_t*
   if (!r || !pose) return rfail(HS_ERR_INVALID, "null");
   double aff[2] = {0, 0};  // thisToNext_aff = AffLight(0, 0)
   if (r->expo1 > 0 && r->expo2 > 0) aff[0] = (double)logf(r->expo2 / r->expo1);
-  RF_TRY(launch(r, pose, aff, 0));
-  const HsRefOut& o = *r->h_out;
+  RF_TRY(run_refine(r, pose, aff));
+  const HsRefCtl& o = *r->h_ctl;
   for (int q = 0; q < 7; q++) pose[q] = o.T[q];
-  r->last_iters = o.iterations;
-  if (iterations) *iterations = o.iterations;
+  if (iterations) *iterations = r->last_iters;
   if (snapped) *snapped = o.snapped;
   if (idepth_out || good_out) {
     const size_t n = r->n;
@@ -242,15 +307,15 @@ int hs_refiner_refine(hs_refiner* r, double pose[7], float* idepth_out, uint8_t*
       if (idepth_out && good[i] && tri[i]) idepth_out[i] = id[i];  // _videpth write-back (:1389-1395)
     }
   }
-  if (!std::isfinite(o.res[0])) return rfail(HS_ERR_NONFINITE, "non-finite refinement energy");
+  if (!std::isfinite(o.resOld[0])) return rfail(HS_ERR_NONFINITE, "non-finite refinement energy");
   return HS_OK;
 }
 
 int hs_refiner_calc_res(hs_refiner* r, const double T7[7], const double aff[2], float* H64, float* b8, float* Hsc64,
                         float* bsc8, float res3[3]) {
   if (!r || !T7 || !aff) return rfail(HS_ERR_INVALID, "null");
-  RF_TRY(launch(r, T7, aff, 1));
-  const HsRefOut& o = *r->h_out;
+  RF_TRY(run_calc(r, T7, aff));
+  const HsRefCtl& o = *r->h_ctl;
   if (H64) std::memcpy(H64, o.H, sizeof(o.H));
   if (b8) std::memcpy(b8, o.b, sizeof(o.b));
   if (Hsc64) std::memcpy(Hsc64, o.Hsc, sizeof(o.Hsc));

@@ -1,36 +1,40 @@
 // hs_refine_kernels.hip — gfx950 kernel of H-SLAM's initializer refinement DirectRefinement (SURVEY.md §8f
-// rank 4, the second Accumulator9 user):
+// rank 4, the second Accumulator9 user).
 //
-//   hs_k_refine   one workgroup (512 threads, 8 waves) runs the whole level-0 LM loop of
-//                 DirectRefinement::Refine (Src/Initializer.cpp:1412-1564) on the device:
-//                   resetPoints (:1897-1924), calcResAndGS (:1926-2153) with its Accumulator9 normal equations,
-//                   the Schur part acc9SC and the calcEC regularizer energy fused in one pass over the points,
-//                   the fixAffine 6x6 fp32 LDLT step + SE3 update on thread 0, doStep (:2155-2186),
-//                   applyStep (:2188-2205) and optReg (:2229-2270) as per-point passes.
-//                 Point state stays in HBM as structure-of-arrays (one thread owns a fixed point set), the
-//                 JbBuffer / JbBuffer_new swap is a plane-index flip.
+//   hs_k_refine_step   one LM iteration of DirectRefinement::Refine (Src/Initializer.cpp:1412-1564) per launch,
+//                      grid = ceil(n / 32) blocks of 256 threads: 8 lanes per point, one lane per pattern pixel.
+//     prologue   (the point's leader lane) applyStep (:2188-2205) + optReg (:2229-2270) of the previous pass if it
+//                was accepted, then doStep (:2155-2186) with the increment the previous launch solved for;
+//                resetPoints (:1897-1924) in the first launch
+//     pass       calcResAndGS (:1926-2153): every lane projects / samples / differentiates its pixel; the leader
+//                folds its group's 8 values in pattern order (energy, maxstep, JbBuffer_new: bit-identical to the
+//                reference's sequential loop, including the prefix before the first failing pixel), decides
+//                isGood_new and adds its acc9SC row (updateSingleWeighted order) and calcEC terms (:2207-2227);
+//                the lanes of good points add their pixel's 9x9 acc9 products
+//     reduction  wave xor trees -> 4 waves in fp64 -> block partials (agent-scope write-through stores) -> the
+//                last block to take the ticket sums the partials in block order (no block waits on another)
+//     LM         the last block's thread 0: the accept test, the lambda / fails / snapped bookkeeping, the fixAffine
+//                6x6 fp32 LDLT step, SE3 exp * refToNew, the next pass's constants; or done
+//   The host enqueues launches in batches and polls `done`; launches after it return at entry.  A final launch
+//   applies the last accepted step.  Per-point state stays in HBM (structure of arrays); the
+//   JbBuffer / JbBuffer_new swap is a plane-index flip carried in the control block.
 //
-// Per-point arithmetic follows the reference's fp32 operation order (fp contraction off): every per-point
-// output of a pass (isGood_new, energy_new, maxstep, JbBuffer_new, lastHessian_new, idepth_new) is
-// bit-identical to the CPU restatement.  The normal-equation and energy sums are fixed-order parallel
-// reductions (wave xor trees, then the 8 waves in order in fp64) where the reference sums sequentially in
-// 4 SSE lanes: those compare within tolerance.  Each point's accumulator contribution is computed in a
-// second sweep over its pattern once the point is known to be good, so the 9x9 sums stay in registers.
+// Per-point arithmetic follows the reference's fp32 operation order (fp contraction off).  The normal-equation
+// and energy sums are fixed-order parallel reductions (the reference sums sequentially in 4 SSE lanes): those
+// compare within tolerance.
 #pragma clang fp contract(off)
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
 
 #include "hs_refine_kernels.h"
-#include "hs_se3.h"
 
 namespace {
 
-constexpr int REF_NT = 512;
-constexpr int REF_NW = REF_NT / 64;
-constexpr int REF_NACC = 45;                         // upper triangle of the 9x9 [J | r] system
-constexpr int REF_NRED = 2 * REF_NACC + 3;           // acc9, acc9SC, E, calcEC old / new
-constexpr float kAlphaK = 2.5f * 2.5f, kAlphaW = 150 * 150, kCoupling = 1;
+constexpr int RB = 256;             // threads per block
+constexpr int RW = RB / 64;         // waves per block
+constexpr int NACC = 45;            // upper triangle of the 9x9 [J | r] system
+constexpr int NX = 12;              // per-lane values folded by the leader: e, maxstep, dp_j * dd (8), r * dd, dd * dd
 __constant__ int kPat[8][2] = {{0, -2}, {-1, -1}, {1, -1}, {-2, 0}, {0, 0}, {2, 0}, {-1, 1}, {0, 2}};
 
 __device__ __forceinline__ float3 ref_interp33(const float4* __restrict__ img, float x, float y, int w) {
@@ -66,7 +70,7 @@ __device__ __forceinline__ float dot8(const float* a, const float* b) {
 }
 
 // Eigen::LDLT<Matrix<float,6,6>> (diagonal pivoting, left-looking) + solve, one thread, register-resident
-__device__ __noinline__ void ldlt6f_solve(const float* __restrict__ A, const float* __restrict__ rhs, float* __restrict__ x) {
+__device__ void ldlt6f_solve(const float* __restrict__ A, const float* __restrict__ rhs, float* __restrict__ x) {
   float dg[6];
   int pm[6];
 #pragma unroll
@@ -132,55 +136,166 @@ __device__ __noinline__ void ldlt6f_solve(const float* __restrict__ A, const flo
   for (int i = 0; i < 6; i++) x[pm[i]] = y[i];
 }
 
-struct RefShared {
-  // pass inputs (thread 0 writes)
-  float RKi[9], t[3], r2a, r2b, alphaOpt, alphaEnergy, tlog[3];
-  // pass outputs
-  double red[REF_NW][REF_NRED];
-  float H[64], b[8], Hsc[64], bsc[8], res[3], ec[2];
-  // LM state
-  double T[7], Tn[7], aff[2], affn[2];
-  float Hm[64], bm[8], Hs[64], bs[8], resOld[3];
-  float inc[8], lambda;
-  int snapped, accept, brk;
-};
-
-// thread 0: the pass constants at (T, aff) (out of line: keeps the fp64 SE3 code out of the pass's registers)
-__device__ __noinline__ void ref_setup(const HsRefArgs& a, RefShared& S, const double T7[7], const double aff[2]) {
-  const hs::SE3 T = hs::SE3::fromData(T7);
-  double R[9];
-  T.rotationMatrix(R);
-  for (int r = 0; r < 3; r++)
-    for (int c = 0; c < 3; c++)
-      S.RKi[r * 3 + c] = (float)(R[r * 3 + 0] * a.Ki[0 * 3 + c] + R[r * 3 + 1] * a.Ki[1 * 3 + c] + R[r * 3 + 2] * a.Ki[2 * 3 + c]);
-  for (int q = 0; q < 3; q++) S.t[q] = (float)T.t[q];
-  S.r2a = (float)exp(aff[0]);
-  S.r2b = (float)aff[1];
-  // EAlpha never receives an update in the reference (its loop feeds E): alphaEnergy = alphaW * |t|^2 * npts
-  const double tsq = T.t[0] * T.t[0] + T.t[1] * T.t[1] + T.t[2] * T.t[2];
-  const float EAlphaA = 0.f;
-  float alphaEnergy = (float)(kAlphaW * (EAlphaA + tsq * a.n));
-  float alphaOpt;
-  if (alphaEnergy > kAlphaK * a.n) {
-    alphaOpt = 0;
-    alphaEnergy = kAlphaK * a.n;
-  } else {
-    alphaOpt = kAlphaW;
+// the LM step of Refine (Src/Initializer.cpp:1447-1466) from the control block's Hm / Hs / bm / bs / lambda:
+// inc, Tn = exp(inc) * T, affn and the constants of the pass at Tn
+__device__ __noinline__ void lm_solve(const HsRefArgs& a, HsRefCtl* C) {
+  const float wM[8] = {1.0f, 1.0f, 1.0f, 0.5f, 0.5f, 0.5f, 10.0f, 1000.0f};  // SCALE_XI_ROT x3, _TRANS x3, A, B
+  const float scl = 0.01f / (a.W * a.H);
+  const float lambda = C->lambda;
+  float Hl[64], bl[8];
+#pragma unroll
+  for (int q = 0; q < 64; q++) Hl[q] = C->Hm[q];
+#pragma unroll
+  for (int i = 0; i < 8; i++) Hl[i * 8 + i] *= (1 + lambda);
+  const float il = 1 / (1 + lambda);
+#pragma unroll
+  for (int q = 0; q < 64; q++) Hl[q] -= C->Hs[q] * il;
+#pragma unroll
+  for (int i = 0; i < 8; i++) bl[i] = C->bm[i] - C->bs[i] * il;
+  float H6[36], x6[6];
+#pragma unroll
+  for (int r = 0; r < 6; r++)
+#pragma unroll
+    for (int c = 0; c < 6; c++) H6[r * 6 + c] = ((wM[r] * Hl[r * 8 + c]) * wM[c]) * scl;
+#pragma unroll
+  for (int r = 0; r < 8; r++) bl[r] = (wM[r] * bl[r]) * scl;
+  ldlt6f_solve(H6, bl, x6);  // fixAffine = true
+  double incd[6];
+#pragma unroll
+  for (int k = 0; k < 6; k++) {
+    C->inc[k] = -(wM[k] * x6[k]);
+    incd[k] = (double)C->inc[k];
   }
-  S.alphaOpt = alphaOpt;
-  S.alphaEnergy = alphaEnergy;
-  double lg[6];
-  T.log(lg);
-  for (int q = 0; q < 3; q++) S.tlog[q] = (float)lg[q];
+  C->inc[6] = C->inc[7] = 0.f;
+  double T[7], Tn[7];
+#pragma unroll
+  for (int q = 0; q < 7; q++) T[q] = C->T[q];
+  const hs::SE3 nw = hs::SE3::exp(incd) * hs::SE3::fromData(T);
+  nw.toData(Tn);
+#pragma unroll
+  for (int q = 0; q < 7; q++) C->Tn[q] = Tn[q];
+  double affn[2] = {C->aff[0] + C->inc[6], C->aff[1] + C->inc[7]};
+  C->affn[0] = affn[0];
+  C->affn[1] = affn[1];
+  HsRefPass pc;
+  hs_ref_pass_consts(Tn, affn, a.Ki, a.n, &pc);
+  C->pc = pc;
 }
 
-struct PixOut {
-  float e, dd, r, ms, dp[8];
-};
+// last block, thread 0: the pass's H / b / Hsc / bsc / res / calcEC from the reduced sums, then the mode's LM logic
+__device__ __noinline__ void lm_finish(const HsRefArgs& a, const double* R, const HsRefPass& pc, int sel) {
+  HsRefCtl* C = a.ctl;
+  const int n = a.n;
+  float H[64], b[8], Hsc[64], bsc[8], res[3], ec[2];
+  int q = 0;
+#pragma unroll
+  for (int r = 0; r < 9; r++)
+#pragma unroll
+    for (int c = r; c < 9; c++, q++) {
+      const float v = (float)R[q], w = (float)R[NACC + q];
+      if (c < 8) {
+        H[r * 8 + c] = H[c * 8 + r] = v;
+        Hsc[r * 8 + c] = Hsc[c * 8 + r] = w;
+      } else {
+        b[r] = v;
+        bsc[r] = w;
+      }
+    }
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    H[k * 8 + k] += pc.alphaOpt * n;
+    b[k] += pc.tlog[k] * pc.alphaOpt * n;
+  }
+  res[0] = (float)R[2 * NACC];
+  res[1] = pc.alphaEnergy;
+  res[2] = (float)(2 * n);  // E.num: npts updates in each of the two energy loops
+  ec[0] = hs_ref_coupling * (float)R[2 * NACC + 1];
+  ec[1] = hs_ref_coupling * (float)R[2 * NACC + 2];
+  if (a.mode == HS_REF_CALC) {
+#pragma unroll
+    for (int k = 0; k < 64; k++) { C->H[k] = H[k]; C->Hsc[k] = Hsc[k]; }
+#pragma unroll
+    for (int k = 0; k < 8; k++) { C->b[k] = b[k]; C->bsc[k] = bsc[k]; }
+#pragma unroll
+    for (int k = 0; k < 3; k++) C->res[k] = res[k];
+    C->jb_sel = sel;
+    C->done = 1;
+    return;
+  }
+  if (a.mode == HS_REF_INIT) {  // the first calcResAndGS + applyStep(0) (Src/Initializer.cpp:1424-1426)
+#pragma unroll
+    for (int k = 0; k < 64; k++) { C->Hm[k] = H[k]; C->Hs[k] = Hsc[k]; }
+#pragma unroll
+    for (int k = 0; k < 8; k++) { C->bm[k] = b[k]; C->bs[k] = bsc[k]; }
+#pragma unroll
+    for (int k = 0; k < 3; k++) C->resOld[k] = res[k];
+#pragma unroll
+    for (int k = 0; k < 7; k++) C->T[k] = a.T0[k];
+    C->aff[0] = a.aff0[0];
+    C->aff[1] = a.aff0[1];
+    C->lambda = 0.1f;
+    C->fails = 0;
+    C->iteration = 0;
+    C->snapped = 0;
+    C->apply_prev = 1;   // applyStep without optReg
+    C->optreg_prev = 0;
+    C->jb_sel = sel;
+    C->done = 0;
+    lm_solve(a, C);
+    return;
+  }
+  // HS_REF_ITER: calcEC + the accept test (Src/Initializer.cpp:1470-1540)
+  const int it = C->iteration;
+  const float reg0 = C->snapped ? ec[0] : 0.f, reg1 = C->snapped ? ec[1] : 0.f;
+  const float eTotalNew = res[0] + res[1] + reg1;
+  const float eTotalOld = C->resOld[0] + C->resOld[1] + reg0;
+  const bool accept = eTotalOld > eTotalNew;
+  float inc[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) inc[k] = C->inc[k];
+  const float incNorm = sqrtf(dot8(inc, inc));
+  if (it < HS_REF_MAXLOG) {
+    float* L = a.log + (size_t)it * HS_REF_LOGW;
+    L[0] = eTotalOld; L[1] = eTotalNew; L[2] = accept ? 1.f : 0.f; L[3] = C->lambda; L[4] = incNorm;
+    L[5] = res[0]; L[6] = res[1]; L[7] = reg1;
+  }
+  int fails = C->fails;
+  if (accept) {
+    if (res[1] == hs_ref_alphaK * n) C->snapped = 1;
+#pragma unroll
+    for (int k = 0; k < 64; k++) { C->Hm[k] = H[k]; C->Hs[k] = Hsc[k]; }
+#pragma unroll
+    for (int k = 0; k < 8; k++) { C->bm[k] = b[k]; C->bs[k] = bsc[k]; }
+#pragma unroll
+    for (int k = 0; k < 3; k++) C->resOld[k] = res[k];
+    C->aff[0] = C->affn[0];
+    C->aff[1] = C->affn[1];
+#pragma unroll
+    for (int k = 0; k < 7; k++) C->T[k] = C->Tn[k];
+    C->lambda *= 0.5f;
+    fails = 0;
+    if (C->lambda < 0.0001f) C->lambda = 0.0001f;
+  } else {
+    fails++;
+    C->lambda *= 4;
+    if (C->lambda > 10000) C->lambda = 10000;
+  }
+  C->fails = fails;
+  C->apply_prev = accept;
+  C->optreg_prev = accept;
+  C->jb_sel = sel;
+  if (!(incNorm > 1e-4f) || it >= 1000 || fails >= 2) {
+    C->done = 1;
+    return;
+  }
+  C->iteration = it + 1;
+  lm_solve(a, C);
+}
 
-// one pattern pixel of calcResAndGS (Src/Initializer.cpp:1970-2039); false = the point is bad
-__device__ __forceinline__ bool ref_pixel(const HsRefArgs& a, const RefShared& S, int idx, float pu, float pv,
-                                          float idn, bool tri, PixOut& o) {
+// one pattern pixel of calcResAndGS (Src/Initializer.cpp:1970-2039); false = the point is bad.  xv: the values the
+// leader folds in pattern order; J: this pixel's acc9 row
+__device__ __forceinline__ bool ref_pixel(const HsRefArgs& a, const HsRefPass& S, int idx, float pu, float pv,
+                                          float idn, bool tri, float* xv, float J[9]) {
   const float x = pu + kPat[idx][0], y = pv + kPat[idx][1];
   float pt[3];
 #pragma unroll
@@ -197,356 +312,309 @@ __device__ __forceinline__ bool ref_pixel(const HsRefArgs& a, const RefShared& S
   const float residual = hit.x - S.r2a * rlR - S.r2b;
   float hw = fabsf(residual) < a.huberTH ? 1 : a.huberTH / fabsf(residual);
   if (!tri) hw = (float)(hw * 0.1);
-  o.e = hw * residual * residual * (2 - hw);
+  xv[0] = hw * residual * residual * (2 - hw);
   const float dxdd = (S.t[0] - S.t[2] * u) / pt[2];
   const float dydd = (S.t[1] - S.t[2] * v) / pt[2];
   if (hw < 1) hw = sqrtf(hw);
   const float dxI = hw * hit.y * a.fx;
   const float dyI = hw * hit.z * a.fy;
-  o.dp[0] = new_idepth * dxI;
-  o.dp[1] = new_idepth * dyI;
-  o.dp[2] = -new_idepth * (u * dxI + v * dyI);
-  o.dp[3] = -u * v * dxI - (1 + v * v) * dyI;
-  o.dp[4] = (1 + u * u) * dxI + u * v * dyI;
-  o.dp[5] = -v * dxI + u * dyI;
-  o.dp[6] = -hw * S.r2a * rlR;
-  o.dp[7] = -hw * 1;
-  o.dd = dxI * dxdd + dyI * dydd;
-  o.r = hw * residual;
+  J[0] = new_idepth * dxI;
+  J[1] = new_idepth * dyI;
+  J[2] = -new_idepth * (u * dxI + v * dyI);
+  J[3] = -u * v * dxI - (1 + v * v) * dyI;
+  J[4] = (1 + u * u) * dxI + u * v * dyI;
+  J[5] = -v * dxI + u * dyI;
+  J[6] = -hw * S.r2a * rlR;
+  J[7] = -hw * 1;
+  const float dd = dxI * dxdd + dyI * dydd;
+  J[8] = hw * residual;
   const float nx = dxdd * a.fx, ny = dydd * a.fy;
-  o.ms = 1.0f / sqrtf(nx * nx + ny * ny);
+  xv[1] = 1.0f / sqrtf(nx * nx + ny * ny);
+#pragma unroll
+  for (int k = 0; k < 8; k++) xv[2 + k] = J[k] * dd;
+  xv[10] = J[8] * dd;
+  xv[11] = dd * dd;
   return true;
 }
 
-// calcResAndGS + calcEC sums at the constants in S; reads JbBuffer_new plane `nsel`
-__device__ void ref_pass(const HsRefArgs& a, RefShared& S, int nsel) {
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const HsRefPoints& P = a.p;
-  float* __restrict__ Jbn = P.jb[nsel];
-  const int n = a.n;
-  const float alphaOpt = S.alphaOpt, thr = 8 * a.outlierTH * 20;
-  float acc[REF_NACC];
-#pragma unroll
-  for (int q = 0; q < REF_NACC; q++) acc[q] = 0.f;
-  float E = 0.f;
-  for (int i = tid; i < n; i += REF_NT) {
-    const float e0 = P.energy[i], e1 = P.energy[n + i];
-    if (!P.good[i]) {
-      P.maxstep[i] = 1e10f;
-      E += e0;
-      P.energy_new[i] = e0;
-      P.energy_new[n + i] = e1;
-      P.good_new[i] = 0;
-      continue;
-    }
-    const float pu = P.u[i], pv = P.v[i], idn = P.idepth_new[i];
-    const bool tri = P.tri[i] != 0;
-    float jb[10];
-#pragma unroll
-    for (int k = 0; k < 10; k++) jb[k] = 0.f;
-    float energy = 0.f, maxstep = 1e10f;
-    bool ok = true;
-    for (int idx = 0; idx < 8; idx++) {
-      PixOut o;
-      if (!ref_pixel(a, S, idx, pu, pv, idn, tri, o)) {
-        ok = false;
-        break;
-      }
-      energy += o.e;
-      if (o.ms < maxstep) maxstep = o.ms;
-#pragma unroll
-      for (int k = 0; k < 8; k++) jb[k] += o.dp[k] * o.dd;
-      jb[8] += o.r * o.dd;
-      jb[9] += o.dd * o.dd;
-    }
-    P.maxstep[i] = maxstep;
-    if (!ok || energy > thr) {
-      E += e0;
-      P.energy_new[i] = e0;
-      P.energy_new[n + i] = e1;
-      P.good_new[i] = 0;
-#pragma unroll
-      for (int k = 0; k < 10; k++) Jbn[(size_t)k * n + i] = jb[k];
-      continue;
-    }
-    E += energy;
-    P.good_new[i] = 1;
-    P.energy_new[i] = energy;
-    P.energy_new[n + i] = (idn - 1) * (idn - 1);
-    // acc9 contribution: the same per-pixel values again (deterministic), 9x9 upper triangle
-    for (int idx = 0; idx < 8; idx++) {
-      PixOut o;
-      ref_pixel(a, S, idx, pu, pv, idn, tri, o);
-      float J[9];
-#pragma unroll
-      for (int k = 0; k < 8; k++) J[k] = o.dp[k];
-      J[8] = o.r;
-      int q = 0;
-#pragma unroll
-      for (int r = 0; r < 9; r++)
-#pragma unroll
-        for (int c = r; c < 9; c++) acc[q++] += J[r] * J[c];
-    }
-    // acc9SC input (Src/Initializer.cpp:2114-2124): JbBuffer_new[8..9] with the alpha / coupling terms
-    const float iR = P.iR[i];
-    P.lastH_new[i] = jb[9];
-    jb[8] += alphaOpt * (idn - 1);
-    jb[9] += alphaOpt;
-    if (alphaOpt == 0) {
-      jb[8] += kCoupling * (idn - iR);
-      jb[9] += kCoupling;
-    }
-    jb[9] = 1 / (1 + jb[9]);
-#pragma unroll
-    for (int k = 0; k < 10; k++) Jbn[(size_t)k * n + i] = jb[k];
-  }
-  // wave xor trees, then the waves in order in fp64
-#pragma unroll
-  for (int q = 0; q < REF_NACC + 1; q++) {
-    float v = q < REF_NACC ? acc[q] : E;
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    if (lane == 0) S.red[wv][q < REF_NACC ? q : 2 * REF_NACC] = (double)v;
-  }
-  // phase 2: acc9SC (updateSingleWeighted order, Src/Initializer.cpp:2125-2130) and the calcEC terms
-  // (:2214-2220) of the points good in this pass, from the JbBuffer_new rows just written (same thread)
-  {
-    float sc[REF_NACC];
-#pragma unroll
-    for (int q = 0; q < REF_NACC; q++) sc[q] = 0.f;
-    float ec0 = 0.f, ec1 = 0.f;
-    for (int i = tid; i < n; i += REF_NT) {
-      if (!P.good_new[i]) continue;
-      float J[9];
-#pragma unroll
-      for (int k = 0; k < 9; k++) J[k] = Jbn[(size_t)k * n + i];
-      const float w = Jbn[(size_t)9 * n + i];
-      int q = 0;
-#pragma unroll
-      for (int r = 0; r < 9; r++) {
-        sc[q++] += J[r] * J[r] * w;
-        J[r] *= w;
-#pragma unroll
-        for (int c = r + 1; c < 9; c++) sc[q++] += J[c] * J[r];
-      }
-      const float iR = P.iR[i];
-      const float rOld = P.idepth[i] - iR, rNew = P.idepth_new[i] - iR;
-      ec0 += rOld * rOld;
-      ec1 += rNew * rNew;
-    }
-#pragma unroll
-    for (int q = 0; q < REF_NACC + 2; q++) {
-      float v = q < REF_NACC ? sc[q] : (q == REF_NACC ? ec0 : ec1);
-      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-      if (lane == 0) S.red[wv][q < REF_NACC ? REF_NACC + q : 2 * REF_NACC + 1 + (q - REF_NACC)] = (double)v;
-    }
-  }
-  __syncthreads();
-  if (tid < REF_NRED) {
-    double s = 0.0;
-    for (int w = 0; w < REF_NW; w++) s += S.red[w][tid];
-    S.red[0][tid] = s;  // wave 0's slot is only read by this thread before the sum
-  }
-  __syncthreads();
-  if (tid == 0) {
-    const double* R = S.red[0];
-    int q = 0;
-    for (int r = 0; r < 9; r++)
-      for (int c = r; c < 9; c++, q++) {
-        const float v = (float)R[q], w = (float)R[REF_NACC + q];
-        if (c < 8) {
-          S.H[r * 8 + c] = S.H[c * 8 + r] = v;
-          S.Hsc[r * 8 + c] = S.Hsc[c * 8 + r] = w;
-        } else if (r < 8) {
-          S.b[r] = v;
-          S.bsc[r] = w;
-        }
-      }
-    for (int k = 0; k < 3; k++) {
-      S.H[k * 8 + k] += alphaOpt * n;
-      S.b[k] += S.tlog[k] * alphaOpt * n;
-    }
-    S.res[0] = (float)R[2 * REF_NACC];
-    S.res[1] = S.alphaEnergy;
-    S.res[2] = (float)(2 * n);  // E.num: npts updates in each of the two loops
-    S.ec[0] = kCoupling * (float)R[2 * REF_NACC + 1];
-    S.ec[1] = kCoupling * (float)R[2 * REF_NACC + 2];
-  }
-  __syncthreads();
-}
+struct RefLds {
+  HsRefPass pc;
+  float inc[8];
+  float lambda;
+  int apply_prev, optreg_prev, snapped, jb_sel;
+  float xv[RB][NX + 1];  // per-lane values for the leader's in-order fold (+1: bank padding)
+  int pgood[HS_REF_PPB];
+  float Jl[RB][10];      // each lane's acc9 row [J | r] (zero unless its point is good)
+  float Pl[HS_REF_PPB][13];  // each point's acc9SC row (JbBuffer_new after the alpha / coupling terms), E, calcEC
+  float pa[NACC][RW];    // acc9 per wave
+  double red[HS_REF_NRED];
+  int last;
+};
+__constant__ unsigned char kQr[NACC] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 1, 2, 2, 2, 2, 2, 2, 2,
+                                        3, 3, 3, 3, 3, 3, 4, 4, 4, 4, 4, 5, 5, 5, 5, 6, 6, 6, 7, 7, 8};
+__constant__ unsigned char kQc[NACC] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 1, 2, 3, 4, 5, 6, 7, 8, 2, 3, 4, 5, 6, 7, 8,
+                                        3, 4, 5, 6, 7, 8, 4, 5, 6, 7, 8, 5, 6, 7, 8, 6, 7, 8, 7, 8, 8};
 
 }  // namespace
 
-__global__ __launch_bounds__(REF_NT) void hs_k_refine(HsRefArgs a) {
-  __shared__ RefShared S;
-  const int tid = threadIdx.x;
-  const HsRefPoints& P = a.p;
+__global__ __launch_bounds__(RB) void hs_k_refine_step(HsRefArgs a) {
+  HsRefCtl* C = a.ctl;
+  const int mode = a.mode;
+  __shared__ RefLds S;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int slot = tid >> 3, k = tid & 7;
+  const int i = blockIdx.x * HS_REF_PPB + slot;
   const int n = a.n;
-  int sel = a.jb_sel;  // plane holding JbBuffer (uniform)
-  // resetPoints
-  for (int i = tid; i < n; i += REF_NT) {
-    P.energy[i] = 0.f;
-    P.energy[n + i] = 0.f;
-    P.idepth_new[i] = P.idepth[i];
+  const bool valid = i < n;
+  const bool leader = k == 0;
+  const HsRefPoints& P = a.p;
+  // every lane's point coordinates, issued before the control-block round trip
+  float pu = 0.f, pv = 0.f;
+  int tri = 0;
+  if (valid) {
+    pu = P.u[i];
+    pv = P.v[i];
+    tri = P.tri[i];
   }
   if (tid == 0) {
-    for (int q = 0; q < 7; q++) S.T[q] = a.T_in[q];
-    S.aff[0] = a.aff_in[0];
-    S.aff[1] = a.aff_in[1];
-    ref_setup(a, S, S.T, S.aff);
+    if (mode == HS_REF_CALC || mode == HS_REF_INIT) {
+      S.pc = a.pc0;
+      S.apply_prev = 0;
+      S.optreg_prev = 0;
+      S.snapped = 0;
+      S.jb_sel = a.jb_sel0;
+      S.last = 0;
+    } else {
+      S.last = C->done;  // (reused as the early-exit flag before the ticket)
+      S.pc = C->pc;
+      for (int q = 0; q < 8; q++) S.inc[q] = C->inc[q];
+      S.lambda = C->lambda;
+      S.apply_prev = C->apply_prev;
+      S.optreg_prev = C->optreg_prev;
+      S.snapped = C->snapped;
+      S.jb_sel = C->jb_sel;
+    }
   }
   __syncthreads();
-  ref_pass(a, S, sel ^ 1);
-  if (a.single_pass) {
-    if (tid == 0) {
-      HsRefOut& o = *a.out;
-      for (int q = 0; q < 64; q++) { o.H[q] = S.H[q]; o.Hsc[q] = S.Hsc[q]; }
-      for (int q = 0; q < 8; q++) { o.b[q] = S.b[q]; o.bsc[q] = S.bsc[q]; }
-      for (int q = 0; q < 3; q++) o.res[q] = S.res[q];
-      o.jb_sel = sel;
-    }
-    return;
-  }
-  // applyStep of the initial evaluation (unconditional)
-  for (int i = tid; i < n; i += REF_NT) {
-    if (!P.good[i]) {
-      P.idepth[i] = P.idepth_new[i] = P.iR[i];
-      continue;
-    }
-    P.energy[i] = P.energy_new[i];
-    P.energy[n + i] = P.energy_new[n + i];
-    P.good[i] = P.good_new[i];
-    P.idepth[i] = P.idepth_new[i];
-    P.lastH[i] = P.lastH_new[i];
-  }
-  sel ^= 1;
-  if (tid == 0) {
-    for (int q = 0; q < 64; q++) { S.Hm[q] = S.H[q]; S.Hs[q] = S.Hsc[q]; }
-    for (int q = 0; q < 8; q++) { S.bm[q] = S.b[q]; S.bs[q] = S.bsc[q]; }
-    for (int q = 0; q < 3; q++) S.resOld[q] = S.res[q];
-    S.lambda = 0.1f;
-    S.snapped = 0;
-  }
-  const float wM[8] = {1.0f, 1.0f, 1.0f, 0.5f, 0.5f, 0.5f, 10.0f, 1000.0f};  // SCALE_XI_ROT x3, SCALE_XI_TRANS x3, A, B
-  const float scl = 0.01f / (a.W * a.H);
-  int fails = 0, iteration = 0;
-  __syncthreads();
-  while (true) {
-    if (tid == 0) {
-      const float lambda = S.lambda;
-      float Hl[64], bl[8];
-      for (int q = 0; q < 64; q++) Hl[q] = S.Hm[q];
-      for (int i = 0; i < 8; i++) Hl[i * 8 + i] *= (1 + lambda);
-      const float il = 1 / (1 + lambda);
-      for (int q = 0; q < 64; q++) Hl[q] -= S.Hs[q] * il;
-      for (int i = 0; i < 8; i++) bl[i] = S.bm[i] - S.bs[i] * il;
-      float H6[36], x6[6];
-      for (int r = 0; r < 6; r++)
-        for (int c = 0; c < 6; c++) H6[r * 6 + c] = ((wM[r] * Hl[r * 8 + c]) * wM[c]) * scl;
-      for (int r = 0; r < 8; r++) bl[r] = (wM[r] * bl[r]) * scl;
-      ldlt6f_solve(H6, bl, x6);  // fixAffine = true
-      double incd[6];
-      for (int k = 0; k < 6; k++) {
-        S.inc[k] = -(wM[k] * x6[k]);
-        incd[k] = (double)S.inc[k];
-      }
-      S.inc[6] = S.inc[7] = 0.f;
-      const hs::SE3 nw = hs::SE3::exp(incd) * hs::SE3::fromData(S.T);
-      nw.toData(S.Tn);
-      S.affn[0] = S.aff[0] + S.inc[6];
-      S.affn[1] = S.aff[1] + S.inc[7];
-      ref_setup(a, S, S.Tn, S.affn);
-    }
-    __syncthreads();
-    {  // doStep (Src/Initializer.cpp:2155-2186) with JbBuffer = plane sel
+  if (mode == HS_REF_ITER && S.last) return;  // the LM has stopped: launches queued after it do nothing (uniform)
+  const int sel = S.jb_sel ^ S.apply_prev;  // JbBuffer plane after this launch's applyStep
+  float* __restrict__ Jbn = P.jb[sel ^ 1];
+  // ---- prologue (the point's leader lane): every load first (the arrays may alias as far as the compiler
+  // knows, so loads after a store would serialize), then applyStep / optReg / doStep in registers
+  float idn = 0.f, idp = 0.f, iR = 0.f, e0 = 0.f, e1 = 0.f;
+  int g = 0;
+  if (valid && leader) {
+    const int g_old = P.good[i];
+    const float id_old = P.idepth[i], iR_old = P.iR[i];
+    if (mode == HS_REF_CALC || mode == HS_REF_INIT) {  // resetPoints
+      g = g_old;
+      idp = id_old;
+      idn = id_old;
+      iR = iR_old;
+      P.energy[i] = 0.f;
+      P.energy[n + i] = 0.f;
+      P.idepth_new[i] = idn;
+    } else {
+      const int gn_prev = P.good_new[i];
+      const float en0 = P.energy_new[i], en1 = P.energy_new[n + i], idn_prev = P.idepth_new[i];
+      const float lhn = P.lastH_new[i], invz = P.invz[i], ms_prev = P.maxstep[i];
+      const float eo0 = P.energy[i], eo1 = P.energy[n + i];
       const float* Jb = P.jb[sel];
-      float inc[8];
+      float jb[10];
 #pragma unroll
-      for (int k = 0; k < 8; k++) inc[k] = S.inc[k];
-      const float lambda = S.lambda;
-      for (int i = tid; i < n; i += REF_NT) {
-        if (!P.good[i]) continue;
-        float jb[10];
-#pragma unroll
-        for (int k = 0; k < 10; k++) jb[k] = Jb[(size_t)k * n + i];
-        const float b = jb[8] + dot8(jb, inc);
-        float step = -b * jb[9] / (1 + lambda);
-        float maxstep = 0.25f * P.maxstep[i];
+      for (int q = 0; q < 10; q++) jb[q] = Jb[(size_t)q * n + i];
+      g = g_old;
+      idp = id_old;
+      iR = iR_old;
+      e0 = eo0;
+      e1 = eo1;
+      float idn_w = idn_prev;
+      if (S.apply_prev) {  // applyStep (+ optReg)
+        if (!g_old) {
+          idp = iR_old;
+          idn_w = iR_old;
+          if (S.optreg_prev && !S.snapped) iR = tri ? invz : iR_old;
+        } else {
+          e0 = en0;
+          e1 = en1;
+          g = gn_prev;
+          idp = idn_prev;
+          if (S.optreg_prev) {
+            if (!S.snapped) iR = tri ? invz : idp;
+            else if (g) iR = idp;
+          }
+          P.energy[i] = e0;
+          P.energy[n + i] = e1;
+          P.good[i] = (uint8_t)g;
+          P.lastH[i] = lhn;
+        }
+        P.idepth[i] = idp;
+        P.iR[i] = iR;
+      }
+      if (mode == HS_REF_ITER && g) {  // doStep with JbBuffer = plane sel (its rows were written by a pass
+        // whose point was good, which this point is)
+        const float b = jb[8] + dot8(jb, S.inc);
+        float step = -b * jb[9] / (1 + S.lambda);
+        float maxstep = 0.25f * ms_prev;
         if (maxstep > 1e10f) maxstep = 1e10f;
         if (step > maxstep) step = maxstep;
         if (step < -maxstep) step = -maxstep;
-        float newIdepth = P.idepth[i] + step;
+        float newIdepth = idp + step;
         if (newIdepth < 1e-3f) newIdepth = 1e-3f;
         if (newIdepth > 50) newIdepth = 50;
-        P.idepth_new[i] = newIdepth;
+        idn_w = newIdepth;
       }
+      idn = idn_w;
+      if (S.apply_prev || (mode == HS_REF_ITER && g)) P.idepth_new[i] = idn;
     }
-    __syncthreads();
-    ref_pass(a, S, sel ^ 1);
-    if (tid == 0) {
-      const float reg0 = S.snapped ? S.ec[0] : 0.f, reg1 = S.snapped ? S.ec[1] : 0.f;  // calcEC
-      const float eTotalNew = S.res[0] + S.res[1] + reg1;
-      const float eTotalOld = S.resOld[0] + S.resOld[1] + reg0;
-      const bool accept = eTotalOld > eTotalNew;
-      const float incNorm = sqrtf(dot8(S.inc, S.inc));
-      if (iteration < HS_REF_MAXLOG) {
-        float* L = a.log + (size_t)iteration * HS_REF_LOGW;
-        L[0] = eTotalOld; L[1] = eTotalNew; L[2] = accept ? 1.f : 0.f; L[3] = S.lambda; L[4] = incNorm;
-        L[5] = S.res[0]; L[6] = S.res[1]; L[7] = reg1;
-      }
-      if (accept) {
-        if (S.res[1] == kAlphaK * n) S.snapped = 1;
-        for (int q = 0; q < 64; q++) { S.Hm[q] = S.H[q]; S.Hs[q] = S.Hsc[q]; }
-        for (int q = 0; q < 8; q++) { S.bm[q] = S.b[q]; S.bs[q] = S.bsc[q]; }
-        for (int q = 0; q < 3; q++) S.resOld[q] = S.res[q];
-        S.aff[0] = S.affn[0];
-        S.aff[1] = S.affn[1];
-        for (int q = 0; q < 7; q++) S.T[q] = S.Tn[q];
-        S.lambda *= 0.5f;
-        fails = 0;
-        if (S.lambda < 0.0001f) S.lambda = 0.0001f;
-      } else {
-        fails++;
-        S.lambda *= 4;
-        if (S.lambda > 10000) S.lambda = 10000;
-      }
-      S.accept = accept;
-      S.brk = !(incNorm > 1e-4f) || iteration >= 1000 || fails >= 2;
-    }
-    __syncthreads();
-    if (S.accept) {  // applyStep + optReg (uniform branch)
-      const bool snapped = S.snapped != 0;
-      for (int i = tid; i < n; i += REF_NT) {
-        if (!P.good[i]) {
-          const float r = P.iR[i];
-          P.idepth[i] = P.idepth_new[i] = r;
-          if (!snapped) P.iR[i] = P.tri[i] ? P.invz[i] : r;
-          continue;
-        }
-        P.energy[i] = P.energy_new[i];
-        P.energy[n + i] = P.energy_new[n + i];
-        const uint8_t g = P.good_new[i];
-        P.good[i] = g;
-        const float idp = P.idepth_new[i];
-        P.idepth[i] = idp;
-        P.lastH[i] = P.lastH_new[i];
-        if (!snapped) P.iR[i] = P.tri[i] ? P.invz[i] : idp;
-        else if (g) P.iR[i] = idp;
-      }
-      sel ^= 1;
-    }
-    const bool brk = S.brk != 0;
-    __syncthreads();  // every thread has read S.accept / S.brk before thread 0 rewrites them
-    if (brk) break;
-    iteration++;
   }
+  if (mode == HS_REF_FINAL) return;
+  const int base = lane & ~7;
+  idn = __shfl(idn, base);
+  g = __shfl(g, base);
+  // ---- pass: one pixel per lane
+  float J[9];
+  bool ok = false;
+  const bool live = valid && g;
+  if (live) ok = ref_pixel(a, S.pc, k, pu, pv, idn, tri != 0, S.xv[tid], J);
+  const unsigned long long failm = __ballot(live && !ok);
+  const unsigned int fb = (unsigned int)(failm >> base) & 0xffu;
+  const int f = fb ? __builtin_ctz(fb) : 8;  // first failing pixel: the reference's loop breaks there
+  __syncthreads();
+  float E = 0.f, ec0 = 0.f, ec1 = 0.f;
+  float* prow = S.Pl[slot];
+  if (valid && leader) {
+    int gn = 0;
+    if (!g) {
+      P.maxstep[i] = 1e10f;
+      E = e0;
+      P.energy_new[i] = e0;
+      P.energy_new[n + i] = e1;
+    } else {
+      float energy = 0.f, maxstep = 1e10f, jb[10];
+#pragma unroll
+      for (int q = 0; q < 10; q++) jb[q] = 0.f;
+      for (int kk = 0; kk < f; kk++) {
+        const float* x = S.xv[tid + kk];
+        energy += x[0];
+        if (x[1] < maxstep) maxstep = x[1];
+#pragma unroll
+        for (int q = 0; q < 10; q++) jb[q] += x[2 + q];
+      }
+      P.maxstep[i] = maxstep;
+      if (f < 8 || energy > 8 * a.outlierTH * 20) {
+        E = e0;
+        P.energy_new[i] = e0;
+        P.energy_new[n + i] = e1;
+      } else {
+        gn = 1;
+        E = energy;
+        P.energy_new[i] = energy;
+        P.energy_new[n + i] = (idn - 1) * (idn - 1);
+        // acc9SC row (Src/Initializer.cpp:2114-2124)
+        const float alphaOpt = S.pc.alphaOpt;
+        P.lastH_new[i] = jb[9];
+        jb[8] += alphaOpt * (idn - 1);
+        jb[9] += alphaOpt;
+        if (alphaOpt == 0) {
+          jb[8] += hs_ref_coupling * (idn - iR);
+          jb[9] += hs_ref_coupling;
+        }
+        jb[9] = 1 / (1 + jb[9]);
+        // calcEC terms (Src/Initializer.cpp:2214-2220)
+        const float rOld = idp - iR, rNew = idn - iR;
+        ec0 = rOld * rOld;
+        ec1 = rNew * rNew;
+      }
+#pragma unroll
+      for (int q = 0; q < 10; q++) {
+        Jbn[(size_t)q * n + i] = jb[q];
+        prow[q] = gn ? jb[q] : 0.f;
+      }
+    }
+    if (!g) {
+#pragma unroll
+      for (int q = 0; q < 10; q++) prow[q] = 0.f;
+    }
+    prow[10] = E;
+    prow[11] = ec0;
+    prow[12] = ec1;
+    P.good_new[i] = (uint8_t)gn;
+    S.pgood[slot] = gn;
+  } else if (leader) {
+    S.pgood[slot] = 0;
+#pragma unroll
+    for (int q = 0; q < 13; q++) prow[q] = 0.f;
+  }
+  __syncthreads();
+  {  // this lane's acc9 row (zero unless its point is good)
+    const bool pg = S.pgood[slot] != 0;
+#pragma unroll
+    for (int q = 0; q < 9; q++) S.Jl[tid][q] = pg ? J[q] : 0.f;
+  }
+  __syncthreads();
+  // ---- block sums in a fixed order: acc9 entry q over each wave's 64 lanes in lane order, then the 4 waves;
+  // acc9SC (updateSingleWeighted form: diagonal (J_r J_r) w, off-diagonal J_c (J_r w)) and E / calcEC over the
+  // 32 points in point order
+  if (tid < NACC * RW) {
+    const int q = tid >> 2, w = tid & 3, r = kQr[q], c = kQc[q];
+    float s = 0.f;
+    for (int l = w * 64; l < w * 64 + 64; l++) s += S.Jl[l][r] * S.Jl[l][c];
+    S.pa[q][w] = s;
+  } else if (tid < NACC * RW + NACC) {
+    const int q = tid - NACC * RW, r = kQr[q], c = kQc[q];
+    float s = 0.f;
+    for (int p = 0; p < HS_REF_PPB; p++) {
+      const float* row = S.Pl[p];
+      const float w = row[9];
+      s += r == c ? row[r] * row[r] * w : row[c] * (row[r] * w);
+    }
+    S.red[NACC + q] = (double)s;
+  } else if (tid < NACC * RW + NACC + 3) {
+    const int q = tid - NACC * RW - NACC;
+    float s = 0.f;
+    for (int p = 0; p < HS_REF_PPB; p++) s += S.Pl[p][10 + q];
+    S.red[2 * NACC + q] = (double)s;
+  }
+  __syncthreads();
+  if (tid < HS_REF_NRED) {
+    double s;
+    if (tid < NACC) {
+      s = 0.0;
+#pragma unroll
+      for (int w = 0; w < RW; w++) s += (double)S.pa[tid][w];
+    } else {
+      s = S.red[tid];
+    }
+    __hip_atomic_store(&a.part[(size_t)blockIdx.x * HS_REF_NRED + tid], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // hand-off: the partials are write-through (agent scope); every storing wave drains, then one lane takes a
+  // ticket; the block whose add returns nblocks - 1 reduces (no block waits on another)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0)
+    S.last = __hip_atomic_fetch_add(a.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.nblocks - 1;
+  __syncthreads();
+  if (!S.last) return;
+  if (tid < HS_REF_NRED) {  // block order, 16 independent write-through loads in flight per thread
+    double s = 0.0;
+    const double* pp = a.part + tid;
+    int b = 0;
+    for (; b + 16 <= a.nblocks; b += 16) {
+      double t[16];
+#pragma unroll
+      for (int j = 0; j < 16; j++)
+        t[j] = __hip_atomic_load(pp + (size_t)(b + j) * HS_REF_NRED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int j = 0; j < 16; j++) s += t[j];
+    }
+    for (; b < a.nblocks; b++)
+      s += __hip_atomic_load(pp + (size_t)b * HS_REF_NRED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    S.red[tid] = s;  // only this thread reads slot tid before the sum
+  }
+  __syncthreads();
   if (tid == 0) {
-    HsRefOut& o = *a.out;
-    for (int q = 0; q < 7; q++) o.T[q] = S.T[q];
-    o.aff[0] = S.aff[0];
-    o.aff[1] = S.aff[1];
-    o.iterations = iteration + 1;
-    o.snapped = S.snapped;
-    o.jb_sel = sel;
-    for (int q = 0; q < 3; q++) o.res[q] = S.resOld[q];
+    lm_finish(a, S.red, S.pc, sel);
+    __hip_atomic_store(a.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
   }
 }
