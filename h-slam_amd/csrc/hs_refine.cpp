@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <algorithm>
 #include <cstring>
 #include <string>
@@ -74,6 +76,7 @@ struct hs_refiner {
   int* d_ticket = nullptr;
   float* d_log = nullptr;
   int last_iters = 0;
+  long long* d_trace = nullptr;  // HS_REF_TRACE=1: per-block stamps of each step launch, dumped to stderr
   double last_ms = 0;
 };
 
@@ -110,12 +113,37 @@ static HsRefArgs make_args(hs_refiner* r, int mode) {
   a.part = r->d_part;
   a.ticket = r->d_ticket;
   a.log = r->d_log;
+  a.trace = r->d_trace;
   return a;
 }
 
 static int enqueue(hs_refiner* r, const HsRefArgs& a) {
   hipLaunchKernelGGL(hs_k_refine_step, dim3(a.nblocks), dim3(256), 0, r->stream, a);
   RF_HIP(hipGetLastError());
+  return HS_OK;
+}
+
+static int dump_trace(hs_refiner* r, int nb, int launch_no) {
+  std::vector<long long> t((size_t)nb * 8);
+  RF_HIP(hipMemcpyAsync(t.data(), r->d_trace, t.size() * sizeof(long long), hipMemcpyDeviceToHost, r->stream));
+  RF_HIP(hipStreamSynchronize(r->stream));
+  int khz = 0;
+  RF_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, r->device));
+  const double us = khz > 0 ? 1e3 / khz : 0.01;
+  long long t0 = t[0];
+  for (int b = 0; b < nb; b++) t0 = std::min(t0, t[(size_t)b * 8]);
+  for (int k = 0; k < 8; k++) {
+    std::vector<double> v;
+    for (int b = 0; b < nb; b++) {
+      const long long x = t[(size_t)b * 8 + k];
+      if (x >= t0) v.push_back((x - t0) * us);
+    }
+    if (v.empty()) continue;
+    std::sort(v.begin(), v.end());
+    std::fprintf(stderr, "[hs refine trace] launch %d cp%d n %3zu min %7.2f med %7.2f max %7.2f us\n", launch_no, k,
+                 v.size(), v.front(), v[v.size() / 2], v.back());
+  }
+  RF_HIP(hipMemsetAsync(r->d_trace, 0, t.size() * sizeof(long long), r->stream));
   return HS_OK;
 }
 
@@ -159,14 +187,16 @@ static int run_refine(hs_refiner* r, const double T7[7], const double aff[2]) {
   RF_TRY(enqueue(r, a));
   HsRefArgs it = make_args(r, HS_REF_ITER);
   int launched = 0, batch = 4;
+  if (r->d_trace) batch = 1;
   for (;;) {
     for (int k = 0; k < batch; k++) RF_TRY(enqueue(r, it));
+    if (r->d_trace && launched < 3) RF_TRY(dump_trace(r, it.nblocks, launched));
     launched += batch;
     RF_HIP(hipMemcpyAsync(&r->h_flags[0], &r->d_ctl->done, sizeof(int), hipMemcpyDeviceToHost, r->stream));
     RF_HIP(hipStreamSynchronize(r->stream));
     if (r->h_flags[0]) break;
     if (launched > HS_REF_MAXLOG + 8) return rfail(HS_ERR_STATE, "refine did not stop within the iteration cap");
-    batch = std::min(2 * batch, 32);
+    if (!r->d_trace) batch = std::min(2 * batch, 32);
   }
   RF_TRY(enqueue(r, make_args(r, HS_REF_FINAL)));  // the pending applyStep + optReg of the last accepted pass
   RF_HIP(hipEventRecord(r->e1, r->stream));
@@ -216,6 +246,7 @@ void hs_refiner_destroy(hs_refiner* r) {
   (void)hipFree(r->d_ctl);
   (void)hipFree(r->d_part);
   (void)hipFree(r->d_ticket);
+  (void)hipFree(r->d_trace);
   (void)hipFree(r->d_log);
   if (r->h_ctl) (void)hipHostFree(r->h_ctl);
   if (r->h_flags) (void)hipHostFree(r->h_flags);
@@ -260,6 +291,12 @@ int hs_refiner_set_points(hs_refiner* r, int n, const float* u, const float* v, 
   RF_HIP(hipMalloc(&r->d_pf, sizeof(float) * PF_COUNT * (size_t)n));
   RF_HIP(hipMalloc(&r->d_pb, 3 * (size_t)n));
   RF_HIP(hipMalloc(&r->d_part, sizeof(double) * HS_REF_NRED * (size_t)((n + HS_REF_PPB - 1) / HS_REF_PPB)));
+  (void)hipFree(r->d_trace);
+  r->d_trace = nullptr;
+  if (const char* e = std::getenv("HS_REF_TRACE"); e && std::atoi(e) > 0) {
+    RF_HIP(hipMalloc(&r->d_trace, sizeof(long long) * 8 * (size_t)((n + HS_REF_PPB - 1) / HS_REF_PPB)));
+    RF_HIP(hipMemset(r->d_trace, 0, sizeof(long long) * 8 * (size_t)((n + HS_REF_PPB - 1) / HS_REF_PPB)));
+  }
   // the ctor's Pnt set-up (Src/Initializer.cpp:1362-1382)
   std::vector<float> pf((size_t)PF_COUNT * n, 0.f);
   std::vector<uint8_t> pb(3 * (size_t)n, 0);

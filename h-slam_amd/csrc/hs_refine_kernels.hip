@@ -337,6 +337,11 @@ __device__ __forceinline__ bool ref_pixel(const HsRefArgs& a, const HsRefPass& S
   return true;
 }
 
+#define REF_TRACE(slot)                                                                        \
+  do {                                                                                         \
+    if (a.trace && threadIdx.x == 0) a.trace[(size_t)blockIdx.x * 8 + (slot)] = wall_clock64(); \
+  } while (0)
+
 struct RefLds {
   HsRefPass pc;
   float inc[8];
@@ -368,6 +373,7 @@ __global__ __launch_bounds__(RB) void hs_k_refine_step(HsRefArgs a) {
   const bool valid = i < n;
   const bool leader = k == 0;
   const HsRefPoints& P = a.p;
+  REF_TRACE(0);
   // every lane's point coordinates, issued before the control-block round trip
   float pu = 0.f, pv = 0.f;
   int tri = 0;
@@ -397,6 +403,7 @@ __global__ __launch_bounds__(RB) void hs_k_refine_step(HsRefArgs a) {
   }
   __syncthreads();
   if (mode == HS_REF_ITER && S.last) return;  // the LM has stopped: launches queued after it do nothing (uniform)
+  REF_TRACE(1);
   const int sel = S.jb_sel ^ S.apply_prev;  // JbBuffer plane after this launch's applyStep
   float* __restrict__ Jbn = P.jb[sel ^ 1];
   // ---- prologue (the point's leader lane): every load first (the arrays may alias as far as the compiler
@@ -469,6 +476,7 @@ __global__ __launch_bounds__(RB) void hs_k_refine_step(HsRefArgs a) {
     }
   }
   if (mode == HS_REF_FINAL) return;
+  REF_TRACE(2);
   const int base = lane & ~7;
   idn = __shfl(idn, base);
   g = __shfl(g, base);
@@ -481,6 +489,7 @@ __global__ __launch_bounds__(RB) void hs_k_refine_step(HsRefArgs a) {
   const unsigned int fb = (unsigned int)(failm >> base) & 0xffu;
   const int f = fb ? __builtin_ctz(fb) : 8;  // first failing pixel: the reference's loop breaks there
   __syncthreads();
+  REF_TRACE(3);
   float E = 0.f, ec0 = 0.f, ec1 = 0.f;
   float* prow = S.Pl[slot];
   if (valid && leader) {
@@ -547,6 +556,7 @@ __global__ __launch_bounds__(RB) void hs_k_refine_step(HsRefArgs a) {
     for (int q = 0; q < 13; q++) prow[q] = 0.f;
   }
   __syncthreads();
+  REF_TRACE(4);
   {  // this lane's acc9 row (zero unless its point is good)
     const bool pg = S.pgood[slot] != 0;
 #pragma unroll
@@ -588,6 +598,7 @@ __global__ __launch_bounds__(RB) void hs_k_refine_step(HsRefArgs a) {
     }
     __hip_atomic_store(&a.part[(size_t)blockIdx.x * HS_REF_NRED + tid], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  REF_TRACE(5);
   // hand-off: the partials are write-through (agent scope); every storing wave drains, then one lane takes a
   // ticket; the block whose add returns nblocks - 1 reduces (no block waits on another)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -595,6 +606,7 @@ __global__ __launch_bounds__(RB) void hs_k_refine_step(HsRefArgs a) {
   if (tid == 0)
     S.last = __hip_atomic_fetch_add(a.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.nblocks - 1;
   __syncthreads();
+  REF_TRACE(6);
   if (!S.last) return;
   if (tid < HS_REF_NRED) {  // block order, 16 independent write-through loads in flight per thread
     double s = 0.0;
@@ -617,4 +629,5 @@ __global__ __launch_bounds__(RB) void hs_k_refine_step(HsRefArgs a) {
     lm_finish(a, S.red, S.pc, sel);
     __hip_atomic_store(a.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
   }
+  REF_TRACE(7);
 }
