@@ -69,8 +69,14 @@ __device__ __forceinline__ float dot8(const float* a, const float* b) {
   return (s[0] + s[2]) + (s[1] + s[3]);
 }
 
-// Eigen::LDLT<Matrix<float,6,6>> (diagonal pivoting, left-looking) + solve, one thread, register-resident
-__device__ void ldlt6f_solve(const float* __restrict__ A, const float* __restrict__ rhs, float* __restrict__ x) {
+// thread 0's LDS workspace for the LM step (dynamically indexed arrays in private memory would live in scratch)
+struct RefWork {
+  float Hn[64], bn[8], Hsn[64], bsn[8];  // this pass's H_out / b_out / H_out_sc / b_out_sc
+  float H6[36], bl[8], x6[8];
+};
+
+// Eigen::LDLT<Matrix<float,6,6>> (diagonal pivoting, left-looking) + solve, one thread, the factor in registers
+__device__ __forceinline__ void ldlt6f_solve(const float* __restrict__ A, const float* __restrict__ rhs, float* __restrict__ x) {
   float dg[6];
   int pm[6];
 #pragma unroll
@@ -138,27 +144,27 @@ __device__ void ldlt6f_solve(const float* __restrict__ A, const float* __restric
 
 // the LM step of Refine (Src/Initializer.cpp:1447-1466) from the control block's Hm / Hs / bm / bs / lambda:
 // inc, Tn = exp(inc) * T, affn and the constants of the pass at Tn
-__device__ __noinline__ void lm_solve(const HsRefArgs& a, HsRefCtl* C) {
+__device__ __forceinline__ void lm_solve(const HsRefArgs& a, HsRefCtl* C, RefWork* W) {
   const float wM[8] = {1.0f, 1.0f, 1.0f, 0.5f, 0.5f, 0.5f, 10.0f, 1000.0f};  // SCALE_XI_ROT x3, _TRANS x3, A, B
   const float scl = 0.01f / (a.W * a.H);
   const float lambda = C->lambda;
-  float Hl[64], bl[8];
-#pragma unroll
-  for (int q = 0; q < 64; q++) Hl[q] = C->Hm[q];
-#pragma unroll
-  for (int i = 0; i < 8; i++) Hl[i * 8 + i] *= (1 + lambda);
+  float* H6 = W->H6;
+  float* bl = W->bl;
+  float* x6 = W->x6;
   const float il = 1 / (1 + lambda);
-#pragma unroll
-  for (int q = 0; q < 64; q++) Hl[q] -= C->Hs[q] * il;
-#pragma unroll
-  for (int i = 0; i < 8; i++) bl[i] = C->bm[i] - C->bs[i] * il;
-  float H6[36], x6[6];
+  // Hl = H with the diagonal * (1 + lambda), minus Hsc / (1 + lambda), then wM Hl wM * (0.01 / (w h)); fixAffine
+  // reads the top-left 6x6 block and the first 6 entries of bl only
 #pragma unroll
   for (int r = 0; r < 6; r++)
 #pragma unroll
-    for (int c = 0; c < 6; c++) H6[r * 6 + c] = ((wM[r] * Hl[r * 8 + c]) * wM[c]) * scl;
+    for (int c = 0; c < 6; c++) {
+      float h = C->Hm[r * 8 + c];
+      if (r == c) h *= (1 + lambda);
+      h -= C->Hs[r * 8 + c] * il;
+      H6[r * 6 + c] = ((wM[r] * h) * wM[c]) * scl;
+    }
 #pragma unroll
-  for (int r = 0; r < 8; r++) bl[r] = (wM[r] * bl[r]) * scl;
+  for (int r = 0; r < 8; r++) bl[r] = (wM[r] * (C->bm[r] - C->bs[r] * il)) * scl;
   ldlt6f_solve(H6, bl, x6);  // fixAffine = true
   double incd[6];
 #pragma unroll
@@ -183,10 +189,14 @@ __device__ __noinline__ void lm_solve(const HsRefArgs& a, HsRefCtl* C) {
 }
 
 // last block, thread 0: the pass's H / b / Hsc / bsc / res / calcEC from the reduced sums, then the mode's LM logic
-__device__ __noinline__ void lm_finish(const HsRefArgs& a, const double* R, const HsRefPass& pc, int sel) {
-  HsRefCtl* C = a.ctl;
+__device__ __forceinline__ void lm_finish(const HsRefArgs& a, HsRefCtl* C, RefWork* W, const double* R,
+                                          const HsRefPass& pc, int sel) {
   const int n = a.n;
-  float H[64], b[8], Hsc[64], bsc[8], res[3], ec[2];
+  float* H = W->Hn;
+  float* b = W->bn;
+  float* Hsc = W->Hsn;
+  float* bsc = W->bsn;
+  float res[3], ec[2];
   int q = 0;
 #pragma unroll
   for (int r = 0; r < 9; r++)
@@ -196,7 +206,7 @@ __device__ __noinline__ void lm_finish(const HsRefArgs& a, const double* R, cons
       if (c < 8) {
         H[r * 8 + c] = H[c * 8 + r] = v;
         Hsc[r * 8 + c] = Hsc[c * 8 + r] = w;
-      } else {
+      } else if (r < 8) {  // column 8 = [b; r'r]: the (8, 8) entry is not part of b
         b[r] = v;
         bsc[r] = w;
       }
@@ -241,7 +251,7 @@ __device__ __noinline__ void lm_finish(const HsRefArgs& a, const double* R, cons
     C->optreg_prev = 0;
     C->jb_sel = sel;
     C->done = 0;
-    lm_solve(a, C);
+    lm_solve(a, C, W);
     return;
   }
   // HS_REF_ITER: calcEC + the accept test (Src/Initializer.cpp:1470-1540)
@@ -289,7 +299,7 @@ __device__ __noinline__ void lm_finish(const HsRefArgs& a, const double* R, cons
     return;
   }
   C->iteration = it + 1;
-  lm_solve(a, C);
+  lm_solve(a, C, W);
 }
 
 // one pattern pixel of calcResAndGS (Src/Initializer.cpp:1970-2039); false = the point is bad.  xv: the values the
@@ -343,10 +353,8 @@ __device__ __forceinline__ bool ref_pixel(const HsRefArgs& a, const HsRefPass& S
   } while (0)
 
 struct RefLds {
-  HsRefPass pc;
-  float inc[8];
-  float lambda;
-  int apply_prev, optreg_prev, snapped, jb_sel;
+  HsRefCtl ctl;          // the device-resident LM state, copied in at entry (the last block writes it back)
+  RefWork wk;
   float xv[RB][NX + 1];  // per-lane values for the leader's in-order fold (+1: bank padding)
   int pgood[HS_REF_PPB];
   float Jl[RB][10];      // each lane's acc9 row [J | r] (zero unless its point is good)
@@ -382,29 +390,25 @@ __global__ __launch_bounds__(RB) void hs_k_refine_step(HsRefArgs a) {
     pv = P.v[i];
     tri = P.tri[i];
   }
-  if (tid == 0) {
-    if (mode == HS_REF_CALC || mode == HS_REF_INIT) {
-      S.pc = a.pc0;
-      S.apply_prev = 0;
-      S.optreg_prev = 0;
-      S.snapped = 0;
-      S.jb_sel = a.jb_sel0;
-      S.last = 0;
-    } else {
-      S.last = C->done;  // (reused as the early-exit flag before the ticket)
-      S.pc = C->pc;
-      for (int q = 0; q < 8; q++) S.inc[q] = C->inc[q];
-      S.lambda = C->lambda;
-      S.apply_prev = C->apply_prev;
-      S.optreg_prev = C->optreg_prev;
-      S.snapped = C->snapped;
-      S.jb_sel = C->jb_sel;
-    }
+  {  // the control block into LDS: one 8-byte word per thread, one round trip
+    constexpr int CW = (int)(sizeof(HsRefCtl) / 8);
+    static_assert(sizeof(HsRefCtl) % 8 == 0, "HsRefCtl is copied as 8-byte words");
+    const uint2* gs = reinterpret_cast<const uint2*>(C);
+    uint2* ls = reinterpret_cast<uint2*>(&S.ctl);
+    for (int w = tid; w < CW; w += RB) ls[w] = gs[w];
   }
   __syncthreads();
-  if (mode == HS_REF_ITER && S.last) return;  // the LM has stopped: launches queued after it do nothing (uniform)
+  if (mode == HS_REF_ITER && S.ctl.done) return;  // the LM has stopped: launches queued after it do nothing (uniform)
+  if (tid == 0 && (mode == HS_REF_CALC || mode == HS_REF_INIT)) {
+    S.ctl.pc = a.pc0;
+    S.ctl.apply_prev = 0;
+    S.ctl.optreg_prev = 0;
+    S.ctl.snapped = 0;
+    S.ctl.jb_sel = a.jb_sel0;
+  }
+  __syncthreads();
   REF_TRACE(1);
-  const int sel = S.jb_sel ^ S.apply_prev;  // JbBuffer plane after this launch's applyStep
+  const int sel = S.ctl.jb_sel ^ S.ctl.apply_prev;  // JbBuffer plane after this launch's applyStep
   float* __restrict__ Jbn = P.jb[sel ^ 1];
   // ---- prologue (the point's leader lane): every load first (the arrays may alias as far as the compiler
   // knows, so loads after a store would serialize), then applyStep / optReg / doStep in registers
@@ -436,18 +440,18 @@ __global__ __launch_bounds__(RB) void hs_k_refine_step(HsRefArgs a) {
       e0 = eo0;
       e1 = eo1;
       float idn_w = idn_prev;
-      if (S.apply_prev) {  // applyStep (+ optReg)
+      if (S.ctl.apply_prev) {  // applyStep (+ optReg)
         if (!g_old) {
           idp = iR_old;
           idn_w = iR_old;
-          if (S.optreg_prev && !S.snapped) iR = tri ? invz : iR_old;
+          if (S.ctl.optreg_prev && !S.ctl.snapped) iR = tri ? invz : iR_old;
         } else {
           e0 = en0;
           e1 = en1;
           g = gn_prev;
           idp = idn_prev;
-          if (S.optreg_prev) {
-            if (!S.snapped) iR = tri ? invz : idp;
+          if (S.ctl.optreg_prev) {
+            if (!S.ctl.snapped) iR = tri ? invz : idp;
             else if (g) iR = idp;
           }
           P.energy[i] = e0;
@@ -460,8 +464,8 @@ __global__ __launch_bounds__(RB) void hs_k_refine_step(HsRefArgs a) {
       }
       if (mode == HS_REF_ITER && g) {  // doStep with JbBuffer = plane sel (its rows were written by a pass
         // whose point was good, which this point is)
-        const float b = jb[8] + dot8(jb, S.inc);
-        float step = -b * jb[9] / (1 + S.lambda);
+        const float b = jb[8] + dot8(jb, S.ctl.inc);
+        float step = -b * jb[9] / (1 + S.ctl.lambda);
         float maxstep = 0.25f * ms_prev;
         if (maxstep > 1e10f) maxstep = 1e10f;
         if (step > maxstep) step = maxstep;
@@ -472,7 +476,7 @@ __global__ __launch_bounds__(RB) void hs_k_refine_step(HsRefArgs a) {
         idn_w = newIdepth;
       }
       idn = idn_w;
-      if (S.apply_prev || (mode == HS_REF_ITER && g)) P.idepth_new[i] = idn;
+      if (S.ctl.apply_prev || (mode == HS_REF_ITER && g)) P.idepth_new[i] = idn;
     }
   }
   if (mode == HS_REF_FINAL) return;
@@ -484,7 +488,7 @@ __global__ __launch_bounds__(RB) void hs_k_refine_step(HsRefArgs a) {
   float J[9];
   bool ok = false;
   const bool live = valid && g;
-  if (live) ok = ref_pixel(a, S.pc, k, pu, pv, idn, tri != 0, S.xv[tid], J);
+  if (live) ok = ref_pixel(a, S.ctl.pc, k, pu, pv, idn, tri != 0, S.xv[tid], J);
   const unsigned long long failm = __ballot(live && !ok);
   const unsigned int fb = (unsigned int)(failm >> base) & 0xffu;
   const int f = fb ? __builtin_ctz(fb) : 8;  // first failing pixel: the reference's loop breaks there
@@ -503,12 +507,15 @@ __global__ __launch_bounds__(RB) void hs_k_refine_step(HsRefArgs a) {
       float energy = 0.f, maxstep = 1e10f, jb[10];
 #pragma unroll
       for (int q = 0; q < 10; q++) jb[q] = 0.f;
-      for (int kk = 0; kk < f; kk++) {
-        const float* x = S.xv[tid + kk];
-        energy += x[0];
-        if (x[1] < maxstep) maxstep = x[1];
 #pragma unroll
-        for (int q = 0; q < 10; q++) jb[q] += x[2 + q];
+      for (int kk = 0; kk < 8; kk++) {
+        if (kk < f) {
+          const float* x = S.xv[tid + kk];
+          energy += x[0];
+          if (x[1] < maxstep) maxstep = x[1];
+#pragma unroll
+          for (int q = 0; q < 10; q++) jb[q] += x[2 + q];
+        }
       }
       P.maxstep[i] = maxstep;
       if (f < 8 || energy > 8 * a.outlierTH * 20) {
@@ -521,7 +528,7 @@ __global__ __launch_bounds__(RB) void hs_k_refine_step(HsRefArgs a) {
         P.energy_new[i] = energy;
         P.energy_new[n + i] = (idn - 1) * (idn - 1);
         // acc9SC row (Src/Initializer.cpp:2114-2124)
-        const float alphaOpt = S.pc.alphaOpt;
+        const float alphaOpt = S.ctl.pc.alphaOpt;
         P.lastH_new[i] = jb[9];
         jb[8] += alphaOpt * (idn - 1);
         jb[9] += alphaOpt;
@@ -569,7 +576,9 @@ __global__ __launch_bounds__(RB) void hs_k_refine_step(HsRefArgs a) {
   if (tid < NACC * RW) {
     const int q = tid >> 2, w = tid & 3, r = kQr[q], c = kQc[q];
     float s = 0.f;
-    for (int l = w * 64; l < w * 64 + 64; l++) s += S.Jl[l][r] * S.Jl[l][c];
+    const int l0 = w * 64;
+#pragma unroll 16
+    for (int l = 0; l < 64; l++) s += S.Jl[l0 + l][r] * S.Jl[l0 + l][c];
     S.pa[q][w] = s;
   } else if (tid < NACC * RW + NACC) {
     const int q = tid - NACC * RW, r = kQr[q], c = kQc[q];
@@ -608,26 +617,33 @@ __global__ __launch_bounds__(RB) void hs_k_refine_step(HsRefArgs a) {
   __syncthreads();
   REF_TRACE(6);
   if (!S.last) return;
-  if (tid < HS_REF_NRED) {  // block order, 16 independent write-through loads in flight per thread
+  if (tid < HS_REF_NRED) {  // block order, up to 64 independent write-through loads in flight per thread
     double s = 0.0;
     const double* pp = a.part + tid;
-    int b = 0;
-    for (; b + 16 <= a.nblocks; b += 16) {
-      double t[16];
+    for (int b = 0; b < a.nblocks; b += 64) {
+      double t[64];
 #pragma unroll
-      for (int j = 0; j < 16; j++)
-        t[j] = __hip_atomic_load(pp + (size_t)(b + j) * HS_REF_NRED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int j = 0; j < 64; j++)
+        t[j] = __hip_atomic_load(pp + (size_t)min(b + j, a.nblocks - 1) * HS_REF_NRED, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
-      for (int j = 0; j < 16; j++) s += t[j];
+      for (int j = 0; j < 64; j++)
+        if (b + j < a.nblocks) s += t[j];
     }
-    for (; b < a.nblocks; b++)
-      s += __hip_atomic_load(pp + (size_t)b * HS_REF_NRED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     S.red[tid] = s;  // only this thread reads slot tid before the sum
   }
   __syncthreads();
   if (tid == 0) {
-    lm_finish(a, S.red, S.pc, sel);
+    const HsRefPass pc = S.ctl.pc;
+    lm_finish(a, &S.ctl, &S.wk, S.red, pc, sel);
     __hip_atomic_store(a.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
+  }
+  __syncthreads();
+  {  // the control block back (the next launch reads it after the kernel boundary)
+    constexpr int CW = (int)(sizeof(HsRefCtl) / 8);
+    const uint2* ls = reinterpret_cast<const uint2*>(&S.ctl);
+    uint2* gs = reinterpret_cast<uint2*>(a.ctl);
+    for (int w = tid; w < CW; w += RB) gs[w] = ls[w];
   }
   REF_TRACE(7);
 }
