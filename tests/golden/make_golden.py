@@ -14,6 +14,8 @@ Fixtures (SURVEY.md §8c list):
   ba_8x200.npz    8 KF x 200 points: the same + the energies of 3 GN iterations
   track_160.npz   CoarseTracker at 160x120: pc arrays per level, calcRes at the truth, trackNewestCoarse
   trace_100.npz   100 traceOn results: ctor outputs, first and second trace
+  refine_300.npz  DirectRefinement at 320x240, 300 keypoints: one calcResAndGS (per-point outputs, H/b/Hsc/bsc,
+                  res) and the Refine LM log + refined pose
 """
 import hashlib
 import os
@@ -48,6 +50,10 @@ def trace_scene_digest(s):
     return digest(*s.host_imgs, s.new_img, s.KRKi, s.Kt, s.aff, s.pt_host, s.pt_u, s.pt_v)
 
 
+def refine_scene_digest(s):
+    return digest(s.img1, s.img2, s.u, s.v, s.tri, s.z, s.T_init, s.K4)
+
+
 # ---------------------------------------------------------------- scenes (shared with tests/test_golden.py)
 K320 = np.array([[128.0, 0, 159.5], [0, 127.2, 119.5], [0, 0, 1.0]])
 
@@ -71,6 +77,32 @@ def scene_track160():
 def scene_trace100():
     from hslam_amd.scene import make_trace_scene
     return make_trace_scene(n_points=100, n_hosts=4, width=320, height=240, seed=104)
+
+
+def scene_refine300():
+    from hslam_amd.scene import make_refine_scene
+    return make_refine_scene(300, width=320, height=240, K=K320, seed=105)
+
+
+def refine_outputs(scene):
+    from oracle_ffi import OracleRefiner
+    o = OracleRefiner(scene)
+    H, b, Hsc, bsc, res = o.calc_res(scene.T_init)
+    out = dict(calc_H=H, calc_b=b, calc_Hsc=Hsc, calc_bsc=bsc, calc_res=res)
+    for k, v in o.points().items():
+        out["calc_" + k] = v
+    o2 = OracleRefiner(scene)
+    T, it, sn = o2.refine(scene.T_init)
+    out.update(refine_T=T, refine_iters=np.int64(it), refine_snapped=np.bool_(sn), refine_log=o2.log())
+    p = o2.points()
+    out.update(refine_idepth=p["idepth"], refine_isGood=p["isGood"])
+    return out
+
+
+def make_refine(scene):
+    out = refine_outputs(scene)
+    out["digest"] = np.array(refine_scene_digest(scene))
+    np.savez_compressed(os.path.join(OUT, "refine_300.npz"), **out)
 
 
 def ba_outputs(o):
@@ -141,6 +173,7 @@ if __name__ == "__main__":
     make_ba("ba_8x200.npz", scene_ba_8x200(), 3)
     make_track(scene_track160())
     make_trace(scene_trace100())
+    make_refine(scene_refine300())
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)), "bytes")

@@ -26,7 +26,8 @@ def _eq(a, b):
 
 @pytest.fixture(scope="module")
 def scenes():
-    return dict(pair=mg.scene_ba_pair64(), w8=mg.scene_ba_8x200(), track=mg.scene_track160(), trace=mg.scene_trace100())
+    return dict(pair=mg.scene_ba_pair64(), w8=mg.scene_ba_8x200(), track=mg.scene_track160(), trace=mg.scene_trace100(),
+                refine=mg.scene_refine300())
 
 
 # ------------------------------------------------------------------------------------------------ CPU
@@ -35,6 +36,14 @@ def test_fixture_inputs_unchanged(scenes):
     assert str(_load("ba_8x200.npz")["digest"]) == mg.ba_scene_digest(scenes["w8"])
     assert str(_load("track_160.npz")["digest"]) == mg.track_scene_digest(scenes["track"])
     assert str(_load("trace_100.npz")["digest"]) == mg.trace_scene_digest(scenes["trace"])
+    assert str(_load("refine_300.npz")["digest"]) == mg.refine_scene_digest(scenes["refine"])
+
+
+def test_oracle_reproduces_refine_fixture(scenes):
+    g = _load("refine_300.npz")
+    out = mg.refine_outputs(scenes["refine"])
+    for k, v in out.items():
+        assert _eq(v, g[k]), k
 
 
 @pytest.mark.parametrize("name,key", [("ba_pair64.npz", "pair"), ("ba_8x200.npz", "w8")])
@@ -143,3 +152,31 @@ def test_gpu_matches_trace_fixture(scenes):
         p = t.points()
         for k in ("status", "idepth_min", "idepth_max", "quality", "uv", "interval"):
             assert _eq(p[k], g[f"trace{rnd}_{k}"]), (rnd, k)
+
+
+@pytest.mark.gpu
+def test_gpu_matches_refine_fixture(scenes):
+    """per-point outputs of calcResAndGS bit-exact; H / res and the Refine trajectory at the bars of
+    tests/test_gpu_refine.py"""
+    from hslam_amd.refine import DirectRefinement
+    s, g = scenes["refine"], _load("refine_300.npz")
+    d = DirectRefinement(s)
+    H, b, Hsc, bsc, res = d.calcResAndGS(s.T_init)
+    p = d.points()
+    good = g["calc_isGood_new"] == 1
+    assert _eq(p["isGood_new"], g["calc_isGood_new"])
+    for k in ("energy_new0", "energy_new1", "maxstep"):
+        assert _eq(p[k], g["calc_" + k]), k
+    assert _eq(p["jb_new"][good], g["calc_jb_new"][good])
+    scale = 1e-4 * np.abs(np.diag(g["calc_H"])).max()
+    assert np.all(np.abs(H - g["calc_H"]) <= 1e-4 * np.abs(g["calc_H"]) + scale)
+    assert abs(res[0] - g["calc_res"][0]) <= 1e-5 * abs(g["calc_res"][0]) and res[1] == g["calc_res"][1]
+    d.set_points(s.u, s.v, s.tri, s.z)
+    T, vid, gd, it, sn = d.Refine(s.T_init)
+    from hslam_amd.se3 import SE3
+    err = float(np.linalg.norm((SE3.from_data(T) * SE3.from_data(g["refine_T"]).inverse()).log()))
+    assert err <= 2e-3
+    L = d.log()
+    n = min(len(L), len(g["refine_log"]), 3)
+    np.testing.assert_allclose(L[:n, [0, 1]], g["refine_log"][:n, [0, 1]], rtol=1e-4)
+    d.close()
