@@ -124,18 +124,18 @@ static int enqueue(hs_refiner* r, const HsRefArgs& a) {
 }
 
 static int dump_trace(hs_refiner* r, int nb, int launch_no) {
-  std::vector<long long> t((size_t)nb * 8);
+  std::vector<long long> t((size_t)nb * 16);
   RF_HIP(hipMemcpyAsync(t.data(), r->d_trace, t.size() * sizeof(long long), hipMemcpyDeviceToHost, r->stream));
   RF_HIP(hipStreamSynchronize(r->stream));
   int khz = 0;
   RF_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, r->device));
   const double us = khz > 0 ? 1e3 / khz : 0.01;
   long long t0 = t[0];
-  for (int b = 0; b < nb; b++) t0 = std::min(t0, t[(size_t)b * 8]);
-  for (int k = 0; k < 8; k++) {
+  for (int b = 0; b < nb; b++) t0 = std::min(t0, t[(size_t)b * 16]);
+  for (int k = 0; k < 16; k++) {
     std::vector<double> v;
     for (int b = 0; b < nb; b++) {
-      const long long x = t[(size_t)b * 8 + k];
+      const long long x = t[(size_t)b * 16 + k];
       if (x >= t0) v.push_back((x - t0) * us);
     }
     if (v.empty()) continue;
@@ -294,8 +294,8 @@ int hs_refiner_set_points(hs_refiner* r, int n, const float* u, const float* v, 
   (void)hipFree(r->d_trace);
   r->d_trace = nullptr;
   if (const char* e = std::getenv("HS_REF_TRACE"); e && std::atoi(e) > 0) {
-    RF_HIP(hipMalloc(&r->d_trace, sizeof(long long) * 8 * (size_t)((n + HS_REF_PPB - 1) / HS_REF_PPB)));
-    RF_HIP(hipMemset(r->d_trace, 0, sizeof(long long) * 8 * (size_t)((n + HS_REF_PPB - 1) / HS_REF_PPB)));
+    RF_HIP(hipMalloc(&r->d_trace, sizeof(long long) * 16 * (size_t)((n + HS_REF_PPB - 1) / HS_REF_PPB)));
+    RF_HIP(hipMemset(r->d_trace, 0, sizeof(long long) * 16 * (size_t)((n + HS_REF_PPB - 1) / HS_REF_PPB)));
   }
   // the ctor's Pnt set-up (Src/Initializer.cpp:1362-1382)
   std::vector<float> pf((size_t)PF_COUNT * n, 0.f);

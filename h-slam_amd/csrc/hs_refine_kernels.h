@@ -64,7 +64,7 @@ struct HsRefArgs {
   double* part;            // [nblocks][HS_REF_NRED] block partial sums
   int* ticket;
   float* log;              // [HS_REF_MAXLOG][HS_REF_LOGW]
-  long long* trace;        // [nblocks][8] wall-clock stamps (HS_REF_TRACE=1), nullable
+  long long* trace;        // [nblocks][16] wall-clock stamps (HS_REF_TRACE=1), nullable
 };
 
 __global__ void hs_k_refine_step(HsRefArgs a);

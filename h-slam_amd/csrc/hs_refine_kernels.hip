@@ -11,10 +11,13 @@
 //                reference's sequential loop, including the prefix before the first failing pixel), decides
 //                isGood_new and adds its acc9SC row (updateSingleWeighted order) and calcEC terms (:2207-2227);
 //                the lanes of good points add their pixel's 9x9 acc9 products
-//     reduction  wave xor trees -> 4 waves in fp64 -> block partials (agent-scope write-through stores) -> the
-//                last block to take the ticket sums the partials in block order (no block waits on another)
-//     LM         the last block's thread 0: the accept test, the lambda / fails / snapped bookkeeping, the fixAffine
-//                6x6 fp32 LDLT step, SE3 exp * refToNew, the next pass's constants; or done
+//     reduction  fixed-order LDS sums (acc9 over each wave's lanes, then the 4 waves; acc9SC / E / calcEC over the
+//                block's 32 points) -> block partials
+//                (agent-scope write-through stores) -> the last block to take the ticket sums the partials in block
+//                order (no block waits on another)
+//     LM         the last block: the sums unpacked by 45 threads; thread 0 the accept test and the lambda / fails /
+//                snapped bookkeeping; the block copies H -> Hm and builds the scaled 6x6 system; thread 0 the
+//                fixAffine fp32 LDLT step, SE3 exp * refToNew and the next pass's constants; or done
 //   The host enqueues launches in batches and polls `done`; launches after it return at entry.  A final launch
 //   applies the last accepted step.  Per-point state stays in HBM (structure of arrays); the
 //   JbBuffer / JbBuffer_new swap is a plane-index flip carried in the control block.
@@ -68,6 +71,11 @@ __device__ __forceinline__ float dot8(const float* a, const float* b) {
   for (int l = 0; l < 4; l++) s[l] = a[l] * b[l] + a[l + 4] * b[l + 4];
   return (s[0] + s[2]) + (s[1] + s[3]);
 }
+
+#define REF_TRACE(slot)                                                                        \
+  do {                                                                                         \
+    if (a.trace && threadIdx.x == 0) a.trace[(size_t)blockIdx.x * 16 + (slot)] = wall_clock64(); \
+  } while (0)
 
 // thread 0's LDS workspace for the LM step (dynamically indexed arrays in private memory would live in scratch)
 struct RefWork {
@@ -142,34 +150,36 @@ __device__ __forceinline__ void ldlt6f_solve(const float* __restrict__ A, const 
   for (int i = 0; i < 6; i++) x[pm[i]] = y[i];
 }
 
-// the LM step of Refine (Src/Initializer.cpp:1447-1466) from the control block's Hm / Hs / bm / bs / lambda:
-// inc, Tn = exp(inc) * T, affn and the constants of the pass at Tn
-__device__ __forceinline__ void lm_solve(const HsRefArgs& a, HsRefCtl* C, RefWork* W) {
+// the LM step of Refine (Src/Initializer.cpp:1447-1466) from the control block's Hm / Hs / bm / bs / lambda.
+// prep (threads 0..35 of the last block): Hl = H with the diagonal * (1 + lambda), minus Hsc / (1 + lambda),
+// then wM Hl wM * (0.01 / (w h)); fixAffine reads the top-left 6x6 block and the first 6 entries of bl only
+__device__ __forceinline__ void lm_solve_prep(const HsRefArgs& a, const HsRefCtl* C, RefWork* W, int t) {
   const float wM[8] = {1.0f, 1.0f, 1.0f, 0.5f, 0.5f, 0.5f, 10.0f, 1000.0f};  // SCALE_XI_ROT x3, _TRANS x3, A, B
   const float scl = 0.01f / (a.W * a.H);
   const float lambda = C->lambda;
-  float* H6 = W->H6;
-  float* bl = W->bl;
-  float* x6 = W->x6;
   const float il = 1 / (1 + lambda);
-  // Hl = H with the diagonal * (1 + lambda), minus Hsc / (1 + lambda), then wM Hl wM * (0.01 / (w h)); fixAffine
-  // reads the top-left 6x6 block and the first 6 entries of bl only
-#pragma unroll
-  for (int r = 0; r < 6; r++)
-#pragma unroll
-    for (int c = 0; c < 6; c++) {
-      float h = C->Hm[r * 8 + c];
-      if (r == c) h *= (1 + lambda);
-      h -= C->Hs[r * 8 + c] * il;
-      H6[r * 6 + c] = ((wM[r] * h) * wM[c]) * scl;
-    }
-#pragma unroll
-  for (int r = 0; r < 8; r++) bl[r] = (wM[r] * (C->bm[r] - C->bs[r] * il)) * scl;
-  ldlt6f_solve(H6, bl, x6);  // fixAffine = true
+  if (t < 36) {
+    const int r = t / 6, c = t - 6 * r;
+    float h = C->Hm[r * 8 + c];
+    if (r == c) h *= (1 + lambda);
+    h -= C->Hs[r * 8 + c] * il;
+    W->H6[t] = ((wM[r] * h) * wM[c]) * scl;
+  } else if (t < 44) {
+    const int r = t - 36;
+    W->bl[r] = (wM[r] * (C->bm[r] - C->bs[r] * il)) * scl;
+  }
+}
+
+// tail (thread 0): the 6x6 LDLT, inc, Tn = exp(inc) * T, affn and the constants of the pass at Tn
+__device__ __forceinline__ void lm_solve_tail(const HsRefArgs& a, HsRefCtl* C, RefWork* W) {
+  const float wM[6] = {1.0f, 1.0f, 1.0f, 0.5f, 0.5f, 0.5f};
+  REF_TRACE(11);
+  ldlt6f_solve(W->H6, W->bl, W->x6);  // fixAffine = true
+  REF_TRACE(12);
   double incd[6];
 #pragma unroll
   for (int k = 0; k < 6; k++) {
-    C->inc[k] = -(wM[k] * x6[k]);
+    C->inc[k] = -(wM[k] * W->x6[k]);
     incd[k] = (double)C->inc[k];
   }
   C->inc[6] = C->inc[7] = 0.f;
@@ -183,34 +193,24 @@ __device__ __forceinline__ void lm_solve(const HsRefArgs& a, HsRefCtl* C, RefWor
   double affn[2] = {C->aff[0] + C->inc[6], C->aff[1] + C->inc[7]};
   C->affn[0] = affn[0];
   C->affn[1] = affn[1];
+  REF_TRACE(13);
   HsRefPass pc;
   hs_ref_pass_consts(Tn, affn, a.Ki, a.n, &pc);
   C->pc = pc;
+  REF_TRACE(14);
 }
 
-// last block, thread 0: the pass's H / b / Hsc / bsc / res / calcEC from the reduced sums, then the mode's LM logic
-__device__ __forceinline__ void lm_finish(const HsRefArgs& a, HsRefCtl* C, RefWork* W, const double* R,
-                                          const HsRefPass& pc, int sel) {
+enum { LM_COPY = 1, LM_SOLVE = 2, LM_OUT = 4 };
+
+// last block, thread 0, after the parallel unpack of the sums into W->Hn / bn / Hsn / bsn: the alpha terms,
+// res / calcEC, and the mode's LM logic.  Returns what the block does next: LM_COPY (H -> Hm etc.), LM_OUT (the
+// single pass's H / b into the control block), LM_SOLVE (the next step)
+__device__ __forceinline__ int lm_decide(const HsRefArgs& a, HsRefCtl* C, RefWork* W, const double* R,
+                                         const HsRefPass& pc, int sel) {
   const int n = a.n;
   float* H = W->Hn;
   float* b = W->bn;
-  float* Hsc = W->Hsn;
-  float* bsc = W->bsn;
   float res[3], ec[2];
-  int q = 0;
-#pragma unroll
-  for (int r = 0; r < 9; r++)
-#pragma unroll
-    for (int c = r; c < 9; c++, q++) {
-      const float v = (float)R[q], w = (float)R[NACC + q];
-      if (c < 8) {
-        H[r * 8 + c] = H[c * 8 + r] = v;
-        Hsc[r * 8 + c] = Hsc[c * 8 + r] = w;
-      } else if (r < 8) {  // column 8 = [b; r'r]: the (8, 8) entry is not part of b
-        b[r] = v;
-        bsc[r] = w;
-      }
-    }
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     H[k * 8 + k] += pc.alphaOpt * n;
@@ -223,20 +223,12 @@ __device__ __forceinline__ void lm_finish(const HsRefArgs& a, HsRefCtl* C, RefWo
   ec[1] = hs_ref_coupling * (float)R[2 * NACC + 2];
   if (a.mode == HS_REF_CALC) {
 #pragma unroll
-    for (int k = 0; k < 64; k++) { C->H[k] = H[k]; C->Hsc[k] = Hsc[k]; }
-#pragma unroll
-    for (int k = 0; k < 8; k++) { C->b[k] = b[k]; C->bsc[k] = bsc[k]; }
-#pragma unroll
     for (int k = 0; k < 3; k++) C->res[k] = res[k];
     C->jb_sel = sel;
     C->done = 1;
-    return;
+    return LM_OUT;
   }
   if (a.mode == HS_REF_INIT) {  // the first calcResAndGS + applyStep(0) (Src/Initializer.cpp:1424-1426)
-#pragma unroll
-    for (int k = 0; k < 64; k++) { C->Hm[k] = H[k]; C->Hs[k] = Hsc[k]; }
-#pragma unroll
-    for (int k = 0; k < 8; k++) { C->bm[k] = b[k]; C->bs[k] = bsc[k]; }
 #pragma unroll
     for (int k = 0; k < 3; k++) C->resOld[k] = res[k];
 #pragma unroll
@@ -251,9 +243,9 @@ __device__ __forceinline__ void lm_finish(const HsRefArgs& a, HsRefCtl* C, RefWo
     C->optreg_prev = 0;
     C->jb_sel = sel;
     C->done = 0;
-    lm_solve(a, C, W);
-    return;
+    return LM_COPY | LM_SOLVE;
   }
+  REF_TRACE(9);
   // HS_REF_ITER: calcEC + the accept test (Src/Initializer.cpp:1470-1540)
   const int it = C->iteration;
   const float reg0 = C->snapped ? ec[0] : 0.f, reg1 = C->snapped ? ec[1] : 0.f;
@@ -273,10 +265,6 @@ __device__ __forceinline__ void lm_finish(const HsRefArgs& a, HsRefCtl* C, RefWo
   if (accept) {
     if (res[1] == hs_ref_alphaK * n) C->snapped = 1;
 #pragma unroll
-    for (int k = 0; k < 64; k++) { C->Hm[k] = H[k]; C->Hs[k] = Hsc[k]; }
-#pragma unroll
-    for (int k = 0; k < 8; k++) { C->bm[k] = b[k]; C->bs[k] = bsc[k]; }
-#pragma unroll
     for (int k = 0; k < 3; k++) C->resOld[k] = res[k];
     C->aff[0] = C->affn[0];
     C->aff[1] = C->affn[1];
@@ -294,12 +282,14 @@ __device__ __forceinline__ void lm_finish(const HsRefArgs& a, HsRefCtl* C, RefWo
   C->apply_prev = accept;
   C->optreg_prev = accept;
   C->jb_sel = sel;
+  const int cp = accept ? LM_COPY : 0;
   if (!(incNorm > 1e-4f) || it >= 1000 || fails >= 2) {
     C->done = 1;
-    return;
+    return cp;
   }
   C->iteration = it + 1;
-  lm_solve(a, C, W);
+  REF_TRACE(10);
+  return cp | LM_SOLVE;
 }
 
 // one pattern pixel of calcResAndGS (Src/Initializer.cpp:1970-2039); false = the point is bad.  xv: the values the
@@ -347,21 +337,18 @@ __device__ __forceinline__ bool ref_pixel(const HsRefArgs& a, const HsRefPass& S
   return true;
 }
 
-#define REF_TRACE(slot)                                                                        \
-  do {                                                                                         \
-    if (a.trace && threadIdx.x == 0) a.trace[(size_t)blockIdx.x * 8 + (slot)] = wall_clock64(); \
-  } while (0)
+
 
 struct RefLds {
   HsRefCtl ctl;          // the device-resident LM state, copied in at entry (the last block writes it back)
   RefWork wk;
   float xv[RB][NX + 1];  // per-lane values for the leader's in-order fold (+1: bank padding)
   int pgood[HS_REF_PPB];
-  float Jl[RB][10];      // each lane's acc9 row [J | r] (zero unless its point is good)
   float Pl[HS_REF_PPB][13];  // each point's acc9SC row (JbBuffer_new after the alpha / coupling terms), E, calcEC
+  float Jl[RB][10];      // each lane's acc9 row [J | r] (zero unless its point is good)
   float pa[NACC][RW];    // acc9 per wave
   double red[HS_REF_NRED];
-  int last;
+  int last, lmflags;
 };
 __constant__ unsigned char kQr[NACC] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 1, 2, 2, 2, 2, 2, 2, 2,
                                         3, 3, 3, 3, 3, 3, 4, 4, 4, 4, 4, 5, 5, 5, 5, 6, 6, 6, 7, 7, 8};
@@ -583,6 +570,7 @@ __global__ __launch_bounds__(RB) void hs_k_refine_step(HsRefArgs a) {
   } else if (tid < NACC * RW + NACC) {
     const int q = tid - NACC * RW, r = kQr[q], c = kQc[q];
     float s = 0.f;
+#pragma unroll 8
     for (int p = 0; p < HS_REF_PPB; p++) {
       const float* row = S.Pl[p];
       const float w = row[9];
@@ -633,11 +621,50 @@ __global__ __launch_bounds__(RB) void hs_k_refine_step(HsRefArgs a) {
     S.red[tid] = s;  // only this thread reads slot tid before the sum
   }
   __syncthreads();
-  if (tid == 0) {
-    const HsRefPass pc = S.ctl.pc;
-    lm_finish(a, &S.ctl, &S.wk, S.red, pc, sel);
-    __hip_atomic_store(a.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
+  if (tid < NACC) {  // unpack entry tid of acc9 / acc9SC into H_out / b_out / H_out_sc / b_out_sc
+    const int r = kQr[tid], c = kQc[tid];
+    const float v = (float)S.red[tid], w = (float)S.red[NACC + tid];
+    if (c < 8) {
+      S.wk.Hn[r * 8 + c] = S.wk.Hn[c * 8 + r] = v;
+      S.wk.Hsn[r * 8 + c] = S.wk.Hsn[c * 8 + r] = w;
+    } else if (r < 8) {  // column 8 = [b; r'r]: the (8, 8) entry is not part of b
+      S.wk.bn[r] = v;
+      S.wk.bsn[r] = w;
+    }
   }
+  __syncthreads();
+  if (tid == 0) {
+    REF_TRACE(8);
+    const HsRefPass pc = S.ctl.pc;
+    S.lmflags = lm_decide(a, &S.ctl, &S.wk, S.red, pc, sel);
+  }
+  __syncthreads();
+  const int fl = S.lmflags;
+  if (tid < 64) {
+    if (fl & LM_COPY) {
+      S.ctl.Hm[tid] = S.wk.Hn[tid];
+      S.ctl.Hs[tid] = S.wk.Hsn[tid];
+      if (tid < 8) {
+        S.ctl.bm[tid] = S.wk.bn[tid];
+        S.ctl.bs[tid] = S.wk.bsn[tid];
+      }
+    }
+    if (fl & LM_OUT) {
+      S.ctl.H[tid] = S.wk.Hn[tid];
+      S.ctl.Hsc[tid] = S.wk.Hsn[tid];
+      if (tid < 8) {
+        S.ctl.b[tid] = S.wk.bn[tid];
+        S.ctl.bsc[tid] = S.wk.bsn[tid];
+      }
+    }
+  }
+  __syncthreads();
+  if (fl & LM_SOLVE) {
+    lm_solve_prep(a, &S.ctl, &S.wk, tid);
+    __syncthreads();
+    if (tid == 0) lm_solve_tail(a, &S.ctl, &S.wk);
+  }
+  if (tid == 0) __hip_atomic_store(a.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
   __syncthreads();
   {  // the control block back (the next launch reads it after the kernel boundary)
     constexpr int CW = (int)(sizeof(HsRefCtl) / 8);
