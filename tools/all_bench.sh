@@ -1,0 +1,25 @@
+#!/bin/bash
+# End-of-round GPU evidence: smoke, pytest -m gpu, the headline bench + rocprof stats, every other workload's
+# bench line and the points sweep.  usage: tools/all_bench.sh TAG   (outputs under gpurun_out/TAG/)
+TAG=${1:-all}
+OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG
+mkdir -p $OUT
+cd $GRAFT_REPO_ROOT
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.txt 2>&1 || { echo "smoke failed rc=$?"; tail -30 $OUT/smoke.txt; exit 1; }
+tail -2 $OUT/smoke.txt
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.txt 2>&1
+rc=$?
+echo "pytest rc=$rc"; tail -3 $OUT/pytest_gpu.txt
+if [ $rc -gt 1 ]; then exit $rc; fi
+timeout -k 10 400 python bench.py --steps 50 --warmup 5 --cpu-seconds 8 > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed rc=$?"; tail -30 $OUT/bench.err; exit 1; }
+cat $OUT/bench.json
+for W in trace track act refine; do
+  timeout -k 10 300 python bench.py --workload $W --steps 20 --warmup 3 --cpu-seconds 8 > $OUT/bench_$W.json 2> $OUT/bench_$W.err || { echo "bench $W failed rc=$?"; tail -20 $OUT/bench_$W.err; exit 1; }
+  head -c 400 $OUT/bench_$W.json; echo
+done
+for P in 20000 200000; do
+  timeout -k 10 200 python bench.py --steps 30 --warmup 3 --no-cpu --points $P > $OUT/p$P.json 2> $OUT/p$P.err || { echo "sweep $P failed"; exit 1; }
+done
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- python3 $GRAFT_REPO_ROOT/bench.py --steps 50 --warmup 5 --no-cpu > $OUT/prof_bench.json 2> $OUT/prof_bench.err
+echo "rocprof rc=$?"
