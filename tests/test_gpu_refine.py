@@ -107,6 +107,15 @@ def test_calc_res_out_of_bounds_and_ragged():
     g.close()
 
 
+def test_calc_res_single_block():
+    """n = 7 < 32 points: one block, a partial point slot range, the last block is the only block"""
+    from hslam_amd.scene import make_refine_scene
+    s = make_refine_scene(7, seed=14)
+    g, o = _pair(s)
+    _check_pass(g, o, s.T_init)
+    g.close()
+
+
 def test_refine_matches_oracle():
     from hslam_amd.scene import make_refine_scene
     s = make_refine_scene(2000)
