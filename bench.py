@@ -38,7 +38,12 @@ def pmc_traffic(points: int, kernel: str = "hs_k_linearize"):
     made by tools/pmc.sh + tools/pmc_summary.py: separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this
     bench at the same --points).  None when no pass at this size has been committed."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    import re
+
+    def version(f):  # r01_v10 after r01_v9: numeric order of the round and version fields
+        return [int(x) for x in re.findall(r"\d+", os.path.basename(f))]
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), key=version)
     for f in reversed(files):
         try:
             d = json.load(open(f))
