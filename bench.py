@@ -309,11 +309,59 @@ def bench_refine(args):
     return res
 
 
+def bench_select(args):
+    """SURVEY §8f rank 4: PixelSelector::makeMaps (makeHists + select + the random sub-sampling) of a new
+    640x480 frame at setting_desiredPointDensity = 2000, from its raw image (the pyramid is built on the device).
+    One step = one makeMaps of a new frame id (makeHists runs every step, as for every new keyframe)."""
+    from hslam_amd.scene import make_select_frames
+    from hslam_amd.select import PixelSelector
+
+    frames = make_select_frames(3, quantize=True)
+    H, W = frames[0].shape
+    sel = PixelSelector(W, H)
+    fid = 0
+    for _ in range(max(1, args.warmup)):
+        sel.makeMapsRaw(frames[fid % 3], fid, 2000.0, want_map=False)
+        fid += 1
+    dev, n_sel = 0.0, 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        _, n_sel = sel.makeMapsRaw(frames[fid % 3], fid, 2000.0, want_map=False)
+        dev += sel.last_stats()[0]
+        fid += 1
+    dt = time.perf_counter() - t0
+    res = {
+        "metric": "frames selected/sec (PixelSelector::makeMaps, 640x480, density 2000)",
+        "value": args.steps / dt, "unit": "frames/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": dt * 1e3 / args.steps, "higher_is_better": True, "scaling": "replicas only",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": "PixelSelector::makeMaps from the raw 640x480 frame (device pyramid), 8-bit texture",
+                   "selected": n_sel, "device_ms_per_frame": dev / args.steps},
+        "cpu_baseline": None,
+    }
+    if not args.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        from oracle_ffi import PixelSelector as OracleSelector, dir_pyramid  # the CPU baseline leg only
+        pyrs = [dir_pyramid(f, 3) for f in frames]
+        o = OracleSelector(W, H, fast=True)
+        n, tt = 0, 0.0
+        while tt < args.cpu_seconds / 2 and n < 500:
+            p, g = pyrs[n % 3]
+            t1 = time.perf_counter()
+            o.makeMaps(10000 + n, p[0], g, 2000.0)
+            tt += time.perf_counter() - t1
+            n += 1
+        res["cpu_baseline"] = {"value": n / tt, "unit": "frames/s", "cores": 1, "kind": "port",
+                               "sample": f"{n} makeMaps calls from the host pyramid (the reference's selector is serial)"}
+        res["speedup_vs_cpu"] = res["value"] / res["cpu_baseline"]["value"]
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=("ba", "trace", "track", "act", "refine"), default="ba",
+    ap.add_argument("--workload", choices=("ba", "trace", "track", "act", "refine", "select"), default="ba",
                     help="ba = the headline metric (C4); trace = C5 traceOn; track = C2 CoarseTracker; "
-                         "act = point activation; refine = initializer DirectRefinement")
+                         "act = point activation; refine = initializer DirectRefinement; select = PixelSelector")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
@@ -322,7 +370,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
     if args.workload != "ba":
-        res = {"trace": bench_trace, "track": bench_track, "act": bench_act, "refine": bench_refine}[args.workload](args)
+        res = {"trace": bench_trace, "track": bench_track, "act": bench_act, "refine": bench_refine, "select": bench_select}[args.workload](args)
         print(json.dumps(res))
         return
 

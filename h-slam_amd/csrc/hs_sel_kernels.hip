@@ -160,29 +160,40 @@ __global__ __launch_bounds__(256) void hs_k_sel_hist(HsSelHistArgs a) {
 // select, pass 1: level-2 existence mask per slot and direction
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void hs_k_sel_mask(HsSelArgs a) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= a.nslots) return;
-  const SlotGeo g = slot_geo(a, s);
+  // 16 lanes per slot: lane `sub` takes the slot's rows y1 = sub, sub + 16, ...; the masks are OR-combined
+  // (order-free, so the result is the sequential loop's)
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int s = t >> 4, sub = t & 15;
+  const SlotGeo g = slot_geo(a, min(s, a.nslots - 1));
   uint32_t m = 0;
-  if (g.valid) {
-    for (int y1 = 0; y1 < g.my1; y1++)
+  if (s < a.nslots && g.valid) {
+    // every load of a pixel is unconditional (clamped index) and the tests are selects, so the loads of
+    // several pixels are in flight together instead of one dependent round trip per pixel
+    const int last = a.W * a.H - 1;
+    for (int y1 = sub; y1 < g.my1; y1 += 16) {
+#pragma unroll 4
       for (int x1 = 0; x1 < g.mx1; x1++) {
         const int xf = g.x0 + x1, yf = g.y0 + y1;
-        if (border_out(a, xf, yf)) continue;
-        const int idx = xf + a.W * yf;
+        const int idx = min(xf + a.W * yf, last);
         const float ag0 = a.g0[idx];
-        if (!(ag0 > th0_of(a, xf, yf) * a.thFactor)) continue;
-        if (!a.dirDist) {
-          m = 0xFFFFu;  // dirNorm = ag0 > 0
-          continue;
-        }
+        const float th = th0_of(a, xf, yf);
         const float dx = a.dI[a.dstride * idx + 1], dy = a.dI[a.dstride * idx + 2];
+        const bool pass = !border_out(a, xf, yf) && (ag0 > th * a.thFactor);
+        uint32_t mm;
+        if (!a.dirDist) {
+          mm = 0xFFFFu;  // dirNorm = ag0 > 0
+        } else {
+          mm = 0;
 #pragma unroll
-        for (int d = 0; d < 16; d++)
-          if (fabsf(dx * kDir[d][0] + dy * kDir[d][1]) > 0.f) m |= 1u << d;
+          for (int d = 0; d < 16; d++) mm |= (fabsf(dx * kDir[d][0] + dy * kDir[d][1]) > 0.f) ? (1u << d) : 0u;
+        }
+        m |= pass ? mm : 0u;
       }
+    }
   }
-  a.mask[s] = (uint16_t)m;
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) m |= (uint32_t)__shfl_xor((int)m, o);
+  if (sub == 0 && s < a.nslots) a.mask[s] = (uint16_t)m;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -260,72 +271,111 @@ __global__ __launch_bounds__(1024) void hs_k_sel_scan(HsSelArgs a) {
 // ------------------------------------------------------------------------------------------------
 // select, pass 3: per-level argmax with the resolved directions, map + counts
 // ------------------------------------------------------------------------------------------------
+// 4 lanes per slot, so a wave is one 4pot-block (16 slots): lane `sub` scans the slot's rows y1 = sub, sub + 4, ...
+// in traversal order; the 4 per-lane argmaxes are combined by (value, first traversal position) — the strict '>'
+// of the reference's row-major loop keeps the first maximum
+__device__ __forceinline__ void argmax4(float& v, int& i, int pos) {
+  uint64_t key = v > 0.f ? ((uint64_t)__float_as_uint(v) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)pos) : 0ull;
+#pragma unroll
+  for (int o = 1; o < 4; o <<= 1) {
+    const uint64_t ky = __shfl_xor(key, o);
+    const int iy = __shfl_xor(i, o);
+    const bool take = ky > key;
+    key = take ? ky : key;
+    i = take ? iy : i;
+  }
+  v = key ? __uint_as_float((uint32_t)(key >> 32)) : 0.f;
+  if (!key) i = -1;
+}
+
 __global__ __launch_bounds__(256) void hs_k_sel_pick(HsSelArgs a) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;  // nslots is a multiple of 16; 16-lane groups = 4pot-blocks
-  const SlotGeo g = slot_geo(a, s);
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;  // nslots is a multiple of 16; a wave = one 4pot-block
+  const int s = t >> 2, sub = t & 3;
+  const SlotGeo g = slot_geo(a, min(s, a.nslots - 1));
   const int sc = min(s, a.nslots - 1);
   const int n2 = a.n2b[sc], n3 = a.n2b[sc & ~3], n4 = a.n2b[sc & ~15];
   const int d2 = a.pattern[n2] & 0xF, d3 = a.pattern[n3] & 0xF, d4 = a.pattern[n4] & 0xF;
   const float d2x = kDir[d2][0], d2y = kDir[d2][1], d3x = kDir[d3][0], d3y = kDir[d3][1];
   const float d4x = kDir[d4][0], d4y = kDir[d4][1];
-  const bool h2 = g.valid && a.has2[sc];
+  const bool valid = s < a.nslots && g.valid;
+  const bool h2 = valid && a.has2[sc];
   float b2v = 0.f, b3v = 0.f, b4v = 0.f;
-  int b2i = -1, b3i = -1, b4i = -1;
-  if (g.valid) {
-    for (int y1 = 0; y1 < g.my1; y1++)
+  int b2i = -1, b3i = -1, b4i = -1, b2p = 0, b3p = 0, b4p = 0;
+  if (valid) {
+    // unconditional (clamped) loads and select-form updates, in traversal order (strict '>': the first maximum)
+    const int last = a.W * a.H - 1;
+    for (int y1 = sub; y1 < g.my1; y1 += 4) {
+#pragma unroll 4
       for (int x1 = 0; x1 < g.mx1; x1++) {
         const int xf = g.x0 + x1, yf = g.y0 + y1;
-        if (border_out(a, xf, yf)) continue;
-        const int idx = xf + a.W * yf;
+        const int pos = y1 * g.mx1 + x1;
+        const bool in = !border_out(a, xf, yf);
+        const int idx = min(xf + a.W * yf, last);
         const float pixelTH0 = th0_of(a, xf, yf);
         const float pixelTH1 = pixelTH0 * a.dw1;
         const float pixelTH2 = pixelTH1 * a.dw2;
         const float dx = a.dI[a.dstride * idx + 1], dy = a.dI[a.dstride * idx + 2];
         const float ag0 = a.g0[idx];
-        if (ag0 > pixelTH0 * a.thFactor) {
+        const int i1 = min((int)(xf * 0.5f + 0.25f) + (int)(yf * 0.5f + 0.25f) * a.w1, a.w1 * (a.H >> 1) - 1);
+        const int i2 = min((int)(xf * 0.25f + 0.125) + (int)(yf * 0.25f + 0.125) * a.w2, a.w2 * (a.H >> 2) - 1);
+        const float ag1 = a.g1[i1];
+        const float ag2 = a.g2[i2];
+        {
           const float dn = a.dirDist ? fabsf(dx * d2x + dy * d2y) : ag0;
-          if (dn > b2v) { b2v = dn; b2i = idx; }
+          const bool up = in && (ag0 > pixelTH0 * a.thFactor) && (dn > b2v);
+          b2v = up ? dn : b2v;
+          b2i = up ? idx : b2i;
+          b2p = up ? pos : b2p;
         }
-        const float ag1 = a.g1[(int)(xf * 0.5f + 0.25f) + (int)(yf * 0.5f + 0.25f) * a.w1];
-        if (ag1 > pixelTH1 * a.thFactor) {
+        {
           const float dn = a.dirDist ? fabsf(dx * d3x + dy * d3y) : ag1;
-          if (dn > b3v) { b3v = dn; b3i = idx; }
+          const bool up = in && (ag1 > pixelTH1 * a.thFactor) && (dn > b3v);
+          b3v = up ? dn : b3v;
+          b3i = up ? idx : b3i;
+          b3p = up ? pos : b3p;
         }
-        const float ag2 = a.g2[(int)(xf * 0.25f + 0.125) + (int)(yf * 0.25f + 0.125) * a.w2];
-        if (ag2 > pixelTH2 * a.thFactor) {
+        {
           const float dn = a.dirDist ? fabsf(dx * d4x + dy * d4y) : ag2;
-          if (dn > b4v) { b4v = dn; b4i = idx; }
+          const bool up = in && (ag2 > pixelTH2 * a.thFactor) && (dn > b4v);
+          b4v = up ? dn : b4v;
+          b4i = up ? idx : b4i;
+          b4p = up ? pos : b4p;
         }
       }
+    }
   }
+  argmax4(b2v, b2i, b2p);
+  argmax4(b3v, b3i, b3p);
+  argmax4(b4v, b4i, b4p);
+  const bool lead = sub == 0;
   // level 2: the slot's own argmax (h2 <=> b2v > 0, the same expression as hs_k_sel_mask)
-  if (h2) a.map[b2i] = 1.f;
+  if (h2 && lead) a.map[b2i] = 1.f;
   // level 3 per 2pot-block: only when none of its 4 slots selected at level 2; max value, first slot on ties
   const uint64_t key = 0xFFFFFFFFull - (uint32_t)s;
-  const uint64_t p3 = (g.valid && b3v > 0.f) ? ((uint64_t)__float_as_uint(b3v) << 32) | key : 0ull;
+  const uint64_t p3 = (valid && b3v > 0.f) ? ((uint64_t)__float_as_uint(b3v) << 32) | key : 0ull;
   uint64_t m3 = p3;
   int any2 = h2;
 #pragma unroll
-  for (int o = 1; o < 4; o <<= 1) {
+  for (int o = 4; o < 16; o <<= 1) {  // the 4 slots of the 2pot-block (4 lanes each)
     const uint64_t y = __shfl_xor(m3, o);
     m3 = y > m3 ? y : m3;
     any2 |= __shfl_xor(any2, o);
   }
   const bool sel3 = !any2 && p3 != 0ull && p3 == m3;
-  if (sel3) a.map[b3i] = 2.f;
+  if (sel3 && lead) a.map[b3i] = 2.f;
   // level 4 per 4pot-block: only when no slot selected at level 2 and no level-3 candidate appeared
-  const uint64_t p4 = (g.valid && b4v > 0.f) ? ((uint64_t)__float_as_uint(b4v) << 32) | key : 0ull;
+  const uint64_t p4 = (valid && b4v > 0.f) ? ((uint64_t)__float_as_uint(b4v) << 32) | key : 0ull;
   uint64_t m4 = p4;
   int any23 = h2 || p3 != 0ull;
 #pragma unroll
-  for (int o = 1; o < 16; o <<= 1) {
+  for (int o = 4; o < 64; o <<= 1) {  // the 16 slots of the 4pot-block: the whole wave
     const uint64_t y = __shfl_xor(m4, o);
     m4 = y > m4 ? y : m4;
     any23 |= __shfl_xor(any23, o);
   }
   const bool sel4 = !any23 && p4 != 0ull && p4 == m4;
-  if (sel4) a.map[b4i] = 4.f;
-  const uint64_t c2 = __ballot(h2), c3 = __ballot(sel3), c4 = __ballot(sel4);
+  if (sel4 && lead) a.map[b4i] = 4.f;
+  const uint64_t c2 = __ballot(h2 && lead), c3 = __ballot(sel3 && lead), c4 = __ballot(sel4 && lead);
   if ((threadIdx.x & 63) == 0) {
     if (c2) atomicAdd(&a.counts[0], __popcll(c2));
     if (c3) atomicAdd(&a.counts[1], __popcll(c3));

@@ -181,12 +181,11 @@ int run_select(hs_selector* s, const float* dI, int dstride, int pot, float thFa
   a.counts = s->d_counts;
   SL_HIP(hipMemsetAsync(s->d_map, 0, (size_t)s->W * s->H * sizeof(float), s->stream));
   SL_HIP(hipMemsetAsync(s->d_counts, 0, 4 * sizeof(int), s->stream));
-  const int grid = (a.nslots + 255) / 256;
-  hipLaunchKernelGGL(hs_k_sel_mask, dim3(grid), dim3(256), 0, s->stream, a);
+  hipLaunchKernelGGL(hs_k_sel_mask, dim3((a.nslots * 16 + 255) / 256), dim3(256), 0, s->stream, a);  // 16 lanes / slot
   SL_HIP(hipGetLastError());
   hipLaunchKernelGGL(hs_k_sel_scan, dim3(1), dim3(1024), 0, s->stream, a);
   SL_HIP(hipGetLastError());
-  hipLaunchKernelGGL(hs_k_sel_pick, dim3(grid), dim3(256), 0, s->stream, a);
+  hipLaunchKernelGGL(hs_k_sel_pick, dim3((a.nslots * 4 + 255) / 256), dim3(256), 0, s->stream, a);  // 4 lanes / slot
   SL_HIP(hipGetLastError());
   SL_HIP(hipMemcpyAsync(s->h_counts, s->d_counts, 4 * sizeof(int), hipMemcpyDeviceToHost, s->stream));
   SL_HIP(hipStreamSynchronize(s->stream));

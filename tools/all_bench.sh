@@ -13,7 +13,7 @@ echo "pytest rc=$rc"; tail -3 $OUT/pytest_gpu.txt
 if [ $rc -gt 1 ]; then exit $rc; fi
 timeout -k 10 400 python bench.py --steps 50 --warmup 5 --cpu-seconds 8 > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed rc=$?"; tail -30 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
-for W in trace track act refine; do
+for W in trace track act refine select; do
   timeout -k 10 300 python bench.py --workload $W --steps 20 --warmup 3 --cpu-seconds 8 > $OUT/bench_$W.json 2> $OUT/bench_$W.err || { echo "bench $W failed rc=$?"; tail -20 $OUT/bench_$W.err; exit 1; }
   head -c 400 $OUT/bench_$W.json; echo
 done
