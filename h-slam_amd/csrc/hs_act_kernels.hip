@@ -245,6 +245,11 @@ __device__ __forceinline__ void bfs_grow_wave(uint8_t* map, int w1, int h1, int*
   }
 }
 
+// seeds taken in one round of the greedy loop: at most kMaxSeeds (their BFS frontiers share the wave list:
+// 6 x a step-39 ring of 312 cells < HS_ACT_WAVE_LIST), pairwise at Chebyshev distance >= kSeedSep (2 x 39 + 2)
+constexpr int kMaxSeeds = 6;
+constexpr int kSeedSep = 2 * (HS_ACT_BFS_STEPS - 1) + 2;
+
 // makeDistanceMap's BFS (whole workgroup), then the selection loop (wave 0).  Inlined once per map location so
 // the LDS instance compiles to ds_* instructions.
 __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* map, int* s_n, int* wl0, int* wl1) {
@@ -283,17 +288,50 @@ __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* ma
       const unsigned long long bm = __ballot(acc);
       if (bm == 0) break;  // every remaining entry of the batch fails: they stay immature
       const int first = (int)__builtin_ctzll(bm);
-      if (lane <= first) pend = false;
-      if (lane == first) {
-        a.toopt[nt] = pt;
-        lower_cell(map, cidx, 0);  // addIntoDistFinal: the cell becomes 0 even when it already was
-        wl0[0] = cell;
+      // The first passing entry is taken, as in the reference.  Later passing entries of the batch are taken in
+      // the same round while each is provably unaffected by the round's earlier seeds: at Chebyshev distance
+      // >= kSeedSep from all of them (their addIntoDistFinal BFS regions, radius <= 39, are disjoint, so one
+      // multi-seed BFS leaves the map the sequential BFS passes leave) and with cheb + frac >= thr (a BFS
+      // distance is >= the Chebyshev distance, so its own test still passes after those seeds).  Entries that
+      // fail now stay failing (the map only decreases); the first passing entry that is not provably
+      // unaffected ends the round.
+      unsigned long long take = 1ull << first;
+      {
+        int sc[kMaxSeeds];
+        sc[0] = __shfl(cell, first);
+        int ns = 1;
+        unsigned long long rest = bm & ~((2ull << first) - 1ull);
+        while (rest && ns < kMaxSeeds) {
+          const int c = (int)__builtin_ctzll(rest);
+          const int cc = __shfl(cell, c);
+          const float cf = __shfl(frac, c), ct = __shfl(thr, c);
+          bool ok = true;
+          for (int q = 0; q < ns; q++) {
+            const int ddx = abs((cc & 0xffff) - (sc[q] & 0xffff)), ddy = abs((cc >> 16) - (sc[q] >> 16));
+            const int ch = ddx > ddy ? ddx : ddy;
+            ok = ok && ch >= kSeedSep && ((float)ch + cf >= ct);
+          }
+          if (!ok) break;
+          sc[ns++] = cc;
+          take |= 1ull << c;
+          rest &= rest - 1ull;
+        }
       }
-      nt++;
+      if (lane <= first) pend = false;
+      const bool mine = (take >> lane) & 1ull;
+      if (mine) {
+        pend = false;
+        const int rank = (int)__popcll(take & ((1ull << lane) - 1ull));
+        a.toopt[nt + rank] = pt;
+        lower_cell(map, cidx, 0);  // addIntoDistFinal: the cell becomes 0 even when it already was
+        wl0[rank] = cell;
+      }
+      const int ntake = (int)__popcll(take);
+      nt += ntake;
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
       const long long c0 = a.prof ? wall_clock64() : 0;
-      bfs_grow_wave(map, a.w1, a.h1, wl0, wl1, 1, cnt);
+      bfs_grow_wave(map, a.w1, a.h1, wl0, wl1, ntake, cnt);
       if (a.prof) cnt[2] += wall_clock64() - c0;
     }
   }
