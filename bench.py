@@ -368,6 +368,9 @@ def main():
     ap.add_argument("--points", type=int, default=2000, help="active points per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--phase-events", type=int, default=0, choices=(0, 1, 2),
+                    help="HIP event pairs inside the timed GN loop (HS_EVENT_TIMING): 0 none (default; each pair "
+                         "adds ~2 us per step), 1 linearize only, 2 every phase")
     args = ap.parse_args()
     if args.workload != "ba":
         res = {"trace": bench_trace, "track": bench_track, "act": bench_act, "refine": bench_refine, "select": bench_select}[args.workload](args)
@@ -384,6 +387,9 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
+    # the timed loop carries no instrumentation unless asked: the roofline's launch duration comes from
+    # hs_ba_time_linearize's back-to-back launches, the phase split from rocprof or --phase-events
+    os.environ["HS_EVENT_TIMING"] = str(args.phase_events)
     from hslam_amd.ba import BAWindow
     from hslam_amd.scene import make_ba_scene
 
@@ -422,7 +428,8 @@ def main():
         n_res_total = int(nr.item())
     tim = ba.timings()
     nt = max(1, tim["timed_iters"])
-    lin_loop_ms = tim["linearize_ms"] / nt  # per-launch event pairs inside the GN loop (+~3 us event overhead)
+    # per-launch event pairs inside the GN loop (+~3 us event overhead); None without --phase-events
+    lin_loop_ms = tim["linearize_ms"] / nt if tim["timed_iters"] > 0 else None
     # the same kernel, same inputs, launched back to back between one event pair: the launch duration
     # rocprofv3 reports (the in-loop pairs add the event-record overhead to a ~9 us kernel)
     lin_ms = ba.time_linearize(max(64, args.steps))
@@ -465,10 +472,10 @@ def main():
             "avg_launch_ms_in_loop_events": lin_loop_ms,
             "timing": "HIP events on the context stream around back-to-back hs_k_linearize launches",
         },
-        "phase_ms_per_step": {  # per-phase split: HS_EVENT_TIMING=2 (default times the linearize kernel only)
-            "solve_step_kernel": tim["solve_ms"] / nt,
+        "phase_ms_per_step": {  # per-phase split: --phase-events 2 (1 times the linearize kernel only)
+            "solve_step_kernel": tim["solve_ms"] / nt if args.phase_events >= 2 else None,
             "linearize_kernel": lin_loop_ms,
-            "accumulate_stitch": tim["acc_stitch_ms"] / nt,
+            "accumulate_stitch": tim["acc_stitch_ms"] / nt if args.phase_events >= 2 else None,
             "event_timed_steps": tim["timed_iters"],
         },
         "cpu_baseline": None,
