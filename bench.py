@@ -2,13 +2,14 @@
 """bench.py — point-residuals/s of H-SLAM's windowed photometric BA on MI355X.
 
 Workload (BASELINE.json configs[3], "C4"): full windowed photometric BA including the
-Schur complement, 8 keyframes x 2000 active points per GPU, 640x480 synthetic scene
-(hslam_amd.scene, seed 20261015), ~13.6k point-residuals per GPU.  One *step* = one
+Schur complement, 8 keyframes x 2000 active points, 640x480 synthetic scene
+(hslam_amd.scene, seed 20261015), ~13.6k point-residuals.  One *step* = one
 Gauss-Newton iteration of System::optimize (solveSystemF + doStepFromBackup +
-linearizeAll + applyRes), i.e. hs_ba_iterate(1).  Multi-GPU: one rank per GPU, every
-rank holds its own 2000-point shard of a (2000 x N)-point window over the same 8 KFs
-("weak" scaling); per step one RCCL all-reduce of the stitched 68x68 system and one
-all-gather of the newest-frame energies.
+linearizeAll + applyRes + the accumulations), i.e. hs_ba_iterate(1).  Multi-GPU: one rank
+per GPU; by default the metric's own 2000-point window is sharded over the ranks (p % N,
+"strong" scaling); --scaling weak gives every rank its own 2000 points.  Per
+step one RCCL all-reduce of the stitched system and one all-gather of the newest-frame
+energies.  --workload ba-kitti runs the same window at KITTI 1232x368 (C5's BA half).
 
 JSON line fields follow the driver contract; `roofline` is for the dominant kernel
 (hs_k_linearize, timed with HIP events on the context's own stream), `cpu_baseline` is
@@ -54,41 +55,75 @@ def pmc_traffic(points: int, kernel: str = "hs_k_linearize"):
     return None, None
 
 
-def cpu_baseline(points: int, seconds: float):
-    """Oracle (C++ restatement of the reference CPU path, -O2 -march=x86-64-v3) on this host."""
+def host_cpu():
+    """Model name of the timing host's CPU (lscpu's 'Model name', read from /proc/cpuinfo) and its logical CPUs."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return model, os.cpu_count()
+
+
+def cpu_baseline(points: int, seconds: float, kitti: bool = False):
+    """Oracle (C++ restatement of the reference CPU path) on this host, built -O2 -march=native here (the
+    reference's flags, CMakeLists.txt:56 + build.sh:4,64; falls back to the portable x86-64-v3 build if the native
+    build fails).  Timed twice: with an IndexThreadReduce-style pool of T threads (T = the host threads this job
+    may use) and single-threaded."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from oracle_ffi import OracleBA  # test infrastructure: the CPU baseline leg only
-    from hslam_amd.scene import make_ba_scene
+    from hslam_amd.scene import make_ba_scene, make_ba_scene_kitti
 
     threads = os.cpu_count() or 1
     env_t = os.environ.get("OMP_NUM_THREADS")
     if env_t and env_t.isdigit():
         threads = min(threads, int(env_t))
-    scene = make_ba_scene(n_points=points)
-    o = OracleBA(scene, nthreads=threads, fast=True)
-    o.linearize_all(reset=True)
-    o.apply_res()
-    o.iterate(0, 3)  # warm-up
-    it, t = 0, 0.0
-    per = []
-    while t < seconds:
-        t0 = time.perf_counter()
-        o.iterate(3 + it, 1)
-        dt = time.perf_counter() - t0
-        per.append(dt)
-        t += dt
-        it += 1
-    per.sort()
-    med = per[len(per) // 2]
+    flags = "-O2 -march=native"
+    try:
+        import oracle_ffi
+        oracle_ffi.load("native")
+        build = "native"
+    except Exception:  # no compiler on this host: the portable build
+        build, flags = True, "-O2 -march=x86-64-v3"
+    scene = make_ba_scene_kitti(points) if kitti else make_ba_scene(n_points=points)
+
+    def timed(nthreads, budget):
+        o = OracleBA(scene, nthreads=nthreads, fast=build)
+        o.linearize_all(reset=True)
+        o.apply_res()
+        o.iterate(0, 3)  # warm-up
+        it, t, per = 0, 0.0, []
+        while t < budget:
+            t0 = time.perf_counter()
+            o.iterate(3 + it, 1)
+            dt = time.perf_counter() - t0
+            per.append(dt)
+            t += dt
+            it += 1
+        per.sort()
+        return scene.n_res * it / t, it, per[len(per) // 2]
+
+    v_mt, n_mt, med_mt = timed(threads, seconds * 2 / 3)
+    v_1, n_1, med_1 = timed(1, seconds / 3)
+    model, ncpu = host_cpu()
+    cfg = "C5 BA window (8 KF x %d pts, KITTI 1232x368)" % points if kitti else "C4 window (8 KF x %d pts)" % points
     return {
-        "value": scene.n_res * it / t,
+        "value": v_mt,
         "unit": "point-residuals/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{it} GN iterations of the C4 window (8 KF x {points} pts, {scene.n_res} residuals) after 3 warm-up "
-                  f"iterations, IndexThreadReduce-style pool with {threads} threads (chunk 50 / ceil(n/T)); "
-                  f"median iteration {med * 1e3:.2f} ms",
-        "median_ms_per_step": med * 1e3,
+        "sample": f"{n_mt} GN iterations of the {cfg}, {scene.n_res} residuals, after 3 warm-up iterations, "
+                  f"IndexThreadReduce-style pool with {threads} threads (chunk 50 / ceil(n/T)); median iteration "
+                  f"{med_mt * 1e3:.2f} ms; oracle built {flags} on this host",
+        "median_ms_per_step": med_mt * 1e3,
+        "single_thread": {"value": v_1, "iterations": n_1, "median_ms_per_step": med_1 * 1e3},
+        "host_cpu_model": model,
+        "host_logical_cpus": ncpu,
+        "build_flags": flags,
     }
 
 
@@ -359,20 +394,26 @@ def bench_select(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=("ba", "trace", "track", "act", "refine", "select"), default="ba",
-                    help="ba = the headline metric (C4); trace = C5 traceOn; track = C2 CoarseTracker; "
-                         "act = point activation; refine = initializer DirectRefinement; select = PixelSelector")
+    ap.add_argument("--workload", choices=("ba", "ba-kitti", "trace", "track", "act", "refine", "select"),
+                    default="ba",
+                    help="ba = the headline metric (C4, 640x480); ba-kitti = C5's BA half (KITTI 1232x368, 5 levels); "
+                         "trace = C5 traceOn; track = C2 CoarseTracker; act = point activation; refine = initializer "
+                         "DirectRefinement; select = PixelSelector")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--points", type=int, default=2000, help="active points per GPU")
+    ap.add_argument("--points", type=int, default=2000,
+                    help="active points of the window (strong scaling) or per GPU (--scaling weak)")
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
+                    help="strong (default): the metric's own 8 KF x --points window sharded over the GPUs; "
+                         "weak: --points per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--phase-events", type=int, default=0, choices=(0, 1, 2),
-                    help="HIP event pairs inside the timed GN loop (HS_EVENT_TIMING): 0 none (default; each pair "
-                         "adds ~2 us per step), 1 linearize only, 2 every phase")
+    ap.add_argument("--phase-events", type=int, default=None, choices=(0, 1, 2),
+                    help="HIP event pairs inside the timed GN loop (sets HS_EVENT_TIMING; default: the environment's "
+                         "value, else 0 = none; each pair adds ~2 us per step), 1 linearize only, 2 every phase")
     args = ap.parse_args()
-    if args.workload != "ba":
+    if args.workload not in ("ba", "ba-kitti"):
         res = {"trace": bench_trace, "track": bench_track, "act": bench_act, "refine": bench_refine, "select": bench_select}[args.workload](args)
         print(json.dumps(res))
         return
@@ -389,11 +430,15 @@ def main():
 
     # the timed loop carries no instrumentation unless asked: the roofline's launch duration comes from
     # hs_ba_time_linearize's back-to-back launches, the phase split from rocprof or --phase-events
-    os.environ["HS_EVENT_TIMING"] = str(args.phase_events)
+    if args.phase_events is not None:
+        os.environ["HS_EVENT_TIMING"] = str(args.phase_events)
+    args.phase_events = int(os.environ.get("HS_EVENT_TIMING", "0") or 0)
     from hslam_amd.ba import BAWindow
-    from hslam_amd.scene import make_ba_scene
+    from hslam_amd.scene import make_ba_scene, make_ba_scene_kitti
 
-    scene = make_ba_scene(n_points=args.points * world)
+    kitti = args.workload == "ba-kitti"
+    n_window = args.points * world if args.scaling == "weak" else args.points
+    scene = make_ba_scene_kitti(n_window) if kitti else make_ba_scene(n_points=n_window)
     shard = scene.shard(rank, world) if world > 1 else scene
     comm = None
     if world > 1:
@@ -434,7 +479,15 @@ def main():
     # rocprofv3 reports (the in-loop pairs add the event-record overhead to a ~9 us kernel)
     lin_ms = ba.time_linearize(max(64, args.steps))
     achieved = BYTES_PER_PRES * shard.n_res / (lin_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(args.points) if world == 1 else (None, None)
+    traffic, traffic_src = pmc_traffic(args.points) if world == 1 and not kitti else (None, None)
+    if kitti:
+        wl = ("C5 BA half (BASELINE.json configs[4]): full windowed photometric BA incl. Schur complement, 8 KF x "
+              f"{n_window} pts, KITTI 1232x368, 5 pyramid levels")
+    else:
+        wl = ("C4 (BASELINE.json configs[3]): full windowed photometric BA incl. Schur complement, 8 KF x "
+              f"{n_window} pts, 640x480, 4 pyramid levels")
+    wl += (f", {args.scaling} scaling over {world} GPU(s) ({shard.n_points} pts on rank {rank}); GN step = "
+           "solve+step+linearize+accumulate (fp32 residuals, fp64 stitch/solve)")
     result = {
         "metric": METRIC,
         "value": n_res_total * args.steps / dt,
@@ -444,16 +497,15 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": dt * 1e3 / args.steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic",
         "config": {
-            "workload": "C4 (BASELINE.json configs[3]): full windowed photometric BA incl. Schur complement, "
-                        f"8 KF x {args.points} pts per GPU, 640x480, 4 pyramid levels, GN step = solve+step+"
-                        "linearize (fp32 residuals, fp64 stitch/solve)",
+            "workload": wl,
             "frames": shard.n_frames,
-            "points_per_gpu": args.points,
+            "points": n_window,
+            "points_per_gpu": shard.n_points,
             "point_residuals": n_res_total,
             "parallelism": f"point-shard x{world}",
         },
@@ -481,7 +533,7 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
-        result["cpu_baseline"] = cpu_baseline(args.points, args.cpu_seconds)
+        result["cpu_baseline"] = cpu_baseline(n_window, args.cpu_seconds, kitti)
         result["speedup_vs_cpu"] = result["value"] / result["cpu_baseline"]["value"]
     ba.close()
     if rank == 0:

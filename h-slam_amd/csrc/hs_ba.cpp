@@ -70,7 +70,7 @@ struct hs_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   std::vector<hipEvent_t> ev;  // 4 per timed iteration
-  int events = 1;              // HS_EVENT_TIMING: 0 none, 1 linearize kernel only (default), 2 every phase
+  int events = 0;              // HS_EVENT_TIMING: 0 none (default), 1 linearize kernel only, 2 every phase
 
   // window (host side)
   int nF = 0, nP = 0, nR = 0, S = 1, W = 4, maxPtsPerBlock = 0;
@@ -245,7 +245,7 @@ static int launch_linearize(hs_ctx* c, int fuse, bool marg = false) {
 
 // all-gather of newest-frame candidates, accumulate, stitch, all-reduce of the systems
 static int launch_reduce(hs_ctx* c, bool skip_threshold = false) {
-  if (c->comm && c->nranks > 1)
+  if (c->comm)
     HS_NCCL(ncclAllGather(c->d_cand + (size_t)c->rank * c->cand_stride, c->d_cand, c->cand_stride, ncclFloat,
                           c->comm, c->stream));
   HsAccArgs a;
@@ -275,7 +275,7 @@ static int launch_reduce(hs_ctx* c, bool skip_threshold = false) {
     HS_HIP(hipMemsetAsync(a.trace, 0, sizeof(long long) * 16 * (c->nF * c->nF * c->S + 3), c->stream));
   hipLaunchKernelGGL(hs_k_accumulate, dim3(c->nF * c->nF * c->S + 3), dim3(256), 0, c->stream, a);
   HS_HIP(hipGetLastError());
-  if (c->comm && c->nranks > 1)
+  if (c->comm)
     HS_NCCL(ncclAllReduce(c->d_sys, c->d_sys, c->sys_len(), ncclDouble, ncclSum, c->comm, c->stream));
   return HS_OK;
 }
@@ -512,7 +512,7 @@ int hs_create(hs_ctx** out, const hs_params* params, int device_id) {
   else hs_params_default(&c->P);
   c->device = device_id;
   const char* ev = std::getenv("HS_EVENT_TIMING");
-  c->events = ev ? std::atoi(ev) : 1;
+  c->events = ev ? std::atoi(ev) : 0;
   if (hipSetDevice(device_id) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc((void**)&c->h_state, sizeof(HsDevState)) != hipSuccess ||
       hipHostMalloc((void**)&c->h_ctl, 8 * sizeof(int)) != hipSuccess) {
@@ -654,7 +654,7 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
 
   // ---- candidate buffer stride: the same on every rank (max point count)
   c->cand_stride = nP > 0 ? nP : 1;
-  if (c->comm && c->nranks > 1) {
+  if (c->comm) {
     int* d_tmp = nullptr;
     HS_TRY(dalloc(&d_tmp, 1));
     HS_HIP(hipMemcpy(d_tmp, &c->cand_stride, sizeof(int), hipMemcpyHostToDevice));
@@ -801,7 +801,10 @@ int hs_ba_do_step(hs_ctx* c, int* canbreak_out) {
 
 int hs_ba_optimize(hs_ctx* c, int max_iters, int allow_break, double* energies_out, int* iters_done) {
   if (!c || c->nF == 0) return fail(HS_ERR_STATE, "no window");
+  if (max_iters < 0) return fail(HS_ERR_INVALID, "max_iters < 0");
   HS_HIP(hipSetDevice(c->device));
+  // energies_out holds max_iters + 1 entries (hs_ba.h) whatever the override below runs
+  const int cap = max_iters + 1;
   // System::optimize: two sequential overrides, so a 2- or 3-frame window runs 15 iterations
   if (c->nF < 3) max_iters = 20;
   if (c->nF < 4) max_iters = 15;
@@ -817,7 +820,7 @@ int hs_ba_optimize(hs_ctx* c, int max_iters, int allow_break, double* energies_o
     HS_HIP(hipMemcpy(&e[0], c->sysE(), sizeof(double), hipMemcpyDeviceToHost));
   }
   c->t_wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  if (energies_out) std::memcpy(energies_out, e.data(), sizeof(double) * (done + 1));
+  if (energies_out) std::memcpy(energies_out, e.data(), sizeof(double) * std::min(done + 1, cap));
   if (iters_done) *iters_done = done;
   return HS_OK;
 }

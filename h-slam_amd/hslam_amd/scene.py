@@ -400,6 +400,17 @@ def make_ba_scene(n_points: int = 2000, n_frames: int = 8, width: int = 640, hei
         res_point=rp, res_target=rt, planes=planes)
 
 
+KITTI_W, KITTI_H = 1232, 368   # Extras/Calib/Kitti00to02.yaml output size
+
+
+def make_ba_scene_kitti(n_points: int = 2000, n_frames: int = 8, seed: int = SEED) -> BAScene:
+    """C5's BA half (BASELINE.json configs[4]): the C4 window at KITTI 1232x368, 5 pyramid levels, fx = fy =
+    718.856.  The pose / depth perturbations are the C4 ones scaled by the focal-length ratio (256 / 718.9), so
+    the initial pixel errors, and with them the IN / OUT mix of the first linearization, match C4's."""
+    return make_ba_scene(n_points=n_points, n_frames=n_frames, width=KITTI_W, height=KITTI_H, seed=seed,
+                         kitti=True, pose_noise=(0.0015, 0.0007), idepth_noise=0.004)
+
+
 def render_depth_at(planes, K, R_c2w, C, pix):
     """Depth (camera Z) of the visible surface at integer pixels (y, x)."""
     ys = pix[:, 0].astype(np.float64)

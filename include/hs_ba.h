@@ -64,7 +64,9 @@ int hs_ba_solve_system(hs_ctx* ctx, int iteration, double* x_out);
 /* doStepFromBackup with all step factors 1; canbreak_out nullable. */
 int hs_ba_do_step(hs_ctx* ctx, int* canbreak_out);
 
-/* System::optimize loop: energies_out[max_iters+1] nullable, iters_done nullable. */
+/* System::optimize loop.  Windows of fewer than 4 frames run 15 iterations whatever max_iters says (the
+   reference's override, Src/FullSystemOptimize.cpp:366-367); energies_out (nullable) receives at most
+   max_iters + 1 energies, iters_done (nullable) the number of iterations actually run. */
 int hs_ba_optimize(hs_ctx* ctx, int max_iters, int allow_break, double* energies_out, int* iters_done);
 
 /* n_iters GN iterations (solve + step + linearize) continuing from the current linearization,
@@ -105,7 +107,7 @@ int hs_ba_marginalize_frame(hs_ctx* ctx, int frame, double* HM_out, double* bM_o
 /* device-event timing of the last hs_ba_optimize / hs_ba_iterate (ms, summed over the timed iterations):
    [0] linearize kernel, [1] accumulate + stitch (+ RCCL exchange), [2] solve + step kernel,
    [3] number of event-timed iterations, [4] total GN loop wall (host clock), [5] iterations.
-   Env HS_EVENT_TIMING: 1 (default) times the linearize kernel only, 2 every phase, 0 none. */
+   Env HS_EVENT_TIMING: 0 (default) none, 1 times the linearize kernel only, 2 every phase. */
 int hs_ba_get_timings(hs_ctx* ctx, double* out6);
 
 /* Roofline timing: reps back-to-back launches of the linearize kernel (no fused point step) on the

@@ -61,12 +61,22 @@ def build(quiet=True):
 _LIBS = {}
 
 
+def build_native():
+    """-O2 -march=native build for the timed CPU baseline, compiled on the host that times it."""
+    r = subprocess.run(["make", "-C", HERE, "-j8", "native"], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("oracle native build failed:\n" + r.stdout + r.stderr)
+
+
 def load(fast=False):
-    name = "liboracle_fast.so" if fast else "liboracle.so"
+    """fast=False: the parity oracle (-ffp-contract=off); True: portable -march=x86-64-v3; "native": -march=native."""
+    name = {False: "liboracle.so", True: "liboracle_fast.so", "native": "liboracle_native.so"}[fast]
     if name in _LIBS:
         return _LIBS[name]
     path = os.path.join(BUILD, name)
-    if not os.path.exists(path):
+    if fast == "native":
+        build_native()  # make: a no-op when current
+    elif not os.path.exists(path):
         build()
     lib = C.CDLL(path)
     vp = C.c_void_p

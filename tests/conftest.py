@@ -26,6 +26,20 @@ def scene_small():
 
 
 @pytest.fixture(scope="session")
+def scene_kitti2k():
+    """C5 BA (BASELINE configs[4]): 8 KF x 2000 points at KITTI 1232x368, 5 levels."""
+    from hslam_amd.scene import make_ba_scene_kitti
+    return make_ba_scene_kitti(2000)
+
+
+@pytest.fixture(scope="session")
+def scene_kitti20k():
+    """C5 BA at the trace size: 8 KF x 20000 points at KITTI 1232x368."""
+    from hslam_amd.scene import make_ba_scene_kitti
+    return make_ba_scene_kitti(20000)
+
+
+@pytest.fixture(scope="session")
 def scene_marg():
     """A nearly converged small window (most residuals IN at the first linearization): marginalization tests."""
     from hslam_amd.scene import make_ba_scene

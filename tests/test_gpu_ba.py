@@ -45,7 +45,7 @@ def _close_b(bg, bo, Ho, tol=H_TOL):
     return bool(np.all(err <= bound)), float((err / np.maximum(bound, 1e-300)).max())
 
 
-@pytest.mark.parametrize("scene_name", ["scene_small", "scene2k"])
+@pytest.mark.parametrize("scene_name", ["scene_small", "scene2k", "scene_kitti2k", "scene_kitti20k"])
 def test_linearize_bit_exact(scene_name, request):
     scene = request.getfixturevalue(scene_name)
     g, o = _pair(scene)
@@ -64,7 +64,7 @@ def test_linearize_bit_exact(scene_name, request):
     assert np.array_equal(g.frames()["energyTH"], o.frames()["energyTH"])
 
 
-@pytest.mark.parametrize("scene_name", ["scene_small", "scene2k"])
+@pytest.mark.parametrize("scene_name", ["scene_small", "scene2k", "scene_kitti2k", "scene_kitti20k"])
 def test_accumulate_systems(scene_name, request):
     scene = request.getfixturevalue(scene_name)
     g, o = _pair(scene)
@@ -180,8 +180,11 @@ def test_marginalize_frame(scene_marg, frame):
     np.testing.assert_allclose(bg, bo, rtol=1e-8, atol=1e-10 * np.abs(bo).max())
 
 
-def test_optimize_trajectory(scene2k):
-    g, o = _pair(scene2k)
+@pytest.mark.parametrize("scene_name", ["scene2k", "scene_kitti2k"])
+def test_optimize_trajectory(scene_name, request):
+    """System::optimize(6) (Src/FullSystemOptimize.cpp:362-494) on the C4 window and on C5's BA half (KITTI
+    1232x368, 5 levels): energies along the trajectory, final frame states and point depths."""
+    g, o = _pair(request.getfixturevalue(scene_name))
     ng, eg = g.optimize(6)
     no, eo = o.optimize(6)
     assert ng == no == 6
@@ -232,3 +235,62 @@ def test_split_accumulation_matches_threaded_reference(scene2k):
     dev_gpu = np.abs(eg - e1) / np.abs(e1)
     assert dev_gpu[0] <= 1e-9
     assert np.all(dev_gpu <= np.maximum(10 * dev_pool, 1e-3))
+
+
+def test_runs_are_bit_reproducible(scene2k):
+    """Two production-partitioned runs (no HS_ACC_EXACT) on the same inputs: identical systems, steps, energies
+    and frame states, bit for bit (fixed-order reductions, no order-dependent atomics)."""
+    from hslam_amd.ba import BAWindow
+    outs = []
+    for _ in range(2):
+        g = BAWindow(scene2k)
+        g.linearizeAll(reset=True)
+        H0, b0 = g.system(0)
+        H2, b2 = g.system(2)
+        x = g.solveSystem(0)
+        g.doStepFromBackup()
+        g.linearizeAll()
+        e = g.iterate(1, 4)
+        outs.append((H0, b0, H2, b2, x, e, g.frames()["state"], g.points()["idepth"]))
+        g.close()
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b)
+
+
+def test_single_rank_communicator_matches_plain(scene_small):
+    """The RCCL path of the library on a 1-rank communicator (hs_comm_init(ctx, id, 0, 1)): the candidate
+    all-gather, the system all-reduce and the stride agreement are enqueued every iteration and must leave the
+    results bit-identical to the communicator-free window."""
+    import os
+    from hslam_amd.ba import BAWindow
+    os.environ["HS_ACC_EXACT"] = "1"
+    try:
+        plain = BAWindow(scene_small)
+        uid = BAWindow.comm_unique_id()
+        ranked = BAWindow(scene_small, comm=(uid, 0, 1))
+    finally:
+        os.environ.pop("HS_ACC_EXACT", None)
+    res = []
+    for g in (plain, ranked):
+        n, e = g.optimize(6)
+        res.append((e, g.frames()["state"], g.frames()["energyTH"], g.points()["idepth"], g.system(0)[0]))
+    for a, b in zip(*res):
+        assert np.array_equal(a, b)
+    plain.close()
+    ranked.close()
+
+
+def test_optimize_energies_buffer_is_bounded():
+    """hs_ba_optimize on a 3-frame window (15 iterations, the reference's override) writes at most max_iters + 1
+    energies into the caller's buffer (include/hs_ba.h), whatever it runs."""
+    import ctypes as C
+    from hslam_amd.ba import BAWindow
+    from hslam_amd._lib import check
+    from hslam_amd.scene import make_ba_scene
+    g = BAWindow(make_ba_scene(n_points=96, n_frames=3, seed=3))
+    guard = np.full(7 + 16, 1234.5)
+    done = C.c_int()
+    check(g.lib.hs_ba_optimize(g.h, 6, 0, guard.ctypes.data_as(C.c_void_p), C.byref(done)))
+    assert done.value == 15
+    assert np.all(np.isfinite(guard[:7])) and np.all(guard[7:] == 1234.5)
+    g.close()
