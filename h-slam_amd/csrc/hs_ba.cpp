@@ -1,9 +1,9 @@
 // hs_ba.cpp — C-ABI implementation (include/hs_ba.h): context, device memory and the
 // device-resident GN loop of System::optimize.  The window state (frames, calib, precalc,
 // systems, steps) lives in HBM between iterations; one GN iteration is the launch sequence
-//   hs_k_solve(SOLVE|APPLY) -> hs_k_linearize(fused point step) -> [all-gather]
-//   -> hs_k_accumulate (+ fused per-pair stitch) -> [all-reduce]
-// with no host synchronisation.  The host only prepares the window (adjoints, nullspace
+//   hs_k_solve(SOLVE|APPLY) -> hs_k_lin (fused point step, linearize, per-lane accumulation, block partials)
+//   -> [all-gather] -> hs_k_reduce (per-host fixed-order sums + per-host stitch) -> [combine + all-reduce]
+// with no host synchronisation and no order-dependent atomics (bit-reproducible).  The host only prepares the window (adjoints, nullspace
 // projector, initial precalc — the reference's once-per-window Eigen/Sophus work) and reads
 // results back.  Compiled by hipcc as HIP together with hs_ba_kernels.hip; no torch, no Eigen.
 #include <hip/hip_runtime.h>
@@ -36,7 +36,7 @@ int fail(int code, const std::string& msg) {
 
 constexpr int kLogCap = 4096;     // energies logged on the device per optimize / iterate call
 constexpr int kEventIters = 128;  // iterations timed with HIP events per call
-constexpr int kPointsPerSplit = 64;  // points per accumulate workgroup (env HS_ACC_SPLIT_POINTS)
+constexpr int kLinBlocksTarget = 512;  // linearize blocks of a window (points per wave grows beyond that)
 }  // namespace
 
 #define HS_HIP(x)                                                                                  \
@@ -73,7 +73,13 @@ struct hs_ctx {
   int events = 0;              // HS_EVENT_TIMING: 0 none (default), 1 linearize kernel only, 2 every phase
 
   // window (host side)
-  int nF = 0, nP = 0, nR = 0, S = 1, W = 4, maxPtsPerBlock = 0;
+  int nF = 0, nP = 0, nR = 0;
+  // hs_k_lin partitioning: blk_begin[h] = first block of host h; W waves per block take points; exact: one wave
+  // per host in point order (HS_ACC_EXACT=1, the single-thread reference's fp32 sums)
+  std::vector<int> blk_begin;
+  int nblk = 0, W = 4, ne = 0, Q = 0;
+  bool exact = false;
+  bool sepValid = false;          // d_sep holds the separate HA / HSC of the last linearization
   std::vector<int> pt_host, res_point, res_target, host_pt_begin;
   std::vector<int> res_of_slot;   // [nP*8]
   std::vector<int8_t> res_order;  // [nP*8]
@@ -82,7 +88,7 @@ struct hs_ctx {
   std::vector<double> HM, bM, Porth, Nproj;
   HsDevState* h_state = nullptr;  // pinned staging of the device state
   int* h_ctl = nullptr;           // pinned: iteration, status, log_count
-  bool haveSystem = false;        // a stitched, not yet solved system is in d_sys
+  bool haveSystem = false;        // a stitched, not yet solved system is in the slots
 
   // device
   float4* d_img[HS_MAXF] = {nullptr};
@@ -96,15 +102,17 @@ struct hs_ctx {
   uint8_t *d_r_state = nullptr, *d_r_active = nullptr;
   float *d_r_energy = nullptr, *d_r_newEnergy = nullptr, *d_r_ewo = nullptr, *d_r_center = nullptr;
   uint8_t* d_p_actmask = nullptr;
-  float *d_p_HdiF = nullptr, *d_p_bdSumF = nullptr, *d_p_Hcd = nullptr, *d_p_JpJdF = nullptr, *d_p_Jrec = nullptr;
+  float *d_p_HdiF = nullptr, *d_p_bdSumF = nullptr, *d_p_Hcd = nullptr, *d_p_JpJdF = nullptr;
   float* d_p_step = nullptr;
-  double* d_p_energy = nullptr;
-  double* d_part = nullptr;
-  int* d_part_cnt = nullptr;
-  double* d_hccbc = nullptr;
+  float* d_part = nullptr;       // [nblk][ne][64] block partials of hs_k_lin
+  double* d_part_e = nullptr;    // [nblk][4] block energies
+  double* d_hostsum = nullptr;   // [nF][ne][64] per-host sums (hs_k_reduce)
+  double* d_slot = nullptr;      // [nF][SL] per-host systems: upper triangle of HA - sc HSC | bA - bSC
+  double* d_sep = nullptr;       // [nF][2][SL] per-host HA | bA, HSC | bSC (granular read-back)
+  double* d_sysE = nullptr;      // [3] energy, sum |idepth|, #points of the last linearization
+  double* d_rank = nullptr;      // [SL + 3] multi-rank: this rank's summed slots + energies, all-reduced
   double *d_adHost = nullptr, *d_adTarget = nullptr;
   float *d_adHostF = nullptr, *d_adTargetF = nullptr;
-  double* d_sys = nullptr;  // HA | bA | HSC | bSC | energy, sum|idepth|, #points
   double *d_HM = nullptr, *d_bM = nullptr, *d_Nproj = nullptr;
   float* d_xAd = nullptr;
   double* d_x = nullptr;
@@ -118,7 +126,7 @@ struct hs_ctx {
   // kernel tracing (env HS_KTRACE=1): per-block wall-clock checkpoints of the last iteration
   bool tracing = false;
   long long *d_tr_lin = nullptr, *d_tr_acc = nullptr, *d_tr_solve = nullptr;
-  int* d_ticket = nullptr;  // [nF*nF] stitch hand-off counters of hs_k_accumulate
+  int* d_ticket = nullptr;  // [nF] stitch hand-off counters of hs_k_reduce
 
   // RCCL
   ncclComm_t comm = nullptr;
@@ -128,13 +136,9 @@ struct hs_ctx {
   double t_lin = 0, t_acc = 0, t_solve = 0, t_timed = 0, t_wall = 0, t_iters = 0;
 
   int dim() const { return 4 + 8 * nF; }
-  size_t sys_len() const { return (size_t)2 * dim() * dim() + 2 * dim() + 3; }
-  size_t acc_len() const { return (size_t)2 * dim() * dim() + 2 * dim(); }
-  double* HA() const { return d_sys; }
-  double* bA() const { return d_sys + dim() * dim(); }
-  double* HSC() const { return d_sys + dim() * dim() + dim(); }
-  double* bSC() const { return d_sys + 2 * dim() * dim() + dim(); }
-  double* sysE() const { return d_sys + 2 * dim() * dim() + 2 * dim(); }
+  int SL() const { return dim() * dim() + dim(); }  // slot: n x n (upper triangle used) + b
+  double* sysE() const { return d_comm_active() ? d_rank + SL() : d_sysE; }
+  bool d_comm_active() const { return comm != nullptr; }
 };
 
 static void free_window(hs_ctx* c) {
@@ -146,8 +150,8 @@ static void free_window(hs_ctx* c) {
                   c->d_priorF, c->d_color, c->d_weight, c->d_res_of_slot, c->d_pt_host, c->d_host_pt_begin,
                   c->d_res_order, c->d_r_state, c->d_r_active, c->d_r_energy, c->d_r_newEnergy, c->d_r_ewo,
                   c->d_r_center, c->d_p_actmask, c->d_p_HdiF, c->d_p_bdSumF, c->d_p_Hcd, c->d_p_JpJdF,
-                  c->d_p_Jrec, c->d_p_step, c->d_p_energy, c->d_part, c->d_part_cnt, c->d_hccbc, c->d_adHost,
-                  c->d_adTarget, c->d_adHostF, c->d_adTargetF, c->d_sys, c->d_HM, c->d_bM, c->d_Nproj, c->d_xAd,
+                  c->d_p_step, c->d_part, c->d_part_e, c->d_hostsum, c->d_slot, c->d_sep, c->d_sysE, c->d_rank,
+                  c->d_adHost, c->d_adTarget, c->d_adHostF, c->d_adTargetF, c->d_HM, c->d_bM, c->d_Nproj, c->d_xAd,
                   c->d_x, c->d_elog, c->d_cand, c->d_tr_lin, c->d_tr_acc, c->d_tr_solve, c->d_ticket,
                   c->d_marg, c->d_adHTdelta};
   for (void* p : ptrs)
@@ -160,11 +164,11 @@ static void free_window(hs_ctx* c) {
   c->d_r_state = c->d_r_active = nullptr;
   c->d_r_energy = c->d_r_newEnergy = c->d_r_ewo = c->d_r_center = nullptr;
   c->d_p_actmask = nullptr;
-  c->d_p_HdiF = c->d_p_bdSumF = c->d_p_Hcd = c->d_p_JpJdF = c->d_p_Jrec = c->d_p_step = nullptr;
-  c->d_p_energy = nullptr;
-  c->d_part = nullptr; c->d_part_cnt = nullptr; c->d_hccbc = nullptr;
+  c->d_p_HdiF = c->d_p_bdSumF = c->d_p_Hcd = c->d_p_JpJdF = c->d_p_step = nullptr;
+  c->d_part = nullptr; c->d_part_e = nullptr; c->d_hostsum = nullptr; c->d_slot = nullptr; c->d_sep = nullptr;
+  c->d_sysE = nullptr; c->d_rank = nullptr;
   c->d_adHost = c->d_adTarget = nullptr; c->d_adHostF = c->d_adTargetF = nullptr;
-  c->d_sys = nullptr; c->d_HM = c->d_bM = c->d_Nproj = nullptr;
+  c->d_HM = c->d_bM = c->d_Nproj = nullptr;
   c->d_xAd = nullptr; c->d_x = nullptr; c->d_elog = nullptr; c->d_cand = nullptr;
   c->d_tr_lin = c->d_tr_acc = c->d_tr_solve = nullptr;
   c->d_ticket = nullptr;
@@ -172,6 +176,7 @@ static void free_window(hs_ctx* c) {
   c->d_adHTdelta = nullptr;
   c->nF = c->nP = c->nR = 0;
   c->haveSystem = false;
+  c->sepValid = false;
 }
 
 // ---------------------------------------------------------------- window preparation (host, once per window)
@@ -206,7 +211,9 @@ static int fetch_state(hs_ctx* c) {
 }
 
 // ---------------------------------------------------------------- launches (asynchronous)
-static int launch_linearize(hs_ctx* c, int fuse, bool marg = false) {
+static size_t lin_lds(const hs_ctx* c) { return (size_t)4 * c->ne * 64 * sizeof(float) + 12 * sizeof(double); }
+
+static int launch_linearize(hs_ctx* c, int fuse, bool marg = false, bool accumulate = true) {
   HsLinArgs a;
   std::memset(&a, 0, sizeof(a));
   if (marg) {  // hs_ba_marginalize_points: flags, adHTdeltaF and cDeltaF uploaded by the caller
@@ -224,59 +231,70 @@ static int launch_linearize(hs_ctx* c, int fuse, bool marg = false) {
   a.nF = c->nF;
   a.write_center = 1;
   a.fuse_step = fuse;
-  for (int i = 0; i <= c->nF; i++) a.host_begin[i] = c->host_pt_begin[i];
+  a.accumulate = accumulate ? 1 : 0;
+  for (int i = 0; i <= c->nF; i++) {
+    a.host_begin[i] = c->host_pt_begin[i];
+    a.blk_begin[i] = c->blk_begin[i];
+  }
+  for (int i = c->nF + 1; i <= HS_MAXF; i++) {
+    a.host_begin[i] = c->nP;
+    a.blk_begin[i] = c->nblk;
+  }
+  a.W = c->W;
   a.pre = c->d_pre;
   a.frameTH = c->d_frameTH;
   a.xAd = c->d_xAd;
-  a.pt_host = c->d_pt_host;
   a.u = c->d_u; a.v = c->d_v; a.idepth = c->d_idepth; a.idepth_zero = c->d_idepth_zero; a.priorF = c->d_priorF;
   a.color = c->d_color; a.weight = c->d_weight;
   a.res_of_slot = c->d_res_of_slot; a.res_order = c->d_res_order;
   a.r_state = c->d_r_state; a.r_active = c->d_r_active; a.r_energy = c->d_r_energy;
   a.r_newEnergy = c->d_r_newEnergy; a.r_ewo = c->d_r_ewo; a.r_center = c->d_r_center;
   a.p_actmask = c->d_p_actmask; a.p_HdiF = c->d_p_HdiF; a.p_bdSumF = c->d_p_bdSumF; a.p_Hcd = c->d_p_Hcd;
-  a.p_JpJdF = c->d_p_JpJdF; a.p_Jrec = c->d_p_Jrec; a.p_energy = c->d_p_energy; a.p_step = c->d_p_step;
+  a.p_JpJdF = c->d_p_JpJdF; a.p_step = c->d_p_step;
   a.newest_cand = c->d_cand + (size_t)c->rank * c->cand_stride;
+  a.part = c->d_part; a.part_e = c->d_part_e;
   a.trace = c->d_tr_lin;
-  if (c->nP > 0) hipLaunchKernelGGL(hs_k_linearize, dim3(c->nP), dim3(64), 0, c->stream, a);
+  if (c->nblk > 0) {
+    if (c->exact) hipLaunchKernelGGL(hs_k_lin_exact, dim3(c->nblk), dim3(256), lin_lds(c), c->stream, a);
+    else hipLaunchKernelGGL(hs_k_lin, dim3(c->nblk), dim3(256), lin_lds(c), c->stream, a);
+  }
   HS_HIP(hipGetLastError());
+  if (accumulate) c->sepValid = false;
   return HS_OK;
 }
 
-// all-gather of newest-frame candidates, accumulate, stitch, all-reduce of the systems
-static int launch_reduce(hs_ctx* c, bool skip_threshold = false) {
+// all-gather of newest-frame candidates, per-host sums + stitch (+ energy, threshold), combine + all-reduce
+static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = false) {
   if (c->comm)
     HS_NCCL(ncclAllGather(c->d_cand + (size_t)c->rank * c->cand_stride, c->d_cand, c->cand_stride, ncclFloat,
                           c->comm, c->stream));
-  HsAccArgs a;
+  HsRedArgs a;
   std::memset(&a, 0, sizeof(a));
-  a.nF = c->nF; a.S = c->S; a.nP = c->nP; a.W = c->W;
-  a.blocked = (c->maxPtsPerBlock + c->W - 1) / c->W > 1000 ? 1 : 0;
-  a.host_pt_begin = c->d_host_pt_begin;
-  a.actmask = c->d_p_actmask; a.HdiF = c->d_p_HdiF; a.bdSumF = c->d_p_bdSumF; a.Hcd = c->d_p_Hcd;
-  a.JpJdF = c->d_p_JpJdF; a.Jrec = c->d_p_Jrec;
-  a.part = c->d_part; a.part_cnt = c->d_part_cnt;
-  a.p_energy = c->d_p_energy; a.idepth = c->d_idepth; a.energy_out = c->sysE();
-  a.hccbc = c->d_hccbc;
+  a.nF = c->nF; a.ne = c->ne; a.exact = c->exact ? 1 : 0; a.Q = c->Q; a.nblk = c->nblk;
+  for (int i = 0; i <= c->nF; i++) a.blk_begin[i] = c->blk_begin[i];
+  a.part = c->d_part; a.part_e = c->d_part_e; a.hostsum = c->d_hostsum; a.ticket = c->d_ticket;
+  a.adHost = c->d_adHost; a.adTarget = c->d_adTarget;
+  a.slot = c->d_slot;
+  a.sep = sep ? c->d_sep : nullptr;
+  a.lambda1 = 1 + 1e-5;         // SOLVER_FIX_LAMBDA (Src/EnergyFunctional.cpp:707-708)
+  a.sc = 1.0f / (1 + 1e-5);     // H -= H_sc * (1.0f / (1 + lambda)) (:763)
+  a.sysE = c->d_sysE;
   a.cand = c->d_cand; a.nranks = c->nranks; a.stride = c->cand_stride;
-  a.trace = c->d_tr_acc;
   a.frameTH = c->d_frameTH; a.newest = c->nF - 1;
   a.frameEnergyTHN = c->P.frameEnergyTHN; a.facMedian = c->P.frameEnergyTHFacMedian;
   a.constWeight = c->P.frameEnergyTHConstWeight; a.overallWeight = c->P.overallEnergyTHWeight;
   a.skip_threshold = skip_threshold ? 1 : 0;
-  HsStitchArgs& st = a.stitch;
-  st.nF = c->nF; st.S = c->S;
-  st.part = c->d_part; st.part_cnt = c->d_part_cnt; st.hccbc = c->d_hccbc;
-  st.adHost = c->d_adHost; st.adTarget = c->d_adTarget;
-  st.HA = c->HA(); st.bA = c->bA(); st.HSC = c->HSC(); st.bSC = c->bSC();
-  st.trace = nullptr;
-  a.ticket = c->d_ticket;
-  if (a.trace)  // which blocks stitch varies per launch: clear the rows so stale checkpoints are not read
-    HS_HIP(hipMemsetAsync(a.trace, 0, sizeof(long long) * 16 * (c->nF * c->nF * c->S + 3), c->stream));
-  hipLaunchKernelGGL(hs_k_accumulate, dim3(c->nF * c->nF * c->S + 3), dim3(256), 0, c->stream, a);
+  a.trace = c->d_tr_acc;
+  hipLaunchKernelGGL(hs_k_reduce, dim3(c->nF * c->Q + 2), dim3(256), 0, c->stream, a);
   HS_HIP(hipGetLastError());
-  if (c->comm)
-    HS_NCCL(ncclAllReduce(c->d_sys, c->d_sys, c->sys_len(), ncclDouble, ncclSum, c->comm, c->stream));
+  if (sep) c->sepValid = true;
+  if (c->comm) {
+    HsCombArgs cb;
+    cb.nF = c->nF; cb.SL = c->SL(); cb.slot = c->d_slot; cb.sysE = c->d_sysE; cb.out = c->d_rank;
+    hipLaunchKernelGGL(hs_k_combine, dim3((c->SL() + 3 + 255) / 256), dim3(256), 0, c->stream, cb);
+    HS_HIP(hipGetLastError());
+    HS_NCCL(ncclAllReduce(c->d_rank, c->d_rank, c->SL() + 3, ncclDouble, ncclSum, c->comm, c->stream));
+  }
   return HS_OK;
 }
 
@@ -287,7 +305,9 @@ static int launch_solve(hs_ctx* c, int flags, int iteration, bool log) {
   a.iteration = iteration;
   a.nF = c->nF;
   a.st = c->d_state;
-  a.HA = c->HA(); a.bA = c->bA(); a.HSC = c->HSC(); a.bSC = c->bSC();
+  a.slot = c->comm ? c->d_rank : c->d_slot;
+  a.nslots = c->comm ? 1 : c->nF;
+  a.SL = c->SL();
   a.HM = c->hm_zero ? nullptr : c->d_HM;
   a.bM = c->d_bM; a.Nproj = c->d_Nproj;
   a.adHostF = c->d_adHostF; a.adTargetF = c->d_adTargetF;
@@ -314,9 +334,8 @@ static int reset_states(hs_ctx* c) {  // PointFrameResidual::resetOOB on every a
 // a full linearizeAll pass from a clean accumulation target (granular API / optimize entry)
 static int linearize_pass(hs_ctx* c, bool reset) {
   if (reset) HS_TRY(reset_states(c));
-  HS_HIP(hipMemsetAsync(c->d_sys, 0, sizeof(double) * c->acc_len(), c->stream));
   HS_TRY(launch_linearize(c, 0));
-  HS_TRY(launch_reduce(c));
+  HS_TRY(launch_reduce(c, false, true));
   c->haveSystem = true;
   return HS_OK;
 }
@@ -371,8 +390,8 @@ static int dump_traces(hs_ctx* c) {
     for (int k = 17; k < 24; k++) std::fprintf(stderr, " s%d=%lld", k, h[k] ? h[k] - h[16] : -1);
     std::fprintf(stderr, "\n");
   }
-  HS_TRY(dump_one("linearize", c->d_tr_lin, c->nP, tick_us, c->stream));
-  HS_TRY(dump_one("accumulate", c->d_tr_acc, c->nF * c->nF * c->S + 3, tick_us, c->stream));
+  HS_TRY(dump_one("linearize", c->d_tr_lin, c->nblk, tick_us, c->stream));
+  HS_TRY(dump_one("reduce", c->d_tr_acc, c->nF * c->Q + 2, tick_us, c->stream));
   return HS_OK;
 }
 
@@ -434,23 +453,6 @@ static int gn_iterations(hs_ctx* c, int it0, int K, bool allow_break, double* en
   for (int q = 0; q <= k; q++)
     if (!std::isfinite(elog[q])) return fail(HS_ERR_NONFINITE, "non-finite energy (isLost)");
   return HS_OK;
-}
-
-// stitchDoubleMT post-processing on a host copy (granular read-back only; the solve kernel does it on the device)
-static void finish_top(std::vector<double>& H, int n, int nF, bool symFrames) {
-  for (int h = 0; h < nF; h++) {
-    const int hIdx = 4 + h * 8;
-    for (int r = 0; r < 8; r++)
-      for (int cc = 0; cc < 4; cc++) H[cc * n + hIdx + r] = H[(hIdx + r) * n + cc];
-    if (!symFrames) continue;
-    for (int t = h + 1; t < nF; t++) {
-      const int tIdx = 4 + t * 8;
-      for (int r = 0; r < 8; r++)
-        for (int cc = 0; cc < 8; cc++) H[(hIdx + r) * n + tIdx + cc] += H[(tIdx + cc) * n + hIdx + r];
-      for (int r = 0; r < 8; r++)
-        for (int cc = 0; cc < 8; cc++) H[(tIdx + r) * n + hIdx + cc] = H[(hIdx + cc) * n + tIdx + r];
-    }
-  }
 }
 
 // ================================================================ C-ABI
@@ -589,17 +591,25 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
     }
     c->host_pt_begin[nF] = nP;
   }
-  int maxHost = 0;
-  for (int h = 0; h < nF; h++) maxHost = std::max(maxHost, c->host_pt_begin[h + 1] - c->host_pt_begin[h]);
-  // accumulate partitioning: S splits per (host, target) x W accumulating waves per split.
-  // HS_ACC_EXACT=1: one partial per (host, target) in point order = the single-thread reference's sums.
-  int splitPts = kPointsPerSplit;
-  if (const char* e = std::getenv("HS_ACC_SPLIT_POINTS")) splitPts = std::max(1, std::atoi(e));
+  // hs_k_lin partitioning.  Production: every host's points are split into blocks of 4 waves x ppw points
+  // (ppw grows with the window so the grid stays near kLinBlocksTarget blocks; env HS_LIN_PPW overrides).
+  // HS_ACC_EXACT=1: one block per host whose wave 0 takes every point in order = the single-thread reference's
+  // fp32 accumulator sums (no shiftUp emulation: at most 1000 points per host).
   const char* ex = std::getenv("HS_ACC_EXACT");
-  const bool exact = ex && ex[0] == '1';
-  c->S = exact ? 1 : std::max(1, std::min(256, (maxHost + splitPts - 1) / splitPts));
-  c->W = exact ? 1 : 4;
-  c->maxPtsPerBlock = (maxHost + c->S - 1) / c->S;
+  c->exact = ex && ex[0] == '1';
+  c->ne = hs_ne(c->exact);
+  c->Q = (c->ne * 64 + 255) / 256;
+  c->blk_begin.assign(nF + 1, 0);
+  int ppw = std::max(1, (nP + 4 * kLinBlocksTarget - 1) / (4 * kLinBlocksTarget));
+  if (const char* e = std::getenv("HS_LIN_PPW")) ppw = std::max(1, std::atoi(e));
+  c->W = c->exact ? 1 : 4;
+  for (int h = 0; h < nF; h++) {
+    const int nh = c->host_pt_begin[h + 1] - c->host_pt_begin[h];
+    if (c->exact && nh > 1000) return fail(HS_ERR_INVALID, "HS_ACC_EXACT supports at most 1000 points per host");
+    const int nb = nh == 0 ? 0 : (c->exact ? 1 : (nh + 4 * ppw - 1) / (4 * ppw));
+    c->blk_begin[h + 1] = c->blk_begin[h] + nb;
+  }
+  c->nblk = c->blk_begin[nF];
 
   // ---- window state: calib (CalibData ctor: setValueScaled, value_zero = value) and frames
   HsDevState& S = *c->h_state;
@@ -688,14 +698,17 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
   HS_TRY(dalloc(&c->d_r_center, (size_t)P8 * 3));
   HS_TRY(dalloc(&c->d_p_actmask, nP)); HS_TRY(dalloc(&c->d_p_HdiF, nP)); HS_TRY(dalloc(&c->d_p_bdSumF, nP));
   HS_TRY(dalloc(&c->d_p_Hcd, (size_t)nP * 4)); HS_TRY(dalloc(&c->d_p_JpJdF, P8 * 8));
-  HS_TRY(dalloc(&c->d_p_Jrec, P8 * HS_JREC)); HS_TRY(dalloc(&c->d_p_step, nP)); HS_TRY(dalloc(&c->d_p_energy, nP));
-  HS_TRY(dalloc(&c->d_part, (size_t)nF * nF * c->S * HS_PART_N));
-  HS_TRY(dalloc(&c->d_part_cnt, (size_t)nF * nF * c->S * 16));
-  HS_TRY(dalloc(&c->d_hccbc, 20));
-  HS_TRY(dalloc(&c->d_ticket, (size_t)nF * nF));  // zeroed; each stitching block resets its own counter
+  HS_TRY(dalloc(&c->d_p_step, nP));
+  HS_TRY(dalloc(&c->d_part, (size_t)std::max(c->nblk, 1) * c->ne * 64));
+  HS_TRY(dalloc(&c->d_part_e, (size_t)std::max(c->nblk, 1) * 4));
+  HS_TRY(dalloc(&c->d_hostsum, (size_t)nF * c->ne * 64));
+  HS_TRY(dalloc(&c->d_slot, (size_t)nF * c->SL()));  // zeroed: the lower triangles are never written
+  HS_TRY(dalloc(&c->d_sep, (size_t)nF * 2 * c->SL()));
+  HS_TRY(dalloc(&c->d_sysE, 4));
+  if (c->comm) HS_TRY(dalloc(&c->d_rank, (size_t)c->SL() + 3));
+  HS_TRY(dalloc(&c->d_ticket, (size_t)nF));  // zeroed; each stitching block resets its own counter
   HS_TRY(dalloc(&c->d_adHost, nF * nF * 64)); HS_TRY(dalloc(&c->d_adTarget, nF * nF * 64));
   HS_TRY(dalloc(&c->d_adHostF, nF * nF * 64)); HS_TRY(dalloc(&c->d_adTargetF, nF * nF * 64));
-  HS_TRY(dalloc(&c->d_sys, c->sys_len()));
   HS_TRY(dalloc(&c->d_HM, (size_t)n * n)); HS_TRY(dalloc(&c->d_bM, n)); HS_TRY(dalloc(&c->d_Nproj, (size_t)2 * n * HS_NNS));
   HS_TRY(dalloc(&c->d_xAd, nF * nF * 8)); HS_TRY(dalloc(&c->d_x, n)); HS_TRY(dalloc(&c->d_elog, kLogCap));
   HS_TRY(dalloc(&c->d_cand, (size_t)c->cand_stride * c->nranks));
@@ -703,8 +716,8 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
   const char* tr = std::getenv("HS_KTRACE");
   c->tracing = tr && tr[0] == '1';
   if (c->tracing) {
-    HS_TRY(dalloc(&c->d_tr_lin, (size_t)std::max(nP, 1) * 16));
-    HS_TRY(dalloc(&c->d_tr_acc, (size_t)(nF * nF * c->S + 3) * 16));
+    HS_TRY(dalloc(&c->d_tr_lin, (size_t)std::max(c->nblk, 1) * 16));
+    HS_TRY(dalloc(&c->d_tr_acc, (size_t)(nF * c->Q + 2) * 16));
     HS_TRY(dalloc(&c->d_tr_solve, 32));
   }
 
@@ -859,12 +872,25 @@ int hs_ba_get_system(hs_ctx* c, int which, double* H, double* b) {
         bb[j] += S.frames[h].prior[i] * S.frames[h].delta_prior[i];
       }
   } else {
-    const double* dH = which == 0 ? c->HA() : c->HSC();
-    const double* db = which == 0 ? c->bA() : c->bSC();
-    HS_HIP(hipMemcpyAsync(HH.data(), dH, sizeof(double) * n * n, hipMemcpyDeviceToHost, c->stream));
-    HS_HIP(hipMemcpyAsync(bb.data(), db, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+    // the per-host HA | bA (which 0) or HSC | bSC (which 2) of the last linearization, summed over the hosts in
+    // host order and mirrored (the stitch writes the upper triangles: stitchDoubleMT's symmetrization and calib-row
+    // copy).  If the last reduce ran without the separate output (the GN loop), it is re-run on the block
+    // partials of that linearization (deterministic: the same sums).
+    if (!c->sepValid) HS_TRY(launch_reduce(c, true, true));
+    const int SL = c->SL();
+    std::vector<double> sep((size_t)nF * 2 * SL);
+    HS_HIP(hipMemcpyAsync(sep.data(), c->d_sep, sizeof(double) * sep.size(), hipMemcpyDeviceToHost, c->stream));
     HS_HIP(hipStreamSynchronize(c->stream));
-    finish_top(HH, n, nF, which == 0);
+    const int part = which == 0 ? 0 : 1;
+    for (int h = 0; h < nF; h++) {
+      const double* src = sep.data() + ((size_t)h * 2 + part) * SL;
+      for (int r = 0; r < n; r++) {
+        for (int q = r; q < n; q++) HH[(size_t)r * n + q] += src[(size_t)r * n + q];
+        bb[r] += src[(size_t)n * n + r];
+      }
+    }
+    for (int r = 0; r < n; r++)
+      for (int q = 0; q < r; q++) HH[(size_t)r * n + q] = HH[(size_t)q * n + r];
   }
   if (H) std::memcpy(H, HH.data(), sizeof(double) * n * n);
   if (b) std::memcpy(b, bb.data(), sizeof(double) * n);
@@ -994,10 +1020,9 @@ int hs_ba_marginalize_points(hs_ctx* c, int n, const int* points, double* HM_out
   for (int i = 0; i < 4; i++) c->cDelta[i] = (float)S.calib.value_minus_value_zero[i];
   if (c->nP > 0) HS_HIP(hipMemcpy(c->d_marg, flag.data(), c->nP, hipMemcpyHostToDevice));
   HS_HIP(hipMemcpy(c->d_adHTdelta, adHTd.data(), sizeof(float) * adHTd.size(), hipMemcpyHostToDevice));
-  // the pass: its own clean accumulation target; setNewFrameEnergyTH is not part of it
-  HS_HIP(hipMemsetAsync(c->d_sys, 0, sizeof(double) * c->acc_len(), c->stream));
+  // the pass; setNewFrameEnergyTH is not part of it
   HS_TRY(launch_linearize(c, 0, true));
-  HS_TRY(launch_reduce(c, true));
+  HS_TRY(launch_reduce(c, true, true));
   HS_HIP(hipStreamSynchronize(c->stream));
   c->haveSystem = true;
   std::vector<double> M((size_t)dim * dim), Mb(dim), Msc((size_t)dim * dim), Mbsc(dim);

@@ -47,42 +47,11 @@ __device__ __forceinline__ float3 interp33(const float4* __restrict__ img, float
   return r;
 }
 
-// One entry of a blocked fp32 accumulator: A (current), A1k, A1m (MatrixAccumulators.h shiftUp).
-struct Blk {
-  float A = 0.f, A1k = 0.f, A1m = 0.f;
-  __device__ __forceinline__ void flush(int f) {
-    if (f & 1) { A1k += A; A = 0.f; }
-    if (f & 2) { A1m += A1k; A1k = 0.f; }
-  }
-  __device__ __forceinline__ float finish() {
-    A1k += A;
-    A1m += A1k;
-    return A1m;
-  }
-};
-// Update counters of one accumulator object (numIn1 / numIn1k / numIn1m).
-struct BlkCnt {
-  int n1 = 0, n1k = 0, n1m = 0;
-  // numIn1++ then shiftUp(false); returns the flushed levels
-  __device__ __forceinline__ int bump() {
-    n1++;
-    int f = 0;
-    if (n1 > 1000) { f |= 1; n1k += n1; n1 = 0; }
-    if (n1k > 1000) { f |= 2; n1m += n1k; n1k = 0; }
-    return f;
-  }
-  __device__ __forceinline__ int total() const { return n1 + n1k + n1m; }
-};
-
 // wall-clock checkpoint of a block (thread 0) when tracing is enabled
 #define HS_TRACE(A, slot)                                                                          \
   do {                                                                                             \
     if ((A).trace && threadIdx.x == 0) (A).trace[(size_t)blockIdx.x * 16 + (slot)] = wall_clock64(); \
   } while (0)
-
-struct LinLds {
-  float s[HS_MAXF][Q_N + 3];
-};
 
 // lane l <- lane l-1 within each row of 16 (DPP row_shr:1; a row's lane 0 gets 0)
 __device__ __forceinline__ float dpp_shr1(float v) {
@@ -126,35 +95,63 @@ __device__ __forceinline__ float point_step(int p, int h, int nF, unsigned m, co
 }  // namespace
 
 // =====================================================================================================
-// linearize: one wave per point
+// linearize + accumulate: a block = 4 waves over an equal share of ONE host's points, one wave per point
 // =====================================================================================================
-__global__ __launch_bounds__(64) void hs_k_linearize(HsLinArgs a) {
-  __shared__ LinLds L;
-  const int lane = threadIdx.x;
+namespace {
+
+// One point's linearization as lane (target slot t, pattern pixel k) holds it.
+struct LinPt {
+  float Jx[10], Jy[10];  // [Jpdc(4) Jpdxi(6)] rows of the lane's residual (when the slot was evaluated)
+  float S[Q_N];          // the slot's pattern-order sums (octet fold at lane 8t+7, broadcast to the octet)
+  float jj;              // JpJdF[t][k] of an active residual, else 0
+  bool active;           // the lane's residual is active after this linearization
+  unsigned mask;         // the point's active slots (uniform)
+  float HdiF, bdSumF, Hcd[4];  // the point's Schur prelude (uniform)
+  double eSum;           // the point's share of linearizeAll's energy (uniform)
+  float idep;            // idepth after the fused step (uniform)
+  // lane-selected accumulator operands (acc_point's layout), formed here from SSA values: select chains over
+  // the struct's arrays would be folded into dynamically indexed loads and keep the struct in scratch
+  float xk, yk;                // Jx[k], Jy[k]
+  float xr10, yr10, xc10, yc10;  // Data (8,8) / (8,9) / (9,9) operands of lanes 0 / 1 / 2
+  float xr14, yr14, t014, t114;  // TopRight (8 + k/3, k%3) operands of lanes 0..5
+  float br15;                  // BotRight[k] of lanes 0..5
+  float hcr, hcc;              // Hcd[r], Hcd[c] of the accHcc / accbc lane
+};
+
+// PointFrameResidual::linearize + applyRes / takeData (Src/OptimizationClasses.cpp:43-256) of point p's <= 7
+// residuals (lane = target slot x pattern pixel), preceded by the fused resubstituteFPt + point step of the
+// previous solve (Src/EnergyFunctional.cpp:249-274), followed by the point sums of
+// AccumulatedTopHessianSSE::addPoint<0> / AccumulatedSCHessianSSE::addPoint (Src/AccumulatedTopHessian.cpp:21-141,
+// Src/AccumulatedSCHessian.cpp:10-33).  Writes the per-residual / per-point state; returns what the
+// accumulators need.  Wave-uniform p.
+__device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int lane, LinPt& o) {
   const int t = lane >> 3;  // target slot
   const int k = lane & 7;   // pattern pixel
-  const int p = blockIdx.x;
   const int nF = a.nF;
-  int h = 0;  // points are sorted by host: the host is found from the kernel-argument boundaries, no load
-#pragma unroll
-  for (int i = 1; i < HS_MAXF; i++) h += (i < nF && p >= a.host_begin[i]) ? 1 : 0;
   const HsCalib cal = a.st->dcal;
-
-  HS_TRACE(a, 0);
-  // everything the linearization reads is loaded up front, unconditionally (clamped indices), so the
-  // prologue is ONE memory round trip: residual state is in the slot layout [point][target slot] and the
-  // host comes from the kernel arguments, so no load depends on another
   if (a.marg && a.marg[p] == 0) {  // marginalization pass, point not marginalized: no active residual
     if (lane == 0) {
-      a.p_energy[p] = 0.0;
       a.p_actmask[p] = 0;
       a.p_HdiF[p] = 0.f;
       a.p_bdSumF[p] = 0.f;
       reinterpret_cast<float4*>(a.p_Hcd)[p] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     if (t == nF - 1 && k == 0) a.newest_cand[p] = -1.f;
+#pragma unroll
+    for (int i = 0; i < 10; i++) o.Jx[i] = o.Jy[i] = 0.f;
+#pragma unroll
+    for (int i = 0; i < Q_N; i++) o.S[i] = 0.f;
+    o.jj = 0.f; o.active = false; o.mask = 0u; o.HdiF = 0.f; o.bdSumF = 0.f;
+    o.Hcd[0] = o.Hcd[1] = o.Hcd[2] = o.Hcd[3] = 0.f;
+    o.eSum = 0.0;
+    o.idep = a.idepth[p];
+    o.xk = o.yk = o.xr10 = o.yr10 = o.xc10 = o.yc10 = o.xr14 = o.yr14 = o.t014 = o.t114 = o.br15 = 0.f;
+    o.hcr = o.hcc = 0.f;
     return;
   }
+  // everything the linearization reads is loaded up front, unconditionally (clamped indices), so the
+  // prologue is ONE memory round trip: residual state is in the slot layout [point][target slot] and the
+  // host comes from the block, so no load depends on another
   const int sl = p * 8 + t;                 // this lane's residual slot
   const int tc_ = t < nF ? t : 0;
   float idep = a.idepth[p], idep0 = a.idepth_zero[p];
@@ -185,14 +182,12 @@ __global__ __launch_bounds__(64) void hs_k_linearize(HsLinArgs a) {
   asm volatile("" ::"v"(fm), "v"(xad), "v"(jpj), "v"(bds), "v"(hdi), "v"(hcd.x), "v"(hcd.y), "v"(hcd.z), "v"(hcd.w),
                "v"(cs0), "v"(cs1), "v"(cs2), "v"(cs3), "v"(ro2.x), "v"(ro2.y));
   if (a.fuse_step) {
-    // resubstituteFPt of the previous linearization (Src/EnergyFunctional.cpp:249-274) + the point part of
-    // doStepFromBackup (stepfacD = 1).  Lane (t, k) forms xAd[h][t][k] * JpJdF[t][k]; the 8-term dot of a
-    // residual is an in-order octet fold, the residual terms are then subtracted in list order (uniform).
+    // resubstituteFPt of the previous linearization + the point part of doStepFromBackup (stepfacD = 1).
+    // Lane (t, k) forms xAd[h][t][k] * JpJdF[t][k]; the 8-term dot of a residual is an in-order octet fold, the
+    // residual terms are then subtracted in list order (uniform).
     const unsigned m = fm;
     const float prod = ((m >> t) & 1u) ? xad * jpj : 0.f;
     const float dsum = octet_fold(prod);
-    // branch-free (no load-dependent scalar control flow here, so every prologue load is one batch):
-    // the list-order subtraction walks the point's residual slots with ds_bpermute reads of the folds
     float b = bds;
     float dot = 0.f;
     dot += cs0 * hcd.x;
@@ -222,7 +217,6 @@ __global__ __launch_bounds__(64) void hs_k_linearize(HsLinArgs a) {
   const int st = has ? (a.marg ? HS_RES_IN : st_raw) : HS_RES_OOB;
   const float oldE = (has && !a.marg) ? oldE_raw : 0.f;
   const float oldNewE = (has && !a.marg) ? oldNewE_raw : 0.f;
-  HS_TRACE(a, 1);
 
   bool oob = false;
   float Jx[10] = {0}, Jy[10] = {0}, Jd0 = 0.f, Jd1 = 0.f;
@@ -345,7 +339,7 @@ __global__ __launch_bounds__(64) void hs_k_linearize(HsLinArgs a) {
             float rz = resF;
             if (a.marg) {
               const float* dp = a.adHTdelta + (h + nF * t) * 8;
-              float jx = 0.f, jy = 0.f, cx = 0.f, cy = 0.f;
+              float jx = 0.f, jy = 0.f, cxx = 0.f, cyy = 0.f;
 #pragma unroll
               for (int i = 0; i < 6; i++) {
                 jx += Jx[4 + i] * dp[i];
@@ -353,12 +347,12 @@ __global__ __launch_bounds__(64) void hs_k_linearize(HsLinArgs a) {
               }
 #pragma unroll
               for (int i = 0; i < 4; i++) {
-                cx += Jx[i] * a.cDelta[i];
-                cy += Jy[i] * a.cDelta[i];
+                cxx += Jx[i] * a.cDelta[i];
+                cyy += Jy[i] * a.cDelta[i];
               }
               const float dF = idep - idep0;
-              const float Jpdx = jx + cx + Jd0 * dF;
-              const float Jpdy = jy + cy + Jd1 * dF;
+              const float Jpdx = jx + cxx + Jd0 * dF;
+              const float Jpdy = jy + cyy + Jd1 * dF;
               rz = rz - hy * Jpdx;
               rz = rz - hz * Jpdy;
               rz = rz - jab0 * dp[6];
@@ -376,27 +370,14 @@ __global__ __launch_bounds__(64) void hs_k_linearize(HsLinArgs a) {
   }
   const unsigned long long oobMask = __ballot(oob);
   const bool slotOob = ((oobMask >> (t * 8)) & 0xffull) != 0ull;
-  HS_TRACE(a, 2);
 
-  // sequential (pattern-order) sums = the reference's running sums: octet folds, published by lane k == 7
-  {
-    float sq[Q_N];
-#pragma unroll
-    for (int qi = 0; qi < Q_N; qi++) sq[qi] = octet_fold(qv[qi]);
-    if (k == 7) {
-#pragma unroll
-      for (int qi = 0; qi < Q_N; qi++) L.s[t][qi] = sq[qi];
-    }
-  }
-  __syncthreads();
-  HS_TRACE(a, 4);
-
-  // ---------------- state decision + applyRes (the 8 lanes of a slot agree; lane k == 0 writes).
-  // Predicated rather than branched: the slot's sums are read from LDS in one batch and every store is
-  // issued under a mask, so the divergent slot cases cost no serialised LDS round trips.
+  // sequential (pattern-order) sums = the reference's running sums: octet folds at lane 8t+7, broadcast to the
+  // octet by ds_bpermute (no LDS round trip, no barrier: the waves of a block run their points independently)
   float S[Q_N];
 #pragma unroll
-  for (int qi = 0; qi < Q_N; qi++) S[qi] = L.s[t][qi];
+  for (int qi = 0; qi < Q_N; qi++) S[qi] = __shfl(octet_fold(qv[qi]), t * 8 + 7);
+
+  // ---------------- state decision + applyRes (the 8 lanes of a slot agree; lane k == 0 writes)
   const bool live = has && st != HS_RES_OOB;      // OOB is sticky: linearize returns state_energy
   const bool eval = live && !slotOob;             // a full linearization of this residual
   const bool isOut = S[0] > thr || S[11] < 2;
@@ -414,13 +395,12 @@ __global__ __launch_bounds__(64) void hs_k_linearize(HsLinArgs a) {
   }
   if (t == nF - 1 && k == 0) a.newest_cand[p] = eval ? S[0] : -1.f;
   if (has && a.write_center && centreOk && k < 3) a.r_center[sl * 3 + k] = centre[k];
-  float tHdd = 0.f, tbd = 0.f, tc[4] = {0.f, 0.f, 0.f, 0.f};  // the slot's terms of the per-point sums
+  float tHdd, tbd, tc[4];  // the slot's terms of the per-point sums
   {
-    // takeData (Include/OptimizationClasses.h:195-201), computed unconditionally, stored when active
+    // takeData (Include/OptimizationClasses.h:155-161), computed unconditionally, stored when active
     const float J00 = S[1], J11 = S[2], J10 = S[3];
     const float aa = J00 * Jd0 + J10 * Jd1;
     const float bb = J10 * Jd0 + J11 * Jd1;
-    // this residual's terms of the point sums (AccumulatedTopHessianSSE::addPoint<0> / SC prelude)
     tbd = S[12] * Jd0 + S[13] * Jd1;
     tHdd = aa * Jd0 + bb * Jd1;
 #pragma unroll
@@ -432,47 +412,9 @@ __global__ __launch_bounds__(64) void hs_k_linearize(HsLinArgs a) {
       jy4 = k == c - 4 ? Jy[c] : jy4;
     }
     const float jj = k < 6 ? jx4 * aa + jy4 * bb : (k == 6 ? S[4] * Jd0 + S[5] * Jd1 : S[6] * Jd0 + S[7] * Jd1);
-    // Jacobian digest entries e = k + 8i (layout: hs_layout.h), selected with constant indices
-    float v0 = Jx[0];
-#pragma unroll
-    for (int c = 1; c < 8; c++) v0 = k == c ? Jx[c] : v0;           // e = k
-    float v1;
-    {
-      float y = Jy[0];
-#pragma unroll
-      for (int c = 1; c < 6; c++) y = k - 2 == c ? Jy[c] : y;      // e = k + 8 >= 10 -> Jy[k - 2]
-      v1 = k == 0 ? Jx[8] : (k == 1 ? Jx[9] : y);
-    }
-    float v2 = Jy[6];                                               // e = k + 16
-    v2 = k == 1 ? Jy[7] : v2;
-    v2 = k == 2 ? Jy[8] : v2;
-    v2 = k == 3 ? Jy[9] : v2;
-    v2 = k == 4 ? J00 : v2;
-    v2 = k == 5 ? J10 : v2;
-    v2 = k == 6 ? J11 : v2;
-    v2 = k == 7 ? S[8] : v2;
-    float v3 = S[9];                                                // e = k + 24
-    v3 = k == 1 ? S[10] : v3;
-    v3 = k == 2 ? S[4] : v3;
-    v3 = k == 3 ? S[5] : v3;
-    v3 = k == 4 ? S[6] : v3;
-    v3 = k == 5 ? S[7] : v3;
-    v3 = k == 6 ? S[12] : v3;
-    v3 = k == 7 ? S[13] : v3;
-    float v4 = S[14];                                               // e = k + 32 (k < 3)
-    v4 = k == 1 ? S[15] : v4;
-    v4 = k == 2 ? S[16] : v4;
-    if (active) {
-      a.p_JpJdF[(p * 8 + t) * 8 + k] = jj;
-      float* jr = a.p_Jrec + (size_t)(p * 8 + t) * HS_JREC;
-      jr[k] = v0;
-      jr[k + 8] = v1;
-      jr[k + 16] = v2;
-      jr[k + 24] = v3;
-      if (k < 3) jr[k + 32] = v4;
-    }
+    if (active) a.p_JpJdF[(p * 8 + t) * 8 + k] = jj;
+    o.jj = active ? jj : 0.f;
   }
-  HS_TRACE(a, 5);
   // ---------------- per-point sums in the point's residual-list order (uniform; readlane from lane 8 * slot)
   {
     const unsigned long long actBits = __ballot(active);
@@ -491,118 +433,236 @@ __global__ __launch_bounds__(64) void hs_k_linearize(HsLinArgs a) {
 #pragma unroll
       for (int c = 0; c < 4; c++) Hcd[c] += readlane_f(tc[c], src);
     }
-    if (lane == 0) {
-      a.p_energy[p] = eSum;
-      a.p_actmask[p] = (uint8_t)mask;
-      if (mask == 0u) {
-        a.p_HdiF[p] = 0.f;
-        a.p_bdSumF[p] = 0.f;
-      } else {
-        // marginalization pass: priorF *= idepthFixPriorMargFac, the sums are the LF ones (AF = 0), and
-        // AccumulatedSCHessianSSE::addPoint(p, shiftPriorToZero = false) (Src/EnergyFunctional.cpp:563,577)
-        const float priorF = a.marg ? a.priorF[p] * a.margPriorFac : a.priorF[p];
-        float Hh = a.marg ? (0.f + Hdd) + priorF : Hdd + 0.f + priorF;  // Hdd_accAF + Hdd_accLF + priorF
-        if ((double)Hh < 1e-10) Hh = (float)1e-10;
-        a.p_HdiF[p] = (float)(1.0 / (double)Hh);
-        float bdSumF = a.marg ? 0.f + bd : bd + 0.f;
-        if (!a.marg) bdSumF += priorF * (idep - idep0);
-        a.p_bdSumF[p] = bdSumF;
-      }
-      if (a.marg)
-        reinterpret_cast<float4*>(a.p_Hcd)[p] = make_float4(0.f + Hcd[0], 0.f + Hcd[1], 0.f + Hcd[2], 0.f + Hcd[3]);
-      else
-        reinterpret_cast<float4*>(a.p_Hcd)[p] = make_float4(Hcd[0] + 0.f, Hcd[1] + 0.f, Hcd[2] + 0.f, Hcd[3] + 0.f);
+    float HdiF = 0.f, bdSumF = 0.f;
+    if (mask != 0u) {
+      // marginalization pass: priorF *= idepthFixPriorMargFac, the sums are the LF ones (AF = 0), and
+      // AccumulatedSCHessianSSE::addPoint(p, shiftPriorToZero = false) (Src/EnergyFunctional.cpp:563,577)
+      const float priorF = a.marg ? a.priorF[p] * a.margPriorFac : a.priorF[p];
+      float Hh = a.marg ? (0.f + Hdd) + priorF : Hdd + 0.f + priorF;  // Hdd_accAF + Hdd_accLF + priorF
+      if ((double)Hh < 1e-10) Hh = (float)1e-10;
+      HdiF = (float)(1.0 / (double)Hh);
+      bdSumF = a.marg ? 0.f + bd : bd + 0.f;
+      if (!a.marg) bdSumF += priorF * (idep - idep0);
     }
+    float4 hc4;
+    if (a.marg) hc4 = make_float4(0.f + Hcd[0], 0.f + Hcd[1], 0.f + Hcd[2], 0.f + Hcd[3]);
+    else hc4 = make_float4(Hcd[0] + 0.f, Hcd[1] + 0.f, Hcd[2] + 0.f, Hcd[3] + 0.f);
+    if (lane == 0) {
+      a.p_actmask[p] = (uint8_t)mask;
+      a.p_HdiF[p] = HdiF;
+      a.p_bdSumF[p] = bdSumF;
+      reinterpret_cast<float4*>(a.p_Hcd)[p] = hc4;
+    }
+    o.mask = mask;
+    o.HdiF = HdiF;
+    o.bdSumF = bdSumF;
+    o.Hcd[0] = hc4.x; o.Hcd[1] = hc4.y; o.Hcd[2] = hc4.z; o.Hcd[3] = hc4.w;
+    o.eSum = eSum;
   }
-  HS_TRACE(a, 3);
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    o.Jx[i] = Jx[i];
+    o.Jy[i] = Jy[i];
+  }
+#pragma unroll
+  for (int i = 0; i < Q_N; i++) o.S[i] = S[i];
+  o.active = active;
+  o.idep = idep;
+  {
+    float xk = Jx[0], yk = Jy[0];
+#pragma unroll
+    for (int c = 1; c < 8; c++) {
+      xk = k == c ? Jx[c] : xk;
+      yk = k == c ? Jy[c] : yk;
+    }
+    o.xk = xk;
+    o.yk = yk;
+    o.xr10 = k == 2 ? Jx[9] : Jx[8];
+    o.yr10 = k == 2 ? Jy[9] : Jy[8];
+    o.xc10 = k == 0 ? Jx[8] : Jx[9];
+    o.yc10 = k == 0 ? Jy[8] : Jy[9];
+    const int kk = k < 3 ? k : k - 3;
+    o.xr14 = k < 3 ? Jx[8] : Jx[9];
+    o.yr14 = k < 3 ? Jy[8] : Jy[9];
+    o.t014 = kk == 0 ? S[4] : (kk == 1 ? S[6] : S[12]);
+    o.t114 = kk == 0 ? S[5] : (kk == 1 ? S[7] : S[13]);
+    o.br15 = k == 0 ? S[8] : k == 1 ? S[9] : k == 2 ? S[14] : k == 3 ? S[10] : k == 4 ? S[15] : S[16];
+    const int r = (lane >> 2) & 3, c = lane & 3;
+    o.hcr = r == 0 ? o.Hcd[0] : r == 1 ? o.Hcd[1] : r == 2 ? o.Hcd[2] : o.Hcd[3];
+    o.hcc = c == 0 ? o.Hcd[0] : c == 1 ? o.Hcd[1] : c == 2 ? o.Hcd[2] : o.Hcd[3];
+  }
 }
 
+// index of the (o1 <= o2) pair of non-host slots in the production accD layout
+__host__ __device__ constexpr int dpair(int o1, int o2) { return o1 * 7 - (o1 * (o1 - 1)) / 2 + (o2 - o1); }
+
+// The lane's accumulators of its block (see hs_kernels.h, HS_E_TOP).  fp32, the reference's per-update
+// expressions (Include/MatrixAccumulators.h), in the wave's point order.
+template <bool kExact>
+struct LinAcc {
+  static constexpr int ND = kExact ? HS_ND_EXACT : HS_ND_PROD;
+  float T[HS_E_TOP];  // AccumulatorApprox entries of (host, t): see acc_point
+  float D[ND];        // accD[host + t1 nF + t2 nF^2][row][col], lane = 8 row + col
+  float E[5];         // accE[host + t nF][k][0..3], accEB[host + t nF][k]
+  float C;            // accHcc[r][c] (lanes 0..15, lane = 4r + c), accbc[r] (lanes 16..19)
+  double e, sid, np;  // energy, sum |idepth|, points
+};
+
+template <bool kExact>
+__device__ __forceinline__ void acc_point(LinAcc<kExact>& A, const LinPt& P, int h, int lane) {
+  // ---- AccumulatedTopHessianSSE::addPoint<0> of the lane's residual: AccumulatorApprox::update / updateTopRight /
+  // updateBotRight (Include/MatrixAccumulators.h:754-915).  Lane (t, k) owns, of the 13x13 (host, t) block:
+  //   T[j]  Data (j, k), j <= k (x/y column k, the rows uniform)      T[8], T[9]  Data (k, 8), (k, 9)
+  //   T[10] Data (8,8) / (8,9) / (9,9) on lanes 0 / 1 / 2            T[11..13]   TopRight (k, a / b / r)
+  //   T[14] TopRight (8 + k/3, k%3) on lanes 0..5                     T[15]       BotRight[k] on lanes 0..5
+  // Entries a lane computes for j > k / k >= 3 / k >= 6 are never read (hs_k_reduce decodes the owners only).
+  if (P.active) {
+    const float a_ = P.S[1], b_ = P.S[3], c_ = P.S[2];  // JIdx2 00, 01, 11
+    const float xk = P.xk, yk = P.yk;
+    // Data[(r, c >= r)] += a x_c x_r + c y_c y_r + b (x_c y_r + y_c x_r), left to right
+    auto dat = [&](float xr, float yr, float xc, float yc) {
+      return ((a_ * xc) * xr + (c_ * yc) * yr) + b_ * ((xc * yr) + (yc * xr));
+    };
+#pragma unroll
+    for (int j = 0; j < 8; j++) A.T[j] += dat(P.Jx[j], P.Jy[j], xk, yk);
+    A.T[8] += dat(xk, yk, P.Jx[8], P.Jy[8]);
+    A.T[9] += dat(xk, yk, P.Jx[9], P.Jy[9]);
+    A.T[10] += dat(P.xr10, P.yr10, P.xc10, P.yc10);
+    // TopRight[3 r + c] += x_r TR0c + y_r TR1c with (TR00, TR10, TR01, TR11, TR02, TR12) = (JabJIdx 00, 01, 10, 11,
+    // JI_r 0, 1)
+    A.T[11] += xk * P.S[4] + yk * P.S[5];
+    A.T[12] += xk * P.S[6] + yk * P.S[7];
+    A.T[13] += xk * P.S[12] + yk * P.S[13];
+    A.T[14] += P.xr14 * P.t014 + P.yr14 * P.t114;
+    // BotRight (Jab2 00, 01, Jab_r 0, Jab2 11, Jab_r 1, rr)
+    A.T[15] += P.br15;
+    // ---- AccumulatedSCHessianSSE::addPoint (Src/AccumulatedSCHessian.cpp:50-51): accE update(JpJdF, Hcd, HdiF),
+    // accEB update(JpJdF, HdiF * bdSumF)
+    const float wl = P.HdiF * P.jj;
+#pragma unroll
+    for (int c = 0; c < 4; c++) A.E[c] += wl * P.Hcd[c];
+    A.E[4] += (P.HdiF * P.bdSumF) * P.jj;
+  }
+  // ---- accD[host + t1 nF + t2 nF^2].update(JpJdF_t1, JpJdF_t2, HdiF) (Src/AccumulatedSCHessian.cpp:38-48): lane
+  // (row, col) = (lane >> 3, lane & 7); JpJdF[t][i] sits in lane 8t + i (zero unless active)
+  {
+    const int dr = lane >> 3, dc = lane & 7;
+    float j1[7], j2[7];
+#pragma unroll
+    for (int o = 0; o < 7; o++) {
+      const int tt = o + (o >= h ? 1 : 0);
+      j1[o] = __shfl(P.jj, tt * 8 + dr);
+      j2[o] = __shfl(P.jj, tt * 8 + dc);
+    }
+#pragma unroll
+    for (int o1 = 0; o1 < 7; o1++) {
+      const float wl = P.HdiF * j1[o1];
+#pragma unroll
+      for (int o2 = kExact ? 0 : o1; o2 < 7; o2++) A.D[kExact ? o1 * 7 + o2 : dpair(o1, o2)] += wl * j2[o2];
+    }
+  }
+  // ---- accHcc.update(Hcd, Hcd, HdiF), accbc.update(Hcd, bdSumF * HdiF) (Src/AccumulatedSCHessian.cpp:32-33)
+  if (P.mask != 0u) A.C += lane < 16 ? (P.HdiF * P.hcr) * P.hcc : (P.bdSumF * P.HdiF) * P.hcc;
+  A.e += P.eSum;
+  A.sid += (double)fabsf(P.idep);
+  A.np += 1.0;
+}
+
+template <bool kExact>
+__device__ __forceinline__ void lin_block(const HsLinArgs& a) {
+  extern __shared__ float lin_stage[];  // [4 waves][ne][64] fp32 partials, then [4][3] fp64 energies
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int b = blockIdx.x;
+  int h = 0;  // the block's host: from the kernel-argument block boundaries, no load
+#pragma unroll
+  for (int i = 1; i < HS_MAXF; i++) h += (i < a.nF && b >= a.blk_begin[i]) ? 1 : 0;
+  const int nb = a.blk_begin[h + 1] - a.blk_begin[h], q = b - a.blk_begin[h];
+  const int hb = a.host_begin[h], nh = a.host_begin[h + 1] - hb;
+  const int pb = hb + (int)((long long)nh * q / nb), pe = hb + (int)((long long)nh * (q + 1) / nb);
+  HS_TRACE(a, 0);
+  LinAcc<kExact> A;
+#pragma unroll
+  for (int i = 0; i < HS_E_TOP; i++) A.T[i] = 0.f;
+#pragma unroll
+  for (int i = 0; i < LinAcc<kExact>::ND; i++) A.D[i] = 0.f;
+#pragma unroll
+  for (int i = 0; i < 5; i++) A.E[i] = 0.f;
+  A.C = 0.f;
+  A.e = A.sid = A.np = 0.0;
+  if (wv < a.W) {
+    for (int p = pb + wv; p < pe; p += a.W) {  // wave-uniform
+      LinPt P;
+      lin_point(a, p, h, lane, P);
+      if (a.accumulate) acc_point<kExact>(A, P, h, lane);
+    }
+  }
+  HS_TRACE(a, 1);
+  if (!a.accumulate) return;
+  // the waves' partials, summed in wave order (fp32) into the block partial; the energies in fp64
+  constexpr int NE = hs_ne(kExact);
+  float* my = lin_stage + wv * NE * 64;
+#pragma unroll
+  for (int i = 0; i < HS_E_TOP; i++) my[i * 64 + lane] = A.T[i];
+#pragma unroll
+  for (int i = 0; i < LinAcc<kExact>::ND; i++) my[(HS_E_TOP + i) * 64 + lane] = A.D[i];
+#pragma unroll
+  for (int i = 0; i < 5; i++) my[(HS_E_TOP + LinAcc<kExact>::ND + i) * 64 + lane] = A.E[i];
+  my[(NE - 1) * 64 + lane] = A.C;
+  double* se = reinterpret_cast<double*>(lin_stage + 4 * NE * 64);
+  if (lane == 0) {
+    se[wv * 3 + 0] = A.e;
+    se[wv * 3 + 1] = A.sid;
+    se[wv * 3 + 2] = A.np;
+  }
+  __syncthreads();
+  float* out = a.part + (size_t)b * NE * 64;
+  for (int i = tid; i < NE * 64; i += 256) {
+    float s = lin_stage[i];
+    for (int w = 1; w < a.W; w++) s += lin_stage[w * NE * 64 + i];
+    out[i] = s;
+  }
+  if (tid < 3) {
+    double s = se[tid];
+    for (int w = 1; w < a.W; w++) s += se[w * 3 + tid];
+    a.part_e[(size_t)b * 4 + tid] = s;
+  }
+  HS_TRACE(a, 2);
+}
+}  // namespace
+
+__global__ __launch_bounds__(256) void hs_k_lin(HsLinArgs a) { lin_block<false>(a); }
+__global__ __launch_bounds__(256) void hs_k_lin_exact(HsLinArgs a) { lin_block<true>(a); }
+
 // =====================================================================================================
-// accumulate: (host i, target slot j, split s) blocks + energy / Hcc,bc / energy threshold blocks
+// reduce + stitch: (host, chunk) blocks sum the host's block partials in block order; the last chunk block of a
+// host stitches the host (fp64) into the host's slot.  Two more blocks: the energy, setNewFrameEnergyTH.
 // =====================================================================================================
 namespace {
-constexpr int ACC_TILE = 64;  // points per LDS tile (one wave does the order-preserving compaction)
-// per-point LDS record: Jacobian digest of residual (p, j) | 1 | 0 | HdiF | bdSumF | Hcd | JpJdF of all slots
-constexpr int R_ONE = 36, R_ZERO = 37, R_HDI = 38, R_BDS = 39, R_HCD = 40, R_JP = 44, R_N = 108;
-struct AccLds {
-  float rec[ACC_TILE][R_N];  // also the staging of the waves' partials (4 x HS_PART_N floats)
-  unsigned char m[ACC_TILE];
-  unsigned char list[ACC_TILE];
-  int cnt;
-  int wcnt[4][16];
-};
-static_assert(ACC_TILE * R_N >= 4 * HS_PART_N, "partial staging fits in the tile records");
-
-// linearizeAll's energy (+ the sumNID / numID statistics of doStepFromBackup); fixed-order tree in fp64
-__device__ void acc_energy_block(const HsAccArgs& a) {
-  __shared__ double red[256], red2[256];
+// linearizeAll's energy (+ the sumNID / numID statistics of doStepFromBackup): block partials in block order
+__device__ void red_energy_block(const HsRedArgs& a) {
+  __shared__ double red[3][256];
   const int tid = threadIdx.x;
-  double s = 0.0, s2 = 0.0;
-  for (int p = tid; p < a.nP; p += 256) {
-    s += a.p_energy[p];
-    s2 += (double)fabsf(a.idepth[p]);
-  }
-  red[tid] = s;
-  red2[tid] = s2;
+  double s[3] = {0.0, 0.0, 0.0};
+  const int per = (a.nblk + 255) / 256, b0 = tid * per, b1 = min(a.nblk, b0 + per);  // contiguous runs
+  for (int b = b0; b < b1; b++)
+#pragma unroll
+    for (int k = 0; k < 3; k++) s[k] += a.part_e[(size_t)b * 4 + k];
+#pragma unroll
+  for (int k = 0; k < 3; k++) red[k][tid] = s[k];
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
-    if (tid < o) {
-      red[tid] += red[tid + o];
-      red2[tid] += red2[tid + o];
-    }
+    if (tid < o)
+#pragma unroll
+      for (int k = 0; k < 3; k++) red[k][tid] += red[k][tid + o];
     __syncthreads();
   }
-  if (tid == 0) {
-    a.energy_out[0] = red[0];
-    a.energy_out[1] = red2[0];
-    a.energy_out[2] = (double)a.nP;
-  }
-}
-
-// accHcc / accbc over all points with an active residual (Src/AccumulatedSCHessian.cpp:32-33);
-// 256 per-thread fp32 accumulators summed in fp64 in a fixed order (the reference sums its
-// per-thread fp32 accumulators in fp64)
-__device__ void acc_hcc_block(const HsAccArgs& a) {
-  __shared__ float red[20][257];
-  __shared__ double part[20][12];
-  const int tid = threadIdx.x;
-  float acc[20];
-  for (int e = 0; e < 20; e++) acc[e] = 0.f;
-  for (int p = tid; p < a.nP; p += 256) {
-    if (a.actmask[p] == 0) continue;
-    const float hdi = a.HdiF[p], bds = a.bdSumF[p];
-    const float4 hc4 = reinterpret_cast<const float4*>(a.Hcd)[p];
-    const float hc[4] = {hc4.x, hc4.y, hc4.z, hc4.w};
-    for (int rr = 0; rr < 4; rr++) {
-      const float wl = hdi * hc[rr];
-      for (int c = 0; c < 4; c++) acc[rr * 4 + c] += wl * hc[c];
-      acc[16 + rr] += bds * hdi * hc[rr];
-    }
-  }
-  for (int e = 0; e < 20; e++) red[e][tid] = acc[e];
-  __syncthreads();
-  const int e = tid / 12, l = tid % 12;
-  if (tid < 240) {
-    double s = 0.0;
-    for (int q = l; q < 256; q += 12) s += (double)red[e][q];
-    part[e][l] = s;
-  }
-  __syncthreads();
-  if (tid < 20) {
-    double t = 0.0;
-    for (int q = 0; q < 12; q++) t += part[tid][q];
-    a.hccbc[tid] = t;
-    // accHcc into the calib block of H_sc, accbc into b_sc (stitchDoubleMT, Include/AccumulatedSCHessian.h:92-99)
-    const int n = 4 + 8 * a.nF;
-    if (tid < 16) atomicAdd(&a.stitch.HSC[(tid >> 2) * n + (tid & 3)], t);
-    else atomicAdd(&a.stitch.bSC[tid - 16], t);
-  }
+  if (tid < 3) a.sysE[tid] = red[tid][0];
 }
 
 // setNewFrameEnergyTH: k-th smallest candidate by a 4-pass radix select with a parallel bin scan.
 // Candidates: one float per point and rank (-1 / negative = none); the ranks' arrays are all-gathered so
 // every rank selects over the same union and computes the same threshold.
-__device__ void acc_energy_th_block(const HsAccArgs& a) {
+__device__ void red_energy_th_block(const HsRedArgs& a) {
   __shared__ unsigned int hist[256], scan[256];
   __shared__ unsigned int s_prefix, s_mask, s_k, s_n;
   const int tid = threadIdx.x;
@@ -658,225 +718,6 @@ __device__ void acc_energy_th_block(const HsAccArgs& a) {
   }
 }
 
-// operand offsets of one AccumulatorApprox entry evaluated as ((a*xc)*xr + (c*yc)*yr) + b*((xc*yr) + (yc*xr));
-// TopRight (xr*T0 + yr*T1) and BotRight (v) are that expression with 1 / 0 operands (same rounding)
-struct TopRole {
-  int oa = R_ZERO, ob = R_ZERO, oc = R_ZERO, oxr = R_ZERO, oxc = R_ZERO, oyr = R_ZERO, oyc = R_ZERO;
-  bool isData = false;
-};
-__device__ __forceinline__ TopRole top_role(int e) {
-  TopRole t;
-  if (e < 55) {
-    int er = 0, ec = 0, idx = 0;
-    for (int rr = 0; rr < 10; rr++)
-      for (int cc = rr; cc < 10; cc++) {
-        if (idx == e) { er = rr; ec = cc; }
-        idx++;
-      }
-    t.isData = true;
-    t.oa = HS_JR_JIDX2 + 0; t.ob = HS_JR_JIDX2 + 1; t.oc = HS_JR_JIDX2 + 2;
-    t.oxr = HS_JR_X + er; t.oxc = HS_JR_X + ec; t.oyr = HS_JR_Y + er; t.oyc = HS_JR_Y + ec;
-  } else if (e < 85) {
-    const int er = (e - 55) / 3, ec = (e - 55) % 3;
-    t.oa = ec == 0 ? HS_JR_JABJIDX + 0 : (ec == 1 ? HS_JR_JABJIDX + 2 : HS_JR_JIR + 0);
-    t.oc = ec == 0 ? HS_JR_JABJIDX + 1 : (ec == 1 ? HS_JR_JABJIDX + 3 : HS_JR_JIR + 1);
-    t.oxr = HS_JR_X + er; t.oyr = HS_JR_Y + er; t.oxc = R_ONE; t.oyc = R_ONE;
-  } else if (e < HS_TOP_N) {
-    const int ec = e - 85;
-    t.oa = ec == 0 ? HS_JR_JAB2 + 0
-         : ec == 1 ? HS_JR_JAB2 + 1
-         : ec == 2 ? HS_JR_JABR + 0
-         : ec == 3 ? HS_JR_JAB2 + 2
-         : ec == 4 ? HS_JR_JABR + 1 : HS_JR_RR;
-    t.oxr = t.oxc = t.oyr = t.oyc = R_ONE;
-  }
-  return t;
-}
-struct AccOps {
-  float t0[7], t1[7];  // top entry operands (lane, 64 + lane)
-  float hdi, wj, x[HS_MAXF];  // accD: HdiF, JpJdF[j][dr], JpJdF[k][dc]
-  float ex, ey;        // accE / accEB operands
-  unsigned m;
-};
-}  // namespace
-
-// Stages one tile of per-point records into LDS: all global loads are issued before any LDS store
-// (clamped, always-valid addresses), then the order-preserving list of points active into j is built.
-__device__ __forceinline__ void acc_load_tile(const HsAccArgs& a, AccLds& T, int t0, int tn, int j) {
-  const int tid = threadIdx.x;
-  const int qa0 = min((tid + 0) >> 4, tn - 1), qa1 = min((tid + 256) >> 4, tn - 1);
-  const int qa2 = min((tid + 512) >> 4, tn - 1), qa3 = min((tid + 768) >> 4, tn - 1);
-  const int w = tid & 15;
-  const float4* jp = reinterpret_cast<const float4*>(a.JpJdF);
-  const float4 j0 = jp[(size_t)(t0 + qa0) * 16 + w], j1 = jp[(size_t)(t0 + qa1) * 16 + w];
-  const float4 j2 = jp[(size_t)(t0 + qa2) * 16 + w], j3 = jp[(size_t)(t0 + qa3) * 16 + w];
-  constexpr int NW = HS_JREC / 4;
-  const int r0 = tid, r1 = tid + 256, r2 = tid + 512;
-  const float4* jr = reinterpret_cast<const float4*>(a.Jrec);
-  const float4 k0 = jr[((size_t)(t0 + min(r0 / NW, tn - 1)) * 8 + j) * NW + r0 % NW];
-  const float4 k1 = jr[((size_t)(t0 + min(r1 / NW, tn - 1)) * 8 + j) * NW + r1 % NW];
-  const float4 k2 = jr[((size_t)(t0 + min(r2 / NW, tn - 1)) * 8 + j) * NW + r2 % NW];
-  const int qs = min(tid, tn - 1);
-  const unsigned char mk = a.actmask[t0 + qs];
-  const float4 hcd = reinterpret_cast<const float4*>(a.Hcd)[t0 + qs];
-  const float hdi = a.HdiF[t0 + qs], bds = a.bdSumF[t0 + qs];
-  __syncthreads();  // the previous tile's records are no longer read
-  // rows >= tn receive copies of the last point; they are never listed
-  *reinterpret_cast<float4*>(&T.rec[(tid + 0) >> 4][R_JP + 4 * w]) = j0;
-  *reinterpret_cast<float4*>(&T.rec[(tid + 256) >> 4][R_JP + 4 * w]) = j1;
-  *reinterpret_cast<float4*>(&T.rec[(tid + 512) >> 4][R_JP + 4 * w]) = j2;
-  *reinterpret_cast<float4*>(&T.rec[(tid + 768) >> 4][R_JP + 4 * w]) = j3;
-  *reinterpret_cast<float4*>(&T.rec[r0 / NW][4 * (r0 % NW)]) = k0;
-  *reinterpret_cast<float4*>(&T.rec[r1 / NW][4 * (r1 % NW)]) = k1;
-  if (r2 < ACC_TILE * NW) *reinterpret_cast<float4*>(&T.rec[r2 / NW][4 * (r2 % NW)]) = k2;
-  if (tid < ACC_TILE) {
-    T.m[tid] = mk;
-    *reinterpret_cast<float4*>(&T.rec[tid][R_HCD]) = hcd;
-    T.rec[tid][R_HDI] = hdi;
-    T.rec[tid][R_BDS] = bds;
-    T.rec[tid][R_ONE] = 1.0f;
-    T.rec[tid][R_ZERO] = 0.0f;
-    const bool act = tid < tn && ((mk >> j) & 1u);
-    const unsigned long long bal = __ballot(act);
-    if (act) T.list[__popcll(bal & ((1ull << tid) - 1ull))] = (unsigned char)tid;
-    if (tid == 0) T.cnt = __popcll(bal);
-  }
-  __syncthreads();
-}
-
-// One (host i, target j, split s) accumulator block.  kBlocked: the reference's 1k/1m flush blocking is
-// emulated (needed when a block sums more than 1000 updates; below that shiftUp never fires and
-// finish() returns the plain running sum, so the counters are dropped).
-// One (host i, target j, split s) block: its 4 waves each accumulate a contiguous share of the split's
-// points (a.W = 1: wave 0 takes all of them, i.e. the single-thread reference order) and write one partial
-// each.  Lane roles: top entries lane / 64+lane, accD (j, k=0..7)[lane>>3][lane&7], accE / accEB lane < 40.
-// kBlocked: the reference's 1k/1m flush blocking is emulated (needed above 1000 updates per partial;
-// below that shiftUp never fires and finish() is the plain running sum, so the counters are dropped).
-template <bool kBlocked>
-__device__ __forceinline__ void acc_pair_block(const HsAccArgs& a, AccLds& T) {
-  const int nF = a.nF, S = a.S, W = a.W;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int b = blockIdx.x;
-  const int ij = b / S, s = b % S;
-  const int i = ij % nF, j = ij / nF;  // host i, target j (accumulator index i + nF*j)
-  const int hb = a.host_pt_begin[i], he = a.host_pt_begin[i + 1];
-  const int span = he - hb;
-  const int pb = hb + (int)((long long)span * s / S), pe = hb + (int)((long long)span * (s + 1) / S);
-
-  const TopRole r0 = top_role(lane), r1 = top_role(64 + lane);
-  const int dr = lane >> 3, dc = lane & 7;
-  const int owj = R_JP + j * 8 + dr;
-  int oex = R_ZERO, oey = R_ZERO;
-  if (lane < 32) { oex = R_JP + j * 8 + (lane >> 2); oey = R_HCD + (lane & 3); }
-  else if (lane < 40) { oex = R_BDS; oey = R_JP + j * 8 + (lane - 32); }
-
-  Blk top0, top1, d[HS_MAXF], ex;
-  BlkCnt ctop, cd[HS_MAXF], cex;
-  int nTop = 0, nD[HS_MAXF];
-#pragma unroll
-  for (int k = 0; k < HS_MAXF; k++) nD[k] = 0;
-
-  auto load = [&](int q, AccOps& o) {
-    const float* R = T.rec[q];
-    o.t0[0] = R[r0.oa]; o.t0[1] = R[r0.ob]; o.t0[2] = R[r0.oc]; o.t0[3] = R[r0.oxr]; o.t0[4] = R[r0.oxc];
-    o.t0[5] = R[r0.oyr]; o.t0[6] = R[r0.oyc];
-    o.t1[0] = R[r1.oa]; o.t1[1] = R[r1.ob]; o.t1[2] = R[r1.oc]; o.t1[3] = R[r1.oxr]; o.t1[4] = R[r1.oxc];
-    o.t1[5] = R[r1.oyr]; o.t1[6] = R[r1.oyc];
-    o.hdi = R[R_HDI]; o.wj = R[owj];
-#pragma unroll
-    for (int k = 0; k < HS_MAXF; k++) o.x[k] = R[R_JP + k * 8 + dc];
-    o.ex = R[oex]; o.ey = R[oey];
-    o.m = T.m[q];
-  };
-  auto topv = [](const float* t) {  // a b c xr xc yr yc
-    return ((t[0] * t[4]) * t[3] + (t[2] * t[6]) * t[5]) + t[1] * ((t[4] * t[5]) + (t[6] * t[3]));
-  };
-
-  for (int t0 = pb; t0 < pe; t0 += ACC_TILE) {
-    const int tn = min(ACC_TILE, pe - t0);
-    acc_load_tile(a, T, t0, tn, j);
-    HS_TRACE(a, 2);
-    const int cnt = T.cnt;
-    const int c0 = wv < W ? (cnt * wv) / W : cnt, c1 = wv < W ? (cnt * (wv + 1)) / W : cnt;
-    AccOps nx;
-    if (c0 < c1) load(T.list[c0], nx);
-    for (int c = c0; c < c1; c++) {
-      const AccOps o = nx;
-      if (c + 1 < c1) load(T.list[c + 1], nx);
-      // ---- AccumulatedTopHessianSSE::addPoint<0>: update() adds Data then shiftUp; BotRight / TopRight after
-      const float u0 = topv(o.t0), u1 = topv(o.t1);
-      const float wl = o.hdi * o.wj;
-      if (kBlocked) {
-        const int f = ctop.bump();
-        if (r0.isData) top0.A += u0;
-        if (r1.isData) top1.A += u1;
-        if (f) { top0.flush(f); top1.flush(f); }
-        if (!r0.isData) top0.A += u0;
-        if (!r1.isData) top1.A += u1;
-#pragma unroll
-        for (int k = 0; k < HS_MAXF; k++)
-          if ((o.m >> k) & 1u) {  // wave-uniform
-            d[k].A += wl * o.x[k];
-            d[k].flush(cd[k].bump());
-          }
-        ex.A += (o.hdi * o.ex) * o.ey;
-        ex.flush(cex.bump());
-      } else {
-        top0.A += u0;
-        top1.A += u1;
-#pragma unroll
-        for (int k = 0; k < HS_MAXF; k++) {
-          const bool bk = (o.m >> k) & 1u;
-          d[k].A = bk ? d[k].A + wl * o.x[k] : d[k].A;
-          nD[k] += bk ? 1 : 0;
-        }
-        ex.A += (o.hdi * o.ex) * o.ey;
-        nTop++;
-      }
-    }
-  }
-  HS_TRACE(a, 1);
-  // the waves' partials are combined in wave order in fp64 (the reference sums its per-thread fp32
-  // accumulators in fp64) into one partial of this split
-  __syncthreads();  // tile records are no longer read
-  float* stage = &T.rec[0][0];
-  if (wv < W) {
-    float* Ps = stage + wv * HS_PART_N;
-    // finish(): A1m = (A1k + A) + A1m  (== A when nothing was flushed)
-    Ps[lane] = top0.finish();
-    if (64 + lane < 96) Ps[64 + lane] = 64 + lane < HS_TOP_N ? top1.finish() : 0.f;
-#pragma unroll
-    for (int k = 0; k < HS_MAXF; k++) Ps[96 + k * 64 + lane] = d[k].finish();
-    if (lane < 40) Ps[96 + 512 + lane] = ex.finish();
-    if (lane == 0) {
-      T.wcnt[wv][0] = kBlocked ? ctop.total() : nTop;
-      T.wcnt[wv][9] = kBlocked ? cex.total() : nTop;
-    }
-    if (lane < HS_MAXF) {
-      int v = 0;
-#pragma unroll
-      for (int k = 0; k < HS_MAXF; k++) v = k == lane ? (kBlocked ? cd[k].total() : nD[k]) : v;
-      T.wcnt[wv][1 + lane] = v;
-    }
-  }
-  __syncthreads();
-  double* P = a.part + ((size_t)ij * S + s) * HS_PART_N;
-  int* PC = a.part_cnt + ((size_t)ij * S + s) * 16;
-  // the partial is handed to the pair's stitching block (hs_k_accumulate): sc1 (write-through) stores
-  for (int e = tid; e < HS_PART_N; e += 256) {
-    double sum = 0.0;
-    for (int w = 0; w < W; w++) sum += (double)stage[w * HS_PART_N + e];
-    __hip_atomic_store(&P[e], sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if (tid < 10) {
-    int c = 0;
-    for (int w = 0; w < W; w++) c += T.wcnt[w][tid];
-    __hip_atomic_store(&PC[tid], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-__device__ void stitch_pair(const HsStitchArgs& a, int ij, long long* trace);
-
 // agent-scope relaxed load = global_load ... sc1 (bypasses this CU's L1; the L2 line of a write-through
 // sc1 store is dropped, so the load is served from memory side)
 template <typename T>
@@ -884,235 +725,289 @@ __device__ __forceinline__ T ld_sc1(const T* p) {
   return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ __launch_bounds__(256) void hs_k_accumulate(HsAccArgs a) {
-  const int nb = a.nF * a.nF * a.S;
-  const int b = blockIdx.x;
+// the (R, C) entry (R <= C) of host-sum octet t's 13x13 AccumulatorApprox block [calib 4 | xi 6 | a | b | r]
+// from the owner lane of the layout in acc_point
+__device__ __forceinline__ double top_entry(const double* hsm, int t, int R, int C) {
+  int e, k;
+  if (C < 8) { e = R; k = C; }                                     // Data (R, C <= 7): lane C, T[R]
+  else if (C < 10) {
+    if (R < 8) { e = C; k = R; }                                   // Data (R, 8 | 9): lane R, T[8 | 9]
+    else { e = 10; k = (R == 8 && C == 8) ? 0 : (R == 8 ? 1 : 2); }  // (8,8) (8,9) (9,9): lanes 0 1 2, T[10]
+  } else if (R < 10) {
+    const int col = C - 10;                                        // TopRight (R, col)
+    if (R < 8) { e = 11 + col; k = R; }
+    else { e = 14; k = (R - 8) * 3 + col; }
+  } else {                                                         // BotRight
+    e = 15;
+    k = R == 10 ? C - 10 : (R == 11 ? 2 + C - 10 : 5);
+  }
+  return hsm[e * 64 + t * 8 + k];
+}
+
+// Stitch of host i (stitchDoubleInternal, Src/AccumulatedTopHessian.cpp:218-280 and
+// Src/AccumulatedSCHessian.cpp:54-133, in fp64) by one 256-thread block, from the host's summed accumulators.
+// Top: per target t the reference's sandwiches adH A adH^T -> (i,i), adT A adT^T -> (t,t), adH A adT^T -> (i,t),
+// adH / adT A84 -> calib columns, adH / adT a8r -> b.  Schur: the host's sum over (t1, t2) of the four sandwiches
+// adX[i,t1] D(t1,t2) adY[i,t2]^T is A D A^T with A(f, t) = [f = i] adH[i,t] + [f = t] adT[i,t] (8nF x 8nF), formed
+// as Y = A D (Y(i, t2) = sum_t1 adH[t1] D(t1,t2), Y(f, t2) = adT[f] D(f, t2)) then Z = Y A^T, in a fixed order.
+// Every output entry is written once (no atomics): the slot holds the upper triangle of HA - sc HSC (diagonal
+// HA (1+lambda) - sc HSC, the solve adds the priors' share) and bA - bSC; `sep` (granular read-back) HA | bA and
+// HSC | bSC separately.
+__device__ void stitch_host(const HsRedArgs& a, int i) {
+  const int nF = a.nF, n = 4 + 8 * nF, nn = n * n, SL = nn + n;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int ND = a.exact ? HS_ND_EXACT : HS_ND_PROD;
+  const int NE64 = a.ne * 64;
+  const int oE = (HS_E_TOP + ND) * 64;  // accE / accEB / Hcc entries
+  __shared__ double hsm[hs_ne(true) * 64];
+  __shared__ double aH[HS_MAXF][64], aT[HS_MAXF][64];
+  __shared__ double A88[HS_MAXF][64], A84[HS_MAXF][32], a8r[HS_MAXF][8], A44[16], a4r[4];
+  __shared__ double Ys[HS_MAXF * HS_MAXF][64];
+  {
+    const double* src = a.hostsum + (size_t)i * NE64;
+    double v[hs_ne(true) * 64 / 256 + 1];
+#pragma unroll
+    for (int u = 0; u < hs_ne(true) * 64 / 256 + 1; u++) v[u] = ld_sc1(&src[min(tid + 256 * u, NE64 - 1)]);
+    double ad[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int q = tid + 256 * u, kk = min(q >> 7, nF - 1), w = q & 127;
+      ad[u] = (w < 64 ? a.adHost : a.adTarget)[(i + nF * kk) * 64 + (w & 63)];
+    }
+#pragma unroll
+    for (int u = 0; u < hs_ne(true) * 64 / 256 + 1; u++)
+      if (tid + 256 * u < NE64) hsm[tid + 256 * u] = v[u];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int q = tid + 256 * u, kk = q >> 7, w = q & 127;
+      if (kk < nF) (w < 64 ? aH[kk] : aT[kk])[w & 63] = ad[u];
+    }
+  }
+  __syncthreads();
+  // ---- decode the top blocks: A88 = [xi a b] x [xi a b], A84 = [xi a b] x calib, a8r = [xi a b] x r
+  for (int q = tid; q < nF * 104; q += 256) {
+    const int t = q / 104, e = q % 104;
+    if (e < 64) {
+      const int R = 4 + (e >> 3), C = 4 + (e & 7);
+      A88[t][e] = top_entry(hsm, t, min(R, C), max(R, C));
+    } else if (e < 96) {
+      const int r = (e - 64) >> 2, c = (e - 64) & 3;
+      A84[t][(e - 64)] = top_entry(hsm, t, c, 4 + r);
+    } else {
+      a8r[t][e - 96] = top_entry(hsm, t, 4 + (e - 96), 12);
+    }
+  }
+  if (tid < 20) {  // A44 / a4r: summed over the targets in target order
+    double s = 0.0;
+    for (int t = 0; t < nF; t++)
+      s += tid < 16 ? top_entry(hsm, t, min(tid >> 2, tid & 3), max(tid >> 2, tid & 3)) : top_entry(hsm, t, tid - 16, 12);
+    if (tid < 16) A44[tid] = s;
+    else a4r[tid - 16] = s;
+  }
+  // D(t1, t2)[l][c] from the host sums (production: only t1 <= t2 is stored, D(t2, t1) = D(t1, t2)^T)
+  auto Dv = [&](int t1, int t2, int l, int c) -> double {
+    const int o1 = t1 - (t1 > i ? 1 : 0), o2 = t2 - (t2 > i ? 1 : 0);
+    if (a.exact) return hsm[(HS_E_TOP + o1 * 7 + o2) * 64 + l * 8 + c];
+    return o1 <= o2 ? hsm[(HS_E_TOP + dpair(o1, o2)) * 64 + l * 8 + c] : hsm[(HS_E_TOP + dpair(o2, o1)) * 64 + c * 8 + l];
+  };
+  // ---- Y = A D: one wave per 8x8 block, lane (r, c)
+  const int r = lane >> 3, c = lane & 7;
+  for (int blk = wv; blk < nF * nF; blk += 4) {
+    const int f = blk / nF, t2 = blk % nF;
+    double y = 0.0;
+    if (t2 != i) {
+      if (f == i) {
+        for (int t1 = 0; t1 < nF; t1++) {
+          if (t1 == i) continue;
+#pragma unroll
+          for (int l = 0; l < 8; l++) y += aH[t1][r * 8 + l] * Dv(t1, t2, l, c);
+        }
+      } else {
+#pragma unroll
+        for (int l = 0; l < 8; l++) y += aT[f][r * 8 + l] * Dv(f, t2, l, c);
+      }
+    }
+    Ys[blk][lane] = y;
+  }
+  __syncthreads();
+  double* slot = a.slot + (size_t)i * SL;
+  double* sepA = a.sep ? a.sep + (size_t)i * 2 * SL : nullptr;
+  double* sepS = a.sep ? sepA + SL : nullptr;
+  auto put = [&](int R, int C, double ha, double hs, bool diag) {
+    slot[R * n + C] = diag ? ha * a.lambda1 - hs * a.sc : ha - hs * a.sc;
+    if (sepA) {
+      sepA[R * n + C] = ha;
+      sepS[R * n + C] = hs;
+    }
+  };
+  // ---- frame blocks (f <= g), one wave per block, lane (r, c)
+  for (int fb = wv; fb < nF * nF; fb += 4) {
+    const int f = fb / nF, g = fb % nF;
+    if (g < f) continue;
+    double hs = 0.0, ha = 0.0;
+    // Schur Z(f, g) = sum_t2 Y(f, t2) A(g, t2)^T
+    if (f == i && g == i) {
+      for (int t2 = 0; t2 < nF; t2++) {
+        if (t2 == i) continue;
+#pragma unroll
+        for (int l = 0; l < 8; l++) hs += Ys[i * nF + t2][r * 8 + l] * aH[t2][c * 8 + l];
+      }
+    } else if (f == i) {
+#pragma unroll
+      for (int l = 0; l < 8; l++) hs += Ys[i * nF + g][r * 8 + l] * aT[g][c * 8 + l];
+    } else if (g == i) {  // Z(f, i) = Z(i, f)^T
+#pragma unroll
+      for (int l = 0; l < 8; l++) hs += Ys[i * nF + f][c * 8 + l] * aT[f][r * 8 + l];
+    } else {
+#pragma unroll
+      for (int l = 0; l < 8; l++) hs += Ys[f * nF + g][r * 8 + l] * aT[g][c * 8 + l];
+    }
+    // top: (i,i) sum_t adH A88 adH^T, (t,t) adT A88 adT^T, (i,t) adH A88 adT^T (its transpose when t < i)
+    auto sandwich = [&](const double* L, const double* M, const double* Rm, int rr, int cc) {
+      double s = 0.0;
+#pragma unroll
+      for (int l = 0; l < 8; l++) {
+        double x = 0.0;
+#pragma unroll
+        for (int m = 0; m < 8; m++) x += L[rr * 8 + m] * M[m * 8 + l];
+        s += x * Rm[cc * 8 + l];
+      }
+      return s;
+    };
+    if (f == i && g == i) {
+      for (int t = 0; t < nF; t++)
+        if (t != i) ha += sandwich(aH[t], A88[t], aH[t], r, c);
+    } else if (f == g) {
+      ha = sandwich(aT[f], A88[f], aT[f], r, c);
+    } else if (f == i) {
+      ha = sandwich(aH[g], A88[g], aT[g], r, c);
+    } else if (g == i) {
+      ha = sandwich(aH[f], A88[f], aT[f], c, r);
+    }
+    if (f < g || r <= c) put(4 + 8 * f + r, 4 + 8 * g + c, ha, hs, f == g && r == c);
+  }
+  // ---- calib x frame (stored in the calib rows): H(4 + 8f + r, cc), thread = (f, r, cc)
+  if (tid < nF * 32) {
+    const int f = tid >> 5, rr = (tid >> 2) & 7, cc = tid & 3;
+    double ha = 0.0, hs = 0.0;
+    auto prod84 = [&](const double* L, int t) {  // (L A84[t])[rr][cc], (L E[t])[rr][cc]
+      double x = 0.0, y = 0.0;
+#pragma unroll
+      for (int m = 0; m < 8; m++) {
+        x += L[rr * 8 + m] * A84[t][m * 4 + cc];
+        y += L[rr * 8 + m] * hsm[oE + cc * 64 + t * 8 + m];
+      }
+      ha += x;
+      hs += y;
+    };
+    if (f == i) {
+      for (int t = 0; t < nF; t++)
+        if (t != i) prod84(aH[t], t);
+    } else {
+      prod84(aT[f], f);
+    }
+    put(cc, 4 + 8 * f + rr, ha, hs, false);
+  }
+  // ---- calib x calib: A44 (top), accHcc (Schur)
+  if (tid >= 256 - 16) {
+    const int q = tid - (256 - 16), rr = q >> 2, cc = q & 3;
+    if (rr <= cc) put(rr, cc, A44[q], hsm[oE + 5 * 64 + q], rr == cc);
+  }
+  // ---- b: frames (adH / adT a8r, adH / adT accEB), calib (a4r, accbc)
+  if (tid < n) {
+    double ba = 0.0, bs = 0.0;
+    if (tid < 4) {
+      ba = a4r[tid];
+      bs = hsm[oE + 5 * 64 + 16 + tid];
+    } else {
+      const int f = (tid - 4) >> 3, rr = (tid - 4) & 7;
+      auto prod8 = [&](const double* L, int t) {
+        double x = 0.0, y = 0.0;
+#pragma unroll
+        for (int m = 0; m < 8; m++) {
+          x += L[rr * 8 + m] * a8r[t][m];
+          y += L[rr * 8 + m] * hsm[oE + 4 * 64 + t * 8 + m];
+        }
+        ba += x;
+        bs += y;
+      };
+      if (f == i) {
+        for (int t = 0; t < nF; t++)
+          if (t != i) prod8(aH[t], t);
+      } else {
+        prod8(aT[f], f);
+      }
+    }
+    slot[nn + tid] = ba - bs;
+    if (sepA) {
+      sepA[nn + tid] = ba;
+      sepS[nn + tid] = bs;
+    }
+  }
+}
+}  // namespace
+
+__global__ __launch_bounds__(256) void hs_k_reduce(HsRedArgs a) {
+  const int nred = a.nF * a.Q;
+  const int b = blockIdx.x, tid = threadIdx.x;
   HS_TRACE(a, 0);
-  if (b == nb) { acc_energy_block(a); HS_TRACE(a, 15); return; }
-  if (b == nb + 1) { acc_hcc_block(a); HS_TRACE(a, 15); return; }
-  if (b == nb + 2) {
-    if (!a.skip_threshold) acc_energy_th_block(a);
+  if (b == nred) { red_energy_block(a); HS_TRACE(a, 15); return; }
+  if (b == nred + 1) {
+    if (!a.skip_threshold) red_energy_th_block(a);
     HS_TRACE(a, 15);
     return;
   }
-  __shared__ AccLds T;
+  const int h = b / a.Q, q = b % a.Q;
+  const int NE64 = a.ne * 64;
+  const int e = q * 256 + tid;  // entry of the host's [ne][64] accumulators
+  const int b0 = a.blk_begin[h], b1 = a.blk_begin[h + 1];
+  if (e < NE64) {
+    // the host's block partials in block order, fp64 (the reference sums its per-thread fp32 accumulators in
+    // fp64); eight loads in flight per batch
+    double s = 0.0;
+    for (int bb = b0; bb < b1; bb += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) v[u] = a.part[(size_t)min(bb + u, b1 - 1) * NE64 + e];
+#pragma unroll
+      for (int u = 0; u < 8; u++)
+        if (bb + u < b1) s += (double)v[u];
+    }
+    __hip_atomic_store(&a.hostsum[(size_t)h * NE64 + e], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  HS_TRACE(a, 1);
+  // hand-off to the host's stitch (MI355X_MICROARCH.md "Valid forms", first table row; cdna_hip_programming.md §6
+  // Guideline 16): the sums were stored sc1 (write-through); every storing wave drains its stores, then after a
+  // barrier ONE lane adds to the host's ticket; the block whose add returns Q - 1 (the last) stitches the host
+  // with sc1 loads of the sums.  No block waits on another (no spin), so any dispatch order and XCD placement is
+  // safe.  This relies on gfx950's sc1 write-through / L1-bypass semantics (measured form, not an architectural
+  // guarantee): the kernel is built for gfx950 only.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "hs_k_reduce's sc1 hand-off is validated on gfx950 only"
+#endif
   __shared__ int s_last;
-  if (a.blocked) acc_pair_block<true>(a, T);
-  else acc_pair_block<false>(a, T);
-  HS_TRACE(a, 11);
-  // hand-off to the pair's stitch (MI355X_MICROARCH.md "Valid forms", counter row; cdna_hip_programming.md
-  // §6 Guideline 16): the partial was stored sc1 (write-through, no L2 write-back fence needed); every
-  // storing wave drains its stores, then after a barrier ONE lane adds to the pair's ticket; the block
-  // whose add returns S - 1 (the last) stitches the pair with sc1 loads of the partials.  No block waits
-  // on another (no spin), so any dispatch order and XCD placement is safe.
-  const int ij = b / a.S;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0)
-    s_last = __hip_atomic_fetch_add(&a.ticket[ij], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.S - 1;
+  if (tid == 0) s_last = __hip_atomic_fetch_add(&a.ticket[h], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.Q - 1;
   __syncthreads();
   if (s_last) {
-    stitch_pair(a.stitch, ij, a.trace ? a.trace + (size_t)blockIdx.x * 16 : nullptr);
-    if (threadIdx.x == 0)  // ready for the next launch (the kernel boundary orders it)
-      __hip_atomic_store(&a.ticket[ij], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    stitch_host(a, h);
+    if (tid == 0)  // ready for the next launch (the kernel boundary orders it)
+      __hip_atomic_store(&a.ticket[h], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   HS_TRACE(a, 15);
 }
 
-// =====================================================================================================
-// stitch (fp64): one block (64 threads) per (host i, target j)
-// =====================================================================================================
-namespace {
-// index of (r, c) in the 10x10 upper-triangle Data block
-__device__ __forceinline__ int tri_idx(int r, int c) {
-  const int lo = r < c ? r : c, hi = r < c ? c : r;
-  return lo * 10 - (lo * (lo - 1)) / 2 + (hi - lo);
-}
-}  // namespace
-
-// lane (r, c) of one wave: X(r, c) = sum_l PH(r, l) M(l, c) and Y(r, c) = sum_l PT(r, l) M(l, c) (rows r of PH / PT
-// in registers), in l order as the reference's 8x8 products; staged to the wave's LDS scratch tx / ty
-__device__ __forceinline__ void left2(const double ph[8], const double pt[8], const double* M, double* tx, double* ty,
-                                      int lane) {
-  const int c = lane & 7;
-  double x = 0.0, y = 0.0;
-#pragma unroll
-  for (int l = 0; l < 8; l++) {
-    const double m = M[l * 8 + c];
-    x += ph[l] * m;
-    y += pt[l] * m;
+// multi-rank: this rank's host slots summed in slot order + its energies -> one vector for the RCCL all-reduce
+__global__ __launch_bounds__(256) void hs_k_combine(HsCombArgs a) {
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  if (q < a.SL) {
+    double s = 0.0;
+    for (int h = 0; h < a.nF; h++) s += a.slot[(size_t)h * a.SL + q];
+    a.out[q] = s;
+  } else if (q < a.SL + 3) {
+    a.out[q] = a.sysE[q - a.SL];
   }
-  tx[lane] = x;
-  ty[lane] = y;
-}
-// out(r, c) = sum_l T(r, l) B(c, l): the right product of a sandwich (T staged by left2)
-__device__ __forceinline__ double right_t(const double* T, const double* B, int lane) {
-  const int r = lane >> 3, c = lane & 7;
-  double o = 0.0;
-#pragma unroll
-  for (int l = 0; l < 8; l++) o += T[r * 8 + l] * B[c * 8 + l];
-  return o;
-}
-
-// stitch of one (host i, target j) pair by a 256-thread block (4 waves): fp64 sum of the split partials,
-// then the top block (wave 0), the Schur rows (i, j, k) for k = wave, wave+4 (all waves) and the calib / b
-// parts, atomically added into HA / bA / HSC / bSC.  trace: the block's checkpoint row (slots 12 / 14).
-__device__ void stitch_pair(const HsStitchArgs& a, int ij, long long* trace) {
-  const int nF = a.nF, S = a.S;
-  const int i = ij % nF, j = ij / nF;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int n = 4 + 8 * nF;
-  const int iIdx = 4 + 8 * i, jIdx = 4 + 8 * j;
-  __shared__ double E[HS_PART_N];  // summed partial: top 96 | D 8x64 | E 32 | EB 8
-  __shared__ double A88[64], A84[32], a8r[8], aH[64], aT[64];
-  __shared__ double aH2[HS_MAXF][64], aT2[HS_MAXF][64], tmpw[4][128];
-  __shared__ int cnt[16];
-  // ---- everything this pair needs, all loads in flight together
-  const double* P0 = a.part + (size_t)ij * S * HS_PART_N;
-  const int* C0 = a.part_cnt + (size_t)ij * S * 16;
-  if (tid < 64) {
-    aH[tid] = a.adHost[ij * 64 + tid];
-    aT[tid] = a.adTarget[ij * 64 + tid];
-  }
-#pragma unroll
-  for (int u = 0; u < 4; u++) {  // adjoints of (i, k) for all k: 2 * 8 * 64 values
-    const int q = tid + 256 * u, kk = q >> 7, w = q & 127;
-    const int kc = min(kk, nF - 1);
-    const double v = (w < 64 ? a.adHost : a.adTarget)[(i + nF * kc) * 64 + (w & 63)];
-    if (kk < nF) (w < 64 ? aH2[kk] : aT2[kk])[w & 63] = v;
-  }
-  // split partials summed in fp64 in split order (stitchDoubleInternal: accH += acc[tid2].H.cast<double>()
-  // for num > 0; a split with num == 0 made no update, so its partial is exactly +0 and adding it is the
-  // same as skipping it).  sc1 loads (the partials were handed off without an acquire fence), four splits
-  // per batch so the loads of a batch are in flight together.
-  double sum[3] = {0.0, 0.0, 0.0};
-  int csum = 0;
-  for (int s0 = 0; s0 < S; s0 += 4) {
-    double v[4][3];
-    int cv[4];
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const int sq = min(s0 + q, S - 1);
-      const double* Ps = P0 + (size_t)sq * HS_PART_N;
-#pragma unroll
-      for (int u = 0; u < 3; u++) v[q][u] = ld_sc1(&Ps[min(tid + 256 * u, HS_PART_N - 1)]);
-      cv[q] = ld_sc1(&C0[sq * 16 + (tid & 15)]);
-    }
-#pragma unroll
-    for (int q = 0; q < 4; q++)
-      if (s0 + q < S) {
-#pragma unroll
-        for (int u = 0; u < 3; u++) sum[u] += v[q][u];
-        csum += cv[q];
-      }
-  }
-#pragma unroll
-  for (int u = 0; u < 3; u++)
-    if (tid + 256 * u < HS_PART_N) E[tid + 256 * u] = sum[u];
-  if (tid < 16) cnt[tid] = csum;
-  __syncthreads();
-  if (trace && tid == 0) trace[12] = wall_clock64();
-  const double* e = E;
-  const double* Hpc = E + 96 + 512;
-  const double* v8 = E + 96 + 512 + 32;
-  const int r = lane >> 3, c = lane & 7;
-  double* tmp = tmpw[wv];
-  double ahr[8], atr[8];  // this lane's rows r of the adjoints, in registers for every left product
-#pragma unroll
-  for (int l = 0; l < 8; l++) {
-    ahr[l] = aH[r * 8 + l];
-    atr[l] = aT[r * 8 + l];
-  }
-  if (wv == 0 && cnt[0] > 0) {  // top block: AccumulatorApprox::finish -> 13x13 [calib4|xi6|a|b|r]
-    const int R = 4 + r, Cc = 4 + c;
-    double v;
-    if (R < 10 && Cc < 10) {
-      v = e[tri_idx(R, Cc)];
-    } else if (R < 10 || Cc < 10) {
-      const int row = R < 10 ? R : Cc, col = (R < 10 ? Cc : R) - 10;
-      v = e[55 + 3 * row + col];
-    } else {
-      const int bi = (R - 10) + (Cc - 10);  // (a,a) 0, (a,b) 1, (b,b) 3
-      v = e[85 + (bi == 2 ? 3 : bi)];
-    }
-    A88[lane] = v;
-    if (lane < 32) {  // A84 = H[4+r][c]
-      const int rr = lane >> 2, cc = lane & 3;
-      const int RR = 4 + rr;
-      A84[lane] = RR < 10 ? e[tri_idx(cc, RR)] : e[55 + 3 * cc + (RR - 10)];
-    }
-    if (lane < 8) {  // a8r = H[4+r][12]
-      const int RR = 4 + lane;
-      a8r[lane] = RR < 10 ? e[55 + 3 * RR + 2] : (RR == 10 ? e[85 + 2] : e[85 + 4]);
-    }
-    __builtin_amdgcn_wave_barrier();
-    // aH A aH^T, aT A aT^T, aH A aT^T: the two left products once, then three right products
-    left2(ahr, atr, A88, tmp, tmp + 64, lane);
-    __builtin_amdgcn_wave_barrier();
-    const double o1 = right_t(tmp, aH, lane), o2 = right_t(tmp + 64, aT, lane), o3 = right_t(tmp, aT, lane);
-    __builtin_amdgcn_wave_barrier();
-    atomicAdd(&a.HA[(iIdx + r) * n + iIdx + c], o1);
-    atomicAdd(&a.HA[(jIdx + r) * n + jIdx + c], o2);
-    atomicAdd(&a.HA[(iIdx + r) * n + jIdx + c], o3);
-    if (lane < 32) {
-      const int rr = lane >> 2, cc = lane & 3;
-      double s1 = 0.0, s2 = 0.0;
-      for (int l = 0; l < 8; l++) {
-        s1 += aH[rr * 8 + l] * A84[l * 4 + cc];
-        s2 += aT[rr * 8 + l] * A84[l * 4 + cc];
-      }
-      atomicAdd(&a.HA[(iIdx + rr) * n + cc], s1);
-      atomicAdd(&a.HA[(jIdx + rr) * n + cc], s2);
-    }
-    if (lane < 16) atomicAdd(&a.HA[(lane >> 2) * n + (lane & 3)], e[tri_idx(lane >> 2, lane & 3)]);
-    if (lane < 8) {
-      double s1 = 0.0, s2 = 0.0;
-      for (int l = 0; l < 8; l++) {
-        s1 += aH[lane * 8 + l] * a8r[l];
-        s2 += aT[lane * 8 + l] * a8r[l];
-      }
-      atomicAdd(&a.bA[iIdx + lane], s1);
-      atomicAdd(&a.bA[jIdx + lane], s2);
-    }
-    if (lane < 4) atomicAdd(&a.bA[lane], e[55 + 3 * lane + 2]);
-  }
-  if (wv == 1) {  // Schur calib columns and b: adH/adT * accE, * accEB
-    if (lane < 32) {
-      const int rr = lane >> 2, cc = lane & 3;
-      double s1 = 0.0, s2 = 0.0;
-      for (int l = 0; l < 8; l++) {
-        s1 += aH[rr * 8 + l] * Hpc[l * 4 + cc];
-        s2 += aT[rr * 8 + l] * Hpc[l * 4 + cc];
-      }
-      atomicAdd(&a.HSC[(iIdx + rr) * n + cc], s1);
-      atomicAdd(&a.HSC[(jIdx + rr) * n + cc], s2);
-    }
-    if (lane < 8) {
-      double s1 = 0.0, s2 = 0.0;
-      for (int l = 0; l < 8; l++) {
-        s1 += aH[lane * 8 + l] * v8[l];
-        s2 += aT[lane * 8 + l] * v8[l];
-      }
-      atomicAdd(&a.bSC[iIdx + lane], s1);
-      atomicAdd(&a.bSC[jIdx + lane], s2);
-    }
-  }
-  for (int kk = wv; kk < nF; kk += 4) {  // Schur rows (i, j, k)
-    if (cnt[1 + kk] == 0) continue;  // accD num == 0
-    const int kIdx = 4 + 8 * kk;
-    const double* D = E + 96 + kk * 64;
-    // X = aH D, Y = aT D once; X aH2^T, Y aT2^T, Y aH2^T, X aT2^T (the reference's four sandwiches)
-    left2(ahr, atr, D, tmp, tmp + 64, lane);
-    __builtin_amdgcn_wave_barrier();
-    const double o1 = right_t(tmp, aH2[kk], lane), o2 = right_t(tmp + 64, aT2[kk], lane);
-    const double o3 = right_t(tmp + 64, aH2[kk], lane), o4 = right_t(tmp, aT2[kk], lane);
-    __builtin_amdgcn_wave_barrier();
-    atomicAdd(&a.HSC[(iIdx + r) * n + iIdx + c], o1);
-    atomicAdd(&a.HSC[(jIdx + r) * n + kIdx + c], o2);
-    atomicAdd(&a.HSC[(jIdx + r) * n + iIdx + c], o3);
-    atomicAdd(&a.HSC[(iIdx + r) * n + kIdx + c], o4);
-  }
-  if (trace && tid == 0) trace[14] = wall_clock64();
 }
 
 // =====================================================================================================
@@ -1409,23 +1304,37 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
 #pragma unroll
     for (int u = 0; u < ST_NU; u++) stw[u] = gs[min(tid + u * SOLVE_NT, ST_WORDS - 1)];
   }
-  double ha[SOLVE_NU], hs[SOLVE_NU], nfv[NF_NU];
-  double bA_q = 0.0, bSC_q = 0.0, bM_q = 0.0;
+  double gs[SOLVE_NU], nfv[NF_NU];
+  double bS_q = 0.0, bM_q = 0.0;
   const double sysE0 = a.sysE[0], sysE1 = a.sysE[1], sysE2 = a.sysE[2];  // energy, sum |idepth|, #points
   if (solve) {
+    // the system slots' upper triangles (entries r <= c of the n x n layout) and b, summed in slot order; two
+    // slots per batch keep 2 x SOLVE_NU loads in flight
 #pragma unroll
-    for (int u = 0; u < SOLVE_NU; u++) {
-      const int idx = min(tid + u * nt, nn - 1);
-      ha[u] = a.HA[idx];
-      hs[u] = a.HSC[idx];
+    for (int u = 0; u < SOLVE_NU; u++) gs[u] = 0.0;
+    for (int s0 = 0; s0 < a.nslots; s0 += 2) {
+      double v[2][SOLVE_NU], vb[2];
+#pragma unroll
+      for (int k = 0; k < 2; k++) {
+        const double* sl = a.slot + (size_t)min(s0 + k, a.nslots - 1) * a.SL;
+#pragma unroll
+        for (int u = 0; u < SOLVE_NU; u++) {
+          const int ix = min(tid + u * nt, nn - 1), r = (int)__umulhi((unsigned)ix, inv_n), c = ix - r * n;
+          v[k][u] = r <= c ? sl[ix] : 0.0;
+        }
+        vb[k] = sl[nn + min(tid, n - 1)];
+      }
+#pragma unroll
+      for (int k = 0; k < 2; k++)
+        if (s0 + k < a.nslots) {
+#pragma unroll
+          for (int u = 0; u < SOLVE_NU; u++) gs[u] += v[k][u];
+          bS_q += vb[k];
+        }
     }
 #pragma unroll
     for (int u = 0; u < NF_NU; u++) nfv[u] = a.Nproj[min(tid + u * SOLVE_NT, 2 * n * HS_NNS - 1)];
-    if (tid < n) {
-      bA_q = a.bA[tid];
-      bSC_q = a.bSC[tid];
-      bM_q = a.bM[tid];
-    }
+    if (tid < n) bM_q = a.bM[tid];
   }
   {
     uint2* ls = reinterpret_cast<uint2*>(st_raw);
@@ -1450,11 +1359,13 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
 #pragma unroll
     for (int u = 0; u < SOLVE_NU; u++)
       if (tid + u * nt < nn) {
-        // raw HA -> B, raw HSC -> LT, both at the padded row stride n + 1 so the transposed reads of the
-        // symmetrization below are (nearly) bank-conflict free; LT is cleared for the LDLT afterwards
+        // the summed upper triangle -> B at the padded row stride n + 1, mirrored (the transposed stores are
+        // nearly bank-conflict free at that stride)
         const int ix = tid + u * nt, r = (int)__umulhi((unsigned)ix, inv_n), c = ix - r * n;
-        B[r * (n + 1) + c] = ha[u];
-        LT[r * (n + 1) + c] = hs[u];
+        if (r <= c) {
+          B[r * (n + 1) + c] = gs[u];
+          B[c * (n + 1) + r] = gs[u];
+        }
       }
     if (tid < n) {
       const int q = tid;
@@ -1468,34 +1379,26 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
         pr = f.prior[(q - 4) % 8];
         bl = f.prior[(q - 4) % 8] * f.delta_prior[(q - 4) % 8];
       }
-      px[q] = pr;  // HL diagonal (priors); staging only: these four arrays are reused below
+      px[q] = pr;  // HL diagonal (priors); staging only: these arrays are reused below
       xs[q] = bl;
-      yv[q] = bA_q;
-      Sv[q] = bSC_q;
+      yv[q] = bS_q;
     }
     __syncthreads();
     HS_TRACE(a, 7);
-    // HFinal = (HL + HM) + HA' ; diag *= (1+lambda) ; HFinal -= HSC' / (1+lambda)   (' = stitchDoubleMT
-    // post-processing: frame off-diagonal blocks symmetrized, calib rows copied from the calib columns)
-    const double sc = (double)(1.0f / (1 + lambda));
+    // HFinal = (HL + HM + HA) diag (1+lambda) - HSC / (1+lambda): the slots carry HA - sc HSC with the diagonal
+    // HA (1+lambda) - sc HSC (hs_k_reduce's stitch); the priors HL (diagonal) and the marginalization prior HM
+    // are added here
+    const double lam1 = 1 + lambda;
     double v[SOLVE_NU];
-    // HM (the marginalization prior) is usually absent: two instances of the loop, chosen by one uniform
-    // branch, so the common one carries no HM registers or loads
+    // HM is usually absent: two instances of the loop, chosen by one uniform branch, so the common one
+    // carries no HM loads
     auto assemble = [&](auto withHM) {
 #pragma unroll
       for (int u = 0; u < SOLVE_NU; u++) {
         const int ix = min(tid + u * nt, nn - 1), r = (int)__umulhi((unsigned)ix, inv_n), c = ix - r * n;
-        const int idx = r * (n + 1) + c, tdx = c * (n + 1) + r;
-        const int fr = r < 4 ? -1 : (r - 4) >> 3, fc = c < 4 ? -1 : (c - 4) >> 3;
-        const double a0 = B[idx], a1 = B[tdx], b0 = LT[idx], b1 = LT[tdx], hl0 = px[r];
+        const double g = B[r * (n + 1) + c];
         const double hm = decltype(withHM)::value ? a.HM[r * n + c] : 0.0;
-        const bool sym = (fr >= 0) & (fc >= 0) & (fr != fc), calrow = (r < 4) & (c >= 4);
-        const double ha_ = sym ? a0 + a1 : (calrow ? a1 : a0);
-        const double hsc = calrow ? b1 : b0;
-        const double hl = r == c ? hl0 : 0.0;
-        double hv = (hl + hm) + ha_;
-        hv = r == c ? hv * (1 + lambda) : hv;
-        v[u] = hv - hsc * sc;
+        v[u] = r == c ? g + (px[r] + hm) * lam1 : g + hm;
       }
     };
     if (a.HM) assemble(std::integral_constant<bool, true>{});
@@ -1505,8 +1408,8 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
       double hmd = 0.0;
       if (a.HM)
         for (int c = 0; c < n; c++) hmd += a.HM[q * n + c] * dl[c];
-      // ((bL + (bM + HM delta)) + bA) - bSC
-      bf[q] = ((xs[q] + (bM_q + hmd)) + yv[q]) - Sv[q];
+      // (bL + (bM + HM delta)) + (bA - bSC)
+      bf[q] = (xs[q] + (bM_q + hmd)) + yv[q];
     }
     // the diagonal of the assembled system (held in registers by its owners) is staged for the scaling
 #pragma unroll
@@ -1659,15 +1562,6 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
         for (int rr = 0; rr < 8; rr++) s2 += xF[4 + 8 * tt + rr] * adt[k][rr];
         a.xAd[o] = s1 + s2;
       }
-    }
-    // the consumed accumulation targets are zeroed for the next linearization (no barrier waits on these)
-    for (int idx = tid; idx < nn; idx += nt) {
-      a.HA[idx] = 0.0;
-      a.HSC[idx] = 0.0;
-    }
-    if (tid < n) {
-      a.bA[tid] = 0.0;
-      a.bSC[tid] = 0.0;
     }
     HS_TRACE(a, 5);
   }

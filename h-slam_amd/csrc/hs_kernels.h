@@ -25,6 +25,16 @@ struct HsDevState {
   int pad[3];
 };
 
+// Per-lane accumulator entries of the fused linearize kernel (hs_k_lin): lane (slot t, pattern k) of a wave
+// keeps, for the (host, t) pair of its block, 16 AccumulatorApprox entries (HS_E_TOP, decoded in hs_k_reduce's
+// stitch), HS_ND(exact) AccumulatorXX<8,8> accD entries (lane = (row, col) of every (t1, t2) block), 4 accE +
+// 1 accEB entries (lane (t, k): row k of accE[host, t]) and one accHcc / accbc entry (lanes 0..19).
+constexpr int HS_E_TOP = 16;
+constexpr int HS_ND_PROD = 28;   // (t1 <= t2) over the 7 non-host slots; D(t2, t1) = D(t1, t2)^T
+constexpr int HS_ND_EXACT = 49;  // every ordered (t1, t2): the single-thread reference's own sums
+__host__ __device__ constexpr int hs_ne(bool exact) { return HS_E_TOP + (exact ? HS_ND_EXACT : HS_ND_PROD) + 5 + 1; }
+__host__ __device__ constexpr int hs_nt(int n) { return n * (n + 1) / 2; }  // upper triangle of the n x n system
+
 struct HsLinArgs {
   const float4* img[HS_MAXF];  // level-0 texels per window frame
   const HsDevState* st;
@@ -32,7 +42,10 @@ struct HsLinArgs {
   int nF;
   int write_center;
   int fuse_step;               // apply resubstitute + point step of the previous solve first
+  int accumulate;              // 1: the per-lane accumulators and the block partials (0: linearize + applyRes only)
   int host_begin[HS_MAXF + 1]; // first point of each host (points are sorted by host)
+  int blk_begin[HS_MAXF + 1];  // first block of each host: block b of host h covers an equal share of its points
+  int W;                       // waves of a block that take points (1 = the single-thread reference's point order)
   // marginalization pass (hs_ba_marginalize_points): only points with marg[p] != 0 are linearized (after
   // resetOOB), their active residuals take fixLinearizationF, the SC prelude uses priorF * margPriorFac and no
   // prior shift; every other point reports no active residual.  nullptr = the normal pass.
@@ -44,11 +57,10 @@ struct HsLinArgs {
   const float* frameTH;        // [nF]
   const float* xAd;            // [nF*nF][8] index h*nF + t (fuse_step)
   // points
-  const int* pt_host;
-  const float* u;
-  const float* v;
   float* idepth;
   float* idepth_zero;
+  const float* u;
+  const float* v;
   const float* priorF;
   const float* color;          // [n][8]
   const float* weight;         // [n][8]
@@ -67,44 +79,30 @@ struct HsLinArgs {
   float* p_bdSumF;
   float* p_Hcd;                // [n][4]
   float* p_JpJdF;              // [n][8][8]
-  float* p_Jrec;               // [n][8][HS_JREC]
-  double* p_energy;            // [n]
   float* p_step;               // [n]
   float* newest_cand;          // [n] energy of the point's residual into the newest frame, -1 = none
+  // block partials: part[blk][ne][64] (fp32, waves summed in wave order), part_e[blk][4] (fp64 energy,
+  // sum |idepth|, #points)
+  float* part;
+  double* part_e;
   long long* trace;            // nullable: per-block wall-clock checkpoints [grid][16]
 };
 
-struct HsStitchArgs {
-  int nF, S;
-  const double* part;
-  const int* part_cnt;
-  const double* hccbc;
+// hs_k_reduce: (host, chunk) blocks sum the host's block partials in block order (fp64), the last chunk block
+// of a host (ticket) stitches the host into its slot; + one energy block and one setNewFrameEnergyTH block.
+struct HsRedArgs {
+  int nF, ne, exact, Q, nblk;
+  int blk_begin[HS_MAXF + 1];
+  const float* part;
+  const double* part_e;
+  double* hostsum;             // [nF][ne][64] (sc1 hand-off to the stitching block)
+  int* ticket;                 // [nF] zero between launches (the stitching block resets its counter)
   const double* adHost;        // [nF*nF][64]  index h + nF*t
   const double* adTarget;
-  double* HA;                  // [n*n] zeroed
-  double* bA;
-  double* HSC;
-  double* bSC;
-  long long* trace;
-};
-
-struct HsAccArgs {
-  int nF, S, nP;
-  int W;                       // waves of a block that accumulate (1: one wave, the reference's point order)
-  int blocked;                 // a (host, target, split) block can exceed 1000 updates: emulate shiftUp
-  const int* host_pt_begin;    // [nF+1]
-  const uint8_t* actmask;
-  const float* HdiF;
-  const float* bdSumF;
-  const float* Hcd;
-  const float* JpJdF;
-  const float* Jrec;
-  double* part;                // [nF*nF][S][HS_PART_N] (fp64 sums of the waves' fp32 partials)
-  int* part_cnt;               // [nF*nF][S][16]: top count, D counts (per k), E count
-  const double* p_energy;
-  const float* idepth;         // |idepth| sum for doStepFromBackup's sumNID
-  double* energy_out;          // [3]: energy, sum |idepth|, number of points
-  double* hccbc;               // [20] finished Hcc (16) + bc (4), fp64
+  double* slot;                // [nF][SL] per host: upper triangle of HA - sc HSC (diagonal: HA (1+lambda) - sc HSC) | bA - bSC
+  double* sep;                 // nullable: [nF][2][SL] per host: HA | bA, HSC | bSC (granular read-back)
+  double lambda1, sc;          // 1 + lambda, (double)(float)(1 / (1 + lambda))
+  double* sysE;                // [3] energy, sum |idepth|, number of points
   // setNewFrameEnergyTH over the candidates of all ranks (rank r at cand + r*stride, -1 = none)
   const float* cand;
   int nranks, stride;
@@ -113,12 +111,15 @@ struct HsAccArgs {
   float frameEnergyTHN, facMedian, constWeight, overallWeight;
   int skip_threshold;          // marginalization pass: setNewFrameEnergyTH is not part of it
   long long* trace;
-  // stitch fused into the accumulate launch: the last split block of a (host, target) pair to finish
-  // (ticket counter) stitches that pair; the Hcc block adds accHcc / accbc itself
-  HsStitchArgs stitch;
-  int* ticket;                 // [nF*nF] zero between launches (the stitching block resets its counter)
 };
 
+// multi-rank: the host slots + energies of this rank summed (slot order) into one vector [SL + 3] for RCCL
+struct HsCombArgs {
+  int nF, SL;
+  const double* slot;
+  const double* sysE;
+  double* out;
+};
 
 enum { HS_SOLVE = 1, HS_APPLY = 2 };
 
@@ -127,10 +128,9 @@ struct HsSolveArgs {
   int iteration;               // < 0: use st->iteration
   int nF;                      // window size (== st->nF)
   HsDevState* st;
-  double* HA;                  // HA | bA | HSC | bSC, consumed then zeroed (SOLVE)
-  double* bA;
-  double* HSC;
-  double* bSC;
+  const double* slot;          // nslots system slots (hs_k_reduce's per-host slots or one all-reduced rank
+  int nslots;                  // vector), stride SL = nt + n, summed in slot order
+  int SL;
   const double* HM;            // nullable: marginalization prior is zero
   const double* bM;
   const double* Nproj;         // [2][n][HS_NNS] nullspace factors N | Npi (P = (N Npi^T + Npi N^T) / 2)
@@ -162,8 +162,10 @@ struct HsResubArgs {
   float* step;
 };
 
-__global__ void hs_k_linearize(HsLinArgs a);
-__global__ void hs_k_accumulate(HsAccArgs a);
+__global__ void hs_k_lin(HsLinArgs a);        // production partitioning
+__global__ void hs_k_lin_exact(HsLinArgs a);  // HS_ACC_EXACT: one wave per host, the reference's sums
+__global__ void hs_k_reduce(HsRedArgs a);
+__global__ void hs_k_combine(HsCombArgs a);
 __global__ void hs_k_solve(HsSolveArgs a);
 __global__ void hs_k_resub(HsResubArgs a);
 __global__ void hs_k_apply_step(int n, const float* step, float* idepth, float* idepth_zero);

@@ -9,10 +9,11 @@
 //               color, weight                                                [n][8]
 //               res_of_slot  residual index per target frame slot (-1 none)  [n][8]
 //               res_order    target slots in the point's residual-list order [n][8]
-//   per point outputs of a linearization (slot layout, read by accumulate / resubstitute):
-//               actmask (bit t = residual into frame t is active), HdiF, bdSumF, Hcd[4],
-//               JpJdF [n][8 slots][8], Jrec [n][8 slots][36] (the residual's Jacobian digest),
-//               energy (double, the point's share of linearizeAll's sum), step
+//   per point outputs of a linearization (slot layout, read by the next iteration's fused point step and
+//               the granular resubstitute): actmask (bit t = residual into frame t is active), HdiF, bdSumF,
+//               Hcd[4], JpJdF [n][8 slots][8], step
+//   block partials of the fused linearize (hs_k_lin): [block][entry][64 lanes] fp32 accumulators + fp64
+//               energies; per-host sums [host][entry][64] fp64; per-host system slots (upper triangles)
 //   residuals : state / energy / new energy / energy-with-outlier / active, centre projection [m][3]
 //   precalc   : HsPrecalc [nF*nF] indexed host*nF + target (Frame::targetPrecalc)
 #pragma once
@@ -22,21 +23,6 @@
 #define HS_MAXF 8
 #define HS_MAXDIM (4 + 8 * HS_MAXF)
 #define HS_TOP_N 91    // 55 (10x10 upper) + 30 (10 x {a,b,r}) + 6 (3x3 upper)
-#define HS_JREC 36     // floats per residual Jacobian digest
-#define HS_PART_N 648  // per (host,target,split) partial: top 96 + D 512 + E 32 + EB 8
-
-// Jrec layout (per residual):
-//   [0..9]  x = [Jpdc0(4) Jpdxi0(6)]   [10..19] y = [Jpdc1 Jpdxi1]
-//   [20..22] JIdx2 00,01,11   [23..25] Jab2 00,01,11   [26..29] JabJIdx 00,01,10,11
-//   [30,31] JI_r   [32,33] Jab_r   [34] rr
-#define HS_JR_X 0
-#define HS_JR_Y 10
-#define HS_JR_JIDX2 20
-#define HS_JR_JAB2 23
-#define HS_JR_JABJIDX 26
-#define HS_JR_JIR 30
-#define HS_JR_JABR 32
-#define HS_JR_RR 34
 
 // FrameFramePrecalc restricted to what the linearize kernel reads
 // (Include/OptimizationClasses.h:55-86)

@@ -114,7 +114,13 @@ class BAWindow:
         return bool(cb.value)
 
     def optimize(self, iters=6, allow_break=False):
-        e = np.zeros(max(iters, 20) + 2)  # System::optimize raises the count to 15/20 for tiny windows
+        # System::optimize's overrides for tiny windows (Src/FullSystemOptimize.cpp:366-367), applied here so the
+        # energy buffer (max_iters + 1 entries, include/hs_ba.h) holds the whole trajectory
+        if self.nF < 3:
+            iters = 20
+        if self.nF < 4:
+            iters = 15
+        e = np.zeros(iters + 1)
         n = C.c_int()
         check(self.lib.hs_ba_optimize(self.h, iters, int(allow_break), ptr(e), C.byref(n)))
         return n.value, e[: n.value + 1]
