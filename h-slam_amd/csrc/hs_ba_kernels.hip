@@ -762,8 +762,14 @@ struct StitchLds {
   double Ys[HS_MAXF * HS_MAXF][64];
 };
 
+#define HS_TRACE_ROW(row, slot)                                        \
+  do {                                                                 \
+    if ((row) && threadIdx.x == 0) (row)[(slot)] = wall_clock64();    \
+  } while (0)
+
 template <bool kExact>
 __device__ void stitch_host(const HsRedArgs& a, int i, StitchLds& L) {
+  long long* trow = a.trace ? a.trace + (size_t)blockIdx.x * 16 : nullptr;
   constexpr int ND = kExact ? HS_ND_EXACT : HS_ND_PROD;
   constexpr int NE = hs_ne(kExact);
   constexpr int oE = (HS_E_TOP + ND) * 64;  // accE / accEB / Hcc entries
@@ -803,6 +809,7 @@ __device__ void stitch_host(const HsRedArgs& a, int i, StitchLds& L) {
     }
   }
   __syncthreads();
+  HS_TRACE_ROW(trow, 2);
   // ---- decode the top blocks: A88 = [xi a b] x [xi a b], A84 = [xi a b] x calib, a8r = [xi a b] x r
   for (int q = tid; q < nF * 104; q += 256) {
     const int t = q / 104, e = q % 104;
@@ -824,12 +831,18 @@ __device__ void stitch_host(const HsRedArgs& a, int i, StitchLds& L) {
     else a4r[tid - 16] = sacc;
   }
   __syncthreads();
-  // D(t1, t2)[l][c]: production stores t1 <= t2 only, D(t2, t1) = D(t1, t2)^T
-  auto Dv = [&](int t1, int t2, int l, int cc) -> double {
-    const int o1 = t1 - (t1 > i ? 1 : 0), o2 = t2 - (t2 > i ? 1 : 0);
-    if (kExact) return hsm[(HS_E_TOP + o1 * 7 + o2) * 64 + l * 8 + cc];
-    return o1 <= o2 ? hsm[(HS_E_TOP + dpair(o1, o2)) * 64 + l * 8 + cc] : hsm[(HS_E_TOP + dpair(o2, o1)) * 64 + cc * 8 + l];
+  HS_TRACE_ROW(trow, 3);
+  // D(t1, t2)[l][c] = hsm[Dbase(t1, t2) + l * ls + c * cs]: production stores t1 <= t2 only, D(t2, t1) = D(t1, t2)^T
+  struct DAt {
+    int base, ls, cs;
   };
+  auto Dat = [&](int t1, int t2) -> DAt {
+    const int o1 = t1 - (t1 > i ? 1 : 0), o2 = t2 - (t2 > i ? 1 : 0);
+    if (kExact) return DAt{(HS_E_TOP + o1 * 7 + o2) * 64, 8, 1};
+    return o1 <= o2 ? DAt{(HS_E_TOP + dpair(o1, o2)) * 64, 8, 1} : DAt{(HS_E_TOP + dpair(o2, o1)) * 64, 1, 8};
+  };
+  // fp64 multiply-adds (the stitch is compared by tolerance; contraction is off file-wide for the fp32 parity code)
+  auto fma = [](double x, double y, double z) { return __builtin_fma(x, y, z); };
   // ---- products: jobs [0, nF) Y(i, t2) (the heavy ones first), then XH / XT, then Y(f != i, t2)
   const int nJ = nF + 2 * nF + nF * nF;
   for (int j = wv; j < nJ; j += 4) {
@@ -839,10 +852,18 @@ __device__ void stitch_host(const HsRedArgs& a, int i, StitchLds& L) {
       if (t2 != i)
         for (int t1 = 0; t1 < nF; t1++) {
           if (t1 == i) continue;
+          const DAt d = Dat(t1, t2);
+          const double* dp = hsm + d.base + c * d.cs;
+          double hv[8], dv[8];
+#pragma unroll
+          for (int l = 0; l < 8; l++) {
+            hv[l] = aH[t1][r * 8 + l];
+            dv[l] = dp[l * d.ls];
+          }
 #pragma unroll
           for (int l = 0; l < 8; l += 2) {
-            y0 += aH[t1][r * 8 + l] * Dv(t1, t2, l, c);
-            y1 += aH[t1][r * 8 + l + 1] * Dv(t1, t2, l + 1, c);
+            y0 = fma(hv[l], dv[l], y0);
+            y1 = fma(hv[l + 1], dv[l + 1], y1);
           }
         }
       Ys[i * nF + t2][lane] = y0 + y1;
@@ -851,19 +872,23 @@ __device__ void stitch_host(const HsRedArgs& a, int i, StitchLds& L) {
       const double* L = ((j - nF) & 1) ? aT[t] : aH[t];
       double x = 0.0;
 #pragma unroll
-      for (int m = 0; m < 8; m++) x += L[r * 8 + m] * A88[t][m * 8 + c];
+      for (int m = 0; m < 8; m++) x = fma(L[r * 8 + m], A88[t][m * 8 + c], x);
       (((j - nF) & 1) ? XT[t] : XH[t])[lane] = x;
     } else {  // Y(f, t2) = adT[f] D(f, t2)
       const int q = j - 3 * nF, f = q / nF, t2 = q % nF;
       if (f == i) continue;
       double y = 0.0;
-      if (t2 != i)
+      if (t2 != i) {
+        const DAt d = Dat(f, t2);
+        const double* dp = hsm + d.base + c * d.cs;
 #pragma unroll
-        for (int l = 0; l < 8; l++) y += aT[f][r * 8 + l] * Dv(f, t2, l, c);
+        for (int l = 0; l < 8; l++) y = fma(aT[f][r * 8 + l], dp[l * d.ls], y);
+      }
       Ys[f * nF + t2][lane] = y;
     }
   }
   __syncthreads();
+  HS_TRACE_ROW(trow, 4);
   double* slot = a.slot + (size_t)i * SL;
   double* sepA = a.sep ? a.sep + (size_t)i * 2 * SL : nullptr;
   double* sepS = a.sep ? sepA + SL : nullptr;
@@ -886,10 +911,10 @@ __device__ void stitch_host(const HsRedArgs& a, int i, StitchLds& L) {
         if (t == i) continue;
 #pragma unroll
         for (int l = 0; l < 8; l += 2) {
-          s0 += Ys[i * nF + t][r * 8 + l] * aH[t][c * 8 + l];
-          s1 += Ys[i * nF + t][r * 8 + l + 1] * aH[t][c * 8 + l + 1];
-          h0 += XH[t][r * 8 + l] * aH[t][c * 8 + l];
-          h1 += XH[t][r * 8 + l + 1] * aH[t][c * 8 + l + 1];
+          s0 = fma(Ys[i * nF + t][r * 8 + l], aH[t][c * 8 + l], s0);
+          s1 = fma(Ys[i * nF + t][r * 8 + l + 1], aH[t][c * 8 + l + 1], s1);
+          h0 = fma(XH[t][r * 8 + l], aH[t][c * 8 + l], h0);
+          h1 = fma(XH[t][r * 8 + l + 1], aH[t][c * 8 + l + 1], h1);
         }
       }
       hs = s0 + s1;
@@ -897,22 +922,23 @@ __device__ void stitch_host(const HsRedArgs& a, int i, StitchLds& L) {
     } else {
       // Schur: Z(i, g) = Y(i, g) adT[g]^T, Z(f, i) = Z(i, f)^T, Z(f, g) = Y(f, g) adT[g]^T
       // top: (t, t) XT[t] adT[t]^T, (i, t) XH[t] adT[t]^T, (t, i) = (i, t)^T
+      // operand rows: (yrow, arow) for hs, (xrow, arow) for ha, all uniform choices of the block
+      const bool tr = g == i;  // the transposed form Z(f, i) = Z(i, f)^T
+      const int ro = tr ? c : r, co = tr ? r : c;
+      const double* yrow = (f == i) ? Ys[i * nF + g] : (g == i ? Ys[i * nF + f] : Ys[f * nF + g]);
+      const double* arow = (f == i) ? aT[g] : (g == i ? aT[f] : aT[g]);
+      const double* xrow = (f == i) ? XH[g] : (g == i ? XH[f] : XT[f]);
+      const bool wantA = f == i || g == i || f == g;
 #pragma unroll
       for (int l = 0; l < 8; l++) {
-        if (f == i) {
-          hs += Ys[i * nF + g][r * 8 + l] * aT[g][c * 8 + l];
-          ha += XH[g][r * 8 + l] * aT[g][c * 8 + l];
-        } else if (g == i) {
-          hs += Ys[i * nF + f][c * 8 + l] * aT[f][r * 8 + l];
-          ha += XH[f][c * 8 + l] * aT[f][r * 8 + l];
-        } else {
-          hs += Ys[f * nF + g][r * 8 + l] * aT[g][c * 8 + l];
-          if (f == g) ha += XT[f][r * 8 + l] * aT[f][c * 8 + l];
-        }
+        hs = fma(yrow[ro * 8 + l], arow[co * 8 + l], hs);
+        ha = fma(xrow[ro * 8 + l], arow[co * 8 + l], ha);
       }
+      if (!wantA) ha = 0.0;
     }
     if (f < g || r <= c) put(4 + 8 * f + r, 4 + 8 * g + c, ha, hs, f == g && r == c);
   }
+  HS_TRACE_ROW(trow, 5);
   // ---- calib x frame (stored in the calib rows): H(4 + 8f + rr, cc), thread = (f, rr, cc)
   if (tid < nF * 32) {
     const int f = tid >> 5, rr = (tid >> 2) & 7, cc = tid & 3;
@@ -1364,18 +1390,17 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
   const double sysE0 = a.sysE[0], sysE1 = a.sysE[1], sysE2 = a.sysE[2];  // energy, sum |idepth|, #points
   if (solve) {
     double v[HS_MAXF][NUQ];
+    // unconditional loads at clamped addresses (a predicated load would split the batch into round trips)
 #pragma unroll
     for (int k = 0; k < HS_MAXF; k++)
 #pragma unroll
-      for (int u = 0; u < NUQ; u++)
-        v[k][u] = (k < a.nslots && qaddr[u] >= 0) ? a.slot[(size_t)k * a.SL + qaddr[u]] : 0.0;
+      for (int u = 0; u < NUQ; u++) v[k][u] = a.slot[(size_t)min(k, a.nslots - 1) * a.SL + max(qaddr[u], 0)];
 #pragma unroll
     for (int u = 0; u < NUQ; u++) {
       double sacc = 0.0;
 #pragma unroll
-      for (int k = 0; k < HS_MAXF; k++)
-        if (k < a.nslots) sacc += v[k][u];
-      gs[u] = sacc;
+      for (int k = 0; k < HS_MAXF; k++) sacc += k < a.nslots ? v[k][u] : 0.0;
+      gs[u] = qaddr[u] >= 0 ? sacc : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < NF_NU; u++) nfv[u] = a.Nproj[min(tid + u * SOLVE_NT, 2 * n * HS_NNS - 1)];
