@@ -2,7 +2,8 @@
 // device-resident GN loop of System::optimize.  The window state (frames, calib, precalc,
 // systems, steps) lives in HBM between iterations; one GN iteration is the launch sequence
 //   hs_k_solve(SOLVE|APPLY) -> hs_k_lin (fused point step, linearize, per-lane accumulation, block partials)
-//   -> [all-gather] -> hs_k_reduce (per-host fixed-order sums + per-host stitch) -> [combine + all-reduce]
+//   -> [all-gather] -> hs_k_reduce (per-host fixed-order sums) -> hs_k_stitch (one block per output block of
+//   the system, fixed-order sums) -> [all-reduce of the system vector]
 // with no host synchronisation and no order-dependent atomics (bit-reproducible).  The host only prepares the window (adjoints, nullspace
 // projector, initial precalc — the reference's once-per-window Eigen/Sophus work) and reads
 // results back.  Compiled by hipcc as HIP together with hs_ba_kernels.hip; no torch, no Eigen.
@@ -107,10 +108,9 @@ struct hs_ctx {
   float* d_part = nullptr;       // [nblk][ne][64] block partials of hs_k_lin
   double* d_part_e = nullptr;    // [nblk][4] block energies
   double* d_hostsum = nullptr;   // [nF][ne][64] per-host sums (hs_k_reduce)
-  double* d_slot = nullptr;      // [nF][SL] per-host systems: upper triangle of HA - sc HSC | bA - bSC
-  double* d_sep = nullptr;       // [nF][2][SL] per-host HA | bA, HSC | bSC (granular read-back)
-  double* d_sysE = nullptr;      // [3] energy, sum |idepth|, #points of the last linearization
-  double* d_rank = nullptr;      // [SL + 3] multi-rank: this rank's summed slots + energies, all-reduced
+  double* d_sys = nullptr;       // [SL + 3] system vector (upper triangle of HA - sc HSC | bA - bSC) + energy,
+                                 // sum |idepth|, #points; all-reduced over the ranks
+  double* d_sep = nullptr;       // [2][SL] HA | bA, HSC | bSC (granular read-back)
   double *d_adHost = nullptr, *d_adTarget = nullptr;
   float *d_adHostF = nullptr, *d_adTargetF = nullptr;
   double *d_HM = nullptr, *d_bM = nullptr, *d_Nproj = nullptr;
@@ -125,8 +125,7 @@ struct hs_ctx {
   float cDelta[4] = {0, 0, 0, 0};
   // kernel tracing (env HS_KTRACE=1): per-block wall-clock checkpoints of the last iteration
   bool tracing = false;
-  long long *d_tr_lin = nullptr, *d_tr_acc = nullptr, *d_tr_solve = nullptr;
-  int* d_ticket = nullptr;  // [nF] stitch hand-off counters of hs_k_reduce
+  long long *d_tr_lin = nullptr, *d_tr_acc = nullptr, *d_tr_solve = nullptr, *d_tr_st = nullptr;
 
   // RCCL
   ncclComm_t comm = nullptr;
@@ -137,8 +136,7 @@ struct hs_ctx {
 
   int dim() const { return 4 + 8 * nF; }
   int SL() const { return dim() * dim() + dim(); }  // slot: n x n (upper triangle used) + b
-  double* sysE() const { return d_comm_active() ? d_rank + SL() : d_sysE; }
-  bool d_comm_active() const { return comm != nullptr; }
+  double* sysE() const { return d_sys + SL(); }
 };
 
 static void free_window(hs_ctx* c) {
@@ -150,9 +148,9 @@ static void free_window(hs_ctx* c) {
                   c->d_priorF, c->d_color, c->d_weight, c->d_res_of_slot, c->d_pt_host, c->d_host_pt_begin,
                   c->d_res_order, c->d_r_state, c->d_r_active, c->d_r_energy, c->d_r_newEnergy, c->d_r_ewo,
                   c->d_r_center, c->d_p_actmask, c->d_p_HdiF, c->d_p_bdSumF, c->d_p_Hcd, c->d_p_JpJdF,
-                  c->d_p_step, c->d_part, c->d_part_e, c->d_hostsum, c->d_slot, c->d_sep, c->d_sysE, c->d_rank,
+                  c->d_p_step, c->d_part, c->d_part_e, c->d_hostsum, c->d_sys, c->d_sep,
                   c->d_adHost, c->d_adTarget, c->d_adHostF, c->d_adTargetF, c->d_HM, c->d_bM, c->d_Nproj, c->d_xAd,
-                  c->d_x, c->d_elog, c->d_cand, c->d_tr_lin, c->d_tr_acc, c->d_tr_solve, c->d_ticket,
+                  c->d_x, c->d_elog, c->d_cand, c->d_tr_lin, c->d_tr_acc, c->d_tr_solve, c->d_tr_st,
                   c->d_marg, c->d_adHTdelta};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -165,13 +163,11 @@ static void free_window(hs_ctx* c) {
   c->d_r_energy = c->d_r_newEnergy = c->d_r_ewo = c->d_r_center = nullptr;
   c->d_p_actmask = nullptr;
   c->d_p_HdiF = c->d_p_bdSumF = c->d_p_Hcd = c->d_p_JpJdF = c->d_p_step = nullptr;
-  c->d_part = nullptr; c->d_part_e = nullptr; c->d_hostsum = nullptr; c->d_slot = nullptr; c->d_sep = nullptr;
-  c->d_sysE = nullptr; c->d_rank = nullptr;
+  c->d_part = nullptr; c->d_part_e = nullptr; c->d_hostsum = nullptr; c->d_sys = nullptr; c->d_sep = nullptr;
   c->d_adHost = c->d_adTarget = nullptr; c->d_adHostF = c->d_adTargetF = nullptr;
   c->d_HM = c->d_bM = c->d_Nproj = nullptr;
   c->d_xAd = nullptr; c->d_x = nullptr; c->d_elog = nullptr; c->d_cand = nullptr;
-  c->d_tr_lin = c->d_tr_acc = c->d_tr_solve = nullptr;
-  c->d_ticket = nullptr;
+  c->d_tr_lin = c->d_tr_acc = c->d_tr_solve = c->d_tr_st = nullptr;
   c->d_marg = nullptr;
   c->d_adHTdelta = nullptr;
   c->nF = c->nP = c->nR = 0;
@@ -263,38 +259,43 @@ static int launch_linearize(hs_ctx* c, int fuse, bool marg = false, bool accumul
   return HS_OK;
 }
 
-// all-gather of newest-frame candidates, per-host sums + stitch (+ energy, threshold), combine + all-reduce
-static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = false) {
-  if (c->comm)
+// all-gather of newest-frame candidates, per-host sums (+ energy, threshold), stitch, all-reduce of the system
+// readback = true: only the separate HA / HSC of the last linearization (d_sep) are re-formed from its host sums;
+// no collective, the system vector and the energies are left as they are
+static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = false, bool readback = false) {
+  if (c->comm && !readback)
     HS_NCCL(ncclAllGather(c->d_cand + (size_t)c->rank * c->cand_stride, c->d_cand, c->cand_stride, ncclFloat,
                           c->comm, c->stream));
   HsRedArgs a;
   std::memset(&a, 0, sizeof(a));
-  a.nF = c->nF; a.ne = c->ne; a.exact = c->exact ? 1 : 0; a.Q = c->Q; a.nblk = c->nblk;
+  a.nF = c->nF; a.ne = c->ne; a.Q = c->Q; a.nblk = c->nblk;
   for (int i = 0; i <= c->nF; i++) a.blk_begin[i] = c->blk_begin[i];
-  a.part = c->d_part; a.part_e = c->d_part_e; a.hostsum = c->d_hostsum; a.ticket = c->d_ticket;
-  a.adHost = c->d_adHost; a.adTarget = c->d_adTarget;
-  a.slot = c->d_slot;
-  a.sep = sep ? c->d_sep : nullptr;
-  a.lambda1 = 1 + 1e-5;         // SOLVER_FIX_LAMBDA (Src/EnergyFunctional.cpp:707-708)
-  a.sc = 1.0f / (1 + 1e-5);     // H -= H_sc * (1.0f / (1 + lambda)) (:763)
-  a.sysE = c->d_sysE;
+  a.part = c->d_part; a.part_e = c->d_part_e; a.hostsum = c->d_hostsum;
+  a.sysE = c->sysE();
   a.cand = c->d_cand; a.nranks = c->nranks; a.stride = c->cand_stride;
   a.frameTH = c->d_frameTH; a.newest = c->nF - 1;
   a.frameEnergyTHN = c->P.frameEnergyTHN; a.facMedian = c->P.frameEnergyTHFacMedian;
   a.constWeight = c->P.frameEnergyTHConstWeight; a.overallWeight = c->P.overallEnergyTHWeight;
   a.skip_threshold = skip_threshold ? 1 : 0;
   a.trace = c->d_tr_acc;
-  hipLaunchKernelGGL(hs_k_reduce, dim3(c->nF * c->Q + 2), dim3(256), 0, c->stream, a);
+  if (!readback) {
+    hipLaunchKernelGGL(hs_k_reduce, dim3(c->nF * c->Q + 2), dim3(256), 0, c->stream, a);
+    HS_HIP(hipGetLastError());
+  }
+  HsStitchArgs st;
+  std::memset(&st, 0, sizeof(st));
+  st.nF = c->nF; st.exact = c->exact ? 1 : 0; st.ne = c->ne;
+  st.hostsum = c->d_hostsum; st.adHost = c->d_adHost; st.adTarget = c->d_adTarget;
+  st.out = readback ? nullptr : c->d_sys;
+  st.sep = sep ? c->d_sep : nullptr;
+  st.lambda1 = 1 + 1e-5;       // SOLVER_FIX_LAMBDA (Src/EnergyFunctional.cpp:707-708)
+  st.sc = 1.0f / (1 + 1e-5);   // H -= H_sc * (1.0f / (1 + lambda)) (:763)
+  st.trace = c->d_tr_st;
+  hipLaunchKernelGGL(hs_k_stitch, dim3(c->nF * (c->nF + 1) / 2 + c->nF + 1), dim3(256), 0, c->stream, st);
   HS_HIP(hipGetLastError());
   if (sep) c->sepValid = true;
-  if (c->comm) {
-    HsCombArgs cb;
-    cb.nF = c->nF; cb.SL = c->SL(); cb.slot = c->d_slot; cb.sysE = c->d_sysE; cb.out = c->d_rank;
-    hipLaunchKernelGGL(hs_k_combine, dim3((c->SL() + 3 + 255) / 256), dim3(256), 0, c->stream, cb);
-    HS_HIP(hipGetLastError());
-    HS_NCCL(ncclAllReduce(c->d_rank, c->d_rank, c->SL() + 3, ncclDouble, ncclSum, c->comm, c->stream));
-  }
+  if (c->comm && !readback)
+    HS_NCCL(ncclAllReduce(c->d_sys, c->d_sys, c->SL() + 3, ncclDouble, ncclSum, c->comm, c->stream));
   return HS_OK;
 }
 
@@ -305,9 +306,7 @@ static int launch_solve(hs_ctx* c, int flags, int iteration, bool log) {
   a.iteration = iteration;
   a.nF = c->nF;
   a.st = c->d_state;
-  a.slot = c->comm ? c->d_rank : c->d_slot;
-  a.nslots = c->comm ? 1 : c->nF;
-  a.SL = c->SL();
+  a.sys = c->d_sys;
   a.HM = c->hm_zero ? nullptr : c->d_HM;
   a.bM = c->d_bM; a.Nproj = c->d_Nproj;
   a.adHostF = c->d_adHostF; a.adTargetF = c->d_adTargetF;
@@ -392,6 +391,7 @@ static int dump_traces(hs_ctx* c) {
   }
   HS_TRY(dump_one("linearize", c->d_tr_lin, c->nblk, tick_us, c->stream));
   HS_TRY(dump_one("reduce", c->d_tr_acc, c->nF * c->Q + 2, tick_us, c->stream));
+  HS_TRY(dump_one("stitch", c->d_tr_st, c->nF * (c->nF + 1) / 2 + c->nF + 1, tick_us, c->stream));
   return HS_OK;
 }
 
@@ -702,11 +702,8 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
   HS_TRY(dalloc(&c->d_part, (size_t)std::max(c->nblk, 1) * c->ne * 64));
   HS_TRY(dalloc(&c->d_part_e, (size_t)std::max(c->nblk, 1) * 4));
   HS_TRY(dalloc(&c->d_hostsum, (size_t)nF * c->ne * 64));
-  HS_TRY(dalloc(&c->d_slot, (size_t)nF * c->SL()));  // zeroed: the lower triangles are never written
-  HS_TRY(dalloc(&c->d_sep, (size_t)nF * 2 * c->SL()));
-  HS_TRY(dalloc(&c->d_sysE, 4));
-  if (c->comm) HS_TRY(dalloc(&c->d_rank, (size_t)c->SL() + 3));
-  HS_TRY(dalloc(&c->d_ticket, (size_t)nF));  // zeroed; each stitching block resets its own counter
+  HS_TRY(dalloc(&c->d_sys, (size_t)c->SL() + 3));  // zeroed: the lower triangle is never written
+  HS_TRY(dalloc(&c->d_sep, (size_t)2 * c->SL()));
   HS_TRY(dalloc(&c->d_adHost, nF * nF * 64)); HS_TRY(dalloc(&c->d_adTarget, nF * nF * 64));
   HS_TRY(dalloc(&c->d_adHostF, nF * nF * 64)); HS_TRY(dalloc(&c->d_adTargetF, nF * nF * 64));
   HS_TRY(dalloc(&c->d_HM, (size_t)n * n)); HS_TRY(dalloc(&c->d_bM, n)); HS_TRY(dalloc(&c->d_Nproj, (size_t)2 * n * HS_NNS));
@@ -718,6 +715,7 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
   if (c->tracing) {
     HS_TRY(dalloc(&c->d_tr_lin, (size_t)std::max(c->nblk, 1) * 16));
     HS_TRY(dalloc(&c->d_tr_acc, (size_t)(nF * c->Q + 2) * 16));
+    HS_TRY(dalloc(&c->d_tr_st, (size_t)(nF * (nF + 1) / 2 + nF + 1) * 16));
     HS_TRY(dalloc(&c->d_tr_solve, 32));
   }
 
@@ -872,25 +870,20 @@ int hs_ba_get_system(hs_ctx* c, int which, double* H, double* b) {
         bb[j] += S.frames[h].prior[i] * S.frames[h].delta_prior[i];
       }
   } else {
-    // the per-host HA | bA (which 0) or HSC | bSC (which 2) of the last linearization, summed over the hosts in
-    // host order and mirrored (the stitch writes the upper triangles: stitchDoubleMT's symmetrization and calib-row
-    // copy).  If the last reduce ran without the separate output (the GN loop), it is re-run on the block
-    // partials of that linearization (deterministic: the same sums).
-    if (!c->sepValid) HS_TRY(launch_reduce(c, true, true));
+    // HA | bA (which 0) or HSC | bSC (which 2) of the last linearization, mirrored (the stitch writes the upper
+    // triangles: stitchDoubleMT's symmetrization and calib-row copy); this rank's share on a multi-rank window.
+    // If the last stitch ran without the separate output (the GN loop), it is re-run on that linearization's
+    // host sums (deterministic: the same sums).
+    if (!c->sepValid) HS_TRY(launch_reduce(c, true, true, true));
     const int SL = c->SL();
-    std::vector<double> sep((size_t)nF * 2 * SL);
+    std::vector<double> sep((size_t)2 * SL);
     HS_HIP(hipMemcpyAsync(sep.data(), c->d_sep, sizeof(double) * sep.size(), hipMemcpyDeviceToHost, c->stream));
     HS_HIP(hipStreamSynchronize(c->stream));
-    const int part = which == 0 ? 0 : 1;
-    for (int h = 0; h < nF; h++) {
-      const double* src = sep.data() + ((size_t)h * 2 + part) * SL;
-      for (int r = 0; r < n; r++) {
-        for (int q = r; q < n; q++) HH[(size_t)r * n + q] += src[(size_t)r * n + q];
-        bb[r] += src[(size_t)n * n + r];
-      }
+    const double* src = sep.data() + (which == 0 ? 0 : SL);
+    for (int r = 0; r < n; r++) {
+      for (int q = r; q < n; q++) HH[(size_t)r * n + q] = HH[(size_t)q * n + r] = src[(size_t)r * n + q];
+      bb[r] = src[(size_t)n * n + r];
     }
-    for (int r = 0; r < n; r++)
-      for (int q = 0; q < r; q++) HH[(size_t)r * n + q] = HH[(size_t)q * n + r];
   }
   if (H) std::memcpy(H, HH.data(), sizeof(double) * n * n);
   if (b) std::memcpy(b, bb.data(), sizeof(double) * n);

@@ -718,16 +718,10 @@ __device__ void red_energy_th_block(const HsRedArgs& a) {
   }
 }
 
-// agent-scope relaxed load = global_load ... sc1 (bypasses this CU's L1; the L2 line of a write-through
-// sc1 store is dropped, so the load is served from memory side)
-template <typename T>
-__device__ __forceinline__ T ld_sc1(const T* p) {
-  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
-// the (R, C) entry (R <= C) of host-sum octet t's 13x13 AccumulatorApprox block [calib 4 | xi 6 | a | b | r]
-// from the owner lane of the layout in acc_point
-__device__ __forceinline__ double top_entry(const double* hsm, int t, int R, int C) {
+// the (R, C) entry (R <= C) of one (host, target) pair's 13x13 AccumulatorApprox block [calib 4 | xi 6 | a | b | r]
+// from its octet of the host sums, oct[e * 8 + k] = entry e of lane k (the owner layout of acc_point)
+__device__ __forceinline__ double top_oct(const double* oct, int R, int C) {
   int e, k;
   if (C < 8) { e = R; k = C; }                                     // Data (R, C <= 7): lane C, T[R]
   else if (C < 10) {
@@ -741,263 +735,41 @@ __device__ __forceinline__ double top_entry(const double* hsm, int t, int R, int
     e = 15;
     k = R == 10 ? C - 10 : (R == 11 ? 2 + C - 10 : 5);
   }
-  return hsm[e * 64 + t * 8 + k];
+  return oct[e * 8 + k];
 }
 
-// Stitch of host i (stitchDoubleInternal, Src/AccumulatedTopHessian.cpp:218-280 and
-// Src/AccumulatedSCHessian.cpp:54-133, in fp64) by one 256-thread block, from the host's summed accumulators.
-// Top: per target t the reference's sandwiches adH A adH^T -> (i,i), adT A adT^T -> (t,t), adH A adT^T -> (i,t),
-// adH / adT A84 -> calib columns, adH / adT a8r -> b.  Schur: the host's sum over (t1, t2) of the four sandwiches
-// adX[i,t1] D(t1,t2) adY[i,t2]^T is A D A^T with A(f, t) = [f = i] adH[i,t] + [f = t] adT[i,t] (8nF x 8nF), formed
-// as Y = A D (Y(i, t2) = sum_t1 adH[t1] D(t1,t2), Y(f, t2) = adT[f] D(f, t2)) then Z = Y A^T, in a fixed order.
-// Every output entry is written once (no atomics): the slot holds the upper triangle of HA - sc HSC (diagonal
-// HA (1+lambda) - sc HSC, the solve adds the priors' share) and bA - bSC; `sep` (granular read-back) HA | bA and
-// HSC | bSC separately.  Products are one wave per 8x8 block, lane (r, c), with independent partial sums so no
-// dependent FMA chain is longer than 16.
-struct StitchLds {
-  double hsm[hs_ne(true) * 64];
-  double aH[HS_MAXF][64], aT[HS_MAXF][64];
-  double A88[HS_MAXF][64], A84[HS_MAXF][32], a8r[HS_MAXF][8], A44[16], a4r[4];
-  double XH[HS_MAXF][64], XT[HS_MAXF][64];  // adH A88, adT A88
-  double Ys[HS_MAXF * HS_MAXF][64];
-};
-
-#define HS_TRACE_ROW(row, slot)                                        \
-  do {                                                                 \
-    if ((row) && threadIdx.x == 0) (row)[(slot)] = wall_clock64();    \
-  } while (0)
-
-template <bool kExact>
-__device__ void stitch_host(const HsRedArgs& a, int i, StitchLds& L) {
-  long long* trow = a.trace ? a.trace + (size_t)blockIdx.x * 16 : nullptr;
-  constexpr int ND = kExact ? HS_ND_EXACT : HS_ND_PROD;
-  constexpr int NE = hs_ne(kExact);
-  constexpr int oE = (HS_E_TOP + ND) * 64;  // accE / accEB / Hcc entries
-  const int nF = a.nF, n = 4 + 8 * nF, nn = n * n, SL = nn + n;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+// 8x8 block products by one wave, lane (r, c): out = L M (L row r, M column c) / out = L M^T
+__device__ __forceinline__ double mm8(const double* L, const double* M, int r, int c) {
+  double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+  for (int l = 0; l < 8; l += 2) {
+    s0 = __builtin_fma(L[r * 8 + l], M[l * 8 + c], s0);
+    s1 = __builtin_fma(L[r * 8 + l + 1], M[(l + 1) * 8 + c], s1);
+  }
+  return s0 + s1;
+}
+__device__ __forceinline__ double mm8t(const double* L, const double* M, int r, int c) {
+  double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+  for (int l = 0; l < 8; l += 2) {
+    s0 = __builtin_fma(L[r * 8 + l], M[c * 8 + l], s0);
+    s1 = __builtin_fma(L[r * 8 + l + 1], M[c * 8 + l + 1], s1);
+  }
+  return s0 + s1;
+}
+// L M R^T by one wave through the wave's LDS scratch (64 doubles)
+__device__ __forceinline__ double sandwich8(const double* L, const double* M, const double* R, double* scr, int lane) {
   const int r = lane >> 3, c = lane & 7;
-  double* hsm = L.hsm;
-  auto& aH = L.aH;
-  auto& aT = L.aT;
-  auto& A88 = L.A88;
-  auto& A84 = L.A84;
-  auto& a8r = L.a8r;
-  auto& A44 = L.A44;
-  auto& a4r = L.a4r;
-  auto& XH = L.XH;
-  auto& XT = L.XT;
-  auto& Ys = L.Ys;
-  {  // every load of the phase in flight together
-    const double* src = a.hostsum + (size_t)i * NE * 64;
-    constexpr int NU = (NE * 64 + 255) / 256;
-    double v[NU];
-#pragma unroll
-    for (int u = 0; u < NU; u++) v[u] = ld_sc1(&src[min(tid + 256 * u, NE * 64 - 1)]);
-    double ad[4];
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const int q = tid + 256 * u, kk = min(q >> 7, nF - 1), w = q & 127;
-      ad[u] = (w < 64 ? a.adHost : a.adTarget)[(i + nF * kk) * 64 + (w & 63)];
-    }
-#pragma unroll
-    for (int u = 0; u < NU; u++)
-      if (tid + 256 * u < NE * 64) hsm[tid + 256 * u] = v[u];
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const int q = tid + 256 * u, kk = q >> 7, w = q & 127;
-      if (kk < nF) (w < 64 ? aH[kk] : aT[kk])[w & 63] = ad[u];
-    }
-  }
-  __syncthreads();
-  HS_TRACE_ROW(trow, 2);
-  // ---- decode the top blocks: A88 = [xi a b] x [xi a b], A84 = [xi a b] x calib, a8r = [xi a b] x r
-  for (int q = tid; q < nF * 104; q += 256) {
-    const int t = q / 104, e = q % 104;
-    if (e < 64) {
-      const int R = 4 + (e >> 3), C = 4 + (e & 7);
-      A88[t][e] = top_entry(hsm, t, min(R, C), max(R, C));
-    } else if (e < 96) {
-      const int rr = (e - 64) >> 2, cc = (e - 64) & 3;
-      A84[t][e - 64] = top_entry(hsm, t, cc, 4 + rr);
-    } else {
-      a8r[t][e - 96] = top_entry(hsm, t, 4 + (e - 96), 12);
-    }
-  }
-  if (tid < 20) {  // A44 / a4r: summed over the targets in target order
-    double sacc = 0.0;
-    for (int t = 0; t < nF; t++)
-      sacc += tid < 16 ? top_entry(hsm, t, min(tid >> 2, tid & 3), max(tid >> 2, tid & 3)) : top_entry(hsm, t, tid - 16, 12);
-    if (tid < 16) A44[tid] = sacc;
-    else a4r[tid - 16] = sacc;
-  }
-  __syncthreads();
-  HS_TRACE_ROW(trow, 3);
-  // D(t1, t2)[l][c] = hsm[Dbase(t1, t2) + l * ls + c * cs]: production stores t1 <= t2 only, D(t2, t1) = D(t1, t2)^T
-  struct DAt {
-    int base, ls, cs;
-  };
-  auto Dat = [&](int t1, int t2) -> DAt {
-    const int o1 = t1 - (t1 > i ? 1 : 0), o2 = t2 - (t2 > i ? 1 : 0);
-    if (kExact) return DAt{(HS_E_TOP + o1 * 7 + o2) * 64, 8, 1};
-    return o1 <= o2 ? DAt{(HS_E_TOP + dpair(o1, o2)) * 64, 8, 1} : DAt{(HS_E_TOP + dpair(o2, o1)) * 64, 1, 8};
-  };
-  // fp64 multiply-adds (the stitch is compared by tolerance; contraction is off file-wide for the fp32 parity code)
-  auto fma = [](double x, double y, double z) { return __builtin_fma(x, y, z); };
-  // ---- products: jobs [0, nF) Y(i, t2) (the heavy ones first), then XH / XT, then Y(f != i, t2)
-  const int nJ = nF + 2 * nF + nF * nF;
-  for (int j = wv; j < nJ; j += 4) {
-    if (j < nF) {  // Y(i, t2) = sum_t1 adH[t1] D(t1, t2), two interleaved partial sums
-      const int t2 = j;
-      double y0 = 0.0, y1 = 0.0;
-      if (t2 != i)
-        for (int t1 = 0; t1 < nF; t1++) {
-          if (t1 == i) continue;
-          const DAt d = Dat(t1, t2);
-          const double* dp = hsm + d.base + c * d.cs;
-          double hv[8], dv[8];
-#pragma unroll
-          for (int l = 0; l < 8; l++) {
-            hv[l] = aH[t1][r * 8 + l];
-            dv[l] = dp[l * d.ls];
-          }
-#pragma unroll
-          for (int l = 0; l < 8; l += 2) {
-            y0 = fma(hv[l], dv[l], y0);
-            y1 = fma(hv[l + 1], dv[l + 1], y1);
-          }
-        }
-      Ys[i * nF + t2][lane] = y0 + y1;
-    } else if (j < 3 * nF) {  // XH[t] = adH A88, XT[t] = adT A88
-      const int t = (j - nF) >> 1;
-      const double* L = ((j - nF) & 1) ? aT[t] : aH[t];
-      double x = 0.0;
-#pragma unroll
-      for (int m = 0; m < 8; m++) x = fma(L[r * 8 + m], A88[t][m * 8 + c], x);
-      (((j - nF) & 1) ? XT[t] : XH[t])[lane] = x;
-    } else {  // Y(f, t2) = adT[f] D(f, t2)
-      const int q = j - 3 * nF, f = q / nF, t2 = q % nF;
-      if (f == i) continue;
-      double y = 0.0;
-      if (t2 != i) {
-        const DAt d = Dat(f, t2);
-        const double* dp = hsm + d.base + c * d.cs;
-#pragma unroll
-        for (int l = 0; l < 8; l++) y = fma(aT[f][r * 8 + l], dp[l * d.ls], y);
-      }
-      Ys[f * nF + t2][lane] = y;
-    }
-  }
-  __syncthreads();
-  HS_TRACE_ROW(trow, 4);
-  double* slot = a.slot + (size_t)i * SL;
-  double* sepA = a.sep ? a.sep + (size_t)i * 2 * SL : nullptr;
-  double* sepS = a.sep ? sepA + SL : nullptr;
-  auto put = [&](int R, int C, double ha, double hs, bool diag) {
-    slot[R * n + C] = diag ? ha * a.lambda1 - hs * a.sc : ha - hs * a.sc;
-    if (sepA) {
-      sepA[R * n + C] = ha;
-      sepS[R * n + C] = hs;
-    }
-  };
-  // ---- frame blocks (f <= g), one wave per block, lane (r, c)
-  for (int fb = wv; fb < nF * nF; fb += 4) {
-    const int f = fb / nF, g = fb % nF;
-    if (g < f) continue;
-    double hs = 0.0, ha = 0.0;
-    if (f == i && g == i) {
-      // Schur Z(i, i) = sum_t2 Y(i, t2) adH[t2]^T; top sum_t XH[t] adH[t]^T; two partial sums each
-      double h0 = 0.0, h1 = 0.0, s0 = 0.0, s1 = 0.0;
-      for (int t = 0; t < nF; t++) {
-        if (t == i) continue;
-#pragma unroll
-        for (int l = 0; l < 8; l += 2) {
-          s0 = fma(Ys[i * nF + t][r * 8 + l], aH[t][c * 8 + l], s0);
-          s1 = fma(Ys[i * nF + t][r * 8 + l + 1], aH[t][c * 8 + l + 1], s1);
-          h0 = fma(XH[t][r * 8 + l], aH[t][c * 8 + l], h0);
-          h1 = fma(XH[t][r * 8 + l + 1], aH[t][c * 8 + l + 1], h1);
-        }
-      }
-      hs = s0 + s1;
-      ha = h0 + h1;
-    } else {
-      // Schur: Z(i, g) = Y(i, g) adT[g]^T, Z(f, i) = Z(i, f)^T, Z(f, g) = Y(f, g) adT[g]^T
-      // top: (t, t) XT[t] adT[t]^T, (i, t) XH[t] adT[t]^T, (t, i) = (i, t)^T
-      // operand rows: (yrow, arow) for hs, (xrow, arow) for ha, all uniform choices of the block
-      const bool tr = g == i;  // the transposed form Z(f, i) = Z(i, f)^T
-      const int ro = tr ? c : r, co = tr ? r : c;
-      const double* yrow = (f == i) ? Ys[i * nF + g] : (g == i ? Ys[i * nF + f] : Ys[f * nF + g]);
-      const double* arow = (f == i) ? aT[g] : (g == i ? aT[f] : aT[g]);
-      const double* xrow = (f == i) ? XH[g] : (g == i ? XH[f] : XT[f]);
-      const bool wantA = f == i || g == i || f == g;
-#pragma unroll
-      for (int l = 0; l < 8; l++) {
-        hs = fma(yrow[ro * 8 + l], arow[co * 8 + l], hs);
-        ha = fma(xrow[ro * 8 + l], arow[co * 8 + l], ha);
-      }
-      if (!wantA) ha = 0.0;
-    }
-    if (f < g || r <= c) put(4 + 8 * f + r, 4 + 8 * g + c, ha, hs, f == g && r == c);
-  }
-  HS_TRACE_ROW(trow, 5);
-  // ---- calib x frame (stored in the calib rows): H(4 + 8f + rr, cc), thread = (f, rr, cc)
-  if (tid < nF * 32) {
-    const int f = tid >> 5, rr = (tid >> 2) & 7, cc = tid & 3;
-    double ha = 0.0, hs = 0.0;
-    auto prod84 = [&](const double* L, int t) {  // (L A84[t])[rr][cc], (L E[t])[rr][cc]
-      double x = 0.0, y = 0.0;
-#pragma unroll
-      for (int m = 0; m < 8; m++) {
-        x += L[rr * 8 + m] * A84[t][m * 4 + cc];
-        y += L[rr * 8 + m] * hsm[oE + cc * 64 + t * 8 + m];
-      }
-      ha += x;
-      hs += y;
-    };
-    if (f == i) {
-      for (int t = 0; t < nF; t++)
-        if (t != i) prod84(aH[t], t);
-    } else {
-      prod84(aT[f], f);
-    }
-    put(cc, 4 + 8 * f + rr, ha, hs, false);
-  }
-  // ---- calib x calib: A44 (top), accHcc (Schur)
-  if (tid >= 256 - 16) {
-    const int q = tid - (256 - 16), rr = q >> 2, cc = q & 3;
-    if (rr <= cc) put(rr, cc, A44[q], hsm[oE + 5 * 64 + q], rr == cc);
-  }
-  // ---- b: frames (adH / adT a8r, adH / adT accEB), calib (a4r, accbc)
-  if (tid < n) {
-    double ba = 0.0, bs = 0.0;
-    if (tid < 4) {
-      ba = a4r[tid];
-      bs = hsm[oE + 5 * 64 + 16 + tid];
-    } else {
-      const int f = (tid - 4) >> 3, rr = (tid - 4) & 7;
-      auto prod8 = [&](const double* L, int t) {
-        double x = 0.0, y = 0.0;
-#pragma unroll
-        for (int m = 0; m < 8; m++) {
-          x += L[rr * 8 + m] * a8r[t][m];
-          y += L[rr * 8 + m] * hsm[oE + 4 * 64 + t * 8 + m];
-        }
-        ba += x;
-        bs += y;
-      };
-      if (f == i) {
-        for (int t = 0; t < nF; t++)
-          if (t != i) prod8(aH[t], t);
-      } else {
-        prod8(aT[f], f);
-      }
-    }
-    slot[nn + tid] = ba - bs;
-    if (sepA) {
-      sepA[nn + tid] = ba;
-      sepS[nn + tid] = bs;
-    }
-  }
+  scr[lane] = mm8(L, M, r, c);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const double v = mm8t(scr, R, r, c);
+  __builtin_amdgcn_wave_barrier();
+  return v;
 }
+
+constexpr int ST_LDS = 15360;  // doubles of the stitch block's LDS (the f == g frame block needs ~14k)
 }  // namespace
 
 __global__ __launch_bounds__(256) void hs_k_reduce(HsRedArgs a) {
@@ -1026,43 +798,330 @@ __global__ __launch_bounds__(256) void hs_k_reduce(HsRedArgs a) {
       for (int u = 0; u < 64; u++)
         if (bb + u < b1) s += (double)v[u];
     }
-    __hip_atomic_store(&a.hostsum[(size_t)h * NE64 + e], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  HS_TRACE(a, 1);
-  // hand-off to the host's stitch (MI355X_MICROARCH.md "Valid forms", first table row; cdna_hip_programming.md §6
-  // Guideline 16): the sums were stored sc1 (write-through); every storing wave drains its stores, then after a
-  // barrier ONE lane adds to the host's ticket; the block whose add returns Q - 1 (the last) stitches the host
-  // with sc1 loads of the sums.  No block waits on another (no spin), so any dispatch order and XCD placement is
-  // safe.  This relies on gfx950's sc1 write-through / L1-bypass semantics (measured form, not an architectural
-  // guarantee): the kernel is built for gfx950 only.
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
-#error "hs_k_reduce's sc1 hand-off is validated on gfx950 only"
-#endif
-  __shared__ int s_last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) s_last = __hip_atomic_fetch_add(&a.ticket[h], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.Q - 1;
-  __syncthreads();
-  if (s_last) {
-    __shared__ StitchLds L;
-    if (a.exact) stitch_host<true>(a, h, L);
-    else stitch_host<false>(a, h, L);
-    if (tid == 0)  // ready for the next launch (the kernel boundary orders it)
-      __hip_atomic_store(&a.ticket[h], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    a.hostsum[(size_t)h * NE64 + e] = s;
   }
   HS_TRACE(a, 15);
 }
 
-// multi-rank: this rank's host slots summed in slot order + its energies -> one vector for the RCCL all-reduce
-__global__ __launch_bounds__(256) void hs_k_combine(HsCombArgs a) {
-  const int q = blockIdx.x * 256 + threadIdx.x;
-  if (q < a.SL) {
-    double s = 0.0;
-    for (int h = 0; h < a.nF; h++) s += a.slot[(size_t)h * a.SL + q];
-    a.out[q] = s;
-  } else if (q < a.SL + 3) {
-    a.out[q] = a.sysE[q - a.SL];
+// stitchDoubleMT (Include/AccumulatedTopHessian.h:69-117, Include/AccumulatedSCHessian.h:70-111) with
+// stitchDoubleInternal (Src/AccumulatedTopHessian.cpp:218-280, Src/AccumulatedSCHessian.cpp:54-133) in fp64, one
+// block per output block:
+//   frame block (f, g), f <= g: top  (f,f): sum_t adH[f,t] A[f,t] adH[f,t]^T + sum_h adT[h,f] A[h,f] adT[h,f]^T,
+//                                     (f,g): adH[f,g] A[f,g] adT[f,g]^T + (adH[g,f] A[g,f] adT[g,f]^T)^T;
+//                               Schur: sum over hosts h of host h's four-sandwich sum, which is A_h D_h A_h^T with
+//                                     A_h(f, t) = [f = h] adH[h,t] + [f = t] adT[h,t]: host h not f, g contributes
+//                                     adT[h,f] D_h(f,g) adT[h,g]^T, host f (Y_f(f,g) = sum_t1 adH[f,t1] D_f(t1,g))
+//                                     Y_f adT[f,g]^T, host g adT[g,f] sum_t2 D_g(f,t2) adH[g,t2]^T (f == g: host f
+//                                     sum_t1 adH[f,t1] sum_t2 D_f(t1,t2) adH[f,t2]^T);
+//   calib x frame f: top adH / adT A84, Schur adH / adT accE, b adH / adT a8r and accEB;
+//   calib x calib: A44 and accHcc, b a4r and accbc, summed over every host and pair.
+// Every term is an 8x8 block formed by one wave (lane (r, c)) and kept in LDS; the terms of an output are summed
+// in one fixed order (hosts, then targets), so the system is bit-reproducible.  The vector holds the upper
+// triangle of HA - sc HSC (diagonal: HA (1 + lambda) - sc HSC; the solve adds the priors) and bA - bSC;
+// `sep` HA | bA and HSC | bSC separately.
+__global__ __launch_bounds__(256) void hs_k_stitch(HsStitchArgs a) {
+  __shared__ double lds[ST_LDS];
+  const int nF = a.nF, n = 4 + 8 * nF, nn = n * n, SL = nn + n;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane >> 3, c = lane & 7;
+  const int NE64 = a.ne * 64;
+  const int ND = a.exact ? HS_ND_EXACT : HS_ND_PROD;
+  const int oE = (HS_E_TOP + ND) * 64;  // accE / accEB / Hcc entries of a host sum
+  const int nFB = nF * (nF + 1) / 2;
+  const int j = blockIdx.x;
+  HS_TRACE(a, 0);
+  auto adH = [&](int h, int t) { return a.adHost + (size_t)(h + nF * t) * 64; };
+  auto adT = [&](int h, int t) { return a.adTarget + (size_t)(h + nF * t) * 64; };
+  auto HS = [&](int h) { return a.hostsum + (size_t)h * NE64; };
+  // D_h(t1, t2)[l][cc] at HS(h)[base + l ls + cc cs] (production stores t1 <= t2 only: D(t2, t1) = D(t1, t2)^T)
+  auto Dat = [&](int h, int t1, int t2, int& base, int& ls, int& cs) {
+    const int o1 = t1 - (t1 > h ? 1 : 0), o2 = t2 - (t2 > h ? 1 : 0);
+    if (a.exact) { base = (HS_E_TOP + o1 * 7 + o2) * 64; ls = 8; cs = 1; }
+    else if (o1 <= o2) { base = (HS_E_TOP + dpair(o1, o2)) * 64; ls = 8; cs = 1; }
+    else { base = (HS_E_TOP + dpair(o2, o1)) * 64; ls = 1; cs = 8; }
+  };
+  // copies the 8x8 block D_h(t1, t2) into dst (row-major), 64 lanes of one wave
+  auto loadD = [&](double* dst, int h, int t1, int t2) {
+    int base, ls, cs;
+    Dat(h, t1, t2, base, ls, cs);
+    dst[lane] = HS(h)[base + r * ls + c * cs];
+  };
+  // the octet (16 entries x 8 lanes) of pair (h, t) into dst[e * 8 + k]; 128 values by the 64 lanes of a wave
+  auto loadOct = [&](double* dst, int h, int t) {
+    const double* src = HS(h);
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+      const int q = lane + 64 * u, e = q >> 3, k = q & 7;
+      dst[q] = src[e * 64 + t * 8 + k];
+    }
+  };
+  auto decodeA88 = [&](double* dst, const double* oct) {  // [xi a b] x [xi a b]
+    const int R = 4 + r, C = 4 + c;
+    dst[lane] = top_oct(oct, min(R, C), max(R, C));
+  };
+  double* out = a.out;
+  double* sepA = a.sep;
+  double* sepS = a.sep ? a.sep + SL : nullptr;
+  auto put = [&](int R, int C, double ha, double hs, bool diag) {
+    if (out) out[R * n + C] = diag ? ha * a.lambda1 - hs * a.sc : ha - hs * a.sc;
+    if (sepA) {
+      sepA[R * n + C] = ha;
+      sepS[R * n + C] = hs;
+    }
+  };
+
+  if (j < nFB) {
+    // ------------------------------------------------------------ frame block (f, g), f <= g
+    int f = 0, g = 0;
+    {
+      int q = j;
+      while (q >= nF - f) { q -= nF - f; f++; }
+      g = f + q;
+    }
+    double* aHf = lds;             // [8][64] adH[f, t]
+    double* aTf = aHf + 512;       // [8][64] adT[h, f]
+    double* aHg = aTf + 512;       // [8][64] adH[g, t]
+    double* aTg = aHg + 512;       // [8][64] adT[h, g]
+    double* Dx = aTg + 512;        // [8][64] D_h(f, g) by host h
+    double* Dq = Dx + 512;         // f < g: [8][64] D_f(t1, g) by t1 | [8][64] D_g(f, t2) by t2; f == g: [8][8][64] D_f
+    double* oc = Dq + 4096;        // octets: f < g: (f, g) | (g, f); f == g: (f, t) by t | (h, f) by h, 128 each
+    double* A8 = oc + 2048;        // decoded A88 per octet [16][64]
+    double* tS = A8 + 1024;        // Schur terms [16][64]
+    double* tA = tS + 1024;        // top terms [16][64]
+    double* scr = tA + 1024;       // per-wave scratch [4][2][64]
+    // ---- loads: each wave takes whole blocks (one 64-lane row each), all issued before the products
+    for (int m = wv; m < 4 * nF; m += 4) {  // adjoints
+      const int t = m % nF, kind = m / nF;
+      const double* src = kind == 0 ? adH(f, t) : kind == 1 ? adT(t, f) : kind == 2 ? adH(g, t) : adT(t, g);
+      (kind == 0 ? aHf : kind == 1 ? aTf : kind == 2 ? aHg : aTg)[t * 64 + lane] = src[lane];
+    }
+    if (f < g) {
+      for (int m = wv; m < 3 * nF; m += 4) {
+        const int x = m % nF, kind = m / nF;
+        if (kind == 0 && x != f && x != g) loadD(Dx + x * 64, x, f, g);
+        if (kind == 1 && x != f) loadD(Dq + x * 64, f, x, g);
+        if (kind == 2 && x != g) loadD(Dq + 512 + x * 64, g, f, x);
+      }
+      if (wv == 0) loadOct(oc, f, g);
+      if (wv == 1) loadOct(oc + 128, g, f);
+    } else {
+      for (int m = wv; m < nF + nF * nF; m += 4) {
+        if (m < nF) {
+          if (m != f) loadD(Dx + m * 64, m, f, f);
+        } else {
+          const int t1 = (m - nF) / nF, t2 = (m - nF) % nF;
+          if (t1 != f && t2 != f) loadD(Dq + (t1 * 8 + t2) * 64, f, t1, t2);
+        }
+      }
+      for (int m = wv; m < 2 * nF; m += 4) {
+        const int x = m % nF;
+        if (x == f) continue;
+        if (m < nF) loadOct(oc + x * 128, f, x);
+        else loadOct(oc + (8 + x) * 128, x, f);
+      }
+    }
+    __syncthreads();
+    HS_TRACE(a, 1);
+    double* sw = scr + wv * 128;
+    if (f < g) {
+      if (wv == 0) decodeA88(A8, oc);
+      if (wv == 1) decodeA88(A8 + 64, oc + 128);
+      __syncthreads();
+      // terms: tS[h] for every host h (the host f / g terms in their host slot), tA[0] and tA[1]
+      for (int h = wv; h < nF; h += 4) {
+        double v;
+        if (h != f && h != g) {
+          v = sandwich8(aTf + h * 64, Dx + h * 64, aTg + h * 64, sw, lane);  // adT[h,f] D_h(f,g) adT[h,g]^T
+        } else if (h == f) {  // (sum_t1 adH[f,t1] D_f(t1, g)) adT[f,g]^T
+          double y0 = 0.0, y1 = 0.0;
+          for (int t1 = 0; t1 < nF; t1++) {
+            if (t1 == f) continue;
+            if (t1 & 1) y1 += mm8(aHf + t1 * 64, Dq + t1 * 64, r, c);
+            else y0 += mm8(aHf + t1 * 64, Dq + t1 * 64, r, c);
+          }
+          sw[lane] = y0 + y1;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          v = mm8t(sw, aTg + f * 64, r, c);
+          __builtin_amdgcn_wave_barrier();
+        } else {  // adT[g,f] (sum_t2 D_g(f, t2) adH[g,t2]^T)
+          double y0 = 0.0, y1 = 0.0;
+          for (int t2 = 0; t2 < nF; t2++) {
+            if (t2 == g) continue;
+            if (t2 & 1) y1 += mm8t(Dq + 512 + t2 * 64, aHg + t2 * 64, r, c);
+            else y0 += mm8t(Dq + 512 + t2 * 64, aHg + t2 * 64, r, c);
+          }
+          sw[lane] = y0 + y1;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          v = mm8(aTf + g * 64, sw, r, c);
+          __builtin_amdgcn_wave_barrier();
+        }
+        tS[h * 64 + lane] = v;
+      }
+      if (wv == 2) tA[lane] = sandwich8(aHf + g * 64, A8, aTg + f * 64, sw, lane);       // adH[f,g] A adT[f,g]^T
+      if (wv == 3) tA[64 + lane] = sandwich8(aHg + f * 64, A8 + 64, aTf + g * 64, sw, lane);  // (g,f) pair, transposed below
+      __syncthreads();
+      HS_TRACE(a, 2);
+      if (tid < 64) {
+        double hs = 0.0;
+        for (int h = 0; h < nF; h++) hs += tS[h * 64 + lane];
+        const double ha = tA[lane] + tA[64 + c * 8 + r];
+        put(4 + 8 * f + r, 4 + 8 * g + c, ha, hs, false);
+      }
+    } else {
+      for (int x = wv; x < 2 * nF; x += 4) {
+        const int t = x % nF, oi = x < nF ? t : 8 + t;  // octet slots: (f, t) at t, (h, f) at 8 + h
+        if (t != f) decodeA88(A8 + oi * 64, oc + oi * 128);
+      }
+      __syncthreads();
+      // Schur terms: tS[h] = adT[h,f] D_h(f,f) adT[h,f]^T (h != f), tS[8 + t1] = adH[f,t1] sum_t2 D_f(t1,t2) adH[f,t2]^T
+      // top terms: tA[t] host pairs (f, t), tA[8 + h] target pairs (h, f)
+      for (int x = wv; x < 4 * nF; x += 4) {
+        const int y = x % nF, kind = x / nF;
+        if (y == f) continue;
+        if (kind == 0) {
+          tS[y * 64 + lane] = sandwich8(aTf + y * 64, Dx + y * 64, aTf + y * 64, sw, lane);
+        } else if (kind == 1) {
+          double v0 = 0.0, v1 = 0.0;
+          for (int t2 = 0; t2 < nF; t2++) {
+            if (t2 == f) continue;
+            if (t2 & 1) v1 += mm8t(Dq + (y * 8 + t2) * 64, aHf + t2 * 64, r, c);
+            else v0 += mm8t(Dq + (y * 8 + t2) * 64, aHf + t2 * 64, r, c);
+          }
+          sw[lane] = v0 + v1;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          tS[(8 + y) * 64 + lane] = mm8(aHf + y * 64, sw, r, c);
+          __builtin_amdgcn_wave_barrier();
+        } else if (kind == 2) {
+          tA[y * 64 + lane] = sandwich8(aHf + y * 64, A8 + y * 64, aHf + y * 64, sw, lane);
+        } else {
+          tA[(8 + y) * 64 + lane] = sandwich8(aTf + y * 64, A8 + (8 + y) * 64, aTf + y * 64, sw, lane);
+        }
+      }
+      __syncthreads();
+      HS_TRACE(a, 2);
+      if (tid < 64 && r <= c) {
+        double hs = 0.0, ha = 0.0;
+        for (int h = 0; h < nF; h++) {  // hosts in order; host f's term is its t1 partials in order
+          if (h != f) {
+            hs += tS[h * 64 + lane];
+          } else {
+            double hf = 0.0;
+            for (int t1 = 0; t1 < nF; t1++)
+              if (t1 != f) hf += tS[(8 + t1) * 64 + lane];
+            hs += hf;
+          }
+        }
+        for (int t = 0; t < nF; t++)
+          if (t != f) ha += tA[t * 64 + lane];
+        for (int h = 0; h < nF; h++)
+          if (h != f) ha += tA[(8 + h) * 64 + lane];
+        put(4 + 8 * f + r, 4 + 8 * f + c, ha, hs, r == c);
+      }
+    }
+  } else if (j < nFB + nF) {
+    // ------------------------------------------------------------ calib x frame f, b of frame f
+    const int f = j - nFB;
+    double* aHf = lds;          // [8][64]
+    double* aTf = aHf + 512;    // [8][64]
+    double* oc = aTf + 512;     // [16][128]: (f, t) by t | (h, f) by h
+    double* Ee = oc + 2048;     // [16][40]: accE (32, [k][c]) | accEB (8) of pair (f, t) by t | (h, f) by h
+    double* pt = Ee + 640;      // [4][40] partials
+    for (int m = wv; m < 2 * nF; m += 4) {
+      const int t = m % nF;
+      (m < nF ? aHf : aTf)[t * 64 + lane] = (m < nF ? adH(f, t) : adT(t, f))[lane];
+      if (t == f) continue;
+      const int hh = m < nF ? f : t, tt = m < nF ? t : f;
+      loadOct(oc + m * 128, hh, tt);
+      if (lane < 40) {  // accE [k][c] (lane = 4k + c), accEB [k]
+        const int k = lane < 32 ? lane >> 2 : lane - 32, cc = lane < 32 ? (lane & 3) : 4;
+        Ee[m * 40 + lane] = HS(hh)[oE + cc * 64 + tt * 8 + k];
+      }
+    }
+    __syncthreads();
+    // thread (output o < 40, quarter q): o < 32: H(4 + 8f + rr, cc), o >= 32: b(4 + 8f + rr); pairs m = q, q + 4, ..
+    if (tid < 160) {
+      const int o = tid % 40, q = tid / 40;
+      const int rr = o < 32 ? o >> 2 : o - 32, cc = o < 32 ? (o & 3) : -1;
+      double ha = 0.0, hs = 0.0;
+      for (int m = q; m < 2 * nF; m += 4) {
+        const int t = m % nF;
+        if (t == f) continue;
+        const double* L = (m < nF ? aHf : aTf) + t * 64 + rr * 8;
+        const double* octm = oc + m * 128;
+        const double* Em = Ee + m * 40;
+        double x = 0.0, y = 0.0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          const double tv = cc >= 0 ? top_oct(octm, cc, 4 + k) : top_oct(octm, 4 + k, 12);  // A84[k][cc] | a8r[k]
+          const double ev = cc >= 0 ? Em[k * 4 + cc] : Em[32 + k];                        // accE[k][cc] | accEB[k]
+          x = __builtin_fma(L[k], tv, x);
+          y = __builtin_fma(L[k], ev, y);
+        }
+        ha += x;
+        hs += y;
+      }
+      pt[q * 40 + o] = ha;
+      pt[160 + q * 40 + o] = hs;
+    }
+    __syncthreads();
+    if (tid < 40) {
+      const int rr = tid < 32 ? tid >> 2 : tid - 32, cc = tid < 32 ? (tid & 3) : -1;
+      const double ha = ((pt[tid] + pt[40 + tid]) + pt[80 + tid]) + pt[120 + tid];
+      const double hs = ((pt[160 + tid] + pt[200 + tid]) + pt[240 + tid]) + pt[280 + tid];
+      if (cc >= 0) {
+        put(cc, 4 + 8 * f + rr, ha, hs, false);
+      } else {
+        if (out) out[nn + 4 + 8 * f + rr] = ha - hs;
+        if (sepA) {
+          sepA[nn + 4 + 8 * f + rr] = ha;
+          sepS[nn + 4 + 8 * f + rr] = hs;
+        }
+      }
+    }
+  } else {
+    // ------------------------------------------------------------ calib x calib (A44, accHcc) and calib b (a4r, accbc)
+    double* pt = lds;  // [8 hosts][20] top sums | [8][20] Schur
+    if (tid < 160) {
+      const int o = tid % 20, h = tid / 20;
+      double ta = 0.0, ts = 0.0;
+      if (h < nF) {
+        const double* src = HS(h);
+        for (int t = 0; t < nF; t++) {
+          if (t == h) continue;
+          // A44 (R, C <= 3): lane C, T[R]; a4r (R, 12): TopRight (R, r) -> lane R, T[13]
+          const int R = o < 16 ? min(o >> 2, o & 3) : o - 16, C = o < 16 ? max(o >> 2, o & 3) : 0;
+          ta += o < 16 ? src[R * 64 + t * 8 + C] : src[13 * 64 + t * 8 + R];
+        }
+        ts = src[oE + 5 * 64 + o];  // accHcc (lanes 0..15) / accbc (16..19) of host h
+      }
+      pt[h * 20 + o] = ta;
+      pt[160 + h * 20 + o] = ts;
+    }
+    __syncthreads();
+    if (tid < 20) {
+      double ta = 0.0, ts = 0.0;
+      for (int h = 0; h < nF; h++) {
+        ta += pt[h * 20 + tid];
+        ts += pt[160 + h * 20 + tid];
+      }
+      if (tid < 16) {
+        const int rr = tid >> 2, cc = tid & 3;
+        if (rr <= cc) put(rr, cc, ta, ts, rr == cc);
+      } else {
+        if (out) out[nn + tid - 16] = ta - ts;
+        if (sepA) {
+          sepA[nn + tid - 16] = ta;
+          sepS[nn + tid - 16] = ts;
+        }
+      }
+    }
   }
+  HS_TRACE(a, 15);
 }
 
 // =====================================================================================================
@@ -1359,8 +1418,8 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
 #pragma unroll
     for (int u = 0; u < ST_NU; u++) stw[u] = gs[min(tid + u * SOLVE_NT, ST_WORDS - 1)];
   }
-  // the system slots: thread entries q = tid + 256 u of the packed upper triangle (then b), read at their
-  // place (r, c) of the n x n slot layout, every slot's loads in ONE batch, summed in slot order
+  // the system vector: thread entries q = tid + 256 u of the packed upper triangle (then b), read at their
+  // place (r, c) of the n x n layout, all loads in one batch (unconditional, clamped addresses)
   constexpr int NUQ = (hs_nt(HS_MAXDIM) + HS_MAXDIM + SOLVE_NT - 1) / SOLVE_NT;
   const int ntri = hs_nt(n);
   int qaddr[NUQ], qr[NUQ], qc[NUQ];
@@ -1389,19 +1448,8 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
   double bM_q = 0.0;
   const double sysE0 = a.sysE[0], sysE1 = a.sysE[1], sysE2 = a.sysE[2];  // energy, sum |idepth|, #points
   if (solve) {
-    double v[HS_MAXF][NUQ];
-    // unconditional loads at clamped addresses (a predicated load would split the batch into round trips)
 #pragma unroll
-    for (int k = 0; k < HS_MAXF; k++)
-#pragma unroll
-      for (int u = 0; u < NUQ; u++) v[k][u] = a.slot[(size_t)min(k, a.nslots - 1) * a.SL + max(qaddr[u], 0)];
-#pragma unroll
-    for (int u = 0; u < NUQ; u++) {
-      double sacc = 0.0;
-#pragma unroll
-      for (int k = 0; k < HS_MAXF; k++) sacc += k < a.nslots ? v[k][u] : 0.0;
-      gs[u] = qaddr[u] >= 0 ? sacc : 0.0;
-    }
+    for (int u = 0; u < NUQ; u++) gs[u] = a.sys[max(qaddr[u], 0)];
 #pragma unroll
     for (int u = 0; u < NF_NU; u++) nfv[u] = a.Nproj[min(tid + u * SOLVE_NT, 2 * n * HS_NNS - 1)];
     if (tid < n) bM_q = a.bM[tid];

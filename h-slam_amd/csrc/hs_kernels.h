@@ -88,20 +88,14 @@ struct HsLinArgs {
   long long* trace;            // nullable: per-block wall-clock checkpoints [grid][16]
 };
 
-// hs_k_reduce: (host, chunk) blocks sum the host's block partials in block order (fp64), the last chunk block
-// of a host (ticket) stitches the host into its slot; + one energy block and one setNewFrameEnergyTH block.
+// hs_k_reduce: (host, chunk) blocks sum the host's block partials in block order (fp64) into the host sums; + one
+// energy block (writes the energies behind the system vector) and one setNewFrameEnergyTH block.
 struct HsRedArgs {
-  int nF, ne, exact, Q, nblk;
+  int nF, ne, Q, nblk;
   int blk_begin[HS_MAXF + 1];
   const float* part;
   const double* part_e;
-  double* hostsum;             // [nF][ne][64] (sc1 hand-off to the stitching block)
-  int* ticket;                 // [nF] zero between launches (the stitching block resets its counter)
-  const double* adHost;        // [nF*nF][64]  index h + nF*t
-  const double* adTarget;
-  double* slot;                // [nF][SL] per host: upper triangle of HA - sc HSC (diagonal: HA (1+lambda) - sc HSC) | bA - bSC
-  double* sep;                 // nullable: [nF][2][SL] per host: HA | bA, HSC | bSC (granular read-back)
-  double lambda1, sc;          // 1 + lambda, (double)(float)(1 / (1 + lambda))
+  double* hostsum;             // [nF][ne][64]
   double* sysE;                // [3] energy, sum |idepth|, number of points
   // setNewFrameEnergyTH over the candidates of all ranks (rank r at cand + r*stride, -1 = none)
   const float* cand;
@@ -113,12 +107,19 @@ struct HsRedArgs {
   long long* trace;
 };
 
-// multi-rank: the host slots + energies of this rank summed (slot order) into one vector [SL + 3] for RCCL
-struct HsCombArgs {
-  int nF, SL;
-  const double* slot;
-  const double* sysE;
-  double* out;
+// hs_k_stitch: stitchDoubleMT of the top and Schur systems from the host sums, one block per output block of the
+// system (8x8 frame blocks f <= g, calib x frame f, calib x calib), every output entry summed over the
+// contributing (host, target) pairs in a fixed order and written once.
+struct HsStitchArgs {
+  int nF, exact, ne;
+  const double* hostsum;
+  const double* adHost;        // [nF*nF][64]  index h + nF*t
+  const double* adTarget;
+  double* out;                 // system vector [SL]: upper triangle of HA - sc HSC (diagonal HA (1+lambda) - sc HSC)
+                               // in the n x n layout, then bA - bSC
+  double* sep;                 // nullable: [2][SL] HA | bA, HSC | bSC (granular read-back)
+  double lambda1, sc;          // 1 + lambda, 1 / (1 + lambda)
+  long long* trace;
 };
 
 enum { HS_SOLVE = 1, HS_APPLY = 2 };
@@ -128,9 +129,8 @@ struct HsSolveArgs {
   int iteration;               // < 0: use st->iteration
   int nF;                      // window size (== st->nF)
   HsDevState* st;
-  const double* slot;          // nslots system slots (hs_k_reduce's per-host slots or one all-reduced rank
-  int nslots;                  // vector), stride SL = nt + n, summed in slot order
-  int SL;
+  const double* sys;           // the system vector of hs_k_stitch (all-reduced over the ranks): [n*n] | [n]
+
   const double* HM;            // nullable: marginalization prior is zero
   const double* bM;
   const double* Nproj;         // [2][n][HS_NNS] nullspace factors N | Npi (P = (N Npi^T + Npi N^T) / 2)
@@ -165,7 +165,7 @@ struct HsResubArgs {
 __global__ void hs_k_lin(HsLinArgs a);        // production partitioning
 __global__ void hs_k_lin_exact(HsLinArgs a);  // HS_ACC_EXACT: one wave per host, the reference's sums
 __global__ void hs_k_reduce(HsRedArgs a);
-__global__ void hs_k_combine(HsCombArgs a);
+__global__ void hs_k_stitch(HsStitchArgs a);
 __global__ void hs_k_solve(HsSolveArgs a);
 __global__ void hs_k_resub(HsResubArgs a);
 __global__ void hs_k_apply_step(int n, const float* step, float* idepth, float* idepth_zero);
