@@ -1176,3 +1176,35 @@ int hs_comm_init(hs_ctx* c, const char* id128, int rank, int nranks) {
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- test hook (not part of include/hs_ba.h)
+// Runs hs_k_stitch alone on host-provided per-host sums and adjoints: tests/test_gpu_stitch.py checks it against a
+// numpy restatement of the reference's pair-wise stitchDoubleInternal.  hostsum [nF][hs_ne(exact)][64], adH / adT
+// [nF*nF][64] (index h + nF t), out [n*n + n], sep [2][n*n + n] (nullable).
+extern "C" int hs_debug_stitch(int nF, int exact, const double* hostsum, const double* adH, const double* adT,
+                               double* out, double* sep) {
+  if (nF < 1 || nF > HS_MAXF || !hostsum || !adH || !adT || !out) return fail(HS_ERR_INVALID, "bad args");
+  const int n = 4 + 8 * nF, SL = n * n + n, ne = hs_ne(exact != 0);
+  double *dh = nullptr, *da = nullptr, *dt = nullptr, *dout = nullptr, *dsep = nullptr;
+  HS_TRY(dalloc(&dh, (size_t)nF * ne * 64));
+  HS_TRY(dalloc(&da, (size_t)nF * nF * 64));
+  HS_TRY(dalloc(&dt, (size_t)nF * nF * 64));
+  HS_TRY(dalloc(&dout, (size_t)SL));
+  HS_TRY(dalloc(&dsep, (size_t)2 * SL));
+  HS_HIP(hipMemcpy(dh, hostsum, sizeof(double) * nF * ne * 64, hipMemcpyHostToDevice));
+  HS_HIP(hipMemcpy(da, adH, sizeof(double) * nF * nF * 64, hipMemcpyHostToDevice));
+  HS_HIP(hipMemcpy(dt, adT, sizeof(double) * nF * nF * 64, hipMemcpyHostToDevice));
+  HsStitchArgs st;
+  std::memset(&st, 0, sizeof(st));
+  st.nF = nF; st.exact = exact ? 1 : 0; st.ne = ne;
+  st.hostsum = dh; st.adHost = da; st.adTarget = dt; st.out = dout; st.sep = dsep;
+  st.lambda1 = 1 + 1e-5;
+  st.sc = 1.0f / (1 + 1e-5);
+  hipLaunchKernelGGL(hs_k_stitch, dim3(nF * (nF + 1) / 2 + nF + 1), dim3(256), 0, 0, st);
+  HS_HIP(hipGetLastError());
+  HS_HIP(hipDeviceSynchronize());
+  HS_HIP(hipMemcpy(out, dout, sizeof(double) * SL, hipMemcpyDeviceToHost));
+  if (sep) HS_HIP(hipMemcpy(sep, dsep, sizeof(double) * 2 * SL, hipMemcpyDeviceToHost));
+  for (double* p : {dh, da, dt, dout, dsep}) (void)hipFree(p);
+  return HS_OK;
+}

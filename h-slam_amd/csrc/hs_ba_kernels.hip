@@ -889,10 +889,12 @@ __global__ __launch_bounds__(256) void hs_k_stitch(HsStitchArgs a) {
     double* tA = tS + 1024;        // top terms [16][64]
     double* scr = tA + 1024;       // per-wave scratch [4][2][64]
     // ---- loads: each wave takes whole blocks (one 64-lane row each), all issued before the products
-    for (int m = wv; m < 4 * nF; m += 4) {  // adjoints
+    for (int m = wv; m < 4 * nF; m += 4) {  // adjoints: aHf | aTf | aHg | aTg are consecutive [8][64] arrays
       const int t = m % nF, kind = m / nF;
-      const double* src = kind == 0 ? adH(f, t) : kind == 1 ? adT(t, f) : kind == 2 ? adH(g, t) : adT(t, g);
-      (kind == 0 ? aHf : kind == 1 ? aTf : kind == 2 ? aHg : aTg)[t * 64 + lane] = src[lane];
+      const bool host = (kind & 1) == 0;  // adH(f | g, t) or adT(t, f | g)
+      const int fg = kind < 2 ? f : g;
+      const int hh = host ? fg : t, tt = host ? t : fg;
+      lds[kind * 512 + t * 64 + lane] = (host ? a.adHost : a.adTarget)[(size_t)(hh + nF * tt) * 64 + lane];
     }
     if (f < g) {
       for (int m = wv; m < 3 * nF; m += 4) {
