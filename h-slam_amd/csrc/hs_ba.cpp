@@ -279,7 +279,7 @@ static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = fals
   a.skip_threshold = skip_threshold ? 1 : 0;
   a.trace = c->d_tr_acc;
   if (!readback) {
-    hipLaunchKernelGGL(hs_k_reduce, dim3(c->nF * c->Q + 2), dim3(256), 0, c->stream, a);
+    hipLaunchKernelGGL(hs_k_reduce, dim3(c->nF * c->Q + 1), dim3(256), 0, c->stream, a);
     HS_HIP(hipGetLastError());
   }
   HsStitchArgs st;
@@ -291,7 +291,9 @@ static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = fals
   st.lambda1 = 1 + 1e-5;       // SOLVER_FIX_LAMBDA (Src/EnergyFunctional.cpp:707-708)
   st.sc = 1.0f / (1 + 1e-5);   // H -= H_sc * (1.0f / (1 + lambda)) (:763)
   st.trace = c->d_tr_st;
-  hipLaunchKernelGGL(hs_k_stitch, dim3(c->nF * (c->nF + 1) / 2 + c->nF + 1), dim3(256), 0, c->stream, st);
+  st.red = a;
+  st.red.skip_threshold = (skip_threshold || readback) ? 1 : 0;
+  hipLaunchKernelGGL(hs_k_stitch, dim3(c->nF * (c->nF + 1) / 2 + c->nF + 2), dim3(256), 0, c->stream, st);
   HS_HIP(hipGetLastError());
   if (sep) c->sepValid = true;
   if (c->comm && !readback)
@@ -390,8 +392,8 @@ static int dump_traces(hs_ctx* c) {
     std::fprintf(stderr, "\n");
   }
   HS_TRY(dump_one("linearize", c->d_tr_lin, c->nblk, tick_us, c->stream));
-  HS_TRY(dump_one("reduce", c->d_tr_acc, c->nF * c->Q + 2, tick_us, c->stream));
-  HS_TRY(dump_one("stitch", c->d_tr_st, c->nF * (c->nF + 1) / 2 + c->nF + 1, tick_us, c->stream));
+  HS_TRY(dump_one("reduce", c->d_tr_acc, c->nF * c->Q + 1, tick_us, c->stream));
+  HS_TRY(dump_one("stitch", c->d_tr_st, c->nF * (c->nF + 1) / 2 + c->nF + 2, tick_us, c->stream));
   return HS_OK;
 }
 
@@ -714,8 +716,8 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
   c->tracing = tr && tr[0] == '1';
   if (c->tracing) {
     HS_TRY(dalloc(&c->d_tr_lin, (size_t)std::max(c->nblk, 1) * 16));
-    HS_TRY(dalloc(&c->d_tr_acc, (size_t)(nF * c->Q + 2) * 16));
-    HS_TRY(dalloc(&c->d_tr_st, (size_t)(nF * (nF + 1) / 2 + nF + 1) * 16));
+    HS_TRY(dalloc(&c->d_tr_acc, (size_t)(nF * c->Q + 1) * 16));
+    HS_TRY(dalloc(&c->d_tr_st, (size_t)(nF * (nF + 1) / 2 + nF + 2) * 16));
     HS_TRY(dalloc(&c->d_tr_solve, 32));
   }
 
@@ -1200,7 +1202,8 @@ extern "C" int hs_debug_stitch(int nF, int exact, const double* hostsum, const d
   st.hostsum = dh; st.adHost = da; st.adTarget = dt; st.out = dout; st.sep = dsep;
   st.lambda1 = 1 + 1e-5;
   st.sc = 1.0f / (1 + 1e-5);
-  hipLaunchKernelGGL(hs_k_stitch, dim3(nF * (nF + 1) / 2 + nF + 1), dim3(256), 0, 0, st);
+  st.red.skip_threshold = 1;
+  hipLaunchKernelGGL(hs_k_stitch, dim3(nF * (nF + 1) / 2 + nF + 2), dim3(256), 0, 0, st);
   HS_HIP(hipGetLastError());
   HS_HIP(hipDeviceSynchronize());
   HS_HIP(hipMemcpy(out, dout, sizeof(double) * SL, hipMemcpyDeviceToHost));

@@ -777,11 +777,6 @@ __global__ __launch_bounds__(256) void hs_k_reduce(HsRedArgs a) {
   const int b = blockIdx.x, tid = threadIdx.x;
   HS_TRACE(a, 0);
   if (b == nred) { red_energy_block(a); HS_TRACE(a, 15); return; }
-  if (b == nred + 1) {
-    if (!a.skip_threshold) red_energy_th_block(a);
-    HS_TRACE(a, 15);
-    return;
-  }
   const int h = b / a.Q, q = b % a.Q;
   const int NE64 = a.ne * 64;
   const int e = q * 256 + tid;  // entry of the host's [ne][64] accumulators
@@ -829,6 +824,11 @@ __global__ __launch_bounds__(256) void hs_k_stitch(HsStitchArgs a) {
   const int nFB = nF * (nF + 1) / 2;
   const int j = blockIdx.x;
   HS_TRACE(a, 0);
+  if (j == nFB + nF + 1) {  // setNewFrameEnergyTH for the next linearization, beside the stitch
+    if (!a.red.skip_threshold) red_energy_th_block(a.red);
+    HS_TRACE(a, 15);
+    return;
+  }
   auto adH = [&](int h, int t) { return a.adHost + (size_t)(h + nF * t) * 64; };
   auto adT = [&](int h, int t) { return a.adTarget + (size_t)(h + nF * t) * 64; };
   auto HS = [&](int h) { return a.hostsum + (size_t)h * NE64; };
@@ -838,21 +838,6 @@ __global__ __launch_bounds__(256) void hs_k_stitch(HsStitchArgs a) {
     if (a.exact) { base = (HS_E_TOP + o1 * 7 + o2) * 64; ls = 8; cs = 1; }
     else if (o1 <= o2) { base = (HS_E_TOP + dpair(o1, o2)) * 64; ls = 8; cs = 1; }
     else { base = (HS_E_TOP + dpair(o2, o1)) * 64; ls = 1; cs = 8; }
-  };
-  // copies the 8x8 block D_h(t1, t2) into dst (row-major), 64 lanes of one wave
-  auto loadD = [&](double* dst, int h, int t1, int t2) {
-    int base, ls, cs;
-    Dat(h, t1, t2, base, ls, cs);
-    dst[lane] = HS(h)[base + r * ls + c * cs];
-  };
-  // the octet (16 entries x 8 lanes) of pair (h, t) into dst[e * 8 + k]; 128 values by the 64 lanes of a wave
-  auto loadOct = [&](double* dst, int h, int t) {
-    const double* src = HS(h);
-#pragma unroll
-    for (int u = 0; u < 2; u++) {
-      const int q = lane + 64 * u, e = q >> 3, k = q & 7;
-      dst[q] = src[e * 64 + t * 8 + k];
-    }
   };
   auto decodeA88 = [&](double* dst, const double* oct) {  // [xi a b] x [xi a b]
     const int R = 4 + r, C = 4 + c;
@@ -888,38 +873,68 @@ __global__ __launch_bounds__(256) void hs_k_stitch(HsStitchArgs a) {
     double* tS = A8 + 1024;        // Schur terms [16][64]
     double* tA = tS + 1024;        // top terms [16][64]
     double* scr = tA + 1024;       // per-wave scratch [4][2][64]
-    // ---- loads: each wave takes whole blocks (one 64-lane row each), all issued before the products
-    for (int m = wv; m < 4 * nF; m += 4) {  // adjoints: aHf | aTf | aHg | aTg are consecutive [8][64] arrays
-      const int t = m % nF, kind = m / nF;
-      const bool host = (kind & 1) == 0;  // adH(f | g, t) or adT(t, f | g)
-      const int fg = kind < 2 ? f : g;
-      const int hh = host ? fg : t, tt = host ? t : fg;
-      lds[kind * 512 + t * 64 + lane] = (host ? a.adHost : a.adTarget)[(size_t)(hh + nF * tt) * 64 + lane];
-    }
-    if (f < g) {
-      for (int m = wv; m < 3 * nF; m += 4) {
-        const int x = m % nF, kind = m / nF;
-        if (kind == 0 && x != f && x != g) loadD(Dx + x * 64, x, f, g);
-        if (kind == 1 && x != f) loadD(Dq + x * 64, f, x, g);
-        if (kind == 2 && x != g) loadD(Dq + 512 + x * 64, g, f, x);
-      }
-      if (wv == 0) loadOct(oc, f, g);
-      if (wv == 1) loadOct(oc + 128, g, f);
-    } else {
-      for (int m = wv; m < nF + nF * nF; m += 4) {
-        if (m < nF) {
-          if (m != f) loadD(Dx + m * 64, m, f, f);
-        } else {
-          const int t1 = (m - nF) / nF, t2 = (m - nF) % nF;
-          if (t1 != f && t2 != f) loadD(Dq + (t1 * 8 + t2) * 64, f, t1, t2);
+    // ---- loads: a flat table (adjoints | D blocks | octets), every thread's loads issued in one batch at
+    // clamped addresses, then the LDS stores (a load per table row would be a dependent round trip each)
+    {
+      const int nAdj = (f < g ? 4 : 2) * nF * 64;
+      const int nD = f < g ? 3 * nF * 64 : (nF + nF * nF) * 64;
+      const int nOct = f < g ? 256 : 2 * nF * 128;
+      const int total = nAdj + nD + nOct;
+      constexpr int SU = 32;
+      double v[SU];
+      int dst[SU];
+#pragma unroll
+      for (int u = 0; u < SU; u++) {
+        const int q = tid + 256 * u;
+        const double* src = a.adHost;
+        int d = -1;
+        if (q < nAdj) {  // aHf | aTf | aHg | aTg
+          const int kind = q / (nF * 64), t = (q >> 6) % nF, ln = q & 63;
+          const bool host = (kind & 1) == 0;
+          const int fg = kind < 2 ? f : g, hh = host ? fg : t, tt = host ? t : fg;
+          src = (host ? a.adHost : a.adTarget) + (size_t)(hh + nF * tt) * 64 + ln;
+          d = kind * 512 + t * 64 + ln;
+        } else if (q < nAdj + nD) {
+          const int qd = q - nAdj, blk = qd >> 6, ln = qd & 63, rr = ln >> 3, cc = ln & 7;
+          int h = -1, t1 = 0, t2 = 0;
+          if (f < g) {
+            const int kind = blk / nF, x = blk % nF;
+            if (kind == 0 && x != f && x != g) { h = x; t1 = f; t2 = g; d = (int)(Dx - lds) + x * 64 + ln; }
+            if (kind == 1 && x != f) { h = f; t1 = x; t2 = g; d = (int)(Dq - lds) + x * 64 + ln; }
+            if (kind == 2 && x != g) { h = g; t1 = f; t2 = x; d = (int)(Dq - lds) + 512 + x * 64 + ln; }
+          } else if (blk < nF) {
+            if (blk != f) { h = blk; t1 = f; t2 = f; d = (int)(Dx - lds) + blk * 64 + ln; }
+          } else {
+            const int x1 = (blk - nF) / nF, x2 = (blk - nF) % nF;
+            if (x1 != f && x2 != f) { h = f; t1 = x1; t2 = x2; d = (int)(Dq - lds) + (x1 * 8 + x2) * 64 + ln; }
+          }
+          if (h >= 0) {
+            int base, ls, cs;
+            Dat(h, t1, t2, base, ls, cs);
+            src = HS(h) + base + rr * ls + cc * cs;
+          }
+        } else if (q < total) {
+          const int qo = q - nAdj - nD, oi = qo >> 7, w = qo & 127, e = w >> 3, k = w & 7;
+          int hh = -1, tt = 0;
+          if (f < g) {
+            if (oi == 0) { hh = f; tt = g; } else { hh = g; tt = f; }
+            d = (int)(oc - lds) + oi * 128 + w;
+          } else {
+            const int x = oi % nF;  // octet slots: (f, t) at t, (h, f) at 8 + h
+            if (x != f) {
+              hh = oi < nF ? f : x;
+              tt = oi < nF ? x : f;
+              d = (int)(oc - lds) + (oi < nF ? x : 8 + x) * 128 + w;
+            }
+          }
+          if (hh >= 0) src = HS(hh) + e * 64 + tt * 8 + k;
         }
+        v[u] = *src;
+        dst[u] = d;
       }
-      for (int m = wv; m < 2 * nF; m += 4) {
-        const int x = m % nF;
-        if (x == f) continue;
-        if (m < nF) loadOct(oc + x * 128, f, x);
-        else loadOct(oc + (8 + x) * 128, x, f);
-      }
+#pragma unroll
+      for (int u = 0; u < SU; u++)
+        if (dst[u] >= 0) lds[dst[u]] = v[u];
     }
     __syncthreads();
     HS_TRACE(a, 1);
@@ -1033,16 +1048,40 @@ __global__ __launch_bounds__(256) void hs_k_stitch(HsStitchArgs a) {
     double* oc = aTf + 512;     // [16][128]: (f, t) by t | (h, f) by h
     double* Ee = oc + 2048;     // [16][40]: accE (32, [k][c]) | accEB (8) of pair (f, t) by t | (h, f) by h
     double* pt = Ee + 640;      // [4][40] partials
-    for (int m = wv; m < 2 * nF; m += 4) {
-      const int t = m % nF;
-      (m < nF ? aHf : aTf)[t * 64 + lane] = (m < nF ? adH(f, t) : adT(t, f))[lane];
-      if (t == f) continue;
-      const int hh = m < nF ? f : t, tt = m < nF ? t : f;
-      loadOct(oc + m * 128, hh, tt);
-      if (lane < 40) {  // accE [k][c] (lane = 4k + c), accEB [k]
-        const int k = lane < 32 ? lane >> 2 : lane - 32, cc = lane < 32 ? (lane & 3) : 4;
-        Ee[m * 40 + lane] = HS(hh)[oE + cc * 64 + tt * 8 + k];
+    {  // flat load table: adjoints (2 nF x 64) | octets (2 nF x 128) | accE / accEB (2 nF x 40), one batch
+      const int nAdj = 2 * nF * 64, nOct = 2 * nF * 128, total = nAdj + nOct + 2 * nF * 40;
+      constexpr int SU = 16;
+      double v[SU];
+      int dst[SU];
+#pragma unroll
+      for (int u = 0; u < SU; u++) {
+        const int q = tid + 256 * u;
+        const double* src = a.adHost;
+        int d = -1;
+        if (q < nAdj) {
+          const int m = q >> 6, ln = q & 63, t = m % nF;
+          src = (m < nF ? adH(f, t) : adT(t, f)) + ln;
+          d = (m < nF ? 0 : 512) + t * 64 + ln;
+        } else if (q < nAdj + nOct) {
+          const int qo = q - nAdj, m = qo >> 7, w = qo & 127, e = w >> 3, k = w & 7, t = m % nF;
+          if (t != f) {
+            src = HS(m < nF ? f : t) + e * 64 + (m < nF ? t : f) * 8 + k;
+            d = (int)(oc - lds) + m * 128 + w;
+          }
+        } else if (q < total) {
+          const int qe = q - nAdj - nOct, m = qe / 40, ln = qe % 40, t = m % nF;
+          if (t != f) {
+            const int k = ln < 32 ? ln >> 2 : ln - 32, cc = ln < 32 ? (ln & 3) : 4;
+            src = HS(m < nF ? f : t) + oE + cc * 64 + (m < nF ? t : f) * 8 + k;  // accE [k][c] (4k + c), accEB [k]
+            d = (int)(Ee - lds) + m * 40 + ln;
+          }
+        }
+        v[u] = *src;
+        dst[u] = d;
       }
+#pragma unroll
+      for (int u = 0; u < SU; u++)
+        if (dst[u] >= 0) lds[dst[u]] = v[u];
     }
     __syncthreads();
     // thread (output o < 40, quarter q): o < 32: H(4 + 8f + rr, cc), o >= 32: b(4 + 8f + rr); pairs m = q, q + 4, ..

@@ -89,7 +89,8 @@ struct HsLinArgs {
 };
 
 // hs_k_reduce: (host, chunk) blocks sum the host's block partials in block order (fp64) into the host sums; + one
-// energy block (writes the energies behind the system vector) and one setNewFrameEnergyTH block.
+// energy block (writes the energies behind the system vector).  The setNewFrameEnergyTH fields are read by the
+// extra block of hs_k_stitch.
 struct HsRedArgs {
   int nF, ne, Q, nblk;
   int blk_begin[HS_MAXF + 1];
@@ -119,6 +120,7 @@ struct HsStitchArgs {
                                // in the n x n layout, then bA - bSC
   double* sep;                 // nullable: [2][SL] HA | bA, HSC | bSC (granular read-back)
   double lambda1, sc;          // 1 + lambda, 1 / (1 + lambda)
+  HsRedArgs red;               // setNewFrameEnergyTH (the launch's last block)
   long long* trace;
 };
 
