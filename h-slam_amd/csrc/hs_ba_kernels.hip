@@ -876,9 +876,11 @@ __global__ __launch_bounds__(256) void hs_k_stitch(HsStitchArgs a) {
     // ---- loads: a flat table (adjoints | D blocks | octets), every thread's loads issued in one batch at
     // clamped addresses, then the LDS stores (a load per table row would be a dependent round trip each)
     {
-      const int nAdj = (f < g ? 4 : 2) * nF * 64;
-      const int nD = f < g ? 3 * nF * 64 : (nF + nF * nF) * 64;
-      const int nOct = f < g ? 256 : 2 * nF * 128;
+      // table rows at power-of-two strides (slot index t < 8 = HS_MAXF; rows with t >= nF are skipped), so the
+      // index math is shifts and masks, not runtime divisions
+      const int nAdj = (f < g ? 4 : 2) * 512;        // [kind][t][64]
+      const int nD = f < g ? 3 * 512 : 512 + 4096;   // f < g: [kind][x][64]; f == g: Dx [h][64] | Dq [t1][t2][64]
+      const int nOct = f < g ? 256 : 16 * 128;       // [slot][128]
       const int total = nAdj + nD + nOct;
       constexpr int SU = 32;
       double v[SU];
@@ -889,24 +891,32 @@ __global__ __launch_bounds__(256) void hs_k_stitch(HsStitchArgs a) {
         const double* src = a.adHost;
         int d = -1;
         if (q < nAdj) {  // aHf | aTf | aHg | aTg
-          const int kind = q / (nF * 64), t = (q >> 6) % nF, ln = q & 63;
+          const int kind = q >> 9, t = (q >> 6) & 7, ln = q & 63;
           const bool host = (kind & 1) == 0;
           const int fg = kind < 2 ? f : g, hh = host ? fg : t, tt = host ? t : fg;
-          src = (host ? a.adHost : a.adTarget) + (size_t)(hh + nF * tt) * 64 + ln;
-          d = kind * 512 + t * 64 + ln;
+          if (t < nF) {
+            src = (host ? a.adHost : a.adTarget) + (size_t)(hh + nF * tt) * 64 + ln;
+            d = q;
+          }
         } else if (q < nAdj + nD) {
-          const int qd = q - nAdj, blk = qd >> 6, ln = qd & 63, rr = ln >> 3, cc = ln & 7;
+          const int qd = q - nAdj, ln = qd & 63, rr = ln >> 3, cc = ln & 7;
           int h = -1, t1 = 0, t2 = 0;
           if (f < g) {
-            const int kind = blk / nF, x = blk % nF;
-            if (kind == 0 && x != f && x != g) { h = x; t1 = f; t2 = g; d = (int)(Dx - lds) + x * 64 + ln; }
-            if (kind == 1 && x != f) { h = f; t1 = x; t2 = g; d = (int)(Dq - lds) + x * 64 + ln; }
-            if (kind == 2 && x != g) { h = g; t1 = f; t2 = x; d = (int)(Dq - lds) + 512 + x * 64 + ln; }
-          } else if (blk < nF) {
-            if (blk != f) { h = blk; t1 = f; t2 = f; d = (int)(Dx - lds) + blk * 64 + ln; }
+            const int kind = qd >> 9, x = (qd >> 6) & 7;
+            if (x < nF) {
+              if (kind == 0 && x != f && x != g) { h = x; t1 = f; t2 = g; d = (int)(Dx - lds) + x * 64 + ln; }
+              if (kind == 1 && x != f) { h = f; t1 = x; t2 = g; d = (int)(Dq - lds) + x * 64 + ln; }
+              if (kind == 2 && x != g) { h = g; t1 = f; t2 = x; d = (int)(Dq - lds) + 512 + x * 64 + ln; }
+            }
+          } else if (qd < 512) {
+            const int x = qd >> 6;
+            if (x < nF && x != f) { h = x; t1 = f; t2 = f; d = (int)(Dx - lds) + qd; }
           } else {
-            const int x1 = (blk - nF) / nF, x2 = (blk - nF) % nF;
-            if (x1 != f && x2 != f) { h = f; t1 = x1; t2 = x2; d = (int)(Dq - lds) + (x1 * 8 + x2) * 64 + ln; }
+            const int x1 = (qd - 512) >> 9, x2 = ((qd - 512) >> 6) & 7;
+            if (x1 < nF && x2 < nF && x1 != f && x2 != f) {
+              h = f; t1 = x1; t2 = x2;
+              d = (int)(Dq - lds) + (qd - 512);
+            }
           }
           if (h >= 0) {
             int base, ls, cs;
@@ -918,16 +928,17 @@ __global__ __launch_bounds__(256) void hs_k_stitch(HsStitchArgs a) {
           int hh = -1, tt = 0;
           if (f < g) {
             if (oi == 0) { hh = f; tt = g; } else { hh = g; tt = f; }
-            d = (int)(oc - lds) + oi * 128 + w;
           } else {
-            const int x = oi % nF;  // octet slots: (f, t) at t, (h, f) at 8 + h
-            if (x != f) {
-              hh = oi < nF ? f : x;
-              tt = oi < nF ? x : f;
-              d = (int)(oc - lds) + (oi < nF ? x : 8 + x) * 128 + w;
+            const int x = oi & 7;  // octet slots: (f, t) at t, (h, f) at 8 + h
+            if (x < nF && x != f) {
+              hh = oi < 8 ? f : x;
+              tt = oi < 8 ? x : f;
             }
           }
-          if (hh >= 0) src = HS(hh) + e * 64 + tt * 8 + k;
+          if (hh >= 0) {
+            src = HS(hh) + e * 64 + tt * 8 + k;
+            d = (int)(oc - lds) + qo;
+          }
         }
         v[u] = *src;
         dst[u] = d;
@@ -1045,12 +1056,13 @@ __global__ __launch_bounds__(256) void hs_k_stitch(HsStitchArgs a) {
     const int f = j - nFB;
     double* aHf = lds;          // [8][64]
     double* aTf = aHf + 512;    // [8][64]
-    double* oc = aTf + 512;     // [16][128]: (f, t) by t | (h, f) by h
-    double* Ee = oc + 2048;     // [16][40]: accE (32, [k][c]) | accEB (8) of pair (f, t) by t | (h, f) by h
-    double* pt = Ee + 640;      // [4][40] partials
-    {  // flat load table: adjoints (2 nF x 64) | octets (2 nF x 128) | accE / accEB (2 nF x 40), one batch
-      const int nAdj = 2 * nF * 64, nOct = 2 * nF * 128, total = nAdj + nOct + 2 * nF * 40;
-      constexpr int SU = 16;
+    double* oc = aTf + 512;     // [16][128]: (f, t) by t | (h, f) by 8 + h
+    double* Ee = oc + 2048;     // [16][40]: accE (32, [k][c]) | accEB (8) of pair (f, t) by t | (h, f) by 8 + h
+    double* pt = Ee + 640;      // [8][40] partials
+    {  // flat load table, slots m < 16 (m < 8: pair (f, m), m >= 8: pair (m - 8, f)): adjoints [m][64] | octets
+       // [m][128] | accE / accEB [m][40], one batch, power-of-two strides
+      constexpr int nAdj = 16 * 64, nOct = 16 * 128, total = nAdj + nOct + 16 * 64;
+      constexpr int SU = 20;
       double v[SU];
       int dst[SU];
 #pragma unroll
@@ -1059,20 +1071,22 @@ __global__ __launch_bounds__(256) void hs_k_stitch(HsStitchArgs a) {
         const double* src = a.adHost;
         int d = -1;
         if (q < nAdj) {
-          const int m = q >> 6, ln = q & 63, t = m % nF;
-          src = (m < nF ? adH(f, t) : adT(t, f)) + ln;
-          d = (m < nF ? 0 : 512) + t * 64 + ln;
+          const int m = q >> 6, ln = q & 63, t = m & 7;
+          if (t < nF) {
+            src = (m < 8 ? adH(f, t) : adT(t, f)) + ln;
+            d = q;
+          }
         } else if (q < nAdj + nOct) {
-          const int qo = q - nAdj, m = qo >> 7, w = qo & 127, e = w >> 3, k = w & 7, t = m % nF;
-          if (t != f) {
-            src = HS(m < nF ? f : t) + e * 64 + (m < nF ? t : f) * 8 + k;
-            d = (int)(oc - lds) + m * 128 + w;
+          const int qo = q - nAdj, m = qo >> 7, w = qo & 127, e = w >> 3, k = w & 7, t = m & 7;
+          if (t < nF && t != f) {
+            src = HS(m < 8 ? f : t) + e * 64 + (m < 8 ? t : f) * 8 + k;
+            d = (int)(oc - lds) + qo;
           }
         } else if (q < total) {
-          const int qe = q - nAdj - nOct, m = qe / 40, ln = qe % 40, t = m % nF;
-          if (t != f) {
+          const int qe = q - nAdj - nOct, m = qe >> 6, ln = qe & 63, t = m & 7;
+          if (t < nF && t != f && ln < 40) {
             const int k = ln < 32 ? ln >> 2 : ln - 32, cc = ln < 32 ? (ln & 3) : 4;
-            src = HS(m < nF ? f : t) + oE + cc * 64 + (m < nF ? t : f) * 8 + k;  // accE [k][c] (4k + c), accEB [k]
+            src = HS(m < 8 ? f : t) + oE + cc * 64 + (m < 8 ? t : f) * 8 + k;  // accE [k][c] (4k + c), accEB [k]
             d = (int)(Ee - lds) + m * 40 + ln;
           }
         }
@@ -1089,10 +1103,10 @@ __global__ __launch_bounds__(256) void hs_k_stitch(HsStitchArgs a) {
       const int o = tid % 40, q = tid / 40;
       const int rr = o < 32 ? o >> 2 : o - 32, cc = o < 32 ? (o & 3) : -1;
       double ha = 0.0, hs = 0.0;
-      for (int m = q; m < 2 * nF; m += 4) {
-        const int t = m % nF;
-        if (t == f) continue;
-        const double* L = (m < nF ? aHf : aTf) + t * 64 + rr * 8;
+      for (int m = q; m < 16; m += 4) {
+        const int t = m & 7;
+        if (t >= nF || t == f) continue;
+        const double* L = (m < 8 ? aHf : aTf) + t * 64 + rr * 8;
         const double* octm = oc + m * 128;
         const double* Em = Ee + m * 40;
         double x = 0.0, y = 0.0;
