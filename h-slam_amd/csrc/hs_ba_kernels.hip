@@ -659,45 +659,51 @@ __device__ void red_energy_block(const HsRedArgs& a) {
   if (tid < 3) a.sysE[tid] = red[tid][0];
 }
 
-// setNewFrameEnergyTH: k-th smallest candidate by a 4-pass radix select with a parallel bin scan.
-// Candidates: one float per point and rank (-1 / negative = none); the ranks' arrays are all-gathered so
-// every rank selects over the same union and computes the same threshold.
+// setNewFrameEnergyTH: k-th smallest candidate by a 4-pass radix select (bins counted with LDS integer atomics:
+// order-independent; bin scan by wave prefix sums).  Candidates: one float per point and rank (-1 / negative =
+// none); the ranks' arrays are all-gathered so every rank selects over the same union and computes the same
+// threshold.  Any block size >= 256.
 __device__ void red_energy_th_block(const HsRedArgs& a) {
-  __shared__ unsigned int hist[256], scan[256];
+  __shared__ unsigned int hist[256], wsum[4];
   __shared__ unsigned int s_prefix, s_mask, s_k, s_n;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63;
+  const bool bin = tid < 256;
   if (tid == 0) {
     s_prefix = 0;
     s_mask = 0;
   }
+  const int total = a.nranks * a.stride;
   for (int pass = 0; pass < 4; pass++) {
     const int shift = 24 - 8 * pass;
-    hist[tid] = 0;
+    if (bin) hist[tid] = 0;
     __syncthreads();
     const unsigned int prefix = s_prefix, mask = s_mask;
-    const int total = a.nranks * a.stride;
-    for (int i = tid; i < total; i += 256) {
+    for (int i = tid; i < total; i += nt) {
       const unsigned int v = __float_as_uint(a.cand[i]);
       if (v < 0x80000000u && (v & mask) == prefix) atomicAdd(&hist[(v >> shift) & 255u], 1u);
     }
     __syncthreads();
-    scan[tid] = hist[tid];
-    __syncthreads();
-    for (int o = 1; o < 256; o <<= 1) {
-      const unsigned int v = tid >= o ? scan[tid - o] : 0u;
-      __syncthreads();
-      scan[tid] += v;
-      __syncthreads();
+    const unsigned int hcount = bin ? hist[tid] : 0u;
+    unsigned int x = hcount;  // inclusive prefix over the wave's 64 bins
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned int y = __shfl_up(x, o);
+      if (lane >= o) x += y;
     }
-    if (pass == 0 && tid == 0) {
-      s_n = scan[255];
-      s_k = (unsigned int)(int)(a.frameEnergyTHN * (float)scan[255]);
+    if (bin && lane == 63) wsum[tid >> 6] = x;
+    __syncthreads();
+    unsigned int off = 0;
+    for (int w = 0; w < 4 && w < (tid >> 6); w++) off += wsum[w];
+    const unsigned int incl = x + off;
+    if (pass == 0 && tid == 255) {
+      s_n = incl;
+      s_k = (unsigned int)(int)(a.frameEnergyTHN * (float)incl);
     }
     __syncthreads();
     if (s_n == 0) break;
-    const unsigned int incl = scan[tid], excl = incl - hist[tid], kk = s_k;
+    const unsigned int excl = incl - hcount, kk = s_k;
     __syncthreads();
-    if (excl <= kk && kk < incl) {
+    if (bin && excl <= kk && kk < incl) {
       s_k = kk - excl;
       s_prefix = prefix | ((unsigned int)tid << shift);
       s_mask = mask | (255u << shift);
@@ -717,7 +723,6 @@ __device__ void red_energy_th_block(const HsRedArgs& a) {
     }
   }
 }
-
 
 // the (R, C) entry (R <= C) of one (host, target) pair's 13x13 AccumulatorApprox block [calib 4 | xi 6 | a | b | r]
 // from its octet of the host sums, oct[e * 8 + k] = entry e of lane k (the owner layout of acc_point)
@@ -769,7 +774,8 @@ __device__ __forceinline__ double sandwich8(const double* L, const double* M, co
   return v;
 }
 
-constexpr int ST_LDS = 15360;  // doubles of the stitch block's LDS (the f == g frame block needs ~14k)
+constexpr int ST_NT = 1024, ST_NW = ST_NT / 64;  // stitch block: 16 waves, one 8x8 term per wave at a time
+constexpr int ST_LDS = 12288 + ST_NW * 64;  // doubles of the stitch block's LDS (the f == g frame block)
 }  // namespace
 
 __global__ __launch_bounds__(256) void hs_k_reduce(HsRedArgs a) {
@@ -814,7 +820,7 @@ __global__ __launch_bounds__(256) void hs_k_reduce(HsRedArgs a) {
 // in one fixed order (hosts, then targets), so the system is bit-reproducible.  The vector holds the upper
 // triangle of HA - sc HSC (diagonal: HA (1 + lambda) - sc HSC; the solve adds the priors) and bA - bSC;
 // `sep` HA | bA and HSC | bSC separately.
-__global__ __launch_bounds__(256) void hs_k_stitch(HsStitchArgs a) {
+__global__ __launch_bounds__(ST_NT) void hs_k_stitch(HsStitchArgs a) {
   __shared__ double lds[ST_LDS];
   const int nF = a.nF, n = 4 + 8 * nF, nn = n * n, SL = nn + n;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane >> 3, c = lane & 7;
@@ -872,7 +878,7 @@ __global__ __launch_bounds__(256) void hs_k_stitch(HsStitchArgs a) {
     double* A8 = oc + 2048;        // decoded A88 per octet [16][64]
     double* tS = A8 + 1024;        // Schur terms [16][64]
     double* tA = tS + 1024;        // top terms [16][64]
-    double* scr = tA + 1024;       // per-wave scratch [4][2][64]
+    double* scr = tA + 1024;       // per-wave scratch [ST_NW][64]
     // ---- loads: a flat table (adjoints | D blocks | octets), every thread's loads issued in one batch at
     // clamped addresses, then the LDS stores (a load per table row would be a dependent round trip each)
     {
@@ -882,12 +888,12 @@ __global__ __launch_bounds__(256) void hs_k_stitch(HsStitchArgs a) {
       const int nD = f < g ? 3 * 512 : 512 + 4096;   // f < g: [kind][x][64]; f == g: Dx [h][64] | Dq [t1][t2][64]
       const int nOct = f < g ? 256 : 16 * 128;       // [slot][128]
       const int total = nAdj + nD + nOct;
-      constexpr int SU = 32;
+      constexpr int SU = (512 * 4 + 4608 + 2048 + ST_NT - 1) / ST_NT;
       double v[SU];
       int dst[SU];
 #pragma unroll
       for (int u = 0; u < SU; u++) {
-        const int q = tid + 256 * u;
+        const int q = tid + ST_NT * u;
         const double* src = a.adHost;
         int d = -1;
         if (q < nAdj) {  // aHf | aTf | aHg | aTg
@@ -949,13 +955,13 @@ __global__ __launch_bounds__(256) void hs_k_stitch(HsStitchArgs a) {
     }
     __syncthreads();
     HS_TRACE(a, 1);
-    double* sw = scr + wv * 128;
+    double* sw = scr + wv * 64;
     if (f < g) {
       if (wv == 0) decodeA88(A8, oc);
       if (wv == 1) decodeA88(A8 + 64, oc + 128);
       __syncthreads();
       // terms: tS[h] for every host h (the host f / g terms in their host slot), tA[0] and tA[1]
-      for (int h = wv; h < nF; h += 4) {
+      for (int h = wv; h < nF; h += ST_NW) {
         double v;
         if (h != f && h != g) {
           v = sandwich8(aTf + h * 64, Dx + h * 64, aTg + h * 64, sw, lane);  // adT[h,f] D_h(f,g) adT[h,g]^T
@@ -988,8 +994,8 @@ __global__ __launch_bounds__(256) void hs_k_stitch(HsStitchArgs a) {
         }
         tS[h * 64 + lane] = v;
       }
-      if (wv == 2) tA[lane] = sandwich8(aHf + g * 64, A8, aTg + f * 64, sw, lane);       // adH[f,g] A adT[f,g]^T
-      if (wv == 3) tA[64 + lane] = sandwich8(aHg + f * 64, A8 + 64, aTf + g * 64, sw, lane);  // (g,f) pair, transposed below
+      if (wv == ST_NW - 2) tA[lane] = sandwich8(aHf + g * 64, A8, aTg + f * 64, sw, lane);       // adH[f,g] A adT[f,g]^T
+      if (wv == ST_NW - 1) tA[64 + lane] = sandwich8(aHg + f * 64, A8 + 64, aTf + g * 64, sw, lane);  // (g,f) pair, transposed below
       __syncthreads();
       HS_TRACE(a, 2);
       if (tid < 64) {
@@ -999,14 +1005,14 @@ __global__ __launch_bounds__(256) void hs_k_stitch(HsStitchArgs a) {
         put(4 + 8 * f + r, 4 + 8 * g + c, ha, hs, false);
       }
     } else {
-      for (int x = wv; x < 2 * nF; x += 4) {
+      for (int x = wv; x < 2 * nF; x += ST_NW) {
         const int t = x % nF, oi = x < nF ? t : 8 + t;  // octet slots: (f, t) at t, (h, f) at 8 + h
         if (t != f) decodeA88(A8 + oi * 64, oc + oi * 128);
       }
       __syncthreads();
       // Schur terms: tS[h] = adT[h,f] D_h(f,f) adT[h,f]^T (h != f), tS[8 + t1] = adH[f,t1] sum_t2 D_f(t1,t2) adH[f,t2]^T
       // top terms: tA[t] host pairs (f, t), tA[8 + h] target pairs (h, f)
-      for (int x = wv; x < 4 * nF; x += 4) {
+      for (int x = wv; x < 4 * nF; x += ST_NW) {
         const int y = x % nF, kind = x / nF;
         if (y == f) continue;
         if (kind == 0) {
@@ -1062,12 +1068,12 @@ __global__ __launch_bounds__(256) void hs_k_stitch(HsStitchArgs a) {
     {  // flat load table, slots m < 16 (m < 8: pair (f, m), m >= 8: pair (m - 8, f)): adjoints [m][64] | octets
        // [m][128] | accE / accEB [m][40], one batch, power-of-two strides
       constexpr int nAdj = 16 * 64, nOct = 16 * 128, total = nAdj + nOct + 16 * 64;
-      constexpr int SU = 20;
+      constexpr int SU = (total + ST_NT - 1) / ST_NT;
       double v[SU];
       int dst[SU];
 #pragma unroll
       for (int u = 0; u < SU; u++) {
-        const int q = tid + 256 * u;
+        const int q = tid + ST_NT * u;
         const double* src = a.adHost;
         int d = -1;
         if (q < nAdj) {
@@ -1184,7 +1190,6 @@ __global__ __launch_bounds__(256) void hs_k_stitch(HsStitchArgs a) {
 // =====================================================================================================
 namespace {
 constexpr int SOLVE_NT = HS_SOLVE_NT;  // 4 waves, one per SIMD: one lower-triangle 4x4 tile per lane in the LDLT
-constexpr int SOLVE_NU = (HS_MAXDIM * HS_MAXDIM + SOLVE_NT - 1) / SOLVE_NT;  // matrix entries per thread
 
 __device__ __forceinline__ double readlane_f64(double v, int lane) {
   const long long b = __double_as_longlong(v);
@@ -1439,16 +1444,13 @@ __device__ __forceinline__ void ldlt_solve_blocked(const double* M, double* LT, 
 }
 
 __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
-  __shared__ double A[HS_MAXDIM * HS_MAXDIM];  // raw HA, then the scaled system, then LDLT scratch
-  __shared__ double B[HS_MAXDIM * (HS_MAXDIM + 1)];  // raw HSC, then the permuted system, then L
+  __shared__ double A[HS_MAXDIM * HS_MAXDIM];  // the scaled system S H S (row-major, stride n)
+  __shared__ double B[26 * HS_MAXDIM];  // LDLT scratch
   __shared__ double LT[HS_MAXDIM * (HS_MAXDIM + 1)];  // L^T of the factorization (zeroed at entry)
   __shared__ double Nf[2 * HS_MAXDIM * HS_NNS];  // nullspace factors N | Npi (prefetched at entry)
   __shared__ double tk[2 * HS_NNS];
-  __shared__ double bf[HS_MAXDIM], Sv[HS_MAXDIM], xs[HS_MAXDIM], yv[HS_MAXDIM], px[HS_MAXDIM], dl[HS_MAXDIM];
-  __shared__ double dgs[HS_MAXDIM];  // |diagonal| of the scaled system (pivot keys)
+  __shared__ double Sv[HS_MAXDIM], xs[HS_MAXDIM], yv[HS_MAXDIM];
   __shared__ float xF[HS_MAXDIM];
-  __shared__ double dgr[HS_MAXDIM];  // raw diagonal of the assembled system
-  __shared__ int pos[HS_MAXDIM], rk[HS_MAXDIM];
   __shared__ int s_it;
   // the window state lives in LDS for the whole kernel: every field is touched by dependent scalar code
   // (steps, SE3 updates, precalc), which would otherwise pay a global-memory round trip per access
@@ -1466,7 +1468,6 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
   constexpr int NF_NU = (2 * HS_MAXDIM * HS_NNS + SOLVE_NT - 1) / SOLVE_NT;
   const bool solve = (a.flags & HS_SOLVE) != 0;
   const int nF = a.nF, n = 4 + 8 * nF, nn = n * n;
-  const unsigned inv_n = (unsigned)((0x100000000ull + n - 1) / n);  // idx / n == umulhi(idx, inv_n) for idx < n*n
   uint2 stw[ST_NU];
   {
     const uint2* gs = reinterpret_cast<const uint2*>(a.st);
@@ -1499,15 +1500,18 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     qr[u] = rr;
     qc[u] = cc;
   }
-  double gs[NUQ], nfv[NF_NU];
-  double bM_q = 0.0;
+  double gs[NUQ], hmq[NUQ], nfv[NF_NU];
   const double sysE0 = a.sysE[0], sysE1 = a.sysE[1], sysE2 = a.sysE[2];  // energy, sum |idepth|, #points
   if (solve) {
+    // HM (the marginalization prior) entries at the same places, bM for the b entries; one batch with the rest
+    const double* hmp = a.HM ? a.HM : a.sys;
 #pragma unroll
-    for (int u = 0; u < NUQ; u++) gs[u] = a.sys[max(qaddr[u], 0)];
+    for (int u = 0; u < NUQ; u++) {
+      gs[u] = a.sys[max(qaddr[u], 0)];
+      hmq[u] = qr[u] == -2 ? a.bM[qc[u]] : hmp[qr[u] >= 0 ? qaddr[u] : 0];
+    }
 #pragma unroll
     for (int u = 0; u < NF_NU; u++) nfv[u] = a.Nproj[min(tid + u * SOLVE_NT, 2 * n * HS_NNS - 1)];
-    if (tid < n) bM_q = a.bM[tid];
   }
   {
     uint2* ls = reinterpret_cast<uint2*>(st_raw);
@@ -1529,140 +1533,63 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
       a.energy_log[st->log_count] = sysE0;
       st->log_count = st->log_count + 1;
     }
+    // HFinal = (HL + HM + HA) diag (1+lambda) - HSC / (1+lambda) and b = (bL + (bM + HM delta)) + (bA - bSC)
+    // (Src/EnergyFunctional.cpp:728-764): the system vector carries HA - sc HSC with the diagonal
+    // HA (1+lambda) - sc HSC and bA - bSC (hs_k_stitch); the priors HL / bL (the frames' prior and the calib prior,
+    // Src/AccumulatedTopHessian.cpp:269-279) and the marginalization prior HM / bM are added here, each entry by
+    // the thread that loaded it.  The owner of a diagonal entry also forms the scaling S = 1 / sqrt(diag + 10)
+    // (:799-801).
+    const double lam1 = 1 + lambda;
+    auto delta = [&](int q) -> double {  // the reference's prior deltas: calib value - value_zero (as float), frame delta
+      return q < 4 ? (double)(float)st->calib.value_minus_value_zero[q] : st->frames[(q - 4) >> 3].delta[(q - 4) & 7];
+    };
+    auto prior = [&](int q) -> double {
+      return q < 4 ? a.initialCalibHessian : st->frames[(q - 4) >> 3].prior[(q - 4) & 7];
+    };
+    double v[NUQ];
 #pragma unroll
     for (int u = 0; u < NUQ; u++) {
-      // the summed upper triangle -> B at the padded row stride n + 1, mirrored; b -> yv
-      if (qr[u] >= 0) {
-        B[qr[u] * (n + 1) + qc[u]] = gs[u];
-        B[qc[u] * (n + 1) + qr[u]] = gs[u];
-      } else if (qr[u] == -2) {
-        yv[qc[u]] = gs[u];
-      }
-    }
-    if (tid < n) {
-      const int q = tid;
-      dl[q] = q < 4 ? (double)(float)st->calib.value_minus_value_zero[q] : st->frames[(q - 4) / 8].delta[(q - 4) % 8];
-      double bl, pr;
-      if (q < 4) {
-        pr = a.initialCalibHessian;
-        bl = a.initialCalibHessian * dl[q];
+      const int r = qr[u], c = qc[u];
+      const double hm = a.HM ? hmq[u] : 0.0;
+      if (r >= 0) {
+        v[u] = r == c ? gs[u] + (prior(r) + hm) * lam1 : gs[u] + hm;
+        if (r == c) Sv[r] = 1.0 / sqrt(v[u] + 10);
+      } else if (r == -2) {  // b entry c
+        const double bl = c < 4 ? a.initialCalibHessian * delta(c)
+                                : st->frames[(c - 4) >> 3].prior[(c - 4) & 7] * st->frames[(c - 4) >> 3].delta_prior[(c - 4) & 7];
+        double hmd = 0.0;
+        if (a.HM)
+          for (int k = 0; k < n; k++) hmd += a.HM[c * n + k] * delta(k);
+        v[u] = (bl + (hmq[u] + hmd)) + gs[u];
       } else {
-        const hs::FrameH& f = st->frames[(q - 4) / 8];
-        pr = f.prior[(q - 4) % 8];
-        bl = f.prior[(q - 4) % 8] * f.delta_prior[(q - 4) % 8];
+        v[u] = 0.0;
       }
-      px[q] = pr;  // HL diagonal (priors); staging only: these arrays are reused below
-      xs[q] = bl;
     }
+    for (int idx = tid; idx < HS_MAXDIM * (HS_MAXDIM + 1); idx += nt) LT[idx] = 0.0;  // L^T: zero on entry
     __syncthreads();
     HS_TRACE(a, 7);
-    // HFinal = (HL + HM + HA) diag (1+lambda) - HSC / (1+lambda): the slots carry HA - sc HSC with the diagonal
-    // HA (1+lambda) - sc HSC (hs_k_reduce's stitch); the priors HL (diagonal) and the marginalization prior HM
-    // are added here
-    const double lam1 = 1 + lambda;
-    double v[SOLVE_NU];
-    // HM is usually absent: two instances of the loop, chosen by one uniform branch, so the common one
-    // carries no HM loads
-    auto assemble = [&](auto withHM) {
+    // the scaled system S H S (mirrored from the upper triangle) and S b
 #pragma unroll
-      for (int u = 0; u < SOLVE_NU; u++) {
-        const int ix = min(tid + u * nt, nn - 1), r = (int)__umulhi((unsigned)ix, inv_n), c = ix - r * n;
-        const double g = B[r * (n + 1) + c];
-        const double hm = decltype(withHM)::value ? a.HM[r * n + c] : 0.0;
-        v[u] = r == c ? g + (px[r] + hm) * lam1 : g + hm;
-      }
-    };
-    if (a.HM) assemble(std::integral_constant<bool, true>{});
-    else assemble(std::integral_constant<bool, false>{});
-    if (tid < n) {
-      const int q = tid;
-      double hmd = 0.0;
-      if (a.HM)
-        for (int c = 0; c < n; c++) hmd += a.HM[q * n + c] * dl[c];
-      // (bL + (bM + HM delta)) + (bA - bSC)
-      bf[q] = (xs[q] + (bM_q + hmd)) + yv[q];
-    }
-    // the diagonal of the assembled system (held in registers by its owners) is staged for the scaling
-#pragma unroll
-    for (int u = 0; u < SOLVE_NU; u++) {
-      const int ix = tid + u * nt, r = (int)__umulhi((unsigned)ix, inv_n), c = ix - r * n;
-      if (ix < nn && r == c) dgr[r] = v[u];
-    }
-    if (tid < HS_MAXDIM) rk[tid] = 0;
-    __syncthreads();
-    HS_TRACE(a, 8);
-    for (int idx = tid; idx < HS_MAXDIM * (HS_MAXDIM + 1); idx += nt) LT[idx] = 0.0;  // L^T: zero on entry
-    // scaling S = 1/sqrt(diag + 10); the pivot keys |S H S|_qq in the scaling's own operation order
-    if (tid < n) {
-      const double hqq = dgr[tid];
-      const double sq = 1.0 / sqrt(hqq + 10);
-      Sv[tid] = sq;
-      dgs[tid] = fabs(sq * hqq * sq);
-      bf[tid] = sq * bf[tid];
-    }
-    __syncthreads();
-    HS_TRACE(a, 9);
-    // the scaled system S H S, straight from the registers (no LDS round trip of the raw system)
-#pragma unroll
-    for (int u = 0; u < SOLVE_NU; u++) {  // all reads first (unconditional), then the predicated stores
-      const int ix = min(tid + u * nt, nn - 1), r = (int)__umulhi((unsigned)ix, inv_n), c = ix - r * n;
-      v[u] = Sv[r] * v[u] * Sv[c];
-    }
-#pragma unroll
-    for (int u = 0; u < SOLVE_NU; u++)
-      if (tid + u * nt < nn) A[tid + u * nt] = v[u];
-    HS_TRACE(a, 10);
-    // Pivot order: descending |diagonal| of the scaled system, Eigen's LDLT rule (left-looking: the largest
-    // remaining |original diagonal| is the next pivot).  Exact ties are broken by the original index; Eigen
-    // breaks them by the current position after its own swaps, which permutes tied rows only: x differs by
-    // rounding, far inside the tolerance on x (the LDLT is parity-unpinned).  Ranks are counted
-    // by all four waves (wave w compares against keys 17w .. 17w + 16) and combined with LDS atomics.
-    {
-      const int ln = tid & 63, w4 = __builtin_amdgcn_readfirstlane(tid >> 6);
-      const int p0 = w4 * (HS_MAXDIM / 4), p1 = min(n, p0 + HS_MAXDIM / 4);
-      double wk[HS_MAXDIM / 4];  // this wave's 17 keys: uniform LDS reads, all issued before any compare
-#pragma unroll
-      for (int q = 0; q < HS_MAXDIM / 4; q++) wk[q] = dgs[min(p0 + q, n - 1)];
-#pragma unroll
-      for (int half = 0; half < 2; half++) {
-        const int e = ln + 64 * half;
-        const double w0 = dgs[min(e, n - 1)];
-        int cnt_ = 0;
-#pragma unroll
-        for (int q = 0; q < HS_MAXDIM / 4; q++) {  // branch-free (& / |, no short-circuit control flow)
-          const int pp = p0 + q;
-          cnt_ += (int)((pp < p1) & ((wk[q] > w0) | ((wk[q] == w0) & (pp < e))));
-        }
-        if (e < n) atomicAdd(&rk[e], cnt_);
+    for (int u = 0; u < NUQ; u++) {
+      const int r = qr[u], c = qc[u];
+      if (r >= 0) {
+        const double w = Sv[r] * v[u] * Sv[c];
+        A[r * n + c] = w;
+        A[c * n + r] = w;
+      } else if (r == -2) {
+        yv[c] = Sv[c] * v[u];
       }
     }
-    HS_TRACE(a, 11);
-    __syncthreads();
-    if (tid < n) pos[rk[tid]] = tid;
-    __syncthreads();
-    HS_TRACE(a, 1);
-    // the permuted system P S H S P^T and right-hand side for the factorization
-    {  // branch-free gather: all index and value reads first (clamped), then the predicated stores
-      int pr_[SOLVE_NU], pc_[SOLVE_NU];
-#pragma unroll
-      for (int u = 0; u < SOLVE_NU; u++) {
-        const int ix = min(tid + u * nt, nn - 1), r = (int)__umulhi((unsigned)ix, inv_n), c = ix - r * n;
-        pr_[u] = pos[r];
-        pc_[u] = pos[c];
-      }
-#pragma unroll
-      for (int u = 0; u < SOLVE_NU; u++) v[u] = A[pr_[u] * n + pc_[u]];
-#pragma unroll
-      for (int u = 0; u < SOLVE_NU; u++)
-        if (tid + u * nt < nn) B[tid + u * nt] = v[u];
-    }
-    if (tid < n) yv[tid] = bf[pos[tid]];
     __syncthreads();
     HS_TRACE(a, 2);
-    ldlt_solve_blocked(B, LT, A, yv, n, tid, a.trace);
+    // scaled LDLT without pivoting: the damped system is symmetric positive definite, for which the
+    // factorization is backward stable without pivoting; Eigen's LDLT (Src/EnergyFunctional.cpp:801) pivots on
+    // the diagonal, which changes x by rounding only (the LDLT is parity-unpinned; tests bound x by
+    // the reference's own 1- vs 8-thread spread)
+    ldlt_solve_blocked(A, LT, B, yv, n, tid, a.trace);
     __syncthreads();
     HS_TRACE(a, 3);
-    if (tid < n) xs[pos[tid]] = Sv[pos[tid]] * yv[tid];
+    if (tid < n) xs[tid] = Sv[tid] * yv[tid];
     __syncthreads();
     HS_TRACE(a, 4);
     // the fp32 adjoints for xAd: requested here so their latency overlaps orthogonalize (holding them in
