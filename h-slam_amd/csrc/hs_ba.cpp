@@ -293,7 +293,7 @@ static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = fals
   st.trace = c->d_tr_st;
   st.red = a;
   st.red.skip_threshold = (skip_threshold || readback) ? 1 : 0;
-  hipLaunchKernelGGL(hs_k_stitch, dim3(c->nF * (c->nF + 1) / 2 + c->nF + 2), dim3(256), 0, c->stream, st);
+  hipLaunchKernelGGL(hs_k_stitch, dim3(c->nF * (c->nF + 1) / 2 + c->nF + 2), dim3(HS_STITCH_NT), 0, c->stream, st);
   HS_HIP(hipGetLastError());
   if (sep) c->sepValid = true;
   if (c->comm && !readback)
@@ -1203,7 +1203,7 @@ extern "C" int hs_debug_stitch(int nF, int exact, const double* hostsum, const d
   st.lambda1 = 1 + 1e-5;
   st.sc = 1.0f / (1 + 1e-5);
   st.red.skip_threshold = 1;
-  hipLaunchKernelGGL(hs_k_stitch, dim3(nF * (nF + 1) / 2 + nF + 2), dim3(256), 0, 0, st);
+  hipLaunchKernelGGL(hs_k_stitch, dim3(nF * (nF + 1) / 2 + nF + 2), dim3(HS_STITCH_NT), 0, 0, st);
   HS_HIP(hipGetLastError());
   HS_HIP(hipDeviceSynchronize());
   HS_HIP(hipMemcpy(out, dout, sizeof(double) * SL, hipMemcpyDeviceToHost));

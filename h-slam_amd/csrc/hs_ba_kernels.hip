@@ -774,7 +774,7 @@ __device__ __forceinline__ double sandwich8(const double* L, const double* M, co
   return v;
 }
 
-constexpr int ST_NT = 1024, ST_NW = ST_NT / 64;  // stitch block: 16 waves, one 8x8 term per wave at a time
+constexpr int ST_NT = HS_STITCH_NT, ST_NW = ST_NT / 64;  // stitch block: 16 waves, one 8x8 term per wave at a time
 constexpr int ST_LDS = 12288 + ST_NW * 64;  // doubles of the stitch block's LDS (the f == g frame block)
 }  // namespace
 

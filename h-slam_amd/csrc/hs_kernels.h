@@ -7,7 +7,8 @@
 #include "hs_host_math.h"
 #include "hs_layout.h"
 
-constexpr int HS_SOLVE_NT = 256;  // hs_k_solve workgroup size
+constexpr int HS_SOLVE_NT = 256;   // hs_k_solve workgroup size
+constexpr int HS_STITCH_NT = 1024; // hs_k_stitch workgroup size
 constexpr int HS_NNS = 7;         // gauge nullspaces: 6 pose + 1 scale (System::getNullspaces)
 
 // Window state owned by the device between GN iterations (updated by hs_k_solve).
