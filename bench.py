@@ -30,11 +30,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "h-slam_amd"))
 
 METRIC = "point-residuals/sec in windowed photometric BA (8 KF × 2k pts), 1→8 GPU"
-BYTES_PER_PRES = 448      # algorithmic bytes per point-residual (fused K1-K5)
+BYTES_PER_PRES = 448      # algorithmic bytes per point-residual (fused K1-K5: hs_k_lin accumulates in
+                          # registers, no per-residual Jacobian record leaves the kernel)
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
-def pmc_traffic(points: int, kernel: str = "hs_k_linearize"):
+def pmc_traffic(points: int, kernel: str = "hs_k_lin"):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/*_pmc_traffic.json,
     made by tools/pmc.sh + tools/pmc_summary.py: separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this
     bench at the same --points).  None when no pass at this size has been committed."""
@@ -511,7 +512,7 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "hs_k_linearize",
+            "kernel": "hs_k_lin",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -522,7 +523,8 @@ def main():
             "units_per_launch": shard.n_res,
             "avg_launch_ms": lin_ms,
             "avg_launch_ms_in_loop_events": lin_loop_ms,
-            "timing": "HIP events on the context stream around back-to-back hs_k_linearize launches",
+            "timing": "HIP events on the context stream around back-to-back hs_k_lin launches (fused linearize + "
+                      "applyRes + top / Schur accumulation into block partials)",
         },
         "phase_ms_per_step": {  # per-phase split: --phase-events 2 (1 times the linearize kernel only)
             "solve_step_kernel": tim["solve_ms"] / nt if args.phase_events >= 2 else None,
