@@ -1450,6 +1450,7 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
   __shared__ double Nf[2 * HS_MAXDIM * HS_NNS];  // nullspace factors N | Npi (prefetched at entry)
   __shared__ double tk[2 * HS_NNS];
   __shared__ double Sv[HS_MAXDIM], xs[HS_MAXDIM], yv[HS_MAXDIM];
+  __shared__ double dgv[2 * HS_MAXDIM], dgm[2 * HS_MAXDIM];  // raw diagonal | b, and HM's diagonal | bM
   __shared__ float xF[HS_MAXDIM];
   __shared__ int s_it;
   // the window state lives in LDS for the whole kernel: every field is touched by dependent scalar code
@@ -1519,12 +1520,26 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     for (int u = 0; u < ST_NU; u++)
       if (tid + u * SOLVE_NT < ST_WORDS) ls[tid + u * SOLVE_NT] = stw[u];
   }
+  if (solve) {  // the raw diagonal (+ HM's) and b (+ bM) entries to LDS for the per-row scaling below
+#pragma unroll
+    for (int u = 0; u < NUQ; u++) {
+      const double hm = a.HM ? hmq[u] : 0.0;
+      if (qr[u] >= 0 && qr[u] == qc[u]) {
+        dgv[qc[u]] = gs[u];
+        dgm[qc[u]] = hm;
+      } else if (qr[u] == -2) {
+        dgv[HS_MAXDIM + qc[u]] = gs[u];
+        dgm[HS_MAXDIM + qc[u]] = hmq[u];
+      }
+    }
+  }
   if (solve) {
 #pragma unroll
     for (int u = 0; u < NF_NU; u++)
       if (tid + u * SOLVE_NT < 2 * n * HS_NNS) Nf[tid + u * SOLVE_NT] = nfv[u];
   }
   __syncthreads();
+  HS_TRACE(a, 8);
   if (tid == 0) s_it = a.iteration >= 0 ? a.iteration : st->iteration;
   const double lambda = 1e-5;  // SOLVER_FIX_LAMBDA
 
@@ -1543,41 +1558,32 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     auto delta = [&](int q) -> double {  // the reference's prior deltas: calib value - value_zero (as float), frame delta
       return q < 4 ? (double)(float)st->calib.value_minus_value_zero[q] : st->frames[(q - 4) >> 3].delta[(q - 4) & 7];
     };
-    auto prior = [&](int q) -> double {
-      return q < 4 ? a.initialCalibHessian : st->frames[(q - 4) >> 3].prior[(q - 4) & 7];
-    };
-    double v[NUQ];
-#pragma unroll
-    for (int u = 0; u < NUQ; u++) {
-      const int r = qr[u], c = qc[u];
-      const double hm = a.HM ? hmq[u] : 0.0;
-      if (r >= 0) {
-        v[u] = r == c ? gs[u] + (prior(r) + hm) * lam1 : gs[u] + hm;
-        if (r == c) Sv[r] = 1.0 / sqrt(v[u] + 10);
-      } else if (r == -2) {  // b entry c
-        const double bl = c < 4 ? a.initialCalibHessian * delta(c)
-                                : st->frames[(c - 4) >> 3].prior[(c - 4) & 7] * st->frames[(c - 4) >> 3].delta_prior[(c - 4) & 7];
-        double hmd = 0.0;
-        if (a.HM)
-          for (int k = 0; k < n; k++) hmd += a.HM[c * n + k] * delta(k);
-        v[u] = (bl + (hmq[u] + hmd)) + gs[u];
-      } else {
-        v[u] = 0.0;
-      }
+    // per row q (one thread each): the assembled diagonal, the scaling and the scaled right-hand side
+    if (tid < n) {
+      const int q = tid;
+      const double pr = q < 4 ? a.initialCalibHessian : st->frames[(q - 4) >> 3].prior[(q - 4) & 7];
+      const double hv = dgv[q] + (pr + dgm[q]) * lam1;
+      const double sq = 1.0 / sqrt(hv + 10);
+      Sv[q] = sq;
+      A[q * n + q] = sq * hv * sq;
+      const double bl = q < 4 ? a.initialCalibHessian * delta(q)
+                              : pr * st->frames[(q - 4) >> 3].delta_prior[(q - 4) & 7];
+      double hmd = 0.0;
+      if (a.HM)
+        for (int k = 0; k < n; k++) hmd += a.HM[q * n + k] * delta(k);
+      yv[q] = sq * ((bl + (dgm[HS_MAXDIM + q] + hmd)) + dgv[HS_MAXDIM + q]);
     }
     for (int idx = tid; idx < HS_MAXDIM * (HS_MAXDIM + 1); idx += nt) LT[idx] = 0.0;  // L^T: zero on entry
     __syncthreads();
     HS_TRACE(a, 7);
-    // the scaled system S H S (mirrored from the upper triangle) and S b
+    // the scaled off-diagonal entries S H S, mirrored from the upper triangle
 #pragma unroll
     for (int u = 0; u < NUQ; u++) {
       const int r = qr[u], c = qc[u];
-      if (r >= 0) {
-        const double w = Sv[r] * v[u] * Sv[c];
+      if (r >= 0 && r != c) {
+        const double w = Sv[r] * (gs[u] + (a.HM ? hmq[u] : 0.0)) * Sv[c];
         A[r * n + c] = w;
         A[c * n + r] = w;
-      } else if (r == -2) {
-        yv[c] = Sv[c] * v[u];
       }
     }
     __syncthreads();
@@ -1695,6 +1701,7 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
       const int hh = pr / nF, tt = pr % nF;
       a.pre[pr] = hs::make_precalc(st->frames[hh], st->frames[tt], st->calib);
     }
+    if (tid == 0) HS_TRACE(a, 10);
     if (tid == 128) {
       float sumA = 0, sumB = 0, sumT = 0, sumR = 0;
       for (int f = 0; f < nF; f++) {
