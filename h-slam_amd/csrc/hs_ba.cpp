@@ -105,6 +105,12 @@ struct hs_ctx {
   uint8_t* d_p_actmask = nullptr;
   float *d_p_HdiF = nullptr, *d_p_bdSumF = nullptr, *d_p_Hcd = nullptr, *d_p_JpJdF = nullptr;
   float* d_p_step = nullptr;
+  // HdiF ping-pong: a linearization reads the previous one's HdiF (fused step) from d_p_HdiF and writes its own into
+  // d_p_HdiF_alt, then the two swap; hdif_solved = the buffer the last point step read (the last solve's SC prelude)
+  float* d_p_HdiF_alt = nullptr;
+  const float* hdif_solved = nullptr;
+  float* d_fix_relBL = nullptr;      // [nP] maxRelBaseline in / out of hs_ba_fix_linearization
+  int* d_fix_nGood = nullptr;        // [nP] numGoodResiduals in / out
   float* d_part = nullptr;       // [nblk][ne][64] block partials of hs_k_lin
   double* d_part_e = nullptr;    // [nblk][4] block energies
   double* d_hostsum = nullptr;   // [nF][ne][64] per-host sums (hs_k_reduce)
@@ -151,7 +157,7 @@ static void free_window(hs_ctx* c) {
                   c->d_p_step, c->d_part, c->d_part_e, c->d_hostsum, c->d_sys, c->d_sep,
                   c->d_adHost, c->d_adTarget, c->d_adHostF, c->d_adTargetF, c->d_HM, c->d_bM, c->d_Nproj, c->d_xAd,
                   c->d_x, c->d_elog, c->d_cand, c->d_tr_lin, c->d_tr_acc, c->d_tr_solve, c->d_tr_st,
-                  c->d_marg, c->d_adHTdelta};
+                  c->d_marg, c->d_adHTdelta, c->d_p_HdiF_alt, c->d_fix_relBL, c->d_fix_nGood};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   c->d_state = nullptr; c->d_pre = nullptr; c->d_frameTH = nullptr;
@@ -170,6 +176,9 @@ static void free_window(hs_ctx* c) {
   c->d_tr_lin = c->d_tr_acc = c->d_tr_solve = c->d_tr_st = nullptr;
   c->d_marg = nullptr;
   c->d_adHTdelta = nullptr;
+  c->d_p_HdiF_alt = c->d_fix_relBL = nullptr;
+  c->hdif_solved = nullptr;
+  c->d_fix_nGood = nullptr;
   c->nF = c->nP = c->nR = 0;
   c->haveSystem = false;
   c->sepValid = false;
@@ -209,7 +218,7 @@ static int fetch_state(hs_ctx* c) {
 // ---------------------------------------------------------------- launches (asynchronous)
 static size_t lin_lds(const hs_ctx* c) { return (size_t)4 * c->ne * 64 * sizeof(float) + 12 * sizeof(double); }
 
-static int launch_linearize(hs_ctx* c, int fuse, bool marg = false, bool accumulate = true) {
+static int launch_linearize(hs_ctx* c, int fuse, bool marg = false, bool accumulate = true, bool fix = false) {
   HsLinArgs a;
   std::memset(&a, 0, sizeof(a));
   if (marg) {  // hs_ba_marginalize_points: flags, adHTdeltaF and cDeltaF uploaded by the caller
@@ -245,16 +254,20 @@ static int launch_linearize(hs_ctx* c, int fuse, bool marg = false, bool accumul
   a.res_of_slot = c->d_res_of_slot; a.res_order = c->d_res_order;
   a.r_state = c->d_r_state; a.r_active = c->d_r_active; a.r_energy = c->d_r_energy;
   a.r_newEnergy = c->d_r_newEnergy; a.r_ewo = c->d_r_ewo; a.r_center = c->d_r_center;
-  a.p_actmask = c->d_p_actmask; a.p_HdiF = c->d_p_HdiF; a.p_bdSumF = c->d_p_bdSumF; a.p_Hcd = c->d_p_Hcd;
+  a.p_actmask = c->d_p_actmask; a.p_HdiF = c->d_p_HdiF_alt; a.p_HdiF_prev = c->d_p_HdiF;
+  a.p_bdSumF = c->d_p_bdSumF; a.p_Hcd = c->d_p_Hcd;
   a.p_JpJdF = c->d_p_JpJdF; a.p_step = c->d_p_step;
+  a.fix_relBL = c->d_fix_relBL; a.fix_nGood = c->d_fix_nGood;
   a.newest_cand = c->d_cand + (size_t)c->rank * c->cand_stride;
   a.part = c->d_part; a.part_e = c->d_part_e;
   a.trace = c->d_tr_lin;
   if (c->nblk > 0) {
-    if (c->exact) hipLaunchKernelGGL(hs_k_lin_exact, dim3(c->nblk), dim3(256), lin_lds(c), c->stream, a);
-    else hipLaunchKernelGGL(hs_k_lin, dim3(c->nblk), dim3(256), lin_lds(c), c->stream, a);
+    auto k = c->exact ? (fix ? hs_k_lin_exact_fix : hs_k_lin_exact) : (fix ? hs_k_lin_fix : hs_k_lin);
+    hipLaunchKernelGGL(k, dim3(c->nblk), dim3(256), lin_lds(c), c->stream, a);
   }
   HS_HIP(hipGetLastError());
+  std::swap(c->d_p_HdiF, c->d_p_HdiF_alt);
+  if (fuse) c->hdif_solved = c->d_p_HdiF_alt;
   if (accumulate) c->sepValid = false;
   return HS_OK;
 }
@@ -700,7 +713,9 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
   HS_TRY(dalloc(&c->d_r_center, (size_t)P8 * 3));
   HS_TRY(dalloc(&c->d_p_actmask, nP)); HS_TRY(dalloc(&c->d_p_HdiF, nP)); HS_TRY(dalloc(&c->d_p_bdSumF, nP));
   HS_TRY(dalloc(&c->d_p_Hcd, (size_t)nP * 4)); HS_TRY(dalloc(&c->d_p_JpJdF, P8 * 8));
-  HS_TRY(dalloc(&c->d_p_step, nP));
+  HS_TRY(dalloc(&c->d_p_step, nP)); HS_TRY(dalloc(&c->d_p_HdiF_alt, nP));
+  c->hdif_solved = c->d_p_HdiF;
+  HS_TRY(dalloc(&c->d_fix_relBL, nP)); HS_TRY(dalloc(&c->d_fix_nGood, nP));
   HS_TRY(dalloc(&c->d_part, (size_t)std::max(c->nblk, 1) * c->ne * 64));
   HS_TRY(dalloc(&c->d_part_e, (size_t)std::max(c->nblk, 1) * 4));
   HS_TRY(dalloc(&c->d_hostsum, (size_t)nF * c->ne * 64));
@@ -785,6 +800,7 @@ int hs_ba_solve_system(hs_ctx* c, int iteration, double* x_out) {
   ra.host = c->d_pt_host; ra.xAd = c->d_xAd; ra.actmask = c->d_p_actmask; ra.bdSumF = c->d_p_bdSumF;
   ra.HdiF = c->d_p_HdiF; ra.Hcd = c->d_p_Hcd; ra.JpJdF = c->d_p_JpJdF; ra.res_order = c->d_res_order;
   ra.idepth = c->d_idepth; ra.idepth_zero = c->d_idepth_zero; ra.step = c->d_p_step;
+  c->hdif_solved = c->d_p_HdiF;
   if (c->nP > 0) hipLaunchKernelGGL(hs_k_resub, dim3((c->nP + 255) / 256), dim3(256), 0, c->stream, ra);
   HS_HIP(hipGetLastError());
   std::vector<double> x(c->dim());
@@ -847,6 +863,87 @@ int hs_ba_iterate(hs_ctx* c, int first_iteration, int n_iters, double* energies_
   int done = 0;
   HS_TRY(gn_iterations(c, first_iteration, n_iters, false, energies_out, &done));
   c->t_wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return HS_OK;
+}
+
+// System::optimize's tail (Src/FullSystemOptimize.cpp:498-516): the newest frame's setEvalPT(PRE_worldToCam,
+// state with only a / b kept) (Include/Frame.h:213-218), setAdjointsF + setPrecalcValues (host, fp64: the same
+// code as hs_ba_set_window), then linearizeAll(true) as one hs_k_lin_fix pass (linearize + applyRes + the per-point
+// maxRelBaseline / numGoodResiduals bookkeeping) followed by the usual reduce / stitch (setNewFrameEnergyTH; the
+// stitched system is that of the fixed linearization).
+int hs_ba_fix_linearization(hs_ctx* c, double* energy_out, uint8_t* drop_out, float* maxRelBaseline,
+                            int* numGoodResiduals, float* HdiF_out) {
+  if (!c || c->nF == 0) return fail(HS_ERR_STATE, "no window");
+  if ((maxRelBaseline == nullptr) != (numGoodResiduals == nullptr))
+    return fail(HS_ERR_INVALID, "maxRelBaseline and numGoodResiduals go together");
+  HS_HIP(hipSetDevice(c->device));
+  const int nF = c->nF, nP = c->nP;
+  // HdiF of the last solve, before this pass relinearizes
+  if (HdiF_out && nP > 0)
+    HS_HIP(hipMemcpyAsync(HdiF_out, c->hdif_solved, sizeof(float) * nP, hipMemcpyDeviceToHost, c->stream));
+  HS_TRY(fetch_state(c));
+  HsDevState& S = *c->h_state;
+  {  // newStateZero = 0 except segment(6, 2) = the newest frame's a / b; setEvalPT(PRE_worldToCam, newStateZero)
+    hs::FrameH& f = S.frames[nF - 1];
+    double nsz[10] = {0, 0, 0, 0, 0, 0, f.state[6], f.state[7], 0, 0};
+    f.evalPT = f.PRE_worldToCam;
+    f.setState(nsz);
+    f.setStateZero(nsz);
+    f.takeData(c->P);
+  }
+  for (int h = 0; h < nF; h++)  // EnergyFunctional::setAdjointsF
+    for (int t = 0; t < nF; t++) {
+      const int idx = h + t * nF;
+      make_adjoints(S.frames[h], S.frames[t], &c->adHost[idx * 64], &c->adTarget[idx * 64]);
+      for (int i = 0; i < 64; i++) {
+        c->adHostF[idx * 64 + i] = (float)c->adHost[idx * 64 + i];
+        c->adTargetF[idx * 64 + i] = (float)c->adTarget[idx * 64 + i];
+      }
+    }
+  compute_projector(c);  // the newest frame's nullspaces moved with its evalPT
+  std::vector<HsPrecalc> pre(nF * nF);  // setPrecalcValues
+  for (int h = 0; h < nF; h++)
+    for (int t = 0; t < nF; t++) pre[h * nF + t] = make_precalc(S.frames[h], S.frames[t], S.calib);
+  const int n = c->dim();
+  HS_HIP(hipMemcpyAsync(c->d_state, c->h_state, sizeof(HsDevState), hipMemcpyHostToDevice, c->stream));
+  HS_HIP(hipMemcpyAsync(c->d_pre, pre.data(), sizeof(HsPrecalc) * nF * nF, hipMemcpyHostToDevice, c->stream));
+  HS_HIP(hipMemcpyAsync(c->d_adHost, c->adHost.data(), sizeof(double) * nF * nF * 64, hipMemcpyHostToDevice, c->stream));
+  HS_HIP(hipMemcpyAsync(c->d_adTarget, c->adTarget.data(), sizeof(double) * nF * nF * 64, hipMemcpyHostToDevice,
+                        c->stream));
+  HS_HIP(hipMemcpyAsync(c->d_adHostF, c->adHostF.data(), sizeof(float) * nF * nF * 64, hipMemcpyHostToDevice,
+                        c->stream));
+  HS_HIP(hipMemcpyAsync(c->d_adTargetF, c->adTargetF.data(), sizeof(float) * nF * nF * 64, hipMemcpyHostToDevice,
+                        c->stream));
+  HS_HIP(hipMemcpyAsync(c->d_Nproj, c->Nproj.data(), sizeof(double) * 2 * n * HS_NNS, hipMemcpyHostToDevice,
+                        c->stream));
+  if (nP > 0) {
+    if (maxRelBaseline) {
+      HS_HIP(hipMemcpyAsync(c->d_fix_relBL, maxRelBaseline, sizeof(float) * nP, hipMemcpyHostToDevice, c->stream));
+      HS_HIP(hipMemcpyAsync(c->d_fix_nGood, numGoodResiduals, sizeof(int) * nP, hipMemcpyHostToDevice, c->stream));
+    } else {
+      HS_HIP(hipMemsetAsync(c->d_fix_relBL, 0, sizeof(float) * nP, c->stream));
+      HS_HIP(hipMemsetAsync(c->d_fix_nGood, 0, sizeof(int) * nP, c->stream));
+    }
+  }
+  // linearizeAll(true): no resetOOB (OOB stays sticky from the GN loop), no point step
+  HS_TRY(launch_linearize(c, 0, false, true, true));
+  HS_TRY(launch_reduce(c, false, true));
+  c->haveSystem = true;
+  double e = 0.0;
+  HS_HIP(hipMemcpyAsync(&c->h_ctl[4], c->sysE(), sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  if (nP > 0 && maxRelBaseline) {
+    HS_HIP(hipMemcpyAsync(maxRelBaseline, c->d_fix_relBL, sizeof(float) * nP, hipMemcpyDeviceToHost, c->stream));
+    HS_HIP(hipMemcpyAsync(numGoodResiduals, c->d_fix_nGood, sizeof(int) * nP, hipMemcpyDeviceToHost, c->stream));
+  }
+  HS_HIP(hipStreamSynchronize(c->stream));
+  std::memcpy(&e, &c->h_ctl[4], sizeof(double));
+  if (energy_out) *energy_out = e;
+  if (drop_out && c->nR > 0) {  // toRemove: every residual not active after applyRes(true)
+    std::vector<uint8_t> act((size_t)nP * 8);
+    HS_HIP(hipMemcpy(act.data(), c->d_r_active, act.size(), hipMemcpyDeviceToHost));
+    for (int r = 0; r < c->nR; r++) drop_out[r] = act[(size_t)c->res_point[r] * 8 + c->res_target[r]] ? 0 : 1;
+  }
+  if (!std::isfinite(e)) return fail(HS_ERR_NONFINITE, "non-finite energy (isLost)");
   return HS_OK;
 }
 

@@ -124,6 +124,10 @@ struct LinPt {
 // AccumulatedTopHessianSSE::addPoint<0> / AccumulatedSCHessianSSE::addPoint (Src/AccumulatedTopHessian.cpp:21-141,
 // Src/AccumulatedSCHessian.cpp:10-33).  Writes the per-residual / per-point state; returns what the
 // accumulators need.  Wave-uniform p.
+// kFix: System::linearizeAll(true)'s bookkeeping (Src/FullSystemOptimize.cpp:26-50): for every residual still active
+// after applyRes the point's maxRelBaseline = max(relBS) and numGoodResiduals++ (isNew is never cleared in the
+// reference, Include/OptimizationClasses.h:98,112), in the point's residual-list order.
+template <bool kFix>
 __device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int lane, LinPt& o) {
   const int t = lane >> 3;  // target slot
   const int k = lane & 7;   // pattern pixel
@@ -173,7 +177,7 @@ __device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int 
   const unsigned fm = a.p_actmask[p];
   const float xad = a.xAd[(h * nF + tc_) * 8 + k];
   const float jpj = a.p_JpJdF[sl * 8 + k];
-  const float bds = a.p_bdSumF[p], hdi = a.p_HdiF[p];
+  const float bds = a.p_bdSumF[p], hdi = a.p_HdiF_prev[p];
   const float4 hcd = reinterpret_cast<const float4*>(a.p_Hcd)[p];
   const float4 cs4 = *reinterpret_cast<const float4*>(a.st->cstep);
   const float cs0 = cs4.x, cs1 = cs4.y, cs2 = cs4.z, cs3 = cs4.w;
@@ -453,6 +457,30 @@ __device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int 
       a.p_bdSumF[p] = bdSumF;
       reinterpret_cast<float4*>(a.p_Hcd)[p] = hc4;
     }
+    if (kFix) {
+      // relBS = 0.01 |ptp_inf.xy / ptp_inf.z - ptp.xy / ptp.z| with ptp_inf = KRKi (u, v, 1), ptp = ptp_inf + Kt
+      // idepth (:35-37; 0.01 is a double), uniform per slot
+      float q0 = pc.KRKi[0] * pu + pc.KRKi[1] * pv + pc.KRKi[2] * 1.f;
+      float q1 = pc.KRKi[3] * pu + pc.KRKi[4] * pv + pc.KRKi[5] * 1.f;
+      float q2 = pc.KRKi[6] * pu + pc.KRKi[7] * pv + pc.KRKi[8] * 1.f;
+      const float r0 = q0 + pc.Kt[0] * idep, r1 = q1 + pc.Kt[1] * idep, r2 = q2 + pc.Kt[2] * idep;
+      const float dx = q0 / q2 - r0 / r2, dy = q1 / q2 - r1 / r2;
+      const float relBS = (float)(0.01 * (double)sqrtf(dx * dx + dy * dy));
+      float mr = a.fix_relBL[p];
+      int ng = a.fix_nGood[p];
+      for (int qn = 0; qn < 8; qn++) {
+        const int tt = res_slot(qn);
+        if (tt < 0) break;
+        if (!((actBits >> (tt * 8)) & 1ull)) continue;
+        const float rb = readlane_f(relBS, tt * 8);
+        if (rb > mr) mr = rb;
+        ng++;
+      }
+      if (lane == 0) {
+        a.fix_relBL[p] = mr;
+        a.fix_nGood[p] = ng;
+      }
+    }
     o.mask = mask;
     o.HdiF = HdiF;
     o.bdSumF = bdSumF;
@@ -568,7 +596,7 @@ __device__ __forceinline__ void acc_point(LinAcc<kExact>& A, const LinPt& P, int
   A.np += 1.0;
 }
 
-template <bool kExact>
+template <bool kExact, bool kFix>
 __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
   extern __shared__ float lin_stage[];  // [4 waves][ne][64] fp32 partials, then [4][3] fp64 energies
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -592,7 +620,7 @@ __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
   if (wv < a.W) {
     for (int p = pb + wv; p < pe; p += a.W) {  // wave-uniform
       LinPt P;
-      lin_point(a, p, h, lane, P);
+      lin_point<kFix>(a, p, h, lane, P);
       if (a.accumulate) acc_point<kExact>(A, P, h, lane);
     }
   }
@@ -630,8 +658,10 @@ __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
 }
 }  // namespace
 
-__global__ __launch_bounds__(256) void hs_k_lin(HsLinArgs a) { lin_block<false>(a); }
-__global__ __launch_bounds__(256) void hs_k_lin_exact(HsLinArgs a) { lin_block<true>(a); }
+__global__ __launch_bounds__(256) void hs_k_lin(HsLinArgs a) { lin_block<false, false>(a); }
+__global__ __launch_bounds__(256) void hs_k_lin_exact(HsLinArgs a) { lin_block<true, false>(a); }
+__global__ __launch_bounds__(256) void hs_k_lin_fix(HsLinArgs a) { lin_block<false, true>(a); }
+__global__ __launch_bounds__(256) void hs_k_lin_exact_fix(HsLinArgs a) { lin_block<true, true>(a); }
 
 // =====================================================================================================
 // reduce + stitch: (host, chunk) blocks sum the host's block partials in block order; the last chunk block of a

@@ -76,11 +76,15 @@ struct HsLinArgs {
   float* r_center;             // [m][3]
   // per point outputs (slot layout)
   uint8_t* p_actmask;
-  float* p_HdiF;
+  float* p_HdiF;               // written (this linearization's SC prelude)
+  const float* p_HdiF_prev;    // read by the fused step: the previous linearization's (ping-pong with p_HdiF)
   float* p_bdSumF;
   float* p_Hcd;                // [n][4]
   float* p_JpJdF;              // [n][8][8]
   float* p_step;               // [n]
+  // linearizeAll(true) bookkeeping (hs_k_lin_fix only): maxRelBaseline / numGoodResiduals per point, in / out
+  float* fix_relBL;
+  int* fix_nGood;
   float* newest_cand;          // [n] energy of the point's residual into the newest frame, -1 = none
   // block partials: part[blk][ne][64] (fp32, waves summed in wave order), part_e[blk][4] (fp64 energy,
   // sum |idepth|, #points)
@@ -167,6 +171,8 @@ struct HsResubArgs {
 
 __global__ void hs_k_lin(HsLinArgs a);        // production partitioning
 __global__ void hs_k_lin_exact(HsLinArgs a);  // HS_ACC_EXACT: one wave per host, the reference's sums
+__global__ void hs_k_lin_fix(HsLinArgs a);        // + linearizeAll(true)'s per-point bookkeeping
+__global__ void hs_k_lin_exact_fix(HsLinArgs a);
 __global__ void hs_k_reduce(HsRedArgs a);
 __global__ void hs_k_stitch(HsStitchArgs a);
 __global__ void hs_k_solve(HsSolveArgs a);

@@ -130,6 +130,19 @@ class BAWindow:
         check(self.lib.hs_ba_iterate(self.h, first_iteration, n_iters, ptr(e)))
         return e
 
+    def fixLinearization(self, max_rel_baseline=None, num_good=None):
+        """System::optimize's tail (Src/FullSystemOptimize.cpp:498-516): newest frame setEvalPT, setAdjointsF,
+        setPrecalcValues, linearizeAll(true).  Returns dict(energy, drop[n_res], maxRelBaseline[n_points],
+        numGoodResiduals[n_points], HdiF[n_points]) (HdiF of the last solve's Schur prelude)."""
+        rb = np.zeros(self.n_points, np.float32) if max_rel_baseline is None else \
+            np.array(max_rel_baseline, np.float32)
+        ng = np.zeros(self.n_points, np.int32) if num_good is None else np.array(num_good, np.int32)
+        drop = np.zeros(self.n_res, np.uint8)
+        hdi = np.zeros(self.n_points, np.float32)
+        e = C.c_double()
+        check(self.lib.hs_ba_fix_linearization(self.h, C.byref(e), ptr(drop), ptr(rb), ptr(ng), ptr(hdi)))
+        return dict(energy=e.value, drop=drop, maxRelBaseline=rb, numGoodResiduals=ng, HdiF=hdi)
+
     # --------------------------------------------------------------- read-back
     def system(self, which):
         H = np.zeros((self.dim, self.dim))

@@ -24,6 +24,9 @@
  *   hs_ba_optimize              System::optimize GN loop (Src/FullSystemOptimize.cpp:362-494),
  *                               setting_forceAceptStep = true.
  *   hs_ba_iterate               the loop body of System::optimize (Src/FullSystemOptimize.cpp:420-494)
+ *   hs_ba_fix_linearization     System::optimize's tail: newest frame setEvalPT, setAdjointsF,
+ *                               setPrecalcValues, linearizeAll(true) (Src/FullSystemOptimize.cpp:498-516,
+ *                               19-52, 102-160)
  *   hs_ba_get_system            HA/bA (accumulateAF_MT), HL/bL (accumulateLF_MT), H_sc/b_sc (accumulateSCF_MT)
  *   hs_ba_get_* / hs_ba_set_marginal_prior   read-back of PointFrameResidual / MapPoint / FrameOptimizationData
  *                               state; EnergyFunctional::HM/bM.
@@ -73,6 +76,24 @@ int hs_ba_optimize(hs_ctx* ctx, int max_iters, int allow_break, double* energies
    iteration numbers first_iteration.. (orthogonalize from iteration 2); no early break.
    energies_out[n_iters] nullable.  This is the benchmark's "step". */
 int hs_ba_iterate(hs_ctx* ctx, int first_iteration, int n_iters, double* energies_out);
+
+/* System::optimize's tail after the GN loop (Src/FullSystemOptimize.cpp:498-516): the newest frame's
+   setEvalPT(PRE_worldToCam, state = state_zero = (0,..,0, a, b, 0, 0)) (Include/Frame.h:213-218), setAdjointsF and
+   setPrecalcValues, then linearizeAll(true) (:19-52, :102-160): every active residual is linearized and applied
+   (applyRes(true)); for each residual still active its point's maxRelBaseline = max(relBS) and
+   numGoodResiduals++ (the reference never clears PointFrameResidual::isNew, so every active residual counts);
+   setNewFrameEnergyTH.
+     energy_out        linearizeAll(true)'s energy; non-finite -> HS_ERR_NONFINITE (the reference's isLost).
+     drop_out[nR]      1 = not active after the pass: the toRemove list (the caller resets the point's
+                       lastResiduals[i].first and calls ef->dropResidual).  The new residual states
+                       (lastResiduals[i].second) and centerProjectedTo come from hs_ba_get_residuals.
+     maxRelBaseline[nP], numGoodResiduals[nP]   the points' values, updated in place (both or neither).
+     HdiF_out[nP]      HdiF of the linearization the last solve consumed (the last accumulateSCF_MT's
+                       AccumulatedSCHessianSSE::addPoint, Src/AccumulatedSCHessian.cpp:28): makeCoarseDepthL0's
+                       weights (Src/CoarseTracker.cpp:124).
+   All outputs nullable.  The context's window afterwards is the fixed one (evalPT moved, system re-stitched). */
+int hs_ba_fix_linearization(hs_ctx* ctx, double* energy_out, uint8_t* drop_out, float* maxRelBaseline,
+                            int* numGoodResiduals, float* HdiF_out);
 
 /* which: 0 = HA/bA, 1 = HL/bL (priors), 2 = H_sc/b_sc. H: dim*dim row-major, b: dim. */
 int hs_ba_get_system(hs_ctx* ctx, int which, double* H, double* b);

@@ -1256,6 +1256,43 @@ struct BA {
            sqrtf(sumT) * sumNID < 0.00005 * th;
   }
 
+  // System::optimize's tail (Src/FullSystemOptimize.cpp:498-509): the newest frame's setEvalPT(PRE_worldToCam,
+  // (0,..,0, a, b, 0, 0)) (Include/Frame.h:213-218), setAdjointsF, setPrecalcValues, then linearizeAll(true)
+  // (:19-52, :102-124): linearize + applyRes(true) per active residual; for residuals still active the point's
+  // maxRelBaseline / numGoodResiduals (isNew is never cleared in the reference); setNewFrameEnergyTH.
+  double fixLinearization(float* relBL, int* nGood, uint8_t* drop) {
+    FrameO& f = frames[nF - 1];
+    double nsz[10] = {0, 0, 0, 0, 0, 0, f.state[6], f.state[7], 0, 0};
+    f.evalPT = f.PRE_worldToCam;
+    f.setState(nsz);
+    f.setStateZero(nsz);
+    setAdjointsF();
+    setPrecalcValues();
+    double E = 0;
+    for (int k : activeResiduals) {
+      ResO& r = res[k];
+      E += linearize(r);
+      applyRes(r);
+      if (r.isActive()) {
+        const PointO& p = points[r.point];
+        const Precalc& pc = precalc[r.host * nF + r.target];
+        float pi[3], pt[3];
+        for (int i = 0; i < 3; i++) {
+          pi[i] = pc.PRE_KRKiTll[i * 3 + 0] * p.u + pc.PRE_KRKiTll[i * 3 + 1] * p.v + pc.PRE_KRKiTll[i * 3 + 2] * 1.f;
+          pt[i] = pi[i] + pc.PRE_KtTll[i] * p.idepth;
+        }
+        const float dx = pi[0] / pi[2] - pt[0] / pt[2], dy = pi[1] / pi[2] - pt[1] / pt[2];
+        const float relBS = 0.01 * std::sqrt(dx * dx + dy * dy);
+        if (relBL && relBS > relBL[r.point]) relBL[r.point] = relBS;
+        if (nGood) nGood[r.point]++;
+      } else if (drop) {
+        drop[k] = 1;
+      }
+    }
+    setNewFrameEnergyTH();
+    return E;
+  }
+
   // K loop bodies of System::optimize continuing from the current linearization
   void iterate(int it0, int K, double* energies) {
     for (int k = 0; k < K; k++) {
@@ -1388,6 +1425,12 @@ double hso_ba_linearize_all(void* h, int reset) {
   return ba->linearizeAll();
 }
 void hso_ba_apply_res(void* h) { ((BA*)h)->applyResAll(); }
+
+/* System::optimize's tail + linearizeAll(true): returns its energy; relBL / nGood [n points] updated in place,
+   drop [n residuals] set to 1 for the toRemove list (entries of other residuals untouched) */
+double hso_ba_fix_linearization(void* h, float* relBL, int* nGood, uint8_t* drop) {
+  return ((BA*)h)->fixLinearization(relBL, nGood, drop);
+}
 
 /* which: 0 = top A (mode 0), 1 = top L (mode 1 + priors), 2 = Schur complement */
 void hso_ba_accumulate(void* h, int which, double* H, double* b) {

@@ -89,6 +89,8 @@ def load(fast=False):
     lib.hso_ba_linearize_all.argtypes = [vp, C.c_int]
     lib.hso_ba_linearize_all.restype = C.c_double
     lib.hso_ba_apply_res.argtypes = [vp]
+    lib.hso_ba_fix_linearization.argtypes = [vp, vp, vp, vp]
+    lib.hso_ba_fix_linearization.restype = C.c_double
     lib.hso_ba_accumulate.argtypes = [vp, C.c_int, vp, vp]
     lib.hso_ba_solve_system.argtypes = [vp, C.c_int, vp]
     lib.hso_ba_backup_state.argtypes = [vp]
@@ -232,6 +234,15 @@ class OracleBA:
 
     def apply_res(self):
         self.lib.hso_ba_apply_res(self.h)
+
+    def fix_linearization(self, max_rel_baseline, num_good):
+        """System::optimize's tail (newest frame setEvalPT, setAdjointsF, setPrecalcValues, linearizeAll(true)).
+        Returns (energy, drop[n_res] uint8, maxRelBaseline, numGoodResiduals)."""
+        rb = np.array(max_rel_baseline, np.float32)
+        ng = np.array(num_good, np.int32)
+        drop = np.zeros(self.scene.n_res, np.uint8)
+        e = self.lib.hso_ba_fix_linearization(self.h, _p(rb), _p(ng), _p(drop))
+        return e, drop, rb, ng
 
     def accumulate(self, which):
         H = np.zeros((self.dim, self.dim))

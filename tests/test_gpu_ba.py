@@ -311,3 +311,56 @@ def test_optimize_energies_buffer_is_bounded():
     assert done.value == 15
     assert np.all(np.isfinite(guard[:7])) and np.all(guard[7:] == 1234.5)
     g.close()
+
+
+@pytest.mark.parametrize("scene_name", ["scene_small", "scene2k", "scene_kitti2k"])
+def test_fix_linearization_bit_exact(scene_name, request):
+    """System::optimize's tail (Src/FullSystemOptimize.cpp:498-516) from the same window state on both sides:
+    newest frame setEvalPT with a / b kept, setAdjointsF, setPrecalcValues, linearizeAll(true).  States, the
+    toRemove list, residual energies, centre projections, maxRelBaseline / numGoodResiduals, frame states and
+    poses, the newest frame's threshold: bit-exact; the energy (double sum, other order) at 1e-9."""
+    scene = request.getfixturevalue(scene_name)
+    g, o = _pair(scene)
+    g.linearizeAll(reset=True)
+    o.linearize_all(reset=True)
+    o.apply_res()
+    rng = np.random.default_rng(5)
+    rb0 = rng.uniform(0.0, 0.02, scene.n_points).astype(np.float32)
+    ng0 = rng.integers(0, 5, scene.n_points).astype(np.int32)
+    out = g.fixLinearization(rb0, ng0)
+    eo, drop_o, rb_o, ng_o = o.fix_linearization(rb0, ng0)
+    rg, ro = g.residuals(), o.residuals()
+    assert np.array_equal(rg["state"], ro["state"])
+    assert np.array_equal(out["drop"], drop_o)
+    assert np.array_equal(out["drop"], (rg["active"] == 0).astype(np.uint8))
+    assert 0 < int(out["drop"].sum()) < scene.n_res
+    act = ro["state"] == 0
+    assert np.array_equal(rg["energy"], ro["energy"].astype(np.float32))
+    assert np.array_equal(rg["center"][act], ro["center"][act])
+    assert np.array_equal(out["maxRelBaseline"], rb_o)
+    assert np.array_equal(out["numGoodResiduals"], ng_o)
+    assert np.array_equal(out["numGoodResiduals"] - ng0, np.bincount(scene.res_point[act], minlength=scene.n_points))
+    assert abs(out["energy"] - eo) <= 1e-9 * abs(eo)
+    fg, fo = g.frames(), o.frames()
+    assert np.array_equal(fg["state"], fo["state"])
+    assert np.array_equal(fg["pose"], fo["pose"])
+    assert np.array_equal(fg["energyTH"], fo["energyTH"])
+    assert np.all(fg["state"][-1, :6] == 0) and np.all(fg["state"][-1, 8:] == 0)
+
+
+def test_fix_linearization_after_optimize(scene2k):
+    """optimize(6) + the tail on both sides (the trajectories differ at the fp-order level): the toRemove lists
+    agree to 0.2% of the residuals, and HdiF_out is the last solve's Schur prelude (the oracle's HdiF after its
+    last accumulateSCF_MT) at the trajectory tolerance."""
+    g, o = _pair(scene2k)
+    g.optimize(6)
+    o.optimize(6)
+    hdi_o = o.points()["HdiF"].copy()
+    z = np.zeros(scene2k.n_points)
+    out = g.fixLinearization(z, z.astype(np.int32))
+    eo, drop_o, _, _ = o.fix_linearization(z.astype(np.float32), z.astype(np.int32))
+    assert np.count_nonzero(out["drop"] != drop_o) <= 0.002 * scene2k.n_res
+    assert abs(out["energy"] - eo) <= 1e-3 * abs(eo)
+    assert np.allclose(out["HdiF"], hdi_o, rtol=2e-3, atol=1e-7)
+    # HdiF_out is not the fixed pass's own prelude
+    assert not np.array_equal(out["HdiF"], g.points()["HdiF"])
