@@ -123,6 +123,7 @@ struct hs_ctx {
   float* d_xAd = nullptr;
   double* d_x = nullptr;
   double* d_elog = nullptr;
+  unsigned int* d_th_hist = nullptr;  // [HS_TH_BINS] threshold select pass-1 histogram (zero between launches)
   float* d_cand = nullptr;  // [nranks][cand_stride] newest-frame energy per point (-1 / NaN = none)
   int cand_stride = 0;
   bool hm_zero = true;      // marginalization prior not set: the solve skips HM
@@ -157,7 +158,7 @@ static void free_window(hs_ctx* c) {
                   c->d_p_step, c->d_part, c->d_part_e, c->d_hostsum, c->d_sys, c->d_sep,
                   c->d_adHost, c->d_adTarget, c->d_adHostF, c->d_adTargetF, c->d_HM, c->d_bM, c->d_Nproj, c->d_xAd,
                   c->d_x, c->d_elog, c->d_cand, c->d_tr_lin, c->d_tr_acc, c->d_tr_solve, c->d_tr_st,
-                  c->d_marg, c->d_adHTdelta, c->d_p_HdiF_alt, c->d_fix_relBL, c->d_fix_nGood};
+                  c->d_marg, c->d_adHTdelta, c->d_p_HdiF_alt, c->d_fix_relBL, c->d_fix_nGood, c->d_th_hist};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   c->d_state = nullptr; c->d_pre = nullptr; c->d_frameTH = nullptr;
@@ -178,6 +179,7 @@ static void free_window(hs_ctx* c) {
   c->d_adHTdelta = nullptr;
   c->d_p_HdiF_alt = c->d_fix_relBL = nullptr;
   c->hdif_solved = nullptr;
+  c->d_th_hist = nullptr;
   c->d_fix_nGood = nullptr;
   c->nF = c->nP = c->nR = 0;
   c->haveSystem = false;
@@ -290,9 +292,12 @@ static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = fals
   a.frameEnergyTHN = c->P.frameEnergyTHN; a.facMedian = c->P.frameEnergyTHFacMedian;
   a.constWeight = c->P.frameEnergyTHConstWeight; a.overallWeight = c->P.overallEnergyTHWeight;
   a.skip_threshold = skip_threshold ? 1 : 0;
+  a.th_hist = c->d_th_hist;
+  // pass-1 histogram blocks of the threshold select: ~4k candidates each, at most 64
+  a.nhist = skip_threshold ? 0 : std::min(64, std::max(1, (c->nranks * c->cand_stride + 4095) / 4096));
   a.trace = c->d_tr_acc;
   if (!readback) {
-    hipLaunchKernelGGL(hs_k_reduce, dim3(c->nF * c->Q + 1), dim3(256), 0, c->stream, a);
+    hipLaunchKernelGGL(hs_k_reduce, dim3(c->nF * c->Q + 1 + a.nhist), dim3(256), 0, c->stream, a);
     HS_HIP(hipGetLastError());
   }
   HsStitchArgs st;
@@ -726,12 +731,13 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
   HS_TRY(dalloc(&c->d_HM, (size_t)n * n)); HS_TRY(dalloc(&c->d_bM, n)); HS_TRY(dalloc(&c->d_Nproj, (size_t)2 * n * HS_NNS));
   HS_TRY(dalloc(&c->d_xAd, nF * nF * 8)); HS_TRY(dalloc(&c->d_x, n)); HS_TRY(dalloc(&c->d_elog, kLogCap));
   HS_TRY(dalloc(&c->d_cand, (size_t)c->cand_stride * c->nranks));
+  HS_TRY(dalloc(&c->d_th_hist, HS_TH_BINS));
   HS_HIP(hipMemset(c->d_cand, 0xff, sizeof(float) * c->cand_stride * c->nranks));  // NaN, sign set: no candidate
   const char* tr = std::getenv("HS_KTRACE");
   c->tracing = tr && tr[0] == '1';
   if (c->tracing) {
     HS_TRY(dalloc(&c->d_tr_lin, (size_t)std::max(c->nblk, 1) * 16));
-    HS_TRY(dalloc(&c->d_tr_acc, (size_t)(nF * c->Q + 1) * 16));
+    HS_TRY(dalloc(&c->d_tr_acc, (size_t)(nF * c->Q + 1 + 64) * 16));  // + the threshold histogram blocks
     HS_TRY(dalloc(&c->d_tr_st, (size_t)(nF * (nF + 1) / 2 + nF + 2) * 16));
     HS_TRY(dalloc(&c->d_tr_solve, 32));
   }
@@ -1280,6 +1286,34 @@ int hs_comm_init(hs_ctx* c, const char* id128, int rank, int nranks) {
 // Runs hs_k_stitch alone on host-provided per-host sums and adjoints: tests/test_gpu_stitch.py checks it against a
 // numpy restatement of the reference's pair-wise stitchDoubleInternal.  hostsum [nF][hs_ne(exact)][64], adH / adT
 // [nF*nF][64] (index h + nF t), out [n*n + n], sep [2][n*n + n] (nullable).
+// test hook (not in the header): setNewFrameEnergyTH's select on n candidates (hs_k_reduce's histogram blocks +
+// the stitch launch's select block); th_out = the newest frame's threshold
+extern "C" int hs_debug_threshold(const float* cand, int n, float thn, float facMedian, float constWeight,
+                                  float overallWeight, float* th_out) {
+  if (n < 1 || !cand || !th_out) return fail(HS_ERR_INVALID, "bad arguments");
+  float *d_c = nullptr, *d_th = nullptr;
+  unsigned int* d_h = nullptr;
+  double* d_e = nullptr;
+  HS_TRY(dalloc(&d_c, n)); HS_TRY(dalloc(&d_th, 1)); HS_TRY(dalloc(&d_h, HS_TH_BINS)); HS_TRY(dalloc(&d_e, 4));
+  HS_HIP(hipMemcpy(d_c, cand, sizeof(float) * n, hipMemcpyHostToDevice));
+  HsRedArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.sysE = d_e; a.cand = d_c; a.nranks = 1; a.stride = n; a.frameTH = d_th; a.newest = 0;
+  a.frameEnergyTHN = thn; a.facMedian = facMedian; a.constWeight = constWeight; a.overallWeight = overallWeight;
+  a.th_hist = d_h;
+  a.nhist = std::min(64, std::max(1, (n + 4095) / 4096));
+  hipLaunchKernelGGL(hs_k_reduce, dim3(1 + a.nhist), dim3(256), 0, 0, a);
+  hipLaunchKernelGGL(hs_k_debug_th, dim3(1), dim3(HS_STITCH_NT), 0, 0, a);
+  HS_HIP(hipGetLastError());
+  unsigned int hz[HS_TH_BINS];
+  HS_HIP(hipMemcpy(th_out, d_th, sizeof(float), hipMemcpyDeviceToHost));
+  HS_HIP(hipMemcpy(hz, d_h, sizeof(hz), hipMemcpyDeviceToHost));
+  (void)hipFree(d_c); (void)hipFree(d_th); (void)hipFree(d_h); (void)hipFree(d_e);
+  for (unsigned int v : hz)
+    if (v) return fail(HS_ERR_STATE, "threshold histogram not re-zeroed");
+  return HS_OK;
+}
+
 extern "C" int hs_debug_stitch(int nF, int exact, const double* hostsum, const double* adH, const double* adT,
                                double* out, double* sep) {
   if (nF < 1 || nF > HS_MAXF || !hostsum || !adH || !adT || !out) return fail(HS_ERR_INVALID, "bad args");

@@ -689,68 +689,149 @@ __device__ void red_energy_block(const HsRedArgs& a) {
   if (tid < 3) a.sysE[tid] = red[tid][0];
 }
 
-// setNewFrameEnergyTH: k-th smallest candidate by a 4-pass radix select (bins counted with LDS integer atomics:
-// order-independent; bin scan by wave prefix sums).  Candidates: one float per point and rank (-1 / negative =
-// none); the ranks' arrays are all-gathered so every rank selects over the same union and computes the same
-// threshold.  Any block size >= 256.
-__device__ void red_energy_th_block(const HsRedArgs& a) {
-  __shared__ unsigned int hist[256], wsum[4];
-  __shared__ unsigned int s_prefix, s_mask, s_k, s_n;
-  const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63;
-  const bool bin = tid < 256;
-  if (tid == 0) {
-    s_prefix = 0;
-    s_mask = 0;
-  }
+// setNewFrameEnergyTH (Src/FullSystemOptimize.cpp:60-101): the k-th smallest candidate, k = (int)(THN * count), by
+// a 3-pass radix select over the candidates' bit patterns (non-negative floats order like their bits).  Candidates:
+// one float per point and rank (negative or NaN = none); the ranks' arrays are all-gathered, so every rank
+// selects over the same union and computes the same threshold.  Pass 1 (bits 30..19) is counted by the nhist
+// histogram blocks of hs_k_reduce (red_th_hist_block, spread over the chip); the stitch launch's last block
+// (red_energy_th_block) selects the bin, then counts bits 18..9 and 8..0 of the survivors, which it compacts into
+// LDS on the way.  All counts are integer: the result is order-independent.
+__device__ void red_th_hist_block(const HsRedArgs& a, int j) {
+  __shared__ unsigned int hh[HS_TH_BINS];
+  const int tid = threadIdx.x, nt = blockDim.x;
+  for (int i = tid; i < HS_TH_BINS; i += nt) hh[i] = 0u;
+  __syncthreads();
   const int total = a.nranks * a.stride;
-  for (int pass = 0; pass < 4; pass++) {
-    const int shift = 24 - 8 * pass;
-    if (bin) hist[tid] = 0;
+  const int per = (total + a.nhist - 1) / a.nhist, i0 = j * per, i1 = min(total, i0 + per);
+  for (int i = i0 + tid; i < i1; i += nt) {
+    const unsigned int v = __float_as_uint(a.cand[i]);
+    if (v <= 0x7f800000u) atomicAdd(&hh[v >> 19], 1u);  // >= 0 and not NaN (state_NewEnergyWithOutlier >= 0)
+  }
+  __syncthreads();
+  for (int i = tid; i < HS_TH_BINS; i += nt)
+    if (hh[i]) atomicAdd(&a.th_hist[i], hh[i]);
+}
+
+// inclusive block prefix sum (wave scans + the waves' totals through wsum[16]); total = the block's sum
+__device__ __forceinline__ unsigned int block_incl_scan(unsigned int x, unsigned int* wsum, unsigned int& total) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[wv] = x;
+  __syncthreads();
+  unsigned int off = 0, tot = 0;
+  for (int w = 0; w < nw; w++) {
+    const unsigned int v = wsum[w];
+    off += w < wv ? v : 0u;
+    tot += v;
+  }
+  __syncthreads();
+  total = tot;
+  return x + off;
+}
+
+constexpr int TH_CAP = 24576;  // survivors of pass 1 kept in LDS (else pass 3 re-reads the candidates)
+
+// sm: >= 1600 + TH_CAP words of LDS (the stitch block's scratch).  blockDim.x == HS_STITCH_NT (4 bins per thread)
+__device__ void red_energy_th_block(const HsRedArgs& a, unsigned int* sm) {
+  static_assert(HS_TH_BINS == 4 * HS_STITCH_NT, "pass-1 bins: 4 per thread");
+  unsigned int* hist2 = sm;          // [1024]
+  unsigned int* hist3 = sm + 1024;   // [512]
+  unsigned int* wsum = sm + 1536;    // [16]
+  unsigned int* ctl = sm + 1552;     // bin, k, survivors, count
+  unsigned int* buf = sm + 1600;     // [TH_CAP]
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int total = a.nranks * a.stride;
+  // ---- pass 1: bins 4 tid .. 4 tid + 3 of the global histogram (then re-zeroed for the next launch)
+  uint4 h4 = reinterpret_cast<const uint4*>(a.th_hist)[tid];
+  reinterpret_cast<uint4*>(a.th_hist)[tid] = make_uint4(0u, 0u, 0u, 0u);
+  for (int i = tid; i < 1024 + 512; i += nt) sm[i] = 0u;
+  if (tid == 0) ctl[2] = 0u;
+  unsigned int n = 0;
+  const unsigned int s4 = h4.x + h4.y + h4.z + h4.w;
+  unsigned int incl = block_incl_scan(s4, wsum, n);
+  if (n == 0) {
+    if (tid == 0) a.frameTH[a.newest] = 12 * 12 * 8;
+    return;
+  }
+  unsigned int kk = (unsigned int)(int)(a.frameEnergyTHN * (float)n);
+  if (incl - s4 <= kk && kk < incl) {
+    unsigned int run = incl - s4;
+    int r = 0;
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+      const unsigned int cq = q == 0 ? h4.x : (q == 1 ? h4.y : h4.z);
+      if (r == q && kk >= run + cq) {
+        run += cq;
+        r = q + 1;
+      }
+    }
+    ctl[0] = 4u * tid + r;
+    ctl[1] = kk - run;
+  }
+  __syncthreads();
+  const unsigned int b1 = ctl[0];
+  kk = ctl[1];
+  // ---- pass 2: bits 18..9 of the candidates in bin b1; survivors compacted into LDS (order irrelevant: counts)
+  for (int i0 = 0; i0 < total; i0 += 4 * nt) {
+    unsigned int v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int i = i0 + u * nt + tid;
+      v[u] = i < total ? __float_as_uint(a.cand[i]) : 0xffffffffu;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+      if (v[u] <= 0x7f800000u && (v[u] >> 19) == b1) {
+        atomicAdd(&hist2[(v[u] >> 9) & 1023u], 1u);
+        const unsigned int pos = atomicAdd(&ctl[2], 1u);
+        if (pos < (unsigned int)TH_CAP) buf[pos] = v[u];
+      }
+  }
+  __syncthreads();
+  const unsigned int ns = ctl[2];
+  {
+    const unsigned int c = hist2[tid];
+    unsigned int tot;
+    const unsigned int in2 = block_incl_scan(c, wsum, tot);
+    if (in2 - c <= kk && kk < in2) {
+      ctl[0] = tid;
+      ctl[1] = kk - (in2 - c);
+    }
     __syncthreads();
-    const unsigned int prefix = s_prefix, mask = s_mask;
+  }
+  const unsigned int p2 = (b1 << 10) | ctl[0];
+  kk = ctl[1];
+  // ---- pass 3: bits 8..0 of the survivors with prefix p2
+  if (ns <= (unsigned int)TH_CAP) {
+    for (unsigned int i = tid; i < ns; i += nt) {
+      const unsigned int v = buf[i];
+      if ((v >> 9) == p2) atomicAdd(&hist3[v & 511u], 1u);
+    }
+  } else {
     for (int i = tid; i < total; i += nt) {
       const unsigned int v = __float_as_uint(a.cand[i]);
-      if (v < 0x80000000u && (v & mask) == prefix) atomicAdd(&hist[(v >> shift) & 255u], 1u);
+      if (v <= 0x7f800000u && (v >> 9) == p2) atomicAdd(&hist3[v & 511u], 1u);
     }
-    __syncthreads();
-    const unsigned int hcount = bin ? hist[tid] : 0u;
-    unsigned int x = hcount;  // inclusive prefix over the wave's 64 bins
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const unsigned int y = __shfl_up(x, o);
-      if (lane >= o) x += y;
-    }
-    if (bin && lane == 63) wsum[tid >> 6] = x;
-    __syncthreads();
-    unsigned int off = 0;
-    for (int w = 0; w < 4 && w < (tid >> 6); w++) off += wsum[w];
-    const unsigned int incl = x + off;
-    if (pass == 0 && tid == 255) {
-      s_n = incl;
-      s_k = (unsigned int)(int)(a.frameEnergyTHN * (float)incl);
-    }
-    __syncthreads();
-    if (s_n == 0) break;
-    const unsigned int excl = incl - hcount, kk = s_k;
-    __syncthreads();
-    if (bin && excl <= kk && kk < incl) {
-      s_k = kk - excl;
-      s_prefix = prefix | ((unsigned int)tid << shift);
-      s_mask = mask | (255u << shift);
-    }
+  }
+  __syncthreads();
+  {
+    const unsigned int c = tid < 512 ? hist3[tid] : 0u;
+    unsigned int tot;
+    const unsigned int in3 = block_incl_scan(c, wsum, tot);
+    if (c != 0u && in3 - c <= kk && kk < in3) ctl[3] = tid;
     __syncthreads();
   }
   if (tid == 0) {
-    if (s_n == 0) {
-      a.frameTH[a.newest] = 12 * 12 * 8;
-    } else {
-      const float nth = sqrtf(__uint_as_float(s_prefix));
-      float th = nth * a.facMedian;
-      th = 26.0f * a.constWeight + th * (1 - a.constWeight);
-      th = th * th;
-      th *= a.overallWeight * a.overallWeight;
-      a.frameTH[a.newest] = th;
-    }
+    const float nth = sqrtf(__uint_as_float((p2 << 9) | ctl[3]));
+    float th = nth * a.facMedian;
+    th = 26.0f * a.constWeight + th * (1 - a.constWeight);
+    th = th * th;
+    th *= a.overallWeight * a.overallWeight;
+    a.frameTH[a.newest] = th;
   }
 }
 
@@ -806,6 +887,7 @@ __device__ __forceinline__ double sandwich8(const double* L, const double* M, co
 
 constexpr int ST_NT = HS_STITCH_NT, ST_NW = ST_NT / 64;  // stitch block: 16 waves, one 8x8 term per wave at a time
 constexpr int ST_LDS = 12288 + ST_NW * 64;  // doubles of the stitch block's LDS (the f == g frame block)
+static_assert(2 * ST_LDS >= 1600 + TH_CAP, "the threshold select's LDS lives in the stitch block's scratch");
 }  // namespace
 
 __global__ __launch_bounds__(256) void hs_k_reduce(HsRedArgs a) {
@@ -813,6 +895,7 @@ __global__ __launch_bounds__(256) void hs_k_reduce(HsRedArgs a) {
   const int b = blockIdx.x, tid = threadIdx.x;
   HS_TRACE(a, 0);
   if (b == nred) { red_energy_block(a); HS_TRACE(a, 15); return; }
+  if (b > nred) { red_th_hist_block(a, b - nred - 1); HS_TRACE(a, 15); return; }
   const int h = b / a.Q, q = b % a.Q;
   const int NE64 = a.ne * 64;
   const int e = q * 256 + tid;  // entry of the host's [ne][64] accumulators
@@ -832,6 +915,11 @@ __global__ __launch_bounds__(256) void hs_k_reduce(HsRedArgs a) {
     a.hostsum[(size_t)h * NE64 + e] = s;
   }
   HS_TRACE(a, 15);
+}
+
+__global__ __launch_bounds__(HS_STITCH_NT) void hs_k_debug_th(HsRedArgs a) {
+  __shared__ unsigned int sm[1600 + TH_CAP];
+  red_energy_th_block(a, sm);
 }
 
 // stitchDoubleMT (Include/AccumulatedTopHessian.h:69-117, Include/AccumulatedSCHessian.h:70-111) with
@@ -861,7 +949,7 @@ __global__ __launch_bounds__(ST_NT) void hs_k_stitch(HsStitchArgs a) {
   const int j = blockIdx.x;
   HS_TRACE(a, 0);
   if (j == nFB + nF + 1) {  // setNewFrameEnergyTH for the next linearization, beside the stitch
-    if (!a.red.skip_threshold) red_energy_th_block(a.red);
+    if (!a.red.skip_threshold) red_energy_th_block(a.red, reinterpret_cast<unsigned int*>(lds));
     HS_TRACE(a, 15);
     return;
   }

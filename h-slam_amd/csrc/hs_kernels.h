@@ -110,8 +110,13 @@ struct HsRedArgs {
   int newest;
   float frameEnergyTHN, facMedian, constWeight, overallWeight;
   int skip_threshold;          // marginalization pass: setNewFrameEnergyTH is not part of it
+  // the select's first radix pass (candidate bits 30..19) as a 4096-bin histogram, counted by nhist blocks of
+  // hs_k_reduce into th_hist (integer atomics: order-independent); consumed and re-zeroed by hs_k_stitch
+  unsigned int* th_hist;
+  int nhist;
   long long* trace;
 };
+constexpr int HS_TH_BINS = 4096;
 
 // hs_k_stitch: stitchDoubleMT of the top and Schur systems from the host sums, one block per output block of the
 // system (8x8 frame blocks f <= g, calib x frame f, calib x calib), every output entry summed over the
@@ -174,6 +179,7 @@ __global__ void hs_k_lin_exact(HsLinArgs a);  // HS_ACC_EXACT: one wave per host
 __global__ void hs_k_lin_fix(HsLinArgs a);        // + linearizeAll(true)'s per-point bookkeeping
 __global__ void hs_k_lin_exact_fix(HsLinArgs a);
 __global__ void hs_k_reduce(HsRedArgs a);
+__global__ void hs_k_debug_th(HsRedArgs a);     // test hook: the threshold select block alone
 __global__ void hs_k_stitch(HsStitchArgs a);
 __global__ void hs_k_solve(HsSolveArgs a);
 __global__ void hs_k_resub(HsResubArgs a);
