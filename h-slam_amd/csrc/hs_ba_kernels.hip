@@ -1307,7 +1307,7 @@ __global__ __launch_bounds__(ST_NT) void hs_k_stitch(HsStitchArgs a) {
 // solve + step (fp64), one workgroup of 256 threads
 // =====================================================================================================
 namespace {
-constexpr int SOLVE_NT = HS_SOLVE_NT;  // 4 waves, one per SIMD: one lower-triangle 4x4 tile per lane in the LDLT
+constexpr int SOLVE_NT = HS_SOLVE_NT;  // 8 waves: the LDLT's panel wave + 7 waves of trailing half-tiles
 
 __device__ __forceinline__ double readlane_f64(double v, int lane) {
   const long long b = __double_as_longlong(v);
@@ -1333,6 +1333,7 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
 //   LT : L transposed, LT[i * LSTR + k] = L(k, i); MUST be zero on entry (its upper part stays zero)
 //   W  : scratch of 26 * HS_MAXDIM doubles;  yv : right-hand side in, solution out
 constexpr int LSTR = HS_MAXDIM + 1;  // padded row stride of LT
+constexpr int LDLT_SCRATCH = 26 * HS_MAXDIM;
 
 // 1/d: v_rcp_f64 (~2^-26 relative) refined by ONE Newton step (~2^-50, 4e-15 relative) -- the pivots' error
 // then sits ~1e11 below the 1e-3 tolerance on x, and the LDLT's critical path is 68 reciprocals long;
@@ -1391,16 +1392,16 @@ __device__ __forceinline__ void panel_row_uniform(const double a[4], double yr, 
   o.yr = yr;
 }
 
-// publishes one panel row r (l = r - K0): LW / LS (zero for the diagonal rows, which take no part in the
-// trailing update), its L entries, and the substituted rhs; lane j < 4 also stores pivot j
+// publishes one panel row r (l = r - K0): its (L D) entries LW (zero for the diagonal rows, which take no part in
+// the trailing update), its L entries into LT (which the next phase reads back), and the substituted rhs; lane
+// j < 4 also stores pivot j
 __device__ __forceinline__ void panel_row_store(const PanelOut& o, const Panel4& P, int r, int l, int K0, double* LWn,
-                                                double* LSn, double* LT, double* Dv, double* yf, double* yv) {
+                                                double* LT, double* Dv, double* yf, double* yv) {
   constexpr int MD = HS_MAXDIM;
   const bool diag = l < 4;
 #pragma unroll
   for (int j = 0; j < 4; j++) {
     LWn[j * MD + r] = diag ? 0.0 : o.lw[j];
-    LSn[j * MD + r] = diag ? 0.0 : o.ls[j];
     LT[(K0 + j) * LSTR + r] = o.ls[j];  // zero on and above the diagonal
   }
   if (diag) {
@@ -1412,13 +1413,13 @@ __device__ __forceinline__ void panel_row_store(const PanelOut& o, const Panel4&
 }
 
 __device__ __forceinline__ void ldlt_solve_blocked(const double* M, double* LT, double* W, double* yv, int n, int tid,
-                                                   long long* trace) {
+                                                   long long* trace, int dbg = 0) {
   constexpr int MD = HS_MAXDIM;
   static_assert((HS_MAXDIM / 4 - 2) * (HS_MAXDIM / 4 - 1) / 2 <= SOLVE_NT - 64, "one trailing tile per lane");
   const int nb = n >> 2;
   double* PBq = W;            // [2][4][MD] column block k+1 before block k's update, column-major
-  double* LWb = W + 8 * MD;   // [2][4][MD] (L D) of panel k
-  double* LSb = W + 16 * MD;  // [2][4][MD] L of panel k
+  double* LWb = W + 8 * MD;   // [2][4][MD] (L D) of panel k (W + 16 MD .. 24 MD unused)
+  // L of panel k is read back from LT (rows below the panel's diagonal block only: no masking needed)
   double* Dv = W + 24 * MD;   // [MD] pivots
   double* yf = W + 25 * MD;   // [MD] forward-substituted rhs of the diagonal rows
   const bool pw = tid < 64;   // the panel wave
@@ -1445,20 +1446,20 @@ __device__ __forceinline__ void ldlt_solve_blocked(const double* M, double* LT, 
     Panel4 P;
     PanelOut o;
     panel_coop(a4, yv[r], tid, P, o);
-    if (tid < n) panel_row_store(o, P, tid, tid, 0, LWb, LSb, LT, Dv, yf, yv);
+    if (tid < n) panel_row_store(o, P, tid, tid, 0, LWb, LT, Dv, yf, yv);
     if (tid + 64 < n) {
       const int r2 = tid + 64;
 #pragma unroll
       for (int c = 0; c < 4; c++) a4[c] = M[r2 * n + c];
       panel_row_uniform(a4, yv[r2], P, o);
-      panel_row_store(o, P, r2, r2, 0, LWb, LSb, LT, Dv, yf, yv);
+      panel_row_store(o, P, r2, r2, 0, LWb, LT, Dv, yf, yv);
     }
   }
   __syncthreads();
   for (int k = 0; k + 1 < nb; k++) {
     const int K0 = 4 * (k + 1);
     const double* LWk = LWb + (k & 1) * 4 * MD;
-    const double* LSk = LSb + (k & 1) * 4 * MD;
+    const double* LSk = LT + 4 * k * LSTR;  // LSk[j * LSTR + row] = L(row, 4k + j)
     if (trace && tid == 0 && k == 4) trace[16] = clock64();
     if (pw) {  // panel k+1: row r = K0 + lane
       const int l = tid, r = min(K0 + l, n - 1);
@@ -1469,7 +1470,7 @@ __device__ __forceinline__ void ldlt_solve_blocked(const double* M, double* LT, 
         a4[j] = PBc[j * MD + r];
         lwk[j] = LWk[j * MD + r];
 #pragma unroll
-        for (int c = 0; c < 4; c++) lsd[c][j] = LSk[j * MD + K0 + c];
+        for (int c = 0; c < 4; c++) lsd[c][j] = LSk[j * LSTR + K0 + c];
       }
       const double yr = yv[r];
 #pragma unroll
@@ -1480,7 +1481,7 @@ __device__ __forceinline__ void ldlt_solve_blocked(const double* M, double* LT, 
       PanelOut o;
       panel_coop(a4, yr, l, P, o);
       if (K0 + l < n)
-        panel_row_store(o, P, r, l, K0, LWb + ((k + 1) & 1) * 4 * MD, LSb + ((k + 1) & 1) * 4 * MD, LT, Dv, yf, yv);
+        panel_row_store(o, P, r, l, K0, LWb + ((k + 1) & 1) * 4 * MD, LT, Dv, yf, yv);
       if (trace && tid == 0 && k == 4) trace[17] = clock64();
     } else if (tile && tc >= k + 2) {  // block k's rank-4 update of a trailing tile
       double lw[4][4], ls[4][4];
@@ -1489,7 +1490,7 @@ __device__ __forceinline__ void ldlt_solve_blocked(const double* M, double* LT, 
 #pragma unroll
         for (int i = 0; i < 4; i++) {
           lw[i][j] = LWk[j * MD + 4 * tr + i];
-          ls[i][j] = LSk[j * MD + 4 * tc + i];
+          ls[i][j] = LSk[j * LSTR + 4 * tc + i];
         }
 #pragma unroll
       for (int j = 0; j < 4; j++)
@@ -1561,9 +1562,65 @@ __device__ __forceinline__ void ldlt_solve_blocked(const double* M, double* LT, 
   }
 }
 
+// FrameOptimizationData::setState's scaling (Include/Frame.h:151-170)
+__device__ __forceinline__ void scale_state(const double s[10], double o[10]) {
+#pragma unroll
+  for (int i = 0; i < 3; i++) o[i] = hs::SCALE_XI_TRANS * s[i];
+#pragma unroll
+  for (int i = 3; i < 6; i++) o[i] = hs::SCALE_XI_ROT * s[i];
+  o[6] = hs::SCALE_A * s[6];
+  o[7] = hs::SCALE_B * s[7];
+  o[8] = hs::SCALE_A * s[8];
+  o[9] = hs::SCALE_B * s[9];
+}
+
+// Sophus SE3::exp (hs_se3.h) for a GN step: for theta^2 < 1e-2 the so3 / V coefficients sin(x/2)/x, cos(x/2),
+// (1 - cos x)/x^2 and (x - sin x)/x^3 come from their Taylor series in u = x^2 (6 terms: truncation < 1e-20
+// relative; no sqrt, trig or division on the chain); the quaternion is normalized with one reciprocal square
+// root.  Larger tangents take the reference formulas.  Differs from Sophus by rounding only.
+__device__ __forceinline__ hs::SE3 se3_exp_step(const double a[6]) {
+  const double w0 = a[3], w1 = a[4], w2 = a[5];
+  const double u = w0 * w0 + w1 * w1 + w2 * w2;
+  if (!(u < 1e-2)) return hs::SE3::exp(a);
+  auto poly = [u](double c0, double c1, double c2, double c3, double c4, double c5) {
+    return __builtin_fma(__builtin_fma(__builtin_fma(__builtin_fma(__builtin_fma(c5, u, c4), u, c3), u, c2), u, c1), u,
+                         c0);
+  };
+  const double imag = poly(1.0 / 2, -1.0 / 48, 1.0 / 3840, -1.0 / 645120, 1.0 / 185794560, -1.0 / 81749606400.0);
+  const double real = poly(1.0, -1.0 / 8, 1.0 / 384, -1.0 / 46080, 1.0 / 10321920, -1.0 / 3715891200.0);
+  const double c1 = poly(1.0 / 2, -1.0 / 24, 1.0 / 720, -1.0 / 40320, 1.0 / 3628800, -1.0 / 479001600);
+  const double c2 = poly(1.0 / 6, -1.0 / 120, 1.0 / 5040, -1.0 / 362880, 1.0 / 39916800, -1.0 / 6227020800.0);
+  hs::SE3 r;
+  const double qx = imag * w0, qy = imag * w1, qz = imag * w2;
+  const double inv = 1.0 / sqrt(qx * qx + qy * qy + qz * qz + real * real);
+  r.q = hs::Quat{qx * inv, qy * inv, qz * inv, real * inv};
+  double O[9], O2[9], V[9];
+  hs::SE3::hat3(a + 3, O);
+  hs::SE3::mm3(O, O, O2);
+#pragma unroll
+  for (int i = 0; i < 9; i++) V[i] = ((i % 4 == 0) ? 1.0 : 0.0) + c1 * O[i] + c2 * O2[i];
+#pragma unroll
+  for (int i = 0; i < 3; i++) r.t[i] = V[i * 3 + 0] * a[0] + V[i * 3 + 1] * a[1] + V[i * 3 + 2] * a[2];
+  return r;
+}
+
+// SE3 product (Sophus fastMultiply: quaternion product + normalize), normalized with one reciprocal square root
+__device__ __forceinline__ hs::SE3 se3_mul_step(const hs::SE3& A, const hs::SE3& B) {
+  hs::SE3 r;
+  double rt[3];
+  hs::qrot(A.q, B.t, rt);
+  r.t[0] = A.t[0] + rt[0];
+  r.t[1] = A.t[1] + rt[1];
+  r.t[2] = A.t[2] + rt[2];
+  const hs::Quat q = hs::qmul(A.q, B.q);
+  const double inv = 1.0 / sqrt(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+  r.q = hs::Quat{q.x * inv, q.y * inv, q.z * inv, q.w * inv};
+  return r;
+}
+
 __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
   __shared__ double A[HS_MAXDIM * HS_MAXDIM];  // the scaled system S H S (row-major, stride n)
-  __shared__ double B[26 * HS_MAXDIM];  // LDLT scratch
+  __shared__ double B[LDLT_SCRATCH];  // LDLT scratch
   __shared__ double LT[HS_MAXDIM * (HS_MAXDIM + 1)];  // L^T of the factorization (zeroed at entry)
   __shared__ double Nf[2 * HS_MAXDIM * HS_NNS];  // nullspace factors N | Npi (prefetched at entry)
   __shared__ double tk[2 * HS_NNS];
@@ -1710,7 +1767,12 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     // factorization is backward stable without pivoting; Eigen's LDLT (Src/EnergyFunctional.cpp:801) pivots on
     // the diagonal, which changes x by rounding only (the LDLT is parity-unpinned; tests bound x by
     // the reference's own 1- vs 8-thread spread)
-    ldlt_solve_blocked(A, LT, B, yv, n, tid, a.trace);
+    if ((a.dbg & 8) && a.trace && tid == 0) a.trace[20] = clock64();
+    for (int rep = 0; rep < ((a.dbg & 8) ? 2 : 1); rep++) {
+      ldlt_solve_blocked(A, LT, B, yv, n, tid, a.trace, a.dbg);
+      __syncthreads();
+      if ((a.dbg & 8) && a.trace && tid == 0) a.trace[21 + rep] = clock64();
+    }
     __syncthreads();
     HS_TRACE(a, 3);
     if (tid < n) xs[tid] = Sv[tid] * yv[tid];
@@ -1789,38 +1851,105 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
   }
   __syncthreads();
   if (a.flags & HS_APPLY) {
-    // backupState + doStepFromBackup(1, 1, 1, 1, 1): calib and frames, then setPrecalcValues
-    if (tid == 0) {
-      hs::CalibH& cal = st->calib;
-      double nv[4];
-      for (int q = 0; q < 4; q++) {
-        cal.value_backup[q] = cal.value[q];
-        nv[q] = cal.value_backup[q] + 1.0f * cal.step[q];
-      }
-      cal.setValue(nv);
-      st->dcal = cal.device();
-    }
-    if (tid >= 64 && tid < 64 + nF) {
-      hs::FrameH& f = st->frames[tid - 64];
-      double s[10];
+    // backupState + doStepFromBackup(1, 1, 1, 1, 1) + setPrecalcValues (Src/FullSystemOptimize.cpp:171-314),
+    // register-resident: thread (h, t) of the nF x nF pairs forms both frames' new poses itself (no stage barrier
+    // between the frame update and the precalc) and then the pair's FrameFramePrecalc::set; the (f, f) threads
+    // write frame f back, thread 0 the calib.  PRE_RTll_0 / PRE_tTll_0 depend on evalPT only and stay as uploaded.
+    const int np = nF * nF;
+    const int hh = tid < np ? tid / nF : 0, tt = tid < np ? tid - hh * nF : 0;
+    double cv[4], sh[10], stH[10], st_t[10], stT[10], evH[7], evT[7];
+    float expH = 1.f, expT = 1.f;
+    double szH7 = 0.0;
+    if (tid < np) {  // every input into registers, then one barrier before any write-back
+#pragma unroll
+      for (int q = 0; q < 4; q++) cv[q] = st->calib.value[q] + 1.0f * st->calib.step[q];
+      const hs::FrameH& H = st->frames[hh];
+      const hs::FrameH& T = st->frames[tt];
+#pragma unroll
       for (int q = 0; q < 10; q++) {
-        f.state_backup[q] = f.state[q];
-        s[q] = f.state_backup[q] + 1.0 * f.step[q];
+        sh[q] = H.state[q];
+        stH[q] = H.step[q];
+        st_t[q] = T.state[q];
+        stT[q] = T.step[q];
       }
-      f.setState(s);
-      for (int q = 0; q < 8; q++) {
-        f.delta[q] = f.state[q] - f.state_zero[q];
-        f.delta_prior[q] = f.state[q] - 0.0;
-      }
+      H.evalPT.toData(evH);
+      T.evalPT.toData(evT);
+      expH = H.ab_exposure;
+      expT = T.ab_exposure;
+      szH7 = H.state_zero[7];
     }
+    if ((a.dbg & 16) && a.trace && tid == 0) a.trace[20] = clock64();
     __syncthreads();
-    HS_TRACE(a, 6);
-    for (int pr = tid; pr < nF * nF; pr += nt) {
-      const int hh = pr / nF, tt = pr % nF;
-      a.pre[pr] = hs::make_precalc(st->frames[hh], st->frames[tt], st->calib);
+    if ((a.dbg & 16) && a.trace && tid == 0) a.trace[21] = clock64();
+    if (tid < np) {
+      double nsH[10], nsT[10];
+#pragma unroll
+      for (int q = 0; q < 10; q++) {
+        nsH[q] = sh[q] + 1.0 * stH[q];
+        nsT[q] = st_t[q] + 1.0 * stT[q];
+      }
+      double scH[10], scT[10];
+      scale_state(nsH, scH);
+      scale_state(nsT, scT);
+      const hs::SE3 PWh = se3_mul_step(se3_exp_step(scH), hs::SE3::fromData(evH));
+      const hs::SE3 PWt = se3_mul_step(se3_exp_step(scT), hs::SE3::fromData(evT));
+      const hs::SE3 PCh = PWh.inverse();
+      if ((a.dbg & 16) && a.trace && tid == 0) a.trace[22] = clock64() + (long long)(PCh.t[0] * 0.0 + PWt.t[1] * 0.0);
+      // FrameFramePrecalc::set: PRE_RTll / PRE_tTll, K R Ki, K t, the affine mode, b0
+      const hs::SE3 l2l = se3_mul_step(PWt, PCh);
+      double R[9];
+      l2l.rotationMatrix(R);
+      float RT[9], tT[3];
+#pragma unroll
+      for (int i = 0; i < 9; i++) RT[i] = (float)R[i];
+#pragma unroll
+      for (int i = 0; i < 3; i++) tT[i] = (float)l2l.t[i];
+      float vsf[4] = {(float)(hs::SCALE_F * cv[0]), (float)(hs::SCALE_F * cv[1]), (float)(hs::SCALE_C * cv[2]),
+                      (float)(hs::SCALE_C * cv[3])};
+      float K[9] = {vsf[0], 0, vsf[2], 0, vsf[1], vsf[3], 0, 0, 1};
+      float Ki[9], KR[9], KRKi[9], Kt[3];
+      hs::inv3f(K, Ki);
+      hs::mm3f(K, RT, KR);
+      hs::mm3f(KR, Ki, KRKi);
+      hs::mv3f(K, tT, Kt);
+      double aff[2];
+      hs::fromToVecExposure(expH, expT, scH[6], scH[7], scT[6], scT[7], aff);
+      HsPrecalc* pc = a.pre + tid;
+#pragma unroll
+      for (int i = 0; i < 9; i++) pc->KRKi[i] = KRKi[i];
+#pragma unroll
+      for (int i = 0; i < 3; i++) pc->Kt[i] = Kt[i];
+      pc->aff[0] = (float)aff[0];
+      pc->aff[1] = (float)aff[1];
+      pc->b0 = (float)(szH7 * hs::SCALE_B);  // aff0_b of the host
+      if ((a.dbg & 16) && a.trace && tid == 0) a.trace[23] = clock64() + (long long)(aff[0] * 0.0 + KRKi[3] * 0.0);
+      if (hh == tt) {  // frame hh: backupState, setState, setDeltaF's delta / delta_prior
+        hs::FrameH& F = st->frames[hh];
+        const hs::SE3 PCw = PCh;
+#pragma unroll
+        for (int q = 0; q < 10; q++) {
+          F.state_backup[q] = sh[q];
+          F.state[q] = nsH[q];
+          F.state_scaled[q] = scH[q];
+        }
+        F.PRE_worldToCam = PWh;
+        F.PRE_camToWorld = PCw;
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+          F.delta[q] = nsH[q] - F.state_zero[q];
+          F.delta_prior[q] = nsH[q] - 0.0;
+        }
+      }
+      if (tid == 0) {
+        hs::CalibH& cal = st->calib;
+#pragma unroll
+        for (int q = 0; q < 4; q++) cal.value_backup[q] = cal.value[q];
+        cal.setValue(cv);
+        st->dcal = cal.device();
+      }
     }
-    if (tid == 0) HS_TRACE(a, 10);
-    if (tid == 128) {
+    HS_TRACE(a, 6);
+    if (tid == 64) {  // canbreak (the steps are not modified above)
       float sumA = 0, sumB = 0, sumT = 0, sumR = 0;
       for (int f = 0; f < nF; f++) {
         const double* sp = st->frames[f].step;
@@ -1837,6 +1966,7 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
                      sqrtf(sumT) * sumNID < 0.00005 * th;
       st->iteration = s_it + 1;
     }
+    if (tid == 0) HS_TRACE(a, 10);
   }
   __syncthreads();
   {  // write the window state back

@@ -7,7 +7,7 @@
 #include "hs_host_math.h"
 #include "hs_layout.h"
 
-constexpr int HS_SOLVE_NT = 256;   // hs_k_solve workgroup size
+constexpr int HS_SOLVE_NT = 512;   // hs_k_solve workgroup size
 constexpr int HS_STITCH_NT = 1024; // hs_k_stitch workgroup size
 constexpr int HS_NNS = 7;         // gauge nullspaces: 6 pose + 1 scale (System::getNullspaces)
 
@@ -156,6 +156,7 @@ struct HsSolveArgs {
   long long* trace;
   double initialCalibHessian;
   float thOptIterations;
+  int dbg;                     // experiments (env HS_SOLVE_DBG); 0 in production
 };
 
 struct HsResubArgs {
