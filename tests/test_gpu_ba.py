@@ -364,3 +364,24 @@ def test_fix_linearization_after_optimize(scene2k):
     assert np.allclose(out["HdiF"], hdi_o, rtol=2e-3, atol=1e-7)
     # HdiF_out is not the fixed pass's own prelude
     assert not np.array_equal(out["HdiF"], g.points()["HdiF"])
+
+
+def test_graph_replay_matches_eager(scene2k):
+    """gn_iterations replays iteration pairs as one captured hipGraph (HS_GRAPH=1) or launches them one by one
+    (default): identical energies, frame states, depths and systems, bit for bit."""
+    import os
+    from hslam_amd.ba import BAWindow
+    res = []
+    for mode in ("0", "1"):
+        os.environ["HS_GRAPH"] = mode
+        try:
+            g = BAWindow(scene2k)
+            g.linearizeAll(reset=True)
+            e1 = g.iterate(0, 5)
+            e2 = g.iterate(5, 4)  # a second call replays the cached graph
+            res.append((e1, e2, g.frames()["state"], g.points()["idepth"], g.system(0)[0]))
+            g.close()
+        finally:
+            os.environ.pop("HS_GRAPH", None)
+    for a, b in zip(*res):
+        assert np.array_equal(a, b)
