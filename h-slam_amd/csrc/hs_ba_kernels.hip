@@ -776,15 +776,16 @@ __device__ void red_energy_th_block(const HsRedArgs& a, unsigned int* sm) {
   const unsigned int b1 = ctl[0];
   kk = ctl[1];
   // ---- pass 2: bits 18..9 of the candidates in bin b1; survivors compacted into LDS (order irrelevant: counts)
-  for (int i0 = 0; i0 < total; i0 += 4 * nt) {
-    unsigned int v[4];
+  constexpr int TH_U = 16;  // candidates in flight per thread (the scan is latency-bound: one block)
+  for (int i0 = 0; i0 < total; i0 += TH_U * nt) {
+    unsigned int v[TH_U];
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
+    for (int u = 0; u < TH_U; u++) {
       const int i = i0 + u * nt + tid;
       v[u] = i < total ? __float_as_uint(a.cand[i]) : 0xffffffffu;
     }
 #pragma unroll
-    for (int u = 0; u < 4; u++)
+    for (int u = 0; u < TH_U; u++)
       if (v[u] <= 0x7f800000u && (v[u] >> 19) == b1) {
         atomicAdd(&hist2[(v[u] >> 9) & 1023u], 1u);
         const unsigned int pos = atomicAdd(&ctl[2], 1u);
@@ -812,9 +813,16 @@ __device__ void red_energy_th_block(const HsRedArgs& a, unsigned int* sm) {
       if ((v >> 9) == p2) atomicAdd(&hist3[v & 511u], 1u);
     }
   } else {
-    for (int i = tid; i < total; i += nt) {
-      const unsigned int v = __float_as_uint(a.cand[i]);
-      if (v <= 0x7f800000u && (v >> 9) == p2) atomicAdd(&hist3[v & 511u], 1u);
+    for (int i0 = 0; i0 < total; i0 += TH_U * nt) {
+      unsigned int v[TH_U];
+#pragma unroll
+      for (int u = 0; u < TH_U; u++) {
+        const int i = i0 + u * nt + tid;
+        v[u] = i < total ? __float_as_uint(a.cand[i]) : 0xffffffffu;
+      }
+#pragma unroll
+      for (int u = 0; u < TH_U; u++)
+        if (v[u] <= 0x7f800000u && (v[u] >> 9) == p2) atomicAdd(&hist3[v[u] & 511u], 1u);
     }
   }
   __syncthreads();
