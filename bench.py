@@ -33,6 +33,7 @@ METRIC = "point-residuals/sec in windowed photometric BA (8 KF × 2k pts), 1→8
 BYTES_PER_PRES = 448      # algorithmic bytes per point-residual (fused K1-K5: hs_k_lin accumulates in
                           # registers, no per-residual Jacobian record leaves the kernel)
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
+TRACK_BYTES_PER_POINT_PASS = 64  # CoarseTracker bytes per reference point per calcRes+GS pass
 
 
 def pmc_traffic(points: int, kernel: str = "hs_k_lin"):
@@ -215,13 +216,25 @@ def bench_track(args):
         ok, T, a = ct.trackNewestCoarse(T0, [0.0, 0.0], s.n_levels - 1, minRes)
         dev += ct.last_ms()
     dt = time.perf_counter() - t0
+    # roofline: 64 B of algorithmic traffic and ~230 FLOP per point-pass (reference point
+    # x calcRes(+calcGSSSE) pass); the units come from the kernel's own pass counters
+    _, passes, point_passes = ct.last_stats(0)
+    dev_ms = dev / args.steps
+    achieved = point_passes * TRACK_BYTES_PER_POINT_PASS / (dev_ms * 1e-3) / 1e9
     res = {
         "metric": "frames tracked/sec (CoarseTracker::trackNewestCoarse, C2 640x480, 5 levels)",
         "value": args.steps / dt, "unit": "frames/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": dt * 1e3 / args.steps, "higher_is_better": True, "scaling": "replicas only",
         "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": "C2 (BASELINE.json configs[1]): trackNewestCoarse from identity, 2000 reference "
-                               "points, 640x480, 5 levels", "ok": bool(ok), "device_ms_per_track": dev / args.steps},
+                               "points, 640x480, 5 levels", "ok": bool(ok), "device_ms_per_track": dev_ms,
+                   "passes": passes, "point_passes": point_passes},
+        "roofline": {"bound": "hbm", "kernel": "hs_k_track", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "bytes_per_unit": TRACK_BYTES_PER_POINT_PASS,
+                     "unit_of_bytes": "reference point x calcRes+calcGSSSE pass", "units_per_launch": point_passes,
+                     "avg_launch_ms": dev_ms, "flop_per_unit": 230,
+                     "achieved_tflops": point_passes * 230 / (dev_ms * 1e-3) / 1e12,
+                     "timing": "HIP events around the single hs_k_track launch of each trackNewestCoarse"},
         "cpu_baseline": None,
     }
     if not args.no_cpu:

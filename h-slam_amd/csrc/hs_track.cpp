@@ -63,6 +63,7 @@ struct hs_tracker {
   double refAff[2] = {0, 0};
   bool haveRef = false, haveFrame = false;
   double last_ms = 0;
+  long long* d_trace = nullptr;  // HS_KTRACE=1: per-hypothesis phase cycles of hs_k_track (stderr)
 };
 
 static int upload_pyr(hs_tracker* t, float4** dst, const float* const* pyr) {
@@ -132,6 +133,13 @@ static int run_tries(hs_tracker* t, int n, const double* h_in, int coarsest, int
   a.single_pass = single_pass;
   a.pass_lvl = lvl;
   a.pass_cutoff = cutoff;
+  const char* kt = std::getenv("HS_KTRACE");
+  if (kt && kt[0] == '1' && !single_pass) {
+    if (t->d_trace) (void)hipFree(t->d_trace);
+    TS_HIP(hipMalloc((void**)&t->d_trace, sizeof(long long) * 16 * n));
+    TS_HIP(hipMemsetAsync(t->d_trace, 0, sizeof(long long) * 16 * n, t->stream));
+    a.trace = t->d_trace;
+  }
   TS_HIP(hipEventRecord(t->e0, t->stream));
   hipLaunchKernelGGL(hs_k_track, dim3(n), dim3(512), 0, t->stream, a);
   TS_HIP(hipGetLastError());
@@ -142,6 +150,12 @@ static int run_tries(hs_tracker* t, int n, const double* h_in, int coarsest, int
   TS_HIP(hipEventElapsedTime(&ms, t->e0, t->e1));
   t->last_ms = ms;
   t->last_n_tries = single_pass ? 0 : n;
+  if (a.trace) {
+    long long h[16];
+    TS_HIP(hipMemcpy(h, t->d_trace, sizeof(h), hipMemcpyDeviceToHost));
+    std::fprintf(stderr, "[trk trace] %.3f ms: point loop %lld, reductions %lld (wave reduce %lld, barrier wait %lld), "
+                 "LM steps %lld cycles over %lld passes\n", ms, h[4], h[5], h[8], h[9], h[6], h[7]);
+  }
   return HS_OK;
 }
 
@@ -455,6 +469,15 @@ int hs_tracker_get_lm_log(hs_tracker* t, int try_idx, int cap, int* n, int* lvl,
       if (inc_norm) inc_norm[i] = lg[3 * i + 2];
     }
   }
+  return HS_OK;
+}
+
+int hs_tracker_last_stats(hs_tracker* t, int try_idx, double* ms, int* passes, long long* point_passes) {
+  if (!t) return tfail(HS_ERR_INVALID, "null tracker");
+  if (try_idx < 0 || try_idx >= t->last_n_tries) return tfail(HS_ERR_INVALID, "no such hypothesis in the last call");
+  if (ms) *ms = t->last_ms;
+  if (passes) *passes = t->h_out[try_idx].passes;
+  if (point_passes) *point_passes = t->h_out[try_idx].point_passes;
   return HS_OK;
 }
 

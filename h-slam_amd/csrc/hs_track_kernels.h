@@ -29,6 +29,8 @@ struct HsTryOut {
   double T[7];
   double aff[2];
   int ok, n_checks, iters, n_warped;
+  int passes;                 // calcRes(+calcGSSSE) passes run
+  long long point_passes;     // sum over the passes of the level's reference points (the roofline's units)
   int check_lvl[HS_TRK_MAXCHECK];
   double check_res[HS_TRK_MAXCHECK];
   double check_flow[HS_TRK_MAXCHECK][3];

@@ -26,6 +26,7 @@
 namespace {
 
 constexpr int TRK_NT = 512;
+constexpr int TRK_B = 4;              // points per thread whose loads are in flight together
 constexpr int TRK_NACC = 45;          // upper triangle of the 9x9 [J | r] normal equations
 constexpr int TRK_NRED = TRK_NACC + 4 + 3;  // + E, flowT, flowRT, flowNum | numE, numSat, numWarped
 
@@ -133,6 +134,9 @@ struct TrkShared {
   double incNorm;
   float lambda, cutoffRep;
   int brk, accept;
+  int passes;
+  long long pointPasses;
+  long long prof[6];  // HS_KTRACE: thread-0 cycles: point loop, reductions, LM step, passes, wave reduce, barrier
 };
 
 // calcRes + calcGSSSE at S.RKi / S.t / S.affLL for level S.lvl; results in S.res / S.H / S.b / S.nWarped
@@ -148,81 +152,123 @@ __device__ void trk_pass(const HsTrackArgs& a, TrkShared& S) {
   const float t0 = S.t[0], t1 = S.t[1], t2 = S.t[2];
   const float aff0 = S.affLL[0], aff1 = S.affLL[1], ags = S.a_gs, b0 = S.b0;
   const float cutoff = S.cutoff, maxEnergy = S.maxEnergy, huberTH = a.huberTH;
+  const long long pc0 = (a.trace && tid == 0) ? clock64() : 0;
   float E = 0.f, sT = 0.f, sRT = 0.f, sN = 0.f;
   int nE = 0, nSat = 0, nW = 0;
   float acc[TRK_NACC];
 #pragma unroll
   for (int q = 0; q < TRK_NACC; q++) acc[q] = 0.f;
-  for (int i = tid; i < n; i += TRK_NT) {
-    const float id = L.pc_id[i], x = L.pc_u[i], y = L.pc_v[i];
-    float pt0 = RKi[0] * x + RKi[1] * y + RKi[2] * 1.f;
-    float pt1 = RKi[3] * x + RKi[4] * y + RKi[5] * 1.f;
-    float pt2 = RKi[6] * x + RKi[7] * y + RKi[8] * 1.f;
-    const float ra0 = pt0, ra1 = pt1, ra2 = pt2;
-    pt0 = pt0 + t0 * id;
-    pt1 = pt1 + t1 * id;
-    pt2 = pt2 + t2 * id;
-    const float u = pt0 / pt2, v = pt1 / pt2;
-    const float Ku = fxl * u + cxl, Kv = fyl * v + cyl;
-    const float new_idepth = id / pt2;
-    if (lvl == 0 && i % 32 == 0) {
-      const float k0 = Ki[0] * x + Ki[1] * y + Ki[2] * 1.f;
-      const float k1 = Ki[3] * x + Ki[4] * y + Ki[5] * 1.f;
-      const float k2 = Ki[6] * x + Ki[7] * y + Ki[8] * 1.f;
-      const float pT0 = k0 + t0 * id, pT1 = k1 + t1 * id, pT2 = k2 + t2 * id;
-      const float pS0 = k0 - t0 * id, pS1 = k1 - t1 * id, pS2 = k2 - t2 * id;
-      const float p30 = ra0 - t0 * id, p31 = ra1 - t1 * id, p32 = ra2 - t2 * id;
-      const float uT = pT0 / pT2, vT = pT1 / pT2;
-      const float KuT = fxl * uT + cxl, KvT = fyl * vT + cyl;
-      const float uT2 = pS0 / pS2, vT2 = pS1 / pS2;
-      const float KuT2 = fxl * uT2 + cxl, KvT2 = fyl * vT2 + cyl;
-      const float u3 = p30 / p32, v3 = p31 / p32;
-      const float Ku3 = fxl * u3 + cxl, Kv3 = fyl * v3 + cyl;
-      float s = (KuT - x) * (KuT - x) + (KvT - y) * (KvT - y);
-      sT += s;
-      s = (KuT2 - x) * (KuT2 - x) + (KvT2 - y) * (KvT2 - y);
-      sT += s;
-      s = (Ku - x) * (Ku - x) + (Kv - y) * (Kv - y);
-      sRT += s;
-      s = (Ku3 - x) * (Ku3 - x) + (Kv3 - y) * (Kv3 - y);
-      sRT += s;
-      sN += 2;
+  // the thread's points i = tid + k TRK_NT in order, TRK_B at a time: every load of a batch (point data, then the
+  // bilinear taps) is issued before any is used, so a batch costs two memory round trips instead of two per point
+  for (int i0 = tid; i0 < n; i0 += TRK_B * TRK_NT) {
+    float id[TRK_B], x[TRK_B], y[TRK_B], refColor[TRK_B];
+#pragma unroll
+    for (int b = 0; b < TRK_B; b++) {
+      const int i = min(i0 + b * TRK_NT, n - 1);
+      id[b] = L.pc_id[i];
+      x[b] = L.pc_u[i];
+      y[b] = L.pc_v[i];
+      refColor[b] = L.pc_col[i];
     }
-    if (!(Ku > 2 && Kv > 2 && Ku < wl - 3 && Kv < hl - 3 && new_idepth > 0)) continue;
-    const float refColor = L.pc_col[i];
-    const float3 hit = interp33(L.img, Ku, Kv, wl);
-    if (!isfinite(hit.x)) continue;
-    const float residual = hit.x - (float)(aff0 * refColor + aff1);
-    const float hw = fabsf(residual) < huberTH ? 1 : huberTH / fabsf(residual);
-    if (fabsf(residual) > cutoff) {
-      E += maxEnergy;
-      nE++;
-      nSat++;
-    } else {
-      E += hw * residual * residual * (2 - hw);
-      nE++;
-      nW++;
-      // calcGSSSE Jacobian of this warped point (Src/CoarseTracker.cpp:282-306)
-      const float dx = hit.y * fxl, dy = hit.z * fyl;
-      float J[9];
-      J[0] = new_idepth * dx;
-      J[1] = new_idepth * dy;
-      J[2] = 0.f - new_idepth * (u * dx + v * dy);
-      J[3] = 0.f - ((u * v) * dx + dy * (1.f + v * v));
-      J[4] = (u * v) * dy + dx * (1.f + u * u);
-      J[5] = u * dy - v * dx;
-      J[6] = ags * (b0 - refColor);
-      J[7] = -1.f;
-      J[8] = residual;
-      int q = 0;
+    float u[TRK_B], v[TRK_B], Ku[TRK_B], Kv[TRK_B], new_idepth[TRK_B];
+    bool inb[TRK_B];
+    float4 tap[TRK_B][4];
+    float fdx[TRK_B], fdy[TRK_B];
 #pragma unroll
-      for (int r = 0; r < 9; r++) {
-        const float Jw = J[r] * hw;
+    for (int b = 0; b < TRK_B; b++) {
+      const int i = i0 + b * TRK_NT;
+      float pt0 = RKi[0] * x[b] + RKi[1] * y[b] + RKi[2] * 1.f;
+      float pt1 = RKi[3] * x[b] + RKi[4] * y[b] + RKi[5] * 1.f;
+      float pt2 = RKi[6] * x[b] + RKi[7] * y[b] + RKi[8] * 1.f;
+      const float ra0 = pt0, ra1 = pt1, ra2 = pt2;
+      pt0 = pt0 + t0 * id[b];
+      pt1 = pt1 + t1 * id[b];
+      pt2 = pt2 + t2 * id[b];
+      u[b] = pt0 / pt2;
+      v[b] = pt1 / pt2;
+      Ku[b] = fxl * u[b] + cxl;
+      Kv[b] = fyl * v[b] + cyl;
+      new_idepth[b] = id[b] / pt2;
+      if (lvl == 0 && i < n && i % 32 == 0) {
+        const float k0 = Ki[0] * x[b] + Ki[1] * y[b] + Ki[2] * 1.f;
+        const float k1 = Ki[3] * x[b] + Ki[4] * y[b] + Ki[5] * 1.f;
+        const float k2 = Ki[6] * x[b] + Ki[7] * y[b] + Ki[8] * 1.f;
+        const float pT0 = k0 + t0 * id[b], pT1 = k1 + t1 * id[b], pT2 = k2 + t2 * id[b];
+        const float pS0 = k0 - t0 * id[b], pS1 = k1 - t1 * id[b], pS2 = k2 - t2 * id[b];
+        const float p30 = ra0 - t0 * id[b], p31 = ra1 - t1 * id[b], p32 = ra2 - t2 * id[b];
+        const float uT = pT0 / pT2, vT = pT1 / pT2;
+        const float KuT = fxl * uT + cxl, KvT = fyl * vT + cyl;
+        const float uT2 = pS0 / pS2, vT2 = pS1 / pS2;
+        const float KuT2 = fxl * uT2 + cxl, KvT2 = fyl * vT2 + cyl;
+        const float u3 = p30 / p32, v3 = p31 / p32;
+        const float Ku3 = fxl * u3 + cxl, Kv3 = fyl * v3 + cyl;
+        float s = (KuT - x[b]) * (KuT - x[b]) + (KvT - y[b]) * (KvT - y[b]);
+        sT += s;
+        s = (KuT2 - x[b]) * (KuT2 - x[b]) + (KvT2 - y[b]) * (KvT2 - y[b]);
+        sT += s;
+        s = (Ku[b] - x[b]) * (Ku[b] - x[b]) + (Kv[b] - y[b]) * (Kv[b] - y[b]);
+        sRT += s;
+        s = (Ku3 - x[b]) * (Ku3 - x[b]) + (Kv3 - y[b]) * (Kv3 - y[b]);
+        sRT += s;
+        sN += 2;
+      }
+      inb[b] = i < n && (Ku[b] > 2 && Kv[b] > 2 && Ku[b] < wl - 3 && Kv[b] < hl - 3 && new_idepth[b] > 0);
+      // bilinear taps (interp33), requested for every point of the batch; out-of-bounds points read pixel 0
+      const float sx = inb[b] ? Ku[b] : 0.f, sy = inb[b] ? Kv[b] : 0.f;
+      const int ix = (int)sx, iy = (int)sy;
+      fdx[b] = sx - ix;
+      fdy[b] = sy - iy;
+      const float4* bp = L.img + ix + iy * wl;
+      tap[b][0] = bp[0];
+      tap[b][1] = bp[1];
+      tap[b][2] = bp[wl];
+      tap[b][3] = bp[wl + 1];
+    }
 #pragma unroll
-        for (int c = r; c < 9; c++) acc[q++] += Jw * J[c];
+    for (int b = 0; b < TRK_B; b++) {
+      if (!inb[b]) continue;
+      const float dx = fdx[b], dy = fdy[b], dxdy = dx * dy;
+      const float w11 = dxdy, w01 = dy - dxdy, w10 = dx - dxdy, w00 = 1 - dx - dy + dxdy;
+      const float4 p00 = tap[b][0], p10 = tap[b][1], p01 = tap[b][2], p11 = tap[b][3];
+      float3 hit;
+      hit.x = w11 * p11.x + w01 * p01.x + w10 * p10.x + w00 * p00.x;
+      hit.y = w11 * p11.y + w01 * p01.y + w10 * p10.y + w00 * p00.y;
+      hit.z = w11 * p11.z + w01 * p01.z + w10 * p10.z + w00 * p00.z;
+      if (!isfinite(hit.x)) continue;
+      const float residual = hit.x - (float)(aff0 * refColor[b] + aff1);
+      const float hw = fabsf(residual) < huberTH ? 1 : huberTH / fabsf(residual);
+      if (fabsf(residual) > cutoff) {
+        E += maxEnergy;
+        nE++;
+        nSat++;
+      } else {
+        E += hw * residual * residual * (2 - hw);
+        nE++;
+        nW++;
+        // calcGSSSE Jacobian of this warped point (Src/CoarseTracker.cpp:282-306)
+        const float gx = hit.y * fxl, gy = hit.z * fyl;
+        const float uu = u[b], vv = v[b], ni = new_idepth[b];
+        float J[9];
+        J[0] = ni * gx;
+        J[1] = ni * gy;
+        J[2] = 0.f - ni * (uu * gx + vv * gy);
+        J[3] = 0.f - ((uu * vv) * gx + gy * (1.f + vv * vv));
+        J[4] = (uu * vv) * gy + gx * (1.f + uu * uu);
+        J[5] = uu * gy - vv * gx;
+        J[6] = ags * (b0 - refColor[b]);
+        J[7] = -1.f;
+        J[8] = residual;
+        int q = 0;
+#pragma unroll
+        for (int r = 0; r < 9; r++) {
+          const float Jw = J[r] * hw;
+#pragma unroll
+          for (int c = r; c < 9; c++) acc[q++] += Jw * J[c];
+        }
       }
     }
   }
+  const long long pc1 = (a.trace && tid == 0) ? clock64() + (long long)(acc[0] * 0.f + acc[44] * 0.f) : 0;
   // wave reductions (fixed xor tree), then the waves in order in fp64
   float vals[TRK_NRED];
 #pragma unroll
@@ -250,7 +296,12 @@ __device__ void trk_pass(const HsTrackArgs& a, TrkShared& S) {
 #pragma unroll
     for (int q = 0; q < TRK_NRED; q++)
       S.red[wv][q] = q < TRK_NACC + 4 ? (double)vals[q] : (double)__float_as_int(vals[q]);
+  const long long pcw = (a.trace && tid == 0) ? clock64() + (long long)(vals[3] * 0.f) : 0;
   __syncthreads();
+  if (a.trace && tid == 0) {
+    S.prof[4] += pcw - pc1;
+    S.prof[5] += clock64() - pcw;
+  }
   if (tid < TRK_NRED) {
     double s = 0.0;
     for (int w = 0; w < TRK_NT / 64; w++) s += S.red[w][tid];
@@ -268,6 +319,8 @@ __device__ void trk_pass(const HsTrackArgs& a, TrkShared& S) {
     S.res[3] = 0;
     S.res[4] = fRT / (fN + 0.1);
     S.res[5] = numSat / (float)numE;
+    S.passes += 1;
+    S.pointPasses += n;
     const int npad = (numW + 3) & ~3;  // buf_warped_n includes the zero padding (quirk kept)
     S.nWarped = npad;
     const double inv = (double)(1.0f / npad);
@@ -285,6 +338,12 @@ __device__ void trk_pass(const HsTrackArgs& a, TrkShared& S) {
         }
         if (c == 8) S.b[r] = (v * inv) * sc[r];
       }
+    if (a.trace) {
+      const long long pc2 = clock64() + (long long)(S.b[7] * 0.0);
+      S.prof[0] += pc1 - pc0;
+      S.prof[1] += pc2 - pc1;
+      S.prof[3] += 1;
+    }
   }
   __syncthreads();
 }
@@ -321,7 +380,11 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
   HsTryOut& out = a.out[h];
   HS_TRACE(a, 0);
   if (a.single_pass) {  // hs_tracker_calc_res
-    if (tid == 0) trk_setup(a, S, a.T_in + 7 * h, a.aff_in + 2 * h, a.pass_lvl, a.pass_cutoff);
+    if (tid == 0) {
+      S.passes = 0;
+      S.pointPasses = 0;
+      trk_setup(a, S, a.T_in + 7 * h, a.aff_in + 2 * h, a.pass_lvl, a.pass_cutoff);
+    }
     __syncthreads();
     trk_pass(a, S);
     if (tid == 0) {
@@ -340,6 +403,9 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
     S.aff[1] = a.aff_in[2 * h + 1];
     out.n_checks = 0;
     out.iters = 0;
+    S.passes = 0;
+    S.pointPasses = 0;
+    for (int q = 0; q < 6; q++) S.prof[q] = 0;
   }
   __syncthreads();
   bool haveRepeated = false;
@@ -369,6 +435,7 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
     for (int iteration = 0; iteration < maxIterations[lvl]; iteration++) {
       __syncthreads();  // every thread has read S.brk of the previous iteration
       if (tid == 0) {
+        const long long lm0 = a.trace ? clock64() : 0;
         out.iters++;
         // Hl = H with the diagonal scaled by (1 + lambda), in LDS (the solver reads it with pivoted indices)
         double* Hl = S.Hl;
@@ -401,6 +468,7 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
         S.incNorm = sqrt(nn);
         S.brk = !(S.incNorm > 1e-3);
         trk_setup(a, S, S.Tn, S.affn, lvl, a.coarseCutoffTH * S.cutoffRep);
+        if (a.trace) S.prof[2] += clock64() + (long long)(S.RKi[4] * 0.f) - lm0;
       }
       __syncthreads();
       trk_pass(a, S);
@@ -463,6 +531,10 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
     if (a.affineOptModeA < 0) out.aff[0] = 0;
     if (a.affineOptModeB < 0) out.aff[1] = 0;
     out.ok = ok ? 1 : 0;
+    out.passes = S.passes;
+    out.point_passes = S.pointPasses;
+    if (a.trace)
+      for (int q = 0; q < 6; q++) a.trace[(size_t)blockIdx.x * 16 + 4 + q] = S.prof[q];
   }
   HS_TRACE(a, 15);
 }

@@ -89,6 +89,7 @@ SIGNATURES = {
     "hs_tracker_track_tries": ([VP, I, VP, VP, VP, C.c_float, VP, VP, VP, VP, VP, VP], I),
     "hs_tracker_get_lm_log": ([VP, I, I, VP, VP, VP, VP, VP], I),
     "hs_tracker_last_ms": ([VP, VP], I),
+    "hs_tracker_last_stats": ([VP, I, VP, VP, VP], I),
     "hs_tracker_set_frame_raw": ([VP, VP, C.c_float], I),
     # include/hs_pyr.h
     "hs_dir_pyramid": ([I, I, I, I, VP, VP, VP], I),

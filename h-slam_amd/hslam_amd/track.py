@@ -121,6 +121,12 @@ class CoarseTracker:
         m = min(n.value, cap)
         return lvl[:m], nr[:m], orr[:m], inc[:m]
 
+    def last_stats(self, try_idx: int = 0):
+        """(device ms, passes, point-passes) of one hypothesis of the last call."""
+        ms, ps, pp = C.c_double(), C.c_int(), C.c_longlong()
+        check(self.lib.hs_tracker_last_stats(self.h, try_idx, C.byref(ms), C.byref(ps), C.byref(pp)))
+        return ms.value, ps.value, pp.value
+
     def last_ms(self):
         ms = C.c_double()
         check(self.lib.hs_tracker_last_ms(self.h, C.byref(ms)))

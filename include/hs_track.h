@@ -75,6 +75,11 @@ int hs_tracker_get_lm_log(hs_tracker* t, int try_idx, int cap, int* n, int* lvl,
 /* device time (ms) of the last track / track_tries call (HIP events on the tracker stream) */
 int hs_tracker_last_ms(hs_tracker* t, double* ms);
 
+/* Work of hypothesis try_idx in the last trackNewestCoarse / try-loop call: the device time of the call (ms), the
+   calcRes(+calcGSSSE) passes it ran and the sum of their levels' reference-point counts (the point-pass units
+   of the tracker's roofline).  Outputs nullable. */
+int hs_tracker_last_stats(hs_tracker* t, int try_idx, double* ms, int* passes, long long* point_passes);
+
 #ifdef __cplusplus
 }
 #endif

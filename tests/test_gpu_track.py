@@ -188,3 +188,45 @@ def test_errors_are_loud(vga):
         g.trackNewestCoarse(SE3().data(), [0, 0], 5, np.full(5, np.nan))   # coarsest must be < 5
     with pytest.raises(HsError):
         CoarseTracker(vga.width, vga.height, vga.K4, 7)
+
+
+@pytest.fixture(scope="module")
+def vga4():
+    """640x480 with the reference's own level rule (Include/CalibData.h:110-115 gives 4 levels here)."""
+    from hslam_amd.scene import make_track_scene
+    return make_track_scene(n_points=2000, n_levels=4)
+
+
+@pytest.mark.parametrize("start", ["identity", "near"])
+def test_track_parity_4_levels(vga4, start):
+    """trackNewestCoarse on the 4-level pyramid: the LM log agrees with the oracle's up to a near-tie, then the
+    final pose / affine / lastResiduals at the bars of the module docstring."""
+    from hslam_amd.se3 import SE3
+    from hslam_amd.track import CoarseTracker
+    from oracle_ffi import OracleTracker
+    g = CoarseTracker(vga4.width, vga4.height, vga4.K4, vga4.n_levels)
+    g.set_scene(vga4)
+    o = OracleTracker(vga4.width, vga4.height, vga4.K4, vga4.n_levels)
+    o.set_scene(vga4)
+    T0 = SE3().data() if start == "identity" else (SE3.exp([0.002, 0, -0.001, 0, 0.001, 0]) *
+                                                   SE3.from_data(vga4.T_true)).data()
+    minRes = np.full(5, np.nan)
+    okg, Tg, ag = g.trackNewestCoarse(T0, [0.0, 0.0], vga4.n_levels - 1, minRes)
+    ro = o.track(T0, [0.0, 0.0], vga4.n_levels - 1, minRes)
+    assert okg == ro["ok"] and okg
+    k = _lm_divergence(g.lm_log(0), o.lm_log())
+    tol_T, tol_a, tol_b = (1e-5, 1e-5, 1e-3) if k is None else (2e-3, 1e-2, 0.5)
+    assert _pose_err(Tg, ro["T"]) < tol_T, k
+    assert abs(ag[0] - ro["aff"][0]) < tol_a and abs(ag[1] - ro["aff"][1]) < tol_b, k
+    lr = g.lastResiduals
+    fin = np.isfinite(ro["lastResiduals"])
+    assert np.array_equal(np.isfinite(lr), fin)
+    assert np.allclose(lr[fin], ro["lastResiduals"][fin], rtol=1e-4 if k is None else 1e-2)
+    # the roofline's work counters: one pass per LM iteration plus >= one calcRes per level
+    ms, passes, point_passes = g.last_stats(0)
+    lv = g.lm_log(0)[0]
+    assert passes >= len(lv) + vga4.n_levels
+    pcn = [len(g.pc(l)["u"]) for l in range(vga4.n_levels)]
+    assert sum(pcn[l] * int((lv == l).sum()) for l in range(vga4.n_levels)) + sum(pcn) <= point_passes
+    assert ms > 0
+    g.close()
