@@ -1090,6 +1090,61 @@ int hs_ba_get_points(hs_ctx* c, float* idepth, float* step, float* HdiF, float* 
   return HS_OK;
 }
 
+// EnergyFunctional::calcLEnergyF_MT / calcMEnergyF (Src/EnergyFunctional.cpp:277-368), the energies System::optimize
+// only evaluates without setting_forceAceptStep (Src/FullSystemOptimize.cpp:337-345,565-572): the frame and calib
+// prior terms and calcMEnergyF on the host in fp64 (the deltas of the current state), the points' prior term on
+// the device (hs_k_lenergy).
+int hs_ba_calc_energies(hs_ctx* c, double* energyL, double* energyM) {
+  if (!c || c->nF == 0) return fail(HS_ERR_STATE, "no window");
+  HS_HIP(hipSetDevice(c->device));
+  HS_TRY(fetch_state(c));
+  const HsDevState& S = *c->h_state;
+  const int nF = c->nF, n = c->dim();
+  double EL = 0.0;
+  for (int f = 0; f < nF; f++) {  // delta_prior .* prior . delta_prior
+    double s = 0.0;
+    for (int i = 0; i < 8; i++) s += S.frames[f].delta_prior[i] * S.frames[f].prior[i] * S.frames[f].delta_prior[i];
+    EL += s;
+  }
+  float cd[4];
+  for (int i = 0; i < 4; i++) cd[i] = (float)S.calib.value_minus_value_zero[i];  // cDeltaF
+  {
+    const float cp = (float)c->P.initialCalibHessian;  // cPriorF
+    float s = 0.f;
+    for (int i = 0; i < 4; i++) s += cd[i] * cp * cd[i];
+    EL += s;
+  }
+  if (c->nP > 0) {
+    float* d_chunk = nullptr;
+    double* d_out = nullptr;
+    HS_TRY(dalloc(&d_chunk, (size_t)(c->nP + 49) / 50));
+    HS_TRY(dalloc(&d_out, 1));
+    hipLaunchKernelGGL(hs_k_lenergy, dim3(1), dim3(256), 0, c->stream, c->nP, c->d_idepth, c->d_idepth_zero,
+                       c->d_priorF, d_chunk, d_out);
+    HS_HIP(hipGetLastError());
+    double ep = 0.0;
+    HS_HIP(hipMemcpyAsync(&ep, d_out, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HS_HIP(hipStreamSynchronize(c->stream));
+    (void)hipFree(d_chunk);
+    (void)hipFree(d_out);
+    EL += ep;
+  }
+  // calcMEnergyF: delta . (2 bM + HM delta), delta = getStitchedDeltaF (Src/EnergyFunctional.cpp:842-846)
+  std::vector<double> d(n);
+  for (int i = 0; i < 4; i++) d[i] = (double)cd[i];
+  for (int f = 0; f < nF; f++)
+    for (int i = 0; i < 8; i++) d[4 + 8 * f + i] = S.frames[f].delta[i];
+  double EM = 0.0;
+  for (int r = 0; r < n; r++) {
+    double hd = 0.0;
+    for (int k = 0; k < n; k++) hd += c->HM[(size_t)r * n + k] * d[k];
+    EM += d[r] * (2 * c->bM[r] + hd);
+  }
+  if (energyL) *energyL = EL;
+  if (energyM) *energyM = EM;
+  return HS_OK;
+}
+
 int hs_ba_get_frames(hs_ctx* c, double* state, float* energyTH, double* pose7, double* calib4) {
   if (!c || c->nF == 0) return fail(HS_ERR_STATE, "no window");
   HS_HIP(hipSetDevice(c->device));

@@ -2010,3 +2010,28 @@ __global__ void hs_k_apply_step(int n, const float* step, float* idepth, float* 
     idepth_zero[p] = nid;
   }
 }
+
+// EnergyFunctional::calcLEnergyPt's point term (Src/EnergyFunctional.cpp:289-347) for the window's points: per
+// IndexThreadReduce chunk of 50 points an Accumulator11 sums deltaF^2 priorF in fp32 (at most 50 updates: no
+// shiftUp; finish() adds three zero lanes), and the chunk values add up in fp64 in chunk order -- the
+// single-thread reference's result.  One block; the window holds no linearized residuals (the marginalization
+// pass consumes them), so the residual terms are empty.
+__global__ __launch_bounds__(256) void hs_k_lenergy(int n, const float* idepth, const float* idepth_zero,
+                                                    const float* priorF, float* chunk, double* out) {
+  const int tid = threadIdx.x;
+  const int nc = (n + 49) / 50;
+  for (int c = tid; c < nc; c += 256) {
+    float A = 0.f;
+    for (int i = 50 * c; i < min(n, 50 * c + 50); i++) {
+      const float dF = idepth[i] - idepth_zero[i];
+      A += dF * dF * priorF[i];
+    }
+    chunk[c] = A;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double s = 0.0;
+    for (int c = 0; c < nc; c++) s += (double)chunk[c];
+    out[0] = s;
+  }
+}

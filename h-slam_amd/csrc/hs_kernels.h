@@ -185,3 +185,5 @@ __global__ void hs_k_stitch(HsStitchArgs a);
 __global__ void hs_k_solve(HsSolveArgs a);
 __global__ void hs_k_resub(HsResubArgs a);
 __global__ void hs_k_apply_step(int n, const float* step, float* idepth, float* idepth_zero);
+__global__ void hs_k_lenergy(int n, const float* idepth, const float* idepth_zero, const float* priorF, float* chunk,
+                             double* out);

@@ -67,6 +67,7 @@ SIGNATURES = {
     "hs_ba_optimize": ([VP, I, I, VP, VP], I),
     "hs_ba_iterate": ([VP, I, I, VP], I),
     "hs_ba_fix_linearization": ([VP, VP, VP, VP, VP, VP], I),
+    "hs_ba_calc_energies": ([VP, VP, VP], I),
     "hs_ba_get_system": ([VP, I, VP, VP], I),
     "hs_ba_get_residuals": ([VP] * 7, I),
     "hs_ba_get_points": ([VP] * 5, I),

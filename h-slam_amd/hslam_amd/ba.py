@@ -58,7 +58,11 @@ class BAWindow:
         arrs = [np.ascontiguousarray(a[p0:p1], np.float32) for a in (s.pt_u, s.pt_v, s.pt_idepth, s.pt_idepth_zero)]
         col = np.ascontiguousarray(s.pt_color[p0:p1], np.float32)
         wgt = np.ascontiguousarray(s.pt_weights[p0:p1], np.float32)
-        pts = hs_points(p1 - p0, ptr(host), *[ptr(a) for a in arrs], ptr(col), ptr(wgt), None)
+        # optional per-point depth priors (PointHessian::hasDepthPrior): scene.pt_has_prior (uint8), else none
+        hp = getattr(s, "pt_has_prior", None)
+        hp = None if hp is None else np.ascontiguousarray(hp[p0:p1], np.uint8)
+        self._keep_prior = hp
+        pts = hs_points(p1 - p0, ptr(host), *[ptr(a) for a in arrs], ptr(col), ptr(wgt), None if hp is None else ptr(hp))
         rp = np.ascontiguousarray(s.res_point[sel_r] - p0, np.int32)
         rt = np.ascontiguousarray(s.res_target[sel_r], np.int32)
         rs = hs_residuals(len(rp), ptr(rp), ptr(rt), None)
@@ -142,6 +146,12 @@ class BAWindow:
         e = C.c_double()
         check(self.lib.hs_ba_fix_linearization(self.h, C.byref(e), ptr(drop), ptr(rb), ptr(ng), ptr(hdi)))
         return dict(energy=e.value, drop=drop, maxRelBaseline=rb, numGoodResiduals=ng, HdiF=hdi)
+
+    def calcEnergies(self):
+        """EnergyFunctional::calcLEnergyF_MT / calcMEnergyF (dormant under setting_forceAceptStep): (L, M)."""
+        el, em = C.c_double(), C.c_double()
+        check(self.lib.hs_ba_calc_energies(self.h, C.byref(el), C.byref(em)))
+        return el.value, em.value
 
     # --------------------------------------------------------------- read-back
     def system(self, which):

@@ -24,6 +24,8 @@
  *   hs_ba_optimize              System::optimize GN loop (Src/FullSystemOptimize.cpp:362-494),
  *                               setting_forceAceptStep = true.
  *   hs_ba_iterate               the loop body of System::optimize (Src/FullSystemOptimize.cpp:420-494)
+ *   hs_ba_calc_energies         calcLEnergyF_MT / calcMEnergyF (dormant under setting_forceAceptStep)
+ *                               (Src/EnergyFunctional.cpp:277-368)
  *   hs_ba_fix_linearization     System::optimize's tail: newest frame setEvalPT, setAdjointsF,
  *                               setPrecalcValues, linearizeAll(true) (Src/FullSystemOptimize.cpp:498-516,
  *                               19-52, 102-160)
@@ -94,6 +96,13 @@ int hs_ba_iterate(hs_ctx* ctx, int first_iteration, int n_iters, double* energie
    All outputs nullable.  The context's window afterwards is the fixed one (evalPT moved, system re-stitched). */
 int hs_ba_fix_linearization(hs_ctx* ctx, double* energy_out, uint8_t* drop_out, float* maxRelBaseline,
                             int* numGoodResiduals, float* HdiF_out);
+
+/* EnergyFunctional::calcLEnergyF_MT and calcMEnergyF (Src/EnergyFunctional.cpp:277-368) on the current state: the
+   energies System::optimize evaluates only when setting_forceAceptStep is off (System::calcLEnergy /
+   calcMEnergy return 0 otherwise, Src/FullSystemOptimize.cpp:337-345,565-572) -- the caller keeps that flag.
+   energyL: frame priors + calib prior + the points' depth priors (the window holds no linearized residuals);
+   energyM: delta . (2 bM + HM delta).  On a multi-rank window energyL's point term is this rank's share. */
+int hs_ba_calc_energies(hs_ctx* ctx, double* energyL, double* energyM);
 
 /* which: 0 = HA/bA, 1 = HL/bL (priors), 2 = H_sc/b_sc. H: dim*dim row-major, b: dim. */
 int hs_ba_get_system(hs_ctx* ctx, int which, double* H, double* b);

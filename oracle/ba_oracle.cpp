@@ -1256,6 +1256,80 @@ struct BA {
            sqrtf(sumT) * sumNID < 0.00005 * th;
   }
 
+  // EnergyFunctional::calcLEnergyF_MT (Src/EnergyFunctional.cpp:289-368): frame priors, calib prior, and per
+  // IndexThreadReduce chunk of 50 points an Accumulator11 over the linearized active residuals' (2 res_toZero +
+  // J delta) J delta and the point prior deltaF^2 priorF
+  double calcLEnergy() {
+    double E = 0;
+    for (const auto& f : frames) {
+      double s = 0;
+      for (int i = 0; i < 8; i++) s += f.delta_prior[i] * f.prior[i] * f.delta_prior[i];
+      E += s;
+    }
+    {
+      float s = 0.f;
+      for (int i = 0; i < 4; i++) s += cDeltaF[i] * cPriorF[i] * cDeltaF[i];
+      E += s;
+    }
+    auto body = [this](int mn, int mx, double* st, int) {
+      float A = 0.f;  // Accumulator11, lane 0 (updateSingle / updateSingleNoShift); <= 50 updates: no shiftUp
+      float lanes[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int i = mn; i < mx; i++) {
+        const PointO& p = points[i];
+        const float dd = p.deltaF;
+        for (int ri : p.residuals) {
+          const ResO& r = res[ri];
+          if (!r.isLinearized || !r.isActive()) continue;
+          const float* dp = &adHTdeltaF[(r.host + nF * r.target) * 8];
+          float jx = 0, jy = 0, cx = 0, cy = 0;
+          for (int k = 0; k < 6; k++) { jx += r.J.Jpdxi[0][k] * dp[k]; jy += r.J.Jpdxi[1][k] * dp[k]; }
+          for (int k = 0; k < 4; k++) { cx += r.J.Jpdc[0][k] * cDeltaF[k]; cy += r.J.Jpdc[1][k] * cDeltaF[k]; }
+          const float Jpx = jx + cx + r.J.Jpdd[0] * dd, Jpy = jy + cy + r.J.Jpdd[1] * dd;
+          for (int k = 0; k < PN; k++) {  // updateSSENoShift over pattern quads: lane k % 4
+            float Jd = r.J.JIdx[0][k] * Jpx;
+            Jd = Jd + r.J.JIdx[1][k] * Jpy;
+            Jd = Jd + r.J.JabF[0][k] * dp[6];
+            Jd = Jd + r.J.JabF[1][k] * dp[7];
+            float r0 = r.res_toZeroF[k];
+            r0 = r0 + r0;
+            r0 = r0 + Jd;
+            lanes[k % 4] += Jd * r0;
+          }
+        }
+        lanes[0] += p.deltaF * p.deltaF * p.priorF;  // updateSingle
+      }
+      (void)A;
+      st[0] += (double)(((lanes[0] + lanes[1]) + lanes[2]) + lanes[3]);  // finish(): shiftUp(true), lane sum
+    };
+    if (mt) {
+      pool->reduce([&](int mn, int mx, double* st, int t) { body(mn, mx, st, t); }, 0, (int)points.size(), 50);
+      return E + pool->stats[0];
+    }
+    double s = 0;
+    for (int i = 0; i < (int)points.size(); i += 50) {
+      double st[1] = {0};
+      body(i, std::min(i + 50, (int)points.size()), st, 0);
+      s += st[0];
+    }
+    return E + s;
+  }
+
+  // EnergyFunctional::calcMEnergyF (Src/EnergyFunctional.cpp:277-286): delta . (2 bM + HM delta)
+  double calcMEnergy() {
+    const int n = dim();
+    std::vector<double> d(n);
+    for (int i = 0; i < 4; i++) d[i] = (double)cDeltaF[i];
+    for (int f = 0; f < nF; f++)
+      for (int i = 0; i < 8; i++) d[4 + 8 * f + i] = frames[f].delta[i];
+    double E = 0;
+    for (int r = 0; r < n; r++) {
+      double hd = 0;
+      for (int k = 0; k < n; k++) hd += HM[r * n + k] * d[k];
+      E += d[r] * (2 * bM[r] + hd);
+    }
+    return E;
+  }
+
   // System::optimize's tail (Src/FullSystemOptimize.cpp:498-509): the newest frame's setEvalPT(PRE_worldToCam,
   // (0,..,0, a, b, 0, 0)) (Include/Frame.h:213-218), setAdjointsF, setPrecalcValues, then linearizeAll(true)
   // (:19-52, :102-124): linearize + applyRes(true) per active residual; for residuals still active the point's
@@ -1425,6 +1499,14 @@ double hso_ba_linearize_all(void* h, int reset) {
   return ba->linearizeAll();
 }
 void hso_ba_apply_res(void* h) { ((BA*)h)->applyResAll(); }
+
+/* calcLEnergyF_MT / calcMEnergyF on the current state (setDeltaF first, as the reference's EFDeltaValid asserts) */
+void hso_ba_calc_energies(void* h, double* L, double* M) {
+  BA* ba = (BA*)h;
+  ba->setDeltaF();
+  if (L) *L = ba->calcLEnergy();
+  if (M) *M = ba->calcMEnergy();
+}
 
 /* System::optimize's tail + linearizeAll(true): returns its energy; relBL / nGood [n points] updated in place,
    drop [n residuals] set to 1 for the toRemove list (entries of other residuals untouched) */

@@ -91,6 +91,7 @@ def load(fast=False):
     lib.hso_ba_apply_res.argtypes = [vp]
     lib.hso_ba_fix_linearization.argtypes = [vp, vp, vp, vp]
     lib.hso_ba_fix_linearization.restype = C.c_double
+    lib.hso_ba_calc_energies.argtypes = [vp, vp, vp]
     lib.hso_ba_accumulate.argtypes = [vp, C.c_int, vp, vp]
     lib.hso_ba_solve_system.argtypes = [vp, C.c_int, vp]
     lib.hso_ba_backup_state.argtypes = [vp]
@@ -199,8 +200,11 @@ class OracleBA:
                     color=np.ascontiguousarray(scene.pt_color, np.float32),
                     weights=np.ascontiguousarray(scene.pt_weights, np.float32))
         self._keep += list(arrs.values())
+        hp = getattr(scene, "pt_has_prior", None)
+        hp = None if hp is None else np.ascontiguousarray(hp, np.uint8)
+        self._keep.append(hp)
         pts = hs_points(scene.n_points, *[_p(arrs[k]) for k in ("host", "u", "v", "idepth", "idepth_zero", "color",
-                                                                 "weights")], None)
+                                                                 "weights")], _p(hp))
         rp = np.ascontiguousarray(scene.res_point, np.int32)
         rt = np.ascontiguousarray(scene.res_target, np.int32)
         self._keep += [rp, rt]
@@ -243,6 +247,12 @@ class OracleBA:
         drop = np.zeros(self.scene.n_res, np.uint8)
         e = self.lib.hso_ba_fix_linearization(self.h, _p(rb), _p(ng), _p(drop))
         return e, drop, rb, ng
+
+    def calc_energies(self):
+        """EnergyFunctional::calcLEnergyF_MT / calcMEnergyF: (L, M)."""
+        el, em = C.c_double(), C.c_double()
+        self.lib.hso_ba_calc_energies(self.h, C.byref(el), C.byref(em))
+        return el.value, em.value
 
     def accumulate(self, which):
         H = np.zeros((self.dim, self.dim))

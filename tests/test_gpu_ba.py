@@ -385,3 +385,33 @@ def test_graph_replay_matches_eager(scene2k):
             os.environ.pop("HS_GRAPH", None)
     for a, b in zip(*res):
         assert np.array_equal(a, b)
+
+
+def test_dormant_energies(scene_small):
+    """EnergyFunctional::calcLEnergyF_MT / calcMEnergyF (Src/EnergyFunctional.cpp:277-368), the energies only a
+    setting_forceAceptStep=false System evaluates: frame / calib priors, the points' depth priors (a third of the
+    points carry one, idepth_zero != idepth) and delta . (2 bM + HM delta) with a random marginal prior; at the
+    window's initial state (rel 1e-12: fp64 sums in another order) and after three GN iterations (the trajectory
+    tolerance)."""
+    import copy
+    s = copy.copy(scene_small)
+    rng = np.random.default_rng(3)
+    s.pt_has_prior = (rng.random(s.n_points) < 0.33).astype(np.uint8)
+    s.pt_idepth_zero = (s.pt_idepth * (1 + 0.01 * rng.standard_normal(s.n_points))).astype(np.float32)
+    sz = np.array(s.frames_state_zero, dtype=np.float64)
+    sz[:, :8] += 1e-3 * rng.standard_normal((sz.shape[0], 8))  # a linearization point away from the state
+    s.frames_state_zero = sz
+    g, o = _pair(s)
+    n = g.dim
+    A = rng.standard_normal((n, n))
+    HM = A @ A.T * 1e-2
+    bM = rng.standard_normal(n) * 1e-2
+    g.set_marginal_prior(HM, bM)
+    o.set_marginal_prior(HM, bM)
+    eg, eo = g.calcEnergies(), o.calc_energies()
+    assert eo[0] > 0 and eo[1] != 0
+    assert abs(eg[0] - eo[0]) <= 1e-12 * abs(eo[0]) and abs(eg[1] - eo[1]) <= 1e-12 * abs(eo[1])
+    g.optimize(3)
+    o.optimize(3)
+    eg, eo = g.calcEnergies(), o.calc_energies()
+    assert abs(eg[0] - eo[0]) <= 1e-3 * abs(eo[0]) + 1e-9 and abs(eg[1] - eo[1]) <= 1e-3 * abs(eo[1]) + 1e-9
