@@ -93,3 +93,13 @@ def test_built_libraries_are_current():
     for so in ("liboracle.so", "liboracle_fast.so"):
         p = os.path.join(ora, "_build", so)
         assert os.path.getmtime(p) >= newest(ora_src), f"{so} is stale: make -C oracle"
+
+
+def test_c_caller_is_built_against_the_headers():
+    """tests/c/ba_caller.c is a plain C99 program (gcc -Wall -Wextra, no HIP headers) against include/hs_ba.h, built
+    by h-slam_amd/csrc/Makefile next to the library: the boundary compiles and links from C.  The GPU suite runs it
+    (tests/test_gpu_c_caller.py)."""
+    exe = os.path.join(ROOT, "h-slam_amd", "lib", "ba_caller")
+    src = os.path.join(ROOT, "tests", "c", "ba_caller.c")
+    assert os.path.exists(exe), "make -C h-slam_amd/csrc"
+    assert os.path.getmtime(exe) >= max(os.path.getmtime(src), os.path.getmtime(os.path.join(ROOT, "include", "hs_ba.h")))
