@@ -271,8 +271,9 @@ class BAScene:
         rsel = remap[self.res_point] >= 0
         out = copy.copy(self)
         for name in ("pt_host", "pt_u", "pt_v", "pt_idepth", "pt_idepth_zero", "pt_color", "pt_weights",
-                     "pt_idepth_true"):
-            setattr(out, name, np.ascontiguousarray(getattr(self, name)[sel]))
+                     "pt_idepth_true", "pt_has_prior"):
+            if getattr(self, name, None) is not None:
+                setattr(out, name, np.ascontiguousarray(getattr(self, name)[sel]))
         out.res_point = remap[self.res_point[rsel]].astype(np.int32)
         out.res_target = np.ascontiguousarray(self.res_target[rsel])
         return out
