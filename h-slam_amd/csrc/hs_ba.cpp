@@ -37,7 +37,7 @@ int fail(int code, const std::string& msg) {
 
 constexpr int kLogCap = 4096;     // energies logged on the device per optimize / iterate call
 constexpr int kEventIters = 128;  // iterations timed with HIP events per call
-constexpr int kLinBlocksTarget = 512;  // linearize blocks of a window (points per wave grows beyond that)
+constexpr int kLinBlocksTarget = 256;  // linearize blocks of a window (points per wave grows beyond that)
 }  // namespace
 
 #define HS_HIP(x)                                                                                  \
@@ -232,7 +232,9 @@ static int fetch_state(hs_ctx* c) {
 }
 
 // ---------------------------------------------------------------- launches (asynchronous)
-static size_t lin_lds(const hs_ctx* c) { return (size_t)4 * c->ne * 64 * sizeof(float) + 12 * sizeof(double); }
+static size_t lin_lds(const hs_ctx* c) {
+  return (size_t)HS_LIN_NW * c->ne * 64 * sizeof(float) + 3 * HS_LIN_NW * sizeof(double);
+}
 
 static int launch_linearize(hs_ctx* c, int fuse, bool marg = false, bool accumulate = true, bool fix = false) {
   HsLinArgs a;
@@ -279,7 +281,7 @@ static int launch_linearize(hs_ctx* c, int fuse, bool marg = false, bool accumul
   a.trace = c->d_tr_lin;
   if (c->nblk > 0) {
     auto k = c->exact ? (fix ? hs_k_lin_exact_fix : hs_k_lin_exact) : (fix ? hs_k_lin_fix : hs_k_lin);
-    hipLaunchKernelGGL(k, dim3(c->nblk), dim3(256), lin_lds(c), c->stream, a);
+    hipLaunchKernelGGL(k, dim3(c->nblk), dim3(HS_LIN_NT), lin_lds(c), c->stream, a);
   }
   HS_HIP(hipGetLastError());
   std::swap(c->d_p_HdiF, c->d_p_HdiF_alt);
@@ -400,6 +402,15 @@ static int dump_one(const char* name, const long long* d, int nblocks, double ti
   if (solve && h[0] && h[24] && h[25] && h[15] > h[0])  // slots 24/25: shader clock
     std::fprintf(stderr, "[hs trace] %-12s shader clock %.0f MHz\n", name,
                  (double)(h[25] - h[24]) / ((h[15] - h[0]) * tick_us));
+  if (std::string(name) == "stitch") {  // per block: start offset and end of the block (us from the first start)
+    std::fprintf(stderr, "[hs trace] stitch blocks (start..end us):");
+    for (int b = 0; b < nblocks; b++)
+      if (h[b * 16] && h[b * 16 + 15])
+        std::fprintf(stderr, " %d:%.1f/%.1f/%.1f/%.1f", b, (h[b * 16] - t0) * tick_us,
+                     h[b * 16 + 1] ? (h[b * 16 + 1] - t0) * tick_us : -1.0, h[b * 16 + 2] ? (h[b * 16 + 2] - t0) * tick_us : -1.0,
+                     (h[b * 16 + 15] - t0) * tick_us);
+    std::fprintf(stderr, "\n");
+  }
   for (int k = 1; k < 16; k++) {
     std::vector<double> v;
     for (int b = 0; b < nblocks; b++)
@@ -652,7 +663,7 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
     }
     c->host_pt_begin[nF] = nP;
   }
-  // hs_k_lin partitioning.  Production: every host's points are split into blocks of 4 waves x ppw points
+  // hs_k_lin partitioning.  Production: every host's points are split into blocks of HS_LIN_NW waves x ppw points
   // (ppw grows with the window so the grid stays near kLinBlocksTarget blocks; env HS_LIN_PPW overrides).
   // HS_ACC_EXACT=1: one block per host whose wave 0 takes every point in order = the single-thread reference's
   // fp32 accumulator sums (no shiftUp emulation: at most 1000 points per host).
@@ -661,13 +672,13 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
   c->ne = hs_ne(c->exact);
   c->Q = (c->ne * 64 + 255) / 256;
   c->blk_begin.assign(nF + 1, 0);
-  int ppw = std::max(1, (nP + 4 * kLinBlocksTarget - 1) / (4 * kLinBlocksTarget));
+  int ppw = std::max(1, (nP + HS_LIN_NW * kLinBlocksTarget - 1) / (HS_LIN_NW * kLinBlocksTarget));
   if (const char* e = std::getenv("HS_LIN_PPW")) ppw = std::max(1, std::atoi(e));
-  c->W = c->exact ? 1 : 4;
+  c->W = c->exact ? 1 : HS_LIN_NW;
   for (int h = 0; h < nF; h++) {
     const int nh = c->host_pt_begin[h + 1] - c->host_pt_begin[h];
     if (c->exact && nh > 1000) return fail(HS_ERR_INVALID, "HS_ACC_EXACT supports at most 1000 points per host");
-    const int nb = nh == 0 ? 0 : (c->exact ? 1 : (nh + 4 * ppw - 1) / (4 * ppw));
+    const int nb = nh == 0 ? 0 : (c->exact ? 1 : (nh + HS_LIN_NW * ppw - 1) / (HS_LIN_NW * ppw));
     c->blk_begin[h + 1] = c->blk_begin[h] + nb;
   }
   c->nblk = c->blk_begin[nF];

@@ -598,7 +598,7 @@ __device__ __forceinline__ void acc_point(LinAcc<kExact>& A, const LinPt& P, int
 
 template <bool kExact, bool kFix>
 __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
-  extern __shared__ float lin_stage[];  // [4 waves][ne][64] fp32 partials, then [4][3] fp64 energies
+  extern __shared__ float lin_stage[];  // [HS_LIN_NW waves][ne][64] fp32 partials, then [HS_LIN_NW][3] fp64 energies
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int b = blockIdx.x;
   int h = 0;  // the block's host: from the kernel-argument block boundaries, no load
@@ -636,7 +636,7 @@ __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
 #pragma unroll
   for (int i = 0; i < 5; i++) my[(HS_E_TOP + LinAcc<kExact>::ND + i) * 64 + lane] = A.E[i];
   my[(NE - 1) * 64 + lane] = A.C;
-  double* se = reinterpret_cast<double*>(lin_stage + 4 * NE * 64);
+  double* se = reinterpret_cast<double*>(lin_stage + HS_LIN_NW * NE * 64);
   if (lane == 0) {
     se[wv * 3 + 0] = A.e;
     se[wv * 3 + 1] = A.sid;
@@ -644,7 +644,7 @@ __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
   }
   __syncthreads();
   float* out = a.part + (size_t)b * NE * 64;
-  for (int i = tid; i < NE * 64; i += 256) {
+  for (int i = tid; i < NE * 64; i += HS_LIN_NT) {
     float s = lin_stage[i];
     for (int w = 1; w < a.W; w++) s += lin_stage[w * NE * 64 + i];
     out[i] = s;
@@ -658,10 +658,10 @@ __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
 }
 }  // namespace
 
-__global__ __launch_bounds__(256) void hs_k_lin(HsLinArgs a) { lin_block<false, false>(a); }
-__global__ __launch_bounds__(256) void hs_k_lin_exact(HsLinArgs a) { lin_block<true, false>(a); }
-__global__ __launch_bounds__(256) void hs_k_lin_fix(HsLinArgs a) { lin_block<false, true>(a); }
-__global__ __launch_bounds__(256) void hs_k_lin_exact_fix(HsLinArgs a) { lin_block<true, true>(a); }
+__global__ __launch_bounds__(HS_LIN_NT) void hs_k_lin(HsLinArgs a) { lin_block<false, false>(a); }
+__global__ __launch_bounds__(HS_LIN_NT) void hs_k_lin_exact(HsLinArgs a) { lin_block<true, false>(a); }
+__global__ __launch_bounds__(HS_LIN_NT) void hs_k_lin_fix(HsLinArgs a) { lin_block<false, true>(a); }
+__global__ __launch_bounds__(HS_LIN_NT) void hs_k_lin_exact_fix(HsLinArgs a) { lin_block<true, true>(a); }
 
 // =====================================================================================================
 // reduce + stitch: (host, chunk) blocks sum the host's block partials in block order; the last chunk block of a
@@ -1138,9 +1138,20 @@ __global__ __launch_bounds__(ST_NT) void hs_k_stitch(HsStitchArgs a) {
       __syncthreads();
       // Schur terms: tS[h] = adT[h,f] D_h(f,f) adT[h,f]^T (h != f), tS[8 + t1] = adH[f,t1] sum_t2 D_f(t1,t2) adH[f,t2]^T
       // top terms: tA[t] host pairs (f, t), tA[8 + h] target pairs (h, f)
-      for (int x = wv; x < 4 * nF; x += ST_NW) {
-        const int y = x % nF, kind = x / nF;
-        if (y == f) continue;
+      // balanced over the 16 waves: the 7 heavy host-f terms (8 products each) on waves 0-6, the 21 two-product
+      // sandwiches round-robin on waves 7-15 (at most 3 each); every term is still formed by one wave
+      const int nHeavy = nF - 1, nSmall = 3 * (nF - 1), nSW = ST_NW - nHeavy;
+      for (int x = (wv < nHeavy ? wv : nHeavy + (wv - nHeavy)); x < nHeavy + nSmall;
+           x += (wv < nHeavy ? nHeavy + nSmall : nSW)) {
+        int kind, y;
+        if (x < nHeavy) {
+          kind = 1;
+          y = x + (x >= f ? 1 : 0);
+        } else {
+          const int sI = x - nHeavy, yi = sI % (nF - 1);
+          kind = sI / (nF - 1) == 0 ? 0 : (sI / (nF - 1) == 1 ? 2 : 3);
+          y = yi + (yi >= f ? 1 : 0);
+        }
         if (kind == 0) {
           tS[y * 64 + lane] = sandwich8(aTf + y * 64, Dx + y * 64, aTf + y * 64, sw, lane);
         } else if (kind == 1) {

@@ -9,6 +9,8 @@
 
 constexpr int HS_SOLVE_NT = 512;   // hs_k_solve workgroup size
 constexpr int HS_STITCH_NT = 1024; // hs_k_stitch workgroup size
+constexpr int HS_LIN_NW = 8;       // hs_k_lin waves per block (production: each takes points; exact mode: wave 0)
+constexpr int HS_LIN_NT = 64 * HS_LIN_NW;
 constexpr int HS_NNS = 7;         // gauge nullspaces: 6 pose + 1 scale (System::getNullspaces)
 
 // Window state owned by the device between GN iterations (updated by hs_k_solve).
