@@ -124,11 +124,54 @@ struct LinPt {
 // AccumulatedTopHessianSSE::addPoint<0> / AccumulatedSCHessianSSE::addPoint (Src/AccumulatedTopHessian.cpp:21-141,
 // Src/AccumulatedSCHessian.cpp:10-33).  Writes the per-residual / per-point state; returns what the
 // accumulators need.  Wave-uniform p.
+// The per-point global inputs of lin_point (lane (t, k)'s view), loaded one point ahead by lin_block so the loads
+// of point p + W are in flight while point p is linearized; every load is unconditional (clamped indices).
+struct LinIn {
+  float idep, idep0, pu, pv;
+  int res;            // res_of_slot of the lane's slot (< 0: none)
+  int st_raw;         // ResState of the slot
+  float oldE_raw, oldNewE_raw;
+  float colorK, weightK;
+  uint2 ro2;          // the point's 8 residual-list slots (int8 each)
+  unsigned fm;        // previous linearization's active mask
+  float jpj, bds, hdi;
+  float4 hcd;
+};
+__device__ __forceinline__ void lin_load(const HsLinArgs& a, int p, int lane, LinIn& in) {
+  const int t = lane >> 3, k = lane & 7, sl = p * 8 + t;
+  in.idep = a.idepth[p];
+  in.idep0 = a.idepth_zero[p];
+  in.pu = a.u[p];
+  in.pv = a.v[p];
+  in.res = a.res_of_slot[sl];
+  in.st_raw = (int)a.r_state[sl];
+  in.oldE_raw = a.r_energy[sl];
+  in.oldNewE_raw = a.r_newEnergy[sl];
+  in.colorK = a.color[p * 8 + k];
+  in.weightK = a.weight[p * 8 + k];
+  in.ro2 = reinterpret_cast<const uint2*>(a.res_order)[p];
+  in.fm = a.p_actmask[p];
+  in.jpj = a.p_JpJdF[sl * 8 + k];
+  in.bds = a.p_bdSumF[p];
+  in.hdi = a.p_HdiF_prev[p];
+  in.hcd = reinterpret_cast<const float4*>(a.p_Hcd)[p];
+}
+
+// per-block constants of lin_point, staged in LDS once per block: the host's precalc records (by target slot),
+// the frames' thresholds, xAd[h][t][k] and the calib step
+struct LinConst {
+  HsPrecalc pre[HS_MAXF];
+  float th[HS_MAXF];
+  float xad[HS_MAXF * 8];
+  float cs[4];
+};
+
 // kFix: System::linearizeAll(true)'s bookkeeping (Src/FullSystemOptimize.cpp:26-50): for every residual still active
 // after applyRes the point's maxRelBaseline = max(relBS) and numGoodResiduals++ (isNew is never cleared in the
 // reference, Include/OptimizationClasses.h:98,112), in the point's residual-list order.
 template <bool kFix>
-__device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int lane, LinPt& o) {
+__device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int lane, const LinIn& in,
+                                          const LinConst& K, LinPt& o) {
   const int t = lane >> 3;  // target slot
   const int k = lane & 7;   // pattern pixel
   const int nF = a.nF;
@@ -148,43 +191,36 @@ __device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int 
     o.jj = 0.f; o.active = false; o.mask = 0u; o.HdiF = 0.f; o.bdSumF = 0.f;
     o.Hcd[0] = o.Hcd[1] = o.Hcd[2] = o.Hcd[3] = 0.f;
     o.eSum = 0.0;
-    o.idep = a.idepth[p];
+    o.idep = in.idep;
     o.xk = o.yk = o.xr10 = o.yr10 = o.xc10 = o.yc10 = o.xr14 = o.yr14 = o.t014 = o.t114 = o.br15 = 0.f;
     o.hcr = o.hcc = 0.f;
     return;
   }
-  // everything the linearization reads is loaded up front, unconditionally (clamped indices), so the
-  // prologue is ONE memory round trip: residual state is in the slot layout [point][target slot] and the
-  // host comes from the block, so no load depends on another
+  // the point's inputs arrived with lin_load (one point ahead); the block constants are in LDS
   const int sl = p * 8 + t;                 // this lane's residual slot
   const int tc_ = t < nF ? t : 0;
-  float idep = a.idepth[p], idep0 = a.idepth_zero[p];
-  const float pu = a.u[p], pv = a.v[p];
-  const bool has = a.res_of_slot[sl] >= 0;
-  const int st_raw = (int)a.r_state[sl];
-  const float oldE_raw = a.r_energy[sl];
-  const float oldNewE_raw = a.r_newEnergy[sl];
-  const float thr = fmaxf(a.frameTH[h], a.frameTH[tc_]);  // std::max<float>(host TH, target TH)
-  const float colorK = a.color[p * 8 + k], weightK = a.weight[p * 8 + k];
-  const HsPrecalc pc = a.pre[h * nF + tc_];
+  float idep = in.idep, idep0 = in.idep0;
+  const float pu = in.pu, pv = in.pv;
+  const bool has = in.res >= 0;
+  const int st_raw = in.st_raw;
+  const float oldE_raw = in.oldE_raw;
+  const float oldNewE_raw = in.oldNewE_raw;
+  const float thr = fmaxf(K.th[h], K.th[tc_]);  // std::max<float>(host TH, target TH)
+  const float colorK = in.colorK, weightK = in.weightK;
+  const HsPrecalc pc = K.pre[tc_];
   // the target's image: selected from the kernel-argument pointers (uniform SGPRs), not loaded per lane
   const float4* timg = a.img[0];
 #pragma unroll
   for (int i = 1; i < HS_MAXF; i++) timg = (t == i) ? a.img[i] : timg;
-  const uint2 ro2 = reinterpret_cast<const uint2*>(a.res_order)[p];  // the point's 8 residual-list slots
+  const uint2 ro2 = in.ro2;  // the point's 8 residual-list slots
   auto res_slot = [&](int q) -> int { return (int)(int8_t)(((q < 4 ? ro2.x : ro2.y) >> (8 * (q & 3))) & 0xffu); };
-  // the previous linearization's per-point data for the fused step (read unconditionally: one batch)
-  const unsigned fm = a.p_actmask[p];
-  const float xad = a.xAd[(h * nF + tc_) * 8 + k];
-  const float jpj = a.p_JpJdF[sl * 8 + k];
-  const float bds = a.p_bdSumF[p], hdi = a.p_HdiF_prev[p];
-  const float4 hcd = reinterpret_cast<const float4*>(a.p_Hcd)[p];
-  const float4 cs4 = *reinterpret_cast<const float4*>(a.st->cstep);
-  const float cs0 = cs4.x, cs1 = cs4.y, cs2 = cs4.z, cs3 = cs4.w;
-  // pin the batch: without this the compiler sinks the fused-step loads into the fuse_step branch, behind
-  // the wait for res_order (a second memory round trip)
-  asm volatile("" ::"v"(fm), "v"(xad), "v"(jpj), "v"(bds), "v"(hdi), "v"(hcd.x), "v"(hcd.y), "v"(hcd.z), "v"(hcd.w),
-               "v"(cs0), "v"(cs1), "v"(cs2), "v"(cs3), "v"(ro2.x), "v"(ro2.y));
+  // the previous linearization's per-point data for the fused step
+  const unsigned fm = in.fm;
+  const float xad = K.xad[tc_ * 8 + k];
+  const float jpj = in.jpj;
+  const float bds = in.bds, hdi = in.hdi;
+  const float4 hcd = in.hcd;
+  const float cs0 = K.cs[0], cs1 = K.cs[1], cs2 = K.cs[2], cs3 = K.cs[3];
   if (a.fuse_step) {
     // resubstituteFPt of the previous linearization + the point part of doStepFromBackup (stepfacD = 1).
     // Lane (t, k) forms xAd[h][t][k] * JpJdF[t][k]; the 8-term dot of a residual is an in-order octet fold, the
@@ -608,6 +644,18 @@ __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
   const int hb = a.host_begin[h], nh = a.host_begin[h + 1] - hb;
   const int pb = hb + (int)((long long)nh * q / nb), pe = hb + (int)((long long)nh * (q + 1) / nb);
   HS_TRACE(a, 0);
+  __shared__ LinConst K;
+  {  // the block's constants: precalc records of host h (by target), thresholds, xAd[h][.][.], calib step
+    const int nF = a.nF;
+    constexpr int PW = (int)(sizeof(HsPrecalc) / 4);
+    static_assert(sizeof(HsPrecalc) % 4 == 0, "precalc staged as words");
+    const int* src = reinterpret_cast<const int*>(a.pre + h * nF);
+    int* dst = reinterpret_cast<int*>(K.pre);
+    for (int i = tid; i < nF * PW; i += HS_LIN_NT) dst[i] = src[i];
+    if (tid < nF) K.th[tid] = a.frameTH[tid];
+    if (tid < nF * 8) K.xad[tid] = a.xAd[h * nF * 8 + tid];
+    if (tid < 4) K.cs[tid] = a.st->cstep[tid];
+  }
   LinAcc<kExact> A;
 #pragma unroll
   for (int i = 0; i < HS_E_TOP; i++) A.T[i] = 0.f;
@@ -617,11 +665,18 @@ __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
   for (int i = 0; i < 5; i++) A.E[i] = 0.f;
   A.C = 0.f;
   A.e = A.sid = A.np = 0.0;
-  if (wv < a.W) {
+  LinIn cur;
+  const bool work = wv < a.W && pb + wv < pe;
+  if (work) lin_load(a, pb + wv, lane, cur);  // in flight across the barrier
+  __syncthreads();
+  if (work) {
     for (int p = pb + wv; p < pe; p += a.W) {  // wave-uniform
+      LinIn nxt;
+      lin_load(a, min(p + a.W, pe - 1), lane, nxt);  // the next point's loads overlap this point's work
       LinPt P;
-      lin_point<kFix>(a, p, h, lane, P);
+      lin_point<kFix>(a, p, h, lane, cur, K, P);
       if (a.accumulate) acc_point<kExact>(A, P, h, lane);
+      cur = nxt;
     }
   }
   HS_TRACE(a, 1);
