@@ -245,7 +245,7 @@ static int launch_linearize(hs_ctx* c, int fuse, bool marg = false, bool accumul
     for (int i = 0; i < 4; i++) a.cDelta[i] = c->cDelta[i];
     a.margPriorFac = c->P.idepthFixPriorMargFac;
   }
-  for (int i = 0; i < c->nF; i++) a.img[i] = c->d_img[i];
+  for (int i = 0; i < HS_MAXF; i++) a.img[i] = c->d_img[i < c->nF ? i : 0];  // the kernel fetches on every slot
   a.st = c->d_state;
   a.lp.huberTH = c->P.huberTH;
   a.lp.outlierTHSumComponent = c->P.outlierTHSumComponent;

@@ -211,7 +211,8 @@ __device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int 
   // the target's image: selected from the kernel-argument pointers (uniform SGPRs), not loaded per lane
   const float4* timg = a.img[0];
 #pragma unroll
-  for (int i = 1; i < HS_MAXF; i++) timg = (t == i) ? a.img[i] : timg;
+  for (int i = 1; i < HS_MAXF; i++) timg = (t == i && i < nF) ? a.img[i] : timg;  // slots past the window: frame 0
+                                                                                   // (fetched, never used)
   const uint2 ro2 = in.ro2;  // the point's 8 residual-list slots
   auto res_slot = [&](int q) -> int { return (int)(int8_t)(((q < 4 ? ro2.x : ro2.y) >> (8 * (q & 3))) & 0xffu); };
   // the previous linearization's per-point data for the fused step
@@ -235,14 +236,16 @@ __device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int 
     dot += cs2 * hcd.z;
     dot += cs3 * hcd.w;
     b -= dot;
+    // lane q gathers the dot of list entry q (one ds_bpermute), then the terms are subtracted in list order
+    const int tq = res_slot(k);
+    const float dq = __shfl(dsum, (tq < 0 ? 0 : tq) * 8 + 7);
     bool live = true;
 #pragma unroll
     for (int q = 0; q < 8; q++) {
       const int tt = res_slot(q);
       live = live && tt >= 0;
       const int ts = tt < 0 ? 0 : tt;
-      const float d = __shfl(dsum, ts * 8 + 7);
-      if (live && ((m >> ts) & 1u)) b -= d;
+      if (live && ((m >> ts) & 1u)) b -= readlane_f(dq, q);
     }
     const float step = m != 0u ? -b * hdi : 0.f;
     idep = idep + 1.0f * step;
@@ -258,14 +261,17 @@ __device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int 
   const float oldE = (has && !a.marg) ? oldE_raw : 0.f;
   const float oldNewE = (has && !a.marg) ? oldNewE_raw : 0.f;
 
-  bool oob = false;
-  float Jx[10] = {0}, Jy[10] = {0}, Jd0 = 0.f, Jd1 = 0.f;
+  // Branch-free: every lane evaluates the whole chain (a wave's lanes diverge here anyway, so branches would run
+  // both sides and re-materialise the zeroed values at every merge); the reference's early exits become the
+  // validity flags okC (centre projection in the image), okP (pattern pixel in the image) and okI (finite
+  // intensity).  Values of a lane whose slot is not fully evaluated are never read: everything downstream is gated
+  // by eval / active, and the texel fetch of an out-of-image pixel is redirected to (2, 2).
+  const bool live0 = has && st != HS_RES_OOB;
+  float Jx[10], Jy[10], Jd0, Jd1;
   float qv[Q_N];
-#pragma unroll
-  for (int qi = 0; qi < Q_N; qi++) qv[qi] = 0.f;
-  float centre[3] = {0.f, 0.f, 0.f};
-  bool centreOk = false;
-  if (has && st != HS_RES_OOB) {
+  float centre[3];
+  bool okC, okI;
+  {
     // centre: projectPoint(u, v, idepth_zero, 0, 0, R_0, t_0)  Include/DirectProjection.h:20-38
     const float Kl0 = (pu + 0 - cal.cxl) * cal.fxli;
     const float Kl1 = (pv + 0 - cal.cyl) * cal.fyli;
@@ -277,137 +283,121 @@ __device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int 
     pt2 = pt2 + pc.t0[2] * idep0;
     const float drescale = 1.0f / pt2;
     const float new_idepth = idep0 * drescale;
-    if (!(drescale > 0)) {
-      oob = true;
-    } else {
-      const float u = pt0 * drescale, v = pt1 * drescale;
-      const float Ku = u * cal.fxl + cal.cxl, Kv = v * cal.fyl + cal.cyl;
-      if (!(Ku > 1.1f && Kv > 1.1f && Ku < (cal.W - 3) && Kv < (cal.H - 3))) {
-        oob = true;
-      } else {
-        centreOk = true;
-        centre[0] = Ku; centre[1] = Kv; centre[2] = new_idepth;
-        const float* R0 = pc.R0;
-        const float* t0 = pc.t0;
-        Jd0 = drescale * (t0[0] - t0[2] * u) * SCALE_IDEPTH * cal.fxl;
-        Jd1 = drescale * (t0[1] - t0[2] * v) * SCALE_IDEPTH * cal.fyl;
-        float cx[4], cy[4];
-        cx[2] = drescale * (R0[6] * u - R0[0]);
-        cx[3] = cal.fxl * drescale * (R0[7] * u - R0[1]) * cal.fyli;
-        cx[0] = Kl0 * cx[2];
-        cx[1] = Kl1 * cx[3];
-        cy[2] = cal.fyl * drescale * (R0[6] * v - R0[3]) * cal.fxli;
-        cy[3] = drescale * (R0[7] * v - R0[4]);
-        cy[0] = Kl0 * cy[2];
-        cy[1] = Kl1 * cy[3];
-        cx[0] = (cx[0] + u) * SCALE_F;
-        cx[1] *= SCALE_F;
-        cx[2] = (cx[2] + 1) * SCALE_C;
-        cx[3] *= SCALE_C;
-        cy[0] *= SCALE_F;
-        cy[1] = (cy[1] + v) * SCALE_F;
-        cy[2] *= SCALE_C;
-        cy[3] = (cy[3] + 1) * SCALE_C;
-        const float fx = cal.fxl, fy = cal.fyl;
-        Jx[0] = cx[0]; Jx[1] = cx[1]; Jx[2] = cx[2]; Jx[3] = cx[3];
-        Jy[0] = cy[0]; Jy[1] = cy[1]; Jy[2] = cy[2]; Jy[3] = cy[3];
-        Jx[4] = new_idepth * fx;
-        Jx[5] = 0;
-        Jx[6] = -new_idepth * u * fx;
-        Jx[7] = -u * v * fx;
-        Jx[8] = (1 + u * u) * fx;
-        Jx[9] = -v * fx;
-        Jy[4] = 0;
-        Jy[5] = new_idepth * fy;
-        Jy[6] = -new_idepth * v * fy;
-        Jy[7] = -(1 + v * v) * fy;
-        Jy[8] = u * v * fy;
-        Jy[9] = u * fy;
+    const float u = pt0 * drescale, v = pt1 * drescale;
+    const float Ku = u * cal.fxl + cal.cxl, Kv = v * cal.fyl + cal.cyl;
+    okC = (drescale > 0) && (Ku > 1.1f && Kv > 1.1f && Ku < (cal.W - 3) && Kv < (cal.H - 3));
+    centre[0] = Ku; centre[1] = Kv; centre[2] = new_idepth;
+    const float* R0 = pc.R0;
+    const float* t0 = pc.t0;
+    Jd0 = drescale * (t0[0] - t0[2] * u) * SCALE_IDEPTH * cal.fxl;
+    Jd1 = drescale * (t0[1] - t0[2] * v) * SCALE_IDEPTH * cal.fyl;
+    float cx[4], cy[4];
+    cx[2] = drescale * (R0[6] * u - R0[0]);
+    cx[3] = cal.fxl * drescale * (R0[7] * u - R0[1]) * cal.fyli;
+    cx[0] = Kl0 * cx[2];
+    cx[1] = Kl1 * cx[3];
+    cy[2] = cal.fyl * drescale * (R0[6] * v - R0[3]) * cal.fxli;
+    cy[3] = drescale * (R0[7] * v - R0[4]);
+    cy[0] = Kl0 * cy[2];
+    cy[1] = Kl1 * cy[3];
+    cx[0] = (cx[0] + u) * SCALE_F;
+    cx[1] *= SCALE_F;
+    cx[2] = (cx[2] + 1) * SCALE_C;
+    cx[3] *= SCALE_C;
+    cy[0] *= SCALE_F;
+    cy[1] = (cy[1] + v) * SCALE_F;
+    cy[2] *= SCALE_C;
+    cy[3] = (cy[3] + 1) * SCALE_C;
+    const float fx = cal.fxl, fy = cal.fyl;
+    Jx[0] = cx[0]; Jx[1] = cx[1]; Jx[2] = cx[2]; Jx[3] = cx[3];
+    Jy[0] = cy[0]; Jy[1] = cy[1]; Jy[2] = cy[2]; Jy[3] = cy[3];
+    Jx[4] = new_idepth * fx;
+    Jx[5] = 0;
+    Jx[6] = -new_idepth * u * fx;
+    Jx[7] = -u * v * fx;
+    Jx[8] = (1 + u * u) * fx;
+    Jx[9] = -v * fx;
+    Jy[4] = 0;
+    Jy[5] = new_idepth * fy;
+    Jy[6] = -new_idepth * v * fy;
+    Jy[7] = -(1 + v * v) * fy;
+    Jy[8] = u * v * fy;
+    Jy[9] = u * fy;
 
-        // pattern pixel k (staticPattern[8], Include/GlobalTypes.h:181-184) as selects: a lane-indexed
-        // constant-memory table would cost a dependent memory round trip here
-        const int pdx = (k == 1 || k == 6) ? -1 : (k == 2) ? 1 : (k == 3) ? -2 : (k == 5) ? 2 : 0;
-        const int pdy = (k == 0) ? -2 : (k <= 2) ? -1 : (k <= 5) ? 0 : (k == 6) ? 1 : 2;
-        const float px = pu + pdx, py = pv + pdy;
-        float q0 = pc.KRKi[0] * px + pc.KRKi[1] * py + pc.KRKi[2] * 1.f;
-        float q1 = pc.KRKi[3] * px + pc.KRKi[4] * py + pc.KRKi[5] * 1.f;
-        float q2 = pc.KRKi[6] * px + pc.KRKi[7] * py + pc.KRKi[8] * 1.f;
-        q0 = q0 + pc.Kt[0] * idep;
-        q1 = q1 + pc.Kt[1] * idep;
-        q2 = q2 + pc.Kt[2] * idep;
-        const float PKu = q0 / q2, PKv = q1 / q2;
-        if (!(PKu > 1.1f && PKv > 1.1f && PKu < (cal.W - 3) && PKv < (cal.H - 3))) {
-          oob = true;
-        } else {
-          float3 hit = interp33(timg, PKu, PKv, cal.W);
-          // all three channels are materialised here: otherwise the compiler sinks the dI/dx, dI/dy loads
-          // under the isfinite(I) branch below, a second dependent memory round trip
-          asm volatile("" : "+v"(hit.x), "+v"(hit.y), "+v"(hit.z));
-          const float color = colorK;
-          const float residual = hit.x - (float)(pc.aff[0] * color + pc.aff[1]);
-          const float drdA = (color - pc.b0);
-          if (!isfinite(hit.x)) {
-            oob = true;
-          } else {
-            float w = sqrtf(a.lp.outlierTHSumComponent /
-                            (a.lp.outlierTHSumComponent + (hit.y * hit.y + hit.z * hit.z)));
-            w = 0.5f * (w + weightK);
-            float hw = fabsf(residual) < a.lp.huberTH ? 1 : a.lp.huberTH / fabsf(residual);
-            qv[0] = w * w * hw * residual * residual * (2 - hw);
-            if (hw < 1) hw = sqrtf(hw);
-            hw = hw * w;
-            const float hy = hit.y * hw, hz = hit.z * hw;
-            const float resF = residual * hw;
-            float jab0 = drdA * hw;
-            float jab1 = hw;
-            qv[1] = hy * hy;
-            qv[2] = hz * hz;
-            qv[3] = hy * hz;
-            qv[4] = drdA * hw * hy;
-            qv[5] = drdA * hw * hz;
-            qv[6] = hw * hy;
-            qv[7] = hw * hz;
-            qv[8] = drdA * drdA * hw * hw;
-            qv[9] = drdA * hw * hw;
-            qv[10] = hw * hw;
-            qv[11] = hw * hw * (hy * hy + hz * hz);
-            if (a.lp.affineOptModeA < 0) jab0 = 0;
-            if (a.lp.affineOptModeB < 0) jab1 = 0;
-            // AccumulatedTopHessianSSE::addPoint<0>: JI_r, Jab_r, rr over resApprox = resF; in the
-            // marginalization pass addPoint<2> over res_toZeroF = resF - [JI Jp, Jab] delta
-            // (fixLinearizationF, Src/OptimizationClasses.cpp:258-284)
-            float rz = resF;
-            if (a.marg) {
-              const float* dp = a.adHTdelta + (h + nF * t) * 8;
-              float jx = 0.f, jy = 0.f, cxx = 0.f, cyy = 0.f;
+    // pattern pixel k (staticPattern[8], Include/GlobalTypes.h:181-184) as selects: a lane-indexed
+    // constant-memory table would cost a dependent memory round trip here
+    const int pdx = (k == 1 || k == 6) ? -1 : (k == 2) ? 1 : (k == 3) ? -2 : (k == 5) ? 2 : 0;
+    const int pdy = (k == 0) ? -2 : (k <= 2) ? -1 : (k <= 5) ? 0 : (k == 6) ? 1 : 2;
+    const float px = pu + pdx, py = pv + pdy;
+    float q0 = pc.KRKi[0] * px + pc.KRKi[1] * py + pc.KRKi[2] * 1.f;
+    float q1 = pc.KRKi[3] * px + pc.KRKi[4] * py + pc.KRKi[5] * 1.f;
+    float q2 = pc.KRKi[6] * px + pc.KRKi[7] * py + pc.KRKi[8] * 1.f;
+    q0 = q0 + pc.Kt[0] * idep;
+    q1 = q1 + pc.Kt[1] * idep;
+    q2 = q2 + pc.Kt[2] * idep;
+    const float PKu = q0 / q2, PKv = q1 / q2;
+    const bool okP = okC && (PKu > 1.1f && PKv > 1.1f && PKu < (cal.W - 3) && PKv < (cal.H - 3));
+    float3 hit = interp33(timg, okP ? PKu : 2.f, okP ? PKv : 2.f, cal.W);
+    const float color = colorK;
+    const float residual = hit.x - (float)(pc.aff[0] * color + pc.aff[1]);
+    const float drdA = (color - pc.b0);
+    okI = okP && isfinite(hit.x);
+    float w = sqrtf(a.lp.outlierTHSumComponent / (a.lp.outlierTHSumComponent + (hit.y * hit.y + hit.z * hit.z)));
+    w = 0.5f * (w + weightK);
+    float hw = fabsf(residual) < a.lp.huberTH ? 1 : a.lp.huberTH / fabsf(residual);
+    qv[0] = w * w * hw * residual * residual * (2 - hw);
+    hw = hw < 1 ? sqrtf(hw) : hw;
+    hw = hw * w;
+    const float hy = hit.y * hw, hz = hit.z * hw;
+    const float resF = residual * hw;
+    float jab0 = drdA * hw;
+    float jab1 = hw;
+    qv[1] = hy * hy;
+    qv[2] = hz * hz;
+    qv[3] = hy * hz;
+    qv[4] = drdA * hw * hy;
+    qv[5] = drdA * hw * hz;
+    qv[6] = hw * hy;
+    qv[7] = hw * hz;
+    qv[8] = drdA * drdA * hw * hw;
+    qv[9] = drdA * hw * hw;
+    qv[10] = hw * hw;
+    qv[11] = hw * hw * (hy * hy + hz * hz);
+    if (a.lp.affineOptModeA < 0) jab0 = 0;
+    if (a.lp.affineOptModeB < 0) jab1 = 0;
+    // AccumulatedTopHessianSSE::addPoint<0>: JI_r, Jab_r, rr over resApprox = resF; in the
+    // marginalization pass addPoint<2> over res_toZeroF = resF - [JI Jp, Jab] delta
+    // (fixLinearizationF, Src/OptimizationClasses.cpp:258-284)
+    float rz = resF;
+    if (a.marg) {
+      const float* dp = a.adHTdelta + (h + nF * t) * 8;
+      float jx = 0.f, jy = 0.f, cxx = 0.f, cyy = 0.f;
 #pragma unroll
-              for (int i = 0; i < 6; i++) {
-                jx += Jx[4 + i] * dp[i];
-                jy += Jy[4 + i] * dp[i];
-              }
-#pragma unroll
-              for (int i = 0; i < 4; i++) {
-                cxx += Jx[i] * a.cDelta[i];
-                cyy += Jy[i] * a.cDelta[i];
-              }
-              const float dF = idep - idep0;
-              const float Jpdx = jx + cxx + Jd0 * dF;
-              const float Jpdy = jy + cyy + Jd1 * dF;
-              rz = rz - hy * Jpdx;
-              rz = rz - hz * Jpdy;
-              rz = rz - jab0 * dp[6];
-              rz = rz - jab1 * dp[7];
-            }
-            qv[12] = rz * hy;
-            qv[13] = rz * hz;
-            qv[14] = rz * jab0;
-            qv[15] = rz * jab1;
-            qv[16] = rz * rz;
-          }
-        }
+      for (int i = 0; i < 6; i++) {
+        jx += Jx[4 + i] * dp[i];
+        jy += Jy[4 + i] * dp[i];
       }
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        cxx += Jx[i] * a.cDelta[i];
+        cyy += Jy[i] * a.cDelta[i];
+      }
+      const float dF = idep - idep0;
+      const float Jpdx = jx + cxx + Jd0 * dF;
+      const float Jpdy = jy + cyy + Jd1 * dF;
+      rz = rz - hy * Jpdx;
+      rz = rz - hz * Jpdy;
+      rz = rz - jab0 * dp[6];
+      rz = rz - jab1 * dp[7];
     }
+    qv[12] = rz * hy;
+    qv[13] = rz * hz;
+    qv[14] = rz * jab0;
+    qv[15] = rz * jab1;
+    qv[16] = rz * rz;
   }
+  const bool oob = live0 && !okI;
+  const bool centreOk = live0 && okC;
   const unsigned long long oobMask = __ballot(oob);
   const bool slotOob = ((oobMask >> (t * 8)) & 0xffull) != 0ull;
 
@@ -458,21 +448,37 @@ __device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int 
   // ---------------- per-point sums in the point's residual-list order (uniform; readlane from lane 8 * slot)
   {
     const unsigned long long actBits = __ballot(active);
-    double eSum = 0.0;
-    float Hdd = 0.f, bd = 0.f, Hcd[4] = {0.f, 0.f, 0.f, 0.f};
-    unsigned mask = 0u;
+    // lane 8t + i carries quantity i of slot t (tbd, tHdd, tc[0..3], -, econ); lane i of every octet gathers
+    // quantity i of the listed residuals (one ds_bpermute per list entry, all in flight), then sums them in list
+    // order: the reference's sequential sums, one lane per quantity
+    const float X = k == 0 ? tbd : k == 1 ? tHdd : k == 2 ? tc[0] : k == 3 ? tc[1] : k == 4 ? tc[2] : k == 5 ? tc[3] : econ;
+    float g[8];
+    int nres = 8;
+#pragma unroll
     for (int qn = 0; qn < 8; qn++) {
       const int tt = res_slot(qn);
-      if (tt < 0) break;
-      const int src = tt * 8;
-      eSum += (double)readlane_f(econ, src);
-      if (!((actBits >> src) & 1ull)) continue;
-      mask |= 1u << tt;
-      bd += readlane_f(tbd, src);
-      Hdd += readlane_f(tHdd, src);
-#pragma unroll
-      for (int c = 0; c < 4; c++) Hcd[c] += readlane_f(tc[c], src);
+      nres = (tt < 0 && qn < nres) ? qn : nres;
+      g[qn] = __shfl(X, (tt < 0 ? 0 : tt) * 8 + k);
     }
+    float qsum = 0.f;
+    double eAcc = 0.0;
+    unsigned mask = 0u;
+#pragma unroll
+    for (int qn = 0; qn < 8; qn++) {
+      if (qn >= nres) break;  // uniform
+      const int tt = res_slot(qn);
+      eAcc += (double)g[qn];  // econ: every listed residual (read from lane 7)
+      if ((actBits >> (tt * 8)) & 1ull) {
+        mask |= 1u << tt;
+        qsum += g[qn];
+      }
+    }
+    const double eSum = __longlong_as_double(((long long)__builtin_amdgcn_readlane((int)(__double_as_longlong(eAcc) >> 32), 7) << 32) |
+                                             (unsigned int)__builtin_amdgcn_readlane((int)__double_as_longlong(eAcc), 7));
+    const float bd = readlane_f(qsum, 0), Hdd = readlane_f(qsum, 1);
+    float Hcd[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) Hcd[c] = readlane_f(qsum, 2 + c);
     float HdiF = 0.f, bdSumF = 0.f;
     if (mask != 0u) {
       // marginalization pass: priorF *= idepthFixPriorMargFac, the sums are the LF ones (AF = 0), and
@@ -680,6 +686,7 @@ __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
     }
   }
   HS_TRACE(a, 1);
+  if (a.trace && lane == 0) a.trace[(size_t)blockIdx.x * 16 + 4 + wv] = wall_clock64();  // each wave's finish
   if (!a.accumulate) return;
   // the waves' partials, summed in wave order (fp32) into the block partial; the energies in fp64
   constexpr int NE = hs_ne(kExact);
@@ -698,11 +705,26 @@ __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
     se[wv * 3 + 2] = A.np;
   }
   __syncthreads();
-  float* out = a.part + (size_t)b * NE * 64;
-  for (int i = tid; i < NE * 64; i += HS_LIN_NT) {
-    float s = lin_stage[i];
-    for (int w = 1; w < a.W; w++) s += lin_stage[w * NE * 64 + i];
-    out[i] = s;
+  HS_TRACE(a, 3);
+  // 16 B per thread and step, every wave's value loaded before the in-order sum (a runtime-bound loop would wait
+  // for each LDS load in turn); waves past W hold no points and are not added
+  static_assert((NE * 64) % 4 == 0, "partials staged as float4");
+  float4* out4 = reinterpret_cast<float4*>(a.part + (size_t)b * NE * 64);
+  const float4* st4 = reinterpret_cast<const float4*>(lin_stage);
+  for (int i = tid; i < NE * 16; i += HS_LIN_NT) {
+    float4 v[HS_LIN_NW];
+#pragma unroll
+    for (int w = 0; w < HS_LIN_NW; w++) v[w] = st4[w * NE * 16 + i];
+    float4 s = v[0];
+#pragma unroll
+    for (int w = 1; w < HS_LIN_NW; w++)
+      if (w < a.W) {
+        s.x += v[w].x;
+        s.y += v[w].y;
+        s.z += v[w].z;
+        s.w += v[w].w;
+      }
+    out4[i] = s;
   }
   if (tid < 3) {
     double s = se[tid];
