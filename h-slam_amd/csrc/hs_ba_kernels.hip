@@ -239,13 +239,17 @@ __device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int 
     // lane q gathers the dot of list entry q (one ds_bpermute), then the terms are subtracted in list order
     const int tq = res_slot(k);
     const float dq = __shfl(dsum, (tq < 0 ? 0 : tq) * 8 + 7);
+    float dl[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) dl[q] = readlane_f(dq, q);  // independent, ahead of the ordered subtractions
     bool live = true;
 #pragma unroll
     for (int q = 0; q < 8; q++) {
       const int tt = res_slot(q);
       live = live && tt >= 0;
       const int ts = tt < 0 ? 0 : tt;
-      if (live && ((m >> ts) & 1u)) b -= readlane_f(dq, q);
+      const float bq = b - dl[q];
+      b = (live && ((m >> ts) & 1u)) ? bq : b;
     }
     const float step = m != 0u ? -b * hdi : 0.f;
     idep = idep + 1.0f * step;
@@ -403,9 +407,16 @@ __device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int 
 
   // sequential (pattern-order) sums = the reference's running sums: octet folds at lane 8t+7, broadcast to the
   // octet by ds_bpermute (no LDS round trip, no barrier: the waves of a block run their points independently)
+  // (the 17 folds advance step by step together: independent DPP adds back to back, no hazard waits)
   float S[Q_N];
 #pragma unroll
-  for (int qi = 0; qi < Q_N; qi++) S[qi] = __shfl(octet_fold(qv[qi]), t * 8 + 7);
+  for (int qi = 0; qi < Q_N; qi++) S[qi] = 0.f + qv[qi];
+#pragma unroll
+  for (int j = 0; j < 7; j++)
+#pragma unroll
+    for (int qi = 0; qi < Q_N; qi++) S[qi] = dpp_shr1(S[qi]) + qv[qi];
+#pragma unroll
+  for (int qi = 0; qi < Q_N; qi++) S[qi] = __shfl(S[qi], t * 8 + 7);
 
   // ---------------- state decision + applyRes (the 8 lanes of a slot agree; lane k == 0 writes)
   const bool live = has && st != HS_RES_OOB;      // OOB is sticky: linearize returns state_energy
