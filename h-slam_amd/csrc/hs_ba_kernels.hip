@@ -213,10 +213,11 @@ __device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int 
 #pragma unroll
   for (int i = 1; i < HS_MAXF; i++) timg = (t == i && i < nF) ? a.img[i] : timg;  // slots past the window: frame 0
                                                                                    // (fetched, never used)
-  const uint2 ro2 = in.ro2;  // the point's 8 residual-list slots
+  // the point's 8 residual-list slots and previous active mask, as scalars (uniform per point)
+  const uint2 ro2 = make_uint2(__builtin_amdgcn_readfirstlane(in.ro2.x), __builtin_amdgcn_readfirstlane(in.ro2.y));
   auto res_slot = [&](int q) -> int { return (int)(int8_t)(((q < 4 ? ro2.x : ro2.y) >> (8 * (q & 3))) & 0xffu); };
   // the previous linearization's per-point data for the fused step
-  const unsigned fm = in.fm;
+  const unsigned fm = __builtin_amdgcn_readfirstlane(in.fm);
   const float xad = K.xad[tc_ * 8 + k];
   const float jpj = in.jpj;
   const float bds = in.bds, hdi = in.hdi;
@@ -475,14 +476,15 @@ __device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int 
     double eAcc = 0.0;
     unsigned mask = 0u;
 #pragma unroll
-    for (int qn = 0; qn < 8; qn++) {
-      if (qn >= nres) break;  // uniform
-      const int tt = res_slot(qn);
-      eAcc += (double)g[qn];  // econ: every listed residual (read from lane 7)
-      if ((actBits >> (tt * 8)) & 1ull) {
-        mask |= 1u << tt;
-        qsum += g[qn];
-      }
+    for (int qn = 0; qn < 8; qn++) {  // fully unrolled, predicated (g stays in registers)
+      const bool listed = qn < nres;  // uniform
+      const int tt = res_slot(qn) & 7;
+      const double e1 = eAcc + (double)g[qn];  // econ: every listed residual (read from lane 7)
+      eAcc = listed ? e1 : eAcc;
+      const bool act = listed && ((actBits >> (tt * 8)) & 1ull);
+      mask |= act ? 1u << tt : 0u;
+      const float q1 = qsum + g[qn];
+      qsum = act ? q1 : qsum;
     }
     const double eSum = __longlong_as_double(((long long)__builtin_amdgcn_readlane((int)(__double_as_longlong(eAcc) >> 32), 7) << 32) |
                                              (unsigned int)__builtin_amdgcn_readlane((int)__double_as_longlong(eAcc), 7));
@@ -652,7 +654,9 @@ __device__ __forceinline__ void acc_point(LinAcc<kExact>& A, const LinPt& P, int
 template <bool kExact, bool kFix>
 __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
   extern __shared__ float lin_stage[];  // [HS_LIN_NW waves][ne][64] fp32 partials, then [HS_LIN_NW][3] fp64 energies
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  // the wave index as a scalar: the point index and everything per point then stays uniform (scalar loads,
+  // scalar branches) instead of being treated as divergent
+  const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int b = blockIdx.x;
   int h = 0;  // the block's host: from the kernel-argument block boundaries, no load
 #pragma unroll
