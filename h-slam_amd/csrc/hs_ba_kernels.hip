@@ -169,9 +169,17 @@ struct LinConst {
 // kFix: System::linearizeAll(true)'s bookkeeping (Src/FullSystemOptimize.cpp:26-50): for every residual still active
 // after applyRes the point's maxRelBaseline = max(relBS) and numGoodResiduals++ (isNew is never cleared in the
 // reference, Include/OptimizationClasses.h:98,112), in the point's residual-list order.
+// per-wave LDS scratch of lin_point / acc_point (inside the wave's own partials area, which is written only after
+// the wave's last point): the pattern values [Q_N][64], the slot sums [8][LW_SS] and the Schur rows [8][8]
+constexpr int LW_SS = 20;  // slot-sum row stride (floats): 16 B aligned rows for ds_read_b128
+constexpr int LW_QR = 68;  // pattern-value row stride: the 16 lanes of a 16 B read cover distinct banks
+constexpr int LW_QS = 0, LW_SUM = Q_N * LW_QR, LW_JJ = LW_SUM + 8 * LW_SS, LW_FLOATS = LW_JJ + 64;
+static_assert(LW_SUM % 4 == 0 && LW_JJ % 4 == 0, "16 B aligned scratch rows");
+static_assert(LW_FLOATS <= hs_ne(false) * 64, "lin scratch fits the wave's partials area");
+
 template <bool kFix>
 __device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int lane, const LinIn& in,
-                                          const LinConst& K, LinPt& o) {
+                                          const LinConst& K, float* ws, LinPt& o) {
   const int t = lane >> 3;  // target slot
   const int k = lane & 7;   // pattern pixel
   const int nF = a.nF;
@@ -408,16 +416,46 @@ __device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int 
 
   // sequential (pattern-order) sums = the reference's running sums: octet folds at lane 8t+7, broadcast to the
   // octet by ds_bpermute (no LDS round trip, no barrier: the waves of a block run their points independently)
-  // (the 17 folds advance step by step together: independent DPP adds back to back, no hazard waits)
+  // through the wave's LDS scratch: the pattern values are transposed so that one lane folds one (quantity, slot)
+  // pair over its 8 pixels in order (two 16 B reads, 8 adds), the 136 sums go back to LDS and every lane reads
+  // the 17 sums of its slot (same-address reads within an octet)
   float S[Q_N];
+  {
+    float* qs = ws + LW_QS;
+    float* ss = ws + LW_SUM;
 #pragma unroll
-  for (int qi = 0; qi < Q_N; qi++) S[qi] = 0.f + qv[qi];
+    for (int qi = 0; qi < Q_N; qi++) qs[qi * LW_QR + lane] = qv[qi];
+    __builtin_amdgcn_wave_barrier();
 #pragma unroll
-  for (int j = 0; j < 7; j++)
+    for (int r = 0; r < 3; r++) {  // pairs lane + 64 r = (quantity qi, slot ts), 136 of them
+      const int pr = lane + 64 * r;
+      if (r < 2 || pr < Q_N * 8) {
+        const int qi = pr >> 3, ts = pr & 7;
+        const float4 x0 = *reinterpret_cast<const float4*>(qs + qi * LW_QR + ts * 8);
+        const float4 x1 = *reinterpret_cast<const float4*>(qs + qi * LW_QR + ts * 8 + 4);
+        float f = 0.f + x0.x;
+        f = f + x0.y;
+        f = f + x0.z;
+        f = f + x0.w;
+        f = f + x1.x;
+        f = f + x1.y;
+        f = f + x1.z;
+        f = f + x1.w;
+        ss[ts * LW_SS + qi] = f;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const float4* sr = reinterpret_cast<const float4*>(ss + t * LW_SS);
 #pragma unroll
-    for (int qi = 0; qi < Q_N; qi++) S[qi] = dpp_shr1(S[qi]) + qv[qi];
-#pragma unroll
-  for (int qi = 0; qi < Q_N; qi++) S[qi] = __shfl(S[qi], t * 8 + 7);
+    for (int i = 0; i < 4; i++) {
+      const float4 v4 = sr[i];
+      S[4 * i] = v4.x;
+      S[4 * i + 1] = v4.y;
+      S[4 * i + 2] = v4.z;
+      S[4 * i + 3] = v4.w;
+    }
+    S[16] = ss[t * LW_SS + 16];
+  }
 
   // ---------------- state decision + applyRes (the 8 lanes of a slot agree; lane k == 0 writes)
   const bool live = has && st != HS_RES_OOB;      // OOB is sticky: linearize returns state_energy
@@ -592,7 +630,7 @@ struct LinAcc {
 };
 
 template <bool kExact>
-__device__ __forceinline__ void acc_point(LinAcc<kExact>& A, const LinPt& P, int h, int lane) {
+__device__ __forceinline__ void acc_point(LinAcc<kExact>& A, const LinPt& P, int h, int lane, float* ws) {
   // ---- AccumulatedTopHessianSSE::addPoint<0> of the lane's residual: AccumulatorApprox::update / updateTopRight /
   // updateBotRight (Include/MatrixAccumulators.h:754-915).  Lane (t, k) owns, of the 13x13 (host, t) block:
   //   T[j]  Data (j, k), j <= k (x/y column k, the rows uniform)      T[8], T[9]  Data (k, 8), (k, 9)
@@ -629,14 +667,16 @@ __device__ __forceinline__ void acc_point(LinAcc<kExact>& A, const LinPt& P, int
   // ---- accD[host + t1 nF + t2 nF^2].update(JpJdF_t1, JpJdF_t2, HdiF) (Src/AccumulatedSCHessian.cpp:38-48): lane
   // (row, col) = (lane >> 3, lane & 7); JpJdF[t][i] sits in lane 8t + i (zero unless active)
   {
+    // rows of the non-host slots through the wave's LDS scratch: jb[i][o] = JpJdF[slot of o][i]
     const int dr = lane >> 3, dc = lane & 7;
-    float j1[7], j2[7];
-#pragma unroll
-    for (int o = 0; o < 7; o++) {
-      const int tt = o + (o >= h ? 1 : 0);
-      j1[o] = __shfl(P.jj, tt * 8 + dr);
-      j2[o] = __shfl(P.jj, tt * 8 + dc);
-    }
+    float* jb = ws + LW_JJ;
+    const int t = lane >> 3, k = lane & 7;
+    if (t != h) jb[k * 8 + t - (t > h ? 1 : 0)] = P.jj;
+    __builtin_amdgcn_wave_barrier();
+    const float4 r0 = *reinterpret_cast<const float4*>(jb + dr * 8), r1 = *reinterpret_cast<const float4*>(jb + dr * 8 + 4);
+    const float4 c0 = *reinterpret_cast<const float4*>(jb + dc * 8), c1 = *reinterpret_cast<const float4*>(jb + dc * 8 + 4);
+    const float j1[7] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z};
+    const float j2[7] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z};
 #pragma unroll
     for (int o1 = 0; o1 < 7; o1++) {
       const float wl = P.HdiF * j1[o1];
@@ -686,6 +726,7 @@ __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
   for (int i = 0; i < 5; i++) A.E[i] = 0.f;
   A.C = 0.f;
   A.e = A.sid = A.np = 0.0;
+  float* ws = lin_stage + wv * hs_ne(kExact) * 64;  // the wave's LDS scratch (its partials area)
   LinIn cur;
   const bool work = wv < a.W && pb + wv < pe;
   if (work) lin_load(a, pb + wv, lane, cur);  // in flight across the barrier
@@ -695,8 +736,8 @@ __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
       LinIn nxt;
       lin_load(a, min(p + a.W, pe - 1), lane, nxt);  // the next point's loads overlap this point's work
       LinPt P;
-      lin_point<kFix>(a, p, h, lane, cur, K, P);
-      if (a.accumulate) acc_point<kExact>(A, P, h, lane);
+      lin_point<kFix>(a, p, h, lane, cur, K, ws, P);
+      if (a.accumulate) acc_point<kExact>(A, P, h, lane, ws);
       cur = nxt;
     }
   }
