@@ -92,7 +92,9 @@ struct hs_ctx {
   bool haveSystem = false;        // a stitched, not yet solved system is in the slots
 
   // device
-  float4* d_img[HS_MAXF] = {nullptr};
+  float4* d_img[HS_MAXF] = {nullptr};  // frame f's level-0 texels: d_img_all + f * img_px
+  float4* d_img_all = nullptr;
+  size_t img_px = 0;
   HsDevState* d_state = nullptr;
   HsPrecalc* d_pre = nullptr;
   float* d_frameTH = nullptr;
@@ -162,10 +164,9 @@ static void drop_graph(hs_ctx* c) {
 static void free_window(hs_ctx* c) {
   drop_graph(c);
   for (int i = 0; i < HS_MAXF; i++) {
-    if (c->d_img[i]) (void)hipFree(c->d_img[i]);
     c->d_img[i] = nullptr;
   }
-  void* ptrs[] = {c->d_state, c->d_pre, c->d_frameTH, c->d_u, c->d_v, c->d_idepth, c->d_idepth_zero,
+  void* ptrs[] = {c->d_img_all, c->d_state, c->d_pre, c->d_frameTH, c->d_u, c->d_v, c->d_idepth, c->d_idepth_zero,
                   c->d_priorF, c->d_color, c->d_weight, c->d_res_of_slot, c->d_pt_host, c->d_host_pt_begin,
                   c->d_res_order, c->d_r_state, c->d_r_active, c->d_r_energy, c->d_r_newEnergy, c->d_r_ewo,
                   c->d_r_center, c->d_p_actmask, c->d_p_HdiF, c->d_p_bdSumF, c->d_p_Hcd, c->d_p_JpJdF,
@@ -189,6 +190,7 @@ static void free_window(hs_ctx* c) {
   c->d_HM = c->d_bM = c->d_Nproj = nullptr;
   c->d_xAd = nullptr; c->d_x = nullptr; c->d_elog = nullptr; c->d_cand = nullptr;
   c->d_tr_lin = c->d_tr_acc = c->d_tr_solve = c->d_tr_st = nullptr;
+  c->d_img_all = nullptr;
   c->d_marg = nullptr;
   c->d_adHTdelta = nullptr;
   c->d_p_HdiF_alt = c->d_fix_relBL = nullptr;
@@ -245,7 +247,8 @@ static int launch_linearize(hs_ctx* c, int fuse, bool marg = false, bool accumul
     for (int i = 0; i < 4; i++) a.cDelta[i] = c->cDelta[i];
     a.margPriorFac = c->P.idepthFixPriorMargFac;
   }
-  for (int i = 0; i < HS_MAXF; i++) a.img[i] = c->d_img[i < c->nF ? i : 0];  // the kernel fetches on every slot
+  a.img = c->d_img_all;
+  a.img_stride = (long long)c->img_px;
   a.st = c->d_state;
   a.lp.huberTH = c->P.huberTH;
   a.lp.outlierTHSumComponent = c->P.outlierTHSumComponent;
@@ -749,8 +752,10 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
   // ---- device allocations + uploads
   const size_t npx = (size_t)cam->width * cam->height;
   std::vector<float4> tex(npx);
+  HS_TRY(dalloc(&c->d_img_all, npx * nF));  // one allocation: the kernel indexes frames by stride
+  c->img_px = npx;
   for (int f = 0; f < nF; f++) {
-    HS_TRY(dalloc(&c->d_img[f], npx));
+    c->d_img[f] = c->d_img_all + f * npx;
     const float* src = images[f];
     for (size_t i = 0; i < npx; i++) tex[i] = make_float4(src[3 * i], src[3 * i + 1], src[3 * i + 2], 0.f);
     HS_HIP(hipMemcpy(c->d_img[f], tex.data(), npx * sizeof(float4), hipMemcpyHostToDevice));

@@ -39,7 +39,8 @@ __host__ __device__ constexpr int hs_ne(bool exact) { return HS_E_TOP + (exact ?
 __host__ __device__ constexpr int hs_nt(int n) { return n * (n + 1) / 2; }  // upper triangle of the n x n system
 
 struct HsLinArgs {
-  const float4* img[HS_MAXF];  // level-0 texels per window frame
+  const float4* img;           // level-0 texels of the window frames, frame f at img + f * img_stride
+  long long img_stride;
   const HsDevState* st;
   HsLinParams lp;
   int nF;
