@@ -269,7 +269,8 @@ static int launch_linearize(hs_ctx* c, int fuse, bool marg = false, bool accumul
   a.W = c->W;
   a.pre = c->d_pre;
   a.frameTH = c->d_frameTH;
-  a.xAd = c->d_xAd;
+  a.adHostF = c->d_adHostF;
+  a.adTargetF = c->d_adTargetF;
   a.u = c->d_u; a.v = c->d_v; a.idepth = c->d_idepth; a.idepth_zero = c->d_idepth_zero; a.priorF = c->d_priorF;
   a.color = c->d_color; a.weight = c->d_weight;
   a.res_of_slot = c->d_res_of_slot; a.res_order = c->d_res_order;
@@ -435,7 +436,8 @@ static int dump_traces(hs_ctx* c) {
     long long h[32];
     HS_HIP(hipMemcpy(h, c->d_tr_solve, sizeof(h), hipMemcpyDeviceToHost));
     std::fprintf(stderr, "[hs trace] solve kb4 cycles:");
-    for (int k = 17; k < 24; k++) std::fprintf(stderr, " s%d=%lld", k, h[k] ? h[k] - h[16] : -1);
+    for (int k = 17; k < 30; k++)
+      if (k < 24 || k > 25) std::fprintf(stderr, " s%d=%lld", k, h[k] ? h[k] - h[16] : -1);
     std::fprintf(stderr, "\n");
   }
   HS_TRY(dump_one("linearize", c->d_tr_lin, c->nblk, tick_us, c->stream));

@@ -711,7 +711,20 @@ __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
     int* dst = reinterpret_cast<int*>(K.pre);
     for (int i = tid; i < nF * PW; i += HS_LIN_NT) dst[i] = src[i];
     if (tid < nF) K.th[tid] = a.frameTH[tid];
-    if (tid < nF * 8) K.xad[tid] = a.xAd[h * nF * 8 + tid];
+    if (a.fuse_step && tid < nF * 8) {
+      // xAd[h][t][c] of the last solve (EnergyFunctional::resubstituteF_MT): the frame steps (float)lastX and the
+      // fp32 adjoints of the pair, in the solve's summation order
+      const int t = tid >> 3, c = tid & 7;
+      const float* aH = a.adHostF + (h + nF * t) * 64;
+      const float* aT = a.adTargetF + (h + nF * t) * 64;
+      const double* lx = a.st->lastX;
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int rr = 0; rr < 8; rr++) s1 += (float)lx[4 + 8 * h + rr] * aH[rr * 8 + c];
+#pragma unroll
+      for (int rr = 0; rr < 8; rr++) s2 += (float)lx[4 + 8 * t + rr] * aT[rr * 8 + c];
+      K.xad[tid] = s1 + s2;
+    }
     if (tid < 4) K.cs[tid] = a.st->cstep[tid];
   }
   LinAcc<kExact> A;
@@ -1469,11 +1482,14 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
 
 // Solves (L D L^T) y = z in place for the permuted, scaled system of one GN step (n = 4 + 8 nF, a multiple
 // of 4): right-looking LDLT in 4-column blocks with one-block look-ahead, ONE workgroup barrier per block.
-//  wave 0 (the panel wave): in phase k it applies block k's rank-4 update to the rows of column block
-//    k + 1 (one row per lane), takes the updated 4x4 diagonal block from lanes 0-3 (readlane), factors it
-//    uniformly, reduces its row to the (L D) / L entries of panel k + 1 and carries the forward substitution;
-//  waves 1-3: every lower 4x4 tile right of the next panel (register-resident, one per lane) takes block
-//    k's rank-4 update; the owners of column block k + 2 publish it for the panel wave's next phase.
+//  wave 0 (the panel wave): lane l owns row l + 4 for the whole factorization and carries its (L D) entries of
+//    the last panel and its forward-substituted rhs in registers.  In phase k it applies block k's rank-4
+//    update to its row of column block k + 1, takes the updated 4x4 diagonal block from lanes 4k .. 4k+3
+//    (readlane), factors it uniformly and reduces its row to the (L D) / L entries of panel k + 1; it publishes
+//    only L (LT), the pivots and the diagonal rows' rhs;
+//  waves 1-7: every lower 4x4 tile right of the next panel (register-resident, one per lane) takes block
+//    k's rank-4 update (its L D rows formed from LT and the pivots); the owners of column block k + 2 publish it
+//    (row-major, 32 B per row) for the panel wave's next phase.
 // The panel chain (the critical path) thus overlaps the trailing update.  fp64 throughout, FMA-contracted,
 // reciprocals by v_rcp_f64 + 2 Newton steps: the solve is checked against the oracle's Eigen-order LDLT by
 // tolerance (the LDLT is parity-unpinned), not bitwise.  The pivot order is applied by the
@@ -1481,7 +1497,7 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
 //   M  : the permuted system (row-major, stride n), read only
 //   LT : L transposed, LT[i * LSTR + k] = L(k, i); MUST be zero on entry (its upper part stays zero)
 //   W  : scratch of 26 * HS_MAXDIM doubles;  yv : right-hand side in, solution out
-constexpr int LSTR = HS_MAXDIM + 1;  // padded row stride of LT
+constexpr int LSTR = HS_MAXDIM + 2;  // padded row stride of LT (even: 16 B aligned 4-entry groups)
 constexpr int LDLT_SCRATCH = 26 * HS_MAXDIM;
 
 // 1/d: v_rcp_f64 (~2^-26 relative) refined by ONE Newton step (~2^-50, 4e-15 relative) -- the pivots' error
@@ -1506,18 +1522,18 @@ struct PanelOut {
 // its entries of the panel columns, yr its rhs; every lane of the wave executes this.  Column by column: the
 // pivot and the reduced entries come from lanes 0-3 by readlane, so the critical path per column is one
 // readlane, one reciprocal and one multiply-add.  A diagonal row l takes L entries only for j < l.
-__device__ __forceinline__ void panel_coop(const double a[4], double yr, int l, Panel4& P, PanelOut& o) {
+__device__ __forceinline__ void panel_coop(const double a[4], double yr, int l, Panel4& P, PanelOut& o, int base = 0) {
   double pr[4] = {a[0], a[1], a[2], a[3]};
 #pragma unroll
   for (int j = 0; j < 4; j++) {
-    const double d = readlane_f64(pr[j], j);
+    const double d = readlane_f64(pr[j], base + j);
     const double dinv = rcp_f64(d);
-    const double ydj = readlane_f64(yr, j);
+    const double ydj = readlane_f64(yr, base + j);
     P.d[j] = d;
     P.dinv[j] = dinv;
     P.yd[j] = ydj;
 #pragma unroll
-    for (int jp = j + 1; jp < 4; jp++) P.q[jp][j] = readlane_f64(pr[j], jp);
+    for (int jp = j + 1; jp < 4; jp++) P.q[jp][j] = readlane_f64(pr[j], base + jp);
     const double lj = pr[j] * dinv;
     o.lw[j] = l > j ? pr[j] : 0.0;
     o.ls[j] = l > j ? lj : 0.0;
@@ -1565,14 +1581,14 @@ __device__ __forceinline__ void ldlt_solve_blocked(const double* M, double* LT, 
                                                    long long* trace, int dbg = 0) {
   constexpr int MD = HS_MAXDIM;
   static_assert((HS_MAXDIM / 4 - 2) * (HS_MAXDIM / 4 - 1) / 2 <= SOLVE_NT - 64, "one trailing tile per lane");
+  static_assert(LSTR % 2 == 0, "16 B aligned LT groups");
   const int nb = n >> 2;
-  double* PBq = W;            // [2][4][MD] column block k+1 before block k's update, column-major
-  double* LWb = W + 8 * MD;   // [2][4][MD] (L D) of panel k (W + 16 MD .. 24 MD unused)
-  // L of panel k is read back from LT (rows below the panel's diagonal block only: no masking needed)
+  double* PBq = W;            // [2][MD][4] column block k+1 before block k's update, row-major (32 B per row)
+  double* LWb = W + 8 * MD;   // [4][MD] (L D) of panel 0 (the panel wave's initial carry)
   double* Dv = W + 24 * MD;   // [MD] pivots
   double* yf = W + 25 * MD;   // [MD] forward-substituted rhs of the diagonal rows
   const bool pw = tid < 64;   // the panel wave
-  // waves 1-3: trailing tile (tr, tc), tc >= 2, row-major over the lower triangle
+  // waves 1-7: trailing tile (tr, tc), tc >= 2, row-major over the lower triangle
   const int u = tid - 64;
   int trp = 0;
   while ((trp + 1) * (trp + 2) / 2 <= u) trp++;
@@ -1585,7 +1601,7 @@ __device__ __forceinline__ void ldlt_solve_blocked(const double* M, double* LT, 
     for (int c = 0; c < 4; c++) v[i][c] = tile ? M[(4 * tr + i) * n + 4 * tc + c] : 0.0;
   if (tid < n)
 #pragma unroll
-    for (int c = 0; c < 4; c++) PBq[4 * MD + c * MD + tid] = M[tid * n + 4 + c];  // column block 1
+    for (int c = 0; c < 4; c++) PBq[4 * MD + tid * 4 + c] = M[tid * n + 4 + c];  // column block 1
   // prologue: panel 0 over rows 0 .. n-1 by the panel wave (lanes 0-3 also take rows 64 .. n-1)
   if (pw) {
     const int r = min(tid, n - 1);
@@ -1605,42 +1621,68 @@ __device__ __forceinline__ void ldlt_solve_blocked(const double* M, double* LT, 
     }
   }
   __syncthreads();
+  // the panel wave's carry: lane l owns row rw = l + 4 (clamped; rows >= n are never stored)
+  const int rw = min(tid + 4, n - 1);
+  double lwc[4] = {0.0, 0.0, 0.0, 0.0}, ycar = 0.0;
+  if (pw) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) lwc[j] = LWb[j * MD + rw];
+    ycar = yv[rw];
+  }
   for (int k = 0; k + 1 < nb; k++) {
     const int K0 = 4 * (k + 1);
-    const double* LWk = LWb + (k & 1) * 4 * MD;
     const double* LSk = LT + 4 * k * LSTR;  // LSk[j * LSTR + row] = L(row, 4k + j)
     if (trace && tid == 0 && k == 4) trace[16] = clock64();
-    if (pw) {  // panel k+1: row r = K0 + lane
-      const int l = tid, r = min(K0 + l, n - 1);
+    if (pw) {  // panel k+1: lane l owns row rw; the diagonal rows are lanes 4k .. 4k+3
       const double* PBc = PBq + ((k + 1) & 1) * 4 * MD;
-      double a4[4], lwk[4], lsd[4][4];
+      const double4 pb = *reinterpret_cast<const double4*>(PBc + rw * 4);
+      double a4[4] = {pb.x, pb.y, pb.z, pb.w};
+      double lsd[4][4];
 #pragma unroll
       for (int j = 0; j < 4; j++) {
-        a4[j] = PBc[j * MD + r];
-        lwk[j] = LWk[j * MD + r];
-#pragma unroll
-        for (int c = 0; c < 4; c++) lsd[c][j] = LSk[j * LSTR + K0 + c];
+        const double4 q4 = *reinterpret_cast<const double4*>(LSk + j * LSTR + K0);  // L(K0 + c, 4k + j)
+        lsd[0][j] = q4.x;
+        lsd[1][j] = q4.y;
+        lsd[2][j] = q4.z;
+        lsd[3][j] = q4.w;
       }
-      const double yr = yv[r];
 #pragma unroll
       for (int j = 0; j < 4; j++)  // block k's update of this row of column block k+1
 #pragma unroll
-        for (int c = 0; c < 4; c++) a4[c] = __builtin_fma(-lwk[j], lsd[c][j], a4[c]);
+        for (int c = 0; c < 4; c++) a4[c] = __builtin_fma(-lwc[j], lsd[c][j], a4[c]);
+      const int l = tid - 4 * k;  // row rw - K0 (< 0: a row of an earlier panel, inert)
       Panel4 P;
       PanelOut o;
-      panel_coop(a4, yr, l, P, o);
-      if (K0 + l < n)
-        panel_row_store(o, P, r, l, K0, LWb + ((k + 1) & 1) * 4 * MD, LT, Dv, yf, yv);
+      panel_coop(a4, ycar, l, P, o, 4 * k);
+      if (l >= 0 && tid + 4 < n) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) LT[(K0 + j) * LSTR + rw] = o.ls[j];  // zero on and above the diagonal
+        if (l < 4) {
+          Dv[rw] = l == 0 ? P.d[0] : l == 1 ? P.d[1] : l == 2 ? P.d[2] : P.d[3];
+          yf[rw] = o.yr;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++) lwc[j] = o.lw[j];
+      ycar = o.yr;
       if (trace && tid == 0 && k == 4) trace[17] = clock64();
     } else if (tile && tc >= k + 2) {  // block k's rank-4 update of a trailing tile
-      double lw[4][4], ls[4][4];
+      double lw[4][4], ls[4][4], dk[4];
 #pragma unroll
-      for (int j = 0; j < 4; j++)
+      for (int j = 0; j < 4; j++) dk[j] = Dv[4 * k + j];
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-          lw[i][j] = LWk[j * MD + 4 * tr + i];
-          ls[i][j] = LSk[j * LSTR + 4 * tc + i];
-        }
+      for (int j = 0; j < 4; j++) {
+        const double4 r4 = *reinterpret_cast<const double4*>(LSk + j * LSTR + 4 * tr);
+        const double4 c4 = *reinterpret_cast<const double4*>(LSk + j * LSTR + 4 * tc);
+        lw[0][j] = r4.x * dk[j];
+        lw[1][j] = r4.y * dk[j];
+        lw[2][j] = r4.z * dk[j];
+        lw[3][j] = r4.w * dk[j];
+        ls[0][j] = c4.x;
+        ls[1][j] = c4.y;
+        ls[2][j] = c4.z;
+        ls[3][j] = c4.w;
+      }
 #pragma unroll
       for (int j = 0; j < 4; j++)
 #pragma unroll
@@ -1651,8 +1693,7 @@ __device__ __forceinline__ void ldlt_solve_blocked(const double* M, double* LT, 
         double* PBn = PBq + (k & 1) * 4 * MD;
 #pragma unroll
         for (int i = 0; i < 4; i++)
-#pragma unroll
-          for (int c = 0; c < 4; c++) PBn[c * MD + 4 * tr + i] = v[i][c];
+          *reinterpret_cast<double4*>(PBn + (4 * tr + i) * 4) = make_double4(v[i][0], v[i][1], v[i][2], v[i][3]);
       }
     }
     if (trace && tid == 64 && k == 4) trace[18] = clock64();
@@ -1683,9 +1724,13 @@ __device__ __forceinline__ void ldlt_solve_blocked(const double* M, double* LT, 
 #pragma unroll
       for (int j = 3; j >= 0; j--) y = __builtin_fma(-LT[i * LSTR + k0 + j], x[j], y);
       if (i < 4) yv[k0 + i] = i == 0 ? x[0] : i == 1 ? x[1] : i == 2 ? x[2] : x[3];
-      kb = 15;
     }
-    for (; kb >= 0; kb--) {
+    (void)kb;
+    // blocks 15 .. 0 unrolled (no loop-carried branches, so the LT loads of later blocks are issued early); the
+    // blocks at and beyond nb (n <= 64) are all zero (LT zeroed at entry, y = 0 past n) and leave y unchanged
+#pragma unroll
+    for (int kb2 = 15; kb2 >= 0; kb2--) {
+      const int kb = kb2;
       const int k0 = 4 * kb;
       double z[4], Li[4], Ld[4][4];
 #pragma unroll
@@ -1769,8 +1814,8 @@ __device__ __forceinline__ hs::SE3 se3_mul_step(const hs::SE3& A, const hs::SE3&
 
 __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
   __shared__ double A[HS_MAXDIM * HS_MAXDIM];  // the scaled system S H S (row-major, stride n)
-  __shared__ double B[LDLT_SCRATCH];  // LDLT scratch
-  __shared__ double LT[HS_MAXDIM * (HS_MAXDIM + 1)];  // L^T of the factorization (zeroed at entry)
+  __shared__ __align__(16) double B[LDLT_SCRATCH];  // LDLT scratch
+  __shared__ __align__(16) double LT[HS_MAXDIM * LSTR];  // L^T of the factorization (zeroed at entry)
   __shared__ double Nf[2 * HS_MAXDIM * HS_NNS];  // nullspace factors N | Npi (prefetched at entry)
   __shared__ double tk[2 * HS_NNS];
   __shared__ double Sv[HS_MAXDIM], xs[HS_MAXDIM], yv[HS_MAXDIM];
@@ -1809,8 +1854,8 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     const int q = tid + SOLVE_NT * u;
     int rr = -1, cc = -1, ad = -1;
     if (q < ntri) {  // row rr: start(rr) = rr n - rr (rr - 1) / 2 <= q < start(rr + 1)
-      const double t2n = 2.0 * n + 1.0;
-      rr = (int)((t2n - sqrt(t2n * t2n - 8.0 * q)) * 0.5);
+      const float t2n = 2.0f * n + 1.0f;  // small integers: exact in fp32; the row is corrected by +-1 below
+      rr = (int)((t2n - sqrtf(t2n * t2n - 8.0f * q)) * 0.5f);
       rr = max(0, min(rr, n - 1));
       if (rr * n - rr * (rr - 1) / 2 > q) rr--;
       if (rr + 1 < n && (rr + 1) * n - (rr + 1) * rr / 2 <= q) rr++;
@@ -1897,7 +1942,7 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
         for (int k = 0; k < n; k++) hmd += a.HM[q * n + k] * delta(k);
       yv[q] = sq * ((bl + (dgm[HS_MAXDIM + q] + hmd)) + dgv[HS_MAXDIM + q]);
     }
-    for (int idx = tid; idx < HS_MAXDIM * (HS_MAXDIM + 1); idx += nt) LT[idx] = 0.0;  // L^T: zero on entry
+    for (int idx = tid; idx < HS_MAXDIM * LSTR; idx += nt) LT[idx] = 0.0;  // L^T: zero on entry
     __syncthreads();
     HS_TRACE(a, 7);
     // the scaled off-diagonal entries S H S, mirrored from the upper triangle
@@ -1927,19 +1972,22 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     if (tid < n) xs[tid] = Sv[tid] * yv[tid];
     __syncthreads();
     HS_TRACE(a, 4);
-    // the fp32 adjoints for xAd: requested here so their latency overlaps orthogonalize (holding them in
-    // registers across the LDLT costs 32 VGPRs of a kernel at the register limit)
+    if ((a.dbg & 32) && a.trace && tid == 0) a.trace[26] = clock64();
+    // xAd (EnergyFunctional::resubstituteF_MT's per-pair adjoint products) for the granular path only: in the
+    // fused GN loop (HS_APPLY) the linearize kernel forms its host's xAd itself from lastX.  The fp32 adjoints
+    // are requested here so their latency overlaps orthogonalize.
+    const bool wxad = !(a.flags & HS_APPLY);
     float adh[2][8], adt[2][8];
 #pragma unroll
     for (int k = 0; k < 2; k++) {
       const int o = min(tid + k * nt, nF * nF * 8 - 1);
       const int pair = o >> 3, c = o & 7, hh = pair / nF, tt = pair - hh * nF;
-      const float* aHf = a.adHostF + (hh + nF * tt) * 64;
-      const float* aTf = a.adTargetF + (hh + nF * tt) * 64;
+      const float* aHf = a.adHostF + (wxad ? (hh + nF * tt) * 64 : 0);
+      const float* aTf = a.adTargetF + (wxad ? (hh + nF * tt) * 64 : 0);
 #pragma unroll
-      for (int rr = 0; rr < 8; rr++) {
-        adh[k][rr] = aHf[rr * 8 + c];
-        adt[k][rr] = aTf[rr * 8 + c];
+      for (int rr = 0; rr < 8; rr++) {  // not issued in the fused path (a barrier would wait for them)
+        adh[k][rr] = wxad ? aHf[rr * 8 + c] : 0.f;
+        adt[k][rr] = wxad ? aTf[rr * 8 + c] : 0.f;
       }
     }
     if (s_it >= 2) {  // SOLVER_ORTHOGONALIZE_X_LATER: x -= P x, P = (N Npi^T + Npi N^T) / 2 (orthogonalize)
@@ -1949,12 +1997,19 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
         const double* col = Nf + (d < HS_NNS ? n * HS_NNS : 0);  // Npi for t1, N for t2
         const int kk = d % HS_NNS;
         double sacc = 0.0;
-        for (int c = part * len; c < (part + 1) * len; c++) sacc = __builtin_fma(col[c * HS_NNS + kk], xs[c], sacc);
+        // unrolled to the longest quarter (the LDS loads are issued together, not one latency per term)
+#pragma unroll
+        for (int cc = 0; cc < HS_MAXDIM / 4; cc++) {
+          const int c = part * len + min(cc, len - 1);
+          const double t = __builtin_fma(col[c * HS_NNS + kk], xs[c], sacc);
+          sacc = cc < len ? t : sacc;
+        }
         sacc += __shfl_xor(sacc, 1);
         sacc += __shfl_xor(sacc, 2);
         if (part == 0) tk[d] = sacc;
       }
       __syncthreads();
+      if ((a.dbg & 32) && a.trace && tid == 0) a.trace[27] = clock64();
       if (tid < n) {
         double s1 = 0.0, s2 = 0.0;
 #pragma unroll
@@ -1982,11 +2037,12 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
       st->frames[tid].step[9] = 0;
     }
     __syncthreads();
+    if ((a.dbg & 32) && a.trace && tid == 0) a.trace[28] = clock64();
     if (tid < 4) st->cstep[tid] = xF[tid];
 #pragma unroll
     for (int k = 0; k < 2; k++) {
       const int o = tid + k * nt;
-      if (o < nF * nF * 8) {
+      if (wxad && o < nF * nF * 8) {
         const int pair = o >> 3, hh = pair / nF, tt = pair - hh * nF;  // xAd[nF*h + t]
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -1996,6 +2052,7 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
         a.xAd[o] = s1 + s2;
       }
     }
+    if ((a.dbg & 32) && a.trace && tid == 0) a.trace[29] = clock64();
     HS_TRACE(a, 5);
   }
   __syncthreads();

@@ -59,7 +59,8 @@ struct HsLinArgs {
   float margPriorFac;          // setting_idepthFixPriorMargFac
   const HsPrecalc* pre;        // [nF*nF] host*nF + target
   const float* frameTH;        // [nF]
-  const float* xAd;            // [nF*nF][8] index h*nF + t (fuse_step)
+  const float* adHostF;        // [nF*nF][64] index h + nF*t: fp32 adjoints (fuse_step: xAd formed per block)
+  const float* adTargetF;
   // points
   float* idepth;
   float* idepth_zero;
