@@ -13,7 +13,7 @@
 //                the lanes of good points add their pixel's 9x9 acc9 products
 //     reduction  fixed-order LDS sums (acc9 over each wave's lanes, then the 4 waves; acc9SC / E / calcEC over the
 //                block's 32 points) -> block partials
-//                (agent-scope write-through stores) -> the last block to take the ticket sums the partials in block
+//                (release fence + acq_rel ticket) -> the last block to take the ticket acquires and sums the partials in block
 //                order (no block waits on another)
 //     LM         the last block: the sums unpacked by 45 threads; thread 0 the accept test and the lambda / fails /
 //                snapped bookkeeping; the block copies H -> Hm and builds the scaled 6x6 system; thread 0 the
@@ -596,15 +596,18 @@ __global__ __launch_bounds__(RB) void hs_k_refine_step(HsRefArgs a) {
     __hip_atomic_store(&a.part[(size_t)blockIdx.x * HS_REF_NRED + tid], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   REF_TRACE(5);
-  // hand-off: the partials are write-through (agent scope); every storing wave drains, then one lane takes a
-  // ticket; the block whose add returns nblocks - 1 reduces (no block waits on another)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // hand-off (HIP memory model, no reliance on write-through behaviour): every thread's partial store is ordered
+  // before the ticket by an agent-scope release fence, the ticket is an acq_rel read-modify-write, and the block
+  // whose add returns nblocks - 1 takes an agent-scope acquire fence before it reads the other blocks' partials
+  // (no block waits on another)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   __syncthreads();
   if (tid == 0)
-    S.last = __hip_atomic_fetch_add(a.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.nblocks - 1;
+    S.last = __hip_atomic_fetch_add(a.ticket, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == a.nblocks - 1;
   __syncthreads();
   REF_TRACE(6);
   if (!S.last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   if (tid < HS_REF_NRED) {  // block order, up to 64 independent write-through loads in flight per thread
     double s = 0.0;
     const double* pp = a.part + tid;

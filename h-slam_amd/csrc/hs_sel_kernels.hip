@@ -130,6 +130,7 @@ __global__ __launch_bounds__(256) void hs_k_sel_hist(HsSelHistArgs a) {
   }
   __syncthreads();
   if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every thread of the last block sees the other blocks' ths
   const int w32 = a.w32, h32 = a.h32;
   auto T = [&](int x, int y) { return __hip_atomic_load(&a.ths[x + y * w32], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
   for (int c = t; c < w32 * h32; c += 256) {
