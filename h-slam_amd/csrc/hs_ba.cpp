@@ -38,6 +38,11 @@ int fail(int code, const std::string& msg) {
 constexpr int kLogCap = 4096;     // energies logged on the device per optimize / iterate call
 constexpr int kEventIters = 128;  // iterations timed with HIP events per call
 constexpr int kLinBlocksTarget = 256;  // linearize blocks of a window (points per wave grows beyond that)
+// hs_k_lin8 (lane = (point, target slot), 8 points per wave at a time) takes the production linearization from this
+// many points up: its wave issues ~2.3x fewer instructions per point (throughput), while hs_k_lin's one-point waves
+// finish a small window sooner (latency).  Env HS_LIN8=0 / 1 forces either.
+constexpr int kLin8MinPoints = 60000;
+constexpr int kLin8BlocksTarget = 512;  // hs_k_lin8 blocks of a window (two 4-wave blocks per CU)
 }  // namespace
 
 #define HS_HIP(x)                                                                                  \
@@ -80,6 +85,7 @@ struct hs_ctx {
   std::vector<int> blk_begin;
   int nblk = 0, W = 4, ne = 0, Q = 0;
   bool exact = false;
+  bool lin8 = false;              // production linearizations run hs_k_lin8 (4-wave blocks, W = 4)
   bool sepValid = false;          // d_sep holds the separate HA / HSC of the last linearization
   std::vector<int> pt_host, res_point, res_target, host_pt_begin;
   std::vector<int> res_of_slot;   // [nP*8]
@@ -284,8 +290,12 @@ static int launch_linearize(hs_ctx* c, int fuse, bool marg = false, bool accumul
   a.part = c->d_part; a.part_e = c->d_part_e;
   a.trace = c->d_tr_lin;
   if (c->nblk > 0) {
-    auto k = c->exact ? (fix ? hs_k_lin_exact_fix : hs_k_lin_exact) : (fix ? hs_k_lin_fix : hs_k_lin);
-    hipLaunchKernelGGL(k, dim3(c->nblk), dim3(HS_LIN_NT), lin_lds(c), c->stream, a);
+    if (c->lin8 && !marg && !fix) {
+      hipLaunchKernelGGL(hs_k_lin8, dim3(c->nblk), dim3(HS_LIN8_NT), 0, c->stream, a);
+    } else {
+      auto k = c->exact ? (fix ? hs_k_lin_exact_fix : hs_k_lin_exact) : (fix ? hs_k_lin_fix : hs_k_lin);
+      hipLaunchKernelGGL(k, dim3(c->nblk), dim3(HS_LIN_NT), lin_lds(c), c->stream, a);
+    }
   }
   HS_HIP(hipGetLastError());
   std::swap(c->d_p_HdiF, c->d_p_HdiF_alt);
@@ -677,13 +687,19 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
   c->ne = hs_ne(c->exact);
   c->Q = (c->ne * 64 + 255) / 256;
   c->blk_begin.assign(nF + 1, 0);
-  int ppw = std::max(1, (nP + HS_LIN_NW * kLinBlocksTarget - 1) / (HS_LIN_NW * kLinBlocksTarget));
+  c->lin8 = !c->exact && nP >= kLin8MinPoints;
+  if (const char* e = std::getenv("HS_LIN8")) c->lin8 = !c->exact && e[0] == '1';
+  // points per block: hs_k_lin HS_LIN_NW waves x ppw points; hs_k_lin8 4 waves x ppw groups of 8 points (its
+  // partition also serves hs_k_lin's marginalization / linearizeAll(true) passes, with W = 4 of its waves)
+  const int bw = c->lin8 ? (HS_LIN8_NT / 64) * 8 : HS_LIN_NW;
+  const int target = c->lin8 ? kLin8BlocksTarget : kLinBlocksTarget;
+  int ppw = std::max(1, (nP + bw * target - 1) / (bw * target));
   if (const char* e = std::getenv("HS_LIN_PPW")) ppw = std::max(1, std::atoi(e));
-  c->W = c->exact ? 1 : HS_LIN_NW;
+  c->W = c->exact ? 1 : (c->lin8 ? HS_LIN8_NT / 64 : HS_LIN_NW);
   for (int h = 0; h < nF; h++) {
     const int nh = c->host_pt_begin[h + 1] - c->host_pt_begin[h];
     if (c->exact && nh > 1000) return fail(HS_ERR_INVALID, "HS_ACC_EXACT supports at most 1000 points per host");
-    const int nb = nh == 0 ? 0 : (c->exact ? 1 : (nh + HS_LIN_NW * ppw - 1) / (HS_LIN_NW * ppw));
+    const int nb = nh == 0 ? 0 : (c->exact ? 1 : (nh + bw * ppw - 1) / (bw * ppw));
     c->blk_begin[h + 1] = c->blk_begin[h] + nb;
   }
   c->nblk = c->blk_begin[nF];

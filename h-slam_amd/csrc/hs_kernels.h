@@ -11,6 +11,7 @@ constexpr int HS_SOLVE_NT = 512;   // hs_k_solve workgroup size
 constexpr int HS_STITCH_NT = 1024; // hs_k_stitch workgroup size
 constexpr int HS_LIN_NW = 8;       // hs_k_lin waves per block (production: each takes points; exact mode: wave 0)
 constexpr int HS_LIN_NT = 64 * HS_LIN_NW;
+constexpr int HS_LIN8_NT = 256;    // hs_k_lin8 workgroup size (4 waves, 8 points per wave at a time)
 constexpr int HS_NNS = 7;         // gauge nullspaces: 6 pose + 1 scale (System::getNullspaces)
 
 // Window state owned by the device between GN iterations (updated by hs_k_solve).
@@ -183,6 +184,7 @@ __global__ void hs_k_lin(HsLinArgs a);        // production partitioning
 __global__ void hs_k_lin_exact(HsLinArgs a);  // HS_ACC_EXACT: one wave per host, the reference's sums
 __global__ void hs_k_lin_fix(HsLinArgs a);        // + linearizeAll(true)'s per-point bookkeeping
 __global__ void hs_k_lin_exact_fix(HsLinArgs a);
+__global__ void hs_k_lin8(HsLinArgs a);       // production: lane = (point, target slot), 8 points per wave
 __global__ void hs_k_reduce(HsRedArgs a);
 __global__ void hs_k_debug_th(HsRedArgs a);     // test hook: the threshold select block alone
 __global__ void hs_k_stitch(HsStitchArgs a);

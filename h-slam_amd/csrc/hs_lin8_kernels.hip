@@ -1,0 +1,586 @@
+// hs_lin8_kernels.hip — the production linearize + accumulate kernel of the BA hot path (gfx950).
+//
+// Same work and outputs as hs_k_lin (hs_ba_kernels.hip) for the production partitioning of the GN loop:
+//   resubstituteFPt + point step of the previous solve (Src/EnergyFunctional.cpp:249-274),
+//   PointFrameResidual::linearize + applyRes / takeData (Src/OptimizationClasses.cpp:43-256),
+//   the per-point Schur prelude of AccumulatedSCHessianSSE::addPoint (Src/AccumulatedSCHessian.cpp:10-33),
+//   and the AccumulatorApprox / accD / accE / accEB / accHcc / accbc updates
+//   (Src/AccumulatedTopHessian.cpp:21-141, Src/AccumulatedSCHessian.cpp:32-51, Include/MatrixAccumulators.h)
+//   into block partials in hs_k_lin's production layout (hs_kernels.h, HS_E_TOP), which hs_k_reduce / hs_k_stitch
+//   consume unchanged.
+// Lane layout: lane = (point pl, target slot t); a wave takes 8 consecutive points at a time and every lane loops
+// over the 8 pattern pixels of its residual.  So the per-residual work (centre projection, Jacobians, state
+// decision, takeData) and the per-point work (fused step, residual-list sums, Schur prelude) are done once per
+// lane instead of once per pixel lane, and the pattern-order sums are plain in-lane running sums: one wave
+// instruction now serves 8 points where hs_k_lin's serves one.  Per-residual arithmetic keeps the reference's
+// operation order (fp contraction off): states, energies, JpJdF, centre projections, HdiF / bdSumF / Hcd and the
+// point steps are bit-identical to hs_k_lin's (and the oracle's).  The accumulators are production sums (fp32 per
+// lane, the block partial in fixed wave / lane order, FMA-contracted), checked against the reference's order by
+// tolerance like hs_k_lin's production partitioning.  Not used for the marginalization pass, linearizeAll(true)'s
+// bookkeeping or HS_ACC_EXACT (hs_k_lin serves those).
+#pragma clang fp contract(off)
+#include <hip/hip_runtime.h>
+
+#include "hs_kernels.h"
+
+namespace {
+
+constexpr float SCALE_F8 = 50.0f, SCALE_C8 = 50.0f, SCALE_IDEPTH8 = 1.0f;
+constexpr int L8_NW = HS_LIN8_NT / 64;  // waves per block
+constexpr int NTOP = 91;  // AccumulatorApprox entries of one (host, target) block: Data 55 | TopRight 30 | BotRight 6
+constexpr int Q8_N = 17;  // per-pixel quantities summed over the pattern
+
+// Data (r, c), r <= c < 10, in the natural per-lane layout
+__host__ __device__ constexpr int didx(int r, int c) { return r * 10 - (r * (r - 1)) / 2 + (c - r); }
+constexpr int TR0 = 55, BR0 = 85;
+
+// getInterpolatedElement33 (Include/GlobalTypes.h:377-388) on float4 texels
+__device__ __forceinline__ float3 interp33_8(const float4* __restrict__ img, float x, float y, int w) {
+  int ix = (int)x, iy = (int)y;
+  float dx = x - ix, dy = y - iy, dxdy = dx * dy;
+  const float4* bp = img + ix + iy * w;
+  const float4 p00 = bp[0], p10 = bp[1], p01 = bp[w], p11 = bp[w + 1];
+  const float w11 = dxdy, w01 = dy - dxdy, w10 = dx - dxdy, w00 = 1 - dx - dy + dxdy;
+  float3 r;
+  r.x = w11 * p11.x + w01 * p01.x + w10 * p10.x + w00 * p00.x;
+  r.y = w11 * p11.y + w01 * p01.y + w10 * p10.y + w00 * p00.y;
+  r.z = w11 * p11.z + w01 * p01.z + w10 * p10.z + w00 * p00.z;
+  return r;
+}
+
+// the block's constants (host h's precalc by target slot, thresholds, xAd[h][t][.], calib step)
+struct L8Const {
+  HsPrecalc pre[HS_MAXF];
+  float th[HS_MAXF];
+  float xad[HS_MAXF * 8];
+  float cs[4];
+};
+// per-wave LDS scratch of a point group
+struct L8Scratch {
+  float ps[8][8][8];  // [point][slot][tbd, tHdd, tc0..3, econ, -]: the residuals' terms of the per-point sums
+  float jb[8][8][8];  // [point][pattern row i][non-host slot o]: JpJdF (0 unless active), accD / accE operand
+  float pp[8][8];     // [point][HdiF, bdSumF, Hcd0..3, -, -]
+};
+// the epilogue's per-wave partials: T (natural layout, summed over the wave's point lanes) and the D / E / C lanes
+struct L8Part {
+  float T[L8_NW][8][NTOP + 1];
+  float DEC[L8_NW][HS_ND_PROD + 6][64];
+};
+union L8Lds {
+  L8Scratch s[L8_NW];
+  L8Part part;
+};
+
+// the owner of entry e of lane (t, k) in hs_k_lin's production layout, as an index of the natural T layout
+// (-1: the entry is never read by hs_k_reduce / hs_k_stitch)
+__device__ __forceinline__ int owner_map(int e, int k) {
+  if (e < 8) return e <= k ? didx(e, k) : -1;           // Data (e, k), e <= k
+  if (e == 8) return didx(k, 8);                         // Data (k, 8)
+  if (e == 9) return didx(k, 9);                         // Data (k, 9)
+  if (e == 10) return k == 0 ? didx(8, 8) : k == 1 ? didx(8, 9) : k == 2 ? didx(9, 9) : -1;
+  if (e < 14) return TR0 + k * 3 + (e - 11);             // TopRight (k, a | b | r)
+  if (e == 14) return k < 6 ? TR0 + (8 + k / 3) * 3 + k % 3 : -1;  // TopRight (8 + k/3, k%3)
+  return k < 6 ? BR0 + k : -1;                           // BotRight[k]
+}
+
+__device__ __forceinline__ float dpp_ror8(float v) {  // lane l <- lane l ^ 8 (rotate a row of 16 by 8)
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false));
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(HS_LIN8_NT) void hs_k_lin8(HsLinArgs a) {
+  __shared__ L8Const K;
+  __shared__ L8Lds U;
+  const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int pl = lane >> 3, t = lane & 7;  // point of the group, target slot
+  const int b = blockIdx.x;
+  const int nF = a.nF;
+  int h = 0;  // the block's host
+#pragma unroll
+  for (int i = 1; i < HS_MAXF; i++) h += (i < nF && b >= a.blk_begin[i]) ? 1 : 0;
+  const int nb = a.blk_begin[h + 1] - a.blk_begin[h], q = b - a.blk_begin[h];
+  const int hb = a.host_begin[h], nh = a.host_begin[h + 1] - hb;
+  const int pb = hb + (int)((long long)nh * q / nb), pe = hb + (int)((long long)nh * (q + 1) / nb);
+  if (a.trace && tid == 0) a.trace[(size_t)b * 16] = wall_clock64();
+  {  // block constants: as hs_k_lin
+    constexpr int PW = (int)(sizeof(HsPrecalc) / 4);
+    const int* src = reinterpret_cast<const int*>(a.pre + h * nF);
+    int* dst = reinterpret_cast<int*>(K.pre);
+    for (int i = tid; i < nF * PW; i += HS_LIN8_NT) dst[i] = src[i];
+    if (tid < nF) K.th[tid] = a.frameTH[tid];
+    if (a.fuse_step && tid < nF * 8) {
+      // xAd[h][t][c] of the last solve (resubstituteF_MT, Src/EnergyFunctional.cpp:222-247), the solve's order
+      const int tt = tid >> 3, c = tid & 7;
+      const float* aH = a.adHostF + (h + nF * tt) * 64;
+      const float* aT = a.adTargetF + (h + nF * tt) * 64;
+      const double* lx = a.st->lastX;
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int rr = 0; rr < 8; rr++) s1 += (float)lx[4 + 8 * h + rr] * aH[rr * 8 + c];
+#pragma unroll
+      for (int rr = 0; rr < 8; rr++) s2 += (float)lx[4 + 8 * tt + rr] * aT[rr * 8 + c];
+      K.xad[tid] = s1 + s2;
+    }
+    if (tid < 4) K.cs[tid] = a.st->cstep[tid];
+  }
+  __syncthreads();
+
+  const HsCalib cal = a.st->dcal;
+  const HsLinParams lp = a.lp;
+  const int tc = t < nF ? t : 0;
+  const float4* timg = a.img + tc * a.img_stride;  // slots past the window read frame 0 (never used)
+  L8Scratch& W = U.s[wv];
+  const int oslot = t - (t > h ? 1 : 0);           // non-host slot index of t (t != h)
+
+  // accumulators: T natural layout of (host h, target t) over the lane's residuals; D lane (row, col) = (pl, t),
+  // E lane (t, k) = (pl, t) read as (slot pl, row t); C lanes 0..19
+  float T[NTOP];
+#pragma unroll
+  for (int i = 0; i < NTOP; i++) T[i] = 0.f;
+  float D[HS_ND_PROD];
+#pragma unroll
+  for (int i = 0; i < HS_ND_PROD; i++) D[i] = 0.f;
+  float E[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  float C = 0.f;
+  double eA = 0.0, sidA = 0.0, npA = 0.0;
+
+  const int ngroups = (pe - pb + 7) >> 3;
+  for (int gi = wv; gi < ngroups; gi += a.W) {  // wave-uniform
+    const int p = pb + gi * 8 + pl;
+    const bool valid = p < pe;
+    const int pc = valid ? p : pe - 1;
+    const int sl = pc * 8 + t;
+    // ---- loads (unconditional, clamped)
+    float idep = a.idepth[pc], idep0 = a.idepth_zero[pc];
+    const float pu = a.u[pc], pv = a.v[pc];
+    const int res = a.res_of_slot[sl];
+    const int st_raw = (int)a.r_state[sl];
+    const float oldE = a.r_energy[sl], oldNewE = a.r_newEnergy[sl];
+    const uint2 ro2 = reinterpret_cast<const uint2*>(a.res_order)[pc];
+    const unsigned fm = a.p_actmask[pc];
+    const float4 jp0 = reinterpret_cast<const float4*>(a.p_JpJdF)[sl * 2];
+    const float4 jp1 = reinterpret_cast<const float4*>(a.p_JpJdF)[sl * 2 + 1];
+    const float bds = a.p_bdSumF[pc], hdi = a.p_HdiF_prev[pc];
+    const float4 hcd = reinterpret_cast<const float4*>(a.p_Hcd)[pc];
+    const float4 co0 = reinterpret_cast<const float4*>(a.color)[pc * 2];
+    const float4 co1 = reinterpret_cast<const float4*>(a.color)[pc * 2 + 1];
+    const float4 we0 = reinterpret_cast<const float4*>(a.weight)[pc * 2];
+    const float4 we1 = reinterpret_cast<const float4*>(a.weight)[pc * 2 + 1];
+    const float priorF = a.priorF[pc];
+    const float colK[8] = {co0.x, co0.y, co0.z, co0.w, co1.x, co1.y, co1.z, co1.w};
+    const float wgtK[8] = {we0.x, we0.y, we0.z, we0.w, we1.x, we1.y, we1.z, we1.w};
+    auto res_slot = [&](int qq) -> int { return (int)(int8_t)(((qq < 4 ? ro2.x : ro2.y) >> (8 * (qq & 3))) & 0xffu); };
+    const HsPrecalc pcr = K.pre[tc];
+    const float thr = fmaxf(K.th[h], K.th[tc]);  // std::max<float>(host TH, target TH)
+
+    if (a.fuse_step) {
+      // resubstituteFPt + the point part of doStepFromBackup (stepfacD = 1): the slot's 8-term dot in order, the
+      // listed residuals' dots subtracted in list order (each lane of the point's octet does the same)
+      const unsigned m = fm;
+      const bool on = (m >> t) & 1u;
+      const float4 x0 = *reinterpret_cast<const float4*>(&K.xad[tc * 8]);
+      const float4 x1 = *reinterpret_cast<const float4*>(&K.xad[tc * 8 + 4]);
+      const float xa[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+      const float jpj[8] = {jp0.x, jp0.y, jp0.z, jp0.w, jp1.x, jp1.y, jp1.z, jp1.w};
+      float dsum = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; k++) dsum = dsum + (on ? xa[k] * jpj[k] : 0.f);
+      float bq = bds;
+      float dot = 0.f;
+      dot += K.cs[0] * hcd.x;
+      dot += K.cs[1] * hcd.y;
+      dot += K.cs[2] * hcd.z;
+      dot += K.cs[3] * hcd.w;
+      bq -= dot;
+      float dl[8];
+#pragma unroll
+      for (int qq = 0; qq < 8; qq++) {
+        const int tt = res_slot(qq);
+        dl[qq] = __shfl(dsum, pl * 8 + (tt < 0 ? 0 : tt));
+      }
+      bool live = true;
+#pragma unroll
+      for (int qq = 0; qq < 8; qq++) {
+        const int tt = res_slot(qq);
+        live = live && tt >= 0;
+        const int ts = tt < 0 ? 0 : tt;
+        const float bn = bq - dl[qq];
+        bq = (live && ((m >> ts) & 1u)) ? bn : bq;
+      }
+      const float step = m != 0u ? -bq * hdi : 0.f;
+      idep = idep + 1.0f * step;
+      idep0 = idep;
+      if (valid && t == 0) {
+        a.idepth[p] = idep;
+        a.idepth_zero[p] = idep;
+        a.p_step[p] = step;
+      }
+    }
+
+    const bool has = valid && res >= 0;
+    const int st = has ? st_raw : HS_RES_OOB;
+    const bool live0 = has && st != HS_RES_OOB;
+    // ---- centre projection + geometric Jacobian: projectPoint(u, v, idepth_zero, 0, 0, R_0, t_0)
+    //      (Include/DirectProjection.h:20-38, Src/OptimizationClasses.cpp:62-118)
+    float Jx[10], Jy[10], Jd0, Jd1, centre[3];
+    bool okC;
+    {
+      const float Kl0 = (pu + 0 - cal.cxl) * cal.fxli;
+      const float Kl1 = (pv + 0 - cal.cyl) * cal.fyli;
+      float pt0 = pcr.R0[0] * Kl0 + pcr.R0[1] * Kl1 + pcr.R0[2] * 1.f;
+      float pt1 = pcr.R0[3] * Kl0 + pcr.R0[4] * Kl1 + pcr.R0[5] * 1.f;
+      float pt2 = pcr.R0[6] * Kl0 + pcr.R0[7] * Kl1 + pcr.R0[8] * 1.f;
+      pt0 = pt0 + pcr.t0[0] * idep0;
+      pt1 = pt1 + pcr.t0[1] * idep0;
+      pt2 = pt2 + pcr.t0[2] * idep0;
+      const float drescale = 1.0f / pt2;
+      const float new_idepth = idep0 * drescale;
+      const float u = pt0 * drescale, v = pt1 * drescale;
+      const float Ku = u * cal.fxl + cal.cxl, Kv = v * cal.fyl + cal.cyl;
+      okC = (drescale > 0) && (Ku > 1.1f && Kv > 1.1f && Ku < (cal.W - 3) && Kv < (cal.H - 3));
+      centre[0] = Ku; centre[1] = Kv; centre[2] = new_idepth;
+      const float* R0 = pcr.R0;
+      const float* t0 = pcr.t0;
+      Jd0 = drescale * (t0[0] - t0[2] * u) * SCALE_IDEPTH8 * cal.fxl;
+      Jd1 = drescale * (t0[1] - t0[2] * v) * SCALE_IDEPTH8 * cal.fyl;
+      float cx[4], cy[4];
+      cx[2] = drescale * (R0[6] * u - R0[0]);
+      cx[3] = cal.fxl * drescale * (R0[7] * u - R0[1]) * cal.fyli;
+      cx[0] = Kl0 * cx[2];
+      cx[1] = Kl1 * cx[3];
+      cy[2] = cal.fyl * drescale * (R0[6] * v - R0[3]) * cal.fxli;
+      cy[3] = drescale * (R0[7] * v - R0[4]);
+      cy[0] = Kl0 * cy[2];
+      cy[1] = Kl1 * cy[3];
+      cx[0] = (cx[0] + u) * SCALE_F8;
+      cx[1] *= SCALE_F8;
+      cx[2] = (cx[2] + 1) * SCALE_C8;
+      cx[3] *= SCALE_C8;
+      cy[0] *= SCALE_F8;
+      cy[1] = (cy[1] + v) * SCALE_F8;
+      cy[2] *= SCALE_C8;
+      cy[3] = (cy[3] + 1) * SCALE_C8;
+      const float fx = cal.fxl, fy = cal.fyl;
+      Jx[0] = cx[0]; Jx[1] = cx[1]; Jx[2] = cx[2]; Jx[3] = cx[3];
+      Jy[0] = cy[0]; Jy[1] = cy[1]; Jy[2] = cy[2]; Jy[3] = cy[3];
+      Jx[4] = new_idepth * fx;
+      Jx[5] = 0;
+      Jx[6] = -new_idepth * u * fx;
+      Jx[7] = -u * v * fx;
+      Jx[8] = (1 + u * u) * fx;
+      Jx[9] = -v * fx;
+      Jy[4] = 0;
+      Jy[5] = new_idepth * fy;
+      Jy[6] = -new_idepth * v * fy;
+      Jy[7] = -(1 + v * v) * fy;
+      Jy[8] = u * v * fy;
+      Jy[9] = u * fy;
+    }
+    // ---- the 8 pattern pixels (staticPattern[8], Include/GlobalTypes.h:181-184) in order: in-lane running sums
+    //      are the reference's pattern-order sums; a failing pixel (the reference's early exit) marks the slot OOB
+    //      and its (redirected, finite) values are never read
+    float S[Q8_N];
+#pragma unroll
+    for (int i = 0; i < Q8_N; i++) S[i] = 0.f;
+    bool slotOob = false;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      constexpr int PDX[8] = {0, -1, 1, -2, 0, 2, -1, 0};
+      constexpr int PDY[8] = {-2, -1, -1, 0, 0, 0, 1, 2};
+      const float px = pu + PDX[k], py = pv + PDY[k];
+      float q0 = pcr.KRKi[0] * px + pcr.KRKi[1] * py + pcr.KRKi[2] * 1.f;
+      float q1 = pcr.KRKi[3] * px + pcr.KRKi[4] * py + pcr.KRKi[5] * 1.f;
+      float q2 = pcr.KRKi[6] * px + pcr.KRKi[7] * py + pcr.KRKi[8] * 1.f;
+      q0 = q0 + pcr.Kt[0] * idep;
+      q1 = q1 + pcr.Kt[1] * idep;
+      q2 = q2 + pcr.Kt[2] * idep;
+      const float PKu = q0 / q2, PKv = q1 / q2;
+      const bool okP = okC && (PKu > 1.1f && PKv > 1.1f && PKu < (cal.W - 3) && PKv < (cal.H - 3));
+      const float3 hit = interp33_8(timg, okP ? PKu : 2.f, okP ? PKv : 2.f, cal.W);
+      const float color = colK[k];
+      const float residual = hit.x - (float)(pcr.aff[0] * color + pcr.aff[1]);
+      const float drdA = (color - pcr.b0);
+      const bool okI = okP && isfinite(hit.x);
+      slotOob = slotOob || (live0 && !okI);
+      float w = sqrtf(lp.outlierTHSumComponent / (lp.outlierTHSumComponent + (hit.y * hit.y + hit.z * hit.z)));
+      w = 0.5f * (w + wgtK[k]);
+      float hw = fabsf(residual) < lp.huberTH ? 1 : lp.huberTH / fabsf(residual);
+      float qv[Q8_N];
+      qv[0] = w * w * hw * residual * residual * (2 - hw);
+      hw = hw < 1 ? sqrtf(hw) : hw;
+      hw = hw * w;
+      const float hy = hit.y * hw, hz = hit.z * hw;
+      const float resF = residual * hw;
+      float jab0 = drdA * hw;
+      float jab1 = hw;
+      qv[1] = hy * hy;
+      qv[2] = hz * hz;
+      qv[3] = hy * hz;
+      qv[4] = drdA * hw * hy;
+      qv[5] = drdA * hw * hz;
+      qv[6] = hw * hy;
+      qv[7] = hw * hz;
+      qv[8] = drdA * drdA * hw * hw;
+      qv[9] = drdA * hw * hw;
+      qv[10] = hw * hw;
+      qv[11] = hw * hw * (hy * hy + hz * hz);
+      if (lp.affineOptModeA < 0) jab0 = 0;
+      if (lp.affineOptModeB < 0) jab1 = 0;
+      const float rz = resF;  // addPoint<0>: resApprox = resF
+      qv[12] = rz * hy;
+      qv[13] = rz * hz;
+      qv[14] = rz * jab0;
+      qv[15] = rz * jab1;
+      qv[16] = rz * rz;
+#pragma unroll
+      for (int i = 0; i < Q8_N; i++) S[i] = S[i] + qv[i];
+    }
+
+    // ---- state decision + applyRes (Src/OptimizationClasses.cpp:128-133,235-256)
+    const bool eval = live0 && !slotOob;
+    const bool isOut = S[0] > thr || S[11] < 2;
+    const float energyLeft = isOut ? thr : S[0];
+    const bool active = eval && !isOut;
+    const float econ = eval ? energyLeft : oldE;
+    if (has) {
+      a.r_ewo[sl] = eval ? S[0] : -1.f;
+      if (live0) {
+        a.r_state[sl] = (uint8_t)(slotOob ? HS_RES_OOB : (isOut ? HS_RES_OUT : HS_RES_IN));
+        a.r_active[sl] = active ? 1 : 0;
+        a.r_energy[sl] = slotOob ? oldNewE : energyLeft;
+        if (!slotOob) a.r_newEnergy[sl] = energyLeft;
+      }
+      if (a.write_center && live0 && okC) {
+        a.r_center[sl * 3 + 0] = centre[0];
+        a.r_center[sl * 3 + 1] = centre[1];
+        a.r_center[sl * 3 + 2] = centre[2];
+      }
+    }
+    if (valid && t == nF - 1) a.newest_cand[p] = eval ? S[0] : -1.f;
+    // ---- takeData (Include/OptimizationClasses.h:155-161): JpJdF and the slot's terms of the per-point sums
+    float jj[8], tbd, tHdd, tcd[4];
+    {
+      const float J00 = S[1], J11 = S[2], J10 = S[3];
+      const float aa = J00 * Jd0 + J10 * Jd1;
+      const float bb = J10 * Jd0 + J11 * Jd1;
+      tbd = S[12] * Jd0 + S[13] * Jd1;
+      tHdd = aa * Jd0 + bb * Jd1;
+#pragma unroll
+      for (int c = 0; c < 4; c++) tcd[c] = Jx[c] * aa + Jy[c] * bb;
+#pragma unroll
+      for (int k = 0; k < 6; k++) jj[k] = Jx[4 + k] * aa + Jy[4 + k] * bb;
+      jj[6] = S[4] * Jd0 + S[5] * Jd1;
+      jj[7] = S[6] * Jd0 + S[7] * Jd1;
+      if (active) {
+        float4* jo = reinterpret_cast<float4*>(a.p_JpJdF) + sl * 2;
+        jo[0] = make_float4(jj[0], jj[1], jj[2], jj[3]);
+        jo[1] = make_float4(jj[4], jj[5], jj[6], jj[7]);
+      }
+    }
+    // ---- per-point sums in the point's residual-list order (every lane of the octet forms them)
+    const unsigned long long actBits = __ballot(active);
+    const unsigned amask8 = (unsigned)(actBits >> (pl * 8)) & 0xffu;  // the point's active slots
+    *reinterpret_cast<float4*>(&W.ps[pl][t][0]) = make_float4(tbd, tHdd, tcd[0], tcd[1]);
+    *reinterpret_cast<float4*>(&W.ps[pl][t][4]) = make_float4(tcd[2], tcd[3], econ, 0.f);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    float qs[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    double eSum = 0.0;
+    unsigned mask = 0u;
+    {
+      float g[8][8];
+#pragma unroll
+      for (int qq = 0; qq < 8; qq++) {
+        const int tt = res_slot(qq) & 7;
+        const float4 g0 = *reinterpret_cast<const float4*>(&W.ps[pl][tt][0]);
+        const float4 g1 = *reinterpret_cast<const float4*>(&W.ps[pl][tt][4]);
+        g[qq][0] = g0.x; g[qq][1] = g0.y; g[qq][2] = g0.z; g[qq][3] = g0.w;
+        g[qq][4] = g1.x; g[qq][5] = g1.y; g[qq][6] = g1.z;
+      }
+      bool listed = true;
+#pragma unroll
+      for (int qq = 0; qq < 8; qq++) {
+        const int tr = res_slot(qq);
+        listed = listed && tr >= 0;
+        const int tt = tr & 7;
+        const double e1 = eSum + (double)g[qq][6];
+        eSum = listed ? e1 : eSum;
+        const bool act = listed && ((amask8 >> tt) & 1u);
+        mask |= act ? 1u << tt : 0u;
+#pragma unroll
+        for (int i = 0; i < 6; i++) {
+          const float s1 = qs[i] + g[qq][i];
+          qs[i] = act ? s1 : qs[i];
+        }
+      }
+    }
+    const float bd = qs[0], Hdd = qs[1];
+    float HdiF = 0.f, bdSumF = 0.f;
+    if (mask != 0u) {
+      float Hh = Hdd + 0.f + priorF;  // Hdd_accAF + Hdd_accLF + priorF
+      if ((double)Hh < 1e-10) Hh = (float)1e-10;
+      HdiF = (float)(1.0 / (double)Hh);
+      bdSumF = bd + 0.f;
+      bdSumF += priorF * (idep - idep0);
+    }
+    const float4 hc4 = make_float4(qs[2] + 0.f, qs[3] + 0.f, qs[4] + 0.f, qs[5] + 0.f);
+    if (valid && t == 0) {
+      a.p_actmask[p] = (uint8_t)mask;
+      a.p_HdiF[p] = HdiF;
+      a.p_bdSumF[p] = bdSumF;
+      reinterpret_cast<float4*>(a.p_Hcd)[p] = hc4;
+      eA += eSum;
+      sidA += (double)fabsf(idep);
+      npA += 1.0;
+    }
+    if (!a.accumulate) continue;
+
+    // ---- AccumulatedTopHessianSSE::addPoint<0> of this lane's residual (AccumulatorApprox update / updateTopRight
+    //      / updateBotRight, Include/MatrixAccumulators.h:754-915): the 13x13 block of (host, t) in natural layout
+    {
+#pragma clang fp contract(fast)
+      if (active) {
+        const float a_ = S[1], b_ = S[3], c_ = S[2];  // JIdx2 00, 01, 11
+        float uu[10], ww[10];
+#pragma unroll
+        for (int r = 0; r < 10; r++) {
+          uu[r] = a_ * Jx[r] + b_ * Jy[r];
+          ww[r] = b_ * Jx[r] + c_ * Jy[r];
+        }
+#pragma unroll
+        for (int r = 0; r < 10; r++)
+#pragma unroll
+          for (int c = r; c < 10; c++) T[didx(r, c)] += uu[r] * Jx[c] + ww[r] * Jy[c];
+        const float tr0[3] = {S[4], S[6], S[12]}, tr1[3] = {S[5], S[7], S[13]};
+#pragma unroll
+        for (int r = 0; r < 10; r++)
+#pragma unroll
+          for (int c = 0; c < 3; c++) T[TR0 + r * 3 + c] += Jx[r] * tr0[c] + Jy[r] * tr1[c];
+        const float br[6] = {S[8], S[9], S[14], S[10], S[15], S[16]};
+#pragma unroll
+        for (int i = 0; i < 6; i++) T[BR0 + i] += br[i];
+      }
+    }
+    // ---- Schur accumulators (Src/AccumulatedSCHessian.cpp:32-51) through the wave's scratch: accD (lane = (row,
+    //      col) of every (o1 <= o2) block), accE / accEB (lane = (slot, row)), accHcc / accbc (lanes 0..19)
+    if (t != h) {
+#pragma unroll
+      for (int i = 0; i < 8; i++) W.jb[pl][i][oslot] = active ? jj[i] : 0.f;
+    }
+    if (t == 0) {
+      *reinterpret_cast<float4*>(&W.pp[pl][0]) = make_float4(HdiF, bdSumF, hc4.x, hc4.y);
+      *reinterpret_cast<float4*>(&W.pp[pl][4]) = make_float4(hc4.z, hc4.w, 0.f, 0.f);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    {
+#pragma clang fp contract(fast)
+      const int dr = pl, dc = t;         // accD lane (row, col)
+      const int es = pl, ek = t;         // accE lane (slot es, row ek)
+      const int eo = es - (es > h ? 1 : 0);
+      const int cr = (lane >> 2) & 3, ccol = lane & 3;
+      const unsigned long long wbits = actBits;
+#pragma unroll
+      for (int qp = 0; qp < 8; qp++) {
+        const unsigned mq = (unsigned)(wbits >> (qp * 8)) & 0xffu;  // uniform
+        if (mq == 0u) continue;
+        const float4 pp0 = *reinterpret_cast<const float4*>(&W.pp[qp][0]);
+        const float4 pp1 = *reinterpret_cast<const float4*>(&W.pp[qp][4]);
+        const float hdf = pp0.x, bsf = pp0.y;
+        const float hcv[4] = {pp0.z, pp0.w, pp1.x, pp1.y};
+        const float4 r0 = *reinterpret_cast<const float4*>(&W.jb[qp][dr][0]);
+        const float4 r1 = *reinterpret_cast<const float4*>(&W.jb[qp][dr][4]);
+        const float4 c0 = *reinterpret_cast<const float4*>(&W.jb[qp][dc][0]);
+        const float4 c1 = *reinterpret_cast<const float4*>(&W.jb[qp][dc][4]);
+        const float j1[7] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z};
+        const float j2[7] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z};
+#pragma unroll
+        for (int o1 = 0; o1 < 7; o1++) {
+          const float wl = hdf * j1[o1];
+#pragma unroll
+          for (int o2 = o1; o2 < 7; o2++) D[o1 * 7 - (o1 * (o1 - 1)) / 2 + (o2 - o1)] += wl * j2[o2];
+        }
+        if (es != h && ((mq >> es) & 1u)) {
+          const float jv = W.jb[qp][ek][eo];
+          const float wl = hdf * jv;
+#pragma unroll
+          for (int c = 0; c < 4; c++) E[c] += wl * hcv[c];
+          E[4] += (hdf * bsf) * jv;
+        }
+        C += lane < 16 ? (hdf * hcv[cr]) * hcv[ccol] : (bsf * hdf) * hcv[ccol];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // the scratch is rewritten by the next group
+  }
+  if (a.trace && tid == 0) a.trace[(size_t)b * 16 + 1] = wall_clock64();
+  if (!a.accumulate) return;
+
+  // ---- epilogue: T summed over the wave's 8 point lanes of each slot (fixed tree: ^8, ^16, ^32), then the block
+  //      partial in hs_k_lin's production layout, waves in order
+#pragma unroll
+  for (int i = 0; i < NTOP; i++) {
+    float v = T[i];
+    v = v + dpp_ror8(v);
+    v = v + __shfl_xor(v, 16);
+    v = v + __shfl_xor(v, 32);
+    T[i] = v;
+  }
+  // the energies of the wave (lanes t == 0 of the 8 point slots, in point-slot order)
+  double eW = 0.0, sW = 0.0, nW = 0.0;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    eW += __shfl(eA, j * 8);
+    sW += __shfl(sidA, j * 8);
+    nW += __shfl(npA, j * 8);
+  }
+  __syncthreads();  // every wave is done with its scratch (the partials area aliases it)
+  L8Part& P = U.part;
+  if (pl == 0) {
+#pragma unroll
+    for (int i = 0; i < NTOP; i++) P.T[wv][t][i] = T[i];
+  }
+#pragma unroll
+  for (int i = 0; i < HS_ND_PROD; i++) P.DEC[wv][i][lane] = D[i];
+#pragma unroll
+  for (int i = 0; i < 5; i++) P.DEC[wv][HS_ND_PROD + i][lane] = E[i];
+  P.DEC[wv][HS_ND_PROD + 5][lane] = C;
+  __shared__ double se[L8_NW][3];
+  if (lane == 0) {
+    se[wv][0] = eW;
+    se[wv][1] = sW;
+    se[wv][2] = nW;
+  }
+  __syncthreads();
+  constexpr int NE = hs_ne(false);
+  static_assert(NE == HS_E_TOP + HS_ND_PROD + 6, "production partial layout");
+  float* out = a.part + (size_t)b * NE * 64;
+  for (int i = tid; i < NE * 64; i += HS_LIN8_NT) {
+    const int e = i >> 6, l = i & 63;
+    float s = 0.f;
+    if (e < HS_E_TOP) {
+      const int tt = l >> 3, kk = l & 7;
+      const int m = owner_map(e, kk);
+      if (m >= 0) {
+        s = P.T[0][tt][m];
+#pragma unroll
+        for (int w = 1; w < L8_NW; w++) s += P.T[w][tt][m];
+      }
+    } else {
+      const int d = e - HS_E_TOP;
+      s = P.DEC[0][d][l];
+#pragma unroll
+      for (int w = 1; w < L8_NW; w++) s += P.DEC[w][d][l];
+    }
+    out[i] = s;
+  }
+  if (tid < 3) {
+    double s = se[0][tid];
+#pragma unroll
+    for (int w = 1; w < L8_NW; w++) s += se[w][tid];
+    a.part_e[(size_t)b * 4 + tid] = s;
+  }
+  if (a.trace && tid == 0) a.trace[(size_t)b * 16 + 2] = wall_clock64();
+}

@@ -1,0 +1,117 @@
+"""GPU parity of hs_k_lin8, the production linearize + accumulate kernel with lane = (point, target slot)
+(h-slam_amd/csrc/hs_lin8_kernels.hip), forced on with HS_LIN8=1 at every window size.
+
+Bars:
+* per-residual outputs (state, active, energy, energy-with-outlier, JpJdF, centre projection) and the per-point
+  Schur prelude (HdiF, bdSumF, the fused point step, idepth): bit-exact against the oracle and against hs_k_lin
+  (HS_LIN8=0) -- the per-residual arithmetic is the reference's, in its order;
+* stitched H / b: the production bar of tests/test_gpu_ba.py (H_TOL, the fp32 accumulation order differs);
+* the GN trajectory: as close to the single-thread oracle as the oracle's own 8-thread pool (x 10), like
+  test_split_accumulation_matches_threaded_reference;
+* two runs: bit-identical (fixed-order block partials, no order-dependent atomics).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from test_gpu_ba import _close_b, _close_H
+
+pytestmark = pytest.mark.gpu
+
+
+def _window(scene, lin8):
+    from hslam_amd.ba import BAWindow
+    os.environ["HS_LIN8"] = "1" if lin8 else "0"
+    try:
+        return BAWindow(scene)
+    finally:
+        os.environ.pop("HS_LIN8", None)
+
+
+@pytest.mark.parametrize("scene_name", ["scene_small", "scene2k", "scene_kitti2k", "scene_kitti20k"])
+def test_lin8_linearize_bit_exact(scene_name, request):
+    from oracle_ffi import OracleBA
+    scene = request.getfixturevalue(scene_name)
+    g = _window(scene, True)
+    o = OracleBA(scene)
+    eg = g.linearizeAll(reset=True)
+    eo = o.linearize_all(reset=True)
+    o.apply_res()
+    rg, ro = g.residuals(), o.residuals()
+    assert np.array_equal(rg["state"], ro["state"])
+    active_o = ro["state"] == 0
+    assert np.array_equal(rg["active"].astype(bool), active_o)
+    assert np.array_equal(rg["energy"], ro["energy"].astype(np.float32))
+    assert np.array_equal(rg["energy_wo"], ro["energy_wo"].astype(np.float32))
+    assert np.array_equal(rg["JpJdF"][active_o], ro["JpJdF"][active_o])
+    assert np.array_equal(rg["center"][active_o], ro["center"][active_o])
+    assert abs(eg - eo) <= 1e-9 * abs(eo)
+    assert np.array_equal(g.frames()["energyTH"], o.frames()["energyTH"])
+    for which in (0, 1, 2):
+        Ho, bo = o.accumulate(which)
+        Hg, bg = g.system(which)
+        okH, rH = _close_H(Hg, Ho)
+        okb, rb = _close_b(bg, bo, Ho)
+        assert okH, f"which={which} H worst ratio {rH}"
+        assert okb, f"which={which} b worst ratio {rb}"
+    g.close()
+
+
+@pytest.mark.parametrize("scene_name", ["scene2k", "scene_kitti20k"])
+def test_lin8_matches_lin(scene_name, request):
+    """hs_k_lin8 against hs_k_lin on the same window through two fused GN iterations: the per-residual and
+    per-point outputs bit-identical after the first linearization (same inputs), the systems at the H bar."""
+    scene = request.getfixturevalue(scene_name)
+    g8, g1 = _window(scene, True), _window(scene, False)
+    for g in (g8, g1):
+        g.linearizeAll(reset=True)
+    r8, r1 = g8.residuals(), g1.residuals()
+    for k in r8:
+        assert np.array_equal(r8[k], r1[k]), k
+    p8, p1 = g8.points(), g1.points()
+    for k in ("HdiF", "bdSumF", "idepth"):
+        assert np.array_equal(p8[k], p1[k]), k
+    for which in (0, 1, 2):
+        H8, b8 = g8.system(which)
+        H1, b1 = g1.system(which)
+        assert _close_H(H8, H1)[0] and _close_b(b8, b1, H1)[0], which
+    # fused GN iterations (hs_k_lin8's in-kernel resubstitution + point step): the two kernels' systems differ in
+    # fp32 accumulation order only, so the energies stay together at the GN-step level
+    e8 = g8.iterate(0, 3)
+    e1 = g1.iterate(0, 3)
+    assert np.all(np.abs(e8 - e1) <= 1e-3 * np.abs(e1)), (e8, e1)
+    g8.close()
+    g1.close()
+
+
+@pytest.mark.parametrize("scene_name", ["scene2k", "scene_kitti2k"])
+def test_lin8_trajectory(scene_name, request):
+    from oracle_ffi import OracleBA
+    scene = request.getfixturevalue(scene_name)
+    g = _window(scene, True)
+    o1 = OracleBA(scene)
+    o8 = OracleBA(scene, nthreads=8)
+    _, eg = g.optimize(6)
+    _, e1 = o1.optimize(6)
+    _, e8 = o8.optimize(6)
+    dev_pool = np.abs(e8 - e1) / np.abs(e1)
+    dev_gpu = np.abs(eg - e1) / np.abs(e1)
+    assert dev_gpu[0] <= 1e-9
+    assert np.all(dev_gpu <= np.maximum(10 * dev_pool, 1e-3))
+    assert eg[-1] < 0.5 * eg[0]
+    g.close()
+
+
+def test_lin8_runs_are_bit_reproducible(scene_kitti20k):
+    outs = []
+    for _ in range(2):
+        g = _window(scene_kitti20k, True)
+        g.linearizeAll(reset=True)
+        H0, b0 = g.system(0)
+        H2, b2 = g.system(2)
+        e = g.iterate(0, 3)
+        outs.append((H0, b0, H2, b2, e, g.frames()["state"], g.points()["idepth"]))
+        g.close()
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b)
