@@ -49,24 +49,24 @@ __device__ __forceinline__ float3 interp33_8(const float4* __restrict__ img, flo
 }
 
 // the block's constants (host h's precalc by target slot, thresholds, xAd[h][t][.], calib step)
-struct L8Const {
+struct __align__(16) L8Const {
   HsPrecalc pre[HS_MAXF];
   float th[HS_MAXF];
   float xad[HS_MAXF * 8];
   float cs[4];
 };
 // per-wave LDS scratch of a point group
-struct L8Scratch {
+struct __align__(16) L8Scratch {
   float ps[8][8][8];  // [point][slot][tbd, tHdd, tc0..3, econ, -]: the residuals' terms of the per-point sums
   float jb[8][8][8];  // [point][pattern row i][non-host slot o]: JpJdF (0 unless active), accD / accE operand
   float pp[8][8];     // [point][HdiF, bdSumF, Hcd0..3, -, -]
 };
 // the epilogue's per-wave partials: T (natural layout, summed over the wave's point lanes) and the D / E / C lanes
-struct L8Part {
+struct __align__(16) L8Part {
   float T[L8_NW][8][NTOP + 1];
   float DEC[L8_NW][HS_ND_PROD + 6][64];
 };
-union L8Lds {
+union __align__(16) L8Lds {
   L8Scratch s[L8_NW];
   L8Part part;
 };
@@ -510,7 +510,8 @@ __global__ __launch_bounds__(HS_LIN8_NT) void hs_k_lin8(HsLinArgs a) {
           for (int c = 0; c < 4; c++) E[c] += wl * hcv[c];
           E[4] += (hdf * bsf) * jv;
         }
-        C += lane < 16 ? (hdf * hcv[cr]) * hcv[ccol] : (bsf * hdf) * hcv[ccol];
+        const float hr = W.pp[qp][2 + cr], hc = W.pp[qp][2 + ccol];  // per-lane LDS addresses, no select chains
+        C += lane < 16 ? (hdf * hr) * hc : (bsf * hdf) * hc;
       }
     }
     __builtin_amdgcn_wave_barrier();  // the scratch is rewritten by the next group

@@ -139,6 +139,25 @@ struct TrkShared {
   long long prof[6];  // HS_KTRACE: thread-0 cycles: point loop, reductions, LM step, passes, wave reduce, barrier
 };
 
+// The wave sum of the xor butterfly (v += shfl_xor(v, o), o = 32 .. 1) as lane 0 holds it, bit for bit, with one
+// cross-lane LDS op instead of six: at step o the lanes i < o that lane 0's result depends on add lane i + o =
+// lane i ^ o, in the same operand order, so the halves are a permlane32 swap, the ^16 step a bpermute and the
+// ^8 .. ^1 steps DPP row shifts (row_shl:o).  Only lane 0's result is meaningful.
+template <int CTRL>
+__device__ __forceinline__ float dpp_row_shl(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float xor_tree_lane0(float v) {
+  const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);  // lanes i < 32: v_i + v_(i + 32)
+  v = v + __shfl_xor(v, 16);
+  v = v + dpp_row_shl<0x108>(v);  // row_shl:8
+  v = v + dpp_row_shl<0x104>(v);
+  v = v + dpp_row_shl<0x102>(v);
+  v = v + dpp_row_shl<0x101>(v);
+  return v;
+}
+
 // calcRes + calcGSSSE at S.RKi / S.t / S.affLL for level S.lvl; results in S.res / S.H / S.b / S.nWarped
 __device__ void trk_pass(const HsTrackArgs& a, TrkShared& S) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -283,9 +302,7 @@ __device__ void trk_pass(const HsTrackArgs& a, TrkShared& S) {
 #pragma unroll
   for (int q = 0; q < TRK_NRED; q++) {
     if (q < TRK_NACC + 4) {
-      float v = vals[q];
-      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-      vals[q] = v;
+      vals[q] = xor_tree_lane0(vals[q]);
     } else {
       int v = __float_as_int(vals[q]);
       for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
