@@ -1768,6 +1768,15 @@ __device__ __forceinline__ void scale_state(const double s[10], double o[10]) {
   o[9] = hs::SCALE_B * s[9];
 }
 
+// 1 / sqrt(x) for a quaternion norm near 1: v_rsq_f64 refined by two Newton steps (no IEEE square root and division
+// on the doStep chain); differs from 1.0 / sqrt(x) by rounding only
+__device__ __forceinline__ double rsqrt_step(double x) {
+  double r = __builtin_amdgcn_rsq(x);
+  r = r * __builtin_fma(-0.5 * x, r * r, 1.5);
+  r = r * __builtin_fma(-0.5 * x, r * r, 1.5);
+  return r;
+}
+
 // Sophus SE3::exp (hs_se3.h) for a GN step: for theta^2 < 1e-2 the so3 / V coefficients sin(x/2)/x, cos(x/2),
 // (1 - cos x)/x^2 and (x - sin x)/x^3 come from their Taylor series in u = x^2 (6 terms: truncation < 1e-20
 // relative; no sqrt, trig or division on the chain); the quaternion is normalized with one reciprocal square
@@ -1786,7 +1795,7 @@ __device__ __forceinline__ hs::SE3 se3_exp_step(const double a[6]) {
   const double c2 = poly(1.0 / 6, -1.0 / 120, 1.0 / 5040, -1.0 / 362880, 1.0 / 39916800, -1.0 / 6227020800.0);
   hs::SE3 r;
   const double qx = imag * w0, qy = imag * w1, qz = imag * w2;
-  const double inv = 1.0 / sqrt(qx * qx + qy * qy + qz * qz + real * real);
+  const double inv = rsqrt_step(qx * qx + qy * qy + qz * qz + real * real);
   r.q = hs::Quat{qx * inv, qy * inv, qz * inv, real * inv};
   double O[9], O2[9], V[9];
   hs::SE3::hat3(a + 3, O);
@@ -1807,7 +1816,7 @@ __device__ __forceinline__ hs::SE3 se3_mul_step(const hs::SE3& A, const hs::SE3&
   r.t[1] = A.t[1] + rt[1];
   r.t[2] = A.t[2] + rt[2];
   const hs::Quat q = hs::qmul(A.q, B.q);
-  const double inv = 1.0 / sqrt(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+  const double inv = rsqrt_step(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
   r.q = hs::Quat{q.x * inv, q.y * inv, q.z * inv, q.w * inv};
   return r;
 }
@@ -1978,16 +1987,18 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     // are requested here so their latency overlaps orthogonalize.
     const bool wxad = !(a.flags & HS_APPLY);
     float adh[2][8], adt[2][8];
+    if (wxad) {  // a uniform branch: the fused path issues none of these loads (a barrier would wait for them)
 #pragma unroll
-    for (int k = 0; k < 2; k++) {
-      const int o = min(tid + k * nt, nF * nF * 8 - 1);
-      const int pair = o >> 3, c = o & 7, hh = pair / nF, tt = pair - hh * nF;
-      const float* aHf = a.adHostF + (wxad ? (hh + nF * tt) * 64 : 0);
-      const float* aTf = a.adTargetF + (wxad ? (hh + nF * tt) * 64 : 0);
+      for (int k = 0; k < 2; k++) {
+        const int o = min(tid + k * nt, nF * nF * 8 - 1);
+        const int pair = o >> 3, c = o & 7, hh = pair / nF, tt = pair - hh * nF;
+        const float* aHf = a.adHostF + (hh + nF * tt) * 64;
+        const float* aTf = a.adTargetF + (hh + nF * tt) * 64;
 #pragma unroll
-      for (int rr = 0; rr < 8; rr++) {  // not issued in the fused path (a barrier would wait for them)
-        adh[k][rr] = wxad ? aHf[rr * 8 + c] : 0.f;
-        adt[k][rr] = wxad ? aTf[rr * 8 + c] : 0.f;
+        for (int rr = 0; rr < 8; rr++) {
+          adh[k][rr] = aHf[rr * 8 + c];
+          adt[k][rr] = aTf[rr * 8 + c];
+        }
       }
     }
     if (s_it >= 2) {  // SOLVER_ORTHOGONALIZE_X_LATER: x -= P x, P = (N Npi^T + Npi N^T) / 2 (orthogonalize)
