@@ -493,7 +493,8 @@ def main():
     # rocprofv3 reports (the in-loop pairs add the event-record overhead to a ~9 us kernel)
     lin_ms = ba.time_linearize(max(64, args.steps))
     achieved = BYTES_PER_PRES * shard.n_res / (lin_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(args.points) if world == 1 and not kitti else (None, None)
+    lin_kernel = ba.partition()["kernel"]  # hs_k_lin (one point per wave) or hs_k_lin8 (8 points per wave)
+    traffic, traffic_src = pmc_traffic(args.points, lin_kernel) if world == 1 and not kitti else (None, None)
     if kitti:
         wl = ("C5 BA half (BASELINE.json configs[4]): full windowed photometric BA incl. Schur complement, 8 KF x "
               f"{n_window} pts, KITTI 1232x368, 5 pyramid levels")
@@ -525,7 +526,7 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "hs_k_lin",
+            "kernel": lin_kernel,
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -536,8 +537,8 @@ def main():
             "units_per_launch": shard.n_res,
             "avg_launch_ms": lin_ms,
             "avg_launch_ms_in_loop_events": lin_loop_ms,
-            "timing": "HIP events on the context stream around back-to-back hs_k_lin launches (fused linearize + "
-                      "applyRes + top / Schur accumulation into block partials)",
+            "timing": f"HIP events on the context stream around back-to-back {lin_kernel} launches (fused "
+                      "linearize + applyRes + top / Schur accumulation into block partials)",
         },
         "phase_ms_per_step": {  # per-phase split: --phase-events 2 (1 times the linearize kernel only)
             "solve_step_kernel": tim["solve_ms"] / nt if args.phase_events >= 2 else None,

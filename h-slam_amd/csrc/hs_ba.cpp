@@ -1375,6 +1375,15 @@ int hs_ba_get_timings(hs_ctx* c, double* out6) {
   return HS_OK;
 }
 
+int hs_ba_get_partition(hs_ctx* c, int* out4) {
+  if (!c || !out4) return fail(HS_ERR_INVALID, "null");
+  out4[0] = c->lin8 ? 1 : 0;
+  out4[1] = c->nblk;
+  out4[2] = c->W;
+  out4[3] = c->exact ? 1 : 0;
+  return HS_OK;
+}
+
 int hs_ba_time_linearize(hs_ctx* c, int reps, double* avg_ms) {
   if (!c || !avg_ms || reps < 1) return fail(HS_ERR_INVALID, "bad args");
   if (c->nF == 0) return fail(HS_ERR_STATE, "no window");

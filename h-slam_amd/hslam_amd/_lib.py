@@ -77,6 +77,7 @@ SIGNATURES = {
     "hs_ba_marginalize_frame": ([VP, I, VP, VP], I),
     "hs_ba_get_timings": ([VP, VP], I),
     "hs_ba_time_linearize": ([VP, I, VP], I),
+    "hs_ba_get_partition": ([VP, VP], I),
     "hs_comm_get_unique_id": ([VP], I),
     "hs_comm_init": ([VP, VP, I, I], I),
     # include/hs_track.h

@@ -189,6 +189,12 @@ class BAWindow:
         return dict(linearize_ms=t[0], acc_stitch_ms=t[1], solve_ms=t[2], timed_iters=int(t[3]), wall_ms=t[4],
                     iters=int(t[5]))
 
+    def partition(self):
+        """The linearize partitioning: dict(kernel='hs_k_lin' | 'hs_k_lin8', blocks, waves, exact)."""
+        o = np.zeros(4, np.int32)
+        check(self.lib.hs_ba_get_partition(self.h, ptr(o)))
+        return dict(kernel="hs_k_lin8" if o[0] else "hs_k_lin", blocks=int(o[1]), waves=int(o[2]), exact=bool(o[3]))
+
     def time_linearize(self, reps: int) -> float:
         """Average ms of `reps` back-to-back linearize launches (one HIP event pair)."""
         t = np.zeros(1)

@@ -145,6 +145,11 @@ int hs_ba_get_timings(hs_ctx* ctx, double* out6);
    re-linearization at the current point depths.  Measurement only (no reference counterpart). */
 int hs_ba_time_linearize(hs_ctx* ctx, int reps, double* avg_ms);
 
+/* The linearize partitioning of the current window: out4 = [kernel (0 hs_k_lin: one point per wave, 1 hs_k_lin8:
+   8 points per wave, the production choice from 60k points; env HS_LIN8 forces it), blocks, waves per block that
+   take points, HS_ACC_EXACT].  Introspection only (no reference counterpart). */
+int hs_ba_get_partition(hs_ctx* ctx, int* out4);
+
 /* multi-GPU (point sharding): 128-byte RCCL unique id from rank 0, broadcast by the caller.
    hs_comm_init must be called before hs_ba_set_window.  Each rank loads its own point shard (same frames);
    per GN iteration the stitched H/b/energy are all-reduced and the newest-frame energies all-gathered. */
