@@ -86,6 +86,13 @@ struct hs_ctx {
   int nblk = 0, W = 4, ne = 0, Q = 0;
   bool exact = false;
   bool lin8 = false;              // production linearizations run hs_k_lin8 (4-wave blocks, W = 4)
+  // setNewFrameEnergyTH's select on a side stream in the fused GN loop (large windows): it depends on the host sums'
+  // pass-1 histogram only, and only the next linearization reads its threshold, so it runs beside the stitch and the
+  // solve instead of in the stitch's last block (env HS_SIDE_TH=0 / 1 forces it off / on)
+  bool side_th = false;
+  bool th_pending = false;        // a side-stream select the main stream has not joined yet
+  hipStream_t side = nullptr;
+  hipEvent_t ev_red = nullptr, ev_th = nullptr;
   bool sepValid = false;          // d_sep holds the separate HA / HSC of the last linearization
   std::vector<int> pt_host, res_point, res_target, host_pt_begin;
   std::vector<int> res_of_slot;   // [nP*8]
@@ -307,7 +314,8 @@ static int launch_linearize(hs_ctx* c, int fuse, bool marg = false, bool accumul
 // all-gather of newest-frame candidates, per-host sums (+ energy, threshold), stitch, all-reduce of the system
 // readback = true: only the separate HA / HSC of the last linearization (d_sep) are re-formed from its host sums;
 // no collective, the system vector and the energies are left as they are
-static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = false, bool readback = false) {
+static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = false, bool readback = false,
+                         bool side_select = false) {
   if (c->comm && !readback)
     HS_NCCL(ncclAllGather(c->d_cand + (size_t)c->rank * c->cand_stride, c->d_cand, c->cand_stride, ncclFloat,
                           c->comm, c->stream));
@@ -330,6 +338,15 @@ static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = fals
     hipLaunchKernelGGL(hs_k_reduce, dim3(c->nF * c->Q + 1 + a.nhist), dim3(256), 0, c->stream, a);
     HS_HIP(hipGetLastError());
   }
+  const bool side = side_select && c->side_th && !skip_threshold && !readback;
+  if (side) {  // the select block alone, on the side stream after the reduce; joined by the next solve
+    HS_HIP(hipEventRecord(c->ev_red, c->stream));
+    HS_HIP(hipStreamWaitEvent(c->side, c->ev_red, 0));
+    hipLaunchKernelGGL(hs_k_debug_th, dim3(1), dim3(HS_STITCH_NT), 0, c->side, a);
+    HS_HIP(hipGetLastError());
+    HS_HIP(hipEventRecord(c->ev_th, c->side));
+    c->th_pending = true;
+  }
   HsStitchArgs st;
   std::memset(&st, 0, sizeof(st));
   st.nF = c->nF; st.exact = c->exact ? 1 : 0; st.ne = c->ne;
@@ -340,7 +357,7 @@ static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = fals
   st.sc = 1.0f / (1 + 1e-5);   // H -= H_sc * (1.0f / (1 + lambda)) (:763)
   st.trace = c->d_tr_st;
   st.red = a;
-  st.red.skip_threshold = (skip_threshold || readback) ? 1 : 0;
+  st.red.skip_threshold = (skip_threshold || readback || side) ? 1 : 0;
   hipLaunchKernelGGL(hs_k_stitch, dim3(c->nF * (c->nF + 1) / 2 + c->nF + 2), dim3(HS_STITCH_NT), 0, c->stream, st);
   HS_HIP(hipGetLastError());
   if (sep) c->sepValid = true;
@@ -369,6 +386,10 @@ static int launch_solve(hs_ctx* c, int flags, int iteration, bool log) {
   if (const char* e = std::getenv("HS_SOLVE_DBG")) a.dbg = std::atoi(e);
   hipLaunchKernelGGL(hs_k_solve, dim3(1), dim3(HS_SOLVE_NT), 0, c->stream, a);
   HS_HIP(hipGetLastError());
+  if (c->th_pending) {  // the solve runs beside the side-stream select; whatever follows it waits for the threshold
+    HS_HIP(hipStreamWaitEvent(c->stream, c->ev_th, 0));
+    c->th_pending = false;
+  }
   return HS_OK;
 }
 
@@ -497,7 +518,7 @@ static int gn_iterations(hs_ctx* c, int it0, int K, bool allow_break, double* en
     if (timed) HS_HIP(hipEventRecord(c->ev[4 * k + 1], c->stream));
     HS_TRY(launch_linearize(c, 1));
     if (timed) HS_HIP(hipEventRecord(c->ev[4 * k + 2], c->stream));
-    HS_TRY(launch_reduce(c));
+    HS_TRY(launch_reduce(c, false, false, false, true));
     if (timed && all) HS_HIP(hipEventRecord(c->ev[4 * k + 3], c->stream));
     if (allow_break) {
       int cb = 0;
@@ -510,6 +531,10 @@ static int gn_iterations(hs_ctx* c, int it0, int K, bool allow_break, double* en
         break;
       }
     }
+  }
+  if (c->th_pending) {  // the last iteration's select
+    HS_HIP(hipStreamWaitEvent(c->stream, c->ev_th, 0));
+    c->th_pending = false;
   }
   c->haveSystem = true;
   // read back: energy log (E of the linearizations consumed by each solve) + the last energy + status
@@ -610,6 +635,9 @@ int hs_create(hs_ctx** out, const hs_params* params, int device_id) {
   }
   c->ev.assign(4 * kEventIters, nullptr);
   for (auto& e : c->ev) HS_HIP(hipEventCreate(&e));
+  HS_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+  HS_HIP(hipEventCreateWithFlags(&c->ev_red, hipEventDisableTiming));
+  HS_HIP(hipEventCreateWithFlags(&c->ev_th, hipEventDisableTiming));
   *out = c;
   return HS_OK;
 }
@@ -618,10 +646,14 @@ void hs_destroy(hs_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->side) (void)hipStreamSynchronize(c->side);
   free_window(c);
   if (c->comm) ncclCommDestroy(c->comm);
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
+  if (c->ev_red) (void)hipEventDestroy(c->ev_red);
+  if (c->ev_th) (void)hipEventDestroy(c->ev_th);
+  if (c->side) (void)hipStreamDestroy(c->side);
   if (c->h_state) (void)hipHostFree(c->h_state);
   if (c->h_ctl) (void)hipHostFree(c->h_ctl);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -689,6 +721,9 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
   c->blk_begin.assign(nF + 1, 0);
   c->lin8 = !c->exact && nP >= kLin8MinPoints;
   if (const char* e = std::getenv("HS_LIN8")) c->lin8 = !c->exact && e[0] == '1';
+  // the side-stream select pays an event hand-off (~1.4 us per step measured at 2k): only where the select is long
+  c->side_th = nP >= kLin8MinPoints;
+  if (const char* e = std::getenv("HS_SIDE_TH")) c->side_th = e[0] == '1';
   // points per block: hs_k_lin HS_LIN_NW waves x ppw points; hs_k_lin8 4 waves x ppw groups of 8 points (its
   // partition also serves hs_k_lin's marginalization / linearizeAll(true) passes, with W = 4 of its waves)
   const int bw = c->lin8 ? (HS_LIN8_NT / 64) * 8 : HS_LIN_NW;
