@@ -86,13 +86,10 @@ struct hs_ctx {
   int nblk = 0, W = 4, ne = 0, Q = 0;
   bool exact = false;
   bool lin8 = false;              // production linearizations run hs_k_lin8 (4-wave blocks, W = 4)
-  // setNewFrameEnergyTH's select on a side stream in the fused GN loop (large windows): it depends on the host sums'
-  // pass-1 histogram only, and only the next linearization reads its threshold, so it runs beside the stitch and the
-  // solve instead of in the stitch's last block (env HS_SIDE_TH=0 / 1 forces it off / on)
-  bool side_th = false;
-  bool th_pending = false;        // a side-stream select the main stream has not joined yet
-  hipStream_t side = nullptr;
-  hipEvent_t ev_red = nullptr, ev_th = nullptr;
+  // large windows: setNewFrameEnergyTH's select as a multi-block pass 2 (np2 extra blocks of the stitch launch) and a
+  // one-block pass 3 over pass 2's survivors, instead of the stitch's single select block scanning every candidate
+  // twice (env HS_TH_MULTI=0 / 1 forces it off / on)
+  bool th_multi = false;
   bool sepValid = false;          // d_sep holds the separate HA / HSC of the last linearization
   std::vector<int> pt_host, res_point, res_target, host_pt_begin;
   std::vector<int> res_of_slot;   // [nP*8]
@@ -139,6 +136,7 @@ struct hs_ctx {
   double* d_x = nullptr;
   double* d_elog = nullptr;
   unsigned int* d_th_hist = nullptr;  // [HS_TH_BINS] threshold select pass-1 histogram (zero between launches)
+  unsigned int *d_th_hist2 = nullptr, *d_th_surv = nullptr, *d_th_nsurv = nullptr;  // multi-block pass 2
   float* d_cand = nullptr;  // [nranks][cand_stride] newest-frame energy per point (-1 / NaN = none)
   int cand_stride = 0;
   bool hm_zero = true;      // marginalization prior not set: the solve skips HM
@@ -186,7 +184,8 @@ static void free_window(hs_ctx* c) {
                   c->d_p_step, c->d_part, c->d_part_e, c->d_hostsum, c->d_sys, c->d_sep,
                   c->d_adHost, c->d_adTarget, c->d_adHostF, c->d_adTargetF, c->d_HM, c->d_bM, c->d_Nproj, c->d_xAd,
                   c->d_x, c->d_elog, c->d_cand, c->d_tr_lin, c->d_tr_acc, c->d_tr_solve, c->d_tr_st,
-                  c->d_marg, c->d_adHTdelta, c->d_p_HdiF_alt, c->d_fix_relBL, c->d_fix_nGood, c->d_th_hist};
+                  c->d_marg, c->d_adHTdelta, c->d_p_HdiF_alt, c->d_fix_relBL, c->d_fix_nGood, c->d_th_hist,
+                  c->d_th_hist2, c->d_th_surv, c->d_th_nsurv};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   c->d_state = nullptr; c->d_pre = nullptr; c->d_frameTH = nullptr;
@@ -209,6 +208,7 @@ static void free_window(hs_ctx* c) {
   c->d_p_HdiF_alt = c->d_fix_relBL = nullptr;
   c->hdif_solved = nullptr;
   c->d_th_hist = nullptr;
+  c->d_th_hist2 = c->d_th_surv = c->d_th_nsurv = nullptr;
   c->d_fix_nGood = nullptr;
   c->nF = c->nP = c->nR = 0;
   c->haveSystem = false;
@@ -314,8 +314,7 @@ static int launch_linearize(hs_ctx* c, int fuse, bool marg = false, bool accumul
 // all-gather of newest-frame candidates, per-host sums (+ energy, threshold), stitch, all-reduce of the system
 // readback = true: only the separate HA / HSC of the last linearization (d_sep) are re-formed from its host sums;
 // no collective, the system vector and the energies are left as they are
-static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = false, bool readback = false,
-                         bool side_select = false) {
+static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = false, bool readback = false) {
   if (c->comm && !readback)
     HS_NCCL(ncclAllGather(c->d_cand + (size_t)c->rank * c->cand_stride, c->d_cand, c->cand_stride, ncclFloat,
                           c->comm, c->stream));
@@ -338,14 +337,12 @@ static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = fals
     hipLaunchKernelGGL(hs_k_reduce, dim3(c->nF * c->Q + 1 + a.nhist), dim3(256), 0, c->stream, a);
     HS_HIP(hipGetLastError());
   }
-  const bool side = side_select && c->side_th && !skip_threshold && !readback;
-  if (side) {  // the select block alone, on the side stream after the reduce; joined by the next solve
-    HS_HIP(hipEventRecord(c->ev_red, c->stream));
-    HS_HIP(hipStreamWaitEvent(c->side, c->ev_red, 0));
-    hipLaunchKernelGGL(hs_k_debug_th, dim3(1), dim3(HS_STITCH_NT), 0, c->side, a);
-    HS_HIP(hipGetLastError());
-    HS_HIP(hipEventRecord(c->ev_th, c->side));
-    c->th_pending = true;
+  const bool multi = c->th_multi && !skip_threshold && !readback;
+  if (multi) {  // pass 2 by np2 extra blocks of the stitch launch, pass 3 by one block after it
+    a.th_hist2 = c->d_th_hist2;
+    a.th_surv = c->d_th_surv;
+    a.th_nsurv = c->d_th_nsurv;
+    a.np2 = std::min(64, std::max(1, (c->nranks * c->cand_stride + 4095) / 4096));
   }
   HsStitchArgs st;
   std::memset(&st, 0, sizeof(st));
@@ -357,9 +354,15 @@ static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = fals
   st.sc = 1.0f / (1 + 1e-5);   // H -= H_sc * (1.0f / (1 + lambda)) (:763)
   st.trace = c->d_tr_st;
   st.red = a;
-  st.red.skip_threshold = (skip_threshold || readback || side) ? 1 : 0;
-  hipLaunchKernelGGL(hs_k_stitch, dim3(c->nF * (c->nF + 1) / 2 + c->nF + 2), dim3(HS_STITCH_NT), 0, c->stream, st);
+  st.red.skip_threshold = (skip_threshold || readback || multi) ? 1 : 0;
+  hipLaunchKernelGGL(hs_k_stitch, dim3(c->nF * (c->nF + 1) / 2 + c->nF + 2 + (multi ? a.np2 : 0)), dim3(HS_STITCH_NT),
+                     0, c->stream, st);
   HS_HIP(hipGetLastError());
+  if (multi) {  // pass 3: the select block over pass 2's histogram and survivors (a side stream measured no faster:
+                // its cross-queue event hand-offs cost what the overlap with the solve saves)
+    hipLaunchKernelGGL(hs_k_th_select, dim3(1), dim3(HS_STITCH_NT), 0, c->stream, a);
+    HS_HIP(hipGetLastError());
+  }
   if (sep) c->sepValid = true;
   if (c->comm && !readback)
     HS_NCCL(ncclAllReduce(c->d_sys, c->d_sys, c->SL() + 3, ncclDouble, ncclSum, c->comm, c->stream));
@@ -386,10 +389,6 @@ static int launch_solve(hs_ctx* c, int flags, int iteration, bool log) {
   if (const char* e = std::getenv("HS_SOLVE_DBG")) a.dbg = std::atoi(e);
   hipLaunchKernelGGL(hs_k_solve, dim3(1), dim3(HS_SOLVE_NT), 0, c->stream, a);
   HS_HIP(hipGetLastError());
-  if (c->th_pending) {  // the solve runs beside the side-stream select; whatever follows it waits for the threshold
-    HS_HIP(hipStreamWaitEvent(c->stream, c->ev_th, 0));
-    c->th_pending = false;
-  }
   return HS_OK;
 }
 
@@ -518,7 +517,7 @@ static int gn_iterations(hs_ctx* c, int it0, int K, bool allow_break, double* en
     if (timed) HS_HIP(hipEventRecord(c->ev[4 * k + 1], c->stream));
     HS_TRY(launch_linearize(c, 1));
     if (timed) HS_HIP(hipEventRecord(c->ev[4 * k + 2], c->stream));
-    HS_TRY(launch_reduce(c, false, false, false, true));
+    HS_TRY(launch_reduce(c));
     if (timed && all) HS_HIP(hipEventRecord(c->ev[4 * k + 3], c->stream));
     if (allow_break) {
       int cb = 0;
@@ -531,10 +530,6 @@ static int gn_iterations(hs_ctx* c, int it0, int K, bool allow_break, double* en
         break;
       }
     }
-  }
-  if (c->th_pending) {  // the last iteration's select
-    HS_HIP(hipStreamWaitEvent(c->stream, c->ev_th, 0));
-    c->th_pending = false;
   }
   c->haveSystem = true;
   // read back: energy log (E of the linearizations consumed by each solve) + the last energy + status
@@ -635,9 +630,6 @@ int hs_create(hs_ctx** out, const hs_params* params, int device_id) {
   }
   c->ev.assign(4 * kEventIters, nullptr);
   for (auto& e : c->ev) HS_HIP(hipEventCreate(&e));
-  HS_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
-  HS_HIP(hipEventCreateWithFlags(&c->ev_red, hipEventDisableTiming));
-  HS_HIP(hipEventCreateWithFlags(&c->ev_th, hipEventDisableTiming));
   *out = c;
   return HS_OK;
 }
@@ -646,14 +638,10 @@ void hs_destroy(hs_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  if (c->side) (void)hipStreamSynchronize(c->side);
   free_window(c);
   if (c->comm) ncclCommDestroy(c->comm);
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
-  if (c->ev_red) (void)hipEventDestroy(c->ev_red);
-  if (c->ev_th) (void)hipEventDestroy(c->ev_th);
-  if (c->side) (void)hipStreamDestroy(c->side);
   if (c->h_state) (void)hipHostFree(c->h_state);
   if (c->h_ctl) (void)hipHostFree(c->h_ctl);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -721,9 +709,9 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
   c->blk_begin.assign(nF + 1, 0);
   c->lin8 = !c->exact && nP >= kLin8MinPoints;
   if (const char* e = std::getenv("HS_LIN8")) c->lin8 = !c->exact && e[0] == '1';
-  // the side-stream select pays an event hand-off (~1.4 us per step measured at 2k): only where the select is long
-  c->side_th = nP >= kLin8MinPoints;
-  if (const char* e = std::getenv("HS_SIDE_TH")) c->side_th = e[0] == '1';
+  // the extra launch of pass 3 costs more than a one-block scan of a small window's candidates
+  c->th_multi = nP >= kLin8MinPoints;
+  if (const char* e = std::getenv("HS_TH_MULTI")) c->th_multi = e[0] == '1';
   // points per block: hs_k_lin HS_LIN_NW waves x ppw points; hs_k_lin8 4 waves x ppw groups of 8 points (its
   // partition also serves hs_k_lin's marginalization / linearizeAll(true) passes, with W = 4 of its waves)
   const int bw = c->lin8 ? (HS_LIN8_NT / 64) * 8 : HS_LIN_NW;
@@ -842,6 +830,9 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
   HS_TRY(dalloc(&c->d_xAd, nF * nF * 8)); HS_TRY(dalloc(&c->d_x, n)); HS_TRY(dalloc(&c->d_elog, kLogCap));
   HS_TRY(dalloc(&c->d_cand, (size_t)c->cand_stride * c->nranks));
   HS_TRY(dalloc(&c->d_th_hist, HS_TH_BINS));
+  HS_TRY(dalloc(&c->d_th_hist2, 1024));
+  HS_TRY(dalloc(&c->d_th_nsurv, 1));
+  HS_TRY(dalloc(&c->d_th_surv, c->th_multi ? HS_TH_SURV : 1));
   HS_HIP(hipMemset(c->d_cand, 0xff, sizeof(float) * c->cand_stride * c->nranks));  // NaN, sign set: no candidate
   const char* tr = std::getenv("HS_KTRACE");
   c->tracing = tr && tr[0] == '1';
@@ -1478,7 +1469,7 @@ extern "C" int hs_debug_threshold(const float* cand, int n, float thn, float fac
   a.th_hist = d_h;
   a.nhist = std::min(64, std::max(1, (n + 4095) / 4096));
   hipLaunchKernelGGL(hs_k_reduce, dim3(1 + a.nhist), dim3(256), 0, 0, a);
-  hipLaunchKernelGGL(hs_k_debug_th, dim3(1), dim3(HS_STITCH_NT), 0, 0, a);
+  hipLaunchKernelGGL(hs_k_th_select, dim3(1), dim3(HS_STITCH_NT), 0, 0, a);
   HS_HIP(hipGetLastError());
   unsigned int hz[HS_TH_BINS];
   HS_HIP(hipMemcpy(th_out, d_th, sizeof(float), hipMemcpyDeviceToHost));

@@ -878,54 +878,62 @@ __device__ __forceinline__ unsigned int block_incl_scan(unsigned int x, unsigned
 
 constexpr int TH_CAP = 24576;  // survivors of pass 1 kept in LDS (else pass 3 re-reads the candidates)
 
-// sm: >= 1600 + TH_CAP words of LDS (the stitch block's scratch).  blockDim.x == HS_STITCH_NT (4 bins per thread)
-__device__ void red_energy_th_block(const HsRedArgs& a, unsigned int* sm) {
+// pass 1's bin: the pass-1 histogram's bin b1 holding the k-th smallest candidate (k = (int)(THN * n)) and the
+// rank kk of the wanted value inside b1; n = number of candidates (0: no candidate).  zero: re-zero the histogram for
+// the next launch (its last reader does).  Every thread of the block calls it; blockDim.x == HS_STITCH_NT.
+__device__ __forceinline__ void th_pass1(const HsRedArgs& a, unsigned int* wsum, unsigned int* ctl, bool zero,
+                                         unsigned int& b1, unsigned int& kk, unsigned int& n) {
   static_assert(HS_TH_BINS == 4 * HS_STITCH_NT, "pass-1 bins: 4 per thread");
-  unsigned int* hist2 = sm;          // [1024]
-  unsigned int* hist3 = sm + 1024;   // [512]
-  unsigned int* wsum = sm + 1536;    // [16]
-  unsigned int* ctl = sm + 1552;     // bin, k, survivors, count
-  unsigned int* buf = sm + 1600;     // [TH_CAP]
-  const int tid = threadIdx.x, nt = blockDim.x;
-  const int total = a.nranks * a.stride;
-  // ---- pass 1: bins 4 tid .. 4 tid + 3 of the global histogram (then re-zeroed for the next launch)
+  const int tid = threadIdx.x;
   uint4 h4 = reinterpret_cast<const uint4*>(a.th_hist)[tid];
-  reinterpret_cast<uint4*>(a.th_hist)[tid] = make_uint4(0u, 0u, 0u, 0u);
-  for (int i = tid; i < 1024 + 512; i += nt) sm[i] = 0u;
-  if (tid == 0) ctl[2] = 0u;
-  unsigned int n = 0;
+  if (zero) reinterpret_cast<uint4*>(a.th_hist)[tid] = make_uint4(0u, 0u, 0u, 0u);
   const unsigned int s4 = h4.x + h4.y + h4.z + h4.w;
-  unsigned int incl = block_incl_scan(s4, wsum, n);
-  if (n == 0) {
-    if (tid == 0) a.frameTH[a.newest] = 12 * 12 * 8;
-    return;
-  }
-  unsigned int kk = (unsigned int)(int)(a.frameEnergyTHN * (float)n);
-  if (incl - s4 <= kk && kk < incl) {
+  const unsigned int incl = block_incl_scan(s4, wsum, n);
+  if (n == 0) return;
+  const unsigned int k = (unsigned int)(int)(a.frameEnergyTHN * (float)n);
+  if (incl - s4 <= k && k < incl) {
     unsigned int run = incl - s4;
     int r = 0;
 #pragma unroll
     for (int q = 0; q < 3; q++) {
       const unsigned int cq = q == 0 ? h4.x : (q == 1 ? h4.y : h4.z);
-      if (r == q && kk >= run + cq) {
+      if (r == q && k >= run + cq) {
         run += cq;
         r = q + 1;
       }
     }
     ctl[0] = 4u * tid + r;
-    ctl[1] = kk - run;
+    ctl[1] = k - run;
   }
   __syncthreads();
-  const unsigned int b1 = ctl[0];
+  b1 = ctl[0];
   kk = ctl[1];
-  // ---- pass 2: bits 18..9 of the candidates in bin b1; survivors compacted into LDS (order irrelevant: counts)
-  constexpr int TH_U = 16;  // candidates in flight per thread (the scan is latency-bound: one block)
-  for (int i0 = 0; i0 < total; i0 += TH_U * nt) {
+}
+
+// Multi-block pass 2 (large windows; the stitch launch's np2 extra blocks): block q counts bits 18..9 of its chunk's
+// candidates in bin b1 into the global pass-2 histogram and appends them to the global survivor list (LDS
+// histogram and LDS compaction first: one global atomic per non-empty bin and one per block for the list range).
+// The pass-3 select (red_energy_th_block with th_hist2 set) runs after the stitch.
+__device__ void red_th_pass2_block(const HsRedArgs& a, int q, unsigned int* sm) {
+  unsigned int* hist2 = sm;          // [1024]
+  unsigned int* wsum = sm + 1024;    // [16]
+  unsigned int* ctl = sm + 1040;     // bin, k, block survivors, list base
+  unsigned int* buf = sm + 1088;     // [TH_CAP]
+  const int tid = threadIdx.x, nt = blockDim.x;
+  for (int i = tid; i < 1024; i += nt) hist2[i] = 0u;
+  if (tid == 0) ctl[2] = 0u;
+  unsigned int b1 = 0, kk = 0, n = 0;
+  th_pass1(a, wsum, ctl, false, b1, kk, n);
+  if (n == 0) return;
+  const int total = a.nranks * a.stride;
+  const int per = (total + a.np2 - 1) / a.np2, i0 = q * per, i1 = min(total, i0 + per);
+  constexpr int TH_U = 16;
+  for (int c0 = i0; c0 < i1; c0 += TH_U * nt) {
     unsigned int v[TH_U];
 #pragma unroll
     for (int u = 0; u < TH_U; u++) {
-      const int i = i0 + u * nt + tid;
-      v[u] = i < total ? __float_as_uint(a.cand[i]) : 0xffffffffu;
+      const int i = c0 + u * nt + tid;
+      v[u] = i < i1 ? __float_as_uint(a.cand[i]) : 0xffffffffu;
     }
 #pragma unroll
     for (int u = 0; u < TH_U; u++)
@@ -936,7 +944,81 @@ __device__ void red_energy_th_block(const HsRedArgs& a, unsigned int* sm) {
       }
   }
   __syncthreads();
-  const unsigned int ns = ctl[2];
+  const unsigned int ns = min(ctl[2], (unsigned int)TH_CAP);
+  if (tid == 0) {
+    // the block's survivors (a chunk beyond TH_CAP counts as an overflow: pass 3 then re-scans the candidates)
+    const unsigned int base = atomicAdd(a.th_nsurv, ctl[2] > (unsigned int)TH_CAP ? 0x40000000u : ns);
+    ctl[3] = base;
+  }
+  for (int i = tid; i < 1024; i += nt)
+    if (hist2[i]) atomicAdd(&a.th_hist2[i], hist2[i]);
+  __syncthreads();
+  const unsigned int base = ctl[3];
+  for (unsigned int i = tid; i < ns; i += nt)
+    if (base + i < (unsigned int)HS_TH_SURV) a.th_surv[base + i] = buf[i];
+}
+
+// sm: >= 1600 + TH_CAP words of LDS (the stitch block's scratch).  blockDim.x == HS_STITCH_NT (4 bins per thread).
+// With a.th_hist2 set, pass 2 is the stitch launch's multi-block one: its histogram and survivor list are read here
+// (and re-zeroed) instead of re-scanning the candidates.
+__device__ void red_energy_th_block(const HsRedArgs& a, unsigned int* sm) {
+  unsigned int* hist2 = sm;          // [1024]
+  unsigned int* hist3 = sm + 1024;   // [512]
+  unsigned int* wsum = sm + 1536;    // [16]
+  unsigned int* ctl = sm + 1552;     // bin, k, survivors, count
+  unsigned int* buf = sm + 1600;     // [TH_CAP]
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int total = a.nranks * a.stride;
+  const bool multi = a.th_hist2 != nullptr;
+  for (int i = tid; i < 1024 + 512; i += nt) sm[i] = 0u;
+  if (tid == 0) ctl[2] = 0u;
+  // ---- pass 1: bins 4 tid .. 4 tid + 3 of the global histogram (then re-zeroed for the next launch)
+  unsigned int b1 = 0, kk = 0, n = 0;
+  th_pass1(a, wsum, ctl, true, b1, kk, n);
+  unsigned int ns = 0, srcn = 0;
+  const unsigned int* src = nullptr;  // the survivors pass 3 reads (nullptr: re-scan the candidates)
+  if (multi) {
+    const unsigned int gs = *a.th_nsurv;
+    for (int i = tid; i < 1024; i += nt) {
+      hist2[i] = a.th_hist2[i];
+      a.th_hist2[i] = 0u;
+    }
+    __syncthreads();
+    if (tid == 0) *a.th_nsurv = 0u;
+    if (gs <= (unsigned int)HS_TH_SURV) {
+      src = a.th_surv;
+      srcn = gs;
+    }
+  }
+  if (n == 0) {
+    if (tid == 0) a.frameTH[a.newest] = 12 * 12 * 8;
+    return;
+  }
+  if (!multi) {
+    // ---- pass 2: bits 18..9 of the candidates in bin b1; survivors compacted into LDS (order irrelevant: counts)
+    constexpr int TH_U = 16;  // candidates in flight per thread (the scan is latency-bound: one block)
+    for (int i0 = 0; i0 < total; i0 += TH_U * nt) {
+      unsigned int v[TH_U];
+#pragma unroll
+      for (int u = 0; u < TH_U; u++) {
+        const int i = i0 + u * nt + tid;
+        v[u] = i < total ? __float_as_uint(a.cand[i]) : 0xffffffffu;
+      }
+#pragma unroll
+      for (int u = 0; u < TH_U; u++)
+        if (v[u] <= 0x7f800000u && (v[u] >> 19) == b1) {
+          atomicAdd(&hist2[(v[u] >> 9) & 1023u], 1u);
+          const unsigned int pos = atomicAdd(&ctl[2], 1u);
+          if (pos < (unsigned int)TH_CAP) buf[pos] = v[u];
+        }
+    }
+    __syncthreads();
+    ns = ctl[2];
+    if (ns <= (unsigned int)TH_CAP) {
+      src = buf;
+      srcn = ns;
+    }
+  }
   {
     const unsigned int c = hist2[tid];
     unsigned int tot;
@@ -950,12 +1032,13 @@ __device__ void red_energy_th_block(const HsRedArgs& a, unsigned int* sm) {
   const unsigned int p2 = (b1 << 10) | ctl[0];
   kk = ctl[1];
   // ---- pass 3: bits 8..0 of the survivors with prefix p2
-  if (ns <= (unsigned int)TH_CAP) {
-    for (unsigned int i = tid; i < ns; i += nt) {
-      const unsigned int v = buf[i];
+  if (src) {
+    for (unsigned int i = tid; i < srcn; i += nt) {
+      const unsigned int v = src[i];
       if ((v >> 9) == p2) atomicAdd(&hist3[v & 511u], 1u);
     }
   } else {
+    constexpr int TH_U = 16;
     for (int i0 = 0; i0 < total; i0 += TH_U * nt) {
       unsigned int v[TH_U];
 #pragma unroll
@@ -1068,7 +1151,7 @@ __global__ __launch_bounds__(256) void hs_k_reduce(HsRedArgs a) {
   HS_TRACE(a, 15);
 }
 
-__global__ __launch_bounds__(HS_STITCH_NT) void hs_k_debug_th(HsRedArgs a) {
+__global__ __launch_bounds__(HS_STITCH_NT) void hs_k_th_select(HsRedArgs a) {
   __shared__ unsigned int sm[1600 + TH_CAP];
   red_energy_th_block(a, sm);
 }
@@ -1102,6 +1185,10 @@ __global__ __launch_bounds__(ST_NT) void hs_k_stitch(HsStitchArgs a) {
   if (j == nFB + nF + 1) {  // setNewFrameEnergyTH for the next linearization, beside the stitch
     if (!a.red.skip_threshold) red_energy_th_block(a.red, reinterpret_cast<unsigned int*>(lds));
     HS_TRACE(a, 15);
+    return;
+  }
+  if (j > nFB + nF + 1) {  // large windows: the select's pass 2, spread over np2 blocks (pass 3 runs after)
+    red_th_pass2_block(a.red, j - (nFB + nF + 2), reinterpret_cast<unsigned int*>(lds));
     return;
   }
   auto adH = [&](int h, int t) { return a.adHost + (size_t)(h + nF * t) * 64; };

@@ -119,9 +119,16 @@ struct HsRedArgs {
   // hs_k_reduce into th_hist (integer atomics: order-independent); consumed and re-zeroed by hs_k_stitch
   unsigned int* th_hist;
   int nhist;
+  // large windows: the select's pass 2 by np2 blocks of the stitch launch (nullptr / 0: the select block scans the
+  // candidates itself): pass-2 histogram [1024], survivor list [HS_TH_SURV] and its length (zero between launches)
+  unsigned int* th_hist2;
+  unsigned int* th_surv;
+  unsigned int* th_nsurv;
+  int np2;
   long long* trace;
 };
 constexpr int HS_TH_BINS = 4096;
+constexpr int HS_TH_SURV = 1 << 20;
 
 // hs_k_stitch: stitchDoubleMT of the top and Schur systems from the host sums, one block per output block of the
 // system (8x8 frame blocks f <= g, calib x frame f, calib x calib), every output entry summed over the
@@ -186,7 +193,7 @@ __global__ void hs_k_lin_fix(HsLinArgs a);        // + linearizeAll(true)'s per-
 __global__ void hs_k_lin_exact_fix(HsLinArgs a);
 __global__ void hs_k_lin8(HsLinArgs a);       // production: lane = (point, target slot), 8 points per wave
 __global__ void hs_k_reduce(HsRedArgs a);
-__global__ void hs_k_debug_th(HsRedArgs a);     // test hook: the threshold select block alone
+__global__ void hs_k_th_select(HsRedArgs a);    // the threshold select block alone (pass 3 of the multi-block select; test hook)
 __global__ void hs_k_stitch(HsStitchArgs a);
 __global__ void hs_k_solve(HsSolveArgs a);
 __global__ void hs_k_resub(HsResubArgs a);

@@ -117,18 +117,18 @@ def test_lin8_runs_are_bit_reproducible(scene_kitti20k):
         assert np.array_equal(a, b)
 
 
-def test_side_stream_select_matches_in_stitch_select(scene2k):
-    """setNewFrameEnergyTH's select on the side stream (HS_SIDE_TH=1, the default from 60k points: it runs beside the
-    stitch and the solve) against the select block of hs_k_stitch (HS_SIDE_TH=0): the same code on the same
-    histogram, so the fused GN loop's energies, thresholds, frame states and depths are bit-identical."""
+def test_multi_block_select_matches_in_stitch_select(scene2k):
+    """setNewFrameEnergyTH's select as a multi-block pass 2 in the stitch launch + a one-block pass 3 (HS_TH_MULTI=1,
+    the default from 60k points) against the stitch's single select block (HS_TH_MULTI=0): the same counts, so the
+    fused GN loop's energies, thresholds, frame states and depths are bit-identical."""
     from hslam_amd.ba import BAWindow
     outs = []
     for mode in ("1", "0"):
-        os.environ["HS_SIDE_TH"] = mode
+        os.environ["HS_TH_MULTI"] = mode
         try:
             g = BAWindow(scene2k)
         finally:
-            os.environ.pop("HS_SIDE_TH", None)
+            os.environ.pop("HS_TH_MULTI", None)
         g.linearizeAll(reset=True)
         e = g.iterate(0, 5)
         f = g.frames()
