@@ -17,8 +17,10 @@ for W in trace track act refine select; do
   timeout -k 10 300 python bench.py --workload $W --steps 20 --warmup 3 --cpu-seconds 8 > $OUT/bench_$W.json 2> $OUT/bench_$W.err || { echo "bench $W failed rc=$?"; tail -20 $OUT/bench_$W.err; exit 1; }
   head -c 400 $OUT/bench_$W.json; echo
 done
-for P in 20000 200000; do
-  timeout -k 10 200 python bench.py --steps 30 --warmup 3 --no-cpu --points $P > $OUT/p$P.json 2> $OUT/p$P.err || { echo "sweep $P failed"; exit 1; }
+timeout -k 10 300 python bench.py --workload ba-kitti --steps 50 --warmup 5 --cpu-seconds 6 > $OUT/bench_ba_kitti.json 2> $OUT/bench_ba_kitti.err || { echo "bench ba-kitti failed"; tail -20 $OUT/bench_ba_kitti.err; exit 1; }
+head -c 300 $OUT/bench_ba_kitti.json; echo
+for P in 20000 200000 2000000; do
+  timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu --points $P > $OUT/p$P.json 2> $OUT/p$P.err || { echo "sweep $P failed"; exit 1; }
 done
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- python3 $GRAFT_REPO_ROOT/bench.py --steps 50 --warmup 5 --no-cpu > $OUT/prof_bench.json 2> $OUT/prof_bench.err
