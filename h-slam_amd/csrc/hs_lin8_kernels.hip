@@ -503,8 +503,8 @@ __global__ __launch_bounds__(HS_LIN8_NT) void hs_k_lin8(HsLinArgs a) {
 #pragma unroll
           for (int o2 = o1; o2 < 7; o2++) D[o1 * 7 - (o1 * (o1 - 1)) / 2 + (o2 - o1)] += wl * j2[o2];
         }
-        if (es != h && ((mq >> es) & 1u)) {
-          const float jv = W.jb[qp][ek][eo];
+        {  // predicated, not branched: jb holds 0 for an inactive residual, and the host slot reads 0
+          const float jv = es != h ? W.jb[qp][ek][min(eo, 6)] : 0.f;
           const float wl = hdf * jv;
 #pragma unroll
           for (int c = 0; c < 4; c++) E[c] += wl * hcv[c];
