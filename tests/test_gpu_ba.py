@@ -109,7 +109,9 @@ def test_solve_and_step(scene2k):
         assert np.linalg.norm(xg - xo) <= max(1e-3, 2 * spread) * np.linalg.norm(xo), (it, spread)
         po, pg, p8 = o.points(), g.points(), o8.points()
         sstep = np.abs(p8["step"] - po["step"]).max()
-        assert np.all(np.abs(pg["step"] - po["step"]) <= np.maximum(1e-2 * np.abs(po["step"]), 2 * sstep + 1e-12))
+        # the point steps inherit x's accumulation-order sensitivity: bounded by 2x the oracle's own 1- vs 8-thread
+        # spread of the same step (measured GPU deviation 0.03-0.07x that spread, tools/dbg/spread_check.py)
+        assert np.abs(pg["step"] - po["step"]).max() <= 2 * sstep + 1e-12, (it, sstep)
         for oo in (o, o8):
             oo.do_step()
         g.doStepFromBackup()
@@ -230,12 +232,18 @@ def test_window_edge_cases():
     ng, e1 = g.optimize(4)
     no, e2 = o.optimize(4)
     assert ng == no == 15  # System::optimize raises the budget to 15 for a 2-frame window
-    # a 2-frame window is poorly conditioned (scale gauge): fp64 rounding differences of the solve
-    # (LDLT order, device sin/cos in the step) are amplified mid-trajectory, so the middle of the
-    # trajectory is compared at 1e-2 and the start / converged end at 1e-3.
+    # a 2-frame window is poorly conditioned (scale gauge): rounding differences of the solve are amplified along
+    # the trajectory.  The bar is tied to the oracle's own 8-thread pool on the same trajectory (measured: GPU
+    # <= 2.1e-5 relative, pool up to 1.6e-4; tools/dbg/spread_check.py): 10x the pool's largest deviation, at least
+    # 1e-4.
+    from oracle_ffi import OracleBA
+    o8 = OracleBA(s, nthreads=8)
+    o8.linearize_all(reset=True)
+    o8.apply_res()
+    _, e8 = o8.optimize(4)
+    pool = np.max(np.abs(e8 - e2) / np.abs(e2))
     assert abs(e1[0] - e2[0]) <= 1e-9 * abs(e2[0])
-    assert np.all(np.abs(e1 - e2) <= 1e-2 * np.abs(e2) + 1e-6)
-    assert abs(e1[-1] - e2[-1]) <= 1e-3 * abs(e2[-1])
+    assert np.all(np.abs(e1 - e2) <= max(10 * pool, 1e-4) * np.abs(e2)), (pool, np.max(np.abs(e1 - e2) / np.abs(e2)))
 
 
 def test_split_accumulation_matches_threaded_reference(scene2k):
