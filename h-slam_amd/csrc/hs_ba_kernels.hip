@@ -2155,50 +2155,63 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
   }
   __syncthreads();
   if (a.flags & HS_APPLY) {
-    // backupState + doStepFromBackup(1, 1, 1, 1, 1) + setPrecalcValues (Src/FullSystemOptimize.cpp:171-314),
-    // register-resident: thread (h, t) of the nF x nF pairs forms both frames' new poses itself (no stage barrier
-    // between the frame update and the precalc) and then the pair's FrameFramePrecalc::set; the (f, f) threads
-    // write frame f back, thread 0 the calib.  PRE_RTll_0 / PRE_tTll_0 depend on evalPT only and stay as uploaded.
+    // backupState + doStepFromBackup(1, 1, 1, 1, 1) + setPrecalcValues (Src/FullSystemOptimize.cpp:171-314) in two
+    // register-resident stages of wave 0: lane f < nF steps frame f (new state, its scaled copy, PRE_worldToCam
+    // = exp(scaled xi) * evalPT and its inverse) and writes it back; after one barrier lane (h, t) of the nF x nF
+    // pairs reads both frames' poses from LDS and forms the pair's FrameFramePrecalc::set; thread 0 writes the
+    // calib.  Each SE(3) exp / product runs once per frame (the stage-free form ran two per lane, on one wave's
+    // serial fp64 issue).  PRE_RTll_0 / PRE_tTll_0 depend on evalPT only and stay as uploaded.
     const int np = nF * nF;
-    const int hh = tid < np ? tid / nF : 0, tt = tid < np ? tid - hh * nF : 0;
-    double cv[4], sh[10], stH[10], st_t[10], stT[10], evH[7], evT[7];
-    float expH = 1.f, expT = 1.f;
-    double szH7 = 0.0;
-    if (tid < np) {  // every input into registers, then one barrier before any write-back
+    double* fx = B;  // LDLT scratch (free now): per frame PRE_worldToCam (7) | PRE_camToWorld (7) | scaled a, b
+    double cv[4];
 #pragma unroll
-      for (int q = 0; q < 4; q++) cv[q] = st->calib.value[q] + 1.0f * st->calib.step[q];
+    for (int q = 0; q < 4; q++) cv[q] = st->calib.value[q] + 1.0f * st->calib.step[q];
+    if (tid < nF) {
+      hs::FrameH& F = st->frames[tid];
+      double sh[10], ns[10], sc[10], ev[7];
+#pragma unroll
+      for (int q = 0; q < 10; q++) {
+        sh[q] = F.state[q];
+        ns[q] = sh[q] + 1.0 * F.step[q];
+      }
+      F.evalPT.toData(ev);
+      scale_state(ns, sc);
+      const hs::SE3 PW = se3_mul_step(se3_exp_step(sc), hs::SE3::fromData(ev));
+      const hs::SE3 PC = PW.inverse();
+      double* o = fx + 16 * tid;
+      PW.toData(o);
+      PC.toData(o + 7);
+      o[14] = sc[6];
+      o[15] = sc[7];
+      // backupState, setState, setDeltaF's delta / delta_prior
+#pragma unroll
+      for (int q = 0; q < 10; q++) {
+        F.state_backup[q] = sh[q];
+        F.state[q] = ns[q];
+        F.state_scaled[q] = sc[q];
+      }
+      F.PRE_worldToCam = PW;
+      F.PRE_camToWorld = PC;
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        F.delta[q] = ns[q] - F.state_zero[q];
+        F.delta_prior[q] = ns[q] - 0.0;
+      }
+    }
+    if ((a.dbg & 16) && a.trace && tid == 0) a.trace[22] = clock64();
+    __syncthreads();
+    if ((a.dbg & 16) && a.trace && tid == 0) a.trace[23] = clock64();
+    if (tid < np) {
+      const int hh = tid / nF, tt = tid - hh * nF;
+      const double* oh = fx + 16 * hh;
+      const double* ot = fx + 16 * tt;
+      hs::SE3 PWt, PCh;
+      PWt.q = hs::Quat{ot[0], ot[1], ot[2], ot[3]};
+      PWt.t[0] = ot[4]; PWt.t[1] = ot[5]; PWt.t[2] = ot[6];
+      PCh.q = hs::Quat{oh[7], oh[8], oh[9], oh[10]};
+      PCh.t[0] = oh[11]; PCh.t[1] = oh[12]; PCh.t[2] = oh[13];
       const hs::FrameH& H = st->frames[hh];
       const hs::FrameH& T = st->frames[tt];
-#pragma unroll
-      for (int q = 0; q < 10; q++) {
-        sh[q] = H.state[q];
-        stH[q] = H.step[q];
-        st_t[q] = T.state[q];
-        stT[q] = T.step[q];
-      }
-      H.evalPT.toData(evH);
-      T.evalPT.toData(evT);
-      expH = H.ab_exposure;
-      expT = T.ab_exposure;
-      szH7 = H.state_zero[7];
-    }
-    if ((a.dbg & 16) && a.trace && tid == 0) a.trace[20] = clock64();
-    __syncthreads();
-    if ((a.dbg & 16) && a.trace && tid == 0) a.trace[21] = clock64();
-    if (tid < np) {
-      double nsH[10], nsT[10];
-#pragma unroll
-      for (int q = 0; q < 10; q++) {
-        nsH[q] = sh[q] + 1.0 * stH[q];
-        nsT[q] = st_t[q] + 1.0 * stT[q];
-      }
-      double scH[10], scT[10];
-      scale_state(nsH, scH);
-      scale_state(nsT, scT);
-      const hs::SE3 PWh = se3_mul_step(se3_exp_step(scH), hs::SE3::fromData(evH));
-      const hs::SE3 PWt = se3_mul_step(se3_exp_step(scT), hs::SE3::fromData(evT));
-      const hs::SE3 PCh = PWh.inverse();
-      if ((a.dbg & 16) && a.trace && tid == 0) a.trace[22] = clock64() + (long long)(PCh.t[0] * 0.0 + PWt.t[1] * 0.0);
       // FrameFramePrecalc::set: PRE_RTll / PRE_tTll, K R Ki, K t, the affine mode, b0
       const hs::SE3 l2l = se3_mul_step(PWt, PCh);
       double R[9];
@@ -2217,7 +2230,7 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
       hs::mm3f(KR, Ki, KRKi);
       hs::mv3f(K, tT, Kt);
       double aff[2];
-      hs::fromToVecExposure(expH, expT, scH[6], scH[7], scT[6], scT[7], aff);
+      hs::fromToVecExposure(H.ab_exposure, T.ab_exposure, oh[14], oh[15], ot[14], ot[15], aff);
       HsPrecalc* pc = a.pre + tid;
 #pragma unroll
       for (int i = 0; i < 9; i++) pc->KRKi[i] = KRKi[i];
@@ -2225,25 +2238,7 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
       for (int i = 0; i < 3; i++) pc->Kt[i] = Kt[i];
       pc->aff[0] = (float)aff[0];
       pc->aff[1] = (float)aff[1];
-      pc->b0 = (float)(szH7 * hs::SCALE_B);  // aff0_b of the host
-      if ((a.dbg & 16) && a.trace && tid == 0) a.trace[23] = clock64() + (long long)(aff[0] * 0.0 + KRKi[3] * 0.0);
-      if (hh == tt) {  // frame hh: backupState, setState, setDeltaF's delta / delta_prior
-        hs::FrameH& F = st->frames[hh];
-        const hs::SE3 PCw = PCh;
-#pragma unroll
-        for (int q = 0; q < 10; q++) {
-          F.state_backup[q] = sh[q];
-          F.state[q] = nsH[q];
-          F.state_scaled[q] = scH[q];
-        }
-        F.PRE_worldToCam = PWh;
-        F.PRE_camToWorld = PCw;
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-          F.delta[q] = nsH[q] - F.state_zero[q];
-          F.delta_prior[q] = nsH[q] - 0.0;
-        }
-      }
+      pc->b0 = (float)(H.state_zero[7] * hs::SCALE_B);  // aff0_b of the host
       if (tid == 0) {
         hs::CalibH& cal = st->calib;
 #pragma unroll
