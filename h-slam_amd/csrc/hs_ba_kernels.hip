@@ -1323,10 +1323,12 @@ __global__ __launch_bounds__(ST_NT) void hs_k_stitch(HsStitchArgs a) {
           v = sandwich8(aTf + h * 64, Dx + h * 64, aTg + h * 64, sw, lane);  // adT[h,f] D_h(f,g) adT[h,g]^T
         } else if (h == f) {  // (sum_t1 adH[f,t1] D_f(t1, g)) adT[f,g]^T
           double y0 = 0.0, y1 = 0.0;
-          for (int t1 = 0; t1 < nF; t1++) {
-            if (t1 == f) continue;
-            if (t1 & 1) y1 += mm8(aHf + t1 * 64, Dq + t1 * 64, r, c);
-            else y0 += mm8(aHf + t1 * 64, Dq + t1 * 64, r, c);
+#pragma unroll
+          for (int t1 = 0; t1 < HS_MAXF; t1++) {
+            const double pv = mm8(aHf + t1 * 64, Dq + t1 * 64, r, c);
+            const bool on = t1 < nF && t1 != f;
+            if (t1 & 1) y1 = on ? y1 + pv : y1;
+            else y0 = on ? y0 + pv : y0;
           }
           sw[lane] = y0 + y1;
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1336,10 +1338,12 @@ __global__ __launch_bounds__(ST_NT) void hs_k_stitch(HsStitchArgs a) {
           __builtin_amdgcn_wave_barrier();
         } else {  // adT[g,f] (sum_t2 D_g(f, t2) adH[g,t2]^T)
           double y0 = 0.0, y1 = 0.0;
-          for (int t2 = 0; t2 < nF; t2++) {
-            if (t2 == g) continue;
-            if (t2 & 1) y1 += mm8t(Dq + 512 + t2 * 64, aHg + t2 * 64, r, c);
-            else y0 += mm8t(Dq + 512 + t2 * 64, aHg + t2 * 64, r, c);
+#pragma unroll
+          for (int t2 = 0; t2 < HS_MAXF; t2++) {
+            const double pv = mm8t(Dq + 512 + t2 * 64, aHg + t2 * 64, r, c);
+            const bool on = t2 < nF && t2 != g;
+            if (t2 & 1) y1 = on ? y1 + pv : y1;
+            else y0 = on ? y0 + pv : y0;
           }
           sw[lane] = y0 + y1;
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1356,7 +1360,11 @@ __global__ __launch_bounds__(ST_NT) void hs_k_stitch(HsStitchArgs a) {
       HS_TRACE(a, 2);
       if (tid < 64) {
         double hs = 0.0;
-        for (int h = 0; h < nF; h++) hs += tS[h * 64 + lane];
+#pragma unroll
+        for (int h = 0; h < HS_MAXF; h++) {  // unrolled with masked slots: the LDS reads issue together
+          const double v = tS[h * 64 + lane];
+          hs = h < nF ? hs + v : hs;
+        }
         const double ha = tA[lane] + tA[64 + c * 8 + r];
         put(4 + 8 * f + r, 4 + 8 * g + c, ha, hs, false);
       }
@@ -1386,10 +1394,12 @@ __global__ __launch_bounds__(ST_NT) void hs_k_stitch(HsStitchArgs a) {
           tS[y * 64 + lane] = sandwich8(aTf + y * 64, Dx + y * 64, aTf + y * 64, sw, lane);
         } else if (kind == 1) {
           double v0 = 0.0, v1 = 0.0;
-          for (int t2 = 0; t2 < nF; t2++) {
-            if (t2 == f) continue;
-            if (t2 & 1) v1 += mm8t(Dq + (y * 8 + t2) * 64, aHf + t2 * 64, r, c);
-            else v0 += mm8t(Dq + (y * 8 + t2) * 64, aHf + t2 * 64, r, c);
+#pragma unroll
+          for (int t2 = 0; t2 < HS_MAXF; t2++) {  // unrolled, the skipped slots masked: the LDS reads issue together
+            const double pv = mm8t(Dq + (y * 8 + t2) * 64, aHf + t2 * 64, r, c);
+            const bool on = t2 < nF && t2 != f;
+            if (t2 & 1) v1 = on ? v1 + pv : v1;
+            else v0 = on ? v0 + pv : v0;
           }
           sw[lane] = v0 + v1;
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1406,21 +1416,23 @@ __global__ __launch_bounds__(ST_NT) void hs_k_stitch(HsStitchArgs a) {
       __syncthreads();
       HS_TRACE(a, 2);
       if (tid < 64 && r <= c) {
-        double hs = 0.0, ha = 0.0;
-        for (int h = 0; h < nF; h++) {  // hosts in order; host f's term is its t1 partials in order
-          if (h != f) {
-            hs += tS[h * 64 + lane];
-          } else {
-            double hf = 0.0;
-            for (int t1 = 0; t1 < nF; t1++)
-              if (t1 != f) hf += tS[(8 + t1) * 64 + lane];
-            hs += hf;
-          }
+        // hosts in order, host f's term its t1 partials in order; then the top terms.  Unrolled over the 8 slots
+        // with the unused ones masked, so the 32 LDS reads issue together instead of one round trip per term
+        double vS[2 * HS_MAXF], vA[2 * HS_MAXF];
+#pragma unroll
+        for (int i = 0; i < 2 * HS_MAXF; i++) {
+          vS[i] = tS[i * 64 + lane];
+          vA[i] = tA[i * 64 + lane];
         }
-        for (int t = 0; t < nF; t++)
-          if (t != f) ha += tA[t * 64 + lane];
-        for (int h = 0; h < nF; h++)
-          if (h != f) ha += tA[(8 + h) * 64 + lane];
+        double hf = 0.0, hs = 0.0, ha = 0.0;
+#pragma unroll
+        for (int t1 = 0; t1 < HS_MAXF; t1++) hf = (t1 < nF && t1 != f) ? hf + vS[HS_MAXF + t1] : hf;
+#pragma unroll
+        for (int h = 0; h < HS_MAXF; h++) hs = h < nF ? hs + (h != f ? vS[h] : hf) : hs;
+#pragma unroll
+        for (int t = 0; t < HS_MAXF; t++) ha = (t < nF && t != f) ? ha + vA[t] : ha;
+#pragma unroll
+        for (int h = 0; h < HS_MAXF; h++) ha = (h < nF && h != f) ? ha + vA[HS_MAXF + h] : ha;
         put(4 + 8 * f + r, 4 + 8 * f + c, ha, hs, r == c);
       }
     }
@@ -2166,6 +2178,7 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     double cv[4];
 #pragma unroll
     for (int q = 0; q < 4; q++) cv[q] = st->calib.value[q] + 1.0f * st->calib.step[q];
+    if ((a.dbg & 16) && a.trace && tid == 0) a.trace[20] = clock64();
     if (tid < nF) {
       hs::FrameH& F = st->frames[tid];
       double sh[10], ns[10], sc[10], ev[7];
@@ -2247,6 +2260,7 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
         st->dcal = cal.device();
       }
     }
+    if ((a.dbg & 16) && a.trace && tid == 0) a.trace[21] = clock64();
     HS_TRACE(a, 6);
     if (tid == 64) {  // canbreak (the steps are not modified above)
       float sumA = 0, sumB = 0, sumT = 0, sumR = 0;
