@@ -1071,7 +1071,7 @@ __device__ void red_energy_th_block(const HsRedArgs& a, unsigned int* sm) {
 
 // the (R, C) entry (R <= C) of one (host, target) pair's 13x13 AccumulatorApprox block [calib 4 | xi 6 | a | b | r]
 // from its octet of the host sums, oct[e * 8 + k] = entry e of lane k (the owner layout of acc_point)
-__device__ __forceinline__ double top_oct(const double* oct, int R, int C) {
+__device__ __forceinline__ int top_oct_index(int R, int C) {
   int e, k;
   if (C < 8) { e = R; k = C; }                                     // Data (R, C <= 7): lane C, T[R]
   else if (C < 10) {
@@ -1085,7 +1085,13 @@ __device__ __forceinline__ double top_oct(const double* oct, int R, int C) {
     e = 15;
     k = R == 10 ? C - 10 : (R == 11 ? 2 + C - 10 : 5);
   }
-  return oct[e * 8 + k];
+  return e * 8 + k;
+}
+__device__ __forceinline__ double top_oct(const double* oct, int R, int C) { return oct[top_oct_index(R, C)]; }
+// the octet offset of entry `ln` (lane (r, c)) of a pair's A88 block ([xi a b] x [xi a b], symmetric)
+__device__ __forceinline__ int a88_index(int ln) {
+  const int R = 4 + (ln >> 3), C = 4 + (ln & 7);
+  return top_oct_index(min(R, C), max(R, C));
 }
 
 // 8x8 block products by one wave, lane (r, c): out = L M (L row r, M column c) / out = L M^T
@@ -1201,10 +1207,6 @@ __global__ __launch_bounds__(ST_NT) void hs_k_stitch(HsStitchArgs a) {
     else if (o1 <= o2) { base = (HS_E_TOP + dpair(o1, o2)) * 64; ls = 8; cs = 1; }
     else { base = (HS_E_TOP + dpair(o2, o1)) * 64; ls = 1; cs = 8; }
   };
-  auto decodeA88 = [&](double* dst, const double* oct) {  // [xi a b] x [xi a b]
-    const int R = 4 + r, C = 4 + c;
-    dst[lane] = top_oct(oct, min(R, C), max(R, C));
-  };
   double* out = a.out;
   double* sepA = a.sep;
   double* sepS = a.sep ? a.sep + SL : nullptr;
@@ -1230,8 +1232,7 @@ __global__ __launch_bounds__(ST_NT) void hs_k_stitch(HsStitchArgs a) {
     double* aTg = aHg + 512;       // [8][64] adT[h, g]
     double* Dx = aTg + 512;        // [8][64] D_h(f, g) by host h
     double* Dq = Dx + 512;         // f < g: [8][64] D_f(t1, g) by t1 | [8][64] D_g(f, t2) by t2; f == g: [8][8][64] D_f
-    double* oc = Dq + 4096;        // octets: f < g: (f, g) | (g, f); f == g: (f, t) by t | (h, f) by h, 128 each
-    double* A8 = oc + 2048;        // decoded A88 per octet [16][64]
+    double* A8 = Dq + 4096;        // A88 blocks [16][64]: f < g: (f, g) | (g, f); f == g: (f, t) by t | (h, f) by 8 + h
     double* tS = A8 + 1024;        // Schur terms [16][64]
     double* tA = tS + 1024;        // top terms [16][64]
     double* scr = tA + 1024;       // per-wave scratch [ST_NW][64]
@@ -1242,9 +1243,9 @@ __global__ __launch_bounds__(ST_NT) void hs_k_stitch(HsStitchArgs a) {
       // index math is shifts and masks, not runtime divisions
       const int nAdj = (f < g ? 4 : 2) * 512;        // [kind][t][64]
       const int nD = f < g ? 3 * 512 : 512 + 4096;   // f < g: [kind][x][64]; f == g: Dx [h][64] | Dq [t1][t2][64]
-      const int nOct = f < g ? 256 : 16 * 128;       // [slot][128]
+      const int nOct = f < g ? 128 : 16 * 64;        // A88 blocks [slot][64], gathered from the pairs' octets
       const int total = nAdj + nD + nOct;
-      constexpr int SU = (512 * 4 + 4608 + 2048 + ST_NT - 1) / ST_NT;
+      constexpr int SU = (512 * 4 + 4608 + 1024 + ST_NT - 1) / ST_NT;
       double v[SU];
       int dst[SU];
 #pragma unroll
@@ -1286,7 +1287,7 @@ __global__ __launch_bounds__(ST_NT) void hs_k_stitch(HsStitchArgs a) {
             src = HS(h) + base + rr * ls + cc * cs;
           }
         } else if (q < total) {
-          const int qo = q - nAdj - nD, oi = qo >> 7, w = qo & 127, e = w >> 3, k = w & 7;
+          const int qo = q - nAdj - nD, oi = qo >> 6, w = a88_index(qo & 63), e = w >> 3, k = w & 7;
           int hh = -1, tt = 0;
           if (f < g) {
             if (oi == 0) { hh = f; tt = g; } else { hh = g; tt = f; }
@@ -1299,7 +1300,7 @@ __global__ __launch_bounds__(ST_NT) void hs_k_stitch(HsStitchArgs a) {
           }
           if (hh >= 0) {
             src = HS(hh) + e * 64 + tt * 8 + k;
-            d = (int)(oc - lds) + qo;
+            d = (int)(A8 - lds) + qo;
           }
         }
         v[u] = *src;
@@ -1313,9 +1314,6 @@ __global__ __launch_bounds__(ST_NT) void hs_k_stitch(HsStitchArgs a) {
     HS_TRACE(a, 1);
     double* sw = scr + wv * 64;
     if (f < g) {
-      if (wv == 0) decodeA88(A8, oc);
-      if (wv == 1) decodeA88(A8 + 64, oc + 128);
-      __syncthreads();
       // terms: tS[h] for every host h (the host f / g terms in their host slot), tA[0] and tA[1]
       for (int h = wv; h < nF; h += ST_NW) {
         double v;
@@ -1369,11 +1367,6 @@ __global__ __launch_bounds__(ST_NT) void hs_k_stitch(HsStitchArgs a) {
         put(4 + 8 * f + r, 4 + 8 * g + c, ha, hs, false);
       }
     } else {
-      for (int x = wv; x < 2 * nF; x += ST_NW) {
-        const int t = x % nF, oi = x < nF ? t : 8 + t;  // octet slots: (f, t) at t, (h, f) at 8 + h
-        if (t != f) decodeA88(A8 + oi * 64, oc + oi * 128);
-      }
-      __syncthreads();
       // Schur terms: tS[h] = adT[h,f] D_h(f,f) adT[h,f]^T (h != f), tS[8 + t1] = adH[f,t1] sum_t2 D_f(t1,t2) adH[f,t2]^T
       // top terms: tA[t] host pairs (f, t), tA[8 + h] target pairs (h, f)
       // balanced over the 16 waves: the 7 heavy host-f terms (8 products each) on waves 0-6, the 21 two-product
