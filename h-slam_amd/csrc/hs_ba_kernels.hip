@@ -777,20 +777,26 @@ __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
   static_assert((NE * 64) % 4 == 0, "partials staged as float4");
   float4* out4 = reinterpret_cast<float4*>(a.part + (size_t)b * NE * 64);
   const float4* st4 = reinterpret_cast<const float4*>(lin_stage);
-  for (int i = tid; i < NE * 16; i += HS_LIN_NT) {
-    float4 v[HS_LIN_NW];
+  // both rounds' loads issued together (the round count is a compile-time constant), then the sums
+  constexpr int NI = (NE * 16 + HS_LIN_NT - 1) / HS_LIN_NT;
+  float4 v[NI][HS_LIN_NW];
 #pragma unroll
-    for (int w = 0; w < HS_LIN_NW; w++) v[w] = st4[w * NE * 16 + i];
-    float4 s = v[0];
+  for (int k = 0; k < NI; k++)
+#pragma unroll
+    for (int w = 0; w < HS_LIN_NW; w++) v[k][w] = st4[w * NE * 16 + min(tid + k * HS_LIN_NT, NE * 16 - 1)];
+#pragma unroll
+  for (int k = 0; k < NI; k++) {
+    const int i = tid + k * HS_LIN_NT;
+    float4 s = v[k][0];
 #pragma unroll
     for (int w = 1; w < HS_LIN_NW; w++)
       if (w < a.W) {
-        s.x += v[w].x;
-        s.y += v[w].y;
-        s.z += v[w].z;
-        s.w += v[w].w;
+        s.x += v[k][w].x;
+        s.y += v[k][w].y;
+        s.z += v[k][w].z;
+        s.w += v[k][w].w;
       }
-    out4[i] = s;
+    if (i < NE * 16) out4[i] = s;
   }
   if (tid < 3) {
     double s = se[tid];
