@@ -1990,6 +1990,9 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
 #pragma unroll
     for (int u = 0; u < NF_NU; u++) nfv[u] = a.Nproj[min(tid + u * SOLVE_NT, 2 * n * HS_NNS - 1)];
   }
+  // L^T must be zero on entry to the LDLT: stored while the prefetch above is in flight
+  if (solve)
+    for (int idx = tid; idx < HS_MAXDIM * LSTR; idx += nt) LT[idx] = 0.0;
   {
     uint2* ls = reinterpret_cast<uint2*>(st_raw);
 #pragma unroll
@@ -2034,12 +2037,13 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     auto delta = [&](int q) -> double {  // the reference's prior deltas: calib value - value_zero (as float), frame delta
       return q < 4 ? (double)(float)st->calib.value_minus_value_zero[q] : st->frames[(q - 4) >> 3].delta[(q - 4) & 7];
     };
-    // per row q (one thread each): the assembled diagonal, the scaling and the scaled right-hand side
+    // per row q (one thread each): the assembled diagonal, the scaling S = 1 / sqrt(diag + 10) (reciprocal square
+    // root + Newton: rounding-level from the IEEE quotient) and the scaled right-hand side
     if (tid < n) {
       const int q = tid;
       const double pr = q < 4 ? a.initialCalibHessian : st->frames[(q - 4) >> 3].prior[(q - 4) & 7];
       const double hv = dgv[q] + (pr + dgm[q]) * lam1;
-      const double sq = 1.0 / sqrt(hv + 10);
+      const double sq = rsqrt_step(hv + 10);
       Sv[q] = sq;
       A[q * n + q] = sq * hv * sq;
       const double bl = q < 4 ? a.initialCalibHessian * delta(q)
@@ -2049,7 +2053,6 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
         for (int k = 0; k < n; k++) hmd += a.HM[q * n + k] * delta(k);
       yv[q] = sq * ((bl + (dgm[HS_MAXDIM + q] + hmd)) + dgv[HS_MAXDIM + q]);
     }
-    for (int idx = tid; idx < HS_MAXDIM * LSTR; idx += nt) LT[idx] = 0.0;  // L^T: zero on entry
     __syncthreads();
     HS_TRACE(a, 7);
     // the scaled off-diagonal entries S H S, mirrored from the upper triangle
