@@ -2103,21 +2103,25 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
       }
     }
     if (s_it >= 2) {  // SOLVER_ORTHOGONALIZE_X_LATER: x -= P x, P = (N Npi^T + Npi N^T) / 2 (orthogonalize)
-      // t1 = Npi^T x, t2 = N^T x: 14 dot products over n, 4 lanes each
-      const int d = tid >> 2, part = tid & 3, len = n >> 2;
+      // t1 = Npi^T x, t2 = N^T x: 14 dot products over n, 16 lanes each (at most 5 terms per lane, then an xor
+      // tree: a short dependent chain)
+      const int d = tid >> 4, part = tid & 15;
+      constexpr int LEN = (HS_MAXDIM + 15) / 16;
       if (d < 2 * HS_NNS) {
         const double* col = Nf + (d < HS_NNS ? n * HS_NNS : 0);  // Npi for t1, N for t2
         const int kk = d % HS_NNS;
         double sacc = 0.0;
-        // unrolled to the longest quarter (the LDS loads are issued together, not one latency per term)
 #pragma unroll
-        for (int cc = 0; cc < HS_MAXDIM / 4; cc++) {
-          const int c = part * len + min(cc, len - 1);
-          const double t = __builtin_fma(col[c * HS_NNS + kk], xs[c], sacc);
-          sacc = cc < len ? t : sacc;
+        for (int cc = 0; cc < LEN; cc++) {
+          const int c = part * LEN + cc;
+          const int cl = min(c, n - 1);
+          const double t = __builtin_fma(col[cl * HS_NNS + kk], xs[cl], sacc);
+          sacc = c < n ? t : sacc;
         }
         sacc += __shfl_xor(sacc, 1);
         sacc += __shfl_xor(sacc, 2);
+        sacc += __shfl_xor(sacc, 4);
+        sacc += __shfl_xor(sacc, 8);
         if (part == 0) tk[d] = sacc;
       }
       __syncthreads();
