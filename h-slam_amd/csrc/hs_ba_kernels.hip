@@ -2126,21 +2126,21 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
       }
       __syncthreads();
       if ((a.dbg & 32) && a.trace && tid == 0) a.trace[27] = clock64();
-      if (tid < n) {
+    }
+    // resubstituteF_MT: frame / calib steps, xAd, cstep; row q's thread first applies its own orthogonalize
+    // update (x_q -= (P x)_q), so no barrier separates the two
+    if (tid < n) {
+      const int q = tid;
+      double xv = xs[q];
+      if (s_it >= 2) {
         double s1 = 0.0, s2 = 0.0;
 #pragma unroll
         for (int kk = 0; kk < HS_NNS; kk++) {
-          s1 = __builtin_fma(Nf[tid * HS_NNS + kk], tk[kk], s1);
-          s2 = __builtin_fma(Nf[n * HS_NNS + tid * HS_NNS + kk], tk[HS_NNS + kk], s2);
+          s1 = __builtin_fma(Nf[q * HS_NNS + kk], tk[kk], s1);
+          s2 = __builtin_fma(Nf[n * HS_NNS + q * HS_NNS + kk], tk[HS_NNS + kk], s2);
         }
-        xs[tid] -= 0.5 * (s1 + s2);
+        xv -= 0.5 * (s1 + s2);
       }
-      __syncthreads();
-    }
-    // resubstituteF_MT: frame / calib steps, xAd, cstep
-    if (tid < n) {
-      const int q = tid;
-      const double xv = xs[q];
       if (!isfinite(xv)) st->status = 1;
       xF[q] = (float)xv;
       st->lastX[q] = xv;
