@@ -2176,9 +2176,9 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     // backupState + doStepFromBackup(1, 1, 1, 1, 1) + setPrecalcValues (Src/FullSystemOptimize.cpp:171-314) in two
     // register-resident stages of wave 0: lane f < nF steps frame f (new state, its scaled copy, PRE_worldToCam
     // = exp(scaled xi) * evalPT and its inverse) and writes it back; after one barrier lane (h, t) of the nF x nF
-    // pairs reads both frames' poses from LDS and forms the pair's FrameFramePrecalc::set; thread 0 writes the
-    // calib.  Each SE(3) exp / product runs once per frame (the stage-free form ran two per lane, on one wave's
-    // serial fp64 issue).  PRE_RTll_0 / PRE_tTll_0 depend on evalPT only and stay as uploaded.
+    // pairs reads both frames' poses from LDS and forms the pair's FrameFramePrecalc::set while thread 64 (wave 1)
+    // writes the calib.  Each SE(3) exp / product runs once per frame (the stage-free form ran two per lane, on one
+    // wave's serial fp64 issue).  PRE_RTll_0 / PRE_tTll_0 depend on evalPT only and stay as uploaded.
     const int np = nF * nF;
     double* fx = B;  // LDLT scratch (free now): per frame PRE_worldToCam (7) | PRE_camToWorld (7) | scaled a, b
     double cv[4];
@@ -2258,13 +2258,13 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
       pc->aff[0] = (float)aff[0];
       pc->aff[1] = (float)aff[1];
       pc->b0 = (float)(H.state_zero[7] * hs::SCALE_B);  // aff0_b of the host
-      if (tid == 0) {
-        hs::CalibH& cal = st->calib;
+    }
+    if (tid == 64) {  // the calib (on wave 1, beside the pair stage: every lane read cv before the barrier)
+      hs::CalibH& cal = st->calib;
 #pragma unroll
-        for (int q = 0; q < 4; q++) cal.value_backup[q] = cal.value[q];
-        cal.setValue(cv);
-        st->dcal = cal.device();
-      }
+      for (int q = 0; q < 4; q++) cal.value_backup[q] = cal.value[q];
+      cal.setValue(cv);
+      st->dcal = cal.device();
     }
     if ((a.dbg & 16) && a.trace && tid == 0) a.trace[21] = clock64();
     HS_TRACE(a, 6);
