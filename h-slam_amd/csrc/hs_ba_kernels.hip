@@ -2174,10 +2174,9 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
   __syncthreads();
   if (a.flags & HS_APPLY) {
     // backupState + doStepFromBackup(1, 1, 1, 1, 1) + setPrecalcValues (Src/FullSystemOptimize.cpp:171-314) in two
-    // register-resident stages of wave 0: lane f < nF steps frame f (new state, its scaled copy, PRE_worldToCam
-    // = exp(scaled xi) * evalPT and its inverse) and writes it back; after one barrier lane (h, t) of the nF x nF
-    // pairs reads both frames' poses from LDS and forms the pair's FrameFramePrecalc::set while thread 64 (wave 1)
-    // writes the calib.  Each SE(3) exp / product runs once per frame (the stage-free form ran two per lane, on one
+    // register-resident stages: lane 64 + f (wave 1) steps frame f (new state, its scaled copy, PRE_worldToCam
+    // = exp(scaled xi) * evalPT and its inverse) into LDS; after one barrier lane (h, t) of wave 0 reads both
+    // frames' poses and forms the pair's FrameFramePrecalc::set while wave 1 writes the frames and the calib back.  Each SE(3) exp / product runs once per frame (the stage-free form ran two per lane, on one
     // wave's serial fp64 issue).  PRE_RTll_0 / PRE_tTll_0 depend on evalPT only and stay as uploaded.
     const int np = nF * nF;
     double* fx = B;  // LDLT scratch (free now): per frame PRE_worldToCam (7) | PRE_camToWorld (7) | scaled a, b
@@ -2185,9 +2184,15 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
 #pragma unroll
     for (int q = 0; q < 4; q++) cv[q] = st->calib.value[q] + 1.0f * st->calib.step[q];
     if ((a.dbg & 16) && a.trace && tid == 0) a.trace[20] = clock64();
-    if (tid < nF) {
-      hs::FrameH& F = st->frames[tid];
-      double sh[10], ns[10], sc[10], ev[7];
+    // stage 1 on wave 1 (lane 64 + f): frame f's new pose into LDS; its write-back waits until after the barrier,
+    // beside wave 0's pair stage
+    const int fw = tid - 64;
+    const bool fl = fw >= 0 && fw < nF;
+    double sh[10], ns[10], sc[10];
+    hs::SE3 PW, PC;
+    if (fl) {
+      const hs::FrameH& F = st->frames[fw];
+      double ev[7];
 #pragma unroll
       for (int q = 0; q < 10; q++) {
         sh[q] = F.state[q];
@@ -2195,27 +2200,13 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
       }
       F.evalPT.toData(ev);
       scale_state(ns, sc);
-      const hs::SE3 PW = se3_mul_step(se3_exp_step(sc), hs::SE3::fromData(ev));
-      const hs::SE3 PC = PW.inverse();
-      double* o = fx + 16 * tid;
+      PW = se3_mul_step(se3_exp_step(sc), hs::SE3::fromData(ev));
+      PC = PW.inverse();
+      double* o = fx + 16 * fw;
       PW.toData(o);
       PC.toData(o + 7);
       o[14] = sc[6];
       o[15] = sc[7];
-      // backupState, setState, setDeltaF's delta / delta_prior
-#pragma unroll
-      for (int q = 0; q < 10; q++) {
-        F.state_backup[q] = sh[q];
-        F.state[q] = ns[q];
-        F.state_scaled[q] = sc[q];
-      }
-      F.PRE_worldToCam = PW;
-      F.PRE_camToWorld = PC;
-#pragma unroll
-      for (int q = 0; q < 8; q++) {
-        F.delta[q] = ns[q] - F.state_zero[q];
-        F.delta_prior[q] = ns[q] - 0.0;
-      }
     }
     if ((a.dbg & 16) && a.trace && tid == 0) a.trace[22] = clock64();
     __syncthreads();
@@ -2258,6 +2249,22 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
       pc->aff[0] = (float)aff[0];
       pc->aff[1] = (float)aff[1];
       pc->b0 = (float)(H.state_zero[7] * hs::SCALE_B);  // aff0_b of the host
+    }
+    if (fl) {  // frame fw: backupState, setState, setDeltaF's delta / delta_prior
+      hs::FrameH& F = st->frames[fw];
+#pragma unroll
+      for (int q = 0; q < 10; q++) {
+        F.state_backup[q] = sh[q];
+        F.state[q] = ns[q];
+        F.state_scaled[q] = sc[q];
+      }
+      F.PRE_worldToCam = PW;
+      F.PRE_camToWorld = PC;
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        F.delta[q] = ns[q] - F.state_zero[q];
+        F.delta_prior[q] = ns[q] - 0.0;
+      }
     }
     if (tid == 64) {  // the calib (on wave 1, beside the pair stage: every lane read cv before the barrier)
       hs::CalibH& cal = st->calib;
