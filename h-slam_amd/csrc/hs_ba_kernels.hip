@@ -1150,13 +1150,22 @@ __global__ __launch_bounds__(256) void hs_k_reduce(HsRedArgs a) {
     // the host's block partials in block order, fp64 (the reference sums its per-thread fp32 accumulators in
     // fp64); up to 64 loads in flight per batch (one batch for <= 64 blocks per host)
     double s = 0.0;
-    for (int bb = b0; bb < b1; bb += 64) {
-      float v[64];
+    if (b1 - b0 <= 32) {  // the headline's 32 blocks per host: one 32-wide batch (no clamped duplicate loads)
+      float v[32];
 #pragma unroll
-      for (int u = 0; u < 64; u++) v[u] = a.part[(size_t)min(bb + u, b1 - 1) * NE64 + e];
+      for (int u = 0; u < 32; u++) v[u] = a.part[(size_t)min(b0 + u, b1 - 1) * NE64 + e];
 #pragma unroll
-      for (int u = 0; u < 64; u++)
-        if (bb + u < b1) s += (double)v[u];
+      for (int u = 0; u < 32; u++)
+        if (b0 + u < b1) s += (double)v[u];
+    } else {
+      for (int bb = b0; bb < b1; bb += 64) {
+        float v[64];
+#pragma unroll
+        for (int u = 0; u < 64; u++) v[u] = a.part[(size_t)min(bb + u, b1 - 1) * NE64 + e];
+#pragma unroll
+        for (int u = 0; u < 64; u++)
+          if (bb + u < b1) s += (double)v[u];
+      }
     }
     a.hostsum[(size_t)h * NE64 + e] = s;
   }
