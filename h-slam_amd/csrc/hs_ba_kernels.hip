@@ -744,7 +744,8 @@ __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
   if (work) {
     for (int p = pb + wv; p < pe; p += a.W) {  // wave-uniform
       LinIn nxt;
-      lin_load(a, min(p + a.W, pe - 1), lane, nxt);  // the next point's loads overlap this point's work
+      if (p + a.W < pe) lin_load(a, p + a.W, lane, nxt);  // the next point's loads overlap this point's work
+      else nxt = cur;  // last point of the wave (a wave-uniform branch): no duplicate loads
       LinPt P;
       lin_point<kFix>(a, p, h, lane, cur, K, ws, P);
       if (a.accumulate) acc_point<kExact>(A, P, h, lane, ws);
