@@ -1991,11 +1991,18 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
   const double sysE0 = a.sysE[0], sysE1 = a.sysE[1], sysE2 = a.sysE[2];  // energy, sum |idepth|, #points
   if (solve) {
     // HM (the marginalization prior) entries at the same places, bM for the b entries; one batch with the rest
-    const double* hmp = a.HM ? a.HM : a.sys;
+    if (a.HM) {
 #pragma unroll
-    for (int u = 0; u < NUQ; u++) {
-      gs[u] = a.sys[max(qaddr[u], 0)];
-      hmq[u] = qr[u] == -2 ? a.bM[qc[u]] : hmp[qr[u] >= 0 ? qaddr[u] : 0];
+      for (int u = 0; u < NUQ; u++) {
+        gs[u] = a.sys[max(qaddr[u], 0)];
+        hmq[u] = qr[u] == -2 ? a.bM[qc[u]] : a.HM[qr[u] >= 0 ? qaddr[u] : 0];
+      }
+    } else {  // no marginalization prior (a uniform branch): only bM is read beside the system
+#pragma unroll
+      for (int u = 0; u < NUQ; u++) {
+        gs[u] = a.sys[max(qaddr[u], 0)];
+        hmq[u] = qr[u] == -2 ? a.bM[qc[u]] : 0.0;
+      }
     }
 #pragma unroll
     for (int u = 0; u < NF_NU; u++) nfv[u] = a.Nproj[min(tid + u * SOLVE_NT, 2 * n * HS_NNS - 1)];
