@@ -6,10 +6,9 @@
 //   the system, fixed-order sums) -> [all-reduce of the system vector]
 // with no host synchronisation and no order-dependent atomics (bit-reproducible).  The host only prepares the window (adjoints, nullspace
 // projector, initial precalc — the reference's once-per-window Eigen/Sophus work) and reads
-// results back.  Compiled by hipcc as HIP together with hs_ba_kernels.hip; no torch, no Eigen.
-#include <hip/hip_runtime.h>
-#include <rccl/rccl.h>
-
+// results back.  Device memory is allocated to capacity once per context (hs_ba_reserve, or the first window that
+// needs more); the incremental keyframe API (hs_ba_window.cpp) edits the window in place.  Compiled by hipcc as HIP
+// together with hs_ba_kernels.hip; no torch, no Eigen.
 #include <algorithm>
 #include <chrono>
 #include <cstddef>
@@ -19,9 +18,7 @@
 #include <string>
 #include <vector>
 
-#include "../../include/hs_ba.h"
-#include "hs_host_math.h"
-#include "hs_kernels.h"
+#include "hs_ba_ctx.h"
 
 using namespace hs;
 
@@ -29,172 +26,55 @@ namespace hs {
 thread_local std::string g_err;  // hs_last_error(), shared by every entry point of the library
 }
 
-namespace {
-int fail(int code, const std::string& msg) {
-  g_err = msg;
-  return code;
-}
+namespace hs {
 
-constexpr int kLogCap = 4096;     // energies logged on the device per optimize / iterate call
-constexpr int kEventIters = 128;  // iterations timed with HIP events per call
-constexpr int kLinBlocksTarget = 256;  // linearize blocks of a window (points per wave grows beyond that)
-// hs_k_lin8 (lane = (point, target slot), 8 points per wave at a time) takes the production linearization from this
-// many points up: its wave issues ~2.3x fewer instructions per point (throughput), while hs_k_lin's one-point waves
-// finish a small window sooner (latency).  Env HS_LIN8=0 / 1 forces either.
-constexpr int kLin8MinPoints = 60000;
-constexpr int kLin8BlocksTarget = 512;  // hs_k_lin8 blocks of a window (two 4-wave blocks per CU)
-}  // namespace
-
-#define HS_HIP(x)                                                                                  \
-  do {                                                                                             \
-    hipError_t e_ = (x);                                                                           \
-    if (e_ != hipSuccess) return fail(HS_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
-  } while (0)
-
-#define HS_NCCL(x)                                                                                    \
-  do {                                                                                                \
-    ncclResult_t r_ = (x);                                                                            \
-    if (r_ != ncclSuccess) return fail(HS_ERR_RCCL, std::string(#x) + ": " + ncclGetErrorString(r_)); \
-  } while (0)
-
-#define HS_TRY(x)        \
-  do {                   \
-    int rc_ = (x);       \
-    if (rc_) return rc_; \
-  } while (0)
-
-template <typename T>
-static int dalloc(T** p, size_t n) {
-  if (n == 0) n = 1;
-  HS_HIP(hipMalloc((void**)p, n * sizeof(T)));
-  HS_HIP(hipMemset(*p, 0, n * sizeof(T)));
-  return HS_OK;
-}
-
-struct hs_ctx {
-  hs_params P;
-  int device = 0;
-  hipStream_t stream = nullptr;
-  std::vector<hipEvent_t> ev;  // 4 per timed iteration
-  int events = 0;              // HS_EVENT_TIMING: 0 none (default), 1 linearize kernel only, 2 every phase
-
-  // window (host side)
-  int nF = 0, nP = 0, nR = 0;
-  // hs_k_lin partitioning: blk_begin[h] = first block of host h; W waves per block take points; exact: one wave
-  // per host in point order (HS_ACC_EXACT=1, the single-thread reference's fp32 sums)
-  std::vector<int> blk_begin;
-  int nblk = 0, W = 4, ne = 0, Q = 0;
-  bool exact = false;
-  bool lin8 = false;              // production linearizations run hs_k_lin8 (4-wave blocks, W = 4)
-  // large windows: setNewFrameEnergyTH's select as a multi-block pass 2 (np2 extra blocks of the stitch launch) and a
-  // one-block pass 3 over pass 2's survivors, instead of the stitch's single select block scanning every candidate
-  // twice (env HS_TH_MULTI=0 / 1 forces it off / on)
-  bool th_multi = false;
-  bool sepValid = false;          // d_sep holds the separate HA / HSC of the last linearization
-  std::vector<int> pt_host, res_point, res_target, host_pt_begin;
-  std::vector<int> res_of_slot;   // [nP*8]
-  std::vector<int8_t> res_order;  // [nP*8]
-  std::vector<double> adHost, adTarget;
-  std::vector<float> adHostF, adTargetF;
-  std::vector<double> HM, bM, Porth, Nproj;
-  HsDevState* h_state = nullptr;  // pinned staging of the device state
-  int* h_ctl = nullptr;           // pinned: iteration, status, log_count
-  bool haveSystem = false;        // a stitched, not yet solved system is in the slots
-
-  // device
-  float4* d_img[HS_MAXF] = {nullptr};  // frame f's level-0 texels: d_img_all + f * img_px
-  float4* d_img_all = nullptr;
-  size_t img_px = 0;
-  HsDevState* d_state = nullptr;
-  HsPrecalc* d_pre = nullptr;
-  float* d_frameTH = nullptr;
-  float *d_u = nullptr, *d_v = nullptr, *d_idepth = nullptr, *d_idepth_zero = nullptr, *d_priorF = nullptr;
-  float *d_color = nullptr, *d_weight = nullptr;
-  int *d_res_of_slot = nullptr, *d_pt_host = nullptr, *d_host_pt_begin = nullptr;
-  int8_t* d_res_order = nullptr;
-  uint8_t *d_r_state = nullptr, *d_r_active = nullptr;
-  float *d_r_energy = nullptr, *d_r_newEnergy = nullptr, *d_r_ewo = nullptr, *d_r_center = nullptr;
-  uint8_t* d_p_actmask = nullptr;
-  float *d_p_HdiF = nullptr, *d_p_bdSumF = nullptr, *d_p_Hcd = nullptr, *d_p_JpJdF = nullptr;
-  float* d_p_step = nullptr;
-  // HdiF ping-pong: a linearization reads the previous one's HdiF (fused step) from d_p_HdiF and writes its own into
-  // d_p_HdiF_alt, then the two swap; hdif_solved = the buffer the last point step read (the last solve's SC prelude)
-  float* d_p_HdiF_alt = nullptr;
-  const float* hdif_solved = nullptr;
-  float* d_fix_relBL = nullptr;      // [nP] maxRelBaseline in / out of hs_ba_fix_linearization
-  int* d_fix_nGood = nullptr;        // [nP] numGoodResiduals in / out
-  float* d_part = nullptr;       // [nblk][ne][64] block partials of hs_k_lin
-  double* d_part_e = nullptr;    // [nblk][4] block energies
-  double* d_hostsum = nullptr;   // [nF][ne][64] per-host sums (hs_k_reduce)
-  double* d_sys = nullptr;       // [SL + 3] system vector (upper triangle of HA - sc HSC | bA - bSC) + energy,
-                                 // sum |idepth|, #points; all-reduced over the ranks
-  double* d_sep = nullptr;       // [2][SL] HA | bA, HSC | bSC (granular read-back)
-  double *d_adHost = nullptr, *d_adTarget = nullptr;
-  float *d_adHostF = nullptr, *d_adTargetF = nullptr;
-  double *d_HM = nullptr, *d_bM = nullptr, *d_Nproj = nullptr;
-  float* d_xAd = nullptr;
-  double* d_x = nullptr;
-  double* d_elog = nullptr;
-  unsigned int* d_th_hist = nullptr;  // [HS_TH_BINS] threshold select pass-1 histogram (zero between launches)
-  unsigned int *d_th_hist2 = nullptr, *d_th_surv = nullptr, *d_th_nsurv = nullptr;  // multi-block pass 2
-  float* d_cand = nullptr;  // [nranks][cand_stride] newest-frame energy per point (-1 / NaN = none)
-  int cand_stride = 0;
-  bool hm_zero = true;      // marginalization prior not set: the solve skips HM
-  uint8_t* d_marg = nullptr;     // [nP] marginalization flags (hs_ba_marginalize_points)
-  float* d_adHTdelta = nullptr;  // [nF*nF][8] EnergyFunctional::adHTdeltaF for fixLinearizationF
-  float cDelta[4] = {0, 0, 0, 0};
-  // kernel tracing (env HS_KTRACE=1): per-block wall-clock checkpoints of the last iteration
-  bool tracing = false;
-  long long *d_tr_lin = nullptr, *d_tr_acc = nullptr, *d_tr_solve = nullptr, *d_tr_st = nullptr;
-
-  // two GN iterations captured as one hipGraph (gn_iterations; env HS_GRAPH=1 enables it: measured 60.2 vs 58.8 us
-  // per step eager at the 2k headline, so eager launches stay the default): valid while the launch
-  // arguments are unchanged (dropped by free_window / hs_ba_set_marginal_prior) and the HdiF ping-pong is at the
-  // parity it was captured at
-  hipGraphExec_t gexec = nullptr;
-  const float* graph_hdif = nullptr;
-
-  // RCCL
-  ncclComm_t comm = nullptr;
-  int rank = 0, nranks = 1;
-
-  // timings of the last optimize / iterate
-  double t_lin = 0, t_acc = 0, t_solve = 0, t_timed = 0, t_wall = 0, t_iters = 0;
-
-  int dim() const { return 4 + 8 * nF; }
-  int SL() const { return dim() * dim() + dim(); }  // slot: n x n (upper triangle used) + b
-  double* sysE() const { return d_sys + SL(); }
-};
-
-static void drop_graph(hs_ctx* c) {
+void drop_graph(hs_ctx* c) {
   if (c->gexec) (void)hipGraphExecDestroy(c->gexec);
   c->gexec = nullptr;
   c->graph_hdif = nullptr;
 }
 
-static void free_window(hs_ctx* c) {
-  drop_graph(c);
-  for (int i = 0; i < HS_MAXF; i++) {
-    c->d_img[i] = nullptr;
+// upper bound of the linearize blocks of any window of at most capP points (make_partition below): every host's
+// points split into blocks of bw * ppw points, ppw chosen so the grid stays near the target; env HS_LIN_PPW forces a
+// ppw (more blocks), HS_ACC_EXACT one block per host
+int max_blocks_for(int capP) {
+  int m = std::max(kLinBlocksTarget, kLin8BlocksTarget) + HS_MAXF;
+  if (const char* e = std::getenv("HS_LIN_PPW")) {
+    const int ppw = std::max(1, std::atoi(e));
+    m = std::max(m, capP / (HS_LIN_NW * ppw) + 1 + HS_MAXF);
   }
-  void* ptrs[] = {c->d_img_all, c->d_state, c->d_pre, c->d_frameTH, c->d_u, c->d_v, c->d_idepth, c->d_idepth_zero,
-                  c->d_priorF, c->d_color, c->d_weight, c->d_res_of_slot, c->d_pt_host, c->d_host_pt_begin,
-                  c->d_res_order, c->d_r_state, c->d_r_active, c->d_r_energy, c->d_r_newEnergy, c->d_r_ewo,
-                  c->d_r_center, c->d_p_actmask, c->d_p_HdiF, c->d_p_bdSumF, c->d_p_Hcd, c->d_p_JpJdF,
-                  c->d_p_step, c->d_part, c->d_part_e, c->d_hostsum, c->d_sys, c->d_sep,
-                  c->d_adHost, c->d_adTarget, c->d_adHostF, c->d_adTargetF, c->d_HM, c->d_bM, c->d_Nproj, c->d_xAd,
-                  c->d_x, c->d_elog, c->d_cand, c->d_tr_lin, c->d_tr_acc, c->d_tr_solve, c->d_tr_st,
-                  c->d_marg, c->d_adHTdelta, c->d_p_HdiF_alt, c->d_fix_relBL, c->d_fix_nGood, c->d_th_hist,
-                  c->d_th_hist2, c->d_th_surv, c->d_th_nsurv};
+  return m;
+}
+
+static void free_buffers(hs_ctx* c) {
+  drop_graph(c);
+  std::vector<void*> ptrs = {
+      c->d_img_all, c->d_raw, c->d_state, c->d_pre, c->d_frameTH, c->d_res_of_slot, c->d_pt_host,
+      c->d_host_pt_begin, c->d_res_order, c->d_r_active, c->d_r_energy, c->d_r_newEnergy, c->d_r_ewo,
+      c->d_p_actmask, c->d_p_HdiF, c->d_p_bdSumF, c->d_p_Hcd, c->d_p_JpJdF, c->d_p_step, c->d_part, c->d_part_e,
+      c->d_hostsum, c->d_sys, c->d_sep, c->d_adHost, c->d_adTarget, c->d_adHostF, c->d_adTargetF, c->d_HM, c->d_bM,
+      c->d_Nproj, c->d_xAd, c->d_x, c->d_elog, c->d_cand, c->d_tr_lin, c->d_tr_acc, c->d_tr_solve, c->d_tr_st,
+      c->d_marg, c->d_adHTdelta, c->d_p_HdiF_alt, c->d_th_hist, c->d_th_hist2, c->d_th_surv, c->d_th_nsurv,
+      c->d_le_chunk, c->d_le_out, c->d_ref_pts, c->d_ref_n, c->d_stage};
+  for (auto& s : c->ps) {
+    for (void* p : {(void*)s.u, (void*)s.v, (void*)s.idepth, (void*)s.idepth_zero, (void*)s.priorF, (void*)s.color,
+                    (void*)s.weight, (void*)s.relBL, (void*)s.nGood, (void*)s.r_state, (void*)s.r_center})
+      ptrs.push_back(p);
+    s = PointSet();
+  }
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  if (c->h_stage) (void)hipHostFree(c->h_stage);
+  if (c->h_raw) (void)hipHostFree(c->h_raw);
+  c->h_stage = nullptr;
+  c->h_stage_cap = 0;
+  c->h_raw = nullptr;
+  c->d_img_all = nullptr; c->d_raw = nullptr;
   c->d_state = nullptr; c->d_pre = nullptr; c->d_frameTH = nullptr;
-  c->d_u = c->d_v = c->d_idepth = c->d_idepth_zero = c->d_priorF = nullptr;
-  c->d_color = c->d_weight = nullptr;
   c->d_res_of_slot = c->d_pt_host = c->d_host_pt_begin = nullptr;
   c->d_res_order = nullptr;
-  c->d_r_state = c->d_r_active = nullptr;
-  c->d_r_energy = c->d_r_newEnergy = c->d_r_ewo = c->d_r_center = nullptr;
+  c->d_r_active = nullptr;
+  c->d_r_energy = c->d_r_newEnergy = c->d_r_ewo = nullptr;
   c->d_p_actmask = nullptr;
   c->d_p_HdiF = c->d_p_bdSumF = c->d_p_Hcd = c->d_p_JpJdF = c->d_p_step = nullptr;
   c->d_part = nullptr; c->d_part_e = nullptr; c->d_hostsum = nullptr; c->d_sys = nullptr; c->d_sep = nullptr;
@@ -202,21 +82,126 @@ static void free_window(hs_ctx* c) {
   c->d_HM = c->d_bM = c->d_Nproj = nullptr;
   c->d_xAd = nullptr; c->d_x = nullptr; c->d_elog = nullptr; c->d_cand = nullptr;
   c->d_tr_lin = c->d_tr_acc = c->d_tr_solve = c->d_tr_st = nullptr;
-  c->d_img_all = nullptr;
   c->d_marg = nullptr;
   c->d_adHTdelta = nullptr;
-  c->d_p_HdiF_alt = c->d_fix_relBL = nullptr;
+  c->d_p_HdiF_alt = nullptr;
   c->hdif_solved = nullptr;
   c->d_th_hist = nullptr;
   c->d_th_hist2 = c->d_th_surv = c->d_th_nsurv = nullptr;
-  c->d_fix_nGood = nullptr;
+  c->d_le_chunk = nullptr; c->d_le_out = nullptr;
+  c->d_ref_pts = nullptr; c->d_ref_n = nullptr;
+  c->d_stage = nullptr;
+  c->d_stage_cap = 0;
+  c->cap_P = c->cap_blk = c->cap_W = c->cap_H = c->cap_stride = 0;
+  bind_point_set(c);
   c->nF = c->nP = c->nR = 0;
   c->haveSystem = false;
   c->sepValid = false;
 }
 
+void bind_point_set(hs_ctx* c) {
+  const PointSet& s = c->ps[c->cur];
+  c->d_u = s.u; c->d_v = s.v; c->d_idepth = s.idepth; c->d_idepth_zero = s.idepth_zero; c->d_priorF = s.priorF;
+  c->d_color = s.color; c->d_weight = s.weight;
+  c->d_fix_relBL = s.relBL; c->d_fix_nGood = s.nGood;
+  c->d_r_state = s.r_state; c->d_r_center = s.r_center;
+}
+
+// candidate-buffer stride: the same on every rank (max point count over the ranks; one small all-reduce)
+int cand_stride_for(hs_ctx* c, int nP, int* stride) {
+  int s = nP > 0 ? nP : 1;
+  if (c->comm) {
+    int* d_tmp = nullptr;
+    HS_TRY(dalloc(&d_tmp, 1));
+    HS_HIP(hipMemcpy(d_tmp, &s, sizeof(int), hipMemcpyHostToDevice));
+    HS_NCCL(ncclAllReduce(d_tmp, d_tmp, 1, ncclInt, ncclMax, c->comm, c->stream));
+    HS_HIP(hipStreamSynchronize(c->stream));
+    HS_HIP(hipMemcpy(&s, d_tmp, sizeof(int), hipMemcpyDeviceToHost));
+    (void)hipFree(d_tmp);
+  }
+  *stride = s;
+  return HS_OK;
+}
+
+// Every device buffer of a window of up to HS_MAXF frames of W x H and capP points, allocated (zeroed) once.  A
+// context keeps its allocation while later windows fit; a window that needs more reallocates (hs_ba_set_window
+// only: the incremental API fails instead, hs_ba_reserve sizes it).
+int ensure_capacity(hs_ctx* c, int W, int H, int capP, int capBlk) {
+  capP = std::max(capP, 1);
+  capBlk = std::max(capBlk, 1);
+  if (c->d_state && W == c->cap_W && H == c->cap_H && capP <= c->cap_P && capBlk <= c->cap_blk) return HS_OK;
+  HS_HIP(hipStreamSynchronize(c->stream));
+  free_buffers(c);
+  const size_t npx = (size_t)W * H, P8 = (size_t)capP * 8;
+  const int nmax = HS_MAXDIM, SLmax = nmax * nmax + nmax, ne = hs_ne(true), FF = HS_MAXF * HS_MAXF;
+  HS_TRY(dalloc(&c->d_img_all, npx * HS_MAXF));
+  c->img_px = npx;
+  HS_TRY(dalloc(&c->d_state, 1));
+  HS_TRY(dalloc(&c->d_pre, FF));
+  HS_TRY(dalloc(&c->d_frameTH, HS_MAXF));
+  for (auto& s : c->ps) {
+    HS_TRY(dalloc(&s.u, capP)); HS_TRY(dalloc(&s.v, capP));
+    HS_TRY(dalloc(&s.idepth, capP)); HS_TRY(dalloc(&s.idepth_zero, capP)); HS_TRY(dalloc(&s.priorF, capP));
+    HS_TRY(dalloc(&s.color, P8)); HS_TRY(dalloc(&s.weight, P8));
+    HS_TRY(dalloc(&s.relBL, capP)); HS_TRY(dalloc(&s.nGood, capP));
+    HS_TRY(dalloc(&s.r_state, P8)); HS_TRY(dalloc(&s.r_center, P8 * 3));
+  }
+  c->cur = 0;
+  HS_TRY(dalloc(&c->d_res_of_slot, P8)); HS_TRY(dalloc(&c->d_res_order, P8));
+  HS_TRY(dalloc(&c->d_pt_host, capP)); HS_TRY(dalloc(&c->d_host_pt_begin, HS_MAXF + 1));
+  // residual state in the slot layout [point][target slot] (P8 entries; slots without a residual unused)
+  HS_TRY(dalloc(&c->d_r_active, P8));
+  HS_TRY(dalloc(&c->d_r_energy, P8)); HS_TRY(dalloc(&c->d_r_newEnergy, P8)); HS_TRY(dalloc(&c->d_r_ewo, P8));
+  HS_TRY(dalloc(&c->d_p_actmask, capP)); HS_TRY(dalloc(&c->d_p_HdiF, capP)); HS_TRY(dalloc(&c->d_p_bdSumF, capP));
+  HS_TRY(dalloc(&c->d_p_Hcd, (size_t)capP * 4)); HS_TRY(dalloc(&c->d_p_JpJdF, P8 * 8));
+  HS_TRY(dalloc(&c->d_p_step, capP)); HS_TRY(dalloc(&c->d_p_HdiF_alt, capP));
+  c->hdif_solved = c->d_p_HdiF;
+  HS_TRY(dalloc(&c->d_part, (size_t)capBlk * ne * 64));
+  HS_TRY(dalloc(&c->d_part_e, (size_t)capBlk * 4));
+  HS_TRY(dalloc(&c->d_hostsum, (size_t)HS_MAXF * ne * 64));
+  HS_TRY(dalloc(&c->d_sys, (size_t)SLmax + 3));
+  HS_TRY(dalloc(&c->d_sep, (size_t)2 * SLmax));
+  HS_TRY(dalloc(&c->d_adHost, FF * 64)); HS_TRY(dalloc(&c->d_adTarget, FF * 64));
+  HS_TRY(dalloc(&c->d_adHostF, FF * 64)); HS_TRY(dalloc(&c->d_adTargetF, FF * 64));
+  HS_TRY(dalloc(&c->d_HM, (size_t)nmax * nmax)); HS_TRY(dalloc(&c->d_bM, nmax));
+  HS_TRY(dalloc(&c->d_Nproj, (size_t)2 * nmax * HS_NNS));
+  HS_TRY(dalloc(&c->d_xAd, FF * 8)); HS_TRY(dalloc(&c->d_x, nmax)); HS_TRY(dalloc(&c->d_elog, kLogCap));
+  int stride = capP;
+  HS_TRY(cand_stride_for(c, capP, &stride));
+  c->cap_stride = stride;
+  HS_TRY(dalloc(&c->d_cand, (size_t)stride * c->nranks));
+  HS_HIP(hipMemset(c->d_cand, 0xff, sizeof(float) * (size_t)stride * c->nranks));  // NaN, sign set: no candidate
+  HS_TRY(dalloc(&c->d_th_hist, HS_TH_BINS));
+  HS_TRY(dalloc(&c->d_th_hist2, 1024));
+  HS_TRY(dalloc(&c->d_th_nsurv, 1));
+  HS_TRY(dalloc(&c->d_th_surv, HS_TH_SURV));
+  HS_TRY(dalloc(&c->d_marg, capP));
+  HS_TRY(dalloc(&c->d_adHTdelta, FF * 8));
+  HS_TRY(dalloc(&c->d_le_chunk, (size_t)(capP + 49) / 50));
+  HS_TRY(dalloc(&c->d_le_out, 1));
+  HS_TRY(dalloc(&c->d_ref_pts, (size_t)4 * capP));
+  HS_TRY(dalloc(&c->d_ref_n, 1));
+  // incremental window: the commit blob (pinned + device) and a raw level-0 image's staging
+  c->h_stage_cap = c->d_stage_cap = stage_bytes(capP);
+  HS_HIP(hipHostMalloc((void**)&c->h_stage, c->h_stage_cap));
+  HS_TRY(dalloc(&c->d_stage, c->d_stage_cap));
+  HS_HIP(hipHostMalloc((void**)&c->h_raw, sizeof(float) * npx));
+  HS_TRY(dalloc(&c->d_raw, npx));
+  const char* tr = std::getenv("HS_KTRACE");
+  c->tracing = tr && tr[0] == '1';
+  if (c->tracing) {
+    HS_TRY(dalloc(&c->d_tr_lin, (size_t)capBlk * 16));
+    HS_TRY(dalloc(&c->d_tr_acc, (size_t)(HS_MAXF * ((ne * 64 + 255) / 256) + 1 + 64) * 16));
+    HS_TRY(dalloc(&c->d_tr_st, (size_t)(HS_MAXF * (HS_MAXF + 1) / 2 + HS_MAXF + 2) * 16));
+    HS_TRY(dalloc(&c->d_tr_solve, 32));
+  }
+  c->cap_W = W; c->cap_H = H; c->cap_P = capP; c->cap_blk = capBlk;
+  bind_point_set(c);
+  return HS_OK;
+}
+
 // ---------------------------------------------------------------- window preparation (host, once per window)
-static void compute_projector(hs_ctx* c) {
+void compute_projector(hs_ctx* c) {
   // System::getNullspaces (pose 6 + scale 1; affine nullspaces are not used by orthogonalize)
   const int n = c->dim();
   const std::vector<FrameH> frames(c->h_state->frames, c->h_state->frames + c->nF);
@@ -240,11 +225,105 @@ static void compute_projector(hs_ctx* c) {
   nullspace_projector(ns, n, c->P.solverModeDelta, c->Porth, &c->Nproj);
 }
 
-static int fetch_state(hs_ctx* c) {
+int fetch_state(hs_ctx* c) {
   HS_HIP(hipMemcpyAsync(c->h_state, c->d_state, sizeof(HsDevState), hipMemcpyDeviceToHost, c->stream));
   HS_HIP(hipStreamSynchronize(c->stream));
+  c->h_state_valid = true;
   return HS_OK;
 }
+
+size_t fstage_bytes() {
+  const int FF = HS_MAXF * HS_MAXF;
+  return FF * sizeof(HsPrecalc) + (size_t)FF * 64 * (2 * sizeof(double) + 2 * sizeof(float)) +
+         (size_t)2 * HS_MAXDIM * HS_NNS * sizeof(double);
+}
+
+int wait_uploads(hs_ctx* c) {
+  HS_HIP(hipEventSynchronize(c->ev_upload));
+  return HS_OK;
+}
+
+// EnergyFunctional::setAdjointsF + System::setPrecalcValues + getNullspaces of the frames in c->h_state (fp64 host
+// algebra, the reference's own place for it), then the state, precalc, adjoints and projector to the device:
+// asynchronous copies from the pinned h_state / h_fstage (the event ev_upload marks their completion; the host waits
+// on it before it rewrites either).
+int upload_frames(hs_ctx* c) {
+  const int nF = c->nF, n = c->dim(), FF = nF * nF;
+  HS_TRY(wait_uploads(c));
+  HsDevState& S = *c->h_state;
+  S.nF = nF;
+  c->adHost.assign(FF * 64, 0.0);
+  c->adTarget.assign(FF * 64, 0.0);
+  c->adHostF.assign(FF * 64, 0.f);
+  c->adTargetF.assign(FF * 64, 0.f);
+  for (int h = 0; h < nF; h++)
+    for (int t = 0; t < nF; t++) {
+      const int idx = h + t * nF;
+      make_adjoints(S.frames[h], S.frames[t], &c->adHost[idx * 64], &c->adTarget[idx * 64]);
+      for (int i = 0; i < 64; i++) {
+        c->adHostF[idx * 64 + i] = (float)c->adHost[idx * 64 + i];
+        c->adTargetF[idx * 64 + i] = (float)c->adTarget[idx * 64 + i];
+      }
+    }
+  compute_projector(c);
+  uint8_t* p = c->h_fstage;
+  HsPrecalc* pre = (HsPrecalc*)p;
+  for (int h = 0; h < nF; h++)
+    for (int t = 0; t < nF; t++) pre[h * nF + t] = make_precalc(S.frames[h], S.frames[t], S.calib);
+  p += HS_MAXF * HS_MAXF * sizeof(HsPrecalc);
+  auto put = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
+    std::memcpy(p, src, bytes);
+    hipError_t e = hipMemcpyAsync(dst, p, bytes, hipMemcpyHostToDevice, c->stream);
+    p += (bytes + 15) & ~(size_t)15;
+    return e;
+  };
+  HS_HIP(hipMemcpyAsync(c->d_state, c->h_state, sizeof(HsDevState), hipMemcpyHostToDevice, c->stream));
+  HS_HIP(hipMemcpyAsync(c->d_pre, pre, sizeof(HsPrecalc) * FF, hipMemcpyHostToDevice, c->stream));
+  HS_HIP(put(c->d_adHost, c->adHost.data(), sizeof(double) * FF * 64));
+  HS_HIP(put(c->d_adTarget, c->adTarget.data(), sizeof(double) * FF * 64));
+  HS_HIP(put(c->d_adHostF, c->adHostF.data(), sizeof(float) * FF * 64));
+  HS_HIP(put(c->d_adTargetF, c->adTargetF.data(), sizeof(float) * FF * 64));
+  HS_HIP(put(c->d_Nproj, c->Nproj.data(), sizeof(double) * 2 * n * HS_NNS));
+  HS_HIP(hipEventRecord(c->ev_upload, c->stream));
+  c->h_state_valid = true;
+  return HS_OK;
+}
+
+// hs_k_lin partitioning of the committed window (host_pt_begin).  Production: every host's points are split into
+// blocks of HS_LIN_NW waves x ppw points (ppw grows with the window so the grid stays near kLinBlocksTarget blocks;
+// env HS_LIN_PPW overrides).  HS_ACC_EXACT=1: one block per host whose wave 0 takes every point in order = the
+// single-thread reference's fp32 accumulator sums (no shiftUp emulation: at most 1000 points per host).
+int make_partition(hs_ctx* c) {
+  const int nF = c->nF, nP = c->nP;
+  const char* ex = std::getenv("HS_ACC_EXACT");
+  c->exact = ex && ex[0] == '1';
+  c->ne = hs_ne(c->exact);
+  c->Q = (c->ne * 64 + 255) / 256;
+  c->blk_begin.assign(nF + 1, 0);
+  c->lin8 = !c->exact && nP >= kLin8MinPoints;
+  if (const char* e = std::getenv("HS_LIN8")) c->lin8 = !c->exact && e[0] == '1';
+  // the extra launch of pass 3 costs more than a one-block scan of a small window's candidates
+  c->th_multi = nP >= kLin8MinPoints;
+  if (const char* e = std::getenv("HS_TH_MULTI")) c->th_multi = e[0] == '1';
+  // points per block: hs_k_lin HS_LIN_NW waves x ppw points; hs_k_lin8 4 waves x ppw groups of 8 points (its
+  // partition also serves hs_k_lin's marginalization / linearizeAll(true) passes, with W = 4 of its waves)
+  const int bw = c->lin8 ? (HS_LIN8_NT / 64) * 8 : HS_LIN_NW;
+  const int target = c->lin8 ? kLin8BlocksTarget : kLinBlocksTarget;
+  int ppw = std::max(1, (nP + bw * target - 1) / (bw * target));
+  if (const char* e = std::getenv("HS_LIN_PPW")) ppw = std::max(1, std::atoi(e));
+  c->W = c->exact ? 1 : (c->lin8 ? HS_LIN8_NT / 64 : HS_LIN_NW);
+  for (int h = 0; h < nF; h++) {
+    const int nh = c->host_pt_begin[h + 1] - c->host_pt_begin[h];
+    if (c->exact && nh > 1000) return fail(HS_ERR_INVALID, "HS_ACC_EXACT supports at most 1000 points per host");
+    const int nb = nh == 0 ? 0 : (c->exact ? 1 : (nh + bw * ppw - 1) / (bw * ppw));
+    c->blk_begin[h + 1] = c->blk_begin[h] + nb;
+  }
+  c->nblk = c->blk_begin[nF];
+  if (c->nblk > c->cap_blk) return fail(HS_ERR_NOMEM, "linearize partition exceeds the block capacity");
+  return HS_OK;
+}
+
+}  // namespace hs
 
 // ---------------------------------------------------------------- launches (asynchronous)
 static size_t lin_lds(const hs_ctx* c) {
@@ -252,6 +331,10 @@ static size_t lin_lds(const hs_ctx* c) {
 }
 
 static int launch_linearize(hs_ctx* c, int fuse, bool marg = false, bool accumulate = true, bool fix = false) {
+  // a pass without the fused point step reads no HdiF: it writes into the buffer that does not hold the last solve's
+  // (efPoint->HdiF stays that of the last accumulateSCF_MT until the next solve: the tail's linearizeAll(true) and a
+  // marginalization pass do not change it, and makeCoarseDepthL0 reads it afterwards)
+  if (!fuse && c->d_p_HdiF_alt == c->hdif_solved) std::swap(c->d_p_HdiF, c->d_p_HdiF_alt);
   HsLinArgs a;
   std::memset(&a, 0, sizeof(a));
   if (marg) {  // hs_ba_marginalize_points: flags, adHTdeltaF and cDeltaF uploaded by the caller
@@ -262,6 +345,7 @@ static int launch_linearize(hs_ctx* c, int fuse, bool marg = false, bool accumul
   }
   a.img = c->d_img_all;
   a.img_stride = (long long)c->img_px;
+  for (int f = 0; f < HS_MAXF; f++) a.img_slot[f] = c->img_slot[f];
   a.st = c->d_state;
   a.lp.huberTH = c->P.huberTH;
   a.lp.outlierTHSumComponent = c->P.outlierTHSumComponent;
@@ -305,6 +389,7 @@ static int launch_linearize(hs_ctx* c, int fuse, bool marg = false, bool accumul
     }
   }
   HS_HIP(hipGetLastError());
+  c->tail_valid = fix;  // d_r_active = linearizeAll(true)'s activity: the toRemove list
   std::swap(c->d_p_HdiF, c->d_p_HdiF_alt);
   if (fuse) c->hdif_solved = c->d_p_HdiF_alt;
   if (accumulate) c->sepValid = false;
@@ -389,6 +474,7 @@ static int launch_solve(hs_ctx* c, int flags, int iteration, bool log) {
   if (const char* e = std::getenv("HS_SOLVE_DBG")) a.dbg = std::atoi(e);
   hipLaunchKernelGGL(hs_k_solve, dim3(1), dim3(HS_SOLVE_NT), 0, c->stream, a);
   HS_HIP(hipGetLastError());
+  c->h_state_valid = false;
   return HS_OK;
 }
 
@@ -562,6 +648,15 @@ static int gn_iterations(hs_ctx* c, int it0, int K, bool allow_break, double* en
   return HS_OK;
 }
 
+// every entry point that needs the device window: pending incremental edits are committed first
+static int begin_call(hs_ctx* c) {
+  if (!c) return fail(HS_ERR_INVALID, "null context");
+  HS_HIP(hipSetDevice(c->device));
+  HS_TRY(commit_if_dirty(c));
+  if (c->nF == 0) return fail(HS_ERR_STATE, "no window");
+  return HS_OK;
+}
+
 // ================================================================ C-ABI
 extern "C" {
 
@@ -624,7 +719,10 @@ int hs_create(hs_ctx** out, const hs_params* params, int device_id) {
   c->events = ev ? std::atoi(ev) : 0;
   if (hipSetDevice(device_id) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc((void**)&c->h_state, sizeof(HsDevState)) != hipSuccess ||
-      hipHostMalloc((void**)&c->h_ctl, 8 * sizeof(int)) != hipSuccess) {
+      hipHostMalloc((void**)&c->h_ctl, 8 * sizeof(int)) != hipSuccess ||
+      hipHostMalloc((void**)&c->h_fstage, fstage_bytes() + 256) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_upload, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_ready, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return fail(HS_ERR_HIP, "stream / pinned allocation failed");
   }
@@ -638,14 +736,44 @@ void hs_destroy(hs_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  free_window(c);
+  free_buffers(c);
   if (c->comm) ncclCommDestroy(c->comm);
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   if (c->h_state) (void)hipHostFree(c->h_state);
   if (c->h_ctl) (void)hipHostFree(c->h_ctl);
+  if (c->h_fstage) (void)hipHostFree(c->h_fstage);
+  if (c->ev_upload) (void)hipEventDestroy(c->ev_upload);
+  if (c->ev_ready) (void)hipEventDestroy(c->ev_ready);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
+}
+
+// every per-window device buffer back to the state of a fresh allocation (zero; candidates NaN) over the first nP
+// points, so a reused context runs a new window exactly as a fresh one would
+static int zero_window(hs_ctx* c, int nP) {
+  hipStream_t s = c->stream;
+  const size_t P = (size_t)std::max(nP, 1), P8 = P * 8;
+  const int nmax = HS_MAXDIM, SLmax = nmax * nmax + nmax, ne = hs_ne(true), FF = HS_MAXF * HS_MAXF;
+  auto z = [&](void* p, size_t bytes) { return hipMemsetAsync(p, 0, bytes, s); };
+  for (auto& q : c->ps) {
+    HS_HIP(z(q.u, P * 4)); HS_HIP(z(q.v, P * 4)); HS_HIP(z(q.idepth, P * 4)); HS_HIP(z(q.idepth_zero, P * 4));
+    HS_HIP(z(q.priorF, P * 4)); HS_HIP(z(q.color, P8 * 4)); HS_HIP(z(q.weight, P8 * 4));
+    HS_HIP(z(q.relBL, P * 4)); HS_HIP(z(q.nGood, P * 4)); HS_HIP(z(q.r_state, P8)); HS_HIP(z(q.r_center, P8 * 12));
+  }
+  HS_HIP(z(c->d_res_of_slot, P8 * 4)); HS_HIP(z(c->d_res_order, P8)); HS_HIP(z(c->d_pt_host, P * 4));
+  HS_HIP(z(c->d_r_active, P8)); HS_HIP(z(c->d_r_energy, P8 * 4)); HS_HIP(z(c->d_r_newEnergy, P8 * 4));
+  HS_HIP(z(c->d_r_ewo, P8 * 4)); HS_HIP(z(c->d_p_actmask, P)); HS_HIP(z(c->d_p_HdiF, P * 4));
+  HS_HIP(z(c->d_p_HdiF_alt, P * 4)); HS_HIP(z(c->d_p_bdSumF, P * 4)); HS_HIP(z(c->d_p_Hcd, P * 16));
+  HS_HIP(z(c->d_p_JpJdF, P8 * 32)); HS_HIP(z(c->d_p_step, P * 4)); HS_HIP(z(c->d_marg, P));
+  HS_HIP(z(c->d_part, (size_t)c->cap_blk * ne * 64 * 4)); HS_HIP(z(c->d_part_e, (size_t)c->cap_blk * 32));
+  HS_HIP(z(c->d_hostsum, (size_t)HS_MAXF * ne * 64 * 8)); HS_HIP(z(c->d_sys, ((size_t)SLmax + 3) * 8));
+  HS_HIP(z(c->d_sep, (size_t)2 * SLmax * 8)); HS_HIP(z(c->d_HM, (size_t)nmax * nmax * 8)); HS_HIP(z(c->d_bM, nmax * 8));
+  HS_HIP(z(c->d_xAd, FF * 32)); HS_HIP(z(c->d_x, nmax * 8)); HS_HIP(z(c->d_elog, kLogCap * 8));
+  HS_HIP(z(c->d_adHTdelta, FF * 32)); HS_HIP(z(c->d_frameTH, HS_MAXF * 4));
+  HS_HIP(hipMemsetAsync(c->d_cand, 0xff, sizeof(float) * (size_t)c->cap_stride * c->nranks, s));
+  c->hdif_solved = c->d_p_HdiF;
+  return HS_OK;
 }
 
 int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr, const float* const* images,
@@ -656,7 +784,7 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
   if (pts->n < 0 || rs->n < 0) return fail(HS_ERR_INVALID, "negative counts");
   HS_HIP(hipSetDevice(c->device));
   HS_HIP(hipStreamSynchronize(c->stream));
-  free_window(c);
+  drop_graph(c);
   const int nP = pts->n, nR = rs->n;
   // ---- validate and index the residual graph (host)
   std::vector<int> pt_host(pts->host, pts->host + nP);
@@ -681,6 +809,18 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
     res_target[r] = t;
     nres[p]++;
   }
+  // ---- capacity: reused while the window fits (no per-window allocation)
+  int stride = nP;
+  HS_TRY(cand_stride_for(c, nP, &stride));
+  const int needP = std::max(nP, stride);
+  HS_TRY(ensure_capacity(c, cam->width, cam->height, needP, max_blocks_for(needP)));
+  c->cam = *cam;
+  c->haveCam = true;
+  c->incremental = false;
+  c->dirty = false;
+  c->wframes.clear();
+  c->wpts.clear();
+  c->staged.clear();
   c->nF = nF;
   c->nP = nP;
   c->nR = nR;
@@ -698,34 +838,10 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
     }
     c->host_pt_begin[nF] = nP;
   }
-  // hs_k_lin partitioning.  Production: every host's points are split into blocks of HS_LIN_NW waves x ppw points
-  // (ppw grows with the window so the grid stays near kLinBlocksTarget blocks; env HS_LIN_PPW overrides).
-  // HS_ACC_EXACT=1: one block per host whose wave 0 takes every point in order = the single-thread reference's
-  // fp32 accumulator sums (no shiftUp emulation: at most 1000 points per host).
-  const char* ex = std::getenv("HS_ACC_EXACT");
-  c->exact = ex && ex[0] == '1';
-  c->ne = hs_ne(c->exact);
-  c->Q = (c->ne * 64 + 255) / 256;
-  c->blk_begin.assign(nF + 1, 0);
-  c->lin8 = !c->exact && nP >= kLin8MinPoints;
-  if (const char* e = std::getenv("HS_LIN8")) c->lin8 = !c->exact && e[0] == '1';
-  // the extra launch of pass 3 costs more than a one-block scan of a small window's candidates
-  c->th_multi = nP >= kLin8MinPoints;
-  if (const char* e = std::getenv("HS_TH_MULTI")) c->th_multi = e[0] == '1';
-  // points per block: hs_k_lin HS_LIN_NW waves x ppw points; hs_k_lin8 4 waves x ppw groups of 8 points (its
-  // partition also serves hs_k_lin's marginalization / linearizeAll(true) passes, with W = 4 of its waves)
-  const int bw = c->lin8 ? (HS_LIN8_NT / 64) * 8 : HS_LIN_NW;
-  const int target = c->lin8 ? kLin8BlocksTarget : kLinBlocksTarget;
-  int ppw = std::max(1, (nP + bw * target - 1) / (bw * target));
-  if (const char* e = std::getenv("HS_LIN_PPW")) ppw = std::max(1, std::atoi(e));
-  c->W = c->exact ? 1 : (c->lin8 ? HS_LIN8_NT / 64 : HS_LIN_NW);
-  for (int h = 0; h < nF; h++) {
-    const int nh = c->host_pt_begin[h + 1] - c->host_pt_begin[h];
-    if (c->exact && nh > 1000) return fail(HS_ERR_INVALID, "HS_ACC_EXACT supports at most 1000 points per host");
-    const int nb = nh == 0 ? 0 : (c->exact ? 1 : (nh + bw * ppw - 1) / (bw * ppw));
-    c->blk_begin[h + 1] = c->blk_begin[h] + nb;
-  }
-  c->nblk = c->blk_begin[nF];
+  c->cand_stride = stride;
+  HS_TRY(make_partition(c));
+  for (int f = 0; f < HS_MAXF; f++) c->img_slot[f] = f;
+  HS_TRY(zero_window(c, nP));
 
   // ---- window state: calib (CalibData ctor: setValueScaled, value_zero = value) and frames
   HsDevState& S = *c->h_state;
@@ -755,101 +871,28 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
   }
   S.dcal = cal.device();
   S.nF = nF;
-  // adjoints (constant while evalPT is fixed)
-  c->adHost.assign(nF * nF * 64, 0.0);
-  c->adTarget.assign(nF * nF * 64, 0.0);
-  c->adHostF.assign(nF * nF * 64, 0.f);
-  c->adTargetF.assign(nF * nF * 64, 0.f);
-  for (int h = 0; h < nF; h++)
-    for (int t = 0; t < nF; t++) {
-      const int idx = h + t * nF;
-      make_adjoints(S.frames[h], S.frames[t], &c->adHost[idx * 64], &c->adTarget[idx * 64]);
-      for (int i = 0; i < 64; i++) {
-        c->adHostF[idx * 64 + i] = (float)c->adHost[idx * 64 + i];
-        c->adTargetF[idx * 64 + i] = (float)c->adTarget[idx * 64 + i];
-      }
-    }
   const int n = c->dim();
   c->HM.assign((size_t)n * n, 0.0);
   c->bM.assign(n, 0.0);
   c->hm_zero = true;
-  compute_projector(c);
-  std::vector<HsPrecalc> pre(nF * nF);
-  for (int h = 0; h < nF; h++)
-    for (int t = 0; t < nF; t++) pre[h * nF + t] = make_precalc(S.frames[h], S.frames[t], cal);
+  HS_TRY(upload_frames(c));
 
-  // ---- candidate buffer stride: the same on every rank (max point count)
-  c->cand_stride = nP > 0 ? nP : 1;
-  if (c->comm) {
-    int* d_tmp = nullptr;
-    HS_TRY(dalloc(&d_tmp, 1));
-    HS_HIP(hipMemcpy(d_tmp, &c->cand_stride, sizeof(int), hipMemcpyHostToDevice));
-    HS_NCCL(ncclAllReduce(d_tmp, d_tmp, 1, ncclInt, ncclMax, c->comm, c->stream));
-    HS_HIP(hipStreamSynchronize(c->stream));
-    HS_HIP(hipMemcpy(&c->cand_stride, d_tmp, sizeof(int), hipMemcpyDeviceToHost));
-    (void)hipFree(d_tmp);
-  }
-
-  // ---- device allocations + uploads
+  // ---- uploads (the legacy whole-window path: pageable host arrays, synchronous)
   const size_t npx = (size_t)cam->width * cam->height;
   std::vector<float4> tex(npx);
-  HS_TRY(dalloc(&c->d_img_all, npx * nF));  // one allocation: the kernel indexes frames by stride
-  c->img_px = npx;
   for (int f = 0; f < nF; f++) {
-    c->d_img[f] = c->d_img_all + f * npx;
     const float* src = images[f];
     for (size_t i = 0; i < npx; i++) tex[i] = make_float4(src[3 * i], src[3 * i + 1], src[3 * i + 2], 0.f);
-    HS_HIP(hipMemcpy(c->d_img[f], tex.data(), npx * sizeof(float4), hipMemcpyHostToDevice));
+    HS_HIP(hipMemcpyAsync(c->d_img_all + (size_t)f * npx, tex.data(), npx * sizeof(float4), hipMemcpyHostToDevice,
+                          c->stream));
+    HS_HIP(hipStreamSynchronize(c->stream));  // tex is reused
   }
   const size_t P8 = (size_t)nP * 8;
-  HS_TRY(dalloc(&c->d_state, 1));
-  HS_TRY(dalloc(&c->d_pre, nF * nF));
-  HS_TRY(dalloc(&c->d_frameTH, nF));
-  HS_TRY(dalloc(&c->d_u, nP)); HS_TRY(dalloc(&c->d_v, nP));
-  HS_TRY(dalloc(&c->d_idepth, nP)); HS_TRY(dalloc(&c->d_idepth_zero, nP)); HS_TRY(dalloc(&c->d_priorF, nP));
-  HS_TRY(dalloc(&c->d_color, P8)); HS_TRY(dalloc(&c->d_weight, P8));
-  HS_TRY(dalloc(&c->d_res_of_slot, P8)); HS_TRY(dalloc(&c->d_res_order, P8));
-  HS_TRY(dalloc(&c->d_pt_host, nP)); HS_TRY(dalloc(&c->d_host_pt_begin, nF + 1));
-  // residual state in the slot layout [point][target slot] (P8 entries; slots without a residual unused)
-  HS_TRY(dalloc(&c->d_r_state, P8)); HS_TRY(dalloc(&c->d_r_active, P8));
-  HS_TRY(dalloc(&c->d_r_energy, P8)); HS_TRY(dalloc(&c->d_r_newEnergy, P8)); HS_TRY(dalloc(&c->d_r_ewo, P8));
-  HS_TRY(dalloc(&c->d_r_center, (size_t)P8 * 3));
-  HS_TRY(dalloc(&c->d_p_actmask, nP)); HS_TRY(dalloc(&c->d_p_HdiF, nP)); HS_TRY(dalloc(&c->d_p_bdSumF, nP));
-  HS_TRY(dalloc(&c->d_p_Hcd, (size_t)nP * 4)); HS_TRY(dalloc(&c->d_p_JpJdF, P8 * 8));
-  HS_TRY(dalloc(&c->d_p_step, nP)); HS_TRY(dalloc(&c->d_p_HdiF_alt, nP));
-  c->hdif_solved = c->d_p_HdiF;
-  HS_TRY(dalloc(&c->d_fix_relBL, nP)); HS_TRY(dalloc(&c->d_fix_nGood, nP));
-  HS_TRY(dalloc(&c->d_part, (size_t)std::max(c->nblk, 1) * c->ne * 64));
-  HS_TRY(dalloc(&c->d_part_e, (size_t)std::max(c->nblk, 1) * 4));
-  HS_TRY(dalloc(&c->d_hostsum, (size_t)nF * c->ne * 64));
-  HS_TRY(dalloc(&c->d_sys, (size_t)c->SL() + 3));  // zeroed: the lower triangle is never written
-  HS_TRY(dalloc(&c->d_sep, (size_t)2 * c->SL()));
-  HS_TRY(dalloc(&c->d_adHost, nF * nF * 64)); HS_TRY(dalloc(&c->d_adTarget, nF * nF * 64));
-  HS_TRY(dalloc(&c->d_adHostF, nF * nF * 64)); HS_TRY(dalloc(&c->d_adTargetF, nF * nF * 64));
-  HS_TRY(dalloc(&c->d_HM, (size_t)n * n)); HS_TRY(dalloc(&c->d_bM, n)); HS_TRY(dalloc(&c->d_Nproj, (size_t)2 * n * HS_NNS));
-  HS_TRY(dalloc(&c->d_xAd, nF * nF * 8)); HS_TRY(dalloc(&c->d_x, n)); HS_TRY(dalloc(&c->d_elog, kLogCap));
-  HS_TRY(dalloc(&c->d_cand, (size_t)c->cand_stride * c->nranks));
-  HS_TRY(dalloc(&c->d_th_hist, HS_TH_BINS));
-  HS_TRY(dalloc(&c->d_th_hist2, 1024));
-  HS_TRY(dalloc(&c->d_th_nsurv, 1));
-  HS_TRY(dalloc(&c->d_th_surv, c->th_multi ? HS_TH_SURV : 1));
-  HS_HIP(hipMemset(c->d_cand, 0xff, sizeof(float) * c->cand_stride * c->nranks));  // NaN, sign set: no candidate
-  const char* tr = std::getenv("HS_KTRACE");
-  c->tracing = tr && tr[0] == '1';
-  if (c->tracing) {
-    HS_TRY(dalloc(&c->d_tr_lin, (size_t)std::max(c->nblk, 1) * 16));
-    HS_TRY(dalloc(&c->d_tr_acc, (size_t)(nF * c->Q + 1 + 64) * 16));  // + the threshold histogram blocks
-    HS_TRY(dalloc(&c->d_tr_st, (size_t)(nF * (nF + 1) / 2 + nF + 2) * 16));
-    HS_TRY(dalloc(&c->d_tr_solve, 32));
-  }
-
   std::vector<float> prior(nP, 0.f);
   for (int i = 0; i < nP; i++)
     prior[i] = (pts->has_depth_prior && pts->has_depth_prior[i]) ? c->P.idepthFixPrior * 1.0f * 1.0f : 0.f;
   std::vector<float> th(nF);
   for (int i = 0; i < nF; i++) th[i] = S.frames[i].frameEnergyTH;
-  HS_HIP(hipMemcpy(c->d_state, c->h_state, sizeof(HsDevState), hipMemcpyHostToDevice));
-  HS_HIP(hipMemcpy(c->d_pre, pre.data(), sizeof(HsPrecalc) * nF * nF, hipMemcpyHostToDevice));
   HS_HIP(hipMemcpy(c->d_frameTH, th.data(), sizeof(float) * nF, hipMemcpyHostToDevice));
   if (nP > 0) {
     HS_HIP(hipMemcpy(c->d_u, pts->u, sizeof(float) * nP, hipMemcpyHostToDevice));
@@ -864,11 +907,6 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
     HS_HIP(hipMemcpy(c->d_pt_host, c->pt_host.data(), sizeof(int) * nP, hipMemcpyHostToDevice));
   }
   HS_HIP(hipMemcpy(c->d_host_pt_begin, c->host_pt_begin.data(), sizeof(int) * (nF + 1), hipMemcpyHostToDevice));
-  HS_HIP(hipMemcpy(c->d_adHost, c->adHost.data(), sizeof(double) * nF * nF * 64, hipMemcpyHostToDevice));
-  HS_HIP(hipMemcpy(c->d_adTarget, c->adTarget.data(), sizeof(double) * nF * nF * 64, hipMemcpyHostToDevice));
-  HS_HIP(hipMemcpy(c->d_adHostF, c->adHostF.data(), sizeof(float) * nF * nF * 64, hipMemcpyHostToDevice));
-  HS_HIP(hipMemcpy(c->d_adTargetF, c->adTargetF.data(), sizeof(float) * nF * nF * 64, hipMemcpyHostToDevice));
-  HS_HIP(hipMemcpy(c->d_Nproj, c->Nproj.data(), sizeof(double) * 2 * n * HS_NNS, hipMemcpyHostToDevice));
   if (nR > 0) {
     if (rs->state) {
       std::vector<uint8_t> slot_state(P8, HS_RES_OOB);
@@ -878,12 +916,14 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
       HS_TRY(reset_states(c));
     }
   }
+  c->pt_handle.resize(nP);
+  for (int i = 0; i < nP; i++) c->pt_handle[i] = i;
   HS_HIP(hipStreamSynchronize(c->stream));
   return HS_OK;
 }
 
 int hs_ba_linearize(hs_ctx* c, int reset, double* energy_out) {
-  if (!c || c->nF == 0) return fail(HS_ERR_STATE, "no window");
+  HS_TRY(begin_call(c));
   HS_HIP(hipSetDevice(c->device));
   HS_TRY(linearize_pass(c, reset != 0));
   double e = 0.0;
@@ -896,7 +936,7 @@ int hs_ba_linearize(hs_ctx* c, int reset, double* energy_out) {
 }
 
 int hs_ba_solve_system(hs_ctx* c, int iteration, double* x_out) {
-  if (!c || c->nF == 0) return fail(HS_ERR_STATE, "no window");
+  HS_TRY(begin_call(c));
   if (!c->haveSystem) return fail(HS_ERR_STATE, "hs_ba_linearize must run first");
   HS_HIP(hipSetDevice(c->device));
   HS_HIP(hipMemsetAsync((char*)c->d_state + offsetof(HsDevState, status), 0, sizeof(int), c->stream));
@@ -921,7 +961,7 @@ int hs_ba_solve_system(hs_ctx* c, int iteration, double* x_out) {
 }
 
 int hs_ba_do_step(hs_ctx* c, int* canbreak_out) {
-  if (!c || c->nF == 0) return fail(HS_ERR_STATE, "no window");
+  HS_TRY(begin_call(c));
   HS_HIP(hipSetDevice(c->device));
   if (c->nP > 0)
     hipLaunchKernelGGL(hs_k_apply_step, dim3((c->nP + 255) / 256), dim3(256), 0, c->stream, c->nP, c->d_p_step,
@@ -936,7 +976,7 @@ int hs_ba_do_step(hs_ctx* c, int* canbreak_out) {
 }
 
 int hs_ba_optimize(hs_ctx* c, int max_iters, int allow_break, double* energies_out, int* iters_done) {
-  if (!c || c->nF == 0) return fail(HS_ERR_STATE, "no window");
+  HS_TRY(begin_call(c));
   if (max_iters < 0) return fail(HS_ERR_INVALID, "max_iters < 0");
   HS_HIP(hipSetDevice(c->device));
   // energies_out holds max_iters + 1 entries (hs_ba.h) whatever the override below runs
@@ -962,7 +1002,7 @@ int hs_ba_optimize(hs_ctx* c, int max_iters, int allow_break, double* energies_o
 }
 
 int hs_ba_iterate(hs_ctx* c, int first_iteration, int n_iters, double* energies_out) {
-  if (!c || c->nF == 0) return fail(HS_ERR_STATE, "no window");
+  HS_TRY(begin_call(c));
   if (!c->haveSystem) return fail(HS_ERR_STATE, "hs_ba_linearize must run first");
   if (n_iters < 0) return fail(HS_ERR_INVALID, "n_iters < 0");
   HS_HIP(hipSetDevice(c->device));
@@ -980,7 +1020,7 @@ int hs_ba_iterate(hs_ctx* c, int first_iteration, int n_iters, double* energies_
 // stitched system is that of the fixed linearization).
 int hs_ba_fix_linearization(hs_ctx* c, double* energy_out, uint8_t* drop_out, float* maxRelBaseline,
                             int* numGoodResiduals, float* HdiF_out) {
-  if (!c || c->nF == 0) return fail(HS_ERR_STATE, "no window");
+  HS_TRY(begin_call(c));
   if ((maxRelBaseline == nullptr) != (numGoodResiduals == nullptr))
     return fail(HS_ERR_INVALID, "maxRelBaseline and numGoodResiduals go together");
   HS_HIP(hipSetDevice(c->device));
@@ -998,39 +1038,12 @@ int hs_ba_fix_linearization(hs_ctx* c, double* energy_out, uint8_t* drop_out, fl
     f.setStateZero(nsz);
     f.takeData(c->P);
   }
-  for (int h = 0; h < nF; h++)  // EnergyFunctional::setAdjointsF
-    for (int t = 0; t < nF; t++) {
-      const int idx = h + t * nF;
-      make_adjoints(S.frames[h], S.frames[t], &c->adHost[idx * 64], &c->adTarget[idx * 64]);
-      for (int i = 0; i < 64; i++) {
-        c->adHostF[idx * 64 + i] = (float)c->adHost[idx * 64 + i];
-        c->adTargetF[idx * 64 + i] = (float)c->adTarget[idx * 64 + i];
-      }
-    }
-  compute_projector(c);  // the newest frame's nullspaces moved with its evalPT
-  std::vector<HsPrecalc> pre(nF * nF);  // setPrecalcValues
-  for (int h = 0; h < nF; h++)
-    for (int t = 0; t < nF; t++) pre[h * nF + t] = make_precalc(S.frames[h], S.frames[t], S.calib);
-  const int n = c->dim();
-  HS_HIP(hipMemcpyAsync(c->d_state, c->h_state, sizeof(HsDevState), hipMemcpyHostToDevice, c->stream));
-  HS_HIP(hipMemcpyAsync(c->d_pre, pre.data(), sizeof(HsPrecalc) * nF * nF, hipMemcpyHostToDevice, c->stream));
-  HS_HIP(hipMemcpyAsync(c->d_adHost, c->adHost.data(), sizeof(double) * nF * nF * 64, hipMemcpyHostToDevice, c->stream));
-  HS_HIP(hipMemcpyAsync(c->d_adTarget, c->adTarget.data(), sizeof(double) * nF * nF * 64, hipMemcpyHostToDevice,
-                        c->stream));
-  HS_HIP(hipMemcpyAsync(c->d_adHostF, c->adHostF.data(), sizeof(float) * nF * nF * 64, hipMemcpyHostToDevice,
-                        c->stream));
-  HS_HIP(hipMemcpyAsync(c->d_adTargetF, c->adTargetF.data(), sizeof(float) * nF * nF * 64, hipMemcpyHostToDevice,
-                        c->stream));
-  HS_HIP(hipMemcpyAsync(c->d_Nproj, c->Nproj.data(), sizeof(double) * 2 * n * HS_NNS, hipMemcpyHostToDevice,
-                        c->stream));
+  HS_TRY(upload_frames(c));  // EnergyFunctional::setAdjointsF, setPrecalcValues, the moved nullspaces
   if (nP > 0) {
     if (maxRelBaseline) {
       HS_HIP(hipMemcpyAsync(c->d_fix_relBL, maxRelBaseline, sizeof(float) * nP, hipMemcpyHostToDevice, c->stream));
       HS_HIP(hipMemcpyAsync(c->d_fix_nGood, numGoodResiduals, sizeof(int) * nP, hipMemcpyHostToDevice, c->stream));
-    } else {
-      HS_HIP(hipMemsetAsync(c->d_fix_relBL, 0, sizeof(float) * nP, c->stream));
-      HS_HIP(hipMemsetAsync(c->d_fix_nGood, 0, sizeof(int) * nP, c->stream));
-    }
+    }  // else: the context's own per-point values (hs_ba_set_window: 0; hs_ba_insert_points: the given seeds)
   }
   // linearizeAll(true): no resetOOB (OOB stays sticky from the GN loop), no point step
   HS_TRY(launch_linearize(c, 0, false, true, true));
@@ -1055,7 +1068,7 @@ int hs_ba_fix_linearization(hs_ctx* c, double* energy_out, uint8_t* drop_out, fl
 }
 
 int hs_ba_get_system(hs_ctx* c, int which, double* H, double* b) {
-  if (!c || c->nF == 0) return fail(HS_ERR_STATE, "no window");
+  HS_TRY(begin_call(c));
   if (which < 0 || which > 2) return fail(HS_ERR_INVALID, "which must be 0, 1 or 2");
   if (!c->haveSystem) return fail(HS_ERR_STATE, "no stitched system (linearize first)");
   HS_HIP(hipSetDevice(c->device));
@@ -1098,7 +1111,7 @@ int hs_ba_get_system(hs_ctx* c, int which, double* H, double* b) {
 
 int hs_ba_get_residuals(hs_ctx* c, uint8_t* state, uint8_t* active, float* energy, float* energy_wo, float* JpJdF,
                         float* center) {
-  if (!c || c->nF == 0) return fail(HS_ERR_STATE, "no window");
+  HS_TRY(begin_call(c));
   HS_HIP(hipSetDevice(c->device));
   HS_HIP(hipStreamSynchronize(c->stream));
   const size_t m = c->nR;
@@ -1138,7 +1151,7 @@ int hs_ba_get_residuals(hs_ctx* c, uint8_t* state, uint8_t* active, float* energ
 }
 
 int hs_ba_get_points(hs_ctx* c, float* idepth, float* step, float* HdiF, float* bdSumF) {
-  if (!c || c->nF == 0) return fail(HS_ERR_STATE, "no window");
+  HS_TRY(begin_call(c));
   HS_HIP(hipSetDevice(c->device));
   HS_HIP(hipStreamSynchronize(c->stream));
   const size_t n = c->nP;
@@ -1155,7 +1168,7 @@ int hs_ba_get_points(hs_ctx* c, float* idepth, float* step, float* HdiF, float* 
 // prior terms and calcMEnergyF on the host in fp64 (the deltas of the current state), the points' prior term on
 // the device (hs_k_lenergy).
 int hs_ba_calc_energies(hs_ctx* c, double* energyL, double* energyM) {
-  if (!c || c->nF == 0) return fail(HS_ERR_STATE, "no window");
+  HS_TRY(begin_call(c));
   HS_HIP(hipSetDevice(c->device));
   HS_TRY(fetch_state(c));
   const HsDevState& S = *c->h_state;
@@ -1175,18 +1188,15 @@ int hs_ba_calc_energies(hs_ctx* c, double* energyL, double* energyM) {
     EL += s;
   }
   if (c->nP > 0) {
-    float* d_chunk = nullptr;
-    double* d_out = nullptr;
-    HS_TRY(dalloc(&d_chunk, (size_t)(c->nP + 49) / 50));
-    HS_TRY(dalloc(&d_out, 1));
+    // the window holds no linearized residuals (PointFrameResidual::isLinearized is never set on this path), so
+    // calcLEnergyPt's residual terms vanish and only the depth priors remain
     hipLaunchKernelGGL(hs_k_lenergy, dim3(1), dim3(256), 0, c->stream, c->nP, c->d_idepth, c->d_idepth_zero,
-                       c->d_priorF, d_chunk, d_out);
+                       c->d_priorF, c->d_le_chunk, c->d_le_out);
     HS_HIP(hipGetLastError());
-    double ep = 0.0;
-    HS_HIP(hipMemcpyAsync(&ep, d_out, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HS_HIP(hipMemcpyAsync(&c->h_ctl[4], c->d_le_out, sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HS_HIP(hipStreamSynchronize(c->stream));
-    (void)hipFree(d_chunk);
-    (void)hipFree(d_out);
+    double ep = 0.0;
+    std::memcpy(&ep, &c->h_ctl[4], sizeof(double));
     EL += ep;
   }
   // calcMEnergyF: delta . (2 bM + HM delta), delta = getStitchedDeltaF (Src/EnergyFunctional.cpp:842-846)
@@ -1206,7 +1216,7 @@ int hs_ba_calc_energies(hs_ctx* c, double* energyL, double* energyM) {
 }
 
 int hs_ba_get_frames(hs_ctx* c, double* state, float* energyTH, double* pose7, double* calib4) {
-  if (!c || c->nF == 0) return fail(HS_ERR_STATE, "no window");
+  HS_TRY(begin_call(c));
   HS_HIP(hipSetDevice(c->device));
   HS_TRY(fetch_state(c));
   const HsDevState& S = *c->h_state;
@@ -1222,7 +1232,7 @@ int hs_ba_get_frames(hs_ctx* c, double* state, float* energyTH, double* pose7, d
 }
 
 int hs_ba_set_marginal_prior(hs_ctx* c, const double* HM, const double* bM) {
-  if (!c || c->nF == 0) return fail(HS_ERR_STATE, "no window");
+  HS_TRY(begin_call(c));
   if (!HM || !bM) return fail(HS_ERR_INVALID, "null HM / bM");
   HS_HIP(hipSetDevice(c->device));
   const int n = c->dim();
@@ -1241,7 +1251,7 @@ int hs_ba_set_marginal_prior(hs_ctx* c, const double* HM, const double* bM) {
 // kernels over the flagged points (resetOOB, linearize, applyRes, fixLinearizationF, addPoint<2>, SC addPoint(p,
 // false)), stitched into M and Msc; HM += margWeightFac (M - Msc), bM likewise.
 int hs_ba_marginalize_points(hs_ctx* c, int n, const int* points, double* HM_out, double* bM_out) {
-  if (!c || c->nF == 0) return fail(HS_ERR_STATE, "no window");
+  HS_TRY(begin_call(c));
   if (n < 0 || (n > 0 && !points)) return fail(HS_ERR_INVALID, "bad point list");
   HS_HIP(hipSetDevice(c->device));
   const int nF = c->nF, dim = c->dim();
@@ -1251,8 +1261,6 @@ int hs_ba_marginalize_points(hs_ctx* c, int n, const int* points, double* HM_out
     if (flag[points[i]]) return fail(HS_ERR_INVALID, "duplicate point in the marginalization list");
     flag[points[i]] = 1;
   }
-  if (!c->d_marg) HS_TRY(dalloc(&c->d_marg, (size_t)std::max(c->nP, 1)));
-  if (!c->d_adHTdelta) HS_TRY(dalloc(&c->d_adHTdelta, (size_t)nF * nF * 8));
   // EnergyFunctional::setDeltaF (Src/EnergyFunctional.cpp:128-152) from the current device state, in fp32
   HS_TRY(fetch_state(c));
   const HsDevState& S = *c->h_state;
@@ -1329,14 +1337,12 @@ static bool inverse8(const double* A, double* Ainv) {
   return true;
 }
 
+}  // extern "C"
+
 // EnergyFunctional::marginalizeFrame (Src/EnergyFunctional.cpp:456-543) on the context's HM / bM: a dense 68x68
-// host operation once per marginalized keyframe (not on the GN path).
-int hs_ba_marginalize_frame(hs_ctx* c, int frame, double* HM_out, double* bM_out) {
-  if (!c || c->nF == 0) return fail(HS_ERR_STATE, "no window");
-  if (frame < 0 || frame >= c->nF) return fail(HS_ERR_INVALID, "frame index out of range");
-  if (c->nF < 2) return fail(HS_ERR_INVALID, "cannot marginalize the only frame");
-  HS_HIP(hipSetDevice(c->device));
-  HS_TRY(fetch_state(c));
+// host operation once per marginalized keyframe (not on the GN path).  HMn / bMn: the (dim-8) prior.
+int hs::marginalize_frame_prior(hs_ctx* c, int frame, std::vector<double>& HMn, std::vector<double>& bMn) {
+  if (!c->h_state_valid) HS_TRY(fetch_state(c));
   const int od = c->dim(), nd = od - 8, f0 = 4 + 8 * frame;
   std::vector<double> HMc = c->HM, bMc = c->bM;
   if (HMc.size() != (size_t)od * od) HMc.assign((size_t)od * od, 0.0);
@@ -1383,14 +1389,28 @@ int hs_ba_marginalize_frame(hs_ctx* c, int frame, double* HM_out, double* bM_out
     for (int k = 0; k < 8; k++) t += bl[k] * b[nd + k];
     b[r] -= t;
   }
-  std::vector<double> HMn((size_t)nd * nd), bMn(nd);
+  HMn.assign((size_t)nd * nd, 0.0);
+  bMn.assign(nd, 0.0);
   for (int r = 0; r < nd; r++) {
     bMn[r] = sv[r] * b[r];
     for (int q = 0; q < nd; q++)
       HMn[(size_t)r * nd + q] = 0.5 * (sv[r] * H[(size_t)r * od + q] * sv[q] + sv[q] * H[(size_t)q * od + r] * sv[r]);
   }
-  if (HM_out) std::memcpy(HM_out, HMn.data(), sizeof(double) * nd * nd);
-  if (bM_out) std::memcpy(bM_out, bMn.data(), sizeof(double) * nd);
+  return HS_OK;
+}
+
+extern "C" {
+
+int hs_ba_marginalize_frame(hs_ctx* c, int frame, double* HM_out, double* bM_out) {
+  if (!c || (c->nF == 0 && !c->dirty)) return fail(HS_ERR_STATE, "no window");
+  HS_HIP(hipSetDevice(c->device));
+  HS_TRY(commit_if_dirty(c));
+  if (frame < 0 || frame >= c->nF) return fail(HS_ERR_INVALID, "frame index out of range");
+  if (c->nF < 2) return fail(HS_ERR_INVALID, "cannot marginalize the only frame");
+  std::vector<double> HMn, bMn;
+  HS_TRY(marginalize_frame_prior(c, frame, HMn, bMn));
+  if (HM_out) std::memcpy(HM_out, HMn.data(), sizeof(double) * HMn.size());
+  if (bM_out) std::memcpy(bM_out, bMn.data(), sizeof(double) * bMn.size());
   return HS_OK;
 }
 
@@ -1412,7 +1432,7 @@ int hs_ba_get_partition(hs_ctx* c, int* out4) {
 
 int hs_ba_time_linearize(hs_ctx* c, int reps, double* avg_ms) {
   if (!c || !avg_ms || reps < 1) return fail(HS_ERR_INVALID, "bad args");
-  if (c->nF == 0) return fail(HS_ERR_STATE, "no window");
+  HS_TRY(begin_call(c));
   HS_HIP(hipSetDevice(c->device));
   HS_HIP(hipEventRecord(c->ev[0], c->stream));
   for (int k = 0; k < reps; k++) HS_TRY(launch_linearize(c, 0));

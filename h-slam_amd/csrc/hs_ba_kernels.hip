@@ -217,7 +217,7 @@ __device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int 
   const float colorK = in.colorK, weightK = in.weightK;
   const HsPrecalc pc = K.pre[tc_];
   // the target's image: selected from the kernel-argument pointers (uniform SGPRs), not loaded per lane
-  const float4* timg = a.img + (t < nF ? t : 0) * a.img_stride;  // slots past the window: frame 0 (never used)
+  const float4* timg = a.img + (long long)hs_img_slot(a.img_slot, tc_) * a.img_stride;  // past the window: frame 0
   // the point's 8 residual-list slots and previous active mask, as scalars (uniform per point)
   const uint2 ro2 = make_uint2(__builtin_amdgcn_readfirstlane(in.ro2.x), __builtin_amdgcn_readfirstlane(in.ro2.y));
   auto res_slot = [&](int q) -> int { return (int)(int8_t)(((q < 4 ? ro2.x : ro2.y) >> (8 * (q & 3))) & 0xffu); };

@@ -39,9 +39,19 @@ constexpr int HS_ND_EXACT = 49;  // every ordered (t1, t2): the single-thread re
 __host__ __device__ constexpr int hs_ne(bool exact) { return HS_E_TOP + (exact ? HS_ND_EXACT : HS_ND_PROD) + 5 + 1; }
 __host__ __device__ constexpr int hs_nt(int n) { return n * (n + 1) / 2; }  // upper triangle of the n x n system
 
+// image slot of window frame t (per lane): a select chain over the uniform kernel arguments, so no per-lane load
+// sits in front of the bilinear taps
+__device__ __forceinline__ int hs_img_slot(const int (&slot)[HS_MAXF], int t) {
+  int r = slot[0];
+#pragma unroll
+  for (int i = 1; i < HS_MAXF; i++) r = (t == i) ? slot[i] : r;
+  return r;
+}
+
 struct HsLinArgs {
-  const float4* img;           // level-0 texels of the window frames, frame f at img + f * img_stride
+  const float4* img;           // level-0 texels of the image slots, slot s at img + s * img_stride
   long long img_stride;
+  int img_slot[HS_MAXF];       // window frame -> image slot (frames keep their slot while the window slides)
   const HsDevState* st;
   HsLinParams lp;
   int nF;

@@ -129,7 +129,7 @@ __global__ __launch_bounds__(HS_LIN8_NT) void hs_k_lin8(HsLinArgs a) {
   const HsCalib cal = a.st->dcal;
   const HsLinParams lp = a.lp;
   const int tc = t < nF ? t : 0;
-  const float4* timg = a.img + tc * a.img_stride;  // slots past the window read frame 0 (never used)
+  const float4* timg = a.img + (long long)hs_img_slot(a.img_slot, tc) * a.img_stride;  // past the window: frame 0
   L8Scratch& W = U.s[wv];
   const int oslot = t - (t > h ? 1 : 0);           // non-host slot index of t (t != h)
 

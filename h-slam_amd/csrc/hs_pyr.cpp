@@ -32,6 +32,19 @@ hipError_t hs_build_dir_pyramid(hipStream_t stream, const float* d_img, int W, i
   return hipSuccess;
 }
 
+hipError_t hs_build_dir_pyramid_upper(hipStream_t stream, int W, int H, int nlev, float4* const* d_lvl) {
+  hipError_t e = hipSuccess;
+  for (int l = 1; l < nlev; l++) {
+    const int wl = W >> l, hl = H >> l, n = wl * hl;
+    hipLaunchKernelGGL(hs_k_pyr_down, dim3((n + 255) / 256), dim3(256), 0, stream, wl, hl, W >> (l - 1), d_lvl[l - 1],
+                       d_lvl[l]);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(hs_k_pyr_grad, dim3((n + 255) / 256), dim3(256), 0, stream, wl, hl, d_lvl[l], nullptr);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  return e;
+}
+
 namespace {
 int pfail(int code, const std::string& msg) {
   hs::g_err = msg;

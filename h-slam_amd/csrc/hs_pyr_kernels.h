@@ -11,3 +11,6 @@ __global__ void hs_k_pyr_grad(int wl, int hl, float4* lvl, float* absg);
 // Enqueued on `stream`; returns the first launch error.
 hipError_t hs_build_dir_pyramid(hipStream_t stream, const float* d_img, int W, int H, int nlev, float4* const* d_lvl,
                                 float* const* d_absg);
+
+// levels 1 .. nlev-1 from a level 0 already in d_lvl[0] (its intensities; the texels' gradients are not read)
+hipError_t hs_build_dir_pyramid_upper(hipStream_t stream, int W, int H, int nlev, float4* const* d_lvl);

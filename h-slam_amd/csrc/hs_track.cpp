@@ -10,12 +10,9 @@
 
 #include "../../include/hs_ba.h"
 #include "../../include/hs_track.h"
+#include "hs_ba_ctx.h"
 #include "hs_track_kernels.h"
 #include "hs_pyr_kernels.h"
-
-namespace hs {
-extern thread_local std::string g_err;
-}
 
 namespace {
 int tfail(int code, const std::string& msg) {
@@ -173,6 +170,44 @@ static bool replay_abort(const HsTryOut& o, const double minRes[5], double lastR
   return o.ok != 0;
 }
 
+// CoarseTracker::makeCoarseDepthL0 (Src/CoarseTracker.cpp:105-263) on the device: the reference points (cu | cv | cid |
+// HdiF at pts + stride * {0,1,2,3}; their count n_host, or *d_n on the device) scattered into the level-0 idepth /
+// weight maps in point order, summed up the pyramid, dilated, normalised and compacted into the pc_* arrays.
+static int make_depth_l0(hs_tracker* t, int n_host, const int* d_n, const float* pts, int stride) {
+  const size_t n0 = (size_t)t->w[0] * t->h[0];
+  TS_HIP(hipMemsetAsync(t->d_id[0], 0, n0 * sizeof(float), t->stream));
+  TS_HIP(hipMemsetAsync(t->d_ws[0], 0, n0 * sizeof(float), t->stream));
+  if (d_n || n_host > 0)
+    hipLaunchKernelGGL(hs_k_trk_scatter_sorted, dim3(1), dim3(1024), sizeof(unsigned long long) * HS_TRK_SCAT_CAP,
+                       t->stream, d_n, n_host, pts, pts + stride, pts + 2 * (size_t)stride, pts + 3 * (size_t)stride,
+                       t->w[0], t->h[0], t->d_id[0], t->d_ws[0]);
+  TS_HIP(hipGetLastError());
+  for (int l = 1; l < t->nlev; l++) {
+    const int np = t->w[l] * t->h[l];
+    hipLaunchKernelGGL(hs_k_trk_down, dim3((np + 255) / 256), dim3(256), 0, t->stream, t->w[l], t->h[l], t->w[l - 1],
+                       t->d_id[l - 1], t->d_ws[l - 1], t->d_id[l], t->d_ws[l]);
+    TS_HIP(hipGetLastError());
+  }
+  for (int l = 0; l < t->nlev; l++) {
+    const int np = t->w[l] * t->h[l];
+    TS_HIP(hipMemcpyAsync(t->d_bak[l], t->d_ws[l], np * sizeof(float), hipMemcpyDeviceToDevice, t->stream));
+    const int inner = np - 2 * t->w[l];
+    hipLaunchKernelGGL(hs_k_trk_dilate, dim3((inner + 255) / 256), dim3(256), 0, t->stream, t->w[l], t->h[l],
+                       l < 2 ? 1 : 0, t->d_bak[l], t->d_id[l], t->d_ws[l]);
+    TS_HIP(hipGetLastError());
+  }
+  for (int l = 0; l < t->nlev; l++) {
+    const int np = t->w[l] * t->h[l], nb = (np + 255) / 256;
+    hipLaunchKernelGGL(hs_k_trk_count, dim3(nb), dim3(256), 0, t->stream, t->w[l], t->h[l], t->d_id[l], t->d_ws[l],
+                       t->d_ref[l], t->d_bcnt);
+    hipLaunchKernelGGL(hs_k_trk_scan, dim3(1), dim3(1024), 0, t->stream, nb, t->d_bcnt, t->d_boff, t->d_pcn + l);
+    hipLaunchKernelGGL(hs_k_trk_compact, dim3(nb), dim3(256), 0, t->stream, t->w[l], t->h[l], t->d_id[l], t->d_ws[l],
+                       t->d_ref[l], t->d_boff, t->d_pu[l], t->d_pv[l], t->d_pid[l], t->d_pcol[l]);
+    TS_HIP(hipGetLastError());
+  }
+  return HS_OK;
+}
+
 extern "C" {
 
 int hs_tracker_create(hs_tracker** out, const hs_params* params, int device_id, int width, int height,
@@ -275,38 +310,53 @@ int hs_tracker_set_ref(hs_tracker* t, const float* const* ref_pyr, float ab_expo
     std::memcpy(h.data() + 3 * n, hdi, 4 * n);
     TS_HIP(hipMemcpy(t->d_pts, h.data(), sizeof(float) * 4 * n, hipMemcpyHostToDevice));
   }
-  // makeCoarseDepthL0
-  const size_t n0 = (size_t)t->w[0] * t->h[0];
-  TS_HIP(hipMemsetAsync(t->d_id[0], 0, n0 * sizeof(float), t->stream));
-  TS_HIP(hipMemsetAsync(t->d_ws[0], 0, n0 * sizeof(float), t->stream));
-  if (n > 0)
-    hipLaunchKernelGGL(hs_k_trk_scatter, dim3(1), dim3(64), 0, t->stream, n, t->d_pts, t->d_pts + n, t->d_pts + 2 * n,
-                       t->d_pts + 3 * n, t->w[0], t->h[0], t->d_id[0], t->d_ws[0]);
-  TS_HIP(hipGetLastError());
-  for (int l = 1; l < t->nlev; l++) {
-    const int np = t->w[l] * t->h[l];
-    hipLaunchKernelGGL(hs_k_trk_down, dim3((np + 255) / 256), dim3(256), 0, t->stream, t->w[l], t->h[l], t->w[l - 1],
-                       t->d_id[l - 1], t->d_ws[l - 1], t->d_id[l], t->d_ws[l]);
-    TS_HIP(hipGetLastError());
-  }
-  for (int l = 0; l < t->nlev; l++) {
-    const int np = t->w[l] * t->h[l];
-    TS_HIP(hipMemcpyAsync(t->d_bak[l], t->d_ws[l], np * sizeof(float), hipMemcpyDeviceToDevice, t->stream));
-    const int inner = np - 2 * t->w[l];
-    hipLaunchKernelGGL(hs_k_trk_dilate, dim3((inner + 255) / 256), dim3(256), 0, t->stream, t->w[l], t->h[l],
-                       l < 2 ? 1 : 0, t->d_bak[l], t->d_id[l], t->d_ws[l]);
-    TS_HIP(hipGetLastError());
-  }
-  for (int l = 0; l < t->nlev; l++) {
-    const int np = t->w[l] * t->h[l], nb = (np + 255) / 256;
-    hipLaunchKernelGGL(hs_k_trk_count, dim3(nb), dim3(256), 0, t->stream, t->w[l], t->h[l], t->d_id[l], t->d_ws[l],
-                       t->d_ref[l], t->d_bcnt);
-    hipLaunchKernelGGL(hs_k_trk_scan, dim3(1), dim3(1024), 0, t->stream, nb, t->d_bcnt, t->d_boff, t->d_pcn + l);
-    hipLaunchKernelGGL(hs_k_trk_compact, dim3(nb), dim3(256), 0, t->stream, t->w[l], t->h[l], t->d_id[l], t->d_ws[l],
-                       t->d_ref[l], t->d_boff, t->d_pu[l], t->d_pv[l], t->d_pid[l], t->d_pcol[l]);
-    TS_HIP(hipGetLastError());
-  }
+  TS_TRY(make_depth_l0(t, n, nullptr, t->d_pts, n));
   TS_HIP(hipStreamSynchronize(t->stream));
+  t->haveRef = true;
+  return HS_OK;
+}
+
+int hs_tracker_frame_texels(hs_tracker* t, int lvl, const void** d_texels) {
+  if (!t || !d_texels) return tfail(HS_ERR_INVALID, "null argument");
+  if (lvl < 0 || lvl >= t->nlev) return tfail(HS_ERR_INVALID, "bad level");
+  if (!t->haveFrame) return tfail(HS_ERR_STATE, "no frame set");
+  *d_texels = t->d_new[lvl];
+  return HS_OK;
+}
+
+// setCoarseTrackingRef(frameHessians) after AddKeyframe's optimize (Src/Mapping.cpp:93-100), fed from the BA context
+// on the device: the points whose residual into the newest frame is IN, in window order (hs_k_win_newest on the BA
+// stream), then makeCoarseDepthL0 on the tracker stream after an event -- no host round trip, no host sync.
+int hs_tracker_set_ref_ba(hs_tracker* t, hs_ctx* ba, int promote_frame, float ab_exposure, const double aff_g2l[2]) {
+  if (!t || !ba || !aff_g2l) return tfail(HS_ERR_INVALID, "null argument");
+  if (ba->device != t->device) return tfail(HS_ERR_INVALID, "tracker and BA context on different devices");
+  TS_HIP(hipSetDevice(t->device));
+  HS_TRY(hs::commit_if_dirty(ba));
+  if (ba->nF < 1) return tfail(HS_ERR_STATE, "empty BA window");
+  if (ba->cam.width != t->W || ba->cam.height != t->H) return tfail(HS_ERR_INVALID, "image size mismatch");
+  if (promote_frame && !t->haveFrame) return tfail(HS_ERR_STATE, "no frame to promote");
+  // the hand-off buffer: points of the BA window (capacity), compacted on the BA's stream
+  hipLaunchKernelGGL(hs_k_win_newest, dim3(1), dim3(1024), 0, ba->stream, ba->nP, ba->nF - 1, ba->d_res_of_slot,
+                     ba->d_r_state, ba->d_r_center, ba->hdif_solved, ba->d_ref_pts, ba->cap_P, ba->d_ref_n);
+  TS_HIP(hipGetLastError());
+  if (!promote_frame)  // the reference pyramid's level 0 is the BA's newest frame image
+    TS_HIP(hipMemcpyAsync(t->d_ref[0], ba->d_img_all + (size_t)ba->img_slot[ba->nF - 1] * ba->img_px,
+                          sizeof(float4) * (size_t)t->W * t->H, hipMemcpyDeviceToDevice, ba->stream));
+  TS_HIP(hipEventRecord(ba->ev_ready, ba->stream));
+  TS_HIP(hipStreamWaitEvent(t->stream, ba->ev_ready, 0));
+  if (promote_frame) {
+    for (int l = 0; l < t->nlev; l++) std::swap(t->d_ref[l], t->d_new[l]);
+    t->haveFrame = false;  // d_new now holds the old reference: the next frame to track must be set
+  } else {
+    TS_HIP(hs_build_dir_pyramid_upper(t->stream, t->W, t->H, t->nlev, t->d_ref));
+  }
+  t->refExposure = ab_exposure;
+  t->refAff[0] = aff_g2l[0];
+  t->refAff[1] = aff_g2l[1];
+  TS_TRY(make_depth_l0(t, 0, ba->d_ref_n, ba->d_ref_pts, ba->cap_P));
+  // the BA stream must not rewrite the hand-off buffer before the tracker consumed it
+  TS_HIP(hipEventRecord(t->e1, t->stream));
+  TS_HIP(hipStreamWaitEvent(ba->stream, t->e1, 0));
   t->haveRef = true;
   return HS_OK;
 }

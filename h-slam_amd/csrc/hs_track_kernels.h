@@ -58,6 +58,9 @@ struct HsTrackArgs {
 __global__ void hs_k_track(HsTrackArgs a);
 __global__ void hs_k_trk_scatter(int n, const float* cu, const float* cv, const float* cid, const float* hdi, int w,
                                  int h, float* idepth0, float* wsum0);
+constexpr int HS_TRK_SCAT_CAP = 8192;  // points sorted in LDS by hs_k_trk_scatter_sorted (dynamic LDS: 8 B each)
+__global__ void hs_k_trk_scatter_sorted(const int* d_n, int n_arg, const float* cu, const float* cv, const float* cid,
+                                        const float* hdi, int w, int h, float* idepth0, float* wsum0);
 __global__ void hs_k_trk_down(int wl, int hl, int wlm1, const float* idm, const float* wsm, float* idl, float* wsl);
 __global__ void hs_k_trk_dilate(int wl, int hl, int diag, const float* bak, float* id, float* ws);
 __global__ void hs_k_trk_count(int wl, int hl, const float* id, const float* ws, const float4* ref, int* blockCount);

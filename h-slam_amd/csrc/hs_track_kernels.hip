@@ -557,9 +557,8 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
 }
 
 // ---------------------------------------------------------------- makeCoarseDepthL0
-__global__ void hs_k_trk_scatter(int n, const float* cu, const float* cv, const float* cid, const float* hdi, int w,
-                                 int h, float* idepth0, float* wsum0) {
-  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+__device__ void hs_k_trk_scatter_seq(int n, const float* cu, const float* cv, const float* cid, const float* hdi,
+                                     int w, int h, float* idepth0, float* wsum0) {
   for (int i = 0; i < n; i++) {  // the reference's order: colliding points add in sequence
     const int u = (int)(cu[i] + 0.5f);
     const int v = (int)(cv[i] + 0.5f);
@@ -568,6 +567,71 @@ __global__ void hs_k_trk_scatter(int n, const float* cu, const float* cv, const 
     const float weight = sqrtf(1e-3 / (hdi[i] + 1e-12));
     idepth0[u + w * v] += new_idepth * weight;
     wsum0[u + w * v] += weight;
+  }
+}
+
+__global__ void hs_k_trk_scatter(int n, const float* cu, const float* cv, const float* cid, const float* hdi, int w,
+                                 int h, float* idepth0, float* wsum0) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  hs_k_trk_scatter_seq(n, cu, cv, cid, hdi, w, h, idepth0, wsum0);
+}
+
+// makeCoarseDepthL0's point loop in parallel with the sequential loop's sums: the points are sorted by (pixel,
+// point index) in LDS (bitonic, one workgroup), and the first point of every pixel's run adds the run in point order,
+// starting from the memset zero -- the very additions of the sequential loop, so the maps are bit-identical.  n comes
+// from the device (d_n, the BA hand-off's count) or the argument; more than kScatCap points fall back to the loop.
+constexpr int kScatCap = 8192;
+__global__ __launch_bounds__(1024) void hs_k_trk_scatter_sorted(const int* d_n, int n_arg, const float* cu,
+                                                                const float* cv, const float* cid, const float* hdi,
+                                                                int w, int h, float* idepth0, float* wsum0) {
+  extern __shared__ unsigned long long skey[];
+  const int n = d_n ? *d_n : n_arg;
+  const int tid = threadIdx.x;
+  if (n > kScatCap) {
+    if (tid == 0) hs_k_trk_scatter_seq(n, cu, cv, cid, hdi, w, h, idepth0, wsum0);
+    return;
+  }
+  int N = 64;
+  while (N < n) N <<= 1;
+  for (int i = tid; i < N; i += 1024) {
+    unsigned long long k = ~0ull;
+    if (i < n) {
+      const int u = (int)(cu[i] + 0.5f);
+      const int v = (int)(cv[i] + 0.5f);
+      if (!(u < 0 || v < 0 || u >= w || v >= h))
+        k = ((unsigned long long)(unsigned)(u + w * v) << 32) | (unsigned)i;
+    }
+    skey[i] = k;
+  }
+  __syncthreads();
+  for (int kk = 2; kk <= N; kk <<= 1)
+    for (int j = kk >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < N; i += 1024) {
+        const int l = i ^ j;
+        if (l > i) {
+          const unsigned long long a = skey[i], b = skey[l];
+          if ((a > b) == ((i & kk) == 0)) {
+            skey[i] = b;
+            skey[l] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  for (int i = tid; i < n; i += 1024) {
+    const unsigned long long k = skey[i];
+    if (k == ~0ull) continue;
+    const unsigned pix = (unsigned)(k >> 32);
+    if (i > 0 && (unsigned)(skey[i - 1] >> 32) == pix) continue;  // not the first point of its pixel
+    float s = 0.f, sw = 0.f;
+    for (int q = i; q < n && (unsigned)(skey[q] >> 32) == pix; q++) {
+      const int p = (int)(skey[q] & 0xffffffffull);
+      const float weight = sqrtf(1e-3 / (hdi[p] + 1e-12));
+      s += cid[p] * weight;
+      sw += weight;
+    }
+    idepth0[pix] = s;
+    wsum0[pix] = sw;
   }
 }
 

@@ -78,6 +78,27 @@ SIGNATURES = {
     "hs_ba_get_timings": ([VP, VP], I),
     "hs_ba_time_linearize": ([VP, I, VP], I),
     "hs_ba_get_partition": ([VP, VP], I),
+    "hs_ba_reserve": ([VP, VP, I], I),
+    "hs_ba_insert_frame": ([VP, VP, VP], I),
+    "hs_ba_set_frame_image": ([VP, I, VP], I),
+    "hs_ba_set_frame_image_raw": ([VP, I, VP], I),
+    "hs_ba_set_frame_image_device": ([VP, I, VP], I),
+    "hs_ba_insert_points": ([VP, VP, VP, VP, VP], I),
+    "hs_ba_insert_residuals": ([VP, I, VP, VP, VP], I),
+    "hs_ba_add_residuals_to_newest": ([VP, VP], I),
+    "hs_ba_drop_residuals": ([VP, I, VP, VP], I),
+    "hs_ba_drop_inactive_residuals": ([VP, VP], I),
+    "hs_ba_remove_points": ([VP, I, VP], I),
+    "hs_ba_remove_points_without_residuals": ([VP, VP, VP], I),
+    "hs_ba_remove_frame": ([VP, I, I], I),
+    "hs_ba_make_idx": ([VP, VP, VP, VP], I),
+    "hs_ba_get_structure": ([VP] * 5, I),
+    "hs_ba_get_marginal_prior": ([VP, VP, VP], I),
+    "hs_ba_synchronize": ([VP], I),
+    "hs_ba_get_point_state": ([VP] * 6, I),
+    "hs_debug_state_size": ([], I),
+    "hs_debug_get_state": ([VP, VP], I),
+    "hs_debug_set_state": ([VP, VP], I),
     "hs_comm_get_unique_id": ([VP], I),
     "hs_comm_init": ([VP, VP, I, I], I),
     # include/hs_track.h
@@ -93,6 +114,8 @@ SIGNATURES = {
     "hs_tracker_last_ms": ([VP, VP], I),
     "hs_tracker_last_stats": ([VP, I, VP, VP, VP], I),
     "hs_tracker_set_frame_raw": ([VP, VP, C.c_float], I),
+    "hs_tracker_set_ref_ba": ([VP, VP, I, C.c_float, VP], I),
+    "hs_tracker_frame_texels": ([VP, I, VP], I),
     # include/hs_pyr.h
     "hs_dir_pyramid": ([I, I, I, I, VP, VP, VP], I),
     # include/hs_trace.h

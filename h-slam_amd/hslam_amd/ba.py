@@ -19,9 +19,30 @@ import numpy as np
 from ._lib import (check, default_params, hs_camera, hs_frame, hs_points, hs_residuals, load, ptr)
 
 
+def _camera(width, height, n_levels, K):
+    return hs_camera(int(width), int(height), int(n_levels), 0, float(K[0, 0]), float(K[1, 1]), float(K[0, 2]),
+                     float(K[1, 2]))
+
+
+def make_frame(evalPT, state=None, state_zero=None, exposure=1.0, energyTH=8 * 8 * 8, fid=1):
+    """hs_frame of a keyframe (FrameOptimizationData: evalPT as SE3 data, state / state_zero, ab_exposure,
+    frameEnergyTH, id; id 0 takes the strong first-frame prior)."""
+    f = hs_frame()
+    f.worldToCam_evalPT[:] = list(map(float, evalPT))
+    f.state[:] = list(map(float, np.zeros(10) if state is None else state))
+    f.state_zero[:] = list(map(float, np.zeros(10) if state_zero is None else state_zero))
+    f.ab_exposure = float(exposure)
+    f.frameEnergyTH = float(energyTH)
+    f.id = int(fid)
+    return f
+
+
 class BAWindow:
-    def __init__(self, scene, device: int = 0, params=None, point_slice=None, comm=None):
-        """scene: hslam_amd.scene.BAScene (or any object with the same fields).
+    def __init__(self, scene=None, device: int = 0, params=None, point_slice=None, comm=None, camera=None,
+                 capacity: int = 0):
+        """scene: hslam_amd.scene.BAScene (or any object with the same fields): the whole window at once
+        (hs_ba_set_window).  Without a scene, an empty incremental window of `capacity` points for `camera`
+        (width, height, n_levels, K) is reserved (hs_ba_reserve) and built with the keyframe calls below.
         point_slice: optional (begin, end) to load only a contiguous shard of the points.
         comm: optional (unique_id_bytes, rank, nranks) -> RCCL communicator (before the window is set)."""
         self.lib = load()
@@ -31,9 +52,15 @@ class BAWindow:
         self.h = h
         if comm is not None:
             self.comm_init(*comm)
-        self.nF = scene.n_frames
-        self.dim = 4 + 8 * self.nF
-        self._set_window(scene, point_slice)
+        if scene is not None:
+            self.nF = scene.n_frames
+            self.dim = 4 + 8 * self.nF
+            self._set_window(scene, point_slice)
+        else:
+            w, hh, nl, K = camera
+            self._cam = _camera(w, hh, nl, np.asarray(K, np.float64))
+            check(self.lib.hs_ba_reserve(self.h, C.byref(self._cam), int(capacity)))
+            self.nF, self.dim, self.n_points, self.n_res = 0, 4, 0, 0
 
     def _set_window(self, s, point_slice):
         nF = s.n_frames
@@ -71,6 +98,122 @@ class BAWindow:
         check(self.lib.hs_ba_set_window(self.h, C.byref(cam), nF, C.cast(fr, C.c_void_p), C.cast(img_ptrs, C.c_void_p),
                                         C.byref(pts), C.byref(rs)))
 
+    # --------------------------------------------------------------- incremental window (keyframe path)
+    def _sync(self):
+        """EnergyFunctional::makeIDX: commit pending edits; refresh the window sizes."""
+        nF, nP, nR = C.c_int(), C.c_int(), C.c_int()
+        check(self.lib.hs_ba_make_idx(self.h, C.byref(nF), C.byref(nP), C.byref(nR)))
+        self.nF, self.n_points, self.n_res = nF.value, nP.value, nR.value
+        self.dim = 4 + 8 * self.nF
+
+    makeIDX = _sync
+
+    def insertFrame(self, frame, image=None, raw=None, device_texels=None):
+        """EnergyFunctional::insertFrame (+ the frame's level-0 image: (h, w, 3) (I, dx, dy) host array, or a raw
+        (h, w) image whose level 0 is built on the device, or a device pointer of float4 texels)."""
+        img = None if image is None else np.ascontiguousarray(image, np.float32)
+        check(self.lib.hs_ba_insert_frame(self.h, C.byref(frame), ptr(img)))
+        idx = self._n_frames_mirror = getattr(self, "_n_frames_mirror", self.nF) + 1
+        if raw is not None:
+            check(self.lib.hs_ba_set_frame_image_raw(self.h, idx - 1, ptr(np.ascontiguousarray(raw, np.float32))))
+        if device_texels is not None:
+            check(self.lib.hs_ba_set_frame_image_device(self.h, idx - 1, C.c_void_p(device_texels)))
+        return idx - 1
+
+    def insertPoints(self, host, u, v, idepth, idepth_zero=None, color=None, weights=None, has_prior=None,
+                     max_rel_baseline=None, num_good=None):
+        """EnergyFunctional::insertPoint for n points (host: window frame index).  Returns their handles."""
+        host = np.ascontiguousarray(host, np.int32)
+        n = len(host)
+        f = [np.ascontiguousarray(a, np.float32) for a in (u, v, idepth, idepth if idepth_zero is None else idepth_zero)]
+        col = np.ascontiguousarray(color, np.float32).reshape(n, 8)
+        wgt = np.ascontiguousarray(weights, np.float32).reshape(n, 8)
+        hp = None if has_prior is None else np.ascontiguousarray(has_prior, np.uint8)
+        pts = hs_points(n, ptr(host), *[ptr(a) for a in f], ptr(col), ptr(wgt), None if hp is None else ptr(hp))
+        rb = None if max_rel_baseline is None else np.ascontiguousarray(max_rel_baseline, np.float32)
+        ng = None if num_good is None else np.ascontiguousarray(num_good, np.int32)
+        out = np.zeros(n, np.int32)
+        check(self.lib.hs_ba_insert_points(self.h, C.byref(pts), ptr(rb), ptr(ng), ptr(out)))
+        return out
+
+    def insertResiduals(self, handles, targets, states=None):
+        """EnergyFunctional::insertResidual (appended to each point's residual list)."""
+        hd = np.ascontiguousarray(handles, np.int32)
+        tg = np.ascontiguousarray(targets, np.int32)
+        st = None if states is None else np.ascontiguousarray(states, np.uint8)
+        check(self.lib.hs_ba_insert_residuals(self.h, len(hd), ptr(hd), ptr(tg), ptr(st)))
+
+    def addResidualsToNewest(self):
+        """AddKeyframe's loop: every point not hosted by the newest frame gets a residual into it (state IN)."""
+        n = C.c_int()
+        check(self.lib.hs_ba_add_residuals_to_newest(self.h, C.byref(n)))
+        return n.value
+
+    def dropResiduals(self, handles, targets):
+        hd = np.ascontiguousarray(handles, np.int32)
+        tg = np.ascontiguousarray(targets, np.int32)
+        check(self.lib.hs_ba_drop_residuals(self.h, len(hd), ptr(hd), ptr(tg)))
+
+    def dropInactiveResiduals(self):
+        """linearizeAll(true)'s toRemove loop after fixLinearization."""
+        n = C.c_int()
+        check(self.lib.hs_ba_drop_inactive_residuals(self.h, C.byref(n)))
+        return n.value
+
+    def removePoints(self, handles):
+        hd = np.ascontiguousarray(handles, np.int32)
+        check(self.lib.hs_ba_remove_points(self.h, len(hd), ptr(hd)))
+
+    def removeOutliers(self):
+        """System::removeOutliers: every point without residuals; returns the removed handles."""
+        out = np.zeros(max(self.n_points + 1, 1) * 2 + 4096, np.int32)
+        n = C.c_int()
+        check(self.lib.hs_ba_remove_points_without_residuals(self.h, ptr(out), C.byref(n)))
+        return out[: n.value].copy()
+
+    def removeFrame(self, frame, marginalize=True):
+        """System::marginalizeFrame (marginalize=True) of window frame `frame` (it must host no point)."""
+        check(self.lib.hs_ba_remove_frame(self.h, int(frame), int(marginalize)))
+        self._n_frames_mirror = getattr(self, "_n_frames_mirror", self.nF) - 1
+
+    def structure(self):
+        """The committed window: dict(handles, pt_host, nres, res_target (activeResiduals order))."""
+        self._sync()
+        o = dict(handles=np.zeros(self.n_points, np.int32), pt_host=np.zeros(self.n_points, np.int32),
+                 nres=np.zeros(self.n_points, np.int32), res_target=np.zeros(self.n_res, np.int32))
+        check(self.lib.hs_ba_get_structure(self.h, *[ptr(o[k]) for k in ("handles", "pt_host", "nres", "res_target")]))
+        o["res_point"] = np.repeat(np.arange(self.n_points, dtype=np.int32), o["nres"])
+        return o
+
+    def marginal_prior(self):
+        self._sync()
+        HM, bM = np.zeros((self.dim, self.dim)), np.zeros(self.dim)
+        check(self.lib.hs_ba_get_marginal_prior(self.h, ptr(HM), ptr(bM)))
+        return HM, bM
+
+    def point_state(self):
+        """dict(idepth, idepth_zero, maxRelBaseline, numGoodResiduals, HdiF (the last solve's)) in window order."""
+        self._sync()
+        n = self.n_points
+        o = dict(idepth=np.zeros(n, np.float32), idepth_zero=np.zeros(n, np.float32),
+                 maxRelBaseline=np.zeros(n, np.float32), numGoodResiduals=np.zeros(n, np.int32),
+                 HdiF=np.zeros(n, np.float32))
+        check(self.lib.hs_ba_get_point_state(self.h, *[ptr(o[k]) for k in ("idepth", "idepth_zero", "maxRelBaseline",
+                                                                             "numGoodResiduals", "HdiF")]))
+        return o
+
+    def synchronize(self):
+        check(self.lib.hs_ba_synchronize(self.h))
+
+    def debug_state(self) -> bytes:
+        buf = C.create_string_buffer(self.lib.hs_debug_state_size())
+        check(self.lib.hs_debug_get_state(self.h, buf))
+        return buf.raw
+
+    def debug_set_state(self, blob: bytes):
+        buf = C.create_string_buffer(blob, len(blob))
+        check(self.lib.hs_debug_set_state(self.h, buf))
+
     def close(self):
         if getattr(self, "h", None):
             self.lib.hs_destroy(self.h)
@@ -94,6 +237,7 @@ class BAWindow:
         """flagPointsForRemoval (per-point part) + EnergyFunctional::marginalizePointsF for window points
         `points` (Src/Mapping.cpp:280-293, Src/EnergyFunctional.cpp:545-609).  Returns the updated (HM, bM);
         the window's linearization is consumed (drop the points and relinearize)."""
+        self._sync()
         p = np.ascontiguousarray(points, np.int32)
         HM, bM = np.zeros((self.dim, self.dim)), np.zeros(self.dim)
         check(self.lib.hs_ba_marginalize_points(self.h, len(p), ptr(p), ptr(HM), ptr(bM)))
@@ -102,6 +246,7 @@ class BAWindow:
     def marginalizeFrame(self, frame):
         """EnergyFunctional::marginalizeFrame (Src/EnergyFunctional.cpp:456-543) on this window's HM / bM:
         returns the (dim-8) prior of the window without `frame`."""
+        self._sync()
         n = self.dim - 8
         HM, bM = np.zeros((n, n)), np.zeros(n)
         check(self.lib.hs_ba_marginalize_frame(self.h, int(frame), ptr(HM), ptr(bM)))
@@ -118,6 +263,7 @@ class BAWindow:
         return bool(cb.value)
 
     def optimize(self, iters=6, allow_break=False):
+        self._sync()
         # System::optimize's overrides for tiny windows (Src/FullSystemOptimize.cpp:366-367), applied here so the
         # energy buffer (max_iters + 1 entries, include/hs_ba.h) holds the whole trajectory
         if self.nF < 3:
@@ -137,7 +283,17 @@ class BAWindow:
     def fixLinearization(self, max_rel_baseline=None, num_good=None):
         """System::optimize's tail (Src/FullSystemOptimize.cpp:498-516): newest frame setEvalPT, setAdjointsF,
         setPrecalcValues, linearizeAll(true).  Returns dict(energy, drop[n_res], maxRelBaseline[n_points],
-        numGoodResiduals[n_points], HdiF[n_points]) (HdiF of the last solve's Schur prelude)."""
+        numGoodResiduals[n_points], HdiF[n_points]) (HdiF of the last solve's Schur prelude).  Without arrays the
+        context's own per-point values are used and returned."""
+        self._sync()
+        if max_rel_baseline is None and num_good is None:
+            drop = np.zeros(self.n_res, np.uint8)
+            hdi = np.zeros(self.n_points, np.float32)
+            e = C.c_double()
+            check(self.lib.hs_ba_fix_linearization(self.h, C.byref(e), ptr(drop), None, None, ptr(hdi)))
+            ps = self.point_state()
+            return dict(energy=e.value, drop=drop, maxRelBaseline=ps["maxRelBaseline"],
+                        numGoodResiduals=ps["numGoodResiduals"], HdiF=hdi)
         rb = np.zeros(self.n_points, np.float32) if max_rel_baseline is None else \
             np.array(max_rel_baseline, np.float32)
         ng = np.zeros(self.n_points, np.int32) if num_good is None else np.array(num_good, np.int32)
@@ -155,12 +311,14 @@ class BAWindow:
 
     # --------------------------------------------------------------- read-back
     def system(self, which):
+        self._sync()
         H = np.zeros((self.dim, self.dim))
         b = np.zeros(self.dim)
         check(self.lib.hs_ba_get_system(self.h, which, ptr(H), ptr(b)))
         return H, b
 
     def residuals(self):
+        self._sync()
         m = self.n_res
         out = dict(state=np.zeros(m, np.uint8), active=np.zeros(m, np.uint8), energy=np.zeros(m, np.float32),
                    energy_wo=np.zeros(m, np.float32), JpJdF=np.zeros((m, 8), np.float32),
@@ -170,12 +328,14 @@ class BAWindow:
         return out
 
     def points(self):
+        self._sync()
         n = self.n_points
         out = {k: np.zeros(n, np.float32) for k in ("idepth", "step", "HdiF", "bdSumF")}
         check(self.lib.hs_ba_get_points(self.h, *[ptr(out[k]) for k in ("idepth", "step", "HdiF", "bdSumF")]))
         return out
 
     def frames(self):
+        self._sync()
         st = np.zeros((self.nF, 10))
         th = np.zeros(self.nF, np.float32)
         pose = np.zeros((self.nF, 7))

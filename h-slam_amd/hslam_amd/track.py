@@ -66,6 +66,24 @@ class CoarseTracker:
         assert a.shape == (self.height, self.width)
         check(self.lib.hs_tracker_set_frame_raw(self.h, ptr(a), float(ab_exposure)))
 
+    def setCoarseTrackingRefBA(self, ba, promote: bool, ab_exposure=1.0, aff_g2l=(0.0, 0.0)):
+        """setCoarseTrackingRef from a BA context (hslam_amd.ba.BAWindow) on the device: the points with an IN
+        residual into its newest frame, no host round trip.  promote: the frame last set here becomes the reference
+        pyramid (else it is rebuilt from the BA's newest frame image)."""
+        aff = np.ascontiguousarray(aff_g2l, dtype=np.float64)
+        check(self.lib.hs_tracker_set_ref_ba(self.h, ba.h, int(promote), float(ab_exposure), ptr(aff)))
+
+    set_ref_ba = setCoarseTrackingRefBA
+
+    def frame_texels(self, lvl: int = 0) -> int:
+        """Device address of level lvl of the frame last set (float4 texels): hs_ba_set_frame_image_device."""
+        p = C.c_void_p()
+        check(self.lib.hs_tracker_frame_texels(self.h, int(lvl), C.byref(p)))
+        return p.value
+
+    def set_frame_raw(self, img, ab_exposure=1.0):
+        self.setNewFrameRaw(img, ab_exposure)
+
     def set_scene(self, s):
         """Reference + new frame of a hslam_amd.scene.TrackScene."""
         self.setCoarseTrackingRef(s.ref_pyr, s.ref_exposure, s.ref_aff, s.pt_u, s.pt_v, s.pt_idepth, s.pt_hdi)

@@ -150,6 +150,83 @@ int hs_ba_time_linearize(hs_ctx* ctx, int reps, double* avg_ms);
    take points, HS_ACC_EXACT].  Introspection only (no reference counterpart). */
 int hs_ba_get_partition(hs_ctx* ctx, int* out4);
 
+/* ---------------------------------------------------------------------------------------------------------------
+ * Incremental window: the keyframe path.  System::AddKeyframe (Src/Mapping.cpp:12-140) edits the window one object
+ * at a time through EnergyFunctional::insertFrame / insertPoint / insertResidual / dropResidual / removePoint /
+ * marginalizeFrame / makeIDX (Src/EnergyFunctional.cpp:371-454,456-543,632-646,819-840) and System::marginalizeFrame
+ * (Src/FullSystemMarginalize.cpp:108-176).  These calls do the same on a context whose device memory hs_ba_reserve
+ * allocated once: an edit changes the host mirror of the window's structure (frames in frameHessians order, each
+ * frame's points in pointHessians order, each point's residual list in PointHessian::residuals order, with the
+ * reference's swap-with-last removals); the next call that needs the device window commits the edits (makeIDX: one
+ * pinned upload of the changed index tables plus new points, one gather kernel that moves the device-resident point
+ * state -- idepth, idepth_zero, priors, colours, maxRelBaseline / numGoodResiduals, the last solve's HdiF, residual
+ * states and centre projections -- into the new order).  Points are named by the handles hs_ba_insert_points
+ * returns, frames by their window index.  After a commit the window equals the one hs_ba_set_window builds from the
+ * same frames, points (window order) and residuals (point order, list order), and every read-back (residuals in
+ * that order) refers to it.  hs_ba_set_window leaves a context these calls can continue from.
+ * --------------------------------------------------------------------------------------------------------------- */
+
+/* Capacity for windows of up to HS_MAX_FRAMES frames of cam's size and max_points points (device memory allocated
+   once; no allocation on the keyframe path).  Starts an empty incremental window. */
+int hs_ba_reserve(hs_ctx* ctx, const hs_camera* cam, int max_points);
+
+/* EnergyFunctional::insertFrame: `frame` becomes the newest window frame (index nF), with takeData's priors; the
+   marginal prior HM / bM grows by 8 zero rows / columns.  image (nullable): level-0 (I, dI/dx, dI/dy) triplets,
+   W*H*3 floats (Frame::DirPyr[0]); else set it with one of the hs_ba_set_frame_image* calls before the next commit. */
+int hs_ba_insert_frame(hs_ctx* ctx, const hs_frame* frame, const float* image);
+/* the frame's level-0 image: host (I, dI/dx, dI/dy) triplets | host raw W*H image (ImageData::fImgL: level 0 of
+   Frame::CreateDirPyrs runs on the device, Src/Frame.cpp:104-181) | device texels (W*H float4 (I, dI/dx, dI/dy, any)
+   on the context's device, e.g. hs_tracker_frame_texels: the keyframe's image never crosses PCIe again; the producer
+   must have completed, as it has when its call returned).  Copies, ordered on the context's stream. */
+int hs_ba_set_frame_image(hs_ctx* ctx, int frame, const float* image);
+int hs_ba_set_frame_image_raw(hs_ctx* ctx, int frame, const float* raw);
+int hs_ba_set_frame_image_device(hs_ctx* ctx, int frame, const void* d_texels);
+
+/* EnergyFunctional::insertPoint for pts->n points (pts->host: window frame index; each appended to its host's point
+   list, Src/Mapping.cpp:449).  maxRelBaseline / numGoodResiduals (nullable => 0) seed the linearizeAll(true)
+   bookkeeping the context keeps per point.  handles_out[n]: the points' handles. */
+int hs_ba_insert_points(hs_ctx* ctx, const hs_points* pts, const float* maxRelBaseline, const int* numGoodResiduals,
+                        int* handles_out);
+/* EnergyFunctional::insertResidual: n residuals (point handle, target window frame), each appended to its point's
+   residual list; states (nullable => IN). */
+int hs_ba_insert_residuals(hs_ctx* ctx, int n, const int* point_handles, const int* targets, const uint8_t* states);
+/* AddKeyframe's loop (Src/Mapping.cpp:40-56): a residual in state IN from every point not hosted by the newest frame
+   into it, frames and points in window order.  n_added (nullable). */
+int hs_ba_add_residuals_to_newest(hs_ctx* ctx, int* n_added);
+/* EnergyFunctional::dropResidual (swap with the last of the point's list) for n (point handle, target) pairs, in
+   the given order. */
+int hs_ba_drop_residuals(hs_ctx* ctx, int n, const int* point_handles, const int* targets);
+/* linearizeAll(true)'s toRemove loop (Src/FullSystemOptimize.cpp:137-159): every residual not active after the last
+   hs_ba_fix_linearization is dropped, in activeResiduals order.  n_dropped (nullable). */
+int hs_ba_drop_inactive_residuals(hs_ctx* ctx, int* n_dropped);
+/* EnergyFunctional::removePoint for n handles; each host's point list is compacted the way
+   System::flagPointsForRemoval does it (Src/Mapping.cpp:318-326: a removed entry takes the list's last one). */
+int hs_ba_remove_points(hs_ctx* ctx, int n, const int* handles);
+/* System::removeOutliers (Src/FullSystemOptimize.cpp:575-598): every point without residuals is removed.
+   handles_out (nullable, capacity nP): the removed handles in removal order; n_out (nullable). */
+int hs_ba_remove_points_without_residuals(hs_ctx* ctx, int* handles_out, int* n_out);
+/* System::marginalizeFrame (Src/FullSystemMarginalize.cpp:108-176) of window frame `frame`, which must host no point:
+   marginalize = 1 runs EnergyFunctional::marginalizeFrame on the context's HM / bM (as hs_ba_marginalize_frame) and
+   keeps the result; 0 drops the frame's rows / columns instead.  Every residual into the frame is dropped (window
+   order), the frame leaves the window (order-preserving, deleteOutOrder) and its image slot is freed. */
+int hs_ba_remove_frame(hs_ctx* ctx, int frame, int marginalize);
+/* EnergyFunctional::makeIDX: commit the pending edits now (otherwise the next call that needs the device window
+   does).  Returns the committed sizes (nullable). */
+int hs_ba_make_idx(hs_ctx* ctx, int* nF, int* nP, int* nR);
+/* waits for the context's queued device work (keyframe timing; no reference counterpart) */
+int hs_ba_synchronize(hs_ctx* ctx);
+/* EnergyFunctional::HM / bM as the context keeps them (dim*dim, dim; nullable).  Commits first. */
+int hs_ba_get_marginal_prior(hs_ctx* ctx, double* HM, double* bM);
+/* the device-resident per-point state a caller mirrors into its MapPoints (window order; commits first; nullable):
+   idepth, idepth_zero, maxRelBaseline, numGoodResiduals, and HdiF of the last solve (efPoint->HdiF as
+   makeCoarseDepthL0 reads it; idepth_hessian = 1 / HdiF for points with an active residual). */
+int hs_ba_get_point_state(hs_ctx* ctx, float* idepth, float* idepth_zero, float* maxRelBaseline, int* numGoodResiduals,
+                          float* HdiF);
+/* the committed window's structure (commits first): handles[nP], pt_host[nP], nres[nP] (residual-list lengths),
+   res_target[nR] (targets in activeResiduals order: points in window order, each point's list in order).
+   All nullable. */
+int hs_ba_get_structure(hs_ctx* ctx, int* handles, int* pt_host, int* nres, int* res_target);
+
 /* multi-GPU (point sharding): 128-byte RCCL unique id from rank 0, broadcast by the caller.
    hs_comm_init must be called before hs_ba_set_window.  Each rank loads its own point shard (same frames);
    per GN iteration the stitched H/b/energy are all-reduced and the newest-frame energies all-gathered. */

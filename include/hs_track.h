@@ -21,6 +21,7 @@
 #ifndef HS_TRACK_H
 #define HS_TRACK_H
 #include "hs_types.h"
+#include "hs_ba.h" /* hs_ctx (the BA context of hs_tracker_set_ref_ba) */
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -41,6 +42,19 @@ void hs_tracker_destroy(hs_tracker* t);
 int hs_tracker_set_ref(hs_tracker* t, const float* const* ref_pyr, float ab_exposure, const double aff_g2l[2],
                        int n_pts, const float* center_u, const float* center_v, const float* center_idepth,
                        const float* HdiF);
+/* setCoarseTrackingRef(frameHessians) as System::AddKeyframe calls it after optimize (Src/Mapping.cpp:93-100;
+   Src/CoarseTracker.cpp:492-504,105-263), fed from a BA context on the same device: the reference points are the BA
+   window's points whose residual into its newest frame is IN (ph->lastResiduals[0], Src/CoarseTracker.cpp:117),
+   in window order, with their centerProjectedTo and the last solve's HdiF -- gathered and scattered on the device,
+   no host round trip and no host synchronisation (the tracker's stream waits on the BA's).
+   promote_frame = 1: the frame last given to hs_tracker_set_frame* is the newest keyframe and becomes the reference
+   pyramid as it is (no copy; set the next frame to track afterwards); 0: the reference pyramid is rebuilt on the
+   device from the BA's newest frame image.  ab_exposure / aff_g2l: the newest keyframe's. */
+int hs_tracker_set_ref_ba(hs_tracker* t, hs_ctx* ba, int promote_frame, float ab_exposure, const double aff_g2l[2]);
+/* device pointer of level lvl of the frame last given to hs_tracker_set_frame* (w_l*h_l float4 texels
+   (I, dI/dx, dI/dy, 0)), valid until the next set_frame / set_ref_ba(promote) call: a keyframe's image goes to the
+   BA context with hs_ba_set_frame_image_device, without crossing PCIe again. */
+int hs_tracker_frame_texels(hs_tracker* t, int lvl, const void** d_texels);
 /* pc arrays of one level (nullable outputs, capacity w_l*h_l); *n = pc_n[lvl] */
 int hs_tracker_get_ref(hs_tracker* t, int lvl, int* n, float* u, float* v, float* idepth, float* color);
 /* the frame to track: its pyramid and ab_exposure */

@@ -1,0 +1,174 @@
+"""The incremental keyframe window (include/hs_ba.h, "Incremental window"): a keyframe sequence run through
+hs_ba_insert_frame / insert_points / insert_residuals / add_residuals_to_newest / drop_inactive_residuals /
+remove_points_without_residuals / marginalize_points / remove_points / remove_frame must give, at every keyframe, the
+window hs_ba_set_window builds from the same frames, points and residual lists: optimize(6) + the tail bit-identical.
+The reference runs the same edits on its EnergyFunctional (Src/EnergyFunctional.cpp:371-454,456-543,632-646) from
+System::AddKeyframe (Src/Mapping.cpp:12-140)."""
+import types
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _rebuild(drv):
+    """A fresh context built with hs_ba_set_window from the incremental window's committed content, with the device
+    frame state (fp64 FrameOptimizationData + calib) transplanted and the marginal prior set."""
+    from hslam_amd.ba import BAWindow
+    ba, seq = drv.ba, drv.seq
+    st = ba.structure()
+    ps = ba.point_state()
+    fr = ba.frames()
+    HM, bM = ba.marginal_prior()
+    hd = st["handles"]
+    cu = np.array([seq.cand[drv.cand_of[int(h)][0]]["u"][drv.cand_of[int(h)][1]] for h in hd], np.float32)
+    cv = np.array([seq.cand[drv.cand_of[int(h)][0]]["v"][drv.cand_of[int(h)][1]] for h in hd], np.float32)
+    col = np.array([seq.cand[drv.cand_of[int(h)][0]]["color"][drv.cand_of[int(h)][1]] for h in hd], np.float32)
+    wgt = np.array([seq.cand[drv.cand_of[int(h)][0]]["weights"][drv.cand_of[int(h)][1]] for h in hd], np.float32)
+    nF = ba.nF
+    s = types.SimpleNamespace(
+        width=seq.width, height=seq.height, K=seq.K, n_levels=seq.n_levels, n_frames=nF,
+        frames_eval=np.array([seq.evals[k] for k in drv.frames]), frames_state=np.zeros((nF, 10)),
+        frames_state_zero=np.zeros((nF, 10)), frames_exposure=np.ones(nF, np.float32),
+        frames_energyTH=fr["energyTH"].astype(np.float32), frames_id=np.array(drv.frames, np.int32),
+        pyramids=[[seq.pyr0[k]] for k in drv.frames], pt_host=st["pt_host"], pt_u=cu, pt_v=cv,
+        pt_idepth=ps["idepth"], pt_idepth_zero=ps["idepth_zero"], pt_color=col, pt_weights=wgt,
+        res_point=st["res_point"], res_target=st["res_target"], n_points=len(hd))
+    rb = BAWindow(s)
+    rb.debug_set_state(ba.debug_state())
+    rb.set_marginal_prior(HM, bM)
+    return rb, ps
+
+
+def _assert_same(a, b, what):
+    if isinstance(a, dict):
+        for k in a:
+            _assert_same(a[k], b[k], f"{what}.{k}")
+        return
+    a, b = np.asarray(a), np.asarray(b)
+    assert a.shape == b.shape and np.array_equal(a.view(np.uint8), b.view(np.uint8)), what
+
+
+@pytest.mark.parametrize("image_path", ["raw", "host"])
+def test_keyframe_sequence_matches_rebuild(image_path):
+    from hslam_amd.keyframe import KeyframeBA, make_ba_sequence
+    seq = make_ba_sequence(n_kf=11, points_per_kf=200)
+    drv = KeyframeBA(seq, window=8, image_path=image_path)
+    drv.bootstrap()
+    ref = {}
+
+    def check(d, phase):
+        if phase == "optimize":
+            rb, ps = _rebuild(d)
+            n, e = rb.optimize(d.iters)
+            tail = rb.fixLinearization(ps["maxRelBaseline"], ps["numGoodResiduals"])
+            ref.update(energies=e, iters=n, tail=tail, frames=rb.frames(), points=rb.points(),
+                       residuals=rb.residuals())
+            rb.close()
+        else:
+            got = dict(frames=d.ba.frames(), points=d.ba.points(), residuals=d.ba.residuals())
+            for k in ("frames", "points", "residuals"):
+                _assert_same(got[k], ref[k], k)
+
+    checked = 0
+    for k in range(7, 11):
+        info = drv.add_keyframe(k, check=check)
+        _assert_same(info["energies"], ref["energies"], "optimize energies")
+        last = drv.history[-1]
+        assert last["iters"] == ref["iters"]
+        checked += 1
+        # the window slid: 8 frames during optimize, the oldest marginalized after
+        drv.ba.makeIDX()
+        assert len(drv.frames) == 7 and drv.ba.nF == 7
+    assert checked == 4
+    HM, bM = drv.ba.marginal_prior()
+    assert np.isfinite(HM).all() and np.abs(HM).max() > 0  # the marginalized frames / points left a prior
+    drv.ba.close()
+
+
+def test_tail_outputs_match_rebuild():
+    """The tail's per-point outputs (maxRelBaseline / numGoodResiduals kept on the device, HdiF, drop list) equal the
+    rebuilt window's."""
+    from hslam_amd.keyframe import KeyframeBA, make_ba_sequence
+    seq = make_ba_sequence(n_kf=9, points_per_kf=150, seed=11)
+    drv = KeyframeBA(seq, window=8)
+    drv.bootstrap()
+    box = {}
+
+    def check(d, phase):
+        if phase == "optimize":
+            rb, ps = _rebuild(d)
+            rb.optimize(d.iters)
+            box["tail"] = rb.fixLinearization(ps["maxRelBaseline"], ps["numGoodResiduals"])
+            rb.close()
+        else:  # the driver ran the tail: compare its read-backs
+            ps = d.ba.point_state()
+            _assert_same(ps["maxRelBaseline"], box["tail"]["maxRelBaseline"], "maxRelBaseline")
+            _assert_same(ps["numGoodResiduals"], box["tail"]["numGoodResiduals"], "numGoodResiduals")
+            res = d.ba.residuals()
+            _assert_same((res["active"] == 0).astype(np.uint8), box["tail"]["drop"], "toRemove")
+            _assert_same(ps["HdiF"], box["tail"]["HdiF"], "HdiF of the last solve")
+
+    for k in (7, 8):
+        drv.add_keyframe(k, check=check)
+    drv.ba.close()
+
+
+def test_tracker_reference_from_ba_matches_host_path():
+    """hs_tracker_set_ref_ba (device gather of the newest frame's IN residuals + makeCoarseDepthL0) gives the pc_*
+    arrays of hs_tracker_set_ref fed the same points on the host (Src/CoarseTracker.cpp:105-130)."""
+    from hslam_amd.keyframe import KeyframeBA, make_ba_sequence
+    from hslam_amd.scene import make_dir_pyramid
+    from hslam_amd.track import CoarseTracker
+    seq = make_ba_sequence(n_kf=9, points_per_kf=200, seed=5)
+    drv = KeyframeBA(seq, window=8)
+    drv.bootstrap()
+    drv.add_keyframe(7, marginalize=False)
+    ba = drv.ba
+    K4 = np.array([seq.K[0, 0], seq.K[1, 1], seq.K[0, 2], seq.K[1, 2]], np.float32)
+    t_dev = CoarseTracker(seq.width, seq.height, K4, seq.n_levels)
+    t_dev.set_ref_ba(ba, False, 1.0, (0.0, 0.0))
+    # the host path: the same points from read-backs
+    st = ba.structure()
+    res = ba.residuals()
+    newest = ba.nF - 1
+    sel = np.nonzero((st["res_target"] == newest) & (res["state"] == 0))[0]
+    pts = st["res_point"][sel]
+    t_host = CoarseTracker(seq.width, seq.height, K4, seq.n_levels)
+    pyr = make_dir_pyramid(seq.raw[drv.frames[-1]], seq.n_levels)
+    t_host.setCoarseTrackingRef(pyr, 1.0, (0.0, 0.0), res["center"][sel, 0], res["center"][sel, 1],
+                                res["center"][sel, 2], ba.point_state()["HdiF"][pts])
+    assert len(sel) > 100
+    for lvl in range(seq.n_levels):
+        a, b = t_dev.pc(lvl), t_host.pc(lvl)
+        for k in a:
+            assert np.array_equal(a[k], b[k]), (lvl, k)
+    t_dev.close()
+    t_host.close()
+    ba.close()
+
+
+def test_incremental_errors():
+    from hslam_amd._lib import HsError
+    from hslam_amd.keyframe import KeyframeBA, make_ba_sequence
+    seq = make_ba_sequence(n_kf=3, points_per_kf=40, seed=3)
+    drv = KeyframeBA(seq, window=8, capacity=60)
+    drv.bootstrap(2)
+    ba = drv.ba
+    with pytest.raises(HsError):   # frame 0 hosts points
+        ba.removeFrame(0)
+    with pytest.raises(HsError):   # a second residual of the same (point, target)
+        h = ba.structure()["handles"][0]
+        ba.insertResiduals([h], [1])
+        ba.insertResiduals([h], [1])
+    ba.close()
+    drv2 = KeyframeBA(seq, window=8, capacity=50)
+    drv2._insert_frame(0, type("T", (), {"run": staticmethod(lambda p, f, *a, **k: f(*a, **k))})())
+    drv2._insert_frame(1, type("T", (), {"run": staticmethod(lambda p, f, *a, **k: f(*a, **k))})())
+    with pytest.raises(HsError):   # 80 points > the reserved 50
+        for _ in range(2):
+            drv2.ba.insertPoints(np.zeros(40, np.int32), seq.cand[0]["u"], seq.cand[0]["v"], seq.cand[0]["idepth"],
+                                 None, seq.cand[0]["color"], seq.cand[0]["weights"])
+        drv2.ba.makeIDX()
+    drv2.ba.close()
