@@ -406,13 +406,78 @@ def bench_select(args):
     return res
 
 
+def bench_keyframe(args):
+    """System::AddKeyframe's BA part per keyframe (Src/Mapping.cpp:12-140) through the incremental C-ABI, the C4
+    window in steady state: 8 KFs x 250 points per host KF during optimize, a new KF's frame image taken from the
+    tracker's device pyramid, residuals of the old points into it, 250 activated points (+ their residuals), makeIDX,
+    optimize(6) + the tail, toRemove / removeOutliers, the tracker's new reference from the BA on the device,
+    flagPointsForRemoval's marginalization (hs_ba_marginalize_points) and drops, marginalizeFrame of the oldest KF.
+    One step = one keyframe.  Phases are the wall time spent in library calls (each call that reads back waits for
+    its work; setup ends with a stream sync); the driver's own System-level decisions (numpy) are excluded."""
+    from hslam_amd.keyframe import KeyframeBA, make_ba_sequence
+    from hslam_amd.track import CoarseTracker
+
+    n_kf = 7 + args.warmup + args.steps
+    seq = make_ba_sequence(n_kf=n_kf, points_per_kf=max(1, args.points // 8))
+    K4 = np.array([seq.K[0, 0], seq.K[1, 1], seq.K[0, 2], seq.K[1, 2]], np.float32)
+    tr = CoarseTracker(seq.width, seq.height, K4, seq.n_levels)
+    drv = KeyframeBA(seq, window=8, tracker=tr, image_path="device")
+    drv.bootstrap()
+    for k in range(7, 7 + args.warmup):
+        drv.add_keyframe(k)
+    rows = []
+    t0 = time.perf_counter()
+    for k in range(7 + args.warmup, n_kf):
+        rows.append(drv.add_keyframe(k))
+    dt = time.perf_counter() - t0
+    lib = np.array([r["lib_s"] for r in rows]) * 1e3
+    ph = {p: np.array([r["phase_s"].get(p, 0.0) for r in rows]) * 1e3
+          for p in ("setup", "optimize", "tail", "post", "track_frame")}
+    pres = np.array([r["n_res"] for r in rows])
+    iters = np.array([r["iters"] for r in rows])
+    res = {
+        "metric": "keyframes/sec (System::AddKeyframe BA part: window update + optimize(6) + tail + tracker "
+                  "reference + marginalization, C4 8 KF x 2k pts)",
+        "value": 1e3 / float(np.mean(lib)), "unit": "keyframes/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": float(np.mean(lib)), "higher_is_better": True,
+        "scaling": "replicas only", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": "C4 keyframe sequence (BASELINE.json configs[3] window in steady state): 8 KF x "
+                               f"{max(1, args.points // 8)} pts per host KF, 640x480, incremental window "
+                               "(hs_ba_insert_* / remove_* / make_idx), frame image from the tracker's device "
+                               "pyramid, tracker reference handed over on the device",
+                   "points_mean": float(np.mean([r["n_points"] for r in rows])),
+                   "point_residuals_mean": float(np.mean(pres)), "gn_iterations": int(iters.max()),
+                   "marginalized_points_mean": float(np.mean([r.get("marginalized_points", 0) for r in rows])),
+                   "parallelism": "single GPU"},
+        "phase_ms_per_keyframe": {p: float(np.median(v)) for p, v in ph.items()},
+        "phase_ms_per_keyframe_mean": {p: float(np.mean(v)) for p, v in ph.items()},
+        "setup_over_gn": float(np.median(ph["setup"]) / np.median(ph["optimize"])),
+        "driver_wall_ms_per_keyframe": dt * 1e3 / args.steps,
+        "roofline": None,
+        "cpu_baseline": None,
+    }
+    if not args.no_cpu:
+        cb = cpu_baseline(args.points, args.cpu_seconds)
+        # a keyframe's BA on the CPU path: optimize(6) = 6 GN iterations after the initial linearization, plus the
+        # tail's linearizeAll(true): ~7 GN-iteration equivalents of the same window (window edits not counted)
+        kf_ms = 7 * cb["median_ms_per_step"]
+        res["cpu_baseline"] = {"value": 1e3 / kf_ms, "unit": "keyframes/s", "cores": cb["cores"], "kind": "port",
+                               "sample": "7 x the median GN iteration of the oracle on the C4 window (" +
+                                         cb["sample"] + "); the reference's window edits are not timed",
+                               "single_thread_keyframes_per_s": 1e3 / (7 * cb["single_thread"]["median_ms_per_step"])}
+        res["speedup_vs_cpu"] = res["value"] / res["cpu_baseline"]["value"]
+    tr.close()
+    drv.ba.close()
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=("ba", "ba-kitti", "trace", "track", "act", "refine", "select"),
+    ap.add_argument("--workload", choices=("ba", "ba-kitti", "keyframe", "trace", "track", "act", "refine", "select"),
                     default="ba",
                     help="ba = the headline metric (C4, 640x480); ba-kitti = C5's BA half (KITTI 1232x368, 5 levels); "
                          "trace = C5 traceOn; track = C2 CoarseTracker; act = point activation; refine = initializer "
-                         "DirectRefinement; select = PixelSelector")
+                         "DirectRefinement; select = PixelSelector; keyframe = AddKeyframe's BA part per keyframe")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
@@ -428,7 +493,8 @@ def main():
                          "value, else 0 = none; each pair adds ~2 us per step), 1 linearize only, 2 every phase")
     args = ap.parse_args()
     if args.workload not in ("ba", "ba-kitti"):
-        res = {"trace": bench_trace, "track": bench_track, "act": bench_act, "refine": bench_refine, "select": bench_select}[args.workload](args)
+        res = {"trace": bench_trace, "track": bench_track, "act": bench_act, "refine": bench_refine,
+               "select": bench_select, "keyframe": bench_keyframe}[args.workload](args)
         print(json.dumps(res))
         return
 
