@@ -173,7 +173,7 @@ int ensure_capacity(hs_ctx* c, int W, int H, int capP, int capBlk) {
   HS_HIP(hipMemset(c->d_cand, 0xff, sizeof(float) * (size_t)stride * c->nranks));  // NaN, sign set: no candidate
   HS_TRY(dalloc(&c->d_th_hist, HS_TH_BINS));
   HS_TRY(dalloc(&c->d_th_hist2, 1024));
-  HS_TRY(dalloc(&c->d_th_nsurv, 1));
+  HS_TRY(dalloc(&c->d_th_nsurv, 2));
   HS_TRY(dalloc(&c->d_th_surv, HS_TH_SURV));
   HS_TRY(dalloc(&c->d_marg, capP));
   HS_TRY(dalloc(&c->d_adHTdelta, FF * 8));
@@ -1475,12 +1475,13 @@ int hs_comm_init(hs_ctx* c, const char* id128, int rank, int nranks) {
 // test hook (not in the header): setNewFrameEnergyTH's select on n candidates (hs_k_reduce's histogram blocks +
 // the stitch launch's select block); th_out = the newest frame's threshold
 extern "C" int hs_debug_threshold(const float* cand, int n, float thn, float facMedian, float constWeight,
-                                  float overallWeight, float* th_out) {
+                                  float overallWeight, int multi, float* th_out) {
   if (n < 1 || !cand || !th_out) return fail(HS_ERR_INVALID, "bad arguments");
   float *d_c = nullptr, *d_th = nullptr;
-  unsigned int* d_h = nullptr;
+  unsigned int *d_h = nullptr, *d_h2 = nullptr, *d_surv = nullptr, *d_ns = nullptr;
   double* d_e = nullptr;
   HS_TRY(dalloc(&d_c, n)); HS_TRY(dalloc(&d_th, 1)); HS_TRY(dalloc(&d_h, HS_TH_BINS)); HS_TRY(dalloc(&d_e, 4));
+  HS_TRY(dalloc(&d_h2, 1024)); HS_TRY(dalloc(&d_surv, HS_TH_SURV)); HS_TRY(dalloc(&d_ns, 2));
   HS_HIP(hipMemcpy(d_c, cand, sizeof(float) * n, hipMemcpyHostToDevice));
   HsRedArgs a;
   std::memset(&a, 0, sizeof(a));
@@ -1489,14 +1490,80 @@ extern "C" int hs_debug_threshold(const float* cand, int n, float thn, float fac
   a.th_hist = d_h;
   a.nhist = std::min(64, std::max(1, (n + 4095) / 4096));
   hipLaunchKernelGGL(hs_k_reduce, dim3(1 + a.nhist), dim3(256), 0, 0, a);
+  if (multi) {  // the large-window path: pass 2 over np2 blocks, then pass 3 on their survivor list
+    a.th_hist2 = d_h2;
+    a.th_surv = d_surv;
+    a.th_nsurv = d_ns;
+    a.np2 = multi > 1 ? std::min(multi, 64) : std::min(64, std::max(1, (n + 4095) / 4096));
+    hipLaunchKernelGGL(hs_k_th_pass2, dim3(a.np2), dim3(HS_STITCH_NT), 0, 0, a);
+  }
   hipLaunchKernelGGL(hs_k_th_select, dim3(1), dim3(HS_STITCH_NT), 0, 0, a);
   HS_HIP(hipGetLastError());
-  unsigned int hz[HS_TH_BINS];
+  std::vector<unsigned int> hz(HS_TH_BINS), h2(1024), ns(2);
   HS_HIP(hipMemcpy(th_out, d_th, sizeof(float), hipMemcpyDeviceToHost));
-  HS_HIP(hipMemcpy(hz, d_h, sizeof(hz), hipMemcpyDeviceToHost));
-  (void)hipFree(d_c); (void)hipFree(d_th); (void)hipFree(d_h); (void)hipFree(d_e);
+  HS_HIP(hipMemcpy(hz.data(), d_h, sizeof(unsigned int) * HS_TH_BINS, hipMemcpyDeviceToHost));
+  HS_HIP(hipMemcpy(h2.data(), d_h2, sizeof(unsigned int) * 1024, hipMemcpyDeviceToHost));
+  HS_HIP(hipMemcpy(ns.data(), d_ns, sizeof(unsigned int) * 2, hipMemcpyDeviceToHost));
+  for (void* p : {(void*)d_c, (void*)d_th, (void*)d_h, (void*)d_e, (void*)d_h2, (void*)d_surv, (void*)d_ns})
+    (void)hipFree(p);
   for (unsigned int v : hz)
     if (v) return fail(HS_ERR_STATE, "threshold histogram not re-zeroed");
+  for (unsigned int v : h2)
+    if (v) return fail(HS_ERR_STATE, "pass-2 histogram not re-zeroed");
+  if (ns[0] || ns[1]) return fail(HS_ERR_STATE, "survivor count / overflow word not re-zeroed");
+  return HS_OK;
+}
+
+// test hook (not in the header): the product SE3 (hs_se3.h) evaluated on the device (on_device = 1, hs_k_debug_se3,
+// including the doStep's series exp / product, ops 1 and 6) or by the same header compiled for the host (0: the
+// host algebra of setAdjointsF / setPrecalcValues); op and layouts as hs_k_debug_se3.
+extern "C" int hs_debug_se3(int on_device, int op, int n, const double* in14, double* out36) {
+  if (n < 1 || !in14 || !out36 || op < 0 || op > 7) return fail(HS_ERR_INVALID, "bad arguments");
+  if (!on_device) {
+    if (op == 1 || op == 6) return fail(HS_ERR_INVALID, "device-only op");
+    for (int i = 0; i < n; i++) {
+      const double* x = in14 + 14 * i;
+      double* o = out36 + 36 * i;
+      hs::SE3 r;
+      switch (op) {
+        case 0: r = hs::SE3::exp(x); r.toData(o); break;
+        case 2: hs::SE3::fromData(x).log(o); break;
+        case 3: hs::SE3::fromData(x).Adj(o); break;
+        case 4: r = hs::SE3::fromData(x) * hs::SE3::fromData(x + 7); r.toData(o); break;
+        case 5: r = hs::SE3::fromData(x).inverse(); r.toData(o); break;
+        default: hs::SE3::fromData(x).rotationMatrix(o); break;
+      }
+    }
+    return HS_OK;
+  }
+  double *d_in = nullptr, *d_out = nullptr;
+  HS_TRY(dalloc(&d_in, (size_t)14 * n));
+  HS_TRY(dalloc(&d_out, (size_t)36 * n));
+  HS_HIP(hipMemcpy(d_in, in14, sizeof(double) * 14 * n, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(hs_k_debug_se3, dim3((n + 63) / 64), dim3(64), 0, 0, op, n, d_in, d_out);
+  HS_HIP(hipGetLastError());
+  HS_HIP(hipMemcpy(out36, d_out, sizeof(double) * 36 * n, hipMemcpyDeviceToHost));
+  (void)hipFree(d_in);
+  (void)hipFree(d_out);
+  return HS_OK;
+}
+
+// test hooks (not in the header): the system vector the ranks all-reduce (SL + 3 doubles: upper triangle of
+// HA (1+lambda on the diagonal) - HSC / (1+lambda) in the n x n layout, bA - bSC, energy, sum |idepth|, #points) and
+// this rank's newest-frame candidates (cand_stride floats, NaN = none) of the last linearization
+extern "C" int hs_debug_get_sysvec(hs_ctx* c, double* out) {
+  if (!c || !out || c->nF == 0) return fail(HS_ERR_INVALID, "null / no window");
+  HS_HIP(hipMemcpyAsync(out, c->d_sys, sizeof(double) * ((size_t)c->SL() + 3), hipMemcpyDeviceToHost, c->stream));
+  HS_HIP(hipStreamSynchronize(c->stream));
+  return HS_OK;
+}
+extern "C" int hs_debug_get_candidates(hs_ctx* c, float* out, int* stride) {
+  if (!c || !stride || c->nF == 0) return fail(HS_ERR_INVALID, "null / no window");
+  *stride = c->cand_stride;
+  if (out)
+    HS_HIP(hipMemcpyAsync(out, c->d_cand + (size_t)c->rank * c->cand_stride, sizeof(float) * c->cand_stride,
+                          hipMemcpyDeviceToHost, c->stream));
+  HS_HIP(hipStreamSynchronize(c->stream));
   return HS_OK;
 }
 

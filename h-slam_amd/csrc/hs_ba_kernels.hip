@@ -951,10 +951,13 @@ __device__ void red_th_pass2_block(const HsRedArgs& a, int q, unsigned int* sm) 
       }
   }
   __syncthreads();
-  const unsigned int ns = min(ctl[2], (unsigned int)TH_CAP);
+  const bool over = ctl[2] > (unsigned int)TH_CAP;
+  const unsigned int ns = over ? 0u : ctl[2];
   if (tid == 0) {
-    // the block's survivors (a chunk beyond TH_CAP counts as an overflow: pass 3 then re-scans the candidates)
-    const unsigned int base = atomicAdd(a.th_nsurv, ctl[2] > (unsigned int)TH_CAP ? 0x40000000u : ns);
+    // the block's survivors go to the global list; a chunk beyond TH_CAP, or a list that would pass HS_TH_SURV, sets
+    // the overflow word (th_nsurv[1]) instead: pass 3 then re-scans the candidates (the count stays a plain sum)
+    const unsigned int base = atomicAdd(&a.th_nsurv[0], ns);
+    if (over || base + ns > (unsigned int)HS_TH_SURV) atomicOr(&a.th_nsurv[1], 1u);
     ctl[3] = base;
   }
   for (int i = tid; i < 1024; i += nt)
@@ -978,21 +981,27 @@ __device__ void red_energy_th_block(const HsRedArgs& a, unsigned int* sm) {
   const int total = a.nranks * a.stride;
   const bool multi = a.th_hist2 != nullptr;
   for (int i = tid; i < 1024 + 512; i += nt) sm[i] = 0u;
-  if (tid == 0) ctl[2] = 0u;
+  if (tid == 0) {
+    ctl[2] = 0u;
+    ctl[3] = 0u;
+  }
   // ---- pass 1: bins 4 tid .. 4 tid + 3 of the global histogram (then re-zeroed for the next launch)
   unsigned int b1 = 0, kk = 0, n = 0;
   th_pass1(a, wsum, ctl, true, b1, kk, n);
   unsigned int ns = 0, srcn = 0;
   const unsigned int* src = nullptr;  // the survivors pass 3 reads (nullptr: re-scan the candidates)
   if (multi) {
-    const unsigned int gs = *a.th_nsurv;
+    const unsigned int gs = a.th_nsurv[0], over = a.th_nsurv[1];
     for (int i = tid; i < 1024; i += nt) {
       hist2[i] = a.th_hist2[i];
       a.th_hist2[i] = 0u;
     }
     __syncthreads();
-    if (tid == 0) *a.th_nsurv = 0u;
-    if (gs <= (unsigned int)HS_TH_SURV) {
+    if (tid == 0) {
+      a.th_nsurv[0] = 0u;
+      a.th_nsurv[1] = 0u;
+    }
+    if (over == 0u && gs <= (unsigned int)HS_TH_SURV) {
       src = a.th_surv;
       srcn = gs;
     }
@@ -1171,6 +1180,12 @@ __global__ __launch_bounds__(256) void hs_k_reduce(HsRedArgs a) {
     a.hostsum[(size_t)h * NE64 + e] = s;
   }
   HS_TRACE(a, 15);
+}
+
+// the multi-block pass 2 alone (test hook hs_debug_threshold; production runs it inside the stitch launch)
+__global__ __launch_bounds__(HS_STITCH_NT) void hs_k_th_pass2(HsRedArgs a) {
+  __shared__ unsigned int sm[1600 + TH_CAP];
+  red_th_pass2_block(a, blockIdx.x, sm);
 }
 
 __global__ __launch_bounds__(HS_STITCH_NT) void hs_k_th_select(HsRedArgs a) {
@@ -1927,6 +1942,28 @@ __device__ __forceinline__ hs::SE3 se3_mul_step(const hs::SE3& A, const hs::SE3&
   const double inv = rsqrt_step(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
   r.q = hs::Quat{q.x * inv, q.y * inv, q.z * inv, q.w * inv};
   return r;
+}
+
+// test hook (hs_debug_se3): the product SE3 of hs_se3.h and the solve's step forms on the device, one element per
+// thread.  op 0 exp | 1 se3_exp_step (the doStep's series exp) | 2 log | 3 Adj | 4 product | 5 inverse |
+// 6 se3_mul_step (the doStep's product) | 7 rotation matrix.  in: [n][14] (tangent6 or data7, second data7 at +7),
+// out: [n][36].
+__global__ void hs_k_debug_se3(int op, int n, const double* in, double* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double* x = in + 14 * i;
+  double* o = out + 36 * i;
+  hs::SE3 r;
+  switch (op) {
+    case 0: r = hs::SE3::exp(x); r.toData(o); break;
+    case 1: r = se3_exp_step(x); r.toData(o); break;
+    case 2: hs::SE3::fromData(x).log(o); break;
+    case 3: hs::SE3::fromData(x).Adj(o); break;
+    case 4: r = hs::SE3::fromData(x) * hs::SE3::fromData(x + 7); r.toData(o); break;
+    case 5: r = hs::SE3::fromData(x).inverse(); r.toData(o); break;
+    case 6: r = se3_mul_step(hs::SE3::fromData(x), hs::SE3::fromData(x + 7)); r.toData(o); break;
+    default: hs::SE3::fromData(x).rotationMatrix(o); break;
+  }
 }
 
 __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {

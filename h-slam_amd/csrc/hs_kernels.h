@@ -133,7 +133,7 @@ struct HsRedArgs {
   // candidates itself): pass-2 histogram [1024], survivor list [HS_TH_SURV] and its length (zero between launches)
   unsigned int* th_hist2;
   unsigned int* th_surv;
-  unsigned int* th_nsurv;
+  unsigned int* th_nsurv;      // [2]: survivor count, overflow flag
   int np2;
   long long* trace;
 };
@@ -203,10 +203,12 @@ __global__ void hs_k_lin_fix(HsLinArgs a);        // + linearizeAll(true)'s per-
 __global__ void hs_k_lin_exact_fix(HsLinArgs a);
 __global__ void hs_k_lin8(HsLinArgs a);       // production: lane = (point, target slot), 8 points per wave
 __global__ void hs_k_reduce(HsRedArgs a);
-__global__ void hs_k_th_select(HsRedArgs a);    // the threshold select block alone (pass 3 of the multi-block select; test hook)
+__global__ void hs_k_th_select(HsRedArgs a);
+__global__ void hs_k_th_pass2(HsRedArgs a);     // the multi-block pass 2 alone (test hook)    // the threshold select block alone (pass 3 of the multi-block select; test hook)
 __global__ void hs_k_stitch(HsStitchArgs a);
 __global__ void hs_k_solve(HsSolveArgs a);
 __global__ void hs_k_resub(HsResubArgs a);
+__global__ void hs_k_debug_se3(int op, int n, const double* in, double* out);  // test hook
 __global__ void hs_k_apply_step(int n, const float* step, float* idepth, float* idepth_zero);
 __global__ void hs_k_lenergy(int n, const float* idepth, const float* idepth_zero, const float* priorF, float* chunk,
                              double* out);

@@ -19,6 +19,28 @@ import numpy as np
 from ._lib import (check, default_params, hs_camera, hs_frame, hs_points, hs_residuals, load, ptr)
 
 
+SOLVER_FIX_LAMBDA = 1e-5  # Src/EnergyFunctional.cpp:707-708
+
+
+def pack_system_vector(HA, bA, HSC, bSC, energy=0.0, sum_idepth=0.0, n_points=0.0):
+    """The vector the ranks of a point-sharded window all-reduce every GN iteration (hs_ba.cpp launch_reduce,
+    hs_k_stitch): the upper triangle of HA diag(1+lambda) - HSC / (1+lambda) in the n x n layout
+    (solveSystemF's combination, Src/EnergyFunctional.cpp:705-763), bA - bSC, then energy, sum |idepth|, #points.
+    Sums over the ranks of the shards' vectors give the full window's."""
+    n = HA.shape[0]
+    sc = 1.0 / (1 + SOLVER_FIX_LAMBDA)
+    H = np.triu(HA - HSC * sc)
+    H[np.diag_indices(n)] = np.diag(HA) * (1 + SOLVER_FIX_LAMBDA) - np.diag(HSC) * sc
+    return np.concatenate([H.ravel(), bA - bSC, [energy, sum_idepth, n_points]])
+
+
+def unpack_system_vector(v, n):
+    """(H upper triangle mirrored, b, energy) of a packed system vector."""
+    H = v[:n * n].reshape(n, n)
+    H = np.triu(H) + np.triu(H, 1).T
+    return H, v[n * n:n * n + n], v[n * n + n]
+
+
 def _camera(width, height, n_levels, K):
     return hs_camera(int(width), int(height), int(n_levels), 0, float(K[0, 0]), float(K[1, 1]), float(K[0, 2]),
                      float(K[1, 2]))
@@ -204,6 +226,22 @@ class BAWindow:
 
     def synchronize(self):
         check(self.lib.hs_ba_synchronize(self.h))
+
+    def system_vector(self):
+        """This rank's packed system vector of the last linearization (what RCCL all-reduces; test hook)."""
+        out = np.zeros(self.dim * self.dim + self.dim + 3)
+        self.lib.hs_debug_get_sysvec.argtypes = [C.c_void_p, C.c_void_p]
+        check(self.lib.hs_debug_get_sysvec(self.h, ptr(out)))
+        return out
+
+    def candidates(self):
+        """This rank's newest-frame candidates of the last linearization (NaN = none; test hook)."""
+        st = C.c_int()
+        self.lib.hs_debug_get_candidates.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        check(self.lib.hs_debug_get_candidates(self.h, None, C.byref(st)))
+        out = np.zeros(st.value, np.float32)
+        check(self.lib.hs_debug_get_candidates(self.h, ptr(out), C.byref(st)))
+        return out
 
     def debug_state(self) -> bytes:
         buf = C.create_string_buffer(self.lib.hs_debug_state_size())

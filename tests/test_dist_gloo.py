@@ -1,10 +1,13 @@
 """Multi-rank (point-sharded) BA semantics, world_size 2 over gloo on CPU.
 
 The GPU path (hs_comm_init + RCCL) shards points p % nranks: every rank linearizes and
-accumulates its own points, the stitched fp64 systems and energies are all-reduced, and the newest-frame
-energies are all-gathered so each rank selects the same 0.7-quantile threshold.  This test runs that
-exact reduction structure with the CPU oracle on each rank and checks it against the unsharded oracle:
-  * energies and H / b (top and Schur) sum to the full-window values,
+accumulates its own points, the library's packed system vector (hslam_amd.ba.pack_system_vector: the upper
+triangle of HA diag(1+lambda) - HSC / (1+lambda), bA - bSC, energies -- the payload hs_ba.cpp all-reduces) is
+summed over the ranks, and the newest-frame energies are all-gathered so each rank selects the same 0.7-quantile
+threshold.  This test runs that exact reduction structure, with the CPU oracle's systems packed in the library's
+layout on each rank, and checks it against the unsharded window (tests/test_gpu_shard.py checks on the GPU that the
+library's own vector is this layout):
+  * the all-reduced vector equals the full window's packed vector (H / b at the H bar, energy 1e-9),
   * the all-gathered quantile threshold equals the full window's setNewFrameEnergyTH,
   * the shards partition the points and keep every point's residuals together.
 """
@@ -57,8 +60,9 @@ def _worker(rank, world, port, out_dir):
     cand = res["energy_wo"][(shard.res_target == newest) & (res["energy_wo"] >= 0)].astype(np.float32)
     HA, bA = o.accumulate(0)
     HS, bS = o.accumulate(2)
-    # all-reduce of the stitched systems + energy (what the GPU path does over RCCL)
-    flat = torch.from_numpy(np.concatenate([HA.ravel(), bA, HS.ravel(), bS, [e]]).astype(np.float64))
+    # all-reduce of the packed system vector (the library's RCCL payload)
+    from hslam_amd.ba import pack_system_vector
+    flat = torch.from_numpy(pack_system_vector(HA, bA, HS, bS, e, 0.0, float(shard.n_points)))
     dist.all_reduce(flat)
     # all-gather of the newest-frame candidates (padded to a common stride, -1 = none)
     n = torch.tensor([cand.size])
@@ -90,14 +94,11 @@ def test_point_sharded_reduction_matches_full_window(tmp_path):
     HA, bA = o.accumulate(0)
     HS, bS = o.accumulate(2)
     n = HA.shape[0]
-    flat = got["flat"]
-    gHA = flat[:n * n].reshape(n, n)
-    gbA = flat[n * n:n * n + n]
-    gHS = flat[n * n + n:2 * n * n + n].reshape(n, n)
-    gbS = flat[2 * n * n + n:2 * n * n + 2 * n]
-    ge = flat[-1]
-    assert abs(ge - e) <= 1e-9 * abs(e)
-    for g, f in ((gHA, HA), (gbA, bA), (gHS, HS), (gbS, bS)):
+    from hslam_amd.ba import pack_system_vector, unpack_system_vector
+    gH, gb, ge = unpack_system_vector(got["flat"], n)
+    fH, fb, fe = unpack_system_vector(pack_system_vector(HA, bA, HS, bS, e, 0.0, scene.n_points), n)
+    assert abs(ge - fe) <= 1e-9 * abs(fe) and got["flat"][-1] == scene.n_points
+    for g, f in ((gH, fH), (gb, fb)):
         scale = np.abs(f).max()
         assert np.all(np.abs(g - f) <= 1e-4 * (np.abs(f) + 1e-3 * scale))
     # quantile over the union == the full window's threshold (bit-exact: selection is order independent)

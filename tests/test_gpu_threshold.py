@@ -1,7 +1,8 @@
 """setNewFrameEnergyTH's select (Src/FullSystemOptimize.cpp:60-101) on the device: hs_k_reduce's pass-1 histogram
 blocks + the select block of the stitch launch (through the test hook hs_debug_threshold), against nth_element
 restated in numpy fp32.  Bit-exact, including the fallback when more than TH_CAP candidates share the first
-12-bit bin, ties, and windows without a newest-frame residual."""
+12-bit bin, ties, and windows without a newest-frame residual.  multi: the large-window path (pass 2 over up to 64
+blocks with a global survivor list, pass 3 on it), including every block overflowing its LDS survivor buffer."""
 import ctypes as C
 
 import numpy as np
@@ -25,15 +26,15 @@ def ref_threshold(c):
     return f32(th * f32(f32(OW) * f32(OW)))
 
 
-def device_threshold(c):
+def device_threshold(c, multi=0, thn=THN, fac=FAC, cw=CW, ow=OW):
     from hslam_amd._lib import check, load
     lib = load()
     fn = lib.hs_debug_threshold
-    fn.argtypes = [C.c_void_p, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, C.c_void_p]
+    fn.argtypes = [C.c_void_p, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, C.c_int, C.c_void_p]
     fn.restype = C.c_int
     c = np.ascontiguousarray(c, np.float32)
     out = np.zeros(1, np.float32)
-    check(fn(c.ctypes.data, c.size, THN, FAC, CW, OW, out.ctypes.data))
+    check(fn(c.ctypes.data, c.size, thn, fac, cw, ow, int(multi), out.ctypes.data))
     return out[0]
 
 
@@ -56,3 +57,22 @@ def _cases():
 @pytest.mark.parametrize("name,c", list(_cases()), ids=[n for n, _ in _cases()])
 def test_threshold_select_matches_nth_element(name, c):
     assert device_threshold(c) == ref_threshold(c)
+
+
+def _multi_cases():
+    rng = np.random.default_rng(12)
+    yield "spread200k", (rng.lognormal(5.0, 2.0, 200_000)).astype(np.float32), 0
+    yield "spread200k_np2_3", (rng.lognormal(5.0, 2.0, 200_000)).astype(np.float32), 3
+    # every pass-2 block keeps more than TH_CAP (24576) survivors: > 64 * TH_CAP equal candidates
+    yield "equal1.7M", np.full(1_700_000, 417.25, np.float32), 0
+    narrow = (1000.0 + rng.integers(0, 64, 400_000) * np.float32(1.0 / 1024)).astype(np.float32)
+    yield "ties400k", narrow, 0
+    mixed = rng.exponential(50.0, 120_000).astype(np.float32)
+    mixed[::3] = -1.0
+    mixed[1::7] = np.nan
+    yield "mixed120k_np2_7", mixed, 7
+
+
+@pytest.mark.parametrize("name,c,np2", list(_multi_cases()), ids=[n for n, _, _ in _multi_cases()])
+def test_multi_block_threshold_matches_nth_element(name, c, np2):
+    assert device_threshold(c, multi=np2 if np2 > 1 else 1) == ref_threshold(c)

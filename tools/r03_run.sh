@@ -5,7 +5,8 @@ shift
 OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG
 mkdir -p $OUT
 cd $GRAFT_REPO_ROOT
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread "$@" > $OUT/pytest_gpu.txt 2>&1
+T=${@:-tests}
+timeout -k 10 600 python -u -m pytest $T -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.txt 2>&1
 rc=$?
 echo "pytest rc=$rc"; grep -E "PASSED|FAILED|ERROR" $OUT/pytest_gpu.txt | tail -5; tail -25 $OUT/pytest_gpu.txt | grep -v PASSED
 if [ $rc -gt 1 ]; then exit $rc; fi
