@@ -578,12 +578,23 @@ static int gn_iterations(hs_ctx* c, int it0, int K, bool allow_break, double* en
     if (c->gexec && c->graph_hdif != c->d_p_HdiF) drop_graph(c);
     if (!c->gexec) {
       const float* hd = c->d_p_HdiF;
+      float *sv_h = c->d_p_HdiF, *sv_a = c->d_p_HdiF_alt, *sv_s = c->hdif_solved;
       hipGraph_t g = nullptr;
       HS_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-      for (int q = 0; q < 2; q++) {
-        HS_TRY(launch_solve(c, HS_SOLVE | HS_APPLY, -1, true));
-        HS_TRY(launch_linearize(c, 1));
-        HS_TRY(launch_reduce(c));
+      int rc = HS_OK;
+      for (int q = 0; q < 2 && rc == HS_OK; q++) {
+        if ((rc = launch_solve(c, HS_SOLVE | HS_APPLY, -1, true)) != HS_OK) break;
+        if ((rc = launch_linearize(c, 1)) != HS_OK) break;
+        rc = launch_reduce(c);
+      }
+      if (rc != HS_OK) {  // leave the stream out of capture mode and the ping-pong as it was
+        hipGraph_t partial = nullptr;
+        (void)hipStreamEndCapture(c->stream, &partial);
+        if (partial) (void)hipGraphDestroy(partial);
+        c->d_p_HdiF = sv_h;
+        c->d_p_HdiF_alt = sv_a;
+        c->hdif_solved = sv_s;
+        return rc;
       }
       HS_HIP(hipStreamEndCapture(c->stream, &g));
       const hipError_t ie = hipGraphInstantiate(&c->gexec, g, nullptr, nullptr, 0);

@@ -61,6 +61,7 @@ struct hs_tracker {
   bool haveRef = false, haveFrame = false;
   double last_ms = 0;
   long long* d_trace = nullptr;  // HS_KTRACE=1: per-hypothesis phase cycles of hs_k_track (stderr)
+  int trace_cap = 0;
 };
 
 static int upload_pyr(hs_tracker* t, float4** dst, const float* const* pyr) {
@@ -132,8 +133,12 @@ static int run_tries(hs_tracker* t, int n, const double* h_in, int coarsest, int
   a.pass_cutoff = cutoff;
   const char* kt = std::getenv("HS_KTRACE");
   if (kt && kt[0] == '1' && !single_pass) {
-    if (t->d_trace) (void)hipFree(t->d_trace);
-    TS_HIP(hipMalloc((void**)&t->d_trace, sizeof(long long) * 16 * n));
+    if (n > t->trace_cap) {  // grown once to the largest hypothesis count (freed by hs_tracker_destroy)
+      if (t->d_trace) (void)hipFree(t->d_trace);
+      t->d_trace = nullptr;
+      TS_HIP(hipMalloc((void**)&t->d_trace, sizeof(long long) * 16 * n));
+      t->trace_cap = n;
+    }
     TS_HIP(hipMemsetAsync(t->d_trace, 0, sizeof(long long) * 16 * n, t->stream));
     a.trace = t->d_trace;
   }
@@ -277,7 +282,8 @@ void hs_tracker_destroy(hs_tracker* t) {
     for (void* p : ps)
       if (p) (void)hipFree(p);
   }
-  void* ps[] = {t->d_pcn, t->d_bcnt, t->d_boff, t->d_pts, t->d_Tin, t->d_out, t->d_lmlog, t->d_lmlvl, t->d_raw};
+  void* ps[] = {t->d_pcn, t->d_bcnt, t->d_boff, t->d_pts, t->d_Tin, t->d_out, t->d_lmlog, t->d_lmlvl, t->d_raw,
+                t->d_trace};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   if (t->h_out) (void)hipHostFree(t->h_out);
