@@ -29,6 +29,15 @@ constexpr float SCALE_F8 = 50.0f, SCALE_C8 = 50.0f, SCALE_IDEPTH8 = 1.0f;
 constexpr int L8_NW = HS_LIN8_NT / 64;  // waves per block
 constexpr int NTOP = 91;  // AccumulatorApprox entries of one (host, target) block: Data 55 | TopRight 30 | BotRight 6
 constexpr int Q8_N = 17;  // per-pixel quantities summed over the pattern
+#ifndef L8_TAP_GROUP
+#define L8_TAP_GROUP 8  // pixels whose taps may be in flight together (8: no scheduling barrier)
+#endif
+#ifndef L8_MIN_WAVES
+#define L8_MIN_WAVES 1  // waves per SIMD the register budget must allow (launch bounds)
+#endif
+#ifndef L8_PREFETCH
+#define L8_PREFETCH 1   // the next point group's inputs are loaded while the current group computes
+#endif
 
 // Data (r, c), r <= c < 10, in the natural per-lane layout
 __host__ __device__ constexpr int didx(int r, int c) { return r * 10 - (r * (r - 1)) / 2 + (c - r); }
@@ -87,9 +96,114 @@ __device__ __forceinline__ float dpp_ror8(float v) {  // lane l <- lane l ^ 8 (r
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false));
 }
 
+constexpr int NTP = 96;  // NTOP padded to 8 x 12: entries NTOP .. NTP-1 of the reduce-scatter are zero
+static_assert(NTP == 8 * 12 && NTP >= NTOP, "12 entries per point lane");
+
+// entry e of the natural layout -> (kind, r, c): Data (r, c) r <= c < 10 | TopRight (r, c) r < 10, c < 3 | BotRight c
+struct TopEntry {
+  int kind, r, c;
+};
+__host__ __device__ constexpr TopEntry top_entry(int e) {
+  if (e < TR0) {
+    int r = 0;
+    while (didx(r, 9) < e) r++;
+    return TopEntry{0, r, r + (e - didx(r, r))};
+  }
+  if (e < BR0) return TopEntry{1, (e - TR0) / 3, (e - TR0) % 3};
+  if (e < NTOP) return TopEntry{2, 0, e - BR0};
+  return TopEntry{3, 0, 0};
+}
+
+// the lane's contribution to entry e (0 for an inactive residual: its operands are zeroed by the caller)
+struct TopOps {
+  float uu[10], ww[10], jx[10], jy[10], tr0[3], tr1[3], br[6];
+};
+template <int E>
+__device__ __forceinline__ float top_value(const TopOps& o) {
+#pragma clang fp contract(fast)
+  constexpr TopEntry te = top_entry(E);
+  if constexpr (te.kind == 0) return o.uu[te.r] * o.jx[te.c] + o.ww[te.r] * o.jy[te.c];
+  else if constexpr (te.kind == 1) return o.jx[te.r] * o.tr0[te.c] + o.jy[te.r] * o.tr1[te.c];
+  else if constexpr (te.kind == 2) return o.br[te.c];
+  else return 0.f;
+}
+
+__device__ __forceinline__ float swap32_add(float x, float y) {  // lanes < 32: x + x(lane + 32); else y(lane - 32) + y
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float swap16_add(float x, float y) {  // rows 0, 2: x + x(row + 1); rows 1, 3: y(row - 1) + y
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// Reduce-scatter of the NTP entries over the 8 point lanes of every target slot (lane = 8 pl + t): afterwards lane
+// (pl, t) holds, for entries e = 12 pl + j (j < 12), the sum over the slot's 8 lanes.  v_permlane32_swap (pl bit 2)
+// and v_permlane16_swap (pl bit 1) exchange half of the remaining entries between partner lanes in one instruction
+// per pair, DPP row_ror:8 (pl bit 0) the last quarter: 84 exchanges + 84 adds for 96 entries, no LDS.  The entries
+// are formed pairwise as the first exchange consumes them, so at most 48 partial sums are live.
+template <int I>
+__device__ __forceinline__ void rs_step_a(const TopOps& o, float (&a)[48]) {
+  if constexpr (I < 48) {
+    a[I] = swap32_add(top_value<I>(o), top_value<48 + I>(o));
+    rs_step_a<I + 1>(o, a);
+  }
+}
+__device__ __forceinline__ void slot_reduce_scatter(const TopOps& o, float (&out)[12], int pl) {
+  float a[48];
+  rs_step_a<0>(o, a);
+  float b[24];
+#pragma unroll
+  for (int i = 0; i < 24; i++) b[i] = swap16_add(a[i], a[24 + i]);
+  const bool odd = (pl & 1) != 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    const float keep = odd ? b[12 + i] : b[i];
+    const float send = odd ? b[i] : b[12 + i];
+    out[i] = keep + dpp_ror8(send);
+  }
+}
+
+// a point group's inputs of one lane (point pl, target slot t), loaded one group ahead (software pipelining: the
+// next group's loads are in flight while the current group computes)
+struct L8In {
+  float idep, idep0, pu, pv;
+  int res, st_raw;
+  float oldE, oldNewE;
+  uint2 ro2;
+  unsigned fm;
+  float4 jp0, jp1;
+  float bds, hdi;
+  float4 hcd, co0, co1, we0, we1;
+  float priorF;
+};
+__device__ __forceinline__ void l8_load(const HsLinArgs& a, int pc, int t, L8In& in) {
+  const int sl = pc * 8 + t;
+  in.idep = a.idepth[pc];
+  in.idep0 = a.idepth_zero[pc];
+  in.pu = a.u[pc];
+  in.pv = a.v[pc];
+  in.res = a.res_of_slot[sl];
+  in.st_raw = (int)a.r_state[sl];
+  in.oldE = a.r_energy[sl];
+  in.oldNewE = a.r_newEnergy[sl];
+  in.ro2 = reinterpret_cast<const uint2*>(a.res_order)[pc];
+  in.fm = a.p_actmask[pc];
+  in.jp0 = reinterpret_cast<const float4*>(a.p_JpJdF)[sl * 2];
+  in.jp1 = reinterpret_cast<const float4*>(a.p_JpJdF)[sl * 2 + 1];
+  in.bds = a.p_bdSumF[pc];
+  in.hdi = a.p_HdiF_prev[pc];
+  in.hcd = reinterpret_cast<const float4*>(a.p_Hcd)[pc];
+  in.co0 = reinterpret_cast<const float4*>(a.color)[pc * 2];
+  in.co1 = reinterpret_cast<const float4*>(a.color)[pc * 2 + 1];
+  in.we0 = reinterpret_cast<const float4*>(a.weight)[pc * 2];
+  in.we1 = reinterpret_cast<const float4*>(a.weight)[pc * 2 + 1];
+  in.priorF = a.priorF[pc];
+}
+
 }  // namespace
 
-__global__ __launch_bounds__(HS_LIN8_NT) void hs_k_lin8(HsLinArgs a) {
+__global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs a) {
   __shared__ L8Const K;
   __shared__ L8Lds U;
   const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -133,11 +247,12 @@ __global__ __launch_bounds__(HS_LIN8_NT) void hs_k_lin8(HsLinArgs a) {
   L8Scratch& W = U.s[wv];
   const int oslot = t - (t > h ? 1 : 0);           // non-host slot index of t (t != h)
 
-  // accumulators: T natural layout of (host h, target t) over the lane's residuals; D lane (row, col) = (pl, t),
-  // E lane (t, k) = (pl, t) read as (slot pl, row t); C lanes 0..19
-  float T[NTOP];
+  // accumulators: T, the (host h, target t) block in natural layout, spread over the slot's 8 point lanes (lane (pl,
+  // t) keeps entries 12 pl .. 12 pl + 11, summed per point group); D lane (row, col) = (pl, t), E lane (t, k) =
+  // (pl, t) read as (slot pl, row t); C lanes 0..19
+  float Td[12];
 #pragma unroll
-  for (int i = 0; i < NTOP; i++) T[i] = 0.f;
+  for (int i = 0; i < 12; i++) Td[i] = 0.f;
   float D[HS_ND_PROD];
 #pragma unroll
   for (int i = 0; i < HS_ND_PROD; i++) D[i] = 0.f;
@@ -146,28 +261,38 @@ __global__ __launch_bounds__(HS_LIN8_NT) void hs_k_lin8(HsLinArgs a) {
   double eA = 0.0, sidA = 0.0, npA = 0.0;
 
   const int ngroups = (pe - pb + 7) >> 3;
+  auto clamp_p = [&](int g) {
+    const int pp = pb + g * 8 + pl;
+    return pp < pe ? pp : (pe > pb ? pe - 1 : pb);
+  };
+  L8In nx;  // the next group's inputs (loaded ahead; clamped addresses, so always valid)
+#if L8_PREFETCH
+  if (wv < ngroups) l8_load(a, clamp_p(wv), t, nx);
+#endif
   for (int gi = wv; gi < ngroups; gi += a.W) {  // wave-uniform
+#if L8_PREFETCH
+    const L8In in = nx;
+    if (gi + a.W < ngroups) l8_load(a, clamp_p(gi + a.W), t, nx);  // in flight during this group's work
+#else
+    l8_load(a, clamp_p(gi), t, nx);
+    const L8In in = nx;
+#endif
     const int p = pb + gi * 8 + pl;
     const bool valid = p < pe;
     const int pc = valid ? p : pe - 1;
     const int sl = pc * 8 + t;
-    // ---- loads (unconditional, clamped)
-    float idep = a.idepth[pc], idep0 = a.idepth_zero[pc];
-    const float pu = a.u[pc], pv = a.v[pc];
-    const int res = a.res_of_slot[sl];
-    const int st_raw = (int)a.r_state[sl];
-    const float oldE = a.r_energy[sl], oldNewE = a.r_newEnergy[sl];
-    const uint2 ro2 = reinterpret_cast<const uint2*>(a.res_order)[pc];
-    const unsigned fm = a.p_actmask[pc];
-    const float4 jp0 = reinterpret_cast<const float4*>(a.p_JpJdF)[sl * 2];
-    const float4 jp1 = reinterpret_cast<const float4*>(a.p_JpJdF)[sl * 2 + 1];
-    const float bds = a.p_bdSumF[pc], hdi = a.p_HdiF_prev[pc];
-    const float4 hcd = reinterpret_cast<const float4*>(a.p_Hcd)[pc];
-    const float4 co0 = reinterpret_cast<const float4*>(a.color)[pc * 2];
-    const float4 co1 = reinterpret_cast<const float4*>(a.color)[pc * 2 + 1];
-    const float4 we0 = reinterpret_cast<const float4*>(a.weight)[pc * 2];
-    const float4 we1 = reinterpret_cast<const float4*>(a.weight)[pc * 2 + 1];
-    const float priorF = a.priorF[pc];
+    float idep = in.idep, idep0 = in.idep0;
+    const float pu = in.pu, pv = in.pv;
+    const int res = in.res;
+    const int st_raw = in.st_raw;
+    const float oldE = in.oldE, oldNewE = in.oldNewE;
+    const uint2 ro2 = in.ro2;
+    const unsigned fm = in.fm;
+    const float4 jp0 = in.jp0, jp1 = in.jp1;
+    const float bds = in.bds, hdi = in.hdi;
+    const float4 hcd = in.hcd;
+    const float4 co0 = in.co0, co1 = in.co1, we0 = in.we0, we1 = in.we1;
+    const float priorF = in.priorF;
     const float colK[8] = {co0.x, co0.y, co0.z, co0.w, co1.x, co1.y, co1.z, co1.w};
     const float wgtK[8] = {we0.x, we0.y, we0.z, we0.w, we1.x, we1.y, we1.z, we1.w};
     auto res_slot = [&](int qq) -> int { return (int)(int8_t)(((qq < 4 ? ro2.x : ro2.y) >> (8 * (qq & 3))) & 0xffu); };
@@ -335,6 +460,9 @@ __global__ __launch_bounds__(HS_LIN8_NT) void hs_k_lin8(HsLinArgs a) {
       qv[16] = rz * rz;
 #pragma unroll
       for (int i = 0; i < Q8_N; i++) S[i] = S[i] + qv[i];
+      // the taps of at most L8_TAP_GROUP pixels in flight per wave (register budget of two waves per SIMD: the
+      // other wave hides the gather latency the compiler's full hoisting hid at one wave per SIMD)
+      if (L8_TAP_GROUP < 8 && (k + 1) % L8_TAP_GROUP == 0) __builtin_amdgcn_sched_barrier(0);
     }
 
     // ---- state decision + applyRes (Src/OptimizationClasses.cpp:128-133,235-256)
@@ -438,30 +566,35 @@ __global__ __launch_bounds__(HS_LIN8_NT) void hs_k_lin8(HsLinArgs a) {
     if (!a.accumulate) continue;
 
     // ---- AccumulatedTopHessianSSE::addPoint<0> of this lane's residual (AccumulatorApprox update / updateTopRight
-    //      / updateBotRight, Include/MatrixAccumulators.h:754-915): the 13x13 block of (host, t) in natural layout
+    //      / updateBotRight, Include/MatrixAccumulators.h:754-915): the 13x13 block of (host, t) in natural layout,
+    //      this group's 8 residuals of every slot summed by the reduce-scatter (an inactive residual contributes 0)
     {
 #pragma clang fp contract(fast)
-      if (active) {
-        const float a_ = S[1], b_ = S[3], c_ = S[2];  // JIdx2 00, 01, 11
-        float uu[10], ww[10];
+      TopOps o;
 #pragma unroll
-        for (int r = 0; r < 10; r++) {
-          uu[r] = a_ * Jx[r] + b_ * Jy[r];
-          ww[r] = b_ * Jx[r] + c_ * Jy[r];
-        }
-#pragma unroll
-        for (int r = 0; r < 10; r++)
-#pragma unroll
-          for (int c = r; c < 10; c++) T[didx(r, c)] += uu[r] * Jx[c] + ww[r] * Jy[c];
-        const float tr0[3] = {S[4], S[6], S[12]}, tr1[3] = {S[5], S[7], S[13]};
-#pragma unroll
-        for (int r = 0; r < 10; r++)
-#pragma unroll
-          for (int c = 0; c < 3; c++) T[TR0 + r * 3 + c] += Jx[r] * tr0[c] + Jy[r] * tr1[c];
-        const float br[6] = {S[8], S[9], S[14], S[10], S[15], S[16]};
-#pragma unroll
-        for (int i = 0; i < 6; i++) T[BR0 + i] += br[i];
+      for (int r = 0; r < 10; r++) {
+        o.jx[r] = active ? Jx[r] : 0.f;
+        o.jy[r] = active ? Jy[r] : 0.f;
       }
+      const float a_ = active ? S[1] : 0.f, b_ = active ? S[3] : 0.f, c_ = active ? S[2] : 0.f;  // JIdx2 00, 01, 11
+#pragma unroll
+      for (int r = 0; r < 10; r++) {
+        o.uu[r] = a_ * o.jx[r] + b_ * o.jy[r];
+        o.ww[r] = b_ * o.jx[r] + c_ * o.jy[r];
+      }
+      const float tr0[3] = {S[4], S[6], S[12]}, tr1[3] = {S[5], S[7], S[13]};
+#pragma unroll
+      for (int c = 0; c < 3; c++) {
+        o.tr0[c] = active ? tr0[c] : 0.f;
+        o.tr1[c] = active ? tr1[c] : 0.f;
+      }
+      const float br[6] = {S[8], S[9], S[14], S[10], S[15], S[16]};
+#pragma unroll
+      for (int i = 0; i < 6; i++) o.br[i] = active ? br[i] : 0.f;
+      float red[12];
+      slot_reduce_scatter(o, red, pl);
+#pragma unroll
+      for (int i = 0; i < 12; i++) Td[i] += red[i];
     }
     // ---- Schur accumulators (Src/AccumulatedSCHessian.cpp:32-51) through the wave's scratch: accD (lane = (row,
     //      col) of every (o1 <= o2) block), accE / accEB (lane = (slot, row)), accHcc / accbc (lanes 0..19)
@@ -519,16 +652,8 @@ __global__ __launch_bounds__(HS_LIN8_NT) void hs_k_lin8(HsLinArgs a) {
   if (a.trace && tid == 0) a.trace[(size_t)b * 16 + 1] = wall_clock64();
   if (!a.accumulate) return;
 
-  // ---- epilogue: T summed over the wave's 8 point lanes of each slot (fixed tree: ^8, ^16, ^32), then the block
-  //      partial in hs_k_lin's production layout, waves in order
-#pragma unroll
-  for (int i = 0; i < NTOP; i++) {
-    float v = T[i];
-    v = v + dpp_ror8(v);
-    v = v + __shfl_xor(v, 16);
-    v = v + __shfl_xor(v, 32);
-    T[i] = v;
-  }
+  // ---- epilogue: the block partial in hs_k_lin's production layout (T entries from their owner lanes), waves in
+  //      order
   // the energies of the wave (lanes t == 0 of the 8 point slots, in point-slot order)
   double eW = 0.0, sW = 0.0, nW = 0.0;
 #pragma unroll
@@ -539,10 +664,9 @@ __global__ __launch_bounds__(HS_LIN8_NT) void hs_k_lin8(HsLinArgs a) {
   }
   __syncthreads();  // every wave is done with its scratch (the partials area aliases it)
   L8Part& P = U.part;
-  if (pl == 0) {
 #pragma unroll
-    for (int i = 0; i < NTOP; i++) P.T[wv][t][i] = T[i];
-  }
+  for (int i = 0; i < 12; i++)
+    if (12 * pl + i < NTOP) P.T[wv][t][12 * pl + i] = Td[i];
 #pragma unroll
   for (int i = 0; i < HS_ND_PROD; i++) P.DEC[wv][i][lane] = D[i];
 #pragma unroll

@@ -13,6 +13,9 @@ import numpy as np
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_ROOT, "lib", "libhslam_amd.so")
+# experiment builds only (h-slam_amd/csrc/Makefile `variant`); unset, the in-tree product library is loaded
+if os.environ.get("HSLAM_AMD_LIB"):
+    LIB_PATH = os.path.abspath(os.environ["HSLAM_AMD_LIB"])
 
 # data-contract structs (include/hs_types.h)
 
