@@ -6,10 +6,13 @@ Schur complement, 8 keyframes x 2000 active points, 640x480 synthetic scene
 (hslam_amd.scene, seed 20261015), ~13.6k point-residuals.  One *step* = one
 Gauss-Newton iteration of System::optimize (solveSystemF + doStepFromBackup +
 linearizeAll + applyRes + the accumulations), i.e. hs_ba_iterate(1).  Multi-GPU: one rank
-per GPU; by default the metric's own 2000-point window is sharded over the ranks (p % N,
-"strong" scaling); --scaling weak gives every rank its own 2000 points.  Per
-step one RCCL all-reduce of the stitched system and one all-gather of the newest-frame
-energies.  --workload ba-kitti runs the same window at KITTI 1232x368 (C5's BA half).
+per GPU; by default every rank holds 2000 points of one 8-keyframe window of 2000 N points
+("weak" scaling: at N = 1 the metric's own window; SURVEY.md §8e shards points p % N), and
+--scaling strong shards the metric's own 2000-point window over the ranks (at
+2000 points the step is the single-CU solve plus latency-bound launches, so strong scaling
+cannot gain there).  Per step one RCCL exchange: the ranks' system vectors + energies and
+their newest-frame candidates, all-gathered in one group call; every rank sums the vectors in
+rank order and selects the threshold beside the solve.  --workload ba-kitti runs the same window at KITTI 1232x368 (C5's BA half).
 
 JSON line fields follow the driver contract; `roofline` is for the dominant kernel
 (hs_k_linearize, timed with HIP events on the context's own stream), `cpu_baseline` is
@@ -483,9 +486,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--points", type=int, default=2000,
                     help="active points of the window (strong scaling) or per GPU (--scaling weak)")
-    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
-                    help="strong (default): the metric's own 8 KF x --points window sharded over the GPUs; "
-                         "weak: --points per GPU")
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="weak",
+                    help="weak (default): --points per GPU, one window of --points x N points; strong: the "
+                         "metric's own 8 KF x --points window sharded over the GPUs")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--phase-events", type=int, default=None, choices=(0, 1, 2),

@@ -2,8 +2,9 @@
 // device-resident GN loop of System::optimize.  The window state (frames, calib, precalc,
 // systems, steps) lives in HBM between iterations; one GN iteration is the launch sequence
 //   hs_k_solve(SOLVE|APPLY) -> hs_k_lin (fused point step, linearize, per-lane accumulation, block partials)
-//   -> [all-gather] -> hs_k_reduce (per-host fixed-order sums) -> hs_k_stitch (one block per output block of
-//   the system, fixed-order sums) -> [all-reduce of the system vector]
+//   -> hs_k_reduce (per-host fixed-order sums) -> hs_k_stitch (one block per output block of the system,
+//   fixed-order sums) -> [multi-rank: one all-gather of the system vectors + candidates; the next solve launch sums
+//   them in rank order and selects the threshold in its second block]
 // with no host synchronisation and no order-dependent atomics (bit-reproducible).  The host only prepares the window (adjoints, nullspace
 // projector, initial precalc — the reference's once-per-window Eigen/Sophus work) and reads
 // results back.  Device memory is allocated to capacity once per context (hs_ba_reserve, or the first window that
@@ -55,7 +56,7 @@ static void free_buffers(hs_ctx* c) {
       c->d_hostsum, c->d_sys, c->d_sep, c->d_adHost, c->d_adTarget, c->d_adHostF, c->d_adTargetF, c->d_HM, c->d_bM,
       c->d_Nproj, c->d_xAd, c->d_x, c->d_elog, c->d_cand, c->d_tr_lin, c->d_tr_acc, c->d_tr_solve, c->d_tr_st,
       c->d_marg, c->d_adHTdelta, c->d_p_HdiF_alt, c->d_th_hist, c->d_th_hist2, c->d_th_surv, c->d_th_nsurv,
-      c->d_le_chunk, c->d_le_out, c->d_ref_pts, c->d_ref_n, c->d_stage};
+      c->d_le_chunk, c->d_le_out, c->d_ref_pts, c->d_ref_n, c->d_stage, c->d_gsys};
   for (auto& s : c->ps) {
     for (void* p : {(void*)s.u, (void*)s.v, (void*)s.idepth, (void*)s.idepth_zero, (void*)s.priorF, (void*)s.color,
                     (void*)s.weight, (void*)s.relBL, (void*)s.nGood, (void*)s.r_state, (void*)s.r_center})
@@ -91,6 +92,8 @@ static void free_buffers(hs_ctx* c) {
   c->d_le_chunk = nullptr; c->d_le_out = nullptr;
   c->d_ref_pts = nullptr; c->d_ref_n = nullptr;
   c->d_stage = nullptr;
+  c->d_gsys = nullptr;
+  c->gath_pending = c->gath_th = false;
   c->d_stage_cap = 0;
   c->cap_P = c->cap_blk = c->cap_W = c->cap_H = c->cap_stride = 0;
   bind_point_set(c);
@@ -110,7 +113,10 @@ void bind_point_set(hs_ctx* c) {
 // candidate-buffer stride: the same on every rank (max point count over the ranks; one small all-reduce)
 int cand_stride_for(hs_ctx* c, int nP, int* stride) {
   int s = nP > 0 ? nP : 1;
-  if (c->comm) {
+  if (!c->group.empty()) {  // in-process group: the stride fixed at hs_ba_debug_group
+    if (s > c->group_stride) return fail(HS_ERR_INVALID, "shard exceeds the group's candidate stride");
+    s = c->group_stride;
+  } else if (c->comm) {
     int* d_tmp = nullptr;
     HS_TRY(dalloc(&d_tmp, 1));
     HS_HIP(hipMemcpy(d_tmp, &s, sizeof(int), hipMemcpyHostToDevice));
@@ -171,6 +177,7 @@ int ensure_capacity(hs_ctx* c, int W, int H, int capP, int capBlk) {
   c->cap_stride = stride;
   HS_TRY(dalloc(&c->d_cand, (size_t)stride * c->nranks));
   HS_HIP(hipMemset(c->d_cand, 0xff, sizeof(float) * (size_t)stride * c->nranks));  // NaN, sign set: no candidate
+  if (c->multi_rank()) HS_TRY(dalloc(&c->d_gsys, ((size_t)SLmax + 3) * c->nranks));
   HS_TRY(dalloc(&c->d_th_hist, HS_TH_BINS));
   HS_TRY(dalloc(&c->d_th_hist2, 1024));
   HS_TRY(dalloc(&c->d_th_nsurv, 2));
@@ -396,13 +403,7 @@ static int launch_linearize(hs_ctx* c, int fuse, bool marg = false, bool accumul
   return HS_OK;
 }
 
-// all-gather of newest-frame candidates, per-host sums (+ energy, threshold), stitch, all-reduce of the system
-// readback = true: only the separate HA / HSC of the last linearization (d_sep) are re-formed from its host sums;
-// no collective, the system vector and the energies are left as they are
-static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = false, bool readback = false) {
-  if (c->comm && !readback)
-    HS_NCCL(ncclAllGather(c->d_cand + (size_t)c->rank * c->cand_stride, c->d_cand, c->cand_stride, ncclFloat,
-                          c->comm, c->stream));
+static HsRedArgs red_args(hs_ctx* c, bool skip_threshold) {
   HsRedArgs a;
   std::memset(&a, 0, sizeof(a));
   a.nF = c->nF; a.ne = c->ne; a.Q = c->Q; a.nblk = c->nblk;
@@ -415,19 +416,79 @@ static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = fals
   a.constWeight = c->P.frameEnergyTHConstWeight; a.overallWeight = c->P.overallEnergyTHWeight;
   a.skip_threshold = skip_threshold ? 1 : 0;
   a.th_hist = c->d_th_hist;
-  // pass-1 histogram blocks of the threshold select: ~4k candidates each, at most 64
-  a.nhist = skip_threshold ? 0 : std::min(64, std::max(1, (c->nranks * c->cand_stride + 4095) / 4096));
+  a.th_hist2 = c->d_th_hist2;
+  a.th_surv = c->d_th_surv;
+  a.th_nsurv = c->d_th_nsurv;
+  // pass-1 histogram blocks / pass-2 blocks of the multi-block select: ~4k candidates each, at most 64
+  a.nhist = a.np2 = std::min(64, std::max(1, (c->nranks * c->cand_stride + 4095) / 4096));
   a.trace = c->d_tr_acc;
+  return a;
+}
+
+// the gathered systems summed (+ the threshold select when it is pending) by hs_k_combine
+static int launch_combine(hs_ctx* c) {
+  HsSolveArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.nF = c->nF;
+  a.gsys = c->d_gsys; a.nranks = c->nranks; a.gstride = c->SL() + 3; a.sys_out = c->d_sys;
+  a.th_local = c->gath_th ? 1 : 0;
+  a.th = red_args(c, false);
+  hipLaunchKernelGGL(hs_k_combine, dim3(c->gath_th ? 2 : 1), dim3(HS_SOLVE_NT), 0, c->stream, a);
+  HS_HIP(hipGetLastError());
+  c->gath_pending = c->gath_th = false;
+  return HS_OK;
+}
+
+// after the exchange: large windows run the multi-block select over the gathered candidates now (three launches:
+// a 1-block select over 10^5..10^6 candidates would outlast the solve beside it); then either the sums are left to
+// the next solve launch (defer, the fused GN loop) or hs_k_combine forms them now
+static int post_exchange(hs_ctx* c, bool th, bool defer) {
+  c->gath_th = th;
+  c->gath_pending = true;
+  if (th && c->th_multi) {
+    HsRedArgs a = red_args(c, false);
+    a.hist_only = 1;
+    hipLaunchKernelGGL(hs_k_reduce, dim3(a.nhist), dim3(256), 0, c->stream, a);
+    hipLaunchKernelGGL(hs_k_th_pass2, dim3(a.np2), dim3(HS_STITCH_NT), 0, c->stream, a);
+    hipLaunchKernelGGL(hs_k_th_select, dim3(1), dim3(HS_STITCH_NT), 0, c->stream, a);
+    HS_HIP(hipGetLastError());
+    c->gath_th = false;
+  }
+  if (!defer) HS_TRY(launch_combine(c));
+  return HS_OK;
+}
+
+// the one collective of a linearization: every rank's system vector + energies and its candidates, all-gathered in
+// one RCCL group (the sums are formed in rank order on every rank, so every rank solves the same system)
+static int exchange(hs_ctx* c, bool th) {
+  const size_t len = (size_t)c->SL() + 3;
+  HS_NCCL(ncclGroupStart());
+  HS_NCCL(ncclAllGather(c->d_sys, c->d_gsys, len, ncclDouble, c->comm, c->stream));
+  if (th)
+    HS_NCCL(ncclAllGather(c->d_cand + (size_t)c->rank * c->cand_stride, c->d_cand, c->cand_stride, ncclFloat,
+                          c->comm, c->stream));
+  HS_NCCL(ncclGroupEnd());
+  return HS_OK;
+}
+
+// per-host sums (+ energy, threshold), stitch; multi-rank: then the exchange.
+// readback = true: only the separate HA / HSC of the last linearization (d_sep) are re-formed from its host sums;
+// no exchange, the system vector and the energies are left as they are.
+// defer (multi-rank, the fused GN loop): the gathered sums and the threshold select run in the next solve launch.
+static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = false, bool readback = false,
+                         bool defer = false) {
+  const bool xch = c->multi_rank() && !readback;
+  HsRedArgs a = red_args(c, skip_threshold);
+  // single rank: pass 1 of the select in hs_k_reduce, the rest in the stitch launch; multi-rank: after the exchange
+  a.nhist = (skip_threshold || xch) ? 0 : a.nhist;
   if (!readback) {
     hipLaunchKernelGGL(hs_k_reduce, dim3(c->nF * c->Q + 1 + a.nhist), dim3(256), 0, c->stream, a);
     HS_HIP(hipGetLastError());
   }
-  const bool multi = c->th_multi && !skip_threshold && !readback;
-  if (multi) {  // pass 2 by np2 extra blocks of the stitch launch, pass 3 by one block after it
-    a.th_hist2 = c->d_th_hist2;
-    a.th_surv = c->d_th_surv;
-    a.th_nsurv = c->d_th_nsurv;
-    a.np2 = std::min(64, std::max(1, (c->nranks * c->cand_stride + 4095) / 4096));
+  const bool multi = c->th_multi && !skip_threshold && !readback && !xch;
+  if (!multi) {  // pass 2 by np2 extra blocks of the stitch launch, pass 3 by one block after it (multi only)
+    a.th_hist2 = nullptr;
+    a.np2 = 0;
   }
   HsStitchArgs st;
   std::memset(&st, 0, sizeof(st));
@@ -439,7 +500,7 @@ static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = fals
   st.sc = 1.0f / (1 + 1e-5);   // H -= H_sc * (1.0f / (1 + lambda)) (:763)
   st.trace = c->d_tr_st;
   st.red = a;
-  st.red.skip_threshold = (skip_threshold || readback || multi) ? 1 : 0;
+  st.red.skip_threshold = (skip_threshold || readback || multi || xch) ? 1 : 0;
   hipLaunchKernelGGL(hs_k_stitch, dim3(c->nF * (c->nF + 1) / 2 + c->nF + 2 + (multi ? a.np2 : 0)), dim3(HS_STITCH_NT),
                      0, c->stream, st);
   HS_HIP(hipGetLastError());
@@ -449,8 +510,16 @@ static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = fals
     HS_HIP(hipGetLastError());
   }
   if (sep) c->sepValid = true;
-  if (c->comm && !readback)
-    HS_NCCL(ncclAllReduce(c->d_sys, c->d_sys, c->SL() + 3, ncclDouble, ncclSum, c->comm, c->stream));
+  if (xch) {
+    if (!c->group.empty()) {  // the group driver exchanges once every member has reduced
+      c->xch_local = true;
+      c->xch_th = !skip_threshold;
+      c->xch_defer = defer;
+      return HS_OK;
+    }
+    HS_TRY(exchange(c, !skip_threshold));
+    HS_TRY(post_exchange(c, !skip_threshold, defer));
+  }
   return HS_OK;
 }
 
@@ -462,17 +531,30 @@ static int launch_solve(hs_ctx* c, int flags, int iteration, bool log) {
   a.nF = c->nF;
   a.st = c->d_state;
   a.sys = c->d_sys;
+  a.sysE = c->sysE();
+  int grid = 1;
+  if (c->gath_pending) {
+    if (!(flags & HS_SOLVE)) {
+      HS_TRY(launch_combine(c));
+    } else {  // the fused GN loop: the gathered sums in the solve's prefetch, the select as block 1 beside it
+      a.sys = c->d_gsys;
+      a.gsys = c->d_gsys; a.nranks = c->nranks; a.gstride = c->SL() + 3; a.sys_out = c->d_sys;
+      a.th_local = c->gath_th ? 1 : 0;
+      a.th = red_args(c, false);
+      grid = c->gath_th ? 2 : 1;
+      c->gath_pending = c->gath_th = false;
+    }
+  }
   a.HM = c->hm_zero ? nullptr : c->d_HM;
   a.bM = c->d_bM; a.Nproj = c->d_Nproj;
   a.adHostF = c->d_adHostF; a.adTargetF = c->d_adTargetF;
   a.xAd = c->d_xAd; a.pre = c->d_pre; a.x_out = c->d_x;
-  a.sysE = c->sysE();
   a.energy_log = log ? c->d_elog : nullptr;
   a.trace = c->d_tr_solve;
   a.initialCalibHessian = c->P.initialCalibHessian;
   a.thOptIterations = c->P.thOptIterations;
   if (const char* e = std::getenv("HS_SOLVE_DBG")) a.dbg = std::atoi(e);
-  hipLaunchKernelGGL(hs_k_solve, dim3(1), dim3(HS_SOLVE_NT), 0, c->stream, a);
+  hipLaunchKernelGGL(hs_k_solve, dim3(grid), dim3(HS_SOLVE_NT), 0, c->stream, a);
   HS_HIP(hipGetLastError());
   c->h_state_valid = false;
   return HS_OK;
@@ -507,7 +589,8 @@ static int set_loop_counters(hs_ctx* c, int iteration) {
 
 // per-kernel checkpoint summary of the last traced launch (stderr): for every checkpoint the
 // min / median / max over blocks of (checkpoint - the block's start) and the launch span, in us
-static int dump_one(const char* name, const long long* d, int nblocks, double tick_us, hipStream_t s) {
+static int dump_one(const char* name, const long long* d, int nblocks, double tick_us, hipStream_t s,
+                    long long* first = nullptr, long long* last = nullptr) {
   const bool solve = std::string(name) == "solve";
   std::vector<long long> h(solve ? 32 : (size_t)nblocks * 16);  // the solve row has 32 slots (16..25: probes)
   HS_HIP(hipMemcpyAsync(h.data(), d, sizeof(long long) * h.size(), hipMemcpyDeviceToHost, s));
@@ -519,6 +602,8 @@ static int dump_one(const char* name, const long long* d, int nblocks, double ti
     for (int k = 1; k < 16; k++) t1 = std::max(t1, h[b * 16 + k]);
   }
   std::fprintf(stderr, "[hs trace] %-12s blocks %5d span %8.2f us\n", name, nblocks, t0 < 0 ? 0.0 : (t1 - t0) * tick_us);
+  if (first) *first = t0;
+  if (last) *last = t1;
   if (solve && h[0] && h[24] && h[25] && h[15] > h[0])  // slots 24/25: shader clock
     std::fprintf(stderr, "[hs trace] %-12s shader clock %.0f MHz\n", name,
                  (double)(h[25] - h[24]) / ((h[15] - h[0]) * tick_us));
@@ -547,7 +632,8 @@ static int dump_traces(hs_ctx* c) {
   int khz = 0;
   HS_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device));
   const double tick_us = khz > 0 ? 1e3 / khz : 0.01;
-  HS_TRY(dump_one("solve", c->d_tr_solve, 1, tick_us, c->stream));
+  long long f[4] = {0, 0, 0, 0}, l[4] = {0, 0, 0, 0};
+  HS_TRY(dump_one("solve", c->d_tr_solve, 1, tick_us, c->stream, &f[0], &l[0]));
   {  // in-loop shader-clock stamps of the solve (slots 16..23, cycles after slot 16)
     long long h[32];
     HS_HIP(hipMemcpy(h, c->d_tr_solve, sizeof(h), hipMemcpyDeviceToHost));
@@ -556,9 +642,15 @@ static int dump_traces(hs_ctx* c) {
       if (k < 24 || k > 25) std::fprintf(stderr, " s%d=%lld", k, h[k] ? h[k] - h[16] : -1);
     std::fprintf(stderr, "\n");
   }
-  HS_TRY(dump_one("linearize", c->d_tr_lin, c->nblk, tick_us, c->stream));
-  HS_TRY(dump_one("reduce", c->d_tr_acc, c->nF * c->Q + 1, tick_us, c->stream));
-  HS_TRY(dump_one("stitch", c->d_tr_st, c->nF * (c->nF + 1) / 2 + c->nF + 2, tick_us, c->stream));
+  HS_TRY(dump_one("linearize", c->d_tr_lin, c->nblk, tick_us, c->stream, &f[1], &l[1]));
+  HS_TRY(dump_one("reduce", c->d_tr_acc, c->nF * c->Q + 1, tick_us, c->stream, &f[2], &l[2]));
+  HS_TRY(dump_one("stitch", c->d_tr_st, c->nF * (c->nF + 1) / 2 + c->nF + 2, tick_us, c->stream, &f[3], &l[3]));
+  // the last iteration's launch chain on the wall clock: each kernel's first block start -> last checkpoint, and the
+  // gap from one kernel's last checkpoint to the next kernel's first block (launch + end-of-kernel release)
+  if (f[0] > 0 && f[1] > 0 && f[2] > 0 && f[3] > 0)
+    std::fprintf(stderr, "[hs trace] chain us: solve %.2f | gap %.2f | lin %.2f | gap %.2f | reduce %.2f | gap %.2f | "
+                 "stitch %.2f\n", (l[0] - f[0]) * tick_us, (f[1] - l[0]) * tick_us, (l[1] - f[1]) * tick_us,
+                 (f[2] - l[1]) * tick_us, (l[2] - f[2]) * tick_us, (f[3] - l[2]) * tick_us, (l[3] - f[3]) * tick_us);
   return HS_OK;
 }
 
@@ -573,7 +665,7 @@ static int gn_iterations(hs_ctx* c, int it0, int K, bool allow_break, double* en
   // hipGraph replay of iteration pairs: no per-iteration host work (no break test, no events, no tracing, no
   // collectives inside a capture)
   const char* ge = std::getenv("HS_GRAPH");
-  const bool graph = (ge && ge[0] == '1') && !allow_break && nev == 0 && !c->tracing && !c->comm && K >= 2;
+  const bool graph = (ge && ge[0] == '1') && !allow_break && nev == 0 && !c->tracing && !c->multi_rank() && K >= 2;
   if (graph) {
     if (c->gexec && c->graph_hdif != c->d_p_HdiF) drop_graph(c);
     if (!c->gexec) {
@@ -614,7 +706,8 @@ static int gn_iterations(hs_ctx* c, int it0, int K, bool allow_break, double* en
     if (timed) HS_HIP(hipEventRecord(c->ev[4 * k + 1], c->stream));
     HS_TRY(launch_linearize(c, 1));
     if (timed) HS_HIP(hipEventRecord(c->ev[4 * k + 2], c->stream));
-    HS_TRY(launch_reduce(c));
+    // multi-rank: the next iteration's solve launch sums the gathered systems and selects the threshold
+    HS_TRY(launch_reduce(c, false, false, false, k + 1 < K && !allow_break));
     if (timed && all) HS_HIP(hipEventRecord(c->ev[4 * k + 3], c->stream));
     if (allow_break) {
       int cb = 0;
@@ -656,6 +749,37 @@ static int gn_iterations(hs_ctx* c, int it0, int K, bool allow_break, double* en
   if (c->h_ctl[1] != 0) return fail(HS_ERR_NONFINITE, "non-finite GN step");
   for (int q = 0; q <= k; q++)
     if (!std::isfinite(elog[q])) return fail(HS_ERR_NONFINITE, "non-finite energy (isLost)");
+  return HS_OK;
+}
+
+// in-process rank group (hs_ba_debug_group): every member has enqueued its local reduce; each member's system vector +
+// energies (and candidates) are copied into every member's gather buffers on the receiver's stream after the
+// sender's reduce, then every member waits until all copies out of its own buffers are enqueued before it goes on
+// (so no member overwrites d_sys / its candidates while a peer still copies them) and finishes like an RCCL rank
+static int group_exchange(const std::vector<hs_ctx*>& g) {
+  for (hs_ctx* s : g) {
+    if (!s->xch_local) return fail(HS_ERR_STATE, "group member without a pending reduce");
+    HS_HIP(hipEventRecord(s->ev_xch[0], s->stream));
+  }
+  for (hs_ctx* r : g) {
+    const size_t len = (size_t)r->SL() + 3;
+    for (hs_ctx* s : g) {
+      HS_HIP(hipStreamWaitEvent(r->stream, s->ev_xch[0], 0));
+      HS_HIP(hipMemcpyAsync(r->d_gsys + (size_t)s->rank * len, s->d_sys, sizeof(double) * len, hipMemcpyDeviceToDevice,
+                            r->stream));
+      if (r->xch_th && r != s)
+        HS_HIP(hipMemcpyAsync(r->d_cand + (size_t)s->rank * r->cand_stride, s->d_cand + (size_t)s->rank * s->cand_stride,
+                              sizeof(float) * r->cand_stride, hipMemcpyDeviceToDevice, r->stream));
+    }
+    HS_HIP(hipEventRecord(r->ev_xch[1], r->stream));
+  }
+  for (hs_ctx* s : g)
+    for (hs_ctx* r : g)
+      if (r != s) HS_HIP(hipStreamWaitEvent(s->stream, r->ev_xch[1], 0));
+  for (hs_ctx* r : g) {
+    r->xch_local = false;
+    HS_TRY(post_exchange(r, r->xch_th, r->xch_defer));
+  }
   return HS_OK;
 }
 
@@ -756,6 +880,10 @@ void hs_destroy(hs_ctx* c) {
   if (c->h_fstage) (void)hipHostFree(c->h_fstage);
   if (c->ev_upload) (void)hipEventDestroy(c->ev_upload);
   if (c->ev_ready) (void)hipEventDestroy(c->ev_ready);
+  for (auto& e : c->ev_xch)
+    if (e) (void)hipEventDestroy(e);
+  for (hs_ctx* p : c->group)  // a destroyed member leaves its group (the others can no longer exchange)
+    if (p != c) p->group.clear();
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -1455,6 +1583,83 @@ int hs_ba_time_linearize(hs_ctx* c, int reps, double* avg_ms) {
   return HS_OK;
 }
 
+// ---- test hook: an in-process rank group on one device (the multi-rank path's exchange without RCCL)
+int hs_ba_debug_group(hs_ctx** ctxs, int n, int cand_stride) {
+  if (!ctxs || n < 1 || cand_stride < 1) return fail(HS_ERR_INVALID, "bad group args");
+  for (int r = 0; r < n; r++) {
+    hs_ctx* c = ctxs[r];
+    if (!c) return fail(HS_ERR_INVALID, "null group member");
+    if (c->nF != 0 || c->d_state) return fail(HS_ERR_STATE, "hs_ba_debug_group must precede the window");
+    if (c->comm || !c->group.empty()) return fail(HS_ERR_STATE, "context already has ranks");
+    if (c->device != ctxs[0]->device) return fail(HS_ERR_INVALID, "group members on different devices");
+  }
+  for (int r = 0; r < n; r++) {
+    hs_ctx* c = ctxs[r];
+    HS_HIP(hipSetDevice(c->device));
+    for (auto& e : c->ev_xch) HS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->group.assign(ctxs, ctxs + n);
+    c->rank = r;
+    c->nranks = n;
+    c->group_stride = cand_stride;
+  }
+  return HS_OK;
+}
+
+static int group_members(hs_ctx** ctxs, int n, std::vector<hs_ctx*>& g) {
+  if (!ctxs || n < 1 || !ctxs[0] || (int)ctxs[0]->group.size() != n) return fail(HS_ERR_INVALID, "not a rank group");
+  g = ctxs[0]->group;
+  for (int r = 0; r < n; r++)
+    if (ctxs[r] != g[r]) return fail(HS_ERR_INVALID, "contexts out of rank order");
+  for (hs_ctx* c : g) HS_TRY(begin_call(c));
+  return HS_OK;
+}
+
+// hs_ba_linearize over the group (energy_out: the summed energy, every member's)
+int hs_ba_group_linearize(hs_ctx** ctxs, int n, int reset, double* energy_out) {
+  std::vector<hs_ctx*> g;
+  HS_TRY(group_members(ctxs, n, g));
+  for (hs_ctx* c : g) {
+    HS_HIP(hipSetDevice(c->device));
+    if (reset) HS_TRY(reset_states(c));
+    HS_TRY(launch_linearize(c, 0));
+    HS_TRY(launch_reduce(c, false, true));
+    c->haveSystem = true;
+  }
+  HS_TRY(group_exchange(g));
+  double e = 0.0;
+  HS_HIP(hipMemcpyAsync(&e, g[0]->sysE(), sizeof(double), hipMemcpyDeviceToHost, g[0]->stream));
+  for (hs_ctx* c : g) HS_HIP(hipStreamSynchronize(c->stream));
+  if (energy_out) *energy_out = e;
+  return HS_OK;
+}
+
+// hs_ba_iterate over the group: the fused GN loop of every member, the exchange once per iteration
+int hs_ba_group_iterate(hs_ctx** ctxs, int n, int first_iteration, int n_iters, double* energies_out) {
+  std::vector<hs_ctx*> g;
+  HS_TRY(group_members(ctxs, n, g));
+  if (n_iters < 0 || n_iters > kLogCap - 1) return fail(HS_ERR_INVALID, "bad n_iters");
+  for (hs_ctx* c : g) {
+    if (!c->haveSystem) return fail(HS_ERR_STATE, "hs_ba_group_linearize must run first");
+    HS_TRY(set_loop_counters(c, first_iteration));
+  }
+  for (int k = 0; k < n_iters; k++) {
+    for (hs_ctx* c : g) {
+      HS_TRY(launch_solve(c, HS_SOLVE | HS_APPLY, -1, true));
+      HS_TRY(launch_linearize(c, 1));
+      HS_TRY(launch_reduce(c, false, false, false, k + 1 < n_iters));
+    }
+    HS_TRY(group_exchange(g));
+  }
+  std::vector<double> elog(n_iters + 1, 0.0);
+  if (n_iters > 0)
+    HS_HIP(hipMemcpyAsync(elog.data(), g[0]->d_elog, sizeof(double) * n_iters, hipMemcpyDeviceToHost, g[0]->stream));
+  HS_HIP(hipMemcpyAsync(&elog[n_iters], g[0]->sysE(), sizeof(double), hipMemcpyDeviceToHost, g[0]->stream));
+  for (hs_ctx* c : g) HS_HIP(hipStreamSynchronize(c->stream));
+  if (energies_out)
+    for (int q = 0; q < n_iters; q++) energies_out[q] = elog[q + 1];
+  return HS_OK;
+}
+
 int hs_comm_get_unique_id(char* id128) {
   if (!id128) return fail(HS_ERR_INVALID, "null");
   ncclUniqueId id;
@@ -1484,7 +1689,8 @@ int hs_comm_init(hs_ctx* c, const char* id128, int rank, int nranks) {
 // numpy restatement of the reference's pair-wise stitchDoubleInternal.  hostsum [nF][hs_ne(exact)][64], adH / adT
 // [nF*nF][64] (index h + nF t), out [n*n + n], sep [2][n*n + n] (nullable).
 // test hook (not in the header): setNewFrameEnergyTH's select on n candidates (hs_k_reduce's histogram blocks +
-// the stitch launch's select block); th_out = the newest frame's threshold
+// the stitch launch's select block; multi > 0: the multi-block pass 2; multi < 0: the multi-rank path's one-block
+// select of the solve / combine launches, pass 1 in LDS); th_out = the newest frame's threshold
 extern "C" int hs_debug_threshold(const float* cand, int n, float thn, float facMedian, float constWeight,
                                   float overallWeight, int multi, float* th_out) {
   if (n < 1 || !cand || !th_out) return fail(HS_ERR_INVALID, "bad arguments");
@@ -1500,15 +1706,23 @@ extern "C" int hs_debug_threshold(const float* cand, int n, float thn, float fac
   a.frameEnergyTHN = thn; a.facMedian = facMedian; a.constWeight = constWeight; a.overallWeight = overallWeight;
   a.th_hist = d_h;
   a.nhist = std::min(64, std::max(1, (n + 4095) / 4096));
-  hipLaunchKernelGGL(hs_k_reduce, dim3(1 + a.nhist), dim3(256), 0, 0, a);
-  if (multi) {  // the large-window path: pass 2 over np2 blocks, then pass 3 on their survivor list
+  if (multi < 0) {
+    HsSolveArgs sa;
+    std::memset(&sa, 0, sizeof(sa));
+    sa.th_local = 1;
+    sa.th = a;
+    hipLaunchKernelGGL(hs_k_combine, dim3(2), dim3(HS_SOLVE_NT), 0, 0, sa);
+  } else {
+    hipLaunchKernelGGL(hs_k_reduce, dim3(1 + a.nhist), dim3(256), 0, 0, a);
+  }
+  if (multi > 0) {  // the large-window path: pass 2 over np2 blocks, then pass 3 on their survivor list
     a.th_hist2 = d_h2;
     a.th_surv = d_surv;
     a.th_nsurv = d_ns;
     a.np2 = multi > 1 ? std::min(multi, 64) : std::min(64, std::max(1, (n + 4095) / 4096));
     hipLaunchKernelGGL(hs_k_th_pass2, dim3(a.np2), dim3(HS_STITCH_NT), 0, 0, a);
   }
-  hipLaunchKernelGGL(hs_k_th_select, dim3(1), dim3(HS_STITCH_NT), 0, 0, a);
+  if (multi >= 0) hipLaunchKernelGGL(hs_k_th_select, dim3(1), dim3(HS_STITCH_NT), 0, 0, a);
   HS_HIP(hipGetLastError());
   std::vector<unsigned int> hz(HS_TH_BINS), h2(1024), ns(2);
   HS_HIP(hipMemcpy(th_out, d_th, sizeof(float), hipMemcpyDeviceToHost));

@@ -210,6 +210,19 @@ struct hs_ctx {
   // RCCL
   ncclComm_t comm = nullptr;
   int rank = 0, nranks = 1;
+  // the multi-rank exchange (launch_reduce / exchange in hs_ba.cpp): one all-gather per linearization of every
+  // rank's system vector + energies into d_gsys [nranks][SL + 3] and of its newest-frame candidates into d_cand.
+  // gath_pending: a gather whose sums are formed by the next solve launch (the fused GN loop); gath_th: its
+  // threshold select is still to run (block 1 of that launch)
+  double* d_gsys = nullptr;
+  bool gath_pending = false, gath_th = false;
+  // in-process rank group (test hook hs_ba_debug_group): the same exchange by device copies between the contexts of
+  // one process, driven by hs_ba_group_linearize / hs_ba_group_iterate
+  std::vector<hs_ctx*> group;
+  int group_stride = 0;
+  bool xch_local = false, xch_th = false, xch_defer = false;  // group: a local reduce awaits the exchange
+  hipEvent_t ev_xch[2] = {nullptr, nullptr};
+  bool multi_rank() const { return comm != nullptr || !group.empty(); }
 
   // timings of the last optimize / iterate
   double t_lin = 0, t_acc = 0, t_solve = 0, t_timed = 0, t_wall = 0, t_iters = 0;

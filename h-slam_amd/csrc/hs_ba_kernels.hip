@@ -885,36 +885,51 @@ __device__ __forceinline__ unsigned int block_incl_scan(unsigned int x, unsigned
 
 constexpr int TH_CAP = 24576;  // survivors of pass 1 kept in LDS (else pass 3 re-reads the candidates)
 
-// pass 1's bin: the pass-1 histogram's bin b1 holding the k-th smallest candidate (k = (int)(THN * n)) and the
-// rank kk of the wanted value inside b1; n = number of candidates (0: no candidate).  zero: re-zero the histogram for
-// the next launch (its last reader does).  Every thread of the block calls it; blockDim.x == HS_STITCH_NT.
-__device__ __forceinline__ void th_pass1(const HsRedArgs& a, unsigned int* wsum, unsigned int* ctl, bool zero,
-                                         unsigned int& b1, unsigned int& kk, unsigned int& n) {
-  static_assert(HS_TH_BINS == 4 * HS_STITCH_NT, "pass-1 bins: 4 per thread");
-  const int tid = threadIdx.x;
-  uint4 h4 = reinterpret_cast<const uint4*>(a.th_hist)[tid];
-  if (zero) reinterpret_cast<uint4*>(a.th_hist)[tid] = make_uint4(0u, 0u, 0u, 0u);
-  const unsigned int s4 = h4.x + h4.y + h4.z + h4.w;
-  const unsigned int incl = block_incl_scan(s4, wsum, n);
-  if (n == 0) return;
-  const unsigned int k = (unsigned int)(int)(a.frameEnergyTHN * (float)n);
-  if (incl - s4 <= k && k < incl) {
-    unsigned int run = incl - s4;
+// The bin of hist[0 .. nbins) that holds the k-th smallest counted element and k's rank inside it (every thread of
+// the block calls it; any block size with nbins <= 8 * blockDim.x).  k = (int)(thn * total) when thn >= 0, else kin;
+// total = the histogram's sum (0: bin / krem are not set).  zero: the histogram is re-zeroed after it is read.
+__device__ __forceinline__ void hist_pick(unsigned int* hist, int nbins, bool zero, float thn, unsigned int kin,
+                                          unsigned int* wsum, unsigned int* ctl, unsigned int& bin,
+                                          unsigned int& krem, unsigned int& total) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int bpt = (nbins + nt - 1) / nt, b0 = tid * bpt;
+  unsigned int hv[8], s = 0u;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    hv[j] = (j < bpt && b0 + j < nbins) ? hist[b0 + j] : 0u;
+    s += hv[j];
+  }
+  if (zero)
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+      if (j < bpt && b0 + j < nbins) hist[b0 + j] = 0u;
+  const unsigned int incl = block_incl_scan(s, wsum, total);
+  if (total == 0u) return;
+  const unsigned int k = thn >= 0.f ? (unsigned int)(int)(thn * (float)total) : kin;
+  if (s != 0u && incl - s <= k && k < incl) {
+    unsigned int run = incl - s;
     int r = 0;
 #pragma unroll
-    for (int q = 0; q < 3; q++) {
-      const unsigned int cq = q == 0 ? h4.x : (q == 1 ? h4.y : h4.z);
-      if (r == q && k >= run + cq) {
-        run += cq;
-        r = q + 1;
+    for (int j = 0; j < 7; j++)
+      if (r == j && j + 1 < bpt && k >= run + hv[j]) {
+        run += hv[j];
+        r = j + 1;
       }
-    }
-    ctl[0] = 4u * tid + r;
+    ctl[0] = (unsigned int)(b0 + r);
     ctl[1] = k - run;
   }
   __syncthreads();
-  b1 = ctl[0];
-  kk = ctl[1];
+  bin = ctl[0];
+  krem = ctl[1];
+  __syncthreads();  // ctl is rewritten by the next pick
+}
+
+// pass 1's bin: the pass-1 histogram's bin b1 holding the k-th smallest candidate (k = (int)(THN * n)) and the
+// rank kk of the wanted value inside b1; n = number of candidates (0: no candidate).  zero: re-zero the histogram for
+// the next launch (its last reader does).  Every thread of the block calls it.
+__device__ __forceinline__ void th_pass1(const HsRedArgs& a, unsigned int* wsum, unsigned int* ctl, bool zero,
+                                         unsigned int& b1, unsigned int& kk, unsigned int& n) {
+  hist_pick(a.th_hist, HS_TH_BINS, zero, a.frameEnergyTHN, 0u, wsum, ctl, b1, kk, n);
 }
 
 // Multi-block pass 2 (large windows; the stitch launch's np2 extra blocks): block q counts bits 18..9 of its chunk's
@@ -968,26 +983,49 @@ __device__ void red_th_pass2_block(const HsRedArgs& a, int q, unsigned int* sm) 
     if (base + i < (unsigned int)HS_TH_SURV) a.th_surv[base + i] = buf[i];
 }
 
-// sm: >= 1600 + TH_CAP words of LDS (the stitch block's scratch).  blockDim.x == HS_STITCH_NT (4 bins per thread).
-// With a.th_hist2 set, pass 2 is the stitch launch's multi-block one: its histogram and survivor list are read here
-// (and re-zeroed) instead of re-scanning the candidates.
-__device__ void red_energy_th_block(const HsRedArgs& a, unsigned int* sm) {
+// The select block: passes 2 and 3 over the candidates in pass 1's bin (any block size).
+// sm: hist2 [1024] | hist3 [512] | wsum [16] | ctl [48] | buf [cap] (survivors of pass 1 kept in LDS; more: pass 3
+// re-scans the candidates) | local: hist1 [HS_TH_BINS].
+// local = false: pass 1 is the global histogram of hs_k_reduce's histogram blocks (read and re-zeroed here); with
+// a.th_hist2 set, pass 2 is the stitch launch's multi-block one (its histogram and survivor list are read and
+// re-zeroed here instead of re-scanning the candidates).  local = true: the block counts pass 1 itself into LDS
+// (the multi-rank path's select beside the solve, over the all-gathered candidates; a.th_hist2 unused).
+__device__ void th_select_block(const HsRedArgs& a, unsigned int* sm, int cap, bool local) {
   unsigned int* hist2 = sm;          // [1024]
   unsigned int* hist3 = sm + 1024;   // [512]
   unsigned int* wsum = sm + 1536;    // [16]
   unsigned int* ctl = sm + 1552;     // bin, k, survivors, count
-  unsigned int* buf = sm + 1600;     // [TH_CAP]
+  unsigned int* buf = sm + 1600;     // [cap]
+  unsigned int* hist1 = sm + 1600 + cap;  // local: [HS_TH_BINS]
   const int tid = threadIdx.x, nt = blockDim.x;
   const int total = a.nranks * a.stride;
-  const bool multi = a.th_hist2 != nullptr;
+  const bool multi = !local && a.th_hist2 != nullptr;
   for (int i = tid; i < 1024 + 512; i += nt) sm[i] = 0u;
+  if (local)
+    for (int i = tid; i < HS_TH_BINS; i += nt) hist1[i] = 0u;
   if (tid == 0) {
     ctl[2] = 0u;
     ctl[3] = 0u;
   }
-  // ---- pass 1: bins 4 tid .. 4 tid + 3 of the global histogram (then re-zeroed for the next launch)
+  constexpr int TH_U = 16;  // candidates in flight per thread (the scans are latency-bound: one block)
+  if (local) {  // ---- pass 1 (bits 30..19) of every candidate into LDS
+    __syncthreads();
+    for (int i0 = 0; i0 < total; i0 += TH_U * nt) {
+      unsigned int v[TH_U];
+#pragma unroll
+      for (int u = 0; u < TH_U; u++) {
+        const int i = i0 + u * nt + tid;
+        v[u] = i < total ? __float_as_uint(a.cand[i]) : 0xffffffffu;
+      }
+#pragma unroll
+      for (int u = 0; u < TH_U; u++)
+        if (v[u] <= 0x7f800000u) atomicAdd(&hist1[v[u] >> 19], 1u);  // >= 0 and not NaN
+    }
+    __syncthreads();
+  }
+  // ---- pass 1's bin (the global histogram is re-zeroed for the next launch)
   unsigned int b1 = 0, kk = 0, n = 0;
-  th_pass1(a, wsum, ctl, true, b1, kk, n);
+  hist_pick(local ? hist1 : a.th_hist, HS_TH_BINS, !local, a.frameEnergyTHN, 0u, wsum, ctl, b1, kk, n);
   unsigned int ns = 0, srcn = 0;
   const unsigned int* src = nullptr;  // the survivors pass 3 reads (nullptr: re-scan the candidates)
   if (multi) {
@@ -1012,7 +1050,6 @@ __device__ void red_energy_th_block(const HsRedArgs& a, unsigned int* sm) {
   }
   if (!multi) {
     // ---- pass 2: bits 18..9 of the candidates in bin b1; survivors compacted into LDS (order irrelevant: counts)
-    constexpr int TH_U = 16;  // candidates in flight per thread (the scan is latency-bound: one block)
     for (int i0 = 0; i0 < total; i0 += TH_U * nt) {
       unsigned int v[TH_U];
 #pragma unroll
@@ -1025,28 +1062,19 @@ __device__ void red_energy_th_block(const HsRedArgs& a, unsigned int* sm) {
         if (v[u] <= 0x7f800000u && (v[u] >> 19) == b1) {
           atomicAdd(&hist2[(v[u] >> 9) & 1023u], 1u);
           const unsigned int pos = atomicAdd(&ctl[2], 1u);
-          if (pos < (unsigned int)TH_CAP) buf[pos] = v[u];
+          if (pos < (unsigned int)cap) buf[pos] = v[u];
         }
     }
     __syncthreads();
     ns = ctl[2];
-    if (ns <= (unsigned int)TH_CAP) {
+    if (ns <= (unsigned int)cap) {
       src = buf;
       srcn = ns;
     }
   }
-  {
-    const unsigned int c = hist2[tid];
-    unsigned int tot;
-    const unsigned int in2 = block_incl_scan(c, wsum, tot);
-    if (in2 - c <= kk && kk < in2) {
-      ctl[0] = tid;
-      ctl[1] = kk - (in2 - c);
-    }
-    __syncthreads();
-  }
-  const unsigned int p2 = (b1 << 10) | ctl[0];
-  kk = ctl[1];
+  unsigned int b2 = 0, tot2 = 0;
+  hist_pick(hist2, 1024, false, -1.f, kk, wsum, ctl, b2, kk, tot2);
+  const unsigned int p2 = (b1 << 10) | b2;
   // ---- pass 3: bits 8..0 of the survivors with prefix p2
   if (src) {
     for (unsigned int i = tid; i < srcn; i += nt) {
@@ -1054,7 +1082,6 @@ __device__ void red_energy_th_block(const HsRedArgs& a, unsigned int* sm) {
       if ((v >> 9) == p2) atomicAdd(&hist3[v & 511u], 1u);
     }
   } else {
-    constexpr int TH_U = 16;
     for (int i0 = 0; i0 < total; i0 += TH_U * nt) {
       unsigned int v[TH_U];
 #pragma unroll
@@ -1068,21 +1095,19 @@ __device__ void red_energy_th_block(const HsRedArgs& a, unsigned int* sm) {
     }
   }
   __syncthreads();
-  {
-    const unsigned int c = tid < 512 ? hist3[tid] : 0u;
-    unsigned int tot;
-    const unsigned int in3 = block_incl_scan(c, wsum, tot);
-    if (c != 0u && in3 - c <= kk && kk < in3) ctl[3] = tid;
-    __syncthreads();
-  }
+  unsigned int b3 = 0, k3 = 0, tot3 = 0;
+  hist_pick(hist3, 512, false, -1.f, kk, wsum, ctl, b3, k3, tot3);
   if (tid == 0) {
-    const float nth = sqrtf(__uint_as_float((p2 << 9) | ctl[3]));
+    const float nth = sqrtf(__uint_as_float((p2 << 9) | b3));
     float th = nth * a.facMedian;
     th = 26.0f * a.constWeight + th * (1 - a.constWeight);
     th = th * th;
     th *= a.overallWeight * a.overallWeight;
     a.frameTH[a.newest] = th;
   }
+}
+__device__ __forceinline__ void red_energy_th_block(const HsRedArgs& a, unsigned int* sm) {
+  th_select_block(a, sm, TH_CAP, false);
 }
 
 // the (R, C) entry (R <= C) of one (host, target) pair's 13x13 AccumulatorApprox block [calib 4 | xi 6 | a | b | r]
@@ -1149,6 +1174,10 @@ static_assert(2 * ST_LDS >= 1600 + TH_CAP, "the threshold select's LDS lives in 
 __global__ __launch_bounds__(256) void hs_k_reduce(HsRedArgs a) {
   const int nred = a.nF * a.Q;
   const int b = blockIdx.x, tid = threadIdx.x;
+  if (a.hist_only) {  // multi-rank large windows: pass 1 over the all-gathered candidates
+    red_th_hist_block(a, b);
+    return;
+  }
   HS_TRACE(a, 0);
   if (b == nred) { red_energy_block(a); HS_TRACE(a, 15); return; }
   if (b > nred) { red_th_hist_block(a, b - nred - 1); HS_TRACE(a, 15); return; }
@@ -1620,6 +1649,9 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
 //   M  : the permuted system (row-major, stride n), read only
 //   LT : L transposed, LT[i * LSTR + k] = L(k, i); MUST be zero on entry (its upper part stays zero)
 //   W  : scratch of 26 * HS_MAXDIM doubles;  yv : right-hand side in, solution out
+// the multi-rank select block of the solve / combine launches lives in the solve's LDS matrix A
+constexpr int SOLVE_TH_CAP = 2 * HS_MAXDIM * HS_MAXDIM - 1600 - HS_TH_BINS;
+static_assert(SOLVE_TH_CAP >= 1024, "survivor space of the multi-rank select");
 constexpr int LSTR = HS_MAXDIM + 2;  // padded row stride of LT (even: 16 B aligned 4-entry groups)
 constexpr int LDLT_SCRATCH = 26 * HS_MAXDIM;
 
@@ -1982,6 +2014,10 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
   static_assert(sizeof(HsDevState) % 8 == 0, "HsDevState is copied as 8-byte words");
   HsDevState* st = reinterpret_cast<HsDevState*>(st_raw);
   const int tid = threadIdx.x, nt = SOLVE_NT;
+  if (blockIdx.x == 1) {  // multi-rank: setNewFrameEnergyTH over the gathered candidates, beside the solve
+    th_select_block(a.th, reinterpret_cast<unsigned int*>(A), SOLVE_TH_CAP, true);
+    return;
+  }
   HS_TRACE(a, 0);
   if (a.trace && threadIdx.x == 0) a.trace[24] = clock64();  // shader clock (effective-clock probe)
   // entry prefetch: every global input (window state, systems, nullspace factors, b vectors, adjoints) is
@@ -2025,7 +2061,20 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     qc[u] = cc;
   }
   double gs[NUQ], hmq[NUQ], nfv[NF_NU];
-  const double sysE0 = a.sysE[0], sysE1 = a.sysE[1], sysE2 = a.sysE[2];  // energy, sum |idepth|, #points
+  // energy, sum |idepth|, #points (multi-rank: the ranks' values summed in rank order)
+  double sysE0, sysE1, sysE2;
+  if (a.gsys) {
+    const double* ge = a.gsys + nn + n;
+    sysE0 = ge[0]; sysE1 = ge[1]; sysE2 = ge[2];
+    for (int r = 1; r < a.nranks; r++) {
+      sysE0 += ge[r * a.gstride];
+      sysE1 += ge[r * a.gstride + 1];
+      sysE2 += ge[r * a.gstride + 2];
+    }
+    if (tid < 3) a.sys_out[nn + n + tid] = tid == 0 ? sysE0 : (tid == 1 ? sysE1 : sysE2);
+  } else {
+    sysE0 = a.sysE[0]; sysE1 = a.sysE[1]; sysE2 = a.sysE[2];
+  }
   if (solve) {
     // HM (the marginalization prior) entries at the same places, bM for the b entries; one batch with the rest
     if (a.HM) {
@@ -2039,6 +2088,14 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
       for (int u = 0; u < NUQ; u++) {
         gs[u] = a.sys[max(qaddr[u], 0)];
         hmq[u] = qr[u] == -2 ? a.bM[qc[u]] : 0.0;
+      }
+    }
+    if (a.gsys) {  // multi-rank: the gathered vectors (a.sys = rank 0's) summed in rank order, the sum kept
+#pragma unroll
+      for (int u = 0; u < NUQ; u++) {
+        const int ad = max(qaddr[u], 0);
+        for (int r = 1; r < a.nranks; r++) gs[u] += a.gsys[r * a.gstride + ad];
+        if (qaddr[u] >= 0) a.sys_out[ad] = gs[u];
       }
     }
 #pragma unroll
@@ -2356,6 +2413,24 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
   }
   if (a.trace && threadIdx.x == 0) a.trace[25] = clock64();
   HS_TRACE(a, 15);
+}
+
+// multi-rank exchange without a following solve (granular calls, the last GN iteration, optimize's break test):
+// block 0 sums the gathered system vectors in rank order into sys_out (the solve's prefetch forms the same sums),
+// block 1 (th_local) selects the threshold over the gathered candidates
+__global__ __launch_bounds__(SOLVE_NT) void hs_k_combine(HsSolveArgs a) {
+  __shared__ double A[HS_MAXDIM * HS_MAXDIM];
+  if (blockIdx.x == 1) {
+    th_select_block(a.th, reinterpret_cast<unsigned int*>(A), SOLVE_TH_CAP, true);
+    return;
+  }
+  if (!a.gsys) return;  // test hook: the select block alone
+  const int n = 4 + 8 * a.nF, len = n * n + n + 3;
+  for (int i = threadIdx.x; i < len; i += SOLVE_NT) {
+    double s = a.gsys[i];
+    for (int r = 1; r < a.nranks; r++) s += a.gsys[r * a.gstride + i];
+    a.sys_out[i] = s;
+  }
 }
 
 // =====================================================================================================

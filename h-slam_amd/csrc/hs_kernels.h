@@ -135,6 +135,7 @@ struct HsRedArgs {
   unsigned int* th_surv;
   unsigned int* th_nsurv;      // [2]: survivor count, overflow flag
   int np2;
+  int hist_only;               // hs_k_reduce: only the nhist histogram blocks (multi-rank path, after the exchange)
   long long* trace;
 };
 constexpr int HS_TH_BINS = 4096;
@@ -179,6 +180,14 @@ struct HsSolveArgs {
   double initialCalibHessian;
   float thOptIterations;
   int dbg;                     // experiments (env HS_SOLVE_DBG); 0 in production
+  // multi-rank exchange (hs_ba.cpp exchange()): gsys = [nranks][gstride] the ranks' system vectors + energies as
+  // all-gathered, summed here in rank order (every rank the same sums) in place of sys / sysE; sys_out receives the
+  // sum.  th_local: the launch's block 1 runs setNewFrameEnergyTH's select over the gathered candidates (th).
+  const double* gsys;
+  int nranks, gstride;
+  double* sys_out;
+  int th_local;
+  HsRedArgs th;
 };
 
 struct HsResubArgs {
@@ -204,9 +213,10 @@ __global__ void hs_k_lin_exact_fix(HsLinArgs a);
 __global__ void hs_k_lin8(HsLinArgs a);       // production: lane = (point, target slot), 8 points per wave
 __global__ void hs_k_reduce(HsRedArgs a);
 __global__ void hs_k_th_select(HsRedArgs a);
-__global__ void hs_k_th_pass2(HsRedArgs a);     // the multi-block pass 2 alone (test hook)    // the threshold select block alone (pass 3 of the multi-block select; test hook)
+__global__ void hs_k_th_pass2(HsRedArgs a);     // the multi-block pass 2 alone (test hook; multi-rank large windows)
 __global__ void hs_k_stitch(HsStitchArgs a);
 __global__ void hs_k_solve(HsSolveArgs a);
+__global__ void hs_k_combine(HsSolveArgs a);   // multi-rank: the gathered systems summed into sys_out (+ block 1: select)
 __global__ void hs_k_resub(HsResubArgs a);
 __global__ void hs_k_debug_se3(int op, int n, const double* in, double* out);  // test hook
 __global__ void hs_k_apply_step(int n, const float* step, float* idepth, float* idepth_zero);

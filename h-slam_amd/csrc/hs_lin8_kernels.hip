@@ -38,6 +38,9 @@ constexpr int Q8_N = 17;  // per-pixel quantities summed over the pattern
 #ifndef L8_PREFETCH
 #define L8_PREFETCH 1   // the next point group's inputs are loaded while the current group computes
 #endif
+#ifndef L8_LDS_ACC
+#define L8_LDS_ACC 0    // the per-lane accumulators (T slice, accD / accE / accEB / accHcc) live in LDS between groups
+#endif
 
 // Data (r, c), r <= c < 10, in the natural per-lane layout
 __host__ __device__ constexpr int didx(int r, int c) { return r * 10 - (r * (r - 1)) / 2 + (c - r); }
@@ -75,10 +78,20 @@ struct __align__(16) L8Part {
   float T[L8_NW][8][NTOP + 1];
   float DEC[L8_NW][HS_ND_PROD + 6][64];
 };
+#if L8_LDS_ACC
+union __align__(16) L8Lds {
+  L8Scratch s[L8_NW];
+};
+// the per-lane accumulators in LDS, [wave][entry][lane] (lane-consecutive: conflict-free b32 accesses): T slice
+// entries 0..11 (lane (pl, t) holds entries 12 pl + i of slot t's natural layout), accD 12..39, accE / accEB 40..44,
+// accHcc / accbc 45
+constexpr int L8_NACC = 12 + HS_ND_PROD + 6;
+#else
 union __align__(16) L8Lds {
   L8Scratch s[L8_NW];
   L8Part part;
 };
+#endif
 
 // the owner of entry e of lane (t, k) in hs_k_lin's production layout, as an index of the natural T layout
 // (-1: the entry is never read by hs_k_reduce / hs_k_stitch)
@@ -206,6 +219,9 @@ __device__ __forceinline__ void l8_load(const HsLinArgs& a, int pc, int t, L8In&
 __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs a) {
   __shared__ L8Const K;
   __shared__ L8Lds U;
+#if L8_LDS_ACC
+  __shared__ float ACC[L8_NW][L8_NACC][64];
+#endif
   const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int pl = lane >> 3, t = lane & 7;  // point of the group, target slot
   const int b = blockIdx.x;
@@ -250,6 +266,10 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
   // accumulators: T, the (host h, target t) block in natural layout, spread over the slot's 8 point lanes (lane (pl,
   // t) keeps entries 12 pl .. 12 pl + 11, summed per point group); D lane (row, col) = (pl, t), E lane (t, k) =
   // (pl, t) read as (slot pl, row t); C lanes 0..19
+#if L8_LDS_ACC
+#pragma unroll
+  for (int i = 0; i < L8_NACC; i++) ACC[wv][i][lane] = 0.f;
+#else
   float Td[12];
 #pragma unroll
   for (int i = 0; i < 12; i++) Td[i] = 0.f;
@@ -258,6 +278,7 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
   for (int i = 0; i < HS_ND_PROD; i++) D[i] = 0.f;
   float E[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   float C = 0.f;
+#endif
   double eA = 0.0, sidA = 0.0, npA = 0.0;
 
   const int ngroups = (pe - pb + 7) >> 3;
@@ -593,8 +614,13 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
       for (int i = 0; i < 6; i++) o.br[i] = active ? br[i] : 0.f;
       float red[12];
       slot_reduce_scatter(o, red, pl);
+#if L8_LDS_ACC
+#pragma unroll
+      for (int i = 0; i < 12; i++) ACC[wv][i][lane] += red[i];
+#else
 #pragma unroll
       for (int i = 0; i < 12; i++) Td[i] += red[i];
+#endif
     }
     // ---- Schur accumulators (Src/AccumulatedSCHessian.cpp:32-51) through the wave's scratch: accD (lane = (row,
     //      col) of every (o1 <= o2) block), accE / accEB (lane = (slot, row)), accHcc / accbc (lanes 0..19)
@@ -616,6 +642,14 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
       const int eo = es - (es > h ? 1 : 0);
       const int cr = (lane >> 2) & 3, ccol = lane & 3;
       const unsigned long long wbits = actBits;
+#if L8_LDS_ACC
+      float D[HS_ND_PROD], E[5], C;
+#pragma unroll
+      for (int i = 0; i < HS_ND_PROD; i++) D[i] = ACC[wv][12 + i][lane];
+#pragma unroll
+      for (int i = 0; i < 5; i++) E[i] = ACC[wv][12 + HS_ND_PROD + i][lane];
+      C = ACC[wv][12 + HS_ND_PROD + 5][lane];
+#endif
 #pragma unroll
       for (int qp = 0; qp < 8; qp++) {
         const unsigned mq = (unsigned)(wbits >> (qp * 8)) & 0xffu;  // uniform
@@ -646,6 +680,13 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
         const float hr = W.pp[qp][2 + cr], hc = W.pp[qp][2 + ccol];  // per-lane LDS addresses, no select chains
         C += lane < 16 ? (hdf * hr) * hc : (bsf * hdf) * hc;
       }
+#if L8_LDS_ACC
+#pragma unroll
+      for (int i = 0; i < HS_ND_PROD; i++) ACC[wv][12 + i][lane] = D[i];
+#pragma unroll
+      for (int i = 0; i < 5; i++) ACC[wv][12 + HS_ND_PROD + i][lane] = E[i];
+      ACC[wv][12 + HS_ND_PROD + 5][lane] = C;
+#endif
     }
     __builtin_amdgcn_wave_barrier();  // the scratch is rewritten by the next group
   }
@@ -663,6 +704,7 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
     nW += __shfl(npA, j * 8);
   }
   __syncthreads();  // every wave is done with its scratch (the partials area aliases it)
+#if !L8_LDS_ACC
   L8Part& P = U.part;
 #pragma unroll
   for (int i = 0; i < 12; i++)
@@ -672,6 +714,7 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
 #pragma unroll
   for (int i = 0; i < 5; i++) P.DEC[wv][HS_ND_PROD + i][lane] = E[i];
   P.DEC[wv][HS_ND_PROD + 5][lane] = C;
+#endif
   __shared__ double se[L8_NW][3];
   if (lane == 0) {
     se[wv][0] = eW;
@@ -689,15 +732,28 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
       const int tt = l >> 3, kk = l & 7;
       const int m = owner_map(e, kk);
       if (m >= 0) {
+#if L8_LDS_ACC
+        const int sl8 = (m / 12) * 8 + tt, si = m % 12;  // entry m of slot tt: lane (m / 12, tt), slice entry m % 12
+        s = ACC[0][si][sl8];
+#pragma unroll
+        for (int w = 1; w < L8_NW; w++) s += ACC[w][si][sl8];
+#else
         s = P.T[0][tt][m];
 #pragma unroll
         for (int w = 1; w < L8_NW; w++) s += P.T[w][tt][m];
+#endif
       }
     } else {
       const int d = e - HS_E_TOP;
+#if L8_LDS_ACC
+      s = ACC[0][12 + d][l];
+#pragma unroll
+      for (int w = 1; w < L8_NW; w++) s += ACC[w][12 + d][l];
+#else
       s = P.DEC[0][d][l];
 #pragma unroll
       for (int w = 1; w < L8_NW; w++) s += P.DEC[w][d][l];
+#endif
     }
     out[i] = s;
   }

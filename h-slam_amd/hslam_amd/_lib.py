@@ -104,6 +104,10 @@ SIGNATURES = {
     "hs_debug_set_state": ([VP, VP], I),
     "hs_comm_get_unique_id": ([VP], I),
     "hs_comm_init": ([VP, VP, I, I], I),
+    # test hooks (not in the header): an in-process rank group on one device, the multi-rank exchange by copies
+    "hs_ba_debug_group": ([VP, I, I], I),
+    "hs_ba_group_linearize": ([VP, I, I, VP], I),
+    "hs_ba_group_iterate": ([VP, I, I, I, VP], I),
     # include/hs_track.h
     "hs_tracker_create": ([VP, VP, I, I, I, I, VP], I),
     "hs_tracker_destroy": ([VP], None),

@@ -260,6 +260,29 @@ class BAWindow:
     def __del__(self):
         self.close()
 
+    @staticmethod
+    def rank_group(shards, device: int = 0, params=None):
+        """Test hook: the shards as the ranks of one in-process group on `device` (hs_ba_debug_group): the
+        library's multi-rank path (one exchange of system vectors + candidates per linearization, rank-order sums,
+        the select beside the solve) with device copies in place of the RCCL all-gather.  Returns RankGroup."""
+        ws = []
+        for _ in shards:
+            w = BAWindow.__new__(BAWindow)
+            w.lib = load()
+            w.params = params if params is not None else default_params()
+            h = C.c_void_p()
+            check(w.lib.hs_create(C.byref(h), C.byref(w.params), device))
+            w.h = h
+            ws.append(w)
+        stride = max(s.n_points for s in shards)
+        arr = (C.c_void_p * len(ws))(*[w.h.value for w in ws])
+        check(ws[0].lib.hs_ba_debug_group(C.cast(arr, C.c_void_p), len(ws), int(stride)))
+        for w, s in zip(ws, shards):
+            w.nF = s.n_frames
+            w.dim = 4 + 8 * w.nF
+            w._set_window(s, None)
+        return RankGroup(ws)
+
     # --------------------------------------------------------------- reference call surface
     def linearizeAll(self, reset=False):
         e = C.c_double()
@@ -409,3 +432,27 @@ class BAWindow:
     def comm_init(self, uid: bytes, rank: int, nranks: int):
         buf = C.create_string_buffer(uid, 128)
         check(self.lib.hs_comm_init(self.h, buf, rank, nranks))
+
+
+class RankGroup:
+    """The members of BAWindow.rank_group, driven together (hs_ba_group_linearize / hs_ba_group_iterate)."""
+
+    def __init__(self, members):
+        self.members = members
+        self._arr = (C.c_void_p * len(members))(*[w.h.value for w in members])
+
+    def linearizeAll(self, reset=False):
+        e = C.c_double()
+        check(self.members[0].lib.hs_ba_group_linearize(C.cast(self._arr, C.c_void_p), len(self.members), int(reset),
+                                                        C.byref(e)))
+        return e.value
+
+    def iterate(self, first_iteration, n_iters):
+        e = np.zeros(n_iters)
+        check(self.members[0].lib.hs_ba_group_iterate(C.cast(self._arr, C.c_void_p), len(self.members),
+                                                      first_iteration, n_iters, ptr(e)))
+        return e
+
+    def close(self):
+        for w in self.members:
+            w.close()

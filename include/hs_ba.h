@@ -229,7 +229,10 @@ int hs_ba_get_structure(hs_ctx* ctx, int* handles, int* pt_host, int* nres, int*
 
 /* multi-GPU (point sharding): 128-byte RCCL unique id from rank 0, broadcast by the caller.
    hs_comm_init must be called before hs_ba_set_window.  Each rank loads its own point shard (same frames);
-   per GN iteration the stitched H/b/energy are all-reduced and the newest-frame energies all-gathered. */
+   per linearization ONE exchange (two all-gathers in one RCCL group call): every rank's stitched system vector +
+   energies and its newest-frame energies.  Every rank sums the vectors in rank order (the same system on every
+   rank, replacing the reduction of Src/EnergyFunctional.cpp:155-220 over the reference's threads) and selects
+   setNewFrameEnergyTH over the gathered energies beside the solve. */
 int hs_comm_get_unique_id(char* id128);
 int hs_comm_init(hs_ctx* ctx, const char* id128, int rank, int nranks);
 

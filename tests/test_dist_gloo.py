@@ -1,14 +1,16 @@
 """Multi-rank (point-sharded) BA semantics, world_size 2 over gloo on CPU.
 
 The GPU path (hs_comm_init + RCCL) shards points p % nranks: every rank linearizes and
-accumulates its own points, the library's packed system vector (hslam_amd.ba.pack_system_vector: the upper
-triangle of HA diag(1+lambda) - HSC / (1+lambda), bA - bSC, energies -- the payload hs_ba.cpp all-reduces) is
-summed over the ranks, and the newest-frame energies are all-gathered so each rank selects the same 0.7-quantile
-threshold.  This test runs that exact reduction structure, with the CPU oracle's systems packed in the library's
-layout on each rank, and checks it against the unsharded window (tests/test_gpu_shard.py checks on the GPU that the
-library's own vector is this layout):
-  * the all-reduced vector equals the full window's packed vector (H / b at the H bar, energy 1e-9),
-  * the all-gathered quantile threshold equals the full window's setNewFrameEnergyTH,
+accumulates its own points, then ONE exchange per linearization all-gathers every rank's packed system vector
+(hslam_amd.ba.pack_system_vector: the upper triangle of HA diag(1+lambda) - HSC / (1+lambda), bA - bSC, energies)
+and its newest-frame candidates (hs_ba.cpp exchange(): two all-gathers in one RCCL group); every rank sums the
+gathered vectors in rank order (so every rank solves the same system, bit for bit) and selects the same
+0.7-quantile threshold over the gathered candidates.  This test runs that exchange, with the CPU oracle's systems
+packed in the library's layout on each rank, and checks it against the unsharded window (tests/test_gpu_shard.py
+runs the library's own exchange with two ranks on one GPU):
+  * both ranks' rank-order sums are bit-identical and equal the full window's packed vector (H / b at the H bar,
+    energy 1e-9),
+  * the gathered quantile threshold equals the full window's setNewFrameEnergyTH,
   * the shards partition the points and keep every point's residuals together.
 """
 import os
@@ -60,10 +62,14 @@ def _worker(rank, world, port, out_dir):
     cand = res["energy_wo"][(shard.res_target == newest) & (res["energy_wo"] >= 0)].astype(np.float32)
     HA, bA = o.accumulate(0)
     HS, bS = o.accumulate(2)
-    # all-reduce of the packed system vector (the library's RCCL payload)
+    # the exchange: all-gather of the packed system vectors (the library's payload), summed in rank order
     from hslam_amd.ba import pack_system_vector
-    flat = torch.from_numpy(pack_system_vector(HA, bA, HS, bS, e, 0.0, float(shard.n_points)))
-    dist.all_reduce(flat)
+    mine = torch.from_numpy(pack_system_vector(HA, bA, HS, bS, e, 0.0, float(shard.n_points)))
+    vecs = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(vecs, mine)
+    flat = vecs[0].clone()
+    for v in vecs[1:]:
+        flat += v
     # all-gather of the newest-frame candidates (padded to a common stride, -1 = none)
     n = torch.tensor([cand.size])
     sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
@@ -75,8 +81,7 @@ def _worker(rank, world, port, out_dir):
     dist.all_gather(gathered, torch.from_numpy(pad))
     union = np.concatenate([g.numpy() for g in gathered])
     union = union[union >= 0]
-    if rank == 0:
-        np.savez(os.path.join(out_dir, "dist.npz"), flat=flat.numpy(), union=union)
+    np.savez(os.path.join(out_dir, f"dist{rank}.npz"), flat=flat.numpy(), union=union)
     dist.destroy_process_group()
 
 
@@ -86,7 +91,10 @@ def test_point_sharded_reduction_matches_full_window(tmp_path):
 
     world = 2
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
-    got = np.load(tmp_path / "dist.npz")
+    got = np.load(tmp_path / "dist0.npz")
+    got1 = np.load(tmp_path / "dist1.npz")
+    assert np.array_equal(got["flat"], got1["flat"])  # every rank solves the same system
+    assert np.array_equal(np.sort(got["union"]), np.sort(got1["union"]))
     scene = make_ba_scene(n_points=240, seed=7)
     o = OracleBA(scene, nthreads=1)
     e = o.linearize_all(reset=True)

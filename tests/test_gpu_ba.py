@@ -293,9 +293,10 @@ def test_runs_are_bit_reproducible(scene2k):
 
 
 def test_single_rank_communicator_matches_plain(scene_small):
-    """The RCCL path of the library on a 1-rank communicator (hs_comm_init(ctx, id, 0, 1)): the candidate
-    all-gather, the system all-reduce and the stride agreement are enqueued every iteration and must leave the
-    results bit-identical to the communicator-free window."""
+    """The RCCL path of the library on a 1-rank communicator (hs_comm_init(ctx, id, 0, 1)): the exchange (the
+    grouped all-gather of the system vector and the candidates), the rank-order sums in the solve's prefetch /
+    hs_k_combine, the one-block select beside the solve and the stride agreement are enqueued every iteration and
+    must leave the results bit-identical to the communicator-free window."""
     import os
     from hslam_amd.ba import BAWindow
     os.environ["HS_ACC_EXACT"] = "1"

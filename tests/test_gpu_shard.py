@@ -58,3 +58,46 @@ def test_two_shards_reproduce_the_full_window(scene2k):
         assert np.array_equal(rs["energy"], rf["energy"][sel])
     for w in [full] + shards:
         w.close()
+
+
+def test_rank_group_runs_the_multi_rank_path(scene2k):
+    """The library's multi-rank path with two ranks on one GPU (the in-process group of hs_ba_debug_group: the
+    exchange is device copies where a multi-GPU run all-gathers over RCCL; every other launch is the RCCL path's):
+    one exchange of [system vector | energies] and candidates per linearization, the rank-order sums, the
+    threshold select over the gathered candidates beside the solve (block 1 of the solve launch) or in hs_k_combine.
+      * after a linearization every rank holds the same summed vector, bit-equal to the sum of the two shards'
+        own vectors in rank order, and the full window's threshold (bit-exact: the union of the candidates);
+      * the fused GN loop (deferred sums: the solve's prefetch) keeps both ranks' frame states bit-identical and
+        follows the full window's trajectory (rel 1e-3, the optimize-trajectory bar)."""
+    from hslam_amd.ba import BAWindow
+    shard_scenes = [scene2k.shard(r, 2) for r in range(2)]
+    full = BAWindow(scene2k)
+    ef = full.linearizeAll(reset=True)
+    alone = [BAWindow(s) for s in shard_scenes]
+    for w in alone:
+        w.linearizeAll(reset=True)
+    vsum = alone[0].system_vector() + alone[1].system_vector()
+    grp = BAWindow.rank_group(shard_scenes)
+    eg = grp.linearizeAll(reset=True)
+    assert abs(eg - ef) <= 1e-9 * abs(ef)
+    newest = scene2k.n_frames - 1
+    th_full = full.frames()["energyTH"][newest]
+    for m in grp.members:
+        assert np.array_equal(m.system_vector(), vsum)
+        assert m.frames()["energyTH"][newest] == th_full
+    K = 4
+    ef_it = full.iterate(0, K)
+    eg_it = grp.iterate(0, K)
+    assert np.all(np.abs(eg_it - ef_it) <= 1e-3 * np.abs(ef_it))
+    s0, s1 = (m.frames() for m in grp.members)
+    assert np.array_equal(s0["state"], s1["state"]) and np.array_equal(s0["energyTH"], s1["energyTH"])
+    sf = full.frames()["state"]
+    assert np.allclose(s0["state"], sf, rtol=1e-3, atol=1e-3 * np.abs(sf).max())
+    # the members' points are the full window's points p % 2 == r (the fused point steps of the shared solves)
+    idf = full.points()["idepth"]
+    for r, m in enumerate(grp.members):
+        idr = m.points()["idepth"]
+        assert np.allclose(idr, idf[r::2], rtol=1e-3, atol=1e-5)
+    for w in [full, *alone]:
+        w.close()
+    grp.close()

@@ -76,3 +76,10 @@ def _multi_cases():
 @pytest.mark.parametrize("name,c,np2", list(_multi_cases()), ids=[n for n, _, _ in _multi_cases()])
 def test_multi_block_threshold_matches_nth_element(name, c, np2):
     assert device_threshold(c, multi=np2 if np2 > 1 else 1) == ref_threshold(c)
+
+
+@pytest.mark.parametrize("name,c", list(_cases()), ids=[n for n, _ in _cases()])
+def test_rank_select_block_matches_nth_element(name, c):
+    """The multi-rank path's one-block select (block 1 of the solve / hs_k_combine launch, 512 threads, pass 1
+    counted in LDS, SOLVE_TH_CAP survivors in the solve's LDS; more: the pass-3 re-scan)."""
+    assert device_threshold(c, multi=-1) == ref_threshold(c)

@@ -19,6 +19,8 @@ for W in trace track act refine select; do
 done
 timeout -k 10 300 python bench.py --workload ba-kitti --steps 50 --warmup 5 --cpu-seconds 6 > $OUT/bench_ba_kitti.json 2> $OUT/bench_ba_kitti.err || { echo "bench ba-kitti failed"; tail -20 $OUT/bench_ba_kitti.err; exit 1; }
 head -c 300 $OUT/bench_ba_kitti.json; echo
+timeout -k 10 300 python bench.py --workload keyframe --steps 10 --warmup 2 --cpu-seconds 6 > $OUT/bench_keyframe.json 2> $OUT/bench_keyframe.err || { echo "bench keyframe failed"; tail -20 $OUT/bench_keyframe.err; exit 1; }
+head -c 300 $OUT/bench_keyframe.json; echo
 for P in 20000 200000 2000000; do
   timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu --points $P > $OUT/p$P.json 2> $OUT/p$P.err || { echo "sweep $P failed"; exit 1; }
 done
