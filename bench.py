@@ -39,10 +39,11 @@ HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
 TRACK_BYTES_PER_POINT_PASS = 64  # CoarseTracker bytes per reference point per calcRes+GS pass
 
 
-def pmc_traffic(points: int, kernel: str = "hs_k_lin"):
+def pmc_traffic(points, kernel: str = "hs_k_lin"):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/*_pmc_traffic.json,
-    made by tools/pmc.sh + tools/pmc_summary.py: separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this
-    bench at the same --points).  None when no pass at this size has been committed."""
+    made by tools/r03_pmc.sh + tools/pmc_summary.py: separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this
+    bench on the same workload).  points: the workload key -- the C4 window's point count, "kitti<N>" for
+    --workload ba-kitti, or the workload name (trace, track).  None when no pass for it has been committed."""
     import glob
     import re
 
@@ -128,6 +129,10 @@ def cpu_baseline(points: int, seconds: float, kitti: bool = False):
         "single_thread": {"value": v_1, "iterations": n_1, "median_ms_per_step": med_1 * 1e3},
         "host_cpu_model": model,
         "host_logical_cpus": ncpu,
+        "cores_note": ("the pool uses the host threads this job is allotted (OMP_NUM_THREADS; 16 per GPU on the GPU "
+                       "pool, which asks jobs to size worker pools to that share), not every logical CPU of the "
+                       "shared machine (host_logical_cpus); the reference sizes its pool by ProcessorCount "
+                       "(CMakeLists.txt:52-54), i.e. it would take the whole host"),
         "build_flags": flags,
     }
 
@@ -172,7 +177,7 @@ def bench_trace(args):
                                "points, 8 host KFs, 1232x368", "points": s.n_points, "hosts": s.n_hosts,
                    "search_steps_per_trace": steps // args.steps, "parallelism": "single GPU"},
         "roofline": {"bound": "hbm", "kernel": "hs_k_trace_on", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic("trace", "hs_k_trace_on")[0],
                      "bytes_per_unit": TRACE_BYTES_PER_STEP, "unit_of_bytes": "discrete-search step (GN taps excluded)",
                      "avg_launch_ms": kern_ms},
         "second_trace_counts": dict(zip(("good", "oob", "outlier", "skipped", "badcondition", "uninitialized"),
@@ -233,7 +238,8 @@ def bench_track(args):
                                "points, 640x480, 5 levels", "ok": bool(ok), "device_ms_per_track": dev_ms,
                    "passes": passes, "point_passes": point_passes},
         "roofline": {"bound": "hbm", "kernel": "hs_k_track", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "bytes_per_unit": TRACK_BYTES_PER_POINT_PASS,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic("track", "hs_k_track")[0],
+                     "bytes_per_unit": TRACK_BYTES_PER_POINT_PASS,
                      "unit_of_bytes": "reference point x calcRes+calcGSSSE pass", "units_per_launch": point_passes,
                      "avg_launch_ms": dev_ms, "flop_per_unit": 230,
                      "achieved_tflops": point_passes * 230 / (dev_ms * 1e-3) / 1e12,
@@ -563,7 +569,8 @@ def main():
     lin_ms = ba.time_linearize(max(64, args.steps))
     achieved = BYTES_PER_PRES * shard.n_res / (lin_ms * 1e-3) / 1e9
     lin_kernel = ba.partition()["kernel"]  # hs_k_lin (one point per wave) or hs_k_lin8 (8 points per wave)
-    traffic, traffic_src = pmc_traffic(args.points, lin_kernel) if world == 1 and not kitti else (None, None)
+    traffic, traffic_src = (pmc_traffic(f"kitti{args.points}" if kitti else args.points, lin_kernel) if world == 1
+                            else (None, None))
     if kitti:
         wl = ("C5 BA half (BASELINE.json configs[4]): full windowed photometric BA incl. Schur complement, 8 KF x "
               f"{n_window} pts, KITTI 1232x368, 5 pyramid levels")

@@ -222,6 +222,11 @@ struct hs_ctx {
   int group_stride = 0;
   bool xch_local = false, xch_th = false, xch_defer = false;  // group: a local reduce awaits the exchange
   hipEvent_t ev_xch[2] = {nullptr, nullptr};
+  // hs_k_redstitch (env HS_FUSE_RS=1): reduce + stitch in one launch, ordered by a device counter that only grows
+  bool fuse_rs = false, capturing = false;
+  unsigned int* d_rs_cnt = nullptr;
+  unsigned int rs_total = 0;  // the counter's value once every launch so far has completed
+  bool rs_traced = false;     // the last reduce + stitch ran fused (the trace dump reads its blocks from d_tr_st)
   bool multi_rank() const { return comm != nullptr || !group.empty(); }
 
   // timings of the last optimize / iterate

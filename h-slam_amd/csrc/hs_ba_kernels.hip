@@ -819,16 +819,19 @@ __global__ __launch_bounds__(HS_LIN_NT) void hs_k_lin_exact_fix(HsLinArgs a) { l
 // =====================================================================================================
 namespace {
 // linearizeAll's energy (+ the sumNID / numID statistics of doStepFromBackup): block partials in block order
+// (threads 0..255 sum; a larger block's other threads only take part in the barriers)
 __device__ void red_energy_block(const HsRedArgs& a) {
   __shared__ double red[3][256];
   const int tid = threadIdx.x;
-  double s[3] = {0.0, 0.0, 0.0};
-  const int per = (a.nblk + 255) / 256, b0 = tid * per, b1 = min(a.nblk, b0 + per);  // contiguous runs
-  for (int b = b0; b < b1; b++)
+  if (tid < 256) {
+    double s[3] = {0.0, 0.0, 0.0};
+    const int per = (a.nblk + 255) / 256, b0 = tid * per, b1 = min(a.nblk, b0 + per);  // contiguous runs
+    for (int b = b0; b < b1; b++)
 #pragma unroll
-    for (int k = 0; k < 3; k++) s[k] += a.part_e[(size_t)b * 4 + k];
+      for (int k = 0; k < 3; k++) s[k] += a.part_e[(size_t)b * 4 + k];
 #pragma unroll
-  for (int k = 0; k < 3; k++) red[k][tid] = s[k];
+    for (int k = 0; k < 3; k++) red[k][tid] = s[k];
+  }
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
     if (tid < o)
@@ -1171,19 +1174,10 @@ constexpr int ST_LDS = 12288 + ST_NW * 64;  // doubles of the stitch block's LDS
 static_assert(2 * ST_LDS >= 1600 + TH_CAP, "the threshold select's LDS lives in the stitch block's scratch");
 }  // namespace
 
-__global__ __launch_bounds__(256) void hs_k_reduce(HsRedArgs a) {
-  const int nred = a.nF * a.Q;
-  const int b = blockIdx.x, tid = threadIdx.x;
-  if (a.hist_only) {  // multi-rank large windows: pass 1 over the all-gathered candidates
-    red_th_hist_block(a, b);
-    return;
-  }
-  HS_TRACE(a, 0);
-  if (b == nred) { red_energy_block(a); HS_TRACE(a, 15); return; }
-  if (b > nred) { red_th_hist_block(a, b - nred - 1); HS_TRACE(a, 15); return; }
-  const int h = b / a.Q, q = b % a.Q;
+// host sums of chunk q of host h (blockDim entries of the host's [ne][64] accumulators per block)
+__device__ __forceinline__ void red_host_chunk(const HsRedArgs& a, int h, int q) {
   const int NE64 = a.ne * 64;
-  const int e = q * 256 + tid;  // entry of the host's [ne][64] accumulators
+  const int e = q * (int)blockDim.x + (int)threadIdx.x;  // entry of the host's [ne][64] accumulators
   const int b0 = a.blk_begin[h], b1 = a.blk_begin[h + 1];
   if (e < NE64) {
     // the host's block partials in block order, fp64 (the reference sums its per-thread fp32 accumulators in
@@ -1208,6 +1202,19 @@ __global__ __launch_bounds__(256) void hs_k_reduce(HsRedArgs a) {
     }
     a.hostsum[(size_t)h * NE64 + e] = s;
   }
+}
+
+__global__ __launch_bounds__(256) void hs_k_reduce(HsRedArgs a) {
+  const int nred = a.nF * a.Q;
+  const int b = blockIdx.x;
+  if (a.hist_only) {  // multi-rank large windows: pass 1 over the all-gathered candidates
+    red_th_hist_block(a, b);
+    return;
+  }
+  HS_TRACE(a, 0);
+  if (b == nred) { red_energy_block(a); HS_TRACE(a, 15); return; }
+  if (b > nred) { red_th_hist_block(a, b - nred - 1); HS_TRACE(a, 15); return; }
+  red_host_chunk(a, b / a.Q, b % a.Q);
   HS_TRACE(a, 15);
 }
 
@@ -1238,15 +1245,13 @@ __global__ __launch_bounds__(HS_STITCH_NT) void hs_k_th_select(HsRedArgs a) {
 // in one fixed order (hosts, then targets), so the system is bit-reproducible.  The vector holds the upper
 // triangle of HA - sc HSC (diagonal: HA (1 + lambda) - sc HSC; the solve adds the priors) and bA - bSC;
 // `sep` HA | bA and HSC | bSC separately.
-__global__ __launch_bounds__(ST_NT) void hs_k_stitch(HsStitchArgs a) {
-  __shared__ double lds[ST_LDS];
+__device__ __forceinline__ void stitch_block(const HsStitchArgs& a, const int j, double* lds) {
   const int nF = a.nF, n = 4 + 8 * nF, nn = n * n, SL = nn + n;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane >> 3, c = lane & 7;
   const int NE64 = a.ne * 64;
   const int ND = a.exact ? HS_ND_EXACT : HS_ND_PROD;
   const int oE = (HS_E_TOP + ND) * 64;  // accE / accEB / Hcc entries of a host sum
   const int nFB = nF * (nF + 1) / 2;
-  const int j = blockIdx.x;
   HS_TRACE(a, 0);
   if (j == nFB + nF + 1) {  // setNewFrameEnergyTH for the next linearization, beside the stitch
     if (!a.red.skip_threshold) red_energy_th_block(a.red, reinterpret_cast<unsigned int*>(lds));
@@ -1615,6 +1620,41 @@ __global__ __launch_bounds__(ST_NT) void hs_k_stitch(HsStitchArgs a) {
     }
   }
   HS_TRACE(a, 15);
+}
+
+__global__ __launch_bounds__(ST_NT) void hs_k_stitch(HsStitchArgs a) {
+  __shared__ double lds[ST_LDS];
+  stitch_block(a, blockIdx.x, lds);
+}
+
+// hs_k_reduce + hs_k_stitch as ONE launch (HS_FUSE_RS=1): blocks 0 .. nR-1 take hs_k_reduce's roles (host-sum
+// chunks of 1024 entries, the energy block, the pass-1 histogram blocks) and signal a counter (every wave's stores
+// written back by an agent-scope release, then one relaxed agent-scope increment); blocks nR.. are the stitch
+// blocks, which wait for the counter to reach its target (an agent-scope acquire after the spin) before reading the
+// host sums.  Reduce blocks have the lower block indices, so they are dispatched first and never wait: no deadlock.
+// The counter only grows; target = (launch epoch) x nR, compared wrap-safe.
+__global__ __launch_bounds__(ST_NT) void hs_k_redstitch(HsStitchArgs a, unsigned int* cnt, unsigned int target,
+                                                        int nR) {
+  __shared__ double lds[ST_LDS];
+  const int b = blockIdx.x;
+  const HsRedArgs& r = a.red;
+  if (b < nR) {
+    const int nred = r.nF * r.Q;
+    if (b < nred) red_host_chunk(r, b / r.Q, b % r.Q);
+    else if (b == nred) red_energy_block(r);
+    else red_th_hist_block(r, b - nred - 1);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  if (threadIdx.x == 0) {
+    while ((int)(__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0)
+      __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the CU's L1 and the XCD's L2 lines invalidated
+  }
+  __syncthreads();  // no wave of the block has loaded anything before this point
+  stitch_block(a, b - nR, lds);
 }
 
 // =====================================================================================================

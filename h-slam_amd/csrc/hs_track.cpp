@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -52,6 +53,8 @@ struct hs_tracker {
   int pts_cap = 0;
   double* d_Tin = nullptr;
   HsTryOut* d_out = nullptr;
+  double* d_part = nullptr;       // [try_cap][2][HS_TRK_MAXG][HS_TRK_NRED] pass partials of the member workgroups
+  unsigned int* d_cnt = nullptr;  // [try_cap] pass counters (zeroed per launch)
   HsTryOut* h_out = nullptr;
   double* d_lmlog = nullptr;
   int* d_lmlvl = nullptr;
@@ -60,7 +63,8 @@ struct hs_tracker {
   double refAff[2] = {0, 0};
   bool haveRef = false, haveFrame = false;
   double last_ms = 0;
-  long long* d_trace = nullptr;  // HS_KTRACE=1: per-hypothesis phase cycles of hs_k_track (stderr)
+  long long* d_trace = nullptr;
+  int last_G = 1;                 // workgroups per hypothesis of the last track launch  // HS_KTRACE=1: per-hypothesis phase cycles of hs_k_track (stderr)
   int trace_cap = 0;
 };
 
@@ -83,12 +87,17 @@ static int ensure_tries(hs_tracker* t, int n) {
   if (t->d_out) (void)hipFree(t->d_out);
   if (t->h_out) (void)hipHostFree(t->h_out);
   if (t->d_lmlog) (void)hipFree(t->d_lmlog);
+  if (t->d_part) (void)hipFree(t->d_part);
+  if (t->d_cnt) (void)hipFree(t->d_cnt);
+  t->d_part = nullptr; t->d_cnt = nullptr;
   if (t->d_lmlvl) (void)hipFree(t->d_lmlvl);
   t->d_Tin = nullptr; t->d_out = nullptr; t->h_out = nullptr; t->d_lmlog = nullptr; t->d_lmlvl = nullptr;
   TS_HIP(hipMalloc((void**)&t->d_Tin, sizeof(double) * 9 * n));  // T (7) | aff (2)
   TS_HIP(hipMalloc((void**)&t->d_out, sizeof(HsTryOut) * n));
   TS_HIP(hipMalloc((void**)&t->d_lmlog, sizeof(double) * 3 * HS_TRK_MAXLOG * n));
   TS_HIP(hipMalloc((void**)&t->d_lmlvl, sizeof(int) * HS_TRK_MAXLOG * n));
+  TS_HIP(hipMalloc((void**)&t->d_part, sizeof(double) * 2 * HS_TRK_MAXG * HS_TRK_NRED * n));
+  TS_HIP(hipMalloc((void**)&t->d_cnt, sizeof(unsigned int) * n));
   TS_HIP(hipHostMalloc((void**)&t->h_out, sizeof(HsTryOut) * n));
   t->try_cap = n;
   return HS_OK;
@@ -131,19 +140,31 @@ static int run_tries(hs_tracker* t, int n, const double* h_in, int coarsest, int
   a.single_pass = single_pass;
   a.pass_lvl = lvl;
   a.pass_cutoff = cutoff;
+  // workgroups per hypothesis: the chip's 256 CUs shared by the hypotheses (every member must be resident at once:
+  // they meet once per pass), at most HS_TRK_MAXG; env HS_TRK_G caps it (1 = the one-workgroup LM loop)
+  int G = 1;  // (default until measured on the GPU)
+  if (const char* e = std::getenv("HS_TRK_G"))
+    G = std::max(1, std::min({HS_TRK_MAXG, 256 / std::max(1, n), std::atoi(e)}));
+  if (single_pass) G = 1;
+  a.G = G;
+  a.part = t->d_part;
+  a.cnt = t->d_cnt;
+  t->last_G = G;
+  if (G > 1) TS_HIP(hipMemsetAsync(t->d_cnt, 0, sizeof(unsigned int) * n, t->stream));
   const char* kt = std::getenv("HS_KTRACE");
   if (kt && kt[0] == '1' && !single_pass) {
-    if (n > t->trace_cap) {  // grown once to the largest hypothesis count (freed by hs_tracker_destroy)
+    const int nb = n * G;
+    if (nb > t->trace_cap) {  // grown once to the largest block count (freed by hs_tracker_destroy)
       if (t->d_trace) (void)hipFree(t->d_trace);
       t->d_trace = nullptr;
-      TS_HIP(hipMalloc((void**)&t->d_trace, sizeof(long long) * 16 * n));
-      t->trace_cap = n;
+      TS_HIP(hipMalloc((void**)&t->d_trace, sizeof(long long) * 16 * nb));
+      t->trace_cap = nb;
     }
-    TS_HIP(hipMemsetAsync(t->d_trace, 0, sizeof(long long) * 16 * n, t->stream));
+    TS_HIP(hipMemsetAsync(t->d_trace, 0, sizeof(long long) * 16 * nb, t->stream));
     a.trace = t->d_trace;
   }
   TS_HIP(hipEventRecord(t->e0, t->stream));
-  hipLaunchKernelGGL(hs_k_track, dim3(n), dim3(512), 0, t->stream, a);
+  hipLaunchKernelGGL(hs_k_track, dim3(n * G), dim3(512), 0, t->stream, a);
   TS_HIP(hipGetLastError());
   TS_HIP(hipEventRecord(t->e1, t->stream));
   TS_HIP(hipMemcpyAsync(t->h_out, t->d_out, sizeof(HsTryOut) * n, hipMemcpyDeviceToHost, t->stream));

@@ -53,7 +53,15 @@ struct HsTrackArgs {
   double* lm_log;       // [n][HS_TRK_MAXLOG][3]: resNew/N, resOld/N (accept test), |inc| (break test) per LM iteration
   int* lm_lvl;          // [n][HS_TRK_MAXLOG]
   long long* trace;
+  // G workgroups per hypothesis (blocks h G .. h G + G - 1): each pass's points are spread over them; their sums
+  // meet in part [n][2][G][HS_TRK_NRED] (pass parity) behind a counter per hypothesis (cnt [n], zero at launch),
+  // and every workgroup forms the same totals (in workgroup order) and runs the same LM step
+  int G;
+  double* part;
+  unsigned int* cnt;
 };
+constexpr int HS_TRK_NRED = 52;  // the reduced values of a pass (45 normal-equation entries, 4 energies / flows, 3 counts)
+constexpr int HS_TRK_MAXG = 32;
 
 __global__ void hs_k_track(HsTrackArgs a);
 __global__ void hs_k_trk_scatter(int n, const float* cu, const float* cv, const float* cid, const float* hdi, int w,

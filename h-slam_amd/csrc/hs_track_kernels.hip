@@ -29,6 +29,7 @@ constexpr int TRK_NT = 512;
 constexpr int TRK_B = 4;              // points per thread whose loads are in flight together
 constexpr int TRK_NACC = 45;          // upper triangle of the 9x9 [J | r] normal equations
 constexpr int TRK_NRED = TRK_NACC + 4 + 3;  // + E, flowT, flowRT, flowNum | numE, numSat, numWarped
+static_assert(TRK_NRED == HS_TRK_NRED, "pass partial layout");
 
 __device__ __forceinline__ float3 interp33(const float4* __restrict__ img, float x, float y, int w) {
   int ix = (int)x, iy = (int)y;
@@ -135,6 +136,7 @@ struct TrkShared {
   float lambda, cutoffRep;
   int brk, accept;
   int passes;
+  int npass, iters, nchecks;  // this workgroup's pass count (partial parity, counter target), LM iterations, checks
   long long pointPasses;
   long long prof[6];  // HS_KTRACE: thread-0 cycles: point loop, reductions, LM step, passes, wave reduce, barrier
 };
@@ -159,8 +161,9 @@ __device__ __forceinline__ float xor_tree_lane0(float v) {
 }
 
 // calcRes + calcGSSSE at S.RKi / S.t / S.affLL for level S.lvl; results in S.res / S.H / S.b / S.nWarped
-__device__ void trk_pass(const HsTrackArgs& a, TrkShared& S) {
+__device__ void trk_pass(const HsTrackArgs& a, TrkShared& S, int h, int g) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int G = a.G, GT = G * TRK_NT;  // the hypothesis' workgroups take points g TRK_NT + tid (mod G TRK_NT)
   const int lvl = S.lvl;
   const HsTrkLevel& L = a.lv[lvl];
   const int n = *L.pc_n, wl = L.w, hl = L.h;
@@ -179,11 +182,11 @@ __device__ void trk_pass(const HsTrackArgs& a, TrkShared& S) {
   for (int q = 0; q < TRK_NACC; q++) acc[q] = 0.f;
   // the thread's points i = tid + k TRK_NT in order, TRK_B at a time: every load of a batch (point data, then the
   // bilinear taps) is issued before any is used, so a batch costs two memory round trips instead of two per point
-  for (int i0 = tid; i0 < n; i0 += TRK_B * TRK_NT) {
+  for (int i0 = g * TRK_NT + tid; i0 < n; i0 += TRK_B * GT) {
     float id[TRK_B], x[TRK_B], y[TRK_B], refColor[TRK_B];
 #pragma unroll
     for (int b = 0; b < TRK_B; b++) {
-      const int i = min(i0 + b * TRK_NT, n - 1);
+      const int i = min(i0 + b * GT, n - 1);
       id[b] = L.pc_id[i];
       x[b] = L.pc_u[i];
       y[b] = L.pc_v[i];
@@ -195,7 +198,7 @@ __device__ void trk_pass(const HsTrackArgs& a, TrkShared& S) {
     float fdx[TRK_B], fdy[TRK_B];
 #pragma unroll
     for (int b = 0; b < TRK_B; b++) {
-      const int i = i0 + b * TRK_NT;
+      const int i = i0 + b * GT;
       float pt0 = RKi[0] * x[b] + RKi[1] * y[b] + RKi[2] * 1.f;
       float pt1 = RKi[3] * x[b] + RKi[4] * y[b] + RKi[5] * 1.f;
       float pt2 = RKi[6] * x[b] + RKi[7] * y[b] + RKi[8] * 1.f;
@@ -325,6 +328,28 @@ __device__ void trk_pass(const HsTrackArgs& a, TrkShared& S) {
     S.red[0][tid] = s;  // wave 0's slot is only read by this thread before the sum
   }
   __syncthreads();
+  if (G > 1) {
+    // the hypothesis' workgroups meet: partials out (agent-scope release by every wave), one relaxed increment,
+    // spin until all G of this pass are in (agent-scope acquire), then every workgroup sums them in workgroup order
+    double* P = a.part + ((size_t)h * 2 + (S.npass & 1)) * G * TRK_NRED;
+    if (tid < TRK_NRED) P[g * TRK_NRED + tid] = S.red[0][tid];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __syncthreads();
+    if (tid == 0) {
+      __hip_atomic_fetch_add(a.cnt + h, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned int target = (unsigned int)G * (unsigned int)(S.npass + 1);
+      while ((int)(__hip_atomic_load(a.cnt + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0)
+        __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    __syncthreads();
+    if (tid < TRK_NRED) {
+      double s = 0.0;
+      for (int gg = 0; gg < G; gg++) s += P[gg * TRK_NRED + tid];
+      S.red[0][tid] = s;
+    }
+    __syncthreads();
+  }
   if (tid == 0) {
     const double* R = S.red[0];
     const float Ef = (float)R[TRK_NACC + 0];
@@ -337,6 +362,7 @@ __device__ void trk_pass(const HsTrackArgs& a, TrkShared& S) {
     S.res[4] = fRT / (fN + 0.1);
     S.res[5] = numSat / (float)numE;
     S.passes += 1;
+    S.npass += 1;
     S.pointPasses += n;
     const int npad = (numW + 3) & ~3;  // buf_warped_n includes the zero padding (quirk kept)
     S.nWarped = npad;
@@ -393,18 +419,20 @@ __device__ void trk_setup(const HsTrackArgs& a, TrkShared& S, const double T7[7]
 __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
   __shared__ TrkShared S;
   const int tid = threadIdx.x;
-  const int h = blockIdx.x;  // hypothesis
+  const int h = blockIdx.x / a.G, g = blockIdx.x - h * a.G;  // hypothesis, member workgroup
+  const bool lead = g == 0;  // the workgroup that writes the hypothesis' outputs (every member computes them)
   HsTryOut& out = a.out[h];
   HS_TRACE(a, 0);
   if (a.single_pass) {  // hs_tracker_calc_res
     if (tid == 0) {
       S.passes = 0;
+      S.npass = 0;
       S.pointPasses = 0;
       trk_setup(a, S, a.T_in + 7 * h, a.aff_in + 2 * h, a.pass_lvl, a.pass_cutoff);
     }
     __syncthreads();
-    trk_pass(a, S);
-    if (tid == 0) {
+    trk_pass(a, S, h, g);
+    if (tid == 0 && lead) {
       for (int q = 0; q < 6; q++) out.res6[q] = S.res[q];
       for (int q = 0; q < 64; q++) out.H[q] = S.H[q];
       for (int q = 0; q < 8; q++) out.b[q] = S.b[q];
@@ -418,8 +446,9 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
     for (int q = 0; q < 7; q++) S.T[q] = a.T_in[7 * h + q];
     S.aff[0] = a.aff_in[2 * h + 0];
     S.aff[1] = a.aff_in[2 * h + 1];
-    out.n_checks = 0;
-    out.iters = 0;
+    S.nchecks = 0;
+    S.iters = 0;
+    S.npass = 0;
     S.passes = 0;
     S.pointPasses = 0;
     for (int q = 0; q < 6; q++) S.prof[q] = 0;
@@ -432,7 +461,7 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
       trk_setup(a, S, S.T, S.aff, lvl, a.coarseCutoffTH * S.cutoffRep);
     }
     __syncthreads();
-    trk_pass(a, S);
+    trk_pass(a, S, h, g);
     while (S.res[5] > 0.6 && S.cutoffRep < 50) {  // uniform: S.res / S.cutoffRep are shared
       __syncthreads();
       if (tid == 0) {
@@ -440,7 +469,7 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
         trk_setup(a, S, S.T, S.aff, lvl, a.coarseCutoffTH * S.cutoffRep);
       }
       __syncthreads();
-      trk_pass(a, S);
+      trk_pass(a, S, h, g);
     }
     if (tid == 0) {  // calcGSSSE of the last calcRes; lambda = 0.01
       for (int q = 0; q < 64; q++) S.Hs[q] = S.H[q];
@@ -453,7 +482,7 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
       __syncthreads();  // every thread has read S.brk of the previous iteration
       if (tid == 0) {
         const long long lm0 = a.trace ? clock64() : 0;
-        out.iters++;
+        S.iters++;
         // Hl = H with the diagonal scaled by (1 + lambda), in LDS (the solver reads it with pivoted indices)
         double* Hl = S.Hl;
         double mb[8], inc[8];
@@ -488,11 +517,11 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
         if (a.trace) S.prof[2] += clock64() + (long long)(S.RKi[4] * 0.f) - lm0;
       }
       __syncthreads();
-      trk_pass(a, S);
+      trk_pass(a, S, h, g);
       if (tid == 0) {
         const bool accept = (S.res[0] / S.res[1]) < (S.resOld[0] / S.resOld[1]);
-        const int it = out.iters - 1;
-        if (it < HS_TRK_MAXLOG) {
+        const int it = S.iters - 1;
+        if (lead && it < HS_TRK_MAXLOG) {
           a.lm_log[((size_t)h * HS_TRK_MAXLOG + it) * 3 + 0] = S.res[0] / S.res[1];
           a.lm_log[((size_t)h * HS_TRK_MAXLOG + it) * 3 + 1] = S.resOld[0] / S.resOld[1];
           a.lm_log[((size_t)h * HS_TRK_MAXLOG + it) * 3 + 2] = S.incNorm;
@@ -515,15 +544,15 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
       if (S.brk) break;
     }
     if (tid == 0) {  // lastResiduals[lvl] / lastFlowIndicators: logged for the caller's abort replay
-      const int c = out.n_checks;
-      if (c < HS_TRK_MAXCHECK) {
+      const int c = S.nchecks;
+      if (lead && c < HS_TRK_MAXCHECK) {
         out.check_lvl[c] = lvl;
         out.check_res[c] = sqrtf((float)(S.resOld[0] / S.resOld[1]));
         out.check_flow[c][0] = S.resOld[2];
         out.check_flow[c][1] = S.resOld[3];
         out.check_flow[c][2] = S.resOld[4];
-        out.n_checks = c + 1;
       }
+      S.nchecks = c < HS_TRK_MAXCHECK ? c + 1 : c;
     }
     const bool rep = S.cutoffRep > 1 && !haveRepeated;
     __syncthreads();
@@ -532,7 +561,9 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
       haveRepeated = true;
     }
   }
-  if (tid == 0) {
+  if (tid == 0 && lead) {
+    out.iters = S.iters;
+    out.n_checks = S.nchecks;
     for (int q = 0; q < 7; q++) out.T[q] = S.T[q];
     out.aff[0] = S.aff[0];
     out.aff[1] = S.aff[1];
