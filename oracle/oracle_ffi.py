@@ -128,6 +128,8 @@ def load(fast=False):
     lib.hso_trk_get_ref.argtypes = [vp, C.c_int, vp, vp, vp, vp]
     lib.hso_trk_get_ref.restype = C.c_int
     lib.hso_trk_calc_res.argtypes = [vp, C.c_int, vp, vp, C.c_float, vp, vp, vp, vp]
+    lib.hso_trk_set_sum_order.argtypes = [vp, C.c_int]
+    lib.hso_trk_set_sum_order.restype = None
     lib.hso_trk_track.argtypes = [vp, vp, vp, C.c_int, vp, vp, vp, vp]
     lib.hso_trk_track.restype = C.c_int
     lib.hso_trk_get_log.argtypes = [vp, C.c_int, vp, vp, vp, vp]
@@ -425,6 +427,11 @@ class OracleTracker:
         ok = self.lib.hso_trk_track(self.h, _p(T), _p(a), coarsest, _p(np.ascontiguousarray(minRes, np.float64)),
                                     _p(lr), _p(fl), C.byref(its))
         return dict(ok=bool(ok), T=T, aff=a, lastResiduals=lr, flow=fl, iters=its.value)
+
+    def set_sum_order(self, order):
+        """Test hook: 0 = the reference's point order, 1 = reversed (every fp32 sum of calcRes / calcGSSSE formed in
+        another order: the spread such a change alone causes bounds the GPU's reduction-order deviation)."""
+        self.lib.hso_trk_set_sum_order(self.h, int(order))
 
     def lm_log(self, cap=512):
         lvl, nr, orr, inc = np.zeros(cap, np.int32), np.zeros(cap), np.zeros(cap), np.zeros(cap)

@@ -25,6 +25,7 @@
 namespace hso {
 
 struct TrackerO {
+  int sum_order = 0;  // 0: the reference's point order; 1: reversed (hso_trk_set_sum_order, the tests' order spread)
   hs_params P;
   int nlev = 0;
   int w[10], h[10];
@@ -161,7 +162,10 @@ struct TrackerO {
     float sumSquaredShiftT = 0, sumSquaredShiftRT = 0, sumSquaredShiftNum = 0;
     const float maxEnergy = 2 * P.huberTH * cutoffTH - P.huberTH * P.huberTH;
     const int nl = pc_n[lvl];
-    for (int i = 0; i < nl; i++) {
+    for (int ii = 0; ii < nl; ii++) {
+      // order 1 (test spread only): the points in reverse order, so every fp32 sum (E, the flows, the warped
+      // buffer that calcGSSSE sums) is formed in another order; the decisions per point are the same
+      const int i = sum_order == 1 ? nl - 1 - ii : ii;
       const float id = pc_idepth[lvl][i], x = pc_u[lvl][i], y = pc_v[lvl][i];
       const float xy1[3] = {x, y, 1};
       float pt[3];
@@ -418,6 +422,9 @@ void hso_trk_calc_res(void* h, int lvl, const double T7[7], const double aff[2],
   if (n_warped) *n_warped = t->bw_n;
   if (H64 && b8) t->calcGSSSE(lvl, H64, b8, aff);
 }
+// test hook: the order the fp32 sums of calcRes / calcGSSSE are formed in (0 reference, 1 reversed point order),
+// so tests can measure how far another summation order moves the LM trajectory
+void hso_trk_set_sum_order(void* h, int order) { ((TrackerO*)h)->sum_order = order; }
 int hso_trk_track(void* h, double T7[7], double aff[2], int coarsest, const double minRes[5], double lastRes[5],
                   double flow[3], int* iters) {
   TrackerO* t = (TrackerO*)h;

@@ -5,11 +5,14 @@ Bars:
 * calcRes categorical counts (numTermsInE, saturated, buf_warped_n): exact;
   energy E (fp32 sum in a different order): rel <= 2e-5; flow indicators rel <= 1e-4;
   calcGSSSE H / b: |d| <= 1e-4 (|ref| + 1e-3 max|diag H|);
-* trackNewestCoarse / the try loop: the per-iteration LM logs (accept-test ratios, step norms) agree to
-  1e-4 rel up to the first decision that is a near-tie in the oracle itself (fp32 sums in another order
-  can flip a tie); if no such tie occurs the final pose agrees to 1e-5 and lastResiduals to 1e-4 rel,
-  otherwise to the LM's own stopping tolerance (pose 2e-3, lastResiduals 1e-2 rel).  ok / haveOneGood /
-  tryIterations: equal.
+* trackNewestCoarse / the try loop: the per-iteration LM logs (accept-test ratios, step norms) agree up to the
+  first decision that is a near-tie in the oracle itself (fp32 sums in another order can flip a tie), at bars tied
+  to the oracle's OWN summation-order spread: the oracle run again with every calcRes / calcGSSSE sum formed in
+  reversed point order (hso_trk_set_sum_order) moves the ratios / step norms / final pose by s; the GPU (whose
+  sums are wave trees and, with HS_TRK_G > 1, workgroup partials) may deviate by max(floor, 10 s) -- floors 1e-4
+  (ratios), 1e-3 (step norms), 1e-5 (pose).  If no tie occurs the final pose agrees to that bar and
+  lastResiduals to 1e-4 rel, otherwise to the LM's own stopping tolerance (pose 2e-3, lastResiduals 1e-2 rel).
+  ok / haveOneGood / tryIterations: equal.
 """
 import numpy as np
 import pytest
@@ -91,7 +94,30 @@ def test_calc_res_parity(vga, pair, which):
             assert np.all(np.abs(bg - bo) <= 1e-4 * (np.abs(bo) + 1e-3 * sb))
 
 
-def _lm_divergence(lg, lo):
+def _order_spread(o, T0, aff, coarsest, minRes):
+    """The oracle's own summation-order spread on this LM run: (ratio, step norm, pose) relative deviations of the
+    reversed-order run from the reference-order run, over their common prefix (until a level or decision differs).
+    Leaves the oracle in the reference order with the reference-order run as its last run."""
+    o.set_sum_order(1)
+    r1 = o.track(T0, aff, coarsest, minRes)
+    l1 = o.lm_log()
+    o.set_sum_order(0)
+    r0 = o.track(T0, aff, coarsest, minRes)
+    l0 = o.lm_log()
+    sr, si = 0.0, 0.0
+    tie = len(l0[0]) != len(l1[0])
+    for k in range(min(len(l0[0]), len(l1[0]))):
+        if l0[0][k] != l1[0][k] or (l0[1][k] < l0[2][k]) != (l1[1][k] < l1[2][k]) or \
+                (l0[3][k] > 1e-3) != (l1[3][k] > 1e-3) or l0[3][k] > 1.0:
+            tie = True
+            break
+        sr = max(sr, abs(l1[1][k] - l0[1][k]) / abs(l0[1][k]), abs(l1[2][k] - l0[2][k]) / abs(l0[2][k]))
+        si = max(si, abs(l1[3][k] - l0[3][k]) / max(l0[3][k], 1e-12))
+    sp = 0.0 if tie else _pose_err(r1["T"], r0["T"])
+    return sr, si, sp
+
+
+def _lm_divergence(lg, lo, spread=(0.0, 0.0, 0.0)):
     """Walk the two LM logs (level, resNew/N, resOld/N, |inc|) in lockstep.  Until the trajectories part, every
     operand agrees to fp32-summation-order precision; they may only part at a decision that is a near-tie in
     the oracle itself (accept: resNew/N vs resOld/N, break: |inc| vs 1e-3) or at a step from a near-singular
@@ -99,15 +125,16 @@ def _lm_divergence(lg, lo):
     decisions."""
     lvg, ng, og, ig = lg
     lvo, no, oo, io = lo
+    tr, ti = max(1e-4, 10 * spread[0]), max(1e-3, 10 * spread[1])
     for k in range(min(len(lvg), len(lvo))):
         assert lvg[k] == lvo[k], k
-        assert abs(ng[k] - no[k]) <= 1e-4 * abs(no[k]), (k, ng[k], no[k])
-        assert abs(og[k] - oo[k]) <= 1e-4 * abs(oo[k]), (k, og[k], oo[k])
+        assert abs(ng[k] - no[k]) <= tr * abs(no[k]), (k, ng[k], no[k], tr)
+        assert abs(og[k] - oo[k]) <= tr * abs(oo[k]), (k, og[k], oo[k], tr)
         if io[k] > 1.0:   # a step of > 1 (scaled units) comes from a near-singular H: fp order decides the rest
             return k
-        assert abs(ig[k] - io[k]) <= 1e-3 * io[k] + 1e-7, (k, ig[k], io[k])
+        assert abs(ig[k] - io[k]) <= ti * io[k] + 1e-7, (k, ig[k], io[k], ti)
         if (ng[k] < og[k]) != (no[k] < oo[k]):
-            assert abs(no[k] - oo[k]) <= 1e-4 * oo[k], ("accept flip without a tie", k)
+            assert abs(no[k] - oo[k]) <= 2 * tr * oo[k], ("accept flip without a tie", k)
             return k
         if (ig[k] > 1e-3) != (io[k] > 1e-3):
             assert abs(io[k] - 1e-3) <= 1e-6, ("break flip without a tie", k)
@@ -124,10 +151,11 @@ def test_track_parity(vga, pair, start):
                                                    SE3.from_data(vga.T_true)).data()
     minRes = np.full(5, np.nan)
     okg, Tg, ag = g.trackNewestCoarse(T0, [0.0, 0.0], vga.n_levels - 1, minRes)
+    spread = _order_spread(o, T0, [0.0, 0.0], vga.n_levels - 1, minRes)
     ro = o.track(T0, [0.0, 0.0], vga.n_levels - 1, minRes)
     assert okg == ro["ok"] and okg
-    k = _lm_divergence(g.lm_log(0), o.lm_log())
-    tol_T, tol_a, tol_b = (1e-5, 1e-5, 1e-3) if k is None else (2e-3, 1e-2, 0.5)
+    k = _lm_divergence(g.lm_log(0), o.lm_log(), spread)
+    tol_T, tol_a, tol_b = (max(1e-5, 10 * spread[2]), 1e-5, 1e-3) if k is None else (2e-3, 1e-2, 0.5)
     assert _pose_err(Tg, ro["T"]) < tol_T, k
     assert abs(ag[0] - ro["aff"][0]) < tol_a and abs(ag[1] - ro["aff"][1]) < tol_b, k
     lr = g.lastResiduals
@@ -172,8 +200,8 @@ def test_track_tries_parity(vga, pair):
         assert np.allclose(og["achievedRes"][fin], oo["achievedRes"][fin], rtol=1e-2)
     # every hypothesis' own LM run agrees with the oracle's run of that hypothesis up to a near-tie
     for i in (0, 1, 5, 17, len(tries) - 1):
-        o.track(tries[i], [0.0, 0.0], vga.n_levels - 1, np.full(5, np.nan))
-        _lm_divergence(g.lm_log(i), o.lm_log())
+        spread = _order_spread(o, tries[i], [0.0, 0.0], vga.n_levels - 1, np.full(5, np.nan))
+        _lm_divergence(g.lm_log(i), o.lm_log(), spread)
 
 
 def test_errors_are_loud(vga):
@@ -212,10 +240,11 @@ def test_track_parity_4_levels(vga4, start):
                                                    SE3.from_data(vga4.T_true)).data()
     minRes = np.full(5, np.nan)
     okg, Tg, ag = g.trackNewestCoarse(T0, [0.0, 0.0], vga4.n_levels - 1, minRes)
+    spread = _order_spread(o, T0, [0.0, 0.0], vga4.n_levels - 1, minRes)
     ro = o.track(T0, [0.0, 0.0], vga4.n_levels - 1, minRes)
     assert okg == ro["ok"] and okg
-    k = _lm_divergence(g.lm_log(0), o.lm_log())
-    tol_T, tol_a, tol_b = (1e-5, 1e-5, 1e-3) if k is None else (2e-3, 1e-2, 0.5)
+    k = _lm_divergence(g.lm_log(0), o.lm_log(), spread)
+    tol_T, tol_a, tol_b = (max(1e-5, 10 * spread[2]), 1e-5, 1e-3) if k is None else (2e-3, 1e-2, 0.5)
     assert _pose_err(Tg, ro["T"]) < tol_T, k
     assert abs(ag[0] - ro["aff"][0]) < tol_a and abs(ag[1] - ro["aff"][1]) < tol_b, k
     lr = g.lastResiduals

@@ -140,6 +140,28 @@ def test_track_converges(tscene, otrk):
     assert np.all(np.isnan(out["lastResiduals"][tscene.n_levels:]))
 
 
+def test_sum_order_spread_is_rounding_level(tscene, otrk):
+    """The order-spread hook the GPU LM bars are tied to (tests/test_gpu_track.py): with every calcRes /
+    calcGSSSE sum formed in reversed point order the per-point decisions are unchanged, the calcRes energy and the
+    normal equations move at fp32 summation-order level only, and the LM run still converges to the same pose."""
+    from hslam_amd.se3 import SE3
+    T = SE3.exp([0.004, -0.003, 0.002, 0.002, 0.001, -0.002]) * SE3.from_data(tscene.T_true)
+    r0 = otrk.calc_res(0, T.data(), [0.0, 0.0], 20.0)
+    otrk.set_sum_order(1)
+    try:
+        r1 = otrk.calc_res(0, T.data(), [0.0, 0.0], 20.0)
+        out1 = otrk.track(SE3().data(), [0.0, 0.0], tscene.n_levels - 1, np.full(5, np.nan))
+    finally:
+        otrk.set_sum_order(0)
+    out0 = otrk.track(SE3().data(), [0.0, 0.0], tscene.n_levels - 1, np.full(5, np.nan))
+    assert r1[3] == r0[3] and r1[0][1] == r0[0][1]            # warped count, numTermsInE
+    assert r1[0][0] != r0[0][0] or not np.array_equal(r1[1], r0[1])  # another order: other roundings
+    assert abs(r1[0][0] - r0[0][0]) <= 1e-5 * abs(r0[0][0])
+    assert np.allclose(r1[1], r0[1], rtol=1e-4, atol=1e-6 * np.abs(r0[1]).max())
+    err = (SE3.from_data(out1["T"]) * SE3.from_data(out0["T"]).inverse()).log()
+    assert out1["ok"] and np.linalg.norm(err) < 1e-4
+
+
 def test_track_abort_keeps_inputs(tscene, otrk):
     from hslam_amd.se3 import SE3
     T0 = SE3().data()
