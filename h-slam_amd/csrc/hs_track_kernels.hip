@@ -22,6 +22,7 @@
 #include <cfloat>
 
 #include "hs_track_kernels.h"
+#include "hs_se3_dev.h"
 
 namespace {
 
@@ -73,7 +74,7 @@ __device__ __forceinline__ void ldlt8_solve(const double* __restrict__ A, const 
         const int tp = pm[k]; pm[k] = pm[j]; pm[j] = tp;
       }
   }
-  double M[8][8], y[8], D[8];
+  double M[8][8], y[8], D[8], Dinv[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
 #pragma unroll
@@ -100,9 +101,12 @@ __device__ __forceinline__ void ldlt8_solve(const double* __restrict__ A, const 
     }
     const double d = M[k][k];
     D[k] = d;
+    // one IEEE division per pivot, then products (Eigen divides every entry: rounding-level only; a single
+    // thread's fp64 division is a ~100-cycle dependent chain, 36 of them were a third of the LM step)
+    Dinv[k] = fabs(d) > DBL_MIN ? 1.0 / d : 0.0;
     if (fabs(d) > DBL_MIN) {
 #pragma unroll
-      for (int i = k + 1; i < 8; i++) M[i][k] /= d;
+      for (int i = k + 1; i < 8; i++) M[i][k] *= Dinv[k];
     }
   }
 #pragma unroll
@@ -110,7 +114,7 @@ __device__ __forceinline__ void ldlt8_solve(const double* __restrict__ A, const 
 #pragma unroll
     for (int k = 0; k < i; k++) y[i] = y[i] - M[i][k] * y[k];
 #pragma unroll
-  for (int i = 0; i < 8; i++) y[i] = fabs(D[i]) > DBL_MIN ? y[i] / D[i] : 0.0;
+  for (int i = 0; i < 8; i++) y[i] = y[i] * Dinv[i];
 #pragma unroll
   for (int i = 7; i >= 0; i--)
 #pragma unroll
@@ -505,7 +509,8 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
         for (int i = 0; i < 8; i++) ssum += incScaled[i];
         if (!isfinite(ssum))
           for (int i = 0; i < 8; i++) incScaled[i] = 0;
-        const hs::SE3 nw = hs::SE3::exp(incScaled) * hs::SE3::fromData(S.T);
+        // the series exp / rsqrt-normalized product of the BA doStep (hs_se3_dev.h): Sophus' up to rounding
+        const hs::SE3 nw = se3_mul_step(se3_exp_step(incScaled), hs::SE3::fromData(S.T));
         nw.toData(S.Tn);
         S.affn[0] = S.aff[0] + incScaled[6];
         S.affn[1] = S.aff[1] + incScaled[7];
