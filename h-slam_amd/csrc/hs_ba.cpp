@@ -180,8 +180,8 @@ int ensure_capacity(hs_ctx* c, int W, int H, int capP, int capBlk) {
   HS_TRY(dalloc(&c->d_cand, (size_t)stride * c->nranks));
   HS_HIP(hipMemset(c->d_cand, 0xff, sizeof(float) * (size_t)stride * c->nranks));  // NaN, sign set: no candidate
   if (c->multi_rank()) HS_TRY(dalloc(&c->d_gsys, ((size_t)SLmax + 3) * c->nranks));
-  HS_TRY(dalloc(&c->d_rs_cnt, 1));
-  HS_HIP(hipMemset(c->d_rs_cnt, 0, sizeof(unsigned int)));
+  HS_TRY(dalloc(&c->d_rs_cnt, 4));  // [0] the counter, [1] the spin-bound flag
+  HS_HIP(hipMemset(c->d_rs_cnt, 0, 4 * sizeof(unsigned int)));
   c->rs_total = 0;
   {
     const char* fe = std::getenv("HS_FUSE_RS");
@@ -759,7 +759,11 @@ static int gn_iterations(hs_ctx* c, int it0, int K, bool allow_break, double* en
   HS_HIP(hipMemcpyAsync(&elog[k], c->sysE(), sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HS_HIP(hipMemcpyAsync(&c->h_ctl[1], (char*)c->d_state + offsetof(HsDevState, status), sizeof(int),
                         hipMemcpyDeviceToHost, c->stream));
+  unsigned int rs_timeout = 0;
+  if (c->fuse_rs) HS_HIP(hipMemcpyAsync(&rs_timeout, c->d_rs_cnt + 1, sizeof(unsigned int), hipMemcpyDeviceToHost,
+                                        c->stream));
   HS_HIP(hipStreamSynchronize(c->stream));
+  if (rs_timeout) return fail(HS_ERR_HIP, "hs_k_redstitch: the reduce blocks never arrived (spin bound hit)");
   double tl = 0, ta = 0, ts = 0;
   for (int q = 0; q < std::min(k, nev); q++) {
     float ms;

@@ -1644,17 +1644,30 @@ __global__ __launch_bounds__(ST_NT) void hs_k_redstitch(HsStitchArgs a, unsigned
     if (b < nred) red_host_chunk(r, b / r.Q, b % r.Q);
     else if (b == nred) red_energy_block(r);
     else red_th_hist_block(r, b - nred - 1);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    // publish (cdna_hip_programming.md §6 Guideline 16): every storing wave drains its stores, the barrier, ONE
+    // lane's agent-scope release (L2 write-back) and its drain, then the relaxed counter add
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     return;
   }
-  if (threadIdx.x == 0) {
-    while ((int)(__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0)
+  if (threadIdx.x == 0) {  // consume: ONE lane polls relaxed (bounded), ONE agent acquire, its drain, the barrier
+    unsigned int spins = 0;
+    while ((int)(__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
       __builtin_amdgcn_s_sleep(1);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the CU's L1 and the XCD's L2 lines invalidated
+      if (++spins == (1u << 24)) {  // ~seconds: the reduce blocks never arrived; flag it (cnt[1]) and go on
+        __hip_atomic_store(cnt + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
-  __syncthreads();  // no wave of the block has loaded anything before this point
+  __syncthreads();  // no wave of the block has loaded a host sum before this point
   stitch_block(a, b - nR, lds);
 }
 

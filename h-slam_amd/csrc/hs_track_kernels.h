@@ -56,9 +56,9 @@ struct HsTrackArgs {
   // G workgroups per hypothesis (blocks h G .. h G + G - 1): each pass's points are spread over them; their sums
   // meet in part [n][2][G][HS_TRK_NRED] (pass parity) behind a counter per hypothesis (cnt [n], zero at launch),
   // and every workgroup forms the same totals (in workgroup order) and runs the same LM step
-  int G;
+  int G, nhyp;
   double* part;
-  unsigned int* cnt;
+  unsigned int* cnt;    // [2 nhyp]: pass counters, then a timeout flag per hypothesis
 };
 constexpr int HS_TRK_NRED = 52;  // the reduced values of a pass (45 normal-equation entries, 4 energies / flows, 3 counts)
 constexpr int HS_TRK_MAXG = 32;

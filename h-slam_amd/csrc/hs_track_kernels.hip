@@ -335,21 +335,36 @@ __device__ void trk_pass(const HsTrackArgs& a, TrkShared& S, int h, int g) {
   if (G > 1) {
     // the hypothesis' workgroups meet: partials out (agent-scope release by every wave), one relaxed increment,
     // spin until all G of this pass are in (agent-scope acquire), then every workgroup sums them in workgroup order
+    // (cdna_hip_programming.md §6 Guideline 16, write-through form): the partials are stored sc1 by wave 0 alone
+    // (tid < 52), drained, and wave 0's lane 0 adds to the counter; every load of them is an sc1 load, so no
+    // release / acquire fence is needed (the loads only wait for the poll, behind a workgroup barrier)
     double* P = a.part + ((size_t)h * 2 + (S.npass & 1)) * G * TRK_NRED;
-    if (tid < TRK_NRED) P[g * TRK_NRED + tid] = S.red[0][tid];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __syncthreads();
-    if (tid == 0) {
-      __hip_atomic_fetch_add(a.cnt + h, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned int target = (unsigned int)G * (unsigned int)(S.npass + 1);
-      while ((int)(__hip_atomic_load(a.cnt + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0)
-        __builtin_amdgcn_s_sleep(1);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (tid < TRK_NRED)
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(P + g * TRK_NRED + tid),
+                         (unsigned long long)__double_as_longlong(S.red[0][tid]), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    if (tid < 64) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (tid == 0) {
+        __hip_atomic_fetch_add(a.cnt + h, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned int target = (unsigned int)G * (unsigned int)(S.npass + 1);
+        unsigned int spins = 0;
+        while ((int)(__hip_atomic_load(a.cnt + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins == (1u << 24)) {  // a member never arrived (~seconds): flag the hypothesis, go on
+            __hip_atomic_store(a.cnt + a.nhyp + h, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+      }
     }
     __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the poll
     if (tid < TRK_NRED) {
       double s = 0.0;
-      for (int gg = 0; gg < G; gg++) s += P[gg * TRK_NRED + tid];
+      for (int gg = 0; gg < G; gg++)
+        s += __longlong_as_double((long long)__hip_atomic_load(
+            reinterpret_cast<unsigned long long*>(P + gg * TRK_NRED + tid), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
       S.red[0][tid] = s;
     }
     __syncthreads();
