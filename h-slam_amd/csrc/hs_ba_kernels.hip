@@ -29,6 +29,10 @@
 #include "hs_kernels.h"
 #include "hs_se3_dev.h"
 
+#ifndef LIN_WT
+#define LIN_WT 0  // hs_k_lin's block partials stored write-through (sc1)
+#endif
+
 namespace {
 
 constexpr float SCALE_F = 50.0f, SCALE_C = 50.0f, SCALE_IDEPTH = 1.0f;
@@ -778,6 +782,9 @@ __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
   // for each LDS load in turn); waves past W hold no points and are not added
   static_assert((NE * 64) % 4 == 0, "partials staged as float4");
   float4* out4 = reinterpret_cast<float4*>(a.part + (size_t)b * NE * 64);
+#if LIN_WT
+  const auto prs = __builtin_amdgcn_make_buffer_rsrc(a.part + (size_t)b * NE * 64, 0, NE * 64 * 4, 0x00020000);
+#endif
   const float4* st4 = reinterpret_cast<const float4*>(lin_stage);
   // both rounds' loads issued together (the round count is a compile-time constant), then the sums
   constexpr int NI = (NE * 16 + HS_LIN_NT - 1) / HS_LIN_NT;
@@ -798,7 +805,18 @@ __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
         s.z += v[k][w].z;
         s.w += v[k][w].w;
       }
+#if LIN_WT
+    // write-through (sc1): the partials leave the XCD's L2 during the kernel instead of in its end-of-kernel
+    // write-back, which the next launch (hs_k_reduce) waits for
+    if (i < NE * 16) {
+      typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+      u4 w;
+      w.x = __float_as_uint(s.x); w.y = __float_as_uint(s.y); w.z = __float_as_uint(s.z); w.w = __float_as_uint(s.w);
+      __builtin_amdgcn_raw_buffer_store_b128(w, prs, i * 16, 0, 16);
+    }
+#else
     if (i < NE * 16) out4[i] = s;
+#endif
   }
   if (tid < 3) {
     double s = se[tid];

@@ -32,14 +32,17 @@ constexpr int Q8_N = 17;  // per-pixel quantities summed over the pattern
 #ifndef L8_TAP_GROUP
 #define L8_TAP_GROUP 8  // pixels whose taps may be in flight together (8: no scheduling barrier)
 #endif
+// Production: occupancy 2 (two waves per SIMD hide each other's tap latency), which the accumulators in LDS and no
+// cross-group prefetch make fit in 256 registers without spills (244).  Measured (r03_b1): 2M points 1929 -> 1512 us
+// per launch (HBM frac 0.39 -> 0.50), 200k 243 -> 200 us, per-residual outputs bit-identical.
 #ifndef L8_MIN_WAVES
-#define L8_MIN_WAVES 1  // waves per SIMD the register budget must allow (launch bounds)
+#define L8_MIN_WAVES 2  // waves per SIMD the register budget must allow (launch bounds)
 #endif
 #ifndef L8_PREFETCH
-#define L8_PREFETCH 1   // the next point group's inputs are loaded while the current group computes
+#define L8_PREFETCH 0   // 1: the next point group's inputs are loaded while the current group computes (occupancy 1)
 #endif
 #ifndef L8_LDS_ACC
-#define L8_LDS_ACC 0    // the per-lane accumulators (T slice, accD / accE / accEB / accHcc) live in LDS between groups
+#define L8_LDS_ACC 1    // the per-lane accumulators (T slice, accD / accE / accEB / accHcc) live in LDS between groups
 #endif
 
 // Data (r, c), r <= c < 10, in the natural per-lane layout

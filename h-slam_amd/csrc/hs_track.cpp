@@ -142,7 +142,9 @@ static int run_tries(hs_tracker* t, int n, const double* h_in, int coarsest, int
   a.pass_cutoff = cutoff;
   // workgroups per hypothesis: the chip's 256 CUs shared by the hypotheses (every member must be resident at once:
   // they meet once per pass), at most HS_TRK_MAXG; env HS_TRK_G caps it (1 = the one-workgroup LM loop)
-  int G = 1;  // (default until measured on the GPU)
+  // 8 measured best at C2 (r03_b1: G = 1 / 8 / 16 / 32: 0.61 / 0.48 / 0.53 / 0.63 ms per track: more members
+  // shorten the point loop but lengthen the per-pass meeting)
+  int G = std::max(1, std::min(8, 256 / std::max(1, n)));
   if (const char* e = std::getenv("HS_TRK_G"))
     G = std::max(1, std::min({HS_TRK_MAXG, 256 / std::max(1, n), std::atoi(e)}));
   if (single_pass) G = 1;

@@ -145,23 +145,49 @@ struct TrkShared {
   long long prof[6];  // HS_KTRACE: thread-0 cycles: point loop, reductions, LM step, passes, wave reduce, barrier
 };
 
-// The wave sum of the xor butterfly (v += shfl_xor(v, o), o = 32 .. 1) as lane 0 holds it, bit for bit, with one
-// cross-lane LDS op instead of six: at step o the lanes i < o that lane 0's result depends on add lane i + o =
-// lane i ^ o, in the same operand order, so the halves are a permlane32 swap, the ^16 step a bpermute and the
-// ^8 .. ^1 steps DPP row shifts (row_shl:o).  Only lane 0's result is meaningful.
+// Wave reduce-scatter of 64 values (v[i], i < 64) over the 64 lanes: afterwards lane l holds the sum of v[l] over
+// all lanes.  Each step pairs every lane with one partner, keeps half of its remaining values (the upper half when
+// its bit of the step is set) and adds the partner's copies of them: permlane32 swap (bit 5), permlane16 swap
+// (bit 4), DPP row_ror:8 (bit 3), row_half_mirror (pairs l, l ^ 7 within 8: bit 2 decides), quad_perm [2,3,0,1]
+// (bit 1) and [1,0,3,2] (bit 0): 63 exchanges + 63 adds for 64 values, against 64 x 6 exchanges of per-value trees.
 template <int CTRL>
-__device__ __forceinline__ float dpp_row_shl(float v) {
+__device__ __forceinline__ float dpp_mov(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
 }
-__device__ __forceinline__ float xor_tree_lane0(float v) {
-  const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  v = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);  // lanes i < 32: v_i + v_(i + 32)
-  v = v + __shfl_xor(v, 16);
-  v = v + dpp_row_shl<0x108>(v);  // row_shl:8
-  v = v + dpp_row_shl<0x104>(v);
-  v = v + dpp_row_shl<0x102>(v);
-  v = v + dpp_row_shl<0x101>(v);
-  return v;
+__device__ __forceinline__ float wave_reduce_scatter64(const float (&v)[64], int lane) {
+  float a[32];
+#pragma unroll
+  for (int i = 0; i < 32; i++) {  // lanes < 32: v_i + v_i(lane + 32); lanes >= 32: v_(32+i)(lane - 32) + v_(32+i)
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[i]), __float_as_uint(v[32 + i]), false, false);
+    a[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  float b[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) {  // rows 0, 2 keep a[i], rows 1, 3 keep a[16 + i]
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a[i]), __float_as_uint(a[16 + i]), false, false);
+    b[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  const bool b3 = (lane & 8) != 0, b2 = (lane & 4) != 0, b1 = (lane & 2) != 0, b0 = (lane & 1) != 0;
+  float c[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {  // partner l ^ 8 (row_ror:8)
+    const float keep = b3 ? b[8 + i] : b[i], send = b3 ? b[i] : b[8 + i];
+    c[i] = keep + dpp_mov<0x128>(send);
+  }
+  float d[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {  // partner (l & ~7) | (7 - (l & 7)) (row_half_mirror): bit 2 differs
+    const float keep = b2 ? c[4 + i] : c[i], send = b2 ? c[i] : c[4 + i];
+    d[i] = keep + dpp_mov<0x141>(send);
+  }
+  float e[2];
+#pragma unroll
+  for (int i = 0; i < 2; i++) {  // partner l ^ 2 (quad_perm [2,3,0,1])
+    const float keep = b1 ? d[2 + i] : d[i], send = b1 ? d[i] : d[2 + i];
+    e[i] = keep + dpp_mov<0x4E>(send);
+  }
+  const float keep = b0 ? e[1] : e[0], send = b0 ? e[0] : e[1];  // partner l ^ 1 (quad_perm [1,0,3,2])
+  return keep + dpp_mov<0xB1>(send);
 }
 
 // calcRes + calcGSSSE at S.RKi / S.t / S.affLL for level S.lvl; results in S.res / S.H / S.b / S.nWarped
@@ -295,32 +321,23 @@ __device__ void trk_pass(const HsTrackArgs& a, TrkShared& S, int h, int g) {
     }
   }
   const long long pc1 = (a.trace && tid == 0) ? clock64() + (long long)(acc[0] * 0.f + acc[44] * 0.f) : 0;
-  // wave reductions (fixed xor tree), then the waves in order in fp64
-  float vals[TRK_NRED];
+  // wave reductions (one reduce-scatter: lane q ends with value q's wave sum; the counts are small integers, exact in
+  // fp32), then the waves in order in fp64
+  float vals[64];
 #pragma unroll
   for (int q = 0; q < TRK_NACC; q++) vals[q] = acc[q];
   vals[TRK_NACC + 0] = E;
   vals[TRK_NACC + 1] = sT;
   vals[TRK_NACC + 2] = sRT;
   vals[TRK_NACC + 3] = sN;
-  vals[TRK_NACC + 4] = __int_as_float(nE);
-  vals[TRK_NACC + 5] = __int_as_float(nSat);
-  vals[TRK_NACC + 6] = __int_as_float(nW);
+  vals[TRK_NACC + 4] = (float)nE;
+  vals[TRK_NACC + 5] = (float)nSat;
+  vals[TRK_NACC + 6] = (float)nW;
 #pragma unroll
-  for (int q = 0; q < TRK_NRED; q++) {
-    if (q < TRK_NACC + 4) {
-      vals[q] = xor_tree_lane0(vals[q]);
-    } else {
-      int v = __float_as_int(vals[q]);
-      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-      vals[q] = __int_as_float(v);
-    }
-  }
-  if (lane == 0)
-#pragma unroll
-    for (int q = 0; q < TRK_NRED; q++)
-      S.red[wv][q] = q < TRK_NACC + 4 ? (double)vals[q] : (double)__float_as_int(vals[q]);
-  const long long pcw = (a.trace && tid == 0) ? clock64() + (long long)(vals[3] * 0.f) : 0;
+  for (int q = TRK_NRED; q < 64; q++) vals[q] = 0.f;
+  const float mine = wave_reduce_scatter64(vals, lane);
+  if (lane < TRK_NRED) S.red[wv][lane] = (double)mine;
+  const long long pcw = (a.trace && tid == 0) ? clock64() + (long long)(mine * 0.f) : 0;
   __syncthreads();
   if (a.trace && tid == 0) {
     S.prof[4] += pcw - pc1;
