@@ -435,12 +435,16 @@ static HsRedArgs red_args(hs_ctx* c, bool skip_threshold) {
   return a;
 }
 
-// the gathered systems summed (+ the threshold select when it is pending) by hs_k_combine
+// what a solve launch would have done beside the solve, when none follows: hs_k_combine's block 0 sums the gathered
+// systems (multi-rank), block 1 selects the threshold (when it is pending)
 static int launch_combine(hs_ctx* c) {
+  if (!c->gath_pending && !c->gath_th) return HS_OK;
   HsSolveArgs a;
   std::memset(&a, 0, sizeof(a));
   a.nF = c->nF;
-  a.gsys = c->d_gsys; a.nranks = c->nranks; a.gstride = c->SL() + 3; a.sys_out = c->d_sys;
+  if (c->gath_pending) {
+    a.gsys = c->d_gsys; a.nranks = c->nranks; a.gstride = c->SL() + 3; a.sys_out = c->d_sys;
+  }
   a.th_local = c->gath_th ? 1 : 0;
   a.th = red_args(c, false);
   hipLaunchKernelGGL(hs_k_combine, dim3(c->gath_th ? 2 : 1), dim3(HS_SOLVE_NT), 0, c->stream, a);
@@ -489,8 +493,12 @@ static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = fals
                          bool defer = false) {
   const bool xch = c->multi_rank() && !readback;
   HsRedArgs a = red_args(c, skip_threshold);
-  // single rank: pass 1 of the select in hs_k_reduce, the rest in the stitch launch; multi-rank: after the exchange
-  a.nhist = (skip_threshold || xch) ? 0 : a.nhist;
+  // setNewFrameEnergyTH: windows below kLin8MinPoints (and every multi-rank window) select in block 1 of the next
+  // solve launch (or hs_k_combine), beside the solve: the select only feeds the next linearize, and as the stitch
+  // launch's last block it outlasted the stitch's blocks by ~1.5 us at 2k.  Large single-rank windows: pass 1 in
+  // hs_k_reduce's histogram blocks, pass 2 in the stitch launch, pass 3 after it.
+  const bool beside = !skip_threshold && !readback && (xch || !c->th_multi);
+  a.nhist = (skip_threshold || beside) ? 0 : a.nhist;
   const bool fused = c->fuse_rs && !readback && !c->capturing;
   if (fused) a.Q = (c->ne * 64 + HS_STITCH_NT - 1) / HS_STITCH_NT;  // 1024-entry host-sum chunks
   if (!readback && !fused) {
@@ -512,7 +520,7 @@ static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = fals
   st.sc = 1.0f / (1 + 1e-5);   // H -= H_sc * (1.0f / (1 + lambda)) (:763)
   st.trace = c->d_tr_st;
   st.red = a;
-  st.red.skip_threshold = (skip_threshold || readback || multi || xch) ? 1 : 0;
+  st.red.skip_threshold = (skip_threshold || readback || multi || beside) ? 1 : 0;
   const int nS = c->nF * (c->nF + 1) / 2 + c->nF + 2 + (multi ? a.np2 : 0);
   if (fused) {
     const int nR = c->nF * a.Q + 1 + a.nhist;
@@ -530,6 +538,10 @@ static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = fals
     HS_HIP(hipGetLastError());
   }
   if (sep) c->sepValid = true;
+  if (beside && !xch) {
+    c->gath_th = true;
+    if (!defer) HS_TRY(launch_combine(c));
+  }
   if (xch) {
     if (!c->group.empty()) {  // the group driver exchanges once every member has reduced
       c->xch_local = true;
@@ -553,12 +565,14 @@ static int launch_solve(hs_ctx* c, int flags, int iteration, bool log) {
   a.sys = c->d_sys;
   a.sysE = c->sysE();
   int grid = 1;
-  if (c->gath_pending) {
+  if (c->gath_pending || c->gath_th) {
     if (!(flags & HS_SOLVE)) {
       HS_TRY(launch_combine(c));
     } else {  // the fused GN loop: the gathered sums in the solve's prefetch, the select as block 1 beside it
-      a.sys = c->d_gsys;
-      a.gsys = c->d_gsys; a.nranks = c->nranks; a.gstride = c->SL() + 3; a.sys_out = c->d_sys;
+      if (c->gath_pending) {
+        a.sys = c->d_gsys;
+        a.gsys = c->d_gsys; a.nranks = c->nranks; a.gstride = c->SL() + 3; a.sys_out = c->d_sys;
+      }
       a.th_local = c->gath_th ? 1 : 0;
       a.th = red_args(c, false);
       grid = c->gath_th ? 2 : 1;

@@ -212,8 +212,8 @@ struct hs_ctx {
   int rank = 0, nranks = 1;
   // the multi-rank exchange (launch_reduce / exchange in hs_ba.cpp): one all-gather per linearization of every
   // rank's system vector + energies into d_gsys [nranks][SL + 3] and of its newest-frame candidates into d_cand.
-  // gath_pending: a gather whose sums are formed by the next solve launch (the fused GN loop); gath_th: its
-  // threshold select is still to run (block 1 of that launch)
+  // gath_pending: a gather whose sums are formed by the next solve launch (the fused GN loop); gath_th: the
+  // threshold select is still to run (block 1 of that launch; single-rank windows below kLin8MinPoints too)
   double* d_gsys = nullptr;
   bool gath_pending = false, gath_th = false;
   // in-process rank group (test hook hs_ba_debug_group): the same exchange by device copies between the contexts of
