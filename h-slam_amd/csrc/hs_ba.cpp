@@ -56,7 +56,7 @@ static void free_buffers(hs_ctx* c) {
       c->d_hostsum, c->d_sys, c->d_sep, c->d_adHost, c->d_adTarget, c->d_adHostF, c->d_adTargetF, c->d_HM, c->d_bM,
       c->d_Nproj, c->d_xAd, c->d_x, c->d_elog, c->d_cand, c->d_tr_lin, c->d_tr_acc, c->d_tr_solve, c->d_tr_st,
       c->d_marg, c->d_adHTdelta, c->d_p_HdiF_alt, c->d_th_hist, c->d_th_hist2, c->d_th_surv, c->d_th_nsurv,
-      c->d_le_chunk, c->d_le_out, c->d_ref_pts, c->d_ref_n, c->d_stage, c->d_gsys, c->d_rs_cnt};
+      c->d_le_chunk, c->d_le_out, c->d_ref_pts, c->d_ref_n, c->d_stage, c->d_gsys};
   for (auto& s : c->ps) {
     for (void* p : {(void*)s.u, (void*)s.v, (void*)s.idepth, (void*)s.idepth_zero, (void*)s.priorF, (void*)s.color,
                     (void*)s.weight, (void*)s.relBL, (void*)s.nGood, (void*)s.r_state, (void*)s.r_center})
@@ -94,8 +94,6 @@ static void free_buffers(hs_ctx* c) {
   c->d_stage = nullptr;
   c->d_gsys = nullptr;
   c->gath_pending = c->gath_th = false;
-  c->d_rs_cnt = nullptr;
-  c->rs_total = 0;
   c->d_stage_cap = 0;
   c->cap_P = c->cap_blk = c->cap_W = c->cap_H = c->cap_stride = 0;
   bind_point_set(c);
@@ -180,13 +178,6 @@ int ensure_capacity(hs_ctx* c, int W, int H, int capP, int capBlk) {
   HS_TRY(dalloc(&c->d_cand, (size_t)stride * c->nranks));
   HS_HIP(hipMemset(c->d_cand, 0xff, sizeof(float) * (size_t)stride * c->nranks));  // NaN, sign set: no candidate
   if (c->multi_rank()) HS_TRY(dalloc(&c->d_gsys, ((size_t)SLmax + 3) * c->nranks));
-  HS_TRY(dalloc(&c->d_rs_cnt, 4));  // [0] the counter, [1] the spin-bound flag
-  HS_HIP(hipMemset(c->d_rs_cnt, 0, 4 * sizeof(unsigned int)));
-  c->rs_total = 0;
-  {
-    const char* fe = std::getenv("HS_FUSE_RS");
-    c->fuse_rs = fe && fe[0] == '1';
-  }
   HS_TRY(dalloc(&c->d_th_hist, HS_TH_BINS));
   HS_TRY(dalloc(&c->d_th_hist2, 1024));
   HS_TRY(dalloc(&c->d_th_nsurv, 2));
@@ -208,8 +199,7 @@ int ensure_capacity(hs_ctx* c, int W, int H, int capP, int capBlk) {
   if (c->tracing) {
     HS_TRY(dalloc(&c->d_tr_lin, (size_t)capBlk * 16));
     HS_TRY(dalloc(&c->d_tr_acc, (size_t)(HS_MAXF * ((ne * 64 + 255) / 256) + 1 + 64) * 16));
-    // + the reduce roles of hs_k_redstitch (1024-entry chunks, the energy block, up to 64 histogram blocks, 64 pass-2)
-    HS_TRY(dalloc(&c->d_tr_st, (size_t)(HS_MAXF * (HS_MAXF + 1) / 2 + HS_MAXF + 2 + HS_MAXF * 8 + 1 + 128) * 16));
+    HS_TRY(dalloc(&c->d_tr_st, (size_t)(HS_MAXF * (HS_MAXF + 1) / 2 + HS_MAXF + 2) * 16));
     HS_TRY(dalloc(&c->d_tr_solve, 32));
   }
   c->cap_W = W; c->cap_H = H; c->cap_P = capP; c->cap_blk = capBlk;
@@ -320,7 +310,7 @@ int make_partition(hs_ctx* c) {
   c->lin8 = !c->exact && nP >= kLin8MinPoints;
   if (const char* e = std::getenv("HS_LIN8")) c->lin8 = !c->exact && e[0] == '1';
   // the extra launch of pass 3 costs more than a one-block scan of a small window's candidates
-  c->th_multi = nP >= kLin8MinPoints;
+  c->th_multi = nP >= kThMultiMinPoints;
   if (const char* e = std::getenv("HS_TH_MULTI")) c->th_multi = e[0] == '1';
   // points per block: hs_k_lin HS_LIN_NW waves x ppw points; hs_k_lin8 4 waves x ppw groups of 8 points (its
   // partition also serves hs_k_lin's marginalization / linearizeAll(true) passes, with W = 4 of its waves)
@@ -499,9 +489,7 @@ static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = fals
   // hs_k_reduce's histogram blocks, pass 2 in the stitch launch, pass 3 after it.
   const bool beside = !skip_threshold && !readback && (xch || !c->th_multi);
   a.nhist = (skip_threshold || beside) ? 0 : a.nhist;
-  const bool fused = c->fuse_rs && !readback && !c->capturing;
-  if (fused) a.Q = (c->ne * 64 + HS_STITCH_NT - 1) / HS_STITCH_NT;  // 1024-entry host-sum chunks
-  if (!readback && !fused) {
+  if (!readback) {
     hipLaunchKernelGGL(hs_k_reduce, dim3(c->nF * c->Q + 1 + a.nhist), dim3(256), 0, c->stream, a);
     HS_HIP(hipGetLastError());
   }
@@ -522,15 +510,7 @@ static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = fals
   st.red = a;
   st.red.skip_threshold = (skip_threshold || readback || multi || beside) ? 1 : 0;
   const int nS = c->nF * (c->nF + 1) / 2 + c->nF + 2 + (multi ? a.np2 : 0);
-  if (fused) {
-    const int nR = c->nF * a.Q + 1 + a.nhist;
-    c->rs_total += (unsigned int)nR;
-    hipLaunchKernelGGL(hs_k_redstitch, dim3(nR + nS), dim3(HS_STITCH_NT), 0, c->stream, st, c->d_rs_cnt, c->rs_total,
-                       nR);
-  } else {
-    hipLaunchKernelGGL(hs_k_stitch, dim3(nS), dim3(HS_STITCH_NT), 0, c->stream, st);
-  }
-  c->rs_traced = fused;
+  hipLaunchKernelGGL(hs_k_stitch, dim3(nS), dim3(HS_STITCH_NT), 0, c->stream, st);
   HS_HIP(hipGetLastError());
   if (multi) {  // pass 3: the select block over pass 2's histogram and survivors (a side stream measured no faster:
                 // its cross-queue event hand-offs cost what the overlap with the solve saves)
@@ -677,14 +657,6 @@ static int dump_traces(hs_ctx* c) {
     std::fprintf(stderr, "\n");
   }
   HS_TRY(dump_one("linearize", c->d_tr_lin, c->nblk, tick_us, c->stream, &f[1], &l[1]));
-  if (c->rs_traced) {  // hs_k_redstitch: only its stitch blocks stamp (at their fused block index)
-    HS_TRY(dump_one("redstitch", c->d_tr_st, c->nF * (c->nF + 1) / 2 + c->nF + 2 + HS_MAXF * 8 + 1 + 128, tick_us,
-                    c->stream, &f[3], &l[3]));
-    if (f[0] > 0 && f[1] > 0 && f[3] > 0)
-      std::fprintf(stderr, "[hs trace] chain us: solve %.2f | gap %.2f | lin %.2f | gap+reduce+stitch %.2f\n",
-                   (l[0] - f[0]) * tick_us, (f[1] - l[0]) * tick_us, (l[1] - f[1]) * tick_us, (l[3] - l[1]) * tick_us);
-    return HS_OK;
-  }
   HS_TRY(dump_one("reduce", c->d_tr_acc, c->nF * c->Q + 1, tick_us, c->stream, &f[2], &l[2]));
   HS_TRY(dump_one("stitch", c->d_tr_st, c->nF * (c->nF + 1) / 2 + c->nF + 2, tick_us, c->stream, &f[3], &l[3]));
   // the last iteration's launch chain on the wall clock: each kernel's first block start -> last checkpoint, and the
@@ -715,14 +687,12 @@ static int gn_iterations(hs_ctx* c, int it0, int K, bool allow_break, double* en
       float *sv_h = c->d_p_HdiF, *sv_a = c->d_p_HdiF_alt, *sv_s = c->hdif_solved;
       hipGraph_t g = nullptr;
       HS_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-      c->capturing = true;  // a replayed graph cannot advance hs_k_redstitch's counter target
       int rc = HS_OK;
       for (int q = 0; q < 2 && rc == HS_OK; q++) {
         if ((rc = launch_solve(c, HS_SOLVE | HS_APPLY, -1, true)) != HS_OK) break;
         if ((rc = launch_linearize(c, 1)) != HS_OK) break;
         rc = launch_reduce(c);
       }
-      c->capturing = false;
       if (rc != HS_OK) {  // leave the stream out of capture mode and the ping-pong as it was
         hipGraph_t partial = nullptr;
         (void)hipStreamEndCapture(c->stream, &partial);
@@ -773,11 +743,7 @@ static int gn_iterations(hs_ctx* c, int it0, int K, bool allow_break, double* en
   HS_HIP(hipMemcpyAsync(&elog[k], c->sysE(), sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HS_HIP(hipMemcpyAsync(&c->h_ctl[1], (char*)c->d_state + offsetof(HsDevState, status), sizeof(int),
                         hipMemcpyDeviceToHost, c->stream));
-  unsigned int rs_timeout = 0;
-  if (c->fuse_rs) HS_HIP(hipMemcpyAsync(&rs_timeout, c->d_rs_cnt + 1, sizeof(unsigned int), hipMemcpyDeviceToHost,
-                                        c->stream));
   HS_HIP(hipStreamSynchronize(c->stream));
-  if (rs_timeout) return fail(HS_ERR_HIP, "hs_k_redstitch: the reduce blocks never arrived (spin bound hit)");
   double tl = 0, ta = 0, ts = 0;
   for (int q = 0; q < std::min(k, nev); q++) {
     float ms;

@@ -51,6 +51,7 @@ constexpr int kLinBlocksTarget = 256;  // linearize blocks of a window (points p
 // many points up: its wave issues ~2.3x fewer instructions per point (throughput), while hs_k_lin's one-point waves
 // finish a small window sooner (latency).  Env HS_LIN8=0 / 1 forces either.
 constexpr int kLin8MinPoints = 60000;
+constexpr int kThMultiMinPoints = 60000;  // the multi-block threshold select (below: one block beside the solve)
 constexpr int kLin8BlocksTarget = 512;  // hs_k_lin8 blocks of a window (two 4-wave blocks per CU)
 
 template <typename T>
@@ -222,11 +223,7 @@ struct hs_ctx {
   int group_stride = 0;
   bool xch_local = false, xch_th = false, xch_defer = false;  // group: a local reduce awaits the exchange
   hipEvent_t ev_xch[2] = {nullptr, nullptr};
-  // hs_k_redstitch (env HS_FUSE_RS=1): reduce + stitch in one launch, ordered by a device counter that only grows
-  bool fuse_rs = false, capturing = false;
-  unsigned int* d_rs_cnt = nullptr;
-  unsigned int rs_total = 0;  // the counter's value once every launch so far has completed
-  bool rs_traced = false;     // the last reduce + stitch ran fused (the trace dump reads its blocks from d_tr_st)
+
   bool multi_rank() const { return comm != nullptr || !group.empty(); }
 
   // timings of the last optimize / iterate

@@ -29,9 +29,6 @@
 #include "hs_kernels.h"
 #include "hs_se3_dev.h"
 
-#ifndef LIN_WT
-#define LIN_WT 0  // hs_k_lin's block partials stored write-through (sc1)
-#endif
 
 namespace {
 
@@ -782,9 +779,6 @@ __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
   // for each LDS load in turn); waves past W hold no points and are not added
   static_assert((NE * 64) % 4 == 0, "partials staged as float4");
   float4* out4 = reinterpret_cast<float4*>(a.part + (size_t)b * NE * 64);
-#if LIN_WT
-  const auto prs = __builtin_amdgcn_make_buffer_rsrc(a.part + (size_t)b * NE * 64, 0, NE * 64 * 4, 0x00020000);
-#endif
   const float4* st4 = reinterpret_cast<const float4*>(lin_stage);
   // both rounds' loads issued together (the round count is a compile-time constant), then the sums
   constexpr int NI = (NE * 16 + HS_LIN_NT - 1) / HS_LIN_NT;
@@ -805,18 +799,7 @@ __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
         s.z += v[k][w].z;
         s.w += v[k][w].w;
       }
-#if LIN_WT
-    // write-through (sc1): the partials leave the XCD's L2 during the kernel instead of in its end-of-kernel
-    // write-back, which the next launch (hs_k_reduce) waits for
-    if (i < NE * 16) {
-      typedef unsigned int u4 __attribute__((ext_vector_type(4)));
-      u4 w;
-      w.x = __float_as_uint(s.x); w.y = __float_as_uint(s.y); w.z = __float_as_uint(s.z); w.w = __float_as_uint(s.w);
-      __builtin_amdgcn_raw_buffer_store_b128(w, prs, i * 16, 0, 16);
-    }
-#else
     if (i < NE * 16) out4[i] = s;
-#endif
   }
   if (tid < 3) {
     double s = se[tid];
@@ -1646,48 +1629,6 @@ __global__ __launch_bounds__(ST_NT) void hs_k_stitch(HsStitchArgs a) {
   stitch_block(a, blockIdx.x, lds);
 }
 
-// hs_k_reduce + hs_k_stitch as ONE launch (HS_FUSE_RS=1): blocks 0 .. nR-1 take hs_k_reduce's roles (host-sum
-// chunks of 1024 entries, the energy block, the pass-1 histogram blocks) and signal a counter (every wave's stores
-// written back by an agent-scope release, then one relaxed agent-scope increment); blocks nR.. are the stitch
-// blocks, which wait for the counter to reach its target (an agent-scope acquire after the spin) before reading the
-// host sums.  Reduce blocks have the lower block indices, so they are dispatched first and never wait: no deadlock.
-// The counter only grows; target = (launch epoch) x nR, compared wrap-safe.
-__global__ __launch_bounds__(ST_NT) void hs_k_redstitch(HsStitchArgs a, unsigned int* cnt, unsigned int target,
-                                                        int nR) {
-  __shared__ double lds[ST_LDS];
-  const int b = blockIdx.x;
-  const HsRedArgs& r = a.red;
-  if (b < nR) {
-    const int nred = r.nF * r.Q;
-    if (b < nred) red_host_chunk(r, b / r.Q, b % r.Q);
-    else if (b == nred) red_energy_block(r);
-    else red_th_hist_block(r, b - nred - 1);
-    // publish (cdna_hip_programming.md §6 Guideline 16): every storing wave drains its stores, the barrier, ONE
-    // lane's agent-scope release (L2 write-back) and its drain, then the relaxed counter add
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    return;
-  }
-  if (threadIdx.x == 0) {  // consume: ONE lane polls relaxed (bounded), ONE agent acquire, its drain, the barrier
-    unsigned int spins = 0;
-    while ((int)(__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins == (1u << 24)) {  // ~seconds: the reduce blocks never arrived; flag it (cnt[1]) and go on
-        __hip_atomic_store(cnt + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();  // no wave of the block has loaded a host sum before this point
-  stitch_block(a, b - nR, lds);
-}
 
 // =====================================================================================================
 // solve + step (fp64), one workgroup of 256 threads

@@ -215,7 +215,6 @@ __global__ void hs_k_reduce(HsRedArgs a);
 __global__ void hs_k_th_select(HsRedArgs a);
 __global__ void hs_k_th_pass2(HsRedArgs a);     // the multi-block pass 2 alone (test hook; multi-rank large windows)
 __global__ void hs_k_stitch(HsStitchArgs a);
-__global__ void hs_k_redstitch(HsStitchArgs a, unsigned int* cnt, unsigned int target, int nR);  // HS_FUSE_RS=1
 __global__ void hs_k_solve(HsSolveArgs a);
 __global__ void hs_k_combine(HsSolveArgs a);   // multi-rank: the gathered systems summed into sys_out (+ block 1: select)
 __global__ void hs_k_resub(HsResubArgs a);

@@ -96,8 +96,8 @@ static int ensure_tries(hs_tracker* t, int n) {
   TS_HIP(hipMalloc((void**)&t->d_out, sizeof(HsTryOut) * n));
   TS_HIP(hipMalloc((void**)&t->d_lmlog, sizeof(double) * 3 * HS_TRK_MAXLOG * n));
   TS_HIP(hipMalloc((void**)&t->d_lmlvl, sizeof(int) * HS_TRK_MAXLOG * n));
-  TS_HIP(hipMalloc((void**)&t->d_part, sizeof(double) * 2 * HS_TRK_MAXG * HS_TRK_NRED * n));
-  TS_HIP(hipMalloc((void**)&t->d_cnt, sizeof(unsigned int) * 2 * n + 16));
+  TS_HIP(hipMalloc((void**)&t->d_part, sizeof(unsigned long long) * 2 * HS_TRK_MAXG * HS_TRK_NRED * 2 * n));
+  TS_HIP(hipMalloc((void**)&t->d_cnt, sizeof(unsigned int) * n + 16));
   TS_HIP(hipHostMalloc((void**)&t->h_out, sizeof(HsTryOut) * n));
   t->try_cap = n;
   return HS_OK;
@@ -153,9 +153,11 @@ static int run_tries(hs_tracker* t, int n, const double* h_in, int coarsest, int
   a.part = t->d_part;
   a.cnt = t->d_cnt;
   t->last_G = G;
-  // the counters and timeout flags, zeroed before every launch (a 16-B multiple from the allocation's start)
-  const size_t cnt_bytes = (sizeof(unsigned int) * 2 * n + 15) & ~(size_t)15;
-  if (G > 1) TS_HIP(hipMemsetAsync(t->d_cnt, 0, cnt_bytes, t->stream));
+  // the granules and the timeout flags, zeroed before every launch (16-B multiples from the allocations' starts)
+  if (G > 1) {
+    TS_HIP(hipMemsetAsync(t->d_part, 0, sizeof(unsigned long long) * 2 * HS_TRK_MAXG * HS_TRK_NRED * 2 * n, t->stream));
+    TS_HIP(hipMemsetAsync(t->d_cnt, 0, (sizeof(unsigned int) * n + 15) & ~(size_t)15, t->stream));
+  }
   const char* kt = std::getenv("HS_KTRACE");
   if (kt && kt[0] == '1' && !single_pass) {
     const int nb = n * G;
@@ -174,7 +176,7 @@ static int run_tries(hs_tracker* t, int n, const double* h_in, int coarsest, int
   TS_HIP(hipEventRecord(t->e1, t->stream));
   TS_HIP(hipMemcpyAsync(t->h_out, t->d_out, sizeof(HsTryOut) * n, hipMemcpyDeviceToHost, t->stream));
   std::vector<unsigned int> tmo(G > 1 ? n : 0);
-  if (G > 1) TS_HIP(hipMemcpyAsync(tmo.data(), t->d_cnt + n, sizeof(unsigned int) * n, hipMemcpyDeviceToHost, t->stream));
+  if (G > 1) TS_HIP(hipMemcpyAsync(tmo.data(), t->d_cnt, sizeof(unsigned int) * n, hipMemcpyDeviceToHost, t->stream));
   TS_HIP(hipStreamSynchronize(t->stream));
   for (unsigned int v : tmo)
     if (v) return tfail(HS_ERR_HIP, "hs_k_track: a member workgroup never reached a pass (spin bound hit)");

@@ -54,14 +54,14 @@ struct HsTrackArgs {
   int* lm_lvl;          // [n][HS_TRK_MAXLOG]
   long long* trace;
   // G workgroups per hypothesis (blocks h G .. h G + G - 1): each pass's points are spread over them; their sums
-  // meet in part [n][2][G][HS_TRK_NRED] (pass parity) behind a counter per hypothesis (cnt [n], zero at launch),
-  // and every workgroup forms the same totals (in workgroup order) and runs the same LM step
+  // meet as tagged granules in part [n][2 (pass parity)][HS_TRK_MAXG][HS_TRK_NRED][2] (u64, zero at launch), and
+  // every workgroup forms the same totals (in workgroup order) and runs the same LM step
   int G, nhyp;
   double* part;
-  unsigned int* cnt;    // [2 nhyp]: pass counters, then a timeout flag per hypothesis
+  unsigned int* cnt;    // [nhyp] timeout flags (a member never arrived)
 };
 constexpr int HS_TRK_NRED = 52;  // the reduced values of a pass (45 normal-equation entries, 4 energies / flows, 3 counts)
-constexpr int HS_TRK_MAXG = 32;
+constexpr int HS_TRK_MAXG = 8;
 
 __global__ void hs_k_track(HsTrackArgs a);
 __global__ void hs_k_trk_scatter(int n, const float* cu, const float* cv, const float* cid, const float* hdi, int w,

@@ -350,39 +350,53 @@ __device__ void trk_pass(const HsTrackArgs& a, TrkShared& S, int h, int g) {
   }
   __syncthreads();
   if (G > 1) {
-    // the hypothesis' workgroups meet: partials out (agent-scope release by every wave), one relaxed increment,
-    // spin until all G of this pass are in (agent-scope acquire), then every workgroup sums them in workgroup order
-    // (cdna_hip_programming.md §6 Guideline 16, write-through form): the partials are stored sc1 by wave 0 alone
-    // (tid < 52), drained, and wave 0's lane 0 adds to the counter; every load of them is an sc1 load, so no
-    // release / acquire fence is needed (the loads only wait for the poll, behind a workgroup barrier)
-    double* P = a.part + ((size_t)h * 2 + (S.npass & 1)) * G * TRK_NRED;
-    if (tid < TRK_NRED)
-      __hip_atomic_store(reinterpret_cast<unsigned long long*>(P + g * TRK_NRED + tid),
-                         (unsigned long long)__double_as_longlong(S.red[0][tid]), __ATOMIC_RELAXED,
+    // The hypothesis' workgroups meet by granules (cdna_hip_programming.md §6 Guideline 16, R2: the data is the
+    // flag): every fp64 partial goes out as two 8-byte {tag = pass + 1, 32-bit half} granules (sc1 stores), and
+    // wave 0 -- lane q for value q -- re-reads the 2 G granules of its value (sc1 loads) until every tag matches,
+    // then sums the G partials in workgroup order.  One memory round trip per poll, no counter, no fences.  The
+    // granules are zeroed before every launch; the pass parity keeps a fast member off a slow member's buffer (it
+    // cannot write pass k + 2 before every member has read pass k).
+    typedef unsigned long long u64;
+    u64* P = reinterpret_cast<u64*>(a.part) + ((size_t)h * 2 + (S.npass & 1)) * HS_TRK_MAXG * TRK_NRED * 2;
+    const unsigned int tg = (unsigned int)(S.npass + 1);
+    const u64 tag = (u64)tg << 32;
+    if (tid < TRK_NRED) {
+      const u64 bits = (u64)__double_as_longlong(S.red[0][tid]);
+      __hip_atomic_store(P + (g * TRK_NRED + tid) * 2, tag | (bits & 0xffffffffull), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(P + (g * TRK_NRED + tid) * 2 + 1, tag | (bits >> 32), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (tid < 64) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (tid == 0) {
-        __hip_atomic_fetch_add(a.cnt + h, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned int target = (unsigned int)G * (unsigned int)(S.npass + 1);
-        unsigned int spins = 0;
-        while ((int)(__hip_atomic_load(a.cnt + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
-          __builtin_amdgcn_s_sleep(1);
-          if (++spins == (1u << 24)) {  // a member never arrived (~seconds): flag the hypothesis, go on
-            __hip_atomic_store(a.cnt + a.nhyp + h, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
+      const int q = min(tid, TRK_NRED - 1);
+      u64 v[2 * HS_TRK_MAXG];
+      unsigned int spins = 0;
+      for (;;) {
+        bool ok = true;
+#pragma unroll
+        for (int gg = 0; gg < HS_TRK_MAXG; gg++)
+          if (gg < G) {
+            v[2 * gg] = __hip_atomic_load(P + (gg * TRK_NRED + q) * 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v[2 * gg + 1] = __hip_atomic_load(P + (gg * TRK_NRED + q) * 2 + 1, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
           }
+#pragma unroll
+        for (int gg = 0; gg < HS_TRK_MAXG; gg++)
+          if (gg < G) ok = ok && (unsigned int)(v[2 * gg] >> 32) == tg && (unsigned int)(v[2 * gg + 1] >> 32) == tg;
+        if (__all(ok)) break;
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins == (1u << 22)) {  // a member never arrived (~seconds): flag the hypothesis, go on
+          if (tid == 0) __hip_atomic_store(a.cnt + h, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
         }
       }
-    }
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the poll
-    if (tid < TRK_NRED) {
-      double s = 0.0;
-      for (int gg = 0; gg < G; gg++)
-        s += __longlong_as_double((long long)__hip_atomic_load(
-            reinterpret_cast<unsigned long long*>(P + gg * TRK_NRED + tid), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      S.red[0][tid] = s;
+      if (tid < TRK_NRED) {
+        double s = 0.0;
+#pragma unroll
+        for (int gg = 0; gg < HS_TRK_MAXG; gg++)
+          if (gg < G) s += __longlong_as_double((long long)((v[2 * gg] & 0xffffffffull) | (v[2 * gg + 1] << 32)));
+        S.red[0][tid] = s;
+      }
     }
     __syncthreads();
   }

@@ -406,33 +406,6 @@ def test_graph_replay_matches_eager(scene2k):
         assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("scene_name", ["scene2k", "scene60k"])
-def test_fused_reduce_stitch_matches_separate(scene_name, request):
-    """hs_k_redstitch (HS_FUSE_RS=1: the reduce roles and the stitch blocks in one launch, ordered by a device
-    counter with agent-scope release / acquire) against the separate hs_k_reduce + hs_k_stitch launches: energies,
-    frame states, depths, systems and thresholds bit-identical over 6 GN iterations (the host-sum chunks are 1024
-    entries instead of 256; every entry's sum is the same loop).  The 60k-point window runs the multi-block
-    threshold select (pass-2 blocks inside the fused launch)."""
-    import os
-    from hslam_amd.ba import BAWindow
-    scene = request.getfixturevalue(scene_name)
-    res = []
-    for mode in ("0", "1"):
-        os.environ["HS_FUSE_RS"] = mode
-        try:
-            g = BAWindow(scene)
-            e0 = g.linearizeAll(reset=True)
-            e1 = g.iterate(0, 6)
-            fr = g.frames()
-            res.append((np.array([e0]), e1, fr["state"], fr["energyTH"], g.points()["idepth"], g.system(0)[0],
-                        g.system(2)[0]))
-            g.close()
-        finally:
-            os.environ.pop("HS_FUSE_RS", None)
-    for a, b in zip(*res):
-        assert np.array_equal(a, b)
-
-
 def test_dormant_energies(scene_small):
     """EnergyFunctional::calcLEnergyF_MT / calcMEnergyF (Src/EnergyFunctional.cpp:277-368), the energies only a
     setting_forceAceptStep=false System evaluates: frame / calib priors, the points' depth priors (a third of the
