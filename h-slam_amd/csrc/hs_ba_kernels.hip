@@ -2364,12 +2364,27 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
       st->iteration = s_it + 1;
     }
     if (tid == 0) HS_TRACE(a, 10);
+    // the frames are final: wave 1 writes them back now, beside wave 0's pair stage, so their stores drain while the
+    // pair stage runs (the kernel's end waits for every store)
+    if (tid >= 64 && tid < 128) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      constexpr int F0 = (int)(offsetof(HsDevState, frames) / 8), FW = (int)(sizeof(HsDevState::frames) / 8);
+      const uint2* ls = reinterpret_cast<const uint2*>(st_raw);
+      uint2* gs = reinterpret_cast<uint2*>(a.st);
+      for (int i = tid - 64; i < FW; i += 64) gs[F0 + i] = ls[F0 + i];
+    }
   }
   __syncthreads();
-  {  // write the window state back
+  {  // write the window state back (after a step: all but the frames, written above)
+    constexpr int F0 = (int)(offsetof(HsDevState, frames) / 8), FW = (int)(sizeof(HsDevState::frames) / 8);
+    static_assert(offsetof(HsDevState, frames) % 8 == 0 && sizeof(HsDevState::frames) % 8 == 0, "word copies");
+    const bool skipF = (a.flags & HS_APPLY) != 0;
     const uint2* ls = reinterpret_cast<const uint2*>(st_raw);
     uint2* gs = reinterpret_cast<uint2*>(a.st);
-    for (int i = tid; i < (int)(sizeof(HsDevState) / 8); i += nt) gs[i] = ls[i];
+    for (int i = tid; i < (int)(sizeof(HsDevState) / 8); i += nt)
+      if (!skipF || i < F0 || i >= F0 + FW) gs[i] = ls[i];
   }
   if (a.trace && threadIdx.x == 0) a.trace[25] = clock64();
   HS_TRACE(a, 15);
