@@ -52,12 +52,14 @@ __device__ __forceinline__ float3 interp33(const float4* __restrict__ img, float
 
 // Eigen LDLT (diagonal pivoting) solve of an 8x8 system by one thread, fully unrolled so every array is
 // register-resident: the pivot order is the swap sequence on the original diagonal (left-looking LDLT).
-__device__ __forceinline__ void ldlt8_solve(const double* __restrict__ A, const double* __restrict__ rhs, double* __restrict__ x) {
+// A's diagonal is read scaled by dscale (the LM damping (1 + lambda): Hl = H with a scaled diagonal, formed on load).
+__device__ __forceinline__ void ldlt8_solve(const double* __restrict__ A, const double* __restrict__ rhs, double* __restrict__ x,
+                                            double dscale = 1.0) {
   double dg[8];
   int pm[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
-    dg[i] = fabs(A[i * 8 + i]);
+    dg[i] = fabs(A[i * 8 + i] * dscale);
     pm[i] = i;
   }
 #pragma unroll
@@ -78,7 +80,7 @@ __device__ __forceinline__ void ldlt8_solve(const double* __restrict__ A, const 
 #pragma unroll
   for (int i = 0; i < 8; i++) {
 #pragma unroll
-    for (int j = 0; j < 8; j++) M[i][j] = A[pm[i] * 8 + pm[j]];
+    for (int j = 0; j < 8; j++) M[i][j] = i == j ? A[pm[i] * 9] * dscale : A[pm[i] * 8 + pm[j]];
     y[i] = rhs[pm[i]];
   }
   // left-looking as Eigen's ldlt_inplace::unblocked: column k is updated with the finished columns j < k
@@ -135,7 +137,7 @@ struct TrkShared {
   // LM state
   double T[7], Tn[7];
   double aff[2], affn[2];
-  double Hs[64], bs[8], resOld[6], Hl[64];
+  double Hs[64], bs[8], resOld[6];
   double incNorm;
   float lambda, cutoffRep;
   int brk, accept;
@@ -533,15 +535,11 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
       if (tid == 0) {
         const long long lm0 = a.trace ? clock64() : 0;
         S.iters++;
-        // Hl = H with the diagonal scaled by (1 + lambda), in LDS (the solver reads it with pivoted indices)
-        double* Hl = S.Hl;
+        // Hl = H with the diagonal scaled by (1 + lambda): formed as the solver loads H (pivoted indices)
         double mb[8], inc[8];
-        for (int q = 0; q < 64; q++) Hl[q] = S.Hs[q];
-#pragma unroll
-        for (int i = 0; i < 8; i++) Hl[i * 8 + i] *= (1 + S.lambda);
 #pragma unroll
         for (int i = 0; i < 8; i++) mb[i] = -S.bs[i];
-        ldlt8_solve(Hl, mb, inc);
+        ldlt8_solve(S.Hs, mb, inc, 1 + S.lambda);
         float extrapFac = 1;
         if (S.lambda < lambdaExtrapolationLimit) extrapFac = sqrtf(sqrtf(lambdaExtrapolationLimit / S.lambda));
         for (int i = 0; i < 8; i++) inc[i] *= extrapFac;
@@ -578,10 +576,8 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
           a.lm_log[((size_t)h * HS_TRK_MAXLOG + it) * 3 + 2] = S.incNorm;
           a.lm_lvl[(size_t)h * HS_TRK_MAXLOG + it] = lvl;
         }
-        if (accept) {
-          for (int q = 0; q < 64; q++) S.Hs[q] = S.H[q];
-          for (int q = 0; q < 8; q++) S.bs[q] = S.b[q];
-          for (int q = 0; q < 6; q++) S.resOld[q] = S.res[q];
+        S.accept = accept ? 1 : 0;
+        if (accept) {  // (H, b, res are taken over by 64 threads after the barrier)
           S.aff[0] = S.affn[0];
           S.aff[1] = S.affn[1];
           for (int q = 0; q < 7; q++) S.T[q] = S.Tn[q];
@@ -592,6 +588,11 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
         }
       }
       __syncthreads();
+      if (S.accept && tid < 64) {  // the accepted pass's normal equations and residuals (read after the next barrier)
+        S.Hs[tid] = S.H[tid];
+        if (tid < 8) S.bs[tid] = S.b[tid];
+        if (tid < 6) S.resOld[tid] = S.res[tid];
+      }
       if (S.brk) break;
     }
     if (tid == 0) {  // lastResiduals[lvl] / lastFlowIndicators: logged for the caller's abort replay
