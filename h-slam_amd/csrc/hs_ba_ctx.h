@@ -49,8 +49,9 @@ constexpr int kEventIters = 128;       // iterations timed with HIP events per c
 constexpr int kLinBlocksTarget = 256;  // linearize blocks of a window (points per wave grows beyond that)
 // hs_k_lin8 (lane = (point, target slot), 8 points per wave at a time) takes the production linearization from this
 // many points up: its wave issues ~2.3x fewer instructions per point (throughput), while hs_k_lin's one-point waves
-// finish a small window sooner (latency).  Env HS_LIN8=0 / 1 forces either.
-constexpr int kLin8MinPoints = 60000;
+// finish a small window sooner (latency).  Measured (r03_b3, per launch): 2k 10.6 vs 16.5 us, 5k 21.1 vs 18.4,
+// 10k 30.2 vs 25.7, 20k 53.8 vs 43.6 (hs_k_lin vs hs_k_lin8).  Env HS_LIN8=0 / 1 forces either.
+constexpr int kLin8MinPoints = 4000;
 constexpr int kThMultiMinPoints = 60000;  // the multi-block threshold select (below: one block beside the solve)
 constexpr int kLin8BlocksTarget = 512;  // hs_k_lin8 blocks of a window (two 4-wave blocks per CU)
 

@@ -45,9 +45,3 @@ def scene_marg():
     from hslam_amd.scene import make_ba_scene
     return make_ba_scene(n_points=240, seed=7, pose_noise=(0.001, 0.0005), idepth_noise=0.002)
 
-
-@pytest.fixture(scope="session")
-def scene60k():
-    """The smallest window on the large-window path (hs_k_lin8, the multi-block threshold select)."""
-    from hslam_amd.scene import make_ba_scene
-    return make_ba_scene(n_points=60000)
