@@ -56,7 +56,7 @@ static void free_buffers(hs_ctx* c) {
       c->d_hostsum, c->d_sys, c->d_sep, c->d_adHost, c->d_adTarget, c->d_adHostF, c->d_adTargetF, c->d_HM, c->d_bM,
       c->d_Nproj, c->d_xAd, c->d_x, c->d_elog, c->d_cand, c->d_tr_lin, c->d_tr_acc, c->d_tr_solve, c->d_tr_st,
       c->d_marg, c->d_adHTdelta, c->d_p_HdiF_alt, c->d_th_hist, c->d_th_hist2, c->d_th_surv, c->d_th_nsurv,
-      c->d_le_chunk, c->d_le_out, c->d_ref_pts, c->d_ref_n, c->d_stage, c->d_gsys};
+      c->d_le_chunk, c->d_le_out, c->d_ref_pts, c->d_ref_n, c->d_stage, c->d_gsys, c->d_sep_aux};
   for (auto& s : c->ps) {
     for (void* p : {(void*)s.u, (void*)s.v, (void*)s.idepth, (void*)s.idepth_zero, (void*)s.priorF, (void*)s.color,
                     (void*)s.weight, (void*)s.relBL, (void*)s.nGood, (void*)s.r_state, (void*)s.r_center})
@@ -93,6 +93,7 @@ static void free_buffers(hs_ctx* c) {
   c->d_ref_pts = nullptr; c->d_ref_n = nullptr;
   c->d_stage = nullptr;
   c->d_gsys = nullptr;
+  c->d_sep_aux = nullptr;
   c->gath_pending = c->gath_th = false;
   c->d_stage_cap = 0;
   c->cap_P = c->cap_blk = c->cap_W = c->cap_H = c->cap_stride = 0;
@@ -165,8 +166,9 @@ int ensure_capacity(hs_ctx* c, int W, int H, int capP, int capBlk) {
   HS_TRY(dalloc(&c->d_part, (size_t)capBlk * ne * 64));
   HS_TRY(dalloc(&c->d_part_e, (size_t)capBlk * 4));
   HS_TRY(dalloc(&c->d_hostsum, (size_t)HS_MAXF * ne * 64));
-  HS_TRY(dalloc(&c->d_sys, (size_t)SLmax + 3));
+  HS_TRY(dalloc(&c->d_sys, (size_t)SLmax + 3 + HS_MAXF * 64));
   HS_TRY(dalloc(&c->d_sep, (size_t)2 * SLmax));
+  HS_TRY(dalloc(&c->d_sep_aux, (size_t)HS_MAXF * 64));
   HS_TRY(dalloc(&c->d_adHost, FF * 64)); HS_TRY(dalloc(&c->d_adTarget, FF * 64));
   HS_TRY(dalloc(&c->d_adHostF, FF * 64)); HS_TRY(dalloc(&c->d_adTargetF, FF * 64));
   HS_TRY(dalloc(&c->d_HM, (size_t)nmax * nmax)); HS_TRY(dalloc(&c->d_bM, nmax));
@@ -177,7 +179,7 @@ int ensure_capacity(hs_ctx* c, int W, int H, int capP, int capBlk) {
   c->cap_stride = stride;
   HS_TRY(dalloc(&c->d_cand, (size_t)stride * c->nranks));
   HS_HIP(hipMemset(c->d_cand, 0xff, sizeof(float) * (size_t)stride * c->nranks));  // NaN, sign set: no candidate
-  if (c->multi_rank()) HS_TRY(dalloc(&c->d_gsys, ((size_t)SLmax + 3) * c->nranks));
+  if (c->multi_rank()) HS_TRY(dalloc(&c->d_gsys, ((size_t)SLmax + 3 + HS_MAXF * 64) * c->nranks));
   HS_TRY(dalloc(&c->d_th_hist, HS_TH_BINS));
   HS_TRY(dalloc(&c->d_th_hist2, 1024));
   HS_TRY(dalloc(&c->d_th_nsurv, 2));
@@ -199,7 +201,7 @@ int ensure_capacity(hs_ctx* c, int W, int H, int capP, int capBlk) {
   if (c->tracing) {
     HS_TRY(dalloc(&c->d_tr_lin, (size_t)capBlk * 16));
     HS_TRY(dalloc(&c->d_tr_acc, (size_t)(HS_MAXF * ((ne * 64 + 255) / 256) + 1 + 64) * 16));
-    HS_TRY(dalloc(&c->d_tr_st, (size_t)(HS_MAXF * (HS_MAXF + 1) / 2 + HS_MAXF + 2) * 16));
+    HS_TRY(dalloc(&c->d_tr_st, (size_t)(HS_MAXF * (HS_MAXF + 1) / 2 + 2 * HS_MAXF + 2) * 16));
     HS_TRY(dalloc(&c->d_tr_solve, 32));
   }
   c->cap_W = W; c->cap_H = H; c->cap_P = capP; c->cap_blk = capBlk;
@@ -433,7 +435,7 @@ static int launch_combine(hs_ctx* c) {
   std::memset(&a, 0, sizeof(a));
   a.nF = c->nF;
   if (c->gath_pending) {
-    a.gsys = c->d_gsys; a.nranks = c->nranks; a.gstride = c->SL() + 3; a.sys_out = c->d_sys;
+    a.gsys = c->d_gsys; a.nranks = c->nranks; a.gstride = c->SX(); a.sys_out = c->d_sys;
   }
   a.th_local = c->gath_th ? 1 : 0;
   a.th = red_args(c, false);
@@ -465,7 +467,7 @@ static int post_exchange(hs_ctx* c, bool th, bool defer) {
 // the one collective of a linearization: every rank's system vector + energies and its candidates, all-gathered in
 // one RCCL group (the sums are formed in rank order on every rank, so every rank solves the same system)
 static int exchange(hs_ctx* c, bool th) {
-  const size_t len = (size_t)c->SL() + 3;
+  const size_t len = (size_t)c->SX();
   HS_NCCL(ncclGroupStart());
   HS_NCCL(ncclAllGather(c->d_sys, c->d_gsys, len, ncclDouble, c->comm, c->stream));
   if (th)
@@ -504,12 +506,15 @@ static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = fals
   st.hostsum = c->d_hostsum; st.adHost = c->d_adHost; st.adTarget = c->d_adTarget;
   st.out = readback ? nullptr : c->d_sys;
   st.sep = sep ? c->d_sep : nullptr;
+  st.aux_out = readback ? nullptr : c->d_sys + c->SL() + 3;
+  st.aux_sep = sep ? c->d_sep_aux : nullptr;
   st.lambda1 = 1 + 1e-5;       // SOLVER_FIX_LAMBDA (Src/EnergyFunctional.cpp:707-708)
   st.sc = 1.0f / (1 + 1e-5);   // H -= H_sc * (1.0f / (1 + lambda)) (:763)
   st.trace = c->d_tr_st;
   st.red = a;
   st.red.skip_threshold = (skip_threshold || readback || multi || beside) ? 1 : 0;
-  const int nS = c->nF * (c->nF + 1) / 2 + c->nF + 2 + (multi ? a.np2 : 0);
+  // the first nF blocks: the diagonal blocks' host-f Schur terms (hs_ba_kernels.hip stitch_diag_schur)
+  const int nS = c->nF + c->nF * (c->nF + 1) / 2 + c->nF + 2 + (multi ? a.np2 : 0);
   hipLaunchKernelGGL(hs_k_stitch, dim3(nS), dim3(HS_STITCH_NT), 0, c->stream, st);
   HS_HIP(hipGetLastError());
   if (multi) {  // pass 3: the select block over pass 2's histogram and survivors (a side stream measured no faster:
@@ -551,7 +556,7 @@ static int launch_solve(hs_ctx* c, int flags, int iteration, bool log) {
     } else {  // the fused GN loop: the gathered sums in the solve's prefetch, the select as block 1 beside it
       if (c->gath_pending) {
         a.sys = c->d_gsys;
-        a.gsys = c->d_gsys; a.nranks = c->nranks; a.gstride = c->SL() + 3; a.sys_out = c->d_sys;
+        a.gsys = c->d_gsys; a.nranks = c->nranks; a.gstride = c->SX(); a.sys_out = c->d_sys;
       }
       a.th_local = c->gath_th ? 1 : 0;
       a.th = red_args(c, false);
@@ -564,6 +569,7 @@ static int launch_solve(hs_ctx* c, int flags, int iteration, bool log) {
   a.adHostF = c->d_adHostF; a.adTargetF = c->d_adTargetF;
   a.xAd = c->d_xAd; a.pre = c->d_pre; a.x_out = c->d_x;
   a.energy_log = log ? c->d_elog : nullptr;
+  a.aux_sc = (double)(1.0f / (1 + 1e-5));  // hs_k_stitch's sc
   a.trace = c->d_tr_solve;
   a.initialCalibHessian = c->P.initialCalibHessian;
   a.thOptIterations = c->P.thOptIterations;
@@ -658,7 +664,8 @@ static int dump_traces(hs_ctx* c) {
   }
   HS_TRY(dump_one("linearize", c->d_tr_lin, c->nblk, tick_us, c->stream, &f[1], &l[1]));
   HS_TRY(dump_one("reduce", c->d_tr_acc, c->nF * c->Q + 1, tick_us, c->stream, &f[2], &l[2]));
-  HS_TRY(dump_one("stitch", c->d_tr_st, c->nF * (c->nF + 1) / 2 + c->nF + 2, tick_us, c->stream, &f[3], &l[3]));
+  HS_TRY(dump_one("stitch", c->d_tr_st, c->nF + c->nF * (c->nF + 1) / 2 + c->nF + 2, tick_us, c->stream, &f[3],
+                  &l[3]));
   // the last iteration's launch chain on the wall clock: each kernel's first block start -> last checkpoint, and the
   // gap from one kernel's last checkpoint to the next kernel's first block (launch + end-of-kernel release)
   if (f[0] > 0 && f[1] > 0 && f[2] > 0 && f[3] > 0)
@@ -776,7 +783,7 @@ static int group_exchange(const std::vector<hs_ctx*>& g) {
     HS_HIP(hipEventRecord(s->ev_xch[0], s->stream));
   }
   for (hs_ctx* r : g) {
-    const size_t len = (size_t)r->SL() + 3;
+    const size_t len = (size_t)r->SX();
     for (hs_ctx* s : g) {
       HS_HIP(hipStreamWaitEvent(r->stream, s->ev_xch[0], 0));
       HS_HIP(hipMemcpyAsync(r->d_gsys + (size_t)s->rank * len, s->d_sys, sizeof(double) * len, hipMemcpyDeviceToDevice,
@@ -920,7 +927,9 @@ static int zero_window(hs_ctx* c, int nP) {
   HS_HIP(z(c->d_p_HdiF_alt, P * 4)); HS_HIP(z(c->d_p_bdSumF, P * 4)); HS_HIP(z(c->d_p_Hcd, P * 16));
   HS_HIP(z(c->d_p_JpJdF, P8 * 32)); HS_HIP(z(c->d_p_step, P * 4)); HS_HIP(z(c->d_marg, P));
   HS_HIP(z(c->d_part, (size_t)c->cap_blk * ne * 64 * 4)); HS_HIP(z(c->d_part_e, (size_t)c->cap_blk * 32));
-  HS_HIP(z(c->d_hostsum, (size_t)HS_MAXF * ne * 64 * 8)); HS_HIP(z(c->d_sys, ((size_t)SLmax + 3) * 8));
+  HS_HIP(z(c->d_hostsum, (size_t)HS_MAXF * ne * 64 * 8));
+  HS_HIP(z(c->d_sys, ((size_t)SLmax + 3 + HS_MAXF * 64) * 8));
+  HS_HIP(z(c->d_sep_aux, (size_t)HS_MAXF * 64 * 8));
   HS_HIP(z(c->d_sep, (size_t)2 * SLmax * 8)); HS_HIP(z(c->d_HM, (size_t)nmax * nmax * 8)); HS_HIP(z(c->d_bM, nmax * 8));
   HS_HIP(z(c->d_xAd, FF * 32)); HS_HIP(z(c->d_x, nmax * 8)); HS_HIP(z(c->d_elog, kLogCap * 8));
   HS_HIP(z(c->d_adHTdelta, FF * 32)); HS_HIP(z(c->d_frameTH, HS_MAXF * 4));
@@ -1251,6 +1260,13 @@ int hs_ba_get_system(hs_ctx* c, int which, double* H, double* b) {
     std::vector<double> sep((size_t)2 * SL);
     HS_HIP(hipMemcpyAsync(sep.data(), c->d_sep, sizeof(double) * sep.size(), hipMemcpyDeviceToHost, c->stream));
     HS_HIP(hipStreamSynchronize(c->stream));
+    if (which == 2) {  // HSC: the diagonal blocks' host-f Schur terms, formed in blocks of their own
+      std::vector<double> aux((size_t)64 * nF);
+      HS_HIP(hipMemcpy(aux.data(), c->d_sep_aux, sizeof(double) * aux.size(), hipMemcpyDeviceToHost));
+      for (int f = 0; f < nF; f++)
+        for (int i = 0; i < 8; i++)
+          for (int k = i; k < 8; k++) sep[SL + (size_t)(4 + 8 * f + i) * n + 4 + 8 * f + k] += aux[f * 64 + i * 8 + k];
+    }
     const double* src = sep.data() + (which == 0 ? 0 : SL);
     for (int r = 0; r < n; r++) {
       for (int q = r; q < n; q++) HH[(size_t)r * n + q] = HH[(size_t)q * n + r] = src[(size_t)r * n + q];
@@ -1790,10 +1806,23 @@ extern "C" int hs_debug_se3(int on_device, int op, int n, const double* in14, do
 // test hooks (not in the header): the system vector the ranks all-reduce (SL + 3 doubles: upper triangle of
 // HA (1+lambda on the diagonal) - HSC / (1+lambda) in the n x n layout, bA - bSC, energy, sum |idepth|, #points) and
 // this rank's newest-frame candidates (cand_stride floats, NaN = none) of the last linearization
-extern "C" int hs_debug_get_sysvec(hs_ctx* c, double* out) {
+// the system vector [SL + 3] as the solve consumes it: the diagonal blocks' host-f Schur terms folded in
+// (out(f, f) -= sc aux[f], the solve prefetch's operation); raw = 1: the unfolded [SX] vector as the stitch wrote it
+// (what a multi-rank exchange moves)
+extern "C" int hs_debug_get_sysvec(hs_ctx* c, double* out, int raw) {
   if (!c || !out || c->nF == 0) return fail(HS_ERR_INVALID, "null / no window");
-  HS_HIP(hipMemcpyAsync(out, c->d_sys, sizeof(double) * ((size_t)c->SL() + 3), hipMemcpyDeviceToHost, c->stream));
+  const int SL = c->SL(), n = c->dim();
+  std::vector<double> v((size_t)c->SX());
+  HS_HIP(hipMemcpyAsync(v.data(), c->d_sys, sizeof(double) * v.size(), hipMemcpyDeviceToHost, c->stream));
   HS_HIP(hipStreamSynchronize(c->stream));
+  if (!raw) {
+    const double sc = (double)(1.0f / (1 + 1e-5));
+    const double* aux = v.data() + SL + 3;
+    for (int f = 0; f < c->nF; f++)
+      for (int i = 0; i < 8; i++)
+        for (int k = i; k < 8; k++) v[(size_t)(4 + 8 * f + i) * n + 4 + 8 * f + k] -= sc * aux[f * 64 + i * 8 + k];
+  }
+  std::memcpy(out, v.data(), sizeof(double) * (raw ? v.size() : (size_t)SL + 3));
   return HS_OK;
 }
 extern "C" int hs_debug_get_candidates(hs_ctx* c, float* out, int* stride) {
@@ -1810,7 +1839,9 @@ extern "C" int hs_debug_stitch(int nF, int exact, const double* hostsum, const d
                                double* out, double* sep) {
   if (nF < 1 || nF > HS_MAXF || !hostsum || !adH || !adT || !out) return fail(HS_ERR_INVALID, "bad args");
   const int n = 4 + 8 * nF, SL = n * n + n, ne = hs_ne(exact != 0);
-  double *dh = nullptr, *da = nullptr, *dt = nullptr, *dout = nullptr, *dsep = nullptr;
+  double *dh = nullptr, *da = nullptr, *dt = nullptr, *dout = nullptr, *dsep = nullptr, *dax = nullptr, *dax2 = nullptr;
+  HS_TRY(dalloc(&dax, (size_t)nF * 64));
+  HS_TRY(dalloc(&dax2, (size_t)nF * 64));
   HS_TRY(dalloc(&dh, (size_t)nF * ne * 64));
   HS_TRY(dalloc(&da, (size_t)nF * nF * 64));
   HS_TRY(dalloc(&dt, (size_t)nF * nF * 64));
@@ -1823,14 +1854,26 @@ extern "C" int hs_debug_stitch(int nF, int exact, const double* hostsum, const d
   std::memset(&st, 0, sizeof(st));
   st.nF = nF; st.exact = exact ? 1 : 0; st.ne = ne;
   st.hostsum = dh; st.adHost = da; st.adTarget = dt; st.out = dout; st.sep = dsep;
+  st.aux_out = dax; st.aux_sep = dax2;
   st.lambda1 = 1 + 1e-5;
   st.sc = 1.0f / (1 + 1e-5);
   st.red.skip_threshold = 1;
-  hipLaunchKernelGGL(hs_k_stitch, dim3(nF * (nF + 1) / 2 + nF + 2), dim3(HS_STITCH_NT), 0, 0, st);
+  hipLaunchKernelGGL(hs_k_stitch, dim3(nF + nF * (nF + 1) / 2 + nF + 2), dim3(HS_STITCH_NT), 0, 0, st);
   HS_HIP(hipGetLastError());
   HS_HIP(hipDeviceSynchronize());
   HS_HIP(hipMemcpy(out, dout, sizeof(double) * SL, hipMemcpyDeviceToHost));
   if (sep) HS_HIP(hipMemcpy(sep, dsep, sizeof(double) * 2 * SL, hipMemcpyDeviceToHost));
-  for (double* p : {dh, da, dt, dout, dsep}) (void)hipFree(p);
+  std::vector<double> ax((size_t)nF * 64), ax2((size_t)nF * 64);
+  HS_HIP(hipMemcpy(ax.data(), dax, sizeof(double) * ax.size(), hipMemcpyDeviceToHost));
+  HS_HIP(hipMemcpy(ax2.data(), dax2, sizeof(double) * ax2.size(), hipMemcpyDeviceToHost));
+  for (double* p : {dh, da, dt, dout, dsep, dax, dax2}) (void)hipFree(p);
+  // the consumers' fold of the diagonal blocks' host-f Schur terms
+  for (int f = 0; f < nF; f++)
+    for (int i = 0; i < 8; i++)
+      for (int k = i; k < 8; k++) {
+        const size_t e = (size_t)(4 + 8 * f + i) * n + 4 + 8 * f + k;
+        out[e] -= st.sc * ax[f * 64 + i * 8 + k];
+        if (sep) sep[SL + e] += ax2[f * 64 + i * 8 + k];
+      }
   return HS_OK;
 }

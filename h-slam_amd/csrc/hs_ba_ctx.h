@@ -175,9 +175,10 @@ struct hs_ctx {
   float* d_part = nullptr;       // [nblk][ne][64] block partials of hs_k_lin
   double* d_part_e = nullptr;    // [nblk][4] block energies
   double* d_hostsum = nullptr;   // [nF][ne][64] per-host sums (hs_k_reduce)
-  double* d_sys = nullptr;       // [SL + 3] system vector (upper triangle of HA - sc HSC | bA - bSC) + energy,
-                                 // sum |idepth|, #points; all-reduced over the ranks
+  double* d_sys = nullptr;       // [SX] system vector (upper triangle of HA - sc HSC | bA - bSC) + energy,
+                                 // sum |idepth|, #points + the diagonal blocks' host-f Schur terms (see SX)
   double* d_sep = nullptr;       // [2][SL] HA | bA, HSC | bSC (granular read-back)
+  double* d_sep_aux = nullptr;   // [HS_MAXF][64] the diagonal blocks' host-f Schur terms of the last sep stitch
   double *d_adHost = nullptr, *d_adTarget = nullptr;
   float *d_adHostF = nullptr, *d_adTargetF = nullptr;
   double *d_HM = nullptr, *d_bM = nullptr, *d_Nproj = nullptr;
@@ -232,6 +233,9 @@ struct hs_ctx {
 
   int dim() const { return 4 + 8 * nF; }
   int SL() const { return dim() * dim() + dim(); }  // slot: n x n (upper triangle used) + b
+  // the whole raw system vector: SL | 3 energies | the diagonal blocks' host-f Schur terms [nF][64] (folded in by
+  // its consumers); what a multi-rank exchange moves
+  int SX() const { return SL() + 3 + 64 * nF; }
   double* sysE() const { return d_sys + SL(); }
 };
 

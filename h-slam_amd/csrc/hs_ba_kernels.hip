@@ -1247,7 +1247,89 @@ __global__ __launch_bounds__(HS_STITCH_NT) void hs_k_th_select(HsRedArgs a) {
 // in one fixed order (hosts, then targets), so the system is bit-reproducible.  The vector holds the upper
 // triangle of HA - sc HSC (diagonal: HA (1 + lambda) - sc HSC; the solve adds the priors) and bA - bSC;
 // `sep` HA | bA and HSC | bSC separately.
-__device__ __forceinline__ void stitch_block(const HsStitchArgs& a, const int j, double* lds) {
+// The heavy part of a diagonal frame block (f, f): host f's own Schur term sum_t1 adH[f,t1] sum_t2 D_f(t1,t2)
+// adH[f,t2]^T (7 terms of 8 products each), in a block of its own (the first nF blocks of the stitch launch) so the
+// diagonal blocks' terms no longer share one CU's LDS bandwidth with the other 21 sandwiches: its sum goes to aux
+// [f][64] (full 8x8), which the consumers fold into (f, f): out -= sc aux (the solve's prefetch, the host read-backs),
+// sepS += aux.
+__device__ void stitch_diag_schur(const HsStitchArgs& a, const int f, double* lds) {
+  const int nF = a.nF;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane >> 3, c = lane & 7;
+  const int NE64 = a.ne * 64;
+  const double* HSf = a.hostsum + (size_t)f * NE64;
+  double* aHf = lds;         // [8][64] adH[f, t]
+  double* Dq = aHf + 512;    // [8][8][64] D_f(t1, t2)
+  double* tS = Dq + 4096;    // [8][64] the term of t1
+  double* scr = tS + 512;    // per-wave scratch [ST_NW][64]
+  {  // one load batch: adjoints | D blocks (power-of-two strides; slots t >= nF or == f skipped)
+    constexpr int SU = (512 + 4096 + ST_NT - 1) / ST_NT;
+    double v[SU];
+    int dst[SU];
+#pragma unroll
+    for (int u = 0; u < SU; u++) {
+      const int q = tid + ST_NT * u;
+      const double* src = a.adHost;
+      int d = -1;
+      if (q < 512) {
+        const int t = q >> 6, ln = q & 63;
+        if (t < nF) {
+          src = a.adHost + (size_t)(f + nF * t) * 64 + ln;
+          d = q;
+        }
+      } else if (q < 512 + 4096) {
+        const int qd = q - 512, x1 = qd >> 9, x2 = (qd >> 6) & 7, ln = qd & 63, rr = ln >> 3, cc = ln & 7;
+        if (x1 < nF && x2 < nF && x1 != f && x2 != f) {
+          const int o1 = x1 - (x1 > f ? 1 : 0), o2 = x2 - (x2 > f ? 1 : 0);
+          int base, ls, cs;
+          if (a.exact) { base = (HS_E_TOP + o1 * 7 + o2) * 64; ls = 8; cs = 1; }
+          else if (o1 <= o2) { base = (HS_E_TOP + dpair(o1, o2)) * 64; ls = 8; cs = 1; }
+          else { base = (HS_E_TOP + dpair(o2, o1)) * 64; ls = 1; cs = 8; }
+          src = HSf + base + rr * ls + cc * cs;
+          d = 512 + qd;
+        }
+      }
+      v[u] = *src;
+      dst[u] = d;
+    }
+#pragma unroll
+    for (int u = 0; u < SU; u++)
+      if (dst[u] >= 0) lds[dst[u]] = v[u];
+  }
+  __syncthreads();
+  HS_TRACE(a, 1);
+  double* sw = scr + wv * 64;
+  for (int x = wv; x < nF - 1; x += ST_NW) {
+    const int y = x + (x >= f ? 1 : 0);
+    double v0 = 0.0, v1 = 0.0;
+#pragma unroll
+    for (int t2 = 0; t2 < HS_MAXF; t2++) {  // unrolled, the skipped slots masked: the LDS reads issue together
+      const double pv = mm8t(Dq + (y * 8 + t2) * 64, aHf + t2 * 64, r, c);
+      const bool on = t2 < nF && t2 != f;
+      if (t2 & 1) v1 = on ? v1 + pv : v1;
+      else v0 = on ? v0 + pv : v0;
+    }
+    sw[lane] = v0 + v1;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    tS[y * 64 + lane] = mm8(aHf + y * 64, sw, r, c);
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  HS_TRACE(a, 2);
+  if (tid < 64) {
+    double vS[HS_MAXF];
+#pragma unroll
+    for (int i = 0; i < HS_MAXF; i++) vS[i] = tS[i * 64 + lane];
+    double hf = 0.0;
+#pragma unroll
+    for (int t1 = 0; t1 < HS_MAXF; t1++) hf = (t1 < nF && t1 != f) ? hf + vS[t1] : hf;
+    if (a.aux_out) a.aux_out[f * 64 + lane] = hf;
+    if (a.aux_sep) a.aux_sep[f * 64 + lane] = hf;
+  }
+}
+
+__device__ __forceinline__ void stitch_block(const HsStitchArgs& a, int j, double* lds) {
   const int nF = a.nF, n = 4 + 8 * nF, nn = n * n, SL = nn + n;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane >> 3, c = lane & 7;
   const int NE64 = a.ne * 64;
@@ -1255,6 +1337,12 @@ __device__ __forceinline__ void stitch_block(const HsStitchArgs& a, const int j,
   const int oE = (HS_E_TOP + ND) * 64;  // accE / accEB / Hcc entries of a host sum
   const int nFB = nF * (nF + 1) / 2;
   HS_TRACE(a, 0);
+  if (j < nF) {  // the first nF blocks: the diagonal blocks' host-f Schur terms
+    stitch_diag_schur(a, j, lds);
+    HS_TRACE(a, 15);
+    return;
+  }
+  j -= nF;
   if (j == nFB + nF + 1) {  // setNewFrameEnergyTH for the next linearization, beside the stitch
     if (!a.red.skip_threshold) red_energy_th_block(a.red, reinterpret_cast<unsigned int*>(lds));
     HS_TRACE(a, 15);
@@ -1298,7 +1386,7 @@ __device__ __forceinline__ void stitch_block(const HsStitchArgs& a, const int j,
     double* aHg = aTf + 512;       // [8][64] adH[g, t]
     double* aTg = aHg + 512;       // [8][64] adT[h, g]
     double* Dx = aTg + 512;        // [8][64] D_h(f, g) by host h
-    double* Dq = Dx + 512;         // f < g: [8][64] D_f(t1, g) by t1 | [8][64] D_g(f, t2) by t2; f == g: [8][8][64] D_f
+    double* Dq = Dx + 512;         // f < g: [8][64] D_f(t1, g) by t1 | [8][64] D_g(f, t2) by t2 (f == g: unused)
     double* A8 = Dq + 4096;        // A88 blocks [16][64]: f < g: (f, g) | (g, f); f == g: (f, t) by t | (h, f) by 8 + h
     double* tS = A8 + 1024;        // Schur terms [16][64]
     double* tA = tS + 1024;        // top terms [16][64]
@@ -1309,10 +1397,10 @@ __device__ __forceinline__ void stitch_block(const HsStitchArgs& a, const int j,
       // table rows at power-of-two strides (slot index t < 8 = HS_MAXF; rows with t >= nF are skipped), so the
       // index math is shifts and masks, not runtime divisions
       const int nAdj = (f < g ? 4 : 2) * 512;        // [kind][t][64]
-      const int nD = f < g ? 3 * 512 : 512 + 4096;   // f < g: [kind][x][64]; f == g: Dx [h][64] | Dq [t1][t2][64]
+      const int nD = f < g ? 3 * 512 : 512;          // f < g: [kind][x][64]; f == g: Dx [h][64] (D_f: its own block)
       const int nOct = f < g ? 128 : 16 * 64;        // A88 blocks [slot][64], gathered from the pairs' octets
       const int total = nAdj + nD + nOct;
-      constexpr int SU = (512 * 4 + 4608 + 1024 + ST_NT - 1) / ST_NT;
+      constexpr int SU = (512 * 4 + 3 * 512 + 128 + ST_NT - 1) / ST_NT;  // the largest table: f < g
       double v[SU];
       int dst[SU];
 #pragma unroll
@@ -1338,15 +1426,9 @@ __device__ __forceinline__ void stitch_block(const HsStitchArgs& a, const int j,
               if (kind == 1 && x != f) { h = f; t1 = x; t2 = g; d = (int)(Dq - lds) + x * 64 + ln; }
               if (kind == 2 && x != g) { h = g; t1 = f; t2 = x; d = (int)(Dq - lds) + 512 + x * 64 + ln; }
             }
-          } else if (qd < 512) {
+          } else {
             const int x = qd >> 6;
             if (x < nF && x != f) { h = x; t1 = f; t2 = f; d = (int)(Dx - lds) + qd; }
-          } else {
-            const int x1 = (qd - 512) >> 9, x2 = ((qd - 512) >> 6) & 7;
-            if (x1 < nF && x2 < nF && x1 != f && x2 != f) {
-              h = f; t1 = x1; t2 = x2;
-              d = (int)(Dq - lds) + (qd - 512);
-            }
           }
           if (h >= 0) {
             int base, ls, cs;
@@ -1434,39 +1516,16 @@ __device__ __forceinline__ void stitch_block(const HsStitchArgs& a, const int j,
         put(4 + 8 * f + r, 4 + 8 * g + c, ha, hs, false);
       }
     } else {
-      // Schur terms: tS[h] = adT[h,f] D_h(f,f) adT[h,f]^T (h != f), tS[8 + t1] = adH[f,t1] sum_t2 D_f(t1,t2) adH[f,t2]^T
-      // top terms: tA[t] host pairs (f, t), tA[8 + h] target pairs (h, f)
-      // balanced over the 16 waves: the 7 heavy host-f terms (8 products each) on waves 0-6, the 21 two-product
-      // sandwiches round-robin on waves 7-15 (at most 3 each); every term is still formed by one wave
-      const int nHeavy = nF - 1, nSmall = 3 * (nF - 1), nSW = ST_NW - nHeavy;
-      for (int x = (wv < nHeavy ? wv : nHeavy + (wv - nHeavy)); x < nHeavy + nSmall;
-           x += (wv < nHeavy ? nHeavy + nSmall : nSW)) {
-        int kind, y;
-        if (x < nHeavy) {
-          kind = 1;
-          y = x + (x >= f ? 1 : 0);
-        } else {
-          const int sI = x - nHeavy, yi = sI % (nF - 1);
-          kind = sI / (nF - 1) == 0 ? 0 : (sI / (nF - 1) == 1 ? 2 : 3);
-          y = yi + (yi >= f ? 1 : 0);
-        }
+      // Schur terms: tS[h] = adT[h,f] D_h(f,f) adT[h,f]^T (h != f); host f's own term (adH[f,t1] sum_t2 D_f(t1,t2)
+      // adH[f,t2]^T, 56 products) is formed by block f of the launch (stitch_diag_schur) and folded in by the
+      // consumers; top terms: tA[t] host pairs (f, t), tA[8 + h] target pairs (h, f).  The 21 two-product
+      // sandwiches round-robin over the 16 waves; every term is formed by one wave
+      const int nSmall = 3 * (nF - 1);
+      for (int x = wv; x < nSmall; x += ST_NW) {
+        const int yi = x % (nF - 1), kind = x / (nF - 1) == 0 ? 0 : (x / (nF - 1) == 1 ? 2 : 3);
+        const int y = yi + (yi >= f ? 1 : 0);
         if (kind == 0) {
           tS[y * 64 + lane] = sandwich8(aTf + y * 64, Dx + y * 64, aTf + y * 64, sw, lane);
-        } else if (kind == 1) {
-          double v0 = 0.0, v1 = 0.0;
-#pragma unroll
-          for (int t2 = 0; t2 < HS_MAXF; t2++) {  // unrolled, the skipped slots masked: the LDS reads issue together
-            const double pv = mm8t(Dq + (y * 8 + t2) * 64, aHf + t2 * 64, r, c);
-            const bool on = t2 < nF && t2 != f;
-            if (t2 & 1) v1 = on ? v1 + pv : v1;
-            else v0 = on ? v0 + pv : v0;
-          }
-          sw[lane] = v0 + v1;
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          tS[(8 + y) * 64 + lane] = mm8(aHf + y * 64, sw, r, c);
-          __builtin_amdgcn_wave_barrier();
         } else if (kind == 2) {
           tA[y * 64 + lane] = sandwich8(aHf + y * 64, A8 + y * 64, aHf + y * 64, sw, lane);
         } else {
@@ -1478,17 +1537,15 @@ __device__ __forceinline__ void stitch_block(const HsStitchArgs& a, const int j,
       if (tid < 64 && r <= c) {
         // hosts in order, host f's term its t1 partials in order; then the top terms.  Unrolled over the 8 slots
         // with the unused ones masked, so the 32 LDS reads issue together instead of one round trip per term
-        double vS[2 * HS_MAXF], vA[2 * HS_MAXF];
+        double vS[HS_MAXF], vA[2 * HS_MAXF];
 #pragma unroll
         for (int i = 0; i < 2 * HS_MAXF; i++) {
-          vS[i] = tS[i * 64 + lane];
+          if (i < HS_MAXF) vS[i] = tS[i * 64 + lane];
           vA[i] = tA[i * 64 + lane];
         }
-        double hf = 0.0, hs = 0.0, ha = 0.0;
+        double hs = 0.0, ha = 0.0;
 #pragma unroll
-        for (int t1 = 0; t1 < HS_MAXF; t1++) hf = (t1 < nF && t1 != f) ? hf + vS[HS_MAXF + t1] : hf;
-#pragma unroll
-        for (int h = 0; h < HS_MAXF; h++) hs = h < nF ? hs + (h != f ? vS[h] : hf) : hs;
+        for (int h = 0; h < HS_MAXF; h++) hs = (h < nF && h != f) ? hs + vS[h] : hs;  // host f: aux (folded later)
 #pragma unroll
         for (int t = 0; t < HS_MAXF; t++) ha = (t < nF && t != f) ? ha + vA[t] : ha;
 #pragma unroll
@@ -2020,7 +2077,16 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     qr[u] = rr;
     qc[u] = cc;
   }
-  double gs[NUQ], hmq[NUQ], nfv[NF_NU];
+  // the diagonal frame blocks' host-f Schur terms after the energies (hs_k_stitch's aux_out): entry (qr, qc) of a
+  // block (f, f) folds in aux [f][qr - 4 - 8 f][qc - 4 - 8 f] (-1: none)
+  const int AUX0 = nn + n + 3;
+  int aaddr[NUQ];
+#pragma unroll
+  for (int u = 0; u < NUQ; u++) {
+    const int fr = (qr[u] - 4) >> 3, fc = (qc[u] - 4) >> 3;
+    aaddr[u] = (qr[u] >= 4 && fr == fc) ? AUX0 + fr * 64 + ((qr[u] - 4) & 7) * 8 + ((qc[u] - 4) & 7) : -1;
+  }
+  double gs[NUQ], hmq[NUQ], nfv[NF_NU], axv[NUQ];
   // energy, sum |idepth|, #points (multi-rank: the ranks' values summed in rank order)
   double sysE0, sysE1, sysE2;
   if (a.gsys) {
@@ -2041,23 +2107,32 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
 #pragma unroll
       for (int u = 0; u < NUQ; u++) {
         gs[u] = a.sys[max(qaddr[u], 0)];
+        axv[u] = a.sys[max(aaddr[u], 0)];
         hmq[u] = qr[u] == -2 ? a.bM[qc[u]] : a.HM[qr[u] >= 0 ? qaddr[u] : 0];
       }
     } else {  // no marginalization prior (a uniform branch): only bM is read beside the system
 #pragma unroll
       for (int u = 0; u < NUQ; u++) {
         gs[u] = a.sys[max(qaddr[u], 0)];
+        axv[u] = a.sys[max(aaddr[u], 0)];
         hmq[u] = qr[u] == -2 ? a.bM[qc[u]] : 0.0;
       }
     }
-    if (a.gsys) {  // multi-rank: the gathered vectors (a.sys = rank 0's) summed in rank order, the sum kept
+    if (a.gsys) {  // multi-rank: the gathered vectors (a.sys = rank 0's) summed in rank order, the raw sums kept
 #pragma unroll
       for (int u = 0; u < NUQ; u++) {
-        const int ad = max(qaddr[u], 0);
-        for (int r = 1; r < a.nranks; r++) gs[u] += a.gsys[r * a.gstride + ad];
+        const int ad = max(qaddr[u], 0), ax = max(aaddr[u], 0);
+        for (int r = 1; r < a.nranks; r++) {
+          gs[u] += a.gsys[r * a.gstride + ad];
+          axv[u] += a.gsys[r * a.gstride + ax];
+        }
         if (qaddr[u] >= 0) a.sys_out[ad] = gs[u];
+        if (aaddr[u] >= 0) a.sys_out[ax] = axv[u];
       }
     }
+#pragma unroll
+    for (int u = 0; u < NUQ; u++)
+      if (aaddr[u] >= 0) gs[u] -= a.aux_sc * axv[u];
 #pragma unroll
     for (int u = 0; u < NF_NU; u++) nfv[u] = a.Nproj[min(tid + u * SOLVE_NT, 2 * n * HS_NNS - 1)];
   }
@@ -2400,7 +2475,7 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_combine(HsSolveArgs a) {
     return;
   }
   if (!a.gsys) return;  // test hook: the select block alone
-  const int n = 4 + 8 * a.nF, len = n * n + n + 3;
+  const int n = 4 + 8 * a.nF, len = n * n + n + 3 + 64 * a.nF;  // + the diagonal blocks' host-f Schur terms
   for (int i = threadIdx.x; i < len; i += SOLVE_NT) {
     double s = a.gsys[i];
     for (int r = 1; r < a.nranks; r++) s += a.gsys[r * a.gstride + i];

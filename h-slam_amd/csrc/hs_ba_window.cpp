@@ -175,7 +175,8 @@ int commit(hs_ctx* c) {
       c->wframes[f].committed = f;
     }
     // the system vector's layout changed: no stale entry of the old layout stays in its (unread) lower triangle
-    HS_HIP(hipMemsetAsync(c->d_sys, 0, sizeof(double) * ((size_t)HS_MAXDIM * HS_MAXDIM + HS_MAXDIM + 3), c->stream));
+    HS_HIP(hipMemsetAsync(c->d_sys, 0, sizeof(double) * ((size_t)HS_MAXDIM * HS_MAXDIM + HS_MAXDIM + 3 + HS_MAXF * 64),
+                          c->stream));
   }
 
   // ---- points: the blob

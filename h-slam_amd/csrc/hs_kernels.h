@@ -152,6 +152,10 @@ struct HsStitchArgs {
   double* out;                 // system vector [SL]: upper triangle of HA - sc HSC (diagonal HA (1+lambda) - sc HSC)
                                // in the n x n layout, then bA - bSC
   double* sep;                 // nullable: [2][SL] HA | bA, HSC | bSC (granular read-back)
+  // the diagonal frame blocks' host-f Schur terms, [nF][64] each (written by the launch's first nF blocks; their
+  // consumers fold them in: out(f, f) -= sc aux_out[f], sepS(f, f) += aux_sep[f]); nullable
+  double* aux_out;
+  double* aux_sep;
   double lambda1, sc;          // 1 + lambda, 1 / (1 + lambda)
   HsRedArgs red;               // setNewFrameEnergyTH (the launch's last block)
   long long* trace;
@@ -188,6 +192,7 @@ struct HsSolveArgs {
   double* sys_out;
   int th_local;
   HsRedArgs th;
+  double aux_sc;               // the stitch's sc: the diagonal blocks' host-f Schur terms (after the energies) fold in
 };
 
 struct HsResubArgs {

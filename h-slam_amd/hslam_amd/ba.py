@@ -227,11 +227,14 @@ class BAWindow:
     def synchronize(self):
         check(self.lib.hs_ba_synchronize(self.h))
 
-    def system_vector(self):
-        """This rank's packed system vector of the last linearization (what RCCL all-reduces; test hook)."""
-        out = np.zeros(self.dim * self.dim + self.dim + 3)
-        self.lib.hs_debug_get_sysvec.argtypes = [C.c_void_p, C.c_void_p]
-        check(self.lib.hs_debug_get_sysvec(self.h, ptr(out)))
+    def system_vector(self, raw=False):
+        """The packed system vector of the last linearization as the solve consumes it (test hook): n*n | n | energy,
+        sum |idepth|, #points.  raw: as the stitch wrote it, the diagonal blocks' host-f Schur terms [nF][64] unfolded
+        at the end (what a multi-rank exchange all-gathers)."""
+        n = self.dim
+        out = np.zeros(n * n + n + 3 + (64 * self.nF if raw else 0))
+        self.lib.hs_debug_get_sysvec.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+        check(self.lib.hs_debug_get_sysvec(self.h, ptr(out), int(raw)))
         return out
 
     def candidates(self):
