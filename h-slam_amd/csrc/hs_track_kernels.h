@@ -61,7 +61,7 @@ struct HsTrackArgs {
   unsigned int* cnt;    // [nhyp] timeout flags (a member never arrived)
 };
 constexpr int HS_TRK_NRED = 52;  // the reduced values of a pass (45 normal-equation entries, 4 energies / flows, 3 counts)
-constexpr int HS_TRK_MAXG = 8;
+constexpr int HS_TRK_MAXG = 16;
 
 __global__ void hs_k_track(HsTrackArgs a);
 __global__ void hs_k_trk_scatter(int n, const float* cu, const float* cv, const float* cid, const float* hdi, int w,
