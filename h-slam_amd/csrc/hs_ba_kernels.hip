@@ -2199,14 +2199,20 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
         for (int k = 0; k < n; k++) hmd += a.HM[q * n + k] * delta(k);
       yv[q] = sq * ((bl + (dgm[HS_MAXDIM + q] + hmd)) + dgv[HS_MAXDIM + q]);
     }
-    __syncthreads();
     HS_TRACE(a, 7);
-    // the scaled off-diagonal entries S H S, mirrored from the upper triangle
+    // the scaled off-diagonal entries S H S, mirrored from the upper triangle; each thread forms the scalings of its
+    // entries' two rows itself (the row threads' operations above, so the same values) instead of reading Sv
+    // behind a barrier
+    auto scale_of = [&](int q) -> double {
+      const double pr = q < 4 ? a.initialCalibHessian : st->frames[(q - 4) >> 3].prior[(q - 4) & 7];
+      const double hv = dgv[q] + (pr + dgm[q]) * lam1;
+      return rsqrt_step(hv + 10);
+    };
 #pragma unroll
     for (int u = 0; u < NUQ; u++) {
       const int r = qr[u], c = qc[u];
       if (r >= 0 && r != c) {
-        const double w = Sv[r] * (gs[u] + (a.HM ? hmq[u] : 0.0)) * Sv[c];
+        const double w = scale_of(r) * (gs[u] + (a.HM ? hmq[u] : 0.0)) * scale_of(c);
         A[r * n + c] = w;
         A[c * n + r] = w;
       }
