@@ -2418,6 +2418,17 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
         F.delta_prior[q] = ns[q] - 0.0;
       }
     }
+    // the frames are final: wave 1 writes them back now, beside wave 0's pair stage, so their stores drain while the
+    // pair stage runs (the kernel's end waits for every store); the calib and canbreak below touch no frame
+    if (tid >= 64 && tid < 128) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      constexpr int F0 = (int)(offsetof(HsDevState, frames) / 8), FW = (int)(sizeof(HsDevState::frames) / 8);
+      const uint2* ls = reinterpret_cast<const uint2*>(st_raw);
+      uint2* gs = reinterpret_cast<uint2*>(a.st);
+      for (int i = tid - 64; i < FW; i += 64) gs[F0 + i] = ls[F0 + i];
+    }
     if (tid == 64) {  // the calib (on wave 1, beside the pair stage: every lane read cv before the barrier)
       hs::CalibH& cal = st->calib;
 #pragma unroll
@@ -2445,17 +2456,6 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
       st->iteration = s_it + 1;
     }
     if (tid == 0) HS_TRACE(a, 10);
-    // the frames are final: wave 1 writes them back now, beside wave 0's pair stage, so their stores drain while the
-    // pair stage runs (the kernel's end waits for every store)
-    if (tid >= 64 && tid < 128) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      constexpr int F0 = (int)(offsetof(HsDevState, frames) / 8), FW = (int)(sizeof(HsDevState::frames) / 8);
-      const uint2* ls = reinterpret_cast<const uint2*>(st_raw);
-      uint2* gs = reinterpret_cast<uint2*>(a.st);
-      for (int i = tid - 64; i < FW; i += 64) gs[F0 + i] = ls[F0 + i];
-    }
   }
   __syncthreads();
   {  // write the window state back (after a step: all but the frames, written above)
