@@ -570,6 +570,8 @@ static int launch_solve(hs_ctx* c, int flags, int iteration, bool log) {
   a.xAd = c->d_xAd; a.pre = c->d_pre; a.x_out = c->d_x;
   a.energy_log = log ? c->d_elog : nullptr;
   a.aux_sc = (double)(1.0f / (1 + 1e-5));  // hs_k_stitch's sc
+  a.reset_it = c->pending_reset;
+  c->pending_reset = -1;
   a.trace = c->d_tr_solve;
   a.initialCalibHessian = c->P.initialCalibHessian;
   a.thOptIterations = c->P.thOptIterations;
@@ -598,7 +600,13 @@ static int linearize_pass(hs_ctx* c, bool reset) {
   return HS_OK;
 }
 
-static int set_loop_counters(hs_ctx* c, int iteration) {
+// via_solve: the next solve launch resets them (its kernel argument); else one host-to-device copy (a captured graph
+// replays its launches' arguments, so the graph path copies)
+static int set_loop_counters(hs_ctx* c, int iteration, bool via_solve = false) {
+  if (via_solve) {
+    c->pending_reset = iteration;
+    return HS_OK;
+  }
   c->h_ctl[0] = iteration;  // iteration
   c->h_ctl[1] = 0;          // status
   c->h_ctl[2] = 0;          // log_count
@@ -679,7 +687,6 @@ static int dump_traces(hs_ctx* c) {
 // energies_out[k] = energy of the linearization after iteration k.
 static int gn_iterations(hs_ctx* c, int it0, int K, bool allow_break, double* energies_out, int* done) {
   if (K > kLogCap - 1) return fail(HS_ERR_INVALID, "too many iterations per call");
-  HS_TRY(set_loop_counters(c, it0));
   int k = 0;
   const int nev = c->events ? std::min(K, kEventIters) : 0;
   const bool all = c->events >= 2;
@@ -687,6 +694,7 @@ static int gn_iterations(hs_ctx* c, int it0, int K, bool allow_break, double* en
   // collectives inside a capture)
   const char* ge = std::getenv("HS_GRAPH");
   const bool graph = (ge && ge[0] == '1') && !allow_break && nev == 0 && !c->tracing && !c->multi_rank() && K >= 2;
+  HS_TRY(set_loop_counters(c, it0, !graph));
   if (graph) {
     if (c->gexec && c->graph_hdif != c->d_p_HdiF) drop_graph(c);
     if (!c->gexec) {
@@ -743,14 +751,15 @@ static int gn_iterations(hs_ctx* c, int it0, int K, bool allow_break, double* en
     }
   }
   c->haveSystem = true;
-  // read back: energy log (E of the linearizations consumed by each solve) + the last energy + status
-  std::vector<double> elog(k + 1, 0.0);
-  if (k > 0)
-    HS_HIP(hipMemcpyAsync(elog.data(), c->d_elog, sizeof(double) * k, hipMemcpyDeviceToHost, c->stream));
-  HS_HIP(hipMemcpyAsync(&elog[k], c->sysE(), sizeof(double), hipMemcpyDeviceToHost, c->stream));
-  HS_HIP(hipMemcpyAsync(&c->h_ctl[1], (char*)c->d_state + offsetof(HsDevState, status), sizeof(int),
-                        hipMemcpyDeviceToHost, c->stream));
+  if (c->pending_reset >= 0) HS_TRY(set_loop_counters(c, it0));  // K == 0: no solve took the reset
+  c->pending_reset = -1;
+  // read back: energy log (E of the linearizations consumed by each solve) + the last energy + status, written by
+  // one small kernel straight into pinned host memory
+  hipLaunchKernelGGL(hs_k_result, dim3(1), dim3(256), 0, c->stream, c->d_elog, k, c->sysE(), c->d_state, c->d_res);
+  HS_HIP(hipGetLastError());
   HS_HIP(hipStreamSynchronize(c->stream));
+  std::vector<double> elog(c->h_res, c->h_res + k + 1);
+  c->h_ctl[1] = (int)c->h_res[k + 1];
   double tl = 0, ta = 0, ts = 0;
   for (int q = 0; q < std::min(k, nev); q++) {
     float ms;
@@ -876,6 +885,8 @@ int hs_create(hs_ctx** out, const hs_params* params, int device_id) {
   if (hipSetDevice(device_id) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc((void**)&c->h_state, sizeof(HsDevState)) != hipSuccess ||
       hipHostMalloc((void**)&c->h_ctl, 8 * sizeof(int)) != hipSuccess ||
+      hipHostMalloc((void**)&c->h_res, sizeof(double) * (kLogCap + 2)) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&c->d_res, c->h_res, 0) != hipSuccess ||
       hipHostMalloc((void**)&c->h_fstage, fstage_bytes() + 256) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_upload, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_ready, hipEventDisableTiming) != hipSuccess) {
@@ -898,6 +909,7 @@ void hs_destroy(hs_ctx* c) {
     if (e) (void)hipEventDestroy(e);
   if (c->h_state) (void)hipHostFree(c->h_state);
   if (c->h_ctl) (void)hipHostFree(c->h_ctl);
+  if (c->h_res) (void)hipHostFree(c->h_res);
   if (c->h_fstage) (void)hipHostFree(c->h_fstage);
   if (c->ev_upload) (void)hipEventDestroy(c->ev_upload);
   if (c->ev_ready) (void)hipEventDestroy(c->ev_ready);

@@ -227,6 +227,11 @@ struct hs_ctx {
   hipEvent_t ev_xch[2] = {nullptr, nullptr};
 
   bool multi_rank() const { return comm != nullptr || !group.empty(); }
+  // the GN loop call's counters, reset by its first solve launch (reset_it; -1: none pending), and its results,
+  // written by hs_k_result into pinned host memory [kLogCap + 2] (one zero-copy write instead of three copies)
+  int pending_reset = -1;
+  double* h_res = nullptr;
+  double* d_res = nullptr;  // the device view of h_res
 
   // timings of the last optimize / iterate
   double t_lin = 0, t_acc = 0, t_solve = 0, t_timed = 0, t_wall = 0, t_iters = 0;

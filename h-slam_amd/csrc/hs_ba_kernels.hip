@@ -2024,6 +2024,7 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
   __shared__ double Sv[HS_MAXDIM], xs[HS_MAXDIM], yv[HS_MAXDIM];
   __shared__ double dgv[2 * HS_MAXDIM], dgm[2 * HS_MAXDIM];  // raw diagonal | b, and HM's diagonal | bM
   __shared__ float xF[HS_MAXDIM];
+  __shared__ double AUXs[HS_MAXF * 64];  // the diagonal blocks' host-f Schur terms (stitch aux_out)
   __shared__ int s_it;
   // the window state lives in LDS for the whole kernel: every field is touched by dependent scalar code
   // (steps, SE3 updates, precalc), which would otherwise pay a global-memory round trip per access
@@ -2077,16 +2078,17 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     qr[u] = rr;
     qc[u] = cc;
   }
-  // the diagonal frame blocks' host-f Schur terms after the energies (hs_k_stitch's aux_out): entry (qr, qc) of a
-  // block (f, f) folds in aux [f][qr - 4 - 8 f][qc - 4 - 8 f] (-1: none)
+  // the diagonal frame blocks' host-f Schur terms after the energies (hs_k_stitch's aux_out, [nF][64]): staged into
+  // LDS (one coalesced load per thread, in the batch below); entry (qr, qc) of a block (f, f) folds in
+  // aux [f][qr - 4 - 8 f][qc - 4 - 8 f] (aaddr: its LDS index, -1: none)
   const int AUX0 = nn + n + 3;
   int aaddr[NUQ];
 #pragma unroll
   for (int u = 0; u < NUQ; u++) {
     const int fr = (qr[u] - 4) >> 3, fc = (qc[u] - 4) >> 3;
-    aaddr[u] = (qr[u] >= 4 && fr == fc) ? AUX0 + fr * 64 + ((qr[u] - 4) & 7) * 8 + ((qc[u] - 4) & 7) : -1;
+    aaddr[u] = (qr[u] >= 4 && fr == fc) ? fr * 64 + ((qr[u] - 4) & 7) * 8 + ((qc[u] - 4) & 7) : -1;
   }
-  double gs[NUQ], hmq[NUQ], nfv[NF_NU], axv[NUQ];
+  double gs[NUQ], hmq[NUQ], nfv[NF_NU], axv = 0.0;
   // energy, sum |idepth|, #points (multi-rank: the ranks' values summed in rank order)
   double sysE0, sysE1, sysE2;
   if (a.gsys) {
@@ -2103,36 +2105,30 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
   }
   if (solve) {
     // HM (the marginalization prior) entries at the same places, bM for the b entries; one batch with the rest
+    axv = a.sys[AUX0 + min(tid, nF * 64 - 1)];
     if (a.HM) {
 #pragma unroll
       for (int u = 0; u < NUQ; u++) {
         gs[u] = a.sys[max(qaddr[u], 0)];
-        axv[u] = a.sys[max(aaddr[u], 0)];
         hmq[u] = qr[u] == -2 ? a.bM[qc[u]] : a.HM[qr[u] >= 0 ? qaddr[u] : 0];
       }
     } else {  // no marginalization prior (a uniform branch): only bM is read beside the system
 #pragma unroll
       for (int u = 0; u < NUQ; u++) {
         gs[u] = a.sys[max(qaddr[u], 0)];
-        axv[u] = a.sys[max(aaddr[u], 0)];
         hmq[u] = qr[u] == -2 ? a.bM[qc[u]] : 0.0;
       }
     }
     if (a.gsys) {  // multi-rank: the gathered vectors (a.sys = rank 0's) summed in rank order, the raw sums kept
 #pragma unroll
       for (int u = 0; u < NUQ; u++) {
-        const int ad = max(qaddr[u], 0), ax = max(aaddr[u], 0);
-        for (int r = 1; r < a.nranks; r++) {
-          gs[u] += a.gsys[r * a.gstride + ad];
-          axv[u] += a.gsys[r * a.gstride + ax];
-        }
+        const int ad = max(qaddr[u], 0);
+        for (int r = 1; r < a.nranks; r++) gs[u] += a.gsys[r * a.gstride + ad];
         if (qaddr[u] >= 0) a.sys_out[ad] = gs[u];
-        if (aaddr[u] >= 0) a.sys_out[ax] = axv[u];
       }
+      for (int r = 1; r < a.nranks; r++) axv += a.gsys[r * a.gstride + AUX0 + min(tid, nF * 64 - 1)];
+      if (tid < nF * 64) a.sys_out[AUX0 + tid] = axv;
     }
-#pragma unroll
-    for (int u = 0; u < NUQ; u++)
-      if (aaddr[u] >= 0) gs[u] -= a.aux_sc * axv[u];
 #pragma unroll
     for (int u = 0; u < NF_NU; u++) nfv[u] = a.Nproj[min(tid + u * SOLVE_NT, 2 * n * HS_NNS - 1)];
   }
@@ -2145,6 +2141,7 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     for (int u = 0; u < ST_NU; u++)
       if (tid + u * SOLVE_NT < ST_WORDS) ls[tid + u * SOLVE_NT] = stw[u];
   }
+  if (solve && tid < nF * 64) AUXs[tid] = axv;
   if (solve) {  // the raw diagonal (+ HM's) and b (+ bM) entries to LDS for the per-row scaling below
 #pragma unroll
     for (int u = 0; u < NUQ; u++) {
@@ -2165,7 +2162,14 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
   }
   __syncthreads();
   HS_TRACE(a, 8);
-  if (tid == 0) s_it = a.iteration >= 0 ? a.iteration : st->iteration;
+  if (tid == 0) {
+    if (a.reset_it >= 0) {  // the first launch of a GN loop call (no separate host-to-device copy of the counters)
+      st->iteration = a.reset_it;
+      st->status = 0;
+      st->log_count = 0;
+    }
+    s_it = a.iteration >= 0 ? a.iteration : st->iteration;
+  }
   const double lambda = 1e-5;  // SOLVER_FIX_LAMBDA
 
   if (solve) {
@@ -2188,7 +2192,9 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     if (tid < n) {
       const int q = tid;
       const double pr = q < 4 ? a.initialCalibHessian : st->frames[(q - 4) >> 3].prior[(q - 4) & 7];
-      const double hv = dgv[q] + (pr + dgm[q]) * lam1;
+      // (frame rows: the diagonal block's host-f Schur term folded in first, as for the off-diagonal entries)
+      const double dq = q < 4 ? dgv[q] : dgv[q] - a.aux_sc * AUXs[((q - 4) >> 3) * 64 + ((q - 4) & 7) * 9];
+      const double hv = dq + (pr + dgm[q]) * lam1;
       const double sq = rsqrt_step(hv + 10);
       Sv[q] = sq;
       A[q * n + q] = sq * hv * sq;
@@ -2199,20 +2205,15 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
         for (int k = 0; k < n; k++) hmd += a.HM[q * n + k] * delta(k);
       yv[q] = sq * ((bl + (dgm[HS_MAXDIM + q] + hmd)) + dgv[HS_MAXDIM + q]);
     }
+    __syncthreads();
     HS_TRACE(a, 7);
-    // the scaled off-diagonal entries S H S, mirrored from the upper triangle; each thread forms the scalings of its
-    // entries' two rows itself (the row threads' operations above, so the same values) instead of reading Sv
-    // behind a barrier
-    auto scale_of = [&](int q) -> double {
-      const double pr = q < 4 ? a.initialCalibHessian : st->frames[(q - 4) >> 3].prior[(q - 4) & 7];
-      const double hv = dgv[q] + (pr + dgm[q]) * lam1;
-      return rsqrt_step(hv + 10);
-    };
+    // the scaled off-diagonal entries S H S, mirrored from the upper triangle
 #pragma unroll
     for (int u = 0; u < NUQ; u++) {
       const int r = qr[u], c = qc[u];
       if (r >= 0 && r != c) {
-        const double w = scale_of(r) * (gs[u] + (a.HM ? hmq[u] : 0.0)) * scale_of(c);
+        const double gf = aaddr[u] >= 0 ? gs[u] - a.aux_sc * AUXs[aaddr[u]] : gs[u];
+        const double w = Sv[r] * (gf + (a.HM ? hmq[u] : 0.0)) * Sv[c];
         A[r * n + c] = w;
         A[c * n + r] = w;
       }
@@ -2486,6 +2487,14 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_combine(HsSolveArgs a) {
     double s = a.gsys[i];
     for (int r = 1; r < a.nranks; r++) s += a.gsys[r * a.gstride + i];
     a.sys_out[i] = s;
+  }
+}
+
+__global__ void hs_k_result(const double* elog, int k, const double* sysE, const HsDevState* st, double* out) {
+  for (int i = threadIdx.x; i < k; i += blockDim.x) out[i] = elog[i];
+  if (threadIdx.x == 0) {
+    out[k] = sysE[0];
+    out[k + 1] = (double)st->status;
   }
 }
 

@@ -193,6 +193,7 @@ struct HsSolveArgs {
   int th_local;
   HsRedArgs th;
   double aux_sc;               // the stitch's sc: the diagonal blocks' host-f Schur terms (after the energies) fold in
+  int reset_it;                // >= 0: the first launch of a GN loop call sets iteration = reset_it, status = log_count = 0
 };
 
 struct HsResubArgs {
@@ -221,7 +222,10 @@ __global__ void hs_k_th_select(HsRedArgs a);
 __global__ void hs_k_th_pass2(HsRedArgs a);     // the multi-block pass 2 alone (test hook; multi-rank large windows)
 __global__ void hs_k_stitch(HsStitchArgs a);
 __global__ void hs_k_solve(HsSolveArgs a);
-__global__ void hs_k_combine(HsSolveArgs a);   // multi-rank: the gathered systems summed into sys_out (+ block 1: select)
+__global__ void hs_k_combine(HsSolveArgs a);
+// the GN loop's results in one zero-copy write to pinned host memory: out[0, k) = elog, out[k] = energy of the last
+// linearization, out[k + 1] = status
+__global__ void hs_k_result(const double* elog, int k, const double* sysE, const HsDevState* st, double* out);   // multi-rank: the gathered systems summed into sys_out (+ block 1: select)
 __global__ void hs_k_resub(HsResubArgs a);
 __global__ void hs_k_debug_se3(int op, int n, const double* in, double* out);  // test hook
 __global__ void hs_k_apply_step(int n, const float* step, float* idepth, float* idepth_zero);
