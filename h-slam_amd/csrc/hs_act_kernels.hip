@@ -191,10 +191,14 @@ __device__ __forceinline__ void bfs_grow_wg(uint8_t* map, int w1, int h1, int*& 
 
 // addIntoDistFinal's growDistBFS from one cell, run by a single wave: the frontier of a one-seed BFS is at most
 // the ring of its step (<= 8k cells), so one wave walks it with no workgroup barrier.  Lane = frontier entry
-// (8 or 16 per pass) x neighbour direction, so a pass is one straight-line sequence: read entry, probe word, CAS,
+// (8 or 16 per pass) x neighbour direction, so a pass is one straight-line sequence: read entry, probe word, lower,
 // append (ballot + mbcnt, no atomics).  The lists are LDS.
+// claim (LDS map only): one bit per cell.  Every writer of step k stores the same byte k, so the lowering is a
+// plain byte store (no compare-and-swap retries when lanes hit the same word) and the one lane that appends the
+// cell to the next frontier is the one whose ds_or sets its claim bit; a cell's bit is cleared when its entry
+// is expanded (or, for the last frontier, at the end), so every bit is zero between calls.  Without claim: CAS.
 __device__ __forceinline__ void bfs_grow_wave(uint8_t* map, int w1, int h1, int* in, int* out, int n,
-                                              long long* cnt) {
+                                              long long* cnt, uint32_t* claim = nullptr) {
   const int lane = threadIdx.x & 63;
   // growDistBFS's neighbour order: +x, -x, +y, -y, then the diagonals (+1+w1, -1+w1, -1-w1, +1-w1)
   const int sub8 = lane & 7, sub4 = lane & 3;
@@ -202,6 +206,7 @@ __device__ __forceinline__ void bfs_grow_wave(uint8_t* map, int w1, int h1, int*
   const int dy8 = (sub8 == 2 || sub8 == 4 || sub8 == 5) ? 1 : ((sub8 == 3 || sub8 == 6 || sub8 == 7) ? -1 : 0);
   const int dx4 = sub4 == 0 ? 1 : (sub4 == 1 ? -1 : 0);
   const int dy4 = sub4 == 2 ? 1 : (sub4 == 3 ? -1 : 0);
+  n = __builtin_amdgcn_readfirstlane(n);  // uniform: the pass loop is a scalar loop
   for (int k = 1; k < HS_ACT_BFS_STEPS && n > 0; k++) {
     // odd steps: 8 entries x 8 directions per pass; even steps: 16 entries x 4 directions
     const bool diag = (k & 1) != 0;
@@ -211,11 +216,13 @@ __device__ __forceinline__ void bfs_grow_wave(uint8_t* map, int w1, int h1, int*
     const int dxy = dx + dy * 65536;
     int m = 0;
     cnt[0]++;
+    int xyn = in[min(slot, n - 1)];  // the entries of the next pass are read one pass ahead
     for (int e0 = 0; e0 < n; e0 += per) {
       cnt[1]++;
       const int e = e0 + slot;
       const bool valid = e < n;
-      const int xy = in[valid ? e : 0];
+      const int xy = xyn;
+      xyn = in[min(e + per, n - 1)];
       const int x = xy & 0xffff, y = xy >> 16;
       const bool live = valid & (x != 0) & (y != 0) & (x != w1 - 1) & (y != h1 - 1);
       const int q = live ? (x + dx) + (y + dy) * w1 : 0;
@@ -224,11 +231,23 @@ __device__ __forceinline__ void bfs_grow_wave(uint8_t* map, int w1, int h1, int*
       uint32_t old = *wp;
       bool want = live & (((old >> sh) & 0xffu) > (uint32_t)k);
       bool got = false;
-      while (want) {
-        const uint32_t pv = atomicCAS(wp, old, (old & ~(0xffu << sh)) | ((uint32_t)k << sh));
-        got = pv == old;
-        old = pv;
-        want = !got & (((old >> sh) & 0xffu) > (uint32_t)k);
+      if (claim) {
+        if (valid && (diag ? sub8 : sub4) == 0) {  // the entry is expanded now: its claim bit is released
+          const int qe = (x + w1 * y);
+          atomicAnd(&claim[qe >> 5], ~(1u << (qe & 31)));
+        }
+        if (want) {
+          map[q] = (uint8_t)k;
+          const uint32_t bit = 1u << (q & 31);
+          got = (atomicOr(&claim[q >> 5], bit) & bit) == 0u;
+        }
+      } else {
+        while (want) {
+          const uint32_t pv = atomicCAS(wp, old, (old & ~(0xffu << sh)) | ((uint32_t)k << sh));
+          got = pv == old;
+          old = pv;
+          want = !got & (((old >> sh) & 0xffu) > (uint32_t)k);
+        }
       }
       const unsigned long long bm = __ballot(got);
       if (got)
@@ -238,10 +257,19 @@ __device__ __forceinline__ void bfs_grow_wave(uint8_t* map, int w1, int h1, int*
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    n = m < HS_ACT_WAVE_LIST ? m : HS_ACT_WAVE_LIST;
+    n = __builtin_amdgcn_readfirstlane(m < HS_ACT_WAVE_LIST ? m : HS_ACT_WAVE_LIST);
     int* t = in;
     in = out;
     out = t;
+  }
+  if (claim) {  // the last frontier is never expanded: release its claims
+    for (int e = lane; e < n; e += 64) {
+      const int xy = in[e];
+      const int qe = (xy & 0xffff) + w1 * (xy >> 16);
+      atomicAnd(&claim[qe >> 5], ~(1u << (qe & 31)));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -252,7 +280,8 @@ constexpr int kSeedSep = 2 * (HS_ACT_BFS_STEPS - 1) + 2;
 
 // makeDistanceMap's BFS (whole workgroup), then the selection loop (wave 0).  Inlined once per map location so
 // the LDS instance compiles to ds_* instructions.
-__device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* map, int* s_n, int* wl0, int* wl1) {
+__device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* map, int* s_n, int* wl0, int* wl1,
+                                           uint32_t* claim = nullptr) {
   int* in = a.list_a;
   int* out = a.list_b;
   bfs_grow_wg(map, a.w1, a.h1, in, out, s_n);
@@ -331,7 +360,7 @@ __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* ma
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
       const long long c0 = a.prof ? wall_clock64() : 0;
-      bfs_grow_wave(map, a.w1, a.h1, wl0, wl1, ntake, cnt);
+      bfs_grow_wave(map, a.w1, a.h1, wl0, wl1, ntake, cnt, claim);
       if (a.prof) cnt[2] += wall_clock64() - c0;
     }
   }
@@ -354,8 +383,10 @@ __global__ void __launch_bounds__(1024) hs_k_act_select(HsActSelectArgs a) {
   if (a.lds_map) {
     const uint32_t* g = reinterpret_cast<const uint32_t*>(a.dist);
     for (int w = threadIdx.x; w < words; w += blockDim.x) s_map32[w] = g[w];
+    uint32_t* claim = s_map32 + words;  // one bit per cell, zero between the BFS calls
+    for (int w = threadIdx.x; w < (a.w1 * a.h1 + 31) / 32; w += blockDim.x) claim[w] = 0u;
     __syncthreads();
-    nt = select_body(a, reinterpret_cast<uint8_t*>(s_map32), s_n, s_wl[0], s_wl[1]);
+    nt = select_body(a, reinterpret_cast<uint8_t*>(s_map32), s_n, s_wl[0], s_wl[1], claim);
     if (threadIdx.x >= 64) return;
     uint32_t* go = reinterpret_cast<uint32_t*>(a.dist);
     for (int w = threadIdx.x; w < words; w += 64) go[w] = s_map32[w];

@@ -138,6 +138,7 @@ struct LinIn {
   unsigned fm;        // previous linearization's active mask
   float jpj, bds, hdi;
   float4 hcd;
+  float priorF;       // the point's idepth prior (its load would otherwise sit in the middle of the point sums)
 };
 __device__ __forceinline__ void lin_load(const HsLinArgs& a, int p, int lane, LinIn& in) {
   const int t = lane >> 3, k = lane & 7, sl = p * 8 + t;
@@ -157,11 +158,13 @@ __device__ __forceinline__ void lin_load(const HsLinArgs& a, int p, int lane, Li
   in.bds = a.p_bdSumF[p];
   in.hdi = a.p_HdiF_prev[p];
   in.hcd = reinterpret_cast<const float4*>(a.p_Hcd)[p];
+  in.priorF = a.priorF[p];
 }
 
 // per-block constants of lin_point, staged in LDS once per block: the host's precalc records (by target slot),
 // the frames' thresholds, xAd[h][t][k] and the calib step
 struct LinConst {
+  HsCalib cal;  // the scaled calib (staged with the rest: a load in lin_point would follow the block barrier)
   HsPrecalc pre[HS_MAXF];
   float th[HS_MAXF];
   float xad[HS_MAXF * 8];
@@ -185,7 +188,7 @@ __device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int 
   const int t = lane >> 3;  // target slot
   const int k = lane & 7;   // pattern pixel
   const int nF = a.nF;
-  const HsCalib cal = a.st->dcal;
+  const HsCalib cal = K.cal;
   if (a.marg && a.marg[p] == 0) {  // marginalization pass, point not marginalized: no active residual
     if (lane == 0) {
       a.p_actmask[p] = 0;
@@ -350,6 +353,7 @@ __device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int 
     const float PKu = q0 / q2, PKv = q1 / q2;
     const bool okP = okC && (PKu > 1.1f && PKv > 1.1f && PKu < (cal.W - 3) && PKv < (cal.H - 3));
     float3 hit = interp33(timg, okP ? PKu : 2.f, okP ? PKv : 2.f, cal.W);
+    if (a.trace && threadIdx.x == 0 && hit.x != -12345.f) a.trace[(size_t)blockIdx.x * 16 + 13] = wall_clock64();
     const float color = colorK;
     const float residual = hit.x - (float)(pc.aff[0] * color + pc.aff[1]);
     const float drdA = (color - pc.b0);
@@ -455,6 +459,7 @@ __device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int 
     }
     S[16] = ss[t * LW_SS + 16];
   }
+  if (a.trace && threadIdx.x == 0 && S[0] != -12345.f) a.trace[(size_t)blockIdx.x * 16 + 14] = wall_clock64();
 
   // ---------------- state decision + applyRes (the 8 lanes of a slot agree; lane k == 0 writes)
   const bool live = has && st != HS_RES_OOB;      // OOB is sticky: linearize returns state_energy
@@ -533,7 +538,7 @@ __device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int 
     if (mask != 0u) {
       // marginalization pass: priorF *= idepthFixPriorMargFac, the sums are the LF ones (AF = 0), and
       // AccumulatedSCHessianSSE::addPoint(p, shiftPriorToZero = false) (Src/EnergyFunctional.cpp:563,577)
-      const float priorF = a.marg ? a.priorF[p] * a.margPriorFac : a.priorF[p];
+      const float priorF = a.marg ? in.priorF * a.margPriorFac : in.priorF;
       float Hh = a.marg ? (0.f + Hdd) + priorF : Hdd + 0.f + priorF;  // Hdd_accAF + Hdd_accLF + priorF
       if ((double)Hh < 1e-10) Hh = (float)1e-10;
       HdiF = (float)(1.0 / (double)Hh);
@@ -579,6 +584,7 @@ __device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int 
     o.Hcd[0] = hc4.x; o.Hcd[1] = hc4.y; o.Hcd[2] = hc4.z; o.Hcd[3] = hc4.w;
     o.eSum = eSum;
   }
+  if (a.trace && threadIdx.x == 0 && o.eSum != -12345.0) a.trace[(size_t)blockIdx.x * 16 + 15] = wall_clock64();
 #pragma unroll
   for (int i = 0; i < 10; i++) {
     o.Jx[i] = Jx[i];
@@ -728,6 +734,10 @@ __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
       K.xad[tid] = s1 + s2;
     }
     if (tid < 4) K.cs[tid] = a.st->cstep[tid];
+    constexpr int CW = (int)(sizeof(HsCalib) / 4);
+    static_assert(sizeof(HsCalib) % 4 == 0, "calib staged as words");
+    if (tid >= 64 && tid < 64 + CW)
+      reinterpret_cast<int*>(&K.cal)[tid - 64] = reinterpret_cast<const int*>(&a.st->dcal)[tid - 64];
   }
   LinAcc<kExact> A;
 #pragma unroll
@@ -743,6 +753,7 @@ __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
   const bool work = wv < a.W && pb + wv < pe;
   if (work) lin_load(a, pb + wv, lane, cur);  // in flight across the barrier
   __syncthreads();
+  HS_TRACE(a, 12);
   if (work) {
     for (int p = pb + wv; p < pe; p += a.W) {  // wave-uniform
       LinIn nxt;
@@ -1745,8 +1756,11 @@ struct PanelOut {
 };
 // wave-cooperative panel factorization: lane l holds row K0 + l (lanes 0-3: the diagonal block's rows), a =
 // its entries of the panel columns, yr its rhs; every lane of the wave executes this.  Column by column: the
-// pivot and the reduced entries come from lanes 0-3 by readlane, so the critical path per column is one
-// readlane, one reciprocal and one multiply-add.  A diagonal row l takes L entries only for j < l.
+// pivot and the reduced entries come from lanes 0-3 by readlane.  The later columns are reduced as
+// a(jp) -= (a(j) q(jp, j)) / d(j), the product formed beside the reciprocal, so the critical path per column is
+// one readlane, the reciprocal (+ Newton step) and one multiply-add; L = a(j) / d(j) and its row mask stay off
+// it (rows l <= j of the diagonal block take garbage updates of entries no later column reads).  A diagonal row
+// l takes L entries only for j < l.
 __device__ __forceinline__ void panel_coop(const double a[4], double yr, int l, Panel4& P, PanelOut& o, int base = 0) {
   double pr[4] = {a[0], a[1], a[2], a[3]};
 #pragma unroll
@@ -1763,7 +1777,7 @@ __device__ __forceinline__ void panel_coop(const double a[4], double yr, int l, 
     o.lw[j] = l > j ? pr[j] : 0.0;
     o.ls[j] = l > j ? lj : 0.0;
 #pragma unroll
-    for (int jp = j + 1; jp < 4; jp++) pr[jp] = __builtin_fma(-o.ls[j], P.q[jp][j], pr[jp]);
+    for (int jp = j + 1; jp < 4; jp++) pr[jp] = __builtin_fma(-(pr[j] * P.q[jp][j]), dinv, pr[jp]);
     yr = __builtin_fma(-o.ls[j], ydj, yr);
   }
   o.yr = yr;
@@ -1776,7 +1790,7 @@ __device__ __forceinline__ void panel_row_uniform(const double a[4], double yr, 
     o.lw[j] = pr[j];
     o.ls[j] = pr[j] * P.dinv[j];
 #pragma unroll
-    for (int jp = j + 1; jp < 4; jp++) pr[jp] = __builtin_fma(-o.ls[j], P.q[jp][j], pr[jp]);
+    for (int jp = j + 1; jp < 4; jp++) pr[jp] = __builtin_fma(-(pr[j] * P.q[jp][j]), P.dinv[j], pr[jp]);
     yr = __builtin_fma(-o.ls[j], P.yd[j], yr);
   }
   o.yr = yr;

@@ -16,7 +16,7 @@
 #include "hs_pyr_kernels.h"
 
 #define HS_MAXF_ACT 8                        // activation window (nF <= 8 keyframes)
-#define HS_ACT_LDS_MAP_MAX (140 * 1024)     // level-1 distance map in LDS up to this size (+16 KB of lists)
+#define HS_ACT_LDS_MAP_MAX (144 * 1024)     // level-1 distance map + its claim bits in LDS up to this size (+16 KB of lists)
 
 namespace hs {
 extern thread_local std::string g_err;
@@ -529,7 +529,8 @@ int hs_tracer_activate(hs_tracer* t, const float K4[4], int nF, const hs_act_fra
   se.w1 = t->w1;
   se.h1 = t->h1;
   const size_t map_bytes = (size_t)((wh1 + 3) & ~3);
-  se.lds_map = map_bytes <= HS_ACT_LDS_MAP_MAX ? 1 : 0;
+  const size_t claim_bytes = (size_t)((wh1 + 31) / 32) * 4;  // the greedy BFS's claim bits (hs_act_kernels.hip)
+  se.lds_map = map_bytes + claim_bytes <= HS_ACT_LDS_MAP_MAX ? 1 : 0;
   se.order = order ? t->d_order : nullptr;
   se.cand = t->d_cand;
   se.cell = t->d_cell;
@@ -545,7 +546,7 @@ int hs_tracer_activate(hs_tracer* t, const float K4[4], int nF, const hs_act_fra
   long long* d_prof = nullptr;
   if (prof_on) TR_HIP(hipMalloc((void**)&d_prof, sizeof(long long) * 8));
   se.prof = d_prof;
-  const size_t lds = se.lds_map ? map_bytes : 0;
+  const size_t lds = se.lds_map ? map_bytes + claim_bytes : 0;
   if (lds > 65536)
     TR_HIP(hipFuncSetAttribute((const void*)hs_k_act_select, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(hs_k_act_select, dim3(1), dim3(1024), lds, s, se);
