@@ -54,8 +54,10 @@ struct hs_tracker {
   double* d_Tin = nullptr;
   HsTryOut* d_out = nullptr;
   double* d_part = nullptr;       // [try_cap][2][HS_TRK_MAXG][HS_TRK_NRED] pass partials of the member workgroups
-  unsigned int* d_cnt = nullptr;  // [try_cap] pass counters (zeroed per launch)
+  unsigned int* d_cnt = nullptr;  // [try_cap] timeout flags, in d_part's allocation after the granules (one memset)
   HsTryOut* h_out = nullptr;
+  double* h_in = nullptr;         // pinned staging of the hypotheses (T | aff), so their upload is asynchronous
+  unsigned int* h_cnt = nullptr;  // pinned read-back of the timeout flags
   double* d_lmlog = nullptr;
   int* d_lmlvl = nullptr;
   int try_cap = 0, last_n_tries = 0;
@@ -81,6 +83,9 @@ static int upload_pyr(hs_tracker* t, float4** dst, const float* const* pyr) {
   return HS_OK;
 }
 
+// the member workgroups' pass granules of n hypotheses: [n][2][HS_TRK_MAXG][HS_TRK_NRED][2] u64
+static size_t part_bytes(int n) { return sizeof(unsigned long long) * 2 * HS_TRK_MAXG * HS_TRK_NRED * 2 * (size_t)n; }
+
 static int ensure_tries(hs_tracker* t, int n) {
   if (n <= t->try_cap) return HS_OK;
   if (t->d_Tin) (void)hipFree(t->d_Tin);
@@ -88,17 +93,20 @@ static int ensure_tries(hs_tracker* t, int n) {
   if (t->h_out) (void)hipHostFree(t->h_out);
   if (t->d_lmlog) (void)hipFree(t->d_lmlog);
   if (t->d_part) (void)hipFree(t->d_part);
-  if (t->d_cnt) (void)hipFree(t->d_cnt);
-  t->d_part = nullptr; t->d_cnt = nullptr;
+  if (t->h_in) (void)hipHostFree(t->h_in);
+  if (t->h_cnt) (void)hipHostFree(t->h_cnt);
+  t->d_part = nullptr; t->d_cnt = nullptr; t->h_in = nullptr; t->h_cnt = nullptr;
   if (t->d_lmlvl) (void)hipFree(t->d_lmlvl);
   t->d_Tin = nullptr; t->d_out = nullptr; t->h_out = nullptr; t->d_lmlog = nullptr; t->d_lmlvl = nullptr;
   TS_HIP(hipMalloc((void**)&t->d_Tin, sizeof(double) * 9 * n));  // T (7) | aff (2)
   TS_HIP(hipMalloc((void**)&t->d_out, sizeof(HsTryOut) * n));
   TS_HIP(hipMalloc((void**)&t->d_lmlog, sizeof(double) * 3 * HS_TRK_MAXLOG * n));
   TS_HIP(hipMalloc((void**)&t->d_lmlvl, sizeof(int) * HS_TRK_MAXLOG * n));
-  TS_HIP(hipMalloc((void**)&t->d_part, sizeof(unsigned long long) * 2 * HS_TRK_MAXG * HS_TRK_NRED * 2 * n));
-  TS_HIP(hipMalloc((void**)&t->d_cnt, sizeof(unsigned int) * n + 16));
+  TS_HIP(hipMalloc((void**)&t->d_part, part_bytes(n) + sizeof(unsigned int) * n + 16));
+  t->d_cnt = reinterpret_cast<unsigned int*>(reinterpret_cast<char*>(t->d_part) + part_bytes(n));
   TS_HIP(hipHostMalloc((void**)&t->h_out, sizeof(HsTryOut) * n));
+  TS_HIP(hipHostMalloc((void**)&t->h_in, sizeof(double) * 9 * n));
+  TS_HIP(hipHostMalloc((void**)&t->h_cnt, sizeof(unsigned int) * n));
   t->try_cap = n;
   return HS_OK;
 }
@@ -129,7 +137,8 @@ static HsTrackArgs make_args(hs_tracker* t) {
 // n hypotheses (T | aff per row in h_in), run to completion without abort
 static int run_tries(hs_tracker* t, int n, const double* h_in, int coarsest, int single_pass, int lvl, float cutoff) {
   TS_TRY(ensure_tries(t, n));
-  TS_HIP(hipMemcpyAsync(t->d_Tin, h_in, sizeof(double) * 9 * n, hipMemcpyHostToDevice, t->stream));
+  std::memcpy(t->h_in, h_in, sizeof(double) * 9 * n);
+  TS_HIP(hipMemcpyAsync(t->d_Tin, t->h_in, sizeof(double) * 9 * n, hipMemcpyHostToDevice, t->stream));
   HsTrackArgs a = make_args(t);
   a.coarsest = coarsest;
   a.T_in = t->d_Tin;
@@ -154,10 +163,9 @@ static int run_tries(hs_tracker* t, int n, const double* h_in, int coarsest, int
   a.cnt = t->d_cnt;
   t->last_G = G;
   // the granules and the timeout flags, zeroed before every launch (16-B multiples from the allocations' starts)
-  if (G > 1) {
-    TS_HIP(hipMemsetAsync(t->d_part, 0, sizeof(unsigned long long) * 2 * HS_TRK_MAXG * HS_TRK_NRED * 2 * n, t->stream));
-    TS_HIP(hipMemsetAsync(t->d_cnt, 0, (sizeof(unsigned int) * n + 15) & ~(size_t)15, t->stream));
-  }
+  if (G > 1)  // the granules of this launch's hypotheses, then the timeout flags (a multiple of 16 B)
+    TS_HIP(hipMemsetAsync(t->d_part, 0, part_bytes(t->try_cap) + ((sizeof(unsigned int) * n + 15) & ~(size_t)15),
+                          t->stream));
   const char* kt = std::getenv("HS_KTRACE");
   if (kt && kt[0] == '1' && !single_pass) {
     const int nb = n * G;
@@ -175,11 +183,10 @@ static int run_tries(hs_tracker* t, int n, const double* h_in, int coarsest, int
   TS_HIP(hipGetLastError());
   TS_HIP(hipEventRecord(t->e1, t->stream));
   TS_HIP(hipMemcpyAsync(t->h_out, t->d_out, sizeof(HsTryOut) * n, hipMemcpyDeviceToHost, t->stream));
-  std::vector<unsigned int> tmo(G > 1 ? n : 0);
-  if (G > 1) TS_HIP(hipMemcpyAsync(tmo.data(), t->d_cnt, sizeof(unsigned int) * n, hipMemcpyDeviceToHost, t->stream));
+  if (G > 1) TS_HIP(hipMemcpyAsync(t->h_cnt, t->d_cnt, sizeof(unsigned int) * n, hipMemcpyDeviceToHost, t->stream));
   TS_HIP(hipStreamSynchronize(t->stream));
-  for (unsigned int v : tmo)
-    if (v) return tfail(HS_ERR_HIP, "hs_k_track: a member workgroup never reached a pass (spin bound hit)");
+  for (int i = 0; G > 1 && i < n; i++)
+    if (t->h_cnt[i]) return tfail(HS_ERR_HIP, "hs_k_track: a member workgroup never reached a pass (spin bound hit)");
   float ms = 0;
   TS_HIP(hipEventElapsedTime(&ms, t->e0, t->e1));
   t->last_ms = ms;
@@ -315,10 +322,12 @@ void hs_tracker_destroy(hs_tracker* t) {
       if (p) (void)hipFree(p);
   }
   void* ps[] = {t->d_pcn, t->d_bcnt, t->d_boff, t->d_pts, t->d_Tin, t->d_out, t->d_lmlog, t->d_lmlvl, t->d_raw,
-                t->d_trace};
+                t->d_trace, t->d_part};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   if (t->h_out) (void)hipHostFree(t->h_out);
+  if (t->h_in) (void)hipHostFree(t->h_in);
+  if (t->h_cnt) (void)hipHostFree(t->h_cnt);
   if (t->e0) (void)hipEventDestroy(t->e0);
   if (t->e1) (void)hipEventDestroy(t->e1);
   if (t->stream) (void)hipStreamDestroy(t->stream);

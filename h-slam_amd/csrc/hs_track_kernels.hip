@@ -418,34 +418,53 @@ __device__ void trk_pass(const HsTrackArgs& a, TrkShared& S, int h, int g) {
     S.pointPasses += n;
     const int npad = (numW + 3) & ~3;  // buf_warped_n includes the zero padding (quirk kept)
     S.nWarped = npad;
-    const double inv = (double)(1.0f / npad);
-    const double sc[8] = {hs_trk_scale_rot, hs_trk_scale_rot, hs_trk_scale_rot, hs_trk_scale_trans,
-                          hs_trk_scale_trans, hs_trk_scale_trans, hs_trk_scale_a, hs_trk_scale_b};
-    int q = 0;
-#pragma unroll
-    for (int r = 0; r < 9; r++)
-#pragma unroll
-      for (int c = r; c < 9; c++) {
-        const double v = (double)(float)R[q++];
-        if (r < 8 && c < 8) {
-          S.H[r * 8 + c] = ((v * inv) * sc[c]) * sc[r];
-          S.H[c * 8 + r] = ((v * inv) * sc[r]) * sc[c];
-        }
-        if (c == 8) S.b[r] = (v * inv) * sc[r];
-      }
     if (a.trace) {
-      const long long pc2 = clock64() + (long long)(S.b[7] * 0.0);
+      const long long pc2 = clock64() + (long long)(S.res[5] * 0.0);
       S.prof[0] += pc1 - pc0;
       S.prof[1] += pc2 - pc1;
       S.prof[3] += 1;
     }
   }
+  if (tid >= 64 && tid < 64 + 45) {  // H / b from the 45 upper-triangle sums (row-major), one entry per thread
+    int q = tid - 64, r = 0;
+    while (q >= 9 - r) {
+      q -= 9 - r;
+      r++;
+    }
+    const int c = r + q;
+    const double* R = S.red[0];
+    const int numW = (int)R[TRK_NACC + 6];
+    const int npad = (numW + 3) & ~3;
+    const double inv = (double)(1.0f / npad);
+    const double v = (double)(float)R[tid - 64];
+    const double sr = r < 3 ? hs_trk_scale_rot : r < 6 ? hs_trk_scale_trans : r == 6 ? hs_trk_scale_a : hs_trk_scale_b;
+    const double scc = c < 3 ? hs_trk_scale_rot : c < 6 ? hs_trk_scale_trans : c == 6 ? hs_trk_scale_a : hs_trk_scale_b;
+    if (c < 8) {
+      S.H[r * 8 + c] = ((v * inv) * scc) * sr;
+      S.H[c * 8 + r] = ((v * inv) * sr) * scc;
+    } else if (r < 8) {  // (8, 8) is the residual square sum, not part of H / b
+      S.b[r] = (v * inv) * sr;
+    }
+  }
   __syncthreads();
 }
 
-// thread 0: the pass inputs for state (T, aff) at level lvl
-__device__ void trk_setup(const HsTrackArgs& a, TrkShared& S, const double T7[7], const double aff[2], int lvl,
-                          float cutoff) {
+// the pass inputs for state (T, aff) at level lvl: the pose part (pose = true: RKi, t) and / or the affine part
+// (pose = false: the relative affine transfer, the cutoff); one thread each, or one thread both
+__device__ void trk_setup_part(const HsTrackArgs& a, TrkShared& S, const double T7[7], const double aff[2], int lvl,
+                               float cutoff, bool pose) {
+  if (!pose) {
+    double rel[2];
+    hs::fromToVecExposure(a.refExposure, a.newExposure, a.refAff[0], a.refAff[1], aff[0], aff[1], rel);
+    S.affLL[0] = (float)rel[0];
+    S.affLL[1] = (float)rel[1];
+    S.a_gs = (float)rel[0];
+    S.b0 = (float)a.refAff[1];
+    S.cutoff = cutoff;
+    S.maxEnergy = 2 * a.huberTH * cutoff - a.huberTH * a.huberTH;
+    S.lvl = lvl;
+    return;
+  }
   const hs::SE3 T = hs::SE3::fromData(T7);
   double Rd[9];
   T.rotationMatrix(Rd);
@@ -455,15 +474,11 @@ __device__ void trk_setup(const HsTrackArgs& a, TrkShared& S, const double T7[7]
   for (int r = 0; r < 3; r++)
     for (int c = 0; c < 3; c++) S.RKi[r * 3 + c] = R[r * 3 + 0] * Ki[0 * 3 + c] + R[r * 3 + 1] * Ki[1 * 3 + c] + R[r * 3 + 2] * Ki[2 * 3 + c];
   for (int q = 0; q < 3; q++) S.t[q] = (float)T.t[q];
-  double rel[2];
-  hs::fromToVecExposure(a.refExposure, a.newExposure, a.refAff[0], a.refAff[1], aff[0], aff[1], rel);
-  S.affLL[0] = (float)rel[0];
-  S.affLL[1] = (float)rel[1];
-  S.a_gs = (float)rel[0];
-  S.b0 = (float)a.refAff[1];
-  S.cutoff = cutoff;
-  S.maxEnergy = 2 * a.huberTH * cutoff - a.huberTH * a.huberTH;
-  S.lvl = lvl;
+}
+__device__ void trk_setup(const HsTrackArgs& a, TrkShared& S, const double T7[7], const double aff[2], int lvl,
+                          float cutoff) {
+  trk_setup_part(a, S, T7, aff, lvl, cutoff, true);
+  trk_setup_part(a, S, T7, aff, lvl, cutoff, false);
 }
 
 }  // namespace
@@ -532,9 +547,11 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
     __syncthreads();
     for (int iteration = 0; iteration < maxIterations[lvl]; iteration++) {
       __syncthreads();  // every thread has read S.brk of the previous iteration
-      if (tid == 0) {
+      // the LM step on two waves: lane 0 of wave 0 the pose (exp, product, RKi), lane 0 of wave 1 the affine part
+      // (fromToVecExposure); both solve the same 8x8 system (same inputs, same increment)
+      if (tid == 0 || tid == 64) {
+        const bool pw = tid == 0;
         const long long lm0 = a.trace ? clock64() : 0;
-        S.iters++;
         // Hl = H with the diagonal scaled by (1 + lambda): formed as the solver loads H (pivoted indices)
         double mb[8], inc[8];
 #pragma unroll
@@ -553,17 +570,23 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
         for (int i = 0; i < 8; i++) ssum += incScaled[i];
         if (!isfinite(ssum))
           for (int i = 0; i < 8; i++) incScaled[i] = 0;
-        // the series exp / rsqrt-normalized product of the BA doStep (hs_se3_dev.h): Sophus' up to rounding
-        const hs::SE3 nw = se3_mul_step(se3_exp_step(incScaled), hs::SE3::fromData(S.T));
-        nw.toData(S.Tn);
-        S.affn[0] = S.aff[0] + incScaled[6];
-        S.affn[1] = S.aff[1] + incScaled[7];
-        double nn = 0;
-        for (int i = 0; i < 8; i++) nn += inc[i] * inc[i];
-        S.incNorm = sqrt(nn);
-        S.brk = !(S.incNorm > 1e-3);
-        trk_setup(a, S, S.Tn, S.affn, lvl, a.coarseCutoffTH * S.cutoffRep);
-        if (a.trace) S.prof[2] += clock64() + (long long)(S.RKi[4] * 0.f) - lm0;
+        if (pw) {
+          S.iters++;
+          // the series exp / rsqrt-normalized product of the BA doStep (hs_se3_dev.h): Sophus' up to rounding
+          const hs::SE3 nw = se3_mul_step(se3_exp_step(incScaled), hs::SE3::fromData(S.T));
+          nw.toData(S.Tn);
+          double nn = 0;
+          for (int i = 0; i < 8; i++) nn += inc[i] * inc[i];
+          S.incNorm = sqrt(nn);
+          S.brk = !(S.incNorm > 1e-3);
+          trk_setup_part(a, S, S.Tn, nullptr, lvl, 0.f, true);
+          if (a.trace) S.prof[2] += clock64() + (long long)(S.RKi[4] * 0.f) - lm0;
+        } else {
+          double affn[2] = {S.aff[0] + incScaled[6], S.aff[1] + incScaled[7]};
+          S.affn[0] = affn[0];
+          S.affn[1] = affn[1];
+          trk_setup_part(a, S, nullptr, affn, lvl, a.coarseCutoffTH * S.cutoffRep, false);
+        }
       }
       __syncthreads();
       trk_pass(a, S, h, g);
