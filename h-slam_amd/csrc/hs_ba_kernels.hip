@@ -2375,9 +2375,55 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
       o[14] = sc[6];
       o[15] = sc[7];
     }
+    if (tid == 128) {  // canbreak on wave 2, beside the frame stage (it reads the steps only, which no stage writes)
+      float sumA = 0, sumB = 0, sumT = 0, sumR = 0;
+      for (int f = 0; f < nF; f++) {
+        const double* sp = st->frames[f].step;
+        sumA += sp[6] * sp[6];
+        sumB += sp[7] * sp[7];
+        sumT += sp[0] * sp[0] + sp[1] * sp[1] + sp[2] * sp[2];
+        sumR += sp[3] * sp[3] + sp[4] * sp[4] + sp[5] * sp[5];
+      }
+      const float nfr = (float)nF;
+      sumA /= nfr; sumB /= nfr; sumR /= nfr; sumT /= nfr;
+      const float sumNID = sysE2 > 0 ? (float)(sysE1 / sysE2) : 0.f;
+      const float th = a.thOptIterations;
+      st->canbreak = sqrtf(sumA) < 0.0005 * th && sqrtf(sumB) < 0.00005 * th && sqrtf(sumR) < 0.00005 * th &&
+                     sqrtf(sumT) * sumNID < 0.00005 * th;
+      st->iteration = s_it + 1;
+    }
+    // the pair stage's pose-free part on wave 0, beside the frame stage: the affine transfer from the frames' new
+    // scaled a / b (the frame stage's own ns -> sc arithmetic), K and K^-1 from the new calib, b0
+    float pK[9], pKi[9];
+    if (tid < np) {
+      const int hh = tid / nF, tt = tid - hh * nF;
+      const hs::FrameH& H = st->frames[hh];
+      const hs::FrameH& T = st->frames[tt];
+      const double ah = hs::SCALE_A * (H.state[6] + 1.0 * H.step[6]), bh = hs::SCALE_B * (H.state[7] + 1.0 * H.step[7]);
+      const double at = hs::SCALE_A * (T.state[6] + 1.0 * T.step[6]), bt = hs::SCALE_B * (T.state[7] + 1.0 * T.step[7]);
+      double aff[2];
+      hs::fromToVecExposure(H.ab_exposure, T.ab_exposure, ah, bh, at, bt, aff);
+      HsPrecalc* pc = a.pre + tid;
+      pc->aff[0] = (float)aff[0];
+      pc->aff[1] = (float)aff[1];
+      pc->b0 = (float)(H.state_zero[7] * hs::SCALE_B);  // aff0_b of the host
+      const float vsf[4] = {(float)(hs::SCALE_F * cv[0]), (float)(hs::SCALE_F * cv[1]), (float)(hs::SCALE_C * cv[2]),
+                            (float)(hs::SCALE_C * cv[3])};
+      const float K[9] = {vsf[0], 0, vsf[2], 0, vsf[1], vsf[3], 0, 0, 1};
+#pragma unroll
+      for (int i = 0; i < 9; i++) pK[i] = K[i];
+      hs::inv3f(pK, pKi);
+    }
     if ((a.dbg & 16) && a.trace && tid == 0) a.trace[22] = clock64();
     __syncthreads();
     if ((a.dbg & 16) && a.trace && tid == 0) a.trace[23] = clock64();
+    if (tid == 192) {  // the calib on wave 3, beside the pair stage (every lane read cv before the barrier)
+      hs::CalibH& cal = st->calib;
+#pragma unroll
+      for (int q = 0; q < 4; q++) cal.value_backup[q] = cal.value[q];
+      cal.setValue(cv);
+      st->dcal = cal.device();
+    }
     if (tid < np) {
       const int hh = tid / nF, tt = tid - hh * nF;
       const double* oh = fx + 16 * hh;
@@ -2387,9 +2433,7 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
       PWt.t[0] = ot[4]; PWt.t[1] = ot[5]; PWt.t[2] = ot[6];
       PCh.q = hs::Quat{oh[7], oh[8], oh[9], oh[10]};
       PCh.t[0] = oh[11]; PCh.t[1] = oh[12]; PCh.t[2] = oh[13];
-      const hs::FrameH& H = st->frames[hh];
-      const hs::FrameH& T = st->frames[tt];
-      // FrameFramePrecalc::set: PRE_RTll / PRE_tTll, K R Ki, K t, the affine mode, b0
+      // FrameFramePrecalc::set: PRE_RTll / PRE_tTll, K R Ki, K t (the affine mode and b0 are stored above)
       const hs::SE3 l2l = se3_mul_step(PWt, PCh);
       double R[9];
       l2l.rotationMatrix(R);
@@ -2398,24 +2442,15 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
       for (int i = 0; i < 9; i++) RT[i] = (float)R[i];
 #pragma unroll
       for (int i = 0; i < 3; i++) tT[i] = (float)l2l.t[i];
-      float vsf[4] = {(float)(hs::SCALE_F * cv[0]), (float)(hs::SCALE_F * cv[1]), (float)(hs::SCALE_C * cv[2]),
-                      (float)(hs::SCALE_C * cv[3])};
-      float K[9] = {vsf[0], 0, vsf[2], 0, vsf[1], vsf[3], 0, 0, 1};
-      float Ki[9], KR[9], KRKi[9], Kt[3];
-      hs::inv3f(K, Ki);
-      hs::mm3f(K, RT, KR);
-      hs::mm3f(KR, Ki, KRKi);
-      hs::mv3f(K, tT, Kt);
-      double aff[2];
-      hs::fromToVecExposure(H.ab_exposure, T.ab_exposure, oh[14], oh[15], ot[14], ot[15], aff);
+      float KR[9], KRKi[9], Kt[3];
+      hs::mm3f(pK, RT, KR);
+      hs::mm3f(KR, pKi, KRKi);
+      hs::mv3f(pK, tT, Kt);
       HsPrecalc* pc = a.pre + tid;
 #pragma unroll
       for (int i = 0; i < 9; i++) pc->KRKi[i] = KRKi[i];
 #pragma unroll
       for (int i = 0; i < 3; i++) pc->Kt[i] = Kt[i];
-      pc->aff[0] = (float)aff[0];
-      pc->aff[1] = (float)aff[1];
-      pc->b0 = (float)(H.state_zero[7] * hs::SCALE_B);  // aff0_b of the host
     }
     if (fl) {  // frame fw: backupState, setState, setDeltaF's delta / delta_prior
       hs::FrameH& F = st->frames[fw];
@@ -2434,42 +2469,21 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
       }
     }
     // the frames are final: wave 1 writes them back now, beside wave 0's pair stage, so their stores drain while the
-    // pair stage runs (the kernel's end waits for every store); the calib and canbreak below touch no frame
+    // pair stage runs (the kernel's end waits for every store); the calib (wave 3) and canbreak (wave 2) run elsewhere
     if (tid >= 64 && tid < 128) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      constexpr int F0 = (int)(offsetof(HsDevState, frames) / 8), FW = (int)(sizeof(HsDevState::frames) / 8);
+      constexpr int F0 = (int)(offsetof(HsDevState, frames) / 8), FW1 = (int)(sizeof(hs::FrameH) / 8);
+      static_assert(sizeof(hs::FrameH) % 8 == 0, "frames are copied as 8-byte words");
       const uint2* ls = reinterpret_cast<const uint2*>(st_raw);
       uint2* gs = reinterpret_cast<uint2*>(a.st);
-      for (int i = tid - 64; i < FW; i += 64) gs[F0 + i] = ls[F0 + i];
-    }
-    if (tid == 64) {  // the calib (on wave 1, beside the pair stage: every lane read cv before the barrier)
-      hs::CalibH& cal = st->calib;
-#pragma unroll
-      for (int q = 0; q < 4; q++) cal.value_backup[q] = cal.value[q];
-      cal.setValue(cv);
-      st->dcal = cal.device();
+      const int fwn = nF * FW1;  // the window's frames only (the solve touches no other slot)
+#pragma unroll 4
+      for (int i = tid - 64; i < fwn; i += 64) gs[F0 + i] = ls[F0 + i];
     }
     if ((a.dbg & 16) && a.trace && tid == 0) a.trace[21] = clock64();
     HS_TRACE(a, 6);
-    if (tid == 64) {  // canbreak (the steps are not modified above)
-      float sumA = 0, sumB = 0, sumT = 0, sumR = 0;
-      for (int f = 0; f < nF; f++) {
-        const double* sp = st->frames[f].step;
-        sumA += sp[6] * sp[6];
-        sumB += sp[7] * sp[7];
-        sumT += sp[0] * sp[0] + sp[1] * sp[1] + sp[2] * sp[2];
-        sumR += sp[3] * sp[3] + sp[4] * sp[4] + sp[5] * sp[5];
-      }
-      const float nfr = (float)nF;
-      sumA /= nfr; sumB /= nfr; sumR /= nfr; sumT /= nfr;
-      const float sumNID = sysE2 > 0 ? (float)(sysE1 / sysE2) : 0.f;
-      const float th = a.thOptIterations;
-      st->canbreak = sqrtf(sumA) < 0.0005 * th && sqrtf(sumB) < 0.00005 * th && sqrtf(sumR) < 0.00005 * th &&
-                     sqrtf(sumT) * sumNID < 0.00005 * th;
-      st->iteration = s_it + 1;
-    }
     if (tid == 0) HS_TRACE(a, 10);
   }
   __syncthreads();
