@@ -195,7 +195,8 @@ static int run_tries(hs_tracker* t, int n, const double* h_in, int coarsest, int
     long long h[16];
     TS_HIP(hipMemcpy(h, t->d_trace, sizeof(h), hipMemcpyDeviceToHost));
     std::fprintf(stderr, "[trk trace] %.3f ms: point loop %lld, reductions %lld (wave reduce %lld, barrier wait %lld), "
-                 "LM steps %lld cycles over %lld passes\n", ms, h[4], h[5], h[8], h[9], h[6], h[7]);
+                 "LM steps %lld (LDLT %lld, exp + product %lld) cycles over %lld passes\n", ms, h[4], h[5], h[8], h[9],
+                 h[6], h[10], h[11], h[7]);
   }
   return HS_OK;
 }

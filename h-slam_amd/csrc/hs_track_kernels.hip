@@ -103,9 +103,12 @@ __device__ __forceinline__ void ldlt8_solve(const double* __restrict__ A, const 
     }
     const double d = M[k][k];
     D[k] = d;
-    // one IEEE division per pivot, then products (Eigen divides every entry: rounding-level only; a single
-    // thread's fp64 division is a ~100-cycle dependent chain, 36 of them were a third of the LM step)
-    Dinv[k] = fabs(d) > DBL_MIN ? 1.0 / d : 0.0;
+    // one reciprocal per pivot, then products (Eigen divides every entry: rounding-level only).  v_rcp_f64 + two
+    // Newton steps (within an ulp of 1 / d) instead of the IEEE division's ~100-cycle dependent sequence
+    double rinv = __builtin_amdgcn_rcp(d);
+    rinv = __builtin_fma(rinv, __builtin_fma(-d, rinv, 1.0), rinv);
+    rinv = __builtin_fma(rinv, __builtin_fma(-d, rinv, 1.0), rinv);
+    Dinv[k] = fabs(d) > DBL_MIN ? rinv : 0.0;
     if (fabs(d) > DBL_MIN) {
 #pragma unroll
       for (int i = k + 1; i < 8; i++) M[i][k] *= Dinv[k];
@@ -144,7 +147,8 @@ struct TrkShared {
   int passes;
   int npass, iters, nchecks;  // this workgroup's pass count (partial parity, counter target), LM iterations, checks
   long long pointPasses;
-  long long prof[6];  // HS_KTRACE: thread-0 cycles: point loop, reductions, LM step, passes, wave reduce, barrier
+  long long prof[8];  // HS_KTRACE: thread-0 cycles: point loop, reductions, LM step, passes, wave reduce, barrier,
+                      // the LM step's LDLT, its exp + product
 };
 
 // Wave reduce-scatter of 64 values (v[i], i < 64) over the 64 lanes: afterwards lane l holds the sum of v[l] over
@@ -518,7 +522,7 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
     S.npass = 0;
     S.passes = 0;
     S.pointPasses = 0;
-    for (int q = 0; q < 6; q++) S.prof[q] = 0;
+    for (int q = 0; q < 8; q++) S.prof[q] = 0;
   }
   __syncthreads();
   bool haveRepeated = false;
@@ -557,6 +561,7 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
 #pragma unroll
         for (int i = 0; i < 8; i++) mb[i] = -S.bs[i];
         ldlt8_solve(S.Hs, mb, inc, 1 + S.lambda);
+        const long long lm1 = a.trace ? clock64() + (long long)(inc[7] * 0.0) : 0;
         float extrapFac = 1;
         if (S.lambda < lambdaExtrapolationLimit) extrapFac = sqrtf(sqrtf(lambdaExtrapolationLimit / S.lambda));
         for (int i = 0; i < 8; i++) inc[i] *= extrapFac;
@@ -575,6 +580,10 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
           // the series exp / rsqrt-normalized product of the BA doStep (hs_se3_dev.h): Sophus' up to rounding
           const hs::SE3 nw = se3_mul_step(se3_exp_step(incScaled), hs::SE3::fromData(S.T));
           nw.toData(S.Tn);
+          if (a.trace) {
+            S.prof[6] += lm1 - lm0;
+            S.prof[7] += clock64() + (long long)(S.Tn[6] * 0.0) - lm1;
+          }
           double nn = 0;
           for (int i = 0; i < 8; i++) nn += inc[i] * inc[i];
           S.incNorm = sqrt(nn);
@@ -657,7 +666,7 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
     out.passes = S.passes;
     out.point_passes = S.pointPasses;
     if (a.trace)
-      for (int q = 0; q < 6; q++) a.trace[(size_t)blockIdx.x * 16 + 4 + q] = S.prof[q];
+      for (int q = 0; q < 8; q++) a.trace[(size_t)blockIdx.x * 16 + 4 + q] = S.prof[q];
   }
   HS_TRACE(a, 15);
 }
