@@ -55,6 +55,15 @@ __device__ __forceinline__ float3 interp33(const float4* __restrict__ img, float
     if ((A).trace && threadIdx.x == 0) (A).trace[(size_t)blockIdx.x * 16 + (slot)] = wall_clock64(); \
   } while (0)
 
+// a double moved between lanes of a row of 16 by one DPP control (quad_perm / row_half_mirror / row_mirror)
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
 // lane l <- lane l-1 within each row of 16 (DPP row_shr:1; a row's lane 0 gets 0)
 __device__ __forceinline__ float dpp_shr1(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xf, 0xf, false));
@@ -2285,10 +2294,12 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
           const double t = __builtin_fma(col[cl * HS_NNS + kk], xs[cl], sacc);
           sacc = c < n ? t : sacc;
         }
-        sacc += __shfl_xor(sacc, 1);
-        sacc += __shfl_xor(sacc, 2);
-        sacc += __shfl_xor(sacc, 4);
-        sacc += __shfl_xor(sacc, 8);
+        // the 16 lanes' butterfly in DPP (no LDS round trip): xor 1, xor 2 (quad_perm), then the 8- and 16-lane
+        // mirrors, which pair the already-equal quads and halves
+        sacc += dpp_f64<0xB1>(sacc);
+        sacc += dpp_f64<0x4E>(sacc);
+        sacc += dpp_f64<0x141>(sacc);
+        sacc += dpp_f64<0x140>(sacc);
         if (part == 0) tk[d] = sacc;
       }
       __syncthreads();
