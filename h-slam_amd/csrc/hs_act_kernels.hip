@@ -192,13 +192,10 @@ __device__ __forceinline__ void bfs_grow_wg(uint8_t* map, int w1, int h1, int*& 
 // addIntoDistFinal's growDistBFS from one cell, run by a single wave: the frontier of a one-seed BFS is at most
 // the ring of its step (<= 8k cells), so one wave walks it with no workgroup barrier.  Lane = frontier entry
 // (8 or 16 per pass) x neighbour direction, so a pass is one straight-line sequence: read entry, probe word, lower,
-// append (ballot + mbcnt, no atomics).  The lists are LDS.
-// claim (LDS map only): one bit per cell.  Every writer of step k stores the same byte k, so the lowering is a
-// plain byte store (no compare-and-swap retries when lanes hit the same word) and the one lane that appends the
-// cell to the next frontier is the one whose ds_or sets its claim bit; a cell's bit is cleared when its entry
-// is expanded (or, for the last frontier, at the end), so every bit is zero between calls.  Without claim: CAS.
+// append (ballot + mbcnt, no atomics).  The lists are LDS.  This form (the map in global memory) lowers by CAS;
+// the LDS map uses bfs_grow_wave_claim below.
 __device__ __forceinline__ void bfs_grow_wave(uint8_t* map, int w1, int h1, int* in, int* out, int n,
-                                              long long* cnt, uint32_t* claim = nullptr) {
+                                              long long* cnt) {
   const int lane = threadIdx.x & 63;
   // growDistBFS's neighbour order: +x, -x, +y, -y, then the diagonals (+1+w1, -1+w1, -1-w1, +1-w1)
   const int sub8 = lane & 7, sub4 = lane & 3;
@@ -231,23 +228,11 @@ __device__ __forceinline__ void bfs_grow_wave(uint8_t* map, int w1, int h1, int*
       uint32_t old = *wp;
       bool want = live & (((old >> sh) & 0xffu) > (uint32_t)k);
       bool got = false;
-      if (claim) {
-        if (valid && (diag ? sub8 : sub4) == 0) {  // the entry is expanded now: its claim bit is released
-          const int qe = (x + w1 * y);
-          atomicAnd(&claim[qe >> 5], ~(1u << (qe & 31)));
-        }
-        if (want) {
-          map[q] = (uint8_t)k;
-          const uint32_t bit = 1u << (q & 31);
-          got = (atomicOr(&claim[q >> 5], bit) & bit) == 0u;
-        }
-      } else {
-        while (want) {
-          const uint32_t pv = atomicCAS(wp, old, (old & ~(0xffu << sh)) | ((uint32_t)k << sh));
-          got = pv == old;
-          old = pv;
-          want = !got & (((old >> sh) & 0xffu) > (uint32_t)k);
-        }
+      while (want) {
+        const uint32_t pv = atomicCAS(wp, old, (old & ~(0xffu << sh)) | ((uint32_t)k << sh));
+        got = pv == old;
+        old = pv;
+        want = !got & (((old >> sh) & 0xffu) > (uint32_t)k);
       }
       const unsigned long long bm = __ballot(got);
       if (got)
@@ -262,15 +247,71 @@ __device__ __forceinline__ void bfs_grow_wave(uint8_t* map, int w1, int h1, int*
     in = out;
     out = t;
   }
-  if (claim) {  // the last frontier is never expanded: release its claims
-    for (int e = lane; e < n; e += 64) {
-      const int xy = in[e];
-      const int qe = (xy & 0xffff) + w1 * (xy >> 16);
-      atomicAnd(&claim[qe >> 5], ~(1u << (qe & 31)));
+}
+
+// bfs_grow_wave for the LDS map with claim bits: every writer of step k stores the same byte k, so the lowering is a
+// plain byte store (no compare-and-swap retries when lanes hit the same word) and the one lane that appends the
+// cell to the next frontier is the one whose ds_or sets its claim bit; a cell's bit is cleared when its entry is
+// expanded (the last frontier's at the end), so every bit is zero between calls.  The pass is branch-free: the
+// lanes that do not lower / clear / append address a dummy word (claim[cwords]) or or / and a no-op mask.
+__device__ __forceinline__ void bfs_grow_wave_claim(uint8_t* map, int w1, int h1, int* in, int* out, int n,
+                                                    long long* cnt, uint32_t* claim, uint32_t* dummy) {
+  const int lane = threadIdx.x & 63;
+  const int sub8 = lane & 7, sub4 = lane & 3;
+  const int dx8 = (sub8 == 0 || sub8 == 4 || sub8 == 7) ? 1 : ((sub8 == 1 || sub8 == 5 || sub8 == 6) ? -1 : 0);
+  const int dy8 = (sub8 == 2 || sub8 == 4 || sub8 == 5) ? 1 : ((sub8 == 3 || sub8 == 6 || sub8 == 7) ? -1 : 0);
+  const int dx4 = sub4 == 0 ? 1 : (sub4 == 1 ? -1 : 0);
+  const int dy4 = sub4 == 2 ? 1 : (sub4 == 3 ? -1 : 0);
+  uint8_t* dummy_byte = reinterpret_cast<uint8_t*>(dummy);
+  int* dummy_int = reinterpret_cast<int*>(dummy);
+  n = __builtin_amdgcn_readfirstlane(n);
+  for (int k = 1; k < HS_ACT_BFS_STEPS && n > 0; k++) {
+    const bool diag = (k & 1) != 0;
+    const int slot = diag ? lane >> 3 : lane >> 2;
+    const int per = diag ? 8 : 16;
+    const int dx = diag ? dx8 : dx4, dy = diag ? dy8 : dy4;
+    const int dxy = dx + dy * 65536;
+    const int doff = dx + dy * w1;
+    const bool lead = (diag ? sub8 : sub4) == 0;  // the lane that releases its entry's claim
+    int m = 0;
+    cnt[0]++;
+    int xyn = in[min(slot, n - 1)];  // the entries of the next pass are read one pass ahead
+    for (int e0 = 0; e0 < n; e0 += per) {
+      cnt[1]++;
+      const int e = e0 + slot;
+      const bool valid = e < n;
+      const int xy = xyn;
+      xyn = in[min(e + per, n - 1)];
+      const int x = xy & 0xffff, y = xy >> 16;
+      const bool live = valid & (x != 0) & (y != 0) & (x != w1 - 1) & (y != h1 - 1);
+      const int base = (int)__umul24((unsigned)y, (unsigned)w1) + x;
+      const int q = live ? base + doff : 0;
+      const uint32_t old = *reinterpret_cast<const uint32_t*>(map + (q & ~3));
+      const bool want = live & (((old >> ((q & 3) * 8)) & 0xffu) > (uint32_t)k);
+      atomicAnd(&claim[base >> 5], (valid & lead) ? ~(1u << (base & 31)) : ~0u);
+      *(want ? map + q : dummy_byte) = (uint8_t)k;
+      const uint32_t bit = want ? 1u << (q & 31) : 0u;
+      const bool got = want & ((atomicOr(&claim[q >> 5], bit) & bit) == 0u);
+      const unsigned long long bm = __ballot(got);
+      *(got ? out + m + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u))
+            : dummy_int) = xy + dxy;
+      m += (int)__popcll(bm);
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    n = __builtin_amdgcn_readfirstlane(m < HS_ACT_WAVE_LIST ? m : HS_ACT_WAVE_LIST);
+    int* t = in;
+    in = out;
+    out = t;
   }
+  // the last frontier is never expanded: release its claims
+  for (int e = lane; e < n; e += 64) {
+    const int xy = in[e];
+    const int qe = (xy & 0xffff) + w1 * (xy >> 16);
+    atomicAnd(&claim[qe >> 5], ~(1u << (qe & 31)));
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
 }
 
 // seeds taken in one round of the greedy loop: at most kMaxSeeds (their BFS frontiers share the wave list:
@@ -281,7 +322,7 @@ constexpr int kSeedSep = 2 * (HS_ACT_BFS_STEPS - 1) + 2;
 // makeDistanceMap's BFS (whole workgroup), then the selection loop (wave 0).  Inlined once per map location so
 // the LDS instance compiles to ds_* instructions.
 __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* map, int* s_n, int* wl0, int* wl1,
-                                           uint32_t* claim = nullptr) {
+                                           uint32_t* claim = nullptr, uint32_t* dummy = nullptr) {
   int* in = a.list_a;
   int* out = a.list_b;
   bfs_grow_wg(map, a.w1, a.h1, in, out, s_n);
@@ -293,24 +334,32 @@ __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* ma
   const int lane = threadIdx.x;
   int nt = 0;
   long long cnt[3] = {0, 0, 0};
-  // candidate batches of 64, the next batch's loads in flight while the current one is processed
+  // candidate batches of 64, the next batch's loads in flight while the current one is processed: every load is
+  // unconditional (clamped index) and nothing tests a loaded value before the next batch, so no wait sits at the
+  // prefetch (a per-entry "pending ? load : 0" made the compiler branch around each load and drain the queue)
   int j = lane;
-  bool npend = j < a.m && a.cand[j] == HS_CAND_PENDING;
-  int ncell = npend ? a.cell[j] : 0;
-  int npt = npend ? (a.order ? a.order[j] : j) : 0;
-  float nfrac = npend ? a.frac[j] : 0.f, nthr = npend ? a.thr[j] : 0.f;
+  unsigned int ncand = 0u;
+  int ncell = 0, npt = 0;
+  float nfrac = 0.f, nthr = 0.f;
+  auto fetch = [&](int jj) {
+    const int jc = max(0, min(jj, a.m - 1));
+    ncand = a.cand[jc];
+    ncell = a.cell[jc];
+    npt = a.order ? a.order[jc] : jc;
+    nfrac = a.frac[jc];
+    nthr = a.thr[jc];
+  };
+  if (a.m > 0) fetch(j);
   for (int base = 0; base < a.m; base += 64) {
-    bool pend = npend;
-    const int cell = ncell;
+    bool pend = (base + lane < a.m) && ncand == HS_CAND_PENDING;
+    const int cell = pend ? ncell : 0;
     const int cidx = xy_index(cell, a.w1);
     const float frac = nfrac, thr = nthr;
     const int pt = npt;
     j = base + 64 + lane;
-    npend = j < a.m && a.cand[j] == HS_CAND_PENDING;
-    ncell = npend ? a.cell[j] : 0;
-    npt = npend ? (a.order ? a.order[j] : j) : 0;
-    nfrac = npend ? a.frac[j] : 0.f;
-    nthr = npend ? a.thr[j] : 0.f;
+    fetch(j);
+    int myslot = -1;  // this lane's place in toopt when it is taken (stored once after the batch: no global store
+                      // inside the round loop, whose completion a later wait would have to drain)
     for (;;) {
       // dist = fwdWarpedIDDistFinal[u + w1 * v] + (ptp[0] - floorf(ptp[0])) >= currentMinActDist * my_type
       const bool acc = pend && (decode(map[cidx]) + frac >= thr);
@@ -351,7 +400,7 @@ __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* ma
       if (mine) {
         pend = false;
         const int rank = (int)__popcll(take & ((1ull << lane) - 1ull));
-        a.toopt[nt + rank] = pt;
+        myslot = nt + rank;
         lower_cell(map, cidx, 0);  // addIntoDistFinal: the cell becomes 0 even when it already was
         wl0[rank] = cell;
       }
@@ -360,9 +409,13 @@ __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* ma
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
       const long long c0 = a.prof ? wall_clock64() : 0;
-      bfs_grow_wave(map, a.w1, a.h1, wl0, wl1, ntake, cnt, claim);
+      if (claim) bfs_grow_wave_claim(map, a.w1, a.h1, wl0, wl1, ntake, cnt, claim, dummy);
+      else bfs_grow_wave(map, a.w1, a.h1, wl0, wl1, ntake, cnt);
       if (a.prof) cnt[2] += wall_clock64() - c0;
     }
+    // one unconditional store per batch (the lanes not taken write their scratch slot toopt[m + lane]), so the
+    // compiler counts it and the next batch waits for its loads only
+    a.toopt[myslot >= 0 ? myslot : a.m + lane] = pt;
   }
   if (a.prof && lane == 0) {
     a.prof[3] = cnt[0];
@@ -383,10 +436,11 @@ __global__ void __launch_bounds__(1024) hs_k_act_select(HsActSelectArgs a) {
   if (a.lds_map) {
     const uint32_t* g = reinterpret_cast<const uint32_t*>(a.dist);
     for (int w = threadIdx.x; w < words; w += blockDim.x) s_map32[w] = g[w];
-    uint32_t* claim = s_map32 + words;  // one bit per cell, zero between the BFS calls
-    for (int w = threadIdx.x; w < (a.w1 * a.h1 + 31) / 32; w += blockDim.x) claim[w] = 0u;
+    uint32_t* claim = s_map32 + words;  // one bit per cell, zero between the BFS calls; then one dummy word
+    const int cwords = (a.w1 * a.h1 + 31) / 32;
+    for (int w = threadIdx.x; w <= cwords; w += blockDim.x) claim[w] = 0u;
     __syncthreads();
-    nt = select_body(a, reinterpret_cast<uint8_t*>(s_map32), s_n, s_wl[0], s_wl[1], claim);
+    nt = select_body(a, reinterpret_cast<uint8_t*>(s_map32), s_n, s_wl[0], s_wl[1], claim, claim + cwords);
     if (threadIdx.x >= 64) return;
     uint32_t* go = reinterpret_cast<uint32_t*>(a.dist);
     for (int w = threadIdx.x; w < words; w += 64) go[w] = s_map32[w];

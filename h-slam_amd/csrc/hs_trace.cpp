@@ -389,7 +389,7 @@ static int act_alloc(hs_tracer* t) {
   TR_HIP(hipMalloc((void**)&t->d_frame_of_slot, sizeof(int) * HS_TRC_MAXHOST));
   TR_HIP(hipMalloc((void**)&t->d_order, sizeof(int) * c));
   TR_HIP(hipMalloc((void**)&t->d_cell, sizeof(int) * c));
-  TR_HIP(hipMalloc((void**)&t->d_toopt, sizeof(int) * c));
+  TR_HIP(hipMalloc((void**)&t->d_toopt, sizeof(int) * (c + 64)));  // + the greedy loop's 64 scratch slots
   TR_HIP(hipMalloc((void**)&t->d_cand, c));
   TR_HIP(hipMalloc((void**)&t->d_action, c));
   TR_HIP(hipMalloc((void**)&t->d_res_in, c));
@@ -529,7 +529,7 @@ int hs_tracer_activate(hs_tracer* t, const float K4[4], int nF, const hs_act_fra
   se.w1 = t->w1;
   se.h1 = t->h1;
   const size_t map_bytes = (size_t)((wh1 + 3) & ~3);
-  const size_t claim_bytes = (size_t)((wh1 + 31) / 32) * 4;  // the greedy BFS's claim bits (hs_act_kernels.hip)
+  const size_t claim_bytes = (size_t)((wh1 + 31) / 32 + 1) * 4;  // the greedy BFS's claim bits + a dummy word
   se.lds_map = map_bytes + claim_bytes <= HS_ACT_LDS_MAP_MAX ? 1 : 0;
   se.order = order ? t->d_order : nullptr;
   se.cand = t->d_cand;

@@ -108,7 +108,7 @@ struct HsActSelectArgs {
   int* list_a;               // [w1*h1] frontier lists
   int* list_b;
   const int* seed_count;
-  int* toopt;                // [m] points to optimize, in order
+  int* toopt;                // [m] points to optimize, in order (+ 64 scratch slots after m)
   int* n_toopt;
   long long* prof;           // nullable: wall_clock64 at entry, after the seed BFS, at exit (HS_ACT_PROF=1)
 };
