@@ -910,6 +910,7 @@ void hs_destroy(hs_ctx* c) {
   if (c->h_state) (void)hipHostFree(c->h_state);
   if (c->h_ctl) (void)hipHostFree(c->h_ctl);
   if (c->h_res) (void)hipHostFree(c->h_res);
+  if (c->h_rb) (void)hipHostFree(c->h_rb);
   if (c->h_fstage) (void)hipHostFree(c->h_fstage);
   if (c->ev_upload) (void)hipEventDestroy(c->ev_upload);
   if (c->ev_ready) (void)hipEventDestroy(c->ev_ready);
@@ -1199,9 +1200,20 @@ int hs_ba_fix_linearization(hs_ctx* c, double* energy_out, uint8_t* drop_out, fl
     return fail(HS_ERR_INVALID, "maxRelBaseline and numGoodResiduals go together");
   HS_HIP(hipSetDevice(c->device));
   const int nF = c->nF, nP = c->nP;
+  // pinned staging of the read-backs: HdiF [nP] floats, then the active flags [nP][8]; one sync for all of them
+  const size_t rb_need = sizeof(float) * (size_t)nP + (size_t)nP * 8;
+  if (rb_need > c->h_rb_cap) {
+    if (c->h_rb) (void)hipHostFree(c->h_rb);
+    c->h_rb = nullptr;
+    c->h_rb_cap = 0;
+    HS_HIP(hipHostMalloc((void**)&c->h_rb, rb_need));
+    c->h_rb_cap = rb_need;
+  }
+  float* h_hdif = reinterpret_cast<float*>(c->h_rb);
+  unsigned char* h_act = c->h_rb + sizeof(float) * (size_t)nP;
   // HdiF of the last solve, before this pass relinearizes
   if (HdiF_out && nP > 0)
-    HS_HIP(hipMemcpyAsync(HdiF_out, c->hdif_solved, sizeof(float) * nP, hipMemcpyDeviceToHost, c->stream));
+    HS_HIP(hipMemcpyAsync(h_hdif, c->hdif_solved, sizeof(float) * nP, hipMemcpyDeviceToHost, c->stream));
   HS_TRY(fetch_state(c));
   HsDevState& S = *c->h_state;
   {  // newStateZero = 0 except segment(6, 2) = the newest frame's a / b; setEvalPT(PRE_worldToCam, newStateZero)
@@ -1229,14 +1241,15 @@ int hs_ba_fix_linearization(hs_ctx* c, double* energy_out, uint8_t* drop_out, fl
     HS_HIP(hipMemcpyAsync(maxRelBaseline, c->d_fix_relBL, sizeof(float) * nP, hipMemcpyDeviceToHost, c->stream));
     HS_HIP(hipMemcpyAsync(numGoodResiduals, c->d_fix_nGood, sizeof(int) * nP, hipMemcpyDeviceToHost, c->stream));
   }
+  const bool want_drop = drop_out && c->nR > 0;
+  if (want_drop)
+    HS_HIP(hipMemcpyAsync(h_act, c->d_r_active, (size_t)nP * 8, hipMemcpyDeviceToHost, c->stream));
   HS_HIP(hipStreamSynchronize(c->stream));
   std::memcpy(&e, &c->h_ctl[4], sizeof(double));
   if (energy_out) *energy_out = e;
-  if (drop_out && c->nR > 0) {  // toRemove: every residual not active after applyRes(true)
-    std::vector<uint8_t> act((size_t)nP * 8);
-    HS_HIP(hipMemcpy(act.data(), c->d_r_active, act.size(), hipMemcpyDeviceToHost));
-    for (int r = 0; r < c->nR; r++) drop_out[r] = act[(size_t)c->res_point[r] * 8 + c->res_target[r]] ? 0 : 1;
-  }
+  if (HdiF_out && nP > 0) std::memcpy(HdiF_out, h_hdif, sizeof(float) * nP);
+  if (want_drop)  // toRemove: every residual not active after applyRes(true)
+    for (int r = 0; r < c->nR; r++) drop_out[r] = h_act[(size_t)c->res_point[r] * 8 + c->res_target[r]] ? 0 : 1;
   if (!std::isfinite(e)) return fail(HS_ERR_NONFINITE, "non-finite energy (isLost)");
   return HS_OK;
 }

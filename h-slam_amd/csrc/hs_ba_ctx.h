@@ -230,6 +230,9 @@ struct hs_ctx {
   // the GN loop call's counters, reset by its first solve launch (reset_it; -1: none pending), and its results,
   // written by hs_k_result into pinned host memory [kLogCap + 2] (one zero-copy write instead of three copies)
   int pending_reset = -1;
+  // pinned staging of per-point / per-slot read-backs (hs_ba_fix_linearization), grown on demand
+  unsigned char* h_rb = nullptr;
+  size_t h_rb_cap = 0;
   double* h_res = nullptr;
   double* d_res = nullptr;  // the device view of h_res
 
