@@ -1201,14 +1201,7 @@ int hs_ba_fix_linearization(hs_ctx* c, double* energy_out, uint8_t* drop_out, fl
   HS_HIP(hipSetDevice(c->device));
   const int nF = c->nF, nP = c->nP;
   // pinned staging of the read-backs: HdiF [nP] floats, then the active flags [nP][8]; one sync for all of them
-  const size_t rb_need = sizeof(float) * (size_t)nP + (size_t)nP * 8;
-  if (rb_need > c->h_rb_cap) {
-    if (c->h_rb) (void)hipHostFree(c->h_rb);
-    c->h_rb = nullptr;
-    c->h_rb_cap = 0;
-    HS_HIP(hipHostMalloc((void**)&c->h_rb, rb_need));
-    c->h_rb_cap = rb_need;
-  }
+  HS_HIP(c->rb_stage(sizeof(float) * (size_t)nP + (size_t)nP * 8));
   float* h_hdif = reinterpret_cast<float*>(c->h_rb);
   unsigned char* h_act = c->h_rb + sizeof(float) * (size_t)nP;
   // HdiF of the last solve, before this pass relinearizes

@@ -230,9 +230,19 @@ struct hs_ctx {
   // the GN loop call's counters, reset by its first solve launch (reset_it; -1: none pending), and its results,
   // written by hs_k_result into pinned host memory [kLogCap + 2] (one zero-copy write instead of three copies)
   int pending_reset = -1;
-  // pinned staging of per-point / per-slot read-backs (hs_ba_fix_linearization), grown on demand
+  // pinned staging of per-point / per-slot read-backs (hs_ba_fix_linearization, hs_ba_get_point_state), grown on
+  // demand (rb_stage)
   unsigned char* h_rb = nullptr;
   size_t h_rb_cap = 0;
+  hipError_t rb_stage(size_t bytes) {
+    if (bytes <= h_rb_cap) return hipSuccess;
+    if (h_rb) (void)hipHostFree(h_rb);
+    h_rb = nullptr;
+    h_rb_cap = 0;
+    const hipError_t e = hipHostMalloc((void**)&h_rb, bytes);
+    if (e == hipSuccess) h_rb_cap = bytes;
+    return e;
+  }
   double* h_res = nullptr;
   double* d_res = nullptr;  // the device view of h_res
 

@@ -676,12 +676,15 @@ int hs_ba_get_point_state(hs_ctx* c, float* idepth, float* idepth_zero, float* r
   HS_TRY(commit_if_dirty(c));
   const size_t n = c->nP;
   if (n == 0) return HS_OK;
-  if (idepth) HS_HIP(hipMemcpyAsync(idepth, c->d_idepth, n * 4, hipMemcpyDeviceToHost, c->stream));
-  if (idepth_zero) HS_HIP(hipMemcpyAsync(idepth_zero, c->d_idepth_zero, n * 4, hipMemcpyDeviceToHost, c->stream));
-  if (relBL) HS_HIP(hipMemcpyAsync(relBL, c->d_fix_relBL, n * 4, hipMemcpyDeviceToHost, c->stream));
-  if (nGood) HS_HIP(hipMemcpyAsync(nGood, c->d_fix_nGood, n * 4, hipMemcpyDeviceToHost, c->stream));
-  if (HdiF) HS_HIP(hipMemcpyAsync(HdiF, c->hdif_solved, n * 4, hipMemcpyDeviceToHost, c->stream));
+  // through the context's pinned staging: asynchronous copies, one sync, then host copies
+  HS_HIP(c->rb_stage(5 * n * 4));
+  void* dst[5] = {idepth, idepth_zero, relBL, nGood, HdiF};
+  const void* src[5] = {c->d_idepth, c->d_idepth_zero, c->d_fix_relBL, c->d_fix_nGood, c->hdif_solved};
+  for (int k = 0; k < 5; k++)
+    if (dst[k]) HS_HIP(hipMemcpyAsync(c->h_rb + k * n * 4, src[k], n * 4, hipMemcpyDeviceToHost, c->stream));
   HS_HIP(hipStreamSynchronize(c->stream));
+  for (int k = 0; k < 5; k++)
+    if (dst[k]) std::memcpy(dst[k], c->h_rb + k * n * 4, n * 4);
   return HS_OK;
 }
 
