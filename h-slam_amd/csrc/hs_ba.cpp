@@ -1468,8 +1468,14 @@ int hs_ba_marginalize_points(hs_ctx* c, int n, const int* points, double* HM_out
       }
     }
   for (int i = 0; i < 4; i++) c->cDelta[i] = (float)S.calib.value_minus_value_zero[i];
-  if (c->nP > 0) HS_HIP(hipMemcpy(c->d_marg, flag.data(), c->nP, hipMemcpyHostToDevice));
-  HS_HIP(hipMemcpy(c->d_adHTdelta, adHTd.data(), sizeof(float) * adHTd.size(), hipMemcpyHostToDevice));
+  {  // both uploads through the pinned staging, asynchronous (the stream sync below precedes any reuse of it)
+    const size_t off = ((size_t)c->nP + 15) & ~(size_t)15, ab = sizeof(float) * adHTd.size();
+    HS_HIP(c->rb_stage(off + ab));
+    std::memcpy(c->h_rb, flag.data(), (size_t)c->nP);
+    std::memcpy(c->h_rb + off, adHTd.data(), ab);
+    if (c->nP > 0) HS_HIP(hipMemcpyAsync(c->d_marg, c->h_rb, c->nP, hipMemcpyHostToDevice, c->stream));
+    HS_HIP(hipMemcpyAsync(c->d_adHTdelta, c->h_rb + off, ab, hipMemcpyHostToDevice, c->stream));
+  }
   // the pass; setNewFrameEnergyTH is not part of it
   HS_TRY(launch_linearize(c, 0, true));
   HS_TRY(launch_reduce(c, true, true));
