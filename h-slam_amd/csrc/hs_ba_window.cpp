@@ -523,9 +523,11 @@ int hs_ba_drop_inactive_residuals(hs_ctx* c, int* n_dropped) {
   HS_TRY(ensure_incremental(c));
   if (c->dirty) return fail(HS_ERR_STATE, "the window changed since hs_ba_fix_linearization");
   if (!c->tail_valid) return fail(HS_ERR_STATE, "hs_ba_fix_linearization must run first");
-  std::vector<uint8_t> act((size_t)c->nP * 8);
+  // the tail's active flags through the context's pinned staging (a pageable copy is a synchronous staged one)
+  HS_HIP(c->rb_stage((size_t)std::max(c->nP, 1) * 8));
+  const uint8_t* act = c->h_rb;
   if (c->nP > 0) {
-    HS_HIP(hipMemcpyAsync(act.data(), c->d_r_active, act.size(), hipMemcpyDeviceToHost, c->stream));
+    HS_HIP(hipMemcpyAsync(c->h_rb, c->d_r_active, (size_t)c->nP * 8, hipMemcpyDeviceToHost, c->stream));
     HS_HIP(hipStreamSynchronize(c->stream));
   }
   // toRemove in activeResiduals order (points in window order, each list in order), then dropResidual one by one
