@@ -480,53 +480,70 @@ def bench_keyframe(args):
     return res
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=("ba", "ba-kitti", "keyframe", "trace", "track", "act", "refine", "select"),
-                    default="ba",
-                    help="ba = the headline metric (C4, 640x480); ba-kitti = C5's BA half (KITTI 1232x368, 5 levels); "
-                         "trace = C5 traceOn; track = C2 CoarseTracker; act = point activation; refine = initializer "
-                         "DirectRefinement; select = PixelSelector; keyframe = AddKeyframe's BA part per keyframe")
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--points", type=int, default=2000,
-                    help="active points of the window (strong scaling) or per GPU (--scaling weak)")
-    ap.add_argument("--scaling", choices=("strong", "weak"), default="weak",
-                    help="weak (default): --points per GPU, one window of --points x N points; strong: the "
-                         "metric's own 8 KF x --points window sharded over the GPUs")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--phase-events", type=int, default=None, choices=(0, 1, 2),
-                    help="HIP event pairs inside the timed GN loop (sets HS_EVENT_TIMING; default: the environment's "
-                         "value, else 0 = none; each pair adds ~2 us per step), 1 linearize only, 2 every phase")
-    args = ap.parse_args()
-    if args.workload not in ("ba", "ba-kitti"):
-        res = {"trace": bench_trace, "track": bench_track, "act": bench_act, "refine": bench_refine,
-               "select": bench_select, "keyframe": bench_keyframe}[args.workload](args)
-        print(json.dumps(res))
-        return
+def launch_ranks(n: int, argv, plumbing: bool = False) -> int:
+    """`--gpus N` without a launcher (WORLD_SIZE unset): N child rank processes, one per GPU, with the
+    torch.distributed.run environment (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT).  This
+    process never touches the GPU (children are started, nothing is exec'd); it counts devices without initialising
+    HIP and fails loudly when there are fewer than N.  Returns the first failing child's exit code (the others are
+    then stopped by PID), else 0.  Rank 0 prints the JSON line."""
+    import socket
+    import subprocess
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
+    if not plumbing:
         import torch
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        ndev = torch.cuda.device_count()  # does not initialise HIP on this image
+        if ndev < n:
+            print(f"bench.py: --gpus {n} needs {n} visible GPUs, this node has {ndev}", file=sys.stderr)
+            return 2
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the other ranks", file=sys.stderr)
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
 
-    # the timed loop carries no instrumentation unless asked: the roofline's launch duration comes from
-    # hs_ba_time_linearize's back-to-back launches, the phase split from rocprof or --phase-events
-    if args.phase_events is not None:
-        os.environ["HS_EVENT_TIMING"] = str(args.phase_events)
-    args.phase_events = int(os.environ.get("HS_EVENT_TIMING", "0") or 0)
+
+def plumbing_rank(args, world, rank, local):
+    """--plumbing-check (CPU test of the launcher): every rank joins a gloo group with the launcher's environment,
+    all-reduces (rank + 1) and reports what it saw; no GPU, no library."""
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    t = torch.tensor([float(rank + 1)])
+    dist.all_reduce(t)
+    n = dist.get_world_size()
+    pts = [len(range(r, args.points, world)) for r in range(world)]  # the strong shard sizes (p % N == rank)
+    if rank == 0:
+        print(json.dumps({"plumbing": True, "world": world, "group_size": n, "allreduce": float(t.item()),
+                          "gpus_flag": args.gpus, "strong_shard_points": pts}))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def run_window(args, n_window, kitti, world, rank, local, dist):
+    """Builds the 8-KF window of n_window points, loads this rank's shard (points p % world == rank), runs W warm-up
+    and then K timed GN iterations between barriers; returns the timing (max over ranks) and the live BAWindow."""
     from hslam_amd.ba import BAWindow
     from hslam_amd.scene import make_ba_scene, make_ba_scene_kitti
 
-    kitti = args.workload == "ba-kitti"
-    n_window = args.points * world if args.scaling == "weak" else args.points
     scene = make_ba_scene_kitti(n_window) if kitti else make_ba_scene(n_points=n_window)
     shard = scene.shard(rank, world) if world > 1 else scene
     comm = None
@@ -535,6 +552,10 @@ def main():
         dist.broadcast_object_list(uid, src=0)
         comm = (uid[0], rank, world)
     ba = BAWindow(shard, device=local if world > 1 else 0, comm=comm)
+    ranks, my_rank = ba.comm_size()
+    if ranks != world or my_rank != rank:
+        raise SystemExit(f"bench.py: the RCCL communicator holds {ranks} ranks (this one {my_rank}), "
+                         f"the launcher started {world} (this one {rank})")
     ba.linearizeAll(reset=True)
     if args.warmup > 0:
         ba.iterate(0, args.warmup)
@@ -560,10 +581,95 @@ def main():
         nr = torch.tensor([shard.n_res], dtype=torch.int64, device="cuda")
         dist.all_reduce(nr)
         n_res_total = int(nr.item())
+    return dict(ba=ba, shard=shard, dt=dt, n_res_total=n_res_total, n_window=n_window, ranks=ranks,
+                value=n_res_total * args.steps / dt, ms_per_step=dt * 1e3 / args.steps)
+
+
+def phase_split(ba, first, steps):
+    """Per-phase device time of the GN step, from HIP event pairs around each launch group of an extra, untimed loop
+    of `steps` iterations (after the timed loop: the event records add ~1-2 us per pair, so the timed loop carries
+    none).  solve = hs_k_solve (solve + step + precalc); linearize = the linearize kernel; accumulate_stitch =
+    hs_k_reduce + hs_k_stitch (+ the RCCL exchange on N > 1)."""
+    ba.set_event_timing(2)
+    ba.iterate(first, steps)
+    ba.set_event_timing(0)
+    t = ba.timings()
+    n = max(1, t["timed_iters"])
+    return {"solve_step_kernel": t["solve_ms"] / n, "linearize_kernel": t["linearize_ms"] / n,
+            "accumulate_stitch": t["acc_stitch_ms"] / n, "event_timed_steps": t["timed_iters"],
+            "timing": "HIP event pairs per launch group in an untimed loop after the timed one"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", choices=("ba", "ba-kitti", "keyframe", "trace", "track", "act", "refine", "select"),
+                    default="ba",
+                    help="ba = the headline metric (C4, 640x480); ba-kitti = C5's BA half (KITTI 1232x368, 5 levels); "
+                         "trace = C5 traceOn; track = C2 CoarseTracker; act = point activation; refine = initializer "
+                         "DirectRefinement; select = PixelSelector; keyframe = AddKeyframe's BA part per keyframe")
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU): without a launcher's WORLD_SIZE, bench.py starts the N rank processes "
+                         "itself; under torch.distributed.run WORLD_SIZE must equal N")
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--points", type=int, default=2000,
+                    help="active points of the window (strong scaling) or per GPU (--scaling weak)")
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
+                    help="strong (default): `value` is the metric's own 8 KF x --points window sharded over the N "
+                         "GPUs; weak: --points per GPU (a window of --points x N).  The other one is measured too "
+                         "(N > 1) and reported beside it")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--phase-events", type=int, default=None, choices=(0, 1, 2),
+                    help="HIP event pairs inside the timed GN loop (sets HS_EVENT_TIMING; default: the environment's "
+                         "value, else 0 = none; each pair adds ~2 us per step), 1 linearize only, 2 every phase")
+    ap.add_argument("--no-phase-split", action="store_true", help="skip the untimed event-timed phase-split loop")
+    ap.add_argument("--plumbing-check", action="store_true", help=argparse.SUPPRESS)
+    args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if args.workload not in ("ba", "ba-kitti"):
+        if args.gpus != 1:
+            raise SystemExit(f"bench.py: --workload {args.workload} is single-GPU (replicas only); --gpus {args.gpus}")
+        res = {"trace": bench_trace, "track": bench_track, "act": bench_act, "refine": bench_refine,
+               "select": bench_select, "keyframe": bench_keyframe}[args.workload](args)
+        print(json.dumps(res))
+        return
+
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], plumbing=args.plumbing_check))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} from the launcher but --gpus {args.gpus}")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.plumbing_check:
+        plumbing_rank(args, world, rank, local)
+        return
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    # the timed loop carries no instrumentation unless asked: the roofline's launch duration comes from
+    # hs_ba_time_linearize's back-to-back launches, the phase split from an untimed event-timed loop afterwards
+    if args.phase_events is not None:
+        os.environ["HS_EVENT_TIMING"] = str(args.phase_events)
+    args.phase_events = int(os.environ.get("HS_EVENT_TIMING", "0") or 0)
+
+    kitti = args.workload == "ba-kitti"
+    n_window = args.points * world if args.scaling == "weak" else args.points
+    run = run_window(args, n_window, kitti, world, rank, local, dist)
+    ba, shard = run["ba"], run["shard"]
     tim = ba.timings()
     nt = max(1, tim["timed_iters"])
     # per-launch event pairs inside the GN loop (+~3 us event overhead); None without --phase-events
     lin_loop_ms = tim["linearize_ms"] / nt if tim["timed_iters"] > 0 else None
+    # continues the timed loop's GN iterations (collective on N > 1: every rank runs it)
+    split = None if args.no_phase_split else phase_split(ba, args.warmup + args.steps, min(max(args.steps, 20), 100))
     # the same kernel, same inputs, launched back to back between one event pair: the launch duration
     # rocprofv3 reports (the in-loop pairs add the event-record overhead to a ~9 us kernel)
     lin_ms = ba.time_linearize(max(64, args.steps))
@@ -571,6 +677,14 @@ def main():
     lin_kernel = ba.partition()["kernel"]  # hs_k_lin (one point per wave) or hs_k_lin8 (8 points per wave)
     traffic, traffic_src = (pmc_traffic(f"kitti{args.points}" if kitti else args.points, lin_kernel) if world == 1
                             else (None, None))
+    ba.close()
+    other = None
+    if world > 1:  # the other scaling mode, same ranks and communicator set-up, reported beside `value`
+        mode = "weak" if args.scaling == "strong" else "strong"
+        o = run_window(args, args.points * world if mode == "weak" else args.points, kitti, world, rank, local, dist)
+        other = {"scaling": mode, "value": o["value"], "ms_per_step": o["ms_per_step"], "points": o["n_window"],
+                 "points_per_gpu_rank0": o["shard"].n_points, "point_residuals": o["n_res_total"]}
+        o["ba"].close()
     if kitti:
         wl = ("C5 BA half (BASELINE.json configs[4]): full windowed photometric BA incl. Schur complement, 8 KF x "
               f"{n_window} pts, KITTI 1232x368, 5 pyramid levels")
@@ -581,12 +695,12 @@ def main():
            "solve+step+linearize+accumulate (fp32 residuals, fp64 stitch/solve)")
     result = {
         "metric": METRIC,
-        "value": n_res_total * args.steps / dt,
+        "value": run["value"],
         "unit": "point-residuals/s",
-        "n_gpus": world,
+        "n_gpus": run["ranks"],
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": dt * 1e3 / args.steps,
+        "ms_per_step": run["ms_per_step"],
         "higher_is_better": True,
         "scaling": args.scaling,
         "vs_baseline": None,
@@ -597,8 +711,11 @@ def main():
             "frames": shard.n_frames,
             "points": n_window,
             "points_per_gpu": shard.n_points,
-            "point_residuals": n_res_total,
-            "parallelism": f"point-shard x{world}",
+            "point_residuals": run["n_res_total"],
+            "parallelism": f"point-shard x{world}" + (" (one RCCL all-gather group call per GN step)" if world > 1
+                                                     else ""),
+            "launcher": "bench.py child ranks" if env_world is None and world > 1 else (
+                "torch.distributed.run" if world > 1 else "single process"),
         },
         "roofline": {
             "bound": "hbm",
@@ -615,22 +732,22 @@ def main():
             "avg_launch_ms_in_loop_events": lin_loop_ms,
             "timing": f"HIP events on the context stream around back-to-back {lin_kernel} launches (fused "
                       "linearize + applyRes + top / Schur accumulation into block partials)",
+            "binding_roof": "latency (one point per wave at 2k; the step is a chain of 4 dependent launches, the "
+                            "single-workgroup fp64 solve the longest)" if shard.n_points < 60000 else
+                            "VALU issue + gather latency at occupancy 2 (DESIGN.md §9)",
         },
-        "phase_ms_per_step": {  # per-phase split: --phase-events 2 (1 times the linearize kernel only)
-            "solve_step_kernel": tim["solve_ms"] / nt if args.phase_events >= 2 else None,
-            "linearize_kernel": lin_loop_ms,
-            "accumulate_stitch": tim["acc_stitch_ms"] / nt if args.phase_events >= 2 else None,
-            "event_timed_steps": tim["timed_iters"],
-        },
+        "phase_ms_per_step": split,
         "cpu_baseline": None,
     }
+    if other is not None:
+        result[f"{other['scaling']}_scaling"] = other
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(n_window, args.cpu_seconds, kitti)
         result["speedup_vs_cpu"] = result["value"] / result["cpu_baseline"]["value"]
-    ba.close()
     if rank == 0:
         print(json.dumps(result))
     if dist is not None:
+        dist.barrier()
         dist.destroy_process_group()
 
 

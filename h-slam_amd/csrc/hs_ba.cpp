@@ -1418,6 +1418,19 @@ int hs_ba_get_frames(hs_ctx* c, double* state, float* energyTH, double* pose7, d
   return HS_OK;
 }
 
+int hs_ba_get_frame_eval(hs_ctx* c, double* evalPT7, double* state_zero) {
+  HS_TRY(begin_call(c));
+  HS_HIP(hipSetDevice(c->device));
+  HS_TRY(fetch_state(c));
+  const HsDevState& S = *c->h_state;
+  for (int i = 0; i < c->nF; i++) {
+    if (evalPT7) S.frames[i].evalPT.toData(evalPT7 + 7 * i);
+    if (state_zero)
+      for (int k = 0; k < 10; k++) state_zero[i * 10 + k] = S.frames[i].state_zero[k];
+  }
+  return HS_OK;
+}
+
 int hs_ba_set_marginal_prior(hs_ctx* c, const double* HM, const double* bM) {
   HS_TRY(begin_call(c));
   if (!HM || !bM) return fail(HS_ERR_INVALID, "null HM / bM");
@@ -1614,6 +1627,12 @@ int hs_ba_get_timings(hs_ctx* c, double* out6) {
   return HS_OK;
 }
 
+int hs_ba_set_event_timing(hs_ctx* c, int mode) {
+  if (!c || mode < 0 || mode > 2) return fail(HS_ERR_INVALID, "bad event-timing mode");
+  c->events = mode;
+  return HS_OK;
+}
+
 int hs_ba_get_partition(hs_ctx* c, int* out4) {
   if (!c || !out4) return fail(HS_ERR_INVALID, "null");
   out4[0] = c->lin8 ? 1 : 0;
@@ -1733,6 +1752,18 @@ int hs_comm_init(hs_ctx* c, const char* id128, int rank, int nranks) {
   HS_NCCL(ncclCommInitRank(&c->comm, nranks, id, rank));
   c->rank = rank;
   c->nranks = nranks;
+  return HS_OK;
+}
+
+int hs_comm_size(hs_ctx* c, int* nranks, int* rank) {
+  if (!c || !nranks || !rank) return fail(HS_ERR_INVALID, "null");
+  if (!c->comm) {
+    *nranks = 1;
+    *rank = 0;
+    return HS_OK;
+  }
+  HS_NCCL(ncclCommCount(c->comm, nranks));
+  HS_NCCL(ncclCommUserRank(c->comm, rank));
   return HS_OK;
 }
 

@@ -423,6 +423,9 @@ int hs_ba_set_frame_image_device(hs_ctx* c, int frame, const void* d_texels) {
   if (!d_texels) return fail(HS_ERR_INVALID, "null texels");
   HS_TRY(frame_slot_ptr(c, frame, &dst));
   HS_HIP(hipMemcpyAsync(dst, d_texels, c->img_px * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
+  // the source belongs to another context (the tracker's d_new, rewritten on the tracker's stream by its next
+  // set_frame): the copy must have read it before this call returns, or the producer's next write races it
+  HS_HIP(hipStreamSynchronize(c->stream));
   return HS_OK;
 }
 

@@ -104,6 +104,9 @@ SIGNATURES = {
     "hs_debug_set_state": ([VP, VP], I),
     "hs_comm_get_unique_id": ([VP], I),
     "hs_comm_init": ([VP, VP, I, I], I),
+    "hs_comm_size": ([VP, VP, VP], I),
+    "hs_ba_set_event_timing": ([VP, I], I),
+    "hs_ba_get_frame_eval": ([VP, VP, VP], I),
     # test hooks (not in the header): an in-process rank group on one device, the multi-rank exchange by copies
     "hs_ba_debug_group": ([VP, I, I], I),
     "hs_ba_group_linearize": ([VP, I, I, VP], I),

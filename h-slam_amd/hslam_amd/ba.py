@@ -207,6 +207,13 @@ class BAWindow:
         o["res_point"] = np.repeat(np.arange(self.n_points, dtype=np.int32), o["nres"])
         return o
 
+    def frame_eval(self):
+        """dict(evalPT [nF][7], state_zero [nF][10]): each frame's linearization point."""
+        self._sync()
+        ev, sz = np.zeros((self.nF, 7)), np.zeros((self.nF, 10))
+        check(self.lib.hs_ba_get_frame_eval(self.h, ptr(ev), ptr(sz)))
+        return dict(evalPT=ev, state_zero=sz)
+
     def marginal_prior(self):
         self._sync()
         HM, bM = np.zeros((self.dim, self.dim)), np.zeros(self.dim)
@@ -413,6 +420,10 @@ class BAWindow:
         return dict(linearize_ms=t[0], acc_stitch_ms=t[1], solve_ms=t[2], timed_iters=int(t[3]), wall_ms=t[4],
                     iters=int(t[5]))
 
+    def set_event_timing(self, mode: int):
+        """HIP event pairs in later GN loops: 0 none, 1 the linearize kernel, 2 every phase (measurement only)."""
+        check(self.lib.hs_ba_set_event_timing(self.h, int(mode)))
+
     def partition(self):
         """The linearize partitioning: dict(kernel='hs_k_lin' | 'hs_k_lin8', blocks, waves, exact)."""
         o = np.zeros(4, np.int32)
@@ -435,6 +446,12 @@ class BAWindow:
     def comm_init(self, uid: bytes, rank: int, nranks: int):
         buf = C.create_string_buffer(uid, 128)
         check(self.lib.hs_comm_init(self.h, buf, rank, nranks))
+
+    def comm_size(self):
+        """(ranks the communicator holds, this context's rank) — from RCCL itself (ncclCommCount); (1, 0) without one."""
+        n, r = C.c_int(), C.c_int()
+        check(self.lib.hs_comm_size(self.h, C.byref(n), C.byref(r)))
+        return n.value, r.value
 
 
 class RankGroup:

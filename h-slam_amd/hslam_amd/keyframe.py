@@ -209,8 +209,10 @@ class KeyframeBA:
         self.ba.makeIDX()
 
     def add_keyframe(self, k, marginalize=True, check=None):
-        """AddKeyframe(k)'s BA part.  check(driver, phase) is called at 'optimize' (before it) and 'tail' (after the
-        tail, before its drops): parity tests rebuild the window there.  Returns dict of per-phase seconds."""
+        """AddKeyframe(k)'s BA part.  check(driver, phase) is called at 'optimize' (before it), 'tail' (after the
+        tail, before its drops), and with marginalization at 'marginalize' (before marginalizePointsF of
+        self.marg_points), 'points_marginalized' (after it) and 'frame_marginalized' (after marginalizeFrame of
+        self.marg_frame): parity tests rebuild the window there.  Returns dict of per-phase seconds."""
         ba, timer = self.ba, _Timer()
         wall0 = time.perf_counter()
         # insertFrame, new residuals of the old points, activation of the previous newest KF's points
@@ -225,7 +227,7 @@ class KeyframeBA:
             check(self, "optimize")
         # optimize + tail
         n_it, energies = timer.run("optimize", ba.optimize, self.iters)
-        tail = timer.run("tail", ba.fixLinearization)
+        tail = self.last_tail = timer.run("tail", ba.fixLinearization)
         if check:
             check(self, "tail")
         # lastResiduals[.].second from the tail's states (System::linearizeAll(true), Src/FullSystemOptimize.cpp:128)
@@ -274,8 +276,13 @@ class KeyframeBA:
             marg = flag & ~drop_now & inl & (idepth_h > MIN_IDEPTH_H_MARG)
             drop = drop_now | (flag & ~marg)
             mpos = np.nonzero(marg)[0].astype(np.int32)
+            self.marg_points, self.marg_frame = mpos, marg_f
+            if check:
+                check(self, "marginalize")  # before marginalizePointsF: the window as the tail and drops left it
             if len(mpos):
                 timer.run("post", ba.marginalizePointsF, mpos)
+            if check:
+                check(self, "points_marginalized")
             rm = hd_all[marg | drop]
             timer.run("post", ba.removePoints, rm)
             for hd in rm:
@@ -283,6 +290,8 @@ class KeyframeBA:
                 self.last_state.pop(int(hd), None)
             timer.run("post", ba.removeFrame, marg_f, True)
             self.frames.pop(marg_f)
+            if check:
+                check(self, "frame_marginalized")
             info.update(marginalized_points=int(marg.sum()), dropped=int(drop.sum()))
         timer.run("post", ba.synchronize)
         info["wall_s"] = time.perf_counter() - wall0

@@ -115,6 +115,10 @@ int hs_ba_get_residuals(hs_ctx* ctx, uint8_t* state, uint8_t* active, float* ene
 int hs_ba_get_points(hs_ctx* ctx, float* idepth, float* step, float* HdiF, float* bdSumF);
 /* per-frame: state[nF][10], frameEnergyTH[nF], PRE_worldToCam[nF][7]; calib value[4] (all nullable) */
 int hs_ba_get_frames(hs_ctx* ctx, double* state, float* energyTH, double* pose7, double* calib4);
+/* per-frame linearization point: worldToCam_evalPT[nF][7] (Sophus data order, as hs_frame) and state_zero[nF][10]
+   (FrameHessian::get_worldToCam_evalPT / get_state_zero, Include/Frame.h:157-176; the optimize tail's setEvalPT
+   moves the newest frame's).  Both nullable. */
+int hs_ba_get_frame_eval(hs_ctx* ctx, double* evalPT7, double* state_zero);
 /* EnergyFunctional::HM / bM (marginalization prior); dim*dim and dim */
 int hs_ba_set_marginal_prior(hs_ctx* ctx, const double* HM, const double* bM);
 
@@ -139,6 +143,9 @@ int hs_ba_marginalize_frame(hs_ctx* ctx, int frame, double* HM_out, double* bM_o
    [3] number of event-timed iterations, [4] total GN loop wall (host clock), [5] iterations.
    Env HS_EVENT_TIMING: 0 (default) none, 1 times the linearize kernel only, 2 every phase. */
 int hs_ba_get_timings(hs_ctx* ctx, double* out6);
+/* Sets the HS_EVENT_TIMING mode (0 / 1 / 2 as above) of this context's later GN loops (the bench times its loop
+   without events, then runs an untimed event-timed loop for the per-phase split).  Measurement only. */
+int hs_ba_set_event_timing(hs_ctx* ctx, int mode);
 
 /* Roofline timing: reps back-to-back launches of the linearize kernel (no fused point step) on the
    context's stream between one HIP event pair; avg_ms = elapsed / reps.  Leaves the residual states of a
@@ -177,7 +184,8 @@ int hs_ba_insert_frame(hs_ctx* ctx, const hs_frame* frame, const float* image);
 /* the frame's level-0 image: host (I, dI/dx, dI/dy) triplets | host raw W*H image (ImageData::fImgL: level 0 of
    Frame::CreateDirPyrs runs on the device, Src/Frame.cpp:104-181) | device texels (W*H float4 (I, dI/dx, dI/dy, any)
    on the context's device, e.g. hs_tracker_frame_texels: the keyframe's image never crosses PCIe again; the producer
-   must have completed, as it has when its call returned).  Copies, ordered on the context's stream. */
+   must have completed, as it has when its call returned; the device copy has read the texels when this call returns,
+   so the producer may overwrite them next).  Copies, ordered on the context's stream. */
 int hs_ba_set_frame_image(hs_ctx* ctx, int frame, const float* image);
 int hs_ba_set_frame_image_raw(hs_ctx* ctx, int frame, const float* raw);
 int hs_ba_set_frame_image_device(hs_ctx* ctx, int frame, const void* d_texels);
@@ -235,6 +243,9 @@ int hs_ba_get_structure(hs_ctx* ctx, int* handles, int* pt_host, int* nres, int*
    setNewFrameEnergyTH over the gathered energies beside the solve. */
 int hs_comm_get_unique_id(char* id128);
 int hs_comm_init(hs_ctx* ctx, const char* id128, int rank, int nranks);
+/* the communicator's own rank count and this context's rank (ncclCommCount / ncclCommUserRank); 1 / 0 without a
+   communicator.  The bench reports n_gpus from it, not from the launcher's environment. */
+int hs_comm_size(hs_ctx* ctx, int* nranks, int* rank);
 
 #ifdef __cplusplus
 }

@@ -1532,6 +1532,13 @@ void hso_ba_solve_system(void* h, int iteration, double* x_out) {
   ba->solveSystemF(iteration, x);
   std::memcpy(x_out, x.data(), sizeof(double) * x.size());
 }
+// CalibHessian::setValue (Include/CalibData.h:60-91) of the current camera values (value_zero stays the create-time
+// camera, as the reference's stays the initial calibration); the precalc records follow
+void hso_ba_set_calib(void* h, const double* value4) {
+  BA* ba = (BA*)h;
+  ba->calib.setValue(value4);
+  ba->setPrecalcValues();
+}
 // EnergyFunctional::HM / bM (the marginalization prior, Include/EnergyFunctional.h:62-63)
 void hso_ba_set_marginal_prior(void* h, const double* HM, const double* bM) {
   BA* ba = (BA*)h;

@@ -96,6 +96,7 @@ def load(fast=False):
     lib.hso_ba_solve_system.argtypes = [vp, C.c_int, vp]
     lib.hso_ba_backup_state.argtypes = [vp]
     lib.hso_ba_set_marginal_prior.argtypes = [vp, vp, vp]
+    lib.hso_ba_set_calib.argtypes = [vp, vp]
     lib.hso_ba_marginalize_points.argtypes = [vp, C.c_int, vp, C.c_float, C.c_float, vp, vp]
     lib.hso_ba_marginalize_frame.argtypes = [vp, C.c_int, vp, vp]
     lib.hso_ba_do_step.argtypes = [vp]
@@ -284,6 +285,10 @@ class OracleBA:
         HM, bM = np.zeros((n, n)), np.zeros(n)
         self.lib.hso_ba_marginalize_frame(self.h, int(f), _p(HM), _p(bM))
         return HM, bM
+
+    def set_calib(self, value4):
+        """CalibHessian::setValue of the current (unscaled) camera values; value_zero stays the scene's K."""
+        self.lib.hso_ba_set_calib(self.h, _p(np.ascontiguousarray(value4, np.float64)))
 
     def set_marginal_prior(self, HM, bM):
         self.lib.hso_ba_set_marginal_prior(self.h, _p(np.ascontiguousarray(HM, np.float64)),

@@ -66,7 +66,7 @@ def test_keyframe_sequence_matches_rebuild(image_path):
             ref.update(energies=e, iters=n, tail=tail, frames=rb.frames(), points=rb.points(),
                        residuals=rb.residuals())
             rb.close()
-        else:
+        elif phase == "tail":
             got = dict(frames=d.ba.frames(), points=d.ba.points(), residuals=d.ba.residuals())
             for k in ("frames", "points", "residuals"):
                 _assert_same(got[k], ref[k], k)
@@ -102,7 +102,7 @@ def test_tail_outputs_match_rebuild():
             rb.optimize(d.iters)
             box["tail"] = rb.fixLinearization(ps["maxRelBaseline"], ps["numGoodResiduals"])
             rb.close()
-        else:  # the driver ran the tail: compare its read-backs
+        elif phase == "tail":  # the driver ran the tail: compare its read-backs
             ps = d.ba.point_state()
             _assert_same(ps["maxRelBaseline"], box["tail"]["maxRelBaseline"], "maxRelBaseline")
             _assert_same(ps["numGoodResiduals"], box["tail"]["numGoodResiduals"], "numGoodResiduals")
@@ -172,3 +172,95 @@ def test_incremental_errors():
                                  None, seq.cand[0]["color"], seq.cand[0]["weights"])
         drv2.ba.makeIDX()
     drv2.ba.close()
+
+
+def _oracle_from(drv):
+    """OracleBA (the CPU restatement) of the incremental window's committed content: frames at their evalPT / state /
+    state_zero, the current calibration, the points' idepth / idepth_zero, the residual lists, and HM / bM."""
+    from oracle_ffi import OracleBA
+    ba, seq = drv.ba, drv.seq
+    st = ba.structure()
+    ps = ba.point_state()
+    fr = ba.frames()
+    fe = ba.frame_eval()
+    HM, bM = ba.marginal_prior()
+    hd = st["handles"]
+    src = [drv.cand_of[int(h)] for h in hd]
+    pick = lambda key: np.array([seq.cand[k][key][i] for k, i in src], np.float32)  # noqa: E731
+    nF = ba.nF
+    s = types.SimpleNamespace(
+        width=seq.width, height=seq.height, K=seq.K, n_levels=seq.n_levels, n_frames=nF,
+        frames_eval=fe["evalPT"], frames_state=fr["state"], frames_state_zero=fe["state_zero"],
+        frames_exposure=np.ones(nF, np.float32), frames_energyTH=fr["energyTH"].astype(np.float32),
+        frames_id=np.array(drv.frames, np.int32), pyramids=[[seq.pyr0[k]] for k in drv.frames],
+        pt_host=st["pt_host"], pt_u=pick("u"), pt_v=pick("v"), pt_idepth=ps["idepth"], pt_idepth_zero=ps["idepth_zero"],
+        pt_color=pick("color"), pt_weights=pick("weights"), res_point=st["res_point"], res_target=st["res_target"],
+        n_points=len(hd), n_res=len(st["res_target"]))
+    o = OracleBA(s)
+    o.set_calib(fr["calib"])
+    o.set_marginal_prior(HM, bM)
+    return o, ps
+
+
+def test_keyframe_sequence_matches_oracle():
+    """The keyframe path against the CPU oracle, not against itself: at every keyframe the oracle is built from the
+    committed window (frames, calibration, points, residual lists, the marginal prior the earlier keyframes left) and
+    runs System::optimize(6) + the tail (Src/FullSystemOptimize.cpp:362-516), then flagPointsForRemoval's
+    marginalizePointsF and marginalizeFrame (Src/Mapping.cpp:12-140, Src/EnergyFunctional.cpp:456-609) on the same
+    inputs as the library.  Five keyframes, each marginalizing the oldest frame, so HM / bM accumulate over the
+    sequence.  Bars: the optimize trajectory and tail as tests/test_gpu_ba.py (energies rel 1e-3, frame states 1e-4,
+    depths rel 1e-3, toRemove within 0.2 % of the residuals, HdiF rel 2e-3); HM / bM after the points at the H bar
+    (fp32 accumulation order); after the frame (a host fp64 Schur on the same HM) at rel 1e-8."""
+    from test_gpu_ba import _close_H, _close_b
+    from hslam_amd.keyframe import KeyframeBA, make_ba_sequence
+    seq = make_ba_sequence(n_kf=12, points_per_kf=200, seed=7)
+    drv = KeyframeBA(seq, window=8, image_path="raw")
+    drv.bootstrap()
+    box = {}
+    log = []
+
+    def check(d, phase):
+        if phase == "optimize":
+            o, ps = _oracle_from(d)
+            n, e = o.optimize(d.iters)
+            hdi = o.points()["HdiF"].copy()
+            eo, drop, _, _ = o.fix_linearization(ps["maxRelBaseline"], ps["numGoodResiduals"])
+            box.update(iters=n, energies=e, frames=o.frames(), points=o.points(), hdif=hdi, tail_e=eo, drop=drop,
+                       n_res=o.scene.n_res)
+        elif phase == "tail":
+            fg, pg = d.ba.frames(), d.ba.points()
+            assert np.allclose(fg["state"], box["frames"]["state"], atol=1e-4)
+            assert np.allclose(pg["idepth"], box["points"]["idepth"], rtol=1e-3, atol=1e-4)
+            t = d.last_tail
+            assert np.count_nonzero(t["drop"] != box["drop"]) <= 0.002 * box["n_res"]
+            assert abs(t["energy"] - box["tail_e"]) <= 1e-3 * abs(box["tail_e"])
+            assert np.allclose(t["HdiF"], box["hdif"], rtol=2e-3, atol=1e-7)
+        elif phase == "marginalize":
+            o, _ = _oracle_from(d)
+            box["o2"] = o
+            box["HMo"], box["bMo"] = o.marginalize_points(d.marg_points) if len(d.marg_points) else (None, None)
+        elif phase == "points_marginalized":
+            HMg, bMg = d.ba.marginal_prior()
+            box["HMg"], box["bMg"] = HMg, bMg
+            if box["HMo"] is not None:
+                okH, rH = _close_H(HMg, box["HMo"])
+                okb, rb = _close_b(bMg, box["bMo"], box["HMo"])
+                assert okH and okb, (rH, rb)
+                log.append((len(d.marg_points), rH, rb))
+        elif phase == "frame_marginalized":
+            o = box.pop("o2")
+            o.set_marginal_prior(box["HMg"], box["bMg"])
+            Ho, bo = o.marginalize_frame(d.marg_frame)
+            Hg, bg = d.ba.marginal_prior()
+            np.testing.assert_allclose(Hg, Ho, rtol=1e-8, atol=1e-10 * np.abs(Ho).max())
+            np.testing.assert_allclose(bg, bo, rtol=1e-8, atol=1e-10 * np.abs(bo).max())
+
+    for k in range(7, 12):
+        info = drv.add_keyframe(k, check=check)
+        assert info["iters"] == box["iters"]
+        eg = np.asarray(info["energies"])
+        assert np.all(np.abs(eg - box["energies"]) <= 1e-3 * np.abs(box["energies"])), k
+    assert len(log) >= 4, log  # points were marginalized at (nearly) every keyframe
+    HM, _ = drv.ba.marginal_prior()
+    assert np.abs(HM).max() > 0
+    drv.ba.close()
