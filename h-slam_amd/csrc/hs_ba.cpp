@@ -1104,6 +1104,7 @@ int hs_ba_linearize(hs_ctx* c, int reset, double* energy_out) {
   double e = 0.0;
   HS_HIP(hipMemcpyAsync(&c->h_ctl[4], c->sysE(), sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HS_HIP(hipStreamSynchronize(c->stream));
+  c->rb_pending = false;
   std::memcpy(&e, &c->h_ctl[4], sizeof(double));
   if (energy_out) *energy_out = e;
   if (!std::isfinite(e)) return fail(HS_ERR_NONFINITE, "non-finite energy (isLost)");
@@ -1202,6 +1203,7 @@ int hs_ba_fix_linearization(hs_ctx* c, double* energy_out, uint8_t* drop_out, fl
   const int nF = c->nF, nP = c->nP;
   // pinned staging of the read-backs: HdiF [nP] floats, then the active flags [nP][8]; one sync for all of them
   HS_HIP(c->rb_stage(sizeof(float) * (size_t)nP + (size_t)nP * 8));
+  c->rb_pending = true;  // cleared after the stream sync below; an early return leaves it for the next rb_stage
   float* h_hdif = reinterpret_cast<float*>(c->h_rb);
   unsigned char* h_act = c->h_rb + sizeof(float) * (size_t)nP;
   // HdiF of the last solve, before this pass relinearizes
@@ -1238,6 +1240,7 @@ int hs_ba_fix_linearization(hs_ctx* c, double* energy_out, uint8_t* drop_out, fl
   if (want_drop)
     HS_HIP(hipMemcpyAsync(h_act, c->d_r_active, (size_t)nP * 8, hipMemcpyDeviceToHost, c->stream));
   HS_HIP(hipStreamSynchronize(c->stream));
+  c->rb_pending = false;
   std::memcpy(&e, &c->h_ctl[4], sizeof(double));
   if (energy_out) *energy_out = e;
   if (HdiF_out && nP > 0) std::memcpy(HdiF_out, h_hdif, sizeof(float) * nP);
@@ -1484,6 +1487,7 @@ int hs_ba_marginalize_points(hs_ctx* c, int n, const int* points, double* HM_out
   {  // both uploads through the pinned staging, asynchronous (the stream sync below precedes any reuse of it)
     const size_t off = ((size_t)c->nP + 15) & ~(size_t)15, ab = sizeof(float) * adHTd.size();
     HS_HIP(c->rb_stage(off + ab));
+    c->rb_pending = true;
     std::memcpy(c->h_rb, flag.data(), (size_t)c->nP);
     std::memcpy(c->h_rb + off, adHTd.data(), ab);
     if (c->nP > 0) HS_HIP(hipMemcpyAsync(c->d_marg, c->h_rb, c->nP, hipMemcpyHostToDevice, c->stream));
@@ -1493,6 +1497,7 @@ int hs_ba_marginalize_points(hs_ctx* c, int n, const int* points, double* HM_out
   HS_TRY(launch_linearize(c, 0, true));
   HS_TRY(launch_reduce(c, true, true));
   HS_HIP(hipStreamSynchronize(c->stream));
+  c->rb_pending = false;
   c->haveSystem = true;
   std::vector<double> M((size_t)dim * dim), Mb(dim), Msc((size_t)dim * dim), Mbsc(dim);
   HS_TRY(hs_ba_get_system(c, 0, M.data(), Mb.data()));    // stitchDouble(M, Mb, usePrior = false)

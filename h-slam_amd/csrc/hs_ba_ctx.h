@@ -234,7 +234,13 @@ struct hs_ctx {
   // demand (rb_stage)
   unsigned char* h_rb = nullptr;
   size_t h_rb_cap = 0;
+  bool rb_pending = false;  // an asynchronous copy from / into h_rb may still be in flight (a call left early)
   hipError_t rb_stage(size_t bytes) {
+    if (rb_pending) {  // the last user returned before its stream sync (an error path): drain before reuse
+      const hipError_t e = hipStreamSynchronize(stream);
+      if (e != hipSuccess) return e;
+      rb_pending = false;
+    }
     if (bytes <= h_rb_cap) return hipSuccess;
     if (h_rb) (void)hipHostFree(h_rb);
     h_rb = nullptr;

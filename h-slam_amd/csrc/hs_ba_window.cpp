@@ -530,8 +530,10 @@ int hs_ba_drop_inactive_residuals(hs_ctx* c, int* n_dropped) {
   HS_HIP(c->rb_stage((size_t)std::max(c->nP, 1) * 8));
   const uint8_t* act = c->h_rb;
   if (c->nP > 0) {
+    c->rb_pending = true;
     HS_HIP(hipMemcpyAsync(c->h_rb, c->d_r_active, (size_t)c->nP * 8, hipMemcpyDeviceToHost, c->stream));
     HS_HIP(hipStreamSynchronize(c->stream));
+    c->rb_pending = false;
   }
   // toRemove in activeResiduals order (points in window order, each list in order), then dropResidual one by one
   int cnt = 0, p = 0;
@@ -685,9 +687,11 @@ int hs_ba_get_point_state(hs_ctx* c, float* idepth, float* idepth_zero, float* r
   HS_HIP(c->rb_stage(5 * n * 4));
   void* dst[5] = {idepth, idepth_zero, relBL, nGood, HdiF};
   const void* src[5] = {c->d_idepth, c->d_idepth_zero, c->d_fix_relBL, c->d_fix_nGood, c->hdif_solved};
+  c->rb_pending = true;
   for (int k = 0; k < 5; k++)
     if (dst[k]) HS_HIP(hipMemcpyAsync(c->h_rb + k * n * 4, src[k], n * 4, hipMemcpyDeviceToHost, c->stream));
   HS_HIP(hipStreamSynchronize(c->stream));
+  c->rb_pending = false;
   for (int k = 0; k < 5; k++)
     if (dst[k]) std::memcpy(dst[k], c->h_rb + k * n * 4, n * 4);
   return HS_OK;

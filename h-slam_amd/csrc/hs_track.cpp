@@ -66,8 +66,10 @@ struct hs_tracker {
   bool haveRef = false, haveFrame = false;
   double last_ms = 0;
   long long* d_trace = nullptr;
-  int last_G = 1;                 // workgroups per hypothesis of the last track launch  // HS_KTRACE=1: per-hypothesis phase cycles of hs_k_track (stderr)
-  int trace_cap = 0;
+  int last_G = 1;                 // workgroups per hypothesis of the last track launch
+  int n_cu = 256;                 // the device's compute units (hipDeviceAttributeMultiprocessorCount)
+  int fallbacks = 0;              // launches rerun with G = 1 after a member-meeting timeout
+  int trace_cap = 0;              // HS_KTRACE=1: per-hypothesis phase cycles of hs_k_track (stderr)
 };
 
 static int upload_pyr(hs_tracker* t, float4** dst, const float* const* pyr) {
@@ -134,8 +136,10 @@ static HsTrackArgs make_args(hs_tracker* t) {
   return a;
 }
 
-// n hypotheses (T | aff per row in h_in), run to completion without abort
-static int run_tries(hs_tracker* t, int n, const double* h_in, int coarsest, int single_pass, int lvl, float cutoff) {
+// n hypotheses (T | aff per row in h_in), run to completion without abort.  force_g1: the one-workgroup LM loop
+// (the rerun after a G-member meeting timed out)
+static int run_tries(hs_tracker* t, int n, const double* h_in, int coarsest, int single_pass, int lvl, float cutoff,
+                     bool force_g1 = false) {
   TS_TRY(ensure_tries(t, n));
   std::memcpy(t->h_in, h_in, sizeof(double) * 9 * n);
   TS_HIP(hipMemcpyAsync(t->d_Tin, t->h_in, sizeof(double) * 9 * n, hipMemcpyHostToDevice, t->stream));
@@ -149,14 +153,20 @@ static int run_tries(hs_tracker* t, int n, const double* h_in, int coarsest, int
   a.single_pass = single_pass;
   a.pass_lvl = lvl;
   a.pass_cutoff = cutoff;
-  // workgroups per hypothesis: the chip's 256 CUs shared by the hypotheses (every member must be resident at once:
-  // they meet once per pass), at most HS_TRK_MAXG; env HS_TRK_G caps it (1 = the one-workgroup LM loop)
-  // 8 measured best at C2 (r03_b1: G = 1 / 8 / 16 / 32: 0.61 / 0.48 / 0.53 / 0.63 ms per track: more members
-  // shorten the point loop but lengthen the per-pass meeting)
-  int G = std::max(1, std::min(8, 256 / std::max(1, n)));
-  if (const char* e = std::getenv("HS_TRK_G"))
-    G = std::max(1, std::min({HS_TRK_MAXG, 256 / std::max(1, n), std::atoi(e)}));
-  if (single_pass) G = 1;
+  // workgroups per hypothesis: the device's CUs shared by the hypotheses, one member per CU (every member must be
+  // resident at once: they meet once per pass), at most HS_TRK_MAXG; env HS_TRK_G caps it (1 = the one-workgroup LM
+  // loop).  8 measured best at C2 (r03_b1: G = 1 / 8 / 16 / 32: 0.61 / 0.48 / 0.53 / 0.63 ms per track: more
+  // members shorten the point loop but lengthen the per-pass meeting).  Members that are not co-resident after all
+  // (a smaller partition, kernels of other streams on the CUs) make a meeting time out: the launch is then rerun
+  // with G = 1, which needs no co-residency.
+  const int cap = std::max(1, t->n_cu / std::max(1, n));
+  int G = std::max(1, std::min(8, cap));
+  if (const char* e = std::getenv("HS_TRK_G")) G = std::max(1, std::min({HS_TRK_MAXG, cap, std::atoi(e)}));
+  if (const char* e = std::getenv("HS_TRK_G_UNCHECKED"))  // test hook: G without the co-residency cap
+    G = std::max(1, std::min(HS_TRK_MAXG, std::atoi(e)));
+  if (single_pass || force_g1) G = 1;
+  a.spin_limit = 1u << 22;  // ~0.1 s of polls
+  if (const char* e = std::getenv("HS_TRK_SPIN")) a.spin_limit = (unsigned int)std::max(1, std::atoi(e));  // test hook
   a.G = G;
   a.nhyp = n;
   a.part = t->d_part;
@@ -186,7 +196,10 @@ static int run_tries(hs_tracker* t, int n, const double* h_in, int coarsest, int
   if (G > 1) TS_HIP(hipMemcpyAsync(t->h_cnt, t->d_cnt, sizeof(unsigned int) * n, hipMemcpyDeviceToHost, t->stream));
   TS_HIP(hipStreamSynchronize(t->stream));
   for (int i = 0; G > 1 && i < n; i++)
-    if (t->h_cnt[i]) return tfail(HS_ERR_HIP, "hs_k_track: a member workgroup never reached a pass (spin bound hit)");
+    if (t->h_cnt[i]) {  // a meeting timed out: the launch's results are void, rerun every hypothesis with G = 1
+      t->fallbacks++;
+      return run_tries(t, n, h_in, coarsest, single_pass, lvl, cutoff, true);
+    }
   float ms = 0;
   TS_HIP(hipEventElapsedTime(&ms, t->e0, t->e1));
   t->last_ms = ms;
@@ -290,6 +303,8 @@ int hs_tracker_create(hs_tracker** out, const hs_params* params, int device_id, 
     delete t;
     return tfail(HS_ERR_HIP, "stream / event creation failed");
   }
+  if (hipDeviceGetAttribute(&t->n_cu, hipDeviceAttributeMultiprocessorCount, device_id) != hipSuccess || t->n_cu < 1)
+    t->n_cu = 1;
   int maxBlocks = 1;
   for (int l = 0; l < n_levels; l++) {
     const size_t n = (size_t)t->w[l] * t->h[l];
@@ -576,6 +591,13 @@ int hs_tracker_last_stats(hs_tracker* t, int try_idx, double* ms, int* passes, l
   if (ms) *ms = t->last_ms;
   if (passes) *passes = t->h_out[try_idx].passes;
   if (point_passes) *point_passes = t->h_out[try_idx].point_passes;
+  return HS_OK;
+}
+
+int hs_tracker_launch_info(hs_tracker* t, int* G, int* fallbacks) {
+  if (!t) return tfail(HS_ERR_INVALID, "null tracker");
+  if (G) *G = t->last_G;
+  if (fallbacks) *fallbacks = t->fallbacks;
   return HS_OK;
 }
 

@@ -50,6 +50,7 @@ struct HsTrackArgs {
   HsTryOut* out;        // [n]
   int single_pass, pass_lvl;
   float pass_cutoff;
+  unsigned int spin_limit;  // polls of the G-member meeting before a hypothesis is flagged (then rerun with G = 1)
   double* lm_log;       // [n][HS_TRK_MAXLOG][3]: resNew/N, resOld/N (accept test), |inc| (break test) per LM iteration
   int* lm_lvl;          // [n][HS_TRK_MAXLOG]
   long long* trace;

@@ -391,7 +391,7 @@ __device__ void trk_pass(const HsTrackArgs& a, TrkShared& S, int h, int g) {
           if (gg < G) ok = ok && (unsigned int)(v[2 * gg] >> 32) == tg && (unsigned int)(v[2 * gg + 1] >> 32) == tg;
         if (__all(ok)) break;
         __builtin_amdgcn_s_sleep(1);
-        if (++spins == (1u << 22)) {  // a member never arrived (~seconds): flag the hypothesis, go on
+        if (++spins >= a.spin_limit) {  // a member never arrived (not co-resident): flag the hypothesis, go on
           if (tid == 0) __hip_atomic_store(a.cnt + h, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }

@@ -123,6 +123,7 @@ SIGNATURES = {
     "hs_tracker_get_lm_log": ([VP, I, I, VP, VP, VP, VP, VP], I),
     "hs_tracker_last_ms": ([VP, VP], I),
     "hs_tracker_last_stats": ([VP, I, VP, VP, VP], I),
+    "hs_tracker_launch_info": ([VP, VP, VP], I),
     "hs_tracker_set_frame_raw": ([VP, VP, C.c_float], I),
     "hs_tracker_set_ref_ba": ([VP, VP, I, C.c_float, VP], I),
     "hs_tracker_frame_texels": ([VP, I, VP], I),

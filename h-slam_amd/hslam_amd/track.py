@@ -139,6 +139,12 @@ class CoarseTracker:
         m = min(n.value, cap)
         return lvl[:m], nr[:m], orr[:m], inc[:m]
 
+    def launch_info(self):
+        """(G workgroups per hypothesis of the last launch, launches rerun with G = 1 after a meeting timeout)."""
+        g, f = C.c_int(), C.c_int()
+        check(self.lib.hs_tracker_launch_info(self.h, C.byref(g), C.byref(f)))
+        return g.value, f.value
+
     def last_stats(self, try_idx: int = 0):
         """(device ms, passes, point-passes) of one hypothesis of the last call."""
         ms, ps, pp = C.c_double(), C.c_int(), C.c_longlong()

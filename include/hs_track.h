@@ -93,6 +93,10 @@ int hs_tracker_last_ms(hs_tracker* t, double* ms);
    calcRes(+calcGSSSE) passes it ran and the sum of their levels' reference-point counts (the point-pass units
    of the tracker's roofline).  Outputs nullable. */
 int hs_tracker_last_stats(hs_tracker* t, int try_idx, double* ms, int* passes, long long* point_passes);
+/* workgroups per hypothesis of the last track launch (G members meeting once per pass, sized from the device's
+   compute units) and the number of launches so far rerun with G = 1 after a member meeting timed out (members not
+   co-resident: a smaller partition, kernels of other streams). */
+int hs_tracker_launch_info(hs_tracker* t, int* G, int* fallbacks);
 
 #ifdef __cplusplus
 }

@@ -125,7 +125,9 @@ def _lm_divergence(lg, lo, spread=(0.0, 0.0, 0.0)):
     decisions."""
     lvg, ng, og, ig = lg
     lvo, no, oo, io = lo
-    tr, ti = max(1e-4, 10 * spread[0]), max(1e-3, 10 * spread[1])
+    # tied to the oracle's own spread, with ceilings so a run with a large spread cannot quietly loosen the check
+    tr, ti = min(max(1e-4, 10 * spread[0]), 1e-3), min(max(1e-3, 10 * spread[1]), 3e-2)
+    print(f"LM bars: ratios {tr:.2e}, step norms {ti:.2e} (oracle order spread {spread[0]:.2e}, {spread[1]:.2e})")
     for k in range(min(len(lvg), len(lvo))):
         assert lvg[k] == lvo[k], k
         assert abs(ng[k] - no[k]) <= tr * abs(no[k]), (k, ng[k], no[k], tr)
@@ -155,7 +157,8 @@ def test_track_parity(vga, pair, start):
     ro = o.track(T0, [0.0, 0.0], vga.n_levels - 1, minRes)
     assert okg == ro["ok"] and okg
     k = _lm_divergence(g.lm_log(0), o.lm_log(), spread)
-    tol_T, tol_a, tol_b = (max(1e-5, 10 * spread[2]), 1e-5, 1e-3) if k is None else (2e-3, 1e-2, 0.5)
+    tol_T, tol_a, tol_b = (min(max(1e-5, 10 * spread[2]), 1e-4), 1e-5, 1e-3) if k is None else (2e-3, 1e-2, 0.5)
+    print(f"pose bar {tol_T:.2e} (oracle order spread {spread[2]:.2e}), first near-tie {k}")
     assert _pose_err(Tg, ro["T"]) < tol_T, k
     assert abs(ag[0] - ro["aff"][0]) < tol_a and abs(ag[1] - ro["aff"][1]) < tol_b, k
     lr = g.lastResiduals
@@ -244,7 +247,8 @@ def test_track_parity_4_levels(vga4, start):
     ro = o.track(T0, [0.0, 0.0], vga4.n_levels - 1, minRes)
     assert okg == ro["ok"] and okg
     k = _lm_divergence(g.lm_log(0), o.lm_log(), spread)
-    tol_T, tol_a, tol_b = (max(1e-5, 10 * spread[2]), 1e-5, 1e-3) if k is None else (2e-3, 1e-2, 0.5)
+    tol_T, tol_a, tol_b = (min(max(1e-5, 10 * spread[2]), 1e-4), 1e-5, 1e-3) if k is None else (2e-3, 1e-2, 0.5)
+    print(f"pose bar {tol_T:.2e} (oracle order spread {spread[2]:.2e}), first near-tie {k}")
     assert _pose_err(Tg, ro["T"]) < tol_T, k
     assert abs(ag[0] - ro["aff"][0]) < tol_a and abs(ag[1] - ro["aff"][1]) < tol_b, k
     lr = g.lastResiduals
@@ -259,3 +263,34 @@ def test_track_parity_4_levels(vga4, start):
     assert sum(pcn[l] * int((lv == l).sum()) for l in range(vga4.n_levels)) + sum(pcn) <= point_passes
     assert ms > 0
     g.close()
+
+
+def test_member_meeting_timeout_falls_back_to_one_workgroup(vga, monkeypatch):
+    """The G member workgroups of a hypothesis meet once per pass and must be co-resident.  With the meeting's poll
+    bound forced to one poll (HS_TRK_SPIN=1) and G past the co-residency cap (HS_TRK_G_UNCHECKED=16), meetings time
+    out; the launch is then rerun with G = 1 and the track is the one-workgroup track, bit for bit."""
+    from hslam_amd.se3 import SE3
+    from hslam_amd.track import CoarseTracker
+    T0 = SE3().data()
+    minRes = np.full(5, np.nan)
+    g1 = CoarseTracker(vga.width, vga.height, vga.K4, vga.n_levels)
+    g1.set_scene(vga)
+    monkeypatch.setenv("HS_TRK_G", "1")
+    ok1, T1, a1 = g1.trackNewestCoarse(T0, [0.0, 0.0], vga.n_levels - 1, minRes)
+    assert g1.launch_info() == (1, 0)
+    monkeypatch.delenv("HS_TRK_G")
+    g2 = CoarseTracker(vga.width, vga.height, vga.K4, vga.n_levels)
+    g2.set_scene(vga)
+    monkeypatch.setenv("HS_TRK_SPIN", "1")
+    monkeypatch.setenv("HS_TRK_G_UNCHECKED", "16")
+    ok2, T2, a2 = g2.trackNewestCoarse(T0, [0.0, 0.0], vga.n_levels - 1, minRes)
+    G, fallbacks = g2.launch_info()
+    assert fallbacks >= 1 and G == 1
+    assert ok1 == ok2 and np.array_equal(T1, T2) and np.array_equal(a1, a2)
+    assert np.array_equal(g1.lastResiduals, g2.lastResiduals, equal_nan=True)
+    monkeypatch.delenv("HS_TRK_SPIN")
+    monkeypatch.delenv("HS_TRK_G_UNCHECKED")
+    ok3, T3, a3 = g2.trackNewestCoarse(T0, [0.0, 0.0], vga.n_levels - 1, minRes)  # co-resident again: G > 1
+    assert g2.launch_info()[0] > 1 and g2.launch_info()[1] == fallbacks and ok3
+    g1.close()
+    g2.close()
