@@ -27,7 +27,6 @@
 #include <type_traits>
 
 #include "hs_kernels.h"
-#include "hs_ldlt.h"
 #include "hs_se3_dev.h"
 
 
@@ -1712,13 +1711,298 @@ __global__ __launch_bounds__(ST_NT) void hs_k_stitch(HsStitchArgs a) {
 // solve + step (fp64), one workgroup of 256 threads
 // =====================================================================================================
 namespace {
-constexpr int SOLVE_NT = HS_SOLVE_NT;  // 8 waves: the LDLT's column-block owners (hs_ldlt.h, W = 8)
+constexpr int SOLVE_NT = HS_SOLVE_NT;  // 8 waves: the LDLT's panel wave + 7 waves of trailing half-tiles
+
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), lane);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
 }  // namespace
 
+
+// Solves (L D L^T) y = z in place for the permuted, scaled system of one GN step (n = 4 + 8 nF, a multiple
+// of 4): right-looking LDLT in 4-column blocks with one-block look-ahead, ONE workgroup barrier per block.
+//  wave 0 (the panel wave): lane l owns row l + 4 for the whole factorization and carries its (L D) entries of
+//    the last panel and its forward-substituted rhs in registers.  In phase k it applies block k's rank-4
+//    update to its row of column block k + 1, takes the updated 4x4 diagonal block from lanes 4k .. 4k+3
+//    (readlane), factors it uniformly and reduces its row to the (L D) / L entries of panel k + 1; it publishes
+//    only L (LT), the pivots and the diagonal rows' rhs;
+//  waves 1-7: every lower 4x4 tile right of the next panel (register-resident, one per lane) takes block
+//    k's rank-4 update (its L D rows formed from LT and the pivots); the owners of column block k + 2 publish it
+//    (row-major, 32 B per row) for the panel wave's next phase.
+// The panel chain (the critical path) thus overlaps the trailing update.  fp64 throughout, FMA-contracted,
+// reciprocals by v_rcp_f64 + 2 Newton steps: the solve is checked against the oracle's Eigen-order LDLT by
+// tolerance (the LDLT is parity-unpinned), not bitwise.  The pivot order is applied by the
+// caller.  Then D^-1 and the backward substitution (one wave, 4x4 diagonal blocks solved uniformly).
+//   M  : the permuted system (row-major, stride n), read only
+//   LT : L transposed, LT[i * LSTR + k] = L(k, i); MUST be zero on entry (its upper part stays zero)
+//   W  : scratch of 26 * HS_MAXDIM doubles;  yv : right-hand side in, solution out
 // the multi-rank select block of the solve / combine launches lives in the solve's LDS matrix A
 constexpr int SOLVE_TH_CAP = 2 * HS_MAXDIM * HS_MAXDIM - 1600 - HS_TH_BINS;
 static_assert(SOLVE_TH_CAP >= 1024, "survivor space of the multi-rank select");
-static_assert(SOLVE_NT == 512, "hs_ldlt::solve<8>: 8 waves");
+constexpr int LSTR = HS_MAXDIM + 2;  // padded row stride of LT (even: 16 B aligned 4-entry groups)
+constexpr int LDLT_SCRATCH = 26 * HS_MAXDIM;
+
+// 1/d: v_rcp_f64 (~2^-26 relative) refined by ONE Newton step (~2^-50, 4e-15 relative) -- the pivots' error
+// then sits ~1e11 below the 1e-3 tolerance on x, and the LDLT's critical path is 68 reciprocals long;
+// 0 for a (near-)zero pivot
+__device__ __forceinline__ double rcp_f64(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  const double e = __builtin_fma(-d, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  return fabs(d) > DBL_MIN ? r : 0.0;
+}
+
+// The panel's uniform factors: pivots d, their reciprocals, the partially reduced diagonal-block entries
+// q(jp, j) (after the columns < j) and the substituted right-hand side yd of the 4 diagonal rows.
+struct Panel4 {
+  double d[4], dinv[4], q[4][4], yd[4];
+};
+struct PanelOut {
+  double lw[4], ls[4], yr;
+};
+// wave-cooperative panel factorization: lane l holds row K0 + l (lanes 0-3: the diagonal block's rows), a =
+// its entries of the panel columns, yr its rhs; every lane of the wave executes this.  Column by column: the
+// pivot and the reduced entries come from lanes 0-3 by readlane.  The later columns are reduced as
+// a(jp) -= (a(j) q(jp, j)) / d(j), the product formed beside the reciprocal, so the critical path per column is
+// one readlane, the reciprocal (+ Newton step) and one multiply-add; L = a(j) / d(j) and its row mask stay off
+// it (rows l <= j of the diagonal block take garbage updates of entries no later column reads).  A diagonal row
+// l takes L entries only for j < l.
+__device__ __forceinline__ void panel_coop(const double a[4], double yr, int l, Panel4& P, PanelOut& o, int base = 0) {
+  double pr[4] = {a[0], a[1], a[2], a[3]};
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const double d = readlane_f64(pr[j], base + j);
+    const double dinv = rcp_f64(d);
+    const double ydj = readlane_f64(yr, base + j);
+    P.d[j] = d;
+    P.dinv[j] = dinv;
+    P.yd[j] = ydj;
+#pragma unroll
+    for (int jp = j + 1; jp < 4; jp++) P.q[jp][j] = readlane_f64(pr[j], base + jp);
+    const double lj = pr[j] * dinv;
+    o.lw[j] = l > j ? pr[j] : 0.0;
+    o.ls[j] = l > j ? lj : 0.0;
+#pragma unroll
+    for (int jp = j + 1; jp < 4; jp++) pr[jp] = __builtin_fma(-(pr[j] * P.q[jp][j]), dinv, pr[jp]);
+    yr = __builtin_fma(-o.ls[j], ydj, yr);
+  }
+  o.yr = yr;
+}
+// a further (non-diagonal) row with the panel's factors: the same operations as panel_coop's lanes l >= 4
+__device__ __forceinline__ void panel_row_uniform(const double a[4], double yr, const Panel4& P, PanelOut& o) {
+  double pr[4] = {a[0], a[1], a[2], a[3]};
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    o.lw[j] = pr[j];
+    o.ls[j] = pr[j] * P.dinv[j];
+#pragma unroll
+    for (int jp = j + 1; jp < 4; jp++) pr[jp] = __builtin_fma(-(pr[j] * P.q[jp][j]), P.dinv[j], pr[jp]);
+    yr = __builtin_fma(-o.ls[j], P.yd[j], yr);
+  }
+  o.yr = yr;
+}
+
+// publishes one panel row r (l = r - K0): its (L D) entries LW (zero for the diagonal rows, which take no part in
+// the trailing update), its L entries into LT (which the next phase reads back), and the substituted rhs; lane
+// j < 4 also stores pivot j
+__device__ __forceinline__ void panel_row_store(const PanelOut& o, const Panel4& P, int r, int l, int K0, double* LWn,
+                                                double* LT, double* Dv, double* yf, double* yv) {
+  constexpr int MD = HS_MAXDIM;
+  const bool diag = l < 4;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    LWn[j * MD + r] = diag ? 0.0 : o.lw[j];
+    LT[(K0 + j) * LSTR + r] = o.ls[j];  // zero on and above the diagonal
+  }
+  if (diag) {
+    Dv[r] = l == 0 ? P.d[0] : l == 1 ? P.d[1] : l == 2 ? P.d[2] : P.d[3];
+    yf[r] = o.yr;
+  } else {
+    yv[r] = o.yr;
+  }
+}
+
+__device__ __forceinline__ void ldlt_solve_blocked(const double* M, double* LT, double* W, double* yv, int n, int tid,
+                                                   long long* trace, int dbg = 0) {
+  constexpr int MD = HS_MAXDIM;
+  static_assert((HS_MAXDIM / 4 - 2) * (HS_MAXDIM / 4 - 1) / 2 <= SOLVE_NT - 64, "one trailing tile per lane");
+  static_assert(LSTR % 2 == 0, "16 B aligned LT groups");
+  const int nb = n >> 2;
+  double* PBq = W;            // [2][MD][4] column block k+1 before block k's update, row-major (32 B per row)
+  double* LWb = W + 8 * MD;   // [4][MD] (L D) of panel 0 (the panel wave's initial carry)
+  double* Dv = W + 24 * MD;   // [MD] pivots
+  double* yf = W + 25 * MD;   // [MD] forward-substituted rhs of the diagonal rows
+  const bool pw = tid < 64;   // the panel wave
+  // waves 1-7: trailing tile (tr, tc), tc >= 2, row-major over the lower triangle
+  const int u = tid - 64;
+  int trp = 0;
+  while ((trp + 1) * (trp + 2) / 2 <= u) trp++;
+  const int tr = 2 + trp, tc = 2 + (u - trp * (trp + 1) / 2);
+  const bool tile = !pw && tr < nb;
+  double v[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+#pragma unroll
+    for (int c = 0; c < 4; c++) v[i][c] = tile ? M[(4 * tr + i) * n + 4 * tc + c] : 0.0;
+  if (tid < n)
+#pragma unroll
+    for (int c = 0; c < 4; c++) PBq[4 * MD + tid * 4 + c] = M[tid * n + 4 + c];  // column block 1
+  // prologue: panel 0 over rows 0 .. n-1 by the panel wave (lanes 0-3 also take rows 64 .. n-1)
+  if (pw) {
+    const int r = min(tid, n - 1);
+    double a4[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) a4[c] = M[r * n + c];
+    Panel4 P;
+    PanelOut o;
+    panel_coop(a4, yv[r], tid, P, o);
+    if (tid < n) panel_row_store(o, P, tid, tid, 0, LWb, LT, Dv, yf, yv);
+    if (tid + 64 < n) {
+      const int r2 = tid + 64;
+#pragma unroll
+      for (int c = 0; c < 4; c++) a4[c] = M[r2 * n + c];
+      panel_row_uniform(a4, yv[r2], P, o);
+      panel_row_store(o, P, r2, r2, 0, LWb, LT, Dv, yf, yv);
+    }
+  }
+  __syncthreads();
+  // the panel wave's carry: lane l owns row rw = l + 4 (clamped; rows >= n are never stored)
+  const int rw = min(tid + 4, n - 1);
+  double lwc[4] = {0.0, 0.0, 0.0, 0.0}, ycar = 0.0;
+  if (pw) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) lwc[j] = LWb[j * MD + rw];
+    ycar = yv[rw];
+  }
+  for (int k = 0; k + 1 < nb; k++) {
+    const int K0 = 4 * (k + 1);
+    const double* LSk = LT + 4 * k * LSTR;  // LSk[j * LSTR + row] = L(row, 4k + j)
+    if (trace && tid == 0 && k == 4) trace[16] = clock64();
+    if (pw) {  // panel k+1: lane l owns row rw; the diagonal rows are lanes 4k .. 4k+3
+      const double* PBc = PBq + ((k + 1) & 1) * 4 * MD;
+      const double4 pb = *reinterpret_cast<const double4*>(PBc + rw * 4);
+      double a4[4] = {pb.x, pb.y, pb.z, pb.w};
+      double lsd[4][4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const double4 q4 = *reinterpret_cast<const double4*>(LSk + j * LSTR + K0);  // L(K0 + c, 4k + j)
+        lsd[0][j] = q4.x;
+        lsd[1][j] = q4.y;
+        lsd[2][j] = q4.z;
+        lsd[3][j] = q4.w;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++)  // block k's update of this row of column block k+1
+#pragma unroll
+        for (int c = 0; c < 4; c++) a4[c] = __builtin_fma(-lwc[j], lsd[c][j], a4[c]);
+      const int l = tid - 4 * k;  // row rw - K0 (< 0: a row of an earlier panel, inert)
+      Panel4 P;
+      PanelOut o;
+      panel_coop(a4, ycar, l, P, o, 4 * k);
+      if (l >= 0 && tid + 4 < n) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) LT[(K0 + j) * LSTR + rw] = o.ls[j];  // zero on and above the diagonal
+        if (l < 4) {
+          Dv[rw] = l == 0 ? P.d[0] : l == 1 ? P.d[1] : l == 2 ? P.d[2] : P.d[3];
+          yf[rw] = o.yr;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++) lwc[j] = o.lw[j];
+      ycar = o.yr;
+      if (trace && tid == 0 && k == 4) trace[17] = clock64();
+    } else if (tile && tc >= k + 2) {  // block k's rank-4 update of a trailing tile
+      double lw[4][4], ls[4][4], dk[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) dk[j] = Dv[4 * k + j];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const double4 r4 = *reinterpret_cast<const double4*>(LSk + j * LSTR + 4 * tr);
+        const double4 c4 = *reinterpret_cast<const double4*>(LSk + j * LSTR + 4 * tc);
+        lw[0][j] = r4.x * dk[j];
+        lw[1][j] = r4.y * dk[j];
+        lw[2][j] = r4.z * dk[j];
+        lw[3][j] = r4.w * dk[j];
+        ls[0][j] = c4.x;
+        ls[1][j] = c4.y;
+        ls[2][j] = c4.z;
+        ls[3][j] = c4.w;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+          for (int c = 0; c < 4; c++) v[i][c] = __builtin_fma(-lw[i][j], ls[c][j], v[i][c]);
+      if (tc == k + 2) {
+        double* PBn = PBq + (k & 1) * 4 * MD;
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+          *reinterpret_cast<double4*>(PBn + (4 * tr + i) * 4) = make_double4(v[i][0], v[i][1], v[i][2], v[i][3]);
+      }
+    }
+    if (trace && tid == 64 && k == 4) trace[18] = clock64();
+    __syncthreads();
+    if (trace && tid == 0 && k == 4) trace[19] = clock64();
+    if (trace && tid == 0 && k == 4) trace[12] = wall_clock64();
+    if (trace && tid == 0 && k == 8) trace[14] = wall_clock64();  // mid-factorization checkpoint
+  }
+  // D^-1 z, then L^T x = D^-1 z by wave 0: lane i owns row i (< 64); rows 64 .. n-1 (at most the last block)
+  // are solved uniformly first.  Per 4-row block the unknowns are solved uniformly from the block's diagonal
+  // L entries, then every lane updates its row in decreasing k; LT is zero on and above the diagonal, so the
+  // updates need no masks and a row of the block ends equal to its unknown.
+  if (pw) {
+    const int i = tid;
+    const int ci = min(i, n - 1);
+    double y = i < n ? yf[ci] * rcp_f64(Dv[ci]) : 0.0;
+    int kb = nb - 1;
+    if (n > 64) {  // the last block (rows 64 .. 67)
+      const int k0 = 64;
+      double x[4];
+#pragma unroll
+      for (int j = 3; j >= 0; j--) {
+        double zz = yf[k0 + j] * rcp_f64(Dv[k0 + j]);
+#pragma unroll
+        for (int jj = 3; jj > j; jj--) zz = __builtin_fma(-LT[(k0 + j) * LSTR + k0 + jj], x[jj], zz);
+        x[j] = zz;
+      }
+#pragma unroll
+      for (int j = 3; j >= 0; j--) y = __builtin_fma(-LT[i * LSTR + k0 + j], x[j], y);
+      if (i < 4) yv[k0 + i] = i == 0 ? x[0] : i == 1 ? x[1] : i == 2 ? x[2] : x[3];
+    }
+    (void)kb;
+    // blocks 15 .. 0 unrolled (no loop-carried branches, so the LT loads of later blocks are issued early); the
+    // blocks at and beyond nb (n <= 64) are all zero (LT zeroed at entry, y = 0 past n) and leave y unchanged
+#pragma unroll
+    for (int kb2 = 15; kb2 >= 0; kb2--) {
+      const int kb = kb2;
+      const int k0 = 4 * kb;
+      double z[4], Li[4], Ld[4][4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        z[j] = readlane_f64(y, k0 + j);
+        Li[j] = LT[i * LSTR + k0 + j];
+#pragma unroll
+        for (int jj = j + 1; jj < 4; jj++) Ld[jj][j] = LT[(k0 + j) * LSTR + k0 + jj];
+      }
+      double x[4];
+#pragma unroll
+      for (int j = 3; j >= 0; j--) {
+        double zz = z[j];
+#pragma unroll
+        for (int jj = 3; jj > j; jj--) zz = __builtin_fma(-Ld[jj][j], x[jj], zz);
+        x[j] = zz;
+      }
+#pragma unroll
+      for (int j = 3; j >= 0; j--) y = __builtin_fma(-Li[j], x[j], y);
+    }
+    if (i < n && i < 64) yv[i] = y;
+    if (trace && tid == 0) trace[13] = wall_clock64();
+  }
+}
 
 // FrameOptimizationData::setState's scaling (Include/Frame.h:151-170)
 __device__ __forceinline__ void scale_state(const double s[10], double o[10]) {
@@ -1756,8 +2040,8 @@ __global__ void hs_k_debug_se3(int op, int n, const double* in, double* out) {
 
 __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
   __shared__ double A[HS_MAXDIM * HS_MAXDIM];  // the scaled system S H S (row-major, stride n)
-  __shared__ __align__(16) double B[16 * HS_MAXF];  // doStep's per-frame poses
-  __shared__ __align__(16) hs_ldlt::Lds LDL;          // the LDLT's published columns (hs_ldlt.h)
+  __shared__ __align__(16) double B[LDLT_SCRATCH];  // LDLT scratch
+  __shared__ __align__(16) double LT[HS_MAXDIM * LSTR];  // L^T of the factorization (zeroed at entry)
   __shared__ double Nf[2 * HS_MAXDIM * HS_NNS];  // nullspace factors N | Npi (prefetched at entry)
   __shared__ double tk[2 * HS_NNS];
   __shared__ double Sv[HS_MAXDIM], xs[HS_MAXDIM], yv[HS_MAXDIM];
@@ -1871,6 +2155,9 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
 #pragma unroll
     for (int u = 0; u < NF_NU; u++) nfv[u] = a.Nproj[min(tid + u * SOLVE_NT, 2 * n * HS_NNS - 1)];
   }
+  // L^T must be zero on entry to the LDLT: stored while the prefetch above is in flight
+  if (solve)
+    for (int idx = tid; idx < HS_MAXDIM * LSTR; idx += nt) LT[idx] = 0.0;
   {
     uint2* ls = reinterpret_cast<uint2*>(st_raw);
 #pragma unroll
@@ -1962,7 +2249,7 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     // the reference's own 1- vs 8-thread spread)
     if ((a.dbg & 8) && a.trace && tid == 0) a.trace[20] = clock64();
     for (int rep = 0; rep < ((a.dbg & 8) ? 2 : 1); rep++) {
-      hs_ldlt::solve<8>(A, yv, nF, LDL, tid);
+      ldlt_solve_blocked(A, LT, B, yv, n, tid, a.trace, a.dbg);
       __syncthreads();
       if ((a.dbg & 8) && a.trace && tid == 0) a.trace[21 + rep] = clock64();
     }

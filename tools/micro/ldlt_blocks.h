@@ -1,5 +1,9 @@
-// hs_ldlt.h — the GN step's scaled LDLT solve (EnergyFunctional::solveSystemF's `SHS.ldlt().solve(Sb)`,
-// Src/EnergyFunctional.cpp:799-801) inside one workgroup.
+// ldlt_blocks.h — round-4 EXPERIMENT (tools/micro/ldlt8.hip), not used by the product: a column-block LDLT of the GN
+// step's scaled system (EnergyFunctional::solveSystemF's `SHS.ldlt().solve(Sb)`, Src/EnergyFunctional.cpp:799-801)
+// inside one workgroup.  Correct (x within 1e-11 of a host fp64 LDLT), but not faster than hs_k_solve's panel LDLT
+// (hs_ba_kernels.hip ldlt_solve_blocked): 28-34k cycles for nF = 8 against ~31k, and the solve kernel measured
+// 28.3 vs 26.2 us per launch with it (gpurun_out/r04_p, r04_q).  Per 4-pivot phase: the owner's apply of the previous
+// block ~500-930 cycles, its block ~650-790, the barrier ~280 (gpurun_out/r04_r).  See DESIGN.md §4 *Solve*.
 //
 // The system is n = 4 + 8 nF (calib rows first, then 8 rows per frame), symmetric positive definite after the
 // damping, factored without pivoting (backward stable for SPD; Eigen's diagonal pivoting changes x by rounding only,
@@ -127,7 +131,8 @@ __device__ __forceinline__ void inv4(const double a[4][4], double g[4][4]) {
 // to two blocks; W = 16: 1024 threads).  Every thread of the workgroup calls it (no preparation of L needed); it ends
 // with a barrier.
 template <int W>
-__device__ void solve(const double* A_, double* yv_, int nF, Lds& L, int tid, long long* trace = nullptr) {
+__device__ void solve(const double* A_, double* yv_, int nF, Lds& L, int tid, long long* trace = nullptr,
+                      long long* ltrace = nullptr) {
   constexpr int C = 4, JB = 16 / W;  // columns per block, blocks per wave
   static_assert(W == 8 || W == 16, "8 or 16 waves");
   typedef double dbl2 __attribute__((ext_vector_type(2)));
@@ -219,7 +224,6 @@ __device__ void solve(const double* A_, double* yv_, int nF, Lds& L, int tid, lo
   auto own_block = [&](int kb, auto jo_tag) {
     constexpr int jo = decltype(jo_tag)::value;
     __builtin_amdgcn_s_setprio(3);
-    if (trace && i == 0) trace[8 + (kb & 15)] = clock64();
     const int k0 = C * kb;
     double B[C][C], d[C], rr[C], Wd[C][C];  // Wd(r, c) = d_c L(r, c): the entry after the steps < c
 #pragma unroll
@@ -253,7 +257,6 @@ __device__ void solve(const double* A_, double* yv_, int nF, Lds& L, int tid, lo
       lm[kc] = i > k ? m[kc] : 0.0;
     }
     compiler_fence();  // the block's stores are issued here
-    if (trace && i == 0) trace[24 + (kb & 15)] = clock64();
     __builtin_amdgcn_s_setprio(0);
     if (w == hold) holder_block(kb, lm);
   };
@@ -286,7 +289,7 @@ __device__ void solve(const double* A_, double* yv_, int nF, Lds& L, int tid, lo
           for (int kc = 0; kc < C; kc++) col[j][c] = __builtin_fma(-u[kc], mb[kc][c], col[j][c]);
       }
     }
-    if (w == hold) {
+    if (w == hold && kb % W != hold) {  // (the holder's own blocks went through holder_block in own_block)
       double lm[C];
 #pragma unroll
       for (int kc = 0; kc < C; kc++) lm[kc] = i > k0 + kc ? mi[kc] : 0.0;
@@ -295,20 +298,24 @@ __device__ void solve(const double* A_, double* yv_, int nF, Lds& L, int tid, lo
   };
   for (int p = 0; p < nb; p++) {  // uniform over the workgroup: every wave takes every barrier
     const int owner = p % W;
+    if (ltrace && w == owner && i == 0) ltrace[p * 4 + 0] = clock64();
     if (p >= 1 && (held(0) || held(JB - 1))) {
       bool pending = false;
 #pragma unroll
       for (int j = 0; j < JB; j++) pending |= held(j) && w + W * j >= p;
       if (pending || w == hold) {
         if (w == owner) __builtin_amdgcn_s_setprio(2);
-        else if (w != hold) __builtin_amdgcn_s_sleep(3);  // ~190 cycles: the next owner's batch reads go first
+        else if (w != hold) __builtin_amdgcn_s_sleep(8);  // ~510 cycles: the next owner's batch reads go first
         apply_block(p - 1);
       }
     }
+    if (ltrace && w == owner && i == 0) ltrace[p * 4 + 1] = clock64();
     if (w == owner) {
       if (p < W) own_block(p, std::integral_constant<int, 0>());
       else own_block(p, std::integral_constant<int, JB - 1>());
     }
+    if (ltrace && w == owner && i == 0) ltrace[p * 4 + 2] = clock64();
+    if (ltrace && w == hold && i == 0) ltrace[p * 4 + 3] = clock64();
     __syncthreads();
   }
   if (trace && tid == 0) trace[2] = clock64();
