@@ -4,13 +4,13 @@
 //                    projection into the newest keyframe, seed byte set to 0 with a word CAS (duplicates dropped).
 // hs_k_act_cand      the per-point part of the selection loop (Mapping.cpp:378-426): delete / skip / the
 //                    projected cell, the sub-pixel fraction and the threshold of every entry of the loop order.
-// hs_k_act_select    one workgroup: growDistBFS of the seeds over the whole workgroup, then the greedy loop on
-//                    wave 0 alone — per batch of 64 entries the first one (in loop order) whose distance passes
-//                    is taken, addIntoDistFinal grows the map from it, the rest of the batch is re-tested.
-//                    BFS steps are frontier-parallel; a cell joins the next frontier only through the CAS that
-//                    lowered it, so the map after each step is the reference's (its per-step result does not
-//                    depend on the order the frontier is walked in).
+// hs_k_act_select    one workgroup: growDistBFS of the seeds over the whole workgroup (frontier-parallel; a cell
+//                    joins the next frontier only through the CAS that lowered it, so the map after each step is
+//                    the reference's), then the greedy loop: per batch of 64 entries wave 0 takes, in loop order,
+//                    each entry whose distance passes and applies its addIntoDistFinal to the rest of the batch
+//                    in closed form (bfs_dist); the workgroup then folds the batch's seeds into the map.
 //                    The map lives in LDS as bytes (0..39, 255 = the reference's 1000) when it fits.
+// hs_k_act_final     the exact distance map after the loop (makeDistanceMap + every addIntoDistFinal), per cell.
 // hs_k_act_optimize  optimizeImmaturePoint (Src/FullSystemOptPoint.cpp:24-175) with
 //                    ImmaturePoint::linearizeResidual (Src/ImmaturePoint.cpp:389-451): one wave per point,
 //                    lane = residual (target frame) x pattern pixel; energy, Hdd and bd are summed in the
@@ -189,238 +189,244 @@ __device__ __forceinline__ void bfs_grow_wg(uint8_t* map, int w1, int h1, int*& 
   }
 }
 
-// addIntoDistFinal's growDistBFS from one cell, run by a single wave: the frontier of a one-seed BFS is at most
-// the ring of its step (<= 8k cells), so one wave walks it with no workgroup barrier.  Lane = frontier entry
-// (8 or 16 per pass) x neighbour direction, so a pass is one straight-line sequence: read entry, probe word, lower,
-// append (ballot + mbcnt, no atomics).  The lists are LDS.  This form (the map in global memory) lowers by CAS;
-// the LDS map uses bfs_grow_wave_claim below.
-__device__ __forceinline__ void bfs_grow_wave(uint8_t* map, int w1, int h1, int* in, int* out, int n,
-                                              long long* cnt) {
-  const int lane = threadIdx.x & 63;
-  // growDistBFS's neighbour order: +x, -x, +y, -y, then the diagonals (+1+w1, -1+w1, -1-w1, +1-w1)
-  const int sub8 = lane & 7, sub4 = lane & 3;
-  const int dx8 = (sub8 == 0 || sub8 == 4 || sub8 == 7) ? 1 : ((sub8 == 1 || sub8 == 5 || sub8 == 6) ? -1 : 0);
-  const int dy8 = (sub8 == 2 || sub8 == 4 || sub8 == 5) ? 1 : ((sub8 == 3 || sub8 == 6 || sub8 == 7) ? -1 : 0);
-  const int dx4 = sub4 == 0 ? 1 : (sub4 == 1 ? -1 : 0);
-  const int dy4 = sub4 == 2 ? 1 : (sub4 == 3 ? -1 : 0);
-  n = __builtin_amdgcn_readfirstlane(n);  // uniform: the pass loop is a scalar loop
-  for (int k = 1; k < HS_ACT_BFS_STEPS && n > 0; k++) {
-    // odd steps: 8 entries x 8 directions per pass; even steps: 16 entries x 4 directions
-    const bool diag = (k & 1) != 0;
-    const int slot = diag ? lane >> 3 : lane >> 2;
-    const int per = diag ? 8 : 16;
-    const int dx = diag ? dx8 : dx4, dy = diag ? dy8 : dy4;
-    const int dxy = dx + dy * 65536;
-    int m = 0;
-    cnt[0]++;
-    int xyn = in[min(slot, n - 1)];  // the entries of the next pass are read one pass ahead
-    for (int e0 = 0; e0 < n; e0 += per) {
-      cnt[1]++;
-      const int e = e0 + slot;
-      const bool valid = e < n;
-      const int xy = xyn;
-      xyn = in[min(e + per, n - 1)];
-      const int x = xy & 0xffff, y = xy >> 16;
-      const bool live = valid & (x != 0) & (y != 0) & (x != w1 - 1) & (y != h1 - 1);
-      const int q = live ? (x + dx) + (y + dy) * w1 : 0;
-      const int sh = (q & 3) * 8;
-      uint32_t* wp = reinterpret_cast<uint32_t*>(map + (q & ~3));
-      uint32_t old = *wp;
-      bool want = live & (((old >> sh) & 0xffu) > (uint32_t)k);
-      bool got = false;
-      while (want) {
-        const uint32_t pv = atomicCAS(wp, old, (old & ~(0xffu << sh)) | ((uint32_t)k << sh));
-        got = pv == old;
-        old = pv;
-        want = !got & (((old >> sh) & 0xffu) > (uint32_t)k);
-      }
-      const unsigned long long bm = __ballot(got);
-      if (got)
-        out[m + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u))] =
-            xy + dxy;
-      m += (int)__popcll(bm);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    n = __builtin_amdgcn_readfirstlane(m < HS_ACT_WAVE_LIST ? m : HS_ACT_WAVE_LIST);
-    int* t = in;
-    in = out;
-    out = t;
+// addIntoDistFinal without a BFS.  growDistBFS from one seed takes 8-neighbour steps at odd k and 4-neighbour steps
+// at even k, so an unobstructed cell at (dx, dy) is first reached at the smallest k with max(|dx|, |dy|) <= k and
+// |dx| + |dy| <= k + ceil(k / 2): k = max(M, (2 L + 1) / 3).  With the map before the call being a union of such
+// waves, the pruned BFS leaves every interior cell at min(map, k) (k <= 39), and a border cell (never expanded)
+// at min(map, k_n + 1) over its interior neighbours n whose value the wave lowered (k_n < map(n), or n the seed),
+// a diagonal move only on an odd step k_n + 1; a seed on the border only sets itself.  Checked against the
+// reference's growDistBFS on random maps and seed sequences, every cell of every map
+// (tests/test_act.py::test_closed_form_bfs_matches_grow_dist_bfs).
+__device__ __forceinline__ int bfs_dist(int dx, int dy) {
+  dx = abs(dx);
+  dy = abs(dy);
+  return max(max(dx, dy), (2 * (dx + dy) + 1) / 3);
+}
+
+// the interior neighbours of a border cell (x == w1 - 1 or y == h1 - 1; x, y > 0) as packed cells, -1 = none
+__device__ __forceinline__ void border_nbrs(int x, int y, int w1, int h1, int nb[3]) {
+  int cx[3], cy[3];
+  if (x == w1 - 1) {
+    cx[0] = cx[1] = cx[2] = x - 1;
+    cy[0] = y - 1; cy[1] = y; cy[2] = y + 1;
+  } else {
+    cy[0] = cy[1] = cy[2] = y - 1;
+    cx[0] = x - 1; cx[1] = x; cx[2] = x + 1;
+  }
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    const bool in = cx[i] >= 1 && cx[i] <= w1 - 2 && cy[i] >= 1 && cy[i] <= h1 - 2;
+    nb[i] = in ? (cx[i] | (cy[i] << 16)) : -1;
   }
 }
 
-// bfs_grow_wave for the LDS map with claim bits: every writer of step k stores the same byte k, so the lowering is a
-// plain byte store (no compare-and-swap retries when lanes hit the same word) and the one lane that appends the
-// cell to the next frontier is the one whose ds_or sets its claim bit; a cell's bit is cleared when its entry is
-// expanded (the last frontier's at the end), so every bit is zero between calls.  The pass is branch-free: the
-// lanes that do not lower / clear / append address a dummy word (claim[cwords]) or or / and a no-op mask.
-__device__ __forceinline__ void bfs_grow_wave_claim(uint8_t* map, int w1, int h1, int* in, int* out, int n,
-                                                    long long* cnt, uint32_t* claim, uint32_t* dummy) {
-  const int lane = threadIdx.x & 63;
-  const int sub8 = lane & 7, sub4 = lane & 3;
-  const int dx8 = (sub8 == 0 || sub8 == 4 || sub8 == 7) ? 1 : ((sub8 == 1 || sub8 == 5 || sub8 == 6) ? -1 : 0);
-  const int dy8 = (sub8 == 2 || sub8 == 4 || sub8 == 5) ? 1 : ((sub8 == 3 || sub8 == 6 || sub8 == 7) ? -1 : 0);
-  const int dx4 = sub4 == 0 ? 1 : (sub4 == 1 ? -1 : 0);
-  const int dy4 = sub4 == 2 ? 1 : (sub4 == 3 ? -1 : 0);
-  uint8_t* dummy_byte = reinterpret_cast<uint8_t*>(dummy);
-  int* dummy_int = reinterpret_cast<int*>(dummy);
-  n = __builtin_amdgcn_readfirstlane(n);
-  for (int k = 1; k < HS_ACT_BFS_STEPS && n > 0; k++) {
-    const bool diag = (k & 1) != 0;
-    const int slot = diag ? lane >> 3 : lane >> 2;
-    const int per = diag ? 8 : 16;
-    const int dx = diag ? dx8 : dx4, dy = diag ? dy8 : dy4;
-    const int dxy = dx + dy * 65536;
-    const int doff = dx + dy * w1;
-    const bool lead = (diag ? sub8 : sub4) == 0;  // the lane that releases its entry's claim
-    int m = 0;
-    cnt[0]++;
-    int xyn = in[min(slot, n - 1)];  // the entries of the next pass are read one pass ahead
-    for (int e0 = 0; e0 < n; e0 += per) {
-      cnt[1]++;
-      const int e = e0 + slot;
-      const bool valid = e < n;
-      const int xy = xyn;
-      xyn = in[min(e + per, n - 1)];
-      const int x = xy & 0xffff, y = xy >> 16;
-      const bool live = valid & (x != 0) & (y != 0) & (x != w1 - 1) & (y != h1 - 1);
-      const int base = (int)__umul24((unsigned)y, (unsigned)w1) + x;
-      const int q = live ? base + doff : 0;
-      const uint32_t old = *reinterpret_cast<const uint32_t*>(map + (q & ~3));
-      const bool want = live & (((old >> ((q & 3) * 8)) & 0xffu) > (uint32_t)k);
-      atomicAnd(&claim[base >> 5], (valid & lead) ? ~(1u << (base & 31)) : ~0u);
-      *(want ? map + q : dummy_byte) = (uint8_t)k;
-      const uint32_t bit = want ? 1u << (q & 31) : 0u;
-      const bool got = want & ((atomicOr(&claim[q >> 5], bit) & bit) == 0u);
-      const unsigned long long bm = __ballot(got);
-      *(got ? out + m + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u))
-            : dummy_int) = xy + dxy;
-      m += (int)__popcll(bm);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    n = __builtin_amdgcn_readfirstlane(m < HS_ACT_WAVE_LIST ? m : HS_ACT_WAVE_LIST);
-    int* t = in;
-    in = out;
-    out = t;
+// one addIntoDistFinal from seed s applied to a border cell (value v) with interior neighbour values nv, limit r
+__device__ __forceinline__ void border_step(int x, int y, int s, int r, const int nb[3], int& v, int nv[3]) {
+  const int sx = s & 0xffff, sy = s >> 16;
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    if (nb[i] < 0) continue;
+    const int nx = nb[i] & 0xffff, ny = nb[i] >> 16;
+    const int dn = bfs_dist(nx - sx, ny - sy);
+    const int t = dn + 1;
+    const bool diag = (nx != x) & (ny != y);
+    if ((dn < nv[i] || nb[i] == s) && t <= r && (!diag || (t & 1))) v = min(v, t);
+    if (dn <= r) nv[i] = min(nv[i], dn);
   }
-  // the last frontier is never expanded: release its claims
-  for (int e = lane; e < n; e += 64) {
-    const int xy = in[e];
-    const int qe = (xy & 0xffff) + w1 * (xy >> 16);
-    atomicAnd(&claim[qe >> 5], ~(1u << (qe & 31)));
-  }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
 }
 
-// seeds taken in one round of the greedy loop: at most kMaxSeeds (their BFS frontiers share the wave list:
-// 6 x a step-39 ring of 312 cells < HS_ACT_WAVE_LIST), pairwise at Chebyshev distance >= kSeedSep (2 x 39 + 2)
-constexpr int kMaxSeeds = 6;
-constexpr int kSeedSep = 2 * (HS_ACT_BFS_STEPS - 1) + 2;
+__device__ __forceinline__ uint32_t ld_word(const uint8_t* map, int w) {
+  return __hip_atomic_load(reinterpret_cast<const uint32_t*>(map) + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int ld_cell(const uint8_t* map, int q) {
+  const uint32_t b = (ld_word(map, q >> 2) >> ((q & 3) * 8)) & 0xffu;
+  return b == 255u ? 1000 : (int)b;
+}
 
-// makeDistanceMap's BFS (whole workgroup), then the selection loop (wave 0).  Inlined once per map location so
-// the LDS instance compiles to ds_* instructions.
-__device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* map, int* s_n, int* wl0, int* wl1,
-                                           uint32_t* claim = nullptr, uint32_t* dummy = nullptr) {
-  int* in = a.list_a;
-  int* out = a.list_b;
-  bfs_grow_wg(map, a.w1, a.h1, in, out, s_n);
-  if (threadIdx.x >= 64) return 0;  // the greedy loop is sequential: wave 0 alone
-  if (a.prof && threadIdx.x == 0) {
+// makeDistanceMap's BFS (whole workgroup), then the selection loop in batches of 64 entries: wave 0 takes, in loop
+// order, every entry whose distance passes, updating the rest of the batch from each new seed in registers; then
+// the whole workgroup folds the batch's seeds into the working map.  The working map only has to decide the test
+// dist + frac >= thr (thr <= T = the largest threshold of the call): it is kept exact up to r = ceil(T) - 1 (seed
+// patches of radius r; cells farther away keep a larger value, which passes every test anyway), and the exact
+// map is formed afterwards by hs_k_act_final.
+__device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* map, int* s_n, int* s_seeds,
+                                           float* s_red) {
+  const int tid = threadIdx.x, nthr = blockDim.x;
+  const int w1 = a.w1, h1 = a.h1, wh1 = w1 * h1;
+  {
+    int* in = a.list_a;
+    int* out = a.list_b;
+    bfs_grow_wg(map, w1, h1, in, out, s_n);
+  }
+  // map0 for the final map; the largest threshold of the pending entries
+  for (int w = tid; w < (wh1 + 3) / 4; w += nthr)
+    reinterpret_cast<uint32_t*>(a.map0)[w] = ld_word(map, w);
+  float tmax = 0.f;
+  bool tnan = false;
+  for (int j = tid; j < a.m; j += nthr)
+    if (a.cand[j] == HS_CAND_PENDING) {
+      const float t = a.thr[j];
+      tnan |= !(t == t);
+      tmax = fmaxf(tmax, t);
+    }
+  for (int o = 32; o > 0; o >>= 1) {
+    tmax = fmaxf(tmax, __shfl_xor(tmax, o));
+    tnan |= __shfl_xor((int)tnan, o) != 0;
+  }
+  if ((tid & 63) == 0) s_red[tid >> 6] = tnan ? 1e30f : tmax;
+  __syncthreads();
+  float T = 0.f;
+  for (int i = 0; i < nthr / 64; i++) T = fmaxf(T, s_red[i]);
+  const int r = T >= 40.f ? HS_ACT_BFS_STEPS - 1 : max(0, (int)ceilf(T) - 1);
+  if (a.prof && tid == 0) {
     a.prof[1] = wall_clock64();
     a.prof[6] = clock64();
   }
-  const int lane = threadIdx.x;
+  const int lane = tid & 63;
+  const bool w0 = tid < 64;
   int nt = 0;
-  long long cnt[3] = {0, 0, 0};
-  // candidate batches of 64, the next batch's loads in flight while the current one is processed: every load is
-  // unconditional (clamped index) and nothing tests a loaded value before the next batch, so no wait sits at the
-  // prefetch (a per-entry "pending ? load : 0" made the compiler branch around each load and drain the queue)
-  int j = lane;
+  long long npatch = 0;
+  // wave 0's candidate batches of 64, the next batch's loads in flight while the current one is processed
   unsigned int ncand = 0u;
   int ncell = 0, npt = 0;
-  float nfrac = 0.f, nthr = 0.f;
+  float nfrac = 0.f, nthr_ = 0.f;
   auto fetch = [&](int jj) {
     const int jc = max(0, min(jj, a.m - 1));
     ncand = a.cand[jc];
     ncell = a.cell[jc];
     npt = a.order ? a.order[jc] : jc;
     nfrac = a.frac[jc];
-    nthr = a.thr[jc];
+    nthr_ = a.thr[jc];
   };
-  if (a.m > 0) fetch(j);
+  if (w0 && a.m > 0) fetch(lane);
+  const int rows = 2 * r + 1, wpr = (2 * r + 1 + 3) / 4 + 1, per_seed = rows * wpr;
   for (int base = 0; base < a.m; base += 64) {
-    bool pend = (base + lane < a.m) && ncand == HS_CAND_PENDING;
-    const int cell = pend ? ncell : 0;
-    const int cidx = xy_index(cell, a.w1);
-    const float frac = nfrac, thr = nthr;
-    const int pt = npt;
-    j = base + 64 + lane;
-    fetch(j);
-    int myslot = -1;  // this lane's place in toopt when it is taken (stored once after the batch: no global store
-                      // inside the round loop, whose completion a later wait would have to drain)
-    for (;;) {
-      // dist = fwdWarpedIDDistFinal[u + w1 * v] + (ptp[0] - floorf(ptp[0])) >= currentMinActDist * my_type
-      const bool acc = pend && (decode(map[cidx]) + frac >= thr);
-      const unsigned long long bm = __ballot(acc);
-      if (bm == 0) break;  // every remaining entry of the batch fails: they stay immature
-      const int first = (int)__builtin_ctzll(bm);
-      // The first passing entry is taken, as in the reference.  Later passing entries of the batch are taken in
-      // the same round while each is provably unaffected by the round's earlier seeds: at Chebyshev distance
-      // >= kSeedSep from all of them (their addIntoDistFinal BFS regions, radius <= 39, are disjoint, so one
-      // multi-seed BFS leaves the map the sequential BFS passes leave) and with cheb + frac >= thr (a BFS
-      // distance is >= the Chebyshev distance, so its own test still passes after those seeds).  Entries that
-      // fail now stay failing (the map only decreases); the first passing entry that is not provably
-      // unaffected ends the round.
-      unsigned long long take = 1ull << first;
-      {
-        int sc[kMaxSeeds];
-        sc[0] = __shfl(cell, first);
-        int ns = 1;
-        unsigned long long rest = bm & ~((2ull << first) - 1ull);
-        while (rest && ns < kMaxSeeds) {
-          const int c = (int)__builtin_ctzll(rest);
-          const int cc = __shfl(cell, c);
-          const float cf = __shfl(frac, c), ct = __shfl(thr, c);
-          bool ok = true;
-          for (int q = 0; q < ns; q++) {
-            const int ddx = abs((cc & 0xffff) - (sc[q] & 0xffff)), ddy = abs((cc >> 16) - (sc[q] >> 16));
-            const int ch = ddx > ddy ? ddx : ddy;
-            ok = ok && ch >= kSeedSep && ((float)ch + cf >= ct);
-          }
-          if (!ok) break;
-          sc[ns++] = cc;
-          take |= 1ull << c;
-          rest &= rest - 1ull;
+    if (w0) {
+      bool pend = (base + lane < a.m) && ncand == HS_CAND_PENDING;
+      const int cell = pend ? ncell : (1 | (1 << 16));
+      const float frac = nfrac, thr = nthr_;
+      const int pt = npt;
+      fetch(base + 64 + lane);
+      const int x = cell & 0xffff, y = cell >> 16;
+      const bool border = (x == w1 - 1) | (y == h1 - 1);
+      int v = ld_cell(map, x + w1 * y);
+      int nb[3], nv[3] = {1000, 1000, 1000};
+      border_nbrs(x, y, w1, h1, nb);
+      if (border) {
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+          if (nb[i] >= 0) nv[i] = ld_cell(map, (nb[i] & 0xffff) + w1 * (nb[i] >> 16));
+      }
+      int myslot = -1, ns = 0;
+      for (;;) {
+        // dist = fwdWarpedIDDistFinal[u + w1 * v] + (ptp[0] - floorf(ptp[0])) >= currentMinActDist * my_type
+        const bool acc = pend && ((float)v + frac >= thr);
+        const unsigned long long bm = __ballot(acc);
+        if (bm == 0) break;  // every remaining entry of the batch fails: they stay immature
+        const int first = (int)__builtin_ctzll(bm);
+        const int sc = __builtin_amdgcn_readfirstlane(__shfl(cell, first));
+        if (lane == first) {
+          myslot = nt;
+          a.seeds[nt] = sc;
+        }
+        if (lane == 0) s_seeds[ns] = sc;
+        ns++;
+        nt++;
+        if (lane <= first) pend = false;
+        // addIntoDistFinal(sc) on the batch's later entries
+        const int sx = sc & 0xffff, sy = sc >> 16;
+        if ((sx == w1 - 1) | (sy == h1 - 1)) {  // a border seed only sets its own cell
+          if (cell == sc) v = 0;
+        } else if (!border) {
+          const int d = bfs_dist(x - sx, y - sy);
+          if (d <= HS_ACT_BFS_STEPS - 1) v = min(v, d);
+        } else {
+          border_step(x, y, sc, HS_ACT_BFS_STEPS - 1, nb, v, nv);
         }
       }
-      if (lane <= first) pend = false;
-      const bool mine = (take >> lane) & 1ull;
-      if (mine) {
-        pend = false;
-        const int rank = (int)__popcll(take & ((1ull << lane) - 1ull));
-        myslot = nt + rank;
-        lower_cell(map, cidx, 0);  // addIntoDistFinal: the cell becomes 0 even when it already was
-        wl0[rank] = cell;
-      }
-      const int ntake = (int)__popcll(take);
-      nt += ntake;
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      const long long c0 = a.prof ? wall_clock64() : 0;
-      if (claim) bfs_grow_wave_claim(map, a.w1, a.h1, wl0, wl1, ntake, cnt, claim, dummy);
-      else bfs_grow_wave(map, a.w1, a.h1, wl0, wl1, ntake, cnt);
-      if (a.prof) cnt[2] += wall_clock64() - c0;
+      // one unconditional store per batch (the lanes not taken write their scratch slot toopt[m + lane])
+      a.toopt[myslot >= 0 ? myslot : a.m + lane] = pt;
+      if (lane == 0) s_n[0] = ns;
     }
-    // one unconditional store per batch (the lanes not taken write their scratch slot toopt[m + lane]), so the
-    // compiler counts it and the next batch waits for its loads only
-    a.toopt[myslot >= 0 ? myslot : a.m + lane] = pt;
+    __syncthreads();
+    const int ns = s_n[0];
+    if (ns > 0) {
+      npatch += ns;
+      // the right column / bottom row cells near a seed (the only border cells an entry can sit on), seeds in order
+      for (int i = tid; i < w1 + h1 - 1; i += nthr) {
+        const int x = i < w1 ? i : w1 - 1, y = i < w1 ? h1 - 1 : i - w1;
+        if (x < 1 || y < 1) continue;
+        bool near = false;
+        for (int j = 0; j < ns; j++) {
+          const int sx = s_seeds[j] & 0xffff, sy = s_seeds[j] >> 16;
+          near |= max(abs(x - sx), abs(y - sy)) <= r + 1;
+        }
+        if (!near) continue;
+        int nb[3], nv[3] = {1000, 1000, 1000};
+        border_nbrs(x, y, w1, h1, nb);
+        for (int k = 0; k < 3; k++)
+          if (nb[k] >= 0) nv[k] = ld_cell(map, (nb[k] & 0xffff) + w1 * (nb[k] >> 16));
+        const int q = x + w1 * y;
+        const int v0 = ld_cell(map, q);
+        int v = v0;
+        for (int j = 0; j < ns; j++) {
+          const int sc = s_seeds[j];
+          if (((sc & 0xffff) == w1 - 1) | ((sc >> 16) == h1 - 1)) {
+            if (sc == (x | (y << 16))) v = 0;
+          } else {
+            border_step(x, y, sc, r, nb, v, nv);
+          }
+        }
+        if (v < v0) {  // no other thread writes this byte; the interior pass below runs after the barrier
+          uint32_t* wp = reinterpret_cast<uint32_t*>(map) + (q >> 2);
+          const int sh = (q & 3) * 8;
+          uint32_t old = ld_word(map, q >> 2);
+          for (;;) {
+            const uint32_t nw = (old & ~(0xffu << sh)) | ((uint32_t)v << sh);
+            const uint32_t pv = atomicCAS(wp, old, nw);
+            if (pv == old) break;
+            old = pv;
+          }
+        }
+      }
+      __syncthreads();
+      // interior cells: min(map, k) over each seed's patch of radius r, one 4-cell word per (seed, row, word) item
+      for (int it = tid; it < ns * per_seed; it += nthr) {
+        const int j = it / per_seed, rem = it - j * per_seed;
+        const int row = rem / wpr, wi = rem - row * wpr;
+        const int sc = s_seeds[j], sx = sc & 0xffff, sy = sc >> 16;
+        if ((sx == w1 - 1) | (sy == h1 - 1)) continue;
+        const int y = sy - r + row;
+        const int x0 = max(1, sx - r), x1 = min(w1 - 2, sx + r);
+        if (y < 1 || y > h1 - 2 || x0 > x1) continue;
+        const int rb = y * w1;
+        const int w = ((rb + x0) >> 2) + wi;
+        if (w > ((rb + x1) >> 2)) continue;
+        uint32_t* wp = reinterpret_cast<uint32_t*>(map) + w;
+        uint32_t old = ld_word(map, w);
+        for (;;) {
+          uint32_t nw = old;
+#pragma unroll
+          for (int b = 0; b < 4; b++) {
+            const int xx = w * 4 + b - rb;
+            if (xx < x0 || xx > x1) continue;
+            const int d = bfs_dist(xx - sx, y - sy);
+            const uint32_t cur = (nw >> (8 * b)) & 0xffu;
+            if (d <= r && (uint32_t)d < cur) nw = (nw & ~(0xffu << (8 * b))) | ((uint32_t)d << (8 * b));
+          }
+          if (nw == old) break;
+          const uint32_t pv = atomicCAS(wp, old, nw);
+          if (pv == old) break;
+          old = pv;
+        }
+      }
+    }
+    __syncthreads();
   }
-  if (a.prof && lane == 0) {
-    a.prof[3] = cnt[0];
-    a.prof[4] = cnt[1];
-    a.prof[5] = cnt[2];
+  if (a.prof && tid == 0) {
+    a.prof[3] = (a.m + 63) / 64;
+    a.prof[4] = npatch;
+    a.prof[5] = r;
   }
   return nt;
 }
@@ -428,7 +434,8 @@ __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* ma
 __global__ void __launch_bounds__(1024) hs_k_act_select(HsActSelectArgs a) {
   extern __shared__ uint32_t s_map32[];
   __shared__ int s_n[2];
-  __shared__ int s_wl[2][HS_ACT_WAVE_LIST];
+  __shared__ int s_seeds[64];
+  __shared__ float s_red[16];
   const int words = (a.w1 * a.h1 + 3) / 4;
   if (a.prof && threadIdx.x == 0) a.prof[0] = wall_clock64();
   if (threadIdx.x == 0) s_n[0] = *a.seed_count;
@@ -436,24 +443,69 @@ __global__ void __launch_bounds__(1024) hs_k_act_select(HsActSelectArgs a) {
   if (a.lds_map) {
     const uint32_t* g = reinterpret_cast<const uint32_t*>(a.dist);
     for (int w = threadIdx.x; w < words; w += blockDim.x) s_map32[w] = g[w];
-    uint32_t* claim = s_map32 + words;  // one bit per cell, zero between the BFS calls; then one dummy word
-    const int cwords = (a.w1 * a.h1 + 31) / 32;
-    for (int w = threadIdx.x; w <= cwords; w += blockDim.x) claim[w] = 0u;
     __syncthreads();
-    nt = select_body(a, reinterpret_cast<uint8_t*>(s_map32), s_n, s_wl[0], s_wl[1], claim, claim + cwords);
-    if (threadIdx.x >= 64) return;
-    uint32_t* go = reinterpret_cast<uint32_t*>(a.dist);
-    for (int w = threadIdx.x; w < words; w += 64) go[w] = s_map32[w];
+    nt = select_body(a, reinterpret_cast<uint8_t*>(s_map32), s_n, s_seeds, s_red);
   } else {
     __syncthreads();
-    nt = select_body(a, a.dist, s_n, s_wl[0], s_wl[1]);
-    if (threadIdx.x >= 64) return;
+    nt = select_body(a, a.dist, s_n, s_seeds, s_red);
   }
   if (threadIdx.x == 0) *a.n_toopt = nt;
   if (a.prof && threadIdx.x == 0) {
     a.prof[2] = wall_clock64();
     a.prof[7] = clock64();
   }
+}
+
+// makeDistanceMap's map + every addIntoDistFinal of the greedy loop, in call order (the closed form above): interior
+// cells take the minimum over the seeds; a border cell runs the seeds in order beside its interior neighbours.  The
+// seeds go through LDS in tiles.
+__global__ void __launch_bounds__(256) hs_k_act_final(HsActFinalArgs a) {
+  __shared__ int tile[1024];
+  const int w1 = a.w1, h1 = a.h1;
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = q < w1 * h1;
+  const int x = live ? q % w1 : 1, y = live ? q / w1 : 1;
+  const bool interior = x >= 1 && x <= w1 - 2 && y >= 1 && y <= h1 - 2;
+  auto val = [&](int c) { const uint8_t b = a.map0[c]; return b == 255 ? 1000 : (int)b; };
+  int v = live ? val(q) : 1000;
+  int nb[3] = {-1, -1, -1}, nv[3] = {1000, 1000, 1000};
+  if (live && !interior) {
+    // every neighbour that is interior (a border cell of the top row / left column has them too)
+    int k = 0;
+    for (int dy = -1; dy <= 1; dy++)
+      for (int dx = -1; dx <= 1; dx++) {
+        const int nx = x + dx, ny = y + dy;
+        if ((dx | dy) == 0 || nx < 1 || nx > w1 - 2 || ny < 1 || ny > h1 - 2 || k >= 3) continue;
+        nb[k] = nx | (ny << 16);
+        nv[k] = val(nx + w1 * ny);
+        k++;
+      }
+  }
+  const int ns = *a.n_seeds;
+  const int self = x | (y << 16);
+  for (int t0 = 0; t0 < ns; t0 += 1024) {
+    const int tn = min(1024, ns - t0);
+    __syncthreads();
+    for (int i = threadIdx.x; i < tn; i += blockDim.x) tile[i] = a.seeds[t0 + i];
+    __syncthreads();
+    if (!live) continue;
+    for (int i = 0; i < tn; i++) {
+      const int sc = tile[i];
+      const int sx = sc & 0xffff, sy = sc >> 16;
+      if ((sx == w1 - 1) | (sy == h1 - 1)) {
+        if (sc == self) v = 0;
+        continue;
+      }
+      if (interior) {
+        const int d = bfs_dist(x - sx, y - sy);
+        if (d <= HS_ACT_BFS_STEPS - 1) v = min(v, d);
+      } else {
+        if (sc == self) v = 0;
+        border_step(x, y, sc, HS_ACT_BFS_STEPS - 1, nb, v, nv);
+      }
+    }
+  }
+  if (live) a.dist[q] = v >= 255 ? 255 : (uint8_t)v;
 }
 
 __global__ void __launch_bounds__(256) hs_k_act_optimize(HsActOptArgs a) {

@@ -234,10 +234,33 @@ void compute_projector(hs_ctx* c) {
   nullspace_projector(ns, n, c->P.solverModeDelta, c->Porth, &c->Nproj);
 }
 
+// the device state -> h_state.  After an optimize tail (hs_k_fix_frames) also the host-side rest of it: the newest
+// frame's setStateZero nullspaces (Include/Frame.h:166-190), the projector (fp64 Jacobi SVD, host) -> device, and the
+// fp32 adjoints the device computed -> adHostF / adTargetF (marginalize_points' setDeltaF)
 int fetch_state(hs_ctx* c) {
+  const bool tail = c->tail_pending;
+  const size_t FF = (size_t)c->nF * c->nF;
   HS_HIP(hipMemcpyAsync(c->h_state, c->d_state, sizeof(HsDevState), hipMemcpyDeviceToHost, c->stream));
+  if (tail) {
+    c->adHostF.assign(FF * 64, 0.f);
+    c->adTargetF.assign(FF * 64, 0.f);
+    HS_HIP(hipMemcpyAsync(c->adHostF.data(), c->d_adHostF, sizeof(float) * FF * 64, hipMemcpyDeviceToHost, c->stream));
+    HS_HIP(hipMemcpyAsync(c->adTargetF.data(), c->d_adTargetF, sizeof(float) * FF * 64, hipMemcpyDeviceToHost,
+                          c->stream));
+  }
   HS_HIP(hipStreamSynchronize(c->stream));
   c->h_state_valid = true;
+  if (tail) {
+    c->tail_pending = false;
+    FrameH& f = c->h_state->frames[c->nF - 1];
+    double sz[10];
+    std::memcpy(sz, f.state_zero, sizeof(sz));
+    f.setStateZero(sz);
+    compute_projector(c);
+    HS_HIP(hipMemcpyAsync(c->d_Nproj, c->Nproj.data(), sizeof(double) * 2 * c->dim() * HS_NNS, hipMemcpyHostToDevice,
+                          c->stream));
+    HS_HIP(hipStreamSynchronize(c->stream));
+  }
   return HS_OK;
 }
 
@@ -261,6 +284,7 @@ int upload_frames(hs_ctx* c) {
   HS_TRY(wait_uploads(c));
   HsDevState& S = *c->h_state;
   S.nF = nF;
+  c->tail_pending = false;  // every frame's adjoints, precalc and the projector are rewritten from h_state
   c->adHost.assign(FF * 64, 0.0);
   c->adTarget.assign(FF * 64, 0.0);
   c->adHostF.assign(FF * 64, 0.f);
@@ -389,6 +413,7 @@ static int launch_linearize(hs_ctx* c, int fuse, bool marg = false, bool accumul
   a.newest_cand = c->d_cand + (size_t)c->rank * c->cand_stride;
   a.part = c->d_part; a.part_e = c->d_part_e;
   a.trace = c->d_tr_lin;
+  a.brk = c->brk_active ? 1 : 0;
   if (c->nblk > 0) {
     if (c->lin8 && !marg && !fix) {
       hipLaunchKernelGGL(hs_k_lin8, dim3(c->nblk), dim3(HS_LIN8_NT), 0, c->stream, a);
@@ -425,6 +450,10 @@ static HsRedArgs red_args(hs_ctx* c, bool skip_threshold) {
   a.nhist = a.np2 = std::min(64, std::max(1, (c->nranks * c->cand_stride + 4095) / 4096));
   a.trace = c->d_tr_acc;
   return a;
+}
+
+static const int* stop_flag(hs_ctx* c) {
+  return reinterpret_cast<const int*>((const char*)c->d_state + offsetof(HsDevState, stop));
 }
 
 // what a solve launch would have done beside the solve, when none follows: hs_k_combine's block 0 sums the gathered
@@ -485,6 +514,7 @@ static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = fals
                          bool defer = false) {
   const bool xch = c->multi_rank() && !readback;
   HsRedArgs a = red_args(c, skip_threshold);
+  if (c->brk_active) a.stop = stop_flag(c);
   // setNewFrameEnergyTH: windows below kLin8MinPoints (and every multi-rank window) select in block 1 of the next
   // solve launch (or hs_k_combine), beside the solve: the select only feeds the next linearize, and as the stitch
   // launch's last block it outlasted the stitch's blocks by ~1.5 us at 2k.  Large single-rank windows: pass 1 in
@@ -541,6 +571,7 @@ static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = fals
 }
 
 static int launch_solve(hs_ctx* c, int flags, int iteration, bool log) {
+  if (c->tail_pending) HS_TRY(fetch_state(c));  // the projector of the moved newest frame
   HsSolveArgs a;
   std::memset(&a, 0, sizeof(a));
   a.flags = flags;
@@ -575,6 +606,8 @@ static int launch_solve(hs_ctx* c, int flags, int iteration, bool log) {
   a.trace = c->d_tr_solve;
   a.initialCalibHessian = c->P.initialCalibHessian;
   a.thOptIterations = c->P.thOptIterations;
+  a.brk = c->brk_active ? 1 : 0;
+  a.minOpt = c->P.minOptIterations;
   if (const char* e = std::getenv("HS_SOLVE_DBG")) a.dbg = std::atoi(e);
   hipLaunchKernelGGL(hs_k_solve, dim3(grid), dim3(HS_SOLVE_NT), 0, c->stream, a);
   HS_HIP(hipGetLastError());
@@ -685,7 +718,8 @@ static int dump_traces(hs_ctx* c) {
 
 // K fused GN iterations continuing from the current (stitched) linearization.
 // energies_out[k] = energy of the linearization after iteration k.
-static int gn_iterations(hs_ctx* c, int it0, int K, bool allow_break, double* energies_out, int* done) {
+static int gn_iterations(hs_ctx* c, int it0, int K, bool allow_break, double* energies_out, int* done,
+                         double* e0 = nullptr) {
   if (K > kLogCap - 1) return fail(HS_ERR_INVALID, "too many iterations per call");
   int k = 0;
   const int nev = c->events ? std::min(K, kEventIters) : 0;
@@ -694,6 +728,12 @@ static int gn_iterations(hs_ctx* c, int it0, int K, bool allow_break, double* en
   // collectives inside a capture)
   const char* ge = std::getenv("HS_GRAPH");
   const bool graph = (ge && ge[0] == '1') && !allow_break && nev == 0 && !c->tracing && !c->multi_rank() && K >= 2;
+  // allow_break on one rank: the break test runs on the device (hs_k_solve), so the K iterations are enqueued with
+  // no host round trip between them; launches after the break return at entry.  Multi-rank windows, tracing and
+  // HS_HOST_BREAK=1 read canbreak back after every iteration instead.
+  const char* hb = std::getenv("HS_HOST_BREAK");
+  const bool dev_brk = allow_break && !c->multi_rank() && !c->tracing && !(hb && hb[0] == '1');
+  if (c->tail_pending) HS_TRY(fetch_state(c));  // before any capture: launch_solve must not sync inside one
   HS_TRY(set_loop_counters(c, it0, !graph));
   if (graph) {
     if (c->gexec && c->graph_hdif != c->d_p_HdiF) drop_graph(c);
@@ -728,17 +768,23 @@ static int gn_iterations(hs_ctx* c, int it0, int K, bool allow_break, double* en
     }
     for (; k + 2 <= K; k += 2) HS_HIP(hipGraphLaunch(c->gexec, c->stream));
   }
+  c->brk_active = dev_brk;
   for (; k < K; k++) {
     const bool timed = k < nev;
     if (timed && all) HS_HIP(hipEventRecord(c->ev[4 * k + 0], c->stream));
-    HS_TRY(launch_solve(c, HS_SOLVE | HS_APPLY, -1, true));
-    if (timed) HS_HIP(hipEventRecord(c->ev[4 * k + 1], c->stream));
-    HS_TRY(launch_linearize(c, 1));
-    if (timed) HS_HIP(hipEventRecord(c->ev[4 * k + 2], c->stream));
-    // multi-rank: the next iteration's solve launch sums the gathered systems and selects the threshold
-    HS_TRY(launch_reduce(c, false, false, false, k + 1 < K && !allow_break));
-    if (timed && all) HS_HIP(hipEventRecord(c->ev[4 * k + 3], c->stream));
-    if (allow_break) {
+    int rc = launch_solve(c, HS_SOLVE | HS_APPLY, -1, true);
+    if (rc == HS_OK && timed) rc = hipEventRecord(c->ev[4 * k + 1], c->stream) == hipSuccess ? HS_OK : HS_ERR_HIP;
+    if (rc == HS_OK) rc = launch_linearize(c, 1);
+    if (rc == HS_OK && timed) rc = hipEventRecord(c->ev[4 * k + 2], c->stream) == hipSuccess ? HS_OK : HS_ERR_HIP;
+    // the next iteration's solve launch sums the gathered systems (multi-rank) and selects the threshold
+    if (rc == HS_OK) rc = launch_reduce(c, false, false, false, (k + 1 < K && !allow_break) || dev_brk);
+    if (rc == HS_OK && timed && all)
+      rc = hipEventRecord(c->ev[4 * k + 3], c->stream) == hipSuccess ? HS_OK : HS_ERR_HIP;
+    if (rc != HS_OK) {
+      c->brk_active = false;
+      return rc == HS_ERR_HIP ? fail(HS_ERR_HIP, "event record failed") : rc;
+    }
+    if (allow_break && !dev_brk) {
       int cb = 0;
       HS_HIP(hipMemcpyAsync(&c->h_ctl[3], (char*)c->d_state + offsetof(HsDevState, canbreak), sizeof(int),
                             hipMemcpyDeviceToHost, c->stream));
@@ -750,14 +796,26 @@ static int gn_iterations(hs_ctx* c, int it0, int K, bool allow_break, double* en
       }
     }
   }
+  c->brk_active = false;
   c->haveSystem = true;
   if (c->pending_reset >= 0) HS_TRY(set_loop_counters(c, it0));  // K == 0: no solve took the reset
   c->pending_reset = -1;
+  if (dev_brk) HS_TRY(launch_combine(c));  // the last linearization's deferred threshold select
   // read back: energy log (E of the linearizations consumed by each solve) + the last energy + status, written by
   // one small kernel straight into pinned host memory
-  hipLaunchKernelGGL(hs_k_result, dim3(1), dim3(256), 0, c->stream, c->d_elog, k, c->sysE(), c->d_state, c->d_res);
+  hipLaunchKernelGGL(hs_k_result, dim3(1), dim3(256), 0, c->stream, c->d_elog, k, c->sysE(), c->d_state, c->d_res,
+                     dev_brk ? 1 : 0, kLogCap + 1);
   HS_HIP(hipGetLastError());
   HS_HIP(hipStreamSynchronize(c->stream));
+  if (dev_brk) {  // launch_linearize swapped the HdiF ping-pong for every launch; the skipped ones wrote nothing
+    const int d = (int)c->h_res[kLogCap + 1];
+    if ((k - d) & 1) {
+      std::swap(c->d_p_HdiF, c->d_p_HdiF_alt);
+      c->hdif_solved = c->d_p_HdiF_alt;
+    }
+    k = d;
+  }
+  if (e0) *e0 = c->h_res[0];
   std::vector<double> elog(c->h_res, c->h_res + k + 1);
   c->h_ctl[1] = (int)c->h_res[k + 1];
   double tl = 0, ta = 0, ts = 0;
@@ -1164,13 +1222,8 @@ int hs_ba_optimize(hs_ctx* c, int max_iters, int allow_break, double* energies_o
   HS_TRY(linearize_pass(c, true));
   int done = 0;
   std::vector<double> e(max_iters + 1, 0.0);
-  HS_TRY(gn_iterations(c, 0, max_iters, allow_break != 0, e.data() + 1, &done));
-  // energy of the initial linearization = the first logged energy
-  if (done > 0) {
-    HS_HIP(hipMemcpy(&e[0], c->d_elog, sizeof(double), hipMemcpyDeviceToHost));
-  } else {
-    HS_HIP(hipMemcpy(&e[0], c->sysE(), sizeof(double), hipMemcpyDeviceToHost));
-  }
+  // e[0]: the energy of the initial linearization (the first logged energy; with no iteration, the current one)
+  HS_TRY(gn_iterations(c, 0, max_iters, allow_break != 0, e.data() + 1, &done, &e[0]));
   c->t_wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (energies_out) std::memcpy(energies_out, e.data(), sizeof(double) * std::min(done + 1, cap));
   if (iters_done) *iters_done = done;
@@ -1200,7 +1253,7 @@ int hs_ba_fix_linearization(hs_ctx* c, double* energy_out, uint8_t* drop_out, fl
   if ((maxRelBaseline == nullptr) != (numGoodResiduals == nullptr))
     return fail(HS_ERR_INVALID, "maxRelBaseline and numGoodResiduals go together");
   HS_HIP(hipSetDevice(c->device));
-  const int nF = c->nF, nP = c->nP;
+  const int nP = c->nP;
   // pinned staging of the read-backs: HdiF [nP] floats, then the active flags [nP][8]; one sync for all of them
   HS_HIP(c->rb_stage(sizeof(float) * (size_t)nP + (size_t)nP * 8));
   c->rb_pending = true;  // cleared after the stream sync below; an early return leaves it for the next rb_stage
@@ -1209,17 +1262,13 @@ int hs_ba_fix_linearization(hs_ctx* c, double* energy_out, uint8_t* drop_out, fl
   // HdiF of the last solve, before this pass relinearizes
   if (HdiF_out && nP > 0)
     HS_HIP(hipMemcpyAsync(h_hdif, c->hdif_solved, sizeof(float) * nP, hipMemcpyDeviceToHost, c->stream));
-  HS_TRY(fetch_state(c));
-  HsDevState& S = *c->h_state;
-  {  // newStateZero = 0 except segment(6, 2) = the newest frame's a / b; setEvalPT(PRE_worldToCam, newStateZero)
-    hs::FrameH& f = S.frames[nF - 1];
-    double nsz[10] = {0, 0, 0, 0, 0, 0, f.state[6], f.state[7], 0, 0};
-    f.evalPT = f.PRE_worldToCam;
-    f.setState(nsz);
-    f.setStateZero(nsz);
-    f.takeData(c->P);
-  }
-  HS_TRY(upload_frames(c));  // EnergyFunctional::setAdjointsF, setPrecalcValues, the moved nullspaces
+  // the newest frame's setEvalPT + EnergyFunctional::setAdjointsF + setPrecalcValues, on the device (the nullspaces
+  // and projector follow on the host when the state is next fetched)
+  hipLaunchKernelGGL(hs_k_fix_frames, dim3(1), dim3(64), 0, c->stream, c->d_state, c->d_pre, c->d_adHost,
+                     c->d_adTarget, c->d_adHostF, c->d_adTargetF, c->P);
+  HS_HIP(hipGetLastError());
+  c->h_state_valid = false;
+  c->tail_pending = true;
   if (nP > 0) {
     if (maxRelBaseline) {
       HS_HIP(hipMemcpyAsync(c->d_fix_relBL, maxRelBaseline, sizeof(float) * nP, hipMemcpyHostToDevice, c->stream));

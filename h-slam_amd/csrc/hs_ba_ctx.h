@@ -129,6 +129,9 @@ struct hs_ctx {
   int img_slot[HS_MAXF] = {0, 1, 2, 3, 4, 5, 6, 7};  // window frame -> image slot
   HsDevState* h_state = nullptr;  // pinned staging of the device state
   bool h_state_valid = false;     // h_state equals the device state (no solve since the last fetch / upload)
+  bool brk_active = false;        // gn_iterations' device-side break: the launches carry the stop checks
+  bool tail_pending = false;      // hs_k_fix_frames moved the newest frame on the device: its nullspaces, the
+                                  // projector and the host adjoint copies follow at the next fetch_state
   int* h_ctl = nullptr;           // pinned: iteration, status, log_count
   bool haveSystem = false;        // a stitched, not yet solved system is in the slots
 

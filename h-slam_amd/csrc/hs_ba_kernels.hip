@@ -710,6 +710,7 @@ __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
   extern __shared__ float lin_stage[];  // [HS_LIN_NW waves][ne][64] fp32 partials, then [HS_LIN_NW][3] fp64 energies
   // the wave index as a scalar: the point index and everything per point then stays uniform (scalar loads,
   // scalar branches) instead of being treated as divergent
+  if (a.brk && a.st->stop) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int b = blockIdx.x;
   int h = 0;  // the block's host: from the kernel-argument block boundaries, no load
@@ -1227,6 +1228,7 @@ __device__ __forceinline__ void red_host_chunk(const HsRedArgs& a, int h, int q)
 }
 
 __global__ __launch_bounds__(256) void hs_k_reduce(HsRedArgs a) {
+  if (a.stop && *a.stop) return;
   const int nred = a.nF * a.Q;
   const int b = blockIdx.x;
   if (a.hist_only) {  // multi-rank large windows: pass 1 over the all-gathered candidates
@@ -1243,11 +1245,13 @@ __global__ __launch_bounds__(256) void hs_k_reduce(HsRedArgs a) {
 // the multi-block pass 2 alone (test hook hs_debug_threshold; production runs it inside the stitch launch)
 __global__ __launch_bounds__(HS_STITCH_NT) void hs_k_th_pass2(HsRedArgs a) {
   __shared__ unsigned int sm[1600 + TH_CAP];
+  if (a.stop && *a.stop) return;
   red_th_pass2_block(a, blockIdx.x, sm);
 }
 
 __global__ __launch_bounds__(HS_STITCH_NT) void hs_k_th_select(HsRedArgs a) {
   __shared__ unsigned int sm[1600 + TH_CAP];
+  if (a.stop && *a.stop) return;
   red_energy_th_block(a, sm);
 }
 
@@ -1703,6 +1707,7 @@ __device__ __forceinline__ void stitch_block(const HsStitchArgs& a, int j, doubl
 
 __global__ __launch_bounds__(ST_NT) void hs_k_stitch(HsStitchArgs a) {
   __shared__ double lds[ST_LDS];
+  if (a.red.stop && *a.red.stop) return;
   stitch_block(a, blockIdx.x, lds);
 }
 
@@ -2055,7 +2060,14 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
   static_assert(sizeof(HsDevState) % 8 == 0, "HsDevState is copied as 8-byte words");
   HsDevState* st = reinterpret_cast<HsDevState*>(st_raw);
   const int tid = threadIdx.x, nt = SOLVE_NT;
-  if (blockIdx.x == 1) {  // multi-rank: setNewFrameEnergyTH over the gathered candidates, beside the solve
+  if (a.brk && a.reset_it < 0 && blockIdx.x == 0) {
+    const HsDevState* g = a.st;
+    if (g->stop || (g->log_count > 0 && g->canbreak && g->iteration - 1 >= a.minOpt)) {
+      if (tid == 0) a.st->stop = 1;  // every thread stops whichever value of stop it read
+      return;
+    }
+  }
+  if (blockIdx.x == 1) {  // setNewFrameEnergyTH over the (gathered) candidates, beside the solve
     th_select_block(a.th, reinterpret_cast<unsigned int*>(A), SOLVE_TH_CAP, true);
     return;
   }
@@ -2190,6 +2202,7 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
       st->iteration = a.reset_it;
       st->status = 0;
       st->log_count = 0;
+      st->stop = 0;
     }
     s_it = a.iteration >= 0 ? a.iteration : st->iteration;
   }
@@ -2529,11 +2542,17 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_combine(HsSolveArgs a) {
   }
 }
 
-__global__ void hs_k_result(const double* elog, int k, const double* sysE, const HsDevState* st, double* out) {
+// brk (optimize's device-side break): the iterations done are the solves that ran (st->log_count), written to
+// out[done_slot]; st->stop is cleared for the next call
+__global__ void hs_k_result(const double* elog, int k, const double* sysE, HsDevState* st, double* out, int brk,
+                            int done_slot) {
+  if (brk) k = min(k, st->log_count);
   for (int i = threadIdx.x; i < k; i += blockDim.x) out[i] = elog[i];
   if (threadIdx.x == 0) {
     out[k] = sysE[0];
     out[k + 1] = (double)st->status;
+    out[done_slot] = (double)k;
+    if (brk) st->stop = 0;
   }
 }
 
@@ -2550,6 +2569,34 @@ __global__ void hs_k_resub(HsResubArgs a) {
     const float nid = a.idepth[p] + 1.0f * step;
     a.idepth[p] = nid;
     a.idepth_zero[p] = nid;
+  }
+}
+
+__global__ void hs_k_fix_frames(HsDevState* st, HsPrecalc* pre, double* adH, double* adT, float* adHF, float* adTF,
+                                hs_params P) {
+  const int nF = st->nF, tid = threadIdx.x;
+  if (tid == 0) {  // newStateZero = 0 except segment(6, 2) = the newest frame's a / b; setEvalPT(PRE_worldToCam, .)
+    hs::FrameH& f = st->frames[nF - 1];
+    double nsz[10] = {0, 0, 0, 0, 0, 0, f.state[6], f.state[7], 0, 0};
+    f.evalPT = f.PRE_worldToCam;
+    f.setState(nsz);
+    for (int i = 0; i < 10; i++) f.state_zero[i] = nsz[i];  // setStateZero's nullspaces: on the host, when read
+    f.takeData(P);
+  }
+  __syncthreads();
+  for (int idx = tid; idx < nF * nF; idx += blockDim.x) {  // idx = h + t nF (adjoints); precalc at h nF + t
+    const int h = idx % nF, t = idx / nF;
+    const hs::FrameH& H = st->frames[h];
+    const hs::FrameH& T = st->frames[t];
+    pre[h * nF + t] = hs::make_precalc(H, T, st->calib);
+    double AH[64], AT[64];
+    hs::make_adjoints(H, T, AH, AT);
+    for (int i = 0; i < 64; i++) {
+      adH[(size_t)idx * 64 + i] = AH[i];
+      adT[(size_t)idx * 64 + i] = AT[i];
+      adHF[(size_t)idx * 64 + i] = (float)AH[i];
+      adTF[(size_t)idx * 64 + i] = (float)AT[i];
+    }
   }
 }
 

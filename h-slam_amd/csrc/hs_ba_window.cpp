@@ -349,6 +349,7 @@ int hs_ba_reserve(hs_ctx* c, const hs_camera* cam, int max_points) {
   }
   S.dcal = cal.device();
   c->h_state_valid = true;
+  c->tail_pending = false;
   HS_HIP(hipMemsetAsync(c->d_cand, 0xff, sizeof(float) * (size_t)c->cap_stride * c->nranks, c->stream));
   HS_HIP(hipStreamSynchronize(c->stream));
   return HS_OK;

@@ -145,7 +145,7 @@ struct FrameH {
     M.log(lm);
     for (int k = 0; k < 6; k++) nullspaces_scale[k] = (lp[k] - lm[k]) / (2e-3);
   }
-  void takeData(const hs_params& P) {
+  HS_HD void takeData(const hs_params& P) {
     double p[10] = {0};
     if (id == 0) {
       for (int i = 0; i < 3; i++) p[i] = P.initialTransPrior;

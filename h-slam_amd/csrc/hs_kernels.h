@@ -26,7 +26,9 @@ struct HsDevState {
   int status;               // != 0: non-finite system / step
   int log_count;            // number of energies written to the log
   int canbreak;
-  int pad[3];
+  int stop;                 // optimize's device-side break: set by the first solve launch that stops, read by the
+                            // iteration's other launches (HsLinArgs.brk, HsRedArgs.stop); cleared by hs_k_result
+  int pad[2];
 };
 
 // Per-lane accumulator entries of the fused linearize kernel (hs_k_lin): lane (slot t, pattern k) of a wave
@@ -106,6 +108,7 @@ struct HsLinArgs {
   float* part;
   double* part_e;
   long long* trace;            // nullable: per-block wall-clock checkpoints [grid][16]
+  int brk;                     // optimize's device-side break: return at entry when st->stop is set
 };
 
 // hs_k_reduce: (host, chunk) blocks sum the host's block partials in block order (fp64) into the host sums; + one
@@ -137,6 +140,7 @@ struct HsRedArgs {
   int np2;
   int hist_only;               // hs_k_reduce: only the nhist histogram blocks (multi-rank path, after the exchange)
   long long* trace;
+  const int* stop;             // nullable: &st->stop (optimize's device-side break; the launch returns when set)
 };
 constexpr int HS_TH_BINS = 4096;
 constexpr int HS_TH_SURV = 1 << 20;
@@ -194,6 +198,10 @@ struct HsSolveArgs {
   HsRedArgs th;
   double aux_sc;               // the stitch's sc: the diagonal blocks' host-f Schur terms (after the energies) fold in
   int reset_it;                // >= 0: the first launch of a GN loop call sets iteration = reset_it, status = log_count = 0
+  // optimize's canbreak on the device (Src/FullSystemOptimize.cpp:493): a launch after the call's first stops (block
+  // 0 returns at entry and sets st->stop) when the previous step allowed it (st->canbreak) and the previous
+  // iteration index was >= minOpt; block 1's threshold select runs anyway (same candidates, same result)
+  int brk, minOpt;
 };
 
 struct HsResubArgs {
@@ -225,9 +233,15 @@ __global__ void hs_k_solve(HsSolveArgs a);
 __global__ void hs_k_combine(HsSolveArgs a);
 // the GN loop's results in one zero-copy write to pinned host memory: out[0, k) = elog, out[k] = energy of the last
 // linearization, out[k + 1] = status
-__global__ void hs_k_result(const double* elog, int k, const double* sysE, const HsDevState* st, double* out);   // multi-rank: the gathered systems summed into sys_out (+ block 1: select)
+__global__ void hs_k_result(const double* elog, int k, const double* sysE, HsDevState* st, double* out, int brk,
+                            int done_slot);   // multi-rank: the gathered systems summed into sys_out (+ block 1: select)
 __global__ void hs_k_resub(HsResubArgs a);
 __global__ void hs_k_debug_se3(int op, int n, const double* in, double* out);  // test hook
 __global__ void hs_k_apply_step(int n, const float* step, float* idepth, float* idepth_zero);
+// System::optimize's tail, frame part (Src/FullSystemOptimize.cpp:498-506) on the device: the newest frame's
+// setEvalPT(PRE_worldToCam, (0,..,0, a, b, 0, 0)) + takeData, then setAdjointsF + setPrecalcValues of every pair (one
+// thread per pair).  The nullspaces of the moved frame are left to the host (hs_ctx::frames_stale).  One block of 64.
+__global__ void hs_k_fix_frames(HsDevState* st, HsPrecalc* pre, double* adH, double* adT, float* adHF, float* adTF,
+                                hs_params P);
 __global__ void hs_k_lenergy(int n, const float* idepth, const float* idepth_zero, const float* priorF, float* chunk,
                              double* out);

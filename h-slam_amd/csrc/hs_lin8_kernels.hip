@@ -225,6 +225,7 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
 #if L8_LDS_ACC
   __shared__ float ACC[L8_NW][L8_NACC][64];
 #endif
+  if (a.brk && a.st->stop) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int pl = lane >> 3, t = lane & 7;  // point of the group, target slot
   const int b = blockIdx.x;

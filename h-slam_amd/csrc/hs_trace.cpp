@@ -16,7 +16,7 @@
 #include "hs_pyr_kernels.h"
 
 #define HS_MAXF_ACT 8                        // activation window (nF <= 8 keyframes)
-#define HS_ACT_LDS_MAP_MAX (144 * 1024)     // level-1 distance map + its claim bits in LDS up to this size (+16 KB of lists)
+#define HS_ACT_LDS_MAP_MAX (156 * 1024)     // level-1 distance map in LDS up to this size
 
 namespace hs {
 extern thread_local std::string g_err;
@@ -73,7 +73,7 @@ struct hs_tracer {
   hs_act_frame* d_act_frames = nullptr;
   hs_act_pair* d_act_pairs = nullptr;
   int* d_frame_of_slot = nullptr;
-  int *d_order = nullptr, *d_cell = nullptr, *d_toopt = nullptr;
+  int *d_order = nullptr, *d_cell = nullptr, *d_toopt = nullptr, *d_act_seeds = nullptr;
   uint8_t *d_cand = nullptr, *d_action = nullptr, *d_res_in = nullptr;
   float *d_frac = nullptr, *d_thr = nullptr, *d_act_idepth = nullptr;
   int* d_ap_frame = nullptr;
@@ -184,7 +184,7 @@ void hs_tracer_destroy(hs_tracer* t) {
                   t->d_gradH, t->d_energyTH, t->d_quality, t->d_idmin, t->d_idmax, t->d_uv, t->d_interval,
                   t->d_status, t->d_steps, t->d_counts, t->d_raw, t->d_type, t->d_dist, t->d_list_a,
                   t->d_list_b, t->d_act_cnt, t->d_act_frames, t->d_act_pairs, t->d_frame_of_slot, t->d_order,
-                  t->d_cell, t->d_toopt, t->d_cand, t->d_action, t->d_res_in, t->d_frac, t->d_thr,
+                  t->d_cell, t->d_toopt, t->d_act_seeds, t->d_cand, t->d_action, t->d_res_in, t->d_frac, t->d_thr,
                   t->d_act_idepth, t->d_ap_frame, t->d_ap_u, t->d_ap_v, t->d_ap_id};
   for (void* b : bufs) (void)hipFree(b);
   (void)hipHostFree(t->h_counts);
@@ -390,6 +390,7 @@ static int act_alloc(hs_tracer* t) {
   TR_HIP(hipMalloc((void**)&t->d_order, sizeof(int) * c));
   TR_HIP(hipMalloc((void**)&t->d_cell, sizeof(int) * c));
   TR_HIP(hipMalloc((void**)&t->d_toopt, sizeof(int) * (c + 64)));  // + the greedy loop's 64 scratch slots
+  TR_HIP(hipMalloc((void**)&t->d_act_seeds, sizeof(int) * c));
   TR_HIP(hipMalloc((void**)&t->d_cand, c));
   TR_HIP(hipMalloc((void**)&t->d_action, c));
   TR_HIP(hipMalloc((void**)&t->d_res_in, c));
@@ -529,8 +530,7 @@ int hs_tracer_activate(hs_tracer* t, const float K4[4], int nF, const hs_act_fra
   se.w1 = t->w1;
   se.h1 = t->h1;
   const size_t map_bytes = (size_t)((wh1 + 3) & ~3);
-  const size_t claim_bytes = (size_t)((wh1 + 31) / 32 + 1) * 4;  // the greedy BFS's claim bits + a dummy word
-  se.lds_map = map_bytes + claim_bytes <= HS_ACT_LDS_MAP_MAX ? 1 : 0;
+  se.lds_map = map_bytes <= HS_ACT_LDS_MAP_MAX ? 1 : 0;
   se.order = order ? t->d_order : nullptr;
   se.cand = t->d_cand;
   se.cell = t->d_cell;
@@ -540,16 +540,27 @@ int hs_tracer_activate(hs_tracer* t, const float K4[4], int nF, const hs_act_fra
   se.list_a = t->d_list_a;
   se.list_b = t->d_list_b;
   se.seed_count = t->d_act_cnt;
+  se.map0 = reinterpret_cast<uint8_t*>(t->d_list_b);  // free once the seed BFS is done
+  se.seeds = t->d_act_seeds;
   se.toopt = t->d_toopt;
   se.n_toopt = t->d_act_cnt + 1;
   static const bool prof_on = getenv("HS_ACT_PROF") != nullptr;
   long long* d_prof = nullptr;
   if (prof_on) TR_HIP(hipMalloc((void**)&d_prof, sizeof(long long) * 8));
   se.prof = d_prof;
-  const size_t lds = se.lds_map ? map_bytes + claim_bytes : 0;
+  const size_t lds = se.lds_map ? map_bytes : 0;
   if (lds > 65536)
     TR_HIP(hipFuncSetAttribute((const void*)hs_k_act_select, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(hs_k_act_select, dim3(1), dim3(1024), lds, s, se);
+  TR_HIP(hipGetLastError());
+  HsActFinalArgs fa;
+  fa.w1 = t->w1;
+  fa.h1 = t->h1;
+  fa.map0 = se.map0;
+  fa.seeds = se.seeds;
+  fa.n_seeds = se.n_toopt;
+  fa.dist = t->d_dist;
+  hipLaunchKernelGGL(hs_k_act_final, dim3((wh1 + 255) / 256), dim3(256), 0, s, fa);
   TR_HIP(hipGetLastError());
   int cnt[2] = {0, 0};
   TR_HIP(hipMemcpyAsync(cnt, t->d_act_cnt, sizeof(cnt), hipMemcpyDeviceToHost, s));
@@ -560,8 +571,8 @@ int hs_tracer_activate(hs_tracer* t, const float K4[4], int nF, const hs_act_fra
     TR_HIP(hipMemcpy(pr, d_prof, sizeof(pr), hipMemcpyDeviceToHost));
     TR_HIP(hipFree(d_prof));
     fprintf(stderr, "hs act prof: seed BFS %.1f us, greedy %.1f us (wall_clock64 @100 MHz), %d selected; "
-            "wave BFS: %lld steps, %lld passes, %.1f us; core clock %.0f MHz\n",
-            (pr[1] - pr[0]) * 1e-2, (pr[2] - pr[1]) * 1e-2, n_toopt, pr[3], pr[4], pr[5] * 1e-2,
+            "%lld batches, %lld seed patches of radius %lld; core clock %.0f MHz\n",
+            (pr[1] - pr[0]) * 1e-2, (pr[2] - pr[1]) * 1e-2, n_toopt, pr[3], pr[4], pr[5],
             (double)(pr[7] - pr[6]) / ((pr[2] - pr[1]) * 1e-2));
   }
   if (n_toopt > 0) {

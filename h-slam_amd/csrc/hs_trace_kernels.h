@@ -55,7 +55,6 @@ __global__ void hs_k_trace_count(int n, const uint8_t* status, const int* steps,
 
 // ---- point activation (System::activatePointsMT), hs_act_kernels.hip ----------------------------------------
 #define HS_ACT_BFS_STEPS 40    // growDistBFS: k = 1 .. 39
-#define HS_ACT_WAVE_LIST 2048  // one-seed BFS frontier capacity (a step-k ring holds <= 8k cells)
 
 // candidate states of the selection loop (per entry of the loop order)
 enum { HS_CAND_SKIP = 0, HS_CAND_DELETE = 1, HS_CAND_PENDING = 2 };
@@ -104,13 +103,24 @@ struct HsActSelectArgs {
   const int* cell;
   const float* frac;
   const float* thr;
-  uint8_t* dist;             // global map (in: seeded, out: final)
+  uint8_t* dist;             // global map (in: seeded; out: the greedy loop's working map, see hs_k_act_final)
   int* list_a;               // [w1*h1] frontier lists
   int* list_b;
   const int* seed_count;
+  uint8_t* map0;             // [w1*h1] out: makeDistanceMap's map (the multi-source BFS), for hs_k_act_final
+  int* seeds;                // [m] out: the cells addIntoDistFinal was called on, in call order
   int* toopt;                // [m] points to optimize, in order (+ 64 scratch slots after m)
   int* n_toopt;
   long long* prof;           // nullable: wall_clock64 at entry, after the seed BFS, at exit (HS_ACT_PROF=1)
+};
+
+// the distance map the reference leaves behind: makeDistanceMap's map + every addIntoDistFinal, one thread per cell
+struct HsActFinalArgs {
+  int w1, h1;
+  const uint8_t* map0;
+  const int* seeds;
+  const int* n_seeds;
+  uint8_t* dist;
 };
 
 // optimizeImmaturePoint, one wave per point to optimize
@@ -140,4 +150,5 @@ struct HsActOptArgs {
 __global__ void hs_k_act_seed(HsActSeedArgs a);
 __global__ void hs_k_act_cand(HsActCandArgs a);
 __global__ void hs_k_act_select(HsActSelectArgs a);
+__global__ void hs_k_act_final(HsActFinalArgs a);
 __global__ void hs_k_act_optimize(HsActOptArgs a);

@@ -142,10 +142,13 @@ class KeyframeBA:
     """System::AddKeyframe's BA part over a BASequence, through the incremental C-ABI (module docstring)."""
 
     def __init__(self, seq: BASequence, device: int = 0, window: int = 8, capacity: int = 0, params=None,
-                 tracker=None, image_path: str = "raw", iters: int = 6):
+                 tracker=None, image_path: str = "raw", iters: int = 6, allow_break: bool = False):
         self.seq = seq
         self.window = window
         self.iters = iters
+        # System::optimize's canbreak (Src/FullSystemOptimize.cpp:493), tested on the device; off by default so that
+        # a parity run's iteration count cannot flip on a borderline step norm
+        self.allow_break = allow_break
         self.tracker = tracker
         self.image_path = image_path
         ppk = len(seq.cand[0]["u"])
@@ -226,7 +229,7 @@ class KeyframeBA:
         if check:
             check(self, "optimize")
         # optimize + tail
-        n_it, energies = timer.run("optimize", ba.optimize, self.iters)
+        n_it, energies = timer.run("optimize", ba.optimize, self.iters, self.allow_break)
         tail = self.last_tail = timer.run("tail", ba.fixLinearization)
         if check:
             check(self, "tail")

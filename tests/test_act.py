@@ -87,6 +87,71 @@ def test_distance_map_single_seed_is_octagonal(vga):
             assert dm[y, x] == (d if d < 40 else 1000), (x, y)
 
 
+def _grow_dist_bfs(m, frontier, w1, h1):
+    """CoarseDistanceMap::growDistBFS (Src/CoarseTracker.cpp:759-857), restated as plain Python."""
+    for k in range(1, 40):
+        nxt = []
+        for (x, y) in frontier:
+            if x == 0 or y == 0 or x == w1 - 1 or y == h1 - 1:
+                continue
+            nb = [(1, 0), (-1, 0), (0, 1), (0, -1)] + ([(1, 1), (-1, 1), (-1, -1), (1, -1)] if k % 2 else [])
+            for dx, dy in nb:
+                if m[y + dy, x + dx] > k:
+                    m[y + dy, x + dx] = k
+                    nxt.append((x + dx, y + dy))
+        frontier = nxt
+
+
+def _closed_form_add(m, sx, sy, w1, h1):
+    """hs_act_kernels.hip's addIntoDistFinal without a BFS (bfs_dist / border_step): interior cells min(map, k),
+    border cells from their interior neighbours the wave lowered, a border seed only itself."""
+    new = m.copy()
+    new[sy, sx] = 0
+    if sx == 0 or sy == 0 or sx == w1 - 1 or sy == h1 - 1:
+        return new
+    ys, xs = np.mgrid[0:h1, 0:w1]
+    ax, ay = np.abs(xs - sx), np.abs(ys - sy)
+    d = np.maximum(np.maximum(ax, ay), (2 * (ax + ay) + 1) // 3)
+    inner = np.zeros_like(m, bool)
+    inner[1:-1, 1:-1] = True
+    upd = inner & (d <= 39)
+    new[upd] = np.minimum(m[upd], d[upd])
+    for by, bx in zip(*np.nonzero(~inner)):
+        v = new[by, bx]
+        for ny in (by - 1, by, by + 1):
+            for nx in (bx - 1, bx, bx + 1):
+                if not (1 <= nx <= w1 - 2 and 1 <= ny <= h1 - 2):
+                    continue
+                t = d[ny, nx] + 1
+                frontier = d[ny, nx] < m[ny, nx] or (nx, ny) == (sx, sy)
+                if frontier and t <= 39 and (nx == bx or ny == by or t % 2 == 1):
+                    v = min(v, t)
+        new[by, bx] = v
+    return new
+
+
+def test_closed_form_bfs_matches_grow_dist_bfs():
+    """The activation kernel replaces addIntoDistFinal's BFS by a closed form (hs_act_kernels.hip bfs_dist,
+    border_step; hs_k_act_final).  Random small maps: makeDistanceMap's multi-seed BFS, then a sequence of
+    addIntoDistFinal calls (seeds anywhere the selection loop can put them: x, y > 0, borders included); after every
+    call the closed form equals the reference's growDistBFS on every cell."""
+    rng = np.random.default_rng(11)
+    for trial in range(40):
+        w1, h1 = int(rng.integers(4, 48)), int(rng.integers(4, 40))
+        m = np.full((h1, w1), 1000, np.int32)
+        seeds = {(int(rng.integers(1, w1)), int(rng.integers(1, h1))) for _ in range(int(rng.integers(0, 5)))}
+        for (x, y) in seeds:
+            m[y, x] = 0
+        _grow_dist_bfs(m, sorted(seeds), w1, h1)
+        for _ in range(int(rng.integers(1, 10))):
+            x, y = int(rng.integers(1, w1)), int(rng.integers(1, h1))
+            ref = m.copy()
+            ref[y, x] = 0
+            _grow_dist_bfs(ref, [(x, y)], w1, h1)
+            assert np.array_equal(_closed_form_add(m, x, y, w1, h1), ref), (trial, (w1, h1), (x, y))
+            m = ref
+
+
 def test_activation_invariants(vga):
     o = oracle_tracer(vga)
     r = activate(o, vga, True)

@@ -385,6 +385,64 @@ def test_fix_linearization_after_optimize(scene2k):
     assert not np.array_equal(out["HdiF"], g.points()["HdiF"])
 
 
+def _break_pair(scene, th_opt, min_opt):
+    """GPU window (production order) + oracle with setting_thOptIterations / setting_minOptIterations."""
+    from hslam_amd._lib import default_params
+    from hslam_amd.ba import BAWindow
+    from oracle_ffi import OracleBA, default_params as oracle_params
+    pg, po = default_params(), oracle_params()
+    pg.thOptIterations = po.thOptIterations = th_opt
+    pg.minOptIterations = po.minOptIterations = min_opt
+    return BAWindow(scene, params=pg), OracleBA(scene, params=po)
+
+
+@pytest.mark.parametrize("min_opt", [1, 3])
+def test_optimize_break_forced(scene2k, min_opt):
+    """System::optimize's break (Src/FullSystemOptimize.cpp:440, 493: canbreak && iteration >= minOptIterations)
+    tested on the device: with thOptIterations huge every step allows the break, so both sides stop after
+    iteration minOptIterations; energies, states and depths at the trajectory bars, and the window goes on
+    (a second call, the tail) from the state of the last iteration that ran."""
+    g, o = _break_pair(scene2k, 1e9, min_opt)
+    ng, eg = g.optimize(6, allow_break=True)
+    no, eo = o.optimize(6, allow_break=True)
+    assert ng == no == min_opt + 1, (ng, no)
+    assert len(eg) == len(eo) == ng + 1
+    assert np.all(np.abs(eg - eo) <= 1e-3 * np.abs(eo))
+    assert np.allclose(g.frames()["state"], o.frames()["state"], atol=1e-4)
+    assert np.allclose(g.points()["idepth"], o.points()["idepth"], rtol=1e-3, atol=1e-4)
+    # the energy of the current linearization is that of the last iteration run
+    assert abs(g.linearizeAll(reset=False) - eg[-1]) <= 1e-9 * abs(eg[-1])
+
+
+def test_optimize_break_device_matches_host(scene2k, monkeypatch):
+    """The device-side break test (launches after the break return at entry; the HdiF ping-pong is put back by the
+    host) and the host-side one (HS_HOST_BREAK=1: canbreak read back after every iteration) give the same run bit
+    for bit: iteration count, energies, frame states, depths, HdiF and the following tail.  A converged window
+    (optimize(6) twice, default thresholds) breaks in the second call as the oracle's does."""
+    from hslam_amd.ba import BAWindow
+    runs = []
+    for host in ("0", "1"):
+        monkeypatch.setenv("HS_HOST_BREAK", host)
+        g = BAWindow(scene2k)
+        g.optimize(6)
+        n, e = g.optimize(6, allow_break=True)
+        z = np.zeros(scene2k.n_points)
+        tail = g.fixLinearization(z, z.astype(np.int32))
+        runs.append((n, e, g.frames()["state"], g.points()["idepth"], tail["HdiF"], tail["energy"], tail["drop"]))
+    (n0, e0, s0, d0, h0, t0, r0), (n1, e1, s1, d1, h1, t1, r1) = runs
+    assert n0 == n1 and np.array_equal(e0, e1)
+    assert np.array_equal(s0, s1) and np.array_equal(d0, d1) and np.array_equal(h0, h1)
+    assert t0 == t1 and np.array_equal(r0, r1)
+    from oracle_ffi import OracleBA
+    o = OracleBA(scene2k)
+    o.optimize(6)
+    no, eo = o.optimize(6, allow_break=True)
+    print(f"converged window: gpu breaks after {n0}, oracle after {no}")
+    assert n0 < 6 and abs(n0 - no) <= 1
+    k = min(n0, no)
+    assert np.all(np.abs(e0[:k + 1] - eo[:k + 1]) <= 1e-3 * np.abs(eo[:k + 1]))
+
+
 def test_graph_replay_matches_eager(scene2k):
     """gn_iterations replays iteration pairs as one captured hipGraph (HS_GRAPH=1) or launches them one by one
     (default): identical energies, frame states, depths and systems, bit for bit."""
