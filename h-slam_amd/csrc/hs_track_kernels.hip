@@ -50,11 +50,23 @@ __device__ __forceinline__ float3 interp33(const float4* __restrict__ img, float
     if ((A).trace && threadIdx.x == 0) (A).trace[(size_t)blockIdx.x * 16 + (slot)] = wall_clock64(); \
   } while (0)
 
-// Eigen LDLT (diagonal pivoting) solve of an 8x8 system by one thread, fully unrolled so every array is
-// register-resident: the pivot order is the swap sequence on the original diagonal (left-looking LDLT).
-// A's diagonal is read scaled by dscale (the LM damping (1 + lambda): Hl = H with a scaled diagonal, formed on load).
-__device__ __forceinline__ void ldlt8_solve(const double* __restrict__ A, const double* __restrict__ rhs, double* __restrict__ x,
-                                            double dscale = 1.0) {
+__device__ __forceinline__ double trk_readlane_f64(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), lane);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Eigen LDLT (diagonal pivoting) solve of an 8x8 system on one wave: the pivot order is the swap sequence on the
+// original diagonal (left-looking LDLT, Eigen's ldlt_inplace::unblocked: column k is updated with the finished
+// columns j < k, temp_j = D_j L_kj, then scaled by the pivot).  Lane i (mod 8) holds row i of the pivoted matrix, so
+// column k's dot products run on the 8 row lanes at once (row k's L entries come by readlane) with the operations of
+// the single-thread form in the same order (the same result bit for bit); a single thread ran it as one ~140-
+// operation dependent fp64 chain.  One reciprocal per pivot (v_rcp_f64 + two Newton steps, within an ulp of 1 / d)
+// instead of Eigen's divisions.  A's diagonal is read scaled by dscale (the LM damping (1 + lambda)).  Every lane
+// of the wave calls it; x is uniform.
+__device__ __forceinline__ void ldlt8_solve_wave(const double* __restrict__ A, const double* __restrict__ rhs,
+                                                 double* __restrict__ x, double dscale, int lane) {
   double dg[8];
   int pm[8];
 #pragma unroll
@@ -76,56 +88,51 @@ __device__ __forceinline__ void ldlt8_solve(const double* __restrict__ A, const 
         const int tp = pm[k]; pm[k] = pm[j]; pm[j] = tp;
       }
   }
-  double M[8][8], y[8], D[8], Dinv[8];
+  const int i = lane & 7;
+  int pi = pm[0];
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
+  for (int q = 1; q < 8; q++) pi = i == q ? pm[q] : pi;
+  double m[8];
 #pragma unroll
-    for (int j = 0; j < 8; j++) M[i][j] = i == j ? A[pm[i] * 9] * dscale : A[pm[i] * 8 + pm[j]];
-    y[i] = rhs[pm[i]];
-  }
-  // left-looking as Eigen's ldlt_inplace::unblocked: column k is updated with the finished columns j < k
-  // (temp_j = D_j L_kj), then scaled by the pivot
+  for (int j = 0; j < 8; j++) m[j] = pm[j] == pi ? A[pi * 9] * dscale : A[pi * 8 + pm[j]];
+  double y = rhs[pi];
+  double D[8], Dinv[8];
 #pragma unroll
   for (int k = 0; k < 8; k++) {
     double temp[8];
 #pragma unroll
-    for (int j = 0; j < k; j++) temp[j] = D[j] * M[k][j];
-    double s = 0;
+    for (int j = 0; j < k; j++) temp[j] = D[j] * trk_readlane_f64(m[j], k);
+    double t = 0;
 #pragma unroll
-    for (int j = 0; j < k; j++) s += M[k][j] * temp[j];
-    M[k][k] -= s;
-#pragma unroll
-    for (int i = k + 1; i < 8; i++) {
-      double t = 0;
-#pragma unroll
-      for (int j = 0; j < k; j++) t += M[i][j] * temp[j];
-      M[i][k] -= t;
-    }
-    const double d = M[k][k];
+    for (int j = 0; j < k; j++) t += m[j] * temp[j];
+    if (i >= k) m[k] -= t;  // row k: the pivot's own update (the single-thread form's s)
+    const double d = trk_readlane_f64(m[k], k);
     D[k] = d;
-    // one reciprocal per pivot, then products (Eigen divides every entry: rounding-level only).  v_rcp_f64 + two
-    // Newton steps (within an ulp of 1 / d) instead of the IEEE division's ~100-cycle dependent sequence
     double rinv = __builtin_amdgcn_rcp(d);
     rinv = __builtin_fma(rinv, __builtin_fma(-d, rinv, 1.0), rinv);
     rinv = __builtin_fma(rinv, __builtin_fma(-d, rinv, 1.0), rinv);
     Dinv[k] = fabs(d) > DBL_MIN ? rinv : 0.0;
-    if (fabs(d) > DBL_MIN) {
-#pragma unroll
-      for (int i = k + 1; i < 8; i++) M[i][k] *= Dinv[k];
-    }
+    if (fabs(d) > DBL_MIN && i > k) m[k] *= Dinv[k];
   }
 #pragma unroll
-  for (int i = 0; i < 8; i++)
+  for (int k = 0; k < 8; k++) {  // forward: y_i -= L(i, k) y_k for k < i, in k order
+    const double yk = trk_readlane_f64(y, k);
+    if (i > k) y = y - m[k] * yk;
+  }
+  double yy[8];
 #pragma unroll
-    for (int k = 0; k < i; k++) y[i] = y[i] - M[i][k] * y[k];
+  for (int q = 0; q < 8; q++) yy[q] = trk_readlane_f64(y, q) * Dinv[q];
 #pragma unroll
-  for (int i = 0; i < 8; i++) y[i] = y[i] * Dinv[i];
+  for (int q = 7; q >= 0; q--)
 #pragma unroll
-  for (int i = 7; i >= 0; i--)
+    for (int j = q + 1; j < 8; j++) yy[q] = yy[q] - trk_readlane_f64(m[q], j) * yy[j];
 #pragma unroll
-    for (int j = i + 1; j < 8; j++) y[i] = y[i] - M[j][i] * y[j];
+  for (int q = 0; q < 8; q++) {
+    double v = yy[0];
 #pragma unroll
-  for (int i = 0; i < 8; i++) x[pm[i]] = y[i];
+    for (int r = 1; r < 8; r++) v = pm[r] == q ? yy[r] : v;
+    x[q] = pm[0] == q ? yy[0] : v;
+  }
 }
 
 struct TrkShared {
@@ -553,14 +560,15 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
       __syncthreads();  // every thread has read S.brk of the previous iteration
       // the LM step on two waves: lane 0 of wave 0 the pose (exp, product, RKi), lane 0 of wave 1 the affine part
       // (fromToVecExposure); both solve the same 8x8 system (same inputs, same increment)
-      if (tid == 0 || tid == 64) {
+      if (tid < 128) {  // waves 0 and 1: the LDLT on 8 row lanes, then lane 0 of each
         const bool pw = tid == 0;
         const long long lm0 = a.trace ? clock64() : 0;
         // Hl = H with the diagonal scaled by (1 + lambda): formed as the solver loads H (pivoted indices)
         double mb[8], inc[8];
 #pragma unroll
         for (int i = 0; i < 8; i++) mb[i] = -S.bs[i];
-        ldlt8_solve(S.Hs, mb, inc, 1 + S.lambda);
+        ldlt8_solve_wave(S.Hs, mb, inc, 1 + S.lambda, tid & 63);
+        if ((tid & 63) == 0) {
         const long long lm1 = a.trace ? clock64() + (long long)(inc[7] * 0.0) : 0;
         float extrapFac = 1;
         if (S.lambda < lambdaExtrapolationLimit) extrapFac = sqrtf(sqrtf(lambdaExtrapolationLimit / S.lambda));
@@ -595,6 +603,7 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
           S.affn[0] = affn[0];
           S.affn[1] = affn[1];
           trk_setup_part(a, S, nullptr, affn, lvl, a.coarseCutoffTH * S.cutoffRep, false);
+        }
         }
       }
       __syncthreads();

@@ -49,7 +49,10 @@ int hs_tracker_set_ref(hs_tracker* t, const float* const* ref_pyr, float ab_expo
    no host round trip and no host synchronisation (the tracker's stream waits on the BA's).
    promote_frame = 1: the frame last given to hs_tracker_set_frame* is the newest keyframe and becomes the reference
    pyramid as it is (no copy; set the next frame to track afterwards); 0: the reference pyramid is rebuilt on the
-   device from the BA's newest frame image.  ab_exposure / aff_g2l: the newest keyframe's. */
+   device from the BA's newest frame image.  ab_exposure / aff_g2l: the newest keyframe's.
+   The new reference replaces the tracker's in place (the reference builds it in coarseTracker_forNewKF and swaps
+   the two under a lock): the tracker must not be tracking on another thread during this call.  A caller that tracks
+   while the next reference is built keeps two trackers and swaps them itself, as the reference does. */
 int hs_tracker_set_ref_ba(hs_tracker* t, hs_ctx* ba, int promote_frame, float ab_exposure, const double aff_g2l[2]);
 /* device pointer of level lvl of the frame last given to hs_tracker_set_frame* (w_l*h_l float4 texels
    (I, dI/dx, dI/dy, 0)), valid until the next set_frame / set_ref_ba(promote) call: a keyframe's image goes to the
