@@ -61,6 +61,30 @@ def pmc_traffic(points, kernel: str = "hs_k_lin"):
     return None, None
 
 
+def pmc_roof(key, kernel: str):
+    """Counter evidence for `kernel` on workload `key` from the newest committed profiles/*_pmc_roof.json
+    (tools/r04_pmc.sh + tools/pmc_roof.py: separate FETCH_SIZE / WRITE_SIZE / SQ+GRBM rocprofv3 passes with the
+    kernel trace beside them): counter DRAM GB/s over the traced launch duration and the SQ issue split.
+    {} when no pass for it has been committed."""
+    import glob
+    import re
+
+    def version(f):
+        return [int(x) for x in re.findall(r"\d+", os.path.basename(f))]
+
+    for f in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_roof.json")), key=version)):
+        try:
+            k = json.load(open(f))["keys"][str(key)][kernel]
+        except (KeyError, ValueError, OSError):
+            continue
+        out = {n: k[n] for n in ("dram_gbs", "dram_frac", "valu_busy_per_simd", "valu_issue_frac", "wait_frac",
+                                 "issue_stall_frac", "effective_clock_mhz", "hbm_bytes_per_launch",
+                                 "avg_launch_us") if k.get(n) is not None}
+        out["source"] = os.path.relpath(f, ROOT)
+        return out
+    return {}
+
+
 def host_cpu():
     """Model name of the timing host's CPU (lscpu's 'Model name', read from /proc/cpuinfo) and its logical CPUs."""
     model = None
@@ -192,7 +216,7 @@ def bench_trace(args):
         "roofline": {"bound": "hbm", "kernel": "hs_k_trace_on", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic("trace", "hs_k_trace_on")[0],
                      "bytes_per_unit": TRACE_BYTES_PER_STEP, "unit_of_bytes": "discrete-search step (GN taps excluded)",
-                     "avg_launch_ms": kern_ms},
+                     "avg_launch_ms": kern_ms, "counters": pmc_roof("trace", "hs_k_trace_on")},
         "second_trace_counts": dict(zip(("good", "oob", "outlier", "skipped", "badcondition", "uninitialized"),
                                         map(int, counts))),
         "cpu_baseline": None,
@@ -781,6 +805,7 @@ def main():
             "avg_launch_ms_in_loop_events": lin_loop_ms,
             "timing": f"HIP events on the context stream around back-to-back {lin_kernel} launches (fused "
                       "linearize + applyRes + top / Schur accumulation into block partials)",
+            "counters": pmc_roof(f"kitti{args.points}" if kitti else args.points, lin_kernel) if world == 1 else {},
             "binding_roof": "latency (one point per wave at 2k; the step is a chain of 4 dependent launches, the "
                             "single-workgroup fp64 solve the longest)" if shard.n_points < 60000 else
                             "VALU issue + gather latency at occupancy 2 (DESIGN.md §9)",

@@ -5,6 +5,7 @@ TAG=$1; FLAG=$2; K=${3:-"solve or optimize or step or graph"}
 OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG
 mkdir -p $OUT
 cd $GRAFT_REPO_ROOT
+if [ -x tools/micro/ldlt_wave ]; then timeout -k 10 60 tools/micro/ldlt_wave > $OUT/ldlt_wave.txt 2>&1; echo "ldlt_wave rc=$?"; cat $OUT/ldlt_wave.txt; fi
 env $FLAG timeout -k 10 600 python -u -m pytest tests/test_gpu_ba.py -m gpu -x -v --timeout 180 --timeout-method thread -k "$K" > $OUT/pytest_flag.txt 2>&1
 rc=$?
 echo "pytest(flag) rc=$rc"; grep -cE "PASSED" $OUT/pytest_flag.txt; grep -E "FAILED|Error" $OUT/pytest_flag.txt | head -10
