@@ -2199,7 +2199,8 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     for (int rep = 0; rep < ((a.dbg & 8) ? 2 : 1); rep++) {
       if (a.dbg & 64) {  // experiment: the single-wave LDLT
         if (tid < 64) {
-          ldlt_factor_wave(A, LT, B, yv, n, tid);
+          if (a.dbg & 128) ldlt_factor_wave_pipe(A, LT, B, yv, n, tid);
+          else ldlt_factor_wave(A, LT, B, yv, n, tid);
           ldlt_backward(LT, B, yv, n, tid, a.trace);
         }
       } else {

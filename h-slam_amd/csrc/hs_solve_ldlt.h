@@ -136,7 +136,7 @@ __device__ __forceinline__ void ldlt_wave_frames(double (&a)[MD], double& y, dou
   }
 }
 
-__device__ __attribute__((noinline)) void ldlt_factor_wave(const double* M, double* LT, double* W, const double* yv, int n,
+static __device__ __attribute__((noinline)) void ldlt_factor_wave(const double* M, double* LT, double* W, const double* yv, int n,
                                                  int lane) {
   constexpr int MD = HS_MAXDIM;
   static_assert(MD == 68, "lane = frame row: 64 frame rows + 4 calib rows");
@@ -185,6 +185,92 @@ __device__ __attribute__((noinline)) void ldlt_factor_wave(const double* M, doub
     ldlt_wave_update<3, MD>(a, lk, colb);  // columns 4 .. MD-1 (the calib columns m < 4 were updated above)
   }
   ldlt_wave_frames<4, MD>(a, y, colb, LT, Dv, n, lane, r, live);
+  if (live) yf[r] = y;
+}
+
+// The same factorization software-pipelined by one pivot: step K first applies its update to column K + 1 and the
+// rhs, publishes column K + 1 (the other of two LDS column buffers) and forms pivot K + 1 (readlane, reciprocal)
+// -- that dependent chain then overlaps step K's remaining column groups instead of following them.
+template <int K, int MD>
+__device__ __forceinline__ void ldlt_wave_pipe(double (&a)[MD], double& y, double* colb, double* LT, double* Dv,
+                                               int lane, int r, bool live, double lk, double yk) {
+  if constexpr (K < MD) {
+    const double* cb = colb + (K & 1) * 64;  // column K: A(m, K) of rows m > K (lane m - 4)
+    double* cn = colb + ((K + 1) & 1) * 64;
+    y = __builtin_fma(-lk, yk, y);
+    double lk1 = 0.0, yk1 = 0.0;
+    if constexpr (K + 1 < MD) {
+      a[K + 1] = __builtin_fma(-lk, cb[K + 1 - 4], a[K + 1]);
+      constexpr int p1 = K + 1 - 4;
+      const double d1 = readlane_f64(a[K + 1], p1);
+      yk1 = readlane_f64(y, p1);
+      cn[lane] = a[K + 1];
+      const double dinv1 = rcp_f64(d1);
+      lk1 = lane > p1 ? a[K + 1] * dinv1 : 0.0;
+      if (lane == 0) Dv[K + 1] = d1;
+      asm volatile("" : "+v"(a[K + 1]), "+v"(lk1), "+v"(y));
+    }
+    if (lane > K - 4 && live) LT[K * LSTR + r] = lk;
+    ldlt_wave_update<K + 1, MD>(a, lk, cb);  // columns K + 2 .. MD - 1
+    ldlt_wave_pipe<K + 1, MD>(a, y, colb, LT, Dv, lane, r, live, lk1, yk1);
+  }
+}
+
+static __device__ __attribute__((noinline)) void ldlt_factor_wave_pipe(const double* M, double* LT, double* W, const double* yv, int n,
+                                                      int lane) {
+  constexpr int MD = HS_MAXDIM;
+  double* colb = W;  // [2][64]
+  double* Dv = W + 24 * MD;
+  double* yf = W + 25 * MD;
+  const int r = lane + 4;
+  const bool live = r < n;
+  const int rr = live ? r : 4;
+  double a[MD];
+#pragma unroll
+  for (int j = 0; j < MD; j++) a[j] = (live && j < n) ? M[rr * n + j] : 0.0;
+  double y = live ? yv[rr] : 0.0;
+  double C[4][4], yc[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    yc[i] = yv[i];
+#pragma unroll
+    for (int j = 0; j < 4; j++) C[i][j] = M[i * n + j];
+  }
+  double* cb = colb + 64;  // the calib steps' column buffer (the frame steps start at buffer 0)
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const double d = C[k][k];
+    const double dinv = rcp_f64(d);
+    cb[lane] = a[k];
+    const double lk = a[k] * dinv;
+    double lc[4];
+#pragma unroll
+    for (int j = k + 1; j < 4; j++) lc[j] = C[j][k] * dinv;
+    y = __builtin_fma(-lk, yc[k], y);
+#pragma unroll
+    for (int j = k + 1; j < 4; j++) yc[j] = __builtin_fma(-lc[j], yc[k], yc[j]);
+#pragma unroll
+    for (int m = k + 1; m < 4; m++) a[m] = __builtin_fma(-lk, C[m][k], a[m]);
+#pragma unroll
+    for (int j = k + 1; j < 4; j++)
+#pragma unroll
+      for (int m = k + 1; m <= j; m++) C[j][m] = __builtin_fma(-lc[j], C[m][k], C[j][m]);
+    if (live) LT[k * LSTR + r] = lk;
+    if (lane == 0) {
+      Dv[k] = d;
+      yf[k] = yc[k];
+#pragma unroll
+      for (int j = k + 1; j < 4; j++) LT[k * LSTR + j] = lc[j];
+    }
+    ldlt_wave_update<3, MD>(a, lk, cb);
+  }
+  // pivot 4 (lane 0), then the pipelined frame steps
+  const double d4 = readlane_f64(a[4], 0);
+  const double yk4 = readlane_f64(y, 0);
+  colb[lane] = a[4];
+  const double lk4 = lane > 0 ? a[4] * rcp_f64(d4) : 0.0;
+  if (lane == 0) Dv[4] = d4;
+  ldlt_wave_pipe<4, MD>(a, y, colb, LT, Dv, lane, r, live, lk4, yk4);
   if (live) yf[r] = y;
 }
 

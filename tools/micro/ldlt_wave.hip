@@ -13,6 +13,7 @@
 
 using namespace hs_solve;
 
+template <bool PIPE>
 __global__ __launch_bounds__(512) void k(const double* Ag, const double* bg, double* xg, int n, long long* tr) {
   __shared__ double A[HS_MAXDIM * HS_MAXDIM], LT[HS_MAXDIM * LSTR], W[26 * HS_MAXDIM], y[HS_MAXDIM];
   const int tid = threadIdx.x, nt = blockDim.x;
@@ -22,7 +23,8 @@ __global__ __launch_bounds__(512) void k(const double* Ag, const double* bg, dou
   __syncthreads();
   if (tid < 64) {
     const long long c0 = clock64();
-    ldlt_factor_wave(A, LT, W, y, n, tid);
+    if (PIPE) ldlt_factor_wave_pipe(A, LT, W, y, n, tid);
+    else ldlt_factor_wave(A, LT, W, y, n, tid);
     const long long c1 = clock64();
     ldlt_backward(LT, W, y, n, tid, nullptr);
     const long long c2 = clock64();
@@ -56,7 +58,8 @@ static void host_solve(const std::vector<double>& A, const std::vector<double>& 
     for (int q = i + 1; q < n; q++) x[i] -= L[q * n + i] * x[q];
 }
 
-int main() {
+template <bool PIPE>
+static int run() {
   int bad = 0;
   for (int nF = 1; nF <= 8; nF++) {
     const int n = 4 + 8 * nF;
@@ -81,10 +84,10 @@ int main() {
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
-    for (int r = 0; r < 3; r++) hipLaunchKernelGGL(k, dim3(1), dim3(512), 0, 0, dA, db, dx, n, dt);
+    for (int r = 0; r < 3; r++) hipLaunchKernelGGL(k<PIPE>, dim3(1), dim3(512), 0, 0, dA, db, dx, n, dt);
     (void)hipEventRecord(e0, 0);
     const int reps = 50;
-    for (int r = 0; r < reps; r++) hipLaunchKernelGGL(k, dim3(1), dim3(512), 0, 0, dA, db, dx, n, dt);
+    for (int r = 0; r < reps; r++) hipLaunchKernelGGL(k<PIPE>, dim3(1), dim3(512), 0, 0, dA, db, dx, n, dt);
     (void)hipEventRecord(e1, 0);
     if (hipDeviceSynchronize() != hipSuccess) { printf("kernel failed\n"); return 1; }
     float ms = 0;
@@ -99,9 +102,11 @@ int main() {
     }
     const double rel = std::sqrt(num / den);
     bad |= !(rel < 1e-10);
-    printf("nF=%d n=%d: rel err %.3e  factor %lld cycles  backward %lld cycles  launch avg %.2f us\n", nF, n, rel,
+    printf("%s nF=%d n=%d: rel err %.3e  factor %lld cycles  backward %lld cycles  launch avg %.2f us\n", PIPE ? "pipe" : "plain", nF, n, rel,
            t[0], t[1], ms * 1e3 / reps);
     (void)hipFree(dA); (void)hipFree(db); (void)hipFree(dx); (void)hipFree(dt);
   }
   return bad;
 }
+
+int main() { return run<false>() | run<true>(); }
