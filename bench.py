@@ -214,7 +214,7 @@ def bench_trace(args):
                                "points, 8 host KFs, 1232x368", "points": s.n_points, "hosts": s.n_hosts,
                    "search_steps_per_trace": steps // args.steps, "parallelism": "single GPU"},
         "roofline": {"bound": "hbm", "kernel": "hs_k_trace_on", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic("trace", "hs_k_trace_on")[0],
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_roof("trace", "hs_k_trace_on").get("hbm_bytes_per_launch", pmc_traffic("trace", "hs_k_trace_on")[0]),
                      "bytes_per_unit": TRACE_BYTES_PER_STEP, "unit_of_bytes": "discrete-search step (GN taps excluded)",
                      "avg_launch_ms": kern_ms, "counters": pmc_roof("trace", "hs_k_trace_on")},
         "second_trace_counts": dict(zip(("good", "oob", "outlier", "skipped", "badcondition", "uninitialized"),
@@ -748,7 +748,9 @@ def main():
     lin_ms = ba.time_linearize(max(64, args.steps))
     achieved = BYTES_PER_PRES * shard.n_res / (lin_ms * 1e-3) / 1e9
     lin_kernel = ba.partition()["kernel"]  # hs_k_lin (one point per wave) or hs_k_lin8 (8 points per wave)
-    traffic, traffic_src = (pmc_traffic(f"kitti{args.points}" if kitti else args.points, lin_kernel) if world == 1
+    roof_ctr = pmc_roof(f"kitti{args.points}" if kitti else args.points, lin_kernel) if world == 1 else {}
+    traffic, traffic_src = ((roof_ctr["hbm_bytes_per_launch"], roof_ctr["source"]) if "hbm_bytes_per_launch" in roof_ctr
+                            else pmc_traffic(f"kitti{args.points}" if kitti else args.points, lin_kernel) if world == 1
                             else (None, None))
     ba.close()
     other = None
@@ -805,7 +807,7 @@ def main():
             "avg_launch_ms_in_loop_events": lin_loop_ms,
             "timing": f"HIP events on the context stream around back-to-back {lin_kernel} launches (fused "
                       "linearize + applyRes + top / Schur accumulation into block partials)",
-            "counters": pmc_roof(f"kitti{args.points}" if kitti else args.points, lin_kernel) if world == 1 else {},
+            "counters": roof_ctr,
             "binding_roof": "latency (one point per wave at 2k; the step is a chain of 4 dependent launches, the "
                             "single-workgroup fp64 solve the longest)" if shard.n_points < 60000 else
                             "VALU issue + gather latency at occupancy 2 (DESIGN.md §9)",

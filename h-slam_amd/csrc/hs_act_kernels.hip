@@ -4,13 +4,12 @@
 //                    projection into the newest keyframe, seed byte set to 0 with a word CAS (duplicates dropped).
 // hs_k_act_cand      the per-point part of the selection loop (Mapping.cpp:378-426): delete / skip / the
 //                    projected cell, the sub-pixel fraction and the threshold of every entry of the loop order.
-// hs_k_act_select    one workgroup: growDistBFS of the seeds over the whole workgroup (frontier-parallel; a cell
-//                    joins the next frontier only through the CAS that lowered it, so the map after each step is
-//                    the reference's), then the greedy loop: per batch of 64 entries wave 0 takes, in loop order,
+// hs_k_act_dist      mode 0: makeDistanceMap's growDistBFS over the seeds in closed form (bfs_dist), per cell.
+// hs_k_act_select    one workgroup, the greedy loop: per batch of 64 entries wave 0 takes, in loop order,
 //                    each entry whose distance passes and applies its addIntoDistFinal to the rest of the batch
 //                    in closed form (bfs_dist); the workgroup then folds the batch's seeds into the map.
 //                    The map lives in LDS as bytes (0..39, 255 = the reference's 1000) when it fits.
-// hs_k_act_final     the exact distance map after the loop (makeDistanceMap + every addIntoDistFinal), per cell.
+//                    mode 1: the exact distance map after the loop (+ every addIntoDistFinal), per cell.
 // hs_k_act_optimize  optimizeImmaturePoint (Src/FullSystemOptPoint.cpp:24-175) with
 //                    ImmaturePoint::linearizeResidual (Src/ImmaturePoint.cpp:389-451): one wave per point,
 //                    lane = residual (target frame) x pattern pixel; energy, Hdd and bd are summed in the
@@ -104,91 +103,6 @@ __global__ void __launch_bounds__(256) hs_k_act_cand(HsActCandArgs a) {
   a.action[i] = (c == HS_CAND_DELETE) ? HS_ACT_DELETED : HS_ACT_KEEP;
 }
 
-// Frontier entries are packed cells x | y << 16 (no division to find a cell's neighbours).
-__device__ __forceinline__ int xy_index(int xy, int w1) { return (xy & 0xffff) + w1 * (xy >> 16); }
-
-// One growDistBFS step's work for one frontier entry: probe the 4 / 8 neighbour words, CAS the bytes that are
-// larger than k (the probe's word is the CAS's expected value), report which neighbours this lane lowered.
-__device__ __forceinline__ unsigned expand_cell(uint8_t* map, int w1, int h1, int xy, bool valid, uint32_t k,
-                                                bool diag, int nbxy[8]) {
-  const int x = xy & 0xffff, y = xy >> 16;
-  const bool live = valid & (x != 0) & (y != 0) & (x != w1 - 1) & (y != h1 - 1);
-  const int idx = live ? x + w1 * y : w1 + 1;
-  const int nbi[8] = {idx + 1, idx - 1, idx + w1, idx - w1, idx + 1 + w1, idx - 1 + w1, idx - 1 - w1, idx + 1 - w1};
-  const int dxy[8] = {1, -1, 1 << 16, -(1 << 16), 1 + (1 << 16), -1 + (1 << 16), -1 - (1 << 16), 1 - (1 << 16)};
-  const int cnt = diag ? 8 : 4;
-  uint32_t word[8];
-#pragma unroll
-  for (int d = 0; d < 8; d++) {
-    nbxy[d] = xy + dxy[d];
-    word[d] = d < cnt ? *reinterpret_cast<const uint32_t*>(map + (nbi[d] & ~3)) : 0u;
-  }
-  // every wanted CAS is issued before any result is waited for; a CAS that lost to another lane's update of
-  // the same word is retried
-  unsigned want = 0;
-  uint32_t prev[8];
-#pragma unroll
-  for (int d = 0; d < 8; d++) {
-    const int sh = (nbi[d] & 3) * 8;
-    const bool w = live & (d < cnt) & (((word[d] >> sh) & 0xffu) > k);
-    want |= (unsigned)w << d;
-    if (w)
-      prev[d] = atomicCAS(reinterpret_cast<uint32_t*>(map + (nbi[d] & ~3)), word[d],
-                          (word[d] & ~(0xffu << sh)) | (k << sh));
-  }
-  unsigned got = 0;
-#pragma unroll
-  for (int d = 0; d < 8; d++) {
-    if (!((want >> d) & 1u)) continue;
-    const int sh = (nbi[d] & 3) * 8;
-    uint32_t old = word[d];
-    uint32_t pv = prev[d];
-    while (pv != old) {  // lost a race on this word: retry while the byte still needs lowering
-      old = pv;
-      if (((old >> sh) & 0xffu) <= k) break;
-      pv = atomicCAS(reinterpret_cast<uint32_t*>(map + (nbi[d] & ~3)), old, (old & ~(0xffu << sh)) | (k << sh));
-    }
-    got |= (unsigned)(pv == old && ((old >> sh) & 0xffu) > k) << d;
-  }
-  return got;
-}
-
-// growDistBFS from the n cells in *in (Src/CoarseTracker.cpp:759-857), frontier-parallel over the workgroup
-// (makeDistanceMap's multi-seed BFS; its frontiers can span the map).  s_n[0] holds the frontier size on entry.
-__device__ __forceinline__ void bfs_grow_wg(uint8_t* map, int w1, int h1, int*& in, int*& out, int* s_n) {
-  const int lane = threadIdx.x & 63;
-  for (int k = 1; k < HS_ACT_BFS_STEPS; k++) {
-    const int n = s_n[0];
-    if (n == 0) break;  // the reference keeps looping over empty lists: nothing changes
-    if (threadIdx.x == 0) s_n[1] = 0;
-    __syncthreads();
-    const bool diag = (k & 1) != 0;
-    for (int e0 = threadIdx.x & ~63; e0 < n; e0 += blockDim.x) {  // wave-uniform trip count
-      const int e = e0 + lane;
-      const int xy = e < n ? in[e] : 0;
-      int nbxy[8];
-      const unsigned got = expand_cell(map, w1, h1, xy, e < n, (uint32_t)k, diag, nbxy);
-#pragma unroll
-      for (int d = 0; d < 8; d++) {
-        const unsigned long long bm = __ballot((got >> d) & 1u);
-        if (bm == 0) continue;
-        int base = 0;
-        if (lane == (int)__builtin_ctzll(bm)) base = atomicAdd(&s_n[1], (int)__popcll(bm));
-        base = __shfl(base, (int)__builtin_ctzll(bm));
-        if ((got >> d) & 1u)
-          out[base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u))] =
-              nbxy[d];
-      }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) s_n[0] = s_n[1];
-    int* t = in;
-    in = out;
-    out = t;
-    __syncthreads();
-  }
-}
-
 // addIntoDistFinal without a BFS.  growDistBFS from one seed takes 8-neighbour steps at odd k and 4-neighbour steps
 // at even k, so an unobstructed cell at (dx, dy) is first reached at the smallest k with max(|dx|, |dy|) <= k and
 // |dx| + |dy| <= k + ceil(k / 2): k = max(M, (2 L + 1) / 3).  With the map before the call being a union of such
@@ -243,24 +157,24 @@ __device__ __forceinline__ int ld_cell(const uint8_t* map, int q) {
   return b == 255u ? 1000 : (int)b;
 }
 
-// makeDistanceMap's BFS (whole workgroup), then the selection loop in batches of 64 entries: wave 0 takes, in loop
+// workgroup barrier that orders LDS only: a global-memory operation in flight (wave 0's prefetch of the next batch,
+// its toopt / seeds stores) is not waited for, as __syncthreads' release fence would
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// makeDistanceMap's map (hs_k_act_map0) in the working map, then the selection loop in batches of 64 entries: wave 0 takes, in loop
 // order, every entry whose distance passes, updating the rest of the batch from each new seed in registers; then
 // the whole workgroup folds the batch's seeds into the working map.  The working map only has to decide the test
 // dist + frac >= thr (thr <= T = the largest threshold of the call): it is kept exact up to r = ceil(T) - 1 (seed
 // patches of radius r; cells farther away keep a larger value, which passes every test anyway), and the exact
-// map is formed afterwards by hs_k_act_final.
+// map is formed afterwards by hs_k_act_dist (mode 1).
 __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* map, int* s_n, int* s_seeds,
                                            float* s_red) {
   const int tid = threadIdx.x, nthr = blockDim.x;
-  const int w1 = a.w1, h1 = a.h1, wh1 = w1 * h1;
-  {
-    int* in = a.list_a;
-    int* out = a.list_b;
-    bfs_grow_wg(map, w1, h1, in, out, s_n);
-  }
-  // map0 for the final map; the largest threshold of the pending entries
-  for (int w = tid; w < (wh1 + 3) / 4; w += nthr)
-    reinterpret_cast<uint32_t*>(a.map0)[w] = ld_word(map, w);
+  const int w1 = a.w1, h1 = a.h1;
   float tmax = 0.f;
   bool tnan = false;
   for (int j = tid; j < a.m; j += nthr)
@@ -274,7 +188,7 @@ __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* ma
     tnan |= __shfl_xor((int)tnan, o) != 0;
   }
   if ((tid & 63) == 0) s_red[tid >> 6] = tnan ? 1e30f : tmax;
-  __syncthreads();
+  __syncthreads();  // (also: the map is in place)
   float T = 0.f;
   for (int i = 0; i < nthr / 64; i++) T = fmaxf(T, s_red[i]);
   const int r = T >= 40.f ? HS_ACT_BFS_STEPS - 1 : max(0, (int)ceilf(T) - 1);
@@ -300,7 +214,9 @@ __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* ma
   };
   if (w0 && a.m > 0) fetch(lane);
   const int rows = 2 * r + 1, wpr = (2 * r + 1 + 3) / 4 + 1, per_seed = rows * wpr;
+  long long t_dec = 0, t_fold = 0;
   for (int base = 0; base < a.m; base += 64) {
+    const long long c0 = a.prof ? wall_clock64() : 0;
     if (w0) {
       bool pend = (base + lane < a.m) && ncand == HS_CAND_PENDING;
       const int cell = pend ? ncell : (1 | (1 << 16));
@@ -318,13 +234,14 @@ __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* ma
           if (nb[i] >= 0) nv[i] = ld_cell(map, (nb[i] & 0xffff) + w1 * (nb[i] >> 16));
       }
       int myslot = -1, ns = 0;
+      int bxm = 0, bym = 0;  // the batch seeds' largest x / y (the border pass is skipped when no seed is near)
       for (;;) {
         // dist = fwdWarpedIDDistFinal[u + w1 * v] + (ptp[0] - floorf(ptp[0])) >= currentMinActDist * my_type
         const bool acc = pend && ((float)v + frac >= thr);
         const unsigned long long bm = __ballot(acc);
         if (bm == 0) break;  // every remaining entry of the batch fails: they stay immature
         const int first = (int)__builtin_ctzll(bm);
-        const int sc = __builtin_amdgcn_readfirstlane(__shfl(cell, first));
+        const int sc = __builtin_amdgcn_readlane(cell, first);
         if (lane == first) {
           myslot = nt;
           a.seeds[nt] = sc;
@@ -332,6 +249,8 @@ __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* ma
         if (lane == 0) s_seeds[ns] = sc;
         ns++;
         nt++;
+        bxm = max(bxm, sc & 0xffff);
+        bym = max(bym, sc >> 16);
         if (lane <= first) pend = false;
         // addIntoDistFinal(sc) on the batch's later entries
         const int sx = sc & 0xffff, sy = sc >> 16;
@@ -346,14 +265,18 @@ __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* ma
       }
       // one unconditional store per batch (the lanes not taken write their scratch slot toopt[m + lane])
       a.toopt[myslot >= 0 ? myslot : a.m + lane] = pt;
-      if (lane == 0) s_n[0] = ns;
+      if (lane == 0) {
+        s_n[0] = ns;
+        s_n[1] = (bxm + r + 1 >= w1 - 1) | (bym + r + 1 >= h1 - 1);
+      }
     }
-    __syncthreads();
+    lds_barrier();  // wave 0's prefetch loads and its toopt / seeds stores stay in flight across it
+    const long long c1 = a.prof ? wall_clock64() : 0;
     const int ns = s_n[0];
     if (ns > 0) {
       npatch += ns;
       // the right column / bottom row cells near a seed (the only border cells an entry can sit on), seeds in order
-      for (int i = tid; i < w1 + h1 - 1; i += nthr) {
+      for (int i = s_n[1] ? tid : w1 + h1; i < w1 + h1 - 1; i += nthr) {
         const int x = i < w1 ? i : w1 - 1, y = i < w1 ? h1 - 1 : i - w1;
         if (x < 1 || y < 1) continue;
         bool near = false;
@@ -389,7 +312,7 @@ __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* ma
           }
         }
       }
-      __syncthreads();
+      lds_barrier();
       // interior cells: min(map, k) over each seed's patch of radius r, one 4-cell word per (seed, row, word) item
       for (int it = tid; it < ns * per_seed; it += nthr) {
         const int j = it / per_seed, rem = it - j * per_seed;
@@ -421,12 +344,18 @@ __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* ma
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
+    if (a.prof) {
+      t_dec += c1 - c0;
+      t_fold += wall_clock64() - c1;
+    }
   }
   if (a.prof && tid == 0) {
     a.prof[3] = (a.m + 63) / 64;
     a.prof[4] = npatch;
     a.prof[5] = r;
+    a.prof[8] = t_dec;
+    a.prof[9] = t_fold;
   }
   return nt;
 }
@@ -438,15 +367,16 @@ __global__ void __launch_bounds__(1024) hs_k_act_select(HsActSelectArgs a) {
   __shared__ float s_red[16];
   const int words = (a.w1 * a.h1 + 3) / 4;
   if (a.prof && threadIdx.x == 0) a.prof[0] = wall_clock64();
-  if (threadIdx.x == 0) s_n[0] = *a.seed_count;
+  const uint32_t* g = reinterpret_cast<const uint32_t*>(a.map0);
+  // one inlined instance per map location, so the LDS one compiles to ds_* instructions (a pointer that may be
+  // either would make every map access a flat one); select_body's first barrier orders the copies before any use
   int nt;
   if (a.lds_map) {
-    const uint32_t* g = reinterpret_cast<const uint32_t*>(a.dist);
     for (int w = threadIdx.x; w < words; w += blockDim.x) s_map32[w] = g[w];
-    __syncthreads();
     nt = select_body(a, reinterpret_cast<uint8_t*>(s_map32), s_n, s_seeds, s_red);
   } else {
-    __syncthreads();
+    uint32_t* m32 = reinterpret_cast<uint32_t*>(a.dist);
+    for (int w = threadIdx.x; w < words; w += blockDim.x) m32[w] = g[w];
     nt = select_body(a, a.dist, s_n, s_seeds, s_red);
   }
   if (threadIdx.x == 0) *a.n_toopt = nt;
@@ -456,56 +386,110 @@ __global__ void __launch_bounds__(1024) hs_k_act_select(HsActSelectArgs a) {
   }
 }
 
-// makeDistanceMap's map + every addIntoDistFinal of the greedy loop, in call order (the closed form above): interior
-// cells take the minimum over the seeds; a border cell runs the seeds in order beside its interior neighbours.  The
-// seeds go through LDS in tiles.
-__global__ void __launch_bounds__(256) hs_k_act_final(HsActFinalArgs a) {
+// Distance maps from seeds in closed form.  Mode 0, makeDistanceMap (Src/CoarseTracker.cpp:726-756): growDistBFS
+// from every seed at once is, per interior cell, the minimum of the seeds' single-seed distances (bfs_dist, <= 39);
+// a border cell (never expanded) takes k_n + 1 from its interior neighbours n (a diagonal move only on an odd
+// step); a seed on the border only sets itself.  Mode 1, the map the greedy loop leaves: makeDistanceMap's map and
+// every addIntoDistFinal in call order -- interior cells the same minimum, border cells the sequential rule of
+// border_step (their neighbours' values before each seed).  Both checked against growDistBFS (tests/test_act.py).
+// Blocks [0, n_tiles): one 16 x 16 tile of interior cells; the tile's seeds are those within Chebyshev 39 of it
+// (a scalar test per seed: the seeds go through LDS in tiles of 1024 and are read as uniform values).  Blocks after:
+// 256 border cells each (every seed within Chebyshev 40 of the wave's cells).
+__global__ void __launch_bounds__(256) hs_k_act_dist(HsActDistArgs a) {
   __shared__ int tile[1024];
-  const int w1 = a.w1, h1 = a.h1;
-  const int q = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool live = q < w1 * h1;
-  const int x = live ? q % w1 : 1, y = live ? q / w1 : 1;
-  const bool interior = x >= 1 && x <= w1 - 2 && y >= 1 && y <= h1 - 2;
-  auto val = [&](int c) { const uint8_t b = a.map0[c]; return b == 255 ? 1000 : (int)b; };
+  constexpr int R = HS_ACT_BFS_STEPS - 1;
+  const int w1 = a.w1, h1 = a.h1, tid = threadIdx.x;
+  const bool itile = (int)blockIdx.x < a.n_tiles;
+  int x, y;
+  bool live;
+  int bx0, bx1, by0, by1;  // the cells' bounding box (uniform per wave)
+  if (itile) {
+    const int tx = blockIdx.x % a.n_tiles_x, ty = blockIdx.x / a.n_tiles_x;
+    x = 1 + 16 * tx + (tid & 15);
+    y = 1 + 16 * ty + (tid >> 4);
+    live = x <= w1 - 2 && y <= h1 - 2;
+    bx0 = 1 + 16 * tx;
+    bx1 = bx0 + 15;
+    by0 = 1 + 16 * ty;
+    by1 = by0 + 15;
+  } else {
+    const int i = ((int)blockIdx.x - a.n_tiles) * 256 + tid;
+    const int nb = 2 * w1 + 2 * (h1 - 2);
+    live = i < nb;
+    const int ii = live ? i : 0;
+    if (ii < w1) { x = ii; y = 0; }
+    else if (ii < 2 * w1) { x = ii - w1; y = h1 - 1; }
+    else if (ii < 2 * w1 + h1 - 2) { x = 0; y = 1 + ii - 2 * w1; }
+    else { x = w1 - 1; y = 1 + ii - (2 * w1 + h1 - 2); }
+    int mnx = live ? x : 1 << 20, mxx = live ? x : -(1 << 20), mny = live ? y : 1 << 20, mxy = live ? y : -(1 << 20);
+    for (int o = 32; o > 0; o >>= 1) {
+      mnx = min(mnx, __shfl_xor(mnx, o));
+      mxx = max(mxx, __shfl_xor(mxx, o));
+      mny = min(mny, __shfl_xor(mny, o));
+      mxy = max(mxy, __shfl_xor(mxy, o));
+    }
+    bx0 = __builtin_amdgcn_readfirstlane(mnx);
+    bx1 = __builtin_amdgcn_readfirstlane(mxx);
+    by0 = __builtin_amdgcn_readfirstlane(mny);
+    by1 = __builtin_amdgcn_readfirstlane(mxy);
+  }
+  const int q = live ? x + w1 * y : 0;
+  auto val = [&](int c) { const uint8_t b = a.init[c]; return b == 255 ? 1000 : (int)b; };
   int v = live ? val(q) : 1000;
+  const int self = x | (y << 16);
   int nb[3] = {-1, -1, -1}, nv[3] = {1000, 1000, 1000};
-  if (live && !interior) {
-    // every neighbour that is interior (a border cell of the top row / left column has them too)
+  if (!itile && live) {
     int k = 0;
     for (int dy = -1; dy <= 1; dy++)
       for (int dx = -1; dx <= 1; dx++) {
         const int nx = x + dx, ny = y + dy;
         if ((dx | dy) == 0 || nx < 1 || nx > w1 - 2 || ny < 1 || ny > h1 - 2 || k >= 3) continue;
         nb[k] = nx | (ny << 16);
-        nv[k] = val(nx + w1 * ny);
+        nv[k] = a.mode ? val(nx + w1 * ny) : 1000;  // mode 1: the neighbours' values before the first seed
         k++;
       }
   }
+  const int reach = itile ? R : R + 1;
   const int ns = *a.n_seeds;
-  const int self = x | (y << 16);
   for (int t0 = 0; t0 < ns; t0 += 1024) {
     const int tn = min(1024, ns - t0);
     __syncthreads();
-    for (int i = threadIdx.x; i < tn; i += blockDim.x) tile[i] = a.seeds[t0 + i];
+    for (int i = tid; i < tn; i += blockDim.x) tile[i] = a.seeds[t0 + i];
     __syncthreads();
-    if (!live) continue;
     for (int i = 0; i < tn; i++) {
-      const int sc = tile[i];
+      const int sc = __builtin_amdgcn_readfirstlane(tile[i]);
       const int sx = sc & 0xffff, sy = sc >> 16;
-      if ((sx == w1 - 1) | (sy == h1 - 1)) {
+      if (sx < bx0 - reach || sx > bx1 + reach || sy < by0 - reach || sy > by1 + reach) continue;  // uniform
+      if ((sx == w1 - 1) | (sy == h1 - 1)) {  // a border seed only sets itself (mode 0: already 0 in init)
         if (sc == self) v = 0;
         continue;
       }
-      if (interior) {
+      if (itile) {
         const int d = bfs_dist(x - sx, y - sy);
-        if (d <= HS_ACT_BFS_STEPS - 1) v = min(v, d);
-      } else {
+        v = min(v, d <= R ? d : 1000);
+      } else if (a.mode) {
         if (sc == self) v = 0;
-        border_step(x, y, sc, HS_ACT_BFS_STEPS - 1, nb, v, nv);
+        border_step(x, y, sc, R, nb, v, nv);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+          const int d = bfs_dist((nb[k] & 0xffff) - sx, (nb[k] >> 16) - sy);
+          if (d <= R) nv[k] = min(nv[k], d);
+        }
       }
     }
   }
-  if (live) a.dist[q] = v >= 255 ? 255 : (uint8_t)v;
+  if (!live) return;
+  if (!itile && !a.mode) {  // makeDistanceMap: every reached interior neighbour was expanded
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      if (nb[k] < 0 || nv[k] >= 1000) continue;
+      const int t = nv[k] + 1;
+      const bool diag = ((nb[k] & 0xffff) != x) & ((nb[k] >> 16) != y);
+      if (t <= R && (!diag || (t & 1))) v = min(v, t);
+    }
+  }
+  a.out[q] = v >= 255 ? 255 : (uint8_t)v;
 }
 
 __global__ void __launch_bounds__(256) hs_k_act_optimize(HsActOptArgs a) {

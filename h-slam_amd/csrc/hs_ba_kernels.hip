@@ -2197,15 +2197,7 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     // the reference's own 1- vs 8-thread spread)
     if ((a.dbg & 8) && a.trace && tid == 0) a.trace[20] = clock64();
     for (int rep = 0; rep < ((a.dbg & 8) ? 2 : 1); rep++) {
-      if (a.dbg & 64) {  // experiment: the single-wave LDLT
-        if (tid < 64) {
-          if (a.dbg & 128) ldlt_factor_wave_pipe(A, LT, B, yv, n, tid);
-          else ldlt_factor_wave(A, LT, B, yv, n, tid);
-          ldlt_backward(LT, B, yv, n, tid, a.trace);
-        }
-      } else {
-        ldlt_solve_blocked(A, LT, B, yv, n, tid, a.trace, a.dbg);
-      }
+      ldlt_solve_blocked(A, LT, B, yv, n, tid, a.trace, a.dbg);
       __syncthreads();
       if ((a.dbg & 8) && a.trace && tid == 0) a.trace[21 + rep] = clock64();
     }

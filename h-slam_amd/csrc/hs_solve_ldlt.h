@@ -1,5 +1,5 @@
-// hs_solve_ldlt.h -- the fp64 LDLT pieces of hs_k_solve shared with tools/micro/ldlt_wave.hip: the single-wave
-// factorization (lane = frame row) and the backward pass.  Device code; include after hip_runtime.h.
+// hs_solve_ldlt.h -- fp64 pieces of hs_k_solve's LDLT shared with tools/micro/ldlt_wave.hip: readlane / reciprocal
+// helpers and the backward pass.  Device code; include after hip_runtime.h.
 #pragma once
 #include <cfloat>
 
@@ -84,194 +84,6 @@ __device__ __forceinline__ void ldlt_backward(const double* LT, double* W, doubl
     if (i < n && i < 64) yv[i] = y;
     if (trace && tid == 0) trace[13] = wall_clock64();
   }
-}
-
-// Single-wave right-looking LDLT (no workgroup barrier): lane l holds row l + 4 of the scaled system in registers
-// (68 doubles), the calib rows 0..3 are uniform and go first.  Per pivot k: the pivot by readlane (uniform for the
-// calib pivots), its reciprocal, the column A(m, k) broadcast through 64 doubles of LDS (one wave: LDS operations
-// complete in order, so the next pivot's store cannot overtake this pivot's loads), then one FMA per trailing
-// column on every lane, 8 columns per scheduling group (the loads of a group in flight together, no more: the row
-// already takes 136 registers); the rhs is forward-substituted alongside.  L goes to LT as it is formed
-// (LT[k * LSTR + r] = L(r, k)), with the pivots Dv and the forward-substituted rhs yf, for ldlt_backward.
-// Wave 0 only.
-template <int K, int MD>
-__device__ __forceinline__ void ldlt_wave_update(double (&a)[MD], double lk, const double* colb) {
-  // a[m] -= lk A(m, K) for m = K+1 .. MD-1, in groups of 8 columns
-#pragma unroll
-  for (int c0 = K + 1; c0 < MD; c0 += 8) {
-    asm volatile("" ::: "memory");
-    double cv[8];
-#pragma unroll
-    for (int q = 0; q < 8; q++)
-      if (c0 + q < MD) cv[q] = colb[c0 + q - 4];
-#pragma unroll
-    for (int q = 0; q < 8; q++)
-      if (c0 + q < MD) a[c0 + q] = __builtin_fma(-lk, cv[q], a[c0 + q]);
-    // the group's updates happen here: without these pins the scheduler runs ahead on the pivot chain and keeps
-    // the deferred groups' loaded columns live (thousands of spilled registers)
-#pragma unroll
-    for (int q = 0; q < 8; q++)
-      if (c0 + q < MD) asm volatile("" : "+v"(a[c0 + q]));
-  }
-}
-
-template <int K, int MD>
-__device__ __forceinline__ void ldlt_wave_frames(double (&a)[MD], double& y, double* colb, double* LT, double* Dv,
-                                                 int n, int lane, int r, bool live) {
-  if constexpr (K < MD) {
-    {  // K >= n: the pivot lane is past the window (zero row): d = 0, dinv = 0, lk = 0, nothing changes
-      constexpr int p = K - 4;
-      const double d = readlane_f64(a[K], p);
-      const double yk = readlane_f64(y, p);
-      colb[lane] = a[K];
-      const double dinv = rcp_f64(d);
-      const bool below = lane > p;
-      const double lk = below ? a[K] * dinv : 0.0;
-      y = __builtin_fma(-lk, yk, y);
-      if (below && live) LT[K * LSTR + r] = lk;
-      if (lane == 0) Dv[K] = d;
-      ldlt_wave_update<K, MD>(a, lk, colb);
-      ldlt_wave_frames<K + 1, MD>(a, y, colb, LT, Dv, n, lane, r, live);
-    }
-  }
-}
-
-static __device__ __attribute__((noinline)) void ldlt_factor_wave(const double* M, double* LT, double* W, const double* yv, int n,
-                                                 int lane) {
-  constexpr int MD = HS_MAXDIM;
-  static_assert(MD == 68, "lane = frame row: 64 frame rows + 4 calib rows");
-  double* colb = W;  // [64]
-  double* Dv = W + 24 * MD;
-  double* yf = W + 25 * MD;
-  const int r = lane + 4;
-  const bool live = r < n;
-  const int rr = live ? r : 4;
-  double a[MD];
-#pragma unroll
-  for (int j = 0; j < MD; j++) a[j] = (live && j < n) ? M[rr * n + j] : 0.0;
-  double y = live ? yv[rr] : 0.0;
-  double C[4][4], yc[4];
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    yc[i] = yv[i];
-#pragma unroll
-    for (int j = 0; j < 4; j++) C[i][j] = M[i * n + j];
-  }
-#pragma unroll
-  for (int k = 0; k < 4; k++) {  // the calib pivots (uniform)
-    const double d = C[k][k];
-    const double dinv = rcp_f64(d);
-    colb[lane] = a[k];
-    const double lk = a[k] * dinv;
-    double lc[4];
-#pragma unroll
-    for (int j = k + 1; j < 4; j++) lc[j] = C[j][k] * dinv;
-    y = __builtin_fma(-lk, yc[k], y);
-#pragma unroll
-    for (int j = k + 1; j < 4; j++) yc[j] = __builtin_fma(-lc[j], yc[k], yc[j]);
-#pragma unroll
-    for (int m = k + 1; m < 4; m++) a[m] = __builtin_fma(-lk, C[m][k], a[m]);
-#pragma unroll
-    for (int j = k + 1; j < 4; j++)
-#pragma unroll
-      for (int m = k + 1; m <= j; m++) C[j][m] = __builtin_fma(-lc[j], C[m][k], C[j][m]);
-    if (live) LT[k * LSTR + r] = lk;
-    if (lane == 0) {
-      Dv[k] = d;
-      yf[k] = yc[k];
-#pragma unroll
-      for (int j = k + 1; j < 4; j++) LT[k * LSTR + j] = lc[j];
-    }
-    ldlt_wave_update<3, MD>(a, lk, colb);  // columns 4 .. MD-1 (the calib columns m < 4 were updated above)
-  }
-  ldlt_wave_frames<4, MD>(a, y, colb, LT, Dv, n, lane, r, live);
-  if (live) yf[r] = y;
-}
-
-// The same factorization software-pipelined by one pivot: step K first applies its update to column K + 1 and the
-// rhs, publishes column K + 1 (the other of two LDS column buffers) and forms pivot K + 1 (readlane, reciprocal)
-// -- that dependent chain then overlaps step K's remaining column groups instead of following them.
-template <int K, int MD>
-__device__ __forceinline__ void ldlt_wave_pipe(double (&a)[MD], double& y, double* colb, double* LT, double* Dv,
-                                               int lane, int r, bool live, double lk, double yk) {
-  if constexpr (K < MD) {
-    const double* cb = colb + (K & 1) * 64;  // column K: A(m, K) of rows m > K (lane m - 4)
-    double* cn = colb + ((K + 1) & 1) * 64;
-    y = __builtin_fma(-lk, yk, y);
-    double lk1 = 0.0, yk1 = 0.0;
-    if constexpr (K + 1 < MD) {
-      a[K + 1] = __builtin_fma(-lk, cb[K + 1 - 4], a[K + 1]);
-      constexpr int p1 = K + 1 - 4;
-      const double d1 = readlane_f64(a[K + 1], p1);
-      yk1 = readlane_f64(y, p1);
-      cn[lane] = a[K + 1];
-      const double dinv1 = rcp_f64(d1);
-      lk1 = lane > p1 ? a[K + 1] * dinv1 : 0.0;
-      if (lane == 0) Dv[K + 1] = d1;
-      asm volatile("" : "+v"(a[K + 1]), "+v"(lk1), "+v"(y));
-    }
-    if (lane > K - 4 && live) LT[K * LSTR + r] = lk;
-    ldlt_wave_update<K + 1, MD>(a, lk, cb);  // columns K + 2 .. MD - 1
-    ldlt_wave_pipe<K + 1, MD>(a, y, colb, LT, Dv, lane, r, live, lk1, yk1);
-  }
-}
-
-static __device__ __attribute__((noinline)) void ldlt_factor_wave_pipe(const double* M, double* LT, double* W, const double* yv, int n,
-                                                      int lane) {
-  constexpr int MD = HS_MAXDIM;
-  double* colb = W;  // [2][64]
-  double* Dv = W + 24 * MD;
-  double* yf = W + 25 * MD;
-  const int r = lane + 4;
-  const bool live = r < n;
-  const int rr = live ? r : 4;
-  double a[MD];
-#pragma unroll
-  for (int j = 0; j < MD; j++) a[j] = (live && j < n) ? M[rr * n + j] : 0.0;
-  double y = live ? yv[rr] : 0.0;
-  double C[4][4], yc[4];
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    yc[i] = yv[i];
-#pragma unroll
-    for (int j = 0; j < 4; j++) C[i][j] = M[i * n + j];
-  }
-  double* cb = colb + 64;  // the calib steps' column buffer (the frame steps start at buffer 0)
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const double d = C[k][k];
-    const double dinv = rcp_f64(d);
-    cb[lane] = a[k];
-    const double lk = a[k] * dinv;
-    double lc[4];
-#pragma unroll
-    for (int j = k + 1; j < 4; j++) lc[j] = C[j][k] * dinv;
-    y = __builtin_fma(-lk, yc[k], y);
-#pragma unroll
-    for (int j = k + 1; j < 4; j++) yc[j] = __builtin_fma(-lc[j], yc[k], yc[j]);
-#pragma unroll
-    for (int m = k + 1; m < 4; m++) a[m] = __builtin_fma(-lk, C[m][k], a[m]);
-#pragma unroll
-    for (int j = k + 1; j < 4; j++)
-#pragma unroll
-      for (int m = k + 1; m <= j; m++) C[j][m] = __builtin_fma(-lc[j], C[m][k], C[j][m]);
-    if (live) LT[k * LSTR + r] = lk;
-    if (lane == 0) {
-      Dv[k] = d;
-      yf[k] = yc[k];
-#pragma unroll
-      for (int j = k + 1; j < 4; j++) LT[k * LSTR + j] = lc[j];
-    }
-    ldlt_wave_update<3, MD>(a, lk, cb);
-  }
-  // pivot 4 (lane 0), then the pipelined frame steps
-  const double d4 = readlane_f64(a[4], 0);
-  const double yk4 = readlane_f64(y, 0);
-  colb[lane] = a[4];
-  const double lk4 = lane > 0 ? a[4] * rcp_f64(d4) : 0.0;
-  if (lane == 0) Dv[4] = d4;
-  ldlt_wave_pipe<4, MD>(a, y, colb, LT, Dv, lane, r, live, lk4, yk4);
-  if (live) yf[r] = y;
 }
 
 }  // namespace hs_solve

@@ -525,6 +525,20 @@ int hs_tracer_activate(hs_tracer* t, const float K4[4], int nF, const hs_act_fra
     hipLaunchKernelGGL(hs_k_act_cand, dim3((m + 255) / 256), dim3(256), 0, s, ca);
     TR_HIP(hipGetLastError());
   }
+  // makeDistanceMap's growDistBFS over the seeds
+  HsActDistArgs ma;
+  ma.w1 = t->w1;
+  ma.h1 = t->h1;
+  ma.mode = 0;
+  ma.n_tiles_x = (t->w1 - 2 + 15) / 16;
+  ma.n_tiles = ma.n_tiles_x * ((t->h1 - 2 + 15) / 16);
+  const int dist_blocks = ma.n_tiles + (2 * t->w1 + 2 * (t->h1 - 2) + 255) / 256;
+  ma.seeds = t->d_list_a;
+  ma.n_seeds = t->d_act_cnt;
+  ma.init = t->d_dist;
+  ma.out = reinterpret_cast<uint8_t*>(t->d_list_b);
+  hipLaunchKernelGGL(hs_k_act_dist, dim3(dist_blocks), dim3(256), 0, s, ma);
+  TR_HIP(hipGetLastError());
   HsActSelectArgs se;
   se.m = m;
   se.w1 = t->w1;
@@ -537,42 +551,38 @@ int hs_tracer_activate(hs_tracer* t, const float K4[4], int nF, const hs_act_fra
   se.frac = t->d_frac;
   se.thr = t->d_thr;
   se.dist = t->d_dist;
-  se.list_a = t->d_list_a;
-  se.list_b = t->d_list_b;
-  se.seed_count = t->d_act_cnt;
-  se.map0 = reinterpret_cast<uint8_t*>(t->d_list_b);  // free once the seed BFS is done
+  se.map0 = reinterpret_cast<uint8_t*>(t->d_list_b);
   se.seeds = t->d_act_seeds;
   se.toopt = t->d_toopt;
   se.n_toopt = t->d_act_cnt + 1;
   static const bool prof_on = getenv("HS_ACT_PROF") != nullptr;
   long long* d_prof = nullptr;
-  if (prof_on) TR_HIP(hipMalloc((void**)&d_prof, sizeof(long long) * 8));
+  if (prof_on) TR_HIP(hipMalloc((void**)&d_prof, sizeof(long long) * 10));
   se.prof = d_prof;
   const size_t lds = se.lds_map ? map_bytes : 0;
   if (lds > 65536)
     TR_HIP(hipFuncSetAttribute((const void*)hs_k_act_select, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(hs_k_act_select, dim3(1), dim3(1024), lds, s, se);
   TR_HIP(hipGetLastError());
-  HsActFinalArgs fa;
-  fa.w1 = t->w1;
-  fa.h1 = t->h1;
-  fa.map0 = se.map0;
+  HsActDistArgs fa = ma;  // the map the greedy loop leaves
+  fa.mode = 1;
   fa.seeds = se.seeds;
   fa.n_seeds = se.n_toopt;
-  fa.dist = t->d_dist;
-  hipLaunchKernelGGL(hs_k_act_final, dim3((wh1 + 255) / 256), dim3(256), 0, s, fa);
+  fa.init = ma.out;
+  fa.out = t->d_dist;
+  hipLaunchKernelGGL(hs_k_act_dist, dim3(dist_blocks), dim3(256), 0, s, fa);
   TR_HIP(hipGetLastError());
   int cnt[2] = {0, 0};
   TR_HIP(hipMemcpyAsync(cnt, t->d_act_cnt, sizeof(cnt), hipMemcpyDeviceToHost, s));
   TR_HIP(hipStreamSynchronize(s));
   const int n_toopt = cnt[1];
   if (d_prof) {
-    long long pr[8];
+    long long pr[10];
     TR_HIP(hipMemcpy(pr, d_prof, sizeof(pr), hipMemcpyDeviceToHost));
     TR_HIP(hipFree(d_prof));
-    fprintf(stderr, "hs act prof: seed BFS %.1f us, greedy %.1f us (wall_clock64 @100 MHz), %d selected; "
-            "%lld batches, %lld seed patches of radius %lld; core clock %.0f MHz\n",
-            (pr[1] - pr[0]) * 1e-2, (pr[2] - pr[1]) * 1e-2, n_toopt, pr[3], pr[4], pr[5],
+    fprintf(stderr, "hs act prof: prologue %.1f us, greedy %.1f us (decisions %.1f, folds %.1f; wall_clock64 @100 MHz), "
+            "%d selected; %lld batches, %lld seed patches of radius %lld; core clock %.0f MHz\n",
+            (pr[1] - pr[0]) * 1e-2, (pr[2] - pr[1]) * 1e-2, pr[8] * 1e-2, pr[9] * 1e-2, n_toopt, pr[3], pr[4], pr[5],
             (double)(pr[7] - pr[6]) / ((pr[2] - pr[1]) * 1e-2));
   }
   if (n_toopt > 0) {

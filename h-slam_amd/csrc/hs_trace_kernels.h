@@ -95,7 +95,18 @@ struct HsActCandArgs {
   uint8_t* action;   // [n points] HS_ACT_*
 };
 
-// the sequential part: multi-source BFS, then the greedy distance test + addIntoDistFinal in loop order
+// a distance map from seeds in closed form (hs_act_kernels.hip bfs_dist): mode 0, makeDistanceMap's multi-seed
+// growDistBFS (Src/CoarseTracker.cpp:726-756); mode 1, the map the greedy loop leaves (makeDistanceMap's map + every
+// addIntoDistFinal, in call order).  Interior cells in 16 x 16 tiles, then the border cells, one thread each.
+struct HsActDistArgs {
+  int w1, h1, mode, n_tiles_x, n_tiles;
+  const int* seeds;          // cells x | y << 16
+  const int* n_seeds;
+  const uint8_t* init;       // [w1*h1] mode 0: 0 at the seeds, 255 elsewhere; mode 1: makeDistanceMap's map
+  uint8_t* out;              // [w1*h1]
+};
+
+// the sequential part: the greedy distance test + addIntoDistFinal in loop order
 struct HsActSelectArgs {
   int m, w1, h1, lds_map;
   const int* order;
@@ -103,24 +114,12 @@ struct HsActSelectArgs {
   const int* cell;
   const float* frac;
   const float* thr;
-  uint8_t* dist;             // global map (in: seeded; out: the greedy loop's working map, see hs_k_act_final)
-  int* list_a;               // [w1*h1] frontier lists
-  int* list_b;
-  const int* seed_count;
-  uint8_t* map0;             // [w1*h1] out: makeDistanceMap's map (the multi-source BFS), for hs_k_act_final
+  uint8_t* dist;             // global working map when the map does not fit LDS (then hs_k_act_dist mode 1 overwrites it)
+  const uint8_t* map0;       // [w1*h1] makeDistanceMap's map (hs_k_act_dist mode 0)
   int* seeds;                // [m] out: the cells addIntoDistFinal was called on, in call order
   int* toopt;                // [m] points to optimize, in order (+ 64 scratch slots after m)
   int* n_toopt;
   long long* prof;           // nullable: wall_clock64 at entry, after the seed BFS, at exit (HS_ACT_PROF=1)
-};
-
-// the distance map the reference leaves behind: makeDistanceMap's map + every addIntoDistFinal, one thread per cell
-struct HsActFinalArgs {
-  int w1, h1;
-  const uint8_t* map0;
-  const int* seeds;
-  const int* n_seeds;
-  uint8_t* dist;
 };
 
 // optimizeImmaturePoint, one wave per point to optimize
@@ -149,6 +148,6 @@ struct HsActOptArgs {
 
 __global__ void hs_k_act_seed(HsActSeedArgs a);
 __global__ void hs_k_act_cand(HsActCandArgs a);
+__global__ void hs_k_act_dist(HsActDistArgs a);
 __global__ void hs_k_act_select(HsActSelectArgs a);
-__global__ void hs_k_act_final(HsActFinalArgs a);
 __global__ void hs_k_act_optimize(HsActOptArgs a);

@@ -130,9 +130,40 @@ def _closed_form_add(m, sx, sy, w1, h1):
     return new
 
 
+def _closed_form_seeds(seeds, w1, h1):
+    """hs_k_act_map0: makeDistanceMap's multi-seed growDistBFS in closed form -- interior cells the minimum of the
+    interior seeds' distances, border cells k_n + 1 from their interior neighbours, border seeds only themselves."""
+    m = np.full((h1, w1), 1000, np.int32)
+    ys, xs = np.mgrid[0:h1, 0:w1]
+    d = np.full((h1, w1), 1000, np.int32)
+    for (x, y) in seeds:
+        m[y, x] = 0
+        if x == 0 or y == 0 or x == w1 - 1 or y == h1 - 1:
+            continue
+        ax, ay = np.abs(xs - x), np.abs(ys - y)
+        dd = np.maximum(np.maximum(ax, ay), (2 * (ax + ay) + 1) // 3)
+        d = np.minimum(d, np.where(dd <= 39, dd, 1000))
+    inner = np.zeros((h1, w1), bool)
+    inner[1:-1, 1:-1] = True
+    out = m.copy()
+    out[inner] = np.minimum(m, d)[inner]
+    for by, bx in zip(*np.nonzero(~inner)):
+        v = out[by, bx]
+        for ny in (by - 1, by, by + 1):
+            for nx in (bx - 1, bx, bx + 1):
+                if not (1 <= nx <= w1 - 2 and 1 <= ny <= h1 - 2) or out[ny, nx] >= 1000:
+                    continue
+                t = out[ny, nx] + 1
+                if t <= 39 and (nx == bx or ny == by or t % 2 == 1):
+                    v = min(v, t)
+        out[by, bx] = v
+    return out
+
+
 def test_closed_form_bfs_matches_grow_dist_bfs():
-    """The activation kernel replaces addIntoDistFinal's BFS by a closed form (hs_act_kernels.hip bfs_dist,
-    border_step; hs_k_act_final).  Random small maps: makeDistanceMap's multi-seed BFS, then a sequence of
+    """The activation kernels replace growDistBFS by a closed form (hs_act_kernels.hip bfs_dist, border_step;
+    hs_k_act_map0, hs_k_act_final).  Random small maps: makeDistanceMap's multi-seed BFS (against the closed form of
+    hs_k_act_map0), then a sequence of
     addIntoDistFinal calls (seeds anywhere the selection loop can put them: x, y > 0, borders included); after every
     call the closed form equals the reference's growDistBFS on every cell."""
     rng = np.random.default_rng(11)
@@ -143,6 +174,7 @@ def test_closed_form_bfs_matches_grow_dist_bfs():
         for (x, y) in seeds:
             m[y, x] = 0
         _grow_dist_bfs(m, sorted(seeds), w1, h1)
+        assert np.array_equal(_closed_form_seeds(sorted(seeds), w1, h1), m), (trial, (w1, h1))
         for _ in range(int(rng.integers(1, 10))):
             x, y = int(rng.integers(1, w1)), int(rng.integers(1, h1))
             ref = m.copy()
