@@ -498,6 +498,8 @@ def bench_keyframe(args):
                    "parallelism": "single GPU"},
         "phase_ms_per_keyframe": {p: float(np.median(v)) for p, v in ph.items()},
         "phase_ms_per_keyframe_mean": {p: float(np.mean(v)) for p, v in ph.items()},
+        "call_ms_per_keyframe": {c: float(np.median([r.get("call_s", {}).get(c, 0.0) for r in rows])) * 1e3
+                                 for c in sorted({c for r in rows for c in r.get("call_s", {})})},
         "setup_over_gn": float(np.median(ph["setup"]) / np.median(ph["optimize"])),
         "driver_wall_ms_per_keyframe": dt * 1e3 / args.steps,
         "roofline": None,

@@ -213,8 +213,12 @@ __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* ma
     nthr_ = a.thr[jc];
   };
   if (w0 && a.m > 0) fetch(lane);
-  const int rows = 2 * r + 1, wpr = (2 * r + 1 + 3) / 4 + 1, per_seed = rows * wpr;
-  long long t_dec = 0, t_fold = 0;
+  const int rows = 2 * r + 1, wpr = (2 * r + 1 + 3) / 4 + 1;
+  int wb_shift = 0, rb_shift = 0;
+  while ((1 << wb_shift) < wpr) wb_shift++;
+  while ((1 << rb_shift) < rows) rb_shift++;
+  const int ps_shift = wb_shift + rb_shift;
+  long long t_dec = 0, t_fold = 0, t_p1 = 0;
   for (int base = 0; base < a.m; base += 64) {
     const long long c0 = a.prof ? wall_clock64() : 0;
     if (w0) {
@@ -242,10 +246,7 @@ __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* ma
         if (bm == 0) break;  // every remaining entry of the batch fails: they stay immature
         const int first = (int)__builtin_ctzll(bm);
         const int sc = __builtin_amdgcn_readlane(cell, first);
-        if (lane == first) {
-          myslot = nt;
-          a.seeds[nt] = sc;
-        }
+        if (lane == first) myslot = nt;
         if (lane == 0) s_seeds[ns] = sc;
         ns++;
         nt++;
@@ -263,8 +264,11 @@ __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* ma
           border_step(x, y, sc, HS_ACT_BFS_STEPS - 1, nb, v, nv);
         }
       }
-      // one unconditional store per batch (the lanes not taken write their scratch slot toopt[m + lane])
+      // one unconditional store per batch (the lanes not taken write their scratch slot toopt[m + lane]); the
+      // batch's seeds from LDS (no global store inside the loop: its completion would be waited for with the
+      // next batch's prefetch)
       a.toopt[myslot >= 0 ? myslot : a.m + lane] = pt;
+      if (lane < ns) a.seeds[nt - ns + lane] = s_seeds[lane];
       if (lane == 0) {
         s_n[0] = ns;
         s_n[1] = (bxm + r + 1 >= w1 - 1) | (bym + r + 1 >= h1 - 1);
@@ -313,10 +317,13 @@ __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* ma
         }
       }
       lds_barrier();
+      if (a.prof) t_p1 += wall_clock64() - c1;
       // interior cells: min(map, k) over each seed's patch of radius r, one 4-cell word per (seed, row, word) item
-      for (int it = tid; it < ns * per_seed; it += nthr) {
-        const int j = it / per_seed, rem = it - j * per_seed;
-        const int row = rem / wpr, wi = rem - row * wpr;
+      // (items laid out in powers of two: shifts, no divisions)
+      for (int it = tid; it < (ns << ps_shift); it += nthr) {
+        const int j = it >> ps_shift, rem = it & ((1 << ps_shift) - 1);
+        const int row = rem >> wb_shift, wi = rem & ((1 << wb_shift) - 1);
+        if (row >= rows || wi >= wpr) continue;
         const int sc = s_seeds[j], sx = sc & 0xffff, sy = sc >> 16;
         if ((sx == w1 - 1) | (sy == h1 - 1)) continue;
         const int y = sy - r + row;
@@ -356,6 +363,7 @@ __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* ma
     a.prof[5] = r;
     a.prof[8] = t_dec;
     a.prof[9] = t_fold;
+    a.prof[10] = t_p1;
   }
   return nt;
 }
@@ -392,92 +400,124 @@ __global__ void __launch_bounds__(1024) hs_k_act_select(HsActSelectArgs a) {
 // step); a seed on the border only sets itself.  Mode 1, the map the greedy loop leaves: makeDistanceMap's map and
 // every addIntoDistFinal in call order -- interior cells the same minimum, border cells the sequential rule of
 // border_step (their neighbours' values before each seed).  Both checked against growDistBFS (tests/test_act.py).
-// Blocks [0, n_tiles): one 16 x 16 tile of interior cells; the tile's seeds are those within Chebyshev 39 of it
-// (a scalar test per seed: the seeds go through LDS in tiles of 1024 and are read as uniform values).  Blocks after:
-// 256 border cells each (every seed within Chebyshev 40 of the wave's cells).
+// Blocks [0, n_tiles): one 16 x 16 tile of interior cells; blocks after: 4 waves of border cells each, every wave
+// within one row or column.  Each wave takes only the seeds within reach of its cells (Chebyshev 39, 40 for border
+// cells): per chunk of 1024 seeds it compacts them, in seed order, into its own LDS list and reads them four at a
+// time as uniform values.
 __global__ void __launch_bounds__(256) hs_k_act_dist(HsActDistArgs a) {
-  __shared__ int tile[1024];
+  __shared__ int4 wtile[4][256];  // per wave: the seeds of the current chunk within reach of its cells, in order
   constexpr int R = HS_ACT_BFS_STEPS - 1;
-  const int w1 = a.w1, h1 = a.h1, tid = threadIdx.x;
+  const int w1 = a.w1, h1 = a.h1, tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
   const bool itile = (int)blockIdx.x < a.n_tiles;
+  if (((a.dbg & 1) && !itile) || ((a.dbg & 2) && itile)) return;
   int x, y;
   bool live;
-  int bx0, bx1, by0, by1;  // the cells' bounding box (uniform per wave)
-  if (itile) {
+  if (itile) {  // 16 x 16 interior cells; wave wv: rows 4 wv .. 4 wv + 3
     const int tx = blockIdx.x % a.n_tiles_x, ty = blockIdx.x / a.n_tiles_x;
     x = 1 + 16 * tx + (tid & 15);
     y = 1 + 16 * ty + (tid >> 4);
     live = x <= w1 - 2 && y <= h1 - 2;
-    bx0 = 1 + 16 * tx;
-    bx1 = bx0 + 15;
-    by0 = 1 + 16 * ty;
-    by1 = by0 + 15;
-  } else {
-    const int i = ((int)blockIdx.x - a.n_tiles) * 256 + tid;
-    const int nb = 2 * w1 + 2 * (h1 - 2);
-    live = i < nb;
-    const int ii = live ? i : 0;
-    if (ii < w1) { x = ii; y = 0; }
-    else if (ii < 2 * w1) { x = ii - w1; y = h1 - 1; }
-    else if (ii < 2 * w1 + h1 - 2) { x = 0; y = 1 + ii - 2 * w1; }
-    else { x = w1 - 1; y = 1 + ii - (2 * w1 + h1 - 2); }
-    int mnx = live ? x : 1 << 20, mxx = live ? x : -(1 << 20), mny = live ? y : 1 << 20, mxy = live ? y : -(1 << 20);
-    for (int o = 32; o > 0; o >>= 1) {
-      mnx = min(mnx, __shfl_xor(mnx, o));
-      mxx = max(mxx, __shfl_xor(mxx, o));
-      mny = min(mny, __shfl_xor(mny, o));
-      mxy = max(mxy, __shfl_xor(mxy, o));
-    }
-    bx0 = __builtin_amdgcn_readfirstlane(mnx);
-    bx1 = __builtin_amdgcn_readfirstlane(mxx);
-    by0 = __builtin_amdgcn_readfirstlane(mny);
-    by1 = __builtin_amdgcn_readfirstlane(mxy);
+  } else {  // border cells: each segment (top row, bottom row, left column, right column) padded to whole waves,
+            // so a wave's cells are at most 64 consecutive cells of one row or column
+    const int gw = ((int)blockIdx.x - a.n_tiles) * 4 + wv;  // global border wave
+    const int sw0 = (w1 + 63) / 64, sw1 = (h1 - 2 + 63) / 64;
+    int seg, off;
+    if (gw < sw0) { seg = 0; off = gw * 64; }
+    else if (gw < 2 * sw0) { seg = 1; off = (gw - sw0) * 64; }
+    else if (gw < 2 * sw0 + sw1) { seg = 2; off = (gw - 2 * sw0) * 64; }
+    else { seg = 3; off = (gw - 2 * sw0 - sw1) * 64; }
+    const int k = off + lane;
+    if (seg < 2) { x = k; y = seg == 0 ? 0 : h1 - 1; live = k < w1 && gw < 2 * sw0 + 2 * sw1; }
+    else { x = seg == 2 ? 0 : w1 - 1; y = 1 + k; live = k < h1 - 2 && gw < 2 * sw0 + 2 * sw1; }
   }
+  // the wave's bounding box (uniform)
+  int bx0 = live ? x : 1 << 20, bx1 = live ? x : -(1 << 20), by0 = live ? y : 1 << 20, by1 = live ? y : -(1 << 20);
+  for (int o = 32; o > 0; o >>= 1) {
+    bx0 = min(bx0, __shfl_xor(bx0, o));
+    bx1 = max(bx1, __shfl_xor(bx1, o));
+    by0 = min(by0, __shfl_xor(by0, o));
+    by1 = max(by1, __shfl_xor(by1, o));
+  }
+  if (__builtin_amdgcn_readfirstlane(bx1) < 0) return;  // no live cell in this wave
   const int q = live ? x + w1 * y : 0;
   auto val = [&](int c) { const uint8_t b = a.init[c]; return b == 255 ? 1000 : (int)b; };
   int v = live ? val(q) : 1000;
   const int self = x | (y << 16);
   int nb[3] = {-1, -1, -1}, nv[3] = {1000, 1000, 1000};
   if (!itile && live) {
-    int k = 0;
+    int kk = 0;
     for (int dy = -1; dy <= 1; dy++)
       for (int dx = -1; dx <= 1; dx++) {
         const int nx = x + dx, ny = y + dy;
-        if ((dx | dy) == 0 || nx < 1 || nx > w1 - 2 || ny < 1 || ny > h1 - 2 || k >= 3) continue;
-        nb[k] = nx | (ny << 16);
-        nv[k] = a.mode ? val(nx + w1 * ny) : 1000;  // mode 1: the neighbours' values before the first seed
-        k++;
+        if ((dx | dy) == 0 || nx < 1 || nx > w1 - 2 || ny < 1 || ny > h1 - 2 || kk >= 3) continue;
+        nb[kk] = nx | (ny << 16);
+        nv[kk] = a.mode ? val(nx + w1 * ny) : 1000;  // mode 1: the neighbours' values before the first seed
+        kk++;
       }
   }
   const int reach = itile ? R : R + 1;
-  const int ns = *a.n_seeds;
+  const int rx0 = bx0 - reach, rx1 = bx1 + reach, ry0 = by0 - reach, ry1 = by1 + reach;
+  const int ns = (a.dbg & 4) ? 0 : *a.n_seeds;
+  int* wt = reinterpret_cast<int*>(wtile[wv]);
   for (int t0 = 0; t0 < ns; t0 += 1024) {
     const int tn = min(1024, ns - t0);
-    __syncthreads();
-    for (int i = tid; i < tn; i += blockDim.x) tile[i] = a.seeds[t0 + i];
-    __syncthreads();
-    for (int i = 0; i < tn; i++) {
-      const int sc = __builtin_amdgcn_readfirstlane(tile[i]);
-      const int sx = sc & 0xffff, sy = sc >> 16;
-      if (sx < bx0 - reach || sx > bx1 + reach || sy < by0 - reach || sy > by1 + reach) continue;  // uniform
-      if ((sx == w1 - 1) | (sy == h1 - 1)) {  // a border seed only sets itself (mode 0: already 0 in init)
-        if (sc == self) v = 0;
-        continue;
-      }
-      if (itile) {
-        const int d = bfs_dist(x - sx, y - sy);
-        v = min(v, d <= R ? d : 1000);
-      } else if (a.mode) {
-        if (sc == self) v = 0;
-        border_step(x, y, sc, R, nb, v, nv);
-      } else {
+    // this wave's seeds of the chunk within reach, compacted in seed order (16 per lane, a wave prefix sum); the
+    // list is the wave's own LDS, whose operations complete in order: no barrier
+    unsigned int msk = 0u;
+    int sv[16];
 #pragma unroll
-        for (int k = 0; k < 3; k++) {
-          const int d = bfs_dist((nb[k] & 0xffff) - sx, (nb[k] >> 16) - sy);
-          if (d <= R) nv[k] = min(nv[k], d);
+    for (int j = 0; j < 16; j++) {
+      const int i = j * 64 + lane;  // coalesced
+      sv[j] = i < tn ? a.seeds[t0 + i] : 0;
+      const int sx = sv[j] & 0xffff, sy = sv[j] >> 16;
+      const bool r = i < tn && sx >= rx0 && sx <= rx1 && sy >= ry0 && sy <= ry1;
+      msk |= (unsigned int)r << j;
+    }
+    // seed order is i = j 64 + lane: compact chunk by chunk of 64 (j), each by a ballot prefix
+    int base = 0;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const bool r = (msk >> j) & 1u;
+      const unsigned long long bm = __ballot(r);
+      if (r) wt[base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u))] = sv[j];
+      base += (int)__popcll(bm);
+    }
+    // pad to a multiple of 4 with a seed out of reach of every cell
+    if (lane < ((4 - (base & 3)) & 3)) wt[base + lane] = 0x7000 | (0x7000 << 16);
+    const int n4 = (base + 3) >> 2;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int i4 = 0; i4 < n4; i4++) {
+      const int4 s4 = wtile[wv][i4];
+      const int sc4[4] = {__builtin_amdgcn_readfirstlane(s4.x), __builtin_amdgcn_readfirstlane(s4.y),
+                          __builtin_amdgcn_readfirstlane(s4.z), __builtin_amdgcn_readfirstlane(s4.w)};
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int sc = sc4[u];
+        const int sx = sc & 0xffff, sy = sc >> 16;
+        if ((sx == w1 - 1) | (sy == h1 - 1)) {  // a border seed only sets itself (mode 0: already 0 in init)
+          if (sc == self) v = 0;
+          continue;
+        }
+        if (itile) {
+          const int d = bfs_dist(x - sx, y - sy);
+          v = min(v, d <= R ? d : 1000);
+        } else if (a.mode) {
+          if (sc == self) v = 0;
+          border_step(x, y, sc, R, nb, v, nv);
+        } else {
+#pragma unroll
+          for (int k = 0; k < 3; k++) {
+            const int d = bfs_dist((nb[k] & 0xffff) - sx, (nb[k] >> 16) - sy);
+            if (d <= R) nv[k] = min(nv[k], d);
+          }
         }
       }
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
   if (!live) return;
   if (!itile && !a.mode) {  // makeDistanceMap: every reached interior neighbour was expanded

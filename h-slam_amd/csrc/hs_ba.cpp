@@ -185,7 +185,7 @@ int ensure_capacity(hs_ctx* c, int W, int H, int capP, int capBlk) {
   HS_TRY(dalloc(&c->d_th_nsurv, 2));
   HS_TRY(dalloc(&c->d_th_surv, HS_TH_SURV));
   HS_TRY(dalloc(&c->d_marg, capP));
-  HS_TRY(dalloc(&c->d_adHTdelta, FF * 8));
+  HS_TRY(dalloc(&c->d_adHTdelta, FF * 8 + 4));  // + cDeltaF
   HS_TRY(dalloc(&c->d_le_chunk, (size_t)(capP + 49) / 50));
   HS_TRY(dalloc(&c->d_le_out, 1));
   HS_TRY(dalloc(&c->d_ref_pts, (size_t)4 * capP));
@@ -234,33 +234,46 @@ void compute_projector(hs_ctx* c) {
   nullspace_projector(ns, n, c->P.solverModeDelta, c->Porth, &c->Nproj);
 }
 
-// the device state -> h_state.  After an optimize tail (hs_k_fix_frames) also the host-side rest of it: the newest
-// frame's setStateZero nullspaces (Include/Frame.h:166-190), the projector (fp64 Jacobi SVD, host) -> device, and the
-// fp32 adjoints the device computed -> adHostF / adTargetF (marginalize_points' setDeltaF)
+// the device state -> h_state.  After an optimize tail (hs_k_fix_frames) the newest frame's setStateZero nullspaces
+// (Include/Frame.h:166-190) are recomputed here on the host; the projector built from them is left to the next
+// solve launch (proj_stale) -- a window edit re-uploads every frame (upload_frames) and builds it anyway.
 int fetch_state(hs_ctx* c) {
-  const bool tail = c->tail_pending;
-  const size_t FF = (size_t)c->nF * c->nF;
   HS_HIP(hipMemcpyAsync(c->h_state, c->d_state, sizeof(HsDevState), hipMemcpyDeviceToHost, c->stream));
-  if (tail) {
-    c->adHostF.assign(FF * 64, 0.f);
-    c->adTargetF.assign(FF * 64, 0.f);
-    HS_HIP(hipMemcpyAsync(c->adHostF.data(), c->d_adHostF, sizeof(float) * FF * 64, hipMemcpyDeviceToHost, c->stream));
-    HS_HIP(hipMemcpyAsync(c->adTargetF.data(), c->d_adTargetF, sizeof(float) * FF * 64, hipMemcpyDeviceToHost,
-                          c->stream));
-  }
   HS_HIP(hipStreamSynchronize(c->stream));
   c->h_state_valid = true;
-  if (tail) {
+  if (c->tail_pending) {
     c->tail_pending = false;
     FrameH& f = c->h_state->frames[c->nF - 1];
     double sz[10];
     std::memcpy(sz, f.state_zero, sizeof(sz));
     f.setStateZero(sz);
-    compute_projector(c);
-    HS_HIP(hipMemcpyAsync(c->d_Nproj, c->Nproj.data(), sizeof(double) * 2 * c->dim() * HS_NNS, hipMemcpyHostToDevice,
-                          c->stream));
-    HS_HIP(hipStreamSynchronize(c->stream));
+    c->proj_stale = true;
   }
+  return HS_OK;
+}
+
+// the projector of the current frames' nullspaces -> device (before a solve, after an optimize tail)
+static int settle_projector(hs_ctx* c) {
+  if (c->tail_pending) HS_TRY(fetch_state(c));
+  if (!c->proj_stale) return HS_OK;
+  compute_projector(c);
+  HS_HIP(hipMemcpyAsync(c->d_Nproj, c->Nproj.data(), sizeof(double) * 2 * c->dim() * HS_NNS, hipMemcpyHostToDevice,
+                        c->stream));
+  HS_HIP(hipStreamSynchronize(c->stream));
+  c->proj_stale = false;
+  return HS_OK;
+}
+
+// HM / bM <- d_HM / d_bM after hs_ba_marginalize_points updated them on the device
+int sync_hm(hs_ctx* c) {
+  if (!c->hm_host_stale) return HS_OK;
+  const int n = c->dim();
+  c->HM.resize((size_t)n * n);
+  c->bM.resize(n);
+  HS_HIP(hipMemcpyAsync(c->HM.data(), c->d_HM, sizeof(double) * n * n, hipMemcpyDeviceToHost, c->stream));
+  HS_HIP(hipMemcpyAsync(c->bM.data(), c->d_bM, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+  HS_HIP(hipStreamSynchronize(c->stream));
+  c->hm_host_stale = false;
   return HS_OK;
 }
 
@@ -285,6 +298,7 @@ int upload_frames(hs_ctx* c) {
   HsDevState& S = *c->h_state;
   S.nF = nF;
   c->tail_pending = false;  // every frame's adjoints, precalc and the projector are rewritten from h_state
+  c->proj_stale = false;
   c->adHost.assign(FF * 64, 0.0);
   c->adTarget.assign(FF * 64, 0.0);
   c->adHostF.assign(FF * 64, 0.f);
@@ -370,10 +384,9 @@ static int launch_linearize(hs_ctx* c, int fuse, bool marg = false, bool accumul
   if (!fuse && c->d_p_HdiF_alt == c->hdif_solved) std::swap(c->d_p_HdiF, c->d_p_HdiF_alt);
   HsLinArgs a;
   std::memset(&a, 0, sizeof(a));
-  if (marg) {  // hs_ba_marginalize_points: flags, adHTdeltaF and cDeltaF uploaded by the caller
+  if (marg) {  // hs_ba_marginalize_points: flags uploaded, adHTdeltaF and cDeltaF formed by hs_k_marg_delta
     a.marg = c->d_marg;
     a.adHTdelta = c->d_adHTdelta;
-    for (int i = 0; i < 4; i++) a.cDelta[i] = c->cDelta[i];
     a.margPriorFac = c->P.idepthFixPriorMargFac;
   }
   a.img = c->d_img_all;
@@ -571,7 +584,7 @@ static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = fals
 }
 
 static int launch_solve(hs_ctx* c, int flags, int iteration, bool log) {
-  if (c->tail_pending) HS_TRY(fetch_state(c));  // the projector of the moved newest frame
+  if (c->tail_pending || c->proj_stale) HS_TRY(settle_projector(c));  // the moved newest frame's projector
   HsSolveArgs a;
   std::memset(&a, 0, sizeof(a));
   a.flags = flags;
@@ -733,7 +746,8 @@ static int gn_iterations(hs_ctx* c, int it0, int K, bool allow_break, double* en
   // HS_HOST_BREAK=1 read canbreak back after every iteration instead.
   const char* hb = std::getenv("HS_HOST_BREAK");
   const bool dev_brk = allow_break && !c->multi_rank() && !c->tracing && !(hb && hb[0] == '1');
-  if (c->tail_pending) HS_TRY(fetch_state(c));  // before any capture: launch_solve must not sync inside one
+  // before any capture: launch_solve must not sync inside one
+  if (c->tail_pending || c->proj_stale) HS_TRY(settle_projector(c));
   HS_TRY(set_loop_counters(c, it0, !graph));
   if (graph) {
     if (c->gexec && c->graph_hdif != c->d_p_HdiF) drop_graph(c);
@@ -1108,6 +1122,7 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
   c->HM.assign((size_t)n * n, 0.0);
   c->bM.assign(n, 0.0);
   c->hm_zero = true;
+  c->hm_host_stale = false;
   HS_TRY(upload_frames(c));
 
   // ---- uploads (the legacy whole-window path: pageable host arrays, synchronous)
@@ -1439,6 +1454,7 @@ int hs_ba_calc_energies(hs_ctx* c, double* energyL, double* energyM) {
     EL += ep;
   }
   // calcMEnergyF: delta . (2 bM + HM delta), delta = getStitchedDeltaF (Src/EnergyFunctional.cpp:842-846)
+  HS_TRY(sync_hm(c));
   std::vector<double> d(n);
   for (int i = 0; i < 4; i++) d[i] = (double)cd[i];
   for (int f = 0; f < nF; f++)
@@ -1490,6 +1506,7 @@ int hs_ba_set_marginal_prior(hs_ctx* c, const double* HM, const double* bM) {
   const int n = c->dim();
   c->HM.assign(HM, HM + n * n);
   c->bM.assign(bM, bM + n);
+  c->hm_host_stale = false;
   c->hm_zero = std::all_of(c->HM.begin(), c->HM.end(), [](double v) { return v == 0.0; });
   drop_graph(c);  // the solve's arguments depend on hm_zero
   HS_HIP(hipMemcpyAsync(c->d_HM, c->HM.data(), sizeof(double) * n * n, hipMemcpyHostToDevice, c->stream));
@@ -1513,54 +1530,36 @@ int hs_ba_marginalize_points(hs_ctx* c, int n, const int* points, double* HM_out
     if (flag[points[i]]) return fail(HS_ERR_INVALID, "duplicate point in the marginalization list");
     flag[points[i]] = 1;
   }
-  // EnergyFunctional::setDeltaF (Src/EnergyFunctional.cpp:128-152) from the current device state, in fp32
-  HS_TRY(fetch_state(c));
-  const HsDevState& S = *c->h_state;
-  std::vector<float> adHTd((size_t)nF * nF * 8);
-  for (int h = 0; h < nF; h++)
-    for (int t = 0; t < nF; t++) {
-      const int idx = h + t * nF;
-      float dh[8], dt[8];
-      for (int i = 0; i < 8; i++) {
-        dh[i] = (float)(S.frames[h].state[i] - S.frames[h].state_zero[i]);
-        dt[i] = (float)(S.frames[t].state[i] - S.frames[t].state_zero[i]);
-      }
-      for (int q = 0; q < 8; q++) {
-        float s1 = 0, s2 = 0;
-        for (int r = 0; r < 8; r++) s1 += dh[r] * c->adHostF[(size_t)idx * 64 + r * 8 + q];
-        for (int r = 0; r < 8; r++) s2 += dt[r] * c->adTargetF[(size_t)idx * 64 + r * 8 + q];
-        adHTd[(size_t)idx * 8 + q] = s1 + s2;
-      }
-    }
-  for (int i = 0; i < 4; i++) c->cDelta[i] = (float)S.calib.value_minus_value_zero[i];
-  {  // both uploads through the pinned staging, asynchronous (the stream sync below precedes any reuse of it)
-    const size_t off = ((size_t)c->nP + 15) & ~(size_t)15, ab = sizeof(float) * adHTd.size();
-    HS_HIP(c->rb_stage(off + ab));
-    c->rb_pending = true;
-    std::memcpy(c->h_rb, flag.data(), (size_t)c->nP);
-    std::memcpy(c->h_rb + off, adHTd.data(), ab);
-    if (c->nP > 0) HS_HIP(hipMemcpyAsync(c->d_marg, c->h_rb, c->nP, hipMemcpyHostToDevice, c->stream));
-    HS_HIP(hipMemcpyAsync(c->d_adHTdelta, c->h_rb + off, ab, hipMemcpyHostToDevice, c->stream));
-  }
-  // the pass; setNewFrameEnergyTH is not part of it
+  // EnergyFunctional::setDeltaF (Src/EnergyFunctional.cpp:128-152) from the device state, in fp32 (hs_k_marg_delta);
+  // the flags through the pinned staging, asynchronous (rb_pending: the next rb_stage waits for the copy)
+  HS_HIP(c->rb_stage((size_t)c->nP + 1));
+  c->rb_pending = true;
+  std::memcpy(c->h_rb, flag.data(), (size_t)c->nP);
+  if (c->nP > 0) HS_HIP(hipMemcpyAsync(c->d_marg, c->h_rb, c->nP, hipMemcpyHostToDevice, c->stream));
+  const int nd = nF * nF * 8 + 4;
+  hipLaunchKernelGGL(hs_k_marg_delta, dim3((nd + 255) / 256), dim3(256), 0, c->stream, c->d_state, c->d_adHostF,
+                     c->d_adTargetF, c->d_adHTdelta);
+  HS_HIP(hipGetLastError());
+  // the pass; setNewFrameEnergyTH is not part of it.  Then HM += w (M - Msc) on the device
   HS_TRY(launch_linearize(c, 0, true));
   HS_TRY(launch_reduce(c, true, true));
-  HS_HIP(hipStreamSynchronize(c->stream));
-  c->rb_pending = false;
-  c->haveSystem = true;
-  std::vector<double> M((size_t)dim * dim), Mb(dim), Msc((size_t)dim * dim), Mbsc(dim);
-  HS_TRY(hs_ba_get_system(c, 0, M.data(), Mb.data()));    // stitchDouble(M, Mb, usePrior = false)
-  HS_TRY(hs_ba_get_system(c, 2, Msc.data(), Mbsc.data()));  // accSSE_bot->stitchDouble(Msc, Mbsc)
+  const int nm = dim * dim + dim;
+  hipLaunchKernelGGL(hs_k_marg_update, dim3((nm + 255) / 256), dim3(256), 0, c->stream, c->d_sep, c->d_sep_aux,
+                     c->d_HM, c->d_bM, nF, c->SL(), (double)c->P.margWeightFac);
+  HS_HIP(hipGetLastError());
   // the window's linearization is consumed: the caller drops the points (hs_ba_set_window) and relinearizes
   c->haveSystem = false;
-  if (c->HM.size() != (size_t)dim * dim) c->HM.assign((size_t)dim * dim, 0.0);
-  if (c->bM.size() != (size_t)dim) c->bM.assign(dim, 0.0);
-  const double w = c->P.margWeightFac;
-  for (size_t i = 0; i < (size_t)dim * dim; i++) c->HM[i] += w * (M[i] - Msc[i]);
-  for (int i = 0; i < dim; i++) c->bM[i] += w * (Mb[i] - Mbsc[i]);
-  HS_TRY(hs_ba_set_marginal_prior(c, c->HM.data(), c->bM.data()));
-  if (HM_out) std::memcpy(HM_out, c->HM.data(), sizeof(double) * dim * dim);
-  if (bM_out) std::memcpy(bM_out, c->bM.data(), sizeof(double) * dim);
+  c->hm_host_stale = true;
+  if (c->hm_zero && n > 0) {
+    c->hm_zero = false;
+    drop_graph(c);  // the solve's arguments depend on hm_zero
+  }
+  if (HM_out || bM_out) {
+    HS_TRY(sync_hm(c));
+    c->rb_pending = false;
+    if (HM_out) std::memcpy(HM_out, c->HM.data(), sizeof(double) * dim * dim);
+    if (bM_out) std::memcpy(bM_out, c->bM.data(), sizeof(double) * dim);
+  }
   return HS_OK;
 }
 
@@ -1603,6 +1602,7 @@ static bool inverse8(const double* A, double* Ainv) {
 // host operation once per marginalized keyframe (not on the GN path).  HMn / bMn: the (dim-8) prior.
 int hs::marginalize_frame_prior(hs_ctx* c, int frame, std::vector<double>& HMn, std::vector<double>& bMn) {
   if (!c->h_state_valid) HS_TRY(fetch_state(c));
+  HS_TRY(sync_hm(c));
   const int od = c->dim(), nd = od - 8, f0 = 4 + 8 * frame;
   std::vector<double> HMc = c->HM, bMc = c->bM;
   if (HMc.size() != (size_t)od * od) HMc.assign((size_t)od * od, 0.0);

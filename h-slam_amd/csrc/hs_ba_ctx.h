@@ -130,8 +130,10 @@ struct hs_ctx {
   HsDevState* h_state = nullptr;  // pinned staging of the device state
   bool h_state_valid = false;     // h_state equals the device state (no solve since the last fetch / upload)
   bool brk_active = false;        // gn_iterations' device-side break: the launches carry the stop checks
-  bool tail_pending = false;      // hs_k_fix_frames moved the newest frame on the device: its nullspaces, the
-                                  // projector and the host adjoint copies follow at the next fetch_state
+  bool tail_pending = false;      // hs_k_fix_frames moved the newest frame on the device: the next fetch_state
+                                  // recomputes its nullspaces on the host and leaves the projector stale
+  bool proj_stale = false;        // Nproj predates the frames' nullspaces: the next solve launch recomputes it
+  bool hm_host_stale = false;     // d_HM / d_bM are newer than HM / bM (device marginalization): sync_hm
   int* h_ctl = nullptr;           // pinned: iteration, status, log_count
   bool haveSystem = false;        // a stitched, not yet solved system is in the slots
 
@@ -197,7 +199,6 @@ struct hs_ctx {
   float* d_adHTdelta = nullptr;  // [nF*nF][8] EnergyFunctional::adHTdeltaF for fixLinearizationF
   float* d_le_chunk = nullptr;   // hs_ba_calc_energies: per-chunk sums
   double* d_le_out = nullptr;
-  float cDelta[4] = {0, 0, 0, 0};
   // BA -> tracker hand-off (hs_tracker_set_ref_ba): points with an IN residual into the newest frame, compacted in
   // point order: cu | cv | cid | HdiF, and their count
   float* d_ref_pts = nullptr;
@@ -271,6 +272,7 @@ namespace hs {
 void drop_graph(hs_ctx* c);
 int ensure_capacity(hs_ctx* c, int W, int H, int capP, int capBlk);
 void bind_point_set(hs_ctx* c);   // d_u ... d_r_center = ps[cur]
+int sync_hm(hs_ctx* c);          // HM / bM <- d_HM / d_bM after a device marginalization
 int fetch_state(hs_ctx* c);
 void compute_projector(hs_ctx* c);
 int make_partition(hs_ctx* c);    // blk_begin / nblk / W / lin8 / th_multi from host_pt_begin

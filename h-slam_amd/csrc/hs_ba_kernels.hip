@@ -402,10 +402,11 @@ __device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int 
         jx += Jx[4 + i] * dp[i];
         jy += Jy[4 + i] * dp[i];
       }
+      const float* cd = a.adHTdelta + nF * nF * 8;  // cDeltaF after the pairs (hs_k_marg_delta)
 #pragma unroll
       for (int i = 0; i < 4; i++) {
-        cxx += Jx[i] * a.cDelta[i];
-        cyy += Jy[i] * a.cDelta[i];
+        cxx += Jx[i] * cd[i];
+        cyy += Jy[i] * cd[i];
       }
       const float dF = idep - idep0;
       const float Jpdx = jx + cxx + Jd0 * dF;
@@ -2504,6 +2505,43 @@ __global__ void hs_k_resub(HsResubArgs a) {
     const float nid = a.idepth[p] + 1.0f * step;
     a.idepth[p] = nid;
     a.idepth_zero[p] = nid;
+  }
+}
+
+// EnergyFunctional::setDeltaF (Src/EnergyFunctional.cpp:128-152) in fp32: adHTdeltaF[h + nF t] = delta_h^T adHostF +
+// delta_t^T adTargetF (each dot product in index order), cDeltaF = (float) calib.value_minus_value_zero.  One thread
+// per (pair, entry).
+__global__ void hs_k_marg_delta(const HsDevState* st, const float* adHF, const float* adTF, float* adHTd) {
+  const int nF = st->nF, o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o < nF * nF * 8) {
+    const int idx = o >> 3, q = o & 7, h = idx % nF, t = idx / nF;
+    float s1 = 0, s2 = 0;
+    for (int r = 0; r < 8; r++) s1 += (float)(st->frames[h].state[r] - st->frames[h].state_zero[r]) * adHF[idx * 64 + r * 8 + q];
+    for (int r = 0; r < 8; r++) s2 += (float)(st->frames[t].state[r] - st->frames[t].state_zero[r]) * adTF[idx * 64 + r * 8 + q];
+    adHTd[o] = s1 + s2;
+  } else if (o < nF * nF * 8 + 4) {
+    adHTd[o] = (float)st->calib.value_minus_value_zero[o - nF * nF * 8];
+  }
+}
+
+// EnergyFunctional::marginalizePointsF's prior update (Src/EnergyFunctional.cpp:596-606): HM += w (M - Msc),
+// bM += w (Mb - Mbsc) with M | Mb = HA | bA and Msc | Mbsc = HSC | bSC of the separate stitch (upper triangles,
+// mirrored; HSC's diagonal blocks plus their host-f Schur terms), the same fp64 operations as the host form
+__global__ void hs_k_marg_update(const double* sep, const double* sep_aux, double* HM, double* bM, int nF, int SL,
+                                 double w) {
+  const int n = 4 + 8 * nF, o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o < n * n) {
+    const int r = o / n, q = o - r * n, lo = min(r, q), hi = max(r, q);
+    const double m = sep[lo * n + hi];
+    double msc = sep[SL + lo * n + hi];
+    if (lo >= 4 && (lo - 4) / 8 == (hi - 4) / 8) {
+      const int f = (lo - 4) / 8;
+      msc += sep_aux[f * 64 + (lo - 4 - 8 * f) * 8 + (hi - 4 - 8 * f)];
+    }
+    HM[o] += w * (m - msc);
+  } else if (o < n * n + n) {
+    const int r = o - n * n;
+    bM[r] += w * (sep[n * n + r] - sep[SL + n * n + r]);
   }
 }
 

@@ -238,6 +238,7 @@ int commit(hs_ctx* c) {
   std::memcpy(c->res_of_slot.data(), ros, sizeof(int) * 8 * (size_t)nP);
   std::memcpy(c->res_order.data(), rord, 8 * (size_t)nP);
   if (k > 0) std::memcpy(stg, c->staged.data(), sizeof(HsStagedPoint) * k);
+  HS_TRY(sync_hm(c));
   if ((int)c->HM.size() != n * n) c->HM.assign((size_t)n * n, 0.0);
   if ((int)c->bM.size() != n) c->bM.assign(n, 0.0);
   std::memcpy(hm, c->HM.data(), 8 * (size_t)n * n);
@@ -328,6 +329,7 @@ int hs_ba_reserve(hs_ctx* c, const hs_camera* cam, int max_points) {
   c->HM.clear();
   c->bM.clear();
   c->hm_zero = true;
+  c->hm_host_stale = false;
   c->cand_stride = c->cap_stride;
   c->cur = 0;
   bind_point_set(c);
@@ -371,6 +373,7 @@ int hs_ba_insert_frame(hs_ctx* c, const hs_frame* frame, const float* image) {
   c->wframes.push_back(w);
   c->wpts.emplace_back();
   // HM.conservativeResize + zero the new rows / columns (Src/EnergyFunctional.cpp:389-394)
+  HS_TRY(sync_hm(c));
   const int n1 = 4 + 8 * ((int)c->wframes.size() - 1), n2 = n1 + 8;
   std::vector<double> HM((size_t)n2 * n2, 0.0), bM(n2, 0.0);
   if ((int)c->HM.size() == n1 * n1)
@@ -590,6 +593,7 @@ int hs_ba_remove_frame(hs_ctx* c, int frame, int marginalize) {
   if (frame < 0 || frame >= (int)c->wframes.size()) return fail(HS_ERR_INVALID, "frame index out of range");
   if (!c->wpts[frame].empty()) return fail(HS_ERR_STATE, "the frame still hosts points (remove them first)");
   HS_TRY(commit_if_dirty(c));  // the prior's Schur complement needs the committed frame state and HM / bM
+  HS_TRY(sync_hm(c));
   const int od = c->dim(), nd = od - 8, f0 = 4 + 8 * frame;
   std::vector<double> HMn, bMn;
   if (marginalize) {
@@ -667,6 +671,7 @@ int hs_ba_synchronize(hs_ctx* c) {
 int hs_ba_get_marginal_prior(hs_ctx* c, double* HM, double* bM) {
   HS_TRY(ensure_incremental(c));
   HS_TRY(commit_if_dirty(c));
+  HS_TRY(sync_hm(c));
   const int n = c->dim();
   if (HM) {
     if ((int)c->HM.size() == n * n) std::memcpy(HM, c->HM.data(), sizeof(double) * n * n);

@@ -67,8 +67,7 @@ struct HsLinArgs {
   // resetOOB), their active residuals take fixLinearizationF, the SC prelude uses priorF * margPriorFac and no
   // prior shift; every other point reports no active residual.  nullptr = the normal pass.
   const uint8_t* marg;
-  const float* adHTdelta;      // [nF*nF][8] index host + nF*target (EnergyFunctional::adHTdeltaF)
-  float cDelta[4];             // EnergyFunctional::cDeltaF
+  const float* adHTdelta;      // [nF*nF][8] index host + nF*target (EnergyFunctional::adHTdeltaF), then cDeltaF [4]
   float margPriorFac;          // setting_idepthFixPriorMargFac
   const HsPrecalc* pre;        // [nF*nF] host*nF + target
   const float* frameTH;        // [nF]
@@ -241,6 +240,11 @@ __global__ void hs_k_apply_step(int n, const float* step, float* idepth, float* 
 // System::optimize's tail, frame part (Src/FullSystemOptimize.cpp:498-506) on the device: the newest frame's
 // setEvalPT(PRE_worldToCam, (0,..,0, a, b, 0, 0)) + takeData, then setAdjointsF + setPrecalcValues of every pair (one
 // thread per pair).  The nullspaces of the moved frame are left to the host (hs_ctx::frames_stale).  One block of 64.
+// hs_ba_marginalize_points on the device: EnergyFunctional::setDeltaF's adHTdeltaF [nF*nF][8] + cDeltaF [4] (after
+// them) from the window state; then HM += w (M - Msc), bM += w (Mb - Mbsc) from the separate stitch outputs
+__global__ void hs_k_marg_delta(const HsDevState* st, const float* adHF, const float* adTF, float* adHTd);
+__global__ void hs_k_marg_update(const double* sep, const double* sep_aux, double* HM, double* bM, int nF, int SL,
+                                 double w);
 __global__ void hs_k_fix_frames(HsDevState* st, HsPrecalc* pre, double* adH, double* adT, float* adHF, float* adTF,
                                 hs_params P);
 __global__ void hs_k_lenergy(int n, const float* idepth, const float* idepth_zero, const float* priorF, float* chunk,

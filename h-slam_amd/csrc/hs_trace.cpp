@@ -530,9 +530,12 @@ int hs_tracer_activate(hs_tracer* t, const float K4[4], int nF, const hs_act_fra
   ma.w1 = t->w1;
   ma.h1 = t->h1;
   ma.mode = 0;
+  static const int act_dbg = getenv("HS_ACT_DBG") ? atoi(getenv("HS_ACT_DBG")) : 0;
+  ma.dbg = act_dbg;
   ma.n_tiles_x = (t->w1 - 2 + 15) / 16;
   ma.n_tiles = ma.n_tiles_x * ((t->h1 - 2 + 15) / 16);
-  const int dist_blocks = ma.n_tiles + (2 * t->w1 + 2 * (t->h1 - 2) + 255) / 256;
+  const int border_waves = 2 * ((t->w1 + 63) / 64) + 2 * ((t->h1 - 2 + 63) / 64);
+  const int dist_blocks = ma.n_tiles + (border_waves + 3) / 4;
   ma.seeds = t->d_list_a;
   ma.n_seeds = t->d_act_cnt;
   ma.init = t->d_dist;
@@ -557,7 +560,7 @@ int hs_tracer_activate(hs_tracer* t, const float K4[4], int nF, const hs_act_fra
   se.n_toopt = t->d_act_cnt + 1;
   static const bool prof_on = getenv("HS_ACT_PROF") != nullptr;
   long long* d_prof = nullptr;
-  if (prof_on) TR_HIP(hipMalloc((void**)&d_prof, sizeof(long long) * 10));
+  if (prof_on) TR_HIP(hipMalloc((void**)&d_prof, sizeof(long long) * 11));
   se.prof = d_prof;
   const size_t lds = se.lds_map ? map_bytes : 0;
   if (lds > 65536)
@@ -577,12 +580,13 @@ int hs_tracer_activate(hs_tracer* t, const float K4[4], int nF, const hs_act_fra
   TR_HIP(hipStreamSynchronize(s));
   const int n_toopt = cnt[1];
   if (d_prof) {
-    long long pr[10];
+    long long pr[11];
     TR_HIP(hipMemcpy(pr, d_prof, sizeof(pr), hipMemcpyDeviceToHost));
     TR_HIP(hipFree(d_prof));
-    fprintf(stderr, "hs act prof: prologue %.1f us, greedy %.1f us (decisions %.1f, folds %.1f; wall_clock64 @100 MHz), "
-            "%d selected; %lld batches, %lld seed patches of radius %lld; core clock %.0f MHz\n",
-            (pr[1] - pr[0]) * 1e-2, (pr[2] - pr[1]) * 1e-2, pr[8] * 1e-2, pr[9] * 1e-2, n_toopt, pr[3], pr[4], pr[5],
+    fprintf(stderr, "hs act prof: prologue %.1f us, greedy %.1f us (decisions %.1f, folds %.1f of which border %.1f; "
+            "wall_clock64 @100 MHz), %d selected; %lld batches, %lld seed patches of radius %lld; core clock %.0f MHz\n",
+            (pr[1] - pr[0]) * 1e-2, (pr[2] - pr[1]) * 1e-2, pr[8] * 1e-2, pr[9] * 1e-2, pr[10] * 1e-2, n_toopt, pr[3],
+            pr[4], pr[5],
             (double)(pr[7] - pr[6]) / ((pr[2] - pr[1]) * 1e-2));
   }
   if (n_toopt > 0) {

@@ -100,6 +100,7 @@ struct HsActCandArgs {
 // addIntoDistFinal, in call order).  Interior cells in 16 x 16 tiles, then the border cells, one thread each.
 struct HsActDistArgs {
   int w1, h1, mode, n_tiles_x, n_tiles;
+  int dbg;                   // experiments (env HS_ACT_DBG): 1 border blocks return, 2 tile blocks return, 4 no seeds
   const int* seeds;          // cells x | y << 16
   const int* n_seeds;
   const uint8_t* init;       // [w1*h1] mode 0: 0 at the seeds, 255 elsewhere; mode 1: makeDistanceMap's map

@@ -304,13 +304,14 @@ class BAWindow:
         check(self.lib.hs_ba_set_marginal_prior(self.h, ptr(np.ascontiguousarray(HM, np.float64)),
                                                 ptr(np.ascontiguousarray(bM, np.float64))))
 
-    def marginalizePointsF(self, points):
+    def marginalizePointsF(self, points, return_prior=True):
         """flagPointsForRemoval (per-point part) + EnergyFunctional::marginalizePointsF for window points
-        `points` (Src/Mapping.cpp:280-293, Src/EnergyFunctional.cpp:545-609).  Returns the updated (HM, bM);
-        the window's linearization is consumed (drop the points and relinearize)."""
+        `points` (Src/Mapping.cpp:280-293, Src/EnergyFunctional.cpp:545-609).  Returns the updated (HM, bM)
+        (return_prior=False: nothing is read back and the call does not wait for the device); the window's
+        linearization is consumed (drop the points and relinearize)."""
         self._sync()
         p = np.ascontiguousarray(points, np.int32)
-        HM, bM = np.zeros((self.dim, self.dim)), np.zeros(self.dim)
+        HM, bM = (np.zeros((self.dim, self.dim)), np.zeros(self.dim)) if return_prior else (None, None)
         check(self.lib.hs_ba_marginalize_points(self.h, len(p), ptr(p), ptr(HM), ptr(bM)))
         return HM, bM
 
@@ -351,18 +352,18 @@ class BAWindow:
         check(self.lib.hs_ba_iterate(self.h, first_iteration, n_iters, ptr(e)))
         return e
 
-    def fixLinearization(self, max_rel_baseline=None, num_good=None):
+    def fixLinearization(self, max_rel_baseline=None, num_good=None, point_state=True):
         """System::optimize's tail (Src/FullSystemOptimize.cpp:498-516): newest frame setEvalPT, setAdjointsF,
         setPrecalcValues, linearizeAll(true).  Returns dict(energy, drop[n_res], maxRelBaseline[n_points],
         numGoodResiduals[n_points], HdiF[n_points]) (HdiF of the last solve's Schur prelude).  Without arrays the
-        context's own per-point values are used and returned."""
+        context's own per-point values are used and returned (point_state=False: not read back, None)."""
         self._sync()
         if max_rel_baseline is None and num_good is None:
             drop = np.zeros(self.n_res, np.uint8)
             hdi = np.zeros(self.n_points, np.float32)
             e = C.c_double()
             check(self.lib.hs_ba_fix_linearization(self.h, C.byref(e), ptr(drop), None, None, ptr(hdi)))
-            ps = self.point_state()
+            ps = self.point_state() if point_state else {"maxRelBaseline": None, "numGoodResiduals": None}
             return dict(energy=e.value, drop=drop, maxRelBaseline=ps["maxRelBaseline"],
                         numGoodResiduals=ps["numGoodResiduals"], HdiF=hdi)
         rb = np.zeros(self.n_points, np.float32) if max_rel_baseline is None else \

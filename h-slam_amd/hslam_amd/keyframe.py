@@ -130,11 +130,15 @@ class _Timer:
 
     def __init__(self):
         self.t = {}
+        self.calls = {}  # per library call (phase/function name)
 
     def run(self, phase, fn, *a, **k):
         t0 = time.perf_counter()
         r = fn(*a, **k)
-        self.t[phase] = self.t.get(phase, 0.0) + (time.perf_counter() - t0)
+        dt = time.perf_counter() - t0
+        self.t[phase] = self.t.get(phase, 0.0) + dt
+        name = f"{phase}/{getattr(fn, '__name__', 'call')}"
+        self.calls[name] = self.calls.get(name, 0.0) + dt
         return r
 
 
@@ -230,7 +234,8 @@ class KeyframeBA:
             check(self, "optimize")
         # optimize + tail
         n_it, energies = timer.run("optimize", ba.optimize, self.iters, self.allow_break)
-        tail = self.last_tail = timer.run("tail", ba.fixLinearization)
+        # the per-point maxRelBaseline / numGoodResiduals stay on the device (read with point_state when needed)
+        tail = self.last_tail = timer.run("tail", ba.fixLinearization, None, None, False)
         if check:
             check(self, "tail")
         # lastResiduals[.].second from the tail's states (System::linearizeAll(true), Src/FullSystemOptimize.cpp:128)
@@ -242,7 +247,6 @@ class KeyframeBA:
             hd = int(handles[st["res_point"][r]])
             self.last_state[hd][0 if st["res_target"][r] == newest else 1] = int(res["state"][r])
         hdif = tail["HdiF"]
-        ngood = tail["numGoodResiduals"]
         # toRemove, removeOutliers, the tracker's new reference
         timer.run("post", ba.dropInactiveResiduals)
         gone = timer.run("post", ba.removeOutliers)
@@ -283,7 +287,7 @@ class KeyframeBA:
             if check:
                 check(self, "marginalize")  # before marginalizePointsF: the window as the tail and drops left it
             if len(mpos):
-                timer.run("post", ba.marginalizePointsF, mpos)
+                timer.run("post", ba.marginalizePointsF, mpos, False)
             if check:
                 check(self, "points_marginalized")
             rm = hd_all[marg | drop]
@@ -299,8 +303,8 @@ class KeyframeBA:
         timer.run("post", ba.synchronize)
         info["wall_s"] = time.perf_counter() - wall0
         info["phase_s"] = dict(timer.t)
+        info["call_s"] = dict(timer.calls)
         info["lib_s"] = sum(v for p, v in timer.t.items() if p != "track_frame")
-        del ngood
         self.history.append(info)
         return info
 
