@@ -171,8 +171,10 @@ __device__ __forceinline__ void lds_barrier() {
 // dist + frac >= thr (thr <= T = the largest threshold of the call): it is kept exact up to r = ceil(T) - 1 (seed
 // patches of radius r; cells farther away keep a larger value, which passes every test anyway), and the exact
 // map is formed afterwards by hs_k_act_dist (mode 1).
+constexpr int kBorderWords = 128;  // border-candidate bitmap of select_body: maps with w1 + h1 <= 4096
+
 __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* map, int* s_n, int* s_seeds,
-                                           float* s_red) {
+                                           float* s_red, uint32_t* s_bcand) {
   const int tid = threadIdx.x, nthr = blockDim.x;
   const int w1 = a.w1, h1 = a.h1;
   float tmax = 0.f;
@@ -187,6 +189,15 @@ __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* ma
     tmax = fmaxf(tmax, __shfl_xor(tmax, o));
     tnan |= __shfl_xor((int)tnan, o) != 0;
   }
+  // the right column / bottom row cells some pending entry sits on (bit x: bottom row; bit w1 + y: right column);
+  // the border pass of a batch only forms those
+  const bool bfilter = w1 + h1 <= 32 * kBorderWords;
+  for (int j = tid; j < a.m; j += nthr)
+    if (bfilter && a.cand[j] == HS_CAND_PENDING) {
+      const int c = a.cell[j], cx = c & 0xffff, cy = c >> 16;
+      if (cy == h1 - 1) atomicOr(&s_bcand[cx >> 5], 1u << (cx & 31));
+      if (cx == w1 - 1) atomicOr(&s_bcand[(w1 + cy) >> 5], 1u << ((w1 + cy) & 31));
+    }
   if ((tid & 63) == 0) s_red[tid >> 6] = tnan ? 1e30f : tmax;
   __syncthreads();  // (also: the map is in place)
   float T = 0.f;
@@ -279,16 +290,28 @@ __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* ma
     const int ns = s_n[0];
     if (ns > 0) {
       npatch += ns;
-      // the right column / bottom row cells near a seed (the only border cells an entry can sit on), seeds in order
-      for (int i = s_n[1] ? tid : w1 + h1; i < w1 + h1 - 1; i += nthr) {
-        const int x = i < w1 ? i : w1 - 1, y = i < w1 ? h1 - 1 : i - w1;
-        if (x < 1 || y < 1) continue;
-        bool near = false;
-        for (int j = 0; j < ns; j++) {
-          const int sx = s_seeds[j] & 0xffff, sy = s_seeds[j] >> 16;
-          near |= max(abs(x - sx), abs(y - sy)) <= r + 1;
+      // the right column / bottom row cells near a seed (the only border cells an entry can sit on), seeds in order:
+      // one item per (seed near the edge, cell within r + 1 of it along the edge); a cell near two seeds is formed
+      // twice, the same value
+      const int span = 2 * r + 3;
+      for (int it = s_n[1] ? tid : 2 * ns * span; it < 2 * ns * span; it += nthr) {
+        const int jj = it / (2 * span), rem = it - jj * 2 * span, side = rem >= span, o = rem - side * span;
+        const int s0 = s_seeds[jj], s0x = s0 & 0xffff, s0y = s0 >> 16;
+        int x, y;
+        if (side == 0) {  // the right column
+          if (s0x + r + 1 < w1 - 1) continue;
+          x = w1 - 1;
+          y = s0y - r - 1 + o;
+        } else {  // the bottom row
+          if (s0y + r + 1 < h1 - 1) continue;
+          y = h1 - 1;
+          x = s0x - r - 1 + o;
         }
-        if (!near) continue;
+        if (x < 1 || y < 1 || x > w1 - 1 || y > h1 - 1) continue;
+        if (bfilter) {  // no entry sits on this cell: its value decides nothing
+          const int bi = side == 0 ? w1 + y : x;
+          if (!((s_bcand[bi >> 5] >> (bi & 31)) & 1u)) continue;
+        }
         int nb[3], nv[3] = {1000, 1000, 1000};
         border_nbrs(x, y, w1, h1, nb);
         for (int k = 0; k < 3; k++)
@@ -304,7 +327,7 @@ __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* ma
             border_step(x, y, sc, r, nb, v, nv);
           }
         }
-        if (v < v0) {  // no other thread writes this byte; the interior pass below runs after the barrier
+        if (v < v0) {  // the interior pass below runs after the barrier; two items of one cell store the same byte
           uint32_t* wp = reinterpret_cast<uint32_t*>(map) + (q >> 2);
           const int sh = (q & 3) * 8;
           uint32_t old = ld_word(map, q >> 2);
@@ -373,6 +396,9 @@ __global__ void __launch_bounds__(1024) hs_k_act_select(HsActSelectArgs a) {
   __shared__ int s_n[2];
   __shared__ int s_seeds[64];
   __shared__ float s_red[16];
+  __shared__ uint32_t s_bcand[kBorderWords];
+  for (int w = threadIdx.x; w < kBorderWords; w += blockDim.x) s_bcand[w] = 0u;
+  __syncthreads();
   const int words = (a.w1 * a.h1 + 3) / 4;
   if (a.prof && threadIdx.x == 0) a.prof[0] = wall_clock64();
   const uint32_t* g = reinterpret_cast<const uint32_t*>(a.map0);
@@ -381,11 +407,11 @@ __global__ void __launch_bounds__(1024) hs_k_act_select(HsActSelectArgs a) {
   int nt;
   if (a.lds_map) {
     for (int w = threadIdx.x; w < words; w += blockDim.x) s_map32[w] = g[w];
-    nt = select_body(a, reinterpret_cast<uint8_t*>(s_map32), s_n, s_seeds, s_red);
+    nt = select_body(a, reinterpret_cast<uint8_t*>(s_map32), s_n, s_seeds, s_red, s_bcand);
   } else {
     uint32_t* m32 = reinterpret_cast<uint32_t*>(a.dist);
     for (int w = threadIdx.x; w < words; w += blockDim.x) m32[w] = g[w];
-    nt = select_body(a, a.dist, s_n, s_seeds, s_red);
+    nt = select_body(a, a.dist, s_n, s_seeds, s_red, s_bcand);
   }
   if (threadIdx.x == 0) *a.n_toopt = nt;
   if (a.prof && threadIdx.x == 0) {
