@@ -239,7 +239,15 @@ void compute_projector(hs_ctx* c) {
 // solve launch (proj_stale) -- a window edit re-uploads every frame (upload_frames) and builds it anyway.
 int fetch_state(hs_ctx* c) {
   HS_HIP(hipMemcpyAsync(c->h_state, c->d_state, sizeof(HsDevState), hipMemcpyDeviceToHost, c->stream));
+  if (c->hm_host_stale) {  // the device marginal prior comes along (one sync for both)
+    const int n = c->dim();
+    c->HM.resize((size_t)n * n);
+    c->bM.resize(n);
+    HS_HIP(hipMemcpyAsync(c->HM.data(), c->d_HM, sizeof(double) * n * n, hipMemcpyDeviceToHost, c->stream));
+    HS_HIP(hipMemcpyAsync(c->bM.data(), c->d_bM, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+  }
   HS_HIP(hipStreamSynchronize(c->stream));
+  c->hm_host_stale = false;
   c->h_state_valid = true;
   if (c->tail_pending) {
     c->tail_pending = false;
@@ -288,36 +296,19 @@ int wait_uploads(hs_ctx* c) {
   return HS_OK;
 }
 
-// EnergyFunctional::setAdjointsF + System::setPrecalcValues + getNullspaces of the frames in c->h_state (fp64 host
-// algebra, the reference's own place for it), then the state, precalc, adjoints and projector to the device:
-// asynchronous copies from the pinned h_state / h_fstage (the event ev_upload marks their completion; the host waits
-// on it before it rewrites either).
+// getNullspaces' projector of the frames in c->h_state (fp64 host algebra), the state and the projector to the
+// device (asynchronous copies from the pinned h_state / h_fstage; the event ev_upload marks their completion, the
+// host waits on it before it rewrites either), then EnergyFunctional::setAdjointsF + System::setPrecalcValues of
+// every frame pair on the device (hs_k_fix_frames, fix = 0).
 int upload_frames(hs_ctx* c) {
-  const int nF = c->nF, n = c->dim(), FF = nF * nF;
+  const int nF = c->nF, n = c->dim();
   HS_TRY(wait_uploads(c));
   HsDevState& S = *c->h_state;
   S.nF = nF;
   c->tail_pending = false;  // every frame's adjoints, precalc and the projector are rewritten from h_state
   c->proj_stale = false;
-  c->adHost.assign(FF * 64, 0.0);
-  c->adTarget.assign(FF * 64, 0.0);
-  c->adHostF.assign(FF * 64, 0.f);
-  c->adTargetF.assign(FF * 64, 0.f);
-  for (int h = 0; h < nF; h++)
-    for (int t = 0; t < nF; t++) {
-      const int idx = h + t * nF;
-      make_adjoints(S.frames[h], S.frames[t], &c->adHost[idx * 64], &c->adTarget[idx * 64]);
-      for (int i = 0; i < 64; i++) {
-        c->adHostF[idx * 64 + i] = (float)c->adHost[idx * 64 + i];
-        c->adTargetF[idx * 64 + i] = (float)c->adTarget[idx * 64 + i];
-      }
-    }
   compute_projector(c);
   uint8_t* p = c->h_fstage;
-  HsPrecalc* pre = (HsPrecalc*)p;
-  for (int h = 0; h < nF; h++)
-    for (int t = 0; t < nF; t++) pre[h * nF + t] = make_precalc(S.frames[h], S.frames[t], S.calib);
-  p += HS_MAXF * HS_MAXF * sizeof(HsPrecalc);
   auto put = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
     std::memcpy(p, src, bytes);
     hipError_t e = hipMemcpyAsync(dst, p, bytes, hipMemcpyHostToDevice, c->stream);
@@ -325,13 +316,12 @@ int upload_frames(hs_ctx* c) {
     return e;
   };
   HS_HIP(hipMemcpyAsync(c->d_state, c->h_state, sizeof(HsDevState), hipMemcpyHostToDevice, c->stream));
-  HS_HIP(hipMemcpyAsync(c->d_pre, pre, sizeof(HsPrecalc) * FF, hipMemcpyHostToDevice, c->stream));
-  HS_HIP(put(c->d_adHost, c->adHost.data(), sizeof(double) * FF * 64));
-  HS_HIP(put(c->d_adTarget, c->adTarget.data(), sizeof(double) * FF * 64));
-  HS_HIP(put(c->d_adHostF, c->adHostF.data(), sizeof(float) * FF * 64));
-  HS_HIP(put(c->d_adTargetF, c->adTargetF.data(), sizeof(float) * FF * 64));
   HS_HIP(put(c->d_Nproj, c->Nproj.data(), sizeof(double) * 2 * n * HS_NNS));
   HS_HIP(hipEventRecord(c->ev_upload, c->stream));
+  // the pairs' precalc and adjoints on the device from the uploaded state (the expressions of the host forms)
+  hipLaunchKernelGGL(hs_k_fix_frames, dim3(1), dim3(64), 0, c->stream, c->d_state, c->d_pre, c->d_adHost,
+                     c->d_adTarget, c->d_adHostF, c->d_adTargetF, c->P, 0);
+  HS_HIP(hipGetLastError());
   c->h_state_valid = true;
   return HS_OK;
 }
@@ -1280,7 +1270,7 @@ int hs_ba_fix_linearization(hs_ctx* c, double* energy_out, uint8_t* drop_out, fl
   // the newest frame's setEvalPT + EnergyFunctional::setAdjointsF + setPrecalcValues, on the device (the nullspaces
   // and projector follow on the host when the state is next fetched)
   hipLaunchKernelGGL(hs_k_fix_frames, dim3(1), dim3(64), 0, c->stream, c->d_state, c->d_pre, c->d_adHost,
-                     c->d_adTarget, c->d_adHostF, c->d_adTargetF, c->P);
+                     c->d_adTarget, c->d_adHostF, c->d_adTargetF, c->P, 1);
   HS_HIP(hipGetLastError());
   c->h_state_valid = false;
   c->tail_pending = true;
@@ -1601,7 +1591,7 @@ static bool inverse8(const double* A, double* Ainv) {
 // EnergyFunctional::marginalizeFrame (Src/EnergyFunctional.cpp:456-543) on the context's HM / bM: a dense 68x68
 // host operation once per marginalized keyframe (not on the GN path).  HMn / bMn: the (dim-8) prior.
 int hs::marginalize_frame_prior(hs_ctx* c, int frame, std::vector<double>& HMn, std::vector<double>& bMn) {
-  if (!c->h_state_valid) HS_TRY(fetch_state(c));
+  if (!c->h_state_valid) HS_TRY(fetch_state(c));  // (brings a device-updated HM / bM along)
   HS_TRY(sync_hm(c));
   const int od = c->dim(), nd = od - 8, f0 = 4 + 8 * frame;
   std::vector<double> HMc = c->HM, bMc = c->bM;

@@ -99,7 +99,7 @@ struct hs_ctx {
   hipEvent_t ev_ready = nullptr;  // cross-stream hand-off (BA -> tracker)
   hipEvent_t ev_upload = nullptr; // the last asynchronous upload from the pinned staging buffers (h_fstage, h_stage,
                                   // h_state, h_raw): waited on before the host rewrites them
-  uint8_t* h_fstage = nullptr;    // pinned: precalc, adjoints, projector of upload_frames
+  uint8_t* h_fstage = nullptr;    // pinned: the projector of upload_frames
   int events = 0;              // HS_EVENT_TIMING: 0 none (default), 1 linearize kernel only, 2 every phase
 
   // ---- capacity (allocated once; hs_ba_reserve or the first hs_ba_set_window that needs more)
@@ -123,8 +123,6 @@ struct hs_ctx {
   std::vector<int> pt_host, res_point, res_target, host_pt_begin;
   std::vector<int> res_of_slot;   // [nP*8]
   std::vector<int8_t> res_order;  // [nP*8]
-  std::vector<double> adHost, adTarget;
-  std::vector<float> adHostF, adTargetF;
   std::vector<double> HM, bM, Porth, Nproj;
   int img_slot[HS_MAXF] = {0, 1, 2, 3, 4, 5, 6, 7};  // window frame -> image slot
   HsDevState* h_state = nullptr;  // pinned staging of the device state

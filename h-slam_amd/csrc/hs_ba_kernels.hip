@@ -2545,10 +2545,12 @@ __global__ void hs_k_marg_update(const double* sep, const double* sep_aux, doubl
   }
 }
 
+// fix = 1: the optimize tail's setEvalPT of the newest frame first; then (both) every frame pair's precalc and
+// adjoints (System::setPrecalcValues, EnergyFunctional::setAdjointsF) from the device state
 __global__ void hs_k_fix_frames(HsDevState* st, HsPrecalc* pre, double* adH, double* adT, float* adHF, float* adTF,
-                                hs_params P) {
+                                hs_params P, int fix) {
   const int nF = st->nF, tid = threadIdx.x;
-  if (tid == 0) {  // newStateZero = 0 except segment(6, 2) = the newest frame's a / b; setEvalPT(PRE_worldToCam, .)
+  if (fix && tid == 0) {  // newStateZero = 0 except segment(6, 2) = the newest frame's a / b; setEvalPT(PRE_worldToCam, .)
     hs::FrameH& f = st->frames[nF - 1];
     double nsz[10] = {0, 0, 0, 0, 0, 0, f.state[6], f.state[7], 0, 0};
     f.evalPT = f.PRE_worldToCam;

@@ -593,6 +593,7 @@ int hs_ba_remove_frame(hs_ctx* c, int frame, int marginalize) {
   if (frame < 0 || frame >= (int)c->wframes.size()) return fail(HS_ERR_INVALID, "frame index out of range");
   if (!c->wpts[frame].empty()) return fail(HS_ERR_STATE, "the frame still hosts points (remove them first)");
   HS_TRY(commit_if_dirty(c));  // the prior's Schur complement needs the committed frame state and HM / bM
+  if (marginalize && !c->h_state_valid) HS_TRY(fetch_state(c));  // one read-back for the state and HM / bM
   HS_TRY(sync_hm(c));
   const int od = c->dim(), nd = od - 8, f0 = 4 + 8 * frame;
   std::vector<double> HMn, bMn;

@@ -246,6 +246,6 @@ __global__ void hs_k_marg_delta(const HsDevState* st, const float* adHF, const f
 __global__ void hs_k_marg_update(const double* sep, const double* sep_aux, double* HM, double* bM, int nF, int SL,
                                  double w);
 __global__ void hs_k_fix_frames(HsDevState* st, HsPrecalc* pre, double* adH, double* adT, float* adHF, float* adTF,
-                                hs_params P);
+                                hs_params P, int fix);
 __global__ void hs_k_lenergy(int n, const float* idepth, const float* idepth_zero, const float* priorF, float* chunk,
                              double* out);

@@ -33,9 +33,21 @@ int tfail(int code, const std::string& msg) {
     if (rc_) return rc_; \
   } while (0)
 
+// a captured makeCoarseDepthL0 (make_depth_l0 from a device count): ~32 launches and copies, replayed as one graph;
+// keyed by everything its launches bake in (the reference pyramid's level pointers swap on a promoted frame)
+struct DepthGraph {
+  const int* d_n = nullptr;
+  const float* pts = nullptr;
+  int stride = 0;
+  const void* ref[HS_TRK_MAXLEV] = {};
+  hipGraphExec_t exec = nullptr;
+};
+
 struct hs_tracker {
   hs_params P;
   int device = 0;
+  DepthGraph dg[2];
+  int dg_next = 0;
   hipStream_t stream = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   int W = 0, H = 0, nlev = 0;
@@ -266,6 +278,48 @@ static int make_depth_l0(hs_tracker* t, int n_host, const int* d_n, const float*
   return HS_OK;
 }
 
+// make_depth_l0 from a device count (hs_tracker_set_ref_ba) as a replayed hipGraph: the host cost of ~32 launches
+// and copies per keyframe becomes one graph launch.  HS_TRK_GRAPH=0 launches them one by one.
+static int make_depth_l0_dev(hs_tracker* t, const int* d_n, const float* pts, int stride) {
+  static const bool off = getenv("HS_TRK_GRAPH") && getenv("HS_TRK_GRAPH")[0] == '0';
+  if (off) return make_depth_l0(t, 0, d_n, pts, stride);
+  auto same = [&](const DepthGraph& g) {
+    if (!g.exec || g.d_n != d_n || g.pts != pts || g.stride != stride) return false;
+    for (int l = 0; l < t->nlev; l++)
+      if (g.ref[l] != t->d_ref[l]) return false;
+    return true;
+  };
+  DepthGraph* hit = same(t->dg[0]) ? &t->dg[0] : same(t->dg[1]) ? &t->dg[1] : nullptr;
+  if (!hit) {
+    DepthGraph& g = t->dg[t->dg_next];
+    t->dg_next ^= 1;
+    if (g.exec) (void)hipGraphExecDestroy(g.exec);
+    g.exec = nullptr;
+    TS_HIP(hipStreamBeginCapture(t->stream, hipStreamCaptureModeThreadLocal));
+    const int rc = make_depth_l0(t, 0, d_n, pts, stride);
+    hipGraph_t graph = nullptr;
+    const hipError_t ec = hipStreamEndCapture(t->stream, &graph);
+    if (rc != HS_OK) {
+      if (graph) (void)hipGraphDestroy(graph);
+      return rc;
+    }
+    if (ec != hipSuccess) return tfail(HS_ERR_HIP, "makeCoarseDepthL0 capture failed");
+    const hipError_t ei = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    if (ei != hipSuccess) {
+      g.exec = nullptr;
+      return tfail(HS_ERR_HIP, "makeCoarseDepthL0 graph instantiation failed");
+    }
+    g.d_n = d_n;
+    g.pts = pts;
+    g.stride = stride;
+    for (int l = 0; l < HS_TRK_MAXLEV; l++) g.ref[l] = l < t->nlev ? t->d_ref[l] : nullptr;
+    hit = &g;
+  }
+  TS_HIP(hipGraphLaunch(hit->exec, t->stream));
+  return HS_OK;
+}
+
 extern "C" {
 
 int hs_tracker_create(hs_tracker** out, const hs_params* params, int device_id, int width, int height,
@@ -331,6 +385,8 @@ void hs_tracker_destroy(hs_tracker* t) {
   if (!t) return;
   (void)hipSetDevice(t->device);
   if (t->stream) (void)hipStreamSynchronize(t->stream);
+  for (auto& g : t->dg)
+    if (g.exec) (void)hipGraphExecDestroy(g.exec);
   for (int l = 0; l < HS_TRK_MAXLEV; l++) {
     void* ps[] = {t->d_ref[l], t->d_new[l], t->d_id[l], t->d_ws[l], t->d_bak[l], t->d_pu[l], t->d_pv[l], t->d_pid[l],
                   t->d_pcol[l]};
@@ -416,7 +472,7 @@ int hs_tracker_set_ref_ba(hs_tracker* t, hs_ctx* ba, int promote_frame, float ab
   t->refExposure = ab_exposure;
   t->refAff[0] = aff_g2l[0];
   t->refAff[1] = aff_g2l[1];
-  TS_TRY(make_depth_l0(t, 0, ba->d_ref_n, ba->d_ref_pts, ba->cap_P));
+  TS_TRY(make_depth_l0_dev(t, ba->d_ref_n, ba->d_ref_pts, ba->cap_P));
   // the BA stream must not rewrite the hand-off buffer before the tracker consumed it
   TS_HIP(hipEventRecord(t->e1, t->stream));
   TS_HIP(hipStreamWaitEvent(ba->stream, t->e1, 0));
