@@ -618,12 +618,12 @@ static int launch_solve(hs_ctx* c, int flags, int iteration, bool log) {
   return HS_OK;
 }
 
-static int reset_states(hs_ctx* c) {  // PointFrameResidual::resetOOB on every active residual
-  const size_t P8 = (size_t)c->nP * 8;  // slot layout
-  HS_HIP(hipMemsetAsync(c->d_r_state, HS_RES_IN, P8, c->stream));
-  HS_HIP(hipMemsetAsync(c->d_r_active, 0, P8, c->stream));
-  HS_HIP(hipMemsetAsync(c->d_r_energy, 0, sizeof(float) * P8, c->stream));
-  HS_HIP(hipMemsetAsync(c->d_r_newEnergy, 0, sizeof(float) * P8, c->stream));
+static int reset_states(hs_ctx* c) {  // PointFrameResidual::resetOOB on every active residual (one launch)
+  const int P8 = c->nP * 8;  // slot layout
+  if (P8 == 0) return HS_OK;
+  hipLaunchKernelGGL(hs_k_reset_res, dim3((P8 + 255) / 256), dim3(256), 0, c->stream, P8, c->d_r_state,
+                     c->d_r_active, c->d_r_energy, c->d_r_newEnergy);
+  HS_HIP(hipGetLastError());
   return HS_OK;
 }
 

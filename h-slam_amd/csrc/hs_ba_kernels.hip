@@ -2508,6 +2508,16 @@ __global__ void hs_k_resub(HsResubArgs a) {
   }
 }
 
+__global__ void hs_k_reset_res(int n8, uint8_t* st, uint8_t* act, float* en, float* nen) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n8) {
+    st[i] = HS_RES_IN;
+    act[i] = 0;
+    en[i] = 0.f;
+    nen[i] = 0.f;
+  }
+}
+
 // EnergyFunctional::setDeltaF (Src/EnergyFunctional.cpp:128-152) in fp32: adHTdeltaF[h + nF t] = delta_h^T adHostF +
 // delta_t^T adTargetF (each dot product in index order), cDeltaF = (float) calib.value_minus_value_zero.  One thread
 // per (pair, entry).

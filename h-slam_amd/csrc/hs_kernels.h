@@ -240,6 +240,8 @@ __global__ void hs_k_apply_step(int n, const float* step, float* idepth, float* 
 // System::optimize's tail, frame part (Src/FullSystemOptimize.cpp:498-506) on the device: the newest frame's
 // setEvalPT(PRE_worldToCam, (0,..,0, a, b, 0, 0)) + takeData, then setAdjointsF + setPrecalcValues of every pair (one
 // thread per pair).  The nullspaces of the moved frame are left to the host (hs_ctx::frames_stale).  One block of 64.
+// PointFrameResidual::resetOOB of every slot: state IN, inactive, energies 0
+__global__ void hs_k_reset_res(int n8, uint8_t* st, uint8_t* act, float* en, float* nen);
 // hs_ba_marginalize_points on the device: EnergyFunctional::setDeltaF's adHTdeltaF [nF*nF][8] + cDeltaF [4] (after
 // them) from the window state; then HM += w (M - Msc), bM += w (Mb - Mbsc) from the separate stitch outputs
 __global__ void hs_k_marg_delta(const HsDevState* st, const float* adHF, const float* adTF, float* adHTd);
