@@ -20,33 +20,51 @@ __device__ __forceinline__ double rsqrt_step(double x) {
 // (1 - cos x)/x^2 and (x - sin x)/x^3 come from their Taylor series in u = x^2 (6 terms: truncation < 1e-20
 // relative; no sqrt, trig or division on the chain); the quaternion is normalized with one reciprocal square
 // root.  Larger tangents take the reference formulas.  Differs from Sophus by rounding only.
-__device__ __forceinline__ hs::SE3 se3_exp_step(const double a[6]) {
-  const double w0 = a[3], w1 = a[4], w2 = a[5];
-  const double u = w0 * w0 + w1 * w1 + w2 * w2;
-  if (!(u < 1e-2)) return hs::SE3::exp(a);
-  auto poly = [u](double c0, double c1, double c2, double c3, double c4, double c5) {
-    return __builtin_fma(__builtin_fma(__builtin_fma(__builtin_fma(__builtin_fma(c5, u, c4), u, c3), u, c2), u, c1), u,
-                         c0);
-  };
-  const double imag = poly(1.0 / 2, -1.0 / 48, 1.0 / 3840, -1.0 / 645120, 1.0 / 185794560, -1.0 / 81749606400.0);
-  const double real = poly(1.0, -1.0 / 8, 1.0 / 384, -1.0 / 46080, 1.0 / 10321920, -1.0 / 3715891200.0);
-  const double c1 = poly(1.0 / 2, -1.0 / 24, 1.0 / 720, -1.0 / 40320, 1.0 / 3628800, -1.0 / 479001600);
-  const double c2 = poly(1.0 / 6, -1.0 / 120, 1.0 / 5040, -1.0 / 362880, 1.0 / 39916800, -1.0 / 6227020800.0);
-  hs::SE3 r;
-  const double qx = imag * w0, qy = imag * w1, qz = imag * w2;
+// the two halves of the series form (u = |w|^2 < 1e-2), so a caller can run them on different waves: the unit
+// quaternion, and the translation V a
+__device__ __forceinline__ double se3_step_poly(double u, double c0, double c1, double c2, double c3, double c4,
+                                                double c5) {
+  return __builtin_fma(__builtin_fma(__builtin_fma(__builtin_fma(__builtin_fma(c5, u, c4), u, c3), u, c2), u, c1), u,
+                       c0);
+}
+__device__ __forceinline__ hs::Quat se3_exp_step_q(const double a[6], double u) {
+  const double imag = se3_step_poly(u, 1.0 / 2, -1.0 / 48, 1.0 / 3840, -1.0 / 645120, 1.0 / 185794560,
+                                    -1.0 / 81749606400.0);
+  const double real = se3_step_poly(u, 1.0, -1.0 / 8, 1.0 / 384, -1.0 / 46080, 1.0 / 10321920, -1.0 / 3715891200.0);
+  const double qx = imag * a[3], qy = imag * a[4], qz = imag * a[5];
   const double inv = rsqrt_step(qx * qx + qy * qy + qz * qz + real * real);
-  r.q = hs::Quat{qx * inv, qy * inv, qz * inv, real * inv};
+  return hs::Quat{qx * inv, qy * inv, qz * inv, real * inv};
+}
+__device__ __forceinline__ void se3_exp_step_t(const double a[6], double u, double t[3]) {
+  const double c1 = se3_step_poly(u, 1.0 / 2, -1.0 / 24, 1.0 / 720, -1.0 / 40320, 1.0 / 3628800, -1.0 / 479001600);
+  const double c2 = se3_step_poly(u, 1.0 / 6, -1.0 / 120, 1.0 / 5040, -1.0 / 362880, 1.0 / 39916800,
+                                  -1.0 / 6227020800.0);
   double O[9], O2[9], V[9];
   hs::SE3::hat3(a + 3, O);
   hs::SE3::mm3(O, O, O2);
 #pragma unroll
   for (int i = 0; i < 9; i++) V[i] = ((i % 4 == 0) ? 1.0 : 0.0) + c1 * O[i] + c2 * O2[i];
 #pragma unroll
-  for (int i = 0; i < 3; i++) r.t[i] = V[i * 3 + 0] * a[0] + V[i * 3 + 1] * a[1] + V[i * 3 + 2] * a[2];
+  for (int i = 0; i < 3; i++) t[i] = V[i * 3 + 0] * a[0] + V[i * 3 + 1] * a[1] + V[i * 3 + 2] * a[2];
+}
+__device__ __forceinline__ double se3_step_u(const double a[6]) { return a[3] * a[3] + a[4] * a[4] + a[5] * a[5]; }
+
+__device__ __forceinline__ hs::SE3 se3_exp_step(const double a[6]) {
+  const double u = se3_step_u(a);
+  if (!(u < 1e-2)) return hs::SE3::exp(a);
+  hs::SE3 r;
+  r.q = se3_exp_step_q(a, u);
+  se3_exp_step_t(a, u, r.t);
   return r;
 }
 
-// SE3 product (Sophus fastMultiply: quaternion product + normalize), normalized with one reciprocal square root
+// SE3 product (Sophus fastMultiply: quaternion product + normalize), normalized with one reciprocal square root;
+// se3_mul_step_q is its rotation half
+__device__ __forceinline__ hs::Quat se3_mul_step_q(const hs::Quat& a, const hs::Quat& b) {
+  const hs::Quat q = hs::qmul(a, b);
+  const double inv = rsqrt_step(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+  return hs::Quat{q.x * inv, q.y * inv, q.z * inv, q.w * inv};
+}
 __device__ __forceinline__ hs::SE3 se3_mul_step(const hs::SE3& A, const hs::SE3& B) {
   hs::SE3 r;
   double rt[3];
@@ -54,9 +72,7 @@ __device__ __forceinline__ hs::SE3 se3_mul_step(const hs::SE3& A, const hs::SE3&
   r.t[0] = A.t[0] + rt[0];
   r.t[1] = A.t[1] + rt[1];
   r.t[2] = A.t[2] + rt[2];
-  const hs::Quat q = hs::qmul(A.q, B.q);
-  const double inv = rsqrt_step(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
-  r.q = hs::Quat{q.x * inv, q.y * inv, q.z * inv, q.w * inv};
+  r.q = se3_mul_step_q(A.q, B.q);
   return r;
 }
 

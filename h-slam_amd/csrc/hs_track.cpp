@@ -5,6 +5,7 @@
 
 #include <cmath>
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -66,10 +67,13 @@ struct hs_tracker {
   double* d_Tin = nullptr;
   HsTryOut* d_out = nullptr;
   double* d_part = nullptr;       // [try_cap][2][HS_TRK_MAXG][HS_TRK_NRED] pass partials of the member workgroups
-  unsigned int* d_cnt = nullptr;  // [try_cap] timeout flags, in d_part's allocation after the granules (one memset)
-  HsTryOut* h_out = nullptr;
+  unsigned int* d_cnt = nullptr;  // [try_cap] timeout flags, then (cnt_bytes on) the outputs d_out: one read-back
+  HsTryOut* h_out = nullptr;      // pinned mirror: h_cnt, then h_out
   double* h_in = nullptr;         // pinned staging of the hypotheses (T | aff), so their upload is asynchronous
-  unsigned int* h_cnt = nullptr;  // pinned read-back of the timeout flags
+  unsigned int* h_cnt = nullptr;
+  unsigned int* dh_cnt = nullptr;  // device aliases of h_cnt / h_out (mapped pinned memory)
+  HsTryOut* dh_out = nullptr;
+  unsigned int epoch = 0;         // the last member-meeting launch's granule epoch (hs_track_kernels.h)
   double* d_lmlog = nullptr;
   int* d_lmlvl = nullptr;
   int try_cap = 0, last_n_tries = 0;
@@ -99,29 +103,36 @@ static int upload_pyr(hs_tracker* t, float4** dst, const float* const* pyr) {
 
 // the member workgroups' pass granules of n hypotheses: [n][2][HS_TRK_MAXG][HS_TRK_NRED][2] u64
 static size_t part_bytes(int n) { return sizeof(unsigned long long) * 2 * HS_TRK_MAXG * HS_TRK_NRED * 2 * (size_t)n; }
+// the timeout flags in front of the outputs, padded to 256 B
+static size_t cnt_bytes(int n) { return (sizeof(unsigned int) * (size_t)n + 255) & ~(size_t)255; }
 
 static int ensure_tries(hs_tracker* t, int n) {
   if (n <= t->try_cap) return HS_OK;
   if (t->d_Tin) (void)hipFree(t->d_Tin);
-  if (t->d_out) (void)hipFree(t->d_out);
-  if (t->h_out) (void)hipHostFree(t->h_out);
+  if (t->d_cnt) (void)hipFree(t->d_cnt);
+  if (t->h_cnt) (void)hipHostFree(t->h_cnt);
   if (t->d_lmlog) (void)hipFree(t->d_lmlog);
   if (t->d_part) (void)hipFree(t->d_part);
   if (t->h_in) (void)hipHostFree(t->h_in);
-  if (t->h_cnt) (void)hipHostFree(t->h_cnt);
   t->d_part = nullptr; t->d_cnt = nullptr; t->h_in = nullptr; t->h_cnt = nullptr;
   if (t->d_lmlvl) (void)hipFree(t->d_lmlvl);
   t->d_Tin = nullptr; t->d_out = nullptr; t->h_out = nullptr; t->d_lmlog = nullptr; t->d_lmlvl = nullptr;
   TS_HIP(hipMalloc((void**)&t->d_Tin, sizeof(double) * 9 * n));  // T (7) | aff (2)
-  TS_HIP(hipMalloc((void**)&t->d_out, sizeof(HsTryOut) * n));
+  TS_HIP(hipMalloc((void**)&t->d_cnt, cnt_bytes(n) + sizeof(HsTryOut) * n));
+  t->d_out = reinterpret_cast<HsTryOut*>(reinterpret_cast<char*>(t->d_cnt) + cnt_bytes(n));
   TS_HIP(hipMalloc((void**)&t->d_lmlog, sizeof(double) * 3 * HS_TRK_MAXLOG * n));
   TS_HIP(hipMalloc((void**)&t->d_lmlvl, sizeof(int) * HS_TRK_MAXLOG * n));
-  TS_HIP(hipMalloc((void**)&t->d_part, part_bytes(n) + sizeof(unsigned int) * n + 16));
-  t->d_cnt = reinterpret_cast<unsigned int*>(reinterpret_cast<char*>(t->d_part) + part_bytes(n));
-  TS_HIP(hipHostMalloc((void**)&t->h_out, sizeof(HsTryOut) * n));
+  TS_HIP(hipMalloc((void**)&t->d_part, part_bytes(n)));
+  // mapped, coherent: the kernel may write the flags and records straight into it (HS_TRK_ZC, run_tries)
+  TS_HIP(hipHostMalloc((void**)&t->h_cnt, cnt_bytes(n) + sizeof(HsTryOut) * n,
+                       hipHostMallocMapped | hipHostMallocCoherent));
+  t->h_out = reinterpret_cast<HsTryOut*>(reinterpret_cast<char*>(t->h_cnt) + cnt_bytes(n));
+  std::memset(t->h_cnt, 0, cnt_bytes(n) + sizeof(HsTryOut) * n);
+  TS_HIP(hipHostGetDevicePointer((void**)&t->dh_cnt, t->h_cnt, 0));
+  t->dh_out = reinterpret_cast<HsTryOut*>(reinterpret_cast<char*>(t->dh_cnt) + cnt_bytes(n));
   TS_HIP(hipHostMalloc((void**)&t->h_in, sizeof(double) * 9 * n));
-  TS_HIP(hipHostMalloc((void**)&t->h_cnt, sizeof(unsigned int) * n));
   t->try_cap = n;
+  t->epoch = 0;  // fresh granules and flags: zeroed at the next member-meeting launch
   return HS_OK;
 }
 
@@ -153,9 +164,15 @@ static HsTrackArgs make_args(hs_tracker* t) {
 static int run_tries(hs_tracker* t, int n, const double* h_in, int coarsest, int single_pass, int lvl, float cutoff,
                      bool force_g1 = false) {
   TS_TRY(ensure_tries(t, n));
-  std::memcpy(t->h_in, h_in, sizeof(double) * 9 * n);
-  TS_HIP(hipMemcpyAsync(t->d_Tin, t->h_in, sizeof(double) * 9 * n, hipMemcpyHostToDevice, t->stream));
   HsTrackArgs a = make_args(t);
+  a.n_inl = 0;
+  if (n <= HS_TRK_INL) {  // a few hypotheses travel in the kernel arguments: no upload
+    a.n_inl = n;
+    std::memcpy(a.inl, h_in, sizeof(double) * 9 * n);
+  } else {
+    std::memcpy(t->h_in, h_in, sizeof(double) * 9 * n);
+    TS_HIP(hipMemcpyAsync(t->d_Tin, t->h_in, sizeof(double) * 9 * n, hipMemcpyHostToDevice, t->stream));
+  }
   a.coarsest = coarsest;
   a.T_in = t->d_Tin;
   a.aff_in = t->d_Tin + 7 * n;
@@ -167,12 +184,12 @@ static int run_tries(hs_tracker* t, int n, const double* h_in, int coarsest, int
   a.pass_cutoff = cutoff;
   // workgroups per hypothesis: the device's CUs shared by the hypotheses, one member per CU (every member must be
   // resident at once: they meet once per pass), at most HS_TRK_MAXG; env HS_TRK_G caps it (1 = the one-workgroup LM
-  // loop).  8 measured best at C2 (r03_b1: G = 1 / 8 / 16 / 32: 0.61 / 0.48 / 0.53 / 0.63 ms per track: more
-  // members shorten the point loop but lengthen the per-pass meeting).  Members that are not co-resident after all
-  // (a smaller partition, kernels of other streams on the CUs) make a meeting time out: the launch is then rerun
-  // with G = 1, which needs no co-residency.
+  // loop).  16 measured best at C2 (r04_trk5: G = 4 / 8 / 12 / 16: 0.287 / 0.260 / 0.258 / 0.254 ms per track; in
+  // round 3, with a costlier point loop and meeting, 8 was: more members shorten the point loop but lengthen the
+  // per-pass meeting).  Members that are not co-resident after all (a smaller partition, kernels of other streams on
+  // the CUs) make a meeting time out: the launch is then rerun with G = 1, which needs no co-residency.
   const int cap = std::max(1, t->n_cu / std::max(1, n));
-  int G = std::max(1, std::min(8, cap));
+  int G = std::max(1, std::min(16, cap));
   if (const char* e = std::getenv("HS_TRK_G")) G = std::max(1, std::min({HS_TRK_MAXG, cap, std::atoi(e)}));
   if (const char* e = std::getenv("HS_TRK_G_UNCHECKED"))  // test hook: G without the co-residency cap
     G = std::max(1, std::min(HS_TRK_MAXG, std::atoi(e)));
@@ -182,12 +199,28 @@ static int run_tries(hs_tracker* t, int n, const double* h_in, int coarsest, int
   a.G = G;
   a.nhyp = n;
   a.part = t->d_part;
-  a.cnt = t->d_cnt;
+  // zero-copy results (default; env HS_TRK_ZC=0: a read-back copy behind the kernel): the lead workgroups write
+  // their records, and timed-out members their flags, into mapped pinned memory, and the host waits for the launch by
+  // polling its end event -- no copy is queued behind the kernel and no blocking synchronize is paid
+  const char* zce = std::getenv("HS_TRK_ZC");
+  const bool zc = !(zce && zce[0] == '0');
+  a.cnt = zc ? t->dh_cnt : t->d_cnt;
+  a.hout = zc ? t->dh_out : nullptr;
   t->last_G = G;
-  // the granules and the timeout flags, zeroed before every launch (16-B multiples from the allocations' starts)
-  if (G > 1)  // the granules of this launch's hypotheses, then the timeout flags (a multiple of 16 B)
-    TS_HIP(hipMemsetAsync(t->d_part, 0, part_bytes(t->try_cap) + ((sizeof(unsigned int) * n + 15) & ~(size_t)15),
-                          t->stream));
+  // a new granule epoch per member-meeting launch; the granules and the timeout flags are zeroed only when the
+  // epoch starts over (a fresh allocation, or 2^20 - 1 launches)
+  if (G > 1) {
+    if (t->epoch == 0 || t->epoch >= (1u << (32 - HS_TRK_PASS_BITS)) - 1) {
+      TS_HIP(hipMemsetAsync(t->d_part, 0, part_bytes(t->try_cap), t->stream));
+      TS_HIP(hipMemsetAsync(t->d_cnt, 0, sizeof(unsigned int) * t->try_cap, t->stream));
+      std::memset(t->h_cnt, 0, sizeof(unsigned int) * t->try_cap);  // (no launch in flight: every call waits)
+      t->epoch = 0;
+    }
+    t->epoch++;
+  }
+  a.epoch = t->epoch;
+  a.solve = 0;
+  if (const char* e = std::getenv("HS_TRK_SOLVE")) a.solve = std::atoi(e) == 1 ? 1 : 0;  // A/B: 1 = the LDLT
   const char* kt = std::getenv("HS_KTRACE");
   if (kt && kt[0] == '1' && !single_pass) {
     const int nb = n * G;
@@ -204,11 +237,26 @@ static int run_tries(hs_tracker* t, int n, const double* h_in, int coarsest, int
   hipLaunchKernelGGL(hs_k_track, dim3(n * G), dim3(512), 0, t->stream, a);
   TS_HIP(hipGetLastError());
   TS_HIP(hipEventRecord(t->e1, t->stream));
-  TS_HIP(hipMemcpyAsync(t->h_out, t->d_out, sizeof(HsTryOut) * n, hipMemcpyDeviceToHost, t->stream));
-  if (G > 1) TS_HIP(hipMemcpyAsync(t->h_cnt, t->d_cnt, sizeof(unsigned int) * n, hipMemcpyDeviceToHost, t->stream));
-  TS_HIP(hipStreamSynchronize(t->stream));
+  if (zc) {
+    // poll the end event; after ~2 s hand over to the blocking synchronize (which also reports a faulted launch)
+    const auto t0 = std::chrono::steady_clock::now();
+    for (long k = 0;; k++) {
+      const hipError_t e = hipEventQuery(t->e1);
+      if (e == hipSuccess) break;
+      if (e != hipErrorNotReady) TS_HIP(e);
+      if ((k & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+        TS_HIP(hipStreamSynchronize(t->stream));
+        break;
+      }
+    }
+  } else {
+    // the timeout flags and the outputs of the n hypotheses, in one read-back
+    TS_HIP(hipMemcpyAsync(t->h_cnt, t->d_cnt, cnt_bytes(t->try_cap) + sizeof(HsTryOut) * n, hipMemcpyDeviceToHost,
+                          t->stream));
+    TS_HIP(hipStreamSynchronize(t->stream));
+  }
   for (int i = 0; G > 1 && i < n; i++)
-    if (t->h_cnt[i]) {  // a meeting timed out: the launch's results are void, rerun every hypothesis with G = 1
+    if (t->h_cnt[i] == t->epoch) {  // a meeting timed out: the launch's results are void, rerun every hypothesis with G = 1
       t->fallbacks++;
       return run_tries(t, n, h_in, coarsest, single_pass, lvl, cutoff, true);
     }
@@ -393,11 +441,10 @@ void hs_tracker_destroy(hs_tracker* t) {
     for (void* p : ps)
       if (p) (void)hipFree(p);
   }
-  void* ps[] = {t->d_pcn, t->d_bcnt, t->d_boff, t->d_pts, t->d_Tin, t->d_out, t->d_lmlog, t->d_lmlvl, t->d_raw,
-                t->d_trace, t->d_part};
+  void* ps[] = {t->d_pcn, t->d_bcnt, t->d_boff, t->d_pts, t->d_Tin, t->d_cnt, t->d_lmlog, t->d_lmlvl, t->d_raw,
+                t->d_trace, t->d_part};  // d_out lives in d_cnt's allocation, h_out in h_cnt's
   for (void* p : ps)
     if (p) (void)hipFree(p);
-  if (t->h_out) (void)hipHostFree(t->h_out);
   if (t->h_in) (void)hipHostFree(t->h_in);
   if (t->h_cnt) (void)hipHostFree(t->h_cnt);
   if (t->e0) (void)hipEventDestroy(t->e0);

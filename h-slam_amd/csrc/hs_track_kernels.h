@@ -39,6 +39,8 @@ struct HsTryOut {
   double b[8];
 };
 
+constexpr int HS_TRK_INL = 4;  // hypotheses passed in the kernel arguments
+
 struct HsTrackArgs {
   HsTrkLevel lv[HS_TRK_MAXLEV];
   int coarsest;
@@ -47,7 +49,10 @@ struct HsTrackArgs {
   double refAff[2];
   const double* T_in;   // [n][7]
   const double* aff_in; // [n][2]
+  int n_inl;            // n <= HS_TRK_INL: the hypotheses come in the arguments (inl: T [n][7] | aff [n][2])
+  double inl[9 * HS_TRK_INL];
   HsTryOut* out;        // [n]
+  HsTryOut* hout;       // [n] or null: the same records in mapped pinned host memory (written at the end)
   int single_pass, pass_lvl;
   float pass_cutoff;
   unsigned int spin_limit;  // polls of the G-member meeting before a hypothesis is flagged (then rerun with G = 1)
@@ -55,12 +60,17 @@ struct HsTrackArgs {
   int* lm_lvl;          // [n][HS_TRK_MAXLOG]
   long long* trace;
   // G workgroups per hypothesis (blocks h G .. h G + G - 1): each pass's points are spread over them; their sums
-  // meet as tagged granules in part [n][2 (pass parity)][HS_TRK_MAXG][HS_TRK_NRED][2] (u64, zero at launch), and
-  // every workgroup forms the same totals (in workgroup order) and runs the same LM step
+  // meet as tagged granules in part [n][2 (pass parity)][HS_TRK_MAXG][HS_TRK_NRED][2] (u64), and every workgroup
+  // forms the same totals (in workgroup order) and runs the same LM step.  A granule's tag is (epoch << 12) |
+  // (pass + 1): the launch's epoch (1 .. 2^20 - 1, one per launch, the buffers zeroed when it wraps) keeps the
+  // granules of earlier launches from matching, so no per-launch memset is needed
   int G, nhyp;
+  unsigned int epoch;
+  int solve;            // the LM step's 8x8 solve: 0 Gauss-Jordan on 64 lanes, 1 Eigen-order LDLT on 8 row lanes
   double* part;
-  unsigned int* cnt;    // [nhyp] timeout flags (a member never arrived)
+  unsigned int* cnt;    // [nhyp] timeout flags (a member never arrived): the epoch of the launch that timed out
 };
+constexpr int HS_TRK_PASS_BITS = 12;  // passes per launch < 4096 (<= 5 levels x (50 + 1 + 6 cutoff repeats) x 2)
 constexpr int HS_TRK_NRED = 52;  // the reduced values of a pass (45 normal-equation entries, 4 energies / flows, 3 counts)
 constexpr int HS_TRK_MAXG = 16;
 

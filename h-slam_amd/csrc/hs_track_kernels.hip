@@ -135,10 +135,55 @@ __device__ __forceinline__ void ldlt8_solve_wave(const double* __restrict__ A, c
   }
 }
 
+__device__ __forceinline__ double trk_bperm_f64(double v, int src_lane) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(b & 0xffffffffll));
+  const int hi = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// The same damped 8x8 solve by Gauss-Jordan elimination on the whole wave: lane 8 i + j holds A(i, j) (the diagonal
+// scaled by dscale) and rhs(i).  Per pivot k every lane fetches A(k, j) and A(i, k) by ds_bpermute and A(k, k),
+// rhs(k) by readlane; row k is scaled by 1 / A(k, k) and every other row loses A(i, k) / A(k, k) times row k.  After
+// eight pivots rhs holds x.  The system is the LM-damped H + lambda diag(H) (symmetric positive semi-definite), so
+// elimination in the natural order is stable without Eigen's diagonal pivoting; an exactly zero pivot (a zero row
+// and column: an affine parameter held fixed) gives x_k = 0 as Eigen's LDLT solve does.  Depth: 8 x (one LDS
+// exchange, a reciprocal, an fma) against the LDLT's 8 dependent dot products plus two substitutions; the result
+// differs from the LDLT's by rounding only (tests/test_gpu_track.py: the LM logs and poses within the oracle's own
+// summation-order spread).  Every lane of the wave calls it; x is uniform.
+__device__ __forceinline__ void gj8_solve_wave(const double* __restrict__ A, const double* __restrict__ rhs,
+                                               double* __restrict__ x, double dscale, int lane) {
+  const int i = lane >> 3, j = lane & 7;
+  double a = A[i * 8 + j];
+  if (i == j) a *= dscale;
+  double r = rhs[i];
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const double akj = trk_bperm_f64(a, k * 8 + j);
+    const double aik = trk_bperm_f64(a, i * 8 + k);
+    const double d = trk_readlane_f64(a, k * 9);
+    const double rk = trk_readlane_f64(r, k * 8);
+    double rinv = __builtin_amdgcn_rcp(d);
+    rinv = __builtin_fma(rinv, __builtin_fma(-d, rinv, 1.0), rinv);
+    rinv = __builtin_fma(rinv, __builtin_fma(-d, rinv, 1.0), rinv);
+    rinv = fabs(d) > DBL_MIN ? rinv : 0.0;
+    if (i == k) {
+      a *= rinv;
+      r *= rinv;
+    } else {
+      const double f = aik * rinv;
+      a = __builtin_fma(-f, akj, a);
+      r = __builtin_fma(-f, rk, r);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 8; q++) x[q] = trk_readlane_f64(r, q * 8);
+}
+
 struct TrkShared {
   // pass inputs (thread 0 writes)
   float RKi[9], t[3], affLL[2], a_gs, b0, cutoff, maxEnergy;
-  int lvl;
+  int lvl, npts;  // npts: the level's reference points (*pc_n)
   // pass outputs
   double red[TRK_NT / 64][TRK_NRED];
   double res[6];
@@ -146,16 +191,18 @@ struct TrkShared {
   int nWarped;
   // LM state
   double T[7], Tn[7];
+  double Tq[4];  // T's quaternion normalized (T as given until the first accepted step, whose Tn is normalized)
   double aff[2], affn[2];
   double Hs[64], bs[8], resOld[6];
   double incNorm;
   float lambda, cutoffRep;
-  int brk, accept;
+  int brk[2];
   int passes;
   int npass, iters, nchecks;  // this workgroup's pass count (partial parity, counter target), LM iterations, checks
   long long pointPasses;
   long long prof[8];  // HS_KTRACE: thread-0 cycles: point loop, reductions, LM step, passes, wave reduce, barrier,
-                      // the LM step's LDLT, its exp + product
+                      // the LM step's solve, its exp + product
+  HsTryOut out;       // the lead's output record (thread 0 writes), copied out by trk_publish
 };
 
 // Wave reduce-scatter of 64 values (v[i], i < 64) over the 64 lanes: afterwards lane l holds the sum of v[l] over
@@ -203,13 +250,14 @@ __device__ __forceinline__ float wave_reduce_scatter64(const float (&v)[64], int
   return keep + dpp_mov<0xB1>(send);
 }
 
-// calcRes + calcGSSSE at S.RKi / S.t / S.affLL for level S.lvl; results in S.res / S.H / S.b / S.nWarped
-__device__ void trk_pass(const HsTrackArgs& a, TrkShared& S, int h, int g) {
+// calcRes + calcGSSSE at S.RKi / S.t / S.affLL for level S.lvl; results in S.res / S.H / S.b / S.nWarped, or (lm:
+// an LM iteration's pass) the accept test and, on accept, the new state and Hs / bs / resOld
+__device__ void trk_pass(const HsTrackArgs& a, TrkShared& S, int h, int g, bool lm = false) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int G = a.G, GT = G * TRK_NT;  // the hypothesis' workgroups take points g TRK_NT + tid (mod G TRK_NT)
   const int lvl = S.lvl;
   const HsTrkLevel& L = a.lv[lvl];
-  const int n = *L.pc_n, wl = L.w, hl = L.h;
+  const int n = S.npts, wl = L.w, hl = L.h;
   const float fxl = L.fx, fyl = L.fy, cxl = L.cx, cyl = L.cy;
   float RKi[9], Ki[9];
 #pragma unroll
@@ -224,16 +272,22 @@ __device__ void trk_pass(const HsTrackArgs& a, TrkShared& S, int h, int g) {
 #pragma unroll
   for (int q = 0; q < TRK_NACC; q++) acc[q] = 0.f;
   // the thread's points i = tid + k TRK_NT in order, TRK_B at a time: every load of a batch (point data, then the
-  // bilinear taps) is issued before any is used, so a batch costs two memory round trips instead of two per point
-  for (int i0 = g * TRK_NT + tid; i0 < n; i0 += TRK_B * GT) {
+  // bilinear taps) is issued before any is used, so a batch costs two memory round trips instead of two per point.
+  // A wave's lanes hold consecutive points, so "slot b of this batch holds a point for some lane" is wave-uniform
+  // (wb + b GT < n): empty slots are skipped whole, loads and projection included.
+  const int wb0 = g * TRK_NT + (tid & ~63);
+  for (int i0 = g * TRK_NT + tid, wb = wb0; wb < n; i0 += TRK_B * GT, wb += TRK_B * GT) {
     float id[TRK_B], x[TRK_B], y[TRK_B], refColor[TRK_B];
 #pragma unroll
     for (int b = 0; b < TRK_B; b++) {
-      const int i = min(i0 + b * GT, n - 1);
-      id[b] = L.pc_id[i];
-      x[b] = L.pc_u[i];
-      y[b] = L.pc_v[i];
-      refColor[b] = L.pc_col[i];
+      id[b] = x[b] = y[b] = refColor[b] = 0.f;
+      if (wb + b * GT < n) {
+        const int i = min(i0 + b * GT, n - 1);
+        id[b] = L.pc_id[i];
+        x[b] = L.pc_u[i];
+        y[b] = L.pc_v[i];
+        refColor[b] = L.pc_col[i];
+      }
     }
     float u[TRK_B], v[TRK_B], Ku[TRK_B], Kv[TRK_B], new_idepth[TRK_B];
     bool inb[TRK_B];
@@ -241,11 +295,13 @@ __device__ void trk_pass(const HsTrackArgs& a, TrkShared& S, int h, int g) {
     float fdx[TRK_B], fdy[TRK_B];
 #pragma unroll
     for (int b = 0; b < TRK_B; b++) {
+      inb[b] = false;
+      fdx[b] = fdy[b] = u[b] = v[b] = Ku[b] = Kv[b] = new_idepth[b] = 0.f;
+      if (wb + b * GT >= n) continue;  // wave-uniform
       const int i = i0 + b * GT;
       float pt0 = RKi[0] * x[b] + RKi[1] * y[b] + RKi[2] * 1.f;
       float pt1 = RKi[3] * x[b] + RKi[4] * y[b] + RKi[5] * 1.f;
       float pt2 = RKi[6] * x[b] + RKi[7] * y[b] + RKi[8] * 1.f;
-      const float ra0 = pt0, ra1 = pt1, ra2 = pt2;
       pt0 = pt0 + t0 * id[b];
       pt1 = pt1 + t1 * id[b];
       pt2 = pt2 + t2 * id[b];
@@ -254,31 +310,8 @@ __device__ void trk_pass(const HsTrackArgs& a, TrkShared& S, int h, int g) {
       Ku[b] = fxl * u[b] + cxl;
       Kv[b] = fyl * v[b] + cyl;
       new_idepth[b] = id[b] / pt2;
-      if (lvl == 0 && i < n && i % 32 == 0) {
-        const float k0 = Ki[0] * x[b] + Ki[1] * y[b] + Ki[2] * 1.f;
-        const float k1 = Ki[3] * x[b] + Ki[4] * y[b] + Ki[5] * 1.f;
-        const float k2 = Ki[6] * x[b] + Ki[7] * y[b] + Ki[8] * 1.f;
-        const float pT0 = k0 + t0 * id[b], pT1 = k1 + t1 * id[b], pT2 = k2 + t2 * id[b];
-        const float pS0 = k0 - t0 * id[b], pS1 = k1 - t1 * id[b], pS2 = k2 - t2 * id[b];
-        const float p30 = ra0 - t0 * id[b], p31 = ra1 - t1 * id[b], p32 = ra2 - t2 * id[b];
-        const float uT = pT0 / pT2, vT = pT1 / pT2;
-        const float KuT = fxl * uT + cxl, KvT = fyl * vT + cyl;
-        const float uT2 = pS0 / pS2, vT2 = pS1 / pS2;
-        const float KuT2 = fxl * uT2 + cxl, KvT2 = fyl * vT2 + cyl;
-        const float u3 = p30 / p32, v3 = p31 / p32;
-        const float Ku3 = fxl * u3 + cxl, Kv3 = fyl * v3 + cyl;
-        float s = (KuT - x[b]) * (KuT - x[b]) + (KvT - y[b]) * (KvT - y[b]);
-        sT += s;
-        s = (KuT2 - x[b]) * (KuT2 - x[b]) + (KvT2 - y[b]) * (KvT2 - y[b]);
-        sT += s;
-        s = (Ku[b] - x[b]) * (Ku[b] - x[b]) + (Kv[b] - y[b]) * (Kv[b] - y[b]);
-        sRT += s;
-        s = (Ku3 - x[b]) * (Ku3 - x[b]) + (Kv3 - y[b]) * (Kv3 - y[b]);
-        sRT += s;
-        sN += 2;
-      }
       inb[b] = i < n && (Ku[b] > 2 && Kv[b] > 2 && Ku[b] < wl - 3 && Kv[b] < hl - 3 && new_idepth[b] > 0);
-      // bilinear taps (interp33), requested for every point of the batch; out-of-bounds points read pixel 0
+      // bilinear taps (interp33), requested for every point of the slot; out-of-bounds points read pixel 0
       const float sx = inb[b] ? Ku[b] : 0.f, sy = inb[b] ? Kv[b] : 0.f;
       const int ix = (int)sx, iy = (int)sy;
       fdx[b] = sx - ix;
@@ -323,14 +356,55 @@ __device__ void trk_pass(const HsTrackArgs& a, TrkShared& S, int h, int g) {
         J[6] = ags * (b0 - refColor[b]);
         J[7] = -1.f;
         J[8] = residual;
+        // the normal-equation sums with fused multiply-adds (their order and rounding are free: the reference sums
+        // in four SSE lanes, the parity bar is relative)
         int q = 0;
 #pragma unroll
         for (int r = 0; r < 9; r++) {
           const float Jw = J[r] * hw;
 #pragma unroll
-          for (int c = r; c < 9; c++) acc[q++] += Jw * J[c];
+          for (int c = r; c < 9; c++, q++) acc[q] = __builtin_fmaf(Jw, J[c], acc[q]);
         }
       }
+    }
+  }
+  // the flow indicators (Src/CoarseTracker.cpp:370-401: level 0, every point with i % 32 == 0): flow point
+  // j = tid G + g of the hypothesis' threads is point 32 j, so they sit on the first waves of every member, away
+  // from the point loop (where the two flow lanes of each wave made the whole wave run the branch per slot)
+  if (lvl == 0) {
+    for (int j = tid * G + g; 32 * j < n; j += GT) {
+      const int i = 32 * j;
+      const float xf = L.pc_u[i], yf = L.pc_v[i], idf = L.pc_id[i];
+      float pt0 = RKi[0] * xf + RKi[1] * yf + RKi[2] * 1.f;
+      float pt1 = RKi[3] * xf + RKi[4] * yf + RKi[5] * 1.f;
+      float pt2 = RKi[6] * xf + RKi[7] * yf + RKi[8] * 1.f;
+      const float ra0 = pt0, ra1 = pt1, ra2 = pt2;
+      pt0 = pt0 + t0 * idf;
+      pt1 = pt1 + t1 * idf;
+      pt2 = pt2 + t2 * idf;
+      const float uu = pt0 / pt2, vv = pt1 / pt2;
+      const float Kuf = fxl * uu + cxl, Kvf = fyl * vv + cyl;
+      const float k0 = Ki[0] * xf + Ki[1] * yf + Ki[2] * 1.f;
+      const float k1 = Ki[3] * xf + Ki[4] * yf + Ki[5] * 1.f;
+      const float k2 = Ki[6] * xf + Ki[7] * yf + Ki[8] * 1.f;
+      const float pT0 = k0 + t0 * idf, pT1 = k1 + t1 * idf, pT2 = k2 + t2 * idf;
+      const float pS0 = k0 - t0 * idf, pS1 = k1 - t1 * idf, pS2 = k2 - t2 * idf;
+      const float p30 = ra0 - t0 * idf, p31 = ra1 - t1 * idf, p32 = ra2 - t2 * idf;
+      const float uT = pT0 / pT2, vT = pT1 / pT2;
+      const float KuT = fxl * uT + cxl, KvT = fyl * vT + cyl;
+      const float uT2 = pS0 / pS2, vT2 = pS1 / pS2;
+      const float KuT2 = fxl * uT2 + cxl, KvT2 = fyl * vT2 + cyl;
+      const float u3 = p30 / p32, v3 = p31 / p32;
+      const float Ku3 = fxl * u3 + cxl, Kv3 = fyl * v3 + cyl;
+      float sf = (KuT - xf) * (KuT - xf) + (KvT - yf) * (KvT - yf);
+      sT += sf;
+      sf = (KuT2 - xf) * (KuT2 - xf) + (KvT2 - yf) * (KvT2 - yf);
+      sT += sf;
+      sf = (Kuf - xf) * (Kuf - xf) + (Kvf - yf) * (Kvf - yf);
+      sRT += sf;
+      sf = (Ku3 - xf) * (Ku3 - xf) + (Kv3 - yf) * (Kv3 - yf);
+      sRT += sf;
+      sN += 2;
     }
   }
   const long long pc1 = (a.trace && tid == 0) ? clock64() + (long long)(acc[0] * 0.f + acc[44] * 0.f) : 0;
@@ -356,32 +430,34 @@ __device__ void trk_pass(const HsTrackArgs& a, TrkShared& S, int h, int g) {
     S.prof[4] += pcw - pc1;
     S.prof[5] += clock64() - pcw;
   }
-  if (tid < TRK_NRED) {
-    double s = 0.0;
-    for (int w = 0; w < TRK_NT / 64; w++) s += S.red[w][tid];
-    S.red[0][tid] = s;  // wave 0's slot is only read by this thread before the sum
-  }
-  __syncthreads();
-  if (G > 1) {
-    // The hypothesis' workgroups meet by granules (cdna_hip_programming.md §6 Guideline 16, R2: the data is the
-    // flag): every fp64 partial goes out as two 8-byte {tag = pass + 1, 32-bit half} granules (sc1 stores), and
-    // wave 0 -- lane q for value q -- re-reads the 2 G granules of its value (sc1 loads) until every tag matches,
-    // then sums the G partials in workgroup order.  One memory round trip per poll, no counter, no fences.  The
-    // granules are zeroed before every launch; the pass parity keeps a fast member off a slow member's buffer (it
-    // cannot write pass k + 2 before every member has read pass k).
-    typedef unsigned long long u64;
-    u64* P = reinterpret_cast<u64*>(a.part) + ((size_t)h * 2 + (S.npass & 1)) * HS_TRK_MAXG * TRK_NRED * 2;
-    const unsigned int tg = (unsigned int)(S.npass + 1);
-    const u64 tag = (u64)tg << 32;
-    if (tid < TRK_NRED) {
-      const u64 bits = (u64)__double_as_longlong(S.red[0][tid]);
-      __hip_atomic_store(P + (g * TRK_NRED + tid) * 2, tag | (bits & 0xffffffffull), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(P + (g * TRK_NRED + tid) * 2 + 1, tag | (bits >> 32), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (tid < 64) {
-      const int q = min(tid, TRK_NRED - 1);
+  if (wv == 0) {
+    // Wave 0 from here to the pass's end, lane q holding value q: the block total (the 8 wave sums, loaded together,
+    // added as a fixed tree), the member meeting, then the pass's results from registers (readlane broadcasts), so
+    // the only barrier left is the one that publishes them.
+    const int q = min(lane, TRK_NRED - 1);
+    double r8[TRK_NT / 64];
+#pragma unroll
+    for (int w = 0; w < TRK_NT / 64; w++) r8[w] = S.red[w][q];
+    double tot = ((r8[0] + r8[1]) + (r8[2] + r8[3])) + ((r8[4] + r8[5]) + (r8[6] + r8[7]));
+    static_assert(TRK_NT / 64 == 8, "block tree");
+    if (G > 1) {
+      // The hypothesis' workgroups meet by granules (cdna_hip_programming.md §6 Guideline 16, R2: the data is the
+      // flag): every fp64 partial goes out as two 8-byte {tag, 32-bit half} granules (sc1 stores), and lane q
+      // re-reads the 2 G granules of its value (sc1 loads) until every tag matches, then sums the G partials in
+      // workgroup order.  One memory round trip per poll, no counter, no fences.  The tag carries the launch's epoch
+      // and the pass, so granules left by earlier launches never match; the pass parity keeps a fast member off a
+      // slow member's buffer (it cannot write pass k + 2 before every member has read pass k).
+      typedef unsigned long long u64;
+      u64* P = reinterpret_cast<u64*>(a.part) + ((size_t)h * 2 + (S.npass & 1)) * HS_TRK_MAXG * TRK_NRED * 2;
+      const unsigned int tg = (a.epoch << HS_TRK_PASS_BITS) | (unsigned int)(S.npass + 1);
+      const u64 tag = (u64)tg << 32;
+      if (lane < TRK_NRED) {
+        const u64 bits = (u64)__double_as_longlong(tot);
+        __hip_atomic_store(P + (g * TRK_NRED + lane) * 2, tag | (bits & 0xffffffffull), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(P + (g * TRK_NRED + lane) * 2 + 1, tag | (bits >> 32), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
       u64 v[2 * HS_TRK_MAXG];
       unsigned int spins = 0;
       for (;;) {
@@ -399,65 +475,105 @@ __device__ void trk_pass(const HsTrackArgs& a, TrkShared& S, int h, int g) {
         if (__all(ok)) break;
         __builtin_amdgcn_s_sleep(1);
         if (++spins >= a.spin_limit) {  // a member never arrived (not co-resident): flag the hypothesis, go on
-          if (tid == 0) __hip_atomic_store(a.cnt + h, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (lane == 0) __hip_atomic_store(a.cnt + h, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
       }
-      if (tid < TRK_NRED) {
-        double s = 0.0;
+      tot = 0.0;
 #pragma unroll
-        for (int gg = 0; gg < HS_TRK_MAXG; gg++)
-          if (gg < G) s += __longlong_as_double((long long)((v[2 * gg] & 0xffffffffull) | (v[2 * gg + 1] << 32)));
-        S.red[0][tid] = s;
+      for (int gg = 0; gg < HS_TRK_MAXG; gg++)
+        if (gg < G) tot += __longlong_as_double((long long)((v[2 * gg] & 0xffffffffull) | (v[2 * gg + 1] << 32)));
+    }
+    const float Ef = (float)trk_readlane_f64(tot, TRK_NACC + 0);
+    const float fT = (float)trk_readlane_f64(tot, TRK_NACC + 1), fRT = (float)trk_readlane_f64(tot, TRK_NACC + 2);
+    const float fN = (float)trk_readlane_f64(tot, TRK_NACC + 3);
+    const int numE = (int)trk_readlane_f64(tot, TRK_NACC + 4), numSat = (int)trk_readlane_f64(tot, TRK_NACC + 5);
+    const int numW = (int)trk_readlane_f64(tot, TRK_NACC + 6);
+    double res[6];
+    res[0] = Ef;
+    res[1] = numE;
+    res[2] = fT / (fN + 0.1);
+    res[3] = 0;
+    res[4] = fRT / (fN + 0.1);
+    res[5] = numSat / (float)numE;
+    const int npad = (numW + 3) & ~3;  // buf_warped_n includes the zero padding (quirk kept)
+    // lm: the LM iteration's accept test (Src/CoarseTracker.cpp:611-640) -- an accepted pass's normal equations
+    // and residuals go straight to Hs / bs / resOld; a plain pass leaves them in H / b / res
+    const double oldRatio = S.resOld[0] / S.resOld[1];
+    const bool accept = lm && (res[0] / res[1]) < oldRatio;
+    double* Hd = accept ? S.Hs : S.H;
+    double* bd = accept ? S.bs : S.b;
+    if (lane < 6 && (!lm || accept)) (accept ? S.resOld : S.res)[lane] = res[lane];
+    if (lane < 45) {  // H / b from the 45 upper-triangle sums (row-major), one entry per lane
+      int qq = lane, r = 0;
+      while (qq >= 9 - r) {
+        qq -= 9 - r;
+        r++;
+      }
+      const int c = r + qq;
+      const double inv = (double)(1.0f / npad);
+      const double vv = (double)(float)tot;
+      const double sr = r < 3 ? hs_trk_scale_rot : r < 6 ? hs_trk_scale_trans : r == 6 ? hs_trk_scale_a : hs_trk_scale_b;
+      const double scc = c < 3 ? hs_trk_scale_rot : c < 6 ? hs_trk_scale_trans : c == 6 ? hs_trk_scale_a : hs_trk_scale_b;
+      if (!lm || accept) {
+        if (c < 8) {
+          Hd[r * 8 + c] = ((vv * inv) * scc) * sr;
+          Hd[c * 8 + r] = ((vv * inv) * sr) * scc;
+        } else if (r < 8) {  // (8, 8) is the residual square sum, not part of H / b
+          bd[r] = (vv * inv) * sr;
+        }
       }
     }
-    __syncthreads();
-  }
-  if (tid == 0) {
-    const double* R = S.red[0];
-    const float Ef = (float)R[TRK_NACC + 0];
-    const int numE = (int)R[TRK_NACC + 4], numSat = (int)R[TRK_NACC + 5], numW = (int)R[TRK_NACC + 6];
-    const float fT = (float)R[TRK_NACC + 1], fRT = (float)R[TRK_NACC + 2], fN = (float)R[TRK_NACC + 3];
-    S.res[0] = Ef;
-    S.res[1] = numE;
-    S.res[2] = fT / (fN + 0.1);
-    S.res[3] = 0;
-    S.res[4] = fRT / (fN + 0.1);
-    S.res[5] = numSat / (float)numE;
-    S.passes += 1;
-    S.npass += 1;
-    S.pointPasses += n;
-    const int npad = (numW + 3) & ~3;  // buf_warped_n includes the zero padding (quirk kept)
-    S.nWarped = npad;
-    if (a.trace) {
-      const long long pc2 = clock64() + (long long)(S.res[5] * 0.0);
-      S.prof[0] += pc1 - pc0;
-      S.prof[1] += pc2 - pc1;
-      S.prof[3] += 1;
-    }
-  }
-  if (tid >= 64 && tid < 64 + 45) {  // H / b from the 45 upper-triangle sums (row-major), one entry per thread
-    int q = tid - 64, r = 0;
-    while (q >= 9 - r) {
-      q -= 9 - r;
-      r++;
-    }
-    const int c = r + q;
-    const double* R = S.red[0];
-    const int numW = (int)R[TRK_NACC + 6];
-    const int npad = (numW + 3) & ~3;
-    const double inv = (double)(1.0f / npad);
-    const double v = (double)(float)R[tid - 64];
-    const double sr = r < 3 ? hs_trk_scale_rot : r < 6 ? hs_trk_scale_trans : r == 6 ? hs_trk_scale_a : hs_trk_scale_b;
-    const double scc = c < 3 ? hs_trk_scale_rot : c < 6 ? hs_trk_scale_trans : c == 6 ? hs_trk_scale_a : hs_trk_scale_b;
-    if (c < 8) {
-      S.H[r * 8 + c] = ((v * inv) * scc) * sr;
-      S.H[c * 8 + r] = ((v * inv) * sr) * scc;
-    } else if (r < 8) {  // (8, 8) is the residual square sum, not part of H / b
-      S.b[r] = (v * inv) * sr;
+    if (lane == 0) {
+      S.passes += 1;
+      S.npass += 1;
+      S.pointPasses += n;
+      S.nWarped = npad;
+      if (lm) {
+        const int it = S.iters - 1;
+        if (g == 0 && it < HS_TRK_MAXLOG) {
+          a.lm_log[((size_t)h * HS_TRK_MAXLOG + it) * 3 + 0] = res[0] / res[1];
+          a.lm_log[((size_t)h * HS_TRK_MAXLOG + it) * 3 + 1] = oldRatio;
+          a.lm_log[((size_t)h * HS_TRK_MAXLOG + it) * 3 + 2] = S.incNorm;
+          a.lm_lvl[(size_t)h * HS_TRK_MAXLOG + it] = lvl;
+        }
+        if (accept) {
+          S.aff[0] = S.affn[0];
+          S.aff[1] = S.affn[1];
+          for (int k = 0; k < 7; k++) S.T[k] = S.Tn[k];
+          for (int k = 0; k < 4; k++) S.Tq[k] = S.Tn[k];
+          S.lambda *= 0.5;
+        } else {
+          S.lambda *= 4;
+          if (S.lambda < 0.001f) S.lambda = 0.001f;  // lambdaExtrapolationLimit
+        }
+      }
+      if (a.trace) {
+        const long long pc2 = clock64() + (long long)(S.nWarped * 0);
+        S.prof[0] += pc1 - pc0;
+        S.prof[1] += pc2 - pc1;
+        S.prof[3] += 1;
+      }
     }
   }
   __syncthreads();
+}
+
+// the pose part of the pass inputs from a unit quaternion (RKi) and / or a translation (t)
+__device__ void trk_setup_pose(const HsTrackArgs& a, TrkShared& S, const hs::Quat* q, const double* t, int lvl) {
+  if (q) {
+    hs::SE3 T;
+    T.q = *q;
+    double Rd[9];
+    T.rotationMatrix(Rd);
+    float R[9];
+    for (int k = 0; k < 9; k++) R[k] = (float)Rd[k];
+    const float* Ki = a.lv[lvl].Ki;
+    for (int r = 0; r < 3; r++)
+      for (int c = 0; c < 3; c++) S.RKi[r * 3 + c] = R[r * 3 + 0] * Ki[0 * 3 + c] + R[r * 3 + 1] * Ki[1 * 3 + c] + R[r * 3 + 2] * Ki[2 * 3 + c];
+  }
+  if (t)
+    for (int k = 0; k < 3; k++) S.t[k] = (float)t[k];
 }
 
 // the pass inputs for state (T, aff) at level lvl: the pose part (pose = true: RKi, t) and / or the affine part
@@ -474,22 +590,33 @@ __device__ void trk_setup_part(const HsTrackArgs& a, TrkShared& S, const double 
     S.cutoff = cutoff;
     S.maxEnergy = 2 * a.huberTH * cutoff - a.huberTH * a.huberTH;
     S.lvl = lvl;
+    S.npts = *a.lv[lvl].pc_n;
     return;
   }
   const hs::SE3 T = hs::SE3::fromData(T7);
-  double Rd[9];
-  T.rotationMatrix(Rd);
-  float R[9];
-  for (int q = 0; q < 9; q++) R[q] = (float)Rd[q];
-  const float* Ki = a.lv[lvl].Ki;
-  for (int r = 0; r < 3; r++)
-    for (int c = 0; c < 3; c++) S.RKi[r * 3 + c] = R[r * 3 + 0] * Ki[0 * 3 + c] + R[r * 3 + 1] * Ki[1 * 3 + c] + R[r * 3 + 2] * Ki[2 * 3 + c];
-  for (int q = 0; q < 3; q++) S.t[q] = (float)T.t[q];
+  trk_setup_pose(a, S, &T.q, T.t, lvl);
 }
 __device__ void trk_setup(const HsTrackArgs& a, TrkShared& S, const double T7[7], const double aff[2], int lvl,
                           float cutoff) {
   trk_setup_part(a, S, T7, aff, lvl, cutoff, true);
   trk_setup_part(a, S, T7, aff, lvl, cutoff, false);
+}
+
+// the lead's output record, LDS -> a.out[h] (device) and, when the caller asked for it, a.hout[h] (mapped pinned
+// host memory: the host reads it once the launch has completed, with no copy behind the kernel); wave 0, 8 B a lane
+__device__ void trk_publish(const HsTrackArgs& a, TrkShared& S, int h, bool lead) {
+  __syncthreads();
+  if (!lead || threadIdx.x >= 64) return;
+  constexpr int NW = sizeof(HsTryOut) / 8;
+  static_assert(sizeof(HsTryOut) % 8 == 0, "output record in 8-B words");
+  const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&S.out);
+  unsigned long long* dd = reinterpret_cast<unsigned long long*>(a.out + h);
+  unsigned long long* dh = a.hout ? reinterpret_cast<unsigned long long*>(a.hout + h) : nullptr;
+  for (int k = threadIdx.x; k < NW; k += 64) {
+    const unsigned long long w = src[k];
+    dd[k] = w;
+    if (dh) dh[k] = w;
+  }
 }
 
 }  // namespace
@@ -499,14 +626,17 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
   const int tid = threadIdx.x;
   const int h = blockIdx.x / a.G, g = blockIdx.x - h * a.G;  // hypothesis, member workgroup
   const bool lead = g == 0;  // the workgroup that writes the hypothesis' outputs (every member computes them)
-  HsTryOut& out = a.out[h];
+  HsTryOut& out = S.out;  // staged in LDS, published by trk_publish
   HS_TRACE(a, 0);
   if (a.single_pass) {  // hs_tracker_calc_res
     if (tid == 0) {
       S.passes = 0;
       S.npass = 0;
       S.pointPasses = 0;
-      trk_setup(a, S, a.T_in + 7 * h, a.aff_in + 2 * h, a.pass_lvl, a.pass_cutoff);
+      double T7[7], aff[2];
+      for (int q = 0; q < 7; q++) T7[q] = a.n_inl ? a.inl[7 * h + q] : a.T_in[7 * h + q];
+      for (int q = 0; q < 2; q++) aff[q] = a.n_inl ? a.inl[7 * a.n_inl + 2 * h + q] : a.aff_in[2 * h + q];
+      trk_setup(a, S, T7, aff, a.pass_lvl, a.pass_cutoff);
     }
     __syncthreads();
     trk_pass(a, S, h, g);
@@ -516,14 +646,20 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
       for (int q = 0; q < 8; q++) out.b[q] = S.b[q];
       out.n_warped = S.nWarped;
     }
+    trk_publish(a, S, h, lead);
     return;
   }
   const int maxIterations[5] = {10, 20, 50, 50, 50};
   const float lambdaExtrapolationLimit = 0.001f;
   if (tid == 0) {
-    for (int q = 0; q < 7; q++) S.T[q] = a.T_in[7 * h + q];
-    S.aff[0] = a.aff_in[2 * h + 0];
-    S.aff[1] = a.aff_in[2 * h + 1];
+    for (int q = 0; q < 7; q++) S.T[q] = a.n_inl ? a.inl[7 * h + q] : a.T_in[7 * h + q];
+    const hs::SE3 T0 = hs::SE3::fromData(S.T);
+    S.Tq[0] = T0.q.x;
+    S.Tq[1] = T0.q.y;
+    S.Tq[2] = T0.q.z;
+    S.Tq[3] = T0.q.w;
+    S.aff[0] = a.n_inl ? a.inl[7 * a.n_inl + 2 * h + 0] : a.aff_in[2 * h + 0];
+    S.aff[1] = a.n_inl ? a.inl[7 * a.n_inl + 2 * h + 1] : a.aff_in[2 * h + 1];
     S.nchecks = 0;
     S.iters = 0;
     S.npass = 0;
@@ -557,84 +693,92 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
     }
     __syncthreads();
     for (int iteration = 0; iteration < maxIterations[lvl]; iteration++) {
-      __syncthreads();  // every thread has read S.brk of the previous iteration
-      // the LM step on two waves: lane 0 of wave 0 the pose (exp, product, RKi), lane 0 of wave 1 the affine part
-      // (fromToVecExposure); both solve the same 8x8 system (same inputs, same increment)
-      if (tid < 128) {  // waves 0 and 1: the LDLT on 8 row lanes, then lane 0 of each
-        const bool pw = tid == 0;
+      // the LM step on four waves, each solving the same 8x8 system (same inputs, same increment), then lane 0 of
+      // each takes a part: wave 0 the rotation (exp, product: the new quaternion, RKi), wave 2 the translation
+      // (exp's V a plus the rotated old translation; it recomputes the exp quaternion), wave 3 the increment norm /
+      // break test, wave 1 the affine part (fromToVecExposure).  A rotation beyond the series range (theta^2 >= 1e-2)
+      // runs the whole reference exp and product on wave 0.  S.Tq is S.T's quaternion normalized (once at the start;
+      // every product normalizes its own).
+      if (tid < 256) {
+        const int wv = tid >> 6;
         const long long lm0 = a.trace ? clock64() : 0;
-        // Hl = H with the diagonal scaled by (1 + lambda): formed as the solver loads H (pivoted indices)
         double mb[8], inc[8];
 #pragma unroll
         for (int i = 0; i < 8; i++) mb[i] = -S.bs[i];
-        ldlt8_solve_wave(S.Hs, mb, inc, 1 + S.lambda, tid & 63);
+        if (a.solve == 0)
+          gj8_solve_wave(S.Hs, mb, inc, 1 + S.lambda, tid & 63);
+        else
+          ldlt8_solve_wave(S.Hs, mb, inc, 1 + S.lambda, tid & 63);
         if ((tid & 63) == 0) {
-        const long long lm1 = a.trace ? clock64() + (long long)(inc[7] * 0.0) : 0;
-        float extrapFac = 1;
-        if (S.lambda < lambdaExtrapolationLimit) extrapFac = sqrtf(sqrtf(lambdaExtrapolationLimit / S.lambda));
-        for (int i = 0; i < 8; i++) inc[i] *= extrapFac;
-        double incScaled[8];
-        for (int i = 0; i < 8; i++) incScaled[i] = inc[i];
-        for (int i = 0; i < 3; i++) incScaled[i] *= hs_trk_scale_rot;
-        for (int i = 3; i < 6; i++) incScaled[i] *= hs_trk_scale_trans;
-        incScaled[6] *= hs_trk_scale_a;
-        incScaled[7] *= hs_trk_scale_b;
-        double ssum = 0;
-        for (int i = 0; i < 8; i++) ssum += incScaled[i];
-        if (!isfinite(ssum))
-          for (int i = 0; i < 8; i++) incScaled[i] = 0;
-        if (pw) {
-          S.iters++;
-          // the series exp / rsqrt-normalized product of the BA doStep (hs_se3_dev.h): Sophus' up to rounding
-          const hs::SE3 nw = se3_mul_step(se3_exp_step(incScaled), hs::SE3::fromData(S.T));
-          nw.toData(S.Tn);
-          if (a.trace) {
-            S.prof[6] += lm1 - lm0;
-            S.prof[7] += clock64() + (long long)(S.Tn[6] * 0.0) - lm1;
+          const long long lm1 = a.trace ? clock64() + (long long)(inc[7] * 0.0) : 0;
+          float extrapFac = 1;
+          if (S.lambda < lambdaExtrapolationLimit) extrapFac = sqrtf(sqrtf(lambdaExtrapolationLimit / S.lambda));
+          for (int i = 0; i < 8; i++) inc[i] *= extrapFac;
+          double incScaled[8];
+          for (int i = 0; i < 8; i++) incScaled[i] = inc[i];
+          for (int i = 0; i < 3; i++) incScaled[i] *= hs_trk_scale_rot;
+          for (int i = 3; i < 6; i++) incScaled[i] *= hs_trk_scale_trans;
+          incScaled[6] *= hs_trk_scale_a;
+          incScaled[7] *= hs_trk_scale_b;
+          double ssum = 0;
+          for (int i = 0; i < 8; i++) ssum += incScaled[i];
+          if (!isfinite(ssum))
+            for (int i = 0; i < 8; i++) incScaled[i] = 0;
+          const double u = se3_step_u(incScaled);
+          const bool series = u < 1e-2;
+          if (wv == 0) {
+            S.iters++;
+            const hs::Quat Tq{S.Tq[0], S.Tq[1], S.Tq[2], S.Tq[3]};
+            if (series) {
+              const hs::Quat q = se3_mul_step_q(se3_exp_step_q(incScaled, u), Tq);
+              S.Tn[0] = q.x;
+              S.Tn[1] = q.y;
+              S.Tn[2] = q.z;
+              S.Tn[3] = q.w;
+              trk_setup_pose(a, S, &q, nullptr, lvl);
+            } else {
+              hs::SE3 T;
+              T.q = Tq;
+              for (int k = 0; k < 3; k++) T.t[k] = S.T[4 + k];
+              const hs::SE3 nw = se3_mul_step(se3_exp_step(incScaled), T);
+              nw.toData(S.Tn);
+              trk_setup_pose(a, S, &nw.q, nw.t, lvl);
+            }
+            if (a.trace) {
+              const long long lm2 = clock64() + (long long)(S.RKi[4] * 0.f);
+              S.prof[6] += lm1 - lm0;
+              S.prof[7] += lm2 - lm1;
+              S.prof[2] += lm2 - lm0;
+            }
+          } else if (wv == 2) {
+            if (series) {
+              const hs::Quat qe = se3_exp_step_q(incScaled, u);
+              double te[3], rt[3], tn[3];
+              se3_exp_step_t(incScaled, u, te);
+              const double tT[3] = {S.T[4], S.T[5], S.T[6]};
+              hs::qrot(qe, tT, rt);
+              for (int k = 0; k < 3; k++) tn[k] = te[k] + rt[k];
+              S.Tn[4] = tn[0];
+              S.Tn[5] = tn[1];
+              S.Tn[6] = tn[2];
+              trk_setup_pose(a, S, nullptr, tn, lvl);
+            }
+          } else if (wv == 3) {
+            double nn = 0;
+            for (int i = 0; i < 8; i++) nn += inc[i] * inc[i];
+            S.incNorm = sqrt(nn);
+            S.brk[iteration & 1] = !(S.incNorm > 1e-3);
+          } else {
+            double affn[2] = {S.aff[0] + incScaled[6], S.aff[1] + incScaled[7]};
+            S.affn[0] = affn[0];
+            S.affn[1] = affn[1];
+            trk_setup_part(a, S, nullptr, affn, lvl, a.coarseCutoffTH * S.cutoffRep, false);
           }
-          double nn = 0;
-          for (int i = 0; i < 8; i++) nn += inc[i] * inc[i];
-          S.incNorm = sqrt(nn);
-          S.brk = !(S.incNorm > 1e-3);
-          trk_setup_part(a, S, S.Tn, nullptr, lvl, 0.f, true);
-          if (a.trace) S.prof[2] += clock64() + (long long)(S.RKi[4] * 0.f) - lm0;
-        } else {
-          double affn[2] = {S.aff[0] + incScaled[6], S.aff[1] + incScaled[7]};
-          S.affn[0] = affn[0];
-          S.affn[1] = affn[1];
-          trk_setup_part(a, S, nullptr, affn, lvl, a.coarseCutoffTH * S.cutoffRep, false);
-        }
         }
       }
       __syncthreads();
-      trk_pass(a, S, h, g);
-      if (tid == 0) {
-        const bool accept = (S.res[0] / S.res[1]) < (S.resOld[0] / S.resOld[1]);
-        const int it = S.iters - 1;
-        if (lead && it < HS_TRK_MAXLOG) {
-          a.lm_log[((size_t)h * HS_TRK_MAXLOG + it) * 3 + 0] = S.res[0] / S.res[1];
-          a.lm_log[((size_t)h * HS_TRK_MAXLOG + it) * 3 + 1] = S.resOld[0] / S.resOld[1];
-          a.lm_log[((size_t)h * HS_TRK_MAXLOG + it) * 3 + 2] = S.incNorm;
-          a.lm_lvl[(size_t)h * HS_TRK_MAXLOG + it] = lvl;
-        }
-        S.accept = accept ? 1 : 0;
-        if (accept) {  // (H, b, res are taken over by 64 threads after the barrier)
-          S.aff[0] = S.affn[0];
-          S.aff[1] = S.affn[1];
-          for (int q = 0; q < 7; q++) S.T[q] = S.Tn[q];
-          S.lambda *= 0.5;
-        } else {
-          S.lambda *= 4;
-          if (S.lambda < lambdaExtrapolationLimit) S.lambda = lambdaExtrapolationLimit;
-        }
-      }
-      __syncthreads();
-      if (S.accept && tid < 64) {  // the accepted pass's normal equations and residuals (read after the next barrier)
-        S.Hs[tid] = S.H[tid];
-        if (tid < 8) S.bs[tid] = S.b[tid];
-        if (tid < 6) S.resOld[tid] = S.res[tid];
-      }
-      if (S.brk) break;
+      trk_pass(a, S, h, g, true);  // the pass, the accept test and the state update; ends with a barrier
+      if (S.brk[iteration & 1]) break;  // (parity: the next step writes the other slot while slow waves read)
     }
     if (tid == 0) {  // lastResiduals[lvl] / lastFlowIndicators: logged for the caller's abort replay
       const int c = S.nchecks;
@@ -677,6 +821,7 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
     if (a.trace)
       for (int q = 0; q < 8; q++) a.trace[(size_t)blockIdx.x * 16 + 4 + q] = S.prof[q];
   }
+  trk_publish(a, S, h, lead);
   HS_TRACE(a, 15);
 }
 

@@ -110,14 +110,21 @@ class CoarseTracker:
 
     # Src/CoarseTracker.cpp:506-683
     def trackNewestCoarse(self, T7, aff, coarsestLvl, minResForAbort):
-        T = np.array(T7, dtype=np.float64)
-        a = np.array(aff, dtype=np.float64)
-        mr = np.ascontiguousarray(minResForAbort, dtype=np.float64)
-        lr, fl = np.zeros(5), np.zeros(3)
-        ok = C.c_int()
-        check(self.lib.hs_tracker_track(self.h, ptr(T), ptr(a), coarsestLvl, ptr(mr), ptr(lr), ptr(fl), C.byref(ok)))
-        self.lastResiduals, self.lastFlowIndicators = lr, fl
-        return bool(ok.value), T, a
+        # one staging block per tracker (T 7 | aff 2 | minRes 5 | lastResiduals 5 | flow 3 | ok), its addresses taken
+        # once: the per-call cost is the copies, not ctypes pointer objects
+        if getattr(self, "_stage", None) is None:
+            self._stage = np.zeros(23)
+            base = self._stage.ctypes.data
+            self._stage_ptrs = tuple(base + 8 * o for o in (0, 7, 9, 14, 19, 22))
+        st = self._stage
+        st[0:7] = T7
+        st[7:9] = aff
+        st[9:14] = minResForAbort
+        st[22] = 0.0
+        pT, pa, pmr, plr, pfl, pok = self._stage_ptrs
+        check(self.lib.hs_tracker_track(self.h, pT, pa, coarsestLvl, pmr, plr, pfl, pok))
+        self.lastResiduals, self.lastFlowIndicators = st[14:19].copy(), st[19:22].copy()
+        return bool(st[22:23].view(np.int32)[0]), st[0:7].copy(), st[7:9].copy()
 
     def track_tries(self, tries, aff_last_2_l, lastCoarseRMSE, reTrackThreshold=None):
         tr = np.ascontiguousarray(np.asarray(tries, dtype=np.float64).reshape(-1, 7))
