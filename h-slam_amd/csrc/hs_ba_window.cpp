@@ -592,7 +592,12 @@ int hs_ba_remove_frame(hs_ctx* c, int frame, int marginalize) {
   HS_TRY(ensure_incremental(c));
   if (frame < 0 || frame >= (int)c->wframes.size()) return fail(HS_ERR_INVALID, "frame index out of range");
   if (!c->wpts[frame].empty()) return fail(HS_ERR_STATE, "the frame still hosts points (remove them first)");
-  HS_TRY(commit_if_dirty(c));  // the prior's Schur complement needs the committed frame state and HM / bM
+  // The prior's Schur complement needs the committed frame state and HM / bM.  Pending point-only changes (removed
+  // points, dropped residuals, staged points) leave both as committed and the frame order unchanged, so they stay
+  // pending: the next commit takes them together with this removal (one commit per keyframe instead of two).
+  bool frames_pending = (int)c->wframes.size() != c->nF;
+  for (int f = 0; f < (int)c->wframes.size() && !frames_pending; f++) frames_pending = c->wframes[f].committed != f;
+  if (frames_pending) HS_TRY(commit_if_dirty(c));
   if (marginalize && !c->h_state_valid) HS_TRY(fetch_state(c));  // one read-back for the state and HM / bM
   HS_TRY(sync_hm(c));
   const int od = c->dim(), nd = od - 8, f0 = 4 + 8 * frame;
