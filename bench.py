@@ -275,7 +275,10 @@ def bench_track(args):
                                "points, 640x480, 5 levels", "ok": bool(ok), "device_ms_per_track": dev_ms,
                    "passes": passes, "point_passes": point_passes},
         "roofline": {"bound": "hbm", "kernel": "hs_k_track", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic("track", "hs_k_track")[0],
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": pmc_roof("track", "hs_k_track").get("hbm_bytes_per_launch",
+                                                                    pmc_traffic("track", "hs_k_track")[0]),
+                     "counters": pmc_roof("track", "hs_k_track"),
                      "bytes_per_unit": TRACK_BYTES_PER_POINT_PASS,
                      "unit_of_bytes": "reference point x calcRes+calcGSSSE pass", "units_per_launch": point_passes,
                      "avg_launch_ms": dev_ms, "flop_per_unit": 230,
