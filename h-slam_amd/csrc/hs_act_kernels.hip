@@ -174,7 +174,7 @@ __device__ __forceinline__ void lds_barrier() {
 constexpr int kBorderWords = 128;  // border-candidate bitmap of select_body: maps with w1 + h1 <= 4096
 
 __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* map, int* s_n, int* s_seeds,
-                                           float* s_red, uint32_t* s_bcand) {
+                                           float* s_red, uint32_t* s_bcand, int* s_wc) {
   const int tid = threadIdx.x, nthr = blockDim.x;
   const int w1 = a.w1, h1 = a.h1;
   float tmax = 0.f;
@@ -209,6 +209,26 @@ __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* ma
   }
   const int lane = tid & 63;
   const bool w0 = tid < 64;
+  // the pending entries (the only ones a batch can take; the others stay as they are) in loop order, compacted into
+  // a.plist, so the batches run over them alone (ballot prefix sums per chunk of the workgroup)
+  for (int c0 = 0; c0 < a.m; c0 += nthr) {
+    const int j = c0 + tid;
+    const bool p = j < a.m && a.cand[j] == HS_CAND_PENDING;
+    const unsigned long long bm = __ballot(p);
+    if (lane == 0) s_wc[tid >> 6] = __popcll(bm);
+    __syncthreads();
+    int off = s_n[2];
+    for (int w = 0; w < (tid >> 6); w++) off += s_wc[w];
+    if (p) a.plist[off + __popcll(bm & ((1ull << lane) - 1ull))] = j;
+    __syncthreads();
+    if (tid == 0) {
+      int tot = 0;
+      for (int w = 0; w < nthr / 64; w++) tot += s_wc[w];
+      s_n[2] += tot;
+    }
+    __syncthreads();
+  }
+  const int np = s_n[2];
   int nt = 0;
   long long npatch = 0;
   // wave 0's candidate batches of 64, the next batch's loads in flight while the current one is processed
@@ -216,24 +236,24 @@ __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* ma
   int ncell = 0, npt = 0;
   float nfrac = 0.f, nthr_ = 0.f;
   auto fetch = [&](int jj) {
-    const int jc = max(0, min(jj, a.m - 1));
+    const int jc = a.plist[max(0, min(jj, np - 1))];
     ncand = a.cand[jc];
     ncell = a.cell[jc];
     npt = a.order ? a.order[jc] : jc;
     nfrac = a.frac[jc];
     nthr_ = a.thr[jc];
   };
-  if (w0 && a.m > 0) fetch(lane);
+  if (w0 && np > 0) fetch(lane);
   const int rows = 2 * r + 1, wpr = (2 * r + 1 + 3) / 4 + 1;
   int wb_shift = 0, rb_shift = 0;
   while ((1 << wb_shift) < wpr) wb_shift++;
   while ((1 << rb_shift) < rows) rb_shift++;
   const int ps_shift = wb_shift + rb_shift;
   long long t_dec = 0, t_fold = 0, t_p1 = 0;
-  for (int base = 0; base < a.m; base += 64) {
+  for (int base = 0; base < np; base += 64) {
     const long long c0 = a.prof ? wall_clock64() : 0;
     if (w0) {
-      bool pend = (base + lane < a.m) && ncand == HS_CAND_PENDING;
+      bool pend = (base + lane < np) && ncand == HS_CAND_PENDING;
       const int cell = pend ? ncell : (1 | (1 << 16));
       const float frac = nfrac, thr = nthr_;
       const int pt = npt;
@@ -381,7 +401,7 @@ __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* ma
     }
   }
   if (a.prof && tid == 0) {
-    a.prof[3] = (a.m + 63) / 64;
+    a.prof[3] = (np + 63) / 64;
     a.prof[4] = npatch;
     a.prof[5] = r;
     a.prof[8] = t_dec;
@@ -393,11 +413,13 @@ __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* ma
 
 __global__ void __launch_bounds__(1024) hs_k_act_select(HsActSelectArgs a) {
   extern __shared__ uint32_t s_map32[];
-  __shared__ int s_n[2];
+  __shared__ int s_n[3];  // batch seeds, near-border flag, pending entries
   __shared__ int s_seeds[64];
   __shared__ float s_red[16];
+  __shared__ int s_wc[16];
   __shared__ uint32_t s_bcand[kBorderWords];
   for (int w = threadIdx.x; w < kBorderWords; w += blockDim.x) s_bcand[w] = 0u;
+  if (threadIdx.x == 0) s_n[2] = 0;
   __syncthreads();
   const int words = (a.w1 * a.h1 + 3) / 4;
   if (a.prof && threadIdx.x == 0) a.prof[0] = wall_clock64();
@@ -407,11 +429,11 @@ __global__ void __launch_bounds__(1024) hs_k_act_select(HsActSelectArgs a) {
   int nt;
   if (a.lds_map) {
     for (int w = threadIdx.x; w < words; w += blockDim.x) s_map32[w] = g[w];
-    nt = select_body(a, reinterpret_cast<uint8_t*>(s_map32), s_n, s_seeds, s_red, s_bcand);
+    nt = select_body(a, reinterpret_cast<uint8_t*>(s_map32), s_n, s_seeds, s_red, s_bcand, s_wc);
   } else {
     uint32_t* m32 = reinterpret_cast<uint32_t*>(a.dist);
     for (int w = threadIdx.x; w < words; w += blockDim.x) m32[w] = g[w];
-    nt = select_body(a, a.dist, s_n, s_seeds, s_red, s_bcand);
+    nt = select_body(a, a.dist, s_n, s_seeds, s_red, s_bcand, s_wc);
   }
   if (threadIdx.x == 0) *a.n_toopt = nt;
   if (a.prof && threadIdx.x == 0) {

@@ -390,7 +390,7 @@ static int act_alloc(hs_tracer* t) {
   TR_HIP(hipMalloc((void**)&t->d_order, sizeof(int) * c));
   TR_HIP(hipMalloc((void**)&t->d_cell, sizeof(int) * c));
   TR_HIP(hipMalloc((void**)&t->d_toopt, sizeof(int) * (c + 64)));  // + the greedy loop's 64 scratch slots
-  TR_HIP(hipMalloc((void**)&t->d_act_seeds, sizeof(int) * c));
+  TR_HIP(hipMalloc((void**)&t->d_act_seeds, sizeof(int) * 2 * (size_t)c));  // seeds | the select's pending list
   TR_HIP(hipMalloc((void**)&t->d_cand, c));
   TR_HIP(hipMalloc((void**)&t->d_action, c));
   TR_HIP(hipMalloc((void**)&t->d_res_in, c));
@@ -556,6 +556,7 @@ int hs_tracer_activate(hs_tracer* t, const float K4[4], int nF, const hs_act_fra
   se.dist = t->d_dist;
   se.map0 = reinterpret_cast<uint8_t*>(t->d_list_b);
   se.seeds = t->d_act_seeds;
+  se.plist = t->d_act_seeds + t->cap;
   se.toopt = t->d_toopt;
   se.n_toopt = t->d_act_cnt + 1;
   static const bool prof_on = getenv("HS_ACT_PROF") != nullptr;

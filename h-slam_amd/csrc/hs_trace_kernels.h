@@ -118,6 +118,7 @@ struct HsActSelectArgs {
   uint8_t* dist;             // global working map when the map does not fit LDS (then hs_k_act_dist mode 1 overwrites it)
   const uint8_t* map0;       // [w1*h1] makeDistanceMap's map (hs_k_act_dist mode 0)
   int* seeds;                // [m] out: the cells addIntoDistFinal was called on, in call order
+  int* plist;                // [m] scratch: the pending entries' indices in loop order
   int* toopt;                // [m] points to optimize, in order (+ 64 scratch slots after m)
   int* n_toopt;
   long long* prof;           // nullable: wall_clock64 at entry, after the seed BFS, at exit (HS_ACT_PROF=1)
