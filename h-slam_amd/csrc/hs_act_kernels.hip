@@ -291,7 +291,8 @@ __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* ma
         } else if (!border) {
           const int d = bfs_dist(x - sx, y - sy);
           if (d <= HS_ACT_BFS_STEPS - 1) v = min(v, d);
-        } else {
+        } else if (pend && max(abs(x - sx), abs(y - sy)) <= HS_ACT_BFS_STEPS) {
+          // (a seed farther than limit + 1 reaches no neighbour: border_step would change nothing)
           border_step(x, y, sc, HS_ACT_BFS_STEPS - 1, nb, v, nv);
         }
       }
@@ -343,7 +344,7 @@ __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* ma
           const int sc = s_seeds[j];
           if (((sc & 0xffff) == w1 - 1) | ((sc >> 16) == h1 - 1)) {
             if (sc == (x | (y << 16))) v = 0;
-          } else {
+          } else if (max(abs(x - (sc & 0xffff)), abs(y - (sc >> 16))) <= r + 1) {  // else: no neighbour reached
             border_step(x, y, sc, r, nb, v, nv);
           }
         }
