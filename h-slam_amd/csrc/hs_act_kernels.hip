@@ -268,7 +268,7 @@ __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* ma
         for (int i = 0; i < 3; i++)
           if (nb[i] >= 0) nv[i] = ld_cell(map, (nb[i] & 0xffff) + w1 * (nb[i] >> 16));
       }
-      int myslot = -1, ns = 0;
+      int myslot = -1, ns = 0, myseed = 0;  // lane k: the batch's k-th seed
       int bxm = 0, bym = 0;  // the batch seeds' largest x / y (the border pass is skipped when no seed is near)
       for (;;) {
         // dist = fwdWarpedIDDistFinal[u + w1 * v] + (ptp[0] - floorf(ptp[0])) >= currentMinActDist * my_type
@@ -278,7 +278,7 @@ __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* ma
         const int first = (int)__builtin_ctzll(bm);
         const int sc = __builtin_amdgcn_readlane(cell, first);
         if (lane == first) myslot = nt;
-        if (lane == 0) s_seeds[ns] = sc;
+        if (lane == ns) myseed = sc;
         ns++;
         nt++;
         bxm = max(bxm, sc & 0xffff);
@@ -300,7 +300,10 @@ __device__ __forceinline__ int select_body(const HsActSelectArgs& a, uint8_t* ma
       // batch's seeds from LDS (no global store inside the loop: its completion would be waited for with the
       // next batch's prefetch)
       a.toopt[myslot >= 0 ? myslot : a.m + lane] = pt;
-      if (lane < ns) a.seeds[nt - ns + lane] = s_seeds[lane];
+      if (lane < ns) {
+        a.seeds[nt - ns + lane] = myseed;
+        s_seeds[lane] = myseed;  // the fold's copy (read after the barrier)
+      }
       if (lane == 0) {
         s_n[0] = ns;
         s_n[1] = (bxm + r + 1 >= w1 - 1) | (bym + r + 1 >= h1 - 1);
