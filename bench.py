@@ -41,7 +41,7 @@ TRACK_BYTES_PER_POINT_PASS = 64  # CoarseTracker bytes per ref
 
 def pmc_traffic(points, kernel: str = "hs_k_lin"):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/*_pmc_traffic.json,
-    made by tools/r03_pmc.sh + tools/pmc_summary.py: separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this
+    made by tools/archive/r03_pmc.sh + tools/pmc_summary.py: separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this
     bench on the same workload).  points: the workload key -- the C4 window's point count, "kitti<N>" for
     --workload ba-kitti, or the workload name (trace, track).  None when no pass for it has been committed."""
     import glob
@@ -63,7 +63,7 @@ def pmc_traffic(points, kernel: str = "hs_k_lin"):
 
 def pmc_roof(key, kernel: str):
     """Counter evidence for `kernel` on workload `key` from the newest committed profiles/*_pmc_roof.json
-    (tools/r04_pmc.sh + tools/pmc_roof.py: separate FETCH_SIZE / WRITE_SIZE / SQ+GRBM rocprofv3 passes with the
+    (tools/archive/r04_pmc.sh + tools/pmc_roof.py: separate FETCH_SIZE / WRITE_SIZE / SQ+GRBM rocprofv3 passes with the
     kernel trace beside them): counter DRAM GB/s over the traced launch duration and the SQ issue split.
     {} when no pass for it has been committed."""
     import glob

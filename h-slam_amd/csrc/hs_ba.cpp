@@ -256,6 +256,13 @@ int fetch_state(hs_ctx* c) {
     std::memcpy(sz, f.state_zero, sizeof(sz));
     f.setStateZero(sz);
     c->proj_stale = true;
+    // the device copy gets the new nullspaces too: a later fetch_state (after a solve) copies the device frame over
+    // h_state, and upload_frames / compute_projector would otherwise rebuild the projector from the old ones
+    HS_TRY(wait_uploads(c));
+    std::memcpy(c->h_fstage, &f, sizeof(FrameH));
+    HS_HIP(hipMemcpyAsync(&c->d_state->frames[c->nF - 1], c->h_fstage, sizeof(FrameH), hipMemcpyHostToDevice,
+                          c->stream));
+    HS_HIP(hipEventRecord(c->ev_upload, c->stream));
   }
   return HS_OK;
 }

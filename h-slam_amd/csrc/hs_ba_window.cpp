@@ -723,6 +723,29 @@ extern "C" int hs_debug_get_state(hs_ctx* c, void* out) {
   std::memcpy(out, c->h_state, sizeof(HsDevState));
   return HS_OK;
 }
+// The largest |difference| between the nullspaces the DEVICE state holds for each frame and setStateZero's
+// (Include/Frame.h:166-190) recomputed from that frame's evalPT: 0 when no frame's device copy is stale.
+extern "C" int hs_debug_nullspace_error(hs_ctx* c, double* err_out) {
+  if (!c || !err_out || c->nF == 0) return fail(HS_ERR_INVALID, "null / no window");
+  HS_TRY(commit_if_dirty(c));
+  if (c->tail_pending) HS_TRY(fetch_state(c));  // settles the moved newest frame (host and device copies)
+  HsDevState dev;
+  HS_HIP(hipMemcpyAsync(&dev, c->d_state, sizeof(HsDevState), hipMemcpyDeviceToHost, c->stream));
+  HS_HIP(hipStreamSynchronize(c->stream));
+  double e = 0;
+  for (int f = 0; f < c->nF; f++) {
+    hs::FrameH r = dev.frames[f];
+    double sz[10];
+    std::memcpy(sz, r.state_zero, sizeof(sz));
+    r.setStateZero(sz);
+    for (int i = 0; i < 6; i++) {
+      e = std::max(e, std::fabs(r.nullspaces_scale[i] - dev.frames[f].nullspaces_scale[i]));
+      for (int k = 0; k < 6; k++) e = std::max(e, std::fabs(r.nullspaces_pose[i][k] - dev.frames[f].nullspaces_pose[i][k]));
+    }
+  }
+  *err_out = e;
+  return HS_OK;
+}
 extern "C" int hs_debug_set_state(hs_ctx* c, const void* in) {
   if (!c || !in || c->nF == 0) return fail(HS_ERR_INVALID, "null / no window");
   HS_TRY(commit_if_dirty(c));

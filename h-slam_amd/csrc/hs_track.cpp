@@ -83,6 +83,7 @@ struct hs_tracker {
   long long* d_trace = nullptr;
   int last_G = 1;                 // workgroups per hypothesis of the last track launch
   int n_cu = 256;                 // the device's compute units (hipDeviceAttributeMultiprocessorCount)
+  int wclk_khz = 100000;          // the constant wall clock the meetings' timeout reads (hipDeviceAttributeWallClockRate)
   int fallbacks = 0;              // launches rerun with G = 1 after a member-meeting timeout
   int trace_cap = 0;              // HS_KTRACE=1: per-hypothesis phase cycles of hs_k_track (stderr)
 };
@@ -193,8 +194,11 @@ static int run_tries(hs_tracker* t, int n, const double* h_in, int coarsest, int
   if (const char* e = std::getenv("HS_TRK_G_UNCHECKED"))  // test hook: G without the co-residency cap
     G = std::max(1, std::min(HS_TRK_MAXG, std::atoi(e)));
   if (single_pass || force_g1) G = 1;
-  a.spin_limit = 1u << 22;  // ~0.1 s of polls
-  if (const char* e = std::getenv("HS_TRK_SPIN")) a.spin_limit = (unsigned int)std::max(1, std::atoi(e));  // test hook
+  // a meeting's time bound: 20 ms of the device's wall clock (a healthy meeting takes a few us); after the first
+  // timeout the launch's members skip every later meeting and leave the LM loop (hs_k_track, S.dead), so a launch
+  // with a missing member costs ~20 ms per member before the G = 1 rerun, not 20 ms per pass
+  a.spin_limit = (unsigned int)std::min<long long>(0xffffffffll, (long long)t->wclk_khz * 20);
+  if (const char* e = std::getenv("HS_TRK_SPIN")) a.spin_limit = (unsigned int)std::max(1, std::atoi(e));  // ticks (test hook)
   a.G = G;
   a.nhyp = n;
   a.part = t->d_part;
@@ -393,6 +397,8 @@ int hs_tracker_create(hs_tracker** out, const hs_params* params, int device_id, 
   }
   if (hipDeviceGetAttribute(&t->n_cu, hipDeviceAttributeMultiprocessorCount, device_id) != hipSuccess || t->n_cu < 1)
     t->n_cu = 1;
+  if (hipDeviceGetAttribute(&t->wclk_khz, hipDeviceAttributeWallClockRate, device_id) != hipSuccess || t->wclk_khz < 1)
+    t->wclk_khz = 100000;
   int maxBlocks = 1;
   for (int l = 0; l < n_levels; l++) {
     const size_t n = (size_t)t->w[l] * t->h[l];

@@ -197,6 +197,8 @@ struct TrkShared {
   double incNorm;
   float lambda, cutoffRep;
   int brk[2];
+  int dead;  // a member meeting timed out: the launch's results are void (the host reruns with G = 1), so every later
+             // meeting is skipped and the LM / level loops end at once
   int passes;
   int npass, iters, nchecks;  // this workgroup's pass count (partial parity, counter target), LM iterations, checks
   long long pointPasses;
@@ -459,7 +461,9 @@ __device__ void trk_pass(const HsTrackArgs& a, TrkShared& S, int h, int g, bool 
                            __HIP_MEMORY_SCOPE_AGENT);
       }
       u64 v[2 * HS_TRK_MAXG];
-      unsigned int spins = 0;
+      // the poll's time bound on the constant 100 MHz wall clock (spin_limit ticks, set by the host from the clock
+      // rate); after a timeout (S.dead) a meeting polls once
+      const unsigned long long t_end = wall_clock64() + (S.dead ? 0ull : (unsigned long long)a.spin_limit);
       for (;;) {
         bool ok = true;
 #pragma unroll
@@ -474,8 +478,11 @@ __device__ void trk_pass(const HsTrackArgs& a, TrkShared& S, int h, int g, bool 
           if (gg < G) ok = ok && (unsigned int)(v[2 * gg] >> 32) == tg && (unsigned int)(v[2 * gg + 1] >> 32) == tg;
         if (__all(ok)) break;
         __builtin_amdgcn_s_sleep(1);
-        if (++spins >= a.spin_limit) {  // a member never arrived (not co-resident): flag the hypothesis, go on
-          if (lane == 0) __hip_atomic_store(a.cnt + h, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (wall_clock64() >= t_end) {  // a member never arrived (not co-resident): flag the hypothesis, go on
+          if (lane == 0) {
+            __hip_atomic_store(a.cnt + h, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            S.dead = 1;
+          }
           break;
         }
       }
@@ -630,6 +637,7 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
   HS_TRACE(a, 0);
   if (a.single_pass) {  // hs_tracker_calc_res
     if (tid == 0) {
+      S.dead = 0;
       S.passes = 0;
       S.npass = 0;
       S.pointPasses = 0;
@@ -661,6 +669,7 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
     S.aff[0] = a.n_inl ? a.inl[7 * a.n_inl + 2 * h + 0] : a.aff_in[2 * h + 0];
     S.aff[1] = a.n_inl ? a.inl[7 * a.n_inl + 2 * h + 1] : a.aff_in[2 * h + 1];
     S.nchecks = 0;
+    S.dead = 0;
     S.iters = 0;
     S.npass = 0;
     S.passes = 0;
@@ -669,14 +678,14 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
   }
   __syncthreads();
   bool haveRepeated = false;
-  for (int lvl = a.coarsest; lvl >= 0; lvl--) {
+  for (int lvl = a.coarsest; lvl >= 0 && !S.dead; lvl--) {  // (S.dead: uniform, read after a pass' barrier)
     if (tid == 0) {
       S.cutoffRep = 1;
       trk_setup(a, S, S.T, S.aff, lvl, a.coarseCutoffTH * S.cutoffRep);
     }
     __syncthreads();
     trk_pass(a, S, h, g);
-    while (S.res[5] > 0.6 && S.cutoffRep < 50) {  // uniform: S.res / S.cutoffRep are shared
+    while (S.res[5] > 0.6 && S.cutoffRep < 50 && !S.dead) {  // uniform: S.res / S.cutoffRep are shared
       __syncthreads();
       if (tid == 0) {
         S.cutoffRep *= 2;
@@ -778,7 +787,7 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
       }
       __syncthreads();
       trk_pass(a, S, h, g, true);  // the pass, the accept test and the state update; ends with a barrier
-      if (S.brk[iteration & 1]) break;  // (parity: the next step writes the other slot while slow waves read)
+      if (S.brk[iteration & 1] || S.dead) break;  // (parity: the next step writes the other slot while slow waves read)
     }
     if (tid == 0) {  // lastResiduals[lvl] / lastFlowIndicators: logged for the caller's abort replay
       const int c = S.nchecks;

@@ -101,6 +101,7 @@ SIGNATURES = {
     "hs_ba_get_point_state": ([VP] * 6, I),
     "hs_debug_state_size": ([], I),
     "hs_debug_get_state": ([VP, VP], I),
+    "hs_debug_nullspace_error": ([VP, VP], I),
     "hs_debug_set_state": ([VP, VP], I),
     "hs_comm_get_unique_id": ([VP], I),
     "hs_comm_init": ([VP, VP, I, I], I),

@@ -258,6 +258,12 @@ class BAWindow:
         check(self.lib.hs_debug_get_state(self.h, buf))
         return buf.raw
 
+    def debug_nullspace_error(self) -> float:
+        """max |device nullspaces - setStateZero(evalPT)| over the window's frames (0: no stale device copy)."""
+        e = C.c_double(0)
+        check(self.lib.hs_debug_nullspace_error(self.h, C.byref(e)))
+        return e.value
+
     def debug_set_state(self, blob: bytes):
         buf = C.create_string_buffer(blob, len(blob))
         check(self.lib.hs_debug_set_state(self.h, buf))

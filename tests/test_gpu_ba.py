@@ -385,6 +385,22 @@ def test_fix_linearization_after_optimize(scene2k):
     assert not np.array_equal(out["HdiF"], g.points()["HdiF"])
 
 
+def test_tail_nullspaces_reach_the_device(scene2k):
+    """The tail moves the newest frame's evalPT on the device (hs_k_fix_frames); its setStateZero nullspaces
+    (Include/Frame.h:166-190) are recomputed on the host at the next state fetch and must reach the device copy too:
+    a later fetch (after a solve), e.g. a frame-changing commit, copies the device frames over the host's and
+    rebuilds the gauge projector from them.  Tail -> optimize -> check the device copy, then a second tail / optimize."""
+    from hslam_amd.ba import BAWindow
+    g = BAWindow(scene2k)
+    z = np.zeros(scene2k.n_points)
+    for _ in range(2):
+        g.optimize(3)
+        g.fixLinearization(z, z.astype(np.int32))
+        g.optimize(2)
+        assert g.debug_nullspace_error() == 0.0
+    g.close()
+
+
 def _break_pair(scene, th_opt, min_opt):
     """GPU window (production order) + oracle with setting_thOptIterations / setting_minOptIterations."""
     from hslam_amd._lib import default_params
@@ -410,6 +426,22 @@ def test_optimize_break_forced(scene2k, min_opt):
     assert np.all(np.abs(eg - eo) <= 1e-3 * np.abs(eo))
     assert np.allclose(g.frames()["state"], o.frames()["state"], atol=1e-4)
     assert np.allclose(g.points()["idepth"], o.points()["idepth"], rtol=1e-3, atol=1e-4)
+    # linearizeAll(false) after the break (Src/FullSystemOptimize.cpp:449, 486) on both sides.  It does not return
+    # eg[-1]: the last linearization run re-set the newest frame's frameEnergyTH (setNewFrameEnergyTH feeds the NEXT
+    # pass only, Src/FullSystemOptimize.cpp:124 vs Src/OptimizationClasses.cpp:221), so this pass clamps a different
+    # residual set -- the oracle moves by the same amount (printed).  Energy, threshold and states vs the oracle.
+    th_g, th_o = g.frames()["energyTH"], o.frames()["energyTH"]
+    assert abs(th_g[-1] - th_o[-1]) <= 1e-3 * abs(th_o[-1])
+    el_g = g.linearizeAll(reset=False)
+    el_o = o.linearize_all(reset=False)
+    o.apply_res()
+    print(f"min_opt={min_opt}: relinearized energy gpu {el_g:.6e} oracle {el_o:.6e}; last iteration's "
+          f"gpu {eg[-1]:.6e} oracle {eo[-1]:.6e}")
+    assert abs(el_g - el_o) <= 1e-3 * abs(el_o)
+    rg, ro = g.residuals(), o.residuals()
+    assert np.count_nonzero(rg["state"] != ro["state"]) <= 0.002 * scene2k.n_res
+    th_g, th_o = g.frames()["energyTH"], o.frames()["energyTH"]
+    assert abs(th_g[-1] - th_o[-1]) <= 1e-3 * abs(th_o[-1])
     # the window goes on from the last iteration run: the tail on both sides
     z = np.zeros(scene2k.n_points)
     tg = g.fixLinearization(z, z.astype(np.int32))

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Roof evidence per kernel from tools/r04_pmc.sh's passes (DIR/p<KEY>/{FETCH_SIZE,WRITE_SIZE,SQ}).
+"""Roof evidence per kernel from tools/archive/r04_pmc.sh's passes (DIR/p<KEY>/{FETCH_SIZE,WRITE_SIZE,SQ}).
 
 Per kernel and key:
 * hbm_bytes_per_launch = 2 * FETCH_SIZE + WRITE_SIZE (FETCH_SIZE in KB, half-counted on gfx950 per
@@ -79,7 +79,7 @@ def summarise(d):
 
 def main():
     d, keys = sys.argv[1], sys.argv[2:]
-    print(json.dumps({"source": "tools/r04_pmc.sh: rocprofv3 --kernel-trace --stats --pmc, separate FETCH_SIZE / "
+    print(json.dumps({"source": "tools/archive/r04_pmc.sh: rocprofv3 --kernel-trace --stats --pmc, separate FETCH_SIZE / "
                                 "WRITE_SIZE / SQ+GRBM passes over `python3 bench.py --no-cpu` (see pmc_roof.py)",
                       "keys": {k: summarise(os.path.join(d, "p" + k)) for k in keys}}, indent=1))
 

@@ -48,7 +48,7 @@ def main():
         d, sizes = sys.argv[2], sys.argv[3:]
         print(json.dumps({
             "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes over `python3 bench.py --no-cpu "
-                      "--points N` (tools/r03_pmc.sh; keys: C4 point counts, kitti<N>, trace, track); hbm_bytes_per_launch = 2*FETCH_SIZE + WRITE_SIZE (gfx950 "
+                      "--points N` (tools/archive/r03_pmc.sh; keys: C4 point counts, kitti<N>, trace, track); hbm_bytes_per_launch = 2*FETCH_SIZE + WRITE_SIZE (gfx950 "
                       "FETCH_SIZE half-count correction, MI355X_MICROARCH.md); FETCH_SIZE counts memory-side requests "
                       "incl. Infinity-Cache hits",
             "points_per_gpu": {n: summarise(os.path.join(d, "p" + n)) for n in sizes}}, indent=1))
