@@ -36,6 +36,7 @@ METRIC = "point-residuals/sec in windowed photometric BA (8 KF × 2k pts), 1→8
 BYTES_PER_PRES = 448      # algorithmic bytes per point-residual (fused K1-K5: hs_k_lin accumulates in
                           # registers, no per-residual Jacobian record leaves the kernel)
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
+STRONG_LARGE_POINTS = 200000  # N > 1: the window whose strong scaling is reported beside the metric's own
 TRACK_BYTES_PER_POINT_PASS = 64  # CoarseTracker bytes per reference point per calcRes+GS pass
 
 
@@ -140,7 +141,11 @@ def cpu_baseline(points: int, seconds: float, kitti: bool = False):
         return {"value": scene.n_res / med, "iterations": it, "median_ms_per_step": med * 1e3,
                 "mean_ms_per_step": t / it * 1e3, "spread_ms": [min(per) * 1e3, max(per) * 1e3]}
 
-    mt = timed(threads, seconds * 0.5)
+    # the pool figure is the median of 3 repeats (each its own window and warm-up): one box's host noise varies
+    # from run to run, the repeats' spread is reported beside it
+    reps = sorted((timed(threads, seconds * 0.5 / 3) for _ in range(3)), key=lambda r: r["value"])
+    mt = dict(reps[1])
+    mt["repeat_values"] = [r["value"] for r in reps]
     one = timed(1, seconds * 0.25)
     # pool scaling below the job's share, side by side (T = nproc is not run: the GPU pool asks jobs to keep
     # worker pools to their share of a shared host; the curve shows how far the port scales before that)
@@ -157,8 +162,10 @@ def cpu_baseline(points: int, seconds: float, kitti: bool = False):
         "kind": "port",
         "sample": f"{mt['iterations']} GN iterations of the {cfg}, {scene.n_res} residuals, after 3 warm-up "
                   f"iterations, IndexThreadReduce-style pool with {threads} threads (chunk 50 / ceil(n/T)); value "
-                  f"from the median iteration {mt['median_ms_per_step']:.2f} ms (mean {mt['mean_ms_per_step']:.2f}); "
-                  f"oracle built {flags} on this host",
+                  f"from the median iteration {mt['median_ms_per_step']:.2f} ms (mean {mt['mean_ms_per_step']:.2f}), "
+                  f"the median of 3 repeats; oracle built {flags} on this host",
+        "repeat_values": mt["repeat_values"],
+        "repeat_spread_rel": (mt["repeat_values"][-1] - mt["repeat_values"][0]) / mt["value"],
         "median_ms_per_step": mt["median_ms_per_step"],
         "mean_ms_per_step": mt["mean_ms_per_step"],
         "spread_ms": mt["spread_ms"],
@@ -525,6 +532,32 @@ def bench_keyframe(args):
     return res
 
 
+def count_gpus(root: str = "/sys/class/kfd/kfd/topology/nodes"):
+    """GPUs this process may use, without loading any HIP / ROCm library: the KFD topology nodes with SIMDs
+    (/sys/class/kfd/kfd/topology/nodes/*/properties 'simd_count' > 0; CPU nodes have none), narrowed by
+    ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES when set.  0 without a KFD (no amdgpu
+    driver: no GPU); None when a topology file is unreadable (the ranks then fail loudly on their own)."""
+    import glob
+    if not os.path.isdir(root):
+        return 0
+    n = 0
+    try:
+        for f in glob.glob(os.path.join(root, "*", "properties")):
+            with open(f) as fh:
+                for line in fh:
+                    k, _, v = line.partition(" ")
+                    if k == "simd_count" and int(v) > 0:
+                        n += 1
+                        break
+    except (OSError, ValueError):
+        return None
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip() != ""]))
+    return n
+
+
 def launch_ranks(n: int, argv, plumbing: bool = False) -> int:
     """`--gpus N` without a launcher (WORLD_SIZE unset): N child rank processes, one per GPU, with the
     torch.distributed.run environment (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT).  This
@@ -535,9 +568,8 @@ def launch_ranks(n: int, argv, plumbing: bool = False) -> int:
     import subprocess
 
     if not plumbing:
-        import torch
-        ndev = torch.cuda.device_count()  # does not initialise HIP on this image
-        if ndev < n:
+        ndev = count_gpus()  # from the KFD topology in sysfs: no HIP library is loaded in this process
+        if ndev is not None and ndev < n:
             print(f"bench.py: --gpus {n} needs {n} visible GPUs, this node has {ndev}", file=sys.stderr)
             return 2
     s = socket.socket()
@@ -702,6 +734,8 @@ def main():
                     help="HIP event pairs inside the timed GN loop (sets HS_EVENT_TIMING; default: the environment's "
                          "value, else 0 = none; each pair adds ~2 us per step), 1 linearize only, 2 every phase")
     ap.add_argument("--no-phase-split", action="store_true", help="skip the untimed event-timed phase-split loop")
+    ap.add_argument("--no-large-strong", action="store_true",
+                    help="N > 1: skip the strong-scaling run of the 200k-point window reported beside `value`")
     ap.add_argument("--plumbing-check", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.gpus < 1:
@@ -758,13 +792,25 @@ def main():
                             else pmc_traffic(f"kitti{args.points}" if kitti else args.points, lin_kernel) if world == 1
                             else (None, None))
     ba.close()
-    other = None
+    other = large = None
     if world > 1:  # the other scaling mode, same ranks and communicator set-up, reported beside `value`
         mode = "weak" if args.scaling == "strong" else "strong"
         o = run_window(args, args.points * world if mode == "weak" else args.points, kitti, world, rank, local, dist)
         other = {"scaling": mode, "value": o["value"], "ms_per_step": o["ms_per_step"], "points": o["n_window"],
                  "points_per_gpu_rank0": o["shard"].n_points, "point_residuals": o["n_res_total"]}
         o["ba"].close()
+        if not kitti and args.points < STRONG_LARGE_POINTS:
+            # strong scaling where the linearization outweighs the replicated solve: the 200k window over the N
+            # ranks (DESIGN.md §7's projection); --no-large-strong skips it
+            if not args.no_large_strong:
+                a2 = argparse.Namespace(**vars(args))
+                a2.steps, a2.warmup = min(args.steps, 20), min(args.warmup, 3)
+                o = run_window(a2, STRONG_LARGE_POINTS, kitti, world, rank, local, dist)
+                large = {"scaling": "strong", "value": o["value"], "ms_per_step": o["ms_per_step"],
+                         "points": o["n_window"], "points_per_gpu_rank0": o["shard"].n_points,
+                         "point_residuals": o["n_res_total"], "steps": a2.steps, "warmup": a2.warmup,
+                         "note": "compare with `python bench.py --points 200000` at N = 1 (same window)"}
+                o["ba"].close()
     if kitti:
         wl = ("C5 BA half (BASELINE.json configs[4]): full windowed photometric BA incl. Schur complement, 8 KF x "
               f"{n_window} pts, KITTI 1232x368, 5 pyramid levels")
@@ -822,6 +868,8 @@ def main():
     }
     if other is not None:
         result[f"{other['scaling']}_scaling"] = other
+    if large is not None:
+        result["strong_scaling_200k"] = large
     if world == 1 and not args.no_phase_split:
         calls = optimize_calls(shard)
         calls["six_steps_ms"] = 6 * run["ms_per_step"]

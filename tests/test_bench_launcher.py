@@ -53,3 +53,20 @@ def test_too_few_gpus_fails_loudly():
 def test_single_gpu_workloads_reject_gpus():
     r = _run(["--workload", "track", "--gpus", "2"], _env())
     assert r.returncode != 0 and "single-GPU" in (r.stderr + r.stdout)
+
+
+def test_count_gpus_reads_the_kfd_topology(tmp_path, monkeypatch):
+    """The launcher counts GPUs from the KFD topology (nodes with SIMDs), narrowed by the visibility variables,
+    without loading a HIP library."""
+    sys.path.insert(0, ROOT)
+    import bench
+    for i, simds in enumerate([0, 1024, 1024, 1024]):  # node 0: the CPU
+        d = tmp_path / str(i)
+        d.mkdir()
+        (d / "properties").write_text(f"cpu_cores_count {0 if simds else 64}\nsimd_count {simds}\narray_count 32\n")
+    for v in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    assert bench.count_gpus(str(tmp_path)) == 3
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,2")
+    assert bench.count_gpus(str(tmp_path)) == 2
+    assert bench.count_gpus(str(tmp_path / "absent")) == 0
