@@ -86,6 +86,32 @@ def pmc_roof(key, kernel: str):
     return {}
 
 
+VALU_LATENCY_FLOOR = 0.3  # below this fraction of both roofs a kernel is latency-bound, not roof-bound
+
+
+def roof_binding(ctr: dict, hbm_alg_frac: float):
+    """The roof that binds a kernel, from its committed counters (pmc_roof): the VALU roof fraction (VALU busy per SIMD
+    = 4 SQ_ACTIVE_INST_VALU / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs): issued VALU cycles over the SIMDs' cycles during the
+    launch) against the HBM fraction (the counter DRAM bytes per second over the 8 TB/s spec, and the algorithmic
+    fraction beside it).  bound = "valu" when the VALU fraction is the larger one and at least VALU_LATENCY_FLOOR,
+    "hbm" when the HBM one is; "latency" (reported as binding_roof, with bound "hbm" as the contract's field) when
+    neither reaches the floor."""
+    valu = ctr.get("valu_busy_per_simd")
+    dram = ctr.get("dram_frac")
+    out = {"valu_frac": valu, "hbm_counter_frac": dram, "hbm_alg_frac": hbm_alg_frac}
+    if valu is None:
+        out["bound"] = "hbm"
+        return out
+    hbm = max(dram or 0.0, hbm_alg_frac)
+    if max(valu, hbm) < VALU_LATENCY_FLOOR:
+        out["bound"], out["binds"] = "hbm", "latency"
+    elif valu >= (dram or 0.0):
+        out["bound"] = out["binds"] = "valu"
+    else:
+        out["bound"] = out["binds"] = "hbm"
+    return out
+
+
 def host_cpu():
     """Model name of the timing host's CPU (lscpu's 'Model name', read from /proc/cpuinfo) and its logical CPUs."""
     model = None
@@ -220,10 +246,11 @@ def bench_trace(args):
         "config": {"workload": "C5 (BASELINE.json configs[4]) traceOn part: ctor + first traceOn of 20k immature "
                                "points, 8 host KFs, 1232x368", "points": s.n_points, "hosts": s.n_hosts,
                    "search_steps_per_trace": steps // args.steps, "parallelism": "single GPU"},
-        "roofline": {"bound": "hbm", "kernel": "hs_k_trace_on", "achieved": achieved, "peak": HBM_PEAK_GBS,
+        "roofline": dict({"bound": "hbm", "kernel": "hs_k_trace_on", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_roof("trace", "hs_k_trace_on").get("hbm_bytes_per_launch", pmc_traffic("trace", "hs_k_trace_on")[0]),
                      "bytes_per_unit": TRACE_BYTES_PER_STEP, "unit_of_bytes": "discrete-search step (GN taps excluded)",
                      "avg_launch_ms": kern_ms, "counters": pmc_roof("trace", "hs_k_trace_on")},
+                     **roof_binding(pmc_roof("trace", "hs_k_trace_on"), achieved / HBM_PEAK_GBS)),
         "second_trace_counts": dict(zip(("good", "oob", "outlier", "skipped", "badcondition", "uninitialized"),
                                         map(int, counts))),
         "cpu_baseline": None,
@@ -866,6 +893,7 @@ def main():
         "phase_ms_per_step": split,
         "cpu_baseline": None,
     }
+    result["roofline"].update(roof_binding(roof_ctr, achieved / HBM_PEAK_GBS))
     if other is not None:
         result[f"{other['scaling']}_scaling"] = other
     if large is not None:

@@ -1599,6 +1599,16 @@ void hso_ba_get_frames(void* h, double* state, float* energyTH, double* pose7, d
   if (calib_value4) for (int k = 0; k < 4; k++) calib_value4[k] = ba->calib.value[k];
 }
 
+/* frames: evalPT data[7] and state_zero[10] (the linearization points; the optimize tail moves the newest one's) */
+void hso_ba_get_frame_eval(void* h, double* eval7, double* state_zero) {
+  BA* ba = (BA*)h;
+  for (int i = 0; i < ba->nF; i++) {
+    const FrameO& f = ba->frames[i];
+    if (eval7) f.evalPT.toData(eval7 + i * 7);
+    if (state_zero) for (int k = 0; k < 10; k++) state_zero[i * 10 + k] = f.state_zero[k];
+  }
+}
+
 /* precalc records (for the device parity tests): per (h,t) 37 floats:
    KRKi[9] Kt[3] RTll_0[9] tTll_0[3] aff[2] b0 | RTll[9] tTll[3] -> 39 */
 void hso_ba_get_precalc(void* h, float* out /*nF*nF*39*/) {

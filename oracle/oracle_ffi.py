@@ -151,6 +151,7 @@ def load(fast=False):
     lib.hso_trc_compact.argtypes = [vp, vp]
     lib.hso_trc_trace.argtypes = [vp] * 4
     lib.hso_trc_get.argtypes = [vp] * 11
+    lib.hso_ba_get_frame_eval.argtypes = [vp, vp, vp]
     lib.hso_sel_create.restype = vp
     lib.hso_sel_create.argtypes = [vp, C.c_int, C.c_int]
     lib.hso_sel_destroy.argtypes = [vp]
@@ -320,6 +321,12 @@ class OracleBA:
         cal = np.zeros(4)
         self.lib.hso_ba_get_frames(self.h, _p(st), _p(th), _p(pose), _p(cal))
         return dict(state=st, energyTH=th, pose=pose, calib=cal)
+
+    def frame_eval(self):
+        """Each frame's evalPT (data[7]) and state_zero[10]."""
+        ev, sz = np.zeros((self.nF, 7)), np.zeros((self.nF, 10))
+        self.lib.hso_ba_get_frame_eval(self.h, _p(ev), _p(sz))
+        return dict(evalPT=ev, state_zero=sz)
 
     def precalc(self):
         out = np.zeros((self.nF * self.nF, 39), np.float32)

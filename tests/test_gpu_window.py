@@ -264,3 +264,54 @@ def test_keyframe_sequence_matches_oracle():
     HM, _ = drv.ba.marginal_prior()
     assert np.abs(HM).max() > 0
     drv.ba.close()
+
+
+def test_keyframe_sequence_drift_vs_oracle():
+    """Drift over a keyframe sequence: the library's keyframe path (hslam_amd.keyframe.KeyframeBA) and ONE oracle
+    instance chain (oracle/oracle_keyframe.py) each run System::AddKeyframe's BA part over five keyframes from their
+    OWN state -- their own optimize / tail results, their own toRemove / removeOutliers / flagPointsForRemoval
+    decisions, their own marginalizePointsF / marginalizeFrame HM / bM (Src/Mapping.cpp:12-140,
+    Src/EnergyFunctional.cpp:456-609).  Nothing is re-seeded between keyframes, so fp-order differences and any
+    decision that flips accumulate.  Compared at the end: the window's frame states and linearization points, the
+    calibration, the marginal prior HM / bM and the point set and depths; along the way the per-keyframe
+    energies.  Bars (stated in each assert) are set above what the two chains measure apart (printed)."""
+    from oracle_keyframe import OracleKeyframeBA
+    from hslam_amd.keyframe import KeyframeBA, make_ba_sequence
+    seq = make_ba_sequence(n_kf=12, points_per_kf=200, seed=7)
+    drv = KeyframeBA(seq, window=8, image_path="raw")
+    drv.bootstrap()
+    orc = OracleKeyframeBA(seq, window=8)
+    orc.bootstrap()
+    for k in range(7, 12):
+        ig = drv.add_keyframe(k)
+        io = orc.add_keyframe(k)
+        eg, eo = np.asarray(ig["energies"]), np.asarray(io["energies"])
+        rel = np.abs(eg - eo) / np.abs(eo)
+        print(f"kf {k}: energies rel dev max {rel.max():.2e}; points gpu {ig['n_points']} oracle {io['n_points']}; "
+              f"marginalized gpu {ig.get('marginalized_points')} oracle {io.get('marginalized_points')}")
+        assert ig["iters"] == io["iters"]
+        assert rel.max() <= 1e-2, (k, rel)
+    assert drv.frames == orc.frames
+    fg, fo = drv.ba.frames(), orc.frame_states()
+    fe = drv.ba.frame_eval()
+    ds = np.abs(fg["state"] - fo["state"]).max()
+    de = np.abs(fe["evalPT"] - fo["eval"]).max()
+    dc = np.abs(fg["calib"] - fo["calib"]).max()
+    HMg, bMg = drv.ba.marginal_prior()
+    scale = np.abs(np.diag(orc.HM)).max()
+    dH = (np.abs(HMg - orc.HM) / (np.abs(orc.HM) + 1e-3 * scale)).max()
+    db = (np.abs(bMg - orc.bM) / (np.abs(orc.bM) + 1e-3 * np.abs(orc.bM).max())).max()
+    pg = {drv.cand_of[int(h)]: float(d) for h, d in zip(drv.ba.structure()["handles"], drv.ba.point_state()["idepth"])}
+    po = orc.point_idepth()
+    common = sorted(set(pg) & set(po))
+    only = len(set(pg) ^ set(po))
+    dd = max(abs(pg[key] - po[key]) / abs(po[key]) for key in common)
+    print(f"final: frame state |d| {ds:.2e}, evalPT |d| {de:.2e}, calib |d| {dc:.2e}, HM worst ratio {dH:.2e}, "
+          f"bM worst ratio {db:.2e}, points common {len(common)} differing {only}, idepth rel {dd:.2e}")
+    assert ds <= 1e-3                 # frame states (scaled tangent units)
+    assert de <= 1e-4                 # linearization points (quaternion / translation data)
+    assert dc <= 1e-6
+    assert dH <= 1e-2 and db <= 1e-2  # HM / bM: |d| <= 1e-2 (|ref| + 1e-3 max|diag|), 100x the single-step H bar
+    assert only <= 0.01 * len(common)
+    assert dd <= 1e-2
+    drv.ba.close()
