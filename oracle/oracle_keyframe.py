@@ -141,8 +141,8 @@ class OracleKeyframeBA:
         for r in np.nonzero(drop)[0]:
             self.P[keys[rp[r]]]["res"].remove(self.frames[rt[r]])
         hdif_of = {key: float(hdif[j]) for j, key in enumerate(keys)}
+        info = dict(energies=energies, iters=n_it, tail_energy=e_tail, n_points=len(keys))
         self._remove_points([key for key in keys if not self.P[key]["res"]])
-        info = dict(energies=energies, iters=n_it, tail_energy=e_tail, n_points=len(self._keys()))
         if marginalize and len(self.frames) >= self.window:  # flagPointsForRemoval (Src/Mapping.cpp:248-328)
             marg_k = self.frames[0]
             keys = self._keys()
