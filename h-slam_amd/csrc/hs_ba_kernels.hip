@@ -103,6 +103,60 @@ __device__ __forceinline__ float point_step(int p, int h, int nF, unsigned m, co
   return -b * HdiF;
 }
 
+// doStepFromBackup -> FrameOptimizationData::setState's pose of one frame (Src/FullSystemOptimize.cpp:212-233,
+// Include/Frame.h:151-170): PRE_worldToCam = exp(scaled state) * evalPT and its inverse, into o[0..6] | o[7..13]
+// (SE3 data); o[14], o[15] = the scaled affine a, b.  The solve's step stage and the fused loop's linearize prologue
+// both run this, so their poses are bit-identical.
+__device__ __forceinline__ void frame_pose_stage(const double sc[10], const hs::SE3& evalPT, double* o,
+                                                 hs::SE3* PWo = nullptr, hs::SE3* PCo = nullptr) {
+  const hs::SE3 PW = se3_mul_step(se3_exp_step(sc), evalPT);
+  const hs::SE3 PC = PW.inverse();
+  PW.toData(o);
+  PC.toData(o + 7);
+  o[14] = sc[6];
+  o[15] = sc[7];
+  if (PWo) *PWo = PW;
+  if (PCo) *PCo = PC;
+}
+
+// FrameFramePrecalc::set's state-dependent part for pair (host h, target t) (Src/OptimizationClasses.cpp:13-39) from
+// the two frames' frame_pose_stage records: PRE_KRKiTll, PRE_KtTll, PRE_aff_mode (AffLight::fromToVecExposure of the
+// scaled a / b) and PRE_b0_mode (the host's aff0_b); vsf = the calib's value_scaledf.  PRE_RTll_0 / PRE_tTll_0
+// depend on evalPT only and are not touched.
+template <typename PC>
+__device__ __forceinline__ void pair_precalc_stage(const double* oh, const double* ot, float exp_h, float exp_t,
+                                                   double state_zero7_h, const float vsf[4], PC& pc) {
+  double aff[2];
+  hs::fromToVecExposure(exp_h, exp_t, oh[14], oh[15], ot[14], ot[15], aff);
+  pc.aff[0] = (float)aff[0];
+  pc.aff[1] = (float)aff[1];
+  pc.b0 = (float)(state_zero7_h * hs::SCALE_B);
+  const float K[9] = {vsf[0], 0, vsf[2], 0, vsf[1], vsf[3], 0, 0, 1};
+  float Ki[9];
+  hs::inv3f(K, Ki);
+  hs::SE3 PWt, PCh;
+  PWt.q = hs::Quat{ot[0], ot[1], ot[2], ot[3]};
+  PWt.t[0] = ot[4]; PWt.t[1] = ot[5]; PWt.t[2] = ot[6];
+  PCh.q = hs::Quat{oh[7], oh[8], oh[9], oh[10]};
+  PCh.t[0] = oh[11]; PCh.t[1] = oh[12]; PCh.t[2] = oh[13];
+  const hs::SE3 l2l = se3_mul_step(PWt, PCh);
+  double R[9];
+  l2l.rotationMatrix(R);
+  float RT[9], tT[3];
+#pragma unroll
+  for (int i = 0; i < 9; i++) RT[i] = (float)R[i];
+#pragma unroll
+  for (int i = 0; i < 3; i++) tT[i] = (float)l2l.t[i];
+  float KR[9], KRKi[9], Kt[3];
+  hs::mm3f(K, RT, KR);
+  hs::mm3f(KR, Ki, KRKi);
+  hs::mv3f(K, tT, Kt);
+#pragma unroll
+  for (int i = 0; i < 9; i++) pc.KRKi[i] = KRKi[i];
+#pragma unroll
+  for (int i = 0; i < 3; i++) pc.Kt[i] = Kt[i];
+}
+
 }  // namespace
 
 // =====================================================================================================
@@ -2009,9 +2063,8 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
   }
   HS_TRACE(a, 0);
   if (a.trace && threadIdx.x == 0) a.trace[24] = clock64();  // shader clock (effective-clock probe)
-  // entry prefetch: every global input (window state, systems, nullspace factors, b vectors, adjoints) is
+  // entry prefetch: every global input (window state, system vector, HM / bM, nullspace factors, energies) is
   // requested into registers before the first LDS store, so the kernel pays ONE memory round trip here
-  // instead of one per dependent load-store loop iteration
   constexpr int ST_WORDS = (int)(sizeof(HsDevState) / 8);
   constexpr int ST_NU = (ST_WORDS + SOLVE_NT - 1) / SOLVE_NT;
   constexpr int NF_NU = (2 * HS_MAXDIM * HS_NNS + SOLVE_NT - 1) / SOLVE_NT;
@@ -2019,35 +2072,29 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
   const int nF = a.nF, n = 4 + 8 * nF, nn = n * n;
   uint2 stw[ST_NU];
   {
-    const uint2* gs = reinterpret_cast<const uint2*>(a.st);
+    const uint2* gst = reinterpret_cast<const uint2*>(a.st);
 #pragma unroll
-    for (int u = 0; u < ST_NU; u++) stw[u] = gs[min(tid + u * SOLVE_NT, ST_WORDS - 1)];
+    for (int u = 0; u < ST_NU; u++) stw[u] = gst[min(tid + u * SOLVE_NT, ST_WORDS - 1)];
   }
-  // the system vector: thread entries q = tid + 256 u of the packed upper triangle (then b), read at their
-  // place (r, c) of the n x n layout, all loads in one batch (unconditional, clamped addresses)
+  // the system vector: thread slots q = tid + 512 u of the packed upper triangle (then b), read at their place
+  // (r, c) of the n x n layout.  The triangle is walked as an (n / 2) x (n + 1) rectangle (n = 4 + 8 nF is even):
+  // rectangle row i holds triangle row i (n - i entries) followed by triangle row n - 1 - i (i + 1 entries), so
+  // (r, c) follows from one reciprocal and selects (24-bit multiplies: full-rate integer ops)
   constexpr int NUQ = (hs_nt(HS_MAXDIM) + HS_MAXDIM + SOLVE_NT - 1) / SOLVE_NT;
   const int ntri = hs_nt(n);
+  const float w1inv = 1.0f / (float)(n + 1);
   int qaddr[NUQ], qr[NUQ], qc[NUQ];
 #pragma unroll
   for (int u = 0; u < NUQ; u++) {
     const int q = tid + SOLVE_NT * u;
-    int rr = -1, cc = -1, ad = -1;
-    if (q < ntri) {  // row rr: start(rr) = rr n - rr (rr - 1) / 2 <= q < start(rr + 1)
-      const float t2n = 2.0f * n + 1.0f;  // small integers: exact in fp32; the row is corrected by +-1 below
-      rr = (int)((t2n - sqrtf(t2n * t2n - 8.0f * q)) * 0.5f);
-      rr = max(0, min(rr, n - 1));
-      if (rr * n - rr * (rr - 1) / 2 > q) rr--;
-      if (rr + 1 < n && (rr + 1) * n - (rr + 1) * rr / 2 <= q) rr++;
-      cc = rr + (q - (rr * n - rr * (rr - 1) / 2));
-      ad = rr * n + cc;
-    } else if (q < ntri + n) {
-      rr = -2;
-      cc = q - ntri;
-      ad = nn + cc;
-    }
-    qaddr[u] = ad;
-    qr[u] = rr;
-    qc[u] = cc;
+    const int i = (int)(((float)q + 0.5f) * w1inv);  // exact: (q + 0.5) / (n + 1) stays >= 0.5 / 69 from an integer
+    const int j = q - __mul24(i, n + 1);
+    const bool upper = j < n - i;
+    const int r = upper ? i : n - 1 - i, c = upper ? i + j : j - 1;
+    const bool tri = q < ntri, isb = !tri && q < ntri + n;
+    qr[u] = tri ? r : (isb ? -2 : -1);
+    qc[u] = tri ? c : (isb ? q - ntri : -1);
+    qaddr[u] = tri ? __mul24(r, n) + c : (isb ? nn + (q - ntri) : -1);
   }
   // the diagonal frame blocks' host-f Schur terms after the energies (hs_k_stitch's aux_out, [nF][64]): staged into
   // LDS (one coalesced load per thread, in the batch below); entry (qr, qc) of a block (f, f) folds in
@@ -2059,38 +2106,46 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     const int fr = (qr[u] - 4) >> 3, fc = (qc[u] - 4) >> 3;
     aaddr[u] = (qr[u] >= 4 && fr == fc) ? fr * 64 + ((qr[u] - 4) & 7) * 8 + ((qc[u] - 4) & 7) : -1;
   }
-  double gs[NUQ], hmq[NUQ], nfv[NF_NU], axv = 0.0;
-  // energy, sum |idepth|, #points (multi-rank: the ranks' values summed in rank order)
-  double sysE0, sysE1, sysE2;
-  if (a.gsys) {
-    const double* ge = a.gsys + nn + n;
-    sysE0 = ge[0]; sysE1 = ge[1]; sysE2 = ge[2];
-    for (int r = 1; r < a.nranks; r++) {
-      sysE0 += ge[r * a.gstride];
-      sysE1 += ge[r * a.gstride + 1];
-      sysE2 += ge[r * a.gstride + 2];
-    }
-    if (tid < 3) a.sys_out[nn + n + tid] = tid == 0 ? sysE0 : (tid == 1 ? sysE1 : sysE2);
-  } else {
-    sysE0 = a.sysE[0]; sysE1 = a.sysE[1]; sysE2 = a.sysE[2];
-  }
+  double gs[NUQ], hmq[NUQ], hml[NUQ], nfv[NF_NU], axv = 0.0;
+  // energy, sum |idepth|, #points as vector loads (a uniform address would make them scalar loads, whose wait
+  // shares lgkmcnt with the LDS stores below)
+  int vz;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
+  double sysE0 = a.sysE[vz], sysE1 = a.sysE[vz + 1], sysE2 = a.sysE[vz + 2];
+  const bool hasHM = a.HM != nullptr;
   if (solve) {
-    // HM (the marginalization prior) entries at the same places, bM for the b entries; one batch with the rest
     axv = a.sys[AUX0 + min(tid, nF * 64 - 1)];
-    if (a.HM) {
+    if (hasHM) {  // HM at the entry (r, c) and at its mirror (c, r) (the latter for HM delta's rows), bM for b
 #pragma unroll
       for (int u = 0; u < NUQ; u++) {
         gs[u] = a.sys[max(qaddr[u], 0)];
         hmq[u] = qr[u] == -2 ? a.bM[qc[u]] : a.HM[qr[u] >= 0 ? qaddr[u] : 0];
+        hml[u] = a.HM[qr[u] >= 0 ? __mul24(qc[u], n) + qr[u] : 0];
       }
     } else {  // no marginalization prior (a uniform branch): only bM is read beside the system
 #pragma unroll
       for (int u = 0; u < NUQ; u++) {
         gs[u] = a.sys[max(qaddr[u], 0)];
         hmq[u] = qr[u] == -2 ? a.bM[qc[u]] : 0.0;
+        hml[u] = 0.0;
       }
     }
-    if (a.gsys) {  // multi-rank: the gathered vectors (a.sys = rank 0's) summed in rank order, the raw sums kept
+#pragma unroll
+    for (int u = 0; u < NF_NU; u++) nfv[u] = a.Nproj[min(tid + u * SOLVE_NT, 2 * n * HS_NNS - 1)];
+  }
+  HS_TRACE(a, 1);  // every load of the prefetch issued
+  if (a.gsys) {  // multi-rank: the gathered vectors (a.sys = rank 0's) summed in rank order, the raw sums kept
+    const double* ge = a.gsys + nn + n;
+    sysE0 = ge[0];  // rank 0's (a.sysE is this rank's own)
+    sysE1 = ge[1];
+    sysE2 = ge[2];
+    for (int r = 1; r < a.nranks; r++) {
+      sysE0 += ge[r * a.gstride];
+      sysE1 += ge[r * a.gstride + 1];
+      sysE2 += ge[r * a.gstride + 2];
+    }
+    if (tid < 3) a.sys_out[nn + n + tid] = tid == 0 ? sysE0 : (tid == 1 ? sysE1 : sysE2);
+    if (solve) {
 #pragma unroll
       for (int u = 0; u < NUQ; u++) {
         const int ad = max(qaddr[u], 0);
@@ -2100,11 +2155,10 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
       for (int r = 1; r < a.nranks; r++) axv += a.gsys[r * a.gstride + AUX0 + min(tid, nF * 64 - 1)];
       if (tid < nF * 64) a.sys_out[AUX0 + tid] = axv;
     }
-#pragma unroll
-    for (int u = 0; u < NF_NU; u++) nfv[u] = a.Nproj[min(tid + u * SOLVE_NT, 2 * n * HS_NNS - 1)];
   }
-  // L^T must be zero on entry to the LDLT: stored while the prefetch above is in flight
-  if (solve)
+  // L^T must be zero on entry to the LDLT: stored while the prefetch above is in flight (with a marginalization
+  // prior, LT first holds HM for the per-row HM delta products and is zeroed after them)
+  if (solve && !hasHM)
     for (int idx = tid; idx < HS_MAXDIM * LSTR; idx += nt) LT[idx] = 0.0;
   {
     uint2* ls = reinterpret_cast<uint2*>(st_raw);
@@ -2112,25 +2166,28 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     for (int u = 0; u < ST_NU; u++)
       if (tid + u * SOLVE_NT < ST_WORDS) ls[tid + u * SOLVE_NT] = stw[u];
   }
+  HS_TRACE(a, 9);  // the window state arrived (thread 0's words)
   if (solve && tid < nF * 64) AUXs[tid] = axv;
   if (solve) {  // the raw diagonal (+ HM's) and b (+ bM) entries to LDS for the per-row scaling below
 #pragma unroll
     for (int u = 0; u < NUQ; u++) {
-      const double hm = a.HM ? hmq[u] : 0.0;
       if (qr[u] >= 0 && qr[u] == qc[u]) {
         dgv[qc[u]] = gs[u];
-        dgm[qc[u]] = hm;
+        dgm[qc[u]] = hmq[u];
       } else if (qr[u] == -2) {
         dgv[HS_MAXDIM + qc[u]] = gs[u];
         dgm[HS_MAXDIM + qc[u]] = hmq[u];
       }
+      if (hasHM && qr[u] >= 0) {
+        LT[qr[u] * LSTR + qc[u]] = hmq[u];
+        LT[qc[u] * LSTR + qr[u]] = hml[u];
+      }
     }
-  }
-  if (solve) {
 #pragma unroll
     for (int u = 0; u < NF_NU; u++)
       if (tid + u * SOLVE_NT < 2 * n * HS_NNS) Nf[tid + u * SOLVE_NT] = nfv[u];
   }
+  HS_TRACE(a, 11);  // thread 0's system entries arrived
   __syncthreads();
   HS_TRACE(a, 8);
   if (tid == 0) {
@@ -2172,20 +2229,22 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
       A[q * n + q] = sq * hv * sq;
       const double bl = q < 4 ? a.initialCalibHessian * delta(q)
                               : pr * st->frames[(q - 4) >> 3].delta_prior[(q - 4) & 7];
-      double hmd = 0.0;
-      if (a.HM)
-        for (int k = 0; k < n; k++) hmd += a.HM[q * n + k] * delta(k);
+      double hmd = 0.0;  // (HM delta)_q in the reference's order, HM's row q staged in LT
+      if (hasHM)
+        for (int k = 0; k < n; k++) hmd += LT[q * LSTR + k] * delta(k);
       yv[q] = sq * ((bl + (dgm[HS_MAXDIM + q] + hmd)) + dgv[HS_MAXDIM + q]);
     }
     __syncthreads();
     HS_TRACE(a, 7);
+    if (hasHM)  // LT's HM rows are read: zero for the LDLT (the barrier after the off-diagonal pass orders it)
+      for (int idx = tid; idx < HS_MAXDIM * LSTR; idx += nt) LT[idx] = 0.0;
     // the scaled off-diagonal entries S H S, mirrored from the upper triangle
 #pragma unroll
     for (int u = 0; u < NUQ; u++) {
       const int r = qr[u], c = qc[u];
       if (r >= 0 && r != c) {
         const double gf = aaddr[u] >= 0 ? gs[u] - a.aux_sc * AUXs[aaddr[u]] : gs[u];
-        const double w = Sv[r] * (gf + (a.HM ? hmq[u] : 0.0)) * Sv[c];
+        const double w = Sv[r] * (gf + hmq[u]) * Sv[c];
         A[r * n + c] = w;
         A[c * n + r] = w;
       }
@@ -2302,9 +2361,9 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
   if (a.flags & HS_APPLY) {
     // backupState + doStepFromBackup(1, 1, 1, 1, 1) + setPrecalcValues (Src/FullSystemOptimize.cpp:171-314) in two
     // register-resident stages: lane 64 + f (wave 1) steps frame f (new state, its scaled copy, PRE_worldToCam
-    // = exp(scaled xi) * evalPT and its inverse) into LDS; after one barrier lane (h, t) of wave 0 reads both
-    // frames' poses and forms the pair's FrameFramePrecalc::set while wave 1 writes the frames and the calib back.  Each SE(3) exp / product runs once per frame (the stage-free form ran two per lane, on one
-    // wave's serial fp64 issue).  PRE_RTll_0 / PRE_tTll_0 depend on evalPT only and stay as uploaded.
+    // = exp(scaled xi) * evalPT and its inverse: frame_pose_stage) into LDS; after one barrier lane (h, t) of wave 0
+    // reads both frames' poses and forms the pair's FrameFramePrecalc::set (pair_precalc_stage) while wave 1 writes
+    // the frames and the calib back.  PRE_RTll_0 / PRE_tTll_0 depend on evalPT only and stay as uploaded.
     const int np = nF * nF;
     double* fx = B;  // LDLT scratch (free now): per frame PRE_worldToCam (7) | PRE_camToWorld (7) | scaled a, b
     double cv[4];
@@ -2319,60 +2378,51 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     hs::SE3 PW, PC;
     if (fl) {
       const hs::FrameH& F = st->frames[fw];
-      double ev[7];
 #pragma unroll
       for (int q = 0; q < 10; q++) {
         sh[q] = F.state[q];
         ns[q] = sh[q] + 1.0 * F.step[q];
       }
-      F.evalPT.toData(ev);
       scale_state(ns, sc);
-      PW = se3_mul_step(se3_exp_step(sc), hs::SE3::fromData(ev));
-      PC = PW.inverse();
-      double* o = fx + 16 * fw;
-      PW.toData(o);
-      PC.toData(o + 7);
-      o[14] = sc[6];
-      o[15] = sc[7];
+      double ev[7];
+      F.evalPT.toData(ev);
+      frame_pose_stage(sc, hs::SE3::fromData(ev), fx + 16 * fw, &PW, &PC);
     }
-    if (tid == 128) {  // canbreak on wave 2, beside the frame stage (it reads the steps only, which no stage writes)
+    if (tid >= 128 && tid < 192) {  // canbreak on wave 2, beside the frame stage (it reads the steps only)
+      // lane f forms frame f's terms (fp64, the reference's expressions), lane 0 adds them in frame order into the
+      // float sums (float += double, as the reference's loop): no chain of dependent LDS reads
+      const int f = min(tid - 128, nF - 1);
+      const double* sp = st->frames[f].step;
+      const double tA = sp[6] * sp[6], tB = sp[7] * sp[7];
+      const double tT = sp[0] * sp[0] + sp[1] * sp[1] + sp[2] * sp[2];
+      const double tR = sp[3] * sp[3] + sp[4] * sp[4] + sp[5] * sp[5];
       float sumA = 0, sumB = 0, sumT = 0, sumR = 0;
-      for (int f = 0; f < nF; f++) {
-        const double* sp = st->frames[f].step;
-        sumA += sp[6] * sp[6];
-        sumB += sp[7] * sp[7];
-        sumT += sp[0] * sp[0] + sp[1] * sp[1] + sp[2] * sp[2];
-        sumR += sp[3] * sp[3] + sp[4] * sp[4] + sp[5] * sp[5];
+      for (int g = 0; g < nF; g++) {
+        sumA += readlane_f64(tA, g);
+        sumB += readlane_f64(tB, g);
+        sumT += readlane_f64(tT, g);
+        sumR += readlane_f64(tR, g);
       }
       const float nfr = (float)nF;
       sumA /= nfr; sumB /= nfr; sumR /= nfr; sumT /= nfr;
       const float sumNID = sysE2 > 0 ? (float)(sysE1 / sysE2) : 0.f;
       const float th = a.thOptIterations;
-      st->canbreak = sqrtf(sumA) < 0.0005 * th && sqrtf(sumB) < 0.00005 * th && sqrtf(sumR) < 0.00005 * th &&
-                     sqrtf(sumT) * sumNID < 0.00005 * th;
-      st->iteration = s_it + 1;
+      if (tid == 128) {
+        st->canbreak = sqrtf(sumA) < 0.0005 * th && sqrtf(sumB) < 0.00005 * th && sqrtf(sumR) < 0.00005 * th &&
+                       sqrtf(sumT) * sumNID < 0.00005 * th;
+        st->iteration = s_it + 1;
+      }
     }
-    // the pair stage's pose-free part on wave 0, beside the frame stage: the affine transfer from the frames' new
-    // scaled a / b (the frame stage's own ns -> sc arithmetic), K and K^-1 from the new calib, b0
-    float pK[9], pKi[9];
+    // the pair stage's inputs that no stage writes, read before the barrier
+    const float vsf[4] = {(float)(hs::SCALE_F * cv[0]), (float)(hs::SCALE_F * cv[1]), (float)(hs::SCALE_C * cv[2]),
+                          (float)(hs::SCALE_C * cv[3])};
+    float exh = 0.f, ext = 0.f;
+    double sz7 = 0.0;
     if (tid < np) {
       const int hh = tid / nF, tt = tid - hh * nF;
-      const hs::FrameH& H = st->frames[hh];
-      const hs::FrameH& T = st->frames[tt];
-      const double ah = hs::SCALE_A * (H.state[6] + 1.0 * H.step[6]), bh = hs::SCALE_B * (H.state[7] + 1.0 * H.step[7]);
-      const double at = hs::SCALE_A * (T.state[6] + 1.0 * T.step[6]), bt = hs::SCALE_B * (T.state[7] + 1.0 * T.step[7]);
-      double aff[2];
-      hs::fromToVecExposure(H.ab_exposure, T.ab_exposure, ah, bh, at, bt, aff);
-      HsPrecalc* pc = a.pre + tid;
-      pc->aff[0] = (float)aff[0];
-      pc->aff[1] = (float)aff[1];
-      pc->b0 = (float)(H.state_zero[7] * hs::SCALE_B);  // aff0_b of the host
-      const float vsf[4] = {(float)(hs::SCALE_F * cv[0]), (float)(hs::SCALE_F * cv[1]), (float)(hs::SCALE_C * cv[2]),
-                            (float)(hs::SCALE_C * cv[3])};
-      const float K[9] = {vsf[0], 0, vsf[2], 0, vsf[1], vsf[3], 0, 0, 1};
-#pragma unroll
-      for (int i = 0; i < 9; i++) pK[i] = K[i];
-      hs::inv3f(pK, pKi);
+      exh = st->frames[hh].ab_exposure;
+      ext = st->frames[tt].ab_exposure;
+      sz7 = st->frames[hh].state_zero[7];
     }
     if ((a.dbg & 16) && a.trace && tid == 0) a.trace[22] = clock64();
     __syncthreads();
@@ -2386,31 +2436,7 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     }
     if (tid < np) {
       const int hh = tid / nF, tt = tid - hh * nF;
-      const double* oh = fx + 16 * hh;
-      const double* ot = fx + 16 * tt;
-      hs::SE3 PWt, PCh;
-      PWt.q = hs::Quat{ot[0], ot[1], ot[2], ot[3]};
-      PWt.t[0] = ot[4]; PWt.t[1] = ot[5]; PWt.t[2] = ot[6];
-      PCh.q = hs::Quat{oh[7], oh[8], oh[9], oh[10]};
-      PCh.t[0] = oh[11]; PCh.t[1] = oh[12]; PCh.t[2] = oh[13];
-      // FrameFramePrecalc::set: PRE_RTll / PRE_tTll, K R Ki, K t (the affine mode and b0 are stored above)
-      const hs::SE3 l2l = se3_mul_step(PWt, PCh);
-      double R[9];
-      l2l.rotationMatrix(R);
-      float RT[9], tT[3];
-#pragma unroll
-      for (int i = 0; i < 9; i++) RT[i] = (float)R[i];
-#pragma unroll
-      for (int i = 0; i < 3; i++) tT[i] = (float)l2l.t[i];
-      float KR[9], KRKi[9], Kt[3];
-      hs::mm3f(pK, RT, KR);
-      hs::mm3f(KR, pKi, KRKi);
-      hs::mv3f(pK, tT, Kt);
-      HsPrecalc* pc = a.pre + tid;
-#pragma unroll
-      for (int i = 0; i < 9; i++) pc->KRKi[i] = KRKi[i];
-#pragma unroll
-      for (int i = 0; i < 3; i++) pc->Kt[i] = Kt[i];
+      pair_precalc_stage(fx + 16 * hh, fx + 16 * tt, exh, ext, sz7, vsf, a.pre[tid]);
     }
     if (fl) {  // frame fw: backupState, setState, setDeltaF's delta / delta_prior
       hs::FrameH& F = st->frames[fw];
@@ -2428,33 +2454,25 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
         F.delta_prior[q] = ns[q] - 0.0;
       }
     }
-    // the frames are final: wave 1 writes them back now, beside wave 0's pair stage, so their stores drain while the
-    // pair stage runs (the kernel's end waits for every store); the calib (wave 3) and canbreak (wave 2) run elsewhere
-    if (tid >= 64 && tid < 128) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      constexpr int F0 = (int)(offsetof(HsDevState, frames) / 8), FW1 = (int)(sizeof(hs::FrameH) / 8);
-      static_assert(sizeof(hs::FrameH) % 8 == 0, "frames are copied as 8-byte words");
-      const uint2* ls = reinterpret_cast<const uint2*>(st_raw);
-      uint2* gs = reinterpret_cast<uint2*>(a.st);
-      const int fwn = nF * FW1;  // the window's frames only (the solve touches no other slot)
-#pragma unroll 4
-      for (int i = tid - 64; i < fwn; i += 64) gs[F0 + i] = ls[F0 + i];
-    }
     if ((a.dbg & 16) && a.trace && tid == 0) a.trace[21] = clock64();
     HS_TRACE(a, 6);
     if (tid == 0) HS_TRACE(a, 10);
   }
   __syncthreads();
-  {  // write the window state back (after a step: all but the frames, written above)
-    constexpr int F0 = (int)(offsetof(HsDevState, frames) / 8), FW = (int)(sizeof(HsDevState::frames) / 8);
-    static_assert(offsetof(HsDevState, frames) % 8 == 0 && sizeof(HsDevState::frames) % 8 == 0, "word copies");
-    const bool skipF = (a.flags & HS_APPLY) != 0;
+  {  // write the window state back: every word by the whole workgroup (the window's frames; HS_MAXF slots beyond
+     // them are untouched by the solve and skipped)
+    constexpr int F0 = (int)(offsetof(HsDevState, frames) / 8), FW1 = (int)(sizeof(hs::FrameH) / 8);
+    constexpr int FW = (int)(sizeof(HsDevState::frames) / 8), SW = (int)(sizeof(HsDevState) / 8);
+    static_assert(offsetof(HsDevState, frames) % 8 == 0 && sizeof(hs::FrameH) % 8 == 0, "word copies");
+    const int fend = F0 + nF * FW1;
     const uint2* ls = reinterpret_cast<const uint2*>(st_raw);
     uint2* gs = reinterpret_cast<uint2*>(a.st);
-    for (int i = tid; i < (int)(sizeof(HsDevState) / 8); i += nt)
-      if (!skipF || i < F0 || i >= F0 + FW) gs[i] = ls[i];
+    constexpr int NU = (SW + SOLVE_NT - 1) / SOLVE_NT;
+#pragma unroll
+    for (int u = 0; u < NU; u++) {
+      const int i = tid + u * SOLVE_NT;
+      if (i < SW && (i < fend || i >= F0 + FW)) gs[i] = ls[i];
+    }
   }
   if (a.trace && threadIdx.x == 0) a.trace[25] = clock64();
   HS_TRACE(a, 15);
