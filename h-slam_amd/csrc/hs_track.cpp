@@ -102,7 +102,10 @@ static int upload_pyr(hs_tracker* t, float4** dst, const float* const* pyr) {
 }
 
 // the member workgroups' pass granules of n hypotheses: [n][2][HS_TRK_MAXG][HS_TRK_NRED][2] u64
-static size_t part_bytes(int n) { return sizeof(unsigned long long) * 2 * HS_TRK_MAXG * HS_TRK_NRED * 2 * (size_t)n; }
+constexpr int kTrkOneMemberPoints = 2048;  // hs_k_track: 512 threads x 4 points in flight
+static size_t meet_bytes(int n) { return sizeof(unsigned long long) * 2 * HS_TRK_MAXG * HS_TRK_NRED * 2 * (size_t)n; }
+// the pass meetings' granules, then the level-end records (hs_track_kernels.h: lvrec), zeroed together
+static size_t part_bytes(int n) { return meet_bytes(n) + sizeof(unsigned long long) * HS_TRK_MAXLVSEQ * 32 * (size_t)n; }
 // the timeout flags in front of the outputs, padded to 256 B
 static size_t cnt_bytes(int n) { return (sizeof(unsigned int) * (size_t)n + 255) & ~(size_t)255; }
 
@@ -202,6 +205,12 @@ static int run_tries(hs_tracker* t, int n, const double* h_in, int coarsest, int
   a.G = G;
   a.nhyp = n;
   a.part = t->d_part;
+  a.lvrec = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(t->d_part) + meet_bytes(t->try_cap));
+  // levels below one workgroup's batch of points run on one member (r05_trk1 at C2: level 4's 936 points, 8 passes:
+  // 0.232 -> 0.226 ms per track; a larger threshold, or fewer members at the finer levels, measured slower: the
+  // point loop outweighs the meeting there).  Env HS_TRK_GMIN, 0 = every level on all G members.
+  a.gmin = kTrkOneMemberPoints;
+  if (const char* e = std::getenv("HS_TRK_GMIN")) a.gmin = std::max(0, std::atoi(e));
   // zero-copy results (default; env HS_TRK_ZC=0: a read-back copy behind the kernel): the lead workgroups write
   // their records, and timed-out members their flags, into mapped pinned memory: no copy is queued behind the kernel
   // (r04_trk5: 0.260 against 0.270 ms per track).  Polling the launch's end event instead of the blocking

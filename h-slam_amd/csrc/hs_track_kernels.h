@@ -65,6 +65,11 @@ struct HsTrackArgs {
   // (pass + 1): the launch's epoch (1 .. 2^20 - 1, one per launch, the buffers zeroed when it wraps) keeps the
   // granules of earlier launches from matching, so no per-launch memset is needed
   int G, nhyp;
+  // per-level member count: a level with fewer than gmin reference points (one workgroup's batch: 512 threads x 4
+  // points) runs on member 0 alone, with no per-pass meeting, and member 0 hands the state to the other members once
+  // at the level's end (lvrec [n][HS_TRK_MAXLVSEQ][32] tagged granules, (epoch << 8) | (level sequence + 1))
+  int gmin;
+  unsigned long long* lvrec;
   unsigned int epoch;
   int solve;            // the LM step's 8x8 solve: 0 Gauss-Jordan on 64 lanes, 1 Eigen-order LDLT on 8 row lanes
   double* part;
@@ -73,6 +78,7 @@ struct HsTrackArgs {
 constexpr int HS_TRK_PASS_BITS = 12;  // passes per launch < 4096 (<= 5 levels x (50 + 1 + 6 cutoff repeats) x 2)
 constexpr int HS_TRK_NRED = 52;  // the reduced values of a pass (45 normal-equation entries, 4 energies / flows, 3 counts)
 constexpr int HS_TRK_MAXG = 16;
+constexpr int HS_TRK_MAXLVSEQ = 8;  // level ends per track (<= 5 levels + one repeated level)
 
 __global__ void hs_k_track(HsTrackArgs a);
 __global__ void hs_k_trk_scatter(int n, const float* cu, const float* cv, const float* cid, const float* hdi, int w,

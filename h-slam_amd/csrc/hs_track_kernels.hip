@@ -197,6 +197,8 @@ struct TrkShared {
   double incNorm;
   float lambda, cutoffRep;
   int brk[2];
+  int Gl;    // the level's members (trk_setup_part: 1 below a.gmin points, else a.G)
+  int lvseq;  // level ends so far (the level-end record's slot and tag)
   int dead;  // a member meeting timed out: the launch's results are void (the host reruns with G = 1), so every later
              // meeting is skipped and the LM / level loops end at once
   int passes;
@@ -256,7 +258,7 @@ __device__ __forceinline__ float wave_reduce_scatter64(const float (&v)[64], int
 // an LM iteration's pass) the accept test and, on accept, the new state and Hs / bs / resOld
 __device__ void trk_pass(const HsTrackArgs& a, TrkShared& S, int h, int g, bool lm = false) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int G = a.G, GT = G * TRK_NT;  // the hypothesis' workgroups take points g TRK_NT + tid (mod G TRK_NT)
+  const int G = S.Gl, GT = G * TRK_NT;  // the level's workgroups take points g TRK_NT + tid (mod G TRK_NT)
   const int lvl = S.lvl;
   const HsTrkLevel& L = a.lv[lvl];
   const int n = S.npts, wl = L.w, hl = L.h;
@@ -598,6 +600,7 @@ __device__ void trk_setup_part(const HsTrackArgs& a, TrkShared& S, const double 
     S.maxEnergy = 2 * a.huberTH * cutoff - a.huberTH * a.huberTH;
     S.lvl = lvl;
     S.npts = *a.lv[lvl].pc_n;
+    S.Gl = S.npts < a.gmin ? 1 : a.G;
     return;
   }
   const hs::SE3 T = hs::SE3::fromData(T7);
@@ -627,6 +630,58 @@ __device__ void trk_publish(const HsTrackArgs& a, TrkShared& S, int h, bool lead
 }
 
 }  // namespace
+
+// The end of a level that some members sat out (S.Gl < a.G): member 0 publishes the state the next level starts from
+// -- T, its normalized quaternion, aff, the pass count (the pass meetings' parity and tags), the cutoff repeat
+// factor (REPEAT LEVEL) and the LM iteration count -- as 32 tagged granules (two per value, as the pass meetings'
+// partials); the other members poll them (bounded by the wall clock, as the pass meetings) and take them over.
+__device__ void trk_level_meet(const HsTrackArgs& a, TrkShared& S, int h, int g) {
+  typedef unsigned long long u64;
+  __syncthreads();  // member 0: the level's last pass is in S
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x, q = lane >> 1;
+    u64* R = a.lvrec + ((size_t)h * HS_TRK_MAXLVSEQ + min(S.lvseq, HS_TRK_MAXLVSEQ - 1)) * 32;
+    const unsigned int tg = (a.epoch << 8) | (unsigned int)(S.lvseq + 1);
+    if (g == 0) {
+      if (lane < 32) {
+        const double v = q < 7 ? S.T[q] : q < 11 ? S.Tq[q - 7] : q < 13 ? S.aff[q - 11] : q == 13 ? (double)S.npass
+                         : q == 14 ? (double)S.cutoffRep : (double)S.iters;
+        const u64 bits = (u64)__double_as_longlong(v);
+        __hip_atomic_store(R + lane, ((u64)tg << 32) | ((lane & 1) ? (bits >> 32) : (bits & 0xffffffffull)),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    } else if (g >= S.Gl) {  // (the level's other members hold the same state already)
+      const unsigned long long t_end = wall_clock64() + (S.dead ? 0ull : (unsigned long long)a.spin_limit);
+      u64 w = 0;
+      for (;;) {
+        w = __hip_atomic_load(R + min(lane, 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__all((unsigned int)(w >> 32) == tg)) break;
+        __builtin_amdgcn_s_sleep(1);
+        if (wall_clock64() >= t_end) {
+          if (lane == 0) {
+            __hip_atomic_store(a.cnt + h, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            S.dead = 1;
+          }
+          break;
+        }
+      }
+      // lane 2 q + 1 holds value q's high half: pair it with the low half of lane 2 q
+      const unsigned int lo = (unsigned int)(w & 0xffffffffull);
+      const unsigned int hi = (unsigned int)__shfl_down((int)lo, 1);
+      const double v = __longlong_as_double((long long)(((u64)hi << 32) | lo));
+      if (!S.dead && lane < 32 && !(lane & 1)) {
+        if (q < 7) S.T[q] = v;
+        else if (q < 11) S.Tq[q - 7] = v;
+        else if (q < 13) S.aff[q - 11] = v;
+        else if (q == 13) S.npass = (int)v;
+        else if (q == 14) S.cutoffRep = (float)v;
+        else S.iters = (int)v;
+      }
+    }
+  }
+  if (threadIdx.x == 0) S.lvseq += 1;
+  __syncthreads();
+}
 
 __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
   __shared__ TrkShared S;
@@ -669,6 +724,7 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
     S.aff[0] = a.n_inl ? a.inl[7 * a.n_inl + 2 * h + 0] : a.aff_in[2 * h + 0];
     S.aff[1] = a.n_inl ? a.inl[7 * a.n_inl + 2 * h + 1] : a.aff_in[2 * h + 1];
     S.nchecks = 0;
+    S.lvseq = 0;
     S.dead = 0;
     S.iters = 0;
     S.npass = 0;
@@ -684,6 +740,8 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
       trk_setup(a, S, S.T, S.aff, lvl, a.coarseCutoffTH * S.cutoffRep);
     }
     __syncthreads();
+    const bool active = g < S.Gl;  // uniform: the level's members
+    if (active) {
     trk_pass(a, S, h, g);
     while (S.res[5] > 0.6 && S.cutoffRep < 50 && !S.dead) {  // uniform: S.res / S.cutoffRep are shared
       __syncthreads();
@@ -800,6 +858,8 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
       }
       S.nchecks = c < HS_TRK_MAXCHECK ? c + 1 : c;
     }
+    }  // active
+    if (S.Gl < a.G) trk_level_meet(a, S, h, g);  // the members that sat the level out take member 0's state
     const bool rep = S.cutoffRep > 1 && !haveRepeated;
     __syncthreads();
     if (rep) {  // REPEAT LEVEL
