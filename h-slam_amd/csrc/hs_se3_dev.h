@@ -22,23 +22,37 @@ __device__ __forceinline__ double rsqrt_step(double x) {
 // root.  Larger tangents take the reference formulas.  Differs from Sophus by rounding only.
 // the two halves of the series form (u = |w|^2 < 1e-2), so a caller can run them on different waves: the unit
 // quaternion, and the translation V a
+// An fp64 constant materialized where it is used (two v_mov_b32 the compiler may not hoist): kernels with long
+// loops around the step (the tracker's LM loop) otherwise keep the series coefficients live across the loop in
+// registers, and at 256 VGPRs spill them to scratch.
+template <unsigned long long B>
+__device__ __forceinline__ double kd() {
+  unsigned int lo, hi;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(lo) : "i"((unsigned int)(B & 0xffffffffull)));
+  asm volatile("v_mov_b32 %0, %1" : "=v"(hi) : "i"((unsigned int)(B >> 32)));
+  return __hiloint2double((int)hi, (int)lo);
+}
+#define HS_KD(x) kd<__builtin_bit_cast(unsigned long long, (double)(x))>()
+
 __device__ __forceinline__ double se3_step_poly(double u, double c0, double c1, double c2, double c3, double c4,
                                                 double c5) {
   return __builtin_fma(__builtin_fma(__builtin_fma(__builtin_fma(__builtin_fma(c5, u, c4), u, c3), u, c2), u, c1), u,
                        c0);
 }
 __device__ __forceinline__ hs::Quat se3_exp_step_q(const double a[6], double u) {
-  const double imag = se3_step_poly(u, 1.0 / 2, -1.0 / 48, 1.0 / 3840, -1.0 / 645120, 1.0 / 185794560,
-                                    -1.0 / 81749606400.0);
-  const double real = se3_step_poly(u, 1.0, -1.0 / 8, 1.0 / 384, -1.0 / 46080, 1.0 / 10321920, -1.0 / 3715891200.0);
+  const double imag = se3_step_poly(u, 1.0 / 2, HS_KD(-1.0 / 48), HS_KD(1.0 / 3840), HS_KD(-1.0 / 645120),
+                                    HS_KD(1.0 / 185794560), HS_KD(-1.0 / 81749606400.0));
+  const double real = se3_step_poly(u, 1.0, HS_KD(-1.0 / 8), HS_KD(1.0 / 384), HS_KD(-1.0 / 46080),
+                                    HS_KD(1.0 / 10321920), HS_KD(-1.0 / 3715891200.0));
   const double qx = imag * a[3], qy = imag * a[4], qz = imag * a[5];
   const double inv = rsqrt_step(qx * qx + qy * qy + qz * qz + real * real);
   return hs::Quat{qx * inv, qy * inv, qz * inv, real * inv};
 }
 __device__ __forceinline__ void se3_exp_step_t(const double a[6], double u, double t[3]) {
-  const double c1 = se3_step_poly(u, 1.0 / 2, -1.0 / 24, 1.0 / 720, -1.0 / 40320, 1.0 / 3628800, -1.0 / 479001600);
-  const double c2 = se3_step_poly(u, 1.0 / 6, -1.0 / 120, 1.0 / 5040, -1.0 / 362880, 1.0 / 39916800,
-                                  -1.0 / 6227020800.0);
+  const double c1 = se3_step_poly(u, 1.0 / 2, HS_KD(-1.0 / 24), HS_KD(1.0 / 720), HS_KD(-1.0 / 40320),
+                                  HS_KD(1.0 / 3628800), HS_KD(-1.0 / 479001600));
+  const double c2 = se3_step_poly(u, HS_KD(1.0 / 6), HS_KD(-1.0 / 120), HS_KD(1.0 / 5040), HS_KD(-1.0 / 362880),
+                                  HS_KD(1.0 / 39916800), HS_KD(-1.0 / 6227020800.0));
   double O[9], O2[9], V[9];
   hs::SE3::hat3(a + 3, O);
   hs::SE3::mm3(O, O, O2);
