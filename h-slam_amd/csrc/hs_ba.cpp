@@ -201,7 +201,7 @@ int ensure_capacity(hs_ctx* c, int W, int H, int capP, int capBlk) {
   if (c->tracing) {
     HS_TRY(dalloc(&c->d_tr_lin, (size_t)capBlk * 16));
     HS_TRY(dalloc(&c->d_tr_acc, (size_t)(HS_MAXF * ((ne * 64 + 255) / 256) + 1 + 64) * 16));
-    HS_TRY(dalloc(&c->d_tr_st, (size_t)(HS_MAXF * (HS_MAXF + 1) / 2 + 2 * HS_MAXF + 2) * 16));
+    HS_TRY(dalloc(&c->d_tr_st, (size_t)(HS_MAXF * (HS_MAXF + 1) / 2 + 2 * HS_MAXF + 2 + 64) * 16));  // + np2 <= 64
     HS_TRY(dalloc(&c->d_tr_solve, 32));
   }
   c->cap_W = W; c->cap_H = H; c->cap_P = capP; c->cap_blk = capBlk;
@@ -352,7 +352,8 @@ int make_partition(hs_ctx* c) {
   // points per block: hs_k_lin HS_LIN_NW waves x ppw points; hs_k_lin8 4 waves x ppw groups of 8 points (its
   // partition also serves hs_k_lin's marginalization / linearizeAll(true) passes, with W = 4 of its waves)
   const int bw = c->lin8 ? (HS_LIN8_NT / 64) * 8 : HS_LIN_NW;
-  const int target = c->lin8 ? kLin8BlocksTarget : kLinBlocksTarget;
+  int target = c->lin8 ? kLin8BlocksTarget : kLinBlocksTarget;
+  if (const char* e = std::getenv("HS_LIN8_BLOCKS"); e && c->lin8) target = std::max(1, std::atoi(e));
   int ppw = std::max(1, (nP + bw * target - 1) / (bw * target));
   if (const char* e = std::getenv("HS_LIN_PPW")) ppw = std::max(1, std::atoi(e));
   c->W = c->exact ? 1 : (c->lin8 ? HS_LIN8_NT / 64 : HS_LIN_NW);
@@ -661,7 +662,7 @@ static int set_loop_counters(hs_ctx* c, int iteration, bool via_solve = false) {
 // per-kernel checkpoint summary of the last traced launch (stderr): for every checkpoint the
 // min / median / max over blocks of (checkpoint - the block's start) and the launch span, in us
 static int dump_one(const char* name, const long long* d, int nblocks, double tick_us, hipStream_t s,
-                    long long* first = nullptr, long long* last = nullptr) {
+                    long long* first = nullptr, long long* last = nullptr, const std::vector<int>* groups = nullptr) {
   const bool solve = std::string(name) == "solve";
   std::vector<long long> h(solve ? 32 : (size_t)nblocks * 16);  // the solve row has 32 slots (16..25: probes)
   HS_HIP(hipMemcpyAsync(h.data(), d, sizeof(long long) * h.size(), hipMemcpyDeviceToHost, s));
@@ -686,6 +687,21 @@ static int dump_one(const char* name, const long long* d, int nblocks, double ti
                      h[b * 16 + 1] ? (h[b * 16 + 1] - t0) * tick_us : -1.0, h[b * 16 + 2] ? (h[b * 16 + 2] - t0) * tick_us : -1.0,
                      (h[b * 16 + 15] - t0) * tick_us);
     std::fprintf(stderr, "\n");
+  }
+  if (groups && groups->size() > 1) {  // per block group (the linearize launch: per host): start and cp1 spread
+    for (size_t gi = 0; gi + 1 < groups->size(); gi++) {
+      std::vector<double> st, e1;
+      for (int b = (*groups)[gi]; b < (*groups)[gi + 1]; b++)
+        if (h[b * 16] && h[b * 16 + 1]) {
+          st.push_back((h[b * 16] - t0) * tick_us);
+          e1.push_back((h[b * 16 + 1] - t0) * tick_us);
+        }
+      if (st.empty()) continue;
+      std::sort(st.begin(), st.end());
+      std::sort(e1.begin(), e1.end());
+      std::fprintf(stderr, "[hs trace] %-12s group %zu: %zu blocks, start %.1f..%.1f, cp1 end min %.1f med %.1f max %.1f us\n",
+                   name, gi, st.size(), st.front(), st.back(), e1.front(), e1[e1.size() / 2], e1.back());
+    }
   }
   for (int k = 1; k < 16; k++) {
     std::vector<double> v;
@@ -713,7 +729,7 @@ static int dump_traces(hs_ctx* c) {
       if (k < 24 || k > 25) std::fprintf(stderr, " s%d=%lld", k, h[k] ? h[k] - h[16] : -1);
     std::fprintf(stderr, "\n");
   }
-  HS_TRY(dump_one("linearize", c->d_tr_lin, c->nblk, tick_us, c->stream, &f[1], &l[1]));
+  HS_TRY(dump_one("linearize", c->d_tr_lin, c->nblk, tick_us, c->stream, &f[1], &l[1], &c->blk_begin));
   HS_TRY(dump_one("reduce", c->d_tr_acc, c->nF * c->Q + 1, tick_us, c->stream, &f[2], &l[2]));
   HS_TRY(dump_one("stitch", c->d_tr_st, c->nF + c->nF * (c->nF + 1) / 2 + c->nF + 2, tick_us, c->stream, &f[3],
                   &l[3]));
@@ -1906,6 +1922,24 @@ extern "C" int hs_debug_se3(int on_device, int op, int n, const double* in14, do
   HS_HIP(hipMemcpy(out36, d_out, sizeof(double) * 36 * n, hipMemcpyDeviceToHost));
   (void)hipFree(d_in);
   (void)hipFree(d_out);
+  return HS_OK;
+}
+
+// test hook (not in the header): hs_k_lin8's range-step-free quotient / square root beside the IEEE ones, out [n][4]
+extern "C" int hs_debug_fastmath(int n, const float* a, const float* b, float* out4) {
+  if (n < 1 || !a || !b || !out4) return fail(HS_ERR_INVALID, "bad arguments");
+  float *d_a = nullptr, *d_b = nullptr, *d_o = nullptr;
+  HS_TRY(dalloc(&d_a, (size_t)n));
+  HS_TRY(dalloc(&d_b, (size_t)n));
+  HS_TRY(dalloc(&d_o, (size_t)4 * n));
+  HS_HIP(hipMemcpy(d_a, a, sizeof(float) * n, hipMemcpyHostToDevice));
+  HS_HIP(hipMemcpy(d_b, b, sizeof(float) * n, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(hs_k_debug_fastmath, dim3((n + 255) / 256), dim3(256), 0, 0, n, d_a, d_b, d_o);
+  HS_HIP(hipGetLastError());
+  HS_HIP(hipMemcpy(out4, d_o, sizeof(float) * 4 * n, hipMemcpyDeviceToHost));
+  (void)hipFree(d_a);
+  (void)hipFree(d_b);
+  (void)hipFree(d_o);
   return HS_OK;
 }
 

@@ -53,7 +53,7 @@ constexpr int kLinBlocksTarget = 256;  // linearize blocks of a window (points p
 // 10k 30.2 vs 25.7, 20k 53.8 vs 43.6 (hs_k_lin vs hs_k_lin8).  Env HS_LIN8=0 / 1 forces either.
 constexpr int kLin8MinPoints = 4000;
 constexpr int kThMultiMinPoints = 60000;  // the multi-block threshold select (below: one block beside the solve)
-constexpr int kLin8BlocksTarget = 512;  // hs_k_lin8 blocks of a window (two 4-wave blocks per CU)
+constexpr int kLin8BlocksTarget = 256;  // hs_k_lin8 blocks of a window (one 8-wave block per CU)
 
 template <typename T>
 inline int dalloc(T** p, size_t n) {

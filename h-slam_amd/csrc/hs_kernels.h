@@ -11,7 +11,10 @@ constexpr int HS_SOLVE_NT = 512;   // hs_k_solve workgroup size
 constexpr int HS_STITCH_NT = 1024; // hs_k_stitch workgroup size
 constexpr int HS_LIN_NW = 8;       // hs_k_lin waves per block (production: each takes points; exact mode: wave 0)
 constexpr int HS_LIN_NT = 64 * HS_LIN_NW;
-constexpr int HS_LIN8_NT = 256;    // hs_k_lin8 workgroup size (4 waves, 8 points per wave at a time)
+#ifndef HS_LIN8_WAVES
+#define HS_LIN8_WAVES 8  // one workgroup per CU (its LDS): waves wv and wv + 4 share a SIMD (hs_k_lin8's L8_PRIO)
+#endif
+constexpr int HS_LIN8_NT = 64 * HS_LIN8_WAVES;  // hs_k_lin8 workgroup size (8 points per wave at a time)
 constexpr int HS_NNS = 7;         // gauge nullspaces: 6 pose + 1 scale (System::getNullspaces)
 
 // Window state owned by the device between GN iterations (updated by hs_k_solve).
@@ -236,6 +239,7 @@ __global__ void hs_k_result(const double* elog, int k, const double* sysE, HsDev
                             int done_slot);   // multi-rank: the gathered systems summed into sys_out (+ block 1: select)
 __global__ void hs_k_resub(HsResubArgs a);
 __global__ void hs_k_debug_se3(int op, int n, const double* in, double* out);  // test hook
+__global__ void hs_k_debug_fastmath(int n, const float* a, const float* b, float* out);  // test hook (hs_lin8)
 __global__ void hs_k_apply_step(int n, const float* step, float* idepth, float* idepth_zero);
 // System::optimize's tail, frame part (Src/FullSystemOptimize.cpp:498-506) on the device: the newest frame's
 // setEvalPT(PRE_worldToCam, (0,..,0, a, b, 0, 0)) + takeData, then setAdjointsF + setPrecalcValues of every pair (one

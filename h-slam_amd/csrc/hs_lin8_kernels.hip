@@ -41,6 +41,18 @@ constexpr int Q8_N = 17;  // per-pixel quantities summed over the pattern
 #ifndef L8_PREFETCH
 #define L8_PREFETCH 0   // 1: the next point group's inputs are loaded while the current group computes (occupancy 1)
 #endif
+#ifndef L8_FAST_OPS
+#define L8_FAST_OPS 7   // div_nr / sqrt_nr for: 1 the projection quotients, 2 the gradient weight, 4 the Huber weight
+#endif
+// Issue priority.  The two waves sharing a SIMD are VALU-bound together; with equal priority the arbiter's
+// oldest-first rule runs the older one ahead and leaves the younger alone on the SIMD at the end.  4 (production):
+// the pair takes turns, priority 1 on alternate groups.  Measured (r05_l6 / r05_l8, per launch, HBM roofline
+// fraction): 2M points 0.516 (4-wave blocks, no priority) -> 0.560 (8-wave blocks + turns); 200k 0.387 -> 0.378 ..
+// 0.388 (VALU-bound either way: the turns equalise the waves' end times, not the SIMD's work).
+// 0: none; 1: alternate per group (all waves in phase); 2: a wave ahead of the block's slowest yields.
+#ifndef L8_PRIO
+#define L8_PRIO 4
+#endif
 #ifndef L8_LDS_ACC
 #define L8_LDS_ACC 1    // the per-lane accumulators (T slice, accD / accE / accEB / accHcc) live in LDS between groups
 #endif
@@ -106,6 +118,31 @@ __device__ __forceinline__ int owner_map(int e, int k) {
   if (e < 14) return TR0 + k * 3 + (e - 11);             // TopRight (k, a | b | r)
   if (e == 14) return k < 6 ? TR0 + (8 + k / 3) * 3 + k % 3 : -1;  // TopRight (8 + k/3, k%3)
   return k < 6 ? BR0 + k : -1;                           // BotRight[k]
+}
+
+// fp32 quotient and square root as the compiler's correctly rounded expansions WITHOUT their range steps
+// (v_div_scale's operand scaling, v_div_fmas's rescale, v_div_fixup; sqrt's 2^32 pre-scale, its 2^-16 unscale and
+// class fix-up).  Where those steps are identities the results are bit-identical to a / b and sqrtf(x)
+// (tests/test_gpu_lin8.py::test_fast_div_sqrt_match_ieee sweeps the ranges):
+//   div_nr(a, b, rcp_nr(b)) == a / b   for |b| in [2^-60, 2^60], |a| >= 2^-60 and |a / b| in [2^-90, 2^90];
+//   sqrt_nr(x) == sqrtf(x)             for x >= 2^-96 (and 0).
+// The pixel loop (9 + 8 VALU per quotient pair / further quotient and 9 per root instead of 22 / 11 / 16) flags a
+// lane whose operands may leave those ranges; its wave then redoes the group with a / b and sqrtf.
+__device__ __forceinline__ float rcp_nr(float b) {
+  const float r = __builtin_amdgcn_rcpf(b);
+  return __builtin_fmaf(__builtin_fmaf(-b, r, 1.0f), r, r);
+}
+__device__ __forceinline__ float div_nr(float a, float b, float r) {
+  float q = a * r;
+  q = __builtin_fmaf(__builtin_fmaf(-b, q, a), r, q);
+  return __builtin_fmaf(__builtin_fmaf(-b, q, a), r, q);
+}
+__device__ __forceinline__ float sqrt_nr(float x) {
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const float sm = __int_as_float(__float_as_int(s) - 1), sp = __int_as_float(__float_as_int(s) + 1);
+  const float rm = __builtin_fmaf(-sm, s, x), rp = __builtin_fmaf(-sp, s, x);
+  const float o = rm <= 0.f ? sm : s;
+  return rp > 0.f ? sp : o;
 }
 
 __device__ __forceinline__ float dpp_ror8(float v) {  // lane l <- lane l ^ 8 (rotate a row of 16 by 8)
@@ -262,6 +299,9 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
 
   const HsCalib cal = a.st->dcal;
   const HsLinParams lp = a.lp;
+  // div_nr / sqrt_nr in the pixel loop: the two thresholds bound its quotients' and roots' ranges (uniform)
+  const bool fast_ok = lp.outlierTHSumComponent >= 0x1p-30f && lp.outlierTHSumComponent <= 0x1p30f &&
+                       lp.huberTH >= 0x1p-30f && lp.huberTH <= 0x1p30f;
   const int tc = t < nF ? t : 0;
   const float4* timg = a.img + (long long)hs_img_slot(a.img_slot, tc) * a.img_stride;  // past the window: frame 0
   L8Scratch& W = U.s[wv];
@@ -294,7 +334,30 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
 #if L8_PREFETCH
   if (wv < ngroups) l8_load(a, clamp_p(wv), t, nx);
 #endif
+#if L8_PRIO == 2
+  __shared__ int l8_prog[L8_NW];
+  if (lane == 0) l8_prog[wv] = 0;
+  __syncthreads();
+#endif
   for (int gi = wv; gi < ngroups; gi += a.W) {  // wave-uniform
+#if L8_PRIO == 1
+    if (((gi - wv) / a.W) & 1) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+#elif L8_PRIO == 4
+    // the two waves sharing a SIMD (wv, wv + 4: workgroup waves go round-robin over the 4 SIMDs) take turns
+    if ((((gi - wv) / a.W) + (wv >> 2)) & 1) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+#elif L8_PRIO == 2
+    {  // the block's waves progress together: a wave ahead of the slowest one yields its issue priority
+      const int k = (gi - wv) / a.W;
+      if (lane == 0) l8_prog[wv] = k;
+      int mn = k;
+#pragma unroll
+      for (int w = 0; w < L8_NW; w++) mn = min(mn, l8_prog[w]);
+      if (__builtin_amdgcn_readfirstlane(mn) < k) __builtin_amdgcn_s_setprio(0);
+      else __builtin_amdgcn_s_setprio(2);
+    }
+#endif
 #if L8_PREFETCH
     const L8In in = nx;
     if (gi + a.W < ngroups) l8_load(a, clamp_p(gi + a.W), t, nx);  // in flight during this group's work
@@ -431,9 +494,16 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
     //      are the reference's pattern-order sums; a failing pixel (the reference's early exit) marks the slot OOB
     //      and its (redirected, finite) values are never read
     float S[Q8_N];
+    bool slotOob = false;
+    // FAST: quotients / square roots by div_nr / sqrt_nr, `bad` set where an operand may leave their exact range
+    // range guards of the FAST forms as integer max / min over the pattern of the operands' magnitude bits (NaN
+    // sorts above +inf): |q2| | the gradient-weight divisor | |residual|
+    unsigned gq2max = 0u, gq2min = 0xffffffffu, gwmax = 0u, grmax = 0u;
+    auto pixels = [&](auto fast_tag) {
+    constexpr bool FAST = decltype(fast_tag)::value;
 #pragma unroll
     for (int i = 0; i < Q8_N; i++) S[i] = 0.f;
-    bool slotOob = false;
+    slotOob = false;
 #pragma unroll
     for (int k = 0; k < 8; k++) {
       constexpr int PDX[8] = {0, -1, 1, -2, 0, 2, -1, 0};
@@ -445,7 +515,21 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
       q0 = q0 + pcr.Kt[0] * idep;
       q1 = q1 + pcr.Kt[1] * idep;
       q2 = q2 + pcr.Kt[2] * idep;
-      const float PKu = q0 / q2, PKv = q1 / q2;
+      float PKu, PKv;
+      if constexpr (FAST && (L8_FAST_OPS & 1)) {
+        // |q2| in range: every in-bounds quotient is exact (out of bounds it stays out of bounds, or NaN)
+        const unsigned aq2 = __float_as_uint(fabsf(q2));
+        gq2max = max(gq2max, aq2);
+        gq2min = min(gq2min, aq2);
+        const float r2 = rcp_nr(q2);
+        PKu = div_nr(q0, q2, r2);
+        PKv = div_nr(q1, q2, r2);
+      } else {
+        PKu = q0 / q2;
+        PKv = q1 / q2;
+      }
+      // (the short-circuit form is a branch region per pixel, which keeps the scheduler from hoisting every pixel's
+      // taps at once: the bitwise form spills)
       const bool okP = okC && (PKu > 1.1f && PKv > 1.1f && PKu < (cal.W - 3) && PKv < (cal.H - 3));
       const float3 hit = interp33_8(timg, okP ? PKu : 2.f, okP ? PKv : 2.f, cal.W);
       const float color = colK[k];
@@ -453,12 +537,30 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
       const float drdA = (color - pcr.b0);
       const bool okI = okP && isfinite(hit.x);
       slotOob = slotOob || (live0 && !okI);
-      float w = sqrtf(lp.outlierTHSumComponent / (lp.outlierTHSumComponent + (hit.y * hit.y + hit.z * hit.z)));
+      const float wden = lp.outlierTHSumComponent + (hit.y * hit.y + hit.z * hit.z);
+      float w, hw;
+      // the uniform thresholds are in [2^-30, 2^30] (checked by the caller): wden <= 2^60 and |residual| <= 2^60
+      // keep both quotients and both square-root arguments in range (NaN operands fail the tests)
+      if constexpr (FAST && (L8_FAST_OPS & 2)) {
+        gwmax = max(gwmax, __float_as_uint(wden));  // wden >= 0 (or NaN)
+        w = sqrt_nr(div_nr(lp.outlierTHSumComponent, wden, rcp_nr(wden)));
+      } else {
+        w = sqrtf(lp.outlierTHSumComponent / wden);
+      }
+      if constexpr (FAST && (L8_FAST_OPS & 4)) {
+        grmax = max(grmax, __float_as_uint(fabsf(residual)));
+        // == (|residual| < huberTH ? 1 : huberTH / |residual|): below the threshold the quotient rounds to >= 1 (or
+        // is NaN for a zero / denormal divisor), and min returns 1 then; a NaN residual is flagged.  No select, so
+        // the compiler keeps the quotient unconditional instead of branching around it
+        hw = fminf(1.0f, div_nr(lp.huberTH, fabsf(residual), rcp_nr(fabsf(residual))));
+      } else {
+        hw = fabsf(residual) < lp.huberTH ? 1 : lp.huberTH / fabsf(residual);
+      }
       w = 0.5f * (w + wgtK[k]);
-      float hw = fabsf(residual) < lp.huberTH ? 1 : lp.huberTH / fabsf(residual);
       float qv[Q8_N];
       qv[0] = w * w * hw * residual * residual * (2 - hw);
-      hw = hw < 1 ? sqrtf(hw) : hw;
+      if constexpr (FAST && (L8_FAST_OPS & 4)) hw = sqrt_nr(hw);  // hw <= 1 and sqrt(1) == 1: == (hw < 1 ? sqrt(hw) : hw)
+      else hw = hw < 1 ? sqrtf(hw) : hw;
       hw = hw * w;
       const float hy = hit.y * hw, hz = hit.z * hw;
       const float resF = residual * hw;
@@ -488,6 +590,13 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
       // the taps of at most L8_TAP_GROUP pixels in flight per wave (register budget of two waves per SIMD: the
       // other wave hides the gather latency the compiler's full hoisting hid at one wave per SIMD)
       if (L8_TAP_GROUP < 8 && (k + 1) % L8_TAP_GROUP == 0) __builtin_amdgcn_sched_barrier(0);
+    }
+    };
+    {
+      if (fast_ok) pixels(std::true_type{});
+      constexpr unsigned LOb = 0x21800000u, HIb = 0x5d800000u;  // 2^-60, 2^60
+      const bool bad = !fast_ok || gq2max > HIb || gq2min < LOb || gwmax > HIb || grmax > HIb;
+      if (__builtin_expect(__ballot(bad) != 0ull, 0)) pixels(std::false_type{});  // rare: the wave redoes the group
     }
 
     // ---- state decision + applyRes (Src/OptimizationClasses.cpp:128-133,235-256)
@@ -695,6 +804,10 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
     __builtin_amdgcn_wave_barrier();  // the scratch is rewritten by the next group
   }
   if (a.trace && tid == 0) a.trace[(size_t)b * 16 + 1] = wall_clock64();
+  if (a.trace && lane == 0 && wv < 8) a.trace[(size_t)b * 16 + 3 + wv] = wall_clock64();  // each wave's loop end
+#if L8_PRIO
+  __builtin_amdgcn_s_setprio(0);
+#endif
   if (!a.accumulate) return;
 
   // ---- epilogue: the block partial in hs_k_lin's production layout (T entries from their owner lanes), waves in
@@ -768,4 +881,13 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
     a.part_e[(size_t)b * 4 + tid] = s;
   }
   if (a.trace && tid == 0) a.trace[(size_t)b * 16 + 2] = wall_clock64();
+}
+
+// test hook (hs_debug_fastmath): out[i] = {div_nr(a, b, rcp_nr(b)), a / b, sqrt_nr(a), sqrtf(a)}
+__global__ void hs_k_debug_fastmath(int n, const float* a, const float* b, float* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float x = a[i], y = b[i];
+  const float4 r = make_float4(div_nr(x, y, rcp_nr(y)), x / y, sqrt_nr(x), sqrtf(x));
+  reinterpret_cast<float4*>(out)[i] = r;
 }

@@ -136,3 +136,71 @@ def test_multi_block_select_matches_in_stitch_select(scene2k):
         g.close()
     for a, b in zip(*outs):
         assert np.array_equal(a, b)
+
+
+def _fastmath(a, b):
+    import ctypes as C
+    from hslam_amd import _lib
+    lib = _lib.load()
+    fn = lib.hs_debug_fastmath
+    fn.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+    fn.restype = C.c_int
+    a = np.ascontiguousarray(a, np.float32)
+    b = np.ascontiguousarray(b, np.float32)
+    out = np.zeros((len(a), 4), np.float32)
+    assert fn(len(a), a.ctypes.data, b.ctypes.data, out.ctypes.data) == 0
+    return out
+
+
+def test_fast_div_sqrt_match_ieee():
+    """hs_k_lin8's range-step-free quotient / square root (div_nr, sqrt_nr) against the device's IEEE a / b and
+    sqrtf, bitwise, over the ranges the pixel loop admits (log-uniform magnitudes, random signs, plus the range ends
+    and exact cases); the IEEE forms against numpy's correctly rounded float32 results."""
+    rng = np.random.default_rng(3)
+    n = 1 << 21
+    lb = rng.uniform(-60, 60, n)
+    lq = rng.uniform(-90, 90, n)
+    lq = np.clip(lq, -60 - lb, 127.9 - lb)  # |a| = |q| |b| in [2^-60, 2^127.9] (finite)
+    sgn = lambda: rng.choice([-1.0, 1.0], n)  # noqa: E731
+    b = (sgn() * np.exp2(lb)).astype(np.float32)
+    a = (sgn() * np.exp2(lq) * b.astype(np.float64)).astype(np.float32)
+    ends = np.array([2.0 ** -60, 2.0 ** 60, 1.0, 3.0, 0.1, 2500.0, 9.0, 2.0 ** 59.5], np.float32)
+    ea, eb = np.meshgrid(ends, ends)
+    a = np.concatenate([a, ea.ravel(), -ea.ravel(), np.zeros(4, np.float32)])
+    b = np.concatenate([b, eb.ravel(), eb.ravel(), np.array([1, -1, 2.0 ** -60, 2.0 ** 60], np.float32)])
+    out = _fastmath(a, b)
+    bad = out[:, 0].view(np.uint32) != out[:, 1].view(np.uint32)
+    assert not bad.any(), (a[bad][:5], b[bad][:5], out[bad][:5])
+    assert np.array_equal(out[:, 1], a / b)
+    ls = rng.uniform(-96, 127.9, n)
+    x = np.concatenate([np.exp2(ls), [0.0, 1.0, 2.0 ** -96, 4.0, 2.0, 0.25]]).astype(np.float32)
+    out = _fastmath(x, np.ones_like(x))
+    assert np.array_equal(out[:, 2].view(np.uint32), out[:, 3].view(np.uint32))
+    assert np.array_equal(out[:, 3], np.sqrt(x))
+
+
+def test_lin8_out_of_range_group_falls_back(scene2k):
+    """Texels whose gradients put the pixel loop's operands outside div_nr / sqrt_nr's exact ranges (|grad|^2 above
+    2^60, infinite gradients): the affected point groups are redone with IEEE a / b and sqrtf, so the per-residual
+    outputs stay bit-identical to hs_k_lin's and the oracle's."""
+    import copy
+
+    from oracle_ffi import OracleBA
+    scene = copy.deepcopy(scene2k)
+    for f, val in ((1, 3e18), (2, np.inf), (3, 1e30)):
+        img = scene.pyramids[f][0]
+        h, w = img.shape[:2]
+        img[h // 4: h // 2, w // 4: w // 2, 1:3] = val
+    g8, g1 = _window(scene, True), _window(scene, False)
+    o = OracleBA(scene)
+    g8.linearizeAll(reset=True)
+    g1.linearizeAll(reset=True)
+    o.linearize_all(reset=True)
+    o.apply_res()
+    r8, r1, ro = g8.residuals(), g1.residuals(), o.residuals()
+    for k in r8:
+        assert np.array_equal(r8[k], r1[k], equal_nan=True), k
+    assert np.array_equal(r8["state"], ro["state"])
+    assert np.array_equal(r8["energy"], ro["energy"].astype(np.float32), equal_nan=True)
+    g8.close()
+    g1.close()

@@ -1,0 +1,18 @@
+import sys, numpy as np
+sys.path.insert(0, 'h-slam_amd')
+from hslam_amd.scene import make_ba_scene
+from hslam_amd.ba import BAWindow
+s = make_ba_scene(n_points=200000)
+g = BAWindow(s)
+g.linearizeAll(reset=True)
+for it in range(3):
+    r = g.residuals()
+    act = r['active'].astype(bool) if 'active' in r else None
+    st = r['state']
+    h = s.pt_host[s.res_point]
+    pa = np.zeros(s.n_points, bool)
+    np.logical_or.at(pa, s.res_point, act)
+    print('iter', it, 'active res per host', [int(act[h == f].sum()) for f in range(s.n_frames)],
+          'active pts', [int(pa[s.pt_host == f].sum()) for f in range(s.n_frames)],
+          'IN', [int((st[h == f] == 0).sum()) for f in range(s.n_frames)])
+    g.iterate(0, 1)
