@@ -53,6 +53,12 @@ constexpr int Q8_N = 17;  // per-pixel quantities summed over the pattern
 #ifndef L8_PRIO
 #define L8_PRIO 4
 #endif
+#ifndef L8_BOUNDS_BITS
+#define L8_BOUNDS_BITS 1  // the pixel bounds test on float bits (one unsigned range compare per coordinate)
+#endif
+#ifndef L8_BUFFER_TAPS
+#define L8_BUFFER_TAPS 1  // the pixel taps as buffer loads with 32-bit offsets (interp33_8b)
+#endif
 #ifndef L8_LDS_ACC
 #define L8_LDS_ACC 1    // the per-lane accumulators (T slice, accD / accE / accEB / accHcc) live in LDS between groups
 #endif
@@ -61,7 +67,27 @@ constexpr int Q8_N = 17;  // per-pixel quantities summed over the pattern
 __host__ __device__ constexpr int didx(int r, int c) { return r * 10 - (r * (r - 1)) / 2 + (c - r); }
 constexpr int TR0 = 55, BR0 = 85;
 
-// getInterpolatedElement33 (Include/GlobalTypes.h:377-388) on float4 texels
+// getInterpolatedElement33 (Include/GlobalTypes.h:377-388) on float4 texels, through one buffer resource over every
+// frame's image: 32-bit texel offsets (one 24-bit multiply-add and one shift-add per pixel instead of 64-bit address
+// arithmetic), the next row by the scalar offset, the x + 1 texel by the instruction offset; dx = fract(x), which is
+// x - (int)x exactly for the non-negative coordinates the caller passes
+__device__ __forceinline__ float3 ld_texel3(__amdgpu_buffer_rsrc_t r, int vo, int so) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b96(r, vo, so, 0);
+  return make_float3(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]));
+}
+__device__ __forceinline__ float3 interp33_8b(__amdgpu_buffer_rsrc_t img, int slot16, float x, float y, int w) {
+  const int ix = (int)x, iy = (int)y;
+  const float dx = __builtin_amdgcn_fractf(x), dy = __builtin_amdgcn_fractf(y), dxdy = dx * dy;
+  const int vo = ((__mul24(iy, w) + ix) << 4) + slot16, row = __builtin_amdgcn_readfirstlane(w << 4);
+  const float3 p00 = ld_texel3(img, vo, 0), p10 = ld_texel3(img, vo + 16, 0), p01 = ld_texel3(img, vo, row),
+               p11 = ld_texel3(img, vo + 16, row);
+  const float w11 = dxdy, w01 = dy - dxdy, w10 = dx - dxdy, w00 = 1 - dx - dy + dxdy;
+  float3 r;
+  r.x = w11 * p11.x + w01 * p01.x + w10 * p10.x + w00 * p00.x;
+  r.y = w11 * p11.y + w01 * p01.y + w10 * p10.y + w00 * p00.y;
+  r.z = w11 * p11.z + w01 * p01.z + w10 * p10.z + w00 * p00.z;
+  return r;
+}
 __device__ __forceinline__ float3 interp33_8(const float4* __restrict__ img, float x, float y, int w) {
   int ix = (int)x, iy = (int)y;
   float dx = x - ix, dy = y - iy, dxdy = dx * dy;
@@ -300,10 +326,24 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
   const HsCalib cal = a.st->dcal;
   const HsLinParams lp = a.lp;
   // div_nr / sqrt_nr in the pixel loop: the two thresholds bound its quotients' and roots' ranges (uniform)
+#if L8_BOUNDS_BITS
+  // the pixel bounds 1.1 < PKu < W - 3, 1.1 < PKv < H - 3 (Src/OptimizationClasses.cpp:152) as unsigned spans of
+  // float bits above 1.1f (an empty interval: span 0)
+  constexpr unsigned kLo1 = 0x3f8ccccdu + 1u;  // __float_as_uint(1.1f) + 1
+  const float wmax = (float)(cal.W - 3), hmax = (float)(cal.H - 3);
+  const unsigned spanU = __builtin_amdgcn_readfirstlane(wmax > 1.1f ? __float_as_uint(wmax) - kLo1 : 0u);
+  const unsigned spanV = __builtin_amdgcn_readfirstlane(hmax > 1.1f ? __float_as_uint(hmax) - kLo1 : 0u);
+#endif
   const bool fast_ok = lp.outlierTHSumComponent >= 0x1p-30f && lp.outlierTHSumComponent <= 0x1p30f &&
                        lp.huberTH >= 0x1p-30f && lp.huberTH <= 0x1p30f;
   const int tc = t < nF ? t : 0;
+#if L8_BUFFER_TAPS
+  // every image slot through one resource (num_records: the whole 32-bit range; taps stay inside the slot's image)
+  const __amdgpu_buffer_rsrc_t timg = __builtin_amdgcn_make_buffer_rsrc((void*)a.img, 0, 0x7fffffff, 0x00020000);
+  const int slot16 = hs_img_slot(a.img_slot, tc) * a.img_stride * 16;  // past the window: frame 0
+#else
   const float4* timg = a.img + (long long)hs_img_slot(a.img_slot, tc) * a.img_stride;  // past the window: frame 0
+#endif
   L8Scratch& W = U.s[wv];
   const int oslot = t - (t > h ? 1 : 0);           // non-host slot index of t (t != h)
 
@@ -530,8 +570,18 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
       }
       // (the short-circuit form is a branch region per pixel, which keeps the scheduler from hoisting every pixel's
       // taps at once: the bitwise form spills)
+#if L8_BOUNDS_BITS
+      // 1.1 < PK < W - 3 as one unsigned range test on the float bits (ordered like the values for positive floats;
+      // negatives, -0 and NaN land above the range): the four compares' short-circuit form became 16-bit flag packing
+      const bool okP = okC && (__float_as_uint(PKu) - kLo1 < spanU) && (__float_as_uint(PKv) - kLo1 < spanV);
+#else
       const bool okP = okC && (PKu > 1.1f && PKv > 1.1f && PKu < (cal.W - 3) && PKv < (cal.H - 3));
+#endif
+#if L8_BUFFER_TAPS
+      const float3 hit = interp33_8b(timg, slot16, okP ? PKu : 2.f, okP ? PKv : 2.f, cal.W);
+#else
       const float3 hit = interp33_8(timg, okP ? PKu : 2.f, okP ? PKv : 2.f, cal.W);
+#endif
       const float color = colK[k];
       const float residual = hit.x - (float)(pcr.aff[0] * color + pcr.aff[1]);
       const float drdA = (color - pcr.b0);
