@@ -204,6 +204,7 @@ static int run_tries(hs_tracker* t, int n, const double* h_in, int coarsest, int
   if (const char* e = std::getenv("HS_TRK_SPIN")) a.spin_limit = (unsigned int)std::max(1, std::atoi(e));  // ticks (test hook)
   a.G = G;
   a.nhyp = n;
+  const int nblk = n * G;
   a.part = t->d_part;
   a.lvrec = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(t->d_part) + meet_bytes(t->try_cap));
   // levels below one workgroup's batch of points run on one member (r05_trk1 at C2: level 4's 936 points, 8 passes:
@@ -236,7 +237,7 @@ static int run_tries(hs_tracker* t, int n, const double* h_in, int coarsest, int
   if (const char* e = std::getenv("HS_TRK_SOLVE")) a.solve = std::atoi(e) == 1 ? 1 : 0;  // A/B: 1 = the LDLT
   const char* kt = std::getenv("HS_KTRACE");
   if (kt && kt[0] == '1' && !single_pass) {
-    const int nb = n * G;
+    const int nb = nblk;
     if (nb > t->trace_cap) {  // grown once to the largest block count (freed by hs_tracker_destroy)
       if (t->d_trace) (void)hipFree(t->d_trace);
       t->d_trace = nullptr;
@@ -247,7 +248,7 @@ static int run_tries(hs_tracker* t, int n, const double* h_in, int coarsest, int
     a.trace = t->d_trace;
   }
   TS_HIP(hipEventRecord(t->e0, t->stream));
-  hipLaunchKernelGGL(hs_k_track, dim3(n * G), dim3(512), 0, t->stream, a);
+  hipLaunchKernelGGL(hs_k_track, dim3(nblk), dim3(512), 0, t->stream, a);
   TS_HIP(hipGetLastError());
   TS_HIP(hipEventRecord(t->e1, t->stream));
   if (!zc)  // the timeout flags and the outputs of the n hypotheses, in one read-back
@@ -266,9 +267,21 @@ static int run_tries(hs_tracker* t, int n, const double* h_in, int coarsest, int
   if (a.trace) {
     long long h[16];
     TS_HIP(hipMemcpy(h, t->d_trace, sizeof(h), hipMemcpyDeviceToHost));
-    std::fprintf(stderr, "[trk trace] %.3f ms: point loop %lld, reductions %lld (wave reduce %lld, barrier wait %lld), "
-                 "LM steps %lld (LDLT %lld, exp + product %lld) cycles over %lld passes\n", ms, h[4], h[5], h[8], h[9],
-                 h[6], h[10], h[11], h[7]);
+    {  // placement probe: block -> xcd / cu (h, g)
+      std::vector<long long> pl((size_t)nblk * 16);
+      TS_HIP(hipMemcpy(pl.data(), t->d_trace, sizeof(long long) * pl.size(), hipMemcpyDeviceToHost));
+      std::fprintf(stderr, "[trk place]");
+      for (int b = 0; b < nblk && b < 64; b++) {
+        const long long v = pl[(size_t)b * 16 + 14];
+        if (pl[(size_t)b * 16] == 0) continue;  // an idle block
+        std::fprintf(stderr, " %d:x%lld/c%lld(h%lld g%lld)", b, v & 15, (v >> 4) & 15, (v >> 8) & 255, (v >> 16) & 255);
+      }
+      std::fprintf(stderr, "\n");
+    }
+    std::fprintf(stderr, "[trk trace] %.3f ms: point loop %lld, reductions %lld (wave reduce %lld, barrier wait %lld, "
+                 "meetings %lld over %lld), LM steps %lld (LDLT %lld, exp + product %lld) cycles over %lld passes "
+                 "(G %d, n %d, fallbacks so far %d); wave-0 tail: tree %lld, meeting + results %lld, bookkeeping %lld\n",
+                 ms, h[4], h[5], h[8], h[9], h[12], h[13], h[6], h[10], h[11], h[7], G, n, t->fallbacks, h[1], h[2], h[3]);
   }
   return HS_OK;
 }

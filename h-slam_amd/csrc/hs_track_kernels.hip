@@ -204,7 +204,11 @@ struct TrkShared {
   int passes;
   int npass, iters, nchecks;  // this workgroup's pass count (partial parity, counter target), LM iterations, checks
   long long pointPasses;
-  long long prof[8];  // HS_KTRACE: thread-0 cycles: point loop, reductions, LM step, passes, wave reduce, barrier,
+  // lane q < 45 of the pass tail: its normal-equation entry (r, c) (H (r, c) at hp & 255, (c, r) at (hp >> 8) & 255,
+  // c == 8: b (r) at hp & 255 with bit 16 set; (8, 8): -1) and the two scales, formed once per launch
+  int hpos[64];
+  double hsr[64], hsc[64];
+  long long prof[13];  // HS_KTRACE: thread-0 cycles: point loop, reductions, LM step, passes, wave reduce, barrier,
                       // the LM step's solve, its exp + product
   HsTryOut out;       // the lead's output record (thread 0 writes), copied out by trk_publish
 };
@@ -442,8 +446,10 @@ __device__ void trk_pass(const HsTrackArgs& a, TrkShared& S, int h, int g, bool 
     double r8[TRK_NT / 64];
 #pragma unroll
     for (int w = 0; w < TRK_NT / 64; w++) r8[w] = S.red[w][q];
+    const long long pt0 = (a.trace && lane == 0) ? clock64() : 0;
     double tot = ((r8[0] + r8[1]) + (r8[2] + r8[3])) + ((r8[4] + r8[5]) + (r8[6] + r8[7]));
     static_assert(TRK_NT / 64 == 8, "block tree");
+    const long long pt1 = (a.trace && lane == 0) ? clock64() + (long long)(tot * 0.0) : 0;
     if (G > 1) {
       // The hypothesis' workgroups meet by granules (cdna_hip_programming.md §6 Guideline 16, R2: the data is the
       // flag): every fp64 partial goes out as two 8-byte {tag, 32-bit half} granules (sc1 stores), and lane q
@@ -463,6 +469,7 @@ __device__ void trk_pass(const HsTrackArgs& a, TrkShared& S, int h, int g, bool 
                            __HIP_MEMORY_SCOPE_AGENT);
       }
       u64 v[2 * HS_TRK_MAXG];
+      const long long pm0 = (a.trace && lane == 0) ? clock64() : 0;
       // the poll's time bound on the constant 100 MHz wall clock (spin_limit ticks, set by the host from the clock
       // rate); after a timeout (S.dead) a meeting polls once
       const unsigned long long t_end = wall_clock64() + (S.dead ? 0ull : (unsigned long long)a.spin_limit);
@@ -488,51 +495,57 @@ __device__ void trk_pass(const HsTrackArgs& a, TrkShared& S, int h, int g, bool 
           break;
         }
       }
+      if (a.trace && lane == 0) {
+        S.prof[8] += clock64() - pm0;  // the meeting: own stores to every member's granules seen
+        S.prof[9] += 1;
+      }
       tot = 0.0;
+      if (G == HS_TRK_MAXG) {  // (uniform) the production member count: no per-slot masks
 #pragma unroll
-      for (int gg = 0; gg < HS_TRK_MAXG; gg++)
-        if (gg < G) tot += __longlong_as_double((long long)((v[2 * gg] & 0xffffffffull) | (v[2 * gg + 1] << 32)));
+        for (int gg = 0; gg < HS_TRK_MAXG; gg++)
+          tot += __longlong_as_double((long long)((v[2 * gg] & 0xffffffffull) | (v[2 * gg + 1] << 32)));
+      } else {
+#pragma unroll
+        for (int gg = 0; gg < HS_TRK_MAXG; gg++)
+          if (gg < G) tot += __longlong_as_double((long long)((v[2 * gg] & 0xffffffffull) | (v[2 * gg + 1] << 32)));
+      }
     }
     const float Ef = (float)trk_readlane_f64(tot, TRK_NACC + 0);
     const float fT = (float)trk_readlane_f64(tot, TRK_NACC + 1), fRT = (float)trk_readlane_f64(tot, TRK_NACC + 2);
     const float fN = (float)trk_readlane_f64(tot, TRK_NACC + 3);
     const int numE = (int)trk_readlane_f64(tot, TRK_NACC + 4), numSat = (int)trk_readlane_f64(tot, TRK_NACC + 5);
     const int numW = (int)trk_readlane_f64(tot, TRK_NACC + 6);
-    double res[6];
-    res[0] = Ef;
-    res[1] = numE;
-    res[2] = fT / (fN + 0.1);
-    res[3] = 0;
-    res[4] = fRT / (fN + 0.1);
-    res[5] = numSat / (float)numE;
+    // res[6] (Src/CoarseTracker.cpp:402-409), lane k < 6 forming res[k] alone: its quotient in parallel with the
+    // other lanes' instead of three quotients in series on every lane
+    const double r0 = Ef, r1 = numE;
+    double rl;
+    {
+      const float q5 = numSat / (float)numE;
+      const double q24 = (double)(lane == 4 ? fRT : fT) / (fN + 0.1);
+      rl = lane == 0 ? r0 : lane == 1 ? r1 : lane == 3 ? 0.0 : lane == 5 ? (double)q5 : q24;
+    }
     const int npad = (numW + 3) & ~3;  // buf_warped_n includes the zero padding (quirk kept)
     // lm: the LM iteration's accept test (Src/CoarseTracker.cpp:611-640) -- an accepted pass's normal equations
     // and residuals go straight to Hs / bs / resOld; a plain pass leaves them in H / b / res
     const double oldRatio = S.resOld[0] / S.resOld[1];
-    const bool accept = lm && (res[0] / res[1]) < oldRatio;
+    const double newRatio = r0 / r1;
+    const bool accept = lm && newRatio < oldRatio;
     double* Hd = accept ? S.Hs : S.H;
     double* bd = accept ? S.bs : S.b;
-    if (lane < 6 && (!lm || accept)) (accept ? S.resOld : S.res)[lane] = res[lane];
-    if (lane < 45) {  // H / b from the 45 upper-triangle sums (row-major), one entry per lane
-      int qq = lane, r = 0;
-      while (qq >= 9 - r) {
-        qq -= 9 - r;
-        r++;
-      }
-      const int c = r + qq;
+    if (lane < 6 && (!lm || accept)) (accept ? S.resOld : S.res)[lane] = rl;
+    if (lane < 45 && (!lm || accept)) {  // H / b from the 45 upper-triangle sums (row-major), one entry per lane
+      const int hp = S.hpos[lane];
       const double inv = (double)(1.0f / npad);
       const double vv = (double)(float)tot;
-      const double sr = r < 3 ? hs_trk_scale_rot : r < 6 ? hs_trk_scale_trans : r == 6 ? hs_trk_scale_a : hs_trk_scale_b;
-      const double scc = c < 3 ? hs_trk_scale_rot : c < 6 ? hs_trk_scale_trans : c == 6 ? hs_trk_scale_a : hs_trk_scale_b;
-      if (!lm || accept) {
-        if (c < 8) {
-          Hd[r * 8 + c] = ((vv * inv) * scc) * sr;
-          Hd[c * 8 + r] = ((vv * inv) * sr) * scc;
-        } else if (r < 8) {  // (8, 8) is the residual square sum, not part of H / b
-          bd[r] = (vv * inv) * sr;
-        }
+      const double sr = S.hsr[lane], scc = S.hsc[lane];
+      if (hp >= 0 && !(hp & 0x10000)) {
+        Hd[hp & 255] = ((vv * inv) * scc) * sr;
+        Hd[(hp >> 8) & 255] = ((vv * inv) * sr) * scc;
+      } else if (hp >= 0) {  // (8, 8) is the residual square sum, not part of H / b
+        bd[hp & 255] = (vv * inv) * sr;
       }
     }
+    const long long pt2 = (a.trace && lane == 0) ? clock64() : 0;
     if (lane == 0) {
       S.passes += 1;
       S.npass += 1;
@@ -541,7 +554,7 @@ __device__ void trk_pass(const HsTrackArgs& a, TrkShared& S, int h, int g, bool 
       if (lm) {
         const int it = S.iters - 1;
         if (g == 0 && it < HS_TRK_MAXLOG) {
-          a.lm_log[((size_t)h * HS_TRK_MAXLOG + it) * 3 + 0] = res[0] / res[1];
+          a.lm_log[((size_t)h * HS_TRK_MAXLOG + it) * 3 + 0] = newRatio;
           a.lm_log[((size_t)h * HS_TRK_MAXLOG + it) * 3 + 1] = oldRatio;
           a.lm_log[((size_t)h * HS_TRK_MAXLOG + it) * 3 + 2] = S.incNorm;
           a.lm_lvl[(size_t)h * HS_TRK_MAXLOG + it] = lvl;
@@ -562,6 +575,9 @@ __device__ void trk_pass(const HsTrackArgs& a, TrkShared& S, int h, int g, bool 
         S.prof[0] += pc1 - pc0;
         S.prof[1] += pc2 - pc1;
         S.prof[3] += 1;
+        S.prof[10] += pt1 - pt0;  // the 8-wave tree (LDS loads + adds)
+        S.prof[11] += pt2 - pt1;  // the meeting (if any) + results to the H / b stores
+        S.prof[12] += pc2 - pt2;  // lane 0's bookkeeping
       }
     }
   }
@@ -687,9 +703,25 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
   __shared__ TrkShared S;
   const int tid = threadIdx.x;
   const int h = blockIdx.x / a.G, g = blockIdx.x - h * a.G;  // hypothesis, member workgroup
+  if (a.trace && tid == 0) {  // placement probe: the XCD (HW_REG_XCC_ID) and CU (HW_REG_HW_ID bits 11:8) of the block
+    const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u;
+    const unsigned cu = (__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 8) & 15u;
+    a.trace[(size_t)blockIdx.x * 16 + 14] = (long long)(xcc | (cu << 4) | ((unsigned)h << 8) | ((unsigned)g << 16));
+  }
   const bool lead = g == 0;  // the workgroup that writes the hypothesis' outputs (every member computes them)
   HsTryOut& out = S.out;  // staged in LDS, published by trk_publish
   HS_TRACE(a, 0);
+  if (tid < 64) {  // the pass tail's per-lane normal-equation entry and scales (S.hpos; ordered by the first barrier)
+    int qq = tid, r = 0;
+    while (r < 9 && qq >= 9 - r) {
+      qq -= 9 - r;
+      r++;
+    }
+    const int c = r + qq;
+    S.hpos[tid] = tid >= 45 || (r == 8 && c == 8) ? -1 : (c < 8 ? (r * 8 + c) | ((c * 8 + r) << 8) : r | 0x10000);
+    S.hsr[tid] = r < 3 ? hs_trk_scale_rot : r < 6 ? hs_trk_scale_trans : r == 6 ? hs_trk_scale_a : hs_trk_scale_b;
+    S.hsc[tid] = c < 3 ? hs_trk_scale_rot : c < 6 ? hs_trk_scale_trans : c == 6 ? hs_trk_scale_a : hs_trk_scale_b;
+  }
   if (a.single_pass) {  // hs_tracker_calc_res
     if (tid == 0) {
       S.dead = 0;
@@ -730,7 +762,7 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
     S.npass = 0;
     S.passes = 0;
     S.pointPasses = 0;
-    for (int q = 0; q < 8; q++) S.prof[q] = 0;
+    for (int q = 0; q < 13; q++) S.prof[q] = 0;
   }
   __syncthreads();
   bool haveRepeated = false;
@@ -887,8 +919,10 @@ __global__ __launch_bounds__(TRK_NT) void hs_k_track(HsTrackArgs a) {
     out.ok = ok ? 1 : 0;
     out.passes = S.passes;
     out.point_passes = S.pointPasses;
-    if (a.trace)
-      for (int q = 0; q < 8; q++) a.trace[(size_t)blockIdx.x * 16 + 4 + q] = S.prof[q];
+    if (a.trace) {
+      for (int q = 0; q < 10; q++) a.trace[(size_t)blockIdx.x * 16 + 4 + q] = S.prof[q];
+      for (int q = 0; q < 3; q++) a.trace[(size_t)blockIdx.x * 16 + 1 + q] = S.prof[10 + q];
+    }
   }
   trk_publish(a, S, h, lead);
   HS_TRACE(a, 15);
