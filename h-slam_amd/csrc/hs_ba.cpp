@@ -50,7 +50,7 @@ int max_blocks_for(int capP) {
 static void free_buffers(hs_ctx* c) {
   drop_graph(c);
   std::vector<void*> ptrs = {
-      c->d_img_all, c->d_raw, c->d_state, c->d_pre, c->d_frameTH, c->d_res_of_slot, c->d_pt_host,
+      c->d_img_all, c->d_img3, c->d_raw, c->d_state, c->d_pre, c->d_frameTH, c->d_res_of_slot, c->d_pt_host,
       c->d_host_pt_begin, c->d_res_order, c->d_r_active, c->d_r_energy, c->d_r_newEnergy, c->d_r_ewo,
       c->d_p_actmask, c->d_p_HdiF, c->d_p_bdSumF, c->d_p_Hcd, c->d_p_JpJdF, c->d_p_step, c->d_part, c->d_part_e,
       c->d_hostsum, c->d_sys, c->d_sep, c->d_adHost, c->d_adTarget, c->d_adHostF, c->d_adTargetF, c->d_HM, c->d_bM,
@@ -70,7 +70,7 @@ static void free_buffers(hs_ctx* c) {
   c->h_stage = nullptr;
   c->h_stage_cap = 0;
   c->h_raw = nullptr;
-  c->d_img_all = nullptr; c->d_raw = nullptr;
+  c->d_img_all = nullptr; c->d_img3 = nullptr; c->d_raw = nullptr;
   c->d_state = nullptr; c->d_pre = nullptr; c->d_frameTH = nullptr;
   c->d_res_of_slot = c->d_pt_host = c->d_host_pt_begin = nullptr;
   c->d_res_order = nullptr;
@@ -142,6 +142,7 @@ int ensure_capacity(hs_ctx* c, int W, int H, int capP, int capBlk) {
   const size_t npx = (size_t)W * H, P8 = (size_t)capP * 8;
   const int nmax = HS_MAXDIM, SLmax = nmax * nmax + nmax, ne = hs_ne(true), FF = HS_MAXF * HS_MAXF;
   HS_TRY(dalloc(&c->d_img_all, npx * HS_MAXF));
+  HS_TRY(dalloc(&c->d_img3, npx * HS_MAXF * 3));
   c->img_px = npx;
   HS_TRY(dalloc(&c->d_state, 1));
   HS_TRY(dalloc(&c->d_pre, FF));
@@ -333,6 +334,16 @@ int upload_frames(hs_ctx* c) {
   return HS_OK;
 }
 
+// refresh image slot s's packed copy (d_img3) from its float4 texels, on the context's stream: every write of a slot
+// (the window upload, hs_ba_set_frame_image / _raw / _device) ends with it
+int pack_slot(hs_ctx* c, int s) {
+  const long long n = (long long)c->img_px;
+  hipLaunchKernelGGL(hs_k_pack_texels, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, n,
+                     c->d_img_all + (size_t)s * c->img_px, c->d_img3 + (size_t)s * c->img_px * 3);
+  HS_HIP(hipGetLastError());
+  return HS_OK;
+}
+
 // hs_k_lin partitioning of the committed window (host_pt_begin).  Production: every host's points are split into
 // blocks of HS_LIN_NW waves x ppw points (ppw grows with the window so the grid stays near kLinBlocksTarget blocks;
 // env HS_LIN_PPW overrides).  HS_ACC_EXACT=1: one block per host whose wave 0 takes every point in order = the
@@ -388,6 +399,7 @@ static int launch_linearize(hs_ctx* c, int fuse, bool marg = false, bool accumul
     a.margPriorFac = c->P.idepthFixPriorMargFac;
   }
   a.img = c->d_img_all;
+  a.img3 = c->d_img3;
   a.img_stride = (long long)c->img_px;
   for (int f = 0; f < HS_MAXF; f++) a.img_slot[f] = c->img_slot[f];
   a.st = c->d_state;
@@ -1147,6 +1159,7 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
     HS_HIP(hipMemcpyAsync(c->d_img_all + (size_t)f * npx, tex.data(), npx * sizeof(float4), hipMemcpyHostToDevice,
                           c->stream));
     HS_HIP(hipStreamSynchronize(c->stream));  // tex is reused
+    HS_TRY(pack_slot(c, f));
   }
   const size_t P8 = (size_t)nP * 8;
   std::vector<float> prior(nP, 0.f);

@@ -151,6 +151,7 @@ struct hs_ctx {
   size_t d_stage_cap = 0;
 
   // ---- device
+  float* d_img3 = nullptr;        // the same slots packed as (I, dI/dx, dI/dy) triplets: hs_k_lin8's taps (pack_slot)
   float4* d_img_all = nullptr;    // HS_MAXF image slots of level-0 texels
   size_t img_px = 0;
   float* d_raw = nullptr;         // raw level-0 staging for hs_ba_set_frame_image_raw
@@ -274,6 +275,7 @@ int sync_hm(hs_ctx* c);          // HM / bM <- d_HM / d_bM after a device margin
 int fetch_state(hs_ctx* c);
 void compute_projector(hs_ctx* c);
 int make_partition(hs_ctx* c);    // blk_begin / nblk / W / lin8 / th_multi from host_pt_begin
+int pack_slot(hs_ctx* c, int s);  // image slot s's packed (I, dx, dy) copy from its texels (after every slot write)
 int upload_frames(hs_ctx* c);     // adjoints, projector, precalc of c->h_state's frames -> device (async)
 int wait_uploads(hs_ctx* c);      // the pinned staging buffers are free for the host again
 size_t fstage_bytes();

@@ -2603,6 +2603,17 @@ __global__ void hs_k_fix_frames(HsDevState* st, HsPrecalc* pre, double* adH, dou
   }
 }
 
+// image slot texels (I, dx, dy, |grad|^2) -> packed (I, dx, dy) triplets for hs_k_lin8's taps: 12 instead of 16 bytes
+// per texel, so a pattern row's taps span fewer cache lines
+__global__ void hs_k_pack_texels(long long n, const float4* src, float* dst3) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float4 t = src[i];
+  dst3[3 * i + 0] = t.x;
+  dst3[3 * i + 1] = t.y;
+  dst3[3 * i + 2] = t.z;
+}
+
 __global__ void hs_k_apply_step(int n, const float* step, float* idepth, float* idepth_zero) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p < n) {

@@ -404,6 +404,7 @@ int hs_ba_set_frame_image(hs_ctx* c, int frame, const float* image) {
   std::vector<float4> tex(c->img_px);
   for (size_t i = 0; i < c->img_px; i++) tex[i] = make_float4(image[3 * i], image[3 * i + 1], image[3 * i + 2], 0.f);
   HS_HIP(hipMemcpyAsync(dst, tex.data(), c->img_px * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+  HS_TRY(pack_slot(c, c->wframes[frame].slot));
   HS_HIP(hipStreamSynchronize(c->stream));
   return HS_OK;
 }
@@ -419,7 +420,7 @@ int hs_ba_set_frame_image_raw(hs_ctx* c, int frame, const float* raw) {
   HS_HIP(hipEventRecord(c->ev_upload, c->stream));
   float4* lv[1] = {dst};
   HS_HIP(hs_build_dir_pyramid(c->stream, c->d_raw, c->cam.width, c->cam.height, 1, lv, nullptr));
-  return HS_OK;
+  return pack_slot(c, c->wframes[frame].slot);
 }
 
 int hs_ba_set_frame_image_device(hs_ctx* c, int frame, const void* d_texels) {
@@ -427,6 +428,7 @@ int hs_ba_set_frame_image_device(hs_ctx* c, int frame, const void* d_texels) {
   if (!d_texels) return fail(HS_ERR_INVALID, "null texels");
   HS_TRY(frame_slot_ptr(c, frame, &dst));
   HS_HIP(hipMemcpyAsync(dst, d_texels, c->img_px * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
+  HS_TRY(pack_slot(c, c->wframes[frame].slot));
   // the source belongs to another context (the tracker's d_new, rewritten on the tracker's stream by its next
   // set_frame): the copy must have read it before this call returns, or the producer's next write races it
   HS_HIP(hipStreamSynchronize(c->stream));

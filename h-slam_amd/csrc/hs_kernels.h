@@ -55,6 +55,7 @@ __device__ __forceinline__ int hs_img_slot(const int (&slot)[HS_MAXF], int t) {
 
 struct HsLinArgs {
   const float4* img;           // level-0 texels of the image slots, slot s at img + s * img_stride
+  const float* img3;           // the same texels packed as 12-byte (I, dx, dy) triplets (hs_k_lin8)
   long long img_stride;
   int img_slot[HS_MAXF];       // window frame -> image slot (frames keep their slot while the window slides)
   const HsDevState* st;
@@ -241,6 +242,7 @@ __global__ void hs_k_resub(HsResubArgs a);
 __global__ void hs_k_debug_se3(int op, int n, const double* in, double* out);  // test hook
 __global__ void hs_k_debug_fastmath(int n, const float* a, const float* b, float* out);  // test hook (hs_lin8)
 __global__ void hs_k_apply_step(int n, const float* step, float* idepth, float* idepth_zero);
+__global__ void hs_k_pack_texels(long long n, const float4* src, float* dst3);  // float4 texels -> (I, dx, dy)
 // System::optimize's tail, frame part (Src/FullSystemOptimize.cpp:498-506) on the device: the newest frame's
 // setEvalPT(PRE_worldToCam, (0,..,0, a, b, 0, 0)) + takeData, then setAdjointsF + setPrecalcValues of every pair (one
 // thread per pair).  The nullspaces of the moved frame are left to the host (hs_ctx::frames_stale).  One block of 64.

@@ -56,6 +56,9 @@ constexpr int Q8_N = 17;  // per-pixel quantities summed over the pattern
 #ifndef L8_BOUNDS_BITS
 #define L8_BOUNDS_BITS 1  // the pixel bounds test on float bits (one unsigned range compare per coordinate)
 #endif
+#ifndef L8_TEXEL_BYTES
+#define L8_TEXEL_BYTES 12  // the taps' texel stride: 12 = the packed (I, dx, dy) copy, 16 = the float4 texels
+#endif
 #ifndef L8_BUFFER_TAPS
 #define L8_BUFFER_TAPS 1  // the pixel taps as buffer loads with 32-bit offsets (interp33_8b)
 #endif
@@ -75,12 +78,13 @@ __device__ __forceinline__ float3 ld_texel3(__amdgpu_buffer_rsrc_t r, int vo, in
   const auto v = __builtin_amdgcn_raw_buffer_load_b96(r, vo, so, 0);
   return make_float3(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]));
 }
-__device__ __forceinline__ float3 interp33_8b(__amdgpu_buffer_rsrc_t img, int slot16, float x, float y, int w) {
+__device__ __forceinline__ float3 interp33_8b(__amdgpu_buffer_rsrc_t img, int slot_b, float x, float y, int w) {
+  constexpr int TB = L8_TEXEL_BYTES;
   const int ix = (int)x, iy = (int)y;
   const float dx = __builtin_amdgcn_fractf(x), dy = __builtin_amdgcn_fractf(y), dxdy = dx * dy;
-  const int vo = ((__mul24(iy, w) + ix) << 4) + slot16, row = __builtin_amdgcn_readfirstlane(w << 4);
-  const float3 p00 = ld_texel3(img, vo, 0), p10 = ld_texel3(img, vo + 16, 0), p01 = ld_texel3(img, vo, row),
-               p11 = ld_texel3(img, vo + 16, row);
+  const int vo = __mul24(__mul24(iy, w) + ix, TB) + slot_b, row = __builtin_amdgcn_readfirstlane(w * TB);
+  const float3 p00 = ld_texel3(img, vo, 0), p10 = ld_texel3(img, vo + TB, 0), p01 = ld_texel3(img, vo, row),
+               p11 = ld_texel3(img, vo + TB, row);
   const float w11 = dxdy, w01 = dy - dxdy, w10 = dx - dxdy, w00 = 1 - dx - dy + dxdy;
   float3 r;
   r.x = w11 * p11.x + w01 * p01.x + w10 * p10.x + w00 * p00.x;
@@ -338,9 +342,11 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
                        lp.huberTH >= 0x1p-30f && lp.huberTH <= 0x1p30f;
   const int tc = t < nF ? t : 0;
 #if L8_BUFFER_TAPS
-  // every image slot through one resource (num_records: the whole 32-bit range; taps stay inside the slot's image)
-  const __amdgpu_buffer_rsrc_t timg = __builtin_amdgcn_make_buffer_rsrc((void*)a.img, 0, 0x7fffffff, 0x00020000);
-  const int slot16 = hs_img_slot(a.img_slot, tc) * a.img_stride * 16;  // past the window: frame 0
+  // every image slot through one resource (num_records: the whole 32-bit range; taps stay inside the slot's image):
+  // the packed 12-byte (I, dx, dy) copy (L8_TEXEL_BYTES 12) or the float4 texels (16)
+  const void* ibase = L8_TEXEL_BYTES == 12 ? (const void*)a.img3 : (const void*)a.img;
+  const __amdgpu_buffer_rsrc_t timg = __builtin_amdgcn_make_buffer_rsrc((void*)ibase, 0, 0x7fffffff, 0x00020000);
+  const int slot16 = hs_img_slot(a.img_slot, tc) * (int)a.img_stride * L8_TEXEL_BYTES;  // past the window: frame 0
 #else
   const float4* timg = a.img + (long long)hs_img_slot(a.img_slot, tc) * a.img_stride;  // past the window: frame 0
 #endif
