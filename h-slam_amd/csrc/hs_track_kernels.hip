@@ -27,7 +27,10 @@
 namespace {
 
 constexpr int TRK_NT = 512;
-constexpr int TRK_B = 4;              // points per thread whose loads are in flight together
+constexpr int TRK_B = 4;
+#ifndef TRK_MEET_F32
+#define TRK_MEET_F32 1  // member meetings exchange fp32 block totals (one granule per value) instead of fp64 (two)
+#endif              // points per thread whose loads are in flight together
 constexpr int TRK_NACC = 45;          // upper triangle of the 9x9 [J | r] normal equations
 constexpr int TRK_NRED = TRK_NACC + 4 + 3;  // + E, flowT, flowRT, flowNum | numE, numSat, numWarped
 static_assert(TRK_NRED == HS_TRK_NRED, "pass partial layout");
@@ -461,6 +464,43 @@ __device__ void trk_pass(const HsTrackArgs& a, TrkShared& S, int h, int g, bool 
       u64* P = reinterpret_cast<u64*>(a.part) + ((size_t)h * 2 + (S.npass & 1)) * HS_TRK_MAXG * TRK_NRED * 2;
       const unsigned int tg = (a.epoch << HS_TRK_PASS_BITS) | (unsigned int)(S.npass + 1);
       const u64 tag = (u64)tg << 32;
+#if TRK_MEET_F32
+      // one granule per value: the member's block total rounded to fp32 (every consumer below reads the pass totals
+      // as fp32: H / b from (float) tot, the energies and counts as floats / small integers), summed over the
+      // members in fp64 in member order: half the stores and polled loads of the fp64 form
+      if (lane < TRK_NRED)
+        __hip_atomic_store(P + g * TRK_NRED + lane, tag | (u64)__float_as_uint((float)tot), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      u64 v[HS_TRK_MAXG];
+      const long long pm0 = (a.trace && lane == 0) ? clock64() : 0;
+      const unsigned long long t_end = wall_clock64() + (S.dead ? 0ull : (unsigned long long)a.spin_limit);
+      for (;;) {
+#pragma unroll
+        for (int gg = 0; gg < HS_TRK_MAXG; gg++)
+          if (gg < G) v[gg] = __hip_atomic_load(P + gg * TRK_NRED + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bool ok = true;
+#pragma unroll
+        for (int gg = 0; gg < HS_TRK_MAXG; gg++) ok &= gg >= G || (unsigned int)(v[gg] >> 32) == tg;
+        if (__all(ok)) break;
+        __builtin_amdgcn_s_sleep(1);
+        if (wall_clock64() >= t_end) {  // a member never arrived (not co-resident): flag the hypothesis, go on
+          if (lane == 0) {
+            __hip_atomic_store(a.cnt + h, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            S.dead = 1;
+          }
+          break;
+        }
+      }
+      if (a.trace && lane == 0) {
+        S.prof[8] += clock64() - pm0;  // the meeting: own stores to every member's granules seen
+        S.prof[9] += 1;
+      }
+      tot = 0.0;
+#pragma unroll
+      for (int gg = 0; gg < HS_TRK_MAXG; gg++)
+        if (gg < G) tot += (double)__uint_as_float((unsigned int)(v[gg] & 0xffffffffull));
+    }
+#else
       if (lane < TRK_NRED) {
         const u64 bits = (u64)__double_as_longlong(tot);
         __hip_atomic_store(P + (g * TRK_NRED + lane) * 2, tag | (bits & 0xffffffffull), __ATOMIC_RELAXED,
@@ -510,6 +550,7 @@ __device__ void trk_pass(const HsTrackArgs& a, TrkShared& S, int h, int g, bool 
           if (gg < G) tot += __longlong_as_double((long long)((v[2 * gg] & 0xffffffffull) | (v[2 * gg + 1] << 32)));
       }
     }
+#endif
     const float Ef = (float)trk_readlane_f64(tot, TRK_NACC + 0);
     const float fT = (float)trk_readlane_f64(tot, TRK_NACC + 1), fRT = (float)trk_readlane_f64(tot, TRK_NACC + 2);
     const float fN = (float)trk_readlane_f64(tot, TRK_NACC + 3);
