@@ -247,10 +247,14 @@ static int run_tries(hs_tracker* t, int n, const double* h_in, int coarsest, int
     TS_HIP(hipMemsetAsync(t->d_trace, 0, sizeof(long long) * 16 * nb, t->stream));
     a.trace = t->d_trace;
   }
-  TS_HIP(hipEventRecord(t->e0, t->stream));
+  // the launch's device time (hs_tracker_last_ms) from an event pair around it; env HS_TRK_NOEVT=1 (read per call)
+  // skips the pair, ~3-4 us of host time per call (r05_trk14), and leaves last_ms at 0
+  const char* ne = std::getenv("HS_TRK_NOEVT");
+  const bool no_evt = ne && ne[0] == '1';
+  if (!no_evt) TS_HIP(hipEventRecord(t->e0, t->stream));
   hipLaunchKernelGGL(hs_k_track, dim3(nblk), dim3(512), 0, t->stream, a);
   TS_HIP(hipGetLastError());
-  TS_HIP(hipEventRecord(t->e1, t->stream));
+  if (!no_evt) TS_HIP(hipEventRecord(t->e1, t->stream));
   if (!zc)  // the timeout flags and the outputs of the n hypotheses, in one read-back
     TS_HIP(hipMemcpyAsync(t->h_cnt, t->d_cnt, cnt_bytes(t->try_cap) + sizeof(HsTryOut) * n, hipMemcpyDeviceToHost,
                           t->stream));
@@ -261,7 +265,7 @@ static int run_tries(hs_tracker* t, int n, const double* h_in, int coarsest, int
       return run_tries(t, n, h_in, coarsest, single_pass, lvl, cutoff, true);
     }
   float ms = 0;
-  TS_HIP(hipEventElapsedTime(&ms, t->e0, t->e1));
+  if (!no_evt) TS_HIP(hipEventElapsedTime(&ms, t->e0, t->e1));
   t->last_ms = ms;
   t->last_n_tries = single_pass ? 0 : n;
   if (a.trace) {
