@@ -49,6 +49,26 @@ __device__ __forceinline__ float3 interp33(const float4* __restrict__ img, float
   return r;
 }
 
+// the same on the packed 12-byte (I, dx, dy) texels of an image slot (HsLinArgs.img3): the 2x2 taps span fewer
+// cache lines than the float4 texels
+__device__ __forceinline__ float3 interp33p(const float* __restrict__ img3, float x, float y, int w) {
+  int ix = (int)x, iy = (int)y;
+  float dx = x - ix, dy = y - iy, dxdy = dx * dy;
+  const float* bp = img3 + 3 * (ix + iy * w);
+  const float* bq = bp + 3 * w;
+  const float3 p00 = make_float3(bp[0], bp[1], bp[2]), p10 = make_float3(bp[3], bp[4], bp[5]);
+  const float3 p01 = make_float3(bq[0], bq[1], bq[2]), p11 = make_float3(bq[3], bq[4], bq[5]);
+  const float w11 = dxdy, w01 = dy - dxdy, w10 = dx - dxdy, w00 = 1 - dx - dy + dxdy;
+  float3 r;
+  r.x = w11 * p11.x + w01 * p01.x + w10 * p10.x + w00 * p00.x;
+  r.y = w11 * p11.y + w01 * p01.y + w10 * p10.y + w00 * p00.y;
+  r.z = w11 * p11.z + w01 * p01.z + w10 * p10.z + w00 * p00.z;
+  return r;
+}
+#ifndef LIN_TEXEL12
+#define LIN_TEXEL12 1  // hs_k_lin's taps from the packed 12-byte texels
+#endif
+
 // wall-clock checkpoint of a block (thread 0) when tracing is enabled
 #define HS_TRACE(A, slot)                                                                          \
   do {                                                                                             \
@@ -286,6 +306,7 @@ __device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int 
   const HsPrecalc pc = K.pre[tc_];
   // the target's image: selected from the kernel-argument pointers (uniform SGPRs), not loaded per lane
   const float4* timg = a.img + (long long)hs_img_slot(a.img_slot, tc_) * a.img_stride;  // past the window: frame 0
+  const float* timg3 = a.img3 + (long long)hs_img_slot(a.img_slot, tc_) * a.img_stride * 3;
   // the point's 8 residual-list slots and previous active mask, as scalars (uniform per point)
   const uint2 ro2 = make_uint2(__builtin_amdgcn_readfirstlane(in.ro2.x), __builtin_amdgcn_readfirstlane(in.ro2.y));
   auto res_slot = [&](int q) -> int { return (int)(int8_t)(((q < 4 ? ro2.x : ro2.y) >> (8 * (q & 3))) & 0xffu); };
@@ -415,7 +436,8 @@ __device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int 
     q2 = q2 + pc.Kt[2] * idep;
     const float PKu = q0 / q2, PKv = q1 / q2;
     const bool okP = okC && (PKu > 1.1f && PKv > 1.1f && PKu < (cal.W - 3) && PKv < (cal.H - 3));
-    float3 hit = interp33(timg, okP ? PKu : 2.f, okP ? PKv : 2.f, cal.W);
+    float3 hit = LIN_TEXEL12 ? interp33p(timg3, okP ? PKu : 2.f, okP ? PKv : 2.f, cal.W)
+                             : interp33(timg, okP ? PKu : 2.f, okP ? PKv : 2.f, cal.W);
     if (a.trace && threadIdx.x == 0 && hit.x != -12345.f) a.trace[(size_t)blockIdx.x * 16 + 13] = wall_clock64();
     const float color = colorK;
     const float residual = hit.x - (float)(pc.aff[0] * color + pc.aff[1]);
