@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cstring>
 #include <string>
+#include <chrono>
 #include <vector>
 
 #include "../../include/hs_ba.h"
@@ -72,6 +73,9 @@ struct hs_tracker {
   unsigned int* h_cnt = nullptr;
   unsigned int* dh_cnt = nullptr;  // device aliases of h_cnt / h_out (mapped pinned memory)
   HsTryOut* dh_out = nullptr;
+  unsigned int* h_done = nullptr;  // pinned done words [try_cap] (HsTrackArgs.hdone) and their device alias
+  unsigned int* dh_done = nullptr;
+  unsigned int seq = 0;            // launch sequence number (the done words' value)
   unsigned int epoch = 0;         // the last member-meeting launch's granule epoch (hs_track_kernels.h)
   double* d_lmlog = nullptr;
   int* d_lmlvl = nullptr;
@@ -108,6 +112,7 @@ static size_t meet_bytes(int n) { return sizeof(unsigned long long) * 2 * HS_TRK
 static size_t part_bytes(int n) { return meet_bytes(n) + sizeof(unsigned long long) * HS_TRK_MAXLVSEQ * 32 * (size_t)n; }
 // the timeout flags in front of the outputs, padded to 256 B
 static size_t cnt_bytes(int n) { return (sizeof(unsigned int) * (size_t)n + 255) & ~(size_t)255; }
+static size_t done_bytes(int n) { return cnt_bytes(n); }  // the pinned done words after the pinned records
 
 static int ensure_tries(hs_tracker* t, int n) {
   if (n <= t->try_cap) return HS_OK;
@@ -127,12 +132,14 @@ static int ensure_tries(hs_tracker* t, int n) {
   TS_HIP(hipMalloc((void**)&t->d_lmlvl, sizeof(int) * HS_TRK_MAXLOG * n));
   TS_HIP(hipMalloc((void**)&t->d_part, part_bytes(n)));
   // mapped, coherent: the kernel may write the flags and records straight into it (HS_TRK_ZC, run_tries)
-  TS_HIP(hipHostMalloc((void**)&t->h_cnt, cnt_bytes(n) + sizeof(HsTryOut) * n,
+  TS_HIP(hipHostMalloc((void**)&t->h_cnt, cnt_bytes(n) + sizeof(HsTryOut) * n + done_bytes(n),
                        hipHostMallocMapped | hipHostMallocCoherent));
   t->h_out = reinterpret_cast<HsTryOut*>(reinterpret_cast<char*>(t->h_cnt) + cnt_bytes(n));
-  std::memset(t->h_cnt, 0, cnt_bytes(n) + sizeof(HsTryOut) * n);
+  t->h_done = reinterpret_cast<unsigned int*>(reinterpret_cast<char*>(t->h_out) + sizeof(HsTryOut) * n);
+  std::memset(t->h_cnt, 0, cnt_bytes(n) + sizeof(HsTryOut) * n + done_bytes(n));
   TS_HIP(hipHostGetDevicePointer((void**)&t->dh_cnt, t->h_cnt, 0));
   t->dh_out = reinterpret_cast<HsTryOut*>(reinterpret_cast<char*>(t->dh_cnt) + cnt_bytes(n));
+  t->dh_done = reinterpret_cast<unsigned int*>(reinterpret_cast<char*>(t->dh_out) + sizeof(HsTryOut) * n);
   TS_HIP(hipHostMalloc((void**)&t->h_in, sizeof(double) * 9 * n));
   t->try_cap = n;
   t->epoch = 0;  // fresh granules and flags: zeroed at the next member-meeting launch
@@ -220,6 +227,8 @@ static int run_tries(hs_tracker* t, int n, const double* h_in, int coarsest, int
   const bool zc = !(zce && zce[0] == '0');
   a.cnt = zc ? t->dh_cnt : t->d_cnt;
   a.hout = zc ? t->dh_out : nullptr;
+  a.hdone = zc ? t->dh_done : nullptr;
+  a.seq = ++t->seq;
   t->last_G = G;
   // a new granule epoch per member-meeting launch; the granules and the timeout flags are zeroed only when the
   // epoch starts over (a fresh allocation, or 2^20 - 1 launches)
@@ -258,7 +267,22 @@ static int run_tries(hs_tracker* t, int n, const double* h_in, int coarsest, int
   if (!zc)  // the timeout flags and the outputs of the n hypotheses, in one read-back
     TS_HIP(hipMemcpyAsync(t->h_cnt, t->d_cnt, cnt_bytes(t->try_cap) + sizeof(HsTryOut) * n, hipMemcpyDeviceToHost,
                           t->stream));
-  TS_HIP(hipStreamSynchronize(t->stream));  // (zero-copy: the records are in place once the launch has completed)
+  // zero-copy without the event pair or a trace: wait for every hypothesis' done word (its record and flags are in
+  // place before it) instead of the launch's end; bounded, then the synchronize as before.  Otherwise the synchronize.
+  bool waited = false;
+  if (zc && no_evt && !a.trace) {
+    const auto t_start = std::chrono::steady_clock::now();
+    for (int spins = 0;; spins++) {
+      bool all = true;
+      for (int i = 0; i < n && all; i++) all = __atomic_load_n(&t->h_done[i], __ATOMIC_ACQUIRE) == a.seq;
+      if (all) {
+        waited = true;
+        break;
+      }
+      if ((spins & 1023) == 1023 && std::chrono::steady_clock::now() - t_start > std::chrono::seconds(2)) break;
+    }
+  }
+  if (!waited) TS_HIP(hipStreamSynchronize(t->stream));  // (zero-copy: the records are in place once the launch completed)
   for (int i = 0; G > 1 && i < n; i++)
     if (t->h_cnt[i] == t->epoch) {  // a meeting timed out: the launch's results are void, rerun every hypothesis with G = 1
       t->fallbacks++;

@@ -74,6 +74,10 @@ struct HsTrackArgs {
   int solve;            // the LM step's 8x8 solve: 0 Gauss-Jordan on 64 lanes, 1 Eigen-order LDLT on 8 row lanes
   double* part;
   unsigned int* cnt;    // [nhyp] timeout flags (a member never arrived): the epoch of the launch that timed out
+  // [nhyp] or null: the lead of hypothesis h stores seq here (system scope, release) after its record (hout) and
+  // flags, so the host may read the results without waiting for the launch's end (hs_track.cpp, run_tries)
+  unsigned int* hdone;
+  unsigned int seq;
 };
 constexpr int HS_TRK_PASS_BITS = 12;  // passes per launch < 4096 (<= 5 levels x (50 + 1 + 6 cutoff repeats) x 2)
 constexpr int HS_TRK_NRED = 52;  // the reduced values of a pass (45 normal-equation entries, 4 energies / flows, 3 counts)

@@ -684,6 +684,8 @@ __device__ void trk_publish(const HsTrackArgs& a, TrkShared& S, int h, bool lead
     dd[k] = w;
     if (dh) dh[k] = w;
   }
+  // the record (and any timeout flag this wave stored) before the done word: the release orders the wave's stores
+  if (a.hdone && threadIdx.x == 0) __hip_atomic_store(a.hdone + h, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 }  // namespace

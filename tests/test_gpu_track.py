@@ -14,6 +14,8 @@ Bars:
   lastResiduals to 1e-4 rel, otherwise to the LM's own stopping tolerance (pose 2e-3, lastResiduals 1e-2 rel).
   ok / haveOneGood / tryIterations: equal.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -265,11 +267,14 @@ def test_track_parity_4_levels(vga4, start):
     g.close()
 
 
-def test_member_meeting_timeout_falls_back_to_one_workgroup(vga, monkeypatch):
+@pytest.mark.parametrize("noevt", ["0", "1"])
+def test_member_meeting_timeout_falls_back_to_one_workgroup(vga, monkeypatch, noevt):
     """The G member workgroups of a hypothesis meet once per pass and must be co-resident.  With the meeting's poll
     bound forced to one poll (HS_TRK_SPIN=1) and G past the co-residency cap (HS_TRK_G_UNCHECKED=16), meetings time
-    out; the launch is then rerun with G = 1 and the track is the one-workgroup track, bit for bit."""
+    out; the launch is then rerun with G = 1 and the track is the one-workgroup track, bit for bit.  noevt = 1: the
+    host takes the results from the leads' done words instead of the stream's end (HS_TRK_NOEVT)."""
     from hslam_amd.se3 import SE3
+    monkeypatch.setenv("HS_TRK_NOEVT", noevt)
     from hslam_amd.track import CoarseTracker
     T0 = SE3().data()
     minRes = np.full(5, np.nan)
@@ -294,3 +299,34 @@ def test_member_meeting_timeout_falls_back_to_one_workgroup(vga, monkeypatch):
     assert g2.launch_info()[0] > 1 and g2.launch_info()[1] == fallbacks and ok3
     g1.close()
     g2.close()
+
+
+def test_done_word_results_match_synchronized(vga):
+    """HS_TRK_NOEVT=1 (no event pair): the host reads each hypothesis' record once its lead's done word (a system-scope
+    release after the record) shows the launch, without waiting for the launch's end.  Tracks and try sequences
+    bit-identical to the synchronized path, over repeated calls (the done words carry a per-launch sequence number)."""
+    from hslam_amd.se3 import SE3
+    from hslam_amd.track import CoarseTracker
+    T0 = SE3().data()
+    minRes = np.full(5, np.nan)
+    outs = {}
+    for mode in ("0", "1"):
+        os.environ["HS_TRK_NOEVT"] = mode
+        try:
+            g = CoarseTracker(vga.width, vga.height, vga.K4, vga.n_levels)
+            g.set_scene(vga)
+            runs = []
+            for _ in range(3):
+                ok, T, a = g.trackNewestCoarse(T0, [0.0, 0.0], vga.n_levels - 1, minRes)
+                runs.append((ok, T, a, g.lastResiduals.copy()))
+            tr = g.track_tries([T0, T0], [0.0, 0.0], np.full(5, np.nan))
+            runs.append(tr)
+            g.close()
+        finally:
+            os.environ.pop("HS_TRK_NOEVT", None)
+        outs[mode] = runs
+    for r0, r1 in zip(outs["0"][:3], outs["1"][:3]):
+        assert r0[0] == r1[0] and np.array_equal(r0[1], r1[1]) and np.array_equal(r0[2], r1[2])
+        assert np.array_equal(r0[3], r1[3], equal_nan=True)
+    t0, t1 = outs["0"][3], outs["1"][3]
+    assert np.array_equal(t0["T"], t1["T"]) and t0["tryIterations"] == t1["tryIterations"]
