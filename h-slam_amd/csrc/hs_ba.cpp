@@ -842,10 +842,28 @@ static int gn_iterations(hs_ctx* c, int it0, int K, bool allow_break, double* en
   if (dev_brk) HS_TRY(launch_combine(c));  // the last linearization's deferred threshold select
   // read back: energy log (E of the linearizations consumed by each solve) + the last energy + status, written by
   // one small kernel straight into pinned host memory
+  const unsigned long long seq = ++c->res_seq;
   hipLaunchKernelGGL(hs_k_result, dim3(1), dim3(256), 0, c->stream, c->d_elog, k, c->sysE(), c->d_state, c->d_res,
-                     dev_brk ? 1 : 0, kLogCap + 1);
+                     dev_brk ? 1 : 0, kLogCap + 1, seq);
   HS_HIP(hipGetLastError());
-  HS_HIP(hipStreamSynchronize(c->stream));
+  // the results are complete once the result kernel's done word shows this call (its release orders them): poll it
+  // (bounded) instead of waiting for the stream's end; the synchronize after the bound surfaces any error.  With
+  // per-iteration events the event reads below wait for the stream anyway.
+  {
+    bool seen = false;
+    if (nev == 0) {
+      const auto t_start = std::chrono::steady_clock::now();
+      const unsigned long long* dw = reinterpret_cast<const unsigned long long*>(c->h_res + kLogCap + 2);
+      for (int spins = 0;; spins++) {
+        if (__atomic_load_n(dw, __ATOMIC_ACQUIRE) == seq) {
+          seen = true;
+          break;
+        }
+        if ((spins & 1023) == 1023 && std::chrono::steady_clock::now() - t_start > std::chrono::seconds(2)) break;
+      }
+    }
+    if (!seen) HS_HIP(hipStreamSynchronize(c->stream));
+  }
   if (dev_brk) {  // launch_linearize swapped the HdiF ping-pong for every launch; the skipped ones wrote nothing
     const int d = (int)c->h_res[kLogCap + 1];
     if ((k - d) & 1) {
@@ -982,7 +1000,8 @@ int hs_create(hs_ctx** out, const hs_params* params, int device_id) {
   if (hipSetDevice(device_id) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc((void**)&c->h_state, sizeof(HsDevState)) != hipSuccess ||
       hipHostMalloc((void**)&c->h_ctl, 8 * sizeof(int)) != hipSuccess ||
-      hipHostMalloc((void**)&c->h_res, sizeof(double) * (kLogCap + 2)) != hipSuccess ||
+      hipHostMalloc((void**)&c->h_res, sizeof(double) * (kLogCap + 3), hipHostMallocMapped | hipHostMallocCoherent) !=
+          hipSuccess ||
       hipHostGetDevicePointer((void**)&c->d_res, c->h_res, 0) != hipSuccess ||
       hipHostMalloc((void**)&c->h_fstage, fstage_bytes() + 256) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_upload, hipEventDisableTiming) != hipSuccess ||

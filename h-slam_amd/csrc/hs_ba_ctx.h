@@ -254,6 +254,7 @@ struct hs_ctx {
   }
   double* h_res = nullptr;
   double* d_res = nullptr;  // the device view of h_res
+  unsigned long long res_seq = 0;  // hs_k_result's done-word sequence (h_res[kLogCap + 2])
 
   // timings of the last optimize / iterate
   double t_lin = 0, t_acc = 0, t_solve = 0, t_timed = 0, t_wall = 0, t_iters = 0;

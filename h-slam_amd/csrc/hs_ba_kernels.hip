@@ -2521,7 +2521,7 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_combine(HsSolveArgs a) {
 // brk (optimize's device-side break): the iterations done are the solves that ran (st->log_count), written to
 // out[done_slot]; st->stop is cleared for the next call
 __global__ void hs_k_result(const double* elog, int k, const double* sysE, HsDevState* st, double* out, int brk,
-                            int done_slot) {
+                            int done_slot, unsigned long long seq) {
   if (brk) k = min(k, st->log_count);
   for (int i = threadIdx.x; i < k; i += blockDim.x) out[i] = elog[i];
   if (threadIdx.x == 0) {
@@ -2530,6 +2530,10 @@ __global__ void hs_k_result(const double* elog, int k, const double* sysE, HsDev
     out[done_slot] = (double)k;
     if (brk) st->stop = 0;
   }
+  __syncthreads();  // every thread's log stores before the done word (the release below orders them)
+  if (threadIdx.x == 0)
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(out + done_slot + 1), seq, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // =====================================================================================================

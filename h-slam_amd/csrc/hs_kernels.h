@@ -235,9 +235,10 @@ __global__ void hs_k_stitch(HsStitchArgs a);
 __global__ void hs_k_solve(HsSolveArgs a);
 __global__ void hs_k_combine(HsSolveArgs a);
 // the GN loop's results in one zero-copy write to pinned host memory: out[0, k) = elog, out[k] = energy of the last
-// linearization, out[k + 1] = status
+// linearization, out[k + 1] = status, out[done_slot] = iterations run; then seq into the 64-bit word at
+// out[done_slot + 1] (system scope, release: the host may take the results from it without the stream's end)
 __global__ void hs_k_result(const double* elog, int k, const double* sysE, HsDevState* st, double* out, int brk,
-                            int done_slot);   // multi-rank: the gathered systems summed into sys_out (+ block 1: select)
+                            int done_slot, unsigned long long seq);   // multi-rank: the gathered systems summed into sys_out (+ block 1: select)
 __global__ void hs_k_resub(HsResubArgs a);
 __global__ void hs_k_debug_se3(int op, int n, const double* in, double* out);  // test hook
 __global__ void hs_k_debug_fastmath(int n, const float* a, const float* b, float* out);  // test hook (hs_lin8)
