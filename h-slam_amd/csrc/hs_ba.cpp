@@ -534,7 +534,7 @@ static int exchange(hs_ctx* c, bool th) {
 // no exchange, the system vector and the energies are left as they are.
 // defer (multi-rank, the fused GN loop): the gathered sums and the threshold select run in the next solve launch.
 static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = false, bool readback = false,
-                         bool defer = false) {
+                         bool defer = false, unsigned long long res_seq = 0, int res_k = 0) {
   const bool xch = c->multi_rank() && !readback;
   HsRedArgs a = red_args(c, skip_threshold);
   if (c->brk_active) a.stop = stop_flag(c);
@@ -568,7 +568,15 @@ static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = fals
   st.red.skip_threshold = (skip_threshold || readback || multi || beside) ? 1 : 0;
   // the first nF blocks: the diagonal blocks' host-f Schur terms (hs_ba_kernels.hip stitch_diag_schur)
   const int nS = c->nF + c->nF * (c->nF + 1) / 2 + c->nF + 2 + (multi ? a.np2 : 0);
-  hipLaunchKernelGGL(hs_k_stitch, dim3(nS), dim3(HS_STITCH_NT), 0, c->stream, st);
+  if (res_seq) {  // the GN loop call's results by one more block of this launch (hs_ba_iterate's last iteration)
+    st.res_out = c->d_res;
+    st.res_elog = c->d_elog;
+    st.res_st = c->d_state;
+    st.res_k = res_k;
+    st.res_slot = kLogCap + 1;
+    st.res_seq = res_seq;
+  }
+  hipLaunchKernelGGL(hs_k_stitch, dim3(nS + (res_seq ? 1 : 0)), dim3(HS_STITCH_NT), 0, c->stream, st);
   HS_HIP(hipGetLastError());
   if (multi) {  // pass 3: the select block over pass 2's histogram and survivors (a side stream measured no faster:
                 // its cross-queue event hand-offs cost what the overlap with the solve saves)
@@ -808,6 +816,10 @@ static int gn_iterations(hs_ctx* c, int it0, int K, bool allow_break, double* en
     for (; k + 2 <= K; k += 2) HS_HIP(hipGraphLaunch(c->gexec, c->stream));
   }
   c->brk_active = dev_brk;
+  // the call's results: written by an extra block of the last iteration's stitch launch when the last iteration is
+  // known in advance (no break test) and launched eagerly on one rank, else by hs_k_result after the loop
+  const unsigned long long seq = ++c->res_seq;
+  const bool fold_res = !allow_break && !c->multi_rank() && k < K;
   for (; k < K; k++) {
     const bool timed = k < nev;
     if (timed && all) HS_HIP(hipEventRecord(c->ev[4 * k + 0], c->stream));
@@ -816,7 +828,9 @@ static int gn_iterations(hs_ctx* c, int it0, int K, bool allow_break, double* en
     if (rc == HS_OK) rc = launch_linearize(c, 1);
     if (rc == HS_OK && timed) rc = hipEventRecord(c->ev[4 * k + 2], c->stream) == hipSuccess ? HS_OK : HS_ERR_HIP;
     // the next iteration's solve launch sums the gathered systems (multi-rank) and selects the threshold
-    if (rc == HS_OK) rc = launch_reduce(c, false, false, false, (k + 1 < K && !allow_break) || dev_brk);
+    const bool last = fold_res && k + 1 == K;
+    if (rc == HS_OK)
+      rc = launch_reduce(c, false, false, false, (k + 1 < K && !allow_break) || dev_brk, last ? seq : 0, last ? K : 0);
     if (rc == HS_OK && timed && all)
       rc = hipEventRecord(c->ev[4 * k + 3], c->stream) == hipSuccess ? HS_OK : HS_ERR_HIP;
     if (rc != HS_OK) {
@@ -842,10 +856,11 @@ static int gn_iterations(hs_ctx* c, int it0, int K, bool allow_break, double* en
   if (dev_brk) HS_TRY(launch_combine(c));  // the last linearization's deferred threshold select
   // read back: energy log (E of the linearizations consumed by each solve) + the last energy + status, written by
   // one small kernel straight into pinned host memory
-  const unsigned long long seq = ++c->res_seq;
-  hipLaunchKernelGGL(hs_k_result, dim3(1), dim3(256), 0, c->stream, c->d_elog, k, c->sysE(), c->d_state, c->d_res,
-                     dev_brk ? 1 : 0, kLogCap + 1, seq);
-  HS_HIP(hipGetLastError());
+  if (!fold_res) {
+    hipLaunchKernelGGL(hs_k_result, dim3(1), dim3(256), 0, c->stream, c->d_elog, k, c->sysE(), c->d_state, c->d_res,
+                       dev_brk ? 1 : 0, kLogCap + 1, seq);
+    HS_HIP(hipGetLastError());
+  }
   // the results are complete once the result kernel's done word shows this call (its release orders them): poll it
   // (bounded) instead of waiting for the stream's end; the synchronize after the bound surfaces any error.  With
   // per-iteration events the event reads below wait for the stream anyway.

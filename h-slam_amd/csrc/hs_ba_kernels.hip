@@ -1782,8 +1782,28 @@ __device__ __forceinline__ void stitch_block(const HsStitchArgs& a, int j, doubl
   HS_TRACE(a, 15);
 }
 
+// hs_k_result's work (below) for the stitch launch's extra block: every input was written by earlier launches
+__device__ void stitch_result_block(const HsStitchArgs& a) {
+  const int k = a.res_k;
+  double* out = a.res_out;
+  for (int i = threadIdx.x; i < k; i += blockDim.x) out[i] = a.res_elog[i];
+  if (threadIdx.x == 0) {
+    out[k] = a.red.sysE[0];
+    out[k + 1] = (double)a.res_st->status;
+    out[a.res_slot] = (double)k;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(out + a.res_slot + 1), a.res_seq, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ __launch_bounds__(ST_NT) void hs_k_stitch(HsStitchArgs a) {
   __shared__ double lds[ST_LDS];
+  if (a.res_out && blockIdx.x == gridDim.x - 1) {
+    stitch_result_block(a);
+    return;
+  }
   if (a.red.stop && *a.red.stop) return;
   stitch_block(a, blockIdx.x, lds);
 }

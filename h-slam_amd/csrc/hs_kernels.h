@@ -166,6 +166,14 @@ struct HsStitchArgs {
   double lambda1, sc;          // 1 + lambda, 1 / (1 + lambda)
   HsRedArgs red;               // setNewFrameEnergyTH (the launch's last block)
   long long* trace;
+  // non-null: the GN loop call's results (hs_k_result's work: elog, the last energy, status, iteration count, then
+  // the done word) by one extra block at the end of the grid -- the call's last stitch launch, instead of a launch
+  // of their own
+  double* res_out;
+  const double* res_elog;
+  const HsDevState* res_st;
+  int res_k, res_slot;
+  unsigned long long res_seq;
 };
 
 enum { HS_SOLVE = 1, HS_APPLY = 2 };
