@@ -277,6 +277,7 @@ int fetch_state(hs_ctx* c);
 void compute_projector(hs_ctx* c);
 int make_partition(hs_ctx* c);    // blk_begin / nblk / W / lin8 / th_multi from host_pt_begin
 int pack_slot(hs_ctx* c, int s);  // image slot s's packed (I, dx, dy) copy from its texels (after every slot write)
+int copy_frame_image_device(hs_ctx* c, int frame, const void* d_texels);
 int upload_frames(hs_ctx* c);     // adjoints, projector, precalc of c->h_state's frames -> device (async)
 int wait_uploads(hs_ctx* c);      // the pinned staging buffers are free for the host again
 size_t fstage_bytes();

@@ -423,14 +423,25 @@ int hs_ba_set_frame_image_raw(hs_ctx* c, int frame, const float* raw) {
   return pack_slot(c, c->wframes[frame].slot);
 }
 
-int hs_ba_set_frame_image_device(hs_ctx* c, int frame, const void* d_texels) {
+}  // extern "C"
+
+namespace hs {
+// window frame `frame`'s image from device texels, ordered on the context's stream; no host synchronisation
+int copy_frame_image_device(hs_ctx* c, int frame, const void* d_texels) {
   float4* dst = nullptr;
   if (!d_texels) return fail(HS_ERR_INVALID, "null texels");
   HS_TRY(frame_slot_ptr(c, frame, &dst));
   HS_HIP(hipMemcpyAsync(dst, d_texels, c->img_px * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
-  HS_TRY(pack_slot(c, c->wframes[frame].slot));
-  // the source belongs to another context (the tracker's d_new, rewritten on the tracker's stream by its next
-  // set_frame): the copy must have read it before this call returns, or the producer's next write races it
+  return pack_slot(c, c->wframes[frame].slot);
+}
+}  // namespace hs
+
+extern "C" {
+
+int hs_ba_set_frame_image_device(hs_ctx* c, int frame, const void* d_texels) {
+  HS_TRY(hs::copy_frame_image_device(c, frame, d_texels));
+  // the source is foreign memory whose producer this context cannot order against: the copy must have read it
+  // before this call returns (hs_tracker_frame_to_ba orders the tracker's hand-off on the device instead)
   HS_HIP(hipStreamSynchronize(c->stream));
   return HS_OK;
 }

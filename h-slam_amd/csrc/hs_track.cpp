@@ -569,6 +569,24 @@ int hs_tracker_set_ref_ba(hs_tracker* t, hs_ctx* ba, int promote_frame, float ab
   return HS_OK;
 }
 
+// AddKeyframe's image hand-off (Src/Mapping.cpp:22, the keyframe's Frame::DirPyr[0] into the window): the level-0
+// texels of the frame last set here become window frame `frame`'s image, ordered on the device both ways -- the BA
+// stream waits for the tracker's stream (the frame's pyramid), the copy and the packed slot run on the BA stream,
+// and the tracker's stream waits for the copy, so its next set_frame cannot rewrite d_new before the copy read it.
+int hs_tracker_frame_to_ba(hs_tracker* t, hs_ctx* ba, int frame) {
+  if (!t || !ba) return tfail(HS_ERR_INVALID, "null argument");
+  if (ba->device != t->device) return tfail(HS_ERR_INVALID, "tracker and BA context on different devices");
+  if (ba->cam.width != t->W || ba->cam.height != t->H) return tfail(HS_ERR_INVALID, "image size mismatch");
+  if (!t->haveFrame) return tfail(HS_ERR_STATE, "no frame set");
+  TS_HIP(hipSetDevice(t->device));
+  TS_HIP(hipEventRecord(t->e1, t->stream));
+  TS_HIP(hipStreamWaitEvent(ba->stream, t->e1, 0));
+  HS_TRY(hs::copy_frame_image_device(ba, frame, t->d_new[0]));
+  TS_HIP(hipEventRecord(ba->ev_ready, ba->stream));
+  TS_HIP(hipStreamWaitEvent(t->stream, ba->ev_ready, 0));
+  return HS_OK;
+}
+
 int hs_tracker_get_ref(hs_tracker* t, int lvl, int* n, float* u, float* v, float* idepth, float* color) {
   if (!t || !n) return tfail(HS_ERR_INVALID, "null argument");
   if (lvl < 0 || lvl >= t->nlev) return tfail(HS_ERR_INVALID, "bad level");

@@ -128,6 +128,7 @@ SIGNATURES = {
     "hs_tracker_set_frame_raw": ([VP, VP, C.c_float], I),
     "hs_tracker_set_ref_ba": ([VP, VP, I, C.c_float, VP], I),
     "hs_tracker_frame_texels": ([VP, I, VP], I),
+    "hs_tracker_frame_to_ba": ([VP, VP, I], I),
     # include/hs_pyr.h
     "hs_dir_pyramid": ([I, I, I, I, VP, VP, VP], I),
     # include/hs_trace.h

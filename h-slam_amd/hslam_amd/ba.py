@@ -130,9 +130,10 @@ class BAWindow:
 
     makeIDX = _sync
 
-    def insertFrame(self, frame, image=None, raw=None, device_texels=None):
+    def insertFrame(self, frame, image=None, raw=None, device_texels=None, tracker=None):
         """EnergyFunctional::insertFrame (+ the frame's level-0 image: (h, w, 3) (I, dx, dy) host array, or a raw
-        (h, w) image whose level 0 is built on the device, or a device pointer of float4 texels)."""
+        (h, w) image whose level 0 is built on the device, or a device pointer of float4 texels, or the frame last
+        set on a hslam_amd.track.CoarseTracker, handed over on the device)."""
         img = None if image is None else np.ascontiguousarray(image, np.float32)
         check(self.lib.hs_ba_insert_frame(self.h, C.byref(frame), ptr(img)))
         idx = self._n_frames_mirror = getattr(self, "_n_frames_mirror", self.nF) + 1
@@ -140,6 +141,8 @@ class BAWindow:
             check(self.lib.hs_ba_set_frame_image_raw(self.h, idx - 1, ptr(np.ascontiguousarray(raw, np.float32))))
         if device_texels is not None:
             check(self.lib.hs_ba_set_frame_image_device(self.h, idx - 1, C.c_void_p(device_texels)))
+        if tracker is not None:
+            tracker.frame_to_ba(self, idx - 1)
         return idx - 1
 
     def insertPoints(self, host, u, v, idepth, idepth_zero=None, color=None, weights=None, has_prior=None,

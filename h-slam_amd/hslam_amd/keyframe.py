@@ -173,12 +173,14 @@ class KeyframeBA:
         ba = self.ba
         if self.image_path == "host":
             timer.run("setup", ba.insertFrame, self._frame(k), image=self.seq.pyr0[k])
-        elif self.image_path == "device" and self.tracker is not None:
+        elif self.image_path in ("device", "device_ptr") and self.tracker is not None:
             # the frame was tracked before it became a keyframe: its pyramid is already on the device (tracking
             # work, reported apart from the BA's)
             timer.run("track_frame", self.tracker.set_frame_raw, self.seq.raw[k])
-            ptr_ = self.tracker.frame_texels(0)
-            timer.run("setup", ba.insertFrame, self._frame(k), device_texels=ptr_)
+            if self.image_path == "device_ptr":  # through the texels' address (hs_ba_set_frame_image_device)
+                timer.run("setup", ba.insertFrame, self._frame(k), device_texels=self.tracker.frame_texels(0))
+            else:
+                timer.run("setup", ba.insertFrame, self._frame(k), tracker=self.tracker)
         else:
             timer.run("setup", ba.insertFrame, self._frame(k), raw=self.seq.raw[k])
         self.frames.append(k)
@@ -254,7 +256,7 @@ class KeyframeBA:
             self.cand_of.pop(int(hd), None)
             self.last_state.pop(int(hd), None)
         if self.tracker is not None:
-            timer.run("post", self.tracker.set_ref_ba, ba, self.image_path == "device")
+            timer.run("post", self.tracker.set_ref_ba, ba, self.image_path in ("device", "device_ptr"))
         # flagPointsForRemoval (Src/Mapping.cpp:248-328), the frame to marginalize: the oldest once the window is full
         info = dict(energies=energies, iters=n_it, n_points=ba.n_points, n_res=ba.n_res, dropped_points=len(gone))
         if marginalize and len(self.frames) >= self.window:

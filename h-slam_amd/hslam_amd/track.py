@@ -81,6 +81,11 @@ class CoarseTracker:
         check(self.lib.hs_tracker_frame_texels(self.h, int(lvl), C.byref(p)))
         return p.value
 
+    def frame_to_ba(self, ba, frame: int):
+        """The frame last set becomes window frame `frame`'s image in ba (hslam_amd.ba.BAWindow), device to
+        device, ordered on the device both ways (hs_tracker_frame_to_ba)."""
+        check(self.lib.hs_tracker_frame_to_ba(self.h, ba.h, int(frame)))
+
     def set_frame_raw(self, img, ab_exposure=1.0):
         self.setNewFrameRaw(img, ab_exposure)
 

@@ -58,6 +58,12 @@ int hs_tracker_set_ref_ba(hs_tracker* t, hs_ctx* ba, int promote_frame, float ab
    (I, dI/dx, dI/dy, 0)), valid until the next set_frame / set_ref_ba(promote) call: a keyframe's image goes to the
    BA context with hs_ba_set_frame_image_device, without crossing PCIe again. */
 int hs_tracker_frame_texels(hs_tracker* t, int lvl, const void** d_texels);
+/* System::AddKeyframe's image hand-off (Src/Mapping.cpp:22: the keyframe's Frame::DirPyr[0] becomes the new window
+   frame's image, EnergyFunctional::insertFrame): level 0 of the frame last given to hs_tracker_set_frame* becomes
+   window frame `frame`'s image in the BA context on the same device.  Ordered on the device both ways, no host
+   synchronisation: the copy follows the tracker's queued work and the tracker's next work follows the copy (unlike
+   hs_ba_set_frame_image_device, which must wait on the host for a producer it cannot order against). */
+int hs_tracker_frame_to_ba(hs_tracker* t, hs_ctx* ba, int frame);
 /* pc arrays of one level (nullable outputs, capacity w_l*h_l); *n = pc_n[lvl] */
 int hs_tracker_get_ref(hs_tracker* t, int lvl, int* n, float* u, float* v, float* idepth, float* color);
 /* the frame to track: its pyramid and ab_exposure */

@@ -50,11 +50,18 @@ def _assert_same(a, b, what):
     assert a.shape == b.shape and np.array_equal(a.view(np.uint8), b.view(np.uint8)), what
 
 
-@pytest.mark.parametrize("image_path", ["raw", "host"])
+@pytest.mark.parametrize("image_path", ["raw", "host", "device", "device_ptr"])
 def test_keyframe_sequence_matches_rebuild(image_path):
+    """device: the keyframe's image from the tracker's pyramid by hs_tracker_frame_to_ba (ordered on the device);
+    device_ptr: the same texels through hs_ba_set_frame_image_device (host-synchronised)."""
     from hslam_amd.keyframe import KeyframeBA, make_ba_sequence
+    from hslam_amd.track import CoarseTracker
     seq = make_ba_sequence(n_kf=11, points_per_kf=200)
-    drv = KeyframeBA(seq, window=8, image_path=image_path)
+    tr = None
+    if image_path.startswith("device"):
+        K4 = np.array([seq.K[0, 0], seq.K[1, 1], seq.K[0, 2], seq.K[1, 2]], np.float32)
+        tr = CoarseTracker(seq.width, seq.height, K4, seq.n_levels)
+    drv = KeyframeBA(seq, window=8, tracker=tr, image_path=image_path)
     drv.bootstrap()
     ref = {}
 
@@ -85,6 +92,8 @@ def test_keyframe_sequence_matches_rebuild(image_path):
     HM, bM = drv.ba.marginal_prior()
     assert np.isfinite(HM).all() and np.abs(HM).max() > 0  # the marginalized frames / points left a prior
     drv.ba.close()
+    if tr is not None:
+        tr.close()
 
 
 def test_tail_outputs_match_rebuild():
