@@ -698,7 +698,11 @@ __device__ void trk_level_meet(const HsTrackArgs& a, TrkShared& S, int h, int g)
   typedef unsigned long long u64;
   __syncthreads();  // member 0: the level's last pass is in S
   if (threadIdx.x < 64) {
-    const int lane = threadIdx.x, q = lane >> 1;
+    // the lane index read here (volatile: not hoisted to the kernel's entry, where the lane terms of this rare path
+    // were kept live across the whole kernel -- spilled to scratch -- and reloaded at every level meeting)
+    int lane;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+    const int q = lane >> 1;
     u64* R = a.lvrec + ((size_t)h * HS_TRK_MAXLVSEQ + min(S.lvseq, HS_TRK_MAXLVSEQ - 1)) * 32;
     const unsigned int tg = (a.epoch << 8) | (unsigned int)(S.lvseq + 1);
     if (g == 0) {
@@ -726,7 +730,7 @@ __device__ void trk_level_meet(const HsTrackArgs& a, TrkShared& S, int h, int g)
       }
       // lane 2 q + 1 holds value q's high half: pair it with the low half of lane 2 q
       const unsigned int lo = (unsigned int)(w & 0xffffffffull);
-      const unsigned int hi = (unsigned int)__shfl_down((int)lo, 1);
+      const unsigned int hi = (unsigned int)__builtin_amdgcn_ds_bpermute((lane + 1) << 2, (int)lo);
       const double v = __longlong_as_double((long long)(((u64)hi << 32) | lo));
       if (!S.dead && lane < 32 && !(lane & 1)) {
         if (q < 7) S.T[q] = v;
