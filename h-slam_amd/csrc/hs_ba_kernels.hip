@@ -65,6 +65,9 @@ __device__ __forceinline__ float3 interp33p(const float* __restrict__ img3, floa
   r.z = w11 * p11.z + w01 * p01.z + w10 * p10.z + w00 * p00.z;
   return r;
 }
+#ifndef LIN_ONE_PATH
+#define LIN_ONE_PATH 1
+#endif
 #ifndef LIN_TEXEL12
 #define LIN_TEXEL12 1  // hs_k_lin's taps from the packed 12-byte texels
 #endif
@@ -841,7 +844,13 @@ __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
   if (work) lin_load(a, pb + wv, lane, cur);  // in flight across the barrier
   __syncthreads();
   HS_TRACE(a, 12);
-  if (work) {
+  if (work && LIN_ONE_PATH && pb + wv + a.W >= pe) {
+    // the wave's only point (the 2k headline: one point per wave): no loop, so nothing is hoisted out of one and
+    // kept live (spilled) across the point's work
+    LinPt P;
+    lin_point<kFix>(a, pb + wv, h, lane, cur, K, ws, P);
+    if (a.accumulate) acc_point<kExact>(A, P, h, lane, ws);
+  } else if (work) {
     for (int p = pb + wv; p < pe; p += a.W) {  // wave-uniform
       LinIn nxt;
       if (p + a.W < pe) lin_load(a, p + a.W, lane, nxt);  // the next point's loads overlap this point's work
