@@ -268,14 +268,15 @@ constexpr int LW_QS = 0, LW_SUM = Q_N * LW_QR, LW_JJ = LW_SUM + 8 * LW_SS, LW_FL
 static_assert(LW_SUM % 4 == 0 && LW_JJ % 4 == 0, "16 B aligned scratch rows");
 static_assert(LW_FLOATS <= hs_ne(false) * 64, "lin scratch fits the wave's partials area");
 
-template <bool kFix>
+// kMarg: the marginalization pass (hs_k_lin_marg*): production launches compile its branches and arguments out
+template <bool kFix, bool kMarg>
 __device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int lane, const LinIn& in,
                                           const LinConst& K, float* ws, LinPt& o) {
   const int t = lane >> 3;  // target slot
   const int k = lane & 7;   // pattern pixel
   const int nF = a.nF;
   const HsCalib cal = K.cal;
-  if (a.marg && a.marg[p] == 0) {  // marginalization pass, point not marginalized: no active residual
+  if (kMarg && a.marg && a.marg[p] == 0) {  // marginalization pass, point not marginalized: no active residual
     if (lane == 0) {
       a.p_actmask[p] = 0;
       a.p_HdiF[p] = 0.f;
@@ -359,9 +360,9 @@ __device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int 
     }
   }
   // the marginalization pass starts from resetOOB (state IN, energies 0; Src/Mapping.cpp:285)
-  const int st = has ? (a.marg ? HS_RES_IN : st_raw) : HS_RES_OOB;
-  const float oldE = (has && !a.marg) ? oldE_raw : 0.f;
-  const float oldNewE = (has && !a.marg) ? oldNewE_raw : 0.f;
+  const int st = has ? ((kMarg && a.marg) ? HS_RES_IN : st_raw) : HS_RES_OOB;
+  const float oldE = (has && !(kMarg && a.marg)) ? oldE_raw : 0.f;
+  const float oldNewE = (has && !(kMarg && a.marg)) ? oldNewE_raw : 0.f;
 
   // Branch-free: every lane evaluates the whole chain (a wave's lanes diverge here anyway, so branches would run
   // both sides and re-materialise the zeroed values at every merge); the reference's early exits become the
@@ -473,7 +474,7 @@ __device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int 
     // marginalization pass addPoint<2> over res_toZeroF = resF - [JI Jp, Jab] delta
     // (fixLinearizationF, Src/OptimizationClasses.cpp:258-284)
     float rz = resF;
-    if (a.marg) {
+    if (kMarg && a.marg) {
       const float* dp = a.adHTdelta + (h + nF * t) * 8;
       float jx = 0.f, jy = 0.f, cxx = 0.f, cyy = 0.f;
 #pragma unroll
@@ -627,15 +628,15 @@ __device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int 
     if (mask != 0u) {
       // marginalization pass: priorF *= idepthFixPriorMargFac, the sums are the LF ones (AF = 0), and
       // AccumulatedSCHessianSSE::addPoint(p, shiftPriorToZero = false) (Src/EnergyFunctional.cpp:563,577)
-      const float priorF = a.marg ? in.priorF * a.margPriorFac : in.priorF;
-      float Hh = a.marg ? (0.f + Hdd) + priorF : Hdd + 0.f + priorF;  // Hdd_accAF + Hdd_accLF + priorF
+      const float priorF = (kMarg && a.marg) ? in.priorF * a.margPriorFac : in.priorF;
+      float Hh = (kMarg && a.marg) ? (0.f + Hdd) + priorF : Hdd + 0.f + priorF;  // Hdd_accAF + Hdd_accLF + priorF
       if ((double)Hh < 1e-10) Hh = (float)1e-10;
       HdiF = (float)(1.0 / (double)Hh);
-      bdSumF = a.marg ? 0.f + bd : bd + 0.f;
-      if (!a.marg) bdSumF += priorF * (idep - idep0);
+      bdSumF = (kMarg && a.marg) ? 0.f + bd : bd + 0.f;
+      if (!(kMarg && a.marg)) bdSumF += priorF * (idep - idep0);
     }
     float4 hc4;
-    if (a.marg) hc4 = make_float4(0.f + Hcd[0], 0.f + Hcd[1], 0.f + Hcd[2], 0.f + Hcd[3]);
+    if (kMarg && a.marg) hc4 = make_float4(0.f + Hcd[0], 0.f + Hcd[1], 0.f + Hcd[2], 0.f + Hcd[3]);
     else hc4 = make_float4(Hcd[0] + 0.f, Hcd[1] + 0.f, Hcd[2] + 0.f, Hcd[3] + 0.f);
     if (lane == 0) {
       a.p_actmask[p] = (uint8_t)mask;
@@ -785,7 +786,7 @@ __device__ __forceinline__ void acc_point(LinAcc<kExact>& A, const LinPt& P, int
   A.np += 1.0;
 }
 
-template <bool kExact, bool kFix>
+template <bool kExact, bool kFix, bool kMarg = false>
 __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
   extern __shared__ float lin_stage[];  // [HS_LIN_NW waves][ne][64] fp32 partials, then [HS_LIN_NW][3] fp64 energies
   // the wave index as a scalar: the point index and everything per point then stays uniform (scalar loads,
@@ -848,7 +849,7 @@ __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
     // the wave's only point (the 2k headline: one point per wave): no loop, so nothing is hoisted out of one and
     // kept live (spilled) across the point's work
     LinPt P;
-    lin_point<kFix>(a, pb + wv, h, lane, cur, K, ws, P);
+    lin_point<kFix, kMarg>(a, pb + wv, h, lane, cur, K, ws, P);
     if (a.accumulate) acc_point<kExact>(A, P, h, lane, ws);
   } else if (work) {
     for (int p = pb + wv; p < pe; p += a.W) {  // wave-uniform
@@ -856,7 +857,7 @@ __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
       if (p + a.W < pe) lin_load(a, p + a.W, lane, nxt);  // the next point's loads overlap this point's work
       else nxt = cur;  // last point of the wave (a wave-uniform branch): no duplicate loads
       LinPt P;
-      lin_point<kFix>(a, p, h, lane, cur, K, ws, P);
+      lin_point<kFix, kMarg>(a, p, h, lane, cur, K, ws, P);
       if (a.accumulate) acc_point<kExact>(A, P, h, lane, ws);
       cur = nxt;
     }
@@ -921,6 +922,8 @@ __global__ __launch_bounds__(HS_LIN_NT) void hs_k_lin(HsLinArgs a) { lin_block<f
 __global__ __launch_bounds__(HS_LIN_NT) void hs_k_lin_exact(HsLinArgs a) { lin_block<true, false>(a); }
 __global__ __launch_bounds__(HS_LIN_NT) void hs_k_lin_fix(HsLinArgs a) { lin_block<false, true>(a); }
 __global__ __launch_bounds__(HS_LIN_NT) void hs_k_lin_exact_fix(HsLinArgs a) { lin_block<true, true>(a); }
+__global__ __launch_bounds__(HS_LIN_NT) void hs_k_lin_marg(HsLinArgs a) { lin_block<false, false, true>(a); }
+__global__ __launch_bounds__(HS_LIN_NT) void hs_k_lin_exact_marg(HsLinArgs a) { lin_block<true, false, true>(a); }
 
 // =====================================================================================================
 // reduce + stitch: (host, chunk) blocks sum the host's block partials in block order; the last chunk block of a
