@@ -442,7 +442,8 @@ static int launch_linearize(hs_ctx* c, int fuse, bool marg = false, bool accumul
       hipLaunchKernelGGL(hs_k_lin8, dim3(c->nblk), dim3(HS_LIN8_NT), 0, c->stream, a);
     } else {
       auto k = marg ? (c->exact ? hs_k_lin_exact_marg : hs_k_lin_marg)
-                    : c->exact ? (fix ? hs_k_lin_exact_fix : hs_k_lin_exact) : (fix ? hs_k_lin_fix : hs_k_lin);
+                    : c->exact ? (fix ? hs_k_lin_exact_fix : hs_k_lin_exact)
+                    : fix ? hs_k_lin_fix : (fuse && !a.trace) ? hs_k_lin : hs_k_lin_gen;
       hipLaunchKernelGGL(k, dim3(c->nblk), dim3(HS_LIN_NT), lin_lds(c), c->stream, a);
     }
   }

@@ -269,9 +269,12 @@ static_assert(LW_SUM % 4 == 0 && LW_JJ % 4 == 0, "16 B aligned scratch rows");
 static_assert(LW_FLOATS <= hs_ne(false) * 64, "lin scratch fits the wave's partials area");
 
 // kMarg: the marginalization pass (hs_k_lin_marg*): production launches compile its branches and arguments out
-template <bool kFix, bool kMarg>
+// kProd: the production launch (hs_k_lin): the fused point step on, no trace -- both compile-time, so their
+// branches and arguments leave the kernel (hs_k_lin_gen keeps them at run time)
+template <bool kFix, bool kMarg, bool kProd>
 __device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int lane, const LinIn& in,
                                           const LinConst& K, float* ws, LinPt& o) {
+  long long* const trc = kProd ? nullptr : a.trace;
   const int t = lane >> 3;  // target slot
   const int k = lane & 7;   // pattern pixel
   const int nF = a.nF;
@@ -321,7 +324,7 @@ __device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int 
   const float bds = in.bds, hdi = in.hdi;
   const float4 hcd = in.hcd;
   const float cs0 = K.cs[0], cs1 = K.cs[1], cs2 = K.cs[2], cs3 = K.cs[3];
-  if (a.fuse_step) {
+  if (kProd || a.fuse_step) {
     // resubstituteFPt of the previous linearization + the point part of doStepFromBackup (stepfacD = 1).
     // Lane (t, k) forms xAd[h][t][k] * JpJdF[t][k]; the 8-term dot of a residual is an in-order octet fold, the
     // residual terms are then subtracted in list order (uniform).
@@ -442,7 +445,7 @@ __device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int 
     const bool okP = okC && (PKu > 1.1f && PKv > 1.1f && PKu < (cal.W - 3) && PKv < (cal.H - 3));
     float3 hit = LIN_TEXEL12 ? interp33p(timg3, okP ? PKu : 2.f, okP ? PKv : 2.f, cal.W)
                              : interp33(timg, okP ? PKu : 2.f, okP ? PKv : 2.f, cal.W);
-    if (a.trace && threadIdx.x == 0 && hit.x != -12345.f) a.trace[(size_t)blockIdx.x * 16 + 13] = wall_clock64();
+    if (trc && threadIdx.x == 0 && hit.x != -12345.f) trc[(size_t)blockIdx.x * 16 + 13] = wall_clock64();
     const float color = colorK;
     const float residual = hit.x - (float)(pc.aff[0] * color + pc.aff[1]);
     const float drdA = (color - pc.b0);
@@ -549,7 +552,7 @@ __device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int 
     }
     S[16] = ss[t * LW_SS + 16];
   }
-  if (a.trace && threadIdx.x == 0 && S[0] != -12345.f) a.trace[(size_t)blockIdx.x * 16 + 14] = wall_clock64();
+  if (trc && threadIdx.x == 0 && S[0] != -12345.f) trc[(size_t)blockIdx.x * 16 + 14] = wall_clock64();
 
   // ---------------- state decision + applyRes (the 8 lanes of a slot agree; lane k == 0 writes)
   const bool live = has && st != HS_RES_OOB;      // OOB is sticky: linearize returns state_energy
@@ -674,7 +677,7 @@ __device__ __forceinline__ void lin_point(const HsLinArgs& a, int p, int h, int 
     o.Hcd[0] = hc4.x; o.Hcd[1] = hc4.y; o.Hcd[2] = hc4.z; o.Hcd[3] = hc4.w;
     o.eSum = eSum;
   }
-  if (a.trace && threadIdx.x == 0 && o.eSum != -12345.0) a.trace[(size_t)blockIdx.x * 16 + 15] = wall_clock64();
+  if (trc && threadIdx.x == 0 && o.eSum != -12345.0) trc[(size_t)blockIdx.x * 16 + 15] = wall_clock64();
 #pragma unroll
   for (int i = 0; i < 10; i++) {
     o.Jx[i] = Jx[i];
@@ -786,8 +789,9 @@ __device__ __forceinline__ void acc_point(LinAcc<kExact>& A, const LinPt& P, int
   A.np += 1.0;
 }
 
-template <bool kExact, bool kFix, bool kMarg = false>
+template <bool kExact, bool kFix, bool kMarg = false, bool kProd = false>
 __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
+  struct { long long* trace; } const T{kProd ? nullptr : a.trace};  // HS_TRACE's view
   extern __shared__ float lin_stage[];  // [HS_LIN_NW waves][ne][64] fp32 partials, then [HS_LIN_NW][3] fp64 energies
   // the wave index as a scalar: the point index and everything per point then stays uniform (scalar loads,
   // scalar branches) instead of being treated as divergent
@@ -800,7 +804,7 @@ __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
   const int nb = a.blk_begin[h + 1] - a.blk_begin[h], q = b - a.blk_begin[h];
   const int hb = a.host_begin[h], nh = a.host_begin[h + 1] - hb;
   const int pb = hb + (int)((long long)nh * q / nb), pe = hb + (int)((long long)nh * (q + 1) / nb);
-  HS_TRACE(a, 0);
+  HS_TRACE(T, 0);
   __shared__ LinConst K;
   {  // the block's constants: precalc records of host h (by target), thresholds, xAd[h][.][.], calib step
     const int nF = a.nF;
@@ -810,7 +814,7 @@ __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
     int* dst = reinterpret_cast<int*>(K.pre);
     for (int i = tid; i < nF * PW; i += HS_LIN_NT) dst[i] = src[i];
     if (tid < nF) K.th[tid] = a.frameTH[tid];
-    if (a.fuse_step && tid < nF * 8) {
+    if ((kProd || a.fuse_step) && tid < nF * 8) {
       // xAd[h][t][c] of the last solve (EnergyFunctional::resubstituteF_MT): the frame steps (float)lastX and the
       // fp32 adjoints of the pair, in the solve's summation order
       const int t = tid >> 3, c = tid & 7;
@@ -844,12 +848,12 @@ __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
   const bool work = wv < a.W && pb + wv < pe;
   if (work) lin_load(a, pb + wv, lane, cur);  // in flight across the barrier
   __syncthreads();
-  HS_TRACE(a, 12);
+  HS_TRACE(T, 12);
   if (work && LIN_ONE_PATH && pb + wv + a.W >= pe) {
     // the wave's only point (the 2k headline: one point per wave): no loop, so nothing is hoisted out of one and
     // kept live (spilled) across the point's work
     LinPt P;
-    lin_point<kFix, kMarg>(a, pb + wv, h, lane, cur, K, ws, P);
+    lin_point<kFix, kMarg, kProd>(a, pb + wv, h, lane, cur, K, ws, P);
     if (a.accumulate) acc_point<kExact>(A, P, h, lane, ws);
   } else if (work) {
     for (int p = pb + wv; p < pe; p += a.W) {  // wave-uniform
@@ -857,13 +861,13 @@ __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
       if (p + a.W < pe) lin_load(a, p + a.W, lane, nxt);  // the next point's loads overlap this point's work
       else nxt = cur;  // last point of the wave (a wave-uniform branch): no duplicate loads
       LinPt P;
-      lin_point<kFix, kMarg>(a, p, h, lane, cur, K, ws, P);
+      lin_point<kFix, kMarg, kProd>(a, p, h, lane, cur, K, ws, P);
       if (a.accumulate) acc_point<kExact>(A, P, h, lane, ws);
       cur = nxt;
     }
   }
-  HS_TRACE(a, 1);
-  if (a.trace && lane == 0) a.trace[(size_t)blockIdx.x * 16 + 4 + wv] = wall_clock64();  // each wave's finish
+  HS_TRACE(T, 1);
+  if (T.trace && lane == 0) T.trace[(size_t)blockIdx.x * 16 + 4 + wv] = wall_clock64();  // each wave's finish
   if (!a.accumulate) return;
   // the waves' partials, summed in wave order (fp32) into the block partial; the energies in fp64
   constexpr int NE = hs_ne(kExact);
@@ -882,7 +886,7 @@ __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
     se[wv * 3 + 2] = A.np;
   }
   __syncthreads();
-  HS_TRACE(a, 3);
+  HS_TRACE(T, 3);
   // 16 B per thread and step, every wave's value loaded before the in-order sum (a runtime-bound loop would wait
   // for each LDS load in turn); waves past W hold no points and are not added
   static_assert((NE * 64) % 4 == 0, "partials staged as float4");
@@ -914,11 +918,12 @@ __device__ __forceinline__ void lin_block(const HsLinArgs& a) {
     for (int w = 1; w < a.W; w++) s += se[w * 3 + tid];
     a.part_e[(size_t)b * 4 + tid] = s;
   }
-  HS_TRACE(a, 2);
+  HS_TRACE(T, 2);
 }
 }  // namespace
 
-__global__ __launch_bounds__(HS_LIN_NT) void hs_k_lin(HsLinArgs a) { lin_block<false, false>(a); }
+__global__ __launch_bounds__(HS_LIN_NT) void hs_k_lin(HsLinArgs a) { lin_block<false, false, false, true>(a); }
+__global__ __launch_bounds__(HS_LIN_NT) void hs_k_lin_gen(HsLinArgs a) { lin_block<false, false>(a); }
 __global__ __launch_bounds__(HS_LIN_NT) void hs_k_lin_exact(HsLinArgs a) { lin_block<true, false>(a); }
 __global__ __launch_bounds__(HS_LIN_NT) void hs_k_lin_fix(HsLinArgs a) { lin_block<false, true>(a); }
 __global__ __launch_bounds__(HS_LIN_NT) void hs_k_lin_exact_fix(HsLinArgs a) { lin_block<true, true>(a); }

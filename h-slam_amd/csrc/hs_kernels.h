@@ -235,6 +235,7 @@ __global__ void hs_k_lin(HsLinArgs a);        // production partitioning
 __global__ void hs_k_lin_exact(HsLinArgs a);  // HS_ACC_EXACT: one wave per host, the reference's sums
 __global__ void hs_k_lin_fix(HsLinArgs a);        // + linearizeAll(true)'s per-point bookkeeping
 __global__ void hs_k_lin_exact_fix(HsLinArgs a);
+__global__ void hs_k_lin_gen(HsLinArgs a);         // hs_k_lin with the point step and the trace as run-time flags
 __global__ void hs_k_lin_marg(HsLinArgs a);        // the marginalization pass (HsLinArgs.marg set)
 __global__ void hs_k_lin_exact_marg(HsLinArgs a);
 __global__ void hs_k_lin8(HsLinArgs a);       // production: lane = (point, target slot), 8 points per wave
