@@ -2638,8 +2638,8 @@ __global__ void hs_k_marg_update(const double* sep, const double* sep_aux, doubl
 
 // fix = 1: the optimize tail's setEvalPT of the newest frame first; then (both) every frame pair's precalc and
 // adjoints (System::setPrecalcValues, EnergyFunctional::setAdjointsF) from the device state
-__global__ void hs_k_fix_frames(HsDevState* st, HsPrecalc* pre, double* adH, double* adT, float* adHF, float* adTF,
-                                hs_params P, int fix) {
+__global__ __launch_bounds__(64) void hs_k_fix_frames(HsDevState* st, HsPrecalc* pre, double* adH, double* adT,
+                                                      float* adHF, float* adTF, hs_params P, int fix) {
   const int nF = st->nF, tid = threadIdx.x;
   if (fix && tid == 0) {  // newStateZero = 0 except segment(6, 2) = the newest frame's a / b; setEvalPT(PRE_worldToCam, .)
     hs::FrameH& f = st->frames[nF - 1];
