@@ -289,18 +289,13 @@ def bench_track(args):
     minRes = np.full(5, np.nan)
     for _ in range(max(1, args.warmup)):
         ct.trackNewestCoarse(T0, [0.0, 0.0], s.n_levels - 1, minRes)
-    # the timed loop without the library's per-call event pair (instrumentation, ~3-4 us of host time per call);
-    # the device time per track from an untimed loop with it afterwards
-    noevt = os.environ.get("HS_TRK_NOEVT")
-    os.environ["HS_TRK_NOEVT"] = "1"
+    # the timed loop in the library's default mode (no per-call event pair: the host takes the results from the
+    # hypotheses' done words); the device time per track from an untimed loop with event timing on afterwards
     t0 = time.perf_counter()
     for _ in range(args.steps):
         ok, T, a = ct.trackNewestCoarse(T0, [0.0, 0.0], s.n_levels - 1, minRes)
     dt = time.perf_counter() - t0
-    if noevt is None:
-        os.environ.pop("HS_TRK_NOEVT")
-    else:
-        os.environ["HS_TRK_NOEVT"] = noevt
+    ct.set_event_timing(True)
     dev = 0.0
     for _ in range(args.steps):
         ct.trackNewestCoarse(T0, [0.0, 0.0], s.n_levels - 1, minRes)
@@ -320,8 +315,9 @@ def bench_track(args):
         "config": {"workload": "C2 (BASELINE.json configs[1]): trackNewestCoarse from identity, 2000 reference "
                                "points, 640x480, 5 levels", "ok": bool(ok), "device_ms_per_track": dev_ms,
                    "passes": passes, "point_passes": point_passes,
-                   "timing": "value / ms_per_step: host clock over the timed loop, the library's per-call event pair "
-                             "off (HS_TRK_NOEVT); device_ms_per_track: that event pair, in an untimed loop after it"},
+                   "timing": "value / ms_per_step: host clock over the timed loop in the library's default mode "
+                             "(no per-call event pair, done-word results); device_ms_per_track: the event pair "
+                             "(hs_tracker_set_event_timing), in an untimed loop after it"},
         "roofline": {"bound": "hbm", "kernel": "hs_k_track", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": pmc_roof("track", "hs_k_track").get("hbm_bytes_per_launch",

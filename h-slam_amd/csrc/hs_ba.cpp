@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "hs_ba_ctx.h"
@@ -56,7 +57,7 @@ static void free_buffers(hs_ctx* c) {
       c->d_hostsum, c->d_sys, c->d_sep, c->d_adHost, c->d_adTarget, c->d_adHostF, c->d_adTargetF, c->d_HM, c->d_bM,
       c->d_Nproj, c->d_xAd, c->d_x, c->d_elog, c->d_cand, c->d_tr_lin, c->d_tr_acc, c->d_tr_solve, c->d_tr_st,
       c->d_marg, c->d_adHTdelta, c->d_p_HdiF_alt, c->d_th_hist, c->d_th_hist2, c->d_th_surv, c->d_th_nsurv,
-      c->d_le_chunk, c->d_le_out, c->d_ref_pts, c->d_ref_n, c->d_stage, c->d_gsys, c->d_sep_aux};
+      c->d_le_chunk, c->d_le_out, c->d_ref_pts, c->d_ref_n, c->d_stage, c->d_gsys, c->d_sep_aux, c->d_ticket};
   for (auto& s : c->ps) {
     for (void* p : {(void*)s.u, (void*)s.v, (void*)s.idepth, (void*)s.idepth_zero, (void*)s.priorF, (void*)s.color,
                     (void*)s.weight, (void*)s.relBL, (void*)s.nGood, (void*)s.r_state, (void*)s.r_center})
@@ -94,6 +95,7 @@ static void free_buffers(hs_ctx* c) {
   c->d_stage = nullptr;
   c->d_gsys = nullptr;
   c->d_sep_aux = nullptr;
+  c->d_ticket = nullptr;
   c->gath_pending = c->gath_th = false;
   c->d_stage_cap = 0;
   c->cap_P = c->cap_blk = c->cap_W = c->cap_H = c->cap_stride = 0;
@@ -111,6 +113,53 @@ void bind_point_set(hs_ctx* c) {
   c->d_r_state = s.r_state; c->d_r_center = s.r_center;
 }
 
+// the communicator is aborted off the calling thread (ncclCommAbort releases the collectives still spinning on the
+// stream, and its frees wait for the device): the call returns HS_ERR_RCCL at once; hs_destroy joins the abort
+int comm_fail(hs_ctx* c, const std::string& msg) {
+  if (c->comm) {
+    ncclComm_t cm = c->comm;
+    const int dev = c->device;
+    c->comm = nullptr;
+    c->abort_thread = std::thread([cm, dev] {
+      (void)hipSetDevice(dev);
+      (void)ncclCommAbort(cm);
+    });
+  }
+  c->comm_lost = true;
+  return fail(HS_ERR_RCCL, msg);
+}
+
+int wait_stream(hs_ctx* c) {
+  if (!c->comm) {
+    if (c->comm_lost) return fail(HS_ERR_RCCL, "communicator aborted by an earlier call");
+    HS_HIP(hipStreamSynchronize(c->stream));
+    return HS_OK;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t q = hipStreamQuery(c->stream);
+    if (q == hipSuccess) return HS_OK;
+    if (q != hipErrorNotReady) return fail(HS_ERR_HIP, std::string("hipStreamQuery: ") + hipGetErrorString(q));
+    ncclResult_t ar = ncclSuccess;
+    const ncclResult_t r = ncclCommGetAsyncError(c->comm, &ar);
+    if (r != ncclSuccess) return comm_fail(c, std::string("ncclCommGetAsyncError: ") + ncclGetErrorString(r));
+    if (ar != ncclSuccess && ar != ncclInProgress)
+      return comm_fail(c, std::string("collective failed: ") + ncclGetErrorString(ar));
+    const auto el = std::chrono::steady_clock::now() - t0;
+    if (el > std::chrono::milliseconds(c->comm_timeout_ms))
+      return comm_fail(c, "collective did not complete within " + std::to_string(c->comm_timeout_ms) +
+                              " ms (a peer rank stalled or died); communicator aborted");
+    if (el > std::chrono::microseconds(200)) std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
+
+int status_error(int status) {
+  if (status & HS_STATUS_STALE)
+    return fail(HS_ERR_STATE, "stale frame adjoints: the stamp of the last upload did not reach the device buffers");
+  if (status) return fail(HS_ERR_NONFINITE, "non-finite GN step");
+  return HS_OK;
+}
+
 // candidate-buffer stride: the same on every rank (max point count over the ranks; one small all-reduce)
 int cand_stride_for(hs_ctx* c, int nP, int* stride) {
   int s = nP > 0 ? nP : 1;
@@ -119,12 +168,16 @@ int cand_stride_for(hs_ctx* c, int nP, int* stride) {
     s = c->group_stride;
   } else if (c->comm) {
     int* d_tmp = nullptr;
-    HS_TRY(dalloc(&d_tmp, 1));
-    HS_HIP(hipMemcpy(d_tmp, &s, sizeof(int), hipMemcpyHostToDevice));
+    HS_TRY(dalloc(&d_tmp, 1, c->stream));
+    // every step on the context's stream (a null-stream copy would not order against it); h_ctl[6]: pinned scratch
+    c->h_ctl[6] = s;
+    HS_HIP(hipMemcpyAsync(d_tmp, &c->h_ctl[6], sizeof(int), hipMemcpyHostToDevice, c->stream));
     HS_NCCL(ncclAllReduce(d_tmp, d_tmp, 1, ncclInt, ncclMax, c->comm, c->stream));
-    HS_HIP(hipStreamSynchronize(c->stream));
-    HS_HIP(hipMemcpy(&s, d_tmp, sizeof(int), hipMemcpyDeviceToHost));
+    HS_HIP(hipMemcpyAsync(&c->h_ctl[6], d_tmp, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    const int rc = wait_stream(c);
     (void)hipFree(d_tmp);
+    if (rc != HS_OK) return rc;
+    s = c->h_ctl[6];
   }
   *stride = s;
   return HS_OK;
@@ -137,73 +190,75 @@ int ensure_capacity(hs_ctx* c, int W, int H, int capP, int capBlk) {
   capP = std::max(capP, 1);
   capBlk = std::max(capBlk, 1);
   if (c->d_state && W == c->cap_W && H == c->cap_H && capP <= c->cap_P && capBlk <= c->cap_blk) return HS_OK;
-  HS_HIP(hipStreamSynchronize(c->stream));
+  HS_TRY(wait_stream(c));
   free_buffers(c);
   const size_t npx = (size_t)W * H, P8 = (size_t)capP * 8;
   const int nmax = HS_MAXDIM, SLmax = nmax * nmax + nmax, ne = hs_ne(true), FF = HS_MAXF * HS_MAXF;
-  HS_TRY(dalloc(&c->d_img_all, npx * HS_MAXF));
-  HS_TRY(dalloc(&c->d_img3, npx * HS_MAXF * 3));
+  HS_TRY(dalloc(&c->d_img_all, npx * HS_MAXF, c->stream));
+  HS_TRY(dalloc(&c->d_img3, npx * HS_MAXF * 3, c->stream));
   c->img_px = npx;
-  HS_TRY(dalloc(&c->d_state, 1));
-  HS_TRY(dalloc(&c->d_pre, FF));
-  HS_TRY(dalloc(&c->d_frameTH, HS_MAXF));
+  HS_TRY(dalloc(&c->d_state, 1, c->stream));
+  HS_TRY(dalloc(&c->d_pre, FF, c->stream));
+  HS_TRY(dalloc(&c->d_frameTH, HS_MAXF, c->stream));
   for (auto& s : c->ps) {
-    HS_TRY(dalloc(&s.u, capP)); HS_TRY(dalloc(&s.v, capP));
-    HS_TRY(dalloc(&s.idepth, capP)); HS_TRY(dalloc(&s.idepth_zero, capP)); HS_TRY(dalloc(&s.priorF, capP));
-    HS_TRY(dalloc(&s.color, P8)); HS_TRY(dalloc(&s.weight, P8));
-    HS_TRY(dalloc(&s.relBL, capP)); HS_TRY(dalloc(&s.nGood, capP));
-    HS_TRY(dalloc(&s.r_state, P8)); HS_TRY(dalloc(&s.r_center, P8 * 3));
+    HS_TRY(dalloc(&s.u, capP, c->stream)); HS_TRY(dalloc(&s.v, capP, c->stream));
+    HS_TRY(dalloc(&s.idepth, capP, c->stream)); HS_TRY(dalloc(&s.idepth_zero, capP, c->stream)); HS_TRY(dalloc(&s.priorF, capP, c->stream));
+    HS_TRY(dalloc(&s.color, P8, c->stream)); HS_TRY(dalloc(&s.weight, P8, c->stream));
+    HS_TRY(dalloc(&s.relBL, capP, c->stream)); HS_TRY(dalloc(&s.nGood, capP, c->stream));
+    HS_TRY(dalloc(&s.r_state, P8, c->stream)); HS_TRY(dalloc(&s.r_center, P8 * 3, c->stream));
   }
   c->cur = 0;
-  HS_TRY(dalloc(&c->d_res_of_slot, P8)); HS_TRY(dalloc(&c->d_res_order, P8));
-  HS_TRY(dalloc(&c->d_pt_host, capP)); HS_TRY(dalloc(&c->d_host_pt_begin, HS_MAXF + 1));
+  HS_TRY(dalloc(&c->d_res_of_slot, P8, c->stream)); HS_TRY(dalloc(&c->d_res_order, P8, c->stream));
+  HS_TRY(dalloc(&c->d_pt_host, capP, c->stream)); HS_TRY(dalloc(&c->d_host_pt_begin, HS_MAXF + 1, c->stream));
   // residual state in the slot layout [point][target slot] (P8 entries; slots without a residual unused)
-  HS_TRY(dalloc(&c->d_r_active, P8));
-  HS_TRY(dalloc(&c->d_r_energy, P8)); HS_TRY(dalloc(&c->d_r_newEnergy, P8)); HS_TRY(dalloc(&c->d_r_ewo, P8));
-  HS_TRY(dalloc(&c->d_p_actmask, capP)); HS_TRY(dalloc(&c->d_p_HdiF, capP)); HS_TRY(dalloc(&c->d_p_bdSumF, capP));
-  HS_TRY(dalloc(&c->d_p_Hcd, (size_t)capP * 4)); HS_TRY(dalloc(&c->d_p_JpJdF, P8 * 8));
-  HS_TRY(dalloc(&c->d_p_step, capP)); HS_TRY(dalloc(&c->d_p_HdiF_alt, capP));
+  HS_TRY(dalloc(&c->d_r_active, P8, c->stream));
+  HS_TRY(dalloc(&c->d_r_energy, P8, c->stream)); HS_TRY(dalloc(&c->d_r_newEnergy, P8, c->stream)); HS_TRY(dalloc(&c->d_r_ewo, P8, c->stream));
+  HS_TRY(dalloc(&c->d_p_actmask, capP, c->stream)); HS_TRY(dalloc(&c->d_p_HdiF, capP, c->stream)); HS_TRY(dalloc(&c->d_p_bdSumF, capP, c->stream));
+  HS_TRY(dalloc(&c->d_p_Hcd, (size_t)capP * 4, c->stream)); HS_TRY(dalloc(&c->d_p_JpJdF, P8 * 8, c->stream));
+  HS_TRY(dalloc(&c->d_p_step, capP, c->stream)); HS_TRY(dalloc(&c->d_p_HdiF_alt, capP, c->stream));
   c->hdif_solved = c->d_p_HdiF;
-  HS_TRY(dalloc(&c->d_part, (size_t)capBlk * ne * 64));
-  HS_TRY(dalloc(&c->d_part_e, (size_t)capBlk * 4));
-  HS_TRY(dalloc(&c->d_hostsum, (size_t)HS_MAXF * ne * 64));
-  HS_TRY(dalloc(&c->d_sys, (size_t)SLmax + 3 + HS_MAXF * 64));
-  HS_TRY(dalloc(&c->d_sep, (size_t)2 * SLmax));
-  HS_TRY(dalloc(&c->d_sep_aux, (size_t)HS_MAXF * 64));
-  HS_TRY(dalloc(&c->d_adHost, FF * 64)); HS_TRY(dalloc(&c->d_adTarget, FF * 64));
-  HS_TRY(dalloc(&c->d_adHostF, FF * 64)); HS_TRY(dalloc(&c->d_adTargetF, FF * 64));
-  HS_TRY(dalloc(&c->d_HM, (size_t)nmax * nmax)); HS_TRY(dalloc(&c->d_bM, nmax));
-  HS_TRY(dalloc(&c->d_Nproj, (size_t)2 * nmax * HS_NNS));
-  HS_TRY(dalloc(&c->d_xAd, FF * 8)); HS_TRY(dalloc(&c->d_x, nmax)); HS_TRY(dalloc(&c->d_elog, kLogCap));
+  HS_TRY(dalloc(&c->d_part, (size_t)capBlk * ne * 64, c->stream));
+  HS_TRY(dalloc(&c->d_part_e, (size_t)capBlk * 4, c->stream));
+  HS_TRY(dalloc(&c->d_hostsum, (size_t)HS_MAXF * ne * 64, c->stream));
+  HS_TRY(dalloc(&c->d_sys, (size_t)SLmax + 3 + HS_MAXF * 64, c->stream));
+  HS_TRY(dalloc(&c->d_sep, (size_t)2 * SLmax, c->stream));
+  HS_TRY(dalloc(&c->d_sep_aux, (size_t)HS_MAXF * 64, c->stream));
+  // the adjoints + one stamp word each (HS_ADJ_STAMP: hs_k_fix_frames' upload sequence, checked by their readers)
+  HS_TRY(dalloc(&c->d_adHost, FF * 64 + 1, c->stream)); HS_TRY(dalloc(&c->d_adTarget, FF * 64 + 1, c->stream));
+  HS_TRY(dalloc(&c->d_adHostF, FF * 64 + 1, c->stream)); HS_TRY(dalloc(&c->d_adTargetF, FF * 64 + 1, c->stream));
+  HS_TRY(dalloc(&c->d_HM, (size_t)nmax * nmax, c->stream)); HS_TRY(dalloc(&c->d_bM, nmax, c->stream));
+  HS_TRY(dalloc(&c->d_Nproj, (size_t)2 * nmax * HS_NNS, c->stream));
+  HS_TRY(dalloc(&c->d_xAd, FF * 8, c->stream)); HS_TRY(dalloc(&c->d_x, nmax, c->stream)); HS_TRY(dalloc(&c->d_elog, kLogCap, c->stream));
   int stride = capP;
   HS_TRY(cand_stride_for(c, capP, &stride));
   c->cap_stride = stride;
-  HS_TRY(dalloc(&c->d_cand, (size_t)stride * c->nranks));
-  HS_HIP(hipMemset(c->d_cand, 0xff, sizeof(float) * (size_t)stride * c->nranks));  // NaN, sign set: no candidate
-  if (c->multi_rank()) HS_TRY(dalloc(&c->d_gsys, ((size_t)SLmax + 3 + HS_MAXF * 64) * c->nranks));
-  HS_TRY(dalloc(&c->d_th_hist, HS_TH_BINS));
-  HS_TRY(dalloc(&c->d_th_hist2, 1024));
-  HS_TRY(dalloc(&c->d_th_nsurv, 2));
-  HS_TRY(dalloc(&c->d_th_surv, HS_TH_SURV));
-  HS_TRY(dalloc(&c->d_marg, capP));
-  HS_TRY(dalloc(&c->d_adHTdelta, FF * 8 + 4));  // + cDeltaF
-  HS_TRY(dalloc(&c->d_le_chunk, (size_t)(capP + 49) / 50));
-  HS_TRY(dalloc(&c->d_le_out, 1));
-  HS_TRY(dalloc(&c->d_ref_pts, (size_t)4 * capP));
-  HS_TRY(dalloc(&c->d_ref_n, 1));
+  HS_TRY(dalloc(&c->d_cand, (size_t)stride * c->nranks, c->stream));
+  HS_HIP(hipMemsetAsync(c->d_cand, 0xff, sizeof(float) * (size_t)stride * c->nranks, c->stream));  // NaN: none
+  if (c->multi_rank()) HS_TRY(dalloc(&c->d_gsys, ((size_t)SLmax + 3 + HS_MAXF * 64) * c->nranks, c->stream));
+  HS_TRY(dalloc(&c->d_th_hist, HS_TH_BINS, c->stream));
+  HS_TRY(dalloc(&c->d_th_hist2, 1024, c->stream));
+  HS_TRY(dalloc(&c->d_th_nsurv, 2, c->stream));
+  HS_TRY(dalloc(&c->d_th_surv, HS_TH_SURV, c->stream));
+  HS_TRY(dalloc(&c->d_marg, capP, c->stream));
+  HS_TRY(dalloc(&c->d_adHTdelta, FF * 8 + 4, c->stream));  // + cDeltaF
+  HS_TRY(dalloc(&c->d_le_chunk, (size_t)(capP + 49) / 50, c->stream));
+  HS_TRY(dalloc(&c->d_le_out, 1, c->stream));
+  HS_TRY(dalloc(&c->d_ref_pts, (size_t)4 * capP, c->stream));
+  HS_TRY(dalloc(&c->d_ref_n, 1, c->stream));
+  HS_TRY(dalloc(&c->d_ticket, 1, c->stream));
   // incremental window: the commit blob (pinned + device) and a raw level-0 image's staging
   c->h_stage_cap = c->d_stage_cap = stage_bytes(capP);
   HS_HIP(hipHostMalloc((void**)&c->h_stage, c->h_stage_cap));
-  HS_TRY(dalloc(&c->d_stage, c->d_stage_cap));
+  HS_TRY(dalloc(&c->d_stage, c->d_stage_cap, c->stream));
   HS_HIP(hipHostMalloc((void**)&c->h_raw, sizeof(float) * npx));
-  HS_TRY(dalloc(&c->d_raw, npx));
+  HS_TRY(dalloc(&c->d_raw, npx, c->stream));
   const char* tr = std::getenv("HS_KTRACE");
   c->tracing = tr && tr[0] == '1';
   if (c->tracing) {
-    HS_TRY(dalloc(&c->d_tr_lin, (size_t)capBlk * 16));
-    HS_TRY(dalloc(&c->d_tr_acc, (size_t)(HS_MAXF * ((ne * 64 + 255) / 256) + 1 + 64) * 16));
-    HS_TRY(dalloc(&c->d_tr_st, (size_t)(HS_MAXF * (HS_MAXF + 1) / 2 + 2 * HS_MAXF + 2 + 64) * 16));  // + np2 <= 64
-    HS_TRY(dalloc(&c->d_tr_solve, 32));
+    HS_TRY(dalloc(&c->d_tr_lin, (size_t)capBlk * 16, c->stream));
+    HS_TRY(dalloc(&c->d_tr_acc, (size_t)(HS_MAXF * ((ne * 64 + 255) / 256) + 1 + 64) * 16, c->stream));
+    HS_TRY(dalloc(&c->d_tr_st, (size_t)(HS_MAXF * (HS_MAXF + 1) / 2 + 2 * HS_MAXF + 2 + 64) * 16, c->stream));  // + np2 <= 64
+    HS_TRY(dalloc(&c->d_tr_solve, 32, c->stream));
   }
   c->cap_W = W; c->cap_H = H; c->cap_P = capP; c->cap_blk = capBlk;
   bind_point_set(c);
@@ -247,7 +302,7 @@ int fetch_state(hs_ctx* c) {
     HS_HIP(hipMemcpyAsync(c->HM.data(), c->d_HM, sizeof(double) * n * n, hipMemcpyDeviceToHost, c->stream));
     HS_HIP(hipMemcpyAsync(c->bM.data(), c->d_bM, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
   }
-  HS_HIP(hipStreamSynchronize(c->stream));
+  HS_TRY(wait_stream(c));
   c->hm_host_stale = false;
   c->h_state_valid = true;
   if (c->tail_pending) {
@@ -275,7 +330,7 @@ static int settle_projector(hs_ctx* c) {
   compute_projector(c);
   HS_HIP(hipMemcpyAsync(c->d_Nproj, c->Nproj.data(), sizeof(double) * 2 * c->dim() * HS_NNS, hipMemcpyHostToDevice,
                         c->stream));
-  HS_HIP(hipStreamSynchronize(c->stream));
+  HS_TRY(wait_stream(c));
   c->proj_stale = false;
   return HS_OK;
 }
@@ -288,7 +343,7 @@ int sync_hm(hs_ctx* c) {
   c->bM.resize(n);
   HS_HIP(hipMemcpyAsync(c->HM.data(), c->d_HM, sizeof(double) * n * n, hipMemcpyDeviceToHost, c->stream));
   HS_HIP(hipMemcpyAsync(c->bM.data(), c->d_bM, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
-  HS_HIP(hipStreamSynchronize(c->stream));
+  HS_TRY(wait_stream(c));
   c->hm_host_stale = false;
   return HS_OK;
 }
@@ -297,6 +352,12 @@ size_t fstage_bytes() {
   const int FF = HS_MAXF * HS_MAXF;
   return FF * sizeof(HsPrecalc) + (size_t)FF * 64 * (2 * sizeof(double) + 2 * sizeof(float)) +
          (size_t)2 * HS_MAXDIM * HS_NNS * sizeof(double);
+}
+
+// the stamp of a new adjoint upload; a captured graph holds the old sequence in its launch arguments, so it goes
+static unsigned int next_adj_seq(hs_ctx* c) {
+  drop_graph(c);
+  return ++c->adj_seq;
 }
 
 int wait_uploads(hs_ctx* c) {
@@ -328,7 +389,7 @@ int upload_frames(hs_ctx* c) {
   HS_HIP(hipEventRecord(c->ev_upload, c->stream));
   // the pairs' precalc and adjoints on the device from the uploaded state (the expressions of the host forms)
   hipLaunchKernelGGL(hs_k_fix_frames, dim3(1), dim3(64), 0, c->stream, c->d_state, c->d_pre, c->d_adHost,
-                     c->d_adTarget, c->d_adHostF, c->d_adTargetF, c->P, 0);
+                     c->d_adTarget, c->d_adHostF, c->d_adTargetF, c->P, 0, next_adj_seq(c));
   HS_HIP(hipGetLastError());
   c->h_state_valid = true;
   return HS_OK;
@@ -357,11 +418,12 @@ int make_partition(hs_ctx* c) {
   c->blk_begin.assign(nF + 1, 0);
   c->lin8 = !c->exact && nP >= kLin8MinPoints;
   if (const char* e = std::getenv("HS_LIN8")) c->lin8 = !c->exact && e[0] == '1';
+  c->lin8 = c->lin8 && lin8_supported(c->cap_W, c->cap_H);  // its 32-bit tap offsets
   // the extra launch of pass 3 costs more than a one-block scan of a small window's candidates
   c->th_multi = nP >= kThMultiMinPoints;
   if (const char* e = std::getenv("HS_TH_MULTI")) c->th_multi = e[0] == '1';
-  // points per block: hs_k_lin HS_LIN_NW waves x ppw points; hs_k_lin8 4 waves x ppw groups of 8 points (its
-  // partition also serves hs_k_lin's marginalization / linearizeAll(true) passes, with W = 4 of its waves)
+  // points per block: hs_k_lin HS_LIN_NW waves x ppw points; hs_k_lin8 HS_LIN8_NT / 64 = 8 waves x ppw groups of 8
+  // points (its partition also serves hs_k_lin's marginalization / linearizeAll(true) passes, with W = 8 waves)
   const int bw = c->lin8 ? (HS_LIN8_NT / 64) * 8 : HS_LIN_NW;
   int target = c->lin8 ? kLin8BlocksTarget : kLinBlocksTarget;
   if (const char* e = std::getenv("HS_LIN8_BLOCKS"); e && c->lin8) target = std::max(1, std::atoi(e));
@@ -577,8 +639,11 @@ static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = fals
     st.res_k = res_k;
     st.res_slot = kLogCap + 1;
     st.res_seq = res_seq;
+    st.res_ticket = c->d_ticket;
   }
-  hipLaunchKernelGGL(hs_k_stitch, dim3(nS + (res_seq ? 1 : 0)), dim3(HS_STITCH_NT), 0, c->stream, st);
+  st.status = reinterpret_cast<int*>((char*)c->d_state + offsetof(HsDevState, status));
+  st.adj_seq = c->adj_seq;
+  hipLaunchKernelGGL(hs_k_stitch, dim3(nS), dim3(HS_STITCH_NT), 0, c->stream, st);
   HS_HIP(hipGetLastError());
   if (multi) {  // pass 3: the select block over pass 2's histogram and survivors (a side stream measured no faster:
                 // its cross-queue event hand-offs cost what the overlap with the solve saves)
@@ -641,6 +706,8 @@ static int launch_solve(hs_ctx* c, int flags, int iteration, bool log) {
   a.thOptIterations = c->P.thOptIterations;
   a.brk = c->brk_active ? 1 : 0;
   a.minOpt = c->P.minOptIterations;
+  a.chk_adj = 1;
+  a.adj_seq = c->adj_seq;
   if (const char* e = std::getenv("HS_SOLVE_DBG")) a.dbg = std::atoi(e);
   hipLaunchKernelGGL(hs_k_solve, dim3(grid), dim3(HS_SOLVE_NT), 0, c->stream, a);
   HS_HIP(hipGetLastError());
@@ -843,7 +910,7 @@ static int gn_iterations(hs_ctx* c, int it0, int K, bool allow_break, double* en
       int cb = 0;
       HS_HIP(hipMemcpyAsync(&c->h_ctl[3], (char*)c->d_state + offsetof(HsDevState, canbreak), sizeof(int),
                             hipMemcpyDeviceToHost, c->stream));
-      HS_HIP(hipStreamSynchronize(c->stream));
+      HS_TRY(wait_stream(c));
       cb = c->h_ctl[3];
       if (cb && it0 + k >= c->P.minOptIterations) {
         k++;
@@ -858,6 +925,14 @@ static int gn_iterations(hs_ctx* c, int it0, int K, bool allow_break, double* en
   if (dev_brk) HS_TRY(launch_combine(c));  // the last linearization's deferred threshold select
   // read back: energy log (E of the linearizations consumed by each solve) + the last energy + status, written by
   // one small kernel straight into pinned host memory
+  if (c->dbg_stall_ms > 0) {  // test hook hs_debug_stall (one-shot)
+    int khz = 0;
+    HS_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device));
+    const long long ticks = (long long)c->dbg_stall_ms * (khz > 0 ? khz : 100000);
+    c->dbg_stall_ms = 0;
+    hipLaunchKernelGGL(hs_k_debug_stall, dim3(1), dim3(64), 0, c->stream, ticks);
+    HS_HIP(hipGetLastError());
+  }
   if (!fold_res) {
     hipLaunchKernelGGL(hs_k_result, dim3(1), dim3(256), 0, c->stream, c->d_elog, k, c->sysE(), c->d_state, c->d_res,
                        dev_brk ? 1 : 0, kLogCap + 1, seq);
@@ -871,15 +946,17 @@ static int gn_iterations(hs_ctx* c, int it0, int K, bool allow_break, double* en
     if (nev == 0) {
       const auto t_start = std::chrono::steady_clock::now();
       const unsigned long long* dw = reinterpret_cast<const unsigned long long*>(c->h_res + kLogCap + 2);
+      // a multi-rank context leaves the spin after 1 ms for wait_stream's bounded poll of the communicator
+      const auto bound = c->comm ? std::chrono::microseconds(1000) : std::chrono::microseconds(2000000);
       for (int spins = 0;; spins++) {
         if (__atomic_load_n(dw, __ATOMIC_ACQUIRE) == seq) {
           seen = true;
           break;
         }
-        if ((spins & 1023) == 1023 && std::chrono::steady_clock::now() - t_start > std::chrono::seconds(2)) break;
+        if ((spins & 1023) == 1023 && std::chrono::steady_clock::now() - t_start > bound) break;
       }
     }
-    if (!seen) HS_HIP(hipStreamSynchronize(c->stream));
+    if (!seen) HS_TRY(wait_stream(c));
   }
   if (dev_brk) {  // launch_linearize swapped the HdiF ping-pong for every launch; the skipped ones wrote nothing
     const int d = (int)c->h_res[kLogCap + 1];
@@ -908,7 +985,7 @@ static int gn_iterations(hs_ctx* c, int it0, int K, bool allow_break, double* en
   if (done) *done = k;
   if (energies_out)
     for (int q = 0; q < k; q++) energies_out[q] = elog[q + 1];
-  if (c->h_ctl[1] != 0) return fail(HS_ERR_NONFINITE, "non-finite GN step");
+  HS_TRY(status_error(c->h_ctl[1]));
   for (int q = 0; q <= k; q++)
     if (!std::isfinite(elog[q])) return fail(HS_ERR_NONFINITE, "non-finite energy (isLost)");
   return HS_OK;
@@ -948,6 +1025,7 @@ static int group_exchange(const std::vector<hs_ctx*>& g) {
 // every entry point that needs the device window: pending incremental edits are committed first
 static int begin_call(hs_ctx* c) {
   if (!c) return fail(HS_ERR_INVALID, "null context");
+  if (c->comm_lost) return fail(HS_ERR_RCCL, "communicator aborted by an earlier call (a peer rank failed)");
   HS_HIP(hipSetDevice(c->device));
   HS_TRY(commit_if_dirty(c));
   if (c->nF == 0) return fail(HS_ERR_STATE, "no window");
@@ -1035,6 +1113,7 @@ int hs_create(hs_ctx** out, const hs_params* params, int device_id) {
 void hs_destroy(hs_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
+  if (c->abort_thread.joinable()) c->abort_thread.join();  // an aborted communicator (comm_fail)
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   free_buffers(c);
   if (c->comm) ncclCommDestroy(c->comm);
@@ -1091,7 +1170,7 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
   if (cam->width < 8 || cam->height < 8) return fail(HS_ERR_INVALID, "bad camera size");
   if (pts->n < 0 || rs->n < 0) return fail(HS_ERR_INVALID, "negative counts");
   HS_HIP(hipSetDevice(c->device));
-  HS_HIP(hipStreamSynchronize(c->stream));
+  HS_TRY(wait_stream(c));
   drop_graph(c);
   const int nP = pts->n, nR = rs->n;
   // ---- validate and index the residual graph (host)
@@ -1194,7 +1273,7 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
     for (size_t i = 0; i < npx; i++) tex[i] = make_float4(src[3 * i], src[3 * i + 1], src[3 * i + 2], 0.f);
     HS_HIP(hipMemcpyAsync(c->d_img_all + (size_t)f * npx, tex.data(), npx * sizeof(float4), hipMemcpyHostToDevice,
                           c->stream));
-    HS_HIP(hipStreamSynchronize(c->stream));  // tex is reused
+    HS_TRY(wait_stream(c));  // tex is reused
     HS_TRY(pack_slot(c, f));
   }
   const size_t P8 = (size_t)nP * 8;
@@ -1203,32 +1282,34 @@ int hs_ba_set_window(hs_ctx* c, const hs_camera* cam, int nF, const hs_frame* fr
     prior[i] = (pts->has_depth_prior && pts->has_depth_prior[i]) ? c->P.idepthFixPrior * 1.0f * 1.0f : 0.f;
   std::vector<float> th(nF);
   for (int i = 0; i < nF; i++) th[i] = S.frames[i].frameEnergyTH;
-  HS_HIP(hipMemcpy(c->d_frameTH, th.data(), sizeof(float) * nF, hipMemcpyHostToDevice));
+  // stream-ordered copies from host vectors that live until the synchronize at the end
+  std::vector<uint8_t> slot_state;
+  HS_HIP(hipMemcpyAsync(c->d_frameTH, th.data(), sizeof(float) * nF, hipMemcpyHostToDevice, c->stream));
   if (nP > 0) {
-    HS_HIP(hipMemcpy(c->d_u, pts->u, sizeof(float) * nP, hipMemcpyHostToDevice));
-    HS_HIP(hipMemcpy(c->d_v, pts->v, sizeof(float) * nP, hipMemcpyHostToDevice));
-    HS_HIP(hipMemcpy(c->d_idepth, pts->idepth, sizeof(float) * nP, hipMemcpyHostToDevice));
-    HS_HIP(hipMemcpy(c->d_idepth_zero, pts->idepth_zero, sizeof(float) * nP, hipMemcpyHostToDevice));
-    HS_HIP(hipMemcpy(c->d_priorF, prior.data(), sizeof(float) * nP, hipMemcpyHostToDevice));
-    HS_HIP(hipMemcpy(c->d_color, pts->color, sizeof(float) * P8, hipMemcpyHostToDevice));
-    HS_HIP(hipMemcpy(c->d_weight, pts->weights, sizeof(float) * P8, hipMemcpyHostToDevice));
-    HS_HIP(hipMemcpy(c->d_res_of_slot, c->res_of_slot.data(), sizeof(int) * P8, hipMemcpyHostToDevice));
-    HS_HIP(hipMemcpy(c->d_res_order, c->res_order.data(), P8, hipMemcpyHostToDevice));
-    HS_HIP(hipMemcpy(c->d_pt_host, c->pt_host.data(), sizeof(int) * nP, hipMemcpyHostToDevice));
+    HS_HIP(hipMemcpyAsync(c->d_u, pts->u, sizeof(float) * nP, hipMemcpyHostToDevice, c->stream));
+    HS_HIP(hipMemcpyAsync(c->d_v, pts->v, sizeof(float) * nP, hipMemcpyHostToDevice, c->stream));
+    HS_HIP(hipMemcpyAsync(c->d_idepth, pts->idepth, sizeof(float) * nP, hipMemcpyHostToDevice, c->stream));
+    HS_HIP(hipMemcpyAsync(c->d_idepth_zero, pts->idepth_zero, sizeof(float) * nP, hipMemcpyHostToDevice, c->stream));
+    HS_HIP(hipMemcpyAsync(c->d_priorF, prior.data(), sizeof(float) * nP, hipMemcpyHostToDevice, c->stream));
+    HS_HIP(hipMemcpyAsync(c->d_color, pts->color, sizeof(float) * P8, hipMemcpyHostToDevice, c->stream));
+    HS_HIP(hipMemcpyAsync(c->d_weight, pts->weights, sizeof(float) * P8, hipMemcpyHostToDevice, c->stream));
+    HS_HIP(hipMemcpyAsync(c->d_res_of_slot, c->res_of_slot.data(), sizeof(int) * P8, hipMemcpyHostToDevice, c->stream));
+    HS_HIP(hipMemcpyAsync(c->d_res_order, c->res_order.data(), P8, hipMemcpyHostToDevice, c->stream));
+    HS_HIP(hipMemcpyAsync(c->d_pt_host, c->pt_host.data(), sizeof(int) * nP, hipMemcpyHostToDevice, c->stream));
   }
-  HS_HIP(hipMemcpy(c->d_host_pt_begin, c->host_pt_begin.data(), sizeof(int) * (nF + 1), hipMemcpyHostToDevice));
+  HS_HIP(hipMemcpyAsync(c->d_host_pt_begin, c->host_pt_begin.data(), sizeof(int) * (nF + 1), hipMemcpyHostToDevice, c->stream));
   if (nR > 0) {
     if (rs->state) {
-      std::vector<uint8_t> slot_state(P8, HS_RES_OOB);
+      slot_state.assign(P8, HS_RES_OOB);
       for (int r = 0; r < nR; r++) slot_state[(size_t)c->res_point[r] * 8 + c->res_target[r]] = rs->state[r];
-      HS_HIP(hipMemcpy(c->d_r_state, slot_state.data(), P8, hipMemcpyHostToDevice));
+      HS_HIP(hipMemcpyAsync(c->d_r_state, slot_state.data(), P8, hipMemcpyHostToDevice, c->stream));
     } else {
       HS_TRY(reset_states(c));
     }
   }
   c->pt_handle.resize(nP);
   for (int i = 0; i < nP; i++) c->pt_handle[i] = i;
-  HS_HIP(hipStreamSynchronize(c->stream));
+  HS_TRY(wait_stream(c));
   return HS_OK;
 }
 
@@ -1238,10 +1319,13 @@ int hs_ba_linearize(hs_ctx* c, int reset, double* energy_out) {
   HS_TRY(linearize_pass(c, reset != 0));
   double e = 0.0;
   HS_HIP(hipMemcpyAsync(&c->h_ctl[4], c->sysE(), sizeof(double), hipMemcpyDeviceToHost, c->stream));
-  HS_HIP(hipStreamSynchronize(c->stream));
+  HS_HIP(hipMemcpyAsync(&c->h_ctl[1], (char*)c->d_state + offsetof(HsDevState, status), sizeof(int),
+                        hipMemcpyDeviceToHost, c->stream));
+  HS_TRY(wait_stream(c));
   c->rb_pending = false;
   std::memcpy(&e, &c->h_ctl[4], sizeof(double));
   if (energy_out) *energy_out = e;
+  if (c->h_ctl[1] & HS_STATUS_STALE) return status_error(c->h_ctl[1]);
   if (!std::isfinite(e)) return fail(HS_ERR_NONFINITE, "non-finite energy (isLost)");
   return HS_OK;
 }
@@ -1265,9 +1349,9 @@ int hs_ba_solve_system(hs_ctx* c, int iteration, double* x_out) {
   HS_HIP(hipMemcpyAsync(x.data(), c->d_x, sizeof(double) * x.size(), hipMemcpyDeviceToHost, c->stream));
   HS_HIP(hipMemcpyAsync(&c->h_ctl[1], (char*)c->d_state + offsetof(HsDevState, status), sizeof(int),
                         hipMemcpyDeviceToHost, c->stream));
-  HS_HIP(hipStreamSynchronize(c->stream));
+  HS_TRY(wait_stream(c));
   if (x_out) std::memcpy(x_out, x.data(), sizeof(double) * x.size());
-  if (c->h_ctl[1] != 0) return fail(HS_ERR_NONFINITE, "non-finite GN step");
+  HS_TRY(status_error(c->h_ctl[1]));
   return HS_OK;
 }
 
@@ -1281,7 +1365,7 @@ int hs_ba_do_step(hs_ctx* c, int* canbreak_out) {
   HS_TRY(launch_solve(c, HS_APPLY, -1, false));
   HS_HIP(hipMemcpyAsync(&c->h_ctl[3], (char*)c->d_state + offsetof(HsDevState, canbreak), sizeof(int),
                         hipMemcpyDeviceToHost, c->stream));
-  HS_HIP(hipStreamSynchronize(c->stream));
+  HS_TRY(wait_stream(c));
   if (canbreak_out) *canbreak_out = c->h_ctl[3] ? 1 : 0;
   return HS_OK;
 }
@@ -1342,7 +1426,7 @@ int hs_ba_fix_linearization(hs_ctx* c, double* energy_out, uint8_t* drop_out, fl
   // the newest frame's setEvalPT + EnergyFunctional::setAdjointsF + setPrecalcValues, on the device (the nullspaces
   // and projector follow on the host when the state is next fetched)
   hipLaunchKernelGGL(hs_k_fix_frames, dim3(1), dim3(64), 0, c->stream, c->d_state, c->d_pre, c->d_adHost,
-                     c->d_adTarget, c->d_adHostF, c->d_adTargetF, c->P, 1);
+                     c->d_adTarget, c->d_adHostF, c->d_adTargetF, c->P, 1, next_adj_seq(c));
   HS_HIP(hipGetLastError());
   c->h_state_valid = false;
   c->tail_pending = true;
@@ -1365,8 +1449,11 @@ int hs_ba_fix_linearization(hs_ctx* c, double* energy_out, uint8_t* drop_out, fl
   const bool want_drop = drop_out && c->nR > 0;
   if (want_drop)
     HS_HIP(hipMemcpyAsync(h_act, c->d_r_active, (size_t)nP * 8, hipMemcpyDeviceToHost, c->stream));
-  HS_HIP(hipStreamSynchronize(c->stream));
+  HS_HIP(hipMemcpyAsync(&c->h_ctl[1], (char*)c->d_state + offsetof(HsDevState, status), sizeof(int),
+                        hipMemcpyDeviceToHost, c->stream));
+  HS_TRY(wait_stream(c));
   c->rb_pending = false;
+  if (c->h_ctl[1] & HS_STATUS_STALE) return status_error(c->h_ctl[1]);
   std::memcpy(&e, &c->h_ctl[4], sizeof(double));
   if (energy_out) *energy_out = e;
   if (HdiF_out && nP > 0) std::memcpy(HdiF_out, h_hdif, sizeof(float) * nP);
@@ -1406,7 +1493,7 @@ int hs_ba_get_system(hs_ctx* c, int which, double* H, double* b) {
     const int SL = c->SL();
     std::vector<double> sep((size_t)2 * SL);
     HS_HIP(hipMemcpyAsync(sep.data(), c->d_sep, sizeof(double) * sep.size(), hipMemcpyDeviceToHost, c->stream));
-    HS_HIP(hipStreamSynchronize(c->stream));
+    HS_TRY(wait_stream(c));
     if (which == 2) {  // HSC: the diagonal blocks' host-f Schur terms, formed in blocks of their own
       std::vector<double> aux((size_t)64 * nF);
       HS_HIP(hipMemcpy(aux.data(), c->d_sep_aux, sizeof(double) * aux.size(), hipMemcpyDeviceToHost));
@@ -1429,7 +1516,7 @@ int hs_ba_get_residuals(hs_ctx* c, uint8_t* state, uint8_t* active, float* energ
                         float* center) {
   HS_TRY(begin_call(c));
   HS_HIP(hipSetDevice(c->device));
-  HS_HIP(hipStreamSynchronize(c->stream));
+  HS_TRY(wait_stream(c));
   const size_t m = c->nR;
   if (m == 0) return HS_OK;
   // slot layout [point][target] -> residual order
@@ -1469,7 +1556,7 @@ int hs_ba_get_residuals(hs_ctx* c, uint8_t* state, uint8_t* active, float* energ
 int hs_ba_get_points(hs_ctx* c, float* idepth, float* step, float* HdiF, float* bdSumF) {
   HS_TRY(begin_call(c));
   HS_HIP(hipSetDevice(c->device));
-  HS_HIP(hipStreamSynchronize(c->stream));
+  HS_TRY(wait_stream(c));
   const size_t n = c->nP;
   if (n == 0) return HS_OK;
   if (idepth) HS_HIP(hipMemcpy(idepth, c->d_idepth, n * 4, hipMemcpyDeviceToHost));
@@ -1510,7 +1597,7 @@ int hs_ba_calc_energies(hs_ctx* c, double* energyL, double* energyM) {
                        c->d_priorF, c->d_le_chunk, c->d_le_out);
     HS_HIP(hipGetLastError());
     HS_HIP(hipMemcpyAsync(&c->h_ctl[4], c->d_le_out, sizeof(double), hipMemcpyDeviceToHost, c->stream));
-    HS_HIP(hipStreamSynchronize(c->stream));
+    HS_TRY(wait_stream(c));
     double ep = 0.0;
     std::memcpy(&ep, &c->h_ctl[4], sizeof(double));
     EL += ep;
@@ -1573,7 +1660,7 @@ int hs_ba_set_marginal_prior(hs_ctx* c, const double* HM, const double* bM) {
   drop_graph(c);  // the solve's arguments depend on hm_zero
   HS_HIP(hipMemcpyAsync(c->d_HM, c->HM.data(), sizeof(double) * n * n, hipMemcpyHostToDevice, c->stream));
   HS_HIP(hipMemcpyAsync(c->d_bM, c->bM.data(), sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
-  HS_HIP(hipStreamSynchronize(c->stream));
+  HS_TRY(wait_stream(c));
   return HS_OK;
 }
 
@@ -1817,7 +1904,7 @@ int hs_ba_group_linearize(hs_ctx** ctxs, int n, int reset, double* energy_out) {
   HS_TRY(group_exchange(g));
   double e = 0.0;
   HS_HIP(hipMemcpyAsync(&e, g[0]->sysE(), sizeof(double), hipMemcpyDeviceToHost, g[0]->stream));
-  for (hs_ctx* c : g) HS_HIP(hipStreamSynchronize(c->stream));
+  for (hs_ctx* c : g) HS_TRY(wait_stream(c));
   if (energy_out) *energy_out = e;
   return HS_OK;
 }
@@ -1843,7 +1930,7 @@ int hs_ba_group_iterate(hs_ctx** ctxs, int n, int first_iteration, int n_iters, 
   if (n_iters > 0)
     HS_HIP(hipMemcpyAsync(elog.data(), g[0]->d_elog, sizeof(double) * n_iters, hipMemcpyDeviceToHost, g[0]->stream));
   HS_HIP(hipMemcpyAsync(&elog[n_iters], g[0]->sysE(), sizeof(double), hipMemcpyDeviceToHost, g[0]->stream));
-  for (hs_ctx* c : g) HS_HIP(hipStreamSynchronize(c->stream));
+  for (hs_ctx* c : g) HS_TRY(wait_stream(c));
   if (energies_out)
     for (int q = 0; q < n_iters; q++) energies_out[q] = elog[q + 1];
   return HS_OK;
@@ -1868,6 +1955,12 @@ int hs_comm_init(hs_ctx* c, const char* id128, int rank, int nranks) {
   HS_NCCL(ncclCommInitRank(&c->comm, nranks, id, rank));
   c->rank = rank;
   c->nranks = nranks;
+  return HS_OK;
+}
+
+int hs_comm_set_timeout(hs_ctx* c, int timeout_ms) {
+  if (!c || timeout_ms < 1) return fail(HS_ERR_INVALID, "bad timeout");
+  c->comm_timeout_ms = timeout_ms;
   return HS_OK;
 }
 
@@ -1898,8 +1991,8 @@ extern "C" int hs_debug_threshold(const float* cand, int n, float thn, float fac
   float *d_c = nullptr, *d_th = nullptr;
   unsigned int *d_h = nullptr, *d_h2 = nullptr, *d_surv = nullptr, *d_ns = nullptr;
   double* d_e = nullptr;
-  HS_TRY(dalloc(&d_c, n)); HS_TRY(dalloc(&d_th, 1)); HS_TRY(dalloc(&d_h, HS_TH_BINS)); HS_TRY(dalloc(&d_e, 4));
-  HS_TRY(dalloc(&d_h2, 1024)); HS_TRY(dalloc(&d_surv, HS_TH_SURV)); HS_TRY(dalloc(&d_ns, 2));
+  HS_TRY(dalloc(&d_c, n, nullptr)); HS_TRY(dalloc(&d_th, 1, nullptr)); HS_TRY(dalloc(&d_h, HS_TH_BINS, nullptr)); HS_TRY(dalloc(&d_e, 4, nullptr));
+  HS_TRY(dalloc(&d_h2, 1024, nullptr)); HS_TRY(dalloc(&d_surv, HS_TH_SURV, nullptr)); HS_TRY(dalloc(&d_ns, 2, nullptr));
   HS_HIP(hipMemcpy(d_c, cand, sizeof(float) * n, hipMemcpyHostToDevice));
   HsRedArgs a;
   std::memset(&a, 0, sizeof(a));
@@ -1963,8 +2056,8 @@ extern "C" int hs_debug_se3(int on_device, int op, int n, const double* in14, do
     return HS_OK;
   }
   double *d_in = nullptr, *d_out = nullptr;
-  HS_TRY(dalloc(&d_in, (size_t)14 * n));
-  HS_TRY(dalloc(&d_out, (size_t)36 * n));
+  HS_TRY(dalloc(&d_in, (size_t)14 * n, nullptr));
+  HS_TRY(dalloc(&d_out, (size_t)36 * n, nullptr));
   HS_HIP(hipMemcpy(d_in, in14, sizeof(double) * 14 * n, hipMemcpyHostToDevice));
   hipLaunchKernelGGL(hs_k_debug_se3, dim3((n + 63) / 64), dim3(64), 0, 0, op, n, d_in, d_out);
   HS_HIP(hipGetLastError());
@@ -1978,9 +2071,9 @@ extern "C" int hs_debug_se3(int on_device, int op, int n, const double* in14, do
 extern "C" int hs_debug_fastmath(int n, const float* a, const float* b, float* out4) {
   if (n < 1 || !a || !b || !out4) return fail(HS_ERR_INVALID, "bad arguments");
   float *d_a = nullptr, *d_b = nullptr, *d_o = nullptr;
-  HS_TRY(dalloc(&d_a, (size_t)n));
-  HS_TRY(dalloc(&d_b, (size_t)n));
-  HS_TRY(dalloc(&d_o, (size_t)4 * n));
+  HS_TRY(dalloc(&d_a, (size_t)n, nullptr));
+  HS_TRY(dalloc(&d_b, (size_t)n, nullptr));
+  HS_TRY(dalloc(&d_o, (size_t)4 * n, nullptr));
   HS_HIP(hipMemcpy(d_a, a, sizeof(float) * n, hipMemcpyHostToDevice));
   HS_HIP(hipMemcpy(d_b, b, sizeof(float) * n, hipMemcpyHostToDevice));
   hipLaunchKernelGGL(hs_k_debug_fastmath, dim3((n + 255) / 256), dim3(256), 0, 0, n, d_a, d_b, d_o);
@@ -2003,7 +2096,7 @@ extern "C" int hs_debug_get_sysvec(hs_ctx* c, double* out, int raw) {
   const int SL = c->SL(), n = c->dim();
   std::vector<double> v((size_t)c->SX());
   HS_HIP(hipMemcpyAsync(v.data(), c->d_sys, sizeof(double) * v.size(), hipMemcpyDeviceToHost, c->stream));
-  HS_HIP(hipStreamSynchronize(c->stream));
+  HS_TRY(wait_stream(c));
   if (!raw) {
     const double sc = (double)(1.0f / (1 + 1e-5));
     const double* aux = v.data() + SL + 3;
@@ -2020,7 +2113,7 @@ extern "C" int hs_debug_get_candidates(hs_ctx* c, float* out, int* stride) {
   if (out)
     HS_HIP(hipMemcpyAsync(out, c->d_cand + (size_t)c->rank * c->cand_stride, sizeof(float) * c->cand_stride,
                           hipMemcpyDeviceToHost, c->stream));
-  HS_HIP(hipStreamSynchronize(c->stream));
+  HS_TRY(wait_stream(c));
   return HS_OK;
 }
 
@@ -2029,13 +2122,13 @@ extern "C" int hs_debug_stitch(int nF, int exact, const double* hostsum, const d
   if (nF < 1 || nF > HS_MAXF || !hostsum || !adH || !adT || !out) return fail(HS_ERR_INVALID, "bad args");
   const int n = 4 + 8 * nF, SL = n * n + n, ne = hs_ne(exact != 0);
   double *dh = nullptr, *da = nullptr, *dt = nullptr, *dout = nullptr, *dsep = nullptr, *dax = nullptr, *dax2 = nullptr;
-  HS_TRY(dalloc(&dax, (size_t)nF * 64));
-  HS_TRY(dalloc(&dax2, (size_t)nF * 64));
-  HS_TRY(dalloc(&dh, (size_t)nF * ne * 64));
-  HS_TRY(dalloc(&da, (size_t)nF * nF * 64));
-  HS_TRY(dalloc(&dt, (size_t)nF * nF * 64));
-  HS_TRY(dalloc(&dout, (size_t)SL));
-  HS_TRY(dalloc(&dsep, (size_t)2 * SL));
+  HS_TRY(dalloc(&dax, (size_t)nF * 64, nullptr));
+  HS_TRY(dalloc(&dax2, (size_t)nF * 64, nullptr));
+  HS_TRY(dalloc(&dh, (size_t)nF * ne * 64, nullptr));
+  HS_TRY(dalloc(&da, (size_t)nF * nF * 64, nullptr));
+  HS_TRY(dalloc(&dt, (size_t)nF * nF * 64, nullptr));
+  HS_TRY(dalloc(&dout, (size_t)SL, nullptr));
+  HS_TRY(dalloc(&dsep, (size_t)2 * SL, nullptr));
   HS_HIP(hipMemcpy(dh, hostsum, sizeof(double) * nF * ne * 64, hipMemcpyHostToDevice));
   HS_HIP(hipMemcpy(da, adH, sizeof(double) * nF * nF * 64, hipMemcpyHostToDevice));
   HS_HIP(hipMemcpy(dt, adT, sizeof(double) * nF * nF * 64, hipMemcpyHostToDevice));
@@ -2066,3 +2159,26 @@ extern "C" int hs_debug_stitch(int nF, int exact, const double* hostsum, const d
       }
   return HS_OK;
 }
+
+// test hook (not in the header): the failure the adjoint stamp guards against -- a zero fill of the fp64 (which 0) or
+// fp32 (which 1) adjoint buffers, stamp included, enqueued on the context's stream after the last upload
+extern "C" int hs_debug_stale_adjoints(hs_ctx* c, int which) {
+  if (!c || c->nF == 0 || which < 0 || which > 1) return fail(HS_ERR_INVALID, "bad arguments / no window");
+  HS_HIP(hipSetDevice(c->device));
+  const size_t n = (size_t)HS_ADJ_STAMP + 1;
+  if (which == 0) HS_HIP(hipMemsetAsync(c->d_adHost, 0, n * sizeof(double), c->stream));
+  else HS_HIP(hipMemsetAsync(c->d_adHostF, 0, n * sizeof(float), c->stream));
+  return HS_OK;
+}
+
+// test hook (not in the header): the next GN loop call withholds its done word for ms milliseconds -- a kernel that
+// spins that long (bounded: it exits by itself) is enqueued after the call's last collective and before its results,
+// so the call's wait finds the stream stalled as behind a collective whose peer stopped
+extern "C" int hs_debug_stall(hs_ctx* c, int ms) {
+  if (!c || ms < 0 || ms > 10000) return fail(HS_ERR_INVALID, "bad arguments");
+  c->dbg_stall_ms = ms;
+  return HS_OK;
+}
+
+// test hook (not in the header, no device work): whether a W x H window may run hs_k_lin8 (lin8_supported)
+extern "C" int hs_debug_lin8_supported(int W, int H) { return hs::lin8_supported(W, H) ? 1 : 0; }

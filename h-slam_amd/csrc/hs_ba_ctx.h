@@ -9,6 +9,7 @@
 
 #include <cstdint>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/hs_ba.h"
@@ -54,12 +55,22 @@ constexpr int kLinBlocksTarget = 256;  // linearize blocks of a window (points p
 constexpr int kLin8MinPoints = 4000;
 constexpr int kThMultiMinPoints = 60000;  // the multi-block threshold select (below: one block beside the solve)
 constexpr int kLin8BlocksTarget = 256;  // hs_k_lin8 blocks of a window (one 8-wave block per CU)
+// hs_k_lin8's taps address the packed slots through one buffer resource with 32-bit offsets: the texel index is formed
+// by 24-bit multiplies (W * H < 2^23) and slot * W * H * 12 + offset must stay below 2^31 over all HS_MAXF slots.
+// Larger images run hs_k_lin (64-bit addressing) at every point count.
+inline bool lin8_supported(int W, int H) {
+  const long long px = (long long)W * H;
+  return px < (1LL << 23) && (long long)HS_MAXF * px * 12 + 12 * (long long)W <= 0x7fffffffLL;
+}
 
+// Allocate and zero-fill n elements; the fill is enqueued on `s`, the stream every later user of the buffer runs on.
+// (A null-stream hipMemset returns before the fill lands and does not order against a hipStreamNonBlocking stream:
+// a context's first kernel could store into a buffer that the fill then zeroed -- tools/micro/memset_order.hip.)
 template <typename T>
-inline int dalloc(T** p, size_t n) {
+inline int dalloc(T** p, size_t n, hipStream_t s) {
   if (n == 0) n = 1;
   HS_HIP(hipMalloc((void**)p, n * sizeof(T)));
-  HS_HIP(hipMemset(*p, 0, n * sizeof(T)));
+  HS_HIP(hipMemsetAsync(*p, 0, n * sizeof(T), s));
   return HS_OK;
 }
 
@@ -114,7 +125,7 @@ struct hs_ctx {
   std::vector<int> blk_begin;
   int nblk = 0, W = 4, ne = 0, Q = 0;
   bool exact = false;
-  bool lin8 = false;              // production linearizations run hs_k_lin8 (4-wave blocks, W = 4)
+  bool lin8 = false;              // production linearizations run hs_k_lin8 (8-wave blocks, W = 8)
   // large windows: setNewFrameEnergyTH's select as a multi-block pass 2 (np2 extra blocks of the stitch launch) and a
   // one-block pass 3 over pass 2's survivors, instead of the stitch's single select block scanning every candidate
   // twice (env HS_TH_MULTI=0 / 1 forces it off / on)
@@ -183,8 +194,10 @@ struct hs_ctx {
                                  // sum |idepth|, #points + the diagonal blocks' host-f Schur terms (see SX)
   double* d_sep = nullptr;       // [2][SL] HA | bA, HSC | bSC (granular read-back)
   double* d_sep_aux = nullptr;   // [HS_MAXF][64] the diagonal blocks' host-f Schur terms of the last sep stitch
-  double *d_adHost = nullptr, *d_adTarget = nullptr;
+  double *d_adHost = nullptr, *d_adTarget = nullptr;  // [HS_MAXF^2][64] + the stamp word (HS_ADJ_STAMP)
   float *d_adHostF = nullptr, *d_adTargetF = nullptr;
+  unsigned int adj_seq = 0;        // sequence of the last adjoint upload enqueued (hs_k_fix_frames' stamp)
+  unsigned int* d_ticket = nullptr;  // hs_k_stitch's retire ticket (zero between launches)
   double *d_HM = nullptr, *d_bM = nullptr, *d_Nproj = nullptr;
   float* d_xAd = nullptr;
   double* d_x = nullptr;
@@ -216,6 +229,12 @@ struct hs_ctx {
   // RCCL
   ncclComm_t comm = nullptr;
   int rank = 0, nranks = 1;
+  // the bounded wait of a multi-rank context (wait_stream): a collective that fails or does not finish within
+  // comm_timeout_ms aborts the communicator; every later call then returns HS_ERR_RCCL (comm_lost)
+  int comm_timeout_ms = 60000;
+  bool comm_lost = false;
+  std::thread abort_thread;  // ncclCommAbort of a lost communicator (joined by hs_destroy)
+  int dbg_stall_ms = 0;  // test hook hs_debug_stall: the next GN loop call's stream stalls before its results
   // the multi-rank exchange (launch_reduce / exchange in hs_ba.cpp): one all-gather per linearization of every
   // rank's system vector + energies into d_gsys [nranks][SL + 3] and of its newest-frame candidates into d_cand.
   // gath_pending: a gather whose sums are formed by the next solve launch (the fused GN loop); gath_th: the
@@ -287,4 +306,11 @@ int marginalize_frame_prior(hs_ctx* c, int frame, std::vector<double>& HMn, std:
 int commit(hs_ctx* c);            // hs_ba_window.cpp: apply pending structural edits (no-op when clean)
 inline int commit_if_dirty(hs_ctx* c) { return c->dirty ? commit(c) : HS_OK; }
 int max_blocks_for(int capP);
+// everything enqueued on the context's stream has finished: hipStreamSynchronize on a single-rank context; on a
+// multi-rank one a bounded poll of the stream and the communicator's asynchronous error (HS_ERR_RCCL + abort on a
+// failure or after comm_timeout_ms)
+int wait_stream(hs_ctx* c);
+int comm_fail(hs_ctx* c, const std::string& msg);  // abort the communicator, HS_ERR_RCCL
+// HsDevState::status of a finished launch chain -> the C-ABI code (HS_STATUS_STALE first: HS_ERR_STATE)
+int status_error(int status);
 }  // namespace hs

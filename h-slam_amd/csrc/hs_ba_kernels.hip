@@ -1817,12 +1817,31 @@ __device__ void stitch_result_block(const HsStitchArgs& a) {
 
 __global__ __launch_bounds__(ST_NT) void hs_k_stitch(HsStitchArgs a) {
   __shared__ double lds[ST_LDS];
-  if (a.res_out && blockIdx.x == gridDim.x - 1) {
-    stitch_result_block(a);
-    return;
+  __shared__ int s_last;
+  // the fp64 adjoints' stamp (HS_ADJ_STAMP), requested before the block's work and compared after it
+  const bool chk = a.status && blockIdx.x == 0 && threadIdx.x == 0;
+  double sH = 0.0, sT = 0.0;
+  if (chk) {
+    sH = a.adHost[HS_ADJ_STAMP];
+    sT = a.adTarget[HS_ADJ_STAMP];
   }
-  if (a.red.stop && *a.red.stop) return;
-  stitch_block(a, blockIdx.x, lds);
+  if (!(a.red.stop && *a.red.stop)) stitch_block(a, blockIdx.x, lds);
+  if (chk) {
+    if (sH != (double)a.adj_seq || sT != (double)a.adj_seq) atomicOr(a.status, (int)HS_STATUS_STALE64);
+    else atomicAnd(a.status, ~(int)HS_STATUS_STALE64);
+  }
+  if (!a.res_out) return;
+  // the GN loop call's results: written by the launch's last block to retire (a ticket), after every block's stores
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    s_last = atomicAdd(a.res_ticket, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  if (threadIdx.x == 0) atomicExch(a.res_ticket, 0u);
+  stitch_result_block(a);
 }
 
 
@@ -2171,6 +2190,9 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
   int vz;
   asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
   double sysE0 = a.sysE[vz], sysE1 = a.sysE[vz + 1], sysE2 = a.sysE[vz + 2];
+  // the fp32 adjoints' stamps (HS_ADJ_STAMP), checked after the counters' reset below
+  const unsigned int sHF = a.chk_adj ? reinterpret_cast<const unsigned int*>(a.adHostF)[HS_ADJ_STAMP + vz] : 0u;
+  const unsigned int sTF = a.chk_adj ? reinterpret_cast<const unsigned int*>(a.adTargetF)[HS_ADJ_STAMP + vz] : 0u;
   const bool hasHM = a.HM != nullptr;
   if (solve) {
     axv = a.sys[AUX0 + min(tid, nF * 64 - 1)];
@@ -2257,6 +2279,8 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
       st->stop = 0;
     }
     s_it = a.iteration >= 0 ? a.iteration : st->iteration;
+    if (a.chk_adj)
+      st->status = (st->status & ~(int)HS_STATUS_STALE32) | ((sHF != a.adj_seq || sTF != a.adj_seq) ? HS_STATUS_STALE32 : 0);
   }
   const double lambda = 1e-5;  // SOLVER_FIX_LAMBDA
 
@@ -2386,7 +2410,7 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
         }
         xv -= 0.5 * (s1 + s2);
       }
-      if (!isfinite(xv)) st->status = 1;
+      if (!isfinite(xv)) st->status |= HS_STATUS_NONFINITE;
       xF[q] = (float)xv;
       st->lastX[q] = xv;
       if (a.x_out) a.x_out[q] = xv;
@@ -2639,7 +2663,8 @@ __global__ void hs_k_marg_update(const double* sep, const double* sep_aux, doubl
 // fix = 1: the optimize tail's setEvalPT of the newest frame first; then (both) every frame pair's precalc and
 // adjoints (System::setPrecalcValues, EnergyFunctional::setAdjointsF) from the device state
 __global__ __launch_bounds__(64) void hs_k_fix_frames(HsDevState* st, HsPrecalc* pre, double* adH, double* adT,
-                                                      float* adHF, float* adTF, hs_params P, int fix) {
+                                                      float* adHF, float* adTF, hs_params P, int fix,
+                                                      unsigned int seq) {
   const int nF = st->nF, tid = threadIdx.x;
   if (fix && tid == 0) {  // newStateZero = 0 except segment(6, 2) = the newest frame's a / b; setEvalPT(PRE_worldToCam, .)
     hs::FrameH& f = st->frames[nF - 1];
@@ -2664,6 +2689,19 @@ __global__ __launch_bounds__(64) void hs_k_fix_frames(HsDevState* st, HsPrecalc*
       adTF[(size_t)idx * 64 + i] = (float)AT[i];
     }
   }
+  if (tid == 0) {  // this upload's stamp (HS_ADJ_STAMP), checked by the stitch / solve launches that read the adjoints
+    adH[HS_ADJ_STAMP] = (double)seq;
+    adT[HS_ADJ_STAMP] = (double)seq;
+    reinterpret_cast<unsigned int*>(adHF)[HS_ADJ_STAMP] = seq;
+    reinterpret_cast<unsigned int*>(adTF)[HS_ADJ_STAMP] = seq;
+  }
+}
+
+// test hook: spins for `ticks` of the 100 MHz wall clock and exits (every wave reaches the bound), standing in for a
+// collective whose peer stalls: the host's bounded wait (wait_stream) must return HS_ERR_RCCL while it runs
+__global__ void hs_k_debug_stall(long long ticks) {
+  const long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
 }
 
 // image slot texels (I, dx, dy, |grad|^2) -> packed (I, dx, dy) triplets for hs_k_lin8's taps: 12 instead of 16 bytes

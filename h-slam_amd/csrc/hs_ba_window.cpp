@@ -308,7 +308,7 @@ int hs_ba_reserve(hs_ctx* c, const hs_camera* cam, int max_points) {
   if (!c || !cam) return fail(HS_ERR_INVALID, "null argument");
   if (cam->width < 8 || cam->height < 8 || max_points < 1) return fail(HS_ERR_INVALID, "bad camera size / capacity");
   HS_HIP(hipSetDevice(c->device));
-  HS_HIP(hipStreamSynchronize(c->stream));
+  HS_TRY(wait_stream(c));
   HS_TRY(ensure_capacity(c, cam->width, cam->height, max_points, max_blocks_for(max_points)));
   drop_graph(c);
   c->cam = *cam;
@@ -353,7 +353,7 @@ int hs_ba_reserve(hs_ctx* c, const hs_camera* cam, int max_points) {
   c->h_state_valid = true;
   c->tail_pending = false;
   HS_HIP(hipMemsetAsync(c->d_cand, 0xff, sizeof(float) * (size_t)c->cap_stride * c->nranks, c->stream));
-  HS_HIP(hipStreamSynchronize(c->stream));
+  HS_TRY(wait_stream(c));
   return HS_OK;
 }
 
@@ -405,7 +405,7 @@ int hs_ba_set_frame_image(hs_ctx* c, int frame, const float* image) {
   for (size_t i = 0; i < c->img_px; i++) tex[i] = make_float4(image[3 * i], image[3 * i + 1], image[3 * i + 2], 0.f);
   HS_HIP(hipMemcpyAsync(dst, tex.data(), c->img_px * sizeof(float4), hipMemcpyHostToDevice, c->stream));
   HS_TRY(pack_slot(c, c->wframes[frame].slot));
-  HS_HIP(hipStreamSynchronize(c->stream));
+  HS_TRY(wait_stream(c));
   return HS_OK;
 }
 
@@ -442,7 +442,7 @@ int hs_ba_set_frame_image_device(hs_ctx* c, int frame, const void* d_texels) {
   HS_TRY(hs::copy_frame_image_device(c, frame, d_texels));
   // the source is foreign memory whose producer this context cannot order against: the copy must have read it
   // before this call returns (hs_tracker_frame_to_ba orders the tracker's hand-off on the device instead)
-  HS_HIP(hipStreamSynchronize(c->stream));
+  HS_TRY(wait_stream(c));
   return HS_OK;
 }
 
@@ -549,7 +549,7 @@ int hs_ba_drop_inactive_residuals(hs_ctx* c, int* n_dropped) {
   if (c->nP > 0) {
     c->rb_pending = true;
     HS_HIP(hipMemcpyAsync(c->h_rb, c->d_r_active, (size_t)c->nP * 8, hipMemcpyDeviceToHost, c->stream));
-    HS_HIP(hipStreamSynchronize(c->stream));
+    HS_TRY(wait_stream(c));
     c->rb_pending = false;
   }
   // toRemove in activeResiduals order (points in window order, each list in order), then dropResidual one by one
@@ -683,7 +683,7 @@ extern "C" {
 int hs_ba_synchronize(hs_ctx* c) {
   if (!c) return fail(HS_ERR_INVALID, "null context");
   HS_HIP(hipSetDevice(c->device));
-  HS_HIP(hipStreamSynchronize(c->stream));
+  HS_TRY(wait_stream(c));
   return HS_OK;
 }
 
@@ -715,7 +715,7 @@ int hs_ba_get_point_state(hs_ctx* c, float* idepth, float* idepth_zero, float* r
   c->rb_pending = true;
   for (int k = 0; k < 5; k++)
     if (dst[k]) HS_HIP(hipMemcpyAsync(c->h_rb + k * n * 4, src[k], n * 4, hipMemcpyDeviceToHost, c->stream));
-  HS_HIP(hipStreamSynchronize(c->stream));
+  HS_TRY(wait_stream(c));
   c->rb_pending = false;
   for (int k = 0; k < 5; k++)
     if (dst[k]) std::memcpy(dst[k], c->h_rb + k * n * 4, n * 4);
@@ -744,7 +744,7 @@ extern "C" int hs_debug_nullspace_error(hs_ctx* c, double* err_out) {
   if (c->tail_pending) HS_TRY(fetch_state(c));  // settles the moved newest frame (host and device copies)
   HsDevState dev;
   HS_HIP(hipMemcpyAsync(&dev, c->d_state, sizeof(HsDevState), hipMemcpyDeviceToHost, c->stream));
-  HS_HIP(hipStreamSynchronize(c->stream));
+  HS_TRY(wait_stream(c));
   double e = 0;
   for (int f = 0; f < c->nF; f++) {
     hs::FrameH r = dev.frames[f];
@@ -766,6 +766,6 @@ extern "C" int hs_debug_set_state(hs_ctx* c, const void* in) {
   std::memcpy((void*)c->h_state, in, sizeof(HsDevState));
   if (c->h_state->nF != c->nF) return fail(HS_ERR_INVALID, "state of a different window size");
   HS_TRY(upload_frames(c));
-  HS_HIP(hipStreamSynchronize(c->stream));
+  HS_TRY(wait_stream(c));
   return HS_OK;
 }

@@ -16,6 +16,15 @@ constexpr int HS_LIN_NT = 64 * HS_LIN_NW;
 #endif
 constexpr int HS_LIN8_NT = 64 * HS_LIN8_WAVES;  // hs_k_lin8 workgroup size (8 points per wave at a time)
 constexpr int HS_NNS = 7;         // gauge nullspaces: 6 pose + 1 scale (System::getNullspaces)
+// The adjoint buffers (fp64 d_adHost / d_adTarget, fp32 d_adHostF / d_adTargetF: [HS_MAXF^2][64]) carry one stamp word
+// after the adjoints: hs_k_fix_frames writes the upload's sequence number there (the fp32 buffers its bits), and every
+// reader launch (hs_k_stitch: fp64, hs_k_solve: fp32) compares it with the sequence of the last upload the host
+// enqueued.  A mismatch -- adjoints that never arrived, or a zero fill landing after them -- sets HS_STATUS_STALE in
+// HsDevState::status, which the C-ABI returns as HS_ERR_STATE instead of a system with zero frame rows.
+constexpr int HS_ADJ_STAMP = HS_MAXF * HS_MAXF * 64;
+// status bits: each stamp check owns its bit and sets / clears it at every launch (the stitch the fp64 one, the
+// solve the fp32 one), so the bits describe the adjoints the last launches read
+enum { HS_STATUS_NONFINITE = 1, HS_STATUS_STALE64 = 2, HS_STATUS_STALE32 = 4, HS_STATUS_STALE = 6 };
 
 // Window state owned by the device between GN iterations (updated by hs_k_solve).
 struct HsDevState {
@@ -174,6 +183,10 @@ struct HsStitchArgs {
   const HsDevState* res_st;
   int res_k, res_slot;
   unsigned long long res_seq;
+  unsigned int* res_ticket;    // with res_out: blocks retired so far (zero between launches); the last one writes the
+                               // results, so the done word means the whole launch has finished
+  int* status;                 // nullable: &HsDevState::status, HS_STATUS_STALE when the fp64 adjoints' stamp is not
+  unsigned int adj_seq;        // the sequence of the last adjoint upload
 };
 
 enum { HS_SOLVE = 1, HS_APPLY = 2 };
@@ -213,6 +226,8 @@ struct HsSolveArgs {
   // 0 returns at entry and sets st->stop) when the previous step allowed it (st->canbreak) and the previous
   // iteration index was >= minOpt; block 1's threshold select runs anyway (same candidates, same result)
   int brk, minOpt;
+  int chk_adj;                 // compare the fp32 adjoints' stamp with adj_seq (HS_STATUS_STALE on a mismatch)
+  unsigned int adj_seq;
 };
 
 struct HsResubArgs {
@@ -266,6 +281,7 @@ __global__ void hs_k_marg_delta(const HsDevState* st, const float* adHF, const f
 __global__ void hs_k_marg_update(const double* sep, const double* sep_aux, double* HM, double* bM, int nF, int SL,
                                  double w);
 __global__ void hs_k_fix_frames(HsDevState* st, HsPrecalc* pre, double* adH, double* adT, float* adHF, float* adTF,
-                                hs_params P, int fix);
+                                hs_params P, int fix, unsigned int seq);
+__global__ void hs_k_debug_stall(long long ticks);  // test hook: a bounded spin on the wall clock (a stalled peer)
 __global__ void hs_k_lenergy(int n, const float* idepth, const float* idepth_zero, const float* priorF, float* chunk,
                              double* out);

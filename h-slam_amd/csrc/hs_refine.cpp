@@ -226,7 +226,8 @@ int hs_refiner_create(hs_refiner** out, int device_id, int width, int height, co
       hipMalloc(&r->d_img1, np * sizeof(float4)) != hipSuccess || hipMalloc(&r->d_img2, np * sizeof(float4)) != hipSuccess ||
       hipMalloc(&r->d_ctl, sizeof(HsRefCtl)) != hipSuccess || hipHostMalloc(&r->h_ctl, sizeof(HsRefCtl)) != hipSuccess ||
       hipHostMalloc(&r->h_flags, 4 * sizeof(int)) != hipSuccess || hipMalloc(&r->d_ticket, sizeof(int)) != hipSuccess ||
-      hipMemset(r->d_ticket, 0, sizeof(int)) != hipSuccess || hipMemset(r->d_ctl, 0, sizeof(HsRefCtl)) != hipSuccess ||
+      hipMemsetAsync(r->d_ticket, 0, sizeof(int), r->stream) != hipSuccess ||
+      hipMemsetAsync(r->d_ctl, 0, sizeof(HsRefCtl), r->stream) != hipSuccess ||
       hipMalloc(&r->d_log, sizeof(float) * HS_REF_MAXLOG * HS_REF_LOGW) != hipSuccess) {
     hs_refiner_destroy(r);
     return rfail(HS_ERR_HIP, "refiner allocation failed");
@@ -295,7 +296,8 @@ int hs_refiner_set_points(hs_refiner* r, int n, const float* u, const float* v, 
   r->d_trace = nullptr;
   if (const char* e = std::getenv("HS_REF_TRACE"); e && std::atoi(e) > 0) {
     RF_HIP(hipMalloc(&r->d_trace, sizeof(long long) * 16 * (size_t)((n + HS_REF_PPB - 1) / HS_REF_PPB)));
-    RF_HIP(hipMemset(r->d_trace, 0, sizeof(long long) * 16 * (size_t)((n + HS_REF_PPB - 1) / HS_REF_PPB)));
+    RF_HIP(hipMemsetAsync(r->d_trace, 0, sizeof(long long) * 16 * (size_t)((n + HS_REF_PPB - 1) / HS_REF_PPB),
+                          r->stream));
   }
   // the ctor's Pnt set-up (Src/Initializer.cpp:1362-1382)
   std::vector<float> pf((size_t)PF_COUNT * n, 0.f);
@@ -391,6 +393,7 @@ int hs_refiner_get_log(hs_refiner* r, int cap, float* out) {
   const int m = std::min(n, cap);
   if (m > 0) {
     RF_HIP(hipSetDevice(r->device));
+    RF_HIP(hipStreamSynchronize(r->stream));
     RF_HIP(hipMemcpy(out, r->d_log, sizeof(float) * HS_REF_LOGW * m, hipMemcpyDeviceToHost));
   }
   return n;

@@ -152,7 +152,7 @@ int hs_tracer_create(hs_tracer** out, const hs_params* params, int device_id, in
   const size_t c = capacity;
   TR_HIP(hipMalloc((void**)&t->d_new, (size_t)width * height * sizeof(float4)));
   TR_HIP(hipMalloc((void**)&t->d_host_tab, sizeof(float4*) * HS_TRC_MAXHOST));
-  TR_HIP(hipMemset(t->d_host_tab, 0, sizeof(float4*) * HS_TRC_MAXHOST));
+  TR_HIP(hipMemsetAsync(t->d_host_tab, 0, sizeof(float4*) * HS_TRC_MAXHOST, t->stream));  // the kernels' stream
   TR_HIP(hipMalloc((void**)&t->d_hosts, sizeof(hs_trace_host) * HS_TRC_MAXHOST));
   TR_HIP(hipMalloc((void**)&t->d_host, sizeof(int) * c));
   TR_HIP(hipMalloc((void**)&t->d_u, sizeof(float) * c));
@@ -200,7 +200,8 @@ int hs_tracer_set_host_image(hs_tracer* t, int slot, const float* img) {
   TR_HIP(hipSetDevice(t->device));
   if (!t->d_host_img[slot]) {
     TR_HIP(hipMalloc((void**)&t->d_host_img[slot], (size_t)t->W * t->H * sizeof(float4)));
-    TR_HIP(hipMemcpy(t->d_host_tab + slot, &t->d_host_img[slot], sizeof(float4*), hipMemcpyHostToDevice));
+    TR_HIP(hipMemcpyAsync(t->d_host_tab + slot, &t->d_host_img[slot], sizeof(float4*), hipMemcpyHostToDevice,
+                          t->stream));
   }
   return upload_img(t, t->d_host_img[slot], img);
 }
@@ -666,7 +667,10 @@ static int compact_array(hs_tracer* t, T* d, int per, const std::vector<int>& ke
   if (n) TR_HIP(hipMemcpy(h.data(), d, sizeof(T) * n * per, hipMemcpyDeviceToHost));
   for (size_t k = 0; k < keep_idx.size(); k++)
     for (int c = 0; c < per; c++) o[k * per + c] = h[(size_t)keep_idx[k] * per + c];
-  if (!o.empty()) TR_HIP(hipMemcpy(d, o.data(), sizeof(T) * o.size(), hipMemcpyHostToDevice));
+  if (!o.empty()) {  // on the kernels' stream; o lives until the copy has landed
+    TR_HIP(hipMemcpyAsync(d, o.data(), sizeof(T) * o.size(), hipMemcpyHostToDevice, t->stream));
+    TR_HIP(hipStreamSynchronize(t->stream));
+  }
   return HS_OK;
 }
 

@@ -50,7 +50,9 @@ struct hs_tracker {
   DepthGraph dg[2];
   int dg_next = 0;
   hipStream_t stream = nullptr;
-  hipEvent_t e0 = nullptr, e1 = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;  // the per-call event pair (hs_tracker_set_event_timing, off by default)
+  hipEvent_t ev_handoff = nullptr;        // cross-stream hand-offs with a BA context (set_ref_ba, frame_to_ba)
+  int evt = 0;                            // hs_tracker_set_event_timing
   int W = 0, H = 0, nlev = 0;
   int w[HS_TRK_MAXLEV], h[HS_TRK_MAXLEV];
   float fx[HS_TRK_MAXLEV], fy[HS_TRK_MAXLEV], cx[HS_TRK_MAXLEV], cy[HS_TRK_MAXLEV], Ki[HS_TRK_MAXLEV][9];
@@ -256,10 +258,11 @@ static int run_tries(hs_tracker* t, int n, const double* h_in, int coarsest, int
     TS_HIP(hipMemsetAsync(t->d_trace, 0, sizeof(long long) * 16 * nb, t->stream));
     a.trace = t->d_trace;
   }
-  // the launch's device time (hs_tracker_last_ms) from an event pair around it; env HS_TRK_NOEVT=1 (read per call)
-  // skips the pair, ~3-4 us of host time per call (r05_trk14), and leaves last_ms at 0
+  // the launch's device time (hs_tracker_last_ms) from an event pair around it, only with event timing on
+  // (hs_tracker_set_event_timing; ~3-4 us of host time per call, r05_trk14): by default the host takes the results
+  // from the hypotheses' done words and last_ms stays 0.  Env HS_TRK_NOEVT=0 / 1 (read per call) forces either.
   const char* ne = std::getenv("HS_TRK_NOEVT");
-  const bool no_evt = ne && ne[0] == '1';
+  const bool no_evt = ne ? ne[0] == '1' : !t->evt;
   if (!no_evt) TS_HIP(hipEventRecord(t->e0, t->stream));
   hipLaunchKernelGGL(hs_k_track, dim3(nblk), dim3(512), 0, t->stream, a);
   TS_HIP(hipGetLastError());
@@ -441,7 +444,8 @@ int hs_tracker_create(hs_tracker** out, const hs_params* params, int device_id, 
     hs::inv3f(K, t->Ki[l]);
   }
   if (hipSetDevice(device_id) != hipSuccess || hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreate(&t->e0) != hipSuccess || hipEventCreate(&t->e1) != hipSuccess) {
+      hipEventCreate(&t->e0) != hipSuccess || hipEventCreate(&t->e1) != hipSuccess ||
+      hipEventCreateWithFlags(&t->ev_handoff, hipEventDisableTiming) != hipSuccess) {
     delete t;
     return tfail(HS_ERR_HIP, "stream / event creation failed");
   }
@@ -464,7 +468,7 @@ int hs_tracker_create(hs_tracker** out, const hs_params* params, int device_id, 
     maxBlocks = std::max(maxBlocks, (int)((n + 255) / 256));
   }
   TS_HIP(hipMalloc((void**)&t->d_pcn, sizeof(int) * HS_TRK_MAXLEV));
-  TS_HIP(hipMemset(t->d_pcn, 0, sizeof(int) * HS_TRK_MAXLEV));
+  TS_HIP(hipMemsetAsync(t->d_pcn, 0, sizeof(int) * HS_TRK_MAXLEV, t->stream));  // on the kernels' stream
   TS_HIP(hipMalloc((void**)&t->d_bcnt, sizeof(int) * maxBlocks));
   TS_HIP(hipMalloc((void**)&t->d_boff, sizeof(int) * maxBlocks));
   *out = t;
@@ -491,6 +495,7 @@ void hs_tracker_destroy(hs_tracker* t) {
   if (t->h_cnt) (void)hipHostFree(t->h_cnt);
   if (t->e0) (void)hipEventDestroy(t->e0);
   if (t->e1) (void)hipEventDestroy(t->e1);
+  if (t->ev_handoff) (void)hipEventDestroy(t->ev_handoff);
   if (t->stream) (void)hipStreamDestroy(t->stream);
   delete t;
 }
@@ -510,13 +515,13 @@ int hs_tracker_set_ref(hs_tracker* t, const float* const* ref_pyr, float ab_expo
     TS_HIP(hipMalloc((void**)&t->d_pts, sizeof(float) * 4 * n));
     t->pts_cap = n;
   }
+  std::vector<float> h((size_t)4 * std::max(n, 0));  // lives until the stream synchronize below
   if (n > 0) {
-    std::vector<float> h((size_t)4 * n);
     std::memcpy(h.data(), cu, 4 * n);
     std::memcpy(h.data() + n, cv, 4 * n);
     std::memcpy(h.data() + 2 * n, cid, 4 * n);
     std::memcpy(h.data() + 3 * n, hdi, 4 * n);
-    TS_HIP(hipMemcpy(t->d_pts, h.data(), sizeof(float) * 4 * n, hipMemcpyHostToDevice));
+    TS_HIP(hipMemcpyAsync(t->d_pts, h.data(), sizeof(float) * 4 * n, hipMemcpyHostToDevice, t->stream));
   }
   TS_TRY(make_depth_l0(t, n, nullptr, t->d_pts, n));
   TS_HIP(hipStreamSynchronize(t->stream));
@@ -563,8 +568,8 @@ int hs_tracker_set_ref_ba(hs_tracker* t, hs_ctx* ba, int promote_frame, float ab
   t->refAff[1] = aff_g2l[1];
   TS_TRY(make_depth_l0_dev(t, ba->d_ref_n, ba->d_ref_pts, ba->cap_P));
   // the BA stream must not rewrite the hand-off buffer before the tracker consumed it
-  TS_HIP(hipEventRecord(t->e1, t->stream));
-  TS_HIP(hipStreamWaitEvent(ba->stream, t->e1, 0));
+  TS_HIP(hipEventRecord(t->ev_handoff, t->stream));
+  TS_HIP(hipStreamWaitEvent(ba->stream, t->ev_handoff, 0));
   t->haveRef = true;
   return HS_OK;
 }
@@ -579,11 +584,18 @@ int hs_tracker_frame_to_ba(hs_tracker* t, hs_ctx* ba, int frame) {
   if (ba->cam.width != t->W || ba->cam.height != t->H) return tfail(HS_ERR_INVALID, "image size mismatch");
   if (!t->haveFrame) return tfail(HS_ERR_STATE, "no frame set");
   TS_HIP(hipSetDevice(t->device));
-  TS_HIP(hipEventRecord(t->e1, t->stream));
-  TS_HIP(hipStreamWaitEvent(ba->stream, t->e1, 0));
-  HS_TRY(hs::copy_frame_image_device(ba, frame, t->d_new[0]));
+  TS_HIP(hipEventRecord(t->ev_handoff, t->stream));
+  TS_HIP(hipStreamWaitEvent(ba->stream, t->ev_handoff, 0));
+  if (const int rc = hs::copy_frame_image_device(ba, frame, t->d_new[0]))
+    return tfail(rc, std::string("hs_tracker_frame_to_ba: ") + hs::g_err);
   TS_HIP(hipEventRecord(ba->ev_ready, ba->stream));
   TS_HIP(hipStreamWaitEvent(t->stream, ba->ev_ready, 0));
+  return HS_OK;
+}
+
+int hs_tracker_set_event_timing(hs_tracker* t, int on) {
+  if (!t) return tfail(HS_ERR_INVALID, "null tracker");
+  t->evt = on ? 1 : 0;
   return HS_OK;
 }
 
@@ -730,6 +742,7 @@ int hs_tracker_get_lm_log(hs_tracker* t, int try_idx, int cap, int* n, int* lvl,
   if (!t || !n) return tfail(HS_ERR_INVALID, "null argument");
   if (try_idx < 0 || try_idx >= t->last_n_tries) return tfail(HS_ERR_INVALID, "no such hypothesis in the last call");
   TS_HIP(hipSetDevice(t->device));
+  TS_HIP(hipStreamSynchronize(t->stream));
   const int iters = t->h_out[try_idx].iters;
   *n = iters;
   const int m = std::min(std::min(iters, cap), HS_TRK_MAXLOG);

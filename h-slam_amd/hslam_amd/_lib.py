@@ -106,12 +106,16 @@ SIGNATURES = {
     "hs_comm_get_unique_id": ([VP], I),
     "hs_comm_init": ([VP, VP, I, I], I),
     "hs_comm_size": ([VP, VP, VP], I),
+    "hs_comm_set_timeout": ([VP, I], I),
     "hs_ba_set_event_timing": ([VP, I], I),
     "hs_ba_get_frame_eval": ([VP, VP, VP], I),
     # test hooks (not in the header): an in-process rank group on one device, the multi-rank exchange by copies
     "hs_ba_debug_group": ([VP, I, I], I),
     "hs_ba_group_linearize": ([VP, I, I, VP], I),
     "hs_ba_group_iterate": ([VP, I, I, I, VP], I),
+    # test hooks (not in the header): a stale adjoint upload, a stalled stream
+    "hs_debug_stale_adjoints": ([VP, I], I),
+    "hs_debug_stall": ([VP, I], I),
     # include/hs_track.h
     "hs_tracker_create": ([VP, VP, I, I, I, I, VP], I),
     "hs_tracker_destroy": ([VP], None),
@@ -123,6 +127,7 @@ SIGNATURES = {
     "hs_tracker_track_tries": ([VP, I, VP, VP, VP, C.c_float, VP, VP, VP, VP, VP, VP], I),
     "hs_tracker_get_lm_log": ([VP, I, I, VP, VP, VP, VP, VP], I),
     "hs_tracker_last_ms": ([VP, VP], I),
+    "hs_tracker_set_event_timing": ([VP, I], I),
     "hs_tracker_last_stats": ([VP, I, VP, VP, VP], I),
     "hs_tracker_launch_info": ([VP, VP, VP], I),
     "hs_tracker_set_frame_raw": ([VP, VP, C.c_float], I),

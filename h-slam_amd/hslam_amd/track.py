@@ -163,6 +163,10 @@ class CoarseTracker:
         check(self.lib.hs_tracker_last_stats(self.h, try_idx, C.byref(ms), C.byref(ps), C.byref(pp)))
         return ms.value, ps.value, pp.value
 
+    def set_event_timing(self, on: bool = True):
+        """hs_tracker_set_event_timing: the per-call event pair (off by default) that last_ms / last_stats report."""
+        check(self.lib.hs_tracker_set_event_timing(self.h, int(bool(on))))
+
     def last_ms(self):
         ms = C.c_double()
         check(self.lib.hs_tracker_last_ms(self.h, C.byref(ms)))

@@ -246,6 +246,12 @@ int hs_comm_init(hs_ctx* ctx, const char* id128, int rank, int nranks);
 /* the communicator's own rank count and this context's rank (ncclCommCount / ncclCommUserRank); 1 / 0 without a
    communicator.  The bench reports n_gpus from it, not from the launcher's environment. */
 int hs_comm_size(hs_ctx* ctx, int* nranks, int* rank);
+/* failure handling of a multi-rank context ("RCCL errors are mapped to status codes"; the reference's
+   isLost, Src/FullSystemOptimize.cpp:512-516): every wait of a context with a communicator polls the stream and
+   ncclCommGetAsyncError under a wall-clock bound (default 60000 ms).  A collective that reports an error, or does not
+   finish within the bound (a peer rank died or stalled), aborts the communicator (ncclCommAbort) and the call returns
+   HS_ERR_RCCL; every later call on the context returns HS_ERR_RCCL as well (destroy it and rebuild the ranks). */
+int hs_comm_set_timeout(hs_ctx* ctx, int timeout_ms);
 
 #ifdef __cplusplus
 }

@@ -95,8 +95,13 @@ int hs_tracker_track_tries(hs_tracker* t, int n_tries, const double* tries7, con
    commented-out printf, Src/CoarseTracker.cpp:613-625). */
 int hs_tracker_get_lm_log(hs_tracker* t, int try_idx, int cap, int* n, int* lvl, double* new_ratio,
                           double* old_ratio, double* inc_norm);
-/* device time (ms) of the last track / track_tries call (HIP events on the tracker stream) */
+/* device time (ms) of the last track / track_tries call (HIP events on the tracker stream); 0 unless event timing
+   is on */
 int hs_tracker_last_ms(hs_tracker* t, double* ms);
+/* per-call event timing (off by default): on, every track / track_tries call records an event pair around its launch
+   and waits for the stream's end (hs_tracker_last_ms reports the device time); off, the host takes each hypothesis'
+   results from its done word as soon as the device wrote it (~3-4 us less host time per call) */
+int hs_tracker_set_event_timing(hs_tracker* t, int on);
 
 /* Work of hypothesis try_idx in the last trackNewestCoarse / try-loop call: the device time of the call (ms), the
    calcRes(+calcGSSSE) passes it ran and the sum of their levels' reference-point counts (the point-pass units

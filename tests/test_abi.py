@@ -103,3 +103,17 @@ def test_c_caller_is_built_against_the_headers():
     src = os.path.join(ROOT, "tests", "c", "ba_caller.c")
     assert os.path.exists(exe), "make -C h-slam_amd/csrc"
     assert os.path.getmtime(exe) >= max(os.path.getmtime(src), os.path.getmtime(os.path.join(ROOT, "include", "hs_ba.h")))
+
+
+def test_lin8_offset_limit():
+    """hs_k_lin8's taps use 32-bit buffer offsets formed by 24-bit multiplies (hs_lin8_kernels.hip interp33_8b): a
+    window runs it only while W * H < 2^23 and all HS_MAXF packed slots stay below 2^31 bytes (lin8_supported,
+    hs_ba_ctx.h); larger images fall back to hs_k_lin.  Pure host rule, checked at the limit without a GPU."""
+    lib = ctypes.CDLL(LIB)
+    f = lib.hs_debug_lin8_supported
+    f.argtypes, f.restype = [ctypes.c_int, ctypes.c_int], ctypes.c_int
+    assert f(640, 480) == 1 and f(1232, 368) == 1
+    assert f(4096, 2047) == 1          # 2^23 - 4096 texels
+    assert f(4096, 2048) == 0          # 2^23 texels: the 24-bit texel index would wrap
+    assert f(3840, 2160) == 1 and f(4096, 2160) == 0
+    assert f(1 << 23, 1) == 0

@@ -151,6 +151,7 @@ def _lm_divergence(lg, lo, spread=(0.0, 0.0, 0.0)):
 def test_track_parity(vga, pair, start):
     from hslam_amd.se3 import SE3
     g, o = pair
+    g.set_event_timing(True)  # last_ms below (off by default: the done-word path)
     T0 = SE3().data() if start == "identity" else (SE3.exp([0.002, 0, -0.001, 0, 0.001, 0]) *
                                                    SE3.from_data(vga.T_true)).data()
     minRes = np.full(5, np.nan)
@@ -238,6 +239,7 @@ def test_track_parity_4_levels(vga4, start):
     from hslam_amd.track import CoarseTracker
     from oracle_ffi import OracleTracker
     g = CoarseTracker(vga4.width, vga4.height, vga4.K4, vga4.n_levels)
+    g.set_event_timing(True)  # last_stats' device time below
     g.set_scene(vga4)
     o = OracleTracker(vga4.width, vga4.height, vga4.K4, vga4.n_levels)
     o.set_scene(vga4)
@@ -272,7 +274,7 @@ def test_member_meeting_timeout_falls_back_to_one_workgroup(vga, monkeypatch, no
     """The G member workgroups of a hypothesis meet once per pass and must be co-resident.  With the meeting's poll
     bound forced to one poll (HS_TRK_SPIN=1) and G past the co-residency cap (HS_TRK_G_UNCHECKED=16), meetings time
     out; the launch is then rerun with G = 1 and the track is the one-workgroup track, bit for bit.  noevt = 1: the
-    host takes the results from the leads' done words instead of the stream's end (HS_TRK_NOEVT)."""
+    host takes the results from the leads' done words instead of the stream's end (HS_TRK_NOEVT; the default)."""
     from hslam_amd.se3 import SE3
     monkeypatch.setenv("HS_TRK_NOEVT", noevt)
     from hslam_amd.track import CoarseTracker
@@ -302,7 +304,7 @@ def test_member_meeting_timeout_falls_back_to_one_workgroup(vga, monkeypatch, no
 
 
 def test_done_word_results_match_synchronized(vga):
-    """HS_TRK_NOEVT=1 (no event pair): the host reads each hypothesis' record once its lead's done word (a system-scope
+    """HS_TRK_NOEVT=1 (no event pair, the library default): the host reads each hypothesis' record once its lead's done word (a system-scope
     release after the record) shows the launch, without waiting for the launch's end.  Tracks and try sequences
     bit-identical to the synchronized path, over repeated calls (the done words carry a per-launch sequence number)."""
     from hslam_amd.se3 import SE3
