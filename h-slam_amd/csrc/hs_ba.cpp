@@ -96,7 +96,8 @@ static void free_buffers(hs_ctx* c) {
   c->d_gsys = nullptr;
   c->d_sep_aux = nullptr;
   c->d_ticket = nullptr;
-  c->gath_pending = c->gath_th = false;
+  c->gath_pending = false;
+  c->gath_th = 0;
   c->d_stage_cap = 0;
   c->cap_P = c->cap_blk = c->cap_W = c->cap_H = c->cap_stride = 0;
   bind_point_set(c);
@@ -553,11 +554,12 @@ static int launch_combine(hs_ctx* c) {
   if (c->gath_pending) {
     a.gsys = c->d_gsys; a.nranks = c->nranks; a.gstride = c->SX(); a.sys_out = c->d_sys;
   }
-  a.th_local = c->gath_th ? 1 : 0;
+  a.th_local = c->gath_th;
   a.th = red_args(c, false);
   hipLaunchKernelGGL(hs_k_combine, dim3(c->gath_th ? 2 : 1), dim3(HS_SOLVE_NT), 0, c->stream, a);
   HS_HIP(hipGetLastError());
-  c->gath_pending = c->gath_th = false;
+  c->gath_pending = false;
+  c->gath_th = 0;
   return HS_OK;
 }
 
@@ -565,16 +567,15 @@ static int launch_combine(hs_ctx* c) {
 // a 1-block select over 10^5..10^6 candidates would outlast the solve beside it); then either the sums are left to
 // the next solve launch (defer, the fused GN loop) or hs_k_combine forms them now
 static int post_exchange(hs_ctx* c, bool th, bool defer) {
-  c->gath_th = th;
+  c->gath_th = th ? 1 : 0;
   c->gath_pending = true;
   if (th && c->th_multi) {
     HsRedArgs a = red_args(c, false);
     a.hist_only = 1;
     hipLaunchKernelGGL(hs_k_reduce, dim3(a.nhist), dim3(256), 0, c->stream, a);
     hipLaunchKernelGGL(hs_k_th_pass2, dim3(a.np2), dim3(HS_STITCH_NT), 0, c->stream, a);
-    hipLaunchKernelGGL(hs_k_th_select, dim3(1), dim3(HS_STITCH_NT), 0, c->stream, a);
     HS_HIP(hipGetLastError());
-    c->gath_th = false;
+    c->gath_th = 2;  // pass 3 as block 1 of the solve / combine launch that follows
   }
   if (!defer) HS_TRY(launch_combine(c));
   return HS_OK;
@@ -645,14 +646,20 @@ static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = fals
   st.adj_seq = c->adj_seq;
   hipLaunchKernelGGL(hs_k_stitch, dim3(nS), dim3(HS_STITCH_NT), 0, c->stream, st);
   HS_HIP(hipGetLastError());
-  if (multi) {  // pass 3: the select block over pass 2's histogram and survivors (a side stream measured no faster:
-                // its cross-queue event hand-offs cost what the overlap with the solve saves)
-    hipLaunchKernelGGL(hs_k_th_select, dim3(1), dim3(HS_STITCH_NT), 0, c->stream, a);
-    HS_HIP(hipGetLastError());
+  if (multi) {  // pass 3: the select over pass 2's histogram and survivors.  It only feeds the next linearize: in the
+                // fused GN loop it runs as block 1 of the next solve launch, beside the solve (defer), else as a
+                // one-block launch now (env HS_TH_BESIDE=0: always the launch)
+    const char* tb = std::getenv("HS_TH_BESIDE");
+    if (defer && !(tb && tb[0] == '0')) {
+      c->gath_th = 2;
+    } else {
+      hipLaunchKernelGGL(hs_k_th_select, dim3(1), dim3(HS_STITCH_NT), 0, c->stream, a);
+      HS_HIP(hipGetLastError());
+    }
   }
   if (sep) c->sepValid = true;
   if (beside && !xch) {
-    c->gath_th = true;
+    c->gath_th = 1;
     if (!defer) HS_TRY(launch_combine(c));
   }
   if (xch) {
@@ -687,10 +694,11 @@ static int launch_solve(hs_ctx* c, int flags, int iteration, bool log) {
         a.sys = c->d_gsys;
         a.gsys = c->d_gsys; a.nranks = c->nranks; a.gstride = c->SX(); a.sys_out = c->d_sys;
       }
-      a.th_local = c->gath_th ? 1 : 0;
+      a.th_local = c->gath_th;
       a.th = red_args(c, false);
       grid = c->gath_th ? 2 : 1;
-      c->gath_pending = c->gath_th = false;
+      c->gath_pending = false;
+      c->gath_th = 0;
     }
   }
   a.HM = c->hm_zero ? nullptr : c->d_HM;

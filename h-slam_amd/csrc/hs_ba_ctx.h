@@ -240,7 +240,11 @@ struct hs_ctx {
   // gath_pending: a gather whose sums are formed by the next solve launch (the fused GN loop); gath_th: the
   // threshold select is still to run (block 1 of that launch; single-rank windows below kLin8MinPoints too)
   double* d_gsys = nullptr;
-  bool gath_pending = false, gath_th = false;
+  // gath_th: setNewFrameEnergyTH's select still to run as block 1 of the next solve / combine launch: 1 the one-block
+  // select over every candidate (pass 1 in LDS), 2 only pass 3 of the multi-block select (passes 1 and 2 ran in the
+  // reduce / stitch launches: large windows, instead of a launch of its own after the stitch)
+  bool gath_pending = false;
+  int gath_th = 0;
   // in-process rank group (test hook hs_ba_debug_group): the same exchange by device copies between the contexts of
   // one process, driven by hs_ba_group_linearize / hs_ba_group_iterate
   std::vector<hs_ctx*> group;

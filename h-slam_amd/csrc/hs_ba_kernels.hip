@@ -2135,8 +2135,9 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
       return;
     }
   }
-  if (blockIdx.x == 1) {  // setNewFrameEnergyTH over the (gathered) candidates, beside the solve
-    th_select_block(a.th, reinterpret_cast<unsigned int*>(A), SOLVE_TH_CAP, true);
+  if (blockIdx.x == 1) {  // setNewFrameEnergyTH over the (gathered) candidates, beside the solve (th_local 1: the
+                          // whole select; 2: pass 3 of the multi-block select, passes 1 and 2 ran before)
+    th_select_block(a.th, reinterpret_cast<unsigned int*>(A), SOLVE_TH_CAP, a.th_local == 1);
     return;
   }
   HS_TRACE(a, 0);
@@ -2567,7 +2568,7 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
 __global__ __launch_bounds__(SOLVE_NT) void hs_k_combine(HsSolveArgs a) {
   __shared__ double A[HS_MAXDIM * HS_MAXDIM];
   if (blockIdx.x == 1) {
-    th_select_block(a.th, reinterpret_cast<unsigned int*>(A), SOLVE_TH_CAP, true);
+    th_select_block(a.th, reinterpret_cast<unsigned int*>(A), SOLVE_TH_CAP, a.th_local == 1);
     return;
   }
   if (!a.gsys) return;  // test hook: the select block alone

@@ -214,7 +214,9 @@ struct HsSolveArgs {
   int dbg;                     // experiments (env HS_SOLVE_DBG); 0 in production
   // multi-rank exchange (hs_ba.cpp exchange()): gsys = [nranks][gstride] the ranks' system vectors + energies as
   // all-gathered, summed here in rank order (every rank the same sums) in place of sys / sysE; sys_out receives the
-  // sum.  th_local: the launch's block 1 runs setNewFrameEnergyTH's select over the gathered candidates (th).
+  // sum.  th_local: the launch's block 1 runs setNewFrameEnergyTH's select over the gathered candidates (th): 1 the
+  // whole select (pass 1 counted in LDS), 2 pass 3 of the multi-block select (th_hist / th_hist2 / th_surv filled by
+  // the reduce and stitch launches).
   const double* gsys;
   int nranks, gstride;
   double* sys_out;

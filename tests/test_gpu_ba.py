@@ -469,13 +469,20 @@ def test_optimize_break_device_matches_host(scene2k, monkeypatch):
     assert n0 == n1 and np.array_equal(e0, e1)
     assert np.array_equal(s0, s1) and np.array_equal(d0, d1) and np.array_equal(h0, h1)
     assert t0 == t1 and np.array_equal(r0, r1)
+    # the break iteration is a categorical output: pinned exactly.  The window's canbreak decision is robust to the
+    # fp order (the oracle's own single-thread and 8-thread pools break at the same iteration, checked here), so
+    # it is not near its threshold and the library must agree with it exactly.
     from oracle_ffi import OracleBA
-    o = OracleBA(scene2k)
-    o.optimize(6)
-    no, eo = o.optimize(6, allow_break=True)
-    print(f"converged window: gpu breaks after {n0}, oracle after {no}")
-    assert n0 < 6 and abs(n0 - no) <= 1
-    k = min(n0, no)
+    nos = []
+    for nt in (1, 8):
+        o = OracleBA(scene2k, nthreads=nt)
+        o.optimize(6)
+        no, eo = o.optimize(6, allow_break=True)
+        nos.append(no)
+    print(f"converged window: gpu breaks after {n0}, oracle after {nos[0]} (1 thread) / {nos[1]} (8 threads)")
+    assert nos[0] == nos[1], nos
+    assert n0 < 6 and n0 == nos[1]
+    k = n0
     assert np.all(np.abs(e0[:k + 1] - eo[:k + 1]) <= 1e-3 * np.abs(eo[:k + 1]))
 
 

@@ -283,7 +283,9 @@ def test_keyframe_sequence_drift_vs_oracle():
     Src/EnergyFunctional.cpp:456-609).  Nothing is re-seeded between keyframes, so fp-order differences and any
     decision that flips accumulate.  Compared at the end: the window's frame states and linearization points, the
     calibration, the marginal prior HM / bM and the point set and depths; along the way the per-keyframe
-    energies.  Bars (stated in each assert) are set above what the two chains measure apart (printed)."""
+    energies.  Bars (stated in each assert) are ~3-4x what the two chains measure apart (printed; both chains are
+    deterministic, so the figures repeat run to run -- profiles/r06_m2_pytest_gpu.txt: energies 9.4e-4, frame state
+    5.7e-5, evalPT 5.1e-5, calib 3.2e-10, HM 9.3e-4, bM 8.0e-4, idepth 9.6e-5, the point sets identical)."""
     from oracle_keyframe import OracleKeyframeBA
     from hslam_amd.keyframe import KeyframeBA, make_ba_sequence
     seq = make_ba_sequence(n_kf=12, points_per_kf=200, seed=7)
@@ -299,7 +301,7 @@ def test_keyframe_sequence_drift_vs_oracle():
         print(f"kf {k}: energies rel dev max {rel.max():.2e}; points gpu {ig['n_points']} oracle {io['n_points']}; "
               f"marginalized gpu {ig.get('marginalized_points')} oracle {io.get('marginalized_points')}")
         assert ig["iters"] == io["iters"]
-        assert rel.max() <= 1e-2, (k, rel)
+        assert rel.max() <= 3e-3, (k, rel)  # measured <= 9.4e-4
     assert drv.frames == orc.frames
     fg, fo = drv.ba.frames(), orc.frame_states()
     fe = drv.ba.frame_eval()
@@ -317,11 +319,11 @@ def test_keyframe_sequence_drift_vs_oracle():
     dd = max(abs(pg[key] - po[key]) / abs(po[key]) for key in common)
     print(f"final: frame state |d| {ds:.2e}, evalPT |d| {de:.2e}, calib |d| {dc:.2e}, HM worst ratio {dH:.2e}, "
           f"bM rel norm {db:.2e}, points common {len(common)} differing {only}, idepth rel {dd:.2e}")
-    assert ds <= 1e-3                 # frame states (scaled tangent units)
-    assert de <= 1e-4                 # linearization points (quaternion / translation data)
-    assert dc <= 1e-6
-    assert dH <= 1e-2                 # HM: |d| <= 1e-2 (|ref| + 1e-3 max|diag|), 100x the single-step H bar
-    assert db <= 1e-2                 # bM: ||d|| <= 1e-2 ||ref||
-    assert only <= 0.01 * len(common)
-    assert dd <= 1e-2
+    assert ds <= 2e-4                 # frame states (scaled tangent units); measured 5.7e-5
+    assert de <= 2e-4                 # linearization points (quaternion / translation data); measured 5.1e-5
+    assert dc <= 1e-8                 # measured 3.2e-10
+    assert dH <= 3e-3                 # HM: |d| <= 3e-3 (|ref| + 1e-3 max|diag|); measured 9.3e-4
+    assert db <= 3e-3                 # bM: ||d|| <= 3e-3 ||ref||; measured 8.0e-4
+    assert only == 0                  # the same point set (every decision agreed)
+    assert dd <= 3e-4                 # measured 9.6e-5
     drv.ba.close()
