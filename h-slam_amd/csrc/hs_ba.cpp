@@ -41,6 +41,7 @@ void drop_graph(hs_ctx* c) {
 // ppw (more blocks), HS_ACC_EXACT one block per host
 int max_blocks_for(int capP) {
   int m = std::max(kLinBlocksTarget, kLin8BlocksTarget) + HS_MAXF;
+  if (const char* e = std::getenv("HS_LIN8_BLOCKS")) m = std::max(m, std::atoi(e) + HS_MAXF);
   if (const char* e = std::getenv("HS_LIN_PPW")) {
     const int ppw = std::max(1, std::atoi(e));
     m = std::max(m, capP / (HS_LIN_NW * ppw) + 1 + HS_MAXF);
@@ -497,6 +498,13 @@ static int launch_linearize(hs_ctx* c, int fuse, bool marg = false, bool accumul
   a.p_JpJdF = c->d_p_JpJdF; a.p_step = c->d_p_step;
   a.fix_relBL = c->d_fix_relBL; a.fix_nGood = c->d_fix_nGood;
   a.newest_cand = c->d_cand + (size_t)c->rank * c->cand_stride;
+  // large single-rank windows: hs_k_lin8 counts setNewFrameEnergyTH's pass-1 histogram itself (env HS_LIN8_HIST=0:
+  // hs_k_reduce's histogram blocks, as before)
+  const char* lh = std::getenv("HS_LIN8_HIST");
+  const bool lin_hist = c->lin8 && !marg && !fix && accumulate && c->th_multi && !c->multi_rank() &&
+                        !(lh && lh[0] == '0');
+  a.th_hist = lin_hist ? c->d_th_hist : nullptr;
+  c->hist_in_lin = lin_hist;
   a.part = c->d_part; a.part_e = c->d_part_e;
   a.trace = c->d_tr_lin;
   a.brk = c->brk_active ? 1 : 0;
@@ -608,7 +616,11 @@ static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = fals
   // launch's last block it outlasted the stitch's blocks by ~1.5 us at 2k.  Large single-rank windows: pass 1 in
   // hs_k_reduce's histogram blocks, pass 2 in the stitch launch, pass 3 after it.
   const bool beside = !skip_threshold && !readback && (xch || !c->th_multi);
-  a.nhist = (skip_threshold || beside) ? 0 : a.nhist;
+  const bool lin_hist = c->hist_in_lin && !readback;  // the linearization counted pass 1 (hs_k_lin8)
+  if (!readback) c->hist_in_lin = false;
+  a.nhist = (skip_threshold || beside || lin_hist) ? 0 : a.nhist;
+  if (lin_hist && skip_threshold)  // counted but not consumed: the histogram must be zero for the next select
+    HS_HIP(hipMemsetAsync(c->d_th_hist, 0, sizeof(unsigned int) * HS_TH_BINS, c->stream));
   if (!readback) {
     hipLaunchKernelGGL(hs_k_reduce, dim3(c->nF * c->Q + 1 + a.nhist), dim3(256), 0, c->stream, a);
     HS_HIP(hipGetLastError());

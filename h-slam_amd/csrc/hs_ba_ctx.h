@@ -130,6 +130,7 @@ struct hs_ctx {
   // one-block pass 3 over pass 2's survivors, instead of the stitch's single select block scanning every candidate
   // twice (env HS_TH_MULTI=0 / 1 forces it off / on)
   bool th_multi = false;
+  bool hist_in_lin = false;       // the last linearize launch counted the select's pass-1 histogram (hs_k_lin8)
   bool sepValid = false;          // d_sep holds the separate HA / HSC of the last linearization
   std::vector<int> pt_host, res_point, res_target, host_pt_begin;
   std::vector<int> res_of_slot;   // [nP*8]

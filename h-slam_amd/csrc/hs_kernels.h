@@ -115,6 +115,10 @@ struct HsLinArgs {
   float* fix_relBL;
   int* fix_nGood;
   float* newest_cand;          // [n] energy of the point's residual into the newest frame, -1 = none
+  // nullable (hs_k_lin8, large single-rank windows): setNewFrameEnergyTH's pass-1 histogram (HsRedArgs::th_hist) of
+  // the candidates, counted as they are written (an LDS histogram per block, its nonzero bins added at the end), in
+  // place of hs_k_reduce's histogram blocks
+  unsigned int* th_hist;
   // block partials: part[blk][ne][64] (fp32, waves summed in wave order), part_e[blk][4] (fp64 energy,
   // sum |idepth|, #points)
   float* part;

@@ -82,7 +82,8 @@ __device__ __forceinline__ float3 interp33_8b(__amdgpu_buffer_rsrc_t img, int sl
   constexpr int TB = L8_TEXEL_BYTES;
   const int ix = (int)x, iy = (int)y;
   const float dx = __builtin_amdgcn_fractf(x), dy = __builtin_amdgcn_fractf(y), dxdy = dx * dy;
-  const int vo = __mul24(__mul24(iy, w) + ix, TB) + slot_b, row = __builtin_amdgcn_readfirstlane(w * TB);
+  const int vo = __mul24(__mul24(iy, w) + ix, TB) + slot_b;
+  const int row = __builtin_amdgcn_readfirstlane(w * TB);
   const float3 p00 = ld_texel3(img, vo, 0), p10 = ld_texel3(img, vo + TB, 0), p01 = ld_texel3(img, vo, row),
                p11 = ld_texel3(img, vo + TB, row);
   const float w11 = dxdy, w01 = dy - dxdy, w10 = dx - dxdy, w00 = 1 - dx - dy + dxdy;
@@ -289,6 +290,7 @@ __device__ __forceinline__ void l8_load(const HsLinArgs& a, int pc, int t, L8In&
 __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs a) {
   __shared__ L8Const K;
   __shared__ L8Lds U;
+  __shared__ unsigned int H1[HS_TH_BINS];  // the block's pass-1 histogram of its candidates (a.th_hist)
 #if L8_LDS_ACC
   __shared__ float ACC[L8_NW][L8_NACC][64];
 #endif
@@ -324,8 +326,11 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
       K.xad[tid] = s1 + s2;
     }
     if (tid < 4) K.cs[tid] = a.st->cstep[tid];
+    if (a.th_hist)
+      for (int i = tid; i < HS_TH_BINS; i += HS_LIN8_NT) H1[i] = 0u;
   }
   __syncthreads();
+  if (a.trace && tid == 0) a.trace[(size_t)b * 16 + 11] = wall_clock64();  // the block constants are in
 
   const HsCalib cal = a.st->dcal;
   const HsLinParams lp = a.lp;
@@ -675,7 +680,12 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
         a.r_center[sl * 3 + 2] = centre[2];
       }
     }
-    if (valid && t == nF - 1) a.newest_cand[p] = eval ? S[0] : -1.f;
+    if (valid && t == nF - 1) {
+      const float cv = eval ? S[0] : -1.f;
+      a.newest_cand[p] = cv;
+      const unsigned cb = __float_as_uint(cv);
+      if (a.th_hist && cb <= 0x7f800000u) atomicAdd(&H1[cb >> 19], 1u);  // >= 0 and not NaN, as red_th_hist_block
+    }
     // ---- takeData (Include/OptimizationClasses.h:155-161): JpJdF and the slot's terms of the per-point sums
     float jj[8], tbd, tHdd, tcd[4];
     {
@@ -858,6 +868,7 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
 #endif
     }
     __builtin_amdgcn_wave_barrier();  // the scratch is rewritten by the next group
+    if (a.trace && tid == 0 && gi == wv) a.trace[(size_t)b * 16 + 12] = wall_clock64();  // wave 0's first group
   }
   if (a.trace && tid == 0) a.trace[(size_t)b * 16 + 1] = wall_clock64();
   if (a.trace && lane == 0 && wv < 8) a.trace[(size_t)b * 16 + 3 + wv] = wall_clock64();  // each wave's loop end
@@ -936,6 +947,9 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
     for (int w = 1; w < L8_NW; w++) s += se[w][tid];
     a.part_e[(size_t)b * 4 + tid] = s;
   }
+  if (a.th_hist)  // (every wave's candidates are in: the barriers above)
+    for (int i = tid; i < HS_TH_BINS; i += HS_LIN8_NT)
+      if (const unsigned int v = H1[i]) atomicAdd(&a.th_hist[i], v);
   if (a.trace && tid == 0) a.trace[(size_t)b * 16 + 2] = wall_clock64();
 }
 

@@ -138,6 +138,30 @@ def test_multi_block_select_matches_in_stitch_select(scene2k):
         assert np.array_equal(a, b)
 
 
+def test_lin8_counted_histogram_matches_reduce_blocks(scene_kitti20k):
+    """The multi-block select's pass-1 histogram counted inside hs_k_lin8 as the candidates are written (the default
+    for large single-rank windows) against hs_k_reduce's histogram blocks (HS_LIN8_HIST=0) and against the one-block
+    select (HS_TH_MULTI=0): integer counts, so the fused GN loop's energies, thresholds, frame states and depths are
+    bit-identical (HS_TH_MULTI=1 / HS_LIN8=1 force the large-window path on the 20k window)."""
+    from hslam_amd.ba import BAWindow
+    outs = []
+    for multi, lin_hist in (("1", "1"), ("1", "0"), ("0", "1")):
+        os.environ.update(HS_TH_MULTI=multi, HS_LIN8="1", HS_LIN8_HIST=lin_hist)
+        try:
+            g = BAWindow(scene_kitti20k)
+            g.linearizeAll(reset=True)
+            e = g.iterate(0, 5)
+            f = g.frames()
+            outs.append((e, f["energyTH"], f["state"], g.points()["idepth"]))
+            g.close()
+        finally:
+            for k in ("HS_TH_MULTI", "HS_LIN8", "HS_LIN8_HIST"):
+                os.environ.pop(k, None)
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert np.array_equal(a, b)
+
+
 def _fastmath(a, b):
     import ctypes as C
     from hslam_amd import _lib
