@@ -1,5 +1,5 @@
 #!/bin/bash
-# round-5 evidence (same as round 4): smoke, every bench line (CPU baselines included), the sweep, rocprofv3 kernel trace + stats of
+# round-6 evidence (as rounds 4-5): smoke, every bench line (CPU baselines included), the sweep, rocprofv3 kernel trace + stats of
 # the headline.  usage: tools/evidence.sh TAG   (outputs under gpurun_out/TAG/)
 TAG=${1:-ev}
 OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG
