@@ -66,7 +66,8 @@ def test_two_shards_reproduce_the_full_window(scene2k):
         w.close()
 
 
-def test_rank_group_runs_the_multi_rank_path(scene2k):
+@pytest.mark.parametrize("th_multi", ["0", "1"])
+def test_rank_group_runs_the_multi_rank_path(scene2k, th_multi, monkeypatch):
     """The library's multi-rank path with two ranks on one GPU (the in-process group of hs_ba_debug_group: the
     exchange is device copies where a multi-GPU run all-gathers over RCCL; every other launch is the RCCL path's):
     one exchange of [system vector | energies] and candidates per linearization, the rank-order sums, the
@@ -74,8 +75,11 @@ def test_rank_group_runs_the_multi_rank_path(scene2k):
       * after a linearization every rank holds the same summed vector, bit-equal to the sum of the two shards'
         own vectors in rank order, and the full window's threshold (bit-exact: the union of the candidates);
       * the fused GN loop (deferred sums: the solve's prefetch) keeps both ranks' frame states bit-identical and
-        follows the full window's trajectory (rel 1e-3, the optimize-trajectory bar)."""
+        follows the full window's trajectory (rel 1e-3, the optimize-trajectory bar).
+    th_multi = 1 forces the large-window select (HS_TH_MULTI): on the ranks, the pass-1 histogram and pass 2 over the
+    gathered candidates after the exchange, pass 3 as block 1 of the next solve / combine launch (round 6)."""
     from hslam_amd.ba import BAWindow
+    monkeypatch.setenv("HS_TH_MULTI", th_multi)
     shard_scenes = [scene2k.shard(r, 2) for r in range(2)]
     full = BAWindow(scene2k)
     ef = full.linearizeAll(reset=True)
