@@ -661,8 +661,10 @@ static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = fals
   if (multi) {  // pass 3: the select over pass 2's histogram and survivors.  It only feeds the next linearize: in the
                 // fused GN loop it runs as block 1 of the next solve launch, beside the solve (defer), else as a
                 // one-block launch now (env HS_TH_BESIDE=0: always the launch)
+    // (not under the device-side break: a launch after the break would rerun pass 3 on the consumed histograms,
+    // where hs_k_th_select's own launch returns at entry)
     const char* tb = std::getenv("HS_TH_BESIDE");
-    if (defer && !(tb && tb[0] == '0')) {
+    if (defer && !c->brk_active && !(tb && tb[0] == '0')) {
       c->gath_th = 2;
     } else {
       hipLaunchKernelGGL(hs_k_th_select, dim3(1), dim3(HS_STITCH_NT), 0, c->stream, a);
@@ -1872,6 +1874,10 @@ int hs_ba_time_linearize(hs_ctx* c, int reps, double* avg_ms) {
   HS_HIP(hipEventRecord(c->ev[0], c->stream));
   for (int k = 0; k < reps; k++) HS_TRY(launch_linearize(c, 0));
   HS_HIP(hipEventRecord(c->ev[1], c->stream));
+  if (c->hist_in_lin) {  // no reduce consumes these passes' pass-1 counts: the next select must find it zero
+    HS_HIP(hipMemsetAsync(c->d_th_hist, 0, sizeof(unsigned int) * HS_TH_BINS, c->stream));
+    c->hist_in_lin = false;
+  }
   HS_HIP(hipEventSynchronize(c->ev[1]));
   float ms = 0;
   HS_HIP(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));

@@ -450,25 +450,31 @@ def test_optimize_break_forced(scene2k, min_opt):
     assert np.count_nonzero(tg["drop"] != drop_o) <= 0.002 * scene2k.n_res
 
 
-def test_optimize_break_device_matches_host(scene2k, monkeypatch):
+@pytest.mark.parametrize("th_multi", ["0", "1"])
+def test_optimize_break_device_matches_host(scene2k, monkeypatch, th_multi):
     """The device-side break test (launches after the break return at entry; the HdiF ping-pong is put back by the
     host) and the host-side one (HS_HOST_BREAK=1: canbreak read back after every iteration) give the same run bit
     for bit: iteration count, energies, frame states, depths, HdiF and the following tail.  A converged window
-    (optimize(6) twice, default thresholds) breaks in the second call as the oracle's does."""
+    (optimize(6) twice, default thresholds) breaks in the second call as the oracle's does.  th_multi = 1 forces the
+    large-window select (HS_TH_MULTI): its pass 3 must not rerun on consumed histograms after the break (the
+    threshold is compared too)."""
     from hslam_amd.ba import BAWindow
+    monkeypatch.setenv("HS_TH_MULTI", th_multi)
     runs = []
     for host in ("0", "1"):
         monkeypatch.setenv("HS_HOST_BREAK", host)
         g = BAWindow(scene2k)
         g.optimize(6)
         n, e = g.optimize(6, allow_break=True)
+        th = g.frames()["energyTH"]
         z = np.zeros(scene2k.n_points)
         tail = g.fixLinearization(z, z.astype(np.int32))
-        runs.append((n, e, g.frames()["state"], g.points()["idepth"], tail["HdiF"], tail["energy"], tail["drop"]))
-    (n0, e0, s0, d0, h0, t0, r0), (n1, e1, s1, d1, h1, t1, r1) = runs
+        runs.append((n, e, g.frames()["state"], g.points()["idepth"], tail["HdiF"], tail["energy"], tail["drop"], th))
+    (n0, e0, s0, d0, h0, t0, r0, th0), (n1, e1, s1, d1, h1, t1, r1, th1) = runs
     assert n0 == n1 and np.array_equal(e0, e1)
     assert np.array_equal(s0, s1) and np.array_equal(d0, d1) and np.array_equal(h0, h1)
     assert t0 == t1 and np.array_equal(r0, r1)
+    assert np.array_equal(th0, th1)
     # the break iteration is a categorical output: pinned exactly.  The window's canbreak decision is robust to the
     # fp order (the oracle's own single-thread and 8-thread pools break at the same iteration, checked here), so
     # it is not near its threshold and the library must agree with it exactly.
