@@ -247,7 +247,7 @@ int ensure_capacity(hs_ctx* c, int W, int H, int capP, int capBlk) {
   HS_TRY(dalloc(&c->d_le_out, 1, c->stream));
   HS_TRY(dalloc(&c->d_ref_pts, (size_t)4 * capP, c->stream));
   HS_TRY(dalloc(&c->d_ref_n, 1, c->stream));
-  HS_TRY(dalloc(&c->d_ticket, 1, c->stream));
+  HS_TRY(dalloc(&c->d_ticket, 2, c->stream));  // [0] the stitch's retire ticket, [1] the adjoint expectation
   // incremental window: the commit blob (pinned + device) and a raw level-0 image's staging
   c->h_stage_cap = c->d_stage_cap = stage_bytes(capP);
   HS_HIP(hipHostMalloc((void**)&c->h_stage, c->h_stage_cap));
@@ -356,11 +356,9 @@ size_t fstage_bytes() {
          (size_t)2 * HS_MAXDIM * HS_NNS * sizeof(double);
 }
 
-// the stamp of a new adjoint upload; a captured graph holds the old sequence in its launch arguments, so it goes
-static unsigned int next_adj_seq(hs_ctx* c) {
-  drop_graph(c);
-  return ++c->adj_seq;
-}
+// the stamp of a new adjoint upload (hs_k_fix_frames also writes it to the expectation word, d_ticket[1], which the
+// readers compare with: no launch argument carries it, so a captured GN loop graph survives the upload)
+static unsigned int next_adj_seq(hs_ctx* c) { return ++c->adj_seq; }
 
 int wait_uploads(hs_ctx* c) {
   HS_HIP(hipEventSynchronize(c->ev_upload));
@@ -391,7 +389,7 @@ int upload_frames(hs_ctx* c) {
   HS_HIP(hipEventRecord(c->ev_upload, c->stream));
   // the pairs' precalc and adjoints on the device from the uploaded state (the expressions of the host forms)
   hipLaunchKernelGGL(hs_k_fix_frames, dim3(1), dim3(64), 0, c->stream, c->d_state, c->d_pre, c->d_adHost,
-                     c->d_adTarget, c->d_adHostF, c->d_adTargetF, c->P, 0, next_adj_seq(c));
+                     c->d_adTarget, c->d_adHostF, c->d_adTargetF, c->P, 0, next_adj_seq(c), c->d_ticket + 1);
   HS_HIP(hipGetLastError());
   c->h_state_valid = true;
   return HS_OK;
@@ -655,7 +653,7 @@ static int launch_reduce(hs_ctx* c, bool skip_threshold = false, bool sep = fals
     st.res_ticket = c->d_ticket;
   }
   st.status = reinterpret_cast<int*>((char*)c->d_state + offsetof(HsDevState, status));
-  st.adj_seq = c->adj_seq;
+  st.adj_expect = c->d_ticket + 1;
   hipLaunchKernelGGL(hs_k_stitch, dim3(nS), dim3(HS_STITCH_NT), 0, c->stream, st);
   HS_HIP(hipGetLastError());
   if (multi) {  // pass 3: the select over pass 2's histogram and survivors.  It only feeds the next linearize: in the
@@ -729,7 +727,7 @@ static int launch_solve(hs_ctx* c, int flags, int iteration, bool log) {
   a.brk = c->brk_active ? 1 : 0;
   a.minOpt = c->P.minOptIterations;
   a.chk_adj = 1;
-  a.adj_seq = c->adj_seq;
+  a.adj_expect = c->d_ticket + 1;
   if (const char* e = std::getenv("HS_SOLVE_DBG")) a.dbg = std::atoi(e);
   hipLaunchKernelGGL(hs_k_solve, dim3(grid), dim3(HS_SOLVE_NT), 0, c->stream, a);
   HS_HIP(hipGetLastError());
@@ -1448,7 +1446,7 @@ int hs_ba_fix_linearization(hs_ctx* c, double* energy_out, uint8_t* drop_out, fl
   // the newest frame's setEvalPT + EnergyFunctional::setAdjointsF + setPrecalcValues, on the device (the nullspaces
   // and projector follow on the host when the state is next fetched)
   hipLaunchKernelGGL(hs_k_fix_frames, dim3(1), dim3(64), 0, c->stream, c->d_state, c->d_pre, c->d_adHost,
-                     c->d_adTarget, c->d_adHostF, c->d_adTargetF, c->P, 1, next_adj_seq(c));
+                     c->d_adTarget, c->d_adHostF, c->d_adTargetF, c->P, 1, next_adj_seq(c), c->d_ticket + 1);
   HS_HIP(hipGetLastError());
   c->h_state_valid = false;
   c->tail_pending = true;

@@ -198,7 +198,8 @@ struct hs_ctx {
   double *d_adHost = nullptr, *d_adTarget = nullptr;  // [HS_MAXF^2][64] + the stamp word (HS_ADJ_STAMP)
   float *d_adHostF = nullptr, *d_adTargetF = nullptr;
   unsigned int adj_seq = 0;        // sequence of the last adjoint upload enqueued (hs_k_fix_frames' stamp)
-  unsigned int* d_ticket = nullptr;  // hs_k_stitch's retire ticket (zero between launches)
+  unsigned int* d_ticket = nullptr;  // [0] hs_k_stitch's retire ticket (zero between launches), [1] the sequence
+                                     // of the last adjoint upload on the device (hs_k_fix_frames; HS_ADJ_STAMP)
   double *d_HM = nullptr, *d_bM = nullptr, *d_Nproj = nullptr;
   float* d_xAd = nullptr;
   double* d_x = nullptr;

@@ -1819,15 +1819,19 @@ __global__ __launch_bounds__(ST_NT) void hs_k_stitch(HsStitchArgs a) {
   __shared__ double lds[ST_LDS];
   __shared__ int s_last;
   // the fp64 adjoints' stamp (HS_ADJ_STAMP), requested before the block's work and compared after it
-  const bool chk = a.status && blockIdx.x == 0 && threadIdx.x == 0;
+  // (a launch stopped by the device-side break stitches nothing and checks nothing)
+  const bool run = !(a.red.stop && *a.red.stop);
+  const bool chk = run && a.status && blockIdx.x == 0 && threadIdx.x == 0;
   double sH = 0.0, sT = 0.0;
+  unsigned int ex = 0u;
   if (chk) {
     sH = a.adHost[HS_ADJ_STAMP];
     sT = a.adTarget[HS_ADJ_STAMP];
+    ex = *a.adj_expect;
   }
-  if (!(a.red.stop && *a.red.stop)) stitch_block(a, blockIdx.x, lds);
+  if (run) stitch_block(a, blockIdx.x, lds);
   if (chk) {
-    if (sH != (double)a.adj_seq || sT != (double)a.adj_seq) atomicOr(a.status, (int)HS_STATUS_STALE64);
+    if (sH != (double)ex || sT != (double)ex) atomicOr(a.status, (int)HS_STATUS_STALE64);
     else atomicAnd(a.status, ~(int)HS_STATUS_STALE64);
   }
   if (!a.res_out) return;
@@ -2194,6 +2198,7 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
   // the fp32 adjoints' stamps (HS_ADJ_STAMP), checked after the counters' reset below
   const unsigned int sHF = a.chk_adj ? reinterpret_cast<const unsigned int*>(a.adHostF)[HS_ADJ_STAMP + vz] : 0u;
   const unsigned int sTF = a.chk_adj ? reinterpret_cast<const unsigned int*>(a.adTargetF)[HS_ADJ_STAMP + vz] : 0u;
+  const unsigned int sEx = a.chk_adj ? a.adj_expect[vz] : 0u;
   const bool hasHM = a.HM != nullptr;
   if (solve) {
     axv = a.sys[AUX0 + min(tid, nF * 64 - 1)];
@@ -2281,7 +2286,7 @@ __global__ __launch_bounds__(SOLVE_NT) void hs_k_solve(HsSolveArgs a) {
     }
     s_it = a.iteration >= 0 ? a.iteration : st->iteration;
     if (a.chk_adj)
-      st->status = (st->status & ~(int)HS_STATUS_STALE32) | ((sHF != a.adj_seq || sTF != a.adj_seq) ? HS_STATUS_STALE32 : 0);
+      st->status = (st->status & ~(int)HS_STATUS_STALE32) | ((sHF != sEx || sTF != sEx) ? HS_STATUS_STALE32 : 0);
   }
   const double lambda = 1e-5;  // SOLVER_FIX_LAMBDA
 
@@ -2665,7 +2670,7 @@ __global__ void hs_k_marg_update(const double* sep, const double* sep_aux, doubl
 // adjoints (System::setPrecalcValues, EnergyFunctional::setAdjointsF) from the device state
 __global__ __launch_bounds__(64) void hs_k_fix_frames(HsDevState* st, HsPrecalc* pre, double* adH, double* adT,
                                                       float* adHF, float* adTF, hs_params P, int fix,
-                                                      unsigned int seq) {
+                                                      unsigned int seq, unsigned int* expect) {
   const int nF = st->nF, tid = threadIdx.x;
   if (fix && tid == 0) {  // newStateZero = 0 except segment(6, 2) = the newest frame's a / b; setEvalPT(PRE_worldToCam, .)
     hs::FrameH& f = st->frames[nF - 1];
@@ -2695,6 +2700,7 @@ __global__ __launch_bounds__(64) void hs_k_fix_frames(HsDevState* st, HsPrecalc*
     adT[HS_ADJ_STAMP] = (double)seq;
     reinterpret_cast<unsigned int*>(adHF)[HS_ADJ_STAMP] = seq;
     reinterpret_cast<unsigned int*>(adTF)[HS_ADJ_STAMP] = seq;
+    *expect = seq;
   }
 }
 

@@ -17,10 +17,12 @@ constexpr int HS_LIN_NT = 64 * HS_LIN_NW;
 constexpr int HS_LIN8_NT = 64 * HS_LIN8_WAVES;  // hs_k_lin8 workgroup size (8 points per wave at a time)
 constexpr int HS_NNS = 7;         // gauge nullspaces: 6 pose + 1 scale (System::getNullspaces)
 // The adjoint buffers (fp64 d_adHost / d_adTarget, fp32 d_adHostF / d_adTargetF: [HS_MAXF^2][64]) carry one stamp word
-// after the adjoints: hs_k_fix_frames writes the upload's sequence number there (the fp32 buffers its bits), and every
-// reader launch (hs_k_stitch: fp64, hs_k_solve: fp32) compares it with the sequence of the last upload the host
-// enqueued.  A mismatch -- adjoints that never arrived, or a zero fill landing after them -- sets HS_STATUS_STALE in
-// HsDevState::status, which the C-ABI returns as HS_ERR_STATE instead of a system with zero frame rows.
+// after the adjoints: hs_k_fix_frames writes the upload's sequence number there (the fp32 buffers its bits) and into
+// a separate expectation word, and every reader launch (hs_k_stitch: fp64, hs_k_solve: fp32) compares the two.  A
+// mismatch -- a zero fill or any other write landing on the buffers after the upload -- sets HS_STATUS_STALE in
+// HsDevState::status, which the C-ABI returns as HS_ERR_STATE instead of a system with zero frame rows.  The
+// expectation lives in device memory, not in the launch arguments, so a captured GN loop graph stays valid across
+// uploads (hs_ba_fix_linearization uploads once per keyframe).
 constexpr int HS_ADJ_STAMP = HS_MAXF * HS_MAXF * 64;
 // status bits: each stamp check owns its bit and sets / clears it at every launch (the stitch the fp64 one, the
 // solve the fp32 one), so the bits describe the adjoints the last launches read
@@ -190,7 +192,7 @@ struct HsStitchArgs {
   unsigned int* res_ticket;    // with res_out: blocks retired so far (zero between launches); the last one writes the
                                // results, so the done word means the whole launch has finished
   int* status;                 // nullable: &HsDevState::status, HS_STATUS_STALE when the fp64 adjoints' stamp is not
-  unsigned int adj_seq;        // the sequence of the last adjoint upload
+  const unsigned int* adj_expect;  // the sequence of the last adjoint upload (written by hs_k_fix_frames)
 };
 
 enum { HS_SOLVE = 1, HS_APPLY = 2 };
@@ -232,8 +234,8 @@ struct HsSolveArgs {
   // 0 returns at entry and sets st->stop) when the previous step allowed it (st->canbreak) and the previous
   // iteration index was >= minOpt; block 1's threshold select runs anyway (same candidates, same result)
   int brk, minOpt;
-  int chk_adj;                 // compare the fp32 adjoints' stamp with adj_seq (HS_STATUS_STALE on a mismatch)
-  unsigned int adj_seq;
+  int chk_adj;                 // compare the fp32 adjoints' stamp with *adj_expect (HS_STATUS_STALE on a mismatch)
+  const unsigned int* adj_expect;
 };
 
 struct HsResubArgs {
@@ -287,7 +289,7 @@ __global__ void hs_k_marg_delta(const HsDevState* st, const float* adHF, const f
 __global__ void hs_k_marg_update(const double* sep, const double* sep_aux, double* HM, double* bM, int nF, int SL,
                                  double w);
 __global__ void hs_k_fix_frames(HsDevState* st, HsPrecalc* pre, double* adH, double* adT, float* adHF, float* adTF,
-                                hs_params P, int fix, unsigned int seq);
+                                hs_params P, int fix, unsigned int seq, unsigned int* expect);
 __global__ void hs_k_debug_stall(long long ticks);  // test hook: a bounded spin on the wall clock (a stalled peer)
 __global__ void hs_k_lenergy(int n, const float* idepth, const float* idepth_zero, const float* priorF, float* chunk,
                              double* out);
