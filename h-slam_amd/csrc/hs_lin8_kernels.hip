@@ -25,6 +25,7 @@
 
 namespace {
 
+typedef float l8f4 __attribute__((ext_vector_type(4)));  // an MFMA accumulator tile row set (v_mfma_f32_16x16x4_f32)
 constexpr float SCALE_F8 = 50.0f, SCALE_C8 = 50.0f, SCALE_IDEPTH8 = 1.0f;
 constexpr int L8_NW = HS_LIN8_NT / 64;  // waves per block
 constexpr int NTOP = 91;  // AccumulatorApprox entries of one (host, target) block: Data 55 | TopRight 30 | BotRight 6
@@ -64,6 +65,12 @@ constexpr int Q8_N = 17;  // per-pixel quantities summed over the pattern
 #endif
 #ifndef L8_LDS_ACC
 #define L8_LDS_ACC 1    // the per-lane accumulators (T slice, accD / accE / accEB / accHcc) live in LDS between groups
+#endif
+#ifndef L8_MFMA_SC
+#define L8_MFMA_SC 1    // the Schur accumulators (accD / accE / accEB / accHcc / accbc) by v_mfma_f32_16x16x4_f32 (below)
+#endif
+#if L8_MFMA_SC && !L8_LDS_ACC
+#error "L8_MFMA_SC keeps its accumulator tiles in LDS (L8_LDS_ACC)"
 #endif
 
 // Data (r, c), r <= c < 10, in the natural per-lane layout
@@ -131,7 +138,20 @@ union __align__(16) L8Lds {
 // the per-lane accumulators in LDS, [wave][entry][lane] (lane-consecutive: conflict-free b32 accesses): T slice
 // entries 0..11 (lane (pl, t) holds entries 12 pl + i of slot t's natural layout), accD 12..39, accE / accEB 40..44,
 // accHcc / accbc 45
-constexpr int L8_NACC = 12 + HS_ND_PROD + 6;
+constexpr int L8_NACC = L8_MFMA_SC ? 12 : 12 + HS_ND_PROD + 6;
+#if L8_MFMA_SC
+// The Schur accumulators of a point group as one product (Src/AccumulatedSCHessian.cpp:32-51): with the rows
+// R = 8 o + i (non-host slot o < 7, JpJdF component i) and a pseudo-slot 7 carrying v = (Hcd0..3, bdSumF, 0, 0, 0),
+//   X_qp[R] = J_qp[i][o] (o < 7) | v_qp[i] (o = 7),   M += sum_qp (HdiF_qp X_qp) X_qp^T   (64 x 64, fp32)
+// holds accD (o1, o2 < 7), accE / accEB (o < 7, the pseudo-slot's columns 0..3 / 4) and accHcc / accbc (the
+// pseudo-slot's rows and columns 0..3 / row 4).  The ten 16 x 16 tiles with block row <= block column are
+// accumulated by v_mfma_f32_16x16x4_f32 over the group's 8 points (two K = 4 steps): an MFMA is a k-ordered fma
+// chain, so every entry is the point-order fma sum the per-lane form built (fma(HdiF J1, J2, acc)), bit for bit,
+// except accEB (fma(HdiF J, bdSumF) here, fma(HdiF bdSumF, J) there).  The A operand of tile row a is HdiF times the
+// B operand of tile column a.  Tile (a, b) of wave w: ACCM[w][tile][lane] = its 4 accumulator rows of the lane.
+constexpr int L8_NTILE = 10;
+__host__ __device__ constexpr int sc_tile(int a, int b) { return a * 4 - (a * (a - 1)) / 2 + (b - a); }
+#endif
 #else
 union __align__(16) L8Lds {
   L8Scratch s[L8_NW];
@@ -294,6 +314,9 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
 #if L8_LDS_ACC
   __shared__ float ACC[L8_NW][L8_NACC][64];
 #endif
+#if L8_MFMA_SC
+  __shared__ l8f4 ACCM[L8_NW][L8_NTILE][64];  // the Schur accumulator tiles (sc_tile), lane-consecutive b128
+#endif
   if (a.brk && a.st->stop) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int pl = lane >> 3, t = lane & 7;  // point of the group, target slot
@@ -364,6 +387,10 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
 #if L8_LDS_ACC
 #pragma unroll
   for (int i = 0; i < L8_NACC; i++) ACC[wv][i][lane] = 0.f;
+#if L8_MFMA_SC
+#pragma unroll
+  for (int i = 0; i < L8_NTILE; i++) ACCM[wv][i][lane] = l8f4{0.f, 0.f, 0.f, 0.f};
+#endif
 #else
   float Td[12];
 #pragma unroll
@@ -807,6 +834,13 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
 #pragma unroll
       for (int i = 0; i < 8; i++) W.jb[pl][i][oslot] = active ? jj[i] : 0.f;
     }
+#if L8_MFMA_SC
+    if (t == h) {  // the pseudo-slot 7: (Hcd0..3, bdSumF) of a valid point (a clamped duplicate contributes nothing)
+      const float v[8] = {hc4.x, hc4.y, hc4.z, hc4.w, bdSumF, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < 8; i++) W.jb[pl][i][7] = valid ? v[i] : 0.f;
+    }
+#endif
     if (t == 0) {
       *reinterpret_cast<float4*>(&W.pp[pl][0]) = make_float4(HdiF, bdSumF, hc4.x, hc4.y);
       *reinterpret_cast<float4*>(&W.pp[pl][4]) = make_float4(hc4.z, hc4.w, 0.f, 0.f);
@@ -814,6 +848,33 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#if L8_MFMA_SC
+    {
+      // operands: lane l supplies row / column (l & 15) of its tile at k = l >> 4, i.e. point qp = 4 kc + (l >> 4),
+      // slot 2 a + bit 3 of l, component l & 7 (sc_tile's layout above)
+      const int hi = (lane >> 3) & 1, ci = lane & 7, kq = lane >> 4;
+      float bo[2][4], ao[2][4];
+#pragma unroll
+      for (int kc = 0; kc < 2; kc++) {
+        const int qp = 4 * kc + kq;
+        const float hdf = W.pp[qp][0];
+#pragma unroll
+        for (int x = 0; x < 4; x++) {
+          bo[kc][x] = W.jb[qp][ci][2 * x + hi];
+          ao[kc][x] = hdf * bo[kc][x];
+        }
+      }
+#pragma unroll
+      for (int x = 0; x < 4; x++)
+#pragma unroll
+        for (int y = x; y < 4; y++) {
+          l8f4 acc = ACCM[wv][sc_tile(x, y)][lane];
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ao[0][x], bo[0][y], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ao[1][x], bo[1][y], acc, 0, 0, 0);
+          ACCM[wv][sc_tile(x, y)][lane] = acc;
+        }
+    }
+#else
     {
 #pragma clang fp contract(fast)
       const int dr = pl, dc = t;         // accD lane (row, col)
@@ -867,6 +928,7 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
       ACC[wv][12 + HS_ND_PROD + 5][lane] = C;
 #endif
     }
+#endif
     __builtin_amdgcn_wave_barrier();  // the scratch is rewritten by the next group
     if (a.trace && tid == 0 && gi == wv) a.trace[(size_t)b * 16 + 12] = wall_clock64();  // wave 0's first group
   }
@@ -929,7 +991,31 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
       }
     } else {
       const int d = e - HS_E_TOP;
-#if L8_LDS_ACC
+#if L8_MFMA_SC
+      // entry d of lane l in the production layout -> (row R, column C) of the product (sc_tile's layout above)
+      int R = -1, Cc = 0;
+      if (d < HS_ND_PROD) {  // accD (o1, o2), o1 <= o2: lane (row dr, col dc)
+        int o1 = 0, q = d;
+        while (q >= 7 - o1) { q -= 7 - o1; o1++; }
+        R = 8 * o1 + (l >> 3);
+        Cc = 8 * (o1 + q) + (l & 7);
+      } else if (d < HS_ND_PROD + 5) {  // accE / accEB: lane (slot es, row ek); the host slot holds 0
+        const int es = l >> 3;
+        if (es != h) {
+          R = 8 * (es - (es > h ? 1 : 0)) + (l & 7);
+          Cc = 56 + (d - HS_ND_PROD);
+        }
+      } else if (l < 20) {  // accHcc (lanes 0..15, (row, col) = ((l >> 2) & 3, l & 3)), accbc (lanes 16..19)
+        R = l < 16 ? 56 + ((l >> 2) & 3) : 60;
+        Cc = 56 + (l & 3);
+      }
+      if (R >= 0) {
+        const int tl = sc_tile(R >> 4, Cc >> 4), m = R & 15, sl = 16 * (m >> 2) + (Cc & 15), v = m & 3;
+        s = ACCM[0][tl][sl][v];
+#pragma unroll
+        for (int w = 1; w < L8_NW; w++) s += ACCM[w][tl][sl][v];
+      }
+#elif L8_LDS_ACC
       s = ACC[0][12 + d][l];
 #pragma unroll
       for (int w = 1; w < L8_NW; w++) s += ACC[w][12 + d][l];
