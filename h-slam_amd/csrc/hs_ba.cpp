@@ -428,12 +428,18 @@ int make_partition(hs_ctx* c) {
   int target = c->lin8 ? kLin8BlocksTarget : kLinBlocksTarget;
   if (const char* e = std::getenv("HS_LIN8_BLOCKS"); e && c->lin8) target = std::max(1, std::atoi(e));
   int ppw = std::max(1, (nP + bw * target - 1) / (bw * target));
-  if (const char* e = std::getenv("HS_LIN_PPW")) ppw = std::max(1, std::atoi(e));
+  const char* pe = std::getenv("HS_LIN_PPW");
+  if (pe) ppw = std::max(1, std::atoi(pe));
+  // hs_k_lin8 with more than one point group per wave: every CU a block.  ceil(nh / (bw ppw)) blocks per host leave
+  // CUs idle (200k points: 31 per host, 248 of 256), and a launch of one block per CU lasts as long as its largest
+  // block; floor(target nh / nP) blocks per host fill the grid (Σ <= target + nF, within the block capacity)
+  const bool fill = c->lin8 && ppw > 1 && !pe && !std::getenv("HS_LIN8_BLOCKS") && !std::getenv("HS_LIN8_NOFILL");
   c->W = c->exact ? 1 : (c->lin8 ? HS_LIN8_NT / 64 : HS_LIN_NW);
   for (int h = 0; h < nF; h++) {
     const int nh = c->host_pt_begin[h + 1] - c->host_pt_begin[h];
     if (c->exact && nh > 1000) return fail(HS_ERR_INVALID, "HS_ACC_EXACT supports at most 1000 points per host");
-    const int nb = nh == 0 ? 0 : (c->exact ? 1 : (nh + bw * ppw - 1) / (bw * ppw));
+    int nb = nh == 0 ? 0 : (c->exact ? 1 : (nh + bw * ppw - 1) / (bw * ppw));
+    if (fill && nh > 0) nb = std::max(nb, (int)((long long)target * nh / nP));
     c->blk_begin[h + 1] = c->blk_begin[h] + nb;
   }
   c->nblk = c->blk_begin[nF];
