@@ -25,7 +25,23 @@
 
 namespace {
 
-typedef float l8f4 __attribute__((ext_vector_type(4)));  // an MFMA accumulator tile row set (v_mfma_f32_16x16x4_f32)
+typedef float l8f2 __attribute__((ext_vector_type(2)));  // a packed-fp32 pair (v_pk_fma_f32)
+// accD's 28 (o1 <= o2) entries as 9 register pairs (o2, o2 + 1) with o2 even -- so the operand pair is an aligned
+// half of the loaded JpJdF quads -- and 10 singles; kind 0: pair p (.x / .y by o2 parity), kind 1: single
+struct DSlot {
+  int kind, idx;
+};
+__host__ __device__ constexpr DSlot d_slot(int o1, int o2) {
+  int np = 0, ns = 0;
+  for (int a = 0; a < 7; a++)
+    for (int b = a; b < 7; b++) {
+      const bool paired = (b & 1) == 0 ? b + 1 < 7 : b - 1 >= a;  // (b, b + 1) or (b - 1, b) inside row a
+      if (a == o1 && b == o2) return paired ? DSlot{0, np} : DSlot{1, ns};
+      if (paired) np += (b & 1);  // a pair is counted at its odd member
+      else ns++;
+    }
+  return DSlot{-1, -1};
+}
 constexpr float SCALE_F8 = 50.0f, SCALE_C8 = 50.0f, SCALE_IDEPTH8 = 1.0f;
 constexpr int L8_NW = HS_LIN8_NT / 64;  // waves per block
 constexpr int NTOP = 91;  // AccumulatorApprox entries of one (host, target) block: Data 55 | TopRight 30 | BotRight 6
@@ -66,14 +82,13 @@ constexpr int Q8_N = 17;  // per-pixel quantities summed over the pattern
 #ifndef L8_LDS_ACC
 #define L8_LDS_ACC 1    // the per-lane accumulators (T slice, accD / accE / accEB / accHcc) live in LDS between groups
 #endif
-#ifndef L8_MFMA_SC
-#define L8_MFMA_SC 1    // the Schur accumulators (accD / accE / accEB / accHcc / accbc) by v_mfma_f32_16x16x4_f32 (below)
-#endif
-#ifndef L8_SC_BATCH
-#define L8_SC_BATCH 5   // Schur tiles whose accumulators are read, multiplied and written back together
-#endif
-#if L8_MFMA_SC && !L8_LDS_ACC
-#error "L8_MFMA_SC keeps its accumulator tiles in LDS (L8_LDS_ACC)"
+#ifndef L8_PK_SC
+// the Schur accumulators' accD / accE updates as packed-fp32 pairs (v_pk_fma_f32) on operand pairs that are aligned
+// halves of the loaded JpJdF quads (no moves to form them); the same fmas, bit for bit.  Measured (r06_nomfma, per
+// launch): 200k 151 -> 144 us, 2M 1324 -> 1254 us, 25k 38.2 -> 37.0 us.  (As one product on v_mfma_f32_16x16x4_f32
+// they measured 137 / 1167 / 36.9 us; the path's specification keeps these small accumulations off the matrix
+// cores, so that form is kept out: tools/archive/r06_lin8_mfma_schur.diff)
+#define L8_PK_SC 1
 #endif
 
 // Data (r, c), r <= c < 10, in the natural per-lane layout
@@ -141,20 +156,7 @@ union __align__(16) L8Lds {
 // the per-lane accumulators in LDS, [wave][entry][lane] (lane-consecutive: conflict-free b32 accesses): T slice
 // entries 0..11 (lane (pl, t) holds entries 12 pl + i of slot t's natural layout), accD 12..39, accE / accEB 40..44,
 // accHcc / accbc 45
-constexpr int L8_NACC = L8_MFMA_SC ? 12 : 12 + HS_ND_PROD + 6;
-#if L8_MFMA_SC
-// The Schur accumulators of a point group as one product (Src/AccumulatedSCHessian.cpp:32-51): with the rows
-// R = 8 o + i (non-host slot o < 7, JpJdF component i) and a pseudo-slot 7 carrying v = (Hcd0..3, bdSumF, 0, 0, 0),
-//   X_qp[R] = J_qp[i][o] (o < 7) | v_qp[i] (o = 7),   M += sum_qp (HdiF_qp X_qp) X_qp^T   (64 x 64, fp32)
-// holds accD (o1, o2 < 7), accE / accEB (o < 7, the pseudo-slot's columns 0..3 / 4) and accHcc / accbc (the
-// pseudo-slot's rows and columns 0..3 / row 4).  The ten 16 x 16 tiles with block row <= block column are
-// accumulated by v_mfma_f32_16x16x4_f32 over the group's 8 points (two K = 4 steps): an MFMA is a k-ordered fma
-// chain, so every entry is the point-order fma sum the per-lane form built (fma(HdiF J1, J2, acc)), bit for bit,
-// except accEB (fma(HdiF J, bdSumF) here, fma(HdiF bdSumF, J) there).  The A operand of tile row a is HdiF times the
-// B operand of tile column a.  Tile (a, b) of wave w: ACCM[w][tile][lane] = its 4 accumulator rows of the lane.
-constexpr int L8_NTILE = 10;
-__host__ __device__ constexpr int sc_tile(int a, int b) { return a * 4 - (a * (a - 1)) / 2 + (b - a); }
-#endif
+constexpr int L8_NACC = 12 + HS_ND_PROD + 6;
 #else
 union __align__(16) L8Lds {
   L8Scratch s[L8_NW];
@@ -317,9 +319,6 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
 #if L8_LDS_ACC
   __shared__ float ACC[L8_NW][L8_NACC][64];
 #endif
-#if L8_MFMA_SC
-  __shared__ l8f4 ACCM[L8_NW][L8_NTILE][64];  // the Schur accumulator tiles (sc_tile), lane-consecutive b128
-#endif
   if (a.brk && a.st->stop) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int pl = lane >> 3, t = lane & 7;  // point of the group, target slot
@@ -390,10 +389,6 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
 #if L8_LDS_ACC
 #pragma unroll
   for (int i = 0; i < L8_NACC; i++) ACC[wv][i][lane] = 0.f;
-#if L8_MFMA_SC
-#pragma unroll
-  for (int i = 0; i < L8_NTILE; i++) ACCM[wv][i][lane] = l8f4{0.f, 0.f, 0.f, 0.f};
-#endif
 #else
   float Td[12];
 #pragma unroll
@@ -837,13 +832,6 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
 #pragma unroll
       for (int i = 0; i < 8; i++) W.jb[pl][i][oslot] = active ? jj[i] : 0.f;
     }
-#if L8_MFMA_SC
-    if (t == h) {  // the pseudo-slot 7: (Hcd0..3, bdSumF) of a valid point (a clamped duplicate contributes nothing)
-      const float v[8] = {hc4.x, hc4.y, hc4.z, hc4.w, bdSumF, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int i = 0; i < 8; i++) W.jb[pl][i][7] = valid ? v[i] : 0.f;
-    }
-#endif
     if (t == 0) {
       *reinterpret_cast<float4*>(&W.pp[pl][0]) = make_float4(HdiF, bdSumF, hc4.x, hc4.y);
       *reinterpret_cast<float4*>(&W.pp[pl][4]) = make_float4(hc4.z, hc4.w, 0.f, 0.f);
@@ -851,44 +839,6 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#if L8_MFMA_SC
-    {
-      // operands: lane l supplies row / column (l & 15) of its tile at k = l >> 4, i.e. point qp = 4 kc + (l >> 4),
-      // slot 2 a + bit 3 of l, component l & 7 (sc_tile's layout above)
-      const int hi = (lane >> 3) & 1, ci = lane & 7, kq = lane >> 4;
-      float bo[2][4], ao[2][4];
-#pragma unroll
-      for (int kc = 0; kc < 2; kc++) {
-        const int qp = 4 * kc + kq;
-        const float hdf = W.pp[qp][0];
-#pragma unroll
-        for (int x = 0; x < 4; x++) {
-          bo[kc][x] = W.jb[qp][ci][2 * x + hi];
-          ao[kc][x] = hdf * bo[kc][x];
-        }
-      }
-      // the tiles in batches of L8_SC_BATCH: their reads in flight together, then the batch's K steps as
-      // independent MFMAs (the 40-cycle dependent latency hidden by the other tiles), then the writes
-      // (measured, r06_scb: batches of 5 / 10 against 1, 200k 162 -> 159 us, 2M 1190 -> 1173 us)
-      constexpr int TX[L8_NTILE] = {0, 0, 0, 0, 1, 1, 1, 2, 2, 3}, TY[L8_NTILE] = {0, 1, 2, 3, 1, 2, 3, 2, 3, 3};
-#pragma unroll
-      for (int t0 = 0; t0 < L8_NTILE; t0 += L8_SC_BATCH) {
-        l8f4 acc[L8_SC_BATCH];
-#pragma unroll
-        for (int u = 0; u < L8_SC_BATCH; u++)
-          if (t0 + u < L8_NTILE) acc[u] = ACCM[wv][t0 + u][lane];
-#pragma unroll
-        for (int kc = 0; kc < 2; kc++)
-#pragma unroll
-          for (int u = 0; u < L8_SC_BATCH; u++)
-            if (t0 + u < L8_NTILE)
-              acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(ao[kc][TX[t0 + u]], bo[kc][TY[t0 + u]], acc[u], 0, 0, 0);
-#pragma unroll
-        for (int u = 0; u < L8_SC_BATCH; u++)
-          if (t0 + u < L8_NTILE) ACCM[wv][t0 + u][lane] = acc[u];
-      }
-    }
-#else
     {
 #pragma clang fp contract(fast)
       const int dr = pl, dc = t;         // accD lane (row, col)
@@ -896,7 +846,24 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
       const int eo = es - (es > h ? 1 : 0);
       const int cr = (lane >> 2) & 3, ccol = lane & 3;
       const unsigned long long wbits = actBits;
-#if L8_LDS_ACC
+#if L8_PK_SC
+      l8f2 DP[9];
+      float DS[10];
+#pragma unroll
+      for (int o1 = 0; o1 < 7; o1++)
+#pragma unroll
+        for (int o2 = o1; o2 < 7; o2++) {
+          const float v = ACC[wv][12 + o1 * 7 - (o1 * (o1 - 1)) / 2 + (o2 - o1)][lane];
+          const DSlot ds = d_slot(o1, o2);
+          if (ds.kind == 1) DS[ds.idx] = v;
+          else if (o2 & 1) DP[ds.idx].y = v;
+          else DP[ds.idx].x = v;
+        }
+      float E[5], C;
+#pragma unroll
+      for (int i = 0; i < 5; i++) E[i] = ACC[wv][12 + HS_ND_PROD + i][lane];
+      C = ACC[wv][12 + HS_ND_PROD + 5][lane];
+#elif L8_LDS_ACC
       float D[HS_ND_PROD], E[5], C;
 #pragma unroll
       for (int i = 0; i < HS_ND_PROD; i++) D[i] = ACC[wv][12 + i][lane];
@@ -918,6 +885,27 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
         const float4 c1 = *reinterpret_cast<const float4*>(&W.jb[qp][dc][4]);
         const float j1[7] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z};
         const float j2[7] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z};
+#if L8_PK_SC
+        const l8f2 j2p[3] = {l8f2{c0.x, c0.y}, l8f2{c0.z, c0.w}, l8f2{c1.x, c1.y}};
+#pragma unroll
+        for (int o1 = 0; o1 < 7; o1++) {
+          const float wl = hdf * j1[o1];
+#pragma unroll
+          for (int o2 = o1; o2 < 7; o2++) {
+            const DSlot ds = d_slot(o1, o2);
+            if (ds.kind == 1) DS[ds.idx] = __builtin_fmaf(wl, j2[o2], DS[ds.idx]);
+            else if ((o2 & 1) == 0) DP[ds.idx] = __builtin_elementwise_fma(l8f2{wl, wl}, j2p[o2 >> 1], DP[ds.idx]);
+          }
+        }
+        {  // predicated, not branched: jb holds 0 for an inactive residual, and the host slot reads 0
+          const float jv = es != h ? W.jb[qp][ek][min(eo, 6)] : 0.f;
+          const float wl = hdf * jv;
+          const l8f2 e01 = __builtin_elementwise_fma(l8f2{wl, wl}, l8f2{pp0.z, pp0.w}, l8f2{E[0], E[1]});
+          const l8f2 e23 = __builtin_elementwise_fma(l8f2{wl, wl}, l8f2{pp1.x, pp1.y}, l8f2{E[2], E[3]});
+          E[0] = e01.x; E[1] = e01.y; E[2] = e23.x; E[3] = e23.y;
+          E[4] += (hdf * bsf) * jv;
+        }
+#else
 #pragma unroll
         for (int o1 = 0; o1 < 7; o1++) {
           const float wl = hdf * j1[o1];
@@ -931,18 +919,29 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
           for (int c = 0; c < 4; c++) E[c] += wl * hcv[c];
           E[4] += (hdf * bsf) * jv;
         }
+#endif
         const float hr = W.pp[qp][2 + cr], hc = W.pp[qp][2 + ccol];  // per-lane LDS addresses, no select chains
         C += lane < 16 ? (hdf * hr) * hc : (bsf * hdf) * hc;
       }
 #if L8_LDS_ACC
+#if L8_PK_SC
+#pragma unroll
+      for (int o1 = 0; o1 < 7; o1++)
+#pragma unroll
+        for (int o2 = o1; o2 < 7; o2++) {
+          const DSlot ds = d_slot(o1, o2);
+          ACC[wv][12 + o1 * 7 - (o1 * (o1 - 1)) / 2 + (o2 - o1)][lane] =
+              ds.kind == 1 ? DS[ds.idx] : ((o2 & 1) ? DP[ds.idx].y : DP[ds.idx].x);
+        }
+#else
 #pragma unroll
       for (int i = 0; i < HS_ND_PROD; i++) ACC[wv][12 + i][lane] = D[i];
+#endif
 #pragma unroll
       for (int i = 0; i < 5; i++) ACC[wv][12 + HS_ND_PROD + i][lane] = E[i];
       ACC[wv][12 + HS_ND_PROD + 5][lane] = C;
 #endif
     }
-#endif
     __builtin_amdgcn_wave_barrier();  // the scratch is rewritten by the next group
     if (a.trace && tid == 0 && gi == wv) a.trace[(size_t)b * 16 + 12] = wall_clock64();  // wave 0's first group
   }
@@ -1005,31 +1004,7 @@ __global__ __launch_bounds__(HS_LIN8_NT, L8_MIN_WAVES) void hs_k_lin8(HsLinArgs 
       }
     } else {
       const int d = e - HS_E_TOP;
-#if L8_MFMA_SC
-      // entry d of lane l in the production layout -> (row R, column C) of the product (sc_tile's layout above)
-      int R = -1, Cc = 0;
-      if (d < HS_ND_PROD) {  // accD (o1, o2), o1 <= o2: lane (row dr, col dc)
-        int o1 = 0, q = d;
-        while (q >= 7 - o1) { q -= 7 - o1; o1++; }
-        R = 8 * o1 + (l >> 3);
-        Cc = 8 * (o1 + q) + (l & 7);
-      } else if (d < HS_ND_PROD + 5) {  // accE / accEB: lane (slot es, row ek); the host slot holds 0
-        const int es = l >> 3;
-        if (es != h) {
-          R = 8 * (es - (es > h ? 1 : 0)) + (l & 7);
-          Cc = 56 + (d - HS_ND_PROD);
-        }
-      } else if (l < 20) {  // accHcc (lanes 0..15, (row, col) = ((l >> 2) & 3, l & 3)), accbc (lanes 16..19)
-        R = l < 16 ? 56 + ((l >> 2) & 3) : 60;
-        Cc = 56 + (l & 3);
-      }
-      if (R >= 0) {
-        const int tl = sc_tile(R >> 4, Cc >> 4), m = R & 15, sl = 16 * (m >> 2) + (Cc & 15), v = m & 3;
-        s = ACCM[0][tl][sl][v];
-#pragma unroll
-        for (int w = 1; w < L8_NW; w++) s += ACCM[w][tl][sl][v];
-      }
-#elif L8_LDS_ACC
+#if L8_LDS_ACC
       s = ACC[0][12 + d][l];
 #pragma unroll
       for (int w = 1; w < L8_NW; w++) s += ACC[w][12 + d][l];
