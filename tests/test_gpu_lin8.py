@@ -103,6 +103,37 @@ def test_lin8_trajectory(scene_name, request):
     g.close()
 
 
+def test_lin8_grid_fills_every_cu(scene_kitti20k):
+    """At 20k points a wave takes more than one point group, so the partition gives every host floor(256 nh / nP)
+    blocks instead of ceil(nh / (64 ppw)): one block per CU of the 256, a host's blocks covering equal shares of its
+    (row-major) points (hs_ba.cpp make_partition; DESIGN.md §4, hs_k_lin8 round 6).  Against the old count
+    (HS_LIN8_NOFILL=1): the per-residual and per-point outputs bit-identical (the blocks only regroup the points), the
+    systems at the H bar (the fp32 block partials group differently)."""
+    g = _window(scene_kitti20k, True)
+    os.environ["HS_LIN8_NOFILL"] = "1"
+    try:
+        g0 = _window(scene_kitti20k, True)
+    finally:
+        os.environ.pop("HS_LIN8_NOFILL", None)
+    nF = len(scene_kitti20k.frames_id)
+    pf, p0 = g.partition(), g0.partition()
+    assert pf["kernel"] == p0["kernel"] == "hs_k_lin8"
+    assert 256 <= pf["blocks"] <= 256 + nF and p0["blocks"] < pf["blocks"], (pf, p0)
+    for w in (g, g0):
+        w.linearizeAll(reset=True)
+    rf, r0 = g.residuals(), g0.residuals()
+    for k in rf:
+        assert np.array_equal(rf[k], r0[k]), k
+    for k in ("HdiF", "bdSumF", "idepth"):
+        assert np.array_equal(g.points()[k], g0.points()[k]), k
+    for which in (0, 1, 2):
+        Hf, bf = g.system(which)
+        H0, b0 = g0.system(which)
+        assert _close_H(Hf, H0)[0] and _close_b(bf, b0, H0)[0], which
+    g.close()
+    g0.close()
+
+
 def test_lin8_runs_are_bit_reproducible(scene_kitti20k):
     outs = []
     for _ in range(2):
