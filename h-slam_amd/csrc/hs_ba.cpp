@@ -431,8 +431,10 @@ int make_partition(hs_ctx* c) {
   const char* pe = std::getenv("HS_LIN_PPW");
   if (pe) ppw = std::max(1, std::atoi(pe));
   // hs_k_lin8 with more than one point group per wave: every CU a block.  ceil(nh / (bw ppw)) blocks per host leave
-  // CUs idle (200k points: 31 per host, 248 of 256), and a launch of one block per CU lasts as long as its largest
-  // block; floor(target nh / nP) blocks per host fill the grid (Σ <= target + nF, within the block capacity)
+  // CUs idle (200k points: 31 per host, 248 of 256) and rotate the host's image bands over the XCDs from host to host
+  // (workgroup w runs on XCD w mod 8); floor(target nh / nP) blocks per host fill the grid (Σ <= target + nF, within
+  // the block capacity) and, at 32 per host, give XCD x the same bands q = x mod 8 of every host (its L2 holds them):
+  // 200k 160 -> 137 us per launch (hs_k_lin8 round 6)
   const bool fill = c->lin8 && ppw > 1 && !pe && !std::getenv("HS_LIN8_BLOCKS") && !std::getenv("HS_LIN8_NOFILL");
   c->W = c->exact ? 1 : (c->lin8 ? HS_LIN8_NT / 64 : HS_LIN_NW);
   for (int h = 0; h < nF; h++) {
