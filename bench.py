@@ -903,6 +903,14 @@ def main():
             "avg_launch_ms_in_loop_events": lin_loop_ms,
             "timing": f"HIP events on the context stream around back-to-back {lin_kernel} launches (fused "
                       "linearize + applyRes + top / Schur accumulation into block partials)",
+            # the GN loop's launch also applies the previous solve's point step (resubstituteFPt, fused): it reads the
+            # last linearization's JpJdF (32 B per residual) and the step's chain heads every point group
+            "avg_launch_ms_gn_loop": (split or {}).get("linearize_kernel"),
+            "frac_gn_loop": (BYTES_PER_PRES * shard.n_res / ((split or {})["linearize_kernel"] * 1e-3) / 1e9
+                             / HBM_PEAK_GBS) if (split or {}).get("linearize_kernel") else None,
+            "gn_loop_timing": "the same kernel inside the fused GN loop (with the point step of the previous solve), "
+                              "HIP event pairs per launch in an untimed loop after the timed one (+~3 us event "
+                              "overhead per launch)",
             "counters": roof_ctr,
             "limiter_note": "one point per wave at 2k: dependent memory round trips (the step is a chain of 4 "
                             "dependent launches, the single-workgroup fp64 solve the longest)" if shard.n_points < 60000
