@@ -134,6 +134,33 @@ def test_lin8_grid_fills_every_cu(scene_kitti20k):
     g0.close()
 
 
+def test_lin8_filled_grid_five_frames():
+    """The filled partition on a 5-frame window of 20k points with unequal hosts (floor(256 nh / nP) blocks per host,
+    Σ within 256 + nF): hs_k_lin8 against hs_k_lin -- per-residual and per-point outputs bit-identical, the systems
+    at the H bar, two fused GN iterations together."""
+    from hslam_amd.scene import make_ba_scene
+    scene = make_ba_scene(n_points=20003, n_frames=5, seed=11)
+    g8, g1 = _window(scene, True), _window(scene, False)
+    p8 = g8.partition()
+    assert p8["kernel"] == "hs_k_lin8" and 250 <= p8["blocks"] <= 256 + 5, p8
+    for g in (g8, g1):
+        g.linearizeAll(reset=True)
+    r8, r1 = g8.residuals(), g1.residuals()
+    for k in r8:
+        assert np.array_equal(r8[k], r1[k]), k
+    for k in ("HdiF", "bdSumF", "idepth"):
+        assert np.array_equal(g8.points()[k], g1.points()[k]), k
+    for which in (0, 1, 2):
+        H8, b8 = g8.system(which)
+        H1, b1 = g1.system(which)
+        assert _close_H(H8, H1)[0] and _close_b(b8, b1, H1)[0], which
+    e8 = g8.iterate(0, 2)
+    e1 = g1.iterate(0, 2)
+    assert np.all(np.abs(e8 - e1) <= 1e-3 * np.abs(e1)), (e8, e1)
+    g8.close()
+    g1.close()
+
+
 def test_lin8_runs_are_bit_reproducible(scene_kitti20k):
     outs = []
     for _ in range(2):
