@@ -85,9 +85,9 @@ constexpr int Q8_N = 17;  // per-pixel quantities summed over the pattern
 #ifndef L8_PK_SC
 // the Schur accumulators' accD / accE updates as packed-fp32 pairs (v_pk_fma_f32) on operand pairs that are aligned
 // halves of the loaded JpJdF quads (no moves to form them); the same fmas, bit for bit.  Measured (per launch,
-// profiles/r06_mfma/valu_mfma_pk_ab.txt): 200k 151 -> 144 us, 2M 1324 -> 1254 us, 25k 38.2 -> 37.0 us.  (As one product on v_mfma_f32_16x16x4_f32
-// they measured 137 / 1167 / 36.9 us; the path's specification keeps these small accumulations off the matrix
-// cores, so that form is kept out: tools/archive/r06_lin8_mfma_schur.diff)
+// profiles/r06_mfma/valu_mfma_pk_ab.txt): 200k 151 -> 144 us, 2M 1324 -> 1254 us, 25k 38.2 -> 37.0 us.  (As one
+// product on v_mfma_f32_16x16x4_f32 they measured 137 / 1167 / 36.9 us; the path's specification keeps these small
+// accumulations off the matrix cores, so that form is kept out: tools/archive/r06_lin8_mfma_schur.diff)
 #define L8_PK_SC 1
 #endif
 
